@@ -1,0 +1,177 @@
+"""Seeded synthetic AOI workloads (BASELINE.json configs 1-5).
+
+Everything is derived from SplitMix64 so that the HIP path, the CPU oracle and
+the committed golden fixtures all consume bit-identical float32 inputs.
+
+* ``cfg1`` -- examples/test_game-style single space: N=1000 Avatars at integer
+  positions in [-400,400) (examples/test_game/Avatar.go:127-134), each tick
+  every entity moves with p=0.5 by the test_client bot random walk
+  ``X += -0.01 + 0.02*rand``, ``Z += -0.01 + 0.01*rand`` in float32
+  (examples/test_client/ClientBot.go:227-233).
+* ``cfg2`` -- one space, N=100k uniform, L=sqrt(N*1250) (mean ~32 neighbours),
+  every entity moves by U(-1,1) per axis per tick.
+* ``cfg3`` -- one space, N=1M, half uniform, half in 256 Gaussian hotspots
+  (sigma 250, centres uniform in [-0.4L,0.4L]^2): skewed cell occupancy.
+* ``cfg4`` -- 8192 independent spaces x 2000 entities, per-space L=1581.1.
+* ``cfg5`` -- one 2^24-entity world, L=sqrt(N*1250).
+
+Each tick's move order (= the seq order the AOI manager sees) is a seeded
+random permutation of that tick's movers (argsort of SplitMix64 keys).
+A move is ``x' = fl32(x + fl32(step))`` with no clamping: the reference has no
+world bounds (Space.GetSpaceRange is unused, engine/entity/Space.go:52-54).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+GAMMA = 0x9E3779B97F4A7C15
+M64 = (1 << 64) - 1
+D_DEFAULT = np.float32(100.0)  # EnableAOI(100), examples/test_game/MySpace.go:55-57
+
+
+def mix64(z: int) -> int:
+    """SplitMix64 finaliser on a Python int."""
+    z &= M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def subseed(seed: int, *tags: int) -> int:
+    h = seed & M64
+    for t in tags:
+        h = mix64(h ^ ((t * GAMMA) & M64))
+    return h
+
+
+def splitmix(seed: int, n: int) -> np.ndarray:
+    """n consecutive SplitMix64 outputs of the stream starting at ``seed``."""
+    with np.errstate(over="ignore"):
+        s = np.uint64(seed & M64) + np.uint64(GAMMA) * np.arange(1, n + 1, dtype=np.uint64)
+        z = s
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def unit_f64(r: np.ndarray) -> np.ndarray:
+    """u = (r >> 11) * 2^-53 in [0,1), double."""
+    return (r >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def unit_f32(r: np.ndarray) -> np.ndarray:
+    """float32 in [0,1) with 24 random bits (rand.Float32 analogue)."""
+    return ((r >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)).astype(np.float32)
+
+
+def permutation(seed: int, n: int) -> np.ndarray:
+    return np.argsort(splitmix(seed, n), kind="stable").astype(np.uint32)
+
+
+@dataclass
+class Workload:
+    name: str
+    n: int
+    D: np.float32
+    x: np.ndarray  # float32 current positions (by slot)
+    z: np.ndarray
+    space: np.ndarray  # uint32 space id per slot
+    n_spaces: int
+    seed: int
+    L: float
+
+    def initial(self):
+        """(slots, x, z, space) of the initial Enter batch, in seq order (slot order)."""
+        slots = np.arange(self.n, dtype=np.uint32)
+        return slots, self.x.copy(), self.z.copy(), self.space.copy()
+
+    def tick(self, t: int):
+        """Return the move batch of tick ``t`` (slots in seq order, new x, new z) and advance."""
+        n = self.n
+        s = subseed(self.seed, 0x71C, t)
+        if self.name == "cfg1":
+            r = splitmix(s, 3 * n)
+            p = unit_f32(r[0:n])
+            movers = np.nonzero(p < np.float32(0.5))[0].astype(np.uint32)
+            rx = unit_f32(r[n:2 * n])[movers]
+            rz = unit_f32(r[2 * n:3 * n])[movers]
+            mr = np.float32(0.01)
+            sx = (np.float32(-mr) + (np.float32(2.0) * mr) * rx).astype(np.float32)
+            sz = (np.float32(-mr) + mr * rz).astype(np.float32)
+        else:
+            r = splitmix(s, 2 * n)
+            movers = np.arange(n, dtype=np.uint32)
+            sx = (2.0 * unit_f64(r[0:n]) - 1.0).astype(np.float32)
+            sz = (2.0 * unit_f64(r[n:2 * n]) - 1.0).astype(np.float32)
+        nx = (self.x[movers] + sx).astype(np.float32)
+        nz = (self.z[movers] + sz).astype(np.float32)
+        order = permutation(subseed(self.seed, 0x0D3, t), movers.size)
+        slots = movers[order]
+        nx, nz = nx[order], nz[order]
+        self.x[slots] = nx
+        self.z[slots] = nz
+        return slots, nx, nz
+
+
+def _uniform_xy(seed: int, n: int, L: float):
+    r = splitmix(seed, 2 * n)
+    x = (unit_f64(r[0:n]) * L - L / 2).astype(np.float32)
+    z = (unit_f64(r[n:2 * n]) * L - L / 2).astype(np.float32)
+    return x, z
+
+
+def make_workload(cfg: str, n: int | None = None, seed: int | None = None,
+                  n_spaces: int | None = None, per_space: int | None = None) -> Workload:
+    """Build config ``cfg`` ('cfg1'..'cfg5'); ``n`` scales cfg2/3/5 at constant density."""
+    idx = int(cfg[-1])
+    if seed is None:
+        seed = 0x5EED0000 + idx
+    D = D_DEFAULT
+    if cfg == "cfg1":
+        n = n or 1000
+        r = splitmix(subseed(seed, 1), 2 * n)
+        x = (np.float32(-400) + (r[0:n] % np.uint64(800)).astype(np.float32)).astype(np.float32)
+        z = (np.float32(-400) + (r[n:2 * n] % np.uint64(800)).astype(np.float32)).astype(np.float32)
+        sp = np.zeros(n, np.uint32)
+        return Workload(cfg, n, D, x, z, sp, 1, seed, 800.0)
+    if cfg in ("cfg2", "cfg5"):
+        n = n or (100_000 if cfg == "cfg2" else 1 << 24)
+        L = math.sqrt(n * 1250.0)
+        x, z = _uniform_xy(subseed(seed, 1), n, L)
+        return Workload(cfg, n, D, x, z, np.zeros(n, np.uint32), 1, seed, L)
+    if cfg == "cfg3":
+        n = n or 1_000_000
+        L = math.sqrt(n * 1250.0)
+        nu = n // 2
+        xu, zu = _uniform_xy(subseed(seed, 1), nu, L)
+        nh = n - nu
+        hot = 256
+        rc = splitmix(subseed(seed, 2), 2 * hot)
+        cx = (unit_f64(rc[0:hot]) * 0.8 - 0.4) * L
+        cz = (unit_f64(rc[hot:]) * 0.8 - 0.4) * L
+        r = splitmix(subseed(seed, 3), 5 * nh)
+        h = (r[0:nh] % np.uint64(hot)).astype(np.int64)
+        u1 = 1.0 - unit_f64(r[nh:2 * nh])  # (0,1]
+        u2 = unit_f64(r[2 * nh:3 * nh])
+        u3 = 1.0 - unit_f64(r[3 * nh:4 * nh])
+        u4 = unit_f64(r[4 * nh:5 * nh])
+        sigma = 250.0
+        gx = np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * math.pi * u2)
+        gz = np.sqrt(-2.0 * np.log(u3)) * np.cos(2.0 * math.pi * u4)
+        xh = (cx[h] + sigma * gx).astype(np.float32)
+        zh = (cz[h] + sigma * gz).astype(np.float32)
+        x = np.concatenate([xu, xh]).astype(np.float32)
+        z = np.concatenate([zu, zh]).astype(np.float32)
+        return Workload(cfg, n, D, x, z, np.zeros(n, np.uint32), 1, seed, L)
+    if cfg == "cfg4":
+        n_spaces = n_spaces or 8192
+        per_space = per_space or 2000
+        n = n_spaces * per_space
+        L = math.sqrt(per_space * 1250.0)
+        x, z = _uniform_xy(subseed(seed, 1), n, L)
+        sp = (np.arange(n, dtype=np.int64) // per_space).astype(np.uint32)
+        return Workload(cfg, n, D, x, z, sp, n_spaces, seed, L)
+    raise ValueError(f"unknown workload {cfg}")

@@ -1,0 +1,272 @@
+"""ctypes front-end of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline, never as a product path.
+
+* ``XZList``   -- one go-aoi ``XZListAOIManager`` restated sequentially
+  (oracle/xzlist.c).
+* ``SpacesOracle`` -- one ``XZList`` per space, global slot ids, the way
+  GoWorld gives every Space its own manager (engine/entity/Space.go:33,105).
+* ``closed_form_pairs`` -- the batch relation of SURVEY.md Appendix B
+  (oracle/closed_form.c).
+
+PARITY UNPINNED: go-aoi (go.mod:29) is absent and the reference holds no AOI
+fixture; see DESIGN.md §Oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+OP_MOVED, OP_ENTER, OP_LEAVE = 0, 1, 2
+EV_ENTER, EV_LEAVE = 1, 2
+DEAD = 0xFFFFFFFF
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = C.CDLL(_LIB)
+        vp, f, i32, i64, sz = C.c_void_p, C.c_float, C.c_int32, C.c_int64, C.c_size_t
+        L.xz_new.restype = vp
+        L.xz_new.argtypes = [f, i32]
+        L.xz_free.argtypes = [vp]
+        L.xz_set_record.argtypes = [vp, C.c_int]
+        for name in ("xz_enter", "xz_moved"):
+            getattr(L, name).argtypes = [vp, i32, f, f]
+            getattr(L, name).restype = C.c_int
+        L.xz_leave.argtypes = [vp, i32]
+        L.xz_leave.restype = C.c_int
+        L.xz_apply.argtypes = [vp, i64, vp, vp, vp, vp]
+        L.xz_apply.restype = i64
+        L.xz_moved_batch.argtypes = [vp, i64, vp, vp, vp]
+        L.xz_moved_batch.restype = i64
+        L.xz_counts.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+        L.xz_num_events.argtypes = [vp]
+        L.xz_num_events.restype = sz
+        L.xz_take_events.argtypes = [vp, vp, vp, vp, sz]
+        L.xz_take_events.restype = sz
+        L.xz_neighbors.argtypes = [vp, i32, vp, i32]
+        L.xz_neighbors.restype = i32
+        L.xz_neighbor_count.argtypes = [vp, i32]
+        L.xz_neighbor_count.restype = i32
+        L.xz_total_pairs.argtypes = [vp]
+        L.xz_total_pairs.restype = i64
+        L.xz_check.argtypes = [vp]
+        L.xz_check.restype = C.c_int
+        L.cf_pairs.argtypes = [i64, vp, vp, vp, vp, vp, C.POINTER(C.POINTER(C.c_uint64))]
+        L.cf_pairs.restype = i64
+        L.cf_free.argtypes = [vp]
+        L.cf_pred.argtypes = [f, f, f, f, f]
+        L.cf_pred.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class XZList:
+    """Sequential go-aoi XZListAOIManager restatement over local ids [0, cap)."""
+
+    def __init__(self, D: float, cap: int, record: bool = True):
+        self._L = lib()
+        self._m = self._L.xz_new(C.c_float(D), cap)
+        self._L.xz_set_record(self._m, 1 if record else 0)
+        self.cap = cap
+
+    def __del__(self):
+        if getattr(self, "_m", None):
+            self._L.xz_free(self._m)
+            self._m = None
+
+    def enter(self, i, x, z):
+        if self._L.xz_enter(self._m, int(i), C.c_float(x), C.c_float(z)):
+            raise RuntimeError(f"Enter({i}) on a live AOI")
+
+    def leave(self, i):
+        if self._L.xz_leave(self._m, int(i)):
+            raise RuntimeError(f"Leave({i}) on an AOI that never entered")
+
+    def moved(self, i, x, z):
+        if self._L.xz_moved(self._m, int(i), C.c_float(x), C.c_float(z)):
+            raise RuntimeError(f"Moved({i}) on an AOI that never entered")
+
+    def apply(self, ops, ids, xs, zs):
+        ops = np.ascontiguousarray(ops, np.uint8)
+        ids = np.ascontiguousarray(ids, np.int32)
+        xs = np.ascontiguousarray(xs, np.float32)
+        zs = np.ascontiguousarray(zs, np.float32)
+        bad = self._L.xz_apply(self._m, ops.size, _p(ops), _p(ids), _p(xs), _p(zs))
+        if bad >= 0:
+            raise RuntimeError(f"op {bad} rejected")
+
+    def moved_batch(self, ids, xs, zs):
+        ids = np.ascontiguousarray(ids, np.int32)
+        xs = np.ascontiguousarray(xs, np.float32)
+        zs = np.ascontiguousarray(zs, np.float32)
+        bad = self._L.xz_moved_batch(self._m, ids.size, _p(ids), _p(xs), _p(zs))
+        if bad >= 0:
+            raise RuntimeError(f"move {bad} rejected")
+
+    def counts(self):
+        e, l = C.c_int64(), C.c_int64()
+        self._L.xz_counts(self._m, C.byref(e), C.byref(l))
+        return e.value, l.value
+
+    def take_events(self):
+        n = self._L.xz_num_events(self._m)
+        t = np.empty(n, np.uint8)
+        a = np.empty(n, np.int32)
+        b = np.empty(n, np.int32)
+        self._L.xz_take_events(self._m, _p(t), _p(a), _p(b), n)
+        return t, a, b
+
+    def neighbors(self, i):
+        cnt = self._L.xz_neighbor_count(self._m, int(i))
+        out = np.empty(max(cnt, 1), np.int32)
+        self._L.xz_neighbors(self._m, int(i), _p(out), out.size)
+        return np.sort(out[:cnt])
+
+    def pairs(self):
+        """All directed neighbour pairs as sorted uint64 keys (a<<32|b), local ids."""
+        keys = []
+        for i in range(self.cap):
+            nb = self.neighbors(i)
+            if nb.size:
+                keys.append((np.uint64(i) << np.uint64(32)) | nb.astype(np.uint64))
+        return np.sort(np.concatenate(keys)) if keys else np.empty(0, np.uint64)
+
+    def check(self):
+        return self._L.xz_check(self._m)
+
+
+class SpacesOracle:
+    """One XZList per space over global slots, replaying a GoWorld op stream.
+
+    Ops are applied in seq order exactly as Space.enter/leave/move would call
+    the manager (engine/entity/Space.go:211,243,259).  Events are kept as
+    (type, a_slot, b_slot).
+    """
+
+    def __init__(self, D_by_space, max_slots: int, record: bool = True):
+        self.D = {int(k): float(v) for k, v in D_by_space.items()}
+        self.max_slots = max_slots
+        self.mgr = {}
+        self.local = {}  # slot -> (space, local id)
+        self.free = {}
+        self.next_local = {}
+        self.local_to_slot = {}
+        self.record = record
+
+    def _m(self, sp):
+        if sp not in self.mgr:
+            self.mgr[sp] = XZList(self.D[sp], self.max_slots, self.record)
+            self.local_to_slot[sp] = np.full(self.max_slots, -1, np.int64)
+        return self.mgr[sp]
+
+    def enter(self, sp, slot, x, z):
+        m = self._m(sp)
+        lid = slot  # local id == slot keeps the mapping trivial
+        m.enter(lid, x, z)
+        self.local[slot] = sp
+        self.local_to_slot[sp][lid] = slot
+
+    def leave(self, slot):
+        sp = self.local.pop(slot)
+        self.mgr[sp].leave(slot)
+
+    def moved(self, slot, x, z):
+        self.mgr[self.local[slot]].moved(slot, x, z)
+
+    def moved_batch(self, slots, xs, zs):
+        """Moves whose slots all live in one space (the common batched case)."""
+        sps = {self.local[int(s)] for s in slots[:1]}
+        sp = sps.pop()
+        self.mgr[sp].moved_batch(slots, xs, zs)
+
+    def take_events(self):
+        ts, as_, bs = [], [], []
+        for sp, m in self.mgr.items():
+            t, a, b = m.take_events()
+            ts.append(t); as_.append(a); bs.append(b)
+        if not ts:
+            return np.empty(0, np.uint8), np.empty(0, np.int32), np.empty(0, np.int32)
+        return np.concatenate(ts), np.concatenate(as_), np.concatenate(bs)
+
+    def pairs(self):
+        keys = [m.pairs() for m in self.mgr.values()]
+        keys = [k for k in keys if k.size]
+        return np.sort(np.concatenate(keys)) if keys else np.empty(0, np.uint64)
+
+    def neighbors(self, slot):
+        if slot not in self.local:
+            return np.empty(0, np.int32)
+        return self.mgr[self.local[slot]].neighbors(slot)
+
+
+def closed_form_pairs(x, z, seq, sp, D_by_space):
+    """Directed neighbour pairs of the closed form (Appendix B), sorted uint64 keys."""
+    L = lib()
+    x = np.ascontiguousarray(x, np.float32)
+    z = np.ascontiguousarray(z, np.float32)
+    seq = np.ascontiguousarray(seq, np.uint64)
+    sp = np.ascontiguousarray(sp, np.uint32)
+    live = sp[sp != DEAD]
+    nsp = int(live.max()) + 1 if live.size else 1
+    D = np.zeros(nsp, np.float32)
+    for k, v in D_by_space.items():
+        if int(k) < nsp:
+            D[int(k)] = v
+    out = C.POINTER(C.c_uint64)()
+    n = L.cf_pairs(x.size, _p(x), _p(z), _p(seq), _p(sp), _p(D), C.byref(out))
+    res = np.ctypeslib.as_array(out, shape=(n,)).copy() if n else np.empty(0, np.uint64)
+    L.cf_free(C.cast(out, C.c_void_p))
+    return res
+
+
+def pred(wx, wz, lx, lz, D):
+    """P_W(L): does W's window [fl32(w-D), fl32(w+D)]^2 contain L?"""
+    return bool(lib().cf_pred(C.c_float(wx), C.c_float(wz), C.c_float(lx), C.c_float(lz), C.c_float(D)))
+
+
+def events_to_keys(t, a, b):
+    """Split an event stream into sorted uint64 key arrays (enter, leave)."""
+    a = np.asarray(a).astype(np.uint64)
+    b = np.asarray(b).astype(np.uint64)
+    k = (a << np.uint64(32)) | b
+    return np.sort(k[t == EV_ENTER]), np.sort(k[t == EV_LEAVE])
+
+
+def net_events(t, a, b):
+    """Net per-flush diff of a sequential event stream: (enter keys, leave keys).
+
+    The sequential manager can emit a transient enter+leave of one pair within
+    a flush; the batch engine reports only the net change.
+    """
+    a = np.asarray(a).astype(np.int64)
+    b = np.asarray(b).astype(np.int64)
+    state = {}
+    for ti, ai, bi in zip(t.tolist(), a.tolist(), b.tolist()):
+        k = (ai << 32) | bi
+        d = 1 if ti == EV_ENTER else -1
+        state[k] = state.get(k, 0) + d
+    ent = np.array(sorted(k for k, v in state.items() if v > 0), np.uint64)
+    lev = np.array(sorted(k for k, v in state.items() if v < 0), np.uint64)
+    for v in state.values():
+        assert v in (-1, 0, 1), "unbalanced event stream"
+    return ent, lev
