@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""AOI tick benchmark (BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3]
+
+A step is one AOI flush (gwaoi_tick_device): one batch of Moved calls --
+every entity of the space moves once, in a seeded random call order -- then
+the GPU pipeline computes the new neighbour relation and compacts the net
+enter/leave events into device memory.  The move batches are generated on the
+host before timing and uploaded to HBM (inputs resident when the timed region
+starts).  At N=1 the workload is config 3 (1M entities, 256 Gaussian crowd
+hotspots + uniform background, AOI distance 100, step U(-1,1)) -- the config
+BASELINE.json quotes the metric on.  With N>1 ranks (torch.distributed.run,
+RCCL) every rank owns its own independent space of the same size (GoWorld
+spaces are independent, Space.go:33): weak scaling, no data-path collective.
+
+Printed: one JSON line with value = entity-moves/s over all ranks, plus
+events/s, p50/p99 tick latency, the roofline of the dominant kernel (HIP
+events on the world's stream) and the CPU baseline (the go-aoi restatement in
+oracle/, one core, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "AOI entity-moves/sec + enter/leave events/sec at 1M entities; p99 tick ms"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOAD_DESC = {
+    "cfg1": "test_game-style single space, 1k entities random walk (bot walk, p=0.5)",
+    "cfg2": "one space, 100k entities uniform, step U(-1,1)",
+    "cfg3": "one space, 1M entities clustered crowd hotspots (256 x sigma 250 + uniform), step U(-1,1)",
+    "cfg4": "8192 spaces x 2k entities (per rank: spaces / n_gpus), step U(-1,1)",
+    "cfg5": "single 16M-entity world (untiled, one GPU), step U(-1,1)",
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def pair_pass_bytes(n: int, events: float) -> float:
+    """Algorithmic HBM bytes of one pair-pass launch over n frame entries
+    (DESIGN.md §Roofline): own record x,z,seq,sp (24 B) + other-time record
+    x,z,seq,sp (24 B) + grid row bounds (~8 cell_start reads, 32 B) +
+    count write / offset read (4 B) + slot (4 B) + 8 B per event written."""
+    return n * 88.0 + 8.0 * events
+
+
+def cpu_baseline(args, wl_factory, target_s: float):
+    """go-aoi XZListAOIManager restatement (oracle/xzlist.c), one core, timed on
+    a prefix of tick 0's move batch of the same workload."""
+    from oracle import oracle
+    wl = wl_factory()
+    m = oracle.XZList(wl.D, wl.n, record=False)
+    slots, x0, z0, sp = wl.initial()
+    if wl.n_spaces != 1:
+        per = wl.n // wl.n_spaces
+        slots, x0, z0 = slots[:per], x0[:per], z0[:per]
+    m.bulk_enter(slots.astype(np.int32), x0, z0)
+    sl, nx, nz = wl.tick(0)
+    if wl.n_spaces != 1:
+        keep = sl < slots.size
+        sl, nx, nz = sl[keep], nx[keep], nz[keep]
+    done = 0
+    chunk = 256
+    t0 = time.perf_counter()
+    while done < sl.size and time.perf_counter() - t0 < target_s:
+        k = min(chunk, sl.size - done)
+        m.moved_batch(sl[done:done + k], nx[done:done + k], nz[done:done + k])
+        done += k
+        chunk = min(chunk * 2, 8192)
+    dt = time.perf_counter() - t0
+    ne, nl = m.counts()
+    return {
+        "value": done / dt,
+        "unit": "entity-moves/s",
+        "events_per_s": (ne + nl) / dt,
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {done} Moved calls of tick 0 of {args.workload} "
+                  f"({'1 space of ' + str(slots.size) if wl.n_spaces != 1 else str(wl.n)} entities), "
+                  f"sequential XZ-list restatement, {dt:.1f} s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOAD_DESC))
+    ap.add_argument("--n", type=int, default=None, help="override entity count (cfg2/3/5)")
+    ap.add_argument("--spaces", type=int, default=None, help="cfg4: total spaces (default 8192)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-stage HIP event timing")
+    ap.add_argument("--cells-per-dist", type=float, default=0.0)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    dist = None
+    if ws > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = local
+
+    from goworld_amd import World
+    from goworld_amd.workload import make_workload
+
+    def wl_factory():
+        if args.workload == "cfg4":
+            total = args.spaces or 8192
+            per_rank = max(1, total // ws)
+            return make_workload("cfg4", seed=0x5EED0004 + 7919 * rank, n_spaces=per_rank)
+        seed = 0x5EED0000 + int(args.workload[-1]) + 7919 * rank
+        return make_workload(args.workload, n=args.n, seed=seed)
+
+    t_setup = time.perf_counter()
+    wl = wl_factory()
+    n = wl.n
+    ticks = args.warmup + args.steps
+    # ---- synthetic move batches, generated before timing, resident in HBM
+    import torch
+    torch.cuda.set_device(device)
+    batches = []
+    for t in range(ticks):
+        sl, nx, nz = wl.tick(t)
+        batches.append((sl, nx, nz))
+    d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
+    d_x = torch.from_numpy(np.stack([b[1] for b in batches])).to(f"cuda:{device}")
+    d_z = torch.from_numpy(np.stack([b[2] for b in batches])).to(f"cuda:{device}")
+    moves_per_tick = [b[0].size for b in batches]
+    del batches
+    torch.cuda.synchronize()
+
+    w = World(n, max_spaces=wl.n_spaces, device=device, timing=not args.no_timing,
+              cells_per_dist=args.cells_per_dist)
+    spaces = [w.space_create(wl.D) for _ in range(wl.n_spaces)]
+    wl0 = wl_factory()  # initial positions (wl has advanced through the batches)
+    slots, x0, z0, sp = wl0.initial()
+    del wl0
+    for s in range(wl.n_spaces):
+        sel = np.nonzero(sp == s)[0] if wl.n_spaces > 1 else slice(None)
+        w.enter_batch(spaces[s], slots[sel], x0[sel], z0[sel])
+    ne0, nl0 = w.tick_device()  # populate: every pair is an enter event
+    setup_s = time.perf_counter() - t_setup
+
+    def step(t):
+        row = t
+        w.moved_batch_device(d_slots[row].data_ptr(), d_x[row].data_ptr(), d_z[row].data_ptr(),
+                             moves_per_tick[row])
+        return w.tick_device()
+
+    for t in range(args.warmup):
+        step(t)
+    w.reset_stage_times()
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    w.sync()
+    lat = []
+    events = 0
+    moves = 0
+    t0 = time.perf_counter()
+    for t in range(args.warmup, ticks):
+        a = time.perf_counter()
+        ne, nl = step(t)
+        lat.append(time.perf_counter() - a)
+        events += ne + nl
+        moves += moves_per_tick[t]
+    w.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    stages = w.stage_times() if not args.no_timing else {}
+    info = w.info()
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed_max = float(tt.item())
+        tot = torch.tensor([float(moves), float(events)], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        moves_all, events_all = float(tot[0]), float(tot[1])
+    else:
+        elapsed_max, moves_all, events_all = elapsed, float(moves), float(events)
+
+    if rank == 0:
+        lat_ms = np.array(lat) * 1e3
+        # dominant kernel = the costliest stage per tick
+        roofline = None
+        stage_ms = {k: v[0] / max(v[1], 1) for k, v in stages.items() if v[1]}
+        if stage_ms:
+            dom = max((k for k in stage_ms if k != "d2h"), key=lambda k: stage_ms[k])
+            ev_tick = events / max(args.steps, 1)
+            if dom.endswith(("_count", "_fill")):
+                alg = pair_pass_bytes(n, ev_tick / 2 if dom.endswith("_fill") else 0.0)
+            else:
+                alg = None
+            if alg is not None:
+                t_s = stage_ms[dom] * 1e-3
+                ach = alg / t_s / 1e9
+                roofline = {"bound": "hbm", "kernel": f"k_pairs ({dom})", "achieved": round(ach, 2),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+                            "traffic": None, "alg_bytes_per_launch": alg,
+                            "avg_launch_ms": round(stage_ms[dom], 4)}
+        cpu = None
+        if not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args, wl_factory, args.cpu_seconds)
+            except Exception as e:  # the baseline must not take the GPU number down with it
+                cpu = {"error": repr(e)}
+        out = {
+            "metric": METRIC,
+            "value": moves_all / elapsed_max,
+            "unit": "entity-moves/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded SplitMix64, generated on host, resident in HBM before timing)",
+            "config": {"workload": f"{args.workload}: {WORKLOAD_DESC[args.workload]}", "entities_per_rank": n,
+                       "spaces_per_rank": wl.n_spaces, "aoi_distance": float(wl.D),
+                       "parallelism": f"space-sharded x{ws} (no data-path collective)",
+                       "total_cells": info["total_cells"]},
+            "events_per_s": events_all / elapsed_max,
+            "p50_tick_ms": float(np.percentile(lat_ms, 50)),
+            "p99_tick_ms": float(np.percentile(lat_ms, 99)),
+            "events_per_tick": events / max(args.steps, 1),
+            "initial_enter_events": ne0,
+            "setup_s": round(setup_s, 2),
+            "roofline": roofline,
+            "stages_ms_per_tick": {k: round(v, 4) for k, v in stage_ms.items()},
+            "cpu_baseline": cpu,
+        }
+        if cpu and "value" in cpu:
+            out["speedup_vs_cpu"] = out["value"] / ws / cpu["value"]
+        print(json.dumps(out), flush=True)
+    w.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,250 @@
+"""ctypes binding of libgwaoi.so (include/gwaoi.h).
+
+The shared library is built in-tree (goworld_amd/lib/libgwaoi.so) by
+``goworld_amd.build``.  There is no fallback: if the library is missing,
+``load()`` raises.  PyTorch, when installed, is imported first so that the
+process holds exactly one HIP runtime (torch bundles its own libamdhip64, and
+libgwaoi then binds to that copy by soname).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgwaoi.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "gwaoi.h")
+
+GWAOI_F_TIMING = 1
+
+STATUS = {
+    0: "GWAOI_OK", -1: "GWAOI_EINVAL", -2: "GWAOI_EBADSLOT", -3: "GWAOI_ESTATE", -4: "GWAOI_ENOMEM",
+    -5: "GWAOI_EDEVICE", -6: "GWAOI_ENONFINITE", -7: "GWAOI_EBADSPACE", -8: "GWAOI_EBUSY",
+    -9: "GWAOI_ECAPACITY",
+}
+
+# every function include/gwaoi.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "gwaoi_world_create", "gwaoi_world_destroy", "gwaoi_space_create", "gwaoi_space_destroy",
+    "gwaoi_enter", "gwaoi_leave", "gwaoi_moved", "gwaoi_enter_batch", "gwaoi_leave_batch",
+    "gwaoi_moved_batch", "gwaoi_moved_batch_device", "gwaoi_tick", "gwaoi_tick_device",
+    "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
+    "gwaoi_reset_stage_times", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
+    "gwaoi_abi_version",
+]
+
+
+class Config(C.Structure):
+    _fields_ = [("max_slots", C.c_uint32), ("max_spaces", C.c_uint32), ("device", C.c_int32),
+                ("flags", C.c_uint32), ("event_capacity", C.c_uint64), ("cells_per_dist", C.c_float)]
+
+
+class Events(C.Structure):
+    _fields_ = [("n_enter", C.c_uint64), ("n_leave", C.c_uint64),
+                ("enter", C.POINTER(C.c_uint32)), ("leave", C.POINTER(C.c_uint32))]
+
+
+class Info(C.Structure):
+    _fields_ = [("ticks", C.c_uint64), ("next_seq", C.c_uint64), ("live", C.c_uint32),
+                ("spaces", C.c_uint32), ("total_cells", C.c_uint32), ("pending_ops", C.c_uint32),
+                ("event_capacity", C.c_uint64)]
+
+
+class StageTime(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("ms", C.c_double), ("calls", C.c_uint64)]
+
+
+class GwaoiError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load libgwaoi.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:  # one HIP runtime per process: bind to torch's copy when torch is present
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, f, sz = C.c_void_p, C.c_uint32, C.c_uint64, C.c_float, C.c_size_t
+    P = C.POINTER
+    sigs = {
+        "gwaoi_world_create": ([P(Config), P(vp)], C.c_int),
+        "gwaoi_world_destroy": ([vp], C.c_int),
+        "gwaoi_space_create": ([vp, f, P(u32)], C.c_int),
+        "gwaoi_space_destroy": ([vp, u32], C.c_int),
+        "gwaoi_enter": ([vp, u32, u32, f, f], C.c_int),
+        "gwaoi_leave": ([vp, u32], C.c_int),
+        "gwaoi_moved": ([vp, u32, f, f], C.c_int),
+        "gwaoi_enter_batch": ([vp, u32, vp, vp, vp, sz], C.c_int),
+        "gwaoi_leave_batch": ([vp, vp, sz], C.c_int),
+        "gwaoi_moved_batch": ([vp, vp, vp, vp, sz], C.c_int),
+        "gwaoi_moved_batch_device": ([vp, vp, vp, vp, sz], C.c_int),
+        "gwaoi_tick": ([vp, P(Events)], C.c_int),
+        "gwaoi_tick_device": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
+        "gwaoi_neighbors": ([vp, u32, vp, sz, P(sz)], C.c_int),
+        "gwaoi_world_info": ([vp, P(Info)], C.c_int),
+        "gwaoi_stage_times": ([vp, P(StageTime), sz, P(sz)], C.c_int),
+        "gwaoi_reset_stage_times": ([vp], C.c_int),
+        "gwaoi_sync": ([vp], C.c_int),
+        "gwaoi_stream": ([vp], vp),
+        "gwaoi_strerror": ([C.c_int], C.c_char_p),
+        "gwaoi_last_error": ([vp], C.c_char_p),
+        "gwaoi_abi_version": ([], C.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class World:
+    """One GPU AOI world: many spaces, one HIP stream (include/gwaoi.h)."""
+
+    def __init__(self, max_slots: int, max_spaces: int = 1, device: int = -1, timing: bool = False,
+                 event_capacity: int = 0, cells_per_dist: float = 0.0):
+        self._L = load()
+        cfg = Config(max_slots, max_spaces, device, GWAOI_F_TIMING if timing else 0, event_capacity,
+                     cells_per_dist)
+        h = C.c_void_p()
+        self._check(self._L.gwaoi_world_create(C.byref(cfg), C.byref(h)), world=False)
+        self._w = h
+        self.max_slots = max_slots
+
+    def close(self):
+        if getattr(self, "_w", None):
+            self._L.gwaoi_world_destroy(self._w)
+            self._w = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, world=True):
+        if rc != 0:
+            msg = self._L.gwaoi_strerror(rc).decode()
+            if world and getattr(self, "_w", None):
+                last = self._L.gwaoi_last_error(self._w).decode()
+                if last:
+                    msg += f" ({last})"
+            raise GwaoiError(rc, msg)
+        return rc
+
+    # ---- spaces / AOIManager calls
+    def space_create(self, aoi_distance) -> int:
+        s = C.c_uint32()
+        self._check(self._L.gwaoi_space_create(self._w, C.c_float(aoi_distance), C.byref(s)))
+        return s.value
+
+    def space_destroy(self, space):
+        self._check(self._L.gwaoi_space_destroy(self._w, space))
+
+    def enter(self, space, slot, x, z):
+        self._check(self._L.gwaoi_enter(self._w, space, slot, C.c_float(x), C.c_float(z)))
+
+    def leave(self, slot):
+        self._check(self._L.gwaoi_leave(self._w, slot))
+
+    def moved(self, slot, x, z):
+        self._check(self._L.gwaoi_moved(self._w, slot, C.c_float(x), C.c_float(z)))
+
+    def enter_batch(self, space, slots, x, z):
+        s = np.ascontiguousarray(slots, np.uint32)
+        x = np.ascontiguousarray(x, np.float32)
+        z = np.ascontiguousarray(z, np.float32)
+        self._check(self._L.gwaoi_enter_batch(self._w, space, _p(s), _p(x), _p(z), s.size))
+
+    def leave_batch(self, slots):
+        s = np.ascontiguousarray(slots, np.uint32)
+        self._check(self._L.gwaoi_leave_batch(self._w, _p(s), s.size))
+
+    def moved_batch(self, slots, x, z):
+        s = np.ascontiguousarray(slots, np.uint32)
+        x = np.ascontiguousarray(x, np.float32)
+        z = np.ascontiguousarray(z, np.float32)
+        self._check(self._L.gwaoi_moved_batch(self._w, _p(s), _p(x), _p(z), s.size))
+
+    def moved_batch_device(self, d_slots: int, d_x: int, d_z: int, n: int):
+        self._check(self._L.gwaoi_moved_batch_device(self._w, C.c_void_p(d_slots), C.c_void_p(d_x),
+                                                     C.c_void_p(d_z), n))
+
+    # ---- flush
+    def tick(self):
+        """Flush; returns (enter_pairs, leave_pairs) as (n,2) uint32 arrays [a, b]."""
+        ev = Events()
+        self._check(self._L.gwaoi_tick(self._w, C.byref(ev)))
+        ne, nl = ev.n_enter, ev.n_leave
+        ent = np.ctypeslib.as_array(ev.enter, shape=(2 * ne,)).reshape(ne, 2).copy() if ne else np.empty((0, 2), np.uint32)
+        lev = np.ctypeslib.as_array(ev.leave, shape=(2 * nl,)).reshape(nl, 2).copy() if nl else np.empty((0, 2), np.uint32)
+        return ent, lev
+
+    def tick_device(self):
+        ne, nl = C.c_uint64(), C.c_uint64()
+        self._check(self._L.gwaoi_tick_device(self._w, C.byref(ne), C.byref(nl)))
+        return ne.value, nl.value
+
+    def events_device(self):
+        e, l = C.c_void_p(), C.c_void_p()
+        self._check(self._L.gwaoi_events_device(self._w, C.byref(e), C.byref(l)))
+        return e.value, l.value
+
+    # ---- queries
+    def neighbors(self, slot, cap=4096):
+        while True:
+            out = np.empty(cap, np.uint32)
+            n = C.c_size_t()
+            self._check(self._L.gwaoi_neighbors(self._w, slot, _p(out), cap, C.byref(n)))
+            if n.value <= cap:
+                return np.sort(out[:n.value])
+            cap = n.value
+
+    def info(self) -> dict:
+        i = Info()
+        self._check(self._L.gwaoi_world_info(self._w, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in Info._fields_}
+
+    def stage_times(self) -> dict:
+        arr = (StageTime * 32)()
+        n = C.c_size_t()
+        self._check(self._L.gwaoi_stage_times(self._w, arr, 32, C.byref(n)))
+        return {arr[i].name.decode(): (arr[i].ms, arr[i].calls) for i in range(min(n.value, 32))}
+
+    def reset_stage_times(self):
+        self._check(self._L.gwaoi_reset_stage_times(self._w))
+
+    def sync(self):
+        self._check(self._L.gwaoi_sync(self._w))
+
+    def stream(self) -> int:
+        return self._L.gwaoi_stream(self._w) or 0
+
+
+def pair_keys(pairs: np.ndarray) -> np.ndarray:
+    """(n,2) uint32 pairs -> sorted uint64 keys a<<32|b."""
+    if pairs.size == 0:
+        return np.empty(0, np.uint64)
+    k = (pairs[:, 0].astype(np.uint64) << np.uint64(32)) | pairs[:, 1].astype(np.uint64)
+    return np.sort(k)

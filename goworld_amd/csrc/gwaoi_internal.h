@@ -1,0 +1,103 @@
+// Internal types shared by the host world (gwaoi_world.cpp) and the HIP
+// kernels (gwaoi_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gw {
+
+constexpr uint32_t SP_DEAD = 0xFFFFFFFFu;  // slot not live (or left this tick)
+constexpr uint32_t SP_KEEP = 0xFFFFFFFEu;  // device move: keep the space of the previous flush
+
+// Device-side validation flags (bit set = problem seen during the tick).
+constexpr uint32_t ERR_NONFINITE = 1u;
+constexpr uint32_t ERR_MOVE_DEAD = 2u;  // device move of a slot that is not live
+constexpr uint32_t ERR_BAD_SLOT = 4u;
+constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreement (bug guard)
+
+// Uniform grid of one space for one flush.  Cell (cx,cz) of space s has the
+// global cell key base + cz*gx + cx.  cellOf() is monotone in the coordinate,
+// so a query range derived from conservative window bounds is complete.
+struct SpaceGrid {
+    float ox, oz;   // grid origin
+    float inv;      // 1 / cell size
+    float D;        // AOI distance of the space (go-aoi aoidist)
+    uint32_t gx, gz;
+    uint32_t base;
+    uint32_t pad;
+};
+
+// One flush's sorted state: entries [0, n) are the live entities ordered by
+// cell key (space-major, then cz, cx), stable in the previous order.
+struct FrameView {
+    const float *x, *z;
+    const uint64_t *seq;
+    const uint32_t *sp, *slot;
+    const uint32_t *cell_start;  // total_cells + 1 entries
+    const SpaceGrid *grid;
+    uint32_t n;
+    uint32_t total_cells;
+};
+
+// The state at the *other* time of a pair pass, stored in the frame's order.
+struct StateView {
+    const float *x, *z;
+    const uint64_t *seq;
+    const uint32_t *sp;
+};
+
+struct TickResult {  // device -> host summary of one tick
+    uint32_t n_enter;
+    uint32_t n_total;
+    uint32_t err;
+    uint32_t pad;
+    unsigned long long total64;
+};
+
+// ---- launchers (gwaoi_kernels.hip) ------------------------------------------
+void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, uint32_t *s_slot,
+                          uint32_t *s_sp, uint64_t *s_seq, uint32_t *rank, hipStream_t st);
+void launch_ops_claim(const uint32_t *op_slot, uint32_t n_ops, uint32_t max_slots,
+                      unsigned long long *lastop, uint32_t tick_id, uint32_t *err, hipStream_t st);
+void launch_ops_apply(const uint32_t *op_slot, const float *op_x, const float *op_z, const uint32_t *op_sp,
+                      uint32_t n_ops, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
+                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, float *s_x, float *s_z,
+                      uint64_t *s_seq, uint32_t *s_sp, const uint32_t *s_slot, uint32_t *err, hipStream_t st);
+void launch_keygen(const float *s_x, const float *s_z, const uint32_t *s_sp, uint32_t n_total,
+                   const SpaceGrid *grid, uint32_t sentinel, uint32_t *keys, uint32_t *vals, hipStream_t st);
+// LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
+// buffer (0 or 1) holds the result.
+struct SortBuffers {
+    uint32_t *keys[2];
+    uint32_t *vals[2];
+    uint32_t *hist;      // >= 256 * tiles
+    uint32_t *scan_tmp;  // scratch for the scan of hist
+    size_t scan_tmp_elems;
+};
+int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st);
+size_t radix_hist_elems(uint32_t n);
+// Exclusive scan (in place allowed); `tmp` needs scan_tmp_elems(n) uint32.
+void scan_exclusive(const uint32_t *in, uint32_t *out, size_t n, uint32_t *tmp, hipStream_t st);
+size_t scan_tmp_elems(size_t n);
+
+void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const float *s_x, const float *s_z,
+                   const uint64_t *s_seq, const uint32_t *s_sp, const uint32_t *s_slot, const float *p_x,
+                   const float *p_z, const uint64_t *p_seq, const uint32_t *p_sp, float *f_x, float *f_z,
+                   uint64_t *f_seq, uint32_t *f_sp, uint32_t *f_slot, float *o_x, float *o_z, uint64_t *o_seq,
+                   uint32_t *o_sp, uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel,
+                   uint32_t n_total, uint32_t *err, hipStream_t st);
+void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
+
+// mode 0 = enter pass (frame = new, other = old state); 1 = leave pass
+// (frame = previous, other = new state).  fill=false counts, fill=true writes.
+void launch_pairs(int mode, bool fill, FrameView F, StateView O, uint64_t seq_base, uint32_t *counts,
+                  const uint32_t *offsets, uint32_t *out_pairs, uint64_t out_cap,
+                  unsigned long long *total64, hipStream_t st);
+void launch_finish(const uint32_t *offsets, uint32_t n_new, uint32_t n_prev, const uint32_t *err,
+                   const unsigned long long *total64, TickResult *res, hipStream_t st);
+void launch_bbox(FrameView F, int *bbox, uint32_t max_spaces, hipStream_t st);
+void launch_neighbors(FrameView F, const uint32_t *rank, uint32_t slot, uint32_t *out, uint32_t cap,
+                      uint32_t *count, hipStream_t st);
+
+}  // namespace gw

@@ -1,0 +1,982 @@
+// gwaoi_world.cpp -- host side of libgwaoi: the C ABI of include/gwaoi.h.
+//
+// Mirrors go-aoi's AOIManager contract as GoWorld's Space drives it
+// (engine/entity/Space.go:105,211,221,243,259; callbacks Entity.go:227-246):
+// calls are queued in order with increasing sequence numbers and flushed by
+// gwaoi_tick(), which runs the HIP pipeline of gwaoi_kernels.hip and returns
+// the net enter/leave events.  Device state lives in HBM between flushes:
+// two sorted frames (previous / current) plus working buffers, all sized for
+// max_slots entities at creation so that a flush never allocates unless the
+// grid or the event buffer must grow.
+
+#include "gwaoi_internal.h"
+#include "../../include/gwaoi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <new>
+#include <string>
+#include <vector>
+
+using gw::SpaceGrid;
+
+namespace {
+
+enum Stage {
+    ST_APPLY,
+    ST_KEYGEN,
+    ST_SORT,
+    ST_GATHER,
+    ST_CELLS,
+    ST_ENTER_COUNT,
+    ST_LEAVE_COUNT,
+    ST_SCAN,
+    ST_ENTER_FILL,
+    ST_LEAVE_FILL,
+    ST_BBOX,
+    ST_D2H,
+    ST_N
+};
+const char *kStageNames[ST_N] = {"apply",      "keygen",      "sort",      "gather",     "cells",
+                                 "enter_count", "leave_count", "scan",      "enter_fill", "leave_fill",
+                                 "bbox",       "d2h"};
+
+struct DevFrame {
+    float *x = nullptr, *z = nullptr;
+    uint64_t *seq = nullptr;
+    uint32_t *sp = nullptr, *slot = nullptr;
+    uint32_t *cell_start = nullptr;
+    size_t cell_cap = 0;  // entries allocated in cell_start
+    SpaceGrid *grid = nullptr;
+    uint32_t n = 0;
+    uint32_t total_cells = 0;
+};
+
+struct SpaceHost {
+    bool used = false;
+    float D = 0.f;
+    uint32_t alive = 0;
+    bool have_bbox = false;  // device bbox of the last flush
+    float bx0 = 0, bz0 = 0, bx1 = 0, bz1 = 0;
+    bool pend = false;  // bbox of Enter positions queued since the last flush
+    float px0 = 0, pz0 = 0, px1 = 0, pz1 = 0;
+    SpaceGrid grid{};
+    bool grid_valid = false;
+};
+
+struct Run {  // a stretch of the op queue: host ops [hbegin, hend) or a device batch
+    bool device;
+    size_t hbegin, hend;
+    const uint32_t *ds;
+    const float *dx, *dz;
+    size_t dn;
+};
+
+}  // namespace
+
+struct gwaoi_world {
+    gwaoi_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t max_slots = 0, max_spaces = 0;
+    float cells_per_dist = 1.0f;
+
+    DevFrame fr[2];
+    int cur = 0;  // fr[cur] = frame of the last flush
+
+    // working set (max_slots entries each)
+    float *sx = nullptr, *sz = nullptr;
+    uint64_t *sseq = nullptr;
+    uint32_t *ssp = nullptr, *sslot = nullptr;
+    float *ox = nullptr, *oz = nullptr;
+    uint64_t *oseq = nullptr;
+    uint32_t *osp = nullptr;
+    uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
+    uint32_t *hist = nullptr;
+    uint32_t *scan_tmp = nullptr;
+    size_t scan_tmp_cap = 0;
+    uint32_t *rank = nullptr;
+    unsigned long long *lastop = nullptr;
+    uint32_t *new_slots_d = nullptr;
+    uint32_t *counts = nullptr;  // 2*max_slots + 1
+    uint32_t *op_slot = nullptr, *op_sp = nullptr;
+    float *op_x = nullptr, *op_z = nullptr;
+    size_t op_cap = 0;
+    uint32_t *events = nullptr;  // 2 * ev_cap uint32
+    uint64_t ev_cap = 0;
+    uint32_t *err = nullptr;
+    unsigned long long *total64 = nullptr;
+    gw::TickResult *res = nullptr;
+    int *bbox = nullptr;
+    uint32_t *nb_out = nullptr, *nb_count = nullptr;
+    size_t nb_cap = 0;
+
+    // pinned host mirrors
+    gw::TickResult *h_res = nullptr;
+    int *h_bbox = nullptr;
+    uint32_t *h_events = nullptr;
+    uint64_t h_ev_cap = 0;
+    SpaceGrid *h_grid = nullptr;
+
+    // host bookkeeping
+    std::vector<uint8_t> alive, in_frame, appended;
+    std::vector<uint32_t> space_of;
+    std::vector<SpaceHost> spaces;
+    uint32_t n_space_ids = 0;  // 1 + highest space id ever created
+    uint32_t n_spaces_live = 0;
+    std::vector<uint32_t> h_op_slot, h_op_sp;
+    std::vector<float> h_op_x, h_op_z;
+    std::vector<Run> runs;
+    size_t n_ops = 0;
+    std::vector<uint32_t> new_slots;
+    uint64_t seq_next = 1;
+    uint32_t tick_id = 0;
+    uint64_t ticks = 0;
+    uint32_t n_alive = 0;
+    uint64_t last_n_enter = 0, last_n_leave = 0;
+
+    // stage timing
+    bool timing = false;
+    hipEvent_t ev[ST_N][2] = {};
+    bool ev_used[ST_N] = {};
+    double stage_ms[ST_N] = {};
+    uint64_t stage_calls[ST_N] = {};
+
+    std::string last_error;
+};
+
+namespace {
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            w->last_error = std::string(#expr) + ": " + hipGetErrorString(e_);               \
+            return GWAOI_EDEVICE;                                                             \
+        }                                                                                     \
+    } while (0)
+
+template <class T>
+int dalloc(gwaoi_world *w, T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e != hipSuccess) {
+        w->last_error = std::string("hipMalloc: ") + hipGetErrorString(e);
+        *p = nullptr;
+        return e == hipErrorOutOfMemory ? GWAOI_ENOMEM : GWAOI_EDEVICE;
+    }
+    return GWAOI_OK;
+}
+
+template <class T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+inline bool finite2(float x, float z) { return std::isfinite(x) && std::isfinite(z); }
+
+void stage_begin(gwaoi_world *w, Stage s) {
+    if (!w->timing) return;
+    (void)hipEventRecord(w->ev[s][0], w->stream);
+    w->ev_used[s] = true;
+}
+void stage_end(gwaoi_world *w, Stage s) {
+    if (!w->timing) return;
+    (void)hipEventRecord(w->ev[s][1], w->stream);
+}
+void stage_collect(gwaoi_world *w) {
+    if (!w->timing) return;
+    for (int s = 0; s < ST_N; ++s) {
+        if (!w->ev_used[s]) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, w->ev[s][0], w->ev[s][1]) == hipSuccess) {
+            w->stage_ms[s] += ms;
+            w->stage_calls[s] += 1;
+        }
+        w->ev_used[s] = false;
+    }
+}
+
+int ensure_scan_tmp(gwaoi_world *w, size_t n) {
+    size_t need = gw::scan_tmp_elems(n) + 16;
+    if (need <= w->scan_tmp_cap) return GWAOI_OK;
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    dfree(w->scan_tmp);
+    int rc = dalloc(w, &w->scan_tmp, need);
+    if (rc) return rc;
+    w->scan_tmp_cap = need;
+    return GWAOI_OK;
+}
+
+int ensure_events(gwaoi_world *w, uint64_t pairs) {
+    if (pairs <= w->ev_cap) return GWAOI_OK;
+    uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, w->ev_cap * 2);
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    dfree(w->events);
+    int rc = dalloc(w, &w->events, 2 * cap);
+    if (rc) {
+        w->ev_cap = 0;
+        return rc;
+    }
+    w->ev_cap = cap;
+    return GWAOI_OK;
+}
+
+int ensure_host_events(gwaoi_world *w, uint64_t pairs) {
+    if (pairs <= w->h_ev_cap) return GWAOI_OK;
+    uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, 1024);
+    if (w->h_events) (void)hipHostFree(w->h_events);
+    w->h_events = nullptr;
+    w->h_ev_cap = 0;
+    HIP_TRY(hipHostMalloc((void **)&w->h_events, 2 * cap * sizeof(uint32_t), hipHostMallocDefault));
+    w->h_ev_cap = cap;
+    return GWAOI_OK;
+}
+
+int ensure_ops(gwaoi_world *w, size_t n) {
+    if (n <= w->op_cap) return GWAOI_OK;
+    size_t cap = std::max<size_t>(n, w->op_cap * 2);
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    dfree(w->op_slot);
+    dfree(w->op_sp);
+    dfree(w->op_x);
+    dfree(w->op_z);
+    int rc;
+    if ((rc = dalloc(w, &w->op_slot, cap)) || (rc = dalloc(w, &w->op_sp, cap)) || (rc = dalloc(w, &w->op_x, cap)) ||
+        (rc = dalloc(w, &w->op_z, cap))) {
+        w->op_cap = 0;
+        return rc;
+    }
+    w->op_cap = cap;
+    return GWAOI_OK;
+}
+
+int ensure_cells(gwaoi_world *w, DevFrame &f, size_t cells) {
+    size_t need = cells + 1;
+    if (need <= f.cell_cap) return GWAOI_OK;
+    size_t cap = std::max(need + need / 4, (size_t)1024);
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    dfree(f.cell_start);
+    int rc = dalloc(w, &f.cell_start, cap);
+    if (rc) {
+        f.cell_cap = 0;
+        return rc;
+    }
+    f.cell_cap = cap;
+    return GWAOI_OK;
+}
+
+void push_host_op(gwaoi_world *w, uint32_t slot, float x, float z, uint32_t sp) {
+    if (w->runs.empty() || w->runs.back().device) {
+        Run r{};
+        r.device = false;
+        r.hbegin = r.hend = w->h_op_slot.size();
+        w->runs.push_back(r);
+    }
+    w->h_op_slot.push_back(slot);
+    w->h_op_x.push_back(x);
+    w->h_op_z.push_back(z);
+    w->h_op_sp.push_back(sp);
+    w->runs.back().hend = w->h_op_slot.size();
+    w->n_ops++;
+}
+
+void note_pending_bbox(SpaceHost &S, float x, float z) {
+    if (!S.pend) {
+        S.pend = true;
+        S.px0 = S.px1 = x;
+        S.pz0 = S.pz1 = z;
+    } else {
+        S.px0 = std::min(S.px0, x);
+        S.px1 = std::max(S.px1, x);
+        S.pz0 = std::min(S.pz0, z);
+        S.pz1 = std::max(S.pz1, z);
+    }
+}
+
+void mark_appended(gwaoi_world *w, uint32_t slot) {
+    if (!w->in_frame[slot] && !w->appended[slot]) {
+        w->appended[slot] = 1;
+        w->new_slots.push_back(slot);
+    }
+}
+
+float o2f(int i) {
+    int b = i ^ ((i >> 31) & 0x7FFFFFFF);
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
+
+// Choose the grid of every space for the coming flush.  Any grid is correct
+// (cellOf is monotone and clamped); this only keeps cells near D wide and the
+// cell count bounded by the population.
+void choose_grids(gwaoi_world *w, uint32_t &total_cells) {
+    uint32_t base = 0;
+    for (uint32_t s = 0; s < w->n_space_ids; ++s) {
+        SpaceHost &S = w->spaces[s];
+        SpaceGrid g{};
+        g.D = S.used ? S.D : 1.0f;
+        bool have = false;
+        float x0 = 0, z0 = 0, x1 = 0, z1 = 0;
+        if (S.used && S.have_bbox && S.alive) {
+            have = true;
+            x0 = S.bx0; z0 = S.bz0; x1 = S.bx1; z1 = S.bz1;
+        }
+        if (S.used && S.pend) {
+            if (!have) {
+                x0 = S.px0; z0 = S.pz0; x1 = S.px1; z1 = S.pz1;
+                have = true;
+            } else {
+                x0 = std::min(x0, S.px0); z0 = std::min(z0, S.pz0);
+                x1 = std::max(x1, S.px1); z1 = std::max(z1, S.pz1);
+            }
+        }
+        if (!S.used || !have || S.alive == 0) {
+            g.ox = g.oz = 0.f;
+            g.inv = 1.0f / g.D;
+            g.gx = g.gz = 1;
+        } else {
+            const double cap = std::max(64.0, 4.0 * (double)S.alive);
+            bool keep = false;
+            if (S.grid_valid) {
+                const SpaceGrid &o = S.grid;
+                const double C = 1.0 / (double)o.inv;
+                const double ex1 = o.ox + C * o.gx, ez1 = o.oz + C * o.gz;
+                const bool inside = x0 >= o.ox && z0 >= o.oz && x1 <= ex1 && z1 <= ez1;
+                const double area_grid = (double)o.gx * o.gz * C * C;
+                const double area_box = ((double)x1 - x0 + 4.0 * g.D) * ((double)z1 - z0 + 4.0 * g.D);
+                keep = inside && (double)o.gx * o.gz <= cap && area_grid <= 4.0 * area_box + 1.0;
+            }
+            if (keep) {
+                g = S.grid;
+            } else {
+                const double m = 2.0 * g.D;
+                const double ox = (double)x0 - m, oz = (double)z0 - m;
+                const double wdt = (double)x1 - x0 + 2 * m, hgt = (double)z1 - z0 + 2 * m;
+                double C = (double)g.D / (double)w->cells_per_dist;
+                double gx, gz;
+                for (;;) {
+                    gx = std::max(1.0, std::ceil(wdt / C));
+                    gz = std::max(1.0, std::ceil(hgt / C));
+                    if (gx * gz <= cap && gx <= 32768 && gz <= 32768) break;
+                    C *= 1.25;
+                }
+                g.ox = (float)ox;
+                g.oz = (float)oz;
+                g.inv = (float)(1.0 / C);
+                g.gx = (uint32_t)gx;
+                g.gz = (uint32_t)gz;
+            }
+        }
+        g.base = base;
+        base += g.gx * g.gz;
+        w->h_grid[s] = g;
+        if (S.used && S.alive) {
+            S.grid = g;
+            S.grid_valid = true;
+        } else {
+            S.grid_valid = false;
+        }
+    }
+    total_cells = base;
+}
+
+gw::FrameView view_of(const DevFrame &f) {
+    gw::FrameView v;
+    v.x = f.x;
+    v.z = f.z;
+    v.seq = f.seq;
+    v.sp = f.sp;
+    v.slot = f.slot;
+    v.cell_start = f.cell_start;
+    v.grid = f.grid;
+    v.n = f.n;
+    v.total_cells = f.total_cells;
+    return v;
+}
+
+int bitlen(uint32_t v) {
+    int b = 0;
+    while (v) {
+        ++b;
+        v >>= 1;
+    }
+    return b;
+}
+
+// The flush.  On return the events of this tick are in w->events (device).
+int run_tick(gwaoi_world *w) {
+    hipStream_t st = w->stream;
+    int rc;
+    const uint32_t tick_id = ++w->tick_id;
+    const uint64_t seq_base = w->seq_next;
+    const uint32_t n_ops = (uint32_t)w->n_ops;
+    w->seq_next += n_ops;
+
+    DevFrame &P = w->fr[w->cur];      // previous flush
+    DevFrame &Fn = w->fr[w->cur ^ 1]; // this flush
+    const uint32_t n_prev = P.n;
+    const uint32_t n_app = (uint32_t)w->new_slots.size();
+    const uint32_t n_total = n_prev + n_app;
+    const uint32_t n_new = w->n_alive;
+
+    // grid for this flush
+    uint32_t total_cells = 0;
+    choose_grids(w, total_cells);
+    if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
+    if ((rc = ensure_ops(w, n_ops))) return rc;
+    const size_t scan_need = std::max<size_t>({gw::radix_hist_elems(std::max(n_total, 1u)),
+                                               (size_t)n_new + n_prev + 1, (size_t)total_cells + 1});
+    if ((rc = ensure_scan_tmp(w, scan_need))) return rc;
+    Fn.total_cells = total_cells;
+    Fn.n = n_new;
+
+    HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * std::max(1u, w->n_space_ids),
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(w->err, 0, sizeof(uint32_t), st));
+    HIP_TRY(hipMemsetAsync(w->total64, 0, sizeof(unsigned long long), st));
+
+    // ---- apply queued ops onto S' = copy of the previous frame
+    stage_begin(w, ST_APPLY);
+    if (n_prev) {
+        HIP_TRY(hipMemcpyAsync(w->sx, P.x, n_prev * sizeof(float), hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->sz, P.z, n_prev * sizeof(float), hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->sseq, P.seq, n_prev * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->ssp, P.sp, n_prev * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->sslot, P.slot, n_prev * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    }
+    if (n_app) {
+        HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, st));
+        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->sslot, w->ssp, w->sseq, w->rank, st);
+    }
+    if (n_ops) {
+        size_t at = 0;
+        for (const Run &r : w->runs) {
+            if (!r.device) {
+                const size_t k = r.hend - r.hbegin;
+                HIP_TRY(hipMemcpyAsync(w->op_slot + at, w->h_op_slot.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+                HIP_TRY(hipMemcpyAsync(w->op_x + at, w->h_op_x.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+                HIP_TRY(hipMemcpyAsync(w->op_z + at, w->h_op_z.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+                HIP_TRY(hipMemcpyAsync(w->op_sp + at, w->h_op_sp.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+                at += k;
+            } else {
+                HIP_TRY(hipMemcpyAsync(w->op_slot + at, r.ds, r.dn * 4, hipMemcpyDeviceToDevice, st));
+                HIP_TRY(hipMemcpyAsync(w->op_x + at, r.dx, r.dn * 4, hipMemcpyDeviceToDevice, st));
+                HIP_TRY(hipMemcpyAsync(w->op_z + at, r.dz, r.dn * 4, hipMemcpyDeviceToDevice, st));
+                HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->op_sp + at), (int)gw::SP_KEEP, r.dn, st));
+                at += r.dn;
+            }
+        }
+        gw::launch_ops_claim(w->op_slot, n_ops, w->max_slots, w->lastop, tick_id, w->err, st);
+        gw::launch_ops_apply(w->op_slot, w->op_x, w->op_z, w->op_sp, n_ops, w->max_slots, w->lastop, tick_id,
+                             w->rank, n_total, seq_base, w->sx, w->sz, w->sseq, w->ssp, w->sslot, w->err, st);
+    }
+    stage_end(w, ST_APPLY);
+
+    // ---- keys + stable sort
+    stage_begin(w, ST_KEYGEN);
+    gw::launch_keygen(w->sx, w->sz, w->ssp, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], st);
+    stage_end(w, ST_KEYGEN);
+    stage_begin(w, ST_SORT);
+    gw::SortBuffers sb;
+    sb.keys[0] = w->keys[0];
+    sb.keys[1] = w->keys[1];
+    sb.vals[0] = w->vals[0];
+    sb.vals[1] = w->vals[1];
+    sb.hist = w->hist;
+    sb.scan_tmp = w->scan_tmp;
+    sb.scan_tmp_elems = w->scan_tmp_cap;
+    const int which = gw::radix_sort(sb, n_total, bitlen(total_cells), st);
+    stage_end(w, ST_SORT);
+    const uint32_t *skeys = w->keys[which];
+    const uint32_t *perm = w->vals[which];
+
+    // ---- new frame + old state in the new order
+    stage_begin(w, ST_GATHER);
+    gw::launch_gather(perm, n_new, n_prev, w->sx, w->sz, w->sseq, w->ssp, w->sslot, P.x, P.z, P.seq, P.sp, Fn.x,
+                      Fn.z, Fn.seq, Fn.sp, Fn.slot, w->ox, w->oz, w->oseq, w->osp, w->rank, skeys, total_cells,
+                      n_total, w->err, st);
+    stage_end(w, ST_GATHER);
+
+    // ---- cell_start = exclusive scan of entities per cell
+    stage_begin(w, ST_CELLS);
+    HIP_TRY(hipMemsetAsync(Fn.cell_start, 0, ((size_t)total_cells + 1) * sizeof(uint32_t), st));
+    gw::launch_cell_count(skeys, n_new, Fn.cell_start, st);
+    gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
+    stage_end(w, ST_CELLS);
+
+    // ---- pair passes
+    gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
+    gw::StateView old_in_new{w->ox, w->oz, w->oseq, w->osp};
+    gw::StateView new_in_prev{w->sx, w->sz, w->sseq, w->ssp};
+    uint32_t *cnt_enter = w->counts;
+    uint32_t *cnt_leave = w->counts + n_new;
+    stage_begin(w, ST_ENTER_COUNT);
+    gw::launch_pairs(0, false, Vn, old_in_new, seq_base, cnt_enter, nullptr, nullptr, 0, w->total64, st);
+    stage_end(w, ST_ENTER_COUNT);
+    stage_begin(w, ST_LEAVE_COUNT);
+    gw::launch_pairs(1, false, Vp, new_in_prev, seq_base, cnt_leave, nullptr, nullptr, 0, w->total64, st);
+    stage_end(w, ST_LEAVE_COUNT);
+    stage_begin(w, ST_SCAN);
+    HIP_TRY(hipMemsetAsync(w->counts + (size_t)n_new + n_prev, 0, sizeof(uint32_t), st));
+    gw::scan_exclusive(w->counts, w->counts, (size_t)n_new + n_prev + 1, w->scan_tmp, st);
+    stage_end(w, ST_SCAN);
+    stage_begin(w, ST_ENTER_FILL);
+    gw::launch_pairs(0, true, Vn, old_in_new, seq_base, nullptr, w->counts, w->events, w->ev_cap, nullptr, st);
+    stage_end(w, ST_ENTER_FILL);
+    stage_begin(w, ST_LEAVE_FILL);
+    gw::launch_pairs(1, true, Vp, new_in_prev, seq_base, nullptr, w->counts + n_new, w->events, w->ev_cap, nullptr,
+                     st);
+    stage_end(w, ST_LEAVE_FILL);
+    gw::launch_finish(w->counts, n_new, n_prev, w->err, w->total64, w->res, st);
+
+    // ---- per-space bounding boxes for the next flush's grid
+    stage_begin(w, ST_BBOX);
+    if (w->n_space_ids) {
+        const uint32_t ms = w->max_spaces;
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)w->bbox, 0x7FFFFFFF, (size_t)2 * ms, st));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->bbox + 2 * (size_t)ms), (int)0x80000000, (size_t)2 * ms, st));
+        gw::launch_bbox(Vn, w->bbox, ms, st);
+        for (int q = 0; q < 4; ++q)
+            HIP_TRY(hipMemcpyAsync(w->h_bbox + (size_t)q * ms, w->bbox + (size_t)q * ms,
+                                   w->n_space_ids * sizeof(int), hipMemcpyDeviceToHost, st));
+    }
+    stage_end(w, ST_BBOX);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(w->h_res, w->res, sizeof(gw::TickResult), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+
+    const gw::TickResult r = *w->h_res;
+    if (r.total64 > 0xFFFFFFFFull) {
+        w->last_error = "more than 2^32-1 events in one flush";
+        return GWAOI_ECAPACITY;
+    }
+    if ((uint64_t)r.n_total > w->ev_cap) {  // grow and re-run the fill passes
+        if ((rc = ensure_events(w, r.n_total))) return rc;
+        gw::launch_pairs(0, true, Vn, old_in_new, seq_base, nullptr, w->counts, w->events, w->ev_cap, nullptr, st);
+        gw::launch_pairs(1, true, Vp, new_in_prev, seq_base, nullptr, w->counts + n_new, w->events, w->ev_cap,
+                         nullptr, st);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    stage_collect(w);
+
+    // ---- commit host bookkeeping
+    w->last_n_enter = r.n_enter;
+    w->last_n_leave = (uint64_t)r.n_total - r.n_enter;
+    for (uint32_t s = 0; s < w->n_space_ids; ++s) {
+        SpaceHost &S = w->spaces[s];
+        S.pend = false;
+        const int ix0 = w->h_bbox[s], iz0 = w->h_bbox[w->max_spaces + s];
+        const int ix1 = w->h_bbox[2 * w->max_spaces + s], iz1 = w->h_bbox[3 * w->max_spaces + s];
+        if (S.used && S.alive && ix0 != 0x7FFFFFFF) {
+            S.have_bbox = true;
+            S.bx0 = o2f(ix0);
+            S.bz0 = o2f(iz0);
+            S.bx1 = o2f(ix1);
+            S.bz1 = o2f(iz1);
+        } else {
+            S.have_bbox = false;
+        }
+    }
+    for (uint32_t s : w->new_slots) w->appended[s] = 0;
+    w->new_slots.clear();
+    std::memcpy(w->in_frame.data(), w->alive.data(), w->max_slots);
+    w->h_op_slot.clear();
+    w->h_op_x.clear();
+    w->h_op_z.clear();
+    w->h_op_sp.clear();
+    w->runs.clear();
+    w->n_ops = 0;
+    w->cur ^= 1;
+    w->ticks++;
+    if (r.err & gw::ERR_COUNT_MISMATCH) {
+        w->last_error = "internal: live-count mismatch between host and device";
+        return GWAOI_EDEVICE;
+    }
+    if (r.err & gw::ERR_NONFINITE) {
+        w->last_error = "device batch held a non-finite coordinate (move dropped)";
+        return GWAOI_ENONFINITE;
+    }
+    if (r.err & (gw::ERR_MOVE_DEAD | gw::ERR_BAD_SLOT)) {
+        w->last_error = "device batch moved a slot that is not live (move dropped)";
+        return GWAOI_ESTATE;
+    }
+    return GWAOI_OK;
+}
+
+}  // namespace
+
+// =============================================================== C ABI =======
+
+extern "C" {
+
+int gwaoi_abi_version(void) { return GWAOI_ABI_VERSION; }
+
+const char *gwaoi_strerror(int s) {
+    switch (s) {
+        case GWAOI_OK: return "ok";
+        case GWAOI_EINVAL: return "invalid argument";
+        case GWAOI_EBADSLOT: return "slot out of range";
+        case GWAOI_ESTATE: return "slot in wrong state (Enter on live / Leave or Moved on non-live)";
+        case GWAOI_ENOMEM: return "out of memory";
+        case GWAOI_EDEVICE: return "HIP device error";
+        case GWAOI_ENONFINITE: return "non-finite coordinate";
+        case GWAOI_EBADSPACE: return "unknown space";
+        case GWAOI_EBUSY: return "space not empty";
+        case GWAOI_ECAPACITY: return "event capacity exceeded";
+        default: return "unknown status";
+    }
+}
+
+const char *gwaoi_last_error(gwaoi_world *w) { return w ? w->last_error.c_str() : "null world"; }
+
+int gwaoi_world_destroy(gwaoi_world *w) {
+    if (!w) return GWAOI_EINVAL;
+    if (w->stream) (void)hipStreamSynchronize(w->stream);
+    for (DevFrame &f : w->fr) {
+        dfree(f.x); dfree(f.z); dfree(f.seq); dfree(f.sp); dfree(f.slot); dfree(f.cell_start); dfree(f.grid);
+    }
+    dfree(w->sx); dfree(w->sz); dfree(w->sseq); dfree(w->ssp); dfree(w->sslot);
+    dfree(w->ox); dfree(w->oz); dfree(w->oseq); dfree(w->osp);
+    for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
+    dfree(w->hist); dfree(w->scan_tmp); dfree(w->rank); dfree(w->lastop); dfree(w->new_slots_d);
+    dfree(w->counts); dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
+    dfree(w->events); dfree(w->err); dfree(w->total64); dfree(w->res); dfree(w->bbox);
+    dfree(w->nb_out); dfree(w->nb_count);
+    if (w->h_res) (void)hipHostFree(w->h_res);
+    if (w->h_bbox) (void)hipHostFree(w->h_bbox);
+    if (w->h_events) (void)hipHostFree(w->h_events);
+    if (w->h_grid) (void)hipHostFree(w->h_grid);
+    for (int s = 0; s < ST_N; ++s)
+        for (int q = 0; q < 2; ++q)
+            if (w->ev[s][q]) (void)hipEventDestroy(w->ev[s][q]);
+    if (w->stream) (void)hipStreamDestroy(w->stream);
+    delete w;
+    return GWAOI_OK;
+}
+
+int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
+    if (!cfg || !out || cfg->max_slots == 0 || cfg->max_spaces == 0 || cfg->max_slots > 0x7FFFFFF0u)
+        return GWAOI_EINVAL;
+    *out = nullptr;
+    gwaoi_world *w = new (std::nothrow) gwaoi_world();
+    if (!w) return GWAOI_ENOMEM;
+    w->cfg = *cfg;
+    w->max_slots = cfg->max_slots;
+    w->max_spaces = cfg->max_spaces;
+    w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 1.0f;
+    w->timing = (cfg->flags & GWAOI_F_TIMING) != 0;
+    int rc = GWAOI_OK;
+    auto fail = [&](int code) {
+        gwaoi_world_destroy(w);
+        return code;
+    };
+    if (cfg->device >= 0) {
+        hipError_t e = hipSetDevice(cfg->device);
+        if (e != hipSuccess) {
+            delete w;
+            return GWAOI_EDEVICE;
+        }
+    }
+    if (hipGetDevice(&w->device) != hipSuccess) {
+        delete w;
+        return GWAOI_EDEVICE;
+    }
+    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+        w->stream = nullptr;
+        return fail(GWAOI_EDEVICE);
+    }
+    const size_t N = w->max_slots;
+    for (DevFrame &f : w->fr) {
+        if ((rc = dalloc(w, &f.x, N)) || (rc = dalloc(w, &f.z, N)) || (rc = dalloc(w, &f.seq, N)) ||
+            (rc = dalloc(w, &f.sp, N)) || (rc = dalloc(w, &f.slot, N)) || (rc = dalloc(w, &f.grid, w->max_spaces)))
+            return fail(rc);
+        if ((rc = ensure_cells(w, f, 1))) return fail(rc);
+    }
+    if ((rc = dalloc(w, &w->sx, N)) || (rc = dalloc(w, &w->sz, N)) || (rc = dalloc(w, &w->sseq, N)) ||
+        (rc = dalloc(w, &w->ssp, N)) || (rc = dalloc(w, &w->sslot, N)) || (rc = dalloc(w, &w->ox, N)) ||
+        (rc = dalloc(w, &w->oz, N)) || (rc = dalloc(w, &w->oseq, N)) || (rc = dalloc(w, &w->osp, N)) ||
+        (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
+        (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
+        (rc = dalloc(w, &w->rank, N)) || (rc = dalloc(w, &w->lastop, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||
+        (rc = dalloc(w, &w->counts, 2 * N + 1)) || (rc = dalloc(w, &w->err, 1)) || (rc = dalloc(w, &w->total64, 1)) ||
+        (rc = dalloc(w, &w->res, 1)) || (rc = dalloc(w, &w->bbox, 4 * (size_t)w->max_spaces)) ||
+        (rc = dalloc(w, &w->nb_count, 1)))
+        return fail(rc);
+    if (hipMemset(w->lastop, 0, N * sizeof(unsigned long long)) != hipSuccess) return fail(GWAOI_EDEVICE);
+    if (hipMemset(w->rank, 0xFF, N * sizeof(uint32_t)) != hipSuccess) return fail(GWAOI_EDEVICE);
+    if ((rc = ensure_scan_tmp(w, std::max<size_t>(2 * N + 1, gw::radix_hist_elems((uint32_t)N))))) return fail(rc);
+    if ((rc = ensure_ops(w, 1024))) return fail(rc);
+    if ((rc = ensure_events(w, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
+        return fail(rc);
+    if (hipHostMalloc((void **)&w->h_res, sizeof(gw::TickResult), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&w->h_bbox, 4 * sizeof(int) * w->max_spaces, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
+        return fail(GWAOI_ENOMEM);
+    if (w->timing) {
+        for (int s = 0; s < ST_N; ++s)
+            for (int q = 0; q < 2; ++q)
+                if (hipEventCreate(&w->ev[s][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
+    }
+    w->alive.assign(N, 0);
+    w->in_frame.assign(N, 0);
+    w->appended.assign(N, 0);
+    w->space_of.assign(N, gw::SP_DEAD);
+    w->spaces.resize(w->max_spaces);
+    *out = w;
+    return GWAOI_OK;
+}
+
+int gwaoi_space_create(gwaoi_world *w, float d, uint32_t *space_out) {
+    if (!w || !space_out) return GWAOI_EINVAL;
+    if (!(d > 0.f) || !std::isfinite(d)) return GWAOI_EINVAL;  // "defaultAOIDistance < 0" panic, Space.go:92-94
+    for (uint32_t s = 0; s < w->max_spaces; ++s) {
+        SpaceHost &S = w->spaces[s];
+        if (S.used) continue;
+        // an id freed in this flush may still own pairs in the previous frame
+        if (s < w->n_space_ids && S.grid_valid) continue;
+        S = SpaceHost();
+        S.used = true;
+        S.D = d;
+        w->n_space_ids = std::max(w->n_space_ids, s + 1);
+        w->n_spaces_live++;
+        *space_out = s;
+        return GWAOI_OK;
+    }
+    return GWAOI_EBADSPACE;
+}
+
+int gwaoi_space_destroy(gwaoi_world *w, uint32_t space) {
+    if (!w) return GWAOI_EINVAL;
+    if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
+    if (w->spaces[space].alive) return GWAOI_EBUSY;
+    w->spaces[space].used = false;
+    w->n_spaces_live--;
+    return GWAOI_OK;
+}
+
+int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z) {
+    if (!w) return GWAOI_EINVAL;
+    if (slot >= w->max_slots) return GWAOI_EBADSLOT;
+    if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
+    if (w->alive[slot]) return GWAOI_ESTATE;
+    if (!finite2(x, z)) return GWAOI_ENONFINITE;
+    w->alive[slot] = 1;
+    w->space_of[slot] = space;
+    w->n_alive++;
+    SpaceHost &S = w->spaces[space];
+    S.alive++;
+    note_pending_bbox(S, x, z);
+    mark_appended(w, slot);
+    push_host_op(w, slot, x, z, space);
+    return GWAOI_OK;
+}
+
+int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
+    if (!w) return GWAOI_EINVAL;
+    if (slot >= w->max_slots) return GWAOI_EBADSLOT;
+    if (!w->alive[slot]) return GWAOI_ESTATE;
+    w->alive[slot] = 0;
+    w->spaces[w->space_of[slot]].alive--;
+    w->space_of[slot] = gw::SP_DEAD;
+    w->n_alive--;
+    push_host_op(w, slot, 0.f, 0.f, gw::SP_DEAD);
+    return GWAOI_OK;
+}
+
+int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z) {
+    if (!w) return GWAOI_EINVAL;
+    if (slot >= w->max_slots) return GWAOI_EBADSLOT;
+    if (!w->alive[slot]) return GWAOI_ESTATE;
+    if (!finite2(x, z)) return GWAOI_ENONFINITE;
+    note_pending_bbox(w->spaces[w->space_of[slot]], x, z);
+    push_host_op(w, slot, x, z, w->space_of[slot]);
+    return GWAOI_OK;
+}
+
+int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, const float *x, const float *z,
+                      size_t n) {
+    if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
+    if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
+    // validate the whole batch first (duplicates inside the batch are Enter-twice)
+    std::vector<uint32_t> seen;
+    seen.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
+        if (w->alive[slots[i]]) return GWAOI_ESTATE;
+        if (!finite2(x[i], z[i])) return GWAOI_ENONFINITE;
+        seen.push_back(slots[i]);
+    }
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return GWAOI_ESTATE;
+    for (size_t i = 0; i < n; ++i) gwaoi_enter(w, space, slots[i], x[i], z[i]);
+    return GWAOI_OK;
+}
+
+int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
+    if (!w || (n && !slots)) return GWAOI_EINVAL;
+    std::vector<uint32_t> seen(slots, slots + n);
+    for (size_t i = 0; i < n; ++i) {
+        if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
+        if (!w->alive[slots[i]]) return GWAOI_ESTATE;
+    }
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return GWAOI_ESTATE;
+    for (size_t i = 0; i < n; ++i) gwaoi_leave(w, slots[i]);
+    return GWAOI_OK;
+}
+
+int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
+    if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
+    for (size_t i = 0; i < n; ++i) {
+        if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
+        if (!w->alive[slots[i]]) return GWAOI_ESTATE;
+        if (!finite2(x[i], z[i])) return GWAOI_ENONFINITE;
+    }
+    for (size_t i = 0; i < n; ++i) gwaoi_moved(w, slots[i], x[i], z[i]);
+    return GWAOI_OK;
+}
+
+int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
+                             size_t n) {
+    if (!w || (n && (!d_slots || !d_x || !d_z))) return GWAOI_EINVAL;
+    if (!n) return GWAOI_OK;
+    if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
+    Run r{};
+    r.device = true;
+    r.ds = d_slots;
+    r.dx = d_x;
+    r.dz = d_z;
+    r.dn = n;
+    w->runs.push_back(r);
+    w->n_ops += n;
+    return GWAOI_OK;
+}
+
+int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    if (!w) return GWAOI_EINVAL;
+    int rc = run_tick(w);
+    if (n_enter) *n_enter = w->last_n_enter;
+    if (n_leave) *n_leave = w->last_n_leave;
+    return rc;
+}
+
+int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave) {
+    if (!w) return GWAOI_EINVAL;
+    if (d_enter) *d_enter = w->events;
+    if (d_leave) *d_leave = w->events + 2 * w->last_n_enter;
+    return GWAOI_OK;
+}
+
+int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
+    if (!w || !out) return GWAOI_EINVAL;
+    int rc = run_tick(w);
+    const uint64_t tot = w->last_n_enter + w->last_n_leave;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    if (rc != GWAOI_OK && rc != GWAOI_ESTATE && rc != GWAOI_ENONFINITE) return rc;
+    int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1));
+    if (rc2) return rc2;
+    stage_begin(w, ST_D2H);
+    if (tot) {
+        hipError_t e = hipMemcpyAsync(w->h_events, w->events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                      w->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+        if (e != hipSuccess) {
+            w->last_error = std::string("event D2H: ") + hipGetErrorString(e);
+            return GWAOI_EDEVICE;
+        }
+    }
+    stage_end(w, ST_D2H);
+    if (w->timing) {
+        (void)hipStreamSynchronize(w->stream);
+        stage_collect(w);
+    }
+    out->n_enter = w->last_n_enter;
+    out->n_leave = w->last_n_leave;
+    out->enter = w->h_events;
+    out->leave = w->h_events + 2 * w->last_n_enter;
+    return rc;
+}
+
+int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, size_t *n_out) {
+    if (!w || (cap && !out)) return GWAOI_EINVAL;
+    if (slot >= w->max_slots) return GWAOI_EBADSLOT;
+    if (n_out) *n_out = 0;
+    if (!w->in_frame[slot]) return GWAOI_ESTATE;
+    const size_t need = std::max<size_t>(cap, 1);
+    if (need > w->nb_cap) {
+        dfree(w->nb_out);
+        int rc = dalloc(w, &w->nb_out, need);
+        if (rc) return rc;
+        w->nb_cap = need;
+    }
+    const DevFrame &F = w->fr[w->cur];
+    HIP_TRY(hipMemsetAsync(w->nb_count, 0, sizeof(uint32_t), w->stream));
+    gw::launch_neighbors(view_of(F), w->rank, slot, w->nb_out, (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu),
+                         w->nb_count, w->stream);
+    HIP_TRY(hipGetLastError());
+    uint32_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, w->nb_count, sizeof(uint32_t), hipMemcpyDeviceToHost, w->stream));
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    const size_t k = std::min<size_t>(cnt, cap);
+    if (k) {
+        HIP_TRY(hipMemcpyAsync(out, w->nb_out, k * sizeof(uint32_t), hipMemcpyDeviceToHost, w->stream));
+        HIP_TRY(hipStreamSynchronize(w->stream));
+    }
+    if (n_out) *n_out = cnt;
+    return GWAOI_OK;
+}
+
+int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
+    if (!w || !info) return GWAOI_EINVAL;
+    info->ticks = w->ticks;
+    info->next_seq = w->seq_next + w->n_ops;
+    info->live = w->fr[w->cur].n;
+    info->spaces = w->n_spaces_live;
+    info->total_cells = w->fr[w->cur].total_cells;
+    info->pending_ops = (uint32_t)w->n_ops;
+    info->event_capacity = w->ev_cap;
+    return GWAOI_OK;
+}
+
+int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t *n_out) {
+    if (!w) return GWAOI_EINVAL;
+    size_t k = std::min<size_t>(cap, ST_N);
+    for (size_t i = 0; i < k; ++i) {
+        std::snprintf(out[i].name, sizeof(out[i].name), "%s", kStageNames[i]);
+        out[i].ms = w->stage_ms[i];
+        out[i].calls = w->stage_calls[i];
+    }
+    if (n_out) *n_out = ST_N;
+    return GWAOI_OK;
+}
+
+int gwaoi_reset_stage_times(gwaoi_world *w) {
+    if (!w) return GWAOI_EINVAL;
+    for (int s = 0; s < ST_N; ++s) {
+        w->stage_ms[s] = 0;
+        w->stage_calls[s] = 0;
+    }
+    return GWAOI_OK;
+}
+
+int gwaoi_sync(gwaoi_world *w) {
+    if (!w) return GWAOI_EINVAL;
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    return GWAOI_OK;
+}
+
+void *gwaoi_stream(gwaoi_world *w) { return w ? (void *)w->stream : nullptr; }
+
+}  // extern "C"

@@ -1,0 +1,159 @@
+/*
+ * gwaoi.h -- C ABI of the MI355X-native AOI engine for GoWorld (libgwaoi.so).
+ *
+ * Drop-in boundary for GoWorld's `aoi.AOIManager` (go-aoi v0.2.0,
+ * /root/reference/go.mod:29) as engine/entity/Space drives it:
+ *
+ *   reference call                                   replaced by
+ *   ---------------------------------------------   -------------------------------
+ *   aoi.NewXZListAOIManager(d)   Space.go:105         gwaoi_space_create
+ *   (space destroyed)            Space.go:33          gwaoi_space_destroy
+ *   aoiMgr.Enter(&e.aoi, x, z)   Space.go:211,221     gwaoi_enter / gwaoi_enter_batch
+ *   aoiMgr.Leave(&e.aoi)         Space.go:243         gwaoi_leave / gwaoi_leave_batch
+ *   aoiMgr.Moved(&e.aoi, x, z)   Space.go:259         gwaoi_moved / gwaoi_moved_batch(_device)
+ *   AOICallback.OnEnterAOI(o)    Entity.go:227-229    replay of gwaoi_events.enter
+ *   AOICallback.OnLeaveAOI(o)    Entity.go:231-233    replay of gwaoi_events.leave
+ *   aoi.InitAOI(&e.aoi, ...)     Entity.go:210        caller-side slot handle (uint32)
+ *
+ * Semantics.  A world holds many independent spaces (one go-aoi manager
+ * each).  Enter/Leave/Moved are queued in call order; each call gets the next
+ * sequence number, exactly as the sequential manager would process it.
+ * gwaoi_tick() flushes the queue: it computes the neighbour relation of every
+ * space at the queued state on the GPU and returns the NET enter/leave events
+ * since the previous flush.  After replaying them (leaves first, then enters)
+ * the callers' InterestedIn/InterestedBy sets are bit-identical to those the
+ * sequential XZListAOIManager produces for the same call sequence: pair {A,B}
+ * is a neighbour iff P_W(L) holds at the current positions, W being the one
+ * of A,B whose Enter/Moved came last and
+ *     P_W(L) = L.x >= fl32(W.x-D) && L.x <= fl32(W.x+D)
+ *           && L.z >= fl32(W.z-D) && L.z <= fl32(W.z+D)        (float32).
+ * A transient enter+leave of one pair inside one flush is not reported (the
+ * reference would emit both callbacks; the final sets are the same).
+ *
+ * Slots.  Go pointers cannot be retained by C (cgo rule), so entities are
+ * named by caller-chosen uint32 slots in [0, max_slots).  A slot may not be
+ * reused for a different entity before the next flush.
+ *
+ * Errors.  Every call returns 0 or a negative gwaoi_status and never aborts.
+ * Misuse that panics in the reference (Moved/Leave before Enter, Enter twice,
+ * EnableAOI with d <= 0, Space.go:92-102) returns GWAOI_ESTATE / GWAOI_EINVAL.
+ *
+ * Threading.  A world is single-threaded (GoWorld's GameService goroutine,
+ * components/game/GameService.go:88-186); it owns one HIP stream on one GPU.
+ */
+#ifndef GWAOI_H
+#define GWAOI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GWAOI_ABI_VERSION 1
+
+typedef struct gwaoi_world gwaoi_world;
+
+typedef enum {
+    GWAOI_OK = 0,
+    GWAOI_EINVAL = -1,     /* null pointer, bad size, aoi distance <= 0          */
+    GWAOI_EBADSLOT = -2,   /* slot >= max_slots                                   */
+    GWAOI_ESTATE = -3,     /* Enter on a live slot; Leave/Moved on a non-live one */
+    GWAOI_ENOMEM = -4,     /* host or device allocation failed                    */
+    GWAOI_EDEVICE = -5,    /* HIP runtime error (see gwaoi_last_error)            */
+    GWAOI_ENONFINITE = -6, /* NaN or infinite coordinate                          */
+    GWAOI_EBADSPACE = -7,  /* unknown / destroyed space id, or too many spaces    */
+    GWAOI_EBUSY = -8,      /* space destroyed while entities are still in it      */
+    GWAOI_ECAPACITY = -9   /* more than 2^32-1 events in one flush                */
+} gwaoi_status;
+
+typedef struct {
+    uint32_t max_slots;      /* slot handles are in [0, max_slots)                   */
+    uint32_t max_spaces;     /* space ids are in [0, max_spaces)                      */
+    int32_t device;          /* HIP device ordinal, -1 = the calling thread's current */
+    uint32_t flags;          /* GWAOI_F_*                                             */
+    uint64_t event_capacity; /* initial device event capacity in pairs (0 = default) */
+    float cells_per_dist;    /* grid cells per AOI distance (0 = default 1.0)         */
+} gwaoi_config;
+
+#define GWAOI_F_TIMING 1u /* time every pipeline stage with HIP events (gwaoi_stage_times) */
+
+typedef struct {
+    uint64_t n_enter;      /* directed enter events; replay pair (a,b) as a.OnEnterAOI(b) */
+    uint64_t n_leave;      /* directed leave events; replay pair (a,b) as a.OnLeaveAOI(b) */
+    const uint32_t *enter; /* 2*n_enter uint32: a0,b0,a1,b1,...  (world-owned host memory,  */
+    const uint32_t *leave; /* 2*n_leave uint32                     valid until the next tick) */
+} gwaoi_events;
+
+typedef struct {
+    uint64_t ticks;        /* completed flushes                       */
+    uint64_t next_seq;     /* sequence number the next call gets      */
+    uint32_t live;         /* live entities after the last flush      */
+    uint32_t spaces;       /* spaces currently created                */
+    uint32_t total_cells;  /* grid cells of the last flush            */
+    uint32_t pending_ops;  /* calls queued since the last flush       */
+    uint64_t event_capacity;
+} gwaoi_info;
+
+typedef struct {
+    char name[32];
+    double ms;             /* accumulated device time (HIP events)     */
+    uint64_t calls;
+} gwaoi_stage_time;
+
+/* ---- world / space lifetime ---------------------------------------------- */
+int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out);
+int gwaoi_world_destroy(gwaoi_world *w);
+
+/* aoi.NewXZListAOIManager(aoi_distance)  -- Space.EnableAOI, Space.go:91-107 */
+int gwaoi_space_create(gwaoi_world *w, float aoi_distance, uint32_t *space_out);
+int gwaoi_space_destroy(gwaoi_world *w, uint32_t space);
+
+/* ---- AOIManager calls (queued; seq = call order) ---------------------------- */
+int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z);
+int gwaoi_leave(gwaoi_world *w, uint32_t slot);
+int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z);
+
+/* Batched forms (array order = call order).  Validated as a whole: on error
+ * nothing is queued. */
+int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, const float *x,
+                      const float *z, size_t n);
+int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n);
+int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z,
+                      size_t n);
+
+/* Moves whose arrays already live in device memory of the world's GPU (the
+ * per-tick position-sync batch, GameService.go:392-404).  The pointers must
+ * stay valid until the next gwaoi_tick*.  Only slots live at the previous
+ * flush may appear; violations and non-finite coordinates are detected on the
+ * device and reported by the next tick (the offending moves are dropped). */
+int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const float *d_x,
+                             const float *d_z, size_t n);
+
+/* ---- flush ------------------------------------------------------------------ */
+/* Run the tick and copy its events to host memory. */
+int gwaoi_tick(gwaoi_world *w, gwaoi_events *out);
+/* Run the tick; events stay in device memory (see gwaoi_events_device). */
+int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
+/* Device pointers of the last tick's events (same layout as gwaoi_events). */
+int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave);
+
+/* ---- queries ----------------------------------------------------------------- */
+/* Neighbours of `slot` at the last flush (unsorted).  *n_out = total count even
+ * when it exceeds cap. */
+int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, size_t *n_out);
+int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info);
+int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t *n_out);
+int gwaoi_reset_stage_times(gwaoi_world *w);
+int gwaoi_sync(gwaoi_world *w);
+void *gwaoi_stream(gwaoi_world *w); /* the world's hipStream_t */
+
+const char *gwaoi_strerror(int status);
+const char *gwaoi_last_error(gwaoi_world *w);
+int gwaoi_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWAOI_H */

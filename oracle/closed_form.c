@@ -61,9 +61,10 @@ static int64_t lower(const cell_ent *e, int64_t n, uint32_t sp, int64_t cx, int6
     return lo;
 }
 
-/* neighbour relation; returns number of pairs written to *out (malloc'd, caller frees via cf_free) */
-int64_t cf_pairs(int64_t n, const float *x, const float *z, const uint64_t *seq, const uint32_t *sp,
-                 const float *D, uint64_t **out) {
+/* neighbour relation; returns number of pairs written to *out (malloc'd,
+ * caller frees via cf_free); sorted ascending when `sort` is set */
+int64_t cf_pairs_ex(int64_t n, const float *x, const float *z, const uint64_t *seq, const uint32_t *sp,
+                    const float *D, uint64_t **out, int sort) {
     cell_ent *e = (cell_ent *)malloc(sizeof(cell_ent) * (n ? n : 1));
     int64_t m = 0;
     for (int64_t i = 0; i < n; i++) {
@@ -99,9 +100,14 @@ int64_t cf_pairs(int64_t n, const float *x, const float *z, const uint64_t *seq,
             }
     }
     free(e);
-    qsort(pairs, len, sizeof(uint64_t), cmp_u64);
+    if (sort) qsort(pairs, len, sizeof(uint64_t), cmp_u64);
     *out = pairs;
     return (int64_t)len;
+}
+
+int64_t cf_pairs(int64_t n, const float *x, const float *z, const uint64_t *seq, const uint32_t *sp,
+                 const float *D, uint64_t **out) {
+    return cf_pairs_ex(n, x, z, seq, sp, D, out, 1);
 }
 
 void cf_free(void *p) { free(p); }

@@ -54,6 +54,8 @@ def lib():
         L.xz_apply.restype = i64
         L.xz_moved_batch.argtypes = [vp, i64, vp, vp, vp]
         L.xz_moved_batch.restype = i64
+        L.xz_bulk_enter.argtypes = [vp, i64, vp, vp, vp]
+        L.xz_bulk_enter.restype = C.c_int
         L.xz_counts.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
         L.xz_num_events.argtypes = [vp]
         L.xz_num_events.restype = sz
@@ -114,6 +116,14 @@ class XZList:
         bad = self._L.xz_apply(self._m, ops.size, _p(ops), _p(ids), _p(xs), _p(zs))
         if bad >= 0:
             raise RuntimeError(f"op {bad} rejected")
+
+    def bulk_enter(self, ids, xs, zs):
+        """Same state as Enter(ids[i]) for i in order on an empty manager, without events."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        xs = np.ascontiguousarray(xs, np.float32)
+        zs = np.ascontiguousarray(zs, np.float32)
+        if self._L.xz_bulk_enter(self._m, ids.size, _p(ids), _p(xs), _p(zs)):
+            raise RuntimeError("bulk_enter needs an empty manager and fresh ids")
 
     def moved_batch(self, ids, xs, zs):
         ids = np.ascontiguousarray(ids, np.int32)

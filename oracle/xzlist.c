@@ -354,6 +354,59 @@ int64_t xz_apply(xzmgr *m, int64_t n, const uint8_t *op, const int32_t *id, cons
     return -1;
 }
 
+/* Bulk equivalent of Enter(id[0..n)) in array order on an empty manager: the
+ * same sorted lists and the same neighbour sets (closed form with seq = array
+ * position) in O(n log n + E) instead of go-aoi's O(n^2)
+ * head-scan inserts.  No events are emitted.  Used only to populate the
+ * bench's cpu_baseline at 1M entities; tests check it against real Enters. */
+extern int64_t cf_pairs_ex(int64_t n, const float *x, const float *z, const uint64_t *seq, const uint32_t *sp,
+                           const float *D, uint64_t **out, int sort);
+static const float *g_sort_c;
+static int cmp_by_c(const void *pa, const void *pb) {
+    int32_t a = *(const int32_t *)pa, b = *(const int32_t *)pb;
+    float ca = g_sort_c[a], cb = g_sort_c[b];
+    return ca < cb ? -1 : (ca > cb);
+}
+int xz_bulk_enter(xzmgr *m, int64_t n, const int32_t *id, const float *x, const float *z) {
+    if (m->xhead != NIL || m->zhead != NIL) return -1;
+    for (int64_t i = 0; i < n; i++)
+        if (id[i] < 0 || id[i] >= m->cap || m->live[id[i]]) return -1;
+    for (int64_t i = 0; i < n; i++) {
+        m->live[id[i]] = 1;
+        m->x[id[i]] = x[i];
+        m->z[id[i]] = z[i];
+        m->mark[id[i]] = 0;
+    }
+    int32_t *ord = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
+    for (int a = 0; a < 2; a++) {
+        axis A = a == 0 ? ax_x(m) : ax_z(m);
+        for (int64_t i = 0; i < n; i++) ord[i] = id[i];
+        g_sort_c = A.c;
+        qsort(ord, n, sizeof(int32_t), cmp_by_c);
+        for (int64_t i = 0; i < n; i++) {
+            A.prev[ord[i]] = i ? ord[i - 1] : NIL;
+            A.next[ord[i]] = i + 1 < n ? ord[i + 1] : NIL;
+        }
+        *A.head = n ? ord[0] : NIL;
+        *A.tail = n ? ord[n - 1] : NIL;
+    }
+    free(ord);
+    uint64_t *seq = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
+    uint32_t *sp = (uint32_t *)calloc(n ? n : 1, sizeof(uint32_t));
+    for (int64_t i = 0; i < n; i++) seq[i] = (uint64_t)i + 1;
+    uint64_t *pairs = NULL;
+    float D = m->D;
+    int64_t np = cf_pairs_ex(n, x, z, seq, sp, &D, &pairs, 0);
+    for (int64_t k = 0; k < np; k++) {
+        int64_t ia = (int64_t)(pairs[k] >> 32), ib = (int64_t)(pairs[k] & 0xFFFFFFFFu);
+        nset_add(&m->nb[id[ia]], id[ib]);
+    }
+    free(pairs);
+    free(seq);
+    free(sp);
+    return 0;
+}
+
 /* Moved() over a prefix of a batch; used by the bench's cpu_baseline leg */
 int64_t xz_moved_batch(xzmgr *m, int64_t n, const int32_t *id, const float *x, const float *z) {
     for (int64_t i = 0; i < n; i++)

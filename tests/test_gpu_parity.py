@@ -1,0 +1,308 @@
+"""HIP path (through the C ABI) vs the CPU oracle: bit-exact event sets.
+
+Every test drives libgwaoi.so exactly as GoWorld's Space drives go-aoi
+(Enter/Leave/Moved in call order, Space.go:211,243,259), flushes, and
+compares the sorted enter/leave sets with the oracle's net events and the
+neighbour relation with the oracle's sets.  Integer/index outputs: bit-exact,
+no tolerance.
+"""
+import numpy as np
+import pytest
+
+from goworld_amd import World, GwaoiError, pair_keys
+from goworld_amd.workload import make_workload
+
+pytestmark = pytest.mark.gpu
+
+D = np.float32(100.0)
+
+
+def f32(bits):
+    return np.frombuffer(np.uint32(bits).tobytes(), np.float32)[0]
+
+
+def flush(w):
+    ent, lev = w.tick()
+    return pair_keys(ent), pair_keys(lev)
+
+
+def test_kat_r1_ownership_gpu():
+    a, b = f32(0xC57CC1A7), f32(0xC58180D4)
+    with World(4) as w:
+        s = w.space_create(D)
+        w.enter(s, 1, b, 0)
+        w.enter(s, 0, a, 0)  # A last: P_A(B) true -> neighbours
+        ent, lev = flush(w)
+        assert ent.tolist() == [(0 << 32) | 1, (1 << 32) | 0] and lev.size == 0
+        w.moved(1, b, 0)  # B last at the same position: P_B(A) false -> leave
+        ent, lev = flush(w)
+        assert ent.size == 0 and lev.tolist() == [(0 << 32) | 1, (1 << 32) | 0]
+        assert w.neighbors(0).size == 0
+
+
+def test_kat_r2_mirror_gpu():
+    a, b = f32(0x43978D94), f32(0x434B1B27)
+    with World(4) as w:
+        s = w.space_create(D)
+        w.enter(s, 0, a, 0)
+        w.enter(s, 1, b, 0)
+        ent, _ = flush(w)
+        assert ent.size == 2
+        w.moved(0, a, 0)
+        _, lev = flush(w)
+        assert lev.size == 2
+
+
+def test_kat_t1_colocated_gpu():
+    with World(16) as w:
+        s = w.space_create(D)
+        for i in range(10):
+            w.enter(s, i, 0.0, 0.0)
+        ent, lev = flush(w)
+        assert ent.size == 90 and lev.size == 0
+        assert w.neighbors(3).tolist() == [i for i in range(10) if i != 3]
+
+
+@pytest.mark.parametrize("dx,expect", [(100.0, True), (-100.0, True),
+                                       (float(np.nextafter(np.float32(100), np.float32(np.inf))), False)])
+def test_kat_t2_t3_bounds_gpu(dx, expect):
+    with World(4) as w:
+        s = w.space_create(D)
+        w.enter(s, 0, 0.0, 0.0)
+        w.enter(s, 1, np.float32(dx), 0.0)
+        w.enter(s, 2, 7000.0, 0.0)
+        w.enter(s, 3, 7000.0, np.float32(dx))
+        ent, _ = flush(w)
+        keys = set(ent.tolist())
+        assert ((0 << 32 | 1) in keys) == expect
+        assert ((2 << 32 | 3) in keys) == expect
+
+
+def test_kat_l1_leave_gpu():
+    with World(8) as w:
+        s = w.space_create(D)
+        for i in range(8):
+            w.enter(s, i, np.float32(i * 10), 0.0)
+        flush(w)
+        w.leave(3)
+        ent, lev = flush(w)
+        assert ent.size == 0 and lev.size == 14
+        assert all(3 not in w.neighbors(i).tolist() for i in range(8) if i != 3)
+
+
+def test_error_paths_gpu():
+    with World(8) as w:
+        s = w.space_create(D)
+        with pytest.raises(GwaoiError):
+            w.moved(0, 1, 1)
+        with pytest.raises(GwaoiError):
+            w.leave(0)
+        with pytest.raises(GwaoiError):
+            w.enter(s, 8, 0, 0)
+        with pytest.raises(GwaoiError):
+            w.enter(s, 0, float("nan"), 0)
+        with pytest.raises(GwaoiError):
+            w.space_create(0.0)
+        w.enter(s, 0, 0, 0)
+        with pytest.raises(GwaoiError):
+            w.enter(s, 0, 0, 0)
+        with pytest.raises(GwaoiError):
+            w.space_destroy(s)
+
+
+def run_stream_vs_oracle(oracle_mod, ops, n, flush_every, D_by_space=None, check_neighbors=True):
+    """Apply one op stream to the GPU world and to one sequential manager per
+    space; after every `flush_every` ops compare net events and relations."""
+    D_by_space = D_by_space or {0: D}
+    orc = oracle_mod.SpacesOracle(D_by_space, n)
+    with World(n, max_spaces=max(D_by_space) + 1) as w:
+        ids = {}
+        for sp in sorted(D_by_space):
+            ids[sp] = w.space_create(D_by_space[sp])
+        for k, op in enumerate(ops):
+            kind = op[0]
+            if kind == 1:
+                _, i, x, z, sp = op
+                w.enter(ids[sp], i, x, z)
+                orc.enter(sp, i, x, z)
+            elif kind == 0:
+                _, i, x, z = op[:4]
+                w.moved(i, x, z)
+                orc.moved(i, x, z)
+            else:
+                w.leave(op[1])
+                orc.leave(op[1])
+            if k % flush_every == flush_every - 1 or k == len(ops) - 1:
+                ge, gl = flush(w)
+                oe, ol = oracle_mod.net_events(*orc.take_events())
+                np.testing.assert_array_equal(ge, oe)
+                np.testing.assert_array_equal(gl, ol)
+                if check_neighbors:
+                    for i in range(0, n, max(1, n // 16)):
+                        if i in orc.local:
+                            np.testing.assert_array_equal(w.neighbors(i), orc.neighbors(i).astype(np.uint32))
+
+
+def boundary_ops(rng, n, steps, span=5000.0, spaces=(0,)):
+    """Enter/Moved/Leave stream on other entities' window edges (+- a few ulps)."""
+    live = np.zeros(n, bool)
+    spc = np.zeros(n, np.int64)
+    px = np.zeros(n, np.float32)
+    pz = np.zeros(n, np.float32)
+    ops = []
+
+    def nudge(v, k):
+        v = np.float32(v)
+        for _ in range(abs(k)):
+            v = np.nextafter(v, np.float32(np.inf) if k > 0 else np.float32(-np.inf))
+        return np.float32(v)
+
+    for _ in range(steps):
+        i = int(rng.integers(n))
+        cand = np.nonzero(live)[0]
+        if cand.size and rng.random() < 0.8:
+            j = int(rng.choice(cand))
+            x = nudge(px[j] + np.float32(rng.choice([-1, 0, 1])) * D, int(rng.integers(-2, 3)))
+            z = nudge(pz[j] + np.float32(rng.choice([-1, 0, 1])) * D, int(rng.integers(-2, 3)))
+        else:
+            x = np.float32(rng.uniform(-span, span))
+            z = np.float32(rng.uniform(-span, span))
+        if not live[i]:
+            sp = int(rng.choice(spaces))
+            ops.append((1, i, x, z, sp))
+            live[i] = True
+            spc[i] = sp
+        elif rng.random() < 0.08:
+            ops.append((2, i))
+            live[i] = False
+            continue
+        else:
+            ops.append((0, i, x, z))
+        px[i], pz[i] = x, z
+    return ops
+
+
+@pytest.mark.parametrize("seed,flush_every", [(11, 1), (12, 7), (13, 50), (14, 400)])
+def test_boundary_stream_gpu(oracle_mod, seed, flush_every):
+    rng = np.random.default_rng(seed)
+    ops = boundary_ops(rng, 64, 1200)
+    run_stream_vs_oracle(oracle_mod, ops, 64, flush_every)
+
+
+def test_boundary_stream_multispace_gpu(oracle_mod):
+    rng = np.random.default_rng(21)
+    ops = boundary_ops(rng, 96, 1500, span=800.0, spaces=(0, 1, 2))
+    run_stream_vs_oracle(oracle_mod, ops, 96, 37, {0: D, 1: np.float32(50.0), 2: np.float32(100.0)})
+
+
+def test_empty_and_ragged_flushes_gpu():
+    with World(32) as w:
+        s = w.space_create(D)
+        assert flush(w)[0].size == 0  # empty world
+        assert flush(w)[0].size == 0
+        w.enter(s, 5, 1.0, 1.0)
+        ent, lev = flush(w)
+        assert ent.size == 0 and lev.size == 0  # a lone entity has no neighbours
+        w.leave(5)
+        assert flush(w)[1].size == 0
+        w.enter(s, 5, 1.0, 1.0)  # slot reuse after a flush
+        w.enter(s, 6, 2.0, 2.0)
+        w.leave(6)  # enter + leave inside one flush: no net event
+        ent, lev = flush(w)
+        assert ent.size == 0 and lev.size == 0
+
+
+def test_cfg1_vs_sequential_oracle_gpu(oracle_mod):
+    """examples/test_game-style space, 1000 Avatars, bot random walk (cfg1)."""
+    wl = make_workload("cfg1")
+    m = oracle_mod.XZList(wl.D, wl.n)
+    with World(wl.n) as w:
+        s = w.space_create(wl.D)
+        slots, x0, z0, _ = wl.initial()
+        w.enter_batch(s, slots, x0, z0)
+        for i in range(wl.n):
+            m.enter(int(slots[i]), x0[i], z0[i])
+        ge, gl = flush(w)
+        oe, ol = oracle_mod.net_events(*m.take_events())
+        np.testing.assert_array_equal(ge, oe)
+        assert gl.size == 0 and ge.size > 10000
+        for t in range(30):
+            sl, nx, nz = wl.tick(t)
+            w.moved_batch(sl, nx, nz)
+            m.moved_batch(sl, nx, nz)
+            ge, gl = flush(w)
+            oe, ol = oracle_mod.net_events(*m.take_events())
+            np.testing.assert_array_equal(ge, oe)
+            np.testing.assert_array_equal(gl, ol)
+
+
+@pytest.mark.parametrize("cfg,n,ticks", [("cfg2", 20000, 4), ("cfg3", 40000, 3)])
+def test_scaled_configs_vs_closed_form_gpu(oracle_mod, cfg, n, ticks):
+    """cfg2/cfg3 at reduced N (same density): GPU events == diff of the
+    closed-form relation, and the GPU relation == the closed form."""
+    wl = make_workload(cfg, n=n)
+    seq = np.zeros(wl.n, np.uint64)
+    sp = np.zeros(wl.n, np.uint32)
+    with World(wl.n) as w:
+        s = w.space_create(wl.D)
+        slots, x0, z0, _ = wl.initial()
+        w.enter_batch(s, slots, x0, z0)
+        seq[slots] = 1 + np.arange(wl.n, dtype=np.uint64)
+        nxt = wl.n + 1
+        ge, _ = flush(w)
+        prev = oracle_mod.closed_form_pairs(wl.x, wl.z, seq, sp, {0: wl.D})
+        np.testing.assert_array_equal(ge, prev)
+        for t in range(ticks):
+            sl, nx, nz = wl.tick(t)
+            w.moved_batch(sl, nx, nz)
+            seq[sl] = nxt + np.arange(sl.size, dtype=np.uint64)
+            nxt += sl.size
+            ge, gl = flush(w)
+            cur = oracle_mod.closed_form_pairs(wl.x, wl.z, seq, sp, {0: wl.D})
+            np.testing.assert_array_equal(ge, np.setdiff1d(cur, prev))
+            np.testing.assert_array_equal(gl, np.setdiff1d(prev, cur))
+            prev = cur
+        for i in range(0, wl.n, wl.n // 7):
+            want = (prev[(prev >> np.uint64(32)) == np.uint64(i)] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            np.testing.assert_array_equal(w.neighbors(i), want)
+
+
+def test_device_batch_matches_host_batch_gpu():
+    torch = pytest.importorskip("torch")
+    wl_a = make_workload("cfg2", n=8000)
+    wl_b = make_workload("cfg2", n=8000)
+    with World(wl_a.n) as wa, World(wl_b.n) as wb:
+        for w, wl in ((wa, wl_a), (wb, wl_b)):
+            s = w.space_create(wl.D)
+            slots, x0, z0, _ = wl.initial()
+            w.enter_batch(s, slots, x0, z0)
+            w.tick()
+        for t in range(3):
+            sl, nx, nz = wl_a.tick(t)
+            wa.moved_batch(sl, nx, nz)
+            ea, la = wa.tick()
+            sl2, nx2, nz2 = wl_b.tick(t)
+            ds = torch.from_numpy(sl2.astype(np.int32)).cuda()
+            dx = torch.from_numpy(nx2).cuda()
+            dz = torch.from_numpy(nz2).cuda()
+            torch.cuda.synchronize()
+            wb.moved_batch_device(ds.data_ptr(), dx.data_ptr(), dz.data_ptr(), sl2.size)
+            eb, lb = wb.tick()
+            np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
+
+
+def test_device_batch_errors_reported_gpu():
+    torch = pytest.importorskip("torch")
+    with World(8) as w:
+        s = w.space_create(D)
+        w.enter(s, 0, 0, 0)
+        w.tick()
+        ds = torch.tensor([0, 5], dtype=torch.int32, device="cuda")  # slot 5 is not live
+        dx = torch.tensor([1.0, 1.0], device="cuda")
+        dz = torch.tensor([1.0, 1.0], device="cuda")
+        torch.cuda.synchronize()
+        w.moved_batch_device(ds.data_ptr(), dx.data_ptr(), dz.data_ptr(), 2)
+        with pytest.raises(GwaoiError):
+            w.tick()
+        assert w.neighbors(0).size == 0

@@ -215,3 +215,22 @@ def test_workload_cfg1_sequential_vs_closed_form(oracle_mod):
     want = oracle_mod.closed_form_pairs(w.x, w.z, seq, np.zeros(w.n, np.uint32), {0: w.D})
     np.testing.assert_array_equal(m.pairs(), want)
     assert want.size > 1000
+
+
+def test_bulk_enter_equals_sequential_enters(oracle_mod):
+    """xz_bulk_enter (used to populate the 1M-entity cpu_baseline) == Enter in order."""
+    from goworld_amd.workload import make_workload
+    w = make_workload("cfg3", n=3000)
+    a = oracle_mod.XZList(w.D, w.n)
+    b = oracle_mod.XZList(w.D, w.n, record=False)
+    order = np.random.default_rng(5).permutation(w.n).astype(np.int32)
+    for i in order:
+        a.enter(int(i), w.x[i], w.z[i])
+    b.bulk_enter(order, w.x[order], w.z[order])
+    assert b.check() == 0
+    np.testing.assert_array_equal(a.pairs(), b.pairs())
+    sl, nx, nz = w.tick(0)
+    a.take_events()
+    a.moved_batch(sl, nx, nz)
+    b.moved_batch(sl, nx, nz)
+    np.testing.assert_array_equal(a.pairs(), b.pairs())
