@@ -12,20 +12,28 @@ constexpr uint32_t SP_KEEP = 0xFFFFFFFEu;  // device move: keep the space of the
 
 // Device-side validation flags (bit set = problem seen during the tick).
 constexpr uint32_t ERR_NONFINITE = 1u;
-constexpr uint32_t ERR_MOVE_DEAD = 2u;  // device move of a slot that is not live
+constexpr uint32_t ERR_MOVE_DEAD = 2u;       // device move of a slot that is not live
 constexpr uint32_t ERR_BAD_SLOT = 4u;
 constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreement (bug guard)
 
+constexpr uint32_t TILE_A = 256;  // entities per pair-pass tile (= threads per workgroup)
+
 // Uniform grid of one space for one flush.  Cell (cx,cz) of space s has the
-// global cell key base + cz*gx + cx.  cellOf() is monotone in the coordinate,
-// so a query range derived from conservative window bounds is complete.
+// global cell key base + cz*gx + cx; its grid row cz is global row
+// row_base + cz.  cellOf() is monotone in the coordinate, so a query range
+// derived from conservative window bounds is complete.
 struct SpaceGrid {
     float ox, oz;   // grid origin
     float inv;      // 1 / cell size
     float D;        // AOI distance of the space (go-aoi aoidist)
     uint32_t gx, gz;
     uint32_t base;
-    uint32_t pad;
+    uint32_t row_base;
+};
+
+// A pair-pass work unit: entities [e0, e1) of one grid row (at most TILE_A).
+struct Tile {
+    uint32_t e0, e1, row, pad;
 };
 
 // One flush's sorted state: entries [0, n) are the live entities ordered by
@@ -47,6 +55,13 @@ struct StateView {
     const uint32_t *sp;
 };
 
+struct TileSet {  // the pair-pass tiles of one frame
+    const Tile *tiles;
+    const uint32_t *n_tiles;     // device count
+    const uint32_t *row_space;   // space id of every global grid row
+    uint32_t bound;              // host upper bound on *n_tiles (launch size)
+};
+
 struct TickResult {  // device -> host summary of one tick
     uint32_t n_enter;
     uint32_t n_total;
@@ -56,24 +71,33 @@ struct TickResult {  // device -> host summary of one tick
 };
 
 // ---- launchers (gwaoi_kernels.hip) ------------------------------------------
+void launch_copy_state(uint32_t n, const float *p_x, const float *p_z, const uint64_t *p_seq, const uint32_t *p_sp,
+                       const uint32_t *p_slot, float *s_x, float *s_z, uint64_t *s_seq, uint32_t *s_sp,
+                       uint32_t *s_slot, hipStream_t st);
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, uint32_t *s_slot,
                           uint32_t *s_sp, uint64_t *s_seq, uint32_t *rank, hipStream_t st);
-void launch_ops_claim(const uint32_t *op_slot, uint32_t n_ops, uint32_t max_slots,
+// One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
+// means a device-resident Moved batch (keep the space).
+void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots,
                       unsigned long long *lastop, uint32_t tick_id, uint32_t *err, hipStream_t st);
-void launch_ops_apply(const uint32_t *op_slot, const float *op_x, const float *op_z, const uint32_t *op_sp,
-                      uint32_t n_ops, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
+void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
+                      uint32_t j0, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
                       const uint32_t *rank, uint32_t n_total, uint64_t seq_base, float *s_x, float *s_z,
                       uint64_t *s_seq, uint32_t *s_sp, const uint32_t *s_slot, uint32_t *err, hipStream_t st);
+// keygen also folds d_rel (int-encoded float, zeroed by the caller): the
+// largest per-axis displacement / D of entities that stayed in their space
+// and moved at most D/4.
 void launch_keygen(const float *s_x, const float *s_z, const uint32_t *s_sp, uint32_t n_total,
-                   const SpaceGrid *grid, uint32_t sentinel, uint32_t *keys, uint32_t *vals, hipStream_t st);
+                   const SpaceGrid *grid, uint32_t sentinel, uint32_t *keys, uint32_t *vals, const float *p_x,
+                   const float *p_z, const uint32_t *p_sp, const SpaceGrid *p_grid, uint32_t n_prev, int *d_rel,
+                   hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
     uint32_t *keys[2];
     uint32_t *vals[2];
-    uint32_t *hist;      // >= 256 * tiles
+    uint32_t *hist;      // >= radix_hist_elems(n)
     uint32_t *scan_tmp;  // scratch for the scan of hist
-    size_t scan_tmp_elems;
 };
 int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st);
 size_t radix_hist_elems(uint32_t n);
@@ -89,13 +113,26 @@ void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const 
                    uint32_t n_total, uint32_t *err, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
-// mode 0 = enter pass (frame = new, other = old state); 1 = leave pass
-// (frame = previous, other = new state).  fill=false counts, fill=true writes.
-void launch_pairs(int mode, bool fill, FrameView F, StateView O, uint64_t seq_base, uint32_t *counts,
-                  const uint32_t *offsets, uint32_t *out_pairs, uint64_t out_cap,
-                  unsigned long long *total64, hipStream_t st);
-void launch_finish(const uint32_t *offsets, uint32_t n_new, uint32_t n_prev, const uint32_t *err,
-                   const unsigned long long *total64, TickResult *res, hipStream_t st);
+// Tiles of a frame: rows split into runs of <= TILE_A entities.
+// row_ntiles needs n_rows + 1 entries; tiles needs tile_bound(n, n_rows).
+void build_tiles(FrameView F, uint32_t n_space_ids, uint32_t n_rows, uint32_t *row_space, uint32_t *row_ntiles,
+                 Tile *tiles, uint32_t *scan_tmp, hipStream_t st);
+inline uint32_t tile_bound(uint32_t n, uint32_t n_rows) { return (n + TILE_A - 1) / TILE_A + n_rows; }
+
+// mode 2 = combined pass over the new frame (other = previous state in the
+// new order); mode 1 = special-entity pass over the previous frame (other =
+// new state in the previous order).  Directed event pairs go to tmp at an
+// atomically reserved offset per tile; per tile t the enter total/base are
+// at [tile_off + t] and the leave total/base at [leave_off + tile_off + t].
+void launch_pairs(int mode, FrameView F, StateView O, TileSet T, uint64_t seq_base, const float *d_rel,
+                  unsigned long long *counter, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
+                  unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st);
+// Copy every tile's events from tmp into tile order (dest = scanned tile_total).
+void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
+                    uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
+                    hipStream_t st);
+void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const uint32_t *err,
+                   const unsigned long long *counter, TickResult *res, hipStream_t st);
 void launch_bbox(FrameView F, int *bbox, uint32_t max_spaces, hipStream_t st);
 void launch_neighbors(FrameView F, const uint32_t *rank, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);

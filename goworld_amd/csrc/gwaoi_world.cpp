@@ -27,24 +27,10 @@ using gw::SpaceGrid;
 
 namespace {
 
-enum Stage {
-    ST_APPLY,
-    ST_KEYGEN,
-    ST_SORT,
-    ST_GATHER,
-    ST_CELLS,
-    ST_ENTER_COUNT,
-    ST_LEAVE_COUNT,
-    ST_SCAN,
-    ST_ENTER_FILL,
-    ST_LEAVE_FILL,
-    ST_BBOX,
-    ST_D2H,
-    ST_N
-};
-const char *kStageNames[ST_N] = {"apply",      "keygen",      "sort",      "gather",     "cells",
-                                 "enter_count", "leave_count", "scan",      "enter_fill", "leave_fill",
-                                 "bbox",       "d2h"};
+enum Stage { ST_APPLY, ST_KEYGEN, ST_SORT, ST_GATHER, ST_CELLS, ST_TILES, ST_COMBINED, ST_SPECIAL, ST_REORDER,
+             ST_BBOX, ST_D2H, ST_N };
+const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",    "gather", "cells", "tiles",
+                                 "combined", "special", "reorder", "bbox",   "d2h"};
 
 struct DevFrame {
     float *x = nullptr, *z = nullptr;
@@ -55,6 +41,13 @@ struct DevFrame {
     SpaceGrid *grid = nullptr;
     uint32_t n = 0;
     uint32_t total_cells = 0;
+    // pair-pass tiles of this frame
+    uint32_t *row_space = nullptr, *row_ntiles = nullptr;
+    size_t row_cap = 0;
+    gw::Tile *tiles = nullptr;
+    size_t tile_cap = 0;
+    uint32_t n_rows = 0;
+    uint32_t tile_bound = 0;
 };
 
 struct SpaceHost {
@@ -103,14 +96,18 @@ struct gwaoi_world {
     uint32_t *rank = nullptr;
     unsigned long long *lastop = nullptr;
     uint32_t *new_slots_d = nullptr;
-    uint32_t *counts = nullptr;  // 2*max_slots + 1
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
     size_t op_cap = 0;
-    uint32_t *events = nullptr;  // 2 * ev_cap uint32
-    uint64_t ev_cap = 0;
+    uint32_t *events = nullptr;      // ev_cap (a,b) pairs: [enters | leaves] in tile order
+    uint32_t *events_tmp = nullptr;  // ev_cap pairs: per-tile chunks at reserved offsets
+    uint64_t ev_cap = 0;             // capacity in directed pairs
+    uint32_t *tile_total = nullptr, *tile_dest = nullptr;
+    unsigned long long *tile_base = nullptr;
+    size_t tile_entries_cap = 0;
     uint32_t *err = nullptr;
-    unsigned long long *total64 = nullptr;
+    int *d_rel = nullptr;  // float bits: max displacement / D of near entities this flush
+    unsigned long long *counter = nullptr;
     gw::TickResult *res = nullptr;
     int *bbox = nullptr;
     uint32_t *nb_out = nullptr, *nb_count = nullptr;
@@ -220,12 +217,57 @@ int ensure_events(gwaoi_world *w, uint64_t pairs) {
     uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, w->ev_cap * 2);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->events);
-    int rc = dalloc(w, &w->events, 2 * cap);
-    if (rc) {
+    dfree(w->events_tmp);
+    int rc;
+    if ((rc = dalloc(w, &w->events, 2 * cap)) || (rc = dalloc(w, &w->events_tmp, 2 * cap))) {
         w->ev_cap = 0;
         return rc;
     }
     w->ev_cap = cap;
+    return GWAOI_OK;
+}
+
+int ensure_tiles(gwaoi_world *w, DevFrame &f, uint32_t n_rows, uint32_t bound) {
+    if ((size_t)n_rows + 1 > f.row_cap) {
+        size_t cap = std::max<size_t>((size_t)n_rows + 1 + n_rows / 4, 256);
+        HIP_TRY(hipStreamSynchronize(w->stream));
+        dfree(f.row_space);
+        dfree(f.row_ntiles);
+        int rc;
+        if ((rc = dalloc(w, &f.row_space, cap)) || (rc = dalloc(w, &f.row_ntiles, cap))) {
+            f.row_cap = 0;
+            return rc;
+        }
+        f.row_cap = cap;
+    }
+    if (bound > f.tile_cap) {
+        size_t cap = std::max<size_t>(bound + bound / 4, 256);
+        HIP_TRY(hipStreamSynchronize(w->stream));
+        dfree(f.tiles);
+        int rc = dalloc(w, &f.tiles, cap);
+        if (rc) {
+            f.tile_cap = 0;
+            return rc;
+        }
+        f.tile_cap = cap;
+    }
+    return GWAOI_OK;
+}
+
+int ensure_tile_entries(gwaoi_world *w, size_t entries) {
+    if (entries + 1 <= w->tile_entries_cap) return GWAOI_OK;
+    size_t cap = std::max<size_t>(entries + 1 + entries / 4, 1024);
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    dfree(w->tile_total);
+    dfree(w->tile_dest);
+    dfree(w->tile_base);
+    int rc;
+    if ((rc = dalloc(w, &w->tile_total, cap)) || (rc = dalloc(w, &w->tile_dest, cap)) ||
+        (rc = dalloc(w, &w->tile_base, cap))) {
+        w->tile_entries_cap = 0;
+        return rc;
+    }
+    w->tile_entries_cap = cap;
     return GWAOI_OK;
 }
 
@@ -318,8 +360,8 @@ float o2f(int i) {
 // Choose the grid of every space for the coming flush.  Any grid is correct
 // (cellOf is monotone and clamped); this only keeps cells near D wide and the
 // cell count bounded by the population.
-void choose_grids(gwaoi_world *w, uint32_t &total_cells) {
-    uint32_t base = 0;
+void choose_grids(gwaoi_world *w, uint32_t &total_cells, uint32_t &total_rows) {
+    uint32_t base = 0, rows = 0;
     for (uint32_t s = 0; s < w->n_space_ids; ++s) {
         SpaceHost &S = w->spaces[s];
         SpaceGrid g{};
@@ -378,6 +420,8 @@ void choose_grids(gwaoi_world *w, uint32_t &total_cells) {
         }
         g.base = base;
         base += g.gx * g.gz;
+        g.row_base = rows;
+        rows += g.gz;
         w->h_grid[s] = g;
         if (S.used && S.alive) {
             S.grid = g;
@@ -387,6 +431,7 @@ void choose_grids(gwaoi_world *w, uint32_t &total_cells) {
         }
     }
     total_cells = base;
+    total_rows = rows;
 }
 
 gw::FrameView view_of(const DevFrame &f) {
@@ -412,6 +457,38 @@ int bitlen(uint32_t v) {
     return b;
 }
 
+// Pair passes + deterministic reorder (re-run after the event buffer grew).
+// Tile-total entries: [enter totals: new-frame tiles | previous-frame tiles]
+// then [leave totals: same order]; their exclusive scan is the final layout
+// [enters | leaves] in tile order.
+void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_base) {
+    hipStream_t st = w->stream;
+    const uint32_t TBn = Fn.n ? Fn.tile_bound : 0, TBp = P.n ? P.tile_bound : 0;
+    const uint32_t half = TBn + TBp, entries = 2 * half;
+    (void)hipMemsetAsync(w->counter, 0, sizeof(unsigned long long), st);
+    (void)hipMemsetAsync(w->tile_total, 0, ((size_t)entries + 1) * sizeof(uint32_t), st);
+    gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
+    gw::StateView old_in_new{w->ox, w->oz, w->oseq, w->osp};
+    gw::StateView new_in_prev{w->sx, w->sz, w->sseq, w->ssp};
+    gw::TileSet Tn{Fn.tiles, Fn.row_ntiles + Fn.n_rows, Fn.row_space, TBn};
+    gw::TileSet Tp{P.tiles, P.row_ntiles + P.n_rows, P.row_space, TBp};
+    const float *drel = reinterpret_cast<const float *>(w->d_rel);
+    stage_begin(w, ST_COMBINED);
+    gw::launch_pairs(2, Vn, old_in_new, Tn, seq_base, drel, w->counter, w->events_tmp, w->ev_cap,
+                     w->tile_total, w->tile_base, 0, half, st);
+    stage_end(w, ST_COMBINED);
+    stage_begin(w, ST_SPECIAL);
+    gw::launch_pairs(1, Vp, new_in_prev, Tp, seq_base, drel, w->counter, w->events_tmp, w->ev_cap,
+                     w->tile_total, w->tile_base, TBn, half, st);
+    stage_end(w, ST_SPECIAL);
+    stage_begin(w, ST_REORDER);
+    gw::scan_exclusive(w->tile_total, w->tile_dest, (size_t)entries + 1, w->scan_tmp, st);
+    gw::launch_reorder(w->tile_dest, w->tile_total, w->tile_base, entries, w->events_tmp, w->events, w->ev_cap,
+                       st);
+    gw::launch_finish(w->tile_dest, half, entries, w->err, w->counter, w->res, st);
+    stage_end(w, ST_REORDER);
+}
+
 // The flush.  On return the events of this tick are in w->events (device).
 int run_tick(gwaoi_world *w) {
     hipStream_t st = w->stream;
@@ -421,70 +498,87 @@ int run_tick(gwaoi_world *w) {
     const uint32_t n_ops = (uint32_t)w->n_ops;
     w->seq_next += n_ops;
 
-    DevFrame &P = w->fr[w->cur];      // previous flush
-    DevFrame &Fn = w->fr[w->cur ^ 1]; // this flush
+    DevFrame &P = w->fr[w->cur];       // previous flush
+    DevFrame &Fn = w->fr[w->cur ^ 1];  // this flush
     const uint32_t n_prev = P.n;
     const uint32_t n_app = (uint32_t)w->new_slots.size();
     const uint32_t n_total = n_prev + n_app;
     const uint32_t n_new = w->n_alive;
 
-    // grid for this flush
-    uint32_t total_cells = 0;
-    choose_grids(w, total_cells);
+    // grid + tiles for this flush
+    uint32_t total_cells = 0, total_rows = 0;
+    choose_grids(w, total_cells, total_rows);
+    const uint32_t tbound = gw::tile_bound(n_new, total_rows);
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
-    if ((rc = ensure_ops(w, n_ops))) return rc;
-    const size_t scan_need = std::max<size_t>({gw::radix_hist_elems(std::max(n_total, 1u)),
-                                               (size_t)n_new + n_prev + 1, (size_t)total_cells + 1});
+    if ((rc = ensure_tiles(w, Fn, total_rows, tbound))) return rc;
+    if ((rc = ensure_tile_entries(w, 2 * ((size_t)tbound + (P.n ? P.tile_bound : 0))))) return rc;
+    size_t host_ops = 0;
+    for (const Run &r : w->runs)
+        if (!r.device) host_ops += r.hend - r.hbegin;
+    if ((rc = ensure_ops(w, host_ops))) return rc;
+    const size_t scan_need = std::max<size_t>({gw::radix_hist_elems(std::max(n_total, 1u)), (size_t)total_cells + 1,
+                                               (size_t)total_rows + 1, w->tile_entries_cap});
     if ((rc = ensure_scan_tmp(w, scan_need))) return rc;
     Fn.total_cells = total_cells;
     Fn.n = n_new;
+    Fn.n_rows = total_rows;
+    Fn.tile_bound = tbound;
 
     HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * std::max(1u, w->n_space_ids),
                            hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(w->err, 0, sizeof(uint32_t), st));
-    HIP_TRY(hipMemsetAsync(w->total64, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(w->d_rel, 0, sizeof(int), st));
 
     // ---- apply queued ops onto S' = copy of the previous frame
     stage_begin(w, ST_APPLY);
-    if (n_prev) {
-        HIP_TRY(hipMemcpyAsync(w->sx, P.x, n_prev * sizeof(float), hipMemcpyDeviceToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->sz, P.z, n_prev * sizeof(float), hipMemcpyDeviceToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->sseq, P.seq, n_prev * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->ssp, P.sp, n_prev * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->sslot, P.slot, n_prev * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    }
+    gw::launch_copy_state(n_prev, P.x, P.z, P.seq, P.sp, P.slot, w->sx, w->sz, w->sseq, w->ssp, w->sslot, st);
     if (n_app) {
         HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
         gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->sslot, w->ssp, w->sseq, w->rank, st);
     }
     if (n_ops) {
-        size_t at = 0;
+        // host runs -> device op buffers; device runs are read in place
+        size_t hat = 0;
         for (const Run &r : w->runs) {
-            if (!r.device) {
-                const size_t k = r.hend - r.hbegin;
-                HIP_TRY(hipMemcpyAsync(w->op_slot + at, w->h_op_slot.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
-                HIP_TRY(hipMemcpyAsync(w->op_x + at, w->h_op_x.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
-                HIP_TRY(hipMemcpyAsync(w->op_z + at, w->h_op_z.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
-                HIP_TRY(hipMemcpyAsync(w->op_sp + at, w->h_op_sp.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
-                at += k;
-            } else {
-                HIP_TRY(hipMemcpyAsync(w->op_slot + at, r.ds, r.dn * 4, hipMemcpyDeviceToDevice, st));
-                HIP_TRY(hipMemcpyAsync(w->op_x + at, r.dx, r.dn * 4, hipMemcpyDeviceToDevice, st));
-                HIP_TRY(hipMemcpyAsync(w->op_z + at, r.dz, r.dn * 4, hipMemcpyDeviceToDevice, st));
-                HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->op_sp + at), (int)gw::SP_KEEP, r.dn, st));
-                at += r.dn;
+            if (r.device) continue;
+            const size_t k = r.hend - r.hbegin;
+            HIP_TRY(hipMemcpyAsync(w->op_slot + hat, w->h_op_slot.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(w->op_x + hat, w->h_op_x.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(w->op_z + hat, w->h_op_z.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(w->op_sp + hat, w->h_op_sp.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+            hat += k;
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            uint32_t j0 = 0;
+            size_t hoff = 0;
+            for (const Run &r : w->runs) {
+                const uint32_t *sl;
+                const float *xs, *zs;
+                const uint32_t *sps;
+                uint32_t k;
+                if (r.device) {
+                    sl = r.ds; xs = r.dx; zs = r.dz; sps = nullptr; k = (uint32_t)r.dn;
+                } else {
+                    k = (uint32_t)(r.hend - r.hbegin);
+                    sl = w->op_slot + hoff; xs = w->op_x + hoff; zs = w->op_z + hoff; sps = w->op_sp + hoff;
+                    hoff += k;
+                }
+                if (pass == 0)
+                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->lastop, tick_id, w->err, st);
+                else
+                    gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->lastop, tick_id, w->rank, n_total,
+                                         seq_base, w->sx, w->sz, w->sseq, w->ssp, w->sslot, w->err, st);
+                j0 += k;
             }
         }
-        gw::launch_ops_claim(w->op_slot, n_ops, w->max_slots, w->lastop, tick_id, w->err, st);
-        gw::launch_ops_apply(w->op_slot, w->op_x, w->op_z, w->op_sp, n_ops, w->max_slots, w->lastop, tick_id,
-                             w->rank, n_total, seq_base, w->sx, w->sz, w->sseq, w->ssp, w->sslot, w->err, st);
     }
     stage_end(w, ST_APPLY);
 
     // ---- keys + stable sort
     stage_begin(w, ST_KEYGEN);
-    gw::launch_keygen(w->sx, w->sz, w->ssp, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], st);
+    gw::launch_keygen(w->sx, w->sz, w->ssp, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.x, P.z, P.sp,
+                      P.grid, n_prev, w->d_rel, st);
     stage_end(w, ST_KEYGEN);
     stage_begin(w, ST_SORT);
     gw::SortBuffers sb;
@@ -494,7 +588,6 @@ int run_tick(gwaoi_world *w) {
     sb.vals[1] = w->vals[1];
     sb.hist = w->hist;
     sb.scan_tmp = w->scan_tmp;
-    sb.scan_tmp_elems = w->scan_tmp_cap;
     const int which = gw::radix_sort(sb, n_total, bitlen(total_cells), st);
     stage_end(w, ST_SORT);
     const uint32_t *skeys = w->keys[which];
@@ -513,31 +606,12 @@ int run_tick(gwaoi_world *w) {
     gw::launch_cell_count(skeys, n_new, Fn.cell_start, st);
     gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
     stage_end(w, ST_CELLS);
+    stage_begin(w, ST_TILES);
+    gw::build_tiles(view_of(Fn), w->n_space_ids, total_rows, Fn.row_space, Fn.row_ntiles, Fn.tiles, w->scan_tmp, st);
+    stage_end(w, ST_TILES);
 
-    // ---- pair passes
-    gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
-    gw::StateView old_in_new{w->ox, w->oz, w->oseq, w->osp};
-    gw::StateView new_in_prev{w->sx, w->sz, w->sseq, w->ssp};
-    uint32_t *cnt_enter = w->counts;
-    uint32_t *cnt_leave = w->counts + n_new;
-    stage_begin(w, ST_ENTER_COUNT);
-    gw::launch_pairs(0, false, Vn, old_in_new, seq_base, cnt_enter, nullptr, nullptr, 0, w->total64, st);
-    stage_end(w, ST_ENTER_COUNT);
-    stage_begin(w, ST_LEAVE_COUNT);
-    gw::launch_pairs(1, false, Vp, new_in_prev, seq_base, cnt_leave, nullptr, nullptr, 0, w->total64, st);
-    stage_end(w, ST_LEAVE_COUNT);
-    stage_begin(w, ST_SCAN);
-    HIP_TRY(hipMemsetAsync(w->counts + (size_t)n_new + n_prev, 0, sizeof(uint32_t), st));
-    gw::scan_exclusive(w->counts, w->counts, (size_t)n_new + n_prev + 1, w->scan_tmp, st);
-    stage_end(w, ST_SCAN);
-    stage_begin(w, ST_ENTER_FILL);
-    gw::launch_pairs(0, true, Vn, old_in_new, seq_base, nullptr, w->counts, w->events, w->ev_cap, nullptr, st);
-    stage_end(w, ST_ENTER_FILL);
-    stage_begin(w, ST_LEAVE_FILL);
-    gw::launch_pairs(1, true, Vp, new_in_prev, seq_base, nullptr, w->counts + n_new, w->events, w->ev_cap, nullptr,
-                     st);
-    stage_end(w, ST_LEAVE_FILL);
-    gw::launch_finish(w->counts, n_new, n_prev, w->err, w->total64, w->res, st);
+    // ---- pair passes: combined over the new grid, special entities over the previous one
+    launch_pair_passes(w, Fn, P, seq_base);
 
     // ---- per-space bounding boxes for the next flush's grid
     stage_begin(w, ST_BBOX);
@@ -545,7 +619,7 @@ int run_tick(gwaoi_world *w) {
         const uint32_t ms = w->max_spaces;
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)w->bbox, 0x7FFFFFFF, (size_t)2 * ms, st));
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->bbox + 2 * (size_t)ms), (int)0x80000000, (size_t)2 * ms, st));
-        gw::launch_bbox(Vn, w->bbox, ms, st);
+        gw::launch_bbox(view_of(Fn), w->bbox, ms, st);
         for (int q = 0; q < 4; ++q)
             HIP_TRY(hipMemcpyAsync(w->h_bbox + (size_t)q * ms, w->bbox + (size_t)q * ms,
                                    w->n_space_ids * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -555,18 +629,19 @@ int run_tick(gwaoi_world *w) {
     HIP_TRY(hipMemcpyAsync(w->h_res, w->res, sizeof(gw::TickResult), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
 
-    const gw::TickResult r = *w->h_res;
+    gw::TickResult r = *w->h_res;
     if (r.total64 > 0xFFFFFFFFull) {
         w->last_error = "more than 2^32-1 events in one flush";
         return GWAOI_ECAPACITY;
     }
-    if ((uint64_t)r.n_total > w->ev_cap) {  // grow and re-run the fill passes
-        if ((rc = ensure_events(w, r.n_total))) return rc;
-        gw::launch_pairs(0, true, Vn, old_in_new, seq_base, nullptr, w->counts, w->events, w->ev_cap, nullptr, st);
-        gw::launch_pairs(1, true, Vp, new_in_prev, seq_base, nullptr, w->counts + n_new, w->events, w->ev_cap,
-                         nullptr, st);
+    if (r.total64 > w->ev_cap) {  // grow and re-run the pair passes
+        stage_collect(w);
+        if ((rc = ensure_events(w, r.total64))) return rc;
+        launch_pair_passes(w, Fn, P, seq_base);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(w->h_res, w->res, sizeof(gw::TickResult), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        r = *w->h_res;
     }
     stage_collect(w);
 
@@ -645,13 +720,15 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     for (DevFrame &f : w->fr) {
         dfree(f.x); dfree(f.z); dfree(f.seq); dfree(f.sp); dfree(f.slot); dfree(f.cell_start); dfree(f.grid);
+        dfree(f.row_space); dfree(f.row_ntiles); dfree(f.tiles);
     }
     dfree(w->sx); dfree(w->sz); dfree(w->sseq); dfree(w->ssp); dfree(w->sslot);
     dfree(w->ox); dfree(w->oz); dfree(w->oseq); dfree(w->osp);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->rank); dfree(w->lastop); dfree(w->new_slots_d);
-    dfree(w->counts); dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
-    dfree(w->events); dfree(w->err); dfree(w->total64); dfree(w->res); dfree(w->bbox);
+    dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
+    dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
+    dfree(w->err); dfree(w->d_rel); dfree(w->counter); dfree(w->res); dfree(w->bbox);
     dfree(w->nb_out); dfree(w->nb_count);
     if (w->h_res) (void)hipHostFree(w->h_res);
     if (w->h_bbox) (void)hipHostFree(w->h_bbox);
@@ -709,13 +786,14 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->rank, N)) || (rc = dalloc(w, &w->lastop, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||
-        (rc = dalloc(w, &w->counts, 2 * N + 1)) || (rc = dalloc(w, &w->err, 1)) || (rc = dalloc(w, &w->total64, 1)) ||
+        (rc = dalloc(w, &w->err, 1)) || (rc = dalloc(w, &w->d_rel, 1)) || (rc = dalloc(w, &w->counter, 1)) ||
         (rc = dalloc(w, &w->res, 1)) || (rc = dalloc(w, &w->bbox, 4 * (size_t)w->max_spaces)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->lastop, 0, N * sizeof(unsigned long long)) != hipSuccess) return fail(GWAOI_EDEVICE);
     if (hipMemset(w->rank, 0xFF, N * sizeof(uint32_t)) != hipSuccess) return fail(GWAOI_EDEVICE);
-    if ((rc = ensure_scan_tmp(w, std::max<size_t>(2 * N + 1, gw::radix_hist_elems((uint32_t)N))))) return fail(rc);
+    if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
+    if ((rc = ensure_tile_entries(w, 2 * (size_t)gw::tile_bound((uint32_t)N, 1024)))) return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     if ((rc = ensure_events(w, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
         return fail(rc);

@@ -306,3 +306,80 @@ def test_device_batch_errors_reported_gpu():
         with pytest.raises(GwaoiError):
             w.tick()
         assert w.neighbors(0).size == 0
+
+
+@pytest.mark.parametrize("seed,spaces", [(31, 1), (32, 3)])
+def test_mixed_churn_vs_closed_form_gpu(oracle_mod, seed, spaces):
+    """Steps, teleports (far movers), leaves, re-enters and space changes in
+    one flush: exercises the combined pass and the special-entity pass.  The
+    reference is the closed form evaluated on the queued state (seq = call order)."""
+    rng = np.random.default_rng(seed)
+    n = 12000
+    L = float(np.sqrt(n / spaces * 1250.0))
+    Ds = {s: np.float32(100.0 if s != 1 else 60.0) for s in range(spaces)}
+    x = (rng.uniform(-L / 2, L / 2, n)).astype(np.float32)
+    z = (rng.uniform(-L / 2, L / 2, n)).astype(np.float32)
+    sp = rng.integers(0, spaces, n).astype(np.uint32)
+    seq = np.zeros(n, np.uint64)
+    live = np.ones(n, bool)
+    nxt = 1
+    with World(n, max_spaces=spaces) as w:
+        ids = [w.space_create(Ds[s]) for s in range(spaces)]
+        order = rng.permutation(n)
+        for i in order:
+            w.enter(ids[sp[i]], int(i), x[i], z[i])
+            seq[i] = nxt
+            nxt += 1
+        w.tick()
+
+        def cf():
+            # relation keyed by (space, a, b): every space is its own go-aoi manager, so a
+            # pair related in space 0 before and in space 2 after is a leave AND an enter
+            spv = np.where(live, sp, oracle_mod.DEAD).astype(np.uint32)
+            k = oracle_mod.closed_form_pairs(x, z, seq, spv, Ds)
+            a = (k >> np.uint64(32)).astype(np.int64)
+            return np.sort((spv[a].astype(np.uint64) << np.uint64(56)) | ((k >> np.uint64(32)) << np.uint64(28))
+                           | (k & np.uint64(0xFFFFFFF)))
+
+        def ab(keys):
+            return np.sort(((keys >> np.uint64(28)) & np.uint64(0xFFFFFFF)) << np.uint64(32)
+                           | (keys & np.uint64(0xFFFFFFF)))
+
+        prev = cf()
+        for t in range(6):
+            ops = []
+            for i in rng.permutation(n):
+                r = rng.random()
+                if live[i]:
+                    if r < 0.01:
+                        ops.append(("leave", i))
+                    elif r < 0.02:  # leave + enter another (or the same) space: space change
+                        ops.append(("leave", i))
+                        ops.append(("enter", i, int(rng.integers(spaces)), rng.uniform(-L / 2, L / 2),
+                                    rng.uniform(-L / 2, L / 2)))
+                    elif r < 0.05:  # teleport
+                        ops.append(("move", i, rng.uniform(-L / 2, L / 2), rng.uniform(-L / 2, L / 2)))
+                    elif r < 0.95:
+                        ops.append(("move", i, x[i] + rng.uniform(-1, 1), z[i] + rng.uniform(-1, 1)))
+                elif r < 0.3:
+                    ops.append(("enter", i, int(rng.integers(spaces)), rng.uniform(-L / 2, L / 2),
+                                rng.uniform(-L / 2, L / 2)))
+            for op in ops:
+                if op[0] == "leave":
+                    w.leave(int(op[1]))
+                    live[op[1]] = False
+                elif op[0] == "enter":
+                    i, s_, xi, zi = op[1], op[2], np.float32(op[3]), np.float32(op[4])
+                    w.enter(ids[s_], int(i), xi, zi)
+                    live[i], sp[i], x[i], z[i], seq[i] = True, s_, xi, zi, nxt
+                    nxt += 1
+                else:
+                    i, xi, zi = op[1], np.float32(op[2]), np.float32(op[3])
+                    w.moved(int(i), xi, zi)
+                    x[i], z[i], seq[i] = xi, zi, nxt
+                    nxt += 1
+            ge, gl = flush(w)
+            cur = cf()
+            np.testing.assert_array_equal(ge, ab(np.setdiff1d(cur, prev)))
+            np.testing.assert_array_equal(gl, ab(np.setdiff1d(prev, cur)))
+            prev = cur
