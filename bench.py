@@ -51,12 +51,28 @@ def dist_env():
     return ws, rank, local
 
 
-def pair_pass_bytes(n: int, events: float) -> float:
-    """Algorithmic HBM bytes of one pair-pass launch over n frame entries
-    (DESIGN.md §Roofline): own record x,z,seq,sp (24 B) + other-time record
-    x,z,seq,sp (24 B) + grid row bounds (~8 cell_start reads, 32 B) +
-    count write / offset read (4 B) + slot (4 B) + 8 B per event written."""
-    return n * 88.0 + 8.0 * events
+def combined_pass_bytes(n: int, total_cells: int, events: float) -> float:
+    """Algorithmic HBM bytes of one k_combined launch (Roofline):
+    every frame entry once as the tile's own entity -- new record (x, z, seq:
+    16 B) + previous-flush record (16 B) -- the cell_start index (4 B per
+    cell) and two directed (slot, slot) pairs per event (16 B).  Candidate
+    re-reads of neighbouring rows are L2/LDS reuse, not algorithmic traffic."""
+    return n * 32.0 + (total_cells + 1) * 4.0 + 16.0 * events
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_k_combined.json")
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per k_combined launch from the committed PMC pass
+    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), if one matches."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(args, wl_factory, target_s: float):
@@ -204,22 +220,23 @@ def main():
 
     if rank == 0:
         lat_ms = np.array(lat) * 1e3
-        # dominant kernel = the costliest stage per tick
+        # dominant kernel = the costliest stage per tick (HIP events on the world's stream)
         roofline = None
         stage_ms = {k: v[0] / max(v[1], 1) for k, v in stages.items() if v[1]}
         if stage_ms:
             dom = max((k for k in stage_ms if k != "d2h"), key=lambda k: stage_ms[k])
             ev_tick = events / max(args.steps, 1)
-            if dom.endswith(("_count", "_fill")):
-                alg = pair_pass_bytes(n, ev_tick / 2 if dom.endswith("_fill") else 0.0)
-            else:
-                alg = None
-            if alg is not None:
+            if dom == "combined":
+                alg = combined_pass_bytes(n, info["total_cells"], ev_tick)
                 t_s = stage_ms[dom] * 1e-3
                 ach = alg / t_s / 1e9
-                roofline = {"bound": "hbm", "kernel": f"k_pairs ({dom})", "achieved": round(ach, 2),
+                roofline = {"bound": "hbm", "kernel": "k_combined", "achieved": round(ach, 2),
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-                            "traffic": None, "alg_bytes_per_launch": alg,
+                            "traffic": pmc_traffic(args.workload), "alg_bytes_per_launch": alg,
+                            "avg_launch_ms": round(stage_ms[dom], 4)}
+            else:
+                roofline = {"bound": "hbm", "kernel": dom, "achieved": None, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": None, "traffic": None,
                             "avg_launch_ms": round(stage_ms[dom], 4)}
         cpu = None
         if not args.no_cpu_baseline:

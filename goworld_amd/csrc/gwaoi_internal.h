@@ -18,14 +18,25 @@ constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreem
 
 constexpr uint32_t TILE_A = 256;  // entities per pair-pass tile (= threads per workgroup)
 
+// One entity state: position (go-aoi Coord = float32) and the sequence
+// number of its last Enter/Moved call.  16 B, one vector access.
+struct alignas(16) Rec16 {
+    float x, z;
+    unsigned long long s;
+};
+
+struct alignas(8) SlotSp {  // caller slot handle + space id (SP_DEAD = not live)
+    uint32_t slot, sp;
+};
+
 // Uniform grid of one space for one flush.  Cell (cx,cz) of space s has the
 // global cell key base + cz*gx + cx; its grid row cz is global row
 // row_base + cz.  cellOf() is monotone in the coordinate, so a query range
 // derived from conservative window bounds is complete.
 struct SpaceGrid {
-    float ox, oz;   // grid origin
-    float inv;      // 1 / cell size
-    float D;        // AOI distance of the space (go-aoi aoidist)
+    float ox, oz;  // grid origin
+    float inv;     // 1 / cell size
+    float D;       // AOI distance of the space (go-aoi aoidist)
     uint32_t gx, gz;
     uint32_t base;
     uint32_t row_base;
@@ -39,58 +50,61 @@ struct Tile {
 // One flush's sorted state: entries [0, n) are the live entities ordered by
 // cell key (space-major, then cz, cx), stable in the previous order.
 struct FrameView {
-    const float *x, *z;
-    const uint64_t *seq;
-    const uint32_t *sp, *slot;
+    const Rec16 *rec;
+    const SlotSp *ss;
     const uint32_t *cell_start;  // total_cells + 1 entries
     const SpaceGrid *grid;
     uint32_t n;
     uint32_t total_cells;
 };
 
-// The state at the *other* time of a pair pass, stored in the frame's order.
-struct StateView {
-    const float *x, *z;
-    const uint64_t *seq;
-    const uint32_t *sp;
-};
-
 struct TileSet {  // the pair-pass tiles of one frame
     const Tile *tiles;
-    const uint32_t *n_tiles;     // device count
-    const uint32_t *row_space;   // space id of every global grid row
-    uint32_t bound;              // host upper bound on *n_tiles (launch size)
+    const uint32_t *n_tiles;    // device count
+    const uint32_t *row_space;  // space id of every global grid row
+    uint32_t bound;             // host upper bound on *n_tiles (launch size)
 };
 
-struct TickResult {  // device -> host summary of one tick
+// Per-tick scalars written by device kernels.
+struct TickScalars {
+    uint32_t err;
+    uint32_t pad;
+    unsigned long long counter;  // directed event pairs reserved by the pair passes
+    float d_rel;                 // largest displacement / D of "near" entities
+    float bmax;                  // largest |x|,|z| of live entities (new positions)
+};
+
+// Device -> host block copied once per tick: result + per-space bbox.
+struct TickOut {
     uint32_t n_enter;
     uint32_t n_total;
     uint32_t err;
     uint32_t pad;
     unsigned long long total64;
+    // followed by int4 bbox[n_spaces] (ordered-int min x, min z, max x, max z)
 };
 
 // ---- launchers (gwaoi_kernels.hip) ------------------------------------------
-void launch_copy_state(uint32_t n, const float *p_x, const float *p_z, const uint64_t *p_seq, const uint32_t *p_sp,
-                       const uint32_t *p_slot, float *s_x, float *s_z, uint64_t *s_seq, uint32_t *s_sp,
-                       uint32_t *s_slot, hipStream_t st);
-void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, uint32_t *s_slot,
-                          uint32_t *s_sp, uint64_t *s_seq, uint32_t *rank, hipStream_t st);
+// Zero the per-tick counters and two ranges; bbox entries get the fold identity.
+void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
+                     uint32_t n_spaces, hipStream_t st);
+void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec, SlotSp *s_ss,
+                       hipStream_t st);
+void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
+                          uint32_t *rank, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
 // means a device-resident Moved batch (keep the space).
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots,
-                      unsigned long long *lastop, uint32_t tick_id, uint32_t *err, hipStream_t st);
+                      unsigned long long *lastop, uint32_t tick_id, TickScalars *sc, hipStream_t st);
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
                       uint32_t j0, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
-                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, float *s_x, float *s_z,
-                      uint64_t *s_seq, uint32_t *s_sp, const uint32_t *s_slot, uint32_t *err, hipStream_t st);
-// keygen also folds d_rel (int-encoded float, zeroed by the caller): the
-// largest per-axis displacement / D of entities that stayed in their space
-// and moved at most D/4.
-void launch_keygen(const float *s_x, const float *s_z, const uint32_t *s_sp, uint32_t n_total,
-                   const SpaceGrid *grid, uint32_t sentinel, uint32_t *keys, uint32_t *vals, const float *p_x,
-                   const float *p_z, const uint32_t *p_sp, const SpaceGrid *p_grid, uint32_t n_prev, int *d_rel,
-                   hipStream_t st);
+                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss,
+                      TickScalars *sc, hipStream_t st);
+// Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
+// partials in blk, 2 * cdiv(n, 256) floats).
+void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
+                   uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
+                   const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
@@ -105,12 +119,10 @@ size_t radix_hist_elems(uint32_t n);
 void scan_exclusive(const uint32_t *in, uint32_t *out, size_t n, uint32_t *tmp, hipStream_t st);
 size_t scan_tmp_elems(size_t n);
 
-void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const float *s_x, const float *s_z,
-                   const uint64_t *s_seq, const uint32_t *s_sp, const uint32_t *s_slot, const float *p_x,
-                   const float *p_z, const uint64_t *p_seq, const uint32_t *p_sp, float *f_x, float *f_z,
-                   uint64_t *f_seq, uint32_t *f_sp, uint32_t *f_slot, float *o_x, float *o_z, uint64_t *o_seq,
-                   uint32_t *o_sp, uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel,
-                   uint32_t n_total, uint32_t *err, hipStream_t st);
+void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec,
+                   uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel, uint32_t n_total,
+                   TickScalars *sc, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
 // Tiles of a frame: rows split into runs of <= TILE_A entities.
@@ -119,22 +131,28 @@ void build_tiles(FrameView F, uint32_t n_space_ids, uint32_t n_rows, uint32_t *r
                  Tile *tiles, uint32_t *scan_tmp, hipStream_t st);
 inline uint32_t tile_bound(uint32_t n, uint32_t n_rows) { return (n + TILE_A - 1) / TILE_A + n_rows; }
 
-// mode 2 = combined pass over the new frame (other = previous state in the
-// new order); mode 1 = special-entity pass over the previous frame (other =
-// new state in the previous order).  Directed event pairs go to tmp at an
-// atomically reserved offset per tile; per tile t the enter total/base are
-// at [tile_off + t] and the leave total/base at [leave_off + tile_off + t].
-void launch_pairs(int mode, FrameView F, StateView O, TileSet T, uint64_t seq_base, const float *d_rel,
-                  unsigned long long *counter, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
+// mode 2 = combined pass over the new frame (O = previous state in the new
+// order, NaN coordinates where not live in the same space); mode 1 =
+// special-entity pass over the previous frame (O = S', the new state in the
+// previous order, with O_ss giving its space).  Directed event pairs go to
+// tmp at an atomically reserved offset per tile; per tile t the enter
+// total/base are at [tile_off + t], the leave total/base at
+// [leave_off + tile_off + t].
+void launch_pairs(int mode, FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, TileSet T, uint64_t seq_base,
+                  TickScalars *sc, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
                   unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st);
 // Copy every tile's events from tmp into tile order (dest = scanned tile_total).
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
                     uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
                     hipStream_t st);
-void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const uint32_t *err,
-                   const unsigned long long *counter, TickResult *res, hipStream_t st);
-void launch_bbox(FrameView F, int *bbox, uint32_t max_spaces, hipStream_t st);
+void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const TickScalars *sc,
+                   TickOut *out, hipStream_t st);
+// Per-space bounding box into the int4 array that follows TickOut.
+size_t bbox_part_bytes(uint32_t n);
+void launch_bbox(FrameView F, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st);
 void launch_neighbors(FrameView F, const uint32_t *rank, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);
+// Zero `n` uint32 (rare re-run path).
+void launch_zero(uint32_t *p, size_t n, hipStream_t st);
 
 }  // namespace gw

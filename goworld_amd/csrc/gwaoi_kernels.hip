@@ -1,25 +1,27 @@
-// gwaoi_kernels.hip -- HIP kernels of the AOI tick for gfx950 (MI355X).
+// gwaoi_kernels.hip -- HIP kernels of the AOI flush for gfx950 (MI355X).
 //
 // One flush (gwaoi_tick) runs, on one stream:
-//   ops_claim/ops_apply  last-writer-wins application of the queued
-//                        Enter/Leave/Moved calls (seq = call order) onto the
-//                        working copy S' of the previous frame
-//   keygen               cell key per entity (space-major uniform grid)
+//   prologue             zero the per-tick counters / ranges
+//   copy_state + ops     S' = previous frame, then the queued Enter/Leave/
+//                        Moved calls applied last-writer-wins (seq = call
+//                        order; only the final state of a slot matters)
+//   keygen               cell key per entity (space-major uniform grid), and
+//                        the per-tick scalars d_rel (largest "near" move / D)
+//                        and bmax (largest |coordinate|)
 //   radix sort           stable LSD sort of (key, index), wave64 multisplit
-//   gather               new frame (sorted SoA) + old state in the new order
-//   cell_count + scan    cell_start table
-//   build_tiles          rows split into tiles of <= 256 entities
-//   pairs (x2)           one workgroup per tile stages the tile's candidate
-//                        rows in LDS and emits enter events (new grid) or
-//                        leave events (previous grid); both evaluate go-aoi's
-//                        float32 window predicate with last-mover ownership
-//                         at both times
-//   reorder              events into deterministic tile order
+//   gather               new frame (sorted) + previous state in the new order
+//   cell_count + scan    cell_start table;  tiles: rows cut into <= 256 entities
+//   pairs<2>             combined pass over the new grid: every unordered pair
+//                        once, go-aoi's float32 window relation at t and t-1
+//                        (last-mover ownership)
+//   pairs<1>             leaves of "special" entities (left, changed space,
+//                        moved > D/4) over the previous grid
+//   reorder + finish     events into deterministic tile order, summary
+//   bbox                 per-space bounding box for the next flush's grid
 //
-// The path is sort/scan/gather/compaction: integer and float32-compare work
-// bounded by HBM and on-chip bandwidth, no dense contraction, so no MFMA.
-// Compile with -ffp-contract=off: the window bounds must be plain float32
-// sums exactly as in go-aoi (`coord - sl.aoidist`).
+// The path is sort/scan/gather/compaction: integer and float32-compare work,
+// no dense contraction, so no MFMA.  Compile with -ffp-contract=off: the
+// window bounds must be plain float32 sums as in go-aoi (`coord - aoidist`).
 
 #include "gwaoi_internal.h"
 
@@ -44,51 +46,86 @@ __device__ __forceinline__ int cell_of(float v, float o, float inv, uint32_t g) 
     return (int)t;
 }
 
-// L inside W's window [fl32(w-D), fl32(w+D)]^2 (bounds precomputed by the caller)
-__device__ __forceinline__ bool in_win(float lx, float lz, float lox, float hix, float loz, float hiz) {
-    return lx >= lox && lx <= hix && lz >= loz && lz <= hiz;
+__device__ __forceinline__ Rec16 ld_rec(const Rec16 *p, uint32_t i) {
+    const uint4 q = reinterpret_cast<const uint4 *>(p)[i];
+    Rec16 r;
+    r.x = __uint_as_float(q.x);
+    r.z = __uint_as_float(q.y);
+    r.s = ((unsigned long long)q.w << 32) | q.z;
+    return r;
 }
 
-// go-aoi relation of a pair under last-mover ownership
-__device__ __forceinline__ bool related(float xa, float za, uint64_t sa, float lox, float hix, float loz, float hiz,
-                                        float xb, float zb, uint64_t sb, float D) {
-    return sa > sb ? in_win(xb, zb, lox, hix, loz, hiz) : in_win(xa, za, xb - D, xb + D, zb - D, zb + D);
+__device__ __forceinline__ void st_rec(Rec16 *p, uint32_t i, const Rec16 &r) {
+    reinterpret_cast<uint4 *>(p)[i] =
+        make_uint4(__float_as_uint(r.x), __float_as_uint(r.z), (uint32_t)r.s, (uint32_t)(r.s >> 32));
+}
+
+__device__ __forceinline__ SlotSp ld_ss(const SlotSp *p, uint32_t i) {
+    const uint2 q = reinterpret_cast<const uint2 *>(p)[i];
+    SlotSp r;
+    r.slot = q.x;
+    r.sp = q.y;
+    return r;
+}
+
+__device__ __forceinline__ void st_ss(SlotSp *p, uint32_t i, uint32_t slot, uint32_t sp) {
+    reinterpret_cast<uint2 *>(p)[i] = make_uint2(slot, sp);
+}
+
+__device__ __forceinline__ float qnan() { return __int_as_float(0x7FC00000); }
+
+// ------------------------------------------------------------- prologue ------
+
+__global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t *z1, uint32_t n1, int4 *bbox,
+                           uint32_t n_spaces) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        sc->err = 0;
+        sc->counter = 0;
+        sc->d_rel = 0.0f;
+        sc->bmax = 0.0f;
+    }
+    if (i < n0) z0[i] = 0;
+    if (i < n1) z1[i] = 0;
+    if (i < n_spaces) bbox[i] = make_int4(INT_MAX, INT_MAX, INT_MIN, INT_MIN);
+}
+
+__global__ void k_zero(uint32_t *p, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
 }
 
 // ------------------------------------------------------------ op apply ------
 
-__global__ void k_copy_state(uint32_t n, const float *__restrict__ p_x, const float *__restrict__ p_z,
-                             const uint64_t *__restrict__ p_seq, const uint32_t *__restrict__ p_sp,
-                             const uint32_t *__restrict__ p_slot, float *s_x, float *s_z, uint64_t *s_seq,
-                             uint32_t *s_sp, uint32_t *s_slot) {
+__global__ void k_copy_state(uint32_t n, const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
+                             Rec16 *s_rec, SlotSp *s_ss) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    s_x[i] = p_x[i];
-    s_z[i] = p_z[i];
-    s_seq[i] = p_seq[i];
-    s_sp[i] = p_sp[i];
-    s_slot[i] = p_slot[i];
+    reinterpret_cast<uint4 *>(s_rec)[i] = reinterpret_cast<const uint4 *>(p_rec)[i];
+    reinterpret_cast<uint2 *>(s_ss)[i] = reinterpret_cast<const uint2 *>(p_ss)[i];
 }
 
 __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t n_prev,
-                                uint32_t *s_slot, uint32_t *s_sp, uint64_t *s_seq, uint32_t *rank) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                Rec16 *s_rec, SlotSp *s_ss, uint32_t *rank) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_app) return;
-    uint32_t s = new_slots[i];
-    uint32_t idx = n_prev + i;
-    s_slot[idx] = s;
-    s_sp[idx] = SP_DEAD;
-    s_seq[idx] = 0;
+    const uint32_t s = new_slots[i];
+    const uint32_t idx = n_prev + i;
+    Rec16 r;
+    r.x = r.z = 0.0f;
+    r.s = 0;
+    st_rec(s_rec, idx, r);
+    st_ss(s_ss, idx, s, SP_DEAD);
     rank[s] = idx;
 }
 
 __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint32_t j0, uint32_t max_slots,
-                            unsigned long long *lastop, uint32_t tick, uint32_t *err) {
+                            unsigned long long *lastop, uint32_t tick, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slots[i];
     if (s >= max_slots) {
-        atomicOr(err, ERR_BAD_SLOT);
+        atomicOr(&sc->err, ERR_BAD_SLOT);
         return;
     }
     atomicMax(&lastop[s], ((unsigned long long)tick << 32) | (j0 + i));
@@ -99,9 +136,8 @@ __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint
 __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
                             const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t n, uint32_t j0,
                             uint32_t max_slots, const unsigned long long *__restrict__ lastop, uint32_t tick,
-                            const uint32_t *__restrict__ rank, uint32_t n_total, uint64_t seq_base, float *s_x,
-                            float *s_z, uint64_t *s_seq, uint32_t *s_sp, const uint32_t *__restrict__ s_slot,
-                            uint32_t *err) {
+                            const uint32_t *__restrict__ rank, uint32_t n_total, uint64_t seq_base, Rec16 *s_rec,
+                            SlotSp *s_ss, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t j = j0 + i;
@@ -109,67 +145,123 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
     if (s >= max_slots) return;
     if (lastop[s] != (((unsigned long long)tick << 32) | j)) return;
     const uint32_t idx = rank[s];
-    if (idx >= n_total || s_slot[idx] != s) {
-        atomicOr(err, ERR_MOVE_DEAD);
+    const SlotSp cur = idx < n_total ? ld_ss(s_ss, idx) : SlotSp{SP_DEAD, SP_DEAD};
+    if (cur.slot != s) {
+        atomicOr(&sc->err, ERR_MOVE_DEAD);
         return;
     }
     uint32_t sp = sps ? sps[i] : SP_KEEP;
+    Rec16 r;
+    r.s = seq_base + j;
     if (sp == SP_DEAD) {  // Leave
-        s_sp[idx] = SP_DEAD;
-        s_seq[idx] = seq_base + j;
+        r.x = r.z = 0.0f;
+        st_rec(s_rec, idx, r);
+        st_ss(s_ss, idx, s, SP_DEAD);
         return;
     }
-    if (sp == SP_KEEP) {  // device-side Moved
-        sp = s_sp[idx];
+    const bool keep = sp == SP_KEEP;
+    if (keep) {  // device-side Moved
+        sp = cur.sp;
         if (sp == SP_DEAD) {
-            atomicOr(err, ERR_MOVE_DEAD);
+            atomicOr(&sc->err, ERR_MOVE_DEAD);
             return;
         }
     }
-    const float x = xs[i], z = zs[i];
-    if (!isfinite(x) || !isfinite(z)) {
-        atomicOr(err, ERR_NONFINITE);
+    r.x = xs[i];
+    r.z = zs[i];
+    if (!isfinite(r.x) || !isfinite(r.z)) {
+        atomicOr(&sc->err, ERR_NONFINITE);
         return;
     }
-    s_x[idx] = x;
-    s_z[idx] = z;
-    s_seq[idx] = seq_base + j;
-    s_sp[idx] = sp;
+    st_rec(s_rec, idx, r);
+    if (!keep && sp != cur.sp) st_ss(s_ss, idx, s, sp);
 }
 
 // --------------------------------------------------------------- keygen ------
 
-// Also folds d_rel = max over "near" entities (live at t-1 and t in the same
-// space, moved at most FAR_FRAC*D per axis) of displacement / D.
-__global__ void k_keygen(const float *__restrict__ x, const float *__restrict__ z, const uint32_t *__restrict__ sp,
-                         uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel, uint32_t *keys,
-                         uint32_t *vals, const float *__restrict__ p_x, const float *__restrict__ p_z,
-                         const uint32_t *__restrict__ p_sp, const SpaceGrid *__restrict__ p_grid, uint32_t n_prev,
-                         int *d_rel) {
+constexpr float FAR_FRAC = 0.25f;  // displacement > FAR_FRAC * D per axis => "special"
+
+// "near" = live at t-1 and at t in the same space and moved at most
+// FAR_FRAC*D per axis.  The special pass uses the complement, computed from
+// the same operands.
+__device__ __forceinline__ bool is_near(float xn, float zn, float xo, float zo, float thr) {
+    return (int)(fabsf(xn - xo) <= thr) & (int)(fabsf(zn - zo) <= thr);
+}
+
+__global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
+                                                uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
+                                                uint32_t *keys, uint32_t *vals, const Rec16 *__restrict__ p_rec,
+                                                const SlotSp *__restrict__ p_ss,
+                                                const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk) {
+    __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    float dr = 0.0f;
+    float dr = 0.0f, bm = 0.0f;
     if (i < n) {
-        const uint32_t s = sp[i];
+        const uint32_t s = ld_ss(s_ss, i).sp;
         uint32_t key = sentinel;
-        const float xi = x[i], zi = z[i];
         if (s != SP_DEAD) {
+            const Rec16 r = ld_rec(s_rec, i);
             const SpaceGrid g = grid[s];
-            const int cx = cell_of(xi, g.ox, g.inv, g.gx);
-            const int cz = cell_of(zi, g.oz, g.inv, g.gz);
+            const int cx = cell_of(r.x, g.ox, g.inv, g.gx);
+            const int cz = cell_of(r.z, g.oz, g.inv, g.gz);
             key = g.base + (uint32_t)cz * g.gx + (uint32_t)cx;
-            if (i < n_prev && p_sp[i] == s) {
+            bm = fmaxf(fabsf(r.x), fabsf(r.z));
+            if (i < n_prev && ld_ss(p_ss, i).sp == s) {
+                const Rec16 p = ld_rec(p_rec, i);
                 const float D = p_grid[s].D;
-                const float dx = fabsf(xi - p_x[i]), dz = fabsf(zi - p_z[i]);
-                const float thr = 0.25f * D;
-                if (dx <= thr && dz <= thr) dr = fmaxf(dx, dz) / D;
+                if (is_near(r.x, r.z, p.x, p.z, FAR_FRAC * D)) dr = fmaxf(fabsf(r.x - p.x), fabsf(r.z - p.z)) / D;
             }
         }
         keys[i] = key;
         vals[i] = i;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) dr = fmaxf(dr, __shfl_xor(dr, o));
-    if (lane() == 0 && dr > 0.0f) atomicMax(d_rel, __float_as_int(dr));
+    for (int o = 32; o > 0; o >>= 1) {
+        dr = fmaxf(dr, __shfl_xor(dr, o));
+        bm = fmaxf(bm, __shfl_xor(bm, o));
+    }
+    if (lane() == 0) {
+        s_m[0][threadIdx.x / WAVE] = dr;
+        s_m[1][threadIdx.x / WAVE] = bm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a = s_m[0][0], b = s_m[1][0];
+        for (int q = 1; q < 256 / WAVE; ++q) {
+            a = fmaxf(a, s_m[0][q]);
+            b = fmaxf(b, s_m[1][q]);
+        }
+        blk[2 * blockIdx.x] = a;
+        blk[2 * blockIdx.x + 1] = b;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict__ blk, uint32_t nb,
+                                                        TickScalars *sc) {
+    __shared__ float s_m[2][1024 / WAVE];
+    float a = 0.0f, b = 0.0f;
+    for (uint32_t i = threadIdx.x; i < nb; i += 1024) {
+        a = fmaxf(a, blk[2 * i]);
+        b = fmaxf(b, blk[2 * i + 1]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a = fmaxf(a, __shfl_xor(a, o));
+        b = fmaxf(b, __shfl_xor(b, o));
+    }
+    if (lane() == 0) {
+        s_m[0][threadIdx.x / WAVE] = a;
+        s_m[1][threadIdx.x / WAVE] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < 1024 / WAVE; ++q) {
+            a = fmaxf(a, s_m[0][q]);
+            b = fmaxf(b, s_m[1][q]);
+        }
+        sc->d_rel = a;
+        sc->bmax = b;
+    }
 }
 
 // ----------------------------------------------------------------- scan ------
@@ -177,6 +269,9 @@ __global__ void k_keygen(const float *__restrict__ x, const float *__restrict__ 
 constexpr int SC_T = 256;
 constexpr int SC_I = 16;
 constexpr int SC_TILE = SC_T * SC_I;
+constexpr int SC1_T = 1024;  // single-workgroup scan
+constexpr int SC1_I = 16;
+constexpr size_t SC1_MAX = (size_t)SC1_T * SC1_I * 4;  // loops over chunks of SC1_T*SC1_I
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 #pragma unroll
@@ -187,7 +282,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
-// exclusive scan of one value per thread over a 256-thread block
+// exclusive scan of one value per thread over a block of NT threads
+template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, uint32_t &total) {
     uint32_t x = wave_incl_scan(v);
     const int w = threadIdx.x / WAVE;
@@ -195,7 +291,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, ui
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < SC_T / WAVE; ++i) {
+    for (int i = 0; i < NT / WAVE; ++i) {
         uint32_t t = ws[i];
         pre += (i < w) ? t : 0u;
         tot += t;
@@ -204,11 +300,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, ui
     return pre + x - v;
 }
 
-__device__ __forceinline__ void load16(const uint32_t *in, size_t base, size_t n, uint32_t (&v)[SC_I]) {
-    if (base + SC_I <= n) {
+template <int NI>
+__device__ __forceinline__ void loadN(const uint32_t *in, size_t base, size_t n, uint32_t (&v)[NI]) {
+    if (base + NI <= n) {
         const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
 #pragma unroll
-        for (int q = 0; q < SC_I / 4; ++q) {
+        for (int q = 0; q < NI / 4; ++q) {
             uint4 t = p[q];
             v[4 * q] = t.x;
             v[4 * q + 1] = t.y;
@@ -217,37 +314,17 @@ __device__ __forceinline__ void load16(const uint32_t *in, size_t base, size_t n
         }
     } else {
 #pragma unroll
-        for (int q = 0; q < SC_I; ++q) v[q] = (base + q < n) ? in[base + q] : 0u;
+        for (int q = 0; q < NI; ++q) v[q] = (base + q < n) ? in[base + q] : 0u;
     }
 }
 
-__global__ __launch_bounds__(SC_T) void k_scan_reduce(const uint32_t *__restrict__ in, size_t n, uint32_t *sums) {
-    __shared__ uint32_t ws[SC_T / WAVE];
-    uint32_t v[SC_I];
-    load16(in, (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I, n, v);
-    uint32_t s = 0;
-#pragma unroll
-    for (int q = 0; q < SC_I; ++q) s += v[q];
-    uint32_t tot;
-    block_excl_scan(s, ws, tot);
-    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(SC_T) void k_scan_down(const uint32_t *in, uint32_t *out, size_t n,
-                                                    const uint32_t *__restrict__ block_off) {
-    __shared__ uint32_t ws[SC_T / WAVE];
-    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I;
-    uint32_t v[SC_I];
-    load16(in, base, n, v);
-    uint32_t s = 0;
-#pragma unroll
-    for (int q = 0; q < SC_I; ++q) s += v[q];
-    uint32_t tot;
-    uint32_t run = block_excl_scan(s, ws, tot) + (block_off ? block_off[blockIdx.x] : 0u);
-    if (base + SC_I <= n) {
+template <int NI>
+__device__ __forceinline__ void storeN_excl(uint32_t *out, size_t base, size_t n, const uint32_t (&v)[NI],
+                                            uint32_t run) {
+    if (base + NI <= n) {
         uint4 *p = reinterpret_cast<uint4 *>(out + base);
 #pragma unroll
-        for (int q = 0; q < SC_I / 4; ++q) {
+        for (int q = 0; q < NI / 4; ++q) {
             uint4 t;
             t.x = run; run += v[4 * q];
             t.y = run; run += v[4 * q + 1];
@@ -257,7 +334,7 @@ __global__ __launch_bounds__(SC_T) void k_scan_down(const uint32_t *in, uint32_t
         }
     } else {
 #pragma unroll
-        for (int q = 0; q < SC_I; ++q)
+        for (int q = 0; q < NI; ++q)
             if (base + q < n) {
                 out[base + q] = run;
                 run += v[q];
@@ -265,32 +342,88 @@ __global__ __launch_bounds__(SC_T) void k_scan_down(const uint32_t *in, uint32_t
     }
 }
 
+__global__ __launch_bounds__(SC_T) void k_scan_reduce(const uint32_t *__restrict__ in, size_t n, uint32_t *sums) {
+    __shared__ uint32_t ws[SC_T / WAVE];
+    uint32_t v[SC_I];
+    loadN<SC_I>(in, (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I, n, v);
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q) s += v[q];
+    uint32_t tot;
+    block_excl_scan<SC_T>(s, ws, tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SC_T) void k_scan_down(const uint32_t *in, uint32_t *out, size_t n,
+                                                    const uint32_t *__restrict__ block_off) {
+    __shared__ uint32_t ws[SC_T / WAVE];
+    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I;
+    uint32_t v[SC_I];
+    loadN<SC_I>(in, base, n, v);
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q) s += v[q];
+    uint32_t tot;
+    const uint32_t run = block_excl_scan<SC_T>(s, ws, tot) + (block_off ? block_off[blockIdx.x] : 0u);
+    storeN_excl<SC_I>(out, base, n, v, run);
+}
+
+// one workgroup, chunks of SC1_T*SC1_I with a running carry (small arrays)
+__global__ __launch_bounds__(SC1_T) void k_scan_single(const uint32_t *in, uint32_t *out, size_t n) {
+    __shared__ uint32_t ws[SC1_T / WAVE];
+    uint32_t carry = 0;
+    for (size_t c0 = 0; c0 < n; c0 += (size_t)SC1_T * SC1_I) {
+        const size_t base = c0 + (size_t)threadIdx.x * SC1_I;
+        uint32_t v[SC1_I];
+        loadN<SC1_I>(in, base, n, v);
+        uint32_t s = 0;
+#pragma unroll
+        for (int q = 0; q < SC1_I; ++q) s += v[q];
+        uint32_t tot;
+        const uint32_t run = block_excl_scan<SC1_T>(s, ws, tot) + carry;
+        storeN_excl<SC1_I>(out, base, n, v, run);
+        carry += tot;
+        __syncthreads();
+    }
+}
+
 // ----------------------------------------------------------- radix sort ------
-// Tile = 4 waves x 8 items x 64 lanes.  Element (wave w, item j, lane l) is
-// index tile*2048 + w*512 + j*64 + l, so processing items in order per wave
-// and waves in order keeps the sort stable.
+// Tile = 4 waves x RS_I items x 64 lanes.  Element (wave w, item j, lane l)
+// is index tile*RS_TILE + w*RS_WSEG + j*64 + l, so processing items in order
+// per wave and waves in order keeps the sort stable.
 
 constexpr int RS_T = 256;
-constexpr int RS_I = 8;
+constexpr int RS_I = 16;
 constexpr int RS_TILE = RS_T * RS_I;
 constexpr int RS_WAVES = RS_T / WAVE;
 constexpr int RS_WSEG = WAVE * RS_I;
 
 __global__ __launch_bounds__(RS_T) void k_rs_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
                                                      int nbits, uint32_t *hist, uint32_t ntiles) {
-    __shared__ uint32_t h[256];
+    __shared__ uint32_t h[RS_WAVES][256];
     const int bins = 1 << nbits;
     const uint32_t mask = (uint32_t)bins - 1u;
-    for (int i = threadIdx.x; i < bins; i += RS_T) h[i] = 0;
+    const int w = threadIdx.x / WAVE;
+    for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_T) (&h[0][0])[i] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * RS_TILE;
-#pragma unroll
+#pragma unroll 4
     for (int i = 0; i < RS_I; ++i) {
-        size_t idx = base + (size_t)i * RS_T + threadIdx.x;
-        if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & mask], 1u);
+        const size_t idx = base + (size_t)i * RS_T + threadIdx.x;
+        const bool valid = idx < n;
+        const uint32_t d = valid ? (keys[idx] >> shift) & mask : 0u;
+        // wave-aggregated increment: one LDS add per distinct digit of the wave
+        unsigned long long peers = __ballot(valid);
+        for (int b = 0; b < nbits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        if (valid && (int)lane() == __ffsll((long long)peers) - 1) h[w][d] += (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < bins; d += RS_T) hist[(size_t)d * ntiles + blockIdx.x] = h[d];
+    for (int d = threadIdx.x; d < bins; d += RS_T)
+        hist[(size_t)d * ntiles + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
 __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restrict__ keys_in,
@@ -313,6 +446,11 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
         const bool valid = idx < n;
         k[j] = valid ? keys_in[idx] : 0u;
         v[j] = valid ? vals_in[idx] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        const size_t idx = wbase + (size_t)j * WAVE + l;
+        const bool valid = idx < n;
         const uint32_t d = (k[j] >> shift) & mask;
         unsigned long long peers = __ballot(valid);
         for (int b = 0; b < nbits; ++b) {
@@ -355,37 +493,25 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 // --------------------------------------------------------------- gather ------
 
 __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
-                         const float *__restrict__ s_x, const float *__restrict__ s_z,
-                         const uint64_t *__restrict__ s_seq, const uint32_t *__restrict__ s_sp,
-                         const uint32_t *__restrict__ s_slot, const float *__restrict__ p_x,
-                         const float *__restrict__ p_z, const uint64_t *__restrict__ p_seq,
-                         const uint32_t *__restrict__ p_sp, float *f_x, float *f_z, uint64_t *f_seq, uint32_t *f_sp,
-                         uint32_t *f_slot, float *o_x, float *o_z, uint64_t *o_seq, uint32_t *o_sp, uint32_t *rank,
-                         const uint32_t *__restrict__ sorted_keys, uint32_t sentinel, uint32_t n_total,
-                         uint32_t *err) {
+                         const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
+                         const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
+                         SlotSp *f_ss, Rec16 *o_rec, uint32_t *rank, const uint32_t *__restrict__ sorted_keys,
+                         uint32_t sentinel, uint32_t n_total, TickScalars *sc) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(err, ERR_COUNT_MISMATCH);
+    if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     if (k >= n_new) return;
-    if (sorted_keys[k] == sentinel) atomicOr(err, ERR_COUNT_MISMATCH);
+    if (sorted_keys[k] == sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     const uint32_t i = perm[k];
-    const uint32_t slot = s_slot[i];
-    f_x[k] = s_x[i];
-    f_z[k] = s_z[i];
-    f_seq[k] = s_seq[i];
-    f_sp[k] = s_sp[i];
-    f_slot[k] = slot;
-    rank[slot] = k;
-    if (i < n_prev) {
-        o_x[k] = p_x[i];
-        o_z[k] = p_z[i];
-        o_seq[k] = p_seq[i];
-        o_sp[k] = p_sp[i];
-    } else {
-        o_x[k] = 0.0f;
-        o_z[k] = 0.0f;
-        o_seq[k] = 0;
-        o_sp[k] = SP_DEAD;
-    }
+    const SlotSp ss = ld_ss(s_ss, i);
+    reinterpret_cast<uint4 *>(f_rec)[k] = reinterpret_cast<const uint4 *>(s_rec)[i];
+    reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(ss.slot, ss.sp);
+    rank[ss.slot] = k;
+    // previous state of the same entity, NaN position unless live in the same space then
+    Rec16 o;
+    o.x = o.z = qnan();
+    o.s = 0;
+    if (i < n_prev && ld_ss(p_ss, i).sp == ss.sp) o = ld_rec(p_rec, i);
+    st_rec(o_rec, k, o);
 }
 
 // Entities per cell from the sorted keys: one atomic per run of equal keys
@@ -417,7 +543,11 @@ __global__ void k_row_space(const SpaceGrid *__restrict__ grid, uint32_t n_space
 
 __global__ void k_row_tiles(FrameView F, const uint32_t *__restrict__ row_space, uint32_t n_rows, uint32_t *cnt) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rows) return;
+    if (r > n_rows) return;
+    if (r == n_rows) {
+        cnt[r] = 0;
+        return;
+    }
     const SpaceGrid g = F.grid[row_space[r]];
     const uint32_t c0 = g.base + (r - g.row_base) * g.gx;
     const uint32_t n_row = F.cell_start[c0 + g.gx] - F.cell_start[c0];
@@ -444,106 +574,84 @@ __global__ void k_fill_tiles(FrameView F, const uint32_t *__restrict__ row_space
 
 // ---------------------------------------------------------------- pairs ------
 // A flush's events are the diff of the go-aoi relation N between the
-// previous state (t-1) and the new state (t) of every pair:
+// previous state (t-1) and the new state (t):
 //   enter(A,B) = N_t(A,B) && !N_t-1(A,B),   leave(A,B) = N_t-1(A,B) && !N_t(A,B)
 // N is symmetric in the pair, so each unordered pair is evaluated once and
 // emitted in both directions.
 //
-// MODE 2 (combined): over the NEW grid.  The entity with the lower frame index
-//   enumerates its partners (own cell row from a+1, then the rows above)
-//   inside the symmetric box |dx|,|dz| <= H + margin, H = D(1 + 2 d_rel),
-//   d_rel = the largest displacement / D of any "near" entity this flush.
-//   Every pair with N_t is inside the box; so is every pair with N_t-1 whose
-//   members both moved at most d_rel*D ("near").
-// MODE 1 (special): over the PREVIOUS grid, only for entities that left,
-//   changed space, or moved more than D/4 ("special").  Emits the leaves of
-//   pairs the combined pass could not see (box test false at t).  A pair of
-//   two specials is emitted by the one with the lower previous-frame index.
-// Invalid other-time state (not live in this space then) is staged as NaN
-// coordinates, which makes every window test false.
+// MODE 2 (combined), over the NEW grid.  The member with the lower frame
+//   index enumerates (its own cell row from a+1, then the rows above) and
+//   keeps the pairs inside the symmetric box |dx|,|dz| <= H + M with
+//   H = D(1 + 2 d_rel) and M = (bmax + 3D) 2^-20 (float32 rounding of the
+//   window bounds and of the differences).  Every pair with N_t is inside;
+//   so is every pair with N_t-1 whose members both moved at most d_rel*D
+//   ("near").  Entities not live in this space at t-1 carry NaN old
+//   coordinates, which makes N_t-1 false.
+// MODE 1 (special), over the PREVIOUS grid, for entities that left, changed
+//   space or moved more than D/4: emits the leaves of pairs that the
+//   combined pass could not see (box test false at t).  A pair of two
+//   specials is emitted by the one with the lower previous-frame index.
 
 constexpr int PT = (int)TILE_A;  // threads per workgroup = entities per tile
-constexpr int PCAP = 1024;       // candidates staged in LDS per chunk
-constexpr int PS = 8;            // events buffered in LDS per thread
+constexpr int PCAP = 512;        // candidates staged in LDS per chunk
+constexpr int PS = 4;            // events buffered in LDS per thread
 constexpr int PMAXR = 32;        // candidate rows a tile may span (else global path)
-constexpr float FAR_FRAC = 0.25f;  // displacement > FAR_FRAC * D => special
 constexpr uint32_t KIND_LEAVE = 0x80000000u;
 
 // go-aoi relation: the owner (larger seq) W's window [fl32(w-D), fl32(w+D)]^2 contains the other
-__device__ __forceinline__ bool rel(float xa, float za, uint64_t sa, float xb, float zb, uint64_t sb, float D) {
+__device__ __forceinline__ bool rel(float xa, float za, unsigned long long sa, float xb, float zb,
+                                    unsigned long long sb, float D) {
     const bool own = sa > sb;
     const float wx = own ? xa : xb, wz = own ? za : zb;
     const float px = own ? xb : xa, pz = own ? zb : za;
     return (int)(px >= wx - D) & (int)(px <= wx + D) & (int)(pz >= wz - D) & (int)(pz <= wz + D);
 }
 
-// symmetric candidate box: |b-a| <= H + (max|coord| + K) * 2^-20 per axis
-__device__ __forceinline__ bool near_sym(float xa, float za, float xb, float zb, float H, float K) {
-    const float mx = (fmaxf(fabsf(xa), fabsf(xb)) + K) * 0x1p-20f;
-    const float mz = (fmaxf(fabsf(za), fabsf(zb)) + K) * 0x1p-20f;
-    return (int)(fabsf(xb - xa) <= H + mx) & (int)(fabsf(zb - za) <= H + mz);
-}
-
-// "special" = left / changed space (NaN new position) or moved more than thr
-__device__ __forceinline__ bool is_special(float xn, float zn, float xo, float zo, float thr) {
-    return !((int)(fabsf(xn - xo) <= thr) & (int)(fabsf(zn - zo) <= thr));
-}
-
-__device__ __forceinline__ float load_drel(const float *p) { return p ? *p : 0.0f; }
-
-struct Rec {  // 16 B staged record
-    float x, z;
-    uint64_t s;
-};
-
-template <int MODE>
-struct PairIn {  // the entity that enumerates (A)
-    Rec now, oth;  // MODE 2: now = t, oth = t-1; MODE 1: now = t-1, oth = t
-    uint32_t a;    // frame index
-    float D, H, K, thr;
-    uint64_t seq_base;
+struct PairCtx {
+    Rec16 now, oth;  // MODE 2: t, t-1 (NaN if absent);  MODE 1: t-1, t (NaN if absent)
+    uint32_t a;      // frame index
+    float D, HM;     // AOI distance, H + M (combined box half-width)
+    unsigned long long seq_base;
     bool chg;
 };
 
-// frame entry j as (this-frame record, other-time record with NaN if invalid)
-__device__ __forceinline__ void load_rec(const FrameView &F, const StateView &O, uint32_t j, Rec &now, Rec &oth) {
-    now.x = F.x[j];
-    now.z = F.z[j];
-    now.s = F.seq[j];
-    const bool ok = O.sp[j] == F.sp[j];
-    oth.x = ok ? O.x[j] : __int_as_float(0x7FC00000);
-    oth.z = ok ? O.z[j] : __int_as_float(0x7FC00000);
-    oth.s = O.seq[j];
-}
-
-// Event kind of pair (A, B): 0 none, 1 enter, 2 leave.
+// 0: no event, 1: enter, 2: leave.  Branch-free.
 template <int MODE>
-__device__ __forceinline__ int pair_kind(const PairIn<MODE> &A, const Rec &bn, const Rec &bo, uint32_t b) {
+__device__ __forceinline__ int pair_kind(const PairCtx &A, const Rec16 &bn, const Rec16 &bo, uint32_t b,
+                                         float thr) {
     if (MODE == 2) {
-        if (!near_sym(A.now.x, A.now.z, bn.x, bn.z, A.H, A.K)) return 0;
-        if (!A.chg && bn.s < A.seq_base) return 0;  // neither touched: unchanged
+        const bool inb = (int)(fabsf(bn.x - A.now.x) <= A.HM) & (int)(fabsf(bn.z - A.now.z) <= A.HM);
+        const bool chg = A.chg | (bn.s >= A.seq_base);
         const bool nt = rel(A.now.x, A.now.z, A.now.s, bn.x, bn.z, bn.s, A.D);
         const bool no = rel(A.oth.x, A.oth.z, A.oth.s, bo.x, bo.z, bo.s, A.D);
-        return nt == no ? 0 : (nt ? 1 : 2);
+        const int k = (int)nt + 2 * (int)no;  // 1: nt only (enter), 2: no only (leave)
+        return (inb & chg & (nt != no)) ? k : 0;
     } else {
-        // previous grid; A is special.  now = t-1 state, oth = t state
-        if (!near_sym(A.now.x, A.now.z, bn.x, bn.z, A.D, 2.0f * A.D)) return 0;
-        if (!rel(A.now.x, A.now.z, A.now.s, bn.x, bn.z, bn.s, A.D)) return 0;       // not related at t-1
-        if (rel(A.oth.x, A.oth.z, A.oth.s, bo.x, bo.z, bo.s, A.D)) return 0;         // still related at t
-        if (near_sym(A.oth.x, A.oth.z, bo.x, bo.z, A.H, A.K)) return 0;              // combined pass saw it
-        if (is_special(bo.x, bo.z, bn.x, bn.z, A.thr) && b < A.a) return 0;          // the other special emits
-        return 2;
+        const bool was = rel(A.now.x, A.now.z, A.now.s, bn.x, bn.z, bn.s, A.D);
+        const bool is = rel(A.oth.x, A.oth.z, A.oth.s, bo.x, bo.z, bo.s, A.D);
+        const bool seen = (int)(fabsf(bo.x - A.oth.x) <= A.HM) & (int)(fabsf(bo.z - A.oth.z) <= A.HM);
+        const bool b_special = !is_near(bo.x, bo.z, bn.x, bn.z, thr);
+        const bool mine = !(b_special && b < A.a);
+        return (was & !is & !seen & mine) ? 2 : 0;
     }
+}
+
+// other-time record of frame entry j (MODE 1 derives validity from O_ss)
+template <int MODE>
+__device__ __forceinline__ Rec16 other_rec(const FrameView &F, const Rec16 *O_rec, const SlotSp *O_ss, uint32_t j) {
+    Rec16 o = ld_rec(O_rec, j);
+    if (MODE == 1 && ld_ss(O_ss, j).sp != ld_ss(F.ss, j).sp) o.x = o.z = qnan();
+    return o;
 }
 
 // Row-major enumeration of A's partners straight from HBM/L2 (fallback and
 // overflow path; same order and predicate as the LDS path).  Counts events
 // per kind; when WRITE, writes (A,B),(B,A) for events number >= skip.
 template <int MODE, bool WRITE>
-__device__ void enum_global(const FrameView &F, const StateView &O, const SpaceGrid &g, const PairIn<MODE> &A,
-                            int cx0, int cx1, int cz0, int cz1, uint32_t skip, uint2 *out, unsigned long long pe,
-                            unsigned long long pl, uint64_t cap, uint32_t &ne, uint32_t &nl) {
-    const uint32_t slot_a = WRITE ? F.slot[A.a] : 0u;
+__device__ void enum_global(const FrameView &F, const Rec16 *O_rec, const SlotSp *O_ss, const SpaceGrid &g,
+                            const PairCtx &A, float thr, int cx0, int cx1, int cz0, int cz1, uint32_t skip, uint2 *out,
+                            unsigned long long pe, unsigned long long pl, uint64_t cap, uint32_t &ne, uint32_t &nl) {
+    const uint32_t slot_a = WRITE ? ld_ss(F.ss, A.a).slot : 0u;
     uint32_t k = 0;
     for (int cz = cz0; cz <= cz1; ++cz) {
         const uint32_t row = g.base + (uint32_t)cz * g.gx;
@@ -552,12 +660,12 @@ __device__ void enum_global(const FrameView &F, const StateView &O, const SpaceG
         if (MODE == 2 && cz == cz0) jb = A.a + 1;
         for (uint32_t b = jb; b < je; ++b) {
             if (MODE == 1 && b == A.a) continue;
-            Rec bn, bo;
-            load_rec(F, O, b, bn, bo);
-            const int kind = pair_kind<MODE>(A, bn, bo, b);
+            const Rec16 bn = ld_rec(F.rec, b);
+            const Rec16 bo = other_rec<MODE>(F, O_rec, O_ss, b);
+            const int kind = pair_kind<MODE>(A, bn, bo, b, thr);
             if (!kind) continue;
             if (WRITE && k >= skip) {
-                const uint32_t slot_b = F.slot[b];
+                const uint32_t slot_b = ld_ss(F.ss, b).slot;
                 const unsigned long long p = kind == 1 ? pe + 2ull * ne : pl + 2ull * nl;
                 if (p + 1 < cap) {
                     out[p] = make_uint2(slot_a, slot_b);
@@ -574,12 +682,14 @@ __device__ void enum_global(const FrameView &F, const StateView &O, const SpaceG
 }
 
 template <int MODE>
-__global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet TS, uint64_t seq_base,
-                                              const float *__restrict__ d_rel, unsigned long long *counter,
-                                              uint2 *tmp, uint64_t cap, uint32_t *tile_total,
-                                              unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off) {
-    __shared__ float4 s_now[PCAP];
-    __shared__ float4 s_oth[PCAP];
+__global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restrict__ O_rec,
+                                              const SlotSp *__restrict__ O_ss, TileSet TS,
+                                              unsigned long long seq_base, const TickScalars *__restrict__ sc,
+                                              unsigned long long *counter, uint2 *tmp, uint64_t cap,
+                                              uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
+                                              uint32_t leave_off) {
+    __shared__ uint4 s_now[PCAP];
+    __shared__ uint4 s_oth[PCAP];
     __shared__ uint32_t s_slot[PCAP];
     __shared__ uint32_t s_ev[PS * PT];
     __shared__ int s_box[4];
@@ -593,45 +703,39 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet 
     const Tile T = TS.tiles[t];
     const uint32_t tid = threadIdx.x;
     const SpaceGrid g = F.grid[TS.row_space[T.row]];
-    const float drel = load_drel(d_rel);
-    PairIn<MODE> A;
+    const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f;
+    const float thr = FAR_FRAC * g.D;
+    PairCtx A;
     A.D = g.D;
-    A.H = g.D * (1.0f + 2.0f * drel);
-    A.K = 3.0f * g.D;
-    A.thr = FAR_FRAC * g.D;
+    A.HM = g.D * (1.0f + 2.0f * sc->d_rel) + M;
     A.seq_base = seq_base;
     A.a = T.e0 + tid;
     bool active = A.a < T.e1;
     int cx0 = 0, cx1 = -1, cz0 = 0, cz1 = -1;
     if (active) {
-        load_rec(F, O, A.a, A.now, A.oth);
+        A.now = ld_rec(F.rec, A.a);
+        A.oth = other_rec<MODE>(F, O_rec, O_ss, A.a);
         if (MODE == 2) {
             A.chg = A.now.s >= seq_base;
-            const float mr = (fabsf(A.now.x) + 2.0f * A.H + A.K) * 0x1p-19f;
-            const float mz = (fabsf(A.now.z) + 2.0f * A.H + A.K) * 0x1p-19f;
-            cx0 = cell_of(A.now.x - A.H - mr, g.ox, g.inv, g.gx);
-            cx1 = cell_of(A.now.x + A.H + mr, g.ox, g.inv, g.gx);
-            cz0 = cell_of(A.now.z, g.oz, g.inv, g.gz);  // own row (= the tile's row)
-            cz1 = cell_of(A.now.z + A.H + mz, g.oz, g.inv, g.gz);
+            const float r = A.HM + M;
+            cx0 = cell_of(A.now.x - r, g.ox, g.inv, g.gx);
+            cx1 = cell_of(A.now.x + r, g.ox, g.inv, g.gx);
+            cz0 = cell_of(A.now.z, g.oz, g.inv, g.gz);  // own row (the tile's row)
+            cz1 = cell_of(A.now.z + r, g.oz, g.inv, g.gz);
         } else {
             A.chg = true;
-            active = is_special(A.oth.x, A.oth.z, A.now.x, A.now.z, A.thr);
-            const float mr = (fabsf(A.now.x) + 3.0f * A.D) * 0x1p-19f;
-            const float mz = (fabsf(A.now.z) + 3.0f * A.D) * 0x1p-19f;
-            cx0 = cell_of(A.now.x - A.D - mr, g.ox, g.inv, g.gx);
-            cx1 = cell_of(A.now.x + A.D + mr, g.ox, g.inv, g.gx);
+            active = !is_near(A.oth.x, A.oth.z, A.now.x, A.now.z, thr);
+            // every partner with N_t-1: |dx| <= D + (|x| + 2D) 2^-24
+            const float mx = (fabsf(A.now.x) + 3.0f * A.D) * 0x1p-20f;
+            const float mz = (fabsf(A.now.z) + 3.0f * A.D) * 0x1p-20f;
+            cx0 = cell_of(A.now.x - A.D - mx, g.ox, g.inv, g.gx);
+            cx1 = cell_of(A.now.x + A.D + mx, g.ox, g.inv, g.gx);
             cz0 = cell_of(A.now.z - A.D - mz, g.oz, g.inv, g.gz);
             cz1 = cell_of(A.now.z + A.D + mz, g.oz, g.inv, g.gz);
         }
     }
-    if (MODE == 1 && !__syncthreads_or(active)) {  // no special entity in this tile
-        if (tid == 0) {
-            tile_total[tile_off + t] = 0;
-            tile_total[leave_off + tile_off + t] = 0;
-        }
-        return;
-    }
-    // tile box = union of the active entities' query cells (wave reductions, then LDS)
+    if (MODE == 1 && !__syncthreads_or(active)) return;  // no special entity: totals stay 0
+    // tile box = union of the active entities' query cells
     {
         int v0 = active ? cx0 : INT_MAX, v1 = active ? cx1 : INT_MIN;
         int v2 = active ? cz0 : INT_MAX, v3 = active ? cz1 : INT_MIN;
@@ -682,11 +786,11 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet 
                 const uint32_t v = base + i;
                 while (v >= s_pre[r + 1]) ++r;
                 const uint32_t j = s_seg[r] + (v - s_pre[r]);
-                Rec bn, bo;
-                load_rec(F, O, j, bn, bo);
-                s_now[i] = make_float4(bn.x, bn.z, __uint_as_float((uint32_t)bn.s), __uint_as_float((uint32_t)(bn.s >> 32)));
-                s_oth[i] = make_float4(bo.x, bo.z, __uint_as_float((uint32_t)bo.s), __uint_as_float((uint32_t)(bo.s >> 32)));
-                s_slot[i] = F.slot[j];
+                s_now[i] = reinterpret_cast<const uint4 *>(F.rec)[j];
+                const Rec16 o = other_rec<MODE>(F, O_rec, O_ss, j);
+                s_oth[i] = make_uint4(__float_as_uint(o.x), __float_as_uint(o.z), (uint32_t)o.s,
+                                      (uint32_t)(o.s >> 32));
+                s_slot[i] = ld_ss(F.ss, j).slot;
             }
             __syncthreads();
             if (active) {
@@ -696,20 +800,22 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet 
                     uint32_t jb = F.cell_start[row + (uint32_t)cx0];
                     const uint32_t je = F.cell_start[row + (uint32_t)cx1 + 1u];
                     if (MODE == 2 && cz == cz0) jb = A.a + 1;
+                    if (jb >= je) continue;
                     const uint32_t vb = s_pre[rr] + (jb - s_seg[rr]);
-                    const uint32_t ve = vb + (je - jb);
-                    const uint32_t lo = max(vb, base), hi = min(ve, base + lim);
+                    const uint32_t lo = max(vb, base), hi = min(vb + (je - jb), base + lim);
                     for (uint32_t v = lo; v < hi; ++v) {
                         const uint32_t i = v - base;
                         const uint32_t b = jb + (v - vb);
-                        if (MODE == 1 && b == A.a) continue;
-                        const float4 qn = s_now[i], qo = s_oth[i];
-                        Rec bn, bo;
-                        bn.x = qn.x; bn.z = qn.y;
-                        bn.s = ((uint64_t)__float_as_uint(qn.w) << 32) | __float_as_uint(qn.z);
-                        bo.x = qo.x; bo.z = qo.y;
-                        bo.s = ((uint64_t)__float_as_uint(qo.w) << 32) | __float_as_uint(qo.z);
-                        const int kind = pair_kind<MODE>(A, bn, bo, b);
+                        const uint4 qn = s_now[i], qo = s_oth[i];
+                        Rec16 bn, bo;
+                        bn.x = __uint_as_float(qn.x);
+                        bn.z = __uint_as_float(qn.y);
+                        bn.s = ((unsigned long long)qn.w << 32) | qn.z;
+                        bo.x = __uint_as_float(qo.x);
+                        bo.z = __uint_as_float(qo.y);
+                        bo.s = ((unsigned long long)qo.w << 32) | qo.z;
+                        int kind = pair_kind<MODE>(A, bn, bo, b, thr);
+                        if (MODE == 1 && b == A.a) kind = 0;
                         if (kind) {
                             if (nk < PS) s_ev[nk * PT + tid] = s_slot[i] | (kind == 2 ? KIND_LEAVE : 0u);
                             ++nk;
@@ -722,13 +828,13 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet 
             __syncthreads();
         }
     } else if (active) {
-        enum_global<MODE, false>(F, O, g, A, cx0, cx1, cz0, cz1, 0, nullptr, 0, 0, 0, ne, nl);
+        enum_global<MODE, false>(F, O_rec, O_ss, g, A, thr, cx0, cx1, cz0, cz1, 0, nullptr, 0, 0, 0, ne, nl);
     }
-    // offsets: directed pairs = 2 per event, enters then leaves of the tile
+    // offsets: directed pairs = 2 per event, the tile's enters then its leaves
     uint32_t te, tl;
-    const uint32_t oe = block_excl_scan(2 * ne, s_ws, te);
+    const uint32_t oe = block_excl_scan<PT>(2 * ne, s_ws, te);
     __syncthreads();
-    const uint32_t ol = block_excl_scan(2 * nl, s_ws, tl);
+    const uint32_t ol = block_excl_scan<PT>(2 * nl, s_ws, tl);
     if (tid == 0) {
         const uint32_t tot = te + tl;
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
@@ -742,7 +848,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet 
     if (active && (ne | nl)) {
         const unsigned long long pe = s_base + oe, pl = s_base + te + ol;
         if (staged) {
-            const uint32_t slot_a = F.slot[A.a];
+            const uint32_t slot_a = ld_ss(F.ss, A.a).slot;
             const uint32_t k = min(nk, (uint32_t)PS);
             uint32_t ie = 0, il = 0;
             for (uint32_t q = 0; q < k; ++q) {
@@ -759,37 +865,402 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, StateView O, TileSet 
             }
             if (nk > PS) {
                 uint32_t we = 0, wl = 0;  // continue after the buffered events, in order
-                enum_global<MODE, true>(F, O, g, A, cx0, cx1, cz0, cz1, PS, tmp, pe + 2ull * ie, pl + 2ull * il,
-                                        cap, we, wl);
+                enum_global<MODE, true>(F, O_rec, O_ss, g, A, thr, cx0, cx1, cz0, cz1, PS, tmp, pe + 2ull * ie,
+                                        pl + 2ull * il, cap, we, wl);
             }
         } else {
             uint32_t we = 0, wl = 0;
-            enum_global<MODE, true>(F, O, g, A, cx0, cx1, cz0, cz1, 0, tmp, pe, pl, cap, we, wl);
+            enum_global<MODE, true>(F, O_rec, O_ss, g, A, thr, cx0, cx1, cz0, cz1, 0, tmp, pe, pl, cap, we, wl);
         }
     }
 }
 
-__global__ void k_reorder(const uint32_t *__restrict__ dest, const uint32_t *__restrict__ tile_total,
-                          const unsigned long long *__restrict__ tile_base, uint32_t n_entries,
-                          const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap) {
-    const uint32_t e = blockIdx.x;
-    if (e >= n_entries) return;
-    const uint32_t cnt = tile_total[e];
-    if (!cnt) return;
-    const unsigned long long src = tile_base[e];
-    const uint64_t dst = dest[e];
-    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x)
-        if (src + k < cap && dst + k < cap) out[dst + k] = tmp[src + k];
+// ------------------------------------------------------- combined pass ------
+// Wave-per-entity form of MODE 2.  A tile's candidate rows are staged in LDS
+// in chunks; each wave takes the tile's entities A in turn (A's state is
+// wave-uniform) and its 64 lanes sweep A's candidates.  A cheap exact filter
+// keeps only the pairs that can have an event:
+//   * neither member touched this flush            -> no event
+//   * both members "near" (moved <= d_rel*D, live in the same space at t-1):
+//     N_t != N_t-1 needs one axis with ||d| - D| <= BW and the other with
+//     |d| <= D + BW at t (BW = 2 d_rel D + M: the displacement of both
+//     members plus the float32 rounding of the window bounds); everything
+//     else keeps its relation
+//   * a "jumper" member (new, changed space, moved > D/4) -> always tested
+// Survivors go to a per-wave LDS queue and get the full go-aoi test
+// (pair_kind<2>) with lanes over queue entries.  Events are buffered per
+// wave in processing order (deterministic); a wave whose buffer overflows
+// replays its sweep and writes the rest straight to the output.
+
+constexpr int CT = 256;
+constexpr int CW = CT / WAVE;
+constexpr int CCAP = 512;   // staged candidates per chunk
+constexpr int QCAP = 256;   // per-wave queue of band survivors
+constexpr int EVW = 128;    // events buffered per wave
+constexpr int AROWS = 6;    // candidate rows per entity (else the per-thread fallback)
+constexpr uint32_t FL_JUMP = 1u, FL_CHG = 2u;
+
+struct CombinedLds {
+    uint4 c4[CCAP];     // staged candidate: x, z (bits), FL_* flags, frame index
+    uint2 q[CW][QCAP];  // queued pairs of a wave: (A's thread index, B's frame index)
+    uint2 ev[CW][EVW];  // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
+    uint32_t seg[PMAXR];
+    uint32_t pre[PMAXR + 1];
+    int box[4];
+    uint32_t wcnt[CW][2];
+    uint32_t ws[CW];
+    unsigned long long base;
+    uint32_t te, tl;
+    int fallback, overflow;
+};
+
+// The lane's own entity A: position, flags and candidate rows as virtual
+// ranges [vb, ve) of the tile's staged candidate list.
+struct LaneA {
+    float x, z;
+    uint32_t fl;
+    uint32_t vb[AROWS], ve[AROWS];
+};
+
+__device__ __forceinline__ uint32_t flags_of(const Rec16 &now, const Rec16 &old, unsigned long long seq_base,
+                                             float thr) {
+    // old NaN (not live in this space at t-1) also fails is_near
+    return (is_near(now.x, now.z, old.x, old.z, thr) ? 0u : FL_JUMP) | (now.s >= seq_base ? FL_CHG : 0u);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+// Full test of the queued pairs of wave w; appends events (deterministic order).
+// REPLAY: count only, and write events number >= EVW straight to the output.
+template <bool REPLAY>
+__device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, const FrameView &F,
+                                            const Rec16 *__restrict__ O_rec, uint32_t e0, const PairCtx &proto,
+                                            float thr, uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap,
+                                            unsigned long long pe, unsigned long long pl) {
+    const uint32_t ln = lane();
+    for (uint32_t q0 = 0; q0 < qn; q0 += WAVE) {
+        const uint32_t e = q0 + ln;
+        int kind = 0;
+        uint32_t a = 0, b = 0;
+        if (e < qn) {
+            const uint2 q = L.q[w][e];
+            a = e0 + q.x;
+            b = q.y;
+            PairCtx A = proto;
+            A.a = a;
+            A.now = ld_rec(F.rec, a);
+            A.oth = ld_rec(O_rec, a);
+            A.chg = A.now.s >= proto.seq_base;
+            const Rec16 bn = ld_rec(F.rec, b), bo = ld_rec(O_rec, b);
+            kind = pair_kind<2>(A, bn, bo, b, thr);
+        }
+        const unsigned long long em = __ballot(kind == 1), lm = __ballot(kind == 2);
+        const uint32_t pos = ne + nl + (uint32_t)__popcll((em | lm) & lanemask_lt());
+        if (kind) {
+            const uint32_t a_slot = ld_ss(F.ss, a).slot, b_slot = ld_ss(F.ss, b).slot;
+            if (!REPLAY) {
+                if (pos < EVW) L.ev[w][pos] = make_uint2(a_slot, b_slot | (kind == 2 ? KIND_LEAVE : 0u));
+            } else if (pos >= EVW) {
+                const uint32_t kidx = kind == 1 ? ne + (uint32_t)__popcll(em & lanemask_lt())
+                                                : nl + (uint32_t)__popcll(lm & lanemask_lt());
+                const unsigned long long p = (kind == 1 ? pe : pl) + 2ull * kidx;
+                if (p + 1 < cap) {
+                    out[p] = make_uint2(a_slot, b_slot);
+                    out[p + 1] = make_uint2(b_slot, a_slot);
+                }
+            }
+        }
+        ne += (uint32_t)__popcll(em);
+        nl += (uint32_t)__popcll(lm);
+    }
+}
+
+// One full sweep of the tile (all chunks).  Every wave takes part in staging;
+// only `work` waves filter and test.  Each lane sweeps its own entity's
+// candidate rows; the loop bounds are wave-uniform (max over lanes).
+template <bool REPLAY>
+__device__ void combined_sweep(CombinedLds &L, const FrameView &F, const Rec16 *__restrict__ O_rec, uint32_t e0,
+                               uint32_t nrows, const LaneA &me, const PairCtx &proto, float thr, float BW, bool work,
+                               uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap, unsigned long long pe,
+                               unsigned long long pl) {
+    const uint32_t tid = threadIdx.x;
+    const int w = tid / WAVE;
+    const uint32_t Ltot = L.pre[nrows];
+    const float D = proto.D, HM = proto.HM, DB = proto.D + BW;
+    uint32_t qn = 0;
+    for (uint32_t base = 0; base < Ltot; base += CCAP) {
+        const uint32_t lim = min(Ltot - base, (uint32_t)CCAP);
+        {  // stage candidates [base, base+lim)
+            int r = 0;
+            for (uint32_t i = tid; i < lim; i += CT) {
+                const uint32_t v = base + i;
+                while (v >= L.pre[r + 1]) ++r;
+                const uint32_t j = L.seg[r] + (v - L.pre[r]);
+                const Rec16 bn = ld_rec(F.rec, j);
+                const Rec16 bo = ld_rec(O_rec, j);
+                L.c4[i] = make_uint4(__float_as_uint(bn.x), __float_as_uint(bn.z),
+                                     flags_of(bn, bo, proto.seq_base, thr), j);
+            }
+        }
+        __syncthreads();
+        if (work) {
+#pragma unroll
+            for (int r = 0; r < AROWS; ++r) {
+                if ((uint32_t)r >= nrows) break;  // uniform
+                const uint32_t lo = max(me.vb[r], base), hi = min(me.ve[r], base + lim);
+                const uint32_t len = hi > lo ? hi - lo : 0u;
+                const uint32_t i0 = lo - base;
+                const uint32_t mx = wave_max_u32(len);
+                for (uint32_t t = 0; t < mx; ++t) {
+                    const bool valid = t < len;
+                    const uint4 c = L.c4[valid ? i0 + t : 0u];
+                    const float dx = fabsf(__uint_as_float(c.x) - me.x), dz = fabsf(__uint_as_float(c.y) - me.z);
+                    const uint32_t fl = c.z | me.fl;
+                    const bool band = ((int)(fabsf(dx - D) <= BW) & (int)(dz <= DB)) |
+                                      ((int)(fabsf(dz - D) <= BW) & (int)(dx <= DB));
+                    const bool keep = valid & (int)(dx <= HM) & (int)(dz <= HM) & (int)((fl & FL_CHG) != 0u) &
+                                      ((int)((fl & FL_JUMP) != 0u) | (int)band);
+                    const unsigned long long m = __ballot(keep);
+                    if (keep) L.q[w][qn + (uint32_t)__popcll(m & lanemask_lt())] = make_uint2(tid, c.w);
+                    qn += (uint32_t)__popcll(m);
+                    if (qn > QCAP - WAVE) {
+                        __builtin_amdgcn_wave_barrier();
+                        drain_queue<REPLAY>(L, w, qn, F, O_rec, e0, proto, thr, ne, nl, out, cap, pe, pl);
+                        qn = 0;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (work && qn) {
+        __builtin_amdgcn_wave_barrier();
+        drain_queue<REPLAY>(L, w, qn, F, O_rec, e0, proto, thr, ne, nl, out, cap, pe, pl);
+    }
+}
+
+__global__ __launch_bounds__(CT) void k_combined(FrameView F, const Rec16 *__restrict__ O_rec, TileSet TS,
+                                                 unsigned long long seq_base, const TickScalars *__restrict__ sc,
+                                                 unsigned long long *counter, uint2 *out, uint64_t cap,
+                                                 uint32_t *tile_total, unsigned long long *tile_base,
+                                                 uint32_t tile_off, uint32_t leave_off) {
+    __shared__ CombinedLds L;
+    const uint32_t t = blockIdx.x;
+    if (t >= *TS.n_tiles) return;  // uniform per workgroup
+    const Tile T = TS.tiles[t];
+    const uint32_t tid = threadIdx.x, ln = lane();
+    const int w = tid / WAVE;
+    const uint32_t nA = T.e1 - T.e0;
+    const SpaceGrid g = F.grid[TS.row_space[T.row]];
+    const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f;
+    const float thr = FAR_FRAC * g.D;
+    PairCtx proto;
+    proto.D = g.D;
+    proto.HM = g.D * (1.0f + 2.0f * sc->d_rel) + M;
+    proto.seq_base = seq_base;
+    proto.a = 0;
+    proto.chg = false;
+    const float BW = 2.0f * sc->d_rel * g.D + M;
+    const float r = proto.HM + M;  // query reach
+
+    // ---- per-entity setup: state, flags, cell ranges
+    const bool active = tid < nA;
+    const uint32_t a = T.e0 + tid;
+    int cx0 = INT_MAX, cx1 = INT_MIN, cz0 = INT_MAX, cz1 = INT_MIN;
+    LaneA me;
+    me.x = me.z = 0.f;
+    me.fl = 0;
+    if (active) {
+        const Rec16 now = ld_rec(F.rec, a), old = ld_rec(O_rec, a);
+        me.x = now.x;
+        me.z = now.z;
+        me.fl = flags_of(now, old, seq_base, thr);
+        cx0 = cell_of(now.x - r, g.ox, g.inv, g.gx);
+        cx1 = cell_of(now.x + r, g.ox, g.inv, g.gx);
+        cz0 = cell_of(now.z, g.oz, g.inv, g.gz);  // own row (the tile's row)
+        cz1 = cell_of(now.z + r, g.oz, g.inv, g.gz);
+    }
+    {
+        int v0 = cx0, v1 = cx1, v2 = cz0, v3 = cz1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            v0 = min(v0, __shfl_xor(v0, o));
+            v1 = max(v1, __shfl_xor(v1, o));
+            v2 = min(v2, __shfl_xor(v2, o));
+            v3 = max(v3, __shfl_xor(v3, o));
+        }
+        if (tid == 0) {
+            L.box[0] = INT_MAX;
+            L.box[1] = INT_MIN;
+            L.box[2] = INT_MAX;
+            L.box[3] = INT_MIN;
+            L.fallback = 0;
+            L.overflow = 0;
+        }
+        __syncthreads();
+        if (ln == 0) {
+            atomicMin(&L.box[0], v0);
+            atomicMax(&L.box[1], v1);
+            atomicMin(&L.box[2], v2);
+            atomicMax(&L.box[3], v3);
+        }
+        if (active && cz1 - cz0 + 1 > AROWS) L.fallback = 1;
+        __syncthreads();
+    }
+    const int CX0 = L.box[0], CX1 = L.box[1], CZ0 = L.box[2], CZ1 = L.box[3];
+    const uint32_t nrows = (uint32_t)(CZ1 - CZ0 + 1);
+    if (nrows > AROWS) L.fallback = 1;  // every thread writes the same value
+    __syncthreads();
+    uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform); per thread in the fallback
+    if (!L.fallback) {
+        if (tid < nrows) {
+            const uint32_t row = g.base + (uint32_t)(CZ0 + (int)tid) * g.gx;
+            const uint32_t b = F.cell_start[row + (uint32_t)CX0];
+            L.seg[tid] = b;
+            L.pre[tid + 1] = F.cell_start[row + (uint32_t)CX1 + 1u] - b;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            L.pre[0] = 0;
+            for (uint32_t q = 0; q < nrows; ++q) L.pre[q + 1] += L.pre[q];
+        }
+        __syncthreads();
+        // this entity's candidate rows as virtual ranges (own row from a+1)
+#pragma unroll
+        for (int rr = 0; rr < AROWS; ++rr) {
+            me.vb[rr] = me.ve[rr] = 0;
+            const int cz = cz0 + rr;
+            if (active && cz <= cz1) {
+                const uint32_t row = g.base + (uint32_t)cz * g.gx;
+                uint32_t jb = F.cell_start[row + (uint32_t)cx0];
+                const uint32_t je = F.cell_start[row + (uint32_t)cx1 + 1u];
+                if (rr == 0) jb = a + 1;
+                const uint32_t vb = L.pre[cz - CZ0] + (jb - L.seg[cz - CZ0]);
+                me.vb[rr] = vb;
+                me.ve[rr] = vb + (je > jb ? je - jb : 0u);
+            }
+        }
+        combined_sweep<false>(L, F, O_rec, T.e0, nrows, me, proto, thr, BW, true, ne, nl, nullptr, 0, 0, 0);
+        if (ln == 0) {
+            L.wcnt[w][0] = ne;
+            L.wcnt[w][1] = nl;
+        }
+    } else if (active) {
+        PairCtx A = proto;
+        A.a = a;
+        A.now = ld_rec(F.rec, a);
+        A.oth = ld_rec(O_rec, a);
+        A.chg = A.now.s >= seq_base;
+        enum_global<2, false>(F, O_rec, nullptr, g, A, thr, cx0, cx1, cz0, cz1, 0, nullptr, 0, 0, 0, ne, nl);
+    }
+    // ---- offsets: 2 directed pairs per event; the tile's enters, then its leaves
+    uint32_t pre_e, pre_l;  // this wave's (or thread's) first enter / leave index in the tile
+    if (!L.fallback) {
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t se = 0, sl = 0;
+            for (int q = 0; q < CW; ++q) {
+                const uint32_t e = L.wcnt[q][0], l = L.wcnt[q][1];
+                L.wcnt[q][0] = se;
+                L.wcnt[q][1] = sl;
+                se += e;
+                sl += l;
+                if (e + l > (uint32_t)EVW) L.overflow = 1;
+            }
+            L.te = se;
+            L.tl = sl;
+        }
+        __syncthreads();
+        pre_e = L.wcnt[w][0];
+        pre_l = L.wcnt[w][1];
+    } else {
+        uint32_t te, tl;
+        pre_e = block_excl_scan<CT>(ne, L.ws, te);
+        __syncthreads();
+        pre_l = block_excl_scan<CT>(nl, L.ws, tl);
+        if (tid == 0) {
+            L.te = te;
+            L.tl = tl;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const uint32_t tot = 2 * (L.te + L.tl);
+        const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+        L.base = b;
+        tile_total[tile_off + t] = 2 * L.te;
+        tile_base[tile_off + t] = b;
+        tile_total[leave_off + tile_off + t] = 2 * L.tl;
+        tile_base[leave_off + tile_off + t] = b + 2ull * L.te;
+    }
+    __syncthreads();
+    const unsigned long long pe = L.base + 2ull * pre_e, pl = L.base + 2ull * L.te + 2ull * pre_l;
+    if (!L.fallback) {
+        // buffered events of this wave, in order, split by kind
+        const uint32_t nbuf = min(ne + nl, (uint32_t)EVW);
+        uint32_t ie = 0, il = 0;
+        for (uint32_t c = 0; c < nbuf; c += WAVE) {
+            const uint32_t e = c + ln;
+            const uint2 ev = e < nbuf ? L.ev[w][e] : make_uint2(0, 0);
+            const bool valid = e < nbuf;
+            const bool lv = (ev.y & KIND_LEAVE) != 0u;
+            const unsigned long long lm = __ballot(valid && lv), em = __ballot(valid && !lv);
+            if (valid) {
+                const uint32_t b_slot = ev.y & ~KIND_LEAVE;
+                const unsigned long long p = lv ? pl + 2ull * (il + (uint32_t)__popcll(lm & lanemask_lt()))
+                                                : pe + 2ull * (ie + (uint32_t)__popcll(em & lanemask_lt()));
+                if (p + 1 < cap) {
+                    out[p] = make_uint2(ev.x, b_slot);
+                    out[p + 1] = make_uint2(b_slot, ev.x);
+                }
+            }
+            ie += (uint32_t)__popcll(em);
+            il += (uint32_t)__popcll(lm);
+        }
+        if (L.overflow) {  // replay: waves past their buffer write the rest directly
+            uint32_t re = 0, rl = 0;
+            combined_sweep<true>(L, F, O_rec, T.e0, nrows, me, proto, thr, BW, ne + nl > (uint32_t)EVW, re, rl, out,
+                                 cap, pe, pl);
+        }
+    } else if (active && (ne | nl)) {
+        PairCtx A = proto;
+        A.a = a;
+        A.now = ld_rec(F.rec, a);
+        A.oth = ld_rec(O_rec, a);
+        A.chg = A.now.s >= seq_base;
+        uint32_t we = 0, wl = 0;
+        enum_global<2, true>(F, O_rec, nullptr, g, A, thr, cx0, cx1, cz0, cz1, 0, out, pe, pl, cap, we, wl);
+    }
+}
+
+// one wave per tile entry, grid-strided
+__global__ __launch_bounds__(256) void k_reorder(const uint32_t *__restrict__ dest,
+                                                 const uint32_t *__restrict__ tile_total,
+                                                 const unsigned long long *__restrict__ tile_base,
+                                                 uint32_t n_entries, const uint2 *__restrict__ tmp, uint2 *out,
+                                                 uint64_t cap) {
+    const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
+    for (uint32_t e = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; e < n_entries; e += waves) {
+        const uint32_t cnt = tile_total[e];
+        if (!cnt) continue;
+        const unsigned long long src = tile_base[e];
+        const uint64_t dst = dest[e];
+        for (uint32_t k = lane(); k < cnt; k += WAVE)
+            if (src + k < cap && dst + k < cap) out[dst + k] = tmp[src + k];
+    }
 }
 
 __global__ void k_finish(const uint32_t *__restrict__ dest, uint32_t n_enter_entries, uint32_t n_entries,
-                         const uint32_t *__restrict__ err, const unsigned long long *__restrict__ counter,
-                         TickResult *res) {
+                         const TickScalars *__restrict__ sc, TickOut *res) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     res->n_enter = dest[n_enter_entries];
     res->n_total = dest[n_entries];
-    res->err = *err;
-    res->total64 = *counter;
+    res->err = sc->err;
+    res->total64 = sc->counter;
 }
 
 // ----------------------------------------------------------------- bbox ------
@@ -799,49 +1270,126 @@ __device__ __forceinline__ int f2o(float f) {
     return i ^ ((i >> 31) & 0x7FFFFFFF);
 }
 
-__device__ __forceinline__ void bbox_flush(int *bbox, uint32_t ms, uint32_t sp, int mnx, int mnz, int mxx, int mxz) {
-    atomicMin(&bbox[sp], mnx);
-    atomicMin(&bbox[ms + sp], mnz);
-    atomicMax(&bbox[2 * ms + sp], mxx);
-    atomicMax(&bbox[3 * ms + sp], mxz);
+__device__ __forceinline__ void bbox_flush(int4 *bbox, uint32_t ns, uint32_t sp, const int (&v)[4]) {
+    if (sp >= ns) return;
+    int *p = reinterpret_cast<int *>(bbox + sp);
+    atomicMin(p + 0, v[0]);
+    atomicMin(p + 1, v[1]);
+    atomicMax(p + 2, v[2]);
+    atomicMax(p + 3, v[3]);
 }
 
 constexpr uint32_t BB_PER_THREAD = 16;
+constexpr uint32_t BB_T = 256;
 
-// Per-space bounding box of the frame (for the next flush's grid).  Each lane
-// folds 16 consecutive entries; runs of one space are merged per wave.
-__global__ void k_bbox(FrameView F, int *bbox, uint32_t ms) {
-    const uint32_t k0 = (blockIdx.x * blockDim.x + threadIdx.x) * BB_PER_THREAD;
+struct BBoxPart {  // one workgroup's fold: space id (SP_DEAD = nothing left) + ordered-int bbox
+    uint32_t sp;
+    int v[4];
+};
+
+// Fold per-thread (space, bbox) over a workgroup: when every thread ends on
+// the same space the block reduces to one part; otherwise each thread flushes
+// its own run with atomics (only at space boundaries).
+__device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], int4 *bbox, uint32_t ns,
+                                           BBoxPart *out) {
+    __shared__ uint32_t s_sp[BB_T / WAVE];
+    __shared__ int s_v[BB_T / WAVE][4];
+    __shared__ int s_uni;
+    const uint32_t first = __shfl(cur, 0);
+    const bool wuni = __all(cur == first || cur == SP_DEAD);
+    int v[4] = {own[0], own[1], own[2], own[3]};
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        v[0] = min(v[0], __shfl_xor(v[0], o));
+        v[1] = min(v[1], __shfl_xor(v[1], o));
+        v[2] = max(v[2], __shfl_xor(v[2], o));
+        v[3] = max(v[3], __shfl_xor(v[3], o));
+    }
+    const int w = threadIdx.x / WAVE;
+    if (threadIdx.x == 0) s_uni = 1;
+    __syncthreads();
+    if (lane() == 0) {
+        s_sp[w] = wuni ? first : SP_KEEP;
+        s_v[w][0] = v[0];
+        s_v[w][1] = v[1];
+        s_v[w][2] = v[2];
+        s_v[w][3] = v[3];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t bsp = SP_DEAD;
+        int r[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+        for (int q = 0; q < (int)(BB_T / WAVE); ++q) {
+            const uint32_t ws = s_sp[q];
+            if (ws == SP_DEAD) continue;
+            if (ws == SP_KEEP || (bsp != SP_DEAD && ws != bsp)) {
+                s_uni = 0;
+                break;
+            }
+            bsp = ws;
+            r[0] = min(r[0], s_v[q][0]);
+            r[1] = min(r[1], s_v[q][1]);
+            r[2] = max(r[2], s_v[q][2]);
+            r[3] = max(r[3], s_v[q][3]);
+        }
+        out->sp = s_uni ? bsp : SP_DEAD;
+        out->v[0] = r[0];
+        out->v[1] = r[1];
+        out->v[2] = r[2];
+        out->v[3] = r[3];
+    }
+    __syncthreads();
+    if (!s_uni && cur != SP_DEAD) bbox_flush(bbox, ns, cur, own);  // mixed spaces: every run flushes
+}
+
+// Level 1: 16 consecutive entries per thread, runs of one space folded.
+__global__ __launch_bounds__(BB_T) void k_bbox(FrameView F, int4 *bbox, uint32_t ns, BBoxPart *parts) {
+    const uint32_t k0 = (blockIdx.x * BB_T + threadIdx.x) * BB_PER_THREAD;
     const uint32_t k1 = min(k0 + BB_PER_THREAD, F.n);
     uint32_t cur = SP_DEAD;
-    int mnx = INT_MAX, mnz = INT_MAX, mxx = INT_MIN, mxz = INT_MIN;
+    int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
     for (uint32_t k = k0; k < k1; ++k) {
-        const uint32_t sp = F.sp[k];
+        const uint32_t sp = ld_ss(F.ss, k).sp;
         if (sp != cur) {
-            if (cur != SP_DEAD && cur < ms) bbox_flush(bbox, ms, cur, mnx, mnz, mxx, mxz);
+            if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
             cur = sp;
-            mnx = mnz = INT_MAX;
-            mxx = mxz = INT_MIN;
+            v[0] = v[1] = INT_MAX;
+            v[2] = v[3] = INT_MIN;
         }
-        const int ix = f2o(F.x[k]), iz = f2o(F.z[k]);
-        mnx = min(mnx, ix);
-        mnz = min(mnz, iz);
-        mxx = max(mxx, ix);
-        mxz = max(mxz, iz);
+        const Rec16 r = ld_rec(F.rec, k);
+        const int ix = f2o(r.x), iz = f2o(r.z);
+        v[0] = min(v[0], ix);
+        v[1] = min(v[1], iz);
+        v[2] = max(v[2], ix);
+        v[3] = max(v[3], iz);
     }
-    const uint32_t first = __shfl(cur, 0);
-    if (__all(cur == first || cur == SP_DEAD)) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            mnx = min(mnx, __shfl_xor(mnx, o));
-            mnz = min(mnz, __shfl_xor(mnz, o));
-            mxx = max(mxx, __shfl_xor(mxx, o));
-            mxz = max(mxz, __shfl_xor(mxz, o));
+    bbox_block(cur, v, bbox, ns, &parts[blockIdx.x]);
+}
+
+// Level 2: one workgroup folds the level-1 parts (space-sorted).
+__global__ __launch_bounds__(BB_T) void k_bbox_parts(const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
+                                                     uint32_t ns, BBoxPart *out) {
+    const uint32_t per = (np + BB_T - 1) / BB_T;
+    const uint32_t p0 = threadIdx.x * per, p1 = min(p0 + per, np);
+    uint32_t cur = SP_DEAD;
+    int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+    for (uint32_t p = p0; p < p1; ++p) {
+        const BBoxPart q = parts[p];
+        if (q.sp == SP_DEAD) continue;
+        if (q.sp != cur) {
+            if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
+            cur = q.sp;
+            v[0] = v[1] = INT_MAX;
+            v[2] = v[3] = INT_MIN;
         }
-        if (lane() == 0 && first != SP_DEAD && first < ms) bbox_flush(bbox, ms, first, mnx, mnz, mxx, mxz);
-    } else if (cur != SP_DEAD && cur < ms) {
-        bbox_flush(bbox, ms, cur, mnx, mnz, mxx, mxz);
+        v[0] = min(v[0], q.v[0]);
+        v[1] = min(v[1], q.v[1]);
+        v[2] = max(v[2], q.v[2]);
+        v[3] = max(v[3], q.v[3]);
     }
+    bbox_block(cur, v, bbox, ns, out);
+    __syncthreads();
+    if (threadIdx.x == 0 && out->sp != SP_DEAD) bbox_flush(bbox, ns, out->sp, out->v);
 }
 
 // ------------------------------------------------------------ neighbors ------
@@ -849,23 +1397,22 @@ __global__ void k_bbox(FrameView F, int *bbox, uint32_t ms) {
 __global__ __launch_bounds__(256) void k_neighbors(FrameView F, const uint32_t *__restrict__ rank, uint32_t slot,
                                                    uint32_t *out, uint32_t cap, uint32_t *count) {
     const uint32_t a = rank[slot];
-    if (a >= F.n || F.slot[a] != slot) return;
-    const float xa = F.x[a], za = F.z[a];
-    const uint64_t sa = F.seq[a];
-    const SpaceGrid g = F.grid[F.sp[a]];
+    if (a >= F.n || ld_ss(F.ss, a).slot != slot) return;
+    const Rec16 A = ld_rec(F.rec, a);
+    const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
     const float D = g.D;
-    const float lox = xa - D, hix = xa + D, loz = za - D, hiz = za + D;
-    const float mx = (fabsf(xa) + 2.0f * D) * 0x1p-21f, mz = (fabsf(za) + 2.0f * D) * 0x1p-21f;
-    const int cx0 = cell_of(lox - mx, g.ox, g.inv, g.gx), cx1 = cell_of(hix + mx, g.ox, g.inv, g.gx);
-    const int cz0 = cell_of(loz - mz, g.oz, g.inv, g.gz), cz1 = cell_of(hiz + mz, g.oz, g.inv, g.gz);
+    const float mx = (fabsf(A.x) + 3.0f * D) * 0x1p-20f, mz = (fabsf(A.z) + 3.0f * D) * 0x1p-20f;
+    const int cx0 = cell_of(A.x - D - mx, g.ox, g.inv, g.gx), cx1 = cell_of(A.x + D + mx, g.ox, g.inv, g.gx);
+    const int cz0 = cell_of(A.z - D - mz, g.oz, g.inv, g.gz), cz1 = cell_of(A.z + D + mz, g.oz, g.inv, g.gz);
     for (int cz = cz0; cz <= cz1; ++cz) {
         const uint32_t row = g.base + (uint32_t)cz * g.gx;
         const uint32_t jb = F.cell_start[row + (uint32_t)cx0], je = F.cell_start[row + (uint32_t)cx1 + 1u];
         for (uint32_t b = jb + threadIdx.x; b < je; b += blockDim.x) {
             if (b == a) continue;
-            if (related(xa, za, sa, lox, hix, loz, hiz, F.x[b], F.z[b], F.seq[b], D)) {
-                uint32_t p = atomicAdd(count, 1u);
-                if (p < cap) out[p] = F.slot[b];
+            const Rec16 B = ld_rec(F.rec, b);
+            if (rel(A.x, A.z, A.s, B.x, B.z, B.s, D)) {
+                const uint32_t p = atomicAdd(count, 1u);
+                if (p < cap) out[p] = ld_ss(F.ss, b).slot;
             }
         }
     }
@@ -875,56 +1422,65 @@ __global__ __launch_bounds__(256) void k_neighbors(FrameView F, const uint32_t *
 
 // ============================================================ launchers ======
 
-void launch_copy_state(uint32_t n, const float *p_x, const float *p_z, const uint64_t *p_seq, const uint32_t *p_sp,
-                       const uint32_t *p_slot, float *s_x, float *s_z, uint64_t *s_seq, uint32_t *s_sp,
-                       uint32_t *s_slot, hipStream_t st) {
-    if (!n) return;
-    k_copy_state<<<cdiv(n, 256), 256, 0, st>>>(n, p_x, p_z, p_seq, p_sp, p_slot, s_x, s_z, s_seq, s_sp, s_slot);
+void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
+                     uint32_t n_spaces, hipStream_t st) {
+    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, 1});
+    k_prologue<<<cdiv(m, 256), 256, 0, st>>>(sc, z0, (uint32_t)n0, z1, (uint32_t)n1, bbox, n_spaces);
 }
 
-void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, uint32_t *s_slot,
-                          uint32_t *s_sp, uint64_t *s_seq, uint32_t *rank, hipStream_t st) {
+void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
+    if (n) k_zero<<<cdiv(n, 256), 256, 0, st>>>(p, n);
+}
+
+void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec, SlotSp *s_ss,
+                       hipStream_t st) {
+    if (!n) return;
+    k_copy_state<<<cdiv(n, 256), 256, 0, st>>>(n, p_rec, p_ss, s_rec, s_ss);
+}
+
+void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
+                          uint32_t *rank, hipStream_t st) {
     if (!n_app) return;
-    k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_slot, s_sp, s_seq, rank);
+    k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_rec, s_ss, rank);
 }
 
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, unsigned long long *lastop,
-                      uint32_t tick_id, uint32_t *err, hipStream_t st) {
+                      uint32_t tick_id, TickScalars *sc, hipStream_t st) {
     if (!n) return;
-    k_ops_claim<<<cdiv(n, 256), 256, 0, st>>>(slots, n, j0, max_slots, lastop, tick_id, err);
+    k_ops_claim<<<cdiv(n, 256), 256, 0, st>>>(slots, n, j0, max_slots, lastop, tick_id, sc);
 }
 
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
                       uint32_t j0, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
-                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, float *s_x, float *s_z,
-                      uint64_t *s_seq, uint32_t *s_sp, const uint32_t *s_slot, uint32_t *err, hipStream_t st) {
+                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss,
+                      TickScalars *sc, hipStream_t st) {
     if (!n) return;
     k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, n, j0, max_slots, lastop, tick_id, rank, n_total,
-                                              seq_base, s_x, s_z, s_seq, s_sp, s_slot, err);
+                                              seq_base, s_rec, s_ss, sc);
 }
 
-void launch_keygen(const float *s_x, const float *s_z, const uint32_t *s_sp, uint32_t n_total,
-                   const SpaceGrid *grid, uint32_t sentinel, uint32_t *keys, uint32_t *vals, const float *p_x,
-                   const float *p_z, const uint32_t *p_sp, const SpaceGrid *p_grid, uint32_t n_prev, int *d_rel,
-                   hipStream_t st) {
-    if (!n_total) return;
-    k_keygen<<<cdiv(n_total, 256), 256, 0, st>>>(s_x, s_z, s_sp, n_total, grid, sentinel, keys, vals, p_x, p_z,
-                                                 p_sp, p_grid, n_prev, d_rel);
+void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
+                   uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
+                   const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, hipStream_t st) {
+    if (!n_total) return;  // the prologue left d_rel = bmax = 0
+    const uint32_t nb = cdiv(n_total, 256);
+    k_keygen<<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid, n_prev, blk);
+    k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
 }
 
 size_t scan_tmp_elems(size_t n) {
-    size_t nb = cdiv(n, SC_TILE);
-    if (nb <= 1) return 0;
+    if (n <= SC1_MAX) return 0;
+    const size_t nb = cdiv(n, SC_TILE);
     return ((nb + 3) & ~(size_t)3) + scan_tmp_elems(nb);
 }
 
 void scan_exclusive(const uint32_t *in, uint32_t *out, size_t n, uint32_t *tmp, hipStream_t st) {
     if (!n) return;
-    const size_t nb = cdiv(n, SC_TILE);
-    if (nb == 1) {
-        k_scan_down<<<1, SC_T, 0, st>>>(in, out, n, nullptr);
+    if (n <= SC1_MAX) {
+        k_scan_single<<<1, SC1_T, 0, st>>>(in, out, n);
         return;
     }
+    const size_t nb = cdiv(n, SC_TILE);
     uint32_t *sums = tmp;
     uint32_t *rest = tmp + ((nb + 3) & ~(size_t)3);
     k_scan_reduce<<<(uint32_t)nb, SC_T, 0, st>>>(in, n, sums);
@@ -954,16 +1510,13 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
     return cur;
 }
 
-void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const float *s_x, const float *s_z,
-                   const uint64_t *s_seq, const uint32_t *s_sp, const uint32_t *s_slot, const float *p_x,
-                   const float *p_z, const uint64_t *p_seq, const uint32_t *p_sp, float *f_x, float *f_z,
-                   uint64_t *f_seq, uint32_t *f_sp, uint32_t *f_slot, float *o_x, float *o_z, uint64_t *o_seq,
-                   uint32_t *o_sp, uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel,
-                   uint32_t n_total, uint32_t *err, hipStream_t st) {
+void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec,
+                   uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel, uint32_t n_total,
+                   TickScalars *sc, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
-    k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_x, s_z, s_seq, s_sp, s_slot, p_x, p_z, p_seq,
-                                            p_sp, f_x, f_z, f_seq, f_sp, f_slot, o_x, o_z, o_seq, o_sp, rank,
-                                            sorted_keys, sentinel, n_total, err);
+    k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, rank,
+                                            sorted_keys, sentinel, n_total, sc);
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {
@@ -974,43 +1527,47 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
 void build_tiles(FrameView F, uint32_t n_space_ids, uint32_t n_rows, uint32_t *row_space, uint32_t *row_ntiles,
                  Tile *tiles, uint32_t *scan_tmp, hipStream_t st) {
     if (n_space_ids) k_row_space<<<cdiv(n_space_ids, 256), 256, 0, st>>>(F.grid, n_space_ids, row_space);
-    (void)hipMemsetAsync(row_ntiles + n_rows, 0, sizeof(uint32_t), st);
-    if (n_rows) k_row_tiles<<<cdiv(n_rows, 256), 256, 0, st>>>(F, row_space, n_rows, row_ntiles);
+    k_row_tiles<<<cdiv((size_t)n_rows + 1, 256), 256, 0, st>>>(F, row_space, n_rows, row_ntiles);
     scan_exclusive(row_ntiles, row_ntiles, (size_t)n_rows + 1, scan_tmp, st);
     if (n_rows) k_fill_tiles<<<cdiv(n_rows, 256), 256, 0, st>>>(F, row_space, n_rows, row_ntiles, tiles);
 }
 
-void launch_pairs(int mode, FrameView F, StateView O, TileSet T, uint64_t seq_base, const float *d_rel,
-                  unsigned long long *counter, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
+void launch_pairs(int mode, FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, TileSet T, uint64_t seq_base,
+                  TickScalars *sc, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
                   unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st) {
     if (!F.n || !T.bound) return;
     uint2 *tmp = reinterpret_cast<uint2 *>(tmp_pairs);
     if (mode == 2)
-        k_pairs<2><<<T.bound, PT, 0, st>>>(F, O, T, seq_base, d_rel, counter, tmp, cap, tile_total, tile_base,
+        k_combined<<<T.bound, CT, 0, st>>>(F, O_rec, T, seq_base, sc, &sc->counter, tmp, cap, tile_total, tile_base,
                                            tile_off, leave_off);
     else
-        k_pairs<1><<<T.bound, PT, 0, st>>>(F, O, T, seq_base, d_rel, counter, tmp, cap, tile_total, tile_base,
-                                           tile_off, leave_off);
+        k_pairs<1><<<T.bound, PT, 0, st>>>(F, O_rec, O_ss, T, seq_base, sc, &sc->counter, tmp, cap, tile_total,
+                                           tile_base, tile_off, leave_off);
 }
 
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
                     uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
                     hipStream_t st) {
     if (!n_entries) return;
-    k_reorder<<<n_entries, 128, 0, st>>>(dest, tile_total, tile_base, n_entries,
-                                         reinterpret_cast<const uint2 *>(tmp_pairs),
-                                         reinterpret_cast<uint2 *>(out_pairs), cap);
+    const uint32_t blocks = std::min<uint32_t>(cdiv(n_entries, 256 / WAVE), 2048);
+    k_reorder<<<blocks, 256, 0, st>>>(dest, tile_total, tile_base, n_entries,
+                                      reinterpret_cast<const uint2 *>(tmp_pairs),
+                                      reinterpret_cast<uint2 *>(out_pairs), cap);
 }
 
-void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const uint32_t *err,
-                   const unsigned long long *counter, TickResult *res, hipStream_t st) {
-    k_finish<<<1, 64, 0, st>>>(dest, n_enter_entries, n_entries, err, counter, res);
+void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const TickScalars *sc,
+                   TickOut *out, hipStream_t st) {
+    k_finish<<<1, 64, 0, st>>>(dest, n_enter_entries, n_entries, sc, out);
 }
 
-void launch_bbox(FrameView F, int *bbox, uint32_t max_spaces, hipStream_t st) {
+size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(cdiv(n, BB_PER_THREAD), BB_T) + 1); }
+
+void launch_bbox(FrameView F, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st) {
     if (!F.n) return;
-    const uint32_t threads = cdiv(F.n, BB_PER_THREAD);
-    k_bbox<<<cdiv(threads, 256), 256, 0, st>>>(F, bbox, max_spaces);
+    BBoxPart *parts = reinterpret_cast<BBoxPart *>(parts_mem);
+    const uint32_t nb = cdiv(cdiv(F.n, BB_PER_THREAD), BB_T);
+    k_bbox<<<nb, BB_T, 0, st>>>(F, bbox, n_spaces, parts);
+    k_bbox_parts<<<1, BB_T, 0, st>>>(parts, nb, bbox, n_spaces, parts + nb);
 }
 
 void launch_neighbors(FrameView F, const uint32_t *rank, uint32_t slot, uint32_t *out, uint32_t cap,

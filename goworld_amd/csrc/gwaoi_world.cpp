@@ -33,12 +33,12 @@ const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",    "gather", "ce
                                  "combined", "special", "reorder", "bbox",   "d2h"};
 
 struct DevFrame {
-    float *x = nullptr, *z = nullptr;
-    uint64_t *seq = nullptr;
-    uint32_t *sp = nullptr, *slot = nullptr;
+    gw::Rec16 *rec = nullptr;
+    gw::SlotSp *ss = nullptr;
     uint32_t *cell_start = nullptr;
     size_t cell_cap = 0;  // entries allocated in cell_start
     SpaceGrid *grid = nullptr;
+    std::vector<SpaceGrid> hgrid;  // host mirror of `grid` (upload only on change)
     uint32_t n = 0;
     uint32_t total_cells = 0;
     // pair-pass tiles of this frame
@@ -83,12 +83,9 @@ struct gwaoi_world {
     int cur = 0;  // fr[cur] = frame of the last flush
 
     // working set (max_slots entries each)
-    float *sx = nullptr, *sz = nullptr;
-    uint64_t *sseq = nullptr;
-    uint32_t *ssp = nullptr, *sslot = nullptr;
-    float *ox = nullptr, *oz = nullptr;
-    uint64_t *oseq = nullptr;
-    uint32_t *osp = nullptr;
+    gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
+    gw::SlotSp *sss = nullptr;
+    gw::Rec16 *orec = nullptr;  // previous state in the new frame's order (NaN if absent)
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;
@@ -105,17 +102,15 @@ struct gwaoi_world {
     uint32_t *tile_total = nullptr, *tile_dest = nullptr;
     unsigned long long *tile_base = nullptr;
     size_t tile_entries_cap = 0;
-    uint32_t *err = nullptr;
-    int *d_rel = nullptr;  // float bits: max displacement / D of near entities this flush
-    unsigned long long *counter = nullptr;
-    gw::TickResult *res = nullptr;
-    int *bbox = nullptr;
+    gw::TickScalars *sc = nullptr;
+    float *blk = nullptr;        // keygen per-block partials
+    void *bbox_parts = nullptr;  // bbox level-1 partials
+    char *dev_out = nullptr;     // TickOut + int4 bbox[max_spaces]
     uint32_t *nb_out = nullptr, *nb_count = nullptr;
     size_t nb_cap = 0;
 
     // pinned host mirrors
-    gw::TickResult *h_res = nullptr;
-    int *h_bbox = nullptr;
+    char *h_out = nullptr;  // TickOut + int4 bbox[max_spaces]
     uint32_t *h_events = nullptr;
     uint64_t h_ev_cap = 0;
     SpaceGrid *h_grid = nullptr;
@@ -436,11 +431,8 @@ void choose_grids(gwaoi_world *w, uint32_t &total_cells, uint32_t &total_rows) {
 
 gw::FrameView view_of(const DevFrame &f) {
     gw::FrameView v;
-    v.x = f.x;
-    v.z = f.z;
-    v.seq = f.seq;
-    v.sp = f.sp;
-    v.slot = f.slot;
+    v.rec = f.rec;
+    v.ss = f.ss;
     v.cell_start = f.cell_start;
     v.grid = f.grid;
     v.n = f.n;
@@ -457,35 +449,32 @@ int bitlen(uint32_t v) {
     return b;
 }
 
-// Pair passes + deterministic reorder (re-run after the event buffer grew).
-// Tile-total entries: [enter totals: new-frame tiles | previous-frame tiles]
-// then [leave totals: same order]; their exclusive scan is the final layout
-// [enters | leaves] in tile order.
+gw::TickOut *tick_out(gwaoi_world *w) { return reinterpret_cast<gw::TickOut *>(w->h_out); }
+const int4 *tick_bbox(gwaoi_world *w) { return reinterpret_cast<const int4 *>(w->h_out + sizeof(gw::TickOut)); }
+int4 *dev_bbox(gwaoi_world *w) { return reinterpret_cast<int4 *>(w->dev_out + sizeof(gw::TickOut)); }
+
+// Pair passes + deterministic reorder.  Tile-total entries: [enter totals:
+// new-frame tiles | previous-frame tiles] then [leave totals: same order];
+// their exclusive scan is the final layout [enters | leaves] in tile order.
 void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_base) {
     hipStream_t st = w->stream;
     const uint32_t TBn = Fn.n ? Fn.tile_bound : 0, TBp = P.n ? P.tile_bound : 0;
     const uint32_t half = TBn + TBp, entries = 2 * half;
-    (void)hipMemsetAsync(w->counter, 0, sizeof(unsigned long long), st);
-    (void)hipMemsetAsync(w->tile_total, 0, ((size_t)entries + 1) * sizeof(uint32_t), st);
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
-    gw::StateView old_in_new{w->ox, w->oz, w->oseq, w->osp};
-    gw::StateView new_in_prev{w->sx, w->sz, w->sseq, w->ssp};
     gw::TileSet Tn{Fn.tiles, Fn.row_ntiles + Fn.n_rows, Fn.row_space, TBn};
     gw::TileSet Tp{P.tiles, P.row_ntiles + P.n_rows, P.row_space, TBp};
-    const float *drel = reinterpret_cast<const float *>(w->d_rel);
     stage_begin(w, ST_COMBINED);
-    gw::launch_pairs(2, Vn, old_in_new, Tn, seq_base, drel, w->counter, w->events_tmp, w->ev_cap,
-                     w->tile_total, w->tile_base, 0, half, st);
+    gw::launch_pairs(2, Vn, w->orec, nullptr, Tn, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total,
+                     w->tile_base, 0, half, st);
     stage_end(w, ST_COMBINED);
     stage_begin(w, ST_SPECIAL);
-    gw::launch_pairs(1, Vp, new_in_prev, Tp, seq_base, drel, w->counter, w->events_tmp, w->ev_cap,
-                     w->tile_total, w->tile_base, TBn, half, st);
+    gw::launch_pairs(1, Vp, w->srec, w->sss, Tp, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total,
+                     w->tile_base, TBn, half, st);
     stage_end(w, ST_SPECIAL);
     stage_begin(w, ST_REORDER);
     gw::scan_exclusive(w->tile_total, w->tile_dest, (size_t)entries + 1, w->scan_tmp, st);
-    gw::launch_reorder(w->tile_dest, w->tile_total, w->tile_base, entries, w->events_tmp, w->events, w->ev_cap,
-                       st);
-    gw::launch_finish(w->tile_dest, half, entries, w->err, w->counter, w->res, st);
+    gw::launch_reorder(w->tile_dest, w->tile_total, w->tile_base, entries, w->events_tmp, w->events, w->ev_cap, st);
+    gw::launch_finish(w->tile_dest, half, entries, w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), st);
     stage_end(w, ST_REORDER);
 }
 
@@ -509,33 +498,39 @@ int run_tick(gwaoi_world *w) {
     uint32_t total_cells = 0, total_rows = 0;
     choose_grids(w, total_cells, total_rows);
     const uint32_t tbound = gw::tile_bound(n_new, total_rows);
+    const uint32_t TBp = P.n ? P.tile_bound : 0;
+    const size_t entries = 2 * ((size_t)tbound + TBp);
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tiles(w, Fn, total_rows, tbound))) return rc;
-    if ((rc = ensure_tile_entries(w, 2 * ((size_t)tbound + (P.n ? P.tile_bound : 0))))) return rc;
+    if ((rc = ensure_tile_entries(w, entries))) return rc;
     size_t host_ops = 0;
     for (const Run &r : w->runs)
         if (!r.device) host_ops += r.hend - r.hbegin;
     if ((rc = ensure_ops(w, host_ops))) return rc;
     const size_t scan_need = std::max<size_t>({gw::radix_hist_elems(std::max(n_total, 1u)), (size_t)total_cells + 1,
-                                               (size_t)total_rows + 1, w->tile_entries_cap});
+                                               (size_t)total_rows + 1, entries + 1});
     if ((rc = ensure_scan_tmp(w, scan_need))) return rc;
     Fn.total_cells = total_cells;
     Fn.n = n_new;
     Fn.n_rows = total_rows;
     Fn.tile_bound = tbound;
 
-    HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * std::max(1u, w->n_space_ids),
-                           hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(w->err, 0, sizeof(uint32_t), st));
-    HIP_TRY(hipMemsetAsync(w->d_rel, 0, sizeof(int), st));
+    const uint32_t ns = std::max(1u, w->n_space_ids);
+    const bool grid_same = Fn.hgrid.size() == ns && !std::memcmp(Fn.hgrid.data(), w->h_grid, ns * sizeof(SpaceGrid));
+    if (!grid_same) {
+        HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * ns, hipMemcpyHostToDevice, st));
+        Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
+    }
+    gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
+                        w->n_space_ids, st);
 
     // ---- apply queued ops onto S' = copy of the previous frame
     stage_begin(w, ST_APPLY);
-    gw::launch_copy_state(n_prev, P.x, P.z, P.seq, P.sp, P.slot, w->sx, w->sz, w->sseq, w->ssp, w->sslot, st);
+    gw::launch_copy_state(n_prev, P.rec, P.ss, w->srec, w->sss, st);
     if (n_app) {
         HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
-        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->sslot, w->ssp, w->sseq, w->rank, st);
+        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->rank, st);
     }
     if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
@@ -565,20 +560,20 @@ int run_tick(gwaoi_world *w) {
                     hoff += k;
                 }
                 if (pass == 0)
-                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->lastop, tick_id, w->err, st);
+                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->lastop, tick_id, w->sc, st);
                 else
                     gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->lastop, tick_id, w->rank, n_total,
-                                         seq_base, w->sx, w->sz, w->sseq, w->ssp, w->sslot, w->err, st);
+                                         seq_base, w->srec, w->sss, w->sc, st);
                 j0 += k;
             }
         }
     }
     stage_end(w, ST_APPLY);
 
-    // ---- keys + stable sort
+    // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, ST_KEYGEN);
-    gw::launch_keygen(w->sx, w->sz, w->ssp, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.x, P.z, P.sp,
-                      P.grid, n_prev, w->d_rel, st);
+    gw::launch_keygen(w->srec, w->sss, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
+                      n_prev, w->blk, w->sc, st);
     stage_end(w, ST_KEYGEN);
     stage_begin(w, ST_SORT);
     gw::SortBuffers sb;
@@ -593,21 +588,20 @@ int run_tick(gwaoi_world *w) {
     const uint32_t *skeys = w->keys[which];
     const uint32_t *perm = w->vals[which];
 
-    // ---- new frame + old state in the new order
+    // ---- new frame + previous state in the new order
     stage_begin(w, ST_GATHER);
-    gw::launch_gather(perm, n_new, n_prev, w->sx, w->sz, w->sseq, w->ssp, w->sslot, P.x, P.z, P.seq, P.sp, Fn.x,
-                      Fn.z, Fn.seq, Fn.sp, Fn.slot, w->ox, w->oz, w->oseq, w->osp, w->rank, skeys, total_cells,
-                      n_total, w->err, st);
+    gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->rank, skeys,
+                      total_cells, n_total, w->sc, st);
     stage_end(w, ST_GATHER);
 
-    // ---- cell_start = exclusive scan of entities per cell
+    // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue)
     stage_begin(w, ST_CELLS);
-    HIP_TRY(hipMemsetAsync(Fn.cell_start, 0, ((size_t)total_cells + 1) * sizeof(uint32_t), st));
     gw::launch_cell_count(skeys, n_new, Fn.cell_start, st);
     gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
     stage_end(w, ST_CELLS);
     stage_begin(w, ST_TILES);
-    gw::build_tiles(view_of(Fn), w->n_space_ids, total_rows, Fn.row_space, Fn.row_ntiles, Fn.tiles, w->scan_tmp, st);
+    gw::build_tiles(view_of(Fn), grid_same ? 0u : w->n_space_ids, total_rows, Fn.row_space, Fn.row_ntiles, Fn.tiles,
+                    w->scan_tmp, st);
     stage_end(w, ST_TILES);
 
     // ---- pair passes: combined over the new grid, special entities over the previous one
@@ -615,21 +609,14 @@ int run_tick(gwaoi_world *w) {
 
     // ---- per-space bounding boxes for the next flush's grid
     stage_begin(w, ST_BBOX);
-    if (w->n_space_ids) {
-        const uint32_t ms = w->max_spaces;
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)w->bbox, 0x7FFFFFFF, (size_t)2 * ms, st));
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->bbox + 2 * (size_t)ms), (int)0x80000000, (size_t)2 * ms, st));
-        gw::launch_bbox(view_of(Fn), w->bbox, ms, st);
-        for (int q = 0; q < 4; ++q)
-            HIP_TRY(hipMemcpyAsync(w->h_bbox + (size_t)q * ms, w->bbox + (size_t)q * ms,
-                                   w->n_space_ids * sizeof(int), hipMemcpyDeviceToHost, st));
-    }
+    gw::launch_bbox(view_of(Fn), dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
     stage_end(w, ST_BBOX);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(w->h_res, w->res, sizeof(gw::TickResult), hipMemcpyDeviceToHost, st));
+    const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
+    HIP_TRY(hipMemcpyAsync(w->h_out, w->dev_out, out_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
 
-    gw::TickResult r = *w->h_res;
+    gw::TickOut r = *tick_out(w);
     if (r.total64 > 0xFFFFFFFFull) {
         w->last_error = "more than 2^32-1 events in one flush";
         return GWAOI_ECAPACITY;
@@ -637,28 +624,29 @@ int run_tick(gwaoi_world *w) {
     if (r.total64 > w->ev_cap) {  // grow and re-run the pair passes
         stage_collect(w);
         if ((rc = ensure_events(w, r.total64))) return rc;
+        gw::launch_zero(w->tile_total, entries + 1, st);
+        gw::launch_zero(reinterpret_cast<uint32_t *>(&w->sc->counter), 2, st);
         launch_pair_passes(w, Fn, P, seq_base);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(w->h_res, w->res, sizeof(gw::TickResult), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(w->h_out, w->dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        r = *w->h_res;
+        r = *tick_out(w);
     }
     stage_collect(w);
 
     // ---- commit host bookkeeping
     w->last_n_enter = r.n_enter;
     w->last_n_leave = (uint64_t)r.n_total - r.n_enter;
+    const int4 *bb = tick_bbox(w);
     for (uint32_t s = 0; s < w->n_space_ids; ++s) {
         SpaceHost &S = w->spaces[s];
         S.pend = false;
-        const int ix0 = w->h_bbox[s], iz0 = w->h_bbox[w->max_spaces + s];
-        const int ix1 = w->h_bbox[2 * w->max_spaces + s], iz1 = w->h_bbox[3 * w->max_spaces + s];
-        if (S.used && S.alive && ix0 != 0x7FFFFFFF) {
+        if (S.used && S.alive && bb[s].x != 0x7FFFFFFF) {
             S.have_bbox = true;
-            S.bx0 = o2f(ix0);
-            S.bz0 = o2f(iz0);
-            S.bx1 = o2f(ix1);
-            S.bz1 = o2f(iz1);
+            S.bx0 = o2f(bb[s].x);
+            S.bz0 = o2f(bb[s].y);
+            S.bx1 = o2f(bb[s].z);
+            S.bz1 = o2f(bb[s].w);
         } else {
             S.have_bbox = false;
         }
@@ -719,19 +707,17 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     for (DevFrame &f : w->fr) {
-        dfree(f.x); dfree(f.z); dfree(f.seq); dfree(f.sp); dfree(f.slot); dfree(f.cell_start); dfree(f.grid);
+        dfree(f.rec); dfree(f.ss); dfree(f.cell_start); dfree(f.grid);
         dfree(f.row_space); dfree(f.row_ntiles); dfree(f.tiles);
     }
-    dfree(w->sx); dfree(w->sz); dfree(w->sseq); dfree(w->ssp); dfree(w->sslot);
-    dfree(w->ox); dfree(w->oz); dfree(w->oseq); dfree(w->osp);
+    dfree(w->srec); dfree(w->sss); dfree(w->orec);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->rank); dfree(w->lastop); dfree(w->new_slots_d);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
     dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
-    dfree(w->err); dfree(w->d_rel); dfree(w->counter); dfree(w->res); dfree(w->bbox);
+    dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
     dfree(w->nb_out); dfree(w->nb_count);
-    if (w->h_res) (void)hipHostFree(w->h_res);
-    if (w->h_bbox) (void)hipHostFree(w->h_bbox);
+    if (w->h_out) (void)hipHostFree(w->h_out);
     if (w->h_events) (void)hipHostFree(w->h_events);
     if (w->h_grid) (void)hipHostFree(w->h_grid);
     for (int s = 0; s < ST_N; ++s)
@@ -775,20 +761,18 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     }
     const size_t N = w->max_slots;
     for (DevFrame &f : w->fr) {
-        if ((rc = dalloc(w, &f.x, N)) || (rc = dalloc(w, &f.z, N)) || (rc = dalloc(w, &f.seq, N)) ||
-            (rc = dalloc(w, &f.sp, N)) || (rc = dalloc(w, &f.slot, N)) || (rc = dalloc(w, &f.grid, w->max_spaces)))
+        if ((rc = dalloc(w, &f.rec, N)) || (rc = dalloc(w, &f.ss, N)) || (rc = dalloc(w, &f.grid, w->max_spaces)))
             return fail(rc);
         if ((rc = ensure_cells(w, f, 1))) return fail(rc);
     }
-    if ((rc = dalloc(w, &w->sx, N)) || (rc = dalloc(w, &w->sz, N)) || (rc = dalloc(w, &w->sseq, N)) ||
-        (rc = dalloc(w, &w->ssp, N)) || (rc = dalloc(w, &w->sslot, N)) || (rc = dalloc(w, &w->ox, N)) ||
-        (rc = dalloc(w, &w->oz, N)) || (rc = dalloc(w, &w->oseq, N)) || (rc = dalloc(w, &w->osp, N)) ||
+    const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * (size_t)w->max_spaces;
+    if ((rc = dalloc(w, &w->srec, N)) || (rc = dalloc(w, &w->sss, N)) || (rc = dalloc(w, &w->orec, N)) ||
         (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->rank, N)) || (rc = dalloc(w, &w->lastop, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||
-        (rc = dalloc(w, &w->err, 1)) || (rc = dalloc(w, &w->d_rel, 1)) || (rc = dalloc(w, &w->counter, 1)) ||
-        (rc = dalloc(w, &w->res, 1)) || (rc = dalloc(w, &w->bbox, 4 * (size_t)w->max_spaces)) ||
-        (rc = dalloc(w, &w->nb_count, 1)))
+        (rc = dalloc(w, &w->sc, 1)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
+        (rc = dalloc(w, (char **)&w->bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
+        (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->lastop, 0, N * sizeof(unsigned long long)) != hipSuccess) return fail(GWAOI_EDEVICE);
     if (hipMemset(w->rank, 0xFF, N * sizeof(uint32_t)) != hipSuccess) return fail(GWAOI_EDEVICE);
@@ -797,8 +781,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     if ((rc = ensure_events(w, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
         return fail(rc);
-    if (hipHostMalloc((void **)&w->h_res, sizeof(gw::TickResult), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&w->h_bbox, 4 * sizeof(int) * w->max_spaces, hipHostMallocDefault) != hipSuccess ||
+    if (hipHostMalloc((void **)&w->h_out, out_bytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
         return fail(GWAOI_ENOMEM);
     if (w->timing) {
