@@ -119,10 +119,12 @@ size_t radix_hist_elems(uint32_t n);
 void scan_exclusive(const uint32_t *in, uint32_t *out, size_t n, uint32_t *tmp, hipStream_t st);
 size_t scan_tmp_elems(size_t n);
 
+// New frame (f_rec/f_ss), previous state in the new order (o_rec), and the
+// combined pass's candidate records cand = {x, z, flags, 0}.
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
-                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec,
-                   uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel, uint32_t n_total,
-                   TickScalars *sc, hipStream_t st);
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                   const SpaceGrid *grid, uint64_t seq_base, uint32_t *rank, const uint32_t *sorted_keys,
+                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
 // Tiles of a frame: rows split into runs of <= TILE_A entities.
@@ -131,13 +133,17 @@ void build_tiles(FrameView F, uint32_t n_space_ids, uint32_t n_rows, uint32_t *r
                  Tile *tiles, uint32_t *scan_tmp, hipStream_t st);
 inline uint32_t tile_bound(uint32_t n, uint32_t n_rows) { return (n + TILE_A - 1) / TILE_A + n_rows; }
 
-// mode 2 = combined pass over the new frame (O = previous state in the new
-// order, NaN coordinates where not live in the same space); mode 1 =
-// special-entity pass over the previous frame (O = S', the new state in the
-// previous order, with O_ss giving its space).  Directed event pairs go to
-// tmp at an atomically reserved offset per tile; per tile t the enter
-// total/base are at [tile_off + t], the leave total/base at
-// [leave_off + tile_off + t].
+// Combined pass over the new frame: blocks of TILE_A consecutive entries
+// (O = previous state in the new order, NaN where not live in the same space).
+// Directed event pairs go to tmp at an atomically reserved offset per block;
+// block t's enter total/base are at [t], its leave total/base at [leave_off + t].
+inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; }
+void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
+                     uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
+                     uint32_t leave_off, hipStream_t st);
+// Special-entity pass (mode 1) over the previous frame's tiles (O = S', the
+// new state in the previous order, with O_ss giving its space); tile t's
+// totals/bases at [tile_off + t] and [leave_off + tile_off + t].
 void launch_pairs(int mode, FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, TileSet T, uint64_t seq_base,
                   TickScalars *sc, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
                   unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st);

@@ -188,6 +188,16 @@ __device__ __forceinline__ bool is_near(float xn, float zn, float xo, float zo, 
     return (int)(fabsf(xn - xo) <= thr) & (int)(fabsf(zn - zo) <= thr);
 }
 
+constexpr uint32_t FL_JUMP = 1u, FL_CHG = 2u;  // candidate flags (k_gather -> k_combined)
+
+// FL_JUMP: not "near" (new in this space, changed space, or moved > FAR_FRAC*D
+// on an axis; an absent previous state has NaN coordinates and fails
+// is_near).  FL_CHG: Enter/Moved called this flush.
+__device__ __forceinline__ uint32_t flags_of(const Rec16 &now, const Rec16 &old, unsigned long long seq_base,
+                                             float thr) {
+    return (is_near(now.x, now.z, old.x, old.z, thr) ? 0u : FL_JUMP) | (now.s >= seq_base ? FL_CHG : 0u);
+}
+
 __global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                                 uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
                                                 uint32_t *keys, uint32_t *vals, const Rec16 *__restrict__ p_rec,
@@ -495,7 +505,8 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
-                         SlotSp *f_ss, Rec16 *o_rec, uint32_t *rank, const uint32_t *__restrict__ sorted_keys,
+                         SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
+                         unsigned long long seq_base, uint32_t *rank, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
@@ -503,7 +514,8 @@ __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint
     if (sorted_keys[k] == sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     const uint32_t i = perm[k];
     const SlotSp ss = ld_ss(s_ss, i);
-    reinterpret_cast<uint4 *>(f_rec)[k] = reinterpret_cast<const uint4 *>(s_rec)[i];
+    const Rec16 now = ld_rec(s_rec, i);
+    st_rec(f_rec, k, now);
     reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(ss.slot, ss.sp);
     rank[ss.slot] = k;
     // previous state of the same entity, NaN position unless live in the same space then
@@ -512,6 +524,8 @@ __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint
     o.s = 0;
     if (i < n_prev && ld_ss(p_ss, i).sp == ss.sp) o = ld_rec(p_rec, i);
     st_rec(o_rec, k, o);
+    const float thr = FAR_FRAC * grid[ss.sp].D;
+    cand[k] = make_uint4(__float_as_uint(now.x), __float_as_uint(now.z), flags_of(now, o, seq_base, thr), 0u);
 }
 
 // Entities per cell from the sorted keys: one atomic per run of equal keys
@@ -876,57 +890,54 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 }
 
 // ------------------------------------------------------- combined pass ------
-// Wave-per-entity form of MODE 2.  A tile's candidate rows are staged in LDS
-// in chunks; each wave takes the tile's entities A in turn (A's state is
-// wave-uniform) and its 64 lanes sweep A's candidates.  A cheap exact filter
-// keeps only the pairs that can have an event:
-//   * neither member touched this flush            -> no event
-//   * both members "near" (moved <= d_rel*D, live in the same space at t-1):
-//     N_t != N_t-1 needs one axis with ||d| - D| <= BW and the other with
-//     |d| <= D + BW at t (BW = 2 d_rel D + M: the displacement of both
-//     members plus the float32 rounding of the window bounds); everything
-//     else keeps its relation
-//   * a "jumper" member (new, changed space, moved > D/4) -> always tested
-// Survivors go to a per-wave LDS queue and get the full go-aoi test
-// (pair_kind<2>) with lanes over queue entries.  Events are buffered per
-// wave in processing order (deterministic); a wave whose buffer overflows
-// replays its sweep and writes the rest straight to the output.
+// Every unordered pair that can have an event this flush is visited once,
+// by one of its members A, in the new frame (sorted by cell).  One lane per A,
+// fixed blocks of 256 consecutive frame entries.
+//
+// Both members "near" (FL_JUMP clear: live in the same space at t-1 and moved
+// at most d_rel*D <= D/4 per axis): N_t != N_t-1 needs the pair in the band
+// (BW = 2 d_rel D + M covers both displacements plus the float32 rounding of
+// the window bounds; lo = D - BW, hi = D + BW, all differences fl(b - a)):
+//   Z : dz in [lo, hi] and |dx| <= hi      (B above A)
+//   X': dx in [lo, hi] and |dz| <  lo      (B right of A, not in Z either way)
+// Z and X' are disjoint and every band pair is in exactly one of them from
+// exactly one side, so A queries two thin strips of cells instead of the
+// whole window.  Pairs where neither member changed are skipped.
+// A "jumper" A (new, changed space, moved > D/4) tests its whole window
+// (|d| <= hi + M) instead; a pair of two jumpers is visited by the lower
+// frame index, and near entities skip jumper partners.
+// Survivors of the cheap filter go to a per-wave LDS queue and get the full
+// go-aoi test (pair_kind<2>) with lanes over queue entries.  Events are
+// buffered per wave in processing order (deterministic); a wave whose buffer
+// overflows replays its sweep and writes the rest straight to the output.
 
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
-constexpr int CCAP = 512;   // staged candidates per chunk
-constexpr int QCAP = 256;   // per-wave queue of band survivors
-constexpr int EVW = 128;    // events buffered per wave
-constexpr int AROWS = 6;    // candidate rows per entity (else the per-thread fallback)
-constexpr uint32_t FL_JUMP = 1u, FL_CHG = 2u;
+constexpr int QCAP = 256;  // per-wave queue of filter survivors
+constexpr int EVW = 128;   // events buffered per wave
 
 struct CombinedLds {
-    uint4 c4[CCAP];     // staged candidate: x, z (bits), FL_* flags, frame index
-    uint2 q[CW][QCAP];  // queued pairs of a wave: (A's thread index, B's frame index)
+    uint2 q[CW][QCAP];  // queued pairs of a wave: (A frame index, B frame index)
     uint2 ev[CW][EVW];  // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
-    uint32_t seg[PMAXR];
-    uint32_t pre[PMAXR + 1];
-    int box[4];
     uint32_t wcnt[CW][2];
-    uint32_t ws[CW];
     unsigned long long base;
     uint32_t te, tl;
-    int fallback, overflow;
+    int overflow;
 };
 
-// The lane's own entity A: position, flags and candidate rows as virtual
-// ranges [vb, ve) of the tile's staged candidate list.
+struct CombinedCtx {  // block-uniform
+    SpaceGrid g;
+    PairCtx proto;
+    float thr, lo, hi, lo_in, M;
+    bool band_ok;  // lo > 0 (else every lane sweeps its whole window)
+};
+
 struct LaneA {
+    uint32_t a;  // frame index
     float x, z;
     uint32_t fl;
-    uint32_t vb[AROWS], ve[AROWS];
+    bool valid, jump;
 };
-
-__device__ __forceinline__ uint32_t flags_of(const Rec16 &now, const Rec16 &old, unsigned long long seq_base,
-                                             float thr) {
-    // old NaN (not live in this space at t-1) also fails is_near
-    return (is_near(now.x, now.z, old.x, old.z, thr) ? 0u : FL_JUMP) | (now.s >= seq_base ? FL_CHG : 0u);
-}
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
@@ -938,9 +949,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // REPLAY: count only, and write events number >= EVW straight to the output.
 template <bool REPLAY>
 __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, const FrameView &F,
-                                            const Rec16 *__restrict__ O_rec, uint32_t e0, const PairCtx &proto,
-                                            float thr, uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap,
-                                            unsigned long long pe, unsigned long long pl) {
+                                         const Rec16 *__restrict__ O_rec, const PairCtx &proto, float thr,
+                                         uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap, unsigned long long pe,
+                                         unsigned long long pl) {
     const uint32_t ln = lane();
     for (uint32_t q0 = 0; q0 < qn; q0 += WAVE) {
         const uint32_t e = q0 + ln;
@@ -948,7 +959,7 @@ __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, 
         uint32_t a = 0, b = 0;
         if (e < qn) {
             const uint2 q = L.q[w][e];
-            a = e0 + q.x;
+            a = q.x;
             b = q.y;
             PairCtx A = proto;
             A.a = a;
@@ -979,261 +990,234 @@ __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, 
     }
 }
 
-// One full sweep of the tile (all chunks).  Every wave takes part in staging;
-// only `work` waves filter and test.  Each lane sweeps its own entity's
-// candidate rows; the loop bounds are wave-uniform (max over lanes).
-template <bool REPLAY>
-__device__ void combined_sweep(CombinedLds &L, const FrameView &F, const Rec16 *__restrict__ O_rec, uint32_t e0,
-                               uint32_t nrows, const LaneA &me, const PairCtx &proto, float thr, float BW, bool work,
-                               uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap, unsigned long long pe,
-                               unsigned long long pl) {
-    const uint32_t tid = threadIdx.x;
-    const int w = tid / WAVE;
-    const uint32_t Ltot = L.pre[nrows];
-    const float D = proto.D, HM = proto.HM, DB = proto.D + BW;
-    uint32_t qn = 0;
-    for (uint32_t base = 0; base < Ltot; base += CCAP) {
-        const uint32_t lim = min(Ltot - base, (uint32_t)CCAP);
-        {  // stage candidates [base, base+lim)
-            int r = 0;
-            for (uint32_t i = tid; i < lim; i += CT) {
-                const uint32_t v = base + i;
-                while (v >= L.pre[r + 1]) ++r;
-                const uint32_t j = L.seg[r] + (v - L.pre[r]);
-                const Rec16 bn = ld_rec(F.rec, j);
-                const Rec16 bo = ld_rec(O_rec, j);
-                L.c4[i] = make_uint4(__float_as_uint(bn.x), __float_as_uint(bn.z),
-                                     flags_of(bn, bo, proto.seq_base, thr), j);
-            }
-        }
-        __syncthreads();
-        if (work) {
-#pragma unroll
-            for (int r = 0; r < AROWS; ++r) {
-                if ((uint32_t)r >= nrows) break;  // uniform
-                const uint32_t lo = max(me.vb[r], base), hi = min(me.ve[r], base + lim);
-                const uint32_t len = hi > lo ? hi - lo : 0u;
-                const uint32_t i0 = lo - base;
-                const uint32_t mx = wave_max_u32(len);
-                for (uint32_t t = 0; t < mx; ++t) {
-                    const bool valid = t < len;
-                    const uint4 c = L.c4[valid ? i0 + t : 0u];
-                    const float dx = fabsf(__uint_as_float(c.x) - me.x), dz = fabsf(__uint_as_float(c.y) - me.z);
-                    const uint32_t fl = c.z | me.fl;
-                    const bool band = ((int)(fabsf(dx - D) <= BW) & (int)(dz <= DB)) |
-                                      ((int)(fabsf(dz - D) <= BW) & (int)(dx <= DB));
-                    const bool keep = valid & (int)(dx <= HM) & (int)(dz <= HM) & (int)((fl & FL_CHG) != 0u) &
-                                      ((int)((fl & FL_JUMP) != 0u) | (int)band);
-                    const unsigned long long m = __ballot(keep);
-                    if (keep) L.q[w][qn + (uint32_t)__popcll(m & lanemask_lt())] = make_uint2(tid, c.w);
-                    qn += (uint32_t)__popcll(m);
-                    if (qn > QCAP - WAVE) {
-                        __builtin_amdgcn_wave_barrier();
-                        drain_queue<REPLAY>(L, w, qn, F, O_rec, e0, proto, thr, ne, nl, out, cap, pe, pl);
-                        qn = 0;
-                    }
-                }
-            }
-        }
-        __syncthreads();
+struct WaveQueue {
+    uint32_t qn;
+    uint32_t ne, nl;
+};
+
+// Append (a, b) for the lanes with keep set.  Wave-uniform.
+__device__ __forceinline__ void qpush(CombinedLds &L, int w, WaveQueue &Q, bool keep, uint32_t a, uint32_t b) {
+    const unsigned long long m = __ballot(keep);
+    if (keep) L.q[w][Q.qn + (uint32_t)__popcll(m & lanemask_lt())] = make_uint2(a, b);
+    Q.qn += (uint32_t)__popcll(m);
+}
+
+// Sweep the cell range [c0, c1] of grid row `row` for every lane (bounds are
+// per lane, loop trip count is the wave maximum).  MODE 0: Z strip, 1: X'
+// strip, 2: whole window of a jumper.
+template <int MODE, bool REPLAY>
+__device__ __forceinline__ void sweep_row(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int row,
+                                          int c0, int c1, const uint4 *__restrict__ cand, const FrameView &F,
+                                          const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
+                                          uint64_t cap, unsigned long long pe, unsigned long long pl) {
+    uint32_t jb = 0, len = 0;
+    if (on) {
+        const uint32_t rb = C.g.base + (uint32_t)row * C.g.gx;
+        jb = F.cell_start[rb + (uint32_t)c0];
+        len = F.cell_start[rb + (uint32_t)c1 + 1u] - jb;
     }
-    if (work && qn) {
-        __builtin_amdgcn_wave_barrier();
-        drain_queue<REPLAY>(L, w, qn, F, O_rec, e0, proto, thr, ne, nl, out, cap, pe, pl);
+    const uint32_t mx = wave_max_u32(len);
+    const float lo = C.lo, hi = C.hi;
+    for (uint32_t t = 0; t < mx; t += 2) {
+        const bool v0 = t < len, v1 = t + 1 < len;
+        const uint32_t b0 = jb + t, b1 = jb + t + 1;
+        const uint4 k0 = cand[v0 ? b0 : 0u], k1 = cand[v1 ? b1 : 0u];
+        bool keep0, keep1;
+        {
+            const float dx0 = __uint_as_float(k0.x) - A.x, dz0 = __uint_as_float(k0.y) - A.z;
+            const float dx1 = __uint_as_float(k1.x) - A.x, dz1 = __uint_as_float(k1.y) - A.z;
+            if (MODE == 0) {
+                keep0 = (int)(dz0 >= lo) & (int)(dz0 <= hi) & (int)(fabsf(dx0) <= hi) & (int)((k0.z & FL_JUMP) == 0u);
+                keep1 = (int)(dz1 >= lo) & (int)(dz1 <= hi) & (int)(fabsf(dx1) <= hi) & (int)((k1.z & FL_JUMP) == 0u);
+            } else if (MODE == 1) {
+                keep0 = (int)(dx0 >= lo) & (int)(dx0 <= hi) & (int)(fabsf(dz0) <= C.lo_in) &
+                        (int)((k0.z & FL_JUMP) == 0u);
+                keep1 = (int)(dx1 >= lo) & (int)(dx1 <= hi) & (int)(fabsf(dz1) <= C.lo_in) &
+                        (int)((k1.z & FL_JUMP) == 0u);
+            } else {
+                keep0 = (int)(fabsf(dx0) <= hi) & (int)(fabsf(dz0) <= hi) & (int)(b0 != A.a) &
+                        ((int)((k0.z & FL_JUMP) == 0u) | (int)(A.a < b0));
+                keep1 = (int)(fabsf(dx1) <= hi) & (int)(fabsf(dz1) <= hi) & (int)(b1 != A.a) &
+                        ((int)((k1.z & FL_JUMP) == 0u) | (int)(A.a < b1));
+            }
+            keep0 = keep0 & v0 & (int)(((k0.z | A.fl) & FL_CHG) != 0u);
+            keep1 = keep1 & v1 & (int)(((k1.z | A.fl) & FL_CHG) != 0u);
+        }
+        qpush(L, w, Q, keep0, A.a, b0);
+        qpush(L, w, Q, keep1, A.a, b1);
+        if (Q.qn > QCAP - 2 * WAVE) {
+            __builtin_amdgcn_wave_barrier();
+            drain_queue<REPLAY>(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl);
+            Q.qn = 0;
+        }
     }
 }
 
-__global__ __launch_bounds__(CT) void k_combined(FrameView F, const Rec16 *__restrict__ O_rec, TileSet TS,
-                                                 unsigned long long seq_base, const TickScalars *__restrict__ sc,
-                                                 unsigned long long *counter, uint2 *out, uint64_t cap,
-                                                 uint32_t *tile_total, unsigned long long *tile_base,
-                                                 uint32_t tile_off, uint32_t leave_off) {
+template <bool REPLAY>
+__device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
+                               const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
+                               uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl) {
+    const int w = threadIdx.x / WAVE;
+    const SpaceGrid &g = C.g;
+    WaveQueue Q{0u, ne, nl};
+    const float lo = C.lo, hi = C.hi, M = C.M;
+    const bool strip = A.valid && !A.jump && C.band_ok;
+    const bool whole = A.valid && (A.jump || !C.band_ok);
+    if (__ballot(strip)) {
+        // Z strip: rows holding z in [z+lo, z+hi], cells holding x in [x-hi, x+hi]
+        int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
+        if (strip) {
+            r0 = cell_of(A.z + lo - M, g.oz, g.inv, g.gz);
+            r1 = cell_of(A.z + hi + M, g.oz, g.inv, g.gz);
+            c0 = cell_of(A.x - hi - M, g.ox, g.inv, g.gx);
+            c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
+        }
+        const int nr = (int)wave_max_u32((uint32_t)(r1 - r0 + 1));
+        for (int k = 0; k < nr; ++k)
+            sweep_row<0, REPLAY>(L, w, Q, A, r0 + k <= r1, r0 + k, c0, c1, cand, F, O_rec, C, out, cap, pe, pl);
+        // X' strip: rows holding z in [z-lo, z+lo], cells holding x in [x+lo, x+hi]
+        r0 = 0, r1 = -1;
+        if (strip) {
+            r0 = cell_of(A.z - lo - M, g.oz, g.inv, g.gz);
+            r1 = cell_of(A.z + lo + M, g.oz, g.inv, g.gz);
+            c0 = cell_of(A.x + lo - M, g.ox, g.inv, g.gx);
+            c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
+        }
+        const int nx = (int)wave_max_u32((uint32_t)(r1 - r0 + 1));
+        for (int k = 0; k < nx; ++k)
+            sweep_row<1, REPLAY>(L, w, Q, A, r0 + k <= r1, r0 + k, c0, c1, cand, F, O_rec, C, out, cap, pe, pl);
+    }
+    if (__ballot(whole)) {
+        const float r = hi + M;
+        int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
+        if (whole) {
+            r0 = cell_of(A.z - r, g.oz, g.inv, g.gz);
+            r1 = cell_of(A.z + r, g.oz, g.inv, g.gz);
+            c0 = cell_of(A.x - r, g.ox, g.inv, g.gx);
+            c1 = cell_of(A.x + r, g.ox, g.inv, g.gx);
+        }
+        const int nr = (int)wave_max_u32((uint32_t)(r1 - r0 + 1));
+        for (int k = 0; k < nr; ++k)
+            sweep_row<2, REPLAY>(L, w, Q, A, r0 + k <= r1, r0 + k, c0, c1, cand, F, O_rec, C, out, cap, pe, pl);
+    }
+    if (Q.qn) {
+        __builtin_amdgcn_wave_barrier();
+        drain_queue<REPLAY>(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl);
+    }
+    ne = Q.ne;
+    nl = Q.nl;
+}
+
+// One block = frame entries [256 t, 256 t + 256).  A block that straddles
+// spaces (small spaces) sweeps once per distinct space among a wave's lanes.
+__global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__restrict__ cand,
+                                                 const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
+                                                 const TickScalars *__restrict__ sc, unsigned long long *counter,
+                                                 uint2 *out, uint64_t cap, uint32_t *tile_total,
+                                                 unsigned long long *tile_base, uint32_t leave_off) {
     __shared__ CombinedLds L;
     const uint32_t t = blockIdx.x;
-    if (t >= *TS.n_tiles) return;  // uniform per workgroup
-    const Tile T = TS.tiles[t];
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
-    const uint32_t nA = T.e1 - T.e0;
-    const SpaceGrid g = F.grid[TS.row_space[T.row]];
-    const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f;
-    const float thr = FAR_FRAC * g.D;
-    PairCtx proto;
-    proto.D = g.D;
-    proto.HM = g.D * (1.0f + 2.0f * sc->d_rel) + M;
-    proto.seq_base = seq_base;
-    proto.a = 0;
-    proto.chg = false;
-    const float BW = 2.0f * sc->d_rel * g.D + M;
-    const float r = proto.HM + M;  // query reach
+    const uint32_t e0 = t * CT;
+    if (tid == 0) L.overflow = 0;
 
-    // ---- per-entity setup: state, flags, cell ranges
-    const bool active = tid < nA;
-    const uint32_t a = T.e0 + tid;
-    int cx0 = INT_MAX, cx1 = INT_MIN, cz0 = INT_MAX, cz1 = INT_MIN;
-    LaneA me;
-    me.x = me.z = 0.f;
-    me.fl = 0;
-    if (active) {
-        const Rec16 now = ld_rec(F.rec, a), old = ld_rec(O_rec, a);
-        me.x = now.x;
-        me.z = now.z;
-        me.fl = flags_of(now, old, seq_base, thr);
-        cx0 = cell_of(now.x - r, g.ox, g.inv, g.gx);
-        cx1 = cell_of(now.x + r, g.ox, g.inv, g.gx);
-        cz0 = cell_of(now.z, g.oz, g.inv, g.gz);  // own row (the tile's row)
-        cz1 = cell_of(now.z + r, g.oz, g.inv, g.gz);
+    LaneA A;
+    A.a = e0 + tid;
+    A.valid = A.a < F.n;
+    const uint32_t ia = A.valid ? A.a : 0u;
+    const uint4 ca = cand[ia];
+    A.x = __uint_as_float(ca.x);
+    A.z = __uint_as_float(ca.y);
+    A.fl = ca.z;
+    A.jump = (ca.z & FL_JUMP) != 0u;
+    // spaces of the block: first and last entry (frame is space-major)
+    const uint32_t my_sp = ld_ss(F.ss, ia).sp;
+
+    uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform)
+    // sweep once per distinct space in this wave (almost always one)
+    auto run = [&](auto replay_tag, uint2 *o, unsigned long long pe, unsigned long long pl, uint32_t &e,
+                   uint32_t &l) {
+        constexpr bool RP = decltype(replay_tag)::value;
+        unsigned long long pending = __ballot(A.valid);
+        while (pending) {
+            const uint32_t lead = (uint32_t)__ffsll((long long)pending) - 1u;
+            const uint32_t sp = __shfl(my_sp, (int)lead);
+            const bool mine = A.valid && my_sp == sp;
+            pending &= ~__ballot(mine);
+            CombinedCtx C;
+            C.g = F.grid[sp];
+            C.M = (sc->bmax + 3.0f * C.g.D) * 0x1p-20f;
+            C.thr = FAR_FRAC * C.g.D;
+            const float BW = 2.0f * sc->d_rel * C.g.D + C.M;
+            C.lo = C.g.D - BW;
+            C.hi = C.g.D + BW;
+            C.lo_in = C.lo > 0.f ? __uint_as_float(__float_as_uint(C.lo) - 1u) : 0.f;
+            C.band_ok = C.lo > 0.f;
+            C.proto.D = C.g.D;
+            C.proto.HM = C.hi;
+            C.proto.seq_base = seq_base;
+            C.proto.a = 0;
+            C.proto.chg = false;
+            LaneA B = A;
+            B.valid = mine;
+            combined_sweep<RP>(L, B, cand, F, O_rec, C, e, l, o, cap, pe, pl);
+        }
+    };
+    run(std::false_type{}, nullptr, 0ull, 0ull, ne, nl);
+    if (ln == 0) {
+        L.wcnt[w][0] = ne;
+        L.wcnt[w][1] = nl;
     }
-    {
-        int v0 = cx0, v1 = cx1, v2 = cz0, v3 = cz1;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            v0 = min(v0, __shfl_xor(v0, o));
-            v1 = max(v1, __shfl_xor(v1, o));
-            v2 = min(v2, __shfl_xor(v2, o));
-            v3 = max(v3, __shfl_xor(v3, o));
-        }
-        if (tid == 0) {
-            L.box[0] = INT_MAX;
-            L.box[1] = INT_MIN;
-            L.box[2] = INT_MAX;
-            L.box[3] = INT_MIN;
-            L.fallback = 0;
-            L.overflow = 0;
-        }
-        __syncthreads();
-        if (ln == 0) {
-            atomicMin(&L.box[0], v0);
-            atomicMax(&L.box[1], v1);
-            atomicMin(&L.box[2], v2);
-            atomicMax(&L.box[3], v3);
-        }
-        if (active && cz1 - cz0 + 1 > AROWS) L.fallback = 1;
-        __syncthreads();
-    }
-    const int CX0 = L.box[0], CX1 = L.box[1], CZ0 = L.box[2], CZ1 = L.box[3];
-    const uint32_t nrows = (uint32_t)(CZ1 - CZ0 + 1);
-    if (nrows > AROWS) L.fallback = 1;  // every thread writes the same value
+    // ---- offsets: 2 directed pairs per event; the block's enters, then its leaves
     __syncthreads();
-    uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform); per thread in the fallback
-    if (!L.fallback) {
-        if (tid < nrows) {
-            const uint32_t row = g.base + (uint32_t)(CZ0 + (int)tid) * g.gx;
-            const uint32_t b = F.cell_start[row + (uint32_t)CX0];
-            L.seg[tid] = b;
-            L.pre[tid + 1] = F.cell_start[row + (uint32_t)CX1 + 1u] - b;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            L.pre[0] = 0;
-            for (uint32_t q = 0; q < nrows; ++q) L.pre[q + 1] += L.pre[q];
-        }
-        __syncthreads();
-        // this entity's candidate rows as virtual ranges (own row from a+1)
-#pragma unroll
-        for (int rr = 0; rr < AROWS; ++rr) {
-            me.vb[rr] = me.ve[rr] = 0;
-            const int cz = cz0 + rr;
-            if (active && cz <= cz1) {
-                const uint32_t row = g.base + (uint32_t)cz * g.gx;
-                uint32_t jb = F.cell_start[row + (uint32_t)cx0];
-                const uint32_t je = F.cell_start[row + (uint32_t)cx1 + 1u];
-                if (rr == 0) jb = a + 1;
-                const uint32_t vb = L.pre[cz - CZ0] + (jb - L.seg[cz - CZ0]);
-                me.vb[rr] = vb;
-                me.ve[rr] = vb + (je > jb ? je - jb : 0u);
-            }
-        }
-        combined_sweep<false>(L, F, O_rec, T.e0, nrows, me, proto, thr, BW, true, ne, nl, nullptr, 0, 0, 0);
-        if (ln == 0) {
-            L.wcnt[w][0] = ne;
-            L.wcnt[w][1] = nl;
-        }
-    } else if (active) {
-        PairCtx A = proto;
-        A.a = a;
-        A.now = ld_rec(F.rec, a);
-        A.oth = ld_rec(O_rec, a);
-        A.chg = A.now.s >= seq_base;
-        enum_global<2, false>(F, O_rec, nullptr, g, A, thr, cx0, cx1, cz0, cz1, 0, nullptr, 0, 0, 0, ne, nl);
-    }
-    // ---- offsets: 2 directed pairs per event; the tile's enters, then its leaves
-    uint32_t pre_e, pre_l;  // this wave's (or thread's) first enter / leave index in the tile
-    if (!L.fallback) {
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t se = 0, sl = 0;
-            for (int q = 0; q < CW; ++q) {
-                const uint32_t e = L.wcnt[q][0], l = L.wcnt[q][1];
-                L.wcnt[q][0] = se;
-                L.wcnt[q][1] = sl;
-                se += e;
-                sl += l;
-                if (e + l > (uint32_t)EVW) L.overflow = 1;
-            }
-            L.te = se;
-            L.tl = sl;
-        }
-        __syncthreads();
-        pre_e = L.wcnt[w][0];
-        pre_l = L.wcnt[w][1];
-    } else {
-        uint32_t te, tl;
-        pre_e = block_excl_scan<CT>(ne, L.ws, te);
-        __syncthreads();
-        pre_l = block_excl_scan<CT>(nl, L.ws, tl);
-        if (tid == 0) {
-            L.te = te;
-            L.tl = tl;
-        }
-        __syncthreads();
-    }
     if (tid == 0) {
-        const uint32_t tot = 2 * (L.te + L.tl);
+        uint32_t se = 0, sl = 0;
+        for (int q = 0; q < CW; ++q) {
+            const uint32_t e = L.wcnt[q][0], l = L.wcnt[q][1];
+            L.wcnt[q][0] = se;
+            L.wcnt[q][1] = sl;
+            se += e;
+            sl += l;
+            if (e + l > (uint32_t)EVW) L.overflow = 1;
+        }
+        L.te = se;
+        L.tl = sl;
+        const uint32_t tot = 2 * (se + sl);
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
         L.base = b;
-        tile_total[tile_off + t] = 2 * L.te;
-        tile_base[tile_off + t] = b;
-        tile_total[leave_off + tile_off + t] = 2 * L.tl;
-        tile_base[leave_off + tile_off + t] = b + 2ull * L.te;
+        tile_total[t] = 2 * se;
+        tile_base[t] = b;
+        tile_total[leave_off + t] = 2 * sl;
+        tile_base[leave_off + t] = b + 2ull * se;
     }
     __syncthreads();
+    const uint32_t pre_e = L.wcnt[w][0], pre_l = L.wcnt[w][1];
     const unsigned long long pe = L.base + 2ull * pre_e, pl = L.base + 2ull * L.te + 2ull * pre_l;
-    if (!L.fallback) {
-        // buffered events of this wave, in order, split by kind
-        const uint32_t nbuf = min(ne + nl, (uint32_t)EVW);
-        uint32_t ie = 0, il = 0;
-        for (uint32_t c = 0; c < nbuf; c += WAVE) {
-            const uint32_t e = c + ln;
-            const uint2 ev = e < nbuf ? L.ev[w][e] : make_uint2(0, 0);
-            const bool valid = e < nbuf;
-            const bool lv = (ev.y & KIND_LEAVE) != 0u;
-            const unsigned long long lm = __ballot(valid && lv), em = __ballot(valid && !lv);
-            if (valid) {
-                const uint32_t b_slot = ev.y & ~KIND_LEAVE;
-                const unsigned long long p = lv ? pl + 2ull * (il + (uint32_t)__popcll(lm & lanemask_lt()))
-                                                : pe + 2ull * (ie + (uint32_t)__popcll(em & lanemask_lt()));
-                if (p + 1 < cap) {
-                    out[p] = make_uint2(ev.x, b_slot);
-                    out[p + 1] = make_uint2(b_slot, ev.x);
-                }
+    // buffered events of this wave, in order, split by kind
+    const uint32_t nbuf = min(ne + nl, (uint32_t)EVW);
+    uint32_t ie = 0, il = 0;
+    for (uint32_t c = 0; c < nbuf; c += WAVE) {
+        const uint32_t e = c + ln;
+        const uint2 ev = e < nbuf ? L.ev[w][e] : make_uint2(0, 0);
+        const bool valid = e < nbuf;
+        const bool lv = (ev.y & KIND_LEAVE) != 0u;
+        const unsigned long long lm = __ballot(valid && lv), em = __ballot(valid && !lv);
+        if (valid) {
+            const uint32_t b_slot = ev.y & ~KIND_LEAVE;
+            const unsigned long long p = lv ? pl + 2ull * (il + (uint32_t)__popcll(lm & lanemask_lt()))
+                                            : pe + 2ull * (ie + (uint32_t)__popcll(em & lanemask_lt()));
+            if (p + 1 < cap) {
+                out[p] = make_uint2(ev.x, b_slot);
+                out[p + 1] = make_uint2(b_slot, ev.x);
             }
-            ie += (uint32_t)__popcll(em);
-            il += (uint32_t)__popcll(lm);
         }
-        if (L.overflow) {  // replay: waves past their buffer write the rest directly
-            uint32_t re = 0, rl = 0;
-            combined_sweep<true>(L, F, O_rec, T.e0, nrows, me, proto, thr, BW, ne + nl > (uint32_t)EVW, re, rl, out,
-                                 cap, pe, pl);
-        }
-    } else if (active && (ne | nl)) {
-        PairCtx A = proto;
-        A.a = a;
-        A.now = ld_rec(F.rec, a);
-        A.oth = ld_rec(O_rec, a);
-        A.chg = A.now.s >= seq_base;
-        uint32_t we = 0, wl = 0;
-        enum_global<2, true>(F, O_rec, nullptr, g, A, thr, cx0, cx1, cz0, cz1, 0, out, pe, pl, cap, we, wl);
+        ie += (uint32_t)__popcll(em);
+        il += (uint32_t)__popcll(lm);
+    }
+    if (ne + nl > (uint32_t)EVW) {  // replay: this wave writes the events past its buffer directly
+        uint32_t re = 0, rl = 0;
+        run(std::true_type{}, out, pe, pl, re, rl);
     }
 }
 
@@ -1511,12 +1495,12 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 }
 
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
-                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec,
-                   uint32_t *rank, const uint32_t *sorted_keys, uint32_t sentinel, uint32_t n_total,
-                   TickScalars *sc, hipStream_t st) {
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                   const SpaceGrid *grid, uint64_t seq_base, uint32_t *rank, const uint32_t *sorted_keys,
+                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
-    k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, rank,
-                                            sorted_keys, sentinel, n_total, sc);
+    k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand,
+                                            grid, seq_base, rank, sorted_keys, sentinel, n_total, sc);
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {
@@ -1537,12 +1521,18 @@ void launch_pairs(int mode, FrameView F, const Rec16 *O_rec, const SlotSp *O_ss,
                   unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st) {
     if (!F.n || !T.bound) return;
     uint2 *tmp = reinterpret_cast<uint2 *>(tmp_pairs);
-    if (mode == 2)
-        k_combined<<<T.bound, CT, 0, st>>>(F, O_rec, T, seq_base, sc, &sc->counter, tmp, cap, tile_total, tile_base,
-                                           tile_off, leave_off);
-    else
-        k_pairs<1><<<T.bound, PT, 0, st>>>(F, O_rec, O_ss, T, seq_base, sc, &sc->counter, tmp, cap, tile_total,
-                                           tile_base, tile_off, leave_off);
+    (void)mode;
+    k_pairs<1><<<T.bound, PT, 0, st>>>(F, O_rec, O_ss, T, seq_base, sc, &sc->counter, tmp, cap, tile_total, tile_base,
+                                       tile_off, leave_off);
+}
+
+void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
+                     uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
+                     uint32_t leave_off, hipStream_t st) {
+    if (!F.n) return;
+    k_combined<<<combined_blocks(F.n), CT, 0, st>>>(F, cand, O_rec, seq_base, sc, &sc->counter,
+                                                    reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base,
+                                                    leave_off);
 }
 
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,

@@ -86,6 +86,7 @@ struct gwaoi_world {
     gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
     gw::SlotSp *sss = nullptr;
     gw::Rec16 *orec = nullptr;  // previous state in the new frame's order (NaN if absent)
+    uint4 *cand = nullptr;      // combined-pass candidate records of the new frame
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;
@@ -458,14 +459,13 @@ int4 *dev_bbox(gwaoi_world *w) { return reinterpret_cast<int4 *>(w->dev_out + si
 // their exclusive scan is the final layout [enters | leaves] in tile order.
 void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_base) {
     hipStream_t st = w->stream;
-    const uint32_t TBn = Fn.n ? Fn.tile_bound : 0, TBp = P.n ? P.tile_bound : 0;
+    const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = P.n ? P.tile_bound : 0;
     const uint32_t half = TBn + TBp, entries = 2 * half;
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
-    gw::TileSet Tn{Fn.tiles, Fn.row_ntiles + Fn.n_rows, Fn.row_space, TBn};
     gw::TileSet Tp{P.tiles, P.row_ntiles + P.n_rows, P.row_space, TBp};
     stage_begin(w, ST_COMBINED);
-    gw::launch_pairs(2, Vn, w->orec, nullptr, Tn, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total,
-                     w->tile_base, 0, half, st);
+    gw::launch_combined(Vn, w->cand, w->orec, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
+                        half, st);
     stage_end(w, ST_COMBINED);
     stage_begin(w, ST_SPECIAL);
     gw::launch_pairs(1, Vp, w->srec, w->sss, Tp, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total,
@@ -499,7 +499,7 @@ int run_tick(gwaoi_world *w) {
     choose_grids(w, total_cells, total_rows);
     const uint32_t tbound = gw::tile_bound(n_new, total_rows);
     const uint32_t TBp = P.n ? P.tile_bound : 0;
-    const size_t entries = 2 * ((size_t)tbound + TBp);
+    const size_t entries = 2 * ((size_t)gw::combined_blocks(n_new) + TBp);
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tiles(w, Fn, total_rows, tbound))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
@@ -590,7 +590,8 @@ int run_tick(gwaoi_world *w) {
 
     // ---- new frame + previous state in the new order
     stage_begin(w, ST_GATHER);
-    gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->rank, skeys,
+    gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
+                      seq_base, w->rank, skeys,
                       total_cells, n_total, w->sc, st);
     stage_end(w, ST_GATHER);
 
@@ -710,7 +711,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
         dfree(f.rec); dfree(f.ss); dfree(f.cell_start); dfree(f.grid);
         dfree(f.row_space); dfree(f.row_ntiles); dfree(f.tiles);
     }
-    dfree(w->srec); dfree(w->sss); dfree(w->orec);
+    dfree(w->srec); dfree(w->sss); dfree(w->orec); dfree(w->cand);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->rank); dfree(w->lastop); dfree(w->new_slots_d);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
@@ -737,7 +738,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->cfg = *cfg;
     w->max_slots = cfg->max_slots;
     w->max_spaces = cfg->max_spaces;
-    w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 1.0f;
+    w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 4.0f;
     w->timing = (cfg->flags & GWAOI_F_TIMING) != 0;
     int rc = GWAOI_OK;
     auto fail = [&](int code) {
@@ -766,7 +767,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         if ((rc = ensure_cells(w, f, 1))) return fail(rc);
     }
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * (size_t)w->max_spaces;
-    if ((rc = dalloc(w, &w->srec, N)) || (rc = dalloc(w, &w->sss, N)) || (rc = dalloc(w, &w->orec, N)) ||
+    if ((rc = dalloc(w, &w->srec, N)) || (rc = dalloc(w, &w->sss, N)) || (rc = dalloc(w, &w->orec, N)) || (rc = dalloc(w, &w->cand, N)) ||
         (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->rank, N)) || (rc = dalloc(w, &w->lastop, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||

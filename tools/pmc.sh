@@ -1,5 +1,5 @@
 #!/bin/bash
-# Extra PMC passes on the cfg3 bench: bash tools_pmc.sh <tag> "<counters pass1>" "<counters pass2>" ...
+# Extra PMC passes on the cfg3 bench: bash tools/pmc.sh <tag> "<counters pass1>" "<counters pass2>" ...
 set -e
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

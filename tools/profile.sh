@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile the cfg3 bench on the GPU box: kernel trace + stats, then PMC passes.
-# usage: bash tools_profile.sh <tag> [bench args...]
+# usage: bash tools/profile.sh <tag> [bench args...]
 set -e
 TAG=${1:-r01}; shift || true
 R=${GRAFT_REPO_ROOT:-$(pwd)}
