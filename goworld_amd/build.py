@@ -43,5 +43,27 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "aoi_manager_test.cpp")
+CPP_TEST_OUT = os.path.join(HERE, "lib", "aoi_manager_test")
+
+
+def build_cpp_tests(force: bool = False, verbose: bool = False) -> str:
+    """Host C++ test of include/gwaoi_aoi.hpp, linked against the in-tree libgwaoi.so."""
+    lib = build(force=force, verbose=verbose)
+    deps = [CPP_TEST_SRC, lib, os.path.join(ROOT, "include", "gwaoi_aoi.hpp"), os.path.join(ROOT, "include", "gwaoi.h")]
+    if (not force and os.path.exists(CPP_TEST_OUT)
+            and all(os.path.getmtime(d) <= os.path.getmtime(CPP_TEST_OUT) for d in deps)):
+        return CPP_TEST_OUT
+    tmp = CPP_TEST_OUT + ".tmp"
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"), CPP_TEST_SRC, "-o", tmp,
+           "-L", os.path.dirname(lib), "-lgwaoi", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, CPP_TEST_OUT)
+    return CPP_TEST_OUT
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_cpp_tests(verbose=True))

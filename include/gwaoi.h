@@ -74,7 +74,7 @@ typedef struct {
     int32_t device;          /* HIP device ordinal, -1 = the calling thread's current */
     uint32_t flags;          /* GWAOI_F_*                                             */
     uint64_t event_capacity; /* initial device event capacity in pairs (0 = default) */
-    float cells_per_dist;    /* grid cells per AOI distance (0 = default 1.0)         */
+    float cells_per_dist;    /* grid cells per AOI distance (0 = default 4.0)         */
 } gwaoi_config;
 
 #define GWAOI_F_TIMING 1u /* time every pipeline stage with HIP events (gwaoi_stage_times) */
