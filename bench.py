@@ -124,6 +124,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-stage HIP event timing")
     ap.add_argument("--cells-per-dist", type=float, default=0.0)
+    ap.add_argument("--host-io-steps", type=int, default=10,
+                    help="extra ticks timed with host move batches in and host event arrays out (PCIe-inclusive)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -153,6 +155,7 @@ def main():
     wl = wl_factory()
     n = wl.n
     ticks = args.warmup + args.steps
+    hio = max(0, args.host_io_steps)
     # ---- synthetic move batches, generated before timing, resident in HBM
     import torch
     torch.cuda.set_device(device)
@@ -160,6 +163,7 @@ def main():
     for t in range(ticks):
         sl, nx, nz = wl.tick(t)
         batches.append((sl, nx, nz))
+    host_batches = [wl.tick(ticks + t) for t in range(hio)]  # PCIe-inclusive leg (host memory)
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
     d_x = torch.from_numpy(np.stack([b[1] for b in batches])).to(f"cuda:{device}")
     d_z = torch.from_numpy(np.stack([b[2] for b in batches])).to(f"cuda:{device}")
@@ -211,6 +215,29 @@ def main():
 
     stages = w.stage_times() if not args.no_timing else {}
     info = w.info()
+
+    # ---- PCIe-inclusive leg: host move arrays -> H2D -> tick -> events D2H into host arrays
+    host_io = None
+    if hio:
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        h_ev = 0
+        h0 = time.perf_counter()
+        for sl, nx, nz in host_batches:
+            w.moved_batch(sl, nx, nz)
+            ent, lev = w.tick()
+            h_ev += len(ent) + len(lev)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        h_el = time.perf_counter() - h0
+        h_el, (h_moves, h_evs) = reduce_over_ranks(dist, h_el, [sum(b[0].size for b in host_batches), h_ev],
+                                                   f"cuda:{device}")
+        host_io = {"value": h_moves / h_el, "unit": "entity-moves/s", "ms_per_step": h_el / hio * 1e3,
+                   "events_per_s": h_evs / h_el, "steps": hio,
+                   "note": "moves from host memory (H2D) + events copied to host arrays (D2H) per tick; "
+                           "not the headline value"}
     elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], f"cuda:{device}")
 
     if rank == 0:
@@ -265,6 +292,7 @@ def main():
             "initial_enter_events": ne0,
             "setup_s": round(setup_s, 2),
             "roofline": roofline,
+            "pcie_inclusive": host_io,
             "stages_ms_per_tick": {k: round(v, 4) for k, v in stage_ms.items()},
             "cpu_baseline": cpu,
         }

@@ -911,6 +911,16 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 // buffered per wave in processing order (deterministic); a wave whose buffer
 // overflows replays its sweep and writes the rest straight to the output.
 
+// Workgroups are dispatched round-robin over the 8 XCDs, each with its own
+// L2.  Neighbouring blocks read the same candidate rows, so give every XCD a
+// contiguous run of blocks: XCD x (bid % 8 == x) takes blocks
+// [x*q + min(x, r), ...) in order, q = nb / 8, r = nb % 8.
+constexpr uint32_t N_XCD = 8;
+__device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t nb) {
+    const uint32_t x = bid % N_XCD, k = bid / N_XCD, q = nb / N_XCD, r = nb % N_XCD;
+    return x * q + min(x, r) + k;
+}
+
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
 constexpr int QCAP = 256;  // per-wave queue of filter survivors
@@ -1116,7 +1126,7 @@ __global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__res
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
                                                  unsigned long long *tile_base, uint32_t leave_off) {
     __shared__ CombinedLds L;
-    const uint32_t t = blockIdx.x;
+    const uint32_t t = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
     const uint32_t e0 = t * CT;
