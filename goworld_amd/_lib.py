@@ -31,7 +31,7 @@ EXPORTS = [
     "gwaoi_enter", "gwaoi_leave", "gwaoi_moved", "gwaoi_enter_batch", "gwaoi_leave_batch",
     "gwaoi_moved_batch", "gwaoi_moved_batch_device", "gwaoi_tick", "gwaoi_tick_device",
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
-    "gwaoi_reset_stage_times", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
+    "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version",
 ]
 
@@ -98,6 +98,7 @@ def load():
         "gwaoi_world_info": ([vp, P(Info)], C.c_int),
         "gwaoi_stage_times": ([vp, P(StageTime), sz, P(sz)], C.c_int),
         "gwaoi_reset_stage_times": ([vp], C.c_int),
+        "gwaoi_set_stage_timing": ([vp, C.c_uint32], C.c_int),
         "gwaoi_sync": ([vp], C.c_int),
         "gwaoi_stream": ([vp], vp),
         "gwaoi_strerror": ([C.c_int], C.c_char_p),
@@ -231,6 +232,18 @@ class World:
         n = C.c_size_t()
         self._check(self._L.gwaoi_stage_times(self._w, arr, 32, C.byref(n)))
         return {arr[i].name.decode(): (arr[i].ms, arr[i].calls) for i in range(min(n.value, 32))}
+
+    def stage_names(self) -> list:
+        arr = (StageTime * 32)()
+        n = C.c_size_t()
+        self._check(self._L.gwaoi_stage_times(self._w, arr, 32, C.byref(n)))
+        return [arr[i].name.decode() for i in range(min(n.value, 32))]
+
+    def set_stage_timing(self, stages=None):
+        """Time the named stages with HIP events (None = all, [] = none)."""
+        names = self.stage_names()
+        mask = (1 << len(names)) - 1 if stages is None else sum(1 << names.index(s) for s in stages)
+        self._check(self._L.gwaoi_set_stage_timing(self._w, mask))
 
     def reset_stage_times(self):
         self._check(self._L.gwaoi_reset_stage_times(self._w))

@@ -29,6 +29,17 @@ struct alignas(8) SlotSp {  // caller slot handle + space id (SP_DEAD = not live
     uint32_t slot, sp;
 };
 
+// Per-slot record, indexed by the caller's slot: everything the op kernels
+// look up for a slot in one 16 B line.  lastop = (tick << 32 | op index) of
+// the slot's last op this flush; rank = its index in S' (previous frame
+// order, or appended); sp = its space in S' before this flush's ops
+// (SP_DEAD if not live).
+struct alignas(16) SlotInfo {
+    unsigned long long lastop;
+    uint32_t rank;
+    uint32_t sp;
+};
+
 // Uniform grid of one space for one flush.  Cell (cx,cz) of space s has the
 // global cell key base + cz*gx + cx; its grid row cz is global row
 // row_base + cz.  cellOf() is monotone in the coordinate, so a query range
@@ -91,14 +102,14 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
 void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec, SlotSp *s_ss,
                        hipStream_t st);
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
-                          uint32_t *rank, hipStream_t st);
+                          SlotInfo *info, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
 // means a device-resident Moved batch (keep the space).
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots,
-                      unsigned long long *lastop, uint32_t tick_id, TickScalars *sc, hipStream_t st);
+                      SlotInfo *info, uint32_t tick_id, TickScalars *sc, hipStream_t st);
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
-                      uint32_t j0, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
-                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss,
+                      uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+                      uint32_t n_total, uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss,
                       TickScalars *sc, hipStream_t st);
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
 // partials in blk, 2 * cdiv(n, 256) floats).
@@ -123,7 +134,7 @@ size_t scan_tmp_elems(size_t n);
 // combined pass's candidate records cand = {x, z, flags, 0}.
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
-                   const SpaceGrid *grid, uint64_t seq_base, uint32_t *rank, const uint32_t *sorted_keys,
+                   const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
@@ -156,7 +167,7 @@ void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_en
 // Per-space bounding box into the int4 array that follows TickOut.
 size_t bbox_part_bytes(uint32_t n);
 void launch_bbox(FrameView F, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st);
-void launch_neighbors(FrameView F, const uint32_t *rank, uint32_t slot, uint32_t *out, uint32_t cap,
+void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);
 // Zero `n` uint32 (rare re-run path).
 void launch_zero(uint32_t *p, size_t n, hipStream_t st);

@@ -106,7 +106,7 @@ __global__ void k_copy_state(uint32_t n, const Rec16 *__restrict__ p_rec, const 
 }
 
 __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t n_prev,
-                                Rec16 *s_rec, SlotSp *s_ss, uint32_t *rank) {
+                                Rec16 *s_rec, SlotSp *s_ss, SlotInfo *info) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_app) return;
     const uint32_t s = new_slots[i];
@@ -116,11 +116,11 @@ __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t
     r.s = 0;
     st_rec(s_rec, idx, r);
     st_ss(s_ss, idx, s, SP_DEAD);
-    rank[s] = idx;
+    reinterpret_cast<uint2 *>(info + s)[1] = make_uint2(idx, SP_DEAD);
 }
 
 __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint32_t j0, uint32_t max_slots,
-                            unsigned long long *lastop, uint32_t tick, TickScalars *sc) {
+                            SlotInfo *info, uint32_t tick, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slots[i];
@@ -128,40 +128,40 @@ __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint
         atomicOr(&sc->err, ERR_BAD_SLOT);
         return;
     }
-    atomicMax(&lastop[s], ((unsigned long long)tick << 32) | (j0 + i));
+    atomicMax(&info[s].lastop, ((unsigned long long)tick << 32) | (j0 + i));
 }
 
 // The last op of a slot in this flush determines its state (closed form:
 // only the final position and the final seq matter).
 __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
                             const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t n, uint32_t j0,
-                            uint32_t max_slots, const unsigned long long *__restrict__ lastop, uint32_t tick,
-                            const uint32_t *__restrict__ rank, uint32_t n_total, uint64_t seq_base, Rec16 *s_rec,
-                            SlotSp *s_ss, TickScalars *sc) {
+                            uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total, uint64_t seq_base,
+                            Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t j = j0 + i;
     const uint32_t s = slots[i];
     if (s >= max_slots) return;
-    if (lastop[s] != (((unsigned long long)tick << 32) | j)) return;
-    const uint32_t idx = rank[s];
-    const SlotSp cur = idx < n_total ? ld_ss(s_ss, idx) : SlotSp{SP_DEAD, SP_DEAD};
-    if (cur.slot != s) {
+    const uint4 si = reinterpret_cast<const uint4 *>(info)[s];  // lastop, rank, sp: one line
+    if ((((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return;
+    const uint32_t idx = si.z, cur_sp = si.w;
+    if (idx >= n_total) {
         atomicOr(&sc->err, ERR_MOVE_DEAD);
         return;
     }
     uint32_t sp = sps ? sps[i] : SP_KEEP;
     Rec16 r;
     r.s = seq_base + j;
-    if (sp == SP_DEAD) {  // Leave
+    if (sp == SP_DEAD) {  // Leave: the slot drops out of the next frame
         r.x = r.z = 0.0f;
         st_rec(s_rec, idx, r);
         st_ss(s_ss, idx, s, SP_DEAD);
+        reinterpret_cast<uint2 *>(info + s)[1] = make_uint2(0xFFFFFFFFu, SP_DEAD);
         return;
     }
     const bool keep = sp == SP_KEEP;
     if (keep) {  // device-side Moved
-        sp = cur.sp;
+        sp = cur_sp;
         if (sp == SP_DEAD) {
             atomicOr(&sc->err, ERR_MOVE_DEAD);
             return;
@@ -174,7 +174,7 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
         return;
     }
     st_rec(s_rec, idx, r);
-    if (!keep && sp != cur.sp) st_ss(s_ss, idx, s, sp);
+    if (!keep && sp != cur_sp) st_ss(s_ss, idx, s, sp);
 }
 
 // --------------------------------------------------------------- keygen ------
@@ -506,7 +506,7 @@ __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
                          SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
-                         unsigned long long seq_base, uint32_t *rank, const uint32_t *__restrict__ sorted_keys,
+                         unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
@@ -517,7 +517,7 @@ __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint
     const Rec16 now = ld_rec(s_rec, i);
     st_rec(f_rec, k, now);
     reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(ss.slot, ss.sp);
-    rank[ss.slot] = k;
+    reinterpret_cast<uint2 *>(info + ss.slot)[1] = make_uint2(k, ss.sp);
     // previous state of the same entity, NaN position unless live in the same space then
     Rec16 o;
     o.x = o.z = qnan();
@@ -1388,9 +1388,9 @@ __global__ __launch_bounds__(BB_T) void k_bbox_parts(const BBoxPart *__restrict_
 
 // ------------------------------------------------------------ neighbors ------
 
-__global__ __launch_bounds__(256) void k_neighbors(FrameView F, const uint32_t *__restrict__ rank, uint32_t slot,
+__global__ __launch_bounds__(256) void k_neighbors(FrameView F, const SlotInfo *__restrict__ info, uint32_t slot,
                                                    uint32_t *out, uint32_t cap, uint32_t *count) {
-    const uint32_t a = rank[slot];
+    const uint32_t a = info[slot].rank;
     if (a >= F.n || ld_ss(F.ss, a).slot != slot) return;
     const Rec16 A = ld_rec(F.rec, a);
     const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
@@ -1433,24 +1433,23 @@ void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16
 }
 
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
-                          uint32_t *rank, hipStream_t st) {
+                          SlotInfo *info, hipStream_t st) {
     if (!n_app) return;
-    k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_rec, s_ss, rank);
+    k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_rec, s_ss, info);
 }
 
-void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, unsigned long long *lastop,
+void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info,
                       uint32_t tick_id, TickScalars *sc, hipStream_t st) {
     if (!n) return;
-    k_ops_claim<<<cdiv(n, 256), 256, 0, st>>>(slots, n, j0, max_slots, lastop, tick_id, sc);
+    k_ops_claim<<<cdiv(n, 256), 256, 0, st>>>(slots, n, j0, max_slots, info, tick_id, sc);
 }
 
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
-                      uint32_t j0, uint32_t max_slots, const unsigned long long *lastop, uint32_t tick_id,
-                      const uint32_t *rank, uint32_t n_total, uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss,
-                      TickScalars *sc, hipStream_t st) {
+                      uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+                      uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st) {
     if (!n) return;
-    k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, n, j0, max_slots, lastop, tick_id, rank, n_total,
-                                              seq_base, s_rec, s_ss, sc);
+    k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, n, j0, max_slots, info, tick_id, n_total, seq_base,
+                                              s_rec, s_ss, sc);
 }
 
 void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
@@ -1506,11 +1505,11 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
-                   const SpaceGrid *grid, uint64_t seq_base, uint32_t *rank, const uint32_t *sorted_keys,
+                   const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
     k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand,
-                                            grid, seq_base, rank, sorted_keys, sentinel, n_total, sc);
+                                            grid, seq_base, info, sorted_keys, sentinel, n_total, sc);
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {
@@ -1570,9 +1569,9 @@ void launch_bbox(FrameView F, int4 *bbox, uint32_t n_spaces, void *parts_mem, hi
     k_bbox_parts<<<1, BB_T, 0, st>>>(parts, nb, bbox, n_spaces, parts + nb);
 }
 
-void launch_neighbors(FrameView F, const uint32_t *rank, uint32_t slot, uint32_t *out, uint32_t cap,
+void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st) {
-    k_neighbors<<<1, 256, 0, st>>>(F, rank, slot, out, cap, count);
+    k_neighbors<<<1, 256, 0, st>>>(F, info, slot, out, cap, count);
 }
 
 }  // namespace gw

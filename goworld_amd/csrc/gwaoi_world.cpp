@@ -91,8 +91,7 @@ struct gwaoi_world {
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;
     size_t scan_tmp_cap = 0;
-    uint32_t *rank = nullptr;
-    unsigned long long *lastop = nullptr;
+    gw::SlotInfo *sinfo = nullptr;  // per slot: last op claim, S' index, space
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
@@ -133,8 +132,8 @@ struct gwaoi_world {
     uint32_t n_alive = 0;
     uint64_t last_n_enter = 0, last_n_leave = 0;
 
-    // stage timing
-    bool timing = false;
+    // stage timing: bit s of timing_mask = time stage s with HIP events
+    uint32_t timing_mask = 0;
     hipEvent_t ev[ST_N][2] = {};
     bool ev_used[ST_N] = {};
     double stage_ms[ST_N] = {};
@@ -176,16 +175,15 @@ void dfree(T *&p) {
 inline bool finite2(float x, float z) { return std::isfinite(x) && std::isfinite(z); }
 
 void stage_begin(gwaoi_world *w, Stage s) {
-    if (!w->timing) return;
+    if (!(w->timing_mask >> s & 1u)) return;
     (void)hipEventRecord(w->ev[s][0], w->stream);
     w->ev_used[s] = true;
 }
 void stage_end(gwaoi_world *w, Stage s) {
-    if (!w->timing) return;
+    if (!(w->timing_mask >> s & 1u)) return;
     (void)hipEventRecord(w->ev[s][1], w->stream);
 }
 void stage_collect(gwaoi_world *w) {
-    if (!w->timing) return;
     for (int s = 0; s < ST_N; ++s) {
         if (!w->ev_used[s]) continue;
         float ms = 0.f;
@@ -530,7 +528,7 @@ int run_tick(gwaoi_world *w) {
     if (n_app) {
         HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
-        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->rank, st);
+        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->sinfo, st);
     }
     if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
@@ -560,9 +558,9 @@ int run_tick(gwaoi_world *w) {
                     hoff += k;
                 }
                 if (pass == 0)
-                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->lastop, tick_id, w->sc, st);
+                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->sinfo, tick_id, w->sc, st);
                 else
-                    gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->lastop, tick_id, w->rank, n_total,
+                    gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->sinfo, tick_id, n_total,
                                          seq_base, w->srec, w->sss, w->sc, st);
                 j0 += k;
             }
@@ -591,7 +589,7 @@ int run_tick(gwaoi_world *w) {
     // ---- new frame + previous state in the new order
     stage_begin(w, ST_GATHER);
     gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
-                      seq_base, w->rank, skeys,
+                      seq_base, w->sinfo, skeys,
                       total_cells, n_total, w->sc, st);
     stage_end(w, ST_GATHER);
 
@@ -713,7 +711,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     }
     dfree(w->srec); dfree(w->sss); dfree(w->orec); dfree(w->cand);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
-    dfree(w->hist); dfree(w->scan_tmp); dfree(w->rank); dfree(w->lastop); dfree(w->new_slots_d);
+    dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
     dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
@@ -739,7 +737,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->max_slots = cfg->max_slots;
     w->max_spaces = cfg->max_spaces;
     w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 4.0f;
-    w->timing = (cfg->flags & GWAOI_F_TIMING) != 0;
+    w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     int rc = GWAOI_OK;
     auto fail = [&](int code) {
         gwaoi_world_destroy(w);
@@ -770,13 +768,15 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if ((rc = dalloc(w, &w->srec, N)) || (rc = dalloc(w, &w->sss, N)) || (rc = dalloc(w, &w->orec, N)) || (rc = dalloc(w, &w->cand, N)) ||
         (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
-        (rc = dalloc(w, &w->rank, N)) || (rc = dalloc(w, &w->lastop, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||
+        (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||
         (rc = dalloc(w, &w->sc, 1)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, (char **)&w->bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
         (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
-    if (hipMemset(w->lastop, 0, N * sizeof(unsigned long long)) != hipSuccess) return fail(GWAOI_EDEVICE);
-    if (hipMemset(w->rank, 0xFF, N * sizeof(uint32_t)) != hipSuccess) return fail(GWAOI_EDEVICE);
+    // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
+    if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
+        hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
+        return fail(GWAOI_EDEVICE);
     if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_tile_entries(w, 2 * (size_t)gw::tile_bound((uint32_t)N, 1024)))) return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
@@ -785,11 +785,9 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (hipHostMalloc((void **)&w->h_out, out_bytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
         return fail(GWAOI_ENOMEM);
-    if (w->timing) {
-        for (int s = 0; s < ST_N; ++s)
-            for (int q = 0; q < 2; ++q)
-                if (hipEventCreate(&w->ev[s][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
-    }
+    for (int s = 0; s < ST_N; ++s)
+        for (int q = 0; q < 2; ++q)
+            if (hipEventCreate(&w->ev[s][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
     w->alive.assign(N, 0);
     w->in_frame.assign(N, 0);
     w->appended.assign(N, 0);
@@ -960,7 +958,7 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
         }
     }
     stage_end(w, ST_D2H);
-    if (w->timing) {
+    if (w->timing_mask) {
         (void)hipStreamSynchronize(w->stream);
         stage_collect(w);
     }
@@ -985,7 +983,7 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
     }
     const DevFrame &F = w->fr[w->cur];
     HIP_TRY(hipMemsetAsync(w->nb_count, 0, sizeof(uint32_t), w->stream));
-    gw::launch_neighbors(view_of(F), w->rank, slot, w->nb_out, (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu),
+    gw::launch_neighbors(view_of(F), w->sinfo, slot, w->nb_out, (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu),
                          w->nb_count, w->stream);
     HIP_TRY(hipGetLastError());
     uint32_t cnt = 0;
@@ -1021,6 +1019,12 @@ int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t 
         out[i].calls = w->stage_calls[i];
     }
     if (n_out) *n_out = ST_N;
+    return GWAOI_OK;
+}
+
+int gwaoi_set_stage_timing(gwaoi_world *w, uint32_t stage_mask) {
+    if (!w) return GWAOI_EINVAL;
+    w->timing_mask = stage_mask & ((1u << ST_N) - 1u);
     return GWAOI_OK;
 }
 

@@ -146,6 +146,9 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
 int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info);
 int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t *n_out);
 int gwaoi_reset_stage_times(gwaoi_world *w);
+/* Time only the stages whose bit is set (bit i = entry i of gwaoi_stage_times);
+ * 0 = no events at all.  GWAOI_F_TIMING at creation sets every bit.          */
+int gwaoi_set_stage_timing(gwaoi_world *w, uint32_t stage_mask);
 int gwaoi_sync(gwaoi_world *w);
 void *gwaoi_stream(gwaoi_world *w); /* the world's hipStream_t */
 
