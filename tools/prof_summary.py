@@ -117,6 +117,16 @@ def main():
         for c, v in sorted(kern[top]["pmc"].items()):
             lines.append(f"- {c}: {v:.6g}")
     open(dst + ".md", "w").write("\n".join(lines) + "\n")
+    kc = kern.get("k_combined")
+    if kc and "hbm_bytes" in kc:
+        # per-launch HBM traffic of the dominant kernel, read by bench.py (roofline.traffic)
+        pm = {"workload": (bench or {}).get("config", {}).get("workload", "cfg3").split(":")[0],
+              "kernel": "k_combined", "source": os.path.basename(dst),
+              "hbm_read_bytes_per_launch": kc["hbm_read_bytes"], "hbm_write_bytes_per_launch": kc["hbm_write_bytes"],
+              "hbm_bytes_per_launch": kc["hbm_bytes"], "steady_median_us": kc.get("steady_median_us"),
+              "note": "median over steady-state dispatches; read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE"}
+        with open(os.path.join(os.path.dirname(dst), "r01_pmc_k_combined.json"), "w") as fh:
+            json.dump(pm, fh, indent=1)
     print("\n".join(lines))
 
 
