@@ -32,7 +32,14 @@ EXPORTS = [
     "gwaoi_moved_batch", "gwaoi_moved_batch_device", "gwaoi_tick", "gwaoi_tick_device",
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
-    "gwaoi_abi_version",
+    "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
+]
+
+# every function include/gwaoi_strips.h declares
+STRIP_EXPORTS = [
+    "gwaoi_strips_create", "gwaoi_strips_destroy", "gwaoi_strips_halo", "gwaoi_strips_route",
+    "gwaoi_strips_route_scatter", "gwaoi_strips_tick", "gwaoi_strips_events_device", "gwaoi_strips_events",
+    "gwaoi_strips_last_error",
 ]
 
 
@@ -49,7 +56,12 @@ class Events(C.Structure):
 class Info(C.Structure):
     _fields_ = [("ticks", C.c_uint64), ("next_seq", C.c_uint64), ("live", C.c_uint32),
                 ("spaces", C.c_uint32), ("total_cells", C.c_uint32), ("pending_ops", C.c_uint32),
-                ("event_capacity", C.c_uint64)]
+                ("event_capacity", C.c_uint64), ("max_slots", C.c_uint32), ("max_spaces", C.c_uint32)]
+
+
+class StripsConfig(C.Structure):
+    _fields_ = [("n_strips", C.c_uint32), ("rank", C.c_uint32), ("edges", C.c_void_p),
+                ("aoi_distance", C.c_float), ("teleport", C.c_float)]
 
 
 class StageTime(C.Structure):
@@ -104,6 +116,18 @@ def load():
         "gwaoi_strerror": ([C.c_int], C.c_char_p),
         "gwaoi_last_error": ([vp], C.c_char_p),
         "gwaoi_abi_version": ([], C.c_int),
+        "gwaoi_enter_seq": ([vp, u32, u32, f, f, u64], C.c_int),
+        "gwaoi_moved_seq": ([vp, u32, f, f, u64], C.c_int),
+        "gwaoi_moved_batch_device_seq": ([vp, vp, vp, vp, vp, sz], C.c_int),
+        "gwaoi_strips_create": ([vp, u32, P(StripsConfig), P(vp)], C.c_int),
+        "gwaoi_strips_destroy": ([vp], C.c_int),
+        "gwaoi_strips_halo": ([vp, P(f)], C.c_int),
+        "gwaoi_strips_route": ([vp, vp, sz, P(u64)], C.c_int),
+        "gwaoi_strips_route_scatter": ([vp, vp, vp], C.c_int),
+        "gwaoi_strips_tick": ([vp, vp, sz, vp, sz, P(u64), P(u64)], C.c_int),
+        "gwaoi_strips_events_device": ([vp, P(vp), P(vp)], C.c_int),
+        "gwaoi_strips_events": ([vp, P(Events)], C.c_int),
+        "gwaoi_strips_last_error": ([vp], C.c_char_p),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -163,14 +187,20 @@ class World:
     def space_destroy(self, space):
         self._check(self._L.gwaoi_space_destroy(self._w, space))
 
-    def enter(self, space, slot, x, z):
-        self._check(self._L.gwaoi_enter(self._w, space, slot, C.c_float(x), C.c_float(z)))
+    def enter(self, space, slot, x, z, seq=None):
+        if seq is None:
+            self._check(self._L.gwaoi_enter(self._w, space, slot, C.c_float(x), C.c_float(z)))
+        else:
+            self._check(self._L.gwaoi_enter_seq(self._w, space, slot, C.c_float(x), C.c_float(z), int(seq)))
 
     def leave(self, slot):
         self._check(self._L.gwaoi_leave(self._w, slot))
 
-    def moved(self, slot, x, z):
-        self._check(self._L.gwaoi_moved(self._w, slot, C.c_float(x), C.c_float(z)))
+    def moved(self, slot, x, z, seq=None):
+        if seq is None:
+            self._check(self._L.gwaoi_moved(self._w, slot, C.c_float(x), C.c_float(z)))
+        else:
+            self._check(self._L.gwaoi_moved_seq(self._w, slot, C.c_float(x), C.c_float(z), int(seq)))
 
     def enter_batch(self, space, slots, x, z):
         s = np.ascontiguousarray(slots, np.uint32)
@@ -188,9 +218,13 @@ class World:
         z = np.ascontiguousarray(z, np.float32)
         self._check(self._L.gwaoi_moved_batch(self._w, _p(s), _p(x), _p(z), s.size))
 
-    def moved_batch_device(self, d_slots: int, d_x: int, d_z: int, n: int):
-        self._check(self._L.gwaoi_moved_batch_device(self._w, C.c_void_p(d_slots), C.c_void_p(d_x),
-                                                     C.c_void_p(d_z), n))
+    def moved_batch_device(self, d_slots: int, d_x: int, d_z: int, n: int, d_seq: int | None = None):
+        if d_seq is None:
+            self._check(self._L.gwaoi_moved_batch_device(self._w, C.c_void_p(d_slots), C.c_void_p(d_x),
+                                                         C.c_void_p(d_z), n))
+        else:
+            self._check(self._L.gwaoi_moved_batch_device_seq(self._w, C.c_void_p(d_slots), C.c_void_p(d_x),
+                                                             C.c_void_p(d_z), C.c_void_p(d_seq), n))
 
     # ---- flush
     def tick(self):

@@ -15,6 +15,7 @@ constexpr uint32_t ERR_NONFINITE = 1u;
 constexpr uint32_t ERR_MOVE_DEAD = 2u;       // device move of a slot that is not live
 constexpr uint32_t ERR_BAD_SLOT = 4u;
 constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreement (bug guard)
+constexpr uint32_t ERR_SEQ = 16u;            // explicit device seq below the flush's floor
 
 constexpr uint32_t TILE_A = 256;  // entities per pair-pass tile (= threads per workgroup)
 
@@ -83,6 +84,7 @@ struct TickScalars {
     unsigned long long counter;  // directed event pairs reserved by the pair passes
     float d_rel;                 // largest displacement / D of "near" entities
     float bmax;                  // largest |x|,|z| of live entities (new positions)
+    unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
 };
 
 // Device -> host block copied once per tick: result + per-space bbox.
@@ -92,6 +94,8 @@ struct TickOut {
     uint32_t err;
     uint32_t pad;
     unsigned long long total64;
+    unsigned long long seq_max;
+    unsigned long long pad2;
     // followed by int4 bbox[n_spaces] (ordered-int min x, min z, max x, max z)
 };
 
@@ -104,13 +108,15 @@ void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
                           SlotInfo *info, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
-// means a device-resident Moved batch (keep the space).
+// means a device-resident Moved batch (keep the space).  Op i gets seq
+// seqs[i] when seqs is given (explicit: checked >= seq_floor, the largest
+// folded into sc->seq_max when track_max), else seq0 + i.
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots,
                       SlotInfo *info, uint32_t tick_id, TickScalars *sc, hipStream_t st);
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
                       uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
-                      uint32_t n_total, uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss,
-                      TickScalars *sc, hipStream_t st);
+                      uint32_t n_total, const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor,
+                      bool track_max, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st);
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
 // partials in blk, 2 * cdiv(n, 256) floats).
 void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,

@@ -84,6 +84,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->counter = 0;
         sc->d_rel = 0.0f;
         sc->bmax = 0.0f;
+        sc->seq_max = 0;
     }
     if (i < n0) z0[i] = 0;
     if (i < n1) z1[i] = 0;
@@ -133,48 +134,73 @@ __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint
 
 // The last op of a slot in this flush determines its state (closed form:
 // only the final position and the final seq matter).
-__global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
-                            const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t n, uint32_t j0,
-                            uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total, uint64_t seq_base,
-                            Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Apply op i if it is its slot's last op of this flush; returns its explicit
+// seq (0 if none / not applied) for the seq_max fold.
+__device__ __forceinline__ unsigned long long op_apply_one(
+    const uint32_t *__restrict__ slots, const float *__restrict__ xs, const float *__restrict__ zs,
+    const uint32_t *__restrict__ sps, uint32_t i, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick,
+    uint32_t n_total, const unsigned long long *__restrict__ seqs, unsigned long long seq0,
+    unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc) {
     const uint32_t j = j0 + i;
     const uint32_t s = slots[i];
-    if (s >= max_slots) return;
+    if (s >= max_slots) return 0;
     const uint4 si = reinterpret_cast<const uint4 *>(info)[s];  // lastop, rank, sp: one line
-    if ((((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return;
+    if ((((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return 0;
     const uint32_t idx = si.z, cur_sp = si.w;
     if (idx >= n_total) {
         atomicOr(&sc->err, ERR_MOVE_DEAD);
-        return;
+        return 0;
     }
     uint32_t sp = sps ? sps[i] : SP_KEEP;
     Rec16 r;
-    r.s = seq_base + j;
+    r.s = seqs ? seqs[i] : seq0 + i;
+    if (r.s < seq_floor) {  // explicit seq older than an earlier flush: the closed form would be wrong
+        atomicOr(&sc->err, ERR_SEQ);
+        return 0;
+    }
     if (sp == SP_DEAD) {  // Leave: the slot drops out of the next frame
         r.x = r.z = 0.0f;
         st_rec(s_rec, idx, r);
         st_ss(s_ss, idx, s, SP_DEAD);
         reinterpret_cast<uint2 *>(info + s)[1] = make_uint2(0xFFFFFFFFu, SP_DEAD);
-        return;
+        return r.s;
     }
     const bool keep = sp == SP_KEEP;
     if (keep) {  // device-side Moved
         sp = cur_sp;
         if (sp == SP_DEAD) {
             atomicOr(&sc->err, ERR_MOVE_DEAD);
-            return;
+            return 0;
         }
     }
     r.x = xs[i];
     r.z = zs[i];
     if (!isfinite(r.x) || !isfinite(r.z)) {
         atomicOr(&sc->err, ERR_NONFINITE);
-        return;
+        return 0;
     }
     st_rec(s_rec, idx, r);
     if (!keep && sp != cur_sp) st_ss(s_ss, idx, s, sp);
+    return r.s;
+}
+
+__global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
+                            const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t n, uint32_t j0,
+                            uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
+                            const unsigned long long *__restrict__ seqs, unsigned long long seq0,
+                            unsigned long long seq_floor, int track_max, Rec16 *s_rec, SlotSp *s_ss,
+                            TickScalars *sc) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long smax = 0;
+    if (i < n) smax = op_apply_one(slots, xs, zs, sps, i, j0, max_slots, info, tick, n_total, seqs, seq0, seq_floor,
+                                   s_rec, s_ss, sc);
+    if (track_max) {  // one atomic per wave, not per op
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(smax, o, WAVE);
+            smax = v > smax ? v : smax;
+        }
+        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
+    }
 }
 
 // --------------------------------------------------------------- keygen ------
@@ -1255,6 +1281,7 @@ __global__ void k_finish(const uint32_t *__restrict__ dest, uint32_t n_enter_ent
     res->n_total = dest[n_entries];
     res->err = sc->err;
     res->total64 = sc->counter;
+    res->seq_max = sc->seq_max;
 }
 
 // ----------------------------------------------------------------- bbox ------
@@ -1446,10 +1473,11 @@ void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t m
 
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
                       uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
-                      uint64_t seq_base, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st) {
+                      const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor, bool track_max,
+                      Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st) {
     if (!n) return;
-    k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, n, j0, max_slots, info, tick_id, n_total, seq_base,
-                                              s_rec, s_ss, sc);
+    k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, n, j0, max_slots, info, tick_id, n_total, seqs, seq0,
+                                              seq_floor, track_max ? 1 : 0, s_rec, s_ss, sc);
 }
 
 void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,

@@ -1,0 +1,688 @@
+// gwaoi_strips.hip -- strip tiling of one oversized space over several GPUs
+// (include/gwaoi_strips.h; BASELINE config 5).
+//
+// A strip rank keeps, per global slot, the entity's state as this rank last
+// saw it (cur) and, for the tick in progress, the state before it (prv,
+// valid when ptick == tick).  "Present" = inside this rank's region
+// [edge_lo - H, edge_hi + H) and in the space; absent records have NaN x.
+//
+// Kernels (all one-lane-per-record, 256-thread blocks, stable block-scan
+// compaction so that every output order is deterministic):
+//   k_route      owner side: op -> halo records per destination + teleports
+//   k_recv       receiver side: records -> world ops (device moves, host
+//                enters/leaves) + per-slot state update
+//   k_tele_mark  mark this tick's teleporters
+//   k_filter     keep the world events this strip owns
+//   k_tele_pairs teleporter x teleporter pairs decided from before/after states
+// The exchange between ranks is the caller's (goworld_amd/strips.py: RCCL
+// all_to_all + all_gather).
+
+#include "gwaoi_internal.h"
+#include "../../include/gwaoi_strips.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+using gw::Rec16;
+
+namespace {
+
+constexpr int BT = 256;
+constexpr int WV = 64;
+constexpr int NW = BT / WV;
+
+constexpr uint32_t SE_STATE = 1u;     // op for an entity this strip does not own / record for a slot in the wrong state
+constexpr uint32_t SE_NONFINITE = 2u;
+constexpr uint32_t SE_BADSLOT = 4u;
+constexpr uint32_t SE_KIND = 8u;
+
+struct StripGeo {
+    uint32_t S, rank;
+    float H, tele, D;
+    uint32_t max_slots;
+    float edge[GWAOI_MAX_STRIPS];  // S-1 interior edges
+    float rlo[GWAOI_MAX_STRIPS];   // region of strip q: [rlo[q], rhi[q])
+    float rhi[GWAOI_MAX_STRIPS];
+};
+
+__device__ __forceinline__ uint32_t strip_of(const StripGeo &g, float x) {
+    uint32_t q = 0;
+    for (uint32_t i = 0; i + 1 < g.S; ++i) q += (x >= g.edge[i]) ? 1u : 0u;
+    return q;
+}
+
+__device__ __forceinline__ unsigned long long region_mask(const StripGeo &g, float x) {
+    unsigned long long m = 0;
+    for (uint32_t q = 0; q < g.S; ++q)
+        if (x >= g.rlo[q] && x < g.rhi[q]) m |= 1ull << q;
+    return m;
+}
+
+__device__ __forceinline__ bool present(const Rec16 &r) { return !isnan(r.x); }
+
+__device__ __forceinline__ Rec16 ld16(const Rec16 *p, uint32_t i) {
+    const uint4 q = reinterpret_cast<const uint4 *>(p)[i];
+    Rec16 r;
+    r.x = __uint_as_float(q.x);
+    r.z = __uint_as_float(q.y);
+    r.s = ((unsigned long long)q.w << 32) | q.z;
+    return r;
+}
+__device__ __forceinline__ void st16(Rec16 *p, uint32_t i, const Rec16 &r) {
+    reinterpret_cast<uint4 *>(p)[i] =
+        make_uint4(__float_as_uint(r.x), __float_as_uint(r.z), (uint32_t)r.s, (uint32_t)(r.s >> 32));
+}
+__device__ __forceinline__ Rec16 absent_rec() {
+    Rec16 r;
+    r.x = r.z = __int_as_float(0x7FC00000);
+    r.s = 0;
+    return r;
+}
+
+// go-aoi window test of the closed form (same operand
+// order as the world kernels): W = the one whose Enter/Moved came last.
+__device__ __forceinline__ bool rel(const Rec16 &a, const Rec16 &b, float D) {
+    const bool own = a.s > b.s;
+    const float wx = own ? a.x : b.x, wz = own ? a.z : b.z;
+    const float px = own ? b.x : a.x, pz = own ? b.z : a.z;
+    return (int)(px >= wx - D) & (int)(px <= wx + D) & (int)(pz >= wz - D) & (int)(pz <= wz + D);
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << __lane_id()) - 1ull; }
+
+// Block-level stable multi-split: every lane holds a destination mask over K
+// classes (K <= 65); class extra_q takes its bit from `extra`.  Phase 0 writes the block's per-class counts to
+// counts[q*nb + blk]; phase 1 returns, through `pos`, each lane's output
+// index for class q (offs = exclusive scan of counts) via the callback.
+template <class Emit>
+__device__ __forceinline__ void multisplit(int phase, unsigned long long mask, bool extra, uint32_t extra_q, uint32_t K,
+                                           uint32_t *counts, const uint32_t *offs, uint32_t nb, Emit emit) {
+    __shared__ uint32_t cnt[GWAOI_MAX_STRIPS + 1][NW];
+    const uint32_t w = threadIdx.x / WV;
+    for (uint32_t q = 0; q < K; ++q) {
+        const bool in = q == extra_q ? extra : (bool)((mask >> q) & 1ull);
+        const unsigned long long b = __ballot(in);
+        if (__lane_id() == 0) cnt[q][w] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (phase == 0) {
+        for (uint32_t q = threadIdx.x; q < K; q += BT) {
+            uint32_t t = 0;
+            for (int k = 0; k < NW; ++k) t += cnt[q][k];
+            counts[(size_t)q * nb + blockIdx.x] = t;
+        }
+        return;
+    }
+    for (uint32_t q = 0; q < K; ++q) {
+        const bool in = q == extra_q ? extra : (bool)((mask >> q) & 1ull);
+        const unsigned long long b = __ballot(in);
+        if (!in) continue;
+        uint32_t base = offs[(size_t)q * nb + blockIdx.x];
+        for (uint32_t k = 0; k < w; ++k) base += cnt[q][k];
+        emit(q, base + (uint32_t)__popcll(b & lanemask_lt()));
+    }
+}
+
+// ---- owner side: classes 0..S-1 = destination ranks, S = teleports
+__global__ void __launch_bounds__(BT) k_route(int phase, const gwaoi_halo_rec *__restrict__ ops, uint32_t n,
+                                              const Rec16 *__restrict__ cur, StripGeo g, uint32_t *counts,
+                                              const uint32_t *__restrict__ offs, uint32_t nb, uint32_t *err,
+                                              gwaoi_halo_rec *send, gwaoi_tele_rec *tele) {
+    const uint32_t i = blockIdx.x * BT + threadIdx.x;
+    unsigned long long mP = 0, mN = 0;
+    bool tp = false;
+    gwaoi_halo_rec op{};
+    Rec16 pv = absent_rec(), nw = absent_rec();
+    if (i < n) {
+        op = ops[i];
+        uint32_t e = 0;
+        if (op.slot >= g.max_slots) {
+            e = SE_BADSLOT;
+        } else {
+            pv = ld16(cur, op.slot);
+            const bool have = present(pv);
+            const bool mine = have && strip_of(g, pv.x) == g.rank;
+            if (op.kind == GWAOI_HALO_MOVE || op.kind == GWAOI_HALO_ENTER) {
+                nw.x = op.x;
+                nw.z = op.z;
+                nw.s = op.seq;
+                if (!isfinite(op.x) || !isfinite(op.z)) e = SE_NONFINITE;
+                else if (op.kind == GWAOI_HALO_MOVE ? !mine : (have || strip_of(g, op.x) != g.rank)) e = SE_STATE;
+            } else if (op.kind == GWAOI_HALO_LEAVE) {
+                if (!mine) e = SE_STATE;
+            } else {
+                e = SE_KIND;
+            }
+        }
+        if (e) {
+            if (phase == 0) atomicOr(err, e);
+        } else {
+            if (op.kind != GWAOI_HALO_ENTER) mP = region_mask(g, pv.x);
+            if (op.kind != GWAOI_HALO_LEAVE) mN = region_mask(g, nw.x);
+            tp = op.kind == GWAOI_HALO_MOVE && fabsf(nw.x - pv.x) > g.tele;
+        }
+    }
+    if (phase == 0 && i == 0) counts[(size_t)(g.S + 1) * nb] = 0;
+    multisplit(phase, mP | mN, tp, g.S, g.S + 1, counts, offs, nb, [&](uint32_t q, uint32_t pos) {
+        if (q < g.S) {
+            const bool inP = (mP >> q) & 1ull, inN = (mN >> q) & 1ull;
+            gwaoi_halo_rec r;
+            r.slot = op.slot;
+            r.kind = inP && inN ? GWAOI_HALO_MOVE : (inN ? GWAOI_HALO_ENTER : GWAOI_HALO_LEAVE);
+            const Rec16 &src = inN ? nw : pv;
+            r.x = src.x;
+            r.z = src.z;
+            r.seq = src.s;
+            send[pos] = r;
+        } else {
+            gwaoi_tele_rec t;
+            t.slot = op.slot;
+            t.flags = 3u;
+            t.px = pv.x;
+            t.pz = pv.z;
+            t.pseq = pv.s;
+            t.x = nw.x;
+            t.z = nw.z;
+            t.seq = nw.s;
+            tele[pos - offs[(size_t)g.S * nb]] = t;
+        }
+    });
+}
+
+// ---- receiver side: classes 0 = world device moves, 1 = host enters, 2 = host leaves
+__global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__restrict__ rv, uint32_t n, Rec16 *cur,
+                                             Rec16 *prv, uint32_t *ptick, uint32_t tick, uint32_t max_slots,
+                                             uint32_t *counts, const uint32_t *__restrict__ offs, uint32_t nb,
+                                             uint32_t *err, uint32_t *m_slot, float *m_x, float *m_z,
+                                             unsigned long long *m_seq, gwaoi_halo_rec *el) {
+    const uint32_t i = blockIdx.x * BT + threadIdx.x;
+    unsigned long long m = 0;
+    gwaoi_halo_rec r{};
+    if (i < n) {
+        r = rv[i];
+        uint32_t e = 0;
+        if (r.slot >= max_slots) {
+            e = SE_BADSLOT;
+        } else if (r.kind > GWAOI_HALO_LEAVE) {
+            e = SE_KIND;
+        } else {
+            const Rec16 c = ld16(cur, r.slot);
+            if ((r.kind == GWAOI_HALO_ENTER) == present(c)) e = SE_STATE;  // a sender sends one record per slot
+            if (phase == 1 && !e) {
+                prv[r.slot] = c;
+                ptick[r.slot] = tick;
+                Rec16 nw = absent_rec();
+                if (r.kind != GWAOI_HALO_LEAVE) {
+                    nw.x = r.x;
+                    nw.z = r.z;
+                    nw.s = r.seq;
+                }
+                st16(cur, r.slot, nw);
+            }
+        }
+        if (e) {
+            if (phase == 0) atomicOr(err, e);
+        } else {
+            m = 1ull << r.kind;
+        }
+    }
+    if (phase == 0 && i == 0) counts[3 * nb] = 0;
+    multisplit(phase, m, false, 0xFFFFFFFFu, 3, counts, offs, nb, [&](uint32_t q, uint32_t pos) {
+        if (q == 0) {
+            m_slot[pos] = r.slot;
+            m_x[pos] = r.x;
+            m_z[pos] = r.z;
+            m_seq[pos] = r.seq;
+        } else {
+            el[pos - offs[nb]] = r;  // enters then leaves, contiguous
+        }
+    });
+}
+
+__global__ void k_tele_mark(const gwaoi_tele_rec *__restrict__ t, uint32_t n, uint32_t *ttick, uint32_t tick,
+                            uint32_t max_slots) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && t[i].slot < max_slots) ttick[t[i].slot] = tick;
+}
+
+__device__ __forceinline__ Rec16 before(const Rec16 *cur, const Rec16 *prv, const uint32_t *ptick, uint32_t s,
+                                        uint32_t tick) {
+    return ptick[s] == tick ? ld16(prv, s) : ld16(cur, s);
+}
+
+// ---- keep the world events this strip owns: class 0 enters (owner after the
+// tick), class 1 leaves (owner before the tick); teleporter pairs are dropped
+// here and decided by k_tele_pairs.
+__global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restrict__ ev, uint32_t ne, uint32_t nl,
+                                               const Rec16 *__restrict__ cur, const Rec16 *__restrict__ prv,
+                                               const uint32_t *__restrict__ ptick, const uint32_t *__restrict__ ttick,
+                                               uint32_t tick, StripGeo g, uint32_t *counts,
+                                               const uint32_t *__restrict__ offs, uint32_t nb, uint32_t leave_gap,
+                                               uint2 *out) {
+    const uint32_t i = blockIdx.x * BT + threadIdx.x;
+    unsigned long long m = 0;
+    uint2 p = make_uint2(0, 0);
+    if (i < ne + nl) {
+        p = ev[i];
+        const bool is_enter = i < ne;
+        const bool tt = ttick[p.x] == tick && ttick[p.y] == tick;
+        if (!tt) {
+            const Rec16 a = is_enter ? ld16(cur, p.x) : before(cur, prv, ptick, p.x, tick);
+            if (present(a) && strip_of(g, a.x) == g.rank) m = is_enter ? 1ull : 2ull;
+        }
+    }
+    if (phase == 0 && i == 0) counts[2 * nb] = 0;
+    multisplit(phase, m, false, 0xFFFFFFFFu, 2, counts, offs, nb,
+               [&](uint32_t q, uint32_t pos) { out[pos + (q ? leave_gap : 0u)] = p; });
+}
+
+// ---- teleporter x teleporter: phase 0 counts, phase 1 writes (atomic slots;
+// the pairs are few and their order is not part of the contract).
+__global__ void k_tele_pairs(int phase, const gwaoi_tele_rec *__restrict__ t, uint32_t n, StripGeo g,
+                             unsigned long long *cnt, uint2 *ent, uint2 *lev) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const gwaoi_tele_rec A = t[i];
+    Rec16 ap, an;
+    ap.x = A.px; ap.z = A.pz; ap.s = A.pseq;
+    an.x = A.x; an.z = A.z; an.s = A.seq;
+    const bool own_now = (A.flags & 2u) && strip_of(g, an.x) == g.rank;
+    const bool own_before = (A.flags & 1u) && strip_of(g, ap.x) == g.rank;
+    if (!own_now && !own_before) return;
+    uint32_t ce = 0, cl = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        if (j == i) continue;
+        const gwaoi_tele_rec B = t[j];
+        Rec16 bp, bn;
+        bp.x = B.px; bp.z = B.pz; bp.s = B.pseq;
+        bn.x = B.x; bn.z = B.z; bn.s = B.seq;
+        const bool was = (A.flags & 1u) && (B.flags & 1u) && rel(ap, bp, g.D);
+        const bool is = (A.flags & 2u) && (B.flags & 2u) && rel(an, bn, g.D);
+        if (own_now && is && !was) {
+            if (phase == 1) ent[atomicAdd(&cnt[0], 1ull)] = make_uint2(A.slot, B.slot);
+            else ++ce;
+        }
+        if (own_before && was && !is) {
+            if (phase == 1) lev[atomicAdd(&cnt[1], 1ull)] = make_uint2(A.slot, B.slot);
+            else ++cl;
+        }
+    }
+    if (phase == 0) {
+        if (ce) atomicAdd(&cnt[0], (unsigned long long)ce);
+        if (cl) atomicAdd(&cnt[1], (unsigned long long)cl);
+    }
+}
+
+// totals of a K-class multisplit: small[q] = offs[q*nb] for q = 0..K, small[K+1] = err
+__global__ void k_totals(const uint32_t *offs, uint32_t K, uint32_t nb, const uint32_t *err, uint32_t *small) {
+    const uint32_t q = threadIdx.x;
+    if (q <= K) small[q] = offs[(size_t)q * nb];
+    if (q == 0) small[K + 1] = *err;
+}
+
+inline uint32_t cdivu(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
+
+}  // namespace
+
+struct gwaoi_strips {
+    gwaoi_world *w = nullptr;
+    uint32_t space = 0;
+    hipStream_t st = nullptr;
+    StripGeo geo{};
+    uint32_t max_slots = 0;
+    Rec16 *cur = nullptr, *prv = nullptr;
+    uint32_t *ptick = nullptr, *ttick = nullptr;
+    uint32_t tick = 0;
+    // multisplit scratch
+    uint32_t *counts = nullptr, *scan_tmp = nullptr, *err = nullptr, *small_d = nullptr;
+    size_t counts_cap = 0, scan_cap = 0;
+    uint32_t *small_h = nullptr;  // pinned
+    // route state
+    const gwaoi_halo_rec *r_ops = nullptr;
+    uint32_t r_n = 0, r_nb = 0;
+    bool routed = false;
+    // received world ops
+    uint32_t *m_slot = nullptr;
+    float *m_x = nullptr, *m_z = nullptr;
+    unsigned long long *m_seq = nullptr;
+    size_t m_cap = 0;
+    gwaoi_halo_rec *el_d = nullptr;
+    size_t el_cap = 0;
+    std::vector<gwaoi_halo_rec> el_h;
+    // teleporter pairs
+    unsigned long long *tcnt = nullptr;
+    uint2 *tpairs = nullptr;
+    size_t tpairs_cap = 0;
+    // this strip's events
+    uint2 *out = nullptr;
+    size_t out_cap = 0;
+    uint64_t n_enter = 0, n_leave = 0;
+    uint32_t *h_events = nullptr;
+    size_t h_cap = 0;
+    std::string last_error;
+};
+
+namespace {
+
+#define S_TRY(expr)                                                          \
+    do {                                                                     \
+        hipError_t e_ = (expr);                                              \
+        if (e_ != hipSuccess) {                                              \
+            s->last_error = std::string(#expr) + ": " + hipGetErrorString(e_); \
+            return GWAOI_EDEVICE;                                            \
+        }                                                                    \
+    } while (0)
+
+template <class T>
+int grow(gwaoi_strips *s, T **p, size_t &cap, size_t need) {
+    if (need <= cap && *p) return GWAOI_OK;
+    const size_t c = std::max<size_t>({need + need / 4, cap * 2, 256});
+    S_TRY(hipStreamSynchronize(s->st));
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc((void **)p, c * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        s->last_error = std::string("hipMalloc: ") + hipGetErrorString(e);
+        return e == hipErrorOutOfMemory ? GWAOI_ENOMEM : GWAOI_EDEVICE;
+    }
+    cap = c;
+    return GWAOI_OK;
+}
+
+// counts (K*nb + 1) -> exclusive scan in place -> totals + err into small_h[0..K+1]
+int ensure_split(gwaoi_strips *s, uint32_t K, uint32_t nb) {
+    const size_t n = (size_t)K * nb + 1;
+    if (int rc = grow(s, &s->counts, s->counts_cap, n)) return rc;
+    if (int rc = grow(s, &s->scan_tmp, s->scan_cap, gw::scan_tmp_elems(n) + 16)) return rc;
+    return GWAOI_OK;
+}
+
+int split_totals(gwaoi_strips *s, uint32_t K, uint32_t nb) {
+    gw::scan_exclusive(s->counts, s->counts, (size_t)K * nb + 1, s->scan_tmp, s->st);
+    k_totals<<<1, 128, 0, s->st>>>(s->counts, K, nb, s->err, s->small_d);
+    S_TRY(hipGetLastError());
+    S_TRY(hipMemcpyAsync(s->small_h, s->small_d, (K + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->st));
+    S_TRY(hipStreamSynchronize(s->st));
+    return GWAOI_OK;
+}
+
+int ensure_moves(gwaoi_strips *s, size_t n) {
+    if (n <= s->m_cap && s->m_slot) return GWAOI_OK;
+    size_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    const size_t need = std::max<size_t>(n, s->m_cap * 2);
+    int rc;
+    if ((rc = grow(s, &s->m_slot, c0, need)) || (rc = grow(s, &s->m_x, c1, need)) ||
+        (rc = grow(s, &s->m_z, c2, need)) || (rc = grow(s, &s->m_seq, c3, need))) {
+        s->m_cap = 0;
+        return rc;
+    }
+    s->m_cap = std::min({c0, c1, c2, c3});
+    return GWAOI_OK;
+}
+
+int strip_err(gwaoi_strips *s, uint32_t e, const char *where) {
+    if (!e) return GWAOI_OK;
+    s->last_error = std::string(where) + ": " +
+                    ((e & SE_BADSLOT) ? "slot out of range" :
+                     (e & SE_KIND) ? "bad record kind" :
+                     (e & SE_NONFINITE) ? "non-finite coordinate" :
+                                          "entity not owned by / in the wrong state for this strip");
+    return (e & SE_BADSLOT) ? GWAOI_EBADSLOT : (e & SE_NONFINITE) ? GWAOI_ENONFINITE :
+           (e & SE_KIND) ? GWAOI_EINVAL : GWAOI_ESTATE;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gwaoi_strips_destroy(gwaoi_strips *s) {
+    if (!s) return GWAOI_EINVAL;
+    if (s->st) (void)hipStreamSynchronize(s->st);
+    void *dev[] = {s->cur, s->prv, s->ptick, s->ttick, s->counts, s->scan_tmp, s->err, s->small_d, s->m_slot,
+                   s->m_x, s->m_z, s->m_seq, s->el_d, s->tcnt, s->tpairs, s->out};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    if (s->small_h) (void)hipHostFree(s->small_h);
+    if (s->h_events) (void)hipHostFree(s->h_events);
+    delete s;
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_create(gwaoi_world *w, uint32_t space, const gwaoi_strips_config *cfg, gwaoi_strips **out) {
+    if (!w || !cfg || !out || cfg->n_strips == 0 || cfg->n_strips > GWAOI_MAX_STRIPS || cfg->rank >= cfg->n_strips ||
+        (cfg->n_strips > 1 && !cfg->edges) || !(cfg->aoi_distance > 0.f) || !std::isfinite(cfg->aoi_distance))
+        return GWAOI_EINVAL;
+    *out = nullptr;
+    for (uint32_t i = 0; i + 2 < cfg->n_strips; ++i)
+        if (!(cfg->edges[i] < cfg->edges[i + 1])) return GWAOI_EINVAL;
+    for (uint32_t i = 0; i + 1 < cfg->n_strips; ++i)
+        if (!std::isfinite(cfg->edges[i])) return GWAOI_EINVAL;
+    gwaoi_info info;
+    if (int rc = gwaoi_world_info(w, &info)) return rc;
+    gwaoi_strips *s = new (std::nothrow) gwaoi_strips();
+    if (!s) return GWAOI_ENOMEM;
+    s->w = w;
+    s->space = space;
+    s->st = (hipStream_t)gwaoi_stream(w);
+    s->max_slots = info.max_slots;
+    StripGeo &g = s->geo;
+    g.S = cfg->n_strips;
+    g.rank = cfg->rank;
+    g.D = cfg->aoi_distance;
+    g.tele = cfg->teleport > 0.f ? cfg->teleport : cfg->aoi_distance / 8.0f;
+    g.max_slots = s->max_slots;
+    // H = 2D + teleport + 1 (the +1 covers float32 rounding of the window
+    // bounds for |x| < 2^24)
+    const double H = 2.0 * (double)g.D + (double)g.tele + 1.0;
+    g.H = (float)H;
+    for (uint32_t q = 0; q < g.S; ++q) {
+        if (q + 1 < g.S) g.edge[q] = cfg->edges[q];
+        const double lo_q = q == 0 ? -INFINITY : (double)cfg->edges[q - 1] - H;
+        const double hi_q = q + 1 == g.S ? INFINITY : (double)cfg->edges[q] + H;
+        float fl = (float)lo_q, fh = (float)hi_q;  // round outward
+        if ((double)fl > lo_q) fl = std::nextafter(fl, -INFINITY);
+        if ((double)fh < hi_q) fh = std::nextafter(fh, INFINITY);
+        g.rlo[q] = fl;
+        g.rhi[q] = fh;
+    }
+    const size_t N = s->max_slots;
+    auto fail = [&](int rc) {
+        gwaoi_strips_destroy(s);
+        return rc;
+    };
+    if (hipMalloc((void **)&s->cur, N * sizeof(Rec16)) != hipSuccess ||
+        hipMalloc((void **)&s->prv, N * sizeof(Rec16)) != hipSuccess ||
+        hipMalloc((void **)&s->ptick, N * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->ttick, N * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->err, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->small_d, 128 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->tcnt, 2 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc((void **)&s->small_h, 128 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        return fail(GWAOI_ENOMEM);
+    if (hipMemsetAsync(s->cur, 0xFF, N * sizeof(Rec16), s->st) != hipSuccess ||  // x = NaN: absent
+        hipMemsetAsync(s->prv, 0xFF, N * sizeof(Rec16), s->st) != hipSuccess ||
+        hipMemsetAsync(s->ptick, 0, N * sizeof(uint32_t), s->st) != hipSuccess ||
+        hipMemsetAsync(s->ttick, 0, N * sizeof(uint32_t), s->st) != hipSuccess ||
+        hipMemsetAsync(s->err, 0, sizeof(uint32_t), s->st) != hipSuccess ||
+        hipStreamSynchronize(s->st) != hipSuccess)
+        return fail(GWAOI_EDEVICE);
+    *out = s;
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_halo(const gwaoi_strips *s, float *halo) {
+    if (!s || !halo) return GWAOI_EINVAL;
+    *halo = s->geo.H;
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint64_t *counts) {
+    if (!s || !counts || (n && !d_ops) || n > 0x7FFFFFFFu) return GWAOI_EINVAL;
+    const uint32_t K = s->geo.S + 1;
+    const uint32_t nb = std::max(1u, cdivu(n, BT));
+    if (int rc = ensure_split(s, K, nb)) return rc;
+    S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), s->st));
+    k_route<<<nb, BT, 0, s->st>>>(0, d_ops, (uint32_t)n, s->cur, s->geo, s->counts, nullptr, nb, s->err, nullptr,
+                                  nullptr);
+    if (int rc = split_totals(s, K, nb)) return rc;
+    if (int rc = strip_err(s, s->small_h[K + 1], "route")) return rc;
+    for (uint32_t q = 0; q < K; ++q) counts[q] = s->small_h[q + 1] - s->small_h[q];
+    s->r_ops = d_ops;
+    s->r_n = (uint32_t)n;
+    s->r_nb = nb;
+    s->routed = true;
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_tele_rec *d_tele) {
+    if (!s || !s->routed) return GWAOI_EINVAL;
+    s->routed = false;
+    k_route<<<s->r_nb, BT, 0, s->st>>>(1, s->r_ops, s->r_n, s->cur, s->geo, s->counts, s->counts, s->r_nb, s->err,
+                                       d_send, d_tele);
+    S_TRY(hipGetLastError());
+    S_TRY(hipStreamSynchronize(s->st));
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_recv, size_t n_recv, const gwaoi_tele_rec *d_tele,
+                      size_t n_tele, uint64_t *n_enter, uint64_t *n_leave) {
+    if (!s || (n_recv && !d_recv) || (n_tele && !d_tele) || n_recv > 0x7FFFFFFFu || n_tele > 0x7FFFFFFFu)
+        return GWAOI_EINVAL;
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    s->n_enter = s->n_leave = 0;
+    const uint32_t tick = ++s->tick;
+    hipStream_t st = s->st;
+    // ---- received records -> world ops + state
+    const uint32_t nb = std::max(1u, cdivu(n_recv, BT));
+    if (int rc = ensure_split(s, 3, nb)) return rc;
+    if (int rc = ensure_moves(s, n_recv)) return rc;
+    S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
+    k_recv<<<nb, BT, 0, st>>>(0, d_recv, (uint32_t)n_recv, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
+                              nullptr, nb, s->err, nullptr, nullptr, nullptr, nullptr, nullptr);
+    if (int rc = split_totals(s, 3, nb)) return rc;
+    if (int rc = strip_err(s, s->small_h[4], "recv")) return rc;
+    const uint32_t n_move = s->small_h[1] - s->small_h[0];
+    const uint32_t n_ent = s->small_h[2] - s->small_h[1];
+    const uint32_t n_lev = s->small_h[3] - s->small_h[2];
+    if (int rc = grow(s, &s->el_d, s->el_cap, (size_t)n_ent + n_lev + 1)) return rc;
+    k_recv<<<nb, BT, 0, st>>>(1, d_recv, (uint32_t)n_recv, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
+                              s->counts, nb, s->err, s->m_slot, s->m_x, s->m_z, s->m_seq, s->el_d);
+    S_TRY(hipGetLastError());
+    s->el_h.resize((size_t)n_ent + n_lev);
+    if (n_ent + n_lev)
+        S_TRY(hipMemcpyAsync(s->el_h.data(), s->el_d, ((size_t)n_ent + n_lev) * sizeof(gwaoi_halo_rec),
+                             hipMemcpyDeviceToHost, st));
+    if (n_tele) {
+        k_tele_mark<<<cdivu(n_tele, 256), 256, 0, st>>>(d_tele, (uint32_t)n_tele, s->ttick, tick, s->max_slots);
+        S_TRY(hipGetLastError());
+    }
+    S_TRY(hipStreamSynchronize(st));
+    // leaves (no seq), then enters in seq order, then the device moves
+    for (uint32_t k = 0; k < n_lev; ++k)
+        if (int rc = gwaoi_leave(s->w, s->el_h[n_ent + k].slot)) {
+            s->last_error = std::string("world leave: ") + gwaoi_last_error(s->w);
+            return rc;
+        }
+    std::sort(s->el_h.begin(), s->el_h.begin() + n_ent,
+              [](const gwaoi_halo_rec &a, const gwaoi_halo_rec &b) { return a.seq < b.seq; });
+    for (uint32_t k = 0; k < n_ent; ++k) {
+        const gwaoi_halo_rec &r = s->el_h[k];
+        if (int rc = gwaoi_enter_seq(s->w, s->space, r.slot, r.x, r.z, r.seq)) {
+            s->last_error = std::string("world enter: ") + gwaoi_last_error(s->w);
+            return rc;
+        }
+    }
+    if (int rc = gwaoi_moved_batch_device_seq(s->w, s->m_slot, s->m_x, s->m_z,
+                                              reinterpret_cast<const uint64_t *>(s->m_seq), n_move)) {
+        s->last_error = std::string("world moves: ") + gwaoi_last_error(s->w);
+        return rc;
+    }
+    uint64_t wne = 0, wnl = 0;
+    if (int rc = gwaoi_tick_device(s->w, &wne, &wnl)) {
+        s->last_error = std::string("world tick: ") + gwaoi_last_error(s->w);
+        return rc;
+    }
+    const uint32_t *wev = nullptr;
+    if (int rc = gwaoi_events_device(s->w, &wev, nullptr)) return rc;
+    // ---- teleporter pairs (counted first so the output can be laid out)
+    uint64_t te = 0, tl = 0;
+    if (n_tele > 1) {
+        S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
+        k_tele_pairs<<<cdivu(n_tele, 256), 256, 0, st>>>(0, d_tele, (uint32_t)n_tele, s->geo, s->tcnt, nullptr,
+                                                         nullptr);
+        unsigned long long hc[2];
+        S_TRY(hipMemcpyAsync(hc, s->tcnt, sizeof(hc), hipMemcpyDeviceToHost, st));
+        S_TRY(hipStreamSynchronize(st));
+        te = hc[0];
+        tl = hc[1];
+        if (int rc = grow(s, &s->tpairs, s->tpairs_cap, te + tl + 1)) return rc;
+        S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
+        k_tele_pairs<<<cdivu(n_tele, 256), 256, 0, st>>>(1, d_tele, (uint32_t)n_tele, s->geo, s->tcnt, s->tpairs,
+                                                         s->tpairs + te);
+        S_TRY(hipGetLastError());
+    }
+    // ---- filter the world's events to this strip's
+    const uint64_t nev = wne + wnl;
+    if (nev > 0x7FFFFFFFull) return GWAOI_ECAPACITY;
+    const uint32_t fb = std::max(1u, cdivu(nev, BT));
+    if (int rc = ensure_split(s, 2, fb)) return rc;
+    k_filter<<<fb, BT, 0, st>>>(0, reinterpret_cast<const uint2 *>(wev), (uint32_t)wne, (uint32_t)wnl, s->cur, s->prv,
+                                s->ptick, s->ttick, tick, s->geo, s->counts, nullptr, fb, 0, nullptr);
+    if (int rc = split_totals(s, 2, fb)) return rc;
+    const uint64_t fe = s->small_h[1] - s->small_h[0], fl = s->small_h[2] - s->small_h[1];
+    const uint64_t tot = fe + te + fl + tl;
+    if (int rc = grow(s, &s->out, s->out_cap, tot + 1)) return rc;
+    k_filter<<<fb, BT, 0, st>>>(1, reinterpret_cast<const uint2 *>(wev), (uint32_t)wne, (uint32_t)wnl, s->cur, s->prv,
+                                s->ptick, s->ttick, tick, s->geo, s->counts, s->counts, fb, (uint32_t)te, s->out);
+    S_TRY(hipGetLastError());
+    if (te) S_TRY(hipMemcpyAsync(s->out + fe, s->tpairs, te * sizeof(uint2), hipMemcpyDeviceToDevice, st));
+    if (tl) S_TRY(hipMemcpyAsync(s->out + fe + te + fl, s->tpairs + te, tl * sizeof(uint2), hipMemcpyDeviceToDevice, st));
+    S_TRY(hipStreamSynchronize(st));
+    s->n_enter = fe + te;
+    s->n_leave = fl + tl;
+    if (n_enter) *n_enter = s->n_enter;
+    if (n_leave) *n_leave = s->n_leave;
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const uint32_t **d_leave) {
+    if (!s) return GWAOI_EINVAL;
+    if (d_enter) *d_enter = reinterpret_cast<const uint32_t *>(s->out);
+    if (d_leave) *d_leave = reinterpret_cast<const uint32_t *>(s->out + s->n_enter);
+    return GWAOI_OK;
+}
+
+int gwaoi_strips_events(gwaoi_strips *s, gwaoi_events *out) {
+    if (!s || !out) return GWAOI_EINVAL;
+    const uint64_t tot = s->n_enter + s->n_leave;
+    if (tot > s->h_cap || !s->h_events) {
+        if (s->h_events) (void)hipHostFree(s->h_events);
+        s->h_events = nullptr;
+        s->h_cap = 0;
+        const size_t c = std::max<size_t>(tot + tot / 4, 1024);
+        S_TRY(hipHostMalloc((void **)&s->h_events, 2 * c * sizeof(uint32_t), hipHostMallocDefault));
+        s->h_cap = c;
+    }
+    if (tot) {
+        S_TRY(hipMemcpyAsync(s->h_events, s->out, tot * sizeof(uint2), hipMemcpyDeviceToHost, s->st));
+        S_TRY(hipStreamSynchronize(s->st));
+    }
+    out->n_enter = s->n_enter;
+    out->n_leave = s->n_leave;
+    out->enter = s->h_events;
+    out->leave = s->h_events + 2 * s->n_enter;
+    return GWAOI_OK;
+}
+
+const char *gwaoi_strips_last_error(gwaoi_strips *s) { return s ? s->last_error.c_str() : "null strips"; }
+
+}  // extern "C"

@@ -67,6 +67,8 @@ struct Run {  // a stretch of the op queue: host ops [hbegin, hend) or a device 
     size_t hbegin, hend;
     const uint32_t *ds;
     const float *dx, *dz;
+    const unsigned long long *dseq;  // explicit device seqs (nullptr: seq0 + i)
+    uint64_t seq0;
     size_t dn;
 };
 
@@ -95,6 +97,7 @@ struct gwaoi_world {
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
+    unsigned long long *op_seq = nullptr;
     size_t op_cap = 0;
     uint32_t *events = nullptr;      // ev_cap (a,b) pairs: [enters | leaves] in tile order
     uint32_t *events_tmp = nullptr;  // ev_cap pairs: per-tile chunks at reserved offsets
@@ -123,10 +126,15 @@ struct gwaoi_world {
     uint32_t n_spaces_live = 0;
     std::vector<uint32_t> h_op_slot, h_op_sp;
     std::vector<float> h_op_x, h_op_z;
+    std::vector<unsigned long long> h_op_seq;
     std::vector<Run> runs;
     size_t n_ops = 0;
     std::vector<uint32_t> new_slots;
-    uint64_t seq_next = 1;
+    std::vector<uint32_t> touched;  // slots whose liveness changed since the last flush
+    // seq_next: the seq the next implicit call gets (advanced at queue time);
+    // seq_floor: seq_next at the last flush = lower bound of this flush's seqs.
+    uint64_t seq_next = 1, seq_floor = 1;
+    bool dev_seq_pending = false;  // an explicit-seq device batch is queued (its max is known after the flush)
     uint32_t tick_id = 0;
     uint64_t ticks = 0;
     uint32_t n_alive = 0;
@@ -284,9 +292,10 @@ int ensure_ops(gwaoi_world *w, size_t n) {
     dfree(w->op_sp);
     dfree(w->op_x);
     dfree(w->op_z);
+    dfree(w->op_seq);
     int rc;
     if ((rc = dalloc(w, &w->op_slot, cap)) || (rc = dalloc(w, &w->op_sp, cap)) || (rc = dalloc(w, &w->op_x, cap)) ||
-        (rc = dalloc(w, &w->op_z, cap))) {
+        (rc = dalloc(w, &w->op_z, cap)) || (rc = dalloc(w, &w->op_seq, cap))) {
         w->op_cap = 0;
         return rc;
     }
@@ -309,7 +318,7 @@ int ensure_cells(gwaoi_world *w, DevFrame &f, size_t cells) {
     return GWAOI_OK;
 }
 
-void push_host_op(gwaoi_world *w, uint32_t slot, float x, float z, uint32_t sp) {
+void push_host_op(gwaoi_world *w, uint32_t slot, float x, float z, uint32_t sp, uint64_t seq) {
     if (w->runs.empty() || w->runs.back().device) {
         Run r{};
         r.device = false;
@@ -320,6 +329,7 @@ void push_host_op(gwaoi_world *w, uint32_t slot, float x, float z, uint32_t sp) 
     w->h_op_x.push_back(x);
     w->h_op_z.push_back(z);
     w->h_op_sp.push_back(sp);
+    w->h_op_seq.push_back(seq);
     w->runs.back().hend = w->h_op_slot.size();
     w->n_ops++;
 }
@@ -481,9 +491,8 @@ int run_tick(gwaoi_world *w) {
     hipStream_t st = w->stream;
     int rc;
     const uint32_t tick_id = ++w->tick_id;
-    const uint64_t seq_base = w->seq_next;
+    const uint64_t seq_base = w->seq_floor;  // every seq of this flush is >= seq_base > every earlier one
     const uint32_t n_ops = (uint32_t)w->n_ops;
-    w->seq_next += n_ops;
 
     DevFrame &P = w->fr[w->cur];       // previous flush
     DevFrame &Fn = w->fr[w->cur ^ 1];  // this flush
@@ -540,6 +549,7 @@ int run_tick(gwaoi_world *w) {
             HIP_TRY(hipMemcpyAsync(w->op_x + hat, w->h_op_x.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
             HIP_TRY(hipMemcpyAsync(w->op_z + hat, w->h_op_z.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
             HIP_TRY(hipMemcpyAsync(w->op_sp + hat, w->h_op_sp.data() + r.hbegin, k * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(w->op_seq + hat, w->h_op_seq.data() + r.hbegin, k * 8, hipMemcpyHostToDevice, st));
             hat += k;
         }
         for (int pass = 0; pass < 2; ++pass) {
@@ -549,19 +559,22 @@ int run_tick(gwaoi_world *w) {
                 const uint32_t *sl;
                 const float *xs, *zs;
                 const uint32_t *sps;
+                const unsigned long long *sq;
+                uint64_t seq0 = 0;
                 uint32_t k;
                 if (r.device) {
-                    sl = r.ds; xs = r.dx; zs = r.dz; sps = nullptr; k = (uint32_t)r.dn;
+                    sl = r.ds; xs = r.dx; zs = r.dz; sps = nullptr; sq = r.dseq; seq0 = r.seq0; k = (uint32_t)r.dn;
                 } else {
                     k = (uint32_t)(r.hend - r.hbegin);
                     sl = w->op_slot + hoff; xs = w->op_x + hoff; zs = w->op_z + hoff; sps = w->op_sp + hoff;
+                    sq = w->op_seq + hoff;
                     hoff += k;
                 }
                 if (pass == 0)
                     gw::launch_ops_claim(sl, k, j0, w->max_slots, w->sinfo, tick_id, w->sc, st);
                 else
-                    gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->sinfo, tick_id, n_total,
-                                         seq_base, w->srec, w->sss, w->sc, st);
+                    gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->sinfo, tick_id, n_total, sq, seq0,
+                                         seq_base, r.device && r.dseq, w->srec, w->sss, w->sc, st);
                 j0 += k;
             }
         }
@@ -652,13 +665,18 @@ int run_tick(gwaoi_world *w) {
     }
     for (uint32_t s : w->new_slots) w->appended[s] = 0;
     w->new_slots.clear();
-    std::memcpy(w->in_frame.data(), w->alive.data(), w->max_slots);
+    for (uint32_t s : w->touched) w->in_frame[s] = w->alive[s];
+    w->touched.clear();
     w->h_op_slot.clear();
     w->h_op_x.clear();
     w->h_op_z.clear();
     w->h_op_sp.clear();
+    w->h_op_seq.clear();
     w->runs.clear();
     w->n_ops = 0;
+    if (w->dev_seq_pending && r.seq_max >= w->seq_next) w->seq_next = r.seq_max + 1;
+    w->dev_seq_pending = false;
+    w->seq_floor = w->seq_next;
     w->cur ^= 1;
     w->ticks++;
     if (r.err & gw::ERR_COUNT_MISMATCH) {
@@ -668,6 +686,10 @@ int run_tick(gwaoi_world *w) {
     if (r.err & gw::ERR_NONFINITE) {
         w->last_error = "device batch held a non-finite coordinate (move dropped)";
         return GWAOI_ENONFINITE;
+    }
+    if (r.err & gw::ERR_SEQ) {
+        w->last_error = "device batch held an explicit seq below the flush's floor (op dropped)";
+        return GWAOI_EINVAL;
     }
     if (r.err & (gw::ERR_MOVE_DEAD | gw::ERR_BAD_SLOT)) {
         w->last_error = "device batch moved a slot that is not live (move dropped)";
@@ -712,7 +734,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->srec); dfree(w->sss); dfree(w->orec); dfree(w->cand);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
-    dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z);
+    dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
     dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
     dfree(w->nb_out); dfree(w->nb_count);
@@ -825,12 +847,29 @@ int gwaoi_space_destroy(gwaoi_world *w, uint32_t space) {
     return GWAOI_OK;
 }
 
-int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z) {
+namespace {
+
+// Explicit seqs must keep call order: >= the next implicit seq, and nothing
+// host-side may follow an explicit device batch inside one flush (its
+// largest seq is only known after the flush).
+int check_seq(gwaoi_world *w, const uint64_t *seq) {
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
+    if (seq && *seq < w->seq_next) return GWAOI_EINVAL;
+    return GWAOI_OK;
+}
+uint64_t take_seq(gwaoi_world *w, const uint64_t *seq) {
+    const uint64_t s = seq ? *seq : w->seq_next;
+    w->seq_next = s + 1;
+    return s;
+}
+
+int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, const uint64_t *seq) {
     if (!w) return GWAOI_EINVAL;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
     if (w->alive[slot]) return GWAOI_ESTATE;
     if (!finite2(x, z)) return GWAOI_ENONFINITE;
+    if (int rc = check_seq(w, seq)) return rc;
     w->alive[slot] = 1;
     w->space_of[slot] = space;
     w->n_alive++;
@@ -838,36 +877,57 @@ int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z)
     S.alive++;
     note_pending_bbox(S, x, z);
     mark_appended(w, slot);
-    push_host_op(w, slot, x, z, space);
+    w->touched.push_back(slot);
+    push_host_op(w, slot, x, z, space, take_seq(w, seq));
     return GWAOI_OK;
+}
+
+int moved_impl(gwaoi_world *w, uint32_t slot, float x, float z, const uint64_t *seq) {
+    if (!w) return GWAOI_EINVAL;
+    if (slot >= w->max_slots) return GWAOI_EBADSLOT;
+    if (!w->alive[slot]) return GWAOI_ESTATE;
+    if (!finite2(x, z)) return GWAOI_ENONFINITE;
+    if (int rc = check_seq(w, seq)) return rc;
+    note_pending_bbox(w->spaces[w->space_of[slot]], x, z);
+    push_host_op(w, slot, x, z, w->space_of[slot], take_seq(w, seq));
+    return GWAOI_OK;
+}
+
+}  // namespace
+
+int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z) {
+    return enter_impl(w, space, slot, x, z, nullptr);
+}
+
+int gwaoi_enter_seq(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, uint64_t seq) {
+    return enter_impl(w, space, slot, x, z, &seq);
 }
 
 int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
     if (!w) return GWAOI_EINVAL;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (!w->alive[slot]) return GWAOI_ESTATE;
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
     w->alive[slot] = 0;
     w->spaces[w->space_of[slot]].alive--;
     w->space_of[slot] = gw::SP_DEAD;
     w->n_alive--;
-    push_host_op(w, slot, 0.f, 0.f, gw::SP_DEAD);
+    w->touched.push_back(slot);
+    push_host_op(w, slot, 0.f, 0.f, gw::SP_DEAD, w->seq_next);  // a Leave's seq is never compared
     return GWAOI_OK;
 }
 
-int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z) {
-    if (!w) return GWAOI_EINVAL;
-    if (slot >= w->max_slots) return GWAOI_EBADSLOT;
-    if (!w->alive[slot]) return GWAOI_ESTATE;
-    if (!finite2(x, z)) return GWAOI_ENONFINITE;
-    note_pending_bbox(w->spaces[w->space_of[slot]], x, z);
-    push_host_op(w, slot, x, z, w->space_of[slot]);
-    return GWAOI_OK;
+int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z) { return moved_impl(w, slot, x, z, nullptr); }
+
+int gwaoi_moved_seq(gwaoi_world *w, uint32_t slot, float x, float z, uint64_t seq) {
+    return moved_impl(w, slot, x, z, &seq);
 }
 
 int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, const float *x, const float *z,
                       size_t n) {
     if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
     // validate the whole batch first (duplicates inside the batch are Enter-twice)
     std::vector<uint32_t> seen;
     seen.reserve(n);
@@ -885,6 +945,7 @@ int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, con
 
 int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
     if (!w || (n && !slots)) return GWAOI_EINVAL;
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
     std::vector<uint32_t> seen(slots, slots + n);
     for (size_t i = 0; i < n; ++i) {
         if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
@@ -898,6 +959,7 @@ int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
 
 int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
     if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
     for (size_t i = 0; i < n; ++i) {
         if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
         if (!w->alive[slots[i]]) return GWAOI_ESTATE;
@@ -912,14 +974,37 @@ int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const floa
     if (!w || (n && (!d_slots || !d_x || !d_z))) return GWAOI_EINVAL;
     if (!n) return GWAOI_OK;
     if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
     Run r{};
     r.device = true;
     r.ds = d_slots;
     r.dx = d_x;
     r.dz = d_z;
+    r.dseq = nullptr;
+    r.seq0 = w->seq_next;
     r.dn = n;
     w->runs.push_back(r);
     w->n_ops += n;
+    w->seq_next += n;
+    return GWAOI_OK;
+}
+
+int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
+                                 const uint64_t *d_seq, size_t n) {
+    if (!w || (n && (!d_slots || !d_x || !d_z || !d_seq))) return GWAOI_EINVAL;
+    if (!n) return GWAOI_OK;
+    if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
+    Run r{};
+    r.device = true;
+    r.ds = d_slots;
+    r.dx = d_x;
+    r.dz = d_z;
+    r.dseq = reinterpret_cast<const unsigned long long *>(d_seq);
+    r.seq0 = 0;
+    r.dn = n;
+    w->runs.push_back(r);
+    w->n_ops += n;
+    w->dev_seq_pending = true;
     return GWAOI_OK;
 }
 
@@ -1001,12 +1086,14 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
 int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
     if (!w || !info) return GWAOI_EINVAL;
     info->ticks = w->ticks;
-    info->next_seq = w->seq_next + w->n_ops;
+    info->next_seq = w->seq_next;
     info->live = w->fr[w->cur].n;
     info->spaces = w->n_spaces_live;
     info->total_cells = w->fr[w->cur].total_cells;
     info->pending_ops = (uint32_t)w->n_ops;
     info->event_capacity = w->ev_cap;
+    info->max_slots = w->max_slots;
+    info->max_spaces = w->max_spaces;
     return GWAOI_OK;
 }
 

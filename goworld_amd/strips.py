@@ -1,0 +1,236 @@
+"""Strip tiling of one oversized space over several GPUs (BASELINE config 5,
+SURVEY.md §8e "Partitioning (config 5)"; C ABI in include/gwaoi_strips.h).
+
+GoWorld gives every Space one AOI manager (engine/entity/Space.go:33,105).
+A space too big for one GPU is cut into x-strips: rank r owns the entities
+with x in [edges[r-1], edges[r]) and mirrors, as ghosts, the ones within the
+halo H of its strip.  Each tick:
+
+1. ``StripShard.route(ops)``: the AOIManager calls of this tick for the
+   entities the rank owned before it (Moved / Leave) or that enter the space
+   inside its strip (Enter) become halo records per destination rank, plus
+   teleport records (HIP kernels, ``k_route``).
+2. ``exchange``: one ``all_to_all_single`` of the records over RCCL (xGMI),
+   after an ``all_gather`` of the per-destination counts; teleport records
+   are all-gathered.  This is the path's one real data exchange.
+3. ``StripShard.finish(recv, tele)``: the records become ops of the rank's
+   gwaoi world (explicit global seqs), the world flushes, and only the events
+   this strip owns are kept (enter: owner after the tick; leave: owner
+   before it).  The union over ranks is the whole space's net diff.
+
+``tile_tick`` runs the three steps for one rank of a ``torch.distributed``
+job; ``local_tick`` runs several strips in one process (loopback exchange,
+used by the single-GPU parity tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from ._lib import Events, GwaoiError, StripsConfig, World, load, _p
+
+HALO_MOVE, HALO_ENTER, HALO_LEAVE = 0, 1, 2
+HALO_DTYPE = np.dtype([("slot", "<u4"), ("x", "<f4"), ("z", "<f4"), ("kind", "<u4"), ("seq", "<u8")])
+TELE_DTYPE = np.dtype([("slot", "<u4"), ("flags", "<u4"), ("px", "<f4"), ("pz", "<f4"), ("pseq", "<u8"),
+                       ("x", "<f4"), ("z", "<f4"), ("seq", "<u8")])
+HALO_WORDS = HALO_DTYPE.itemsize // 4  # 6 int32 per record (torch transport dtype)
+TELE_WORDS = TELE_DTYPE.itemsize // 4  # 10
+
+
+def default_teleport(D: float) -> float:
+    return float(np.float32(D) / np.float32(8.0))
+
+
+def halo_width(D: float, teleport: float = 0.0) -> float:
+    """H = 2D + teleport + 1 (include/gwaoi_strips.h)."""
+    t = teleport if teleport > 0 else default_teleport(D)
+    return float(np.float32(2.0 * float(np.float32(D)) + float(np.float32(t)) + 1.0))
+
+
+def even_edges(n_strips: int, lo: float, hi: float) -> np.ndarray:
+    """n_strips-1 interior x edges cutting [lo, hi) into equal strips."""
+    return np.linspace(lo, hi, n_strips + 1)[1:-1].astype(np.float32)
+
+
+def balanced_edges(x: np.ndarray, n_strips: int) -> np.ndarray:
+    """Interior edges at the entity-count quantiles of x (equal owned counts)."""
+    if n_strips <= 1:
+        return np.empty(0, np.float32)
+    q = np.quantile(np.asarray(x, np.float64), np.arange(1, n_strips) / n_strips)
+    e = q.astype(np.float32)
+    for i in range(1, e.size):  # strictly increasing
+        if e[i] <= e[i - 1]:
+            e[i] = np.nextafter(e[i - 1], np.float32(np.inf))
+    return e
+
+
+def owner_of(x: np.ndarray, edges: np.ndarray) -> np.ndarray:
+    """Strip owning each x (same float32 compares as the device strip_of)."""
+    return np.searchsorted(np.asarray(edges, np.float32), np.asarray(x, np.float32), side="right").astype(np.int64)
+
+
+def make_ops(slots, x, z, seq, kind=HALO_MOVE) -> np.ndarray:
+    """Structured op array (HALO_DTYPE) of one tick's calls."""
+    slots = np.asarray(slots, np.uint32)
+    a = np.empty(slots.size, HALO_DTYPE)
+    a["slot"] = slots
+    a["x"] = np.asarray(x, np.float32) if x is not None else 0.0
+    a["z"] = np.asarray(z, np.float32) if z is not None else 0.0
+    a["kind"] = kind
+    a["seq"] = np.asarray(seq, np.uint64)
+    return a
+
+
+def as_words(rec: np.ndarray, words: int):
+    """Structured records -> torch int32 (n, words) view (CPU tensor)."""
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(rec).view(np.int32).reshape(-1, words))
+
+
+class StripShard:
+    """One strip: a gwaoi world holding the strip's owned entities + ghosts,
+    and the strip layer (libgwaoi, include/gwaoi_strips.h) on top of it."""
+
+    def __init__(self, max_slots: int, D: float, edges: Sequence[float], rank: int, teleport: float = 0.0,
+                 device: int = 0, event_capacity: int = 0, cells_per_dist: float = 0.0):
+        import torch
+        self._L = load()
+        self.torch = torch
+        self.device = device
+        self.dev = torch.device(f"cuda:{device}")
+        self.edges = np.ascontiguousarray(edges, np.float32)
+        self.n_strips = self.edges.size + 1
+        self.rank = rank
+        self.D = np.float32(D)
+        self.world = World(max_slots, 1, device=device, event_capacity=event_capacity,
+                           cells_per_dist=cells_per_dist)
+        self.space = self.world.space_create(D)
+        cfg = StripsConfig(self.n_strips, rank, _p(self.edges) if self.edges.size else None, C.c_float(D),
+                           C.c_float(teleport))
+        h = C.c_void_p()
+        self._check(self._L.gwaoi_strips_create(self.world._w, self.space, C.byref(cfg), C.byref(h)), strips=False)
+        self._s = h
+        hf = C.c_float()
+        self._check(self._L.gwaoi_strips_halo(self._s, C.byref(hf)))
+        self.halo = hf.value
+
+    def close(self):
+        if getattr(self, "_s", None):
+            self._L.gwaoi_strips_destroy(self._s)
+            self._s = None
+        if getattr(self, "world", None) is not None:
+            self.world.close()
+            self.world = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc, strips=True):
+        if rc != 0:
+            msg = self._L.gwaoi_strips_last_error(self._s).decode() if strips and getattr(self, "_s", None) else ""
+            raise GwaoiError(rc, self._L.gwaoi_strerror(rc).decode() + (f" ({msg})" if msg else ""))
+        return rc
+
+    # ---- step 1: route this tick's owned ops
+    def route(self, ops):
+        """ops: device int32 (n, 6) tensor of HALO_DTYPE records.  Returns
+        (send (m,6) int32 grouped by destination rank, counts[n_strips] int64,
+        tele (k,10) int32)."""
+        torch = self.torch
+        n = int(ops.shape[0])
+        counts = (C.c_uint64 * (self.n_strips + 1))()
+        self._check(self._L.gwaoi_strips_route(self._s, C.c_void_p(ops.data_ptr() if n else 0), n, counts))
+        c = np.array(counts[:], np.int64)
+        send = torch.empty((int(c[:-1].sum()), HALO_WORDS), dtype=torch.int32, device=self.dev)
+        tele = torch.empty((int(c[-1]), TELE_WORDS), dtype=torch.int32, device=self.dev)
+        self._check(self._L.gwaoi_strips_route_scatter(self._s, C.c_void_p(send.data_ptr() if send.numel() else 0),
+                                                       C.c_void_p(tele.data_ptr() if tele.numel() else 0)))
+        return send, c[:-1], tele
+
+    # ---- step 3: apply the exchanged records, flush, keep this strip's events
+    def finish(self, recv, tele) -> Tuple[int, int]:
+        ne, nl = C.c_uint64(), C.c_uint64()
+        nr, nt = int(recv.shape[0]), int(tele.shape[0])
+        self._check(self._L.gwaoi_strips_tick(self._s, C.c_void_p(recv.data_ptr() if nr else 0), nr,
+                                              C.c_void_p(tele.data_ptr() if nt else 0), nt, C.byref(ne),
+                                              C.byref(nl)))
+        return ne.value, nl.value
+
+    def events(self):
+        """This strip's events of the last tick as (n,2) uint32 arrays [a, b]."""
+        ev = Events()
+        self._check(self._L.gwaoi_strips_events(self._s, C.byref(ev)))
+        ne, nl = ev.n_enter, ev.n_leave
+        ent = np.ctypeslib.as_array(ev.enter, shape=(2 * ne,)).reshape(ne, 2).copy() if ne else np.empty((0, 2), np.uint32)
+        lev = np.ctypeslib.as_array(ev.leave, shape=(2 * nl,)).reshape(nl, 2).copy() if nl else np.empty((0, 2), np.uint32)
+        return ent, lev
+
+    def events_device(self):
+        e, l = C.c_void_p(), C.c_void_p()
+        self._check(self._L.gwaoi_strips_events_device(self._s, C.byref(e), C.byref(l)))
+        return e.value, l.value
+
+
+# ---------------------------------------------------------------- exchange ---
+
+def exchange(dist, send, counts, tele, group=None):
+    """The halo exchange of one tick over torch.distributed (RCCL on GPU
+    tensors, gloo on CPU ones): counts all-gathered, records all-to-all'd,
+    teleport records all-gathered.  Returns (recv records, all teleports)."""
+    import torch
+    S = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = send.device
+    mine = torch.tensor(list(np.asarray(counts, np.int64)) + [int(tele.shape[0])], dtype=torch.int64, device=dev)
+    rows = [torch.empty_like(mine) for _ in range(S)]
+    dist.all_gather(rows, mine, group=group)
+    M = torch.stack(rows).cpu().numpy()  # M[src, dst]; column S = teleports of src
+    in_splits = [int(v) for v in M[rank, :S]]
+    out_splits = [int(v) for v in M[:, rank]]
+    recv = torch.empty((sum(out_splits), send.shape[1]), dtype=send.dtype, device=dev)
+    dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
+    T = M[:, S]
+    if T.sum() == 0:
+        return recv, tele[:0]
+    pad = int(T.max())
+    buf = torch.zeros((pad, tele.shape[1]), dtype=tele.dtype, device=dev)
+    buf[:tele.shape[0]] = tele
+    parts = [torch.empty_like(buf) for _ in range(S)]
+    dist.all_gather(parts, buf, group=group)
+    return recv, torch.cat([parts[r][:int(T[r])] for r in range(S)])
+
+
+def exchange_local(outs: List[Tuple]):
+    """Loopback exchange for several strips in one process: outs[r] =
+    (send, counts, tele) of strip r.  Returns [(recv, tele_all)] per strip,
+    in the same source order as the all_to_all (source rank order)."""
+    import torch
+    S = len(outs)
+    starts = []
+    for send, counts, _ in outs:
+        c = np.concatenate([[0], np.cumsum(counts)])
+        starts.append(c)
+    tele_all = torch.cat([o[2] for o in outs]) if S else None
+    res = []
+    for q in range(S):
+        parts = [outs[r][0][int(starts[r][q]):int(starts[r][q + 1])] for r in range(S)]
+        res.append((torch.cat(parts), tele_all))
+    return res
+
+
+def tile_tick(shard: StripShard, dist, ops, group=None) -> Tuple[int, int]:
+    """One tick of this rank's strip in a torch.distributed job."""
+    send, counts, tele = shard.route(ops)
+    recv, tele_all = exchange(dist, send, counts, tele, group=group)
+    shard.torch.cuda.current_stream(shard.dev).synchronize()
+    return shard.finish(recv, tele_all)
+
+
+def local_tick(shards: Sequence[StripShard], ops_per_strip) -> List[Tuple[int, int]]:
+    """One tick of several strips in one process (loopback exchange)."""
+    outs = [sh.route(o) for sh, o in zip(shards, ops_per_strip)]
+    ex = exchange_local(outs)
+    shards[0].torch.cuda.synchronize()
+    return [sh.finish(r, t) for sh, (r, t) in zip(shards, ex)]

@@ -94,6 +94,8 @@ typedef struct {
     uint32_t total_cells;  /* grid cells of the last flush            */
     uint32_t pending_ops;  /* calls queued since the last flush       */
     uint64_t event_capacity;
+    uint32_t max_slots;    /* creation config                         */
+    uint32_t max_spaces;
 } gwaoi_info;
 
 typedef struct {
@@ -130,6 +132,24 @@ int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, con
  * device and reported by the next tick (the offending moves are dropped). */
 int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const float *d_x,
                              const float *d_z, size_t n);
+
+/* ---- explicit sequence numbers ---------------------------------------------
+ * The relation depends on call order only through each entity's seq (the
+ * one of A,B whose Enter/Moved came last owns the window test).  These forms
+ * take the seq from the caller instead of the world's counter: for a world
+ * that is one strip of a larger space fed by several hosts (gwaoi_strips.h),
+ * and to restore frozen AOI state with its original order (EntityManager.go
+ * freeze/restore, :554-656).  Rules: an explicit seq must be >= the next
+ * seq the world would hand out (gwaoi_info.next_seq; host calls check it and
+ * return GWAOI_EINVAL) and the caller keeps them unique; afterwards the
+ * world's counter continues above it.  Device seqs are checked on the device
+ * against the flush's floor (violations: the op is dropped, the tick returns
+ * GWAOI_EINVAL).  After a device explicit batch, no other call may be queued
+ * before the next flush (GWAOI_ESTATE). */
+int gwaoi_enter_seq(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, uint64_t seq);
+int gwaoi_moved_seq(gwaoi_world *w, uint32_t slot, float x, float z, uint64_t seq);
+int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
+                                 const uint64_t *d_seq, size_t n);
 
 /* ---- flush ------------------------------------------------------------------ */
 /* Run the tick and copy its events to host memory. */

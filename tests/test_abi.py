@@ -11,8 +11,8 @@ from goworld_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "gwaoi.h")).read()
+def header_functions(name="gwaoi.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(gwaoi_[a-z_0-9]+)\s*\(", src)))
 
@@ -26,10 +26,11 @@ def lib():
 
 def test_header_lists_match_binding():
     assert header_functions() == sorted(_lib.EXPORTS)
+    assert header_functions("gwaoi_strips.h") == sorted(_lib.STRIP_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol(lib):
-    for name in header_functions():
+    for name in header_functions() + header_functions("gwaoi_strips.h"):
         assert hasattr(lib, name), name
         assert C.cast(getattr(lib, name), C.c_void_p).value
 

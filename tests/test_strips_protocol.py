@@ -1,0 +1,116 @@
+"""Strip tiling of one space (config 5) on CPU: the protocol and the exchange.
+
+The strips' union of events must equal, tick by tick, the net events of one
+unsplit sequential go-aoi manager (oracle/xzlist.c) fed the same global call
+stream -- including teleports across strips, teleporting pairs that stay
+neighbours, Leaves, Enters and entities parked on strip edges and halo
+bounds.  Each strip is the numpy model of gwaoi_strips.hip (tests/strip_model.py)
+over its own sequential manager; the world_size-2 case runs the real
+torch.distributed exchange (goworld_amd.strips.exchange) over gloo.
+Bit-exact sets, no tolerance.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from goworld_amd.strips import as_words, exchange, exchange_local, HALO_WORDS, owner_of
+from strip_model import ModelShard
+from strip_scenario import D, Scenario, split_by_owner
+
+
+def reference_ticks(oracle, sc: Scenario, ticks: int):
+    m = oracle.XZList(D, sc.max_slots)
+    out = []
+    for _ in range(ticks):
+        kind, sl, nx, nz, seq, px = sc.tick()
+        m.apply(kind.astype(np.uint8), sl.astype(np.int32), nx, nz)
+        out.append(oracle.net_events(*m.take_events()))
+    return out
+
+
+def run_strips_local(oracle, sc: Scenario, ticks: int):
+    S = sc.edges.size + 1
+    shards = [ModelShard(sc.max_slots, D, sc.edges, r, oracle) for r in range(S)]
+    out = []
+    for _ in range(ticks):
+        per = split_by_owner(*sc.tick(), sc.edges)
+        routed = [sh.route(as_words(o, HALO_WORDS)) for sh, o in zip(shards, per)]
+        for sh, (recv, tele) in zip(shards, exchange_local(routed)):
+            sh.finish(recv, tele)
+        out.append(tuple(np.concatenate([sh.last[i] for sh in shards]) for i in (0, 1)))
+    return out
+
+
+def assert_same(got, ref):
+    for t, ((ge, gl), (re_, rl)) in enumerate(zip(got, ref)):
+        assert np.unique(ge).size == ge.size and np.unique(gl).size == gl.size, f"tick {t}: duplicate events"
+        assert np.array_equal(np.sort(ge), re_), f"tick {t}: enter events differ"
+        assert np.array_equal(np.sort(gl), rl), f"tick {t}: leave events differ"
+
+
+@pytest.mark.parametrize("n_strips,seed", [(2, 11), (4, 7)])
+def test_strip_protocol_loopback_matches_one_manager(oracle_mod, n_strips, seed):
+    ticks = 5
+    ref = reference_ticks(oracle_mod, Scenario(n0=4000, n_strips=n_strips, seed=seed), ticks)
+    got = run_strips_local(oracle_mod, Scenario(n0=4000, n_strips=n_strips, seed=seed), ticks)
+    assert_same(got, ref)
+    assert sum(e.size for e, _ in ref[1:]) > 0 and sum(l.size for _, l in ref[1:]) > 0
+
+
+def test_scenario_exercises_strip_hazards():
+    sc = Scenario(n0=4000, n_strips=4, seed=7)
+    sc.tick()
+    kind, sl, nx, nz, seq, px = sc.tick()
+    own_b = owner_of(np.nan_to_num(px), sc.edges)
+    own_a = owner_of(nx, sc.edges)
+    moved = kind == 0
+    assert np.any(moved & (own_a != own_b))  # ownership changes (migration)
+    assert np.sum(moved & (np.abs(nx - px) > 12.5)) >= 20  # teleporters
+    assert np.any(kind == 1) and np.any(kind == 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, seed, ticks, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from oracle import oracle
+    sc = Scenario(n0=3000, n_strips=ws, seed=seed)
+    sh = ModelShard(sc.max_slots, D, sc.edges, rank, oracle)
+    res = []
+    for _ in range(ticks):
+        ops = split_by_owner(*sc.tick(), sc.edges)[rank]
+        send, counts, tele = sh.route(as_words(ops, HALO_WORDS))
+        recv, tele_all = exchange(dist, send, counts, tele)
+        sh.finish(recv, tele_all)
+        res.append((sh.last[0].tolist(), sh.last[1].tolist()))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_strip_exchange(oracle_mod):
+    ws, seed, ticks = 2, 5, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, seed, ticks, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    parts = dict(q.get(timeout=300) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = [tuple(np.array(parts[0][t][i] + parts[1][t][i], np.uint64) for i in (0, 1)) for t in range(ticks)]
+    ref = reference_ticks(oracle_mod, Scenario(n0=3000, n_strips=ws, seed=seed), ticks)
+    assert_same(got, ref)
