@@ -40,7 +40,8 @@ WORKLOAD_DESC = {
     "cfg2": "one space, 100k entities uniform, step U(-1,1)",
     "cfg3": "one space, 1M entities clustered crowd hotspots (256 x sigma 250 + uniform), step U(-1,1)",
     "cfg4": "8192 spaces x 2k entities (per rank: spaces / n_gpus), step U(-1,1)",
-    "cfg5": "single 16M-entity world (untiled, one GPU), step U(-1,1)",
+    "cfg5": "single 2^24-entity world uniform (L=sqrt(N*1250)), step U(-1,1), tiled into one x-strip per rank "
+            "with halo exchange over RCCL",
 }
 
 
@@ -112,6 +113,113 @@ def cpu_baseline(args, wl_factory, target_s: float):
     }
 
 
+def run_strips(args, ws, rank, local, dist):
+    """Config 5: one 2^24-entity space cut into one x-strip per rank; every
+    tick routes the owned moves, exchanges halo records over RCCL
+    (all_gather of counts + all_to_all of records) and flushes each strip's
+    world (goworld_amd/strips.py).  Inputs are generated on the GPU before
+    timing (DeviceUniformWorkload); value = all N moves per tick / max time."""
+    import torch
+    from goworld_amd.shard import reduce_over_ranks
+    from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local
+    from goworld_amd.workload import DeviceUniformWorkload
+
+    dev = torch.device(f"cuda:{local}")
+    n = args.n or (1 << 24)
+    t_setup = time.perf_counter()
+    wl = DeviceUniformWorkload(n, 0x5EED0005, dev)
+    edges = even_edges(ws, -wl.L / 2, wl.L / 2)
+    edges_t = torch.from_numpy(edges).to(dev)
+    ticks = args.warmup + args.steps
+    init_ops = wl.initial_ops(edges_t, rank)
+    ops = [wl.tick_ops(edges_t, rank) for _ in range(ticks)]
+    del wl
+    torch.cuda.synchronize()
+    sh = StripShard(n, float(D_CFG5), edges, rank, device=local, cells_per_dist=args.cells_per_dist)
+
+    def one(o, phases=None):
+        a = time.perf_counter()
+        send, counts, tele = sh.route(o)
+        b = time.perf_counter()
+        if dist is not None:
+            recv, tele_all = exchange(dist, send, counts, tele, via_cpu=args.dist_backend == "gloo")
+        else:
+            recv, tele_all = exchange_local([(send, counts, tele)])[0]
+        torch.cuda.current_stream(dev).synchronize()
+        c = time.perf_counter()
+        r = sh.finish(recv, tele_all)
+        if phases is not None:
+            phases[0] += b - a
+            phases[1] += c - b
+            phases[2] += time.perf_counter() - c
+        return r, int(counts.sum() - counts[rank]), int(recv.shape[0])
+
+    (ne0, nl0), _, _ = one(init_ops)
+    setup_s = time.perf_counter() - t_setup
+    for t in range(args.warmup):
+        one(ops[t])
+    w = sh.world
+    w.set_stage_timing([] if args.no_timing else ["combined"])
+    w.reset_stage_times()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lat, events, sent, recvd = [], 0, 0, 0
+    phases = [0.0, 0.0, 0.0]
+    t0 = time.perf_counter()
+    for t in range(args.warmup, ticks):
+        a = time.perf_counter()
+        (ne, nl), ns, nr = one(ops[t], phases)
+        lat.append(time.perf_counter() - a)
+        events += ne + nl
+        sent += ns
+        recvd += nr
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timed = w.stage_times() if not args.no_timing else {}
+    info = w.info()
+    el_max, (moves_all, events_all, halo_all, live_all) = reduce_over_ranks(
+        dist, elapsed, [n * args.steps / ws, events, sent, info["live"]],
+        "cpu" if args.dist_backend == "gloo" else dev)
+    if rank == 0:
+        lat_ms = np.array(lat) * 1e3
+        tm = {k: v[0] / max(v[1], 1) for k, v in timed.items() if v[1]}
+        roofline = None
+        if "combined" in tm:
+            alg = combined_pass_bytes(info["live"], info["total_cells"], events / max(args.steps, 1))
+            ach = alg / (tm["combined"] * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "kernel": "k_combined", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                        "alg_bytes_per_launch": alg, "avg_launch_ms": round(tm["combined"], 4),
+                        "note": "rank 0's strip world"}
+        out = {
+            "metric": METRIC, "value": moves_all / el_max, "unit": "entity-moves/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el_max / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (torch Philox on the GPU, generated before timing, resident in HBM)",
+            "config": {"workload": f"cfg5: {WORKLOAD_DESC['cfg5']}", "entities": n, "strips": ws,
+                       "aoi_distance": float(D_CFG5), "halo": sh.halo,
+                       "parallelism": f"one x-strip per rank x{ws}, halo records all_to_all over RCCL"},
+            "events_per_s": events_all / el_max,
+            "p50_tick_ms": float(np.percentile(lat_ms, 50)), "p99_tick_ms": float(np.percentile(lat_ms, 99)),
+            "events_per_tick": events_all / max(args.steps, 1), "initial_enter_events_rank0": ne0,
+            "halo_records_per_tick": halo_all / max(args.steps, 1),
+            "halo_note": "records sent to other ranks (24 B each), all ranks",
+            "strip_world_entities_sum": live_all, "setup_s": round(setup_s, 2),
+            "rank0_phase_ms_per_tick": {"route": round(phases[0] / args.steps * 1e3, 4),
+                                        "exchange": round(phases[1] / args.steps * 1e3, 4),
+                                        "tick_filter": round(phases[2] / args.steps * 1e3, 4)},
+            "roofline": roofline, "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    sh.close()
+
+
+D_CFG5 = np.float32(100.0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,6 +230,8 @@ def main():
     ap.add_argument("--spaces", type=int, default=None, help="cfg4: total spaces (default 8192)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: exchange through host memory (multi-rank rehearsal on one GPU)")
     ap.add_argument("--no-timing", action="store_true", help="no HIP events at all (no roofline / breakdown)")
     ap.add_argument("--breakdown-steps", type=int, default=10,
                     help="extra ticks after the timed region with every stage timed by HIP events")
@@ -136,8 +246,14 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
     device = local
+    red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{device}"
+    if args.workload == "cfg5":
+        run_strips(args, ws, rank, local, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from goworld_amd import World
     from goworld_amd.shard import assign_spaces, reduce_over_ranks
@@ -248,12 +364,12 @@ def main():
             dist.barrier()
         h_el = time.perf_counter() - h0
         h_el, (h_moves, h_evs) = reduce_over_ranks(dist, h_el, [sum(b[0].size for b in host_batches), h_ev],
-                                                   f"cuda:{device}")
+                                                   red_dev)
         host_io = {"value": h_moves / h_el, "unit": "entity-moves/s", "ms_per_step": h_el / hio * 1e3,
                    "events_per_s": h_evs / h_el, "steps": hio,
                    "note": "moves from host memory (H2D) + events copied to host arrays (D2H) per tick; "
                            "not the headline value"}
-    elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], f"cuda:{device}")
+    elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], red_dev)
 
     if rank == 0:
         lat_ms = np.array(lat) * 1e3

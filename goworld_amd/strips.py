@@ -175,11 +175,18 @@ class StripShard:
 
 # ---------------------------------------------------------------- exchange ---
 
-def exchange(dist, send, counts, tele, group=None):
+def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     """The halo exchange of one tick over torch.distributed (RCCL on GPU
     tensors, gloo on CPU ones): counts all-gathered, records all-to-all'd,
-    teleport records all-gathered.  Returns (recv records, all teleports)."""
+    teleport records all-gathered.  Returns (recv records, all teleports).
+    via_cpu: GPU tensors go through host memory (gloo rehearsal of several
+    ranks sharing one GPU; RCCL allows one rank per device)."""
     import torch
+    if via_cpu and send.is_cuda:
+        dev = send.device
+        torch.cuda.current_stream(dev).synchronize()
+        r, t = exchange(dist, send.cpu(), counts, tele.cpu(), group)
+        return r.to(dev), t.to(dev)
     S = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = send.device

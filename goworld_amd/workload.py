@@ -175,3 +175,78 @@ def make_workload(cfg: str, n: int | None = None, seed: int | None = None,
         sp = (np.arange(n, dtype=np.int64) // per_space).astype(np.uint32)
         return Workload(cfg, n, D, x, z, sp, n_spaces, seed, L)
     raise ValueError(f"unknown workload {cfg}")
+
+
+class DeviceUniformWorkload:
+    """Config 5 generated on the GPU with torch (bench only): N entities
+    uniform in [-L/2, L/2)^2 with L = sqrt(N*1250), every tick every entity
+    moves by U(-1,1) per axis in float32, in a random global call order.
+
+    Every rank of a strip-tiled run replays the same global simulation from
+    the same seed (Philox streams are identical on every device) and keeps
+    only the ops of the entities its strip owned before the tick, as
+    int32 (n, 6) halo records (goworld_amd.strips.HALO_DTYPE).  The numpy
+    generators above feed the parity tests; this one only has to produce a
+    workload of config 5's shape fast enough to pre-generate 16.8M moves per
+    tick before the timed region."""
+
+    def __init__(self, n: int, seed: int, device):
+        import torch
+        self.torch = torch
+        self.n = n
+        self.dev = torch.device(device)
+        self.L = math.sqrt(n * 1250.0)
+        self.D = D_DEFAULT
+        self.seed = seed
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(seed)
+        self.x = ((torch.rand(n, generator=g, device=self.dev, dtype=torch.float64) * self.L - self.L / 2)
+                  .to(torch.float32))
+        self.z = ((torch.rand(n, generator=g, device=self.dev, dtype=torch.float64) * self.L - self.L / 2)
+                  .to(torch.float32))
+        self.next_seq = 1
+        self.t = 0
+
+    def _records(self, slots, x, z, kind, seq):
+        torch = self.torch
+        r = torch.empty((slots.numel(), 6), dtype=torch.int32, device=self.dev)
+        r[:, 0] = slots.to(torch.int32)
+        r[:, 1] = x.view(torch.int32)
+        r[:, 2] = z.view(torch.int32)
+        r[:, 3] = kind
+        r[:, 4] = (seq & 0xFFFFFFFF).to(torch.int64).to(torch.int32)
+        r[:, 5] = (seq >> 32).to(torch.int32)
+        return r
+
+    def owner(self, x, edges_t):
+        return self.torch.bucketize(x, edges_t, right=True)
+
+    def initial_ops(self, edges_t, rank: int):
+        """Enter ops (kind 1) of the entities whose start position is in strip `rank`; seq = 1 + slot."""
+        torch = self.torch
+        own = self.owner(self.x, edges_t) == rank
+        slots = torch.nonzero(own).flatten()
+        seq = 1 + slots.to(torch.int64)
+        self.next_seq = max(self.next_seq, self.n + 1)
+        return self._records(slots, self.x[slots], self.z[slots], 1, seq)
+
+    def tick_ops(self, edges_t, rank: int):
+        """Moved ops of tick t for the entities strip `rank` owns before it; advances the world."""
+        torch = self.torch
+        g = torch.Generator(device=self.dev)
+        g.manual_seed((self.seed * 1000003 + self.t) & 0x7FFFFFFFFFFFFFFF)
+        sx = (2 * torch.rand(self.n, generator=g, device=self.dev, dtype=torch.float64) - 1).to(torch.float32)
+        sz = (2 * torch.rand(self.n, generator=g, device=self.dev, dtype=torch.float64) - 1).to(torch.float32)
+        order = torch.randperm(self.n, generator=g, device=self.dev)
+        pos = torch.empty_like(order)
+        pos[order] = torch.arange(self.n, device=self.dev)
+        own = self.owner(self.x, edges_t) == rank
+        nx = self.x + sx
+        nz = self.z + sz
+        slots = torch.nonzero(own).flatten()
+        seq = self.next_seq + pos[slots]
+        rec = self._records(slots, nx[slots], nz[slots], 0, seq)
+        self.x, self.z = nx, nz
+        self.next_seq += self.n
+        self.t += 1
+        return rec
