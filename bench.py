@@ -121,7 +121,7 @@ def run_strips(args, ws, rank, local, dist):
     timing (DeviceUniformWorkload); value = all N moves per tick / max time."""
     import torch
     from goworld_amd.shard import reduce_over_ranks
-    from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local
+    from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local, local_slice
     from goworld_amd.workload import DeviceUniformWorkload
 
     dev = torch.device(f"cuda:{local}")
@@ -147,7 +147,7 @@ def run_strips(args, ws, rank, local, dist):
             recv, tele_all = exchange_local([(send, counts, tele)])[0]
         torch.cuda.current_stream(dev).synchronize()
         c = time.perf_counter()
-        r = sh.finish(recv, tele_all)
+        r = sh.finish(local_slice(send, counts, rank), recv, tele_all)
         if phases is not None:
             phases[0] += b - a
             phases[1] += c - b
@@ -226,7 +226,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOAD_DESC))
-    ap.add_argument("--n", type=int, default=None, help="override entity count (cfg2/3/5)")
+    ap.add_argument("--entities", dest="n", type=int, default=None, help="override entity count (cfg2/3/5)")
     ap.add_argument("--spaces", type=int, default=None, help="cfg4: total spaces (default 8192)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -245,6 +245,8 @@ def main():
     if ws > 1:
         import torch
         import torch.distributed as dist
+        if args.dist_backend == "gloo":  # rehearsal: several ranks may share a GPU
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend)
     device = local

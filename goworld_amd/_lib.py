@@ -124,7 +124,7 @@ def load():
         "gwaoi_strips_halo": ([vp, P(f)], C.c_int),
         "gwaoi_strips_route": ([vp, vp, sz, P(u64)], C.c_int),
         "gwaoi_strips_route_scatter": ([vp, vp, vp], C.c_int),
-        "gwaoi_strips_tick": ([vp, vp, sz, vp, sz, P(u64), P(u64)], C.c_int),
+        "gwaoi_strips_tick": ([vp, vp, sz, vp, sz, vp, sz, P(u64), P(u64)], C.c_int),
         "gwaoi_strips_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_strips_events": ([vp, P(Events)], C.c_int),
         "gwaoi_strips_last_error": ([vp], C.c_char_p),

@@ -196,7 +196,8 @@ __global__ void __launch_bounds__(BT) k_route(int phase, const gwaoi_halo_rec *_
 }
 
 // ---- receiver side: classes 0 = world device moves, 1 = host enters, 2 = host leaves
-__global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__restrict__ rv, uint32_t n, Rec16 *cur,
+__global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__restrict__ lv, uint32_t n_local,
+                                             const gwaoi_halo_rec *__restrict__ rv, uint32_t n, Rec16 *cur,
                                              Rec16 *prv, uint32_t *ptick, uint32_t tick, uint32_t max_slots,
                                              uint32_t *counts, const uint32_t *__restrict__ offs, uint32_t nb,
                                              uint32_t *err, uint32_t *m_slot, float *m_x, float *m_z,
@@ -204,8 +205,8 @@ __global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__
     const uint32_t i = blockIdx.x * BT + threadIdx.x;
     unsigned long long m = 0;
     gwaoi_halo_rec r{};
-    if (i < n) {
-        r = rv[i];
+    if (i < n) {  // this rank's own records first, then the received ones
+        r = i < n_local ? lv[i] : rv[i - n_local];
         uint32_t e = 0;
         if (r.slot >= max_slots) {
             e = SE_BADSLOT;
@@ -552,21 +553,24 @@ int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_te
     return GWAOI_OK;
 }
 
-int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_recv, size_t n_recv, const gwaoi_tele_rec *d_tele,
-                      size_t n_tele, uint64_t *n_enter, uint64_t *n_leave) {
-    if (!s || (n_recv && !d_recv) || (n_tele && !d_tele) || n_recv > 0x7FFFFFFFu || n_tele > 0x7FFFFFFFu)
+int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local, const gwaoi_halo_rec *d_recv,
+                      size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele, uint64_t *n_enter,
+                      uint64_t *n_leave) {
+    if (!s || (n_local && !d_local) || (n_recv && !d_recv) || (n_tele && !d_tele) || n_tele > 0x7FFFFFFFu ||
+        n_local + n_recv > 0x7FFFFFFFu)
         return GWAOI_EINVAL;
+    const size_t n_all = n_local + n_recv;
     if (n_enter) *n_enter = 0;
     if (n_leave) *n_leave = 0;
     s->n_enter = s->n_leave = 0;
     const uint32_t tick = ++s->tick;
     hipStream_t st = s->st;
     // ---- received records -> world ops + state
-    const uint32_t nb = std::max(1u, cdivu(n_recv, BT));
+    const uint32_t nb = std::max(1u, cdivu(n_all, BT));
     if (int rc = ensure_split(s, 3, nb)) return rc;
-    if (int rc = ensure_moves(s, n_recv)) return rc;
+    if (int rc = ensure_moves(s, n_all)) return rc;
     S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
-    k_recv<<<nb, BT, 0, st>>>(0, d_recv, (uint32_t)n_recv, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
+    k_recv<<<nb, BT, 0, st>>>(0, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
                               nullptr, nb, s->err, nullptr, nullptr, nullptr, nullptr, nullptr);
     if (int rc = split_totals(s, 3, nb)) return rc;
     if (int rc = strip_err(s, s->small_h[4], "recv")) return rc;
@@ -574,7 +578,7 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_recv, size_t n_re
     const uint32_t n_ent = s->small_h[2] - s->small_h[1];
     const uint32_t n_lev = s->small_h[3] - s->small_h[2];
     if (int rc = grow(s, &s->el_d, s->el_cap, (size_t)n_ent + n_lev + 1)) return rc;
-    k_recv<<<nb, BT, 0, st>>>(1, d_recv, (uint32_t)n_recv, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
+    k_recv<<<nb, BT, 0, st>>>(1, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
                               s->counts, nb, s->err, s->m_slot, s->m_x, s->m_z, s->m_seq, s->el_d);
     S_TRY(hipGetLastError());
     s->el_h.resize((size_t)n_ent + n_lev);

@@ -150,10 +150,13 @@ class StripShard:
         return send, c[:-1], tele
 
     # ---- step 3: apply the exchanged records, flush, keep this strip's events
-    def finish(self, recv, tele) -> Tuple[int, int]:
+    def finish(self, local, recv, tele) -> Tuple[int, int]:
+        """local: this strip's own slice of its send buffer; recv: the records
+        from the other strips; tele: all teleport records."""
         ne, nl = C.c_uint64(), C.c_uint64()
-        nr, nt = int(recv.shape[0]), int(tele.shape[0])
-        self._check(self._L.gwaoi_strips_tick(self._s, C.c_void_p(recv.data_ptr() if nr else 0), nr,
+        nlo, nr, nt = int(local.shape[0]), int(recv.shape[0]), int(tele.shape[0])
+        self._check(self._L.gwaoi_strips_tick(self._s, C.c_void_p(local.data_ptr() if nlo else 0), nlo,
+                                              C.c_void_p(recv.data_ptr() if nr else 0), nr,
                                               C.c_void_p(tele.data_ptr() if nt else 0), nt, C.byref(ne),
                                               C.byref(nl)))
         return ne.value, nl.value
@@ -175,10 +178,18 @@ class StripShard:
 
 # ---------------------------------------------------------------- exchange ---
 
+def local_slice(send, counts, rank):
+    """This rank's own records inside its send buffer (they never travel)."""
+    c = np.concatenate([[0], np.cumsum(counts)])
+    return send[int(c[rank]):int(c[rank + 1])]
+
+
 def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     """The halo exchange of one tick over torch.distributed (RCCL on GPU
-    tensors, gloo on CPU ones): counts all-gathered, records all-to-all'd,
-    teleport records all-gathered.  Returns (recv records, all teleports).
+    tensors, gloo on CPU ones): counts all-gathered, the records for other
+    ranks all-to-all'd (a rank's own slice stays put: ``local_slice``),
+    teleport records all-gathered.  Returns (records from the other ranks,
+    all teleports).
     via_cpu: GPU tensors go through host memory (gloo rehearsal of several
     ranks sharing one GPU; RCCL allows one rank per device)."""
     import torch
@@ -196,6 +207,11 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     M = torch.stack(rows).cpu().numpy()  # M[src, dst]; column S = teleports of src
     in_splits = [int(v) for v in M[rank, :S]]
     out_splits = [int(v) for v in M[:, rank]]
+    # the own slice is cut out on both sides: send without it, receive without it
+    lo = sum(in_splits[:rank])
+    if in_splits[rank]:
+        send = torch.cat([send[:lo], send[lo + in_splits[rank]:]])
+    in_splits[rank] = out_splits[rank] = 0
     recv = torch.empty((sum(out_splits), send.shape[1]), dtype=send.dtype, device=dev)
     dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
     T = M[:, S]
@@ -211,8 +227,8 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
 
 def exchange_local(outs: List[Tuple]):
     """Loopback exchange for several strips in one process: outs[r] =
-    (send, counts, tele) of strip r.  Returns [(recv, tele_all)] per strip,
-    in the same source order as the all_to_all (source rank order)."""
+    (send, counts, tele) of strip r.  Returns [(recv, tele_all)] per strip
+    (records from the other strips in source rank order, like ``exchange``)."""
     import torch
     S = len(outs)
     starts = []
@@ -222,7 +238,9 @@ def exchange_local(outs: List[Tuple]):
     tele_all = torch.cat([o[2] for o in outs]) if S else None
     res = []
     for q in range(S):
-        parts = [outs[r][0][int(starts[r][q]):int(starts[r][q + 1])] for r in range(S)]
+        parts = [outs[r][0][int(starts[r][q]):int(starts[r][q + 1])] for r in range(S) if r != q]
+        if not parts:
+            parts = [outs[q][0][:0]]
         res.append((torch.cat(parts), tele_all))
     return res
 
@@ -232,7 +250,7 @@ def tile_tick(shard: StripShard, dist, ops, group=None) -> Tuple[int, int]:
     send, counts, tele = shard.route(ops)
     recv, tele_all = exchange(dist, send, counts, tele, group=group)
     shard.torch.cuda.current_stream(shard.dev).synchronize()
-    return shard.finish(recv, tele_all)
+    return shard.finish(local_slice(send, counts, dist.get_rank(group)), recv, tele_all)
 
 
 def local_tick(shards: Sequence[StripShard], ops_per_strip) -> List[Tuple[int, int]]:
@@ -240,4 +258,4 @@ def local_tick(shards: Sequence[StripShard], ops_per_strip) -> List[Tuple[int, i
     outs = [sh.route(o) for sh, o in zip(shards, ops_per_strip)]
     ex = exchange_local(outs)
     shards[0].torch.cuda.synchronize()
-    return [sh.finish(r, t) for sh, (r, t) in zip(shards, ex)]
+    return [sh.finish(local_slice(o[0], o[1], q), r, t) for q, (sh, o, (r, t)) in enumerate(zip(shards, outs, ex))]

@@ -27,8 +27,9 @@
  *      destination rank, into caller device buffers.
  *   3. the caller exchanges them (all_to_all over RCCL / xGMI; teleports
  *      all-gathered) -- see goworld_amd/strips.py.
- *   4. gwaoi_strips_tick(recv, tele_all) -- applies the received records to the
- *      world, flushes it, and filters its events to the ones this strip owns.
+ *   4. gwaoi_strips_tick(local, recv, tele_all) -- applies its own and the
+ *      received records to the world, flushes it, and filters its events to
+ *      the ones this strip owns.
  *
  * Single-threaded per strip, on the world's stream.  All counts are records.
  */
@@ -90,11 +91,13 @@ int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, u
  * records grouped by destination rank (rank order), d_tele counts[n_strips].
  * Returns after the writes completed (the caller's transport may read them). */
 int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_tele_rec *d_tele);
-/* 4. Apply the records received from every rank (including this one) and the
- * all-gathered teleport records, flush the world and keep this strip's
- * events.  The inputs must be complete (caller synchronised its transport). */
-int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_recv, size_t n_recv, const gwaoi_tele_rec *d_tele,
-                      size_t n_tele, uint64_t *n_enter, uint64_t *n_leave);
+/* 4. Apply this rank's own records (d_local: its slice of d_send, never sent),
+ * the records received from the other ranks and the all-gathered teleport
+ * records, flush the world and keep this strip's events.  The inputs must
+ * be complete (the caller synchronised its transport). */
+int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local, const gwaoi_halo_rec *d_recv,
+                      size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele, uint64_t *n_enter,
+                      uint64_t *n_leave);
 /* Device pointers of this strip's events of the last tick (layout of
  * gwaoi_events: enter pairs, then leave pairs, a0,b0,a1,b1,...). */
 int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const uint32_t **d_leave);

@@ -113,11 +113,12 @@ class ModelShard:
             return self.prv[s], self.pseq[s]
         return self.cur[s], self.cseq[s]
 
-    def finish(self, recv, tele):
+    def finish(self, local, recv, tele):
         O = self.oracle
         self.tick_id += 1
         t = self.tick_id
-        recv = np.frombuffer(recv.numpy().tobytes(), HALO_DTYPE)
+        recv = np.concatenate([np.frombuffer(local.numpy().tobytes(), HALO_DTYPE),
+                               np.frombuffer(recv.numpy().tobytes(), HALO_DTYPE)])
         tele = np.frombuffer(tele.numpy().tobytes(), TELE_DTYPE)
         leaves, rest = [], []
         for r in recv:

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from goworld_amd.strips import as_words, exchange, exchange_local, HALO_WORDS, owner_of
+from goworld_amd.strips import as_words, exchange, exchange_local, local_slice, HALO_WORDS, owner_of
 from strip_model import ModelShard
 from strip_scenario import D, Scenario, split_by_owner
 
@@ -38,8 +38,8 @@ def run_strips_local(oracle, sc: Scenario, ticks: int):
     for _ in range(ticks):
         per = split_by_owner(*sc.tick(), sc.edges)
         routed = [sh.route(as_words(o, HALO_WORDS)) for sh, o in zip(shards, per)]
-        for sh, (recv, tele) in zip(shards, exchange_local(routed)):
-            sh.finish(recv, tele)
+        for q, (sh, (recv, tele)) in enumerate(zip(shards, exchange_local(routed))):
+            sh.finish(local_slice(routed[q][0], routed[q][1], q), recv, tele)
         out.append(tuple(np.concatenate([sh.last[i] for sh in shards]) for i in (0, 1)))
     return out
 
@@ -92,7 +92,7 @@ def _worker(rank, ws, port, seed, ticks, q):
         ops = split_by_owner(*sc.tick(), sc.edges)[rank]
         send, counts, tele = sh.route(as_words(ops, HALO_WORDS))
         recv, tele_all = exchange(dist, send, counts, tele)
-        sh.finish(recv, tele_all)
+        sh.finish(local_slice(send, counts, rank), recv, tele_all)
         res.append((sh.last[0].tolist(), sh.last[1].tolist()))
     q.put((rank, res))
     dist.barrier()
