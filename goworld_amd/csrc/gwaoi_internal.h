@@ -85,6 +85,8 @@ struct TickScalars {
     float d_rel;                 // largest displacement / D of "near" entities
     float bmax;                  // largest |x|,|z| of live entities (new positions)
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
+    uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply)
+    uint32_t pad2;
 };
 
 // Device -> host block copied once per tick: result + per-space bbox.
@@ -117,11 +119,41 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
                       uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
                       uint32_t n_total, const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor,
                       bool track_max, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st);
+// A flush whose queue is only device Moved batches (<= MAX_MOVE_RUNS of them):
+// single-pass claim+apply, then a fixup of the slots moved more than once.
+constexpr uint32_t MAX_MOVE_RUNS = 4;
+struct MoveRun {
+    const uint32_t *ds;
+    const float *dx, *dz;
+    const unsigned long long *dseq;  // explicit seqs (nullptr: seq0 + i)
+    unsigned long long seq0;
+    uint32_t j0, n;  // first op index in the flush, ops
+};
+struct MoveRuns {
+    MoveRun r[MAX_MOVE_RUNS];
+    uint32_t count;
+};
+void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+                  uint64_t seq_floor, Rec16 *s_rec, const Rec16 *p_rec, uint32_t n_prev, TickScalars *sc,
+                  uint32_t *coll, hipStream_t st);
+
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
-// partials in blk, 2 * cdiv(n, 256) floats).
+// partials in blk, 2 * cdiv(n, 256) floats).  cnt64 != nullptr (grid
+// unchanged): also per-cell entity counts (low word) and arrival counts
+// (high word; arrival = cell differs from p_key[i], or i >= n_prev).
 void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
-                   const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, hipStream_t st);
+                   const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
+                   unsigned long long *cnt64, hipStream_t st);
+// The stable sort of S' by key when the grid is the previous frame's: the
+// new cell_start (from cnt64) plus, per cell, a merge of the entities that
+// stayed with the arrivals.  Writes perm / skeys like radix_sort and the
+// frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems.
+size_t incr_sort_tmp_elems(size_t cells);
+void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
+                      const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
+                      uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
+                      unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
@@ -141,7 +173,7 @@ size_t scan_tmp_elems(size_t n);
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
-                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, hipStream_t st);
+                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
 // Tiles of a frame: rows split into runs of <= TILE_A entities.

@@ -85,6 +85,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->d_rel = 0.0f;
         sc->bmax = 0.0f;
         sc->seq_max = 0;
+        sc->ncoll = 0;
     }
     if (i < n0) z0[i] = 0;
     if (i < n1) z1[i] = 0;
@@ -140,12 +141,12 @@ __device__ __forceinline__ unsigned long long op_apply_one(
     const uint32_t *__restrict__ slots, const float *__restrict__ xs, const float *__restrict__ zs,
     const uint32_t *__restrict__ sps, uint32_t i, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick,
     uint32_t n_total, const unsigned long long *__restrict__ seqs, unsigned long long seq0,
-    unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc) {
+    unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, bool check_claim = true) {
     const uint32_t j = j0 + i;
     const uint32_t s = slots[i];
     if (s >= max_slots) return 0;
     const uint4 si = reinterpret_cast<const uint4 *>(info)[s];  // lastop, rank, sp: one line
-    if ((((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return 0;
+    if (check_claim && (((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return 0;
     const uint32_t idx = si.z, cur_sp = si.w;
     if (idx >= n_total) {
         atomicOr(&sc->err, ERR_MOVE_DEAD);
@@ -203,6 +204,56 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
     }
 }
 
+// Device Moved batches only (the per-tick position sync): one pass instead of
+// claim + apply.  Each op claims its slot with a returning atomicMax and, if
+// it is the highest claim so far, writes its state.  Two ops of one slot in
+// one flush both may write, in any order: every such slot is listed in
+// `coll` (by whichever op sees the other's claim) and k_moves_fixup rewrites
+// it from the final winner after this kernel has drained.
+__global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
+                              unsigned long long seq_floor, Rec16 *s_rec, TickScalars *sc, uint32_t *coll) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long smax = 0;
+    if (i < R.n) {
+        const uint32_t s = R.ds[i];
+        if (s >= max_slots) {
+            atomicOr(&sc->err, ERR_BAD_SLOT);
+        } else {
+            const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
+            const unsigned long long old = atomicMax(&info[s].lastop, mine);
+            if ((uint32_t)(old >> 32) == tick) coll[atomicAdd(&sc->ncoll, 1u)] = s;
+            if (old < mine)
+                smax = op_apply_one(R.ds, R.dx, R.dz, nullptr, i, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
+                                    seq_floor, s_rec, nullptr, sc, false);
+        }
+    }
+    if (R.dseq) {  // one atomic per wave, not per op
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(smax, o, WAVE);
+            smax = v > smax ? v : smax;
+        }
+        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
+    }
+}
+
+__global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
+                              unsigned long long seq_floor, Rec16 *s_rec, const Rec16 *__restrict__ p_rec,
+                              uint32_t n_prev, TickScalars *sc, const uint32_t *__restrict__ coll) {
+    const uint32_t nc = sc->ncoll;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
+        const uint32_t s = coll[k];
+        const uint4 si = reinterpret_cast<const uint4 *>(info)[s];
+        const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
+        uint32_t q = 0;
+        while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
+        const MoveRun &R = RS.r[q];
+        // start from the previous state so that a dropped (invalid) winner leaves it unchanged
+        if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
+        op_apply_one(R.ds, R.dx, R.dz, nullptr, j - R.j0, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
+                     seq_floor, s_rec, nullptr, sc, true);
+    }
+}
+
 // --------------------------------------------------------------- keygen ------
 
 constexpr float FAR_FRAC = 0.25f;  // displacement > FAR_FRAC * D per axis => "special"
@@ -224,17 +275,24 @@ __device__ __forceinline__ uint32_t flags_of(const Rec16 &now, const Rec16 &old,
     return (is_near(now.x, now.z, old.x, old.z, thr) ? 0u : FL_JUMP) | (now.s >= seq_base ? FL_CHG : 0u);
 }
 
+// INCR (the grid is the previous frame's): also count, per cell, the
+// entities (low word of cnt64) and the "arrivals" -- entities whose cell
+// differs from their previous-frame cell, or new in the frame (high word).
+// S' is the previous frame (sorted by the same keys) plus appended entries,
+// so equal keys come in runs and one atomic per run and wave suffices.
+template <bool INCR>
 __global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                                 uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
                                                 uint32_t *keys, uint32_t *vals, const Rec16 *__restrict__ p_rec,
                                                 const SlotSp *__restrict__ p_ss,
-                                                const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk) {
+                                                const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
+                                                const uint32_t *__restrict__ p_key, unsigned long long *cnt64) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     float dr = 0.0f, bm = 0.0f;
+    uint32_t key = sentinel;
     if (i < n) {
         const uint32_t s = ld_ss(s_ss, i).sp;
-        uint32_t key = sentinel;
         if (s != SP_DEAD) {
             const Rec16 r = ld_rec(s_rec, i);
             const SpaceGrid g = grid[s];
@@ -249,7 +307,21 @@ __global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec,
             }
         }
         keys[i] = key;
-        vals[i] = i;
+        if (!INCR) vals[i] = i;
+    }
+    if (INCR) {
+        const bool live = i < n && key != sentinel;
+        const uint32_t l = lane();
+        const uint32_t prev_key = __shfl_up(key, 1);
+        const bool head = live && (l == 0 || prev_key != key);
+        const unsigned long long heads = __ballot(head);
+        const unsigned long long lives = __ballot(live);
+        if (head) {  // run = this lane .. before the next head (or the next non-live lane)
+            const unsigned long long above = (heads | ~lives) & ~((2ull << l) - 1ull);
+            const uint32_t next = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
+            atomicAdd(&cnt64[key], (unsigned long long)(next - l));
+        }
+        if (live && (i >= n_prev || p_key[i] != key)) atomicAdd(&cnt64[key], 1ull << 32);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -526,6 +598,157 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
     }
 }
 
+// ------------------------------------------------- incremental frame sort ------
+// When the grid is unchanged the new frame is a merge: per cell, the
+// entities that stayed (in previous-frame order, i.e. by S' index) and the
+// few "arrivals" (moved in from another cell or new), interleaved by S'
+// index -- exactly the stable sort of S' by the new keys, without sorting.
+//   k_keygen<true>   counts per cell: entities (lo) and arrivals (hi)
+//   scan64           exclusive scans -> the new cell_start and arrival offsets
+//   k_arrive         arrivals into per-cell lists (atomic order, fixed later)
+//   k_cell_merge     one lane per cell: sort its arrivals, merge with the stayers
+
+__global__ __launch_bounds__(SC_T) void k_scan64_reduce(const unsigned long long *__restrict__ in, size_t n,
+                                                        unsigned long long *sums) {
+    __shared__ unsigned long long ws[SC_T / WAVE];
+    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I;
+    unsigned long long s = 0;
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q) s += base + q < n ? in[base + q] : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane() == 0) ws[threadIdx.x / WAVE] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < SC_T / WAVE; ++w) t += ws[w];
+        sums[blockIdx.x] = t;
+    }
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long x) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o);
+        if ((int)lane() >= o) x += y;
+    }
+    return x;
+}
+
+template <int NT>
+__device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long long v, unsigned long long *ws,
+                                                                unsigned long long &total) {
+    const unsigned long long x = wave_incl_scan64(v);
+    const int w = threadIdx.x / WAVE;
+    if (lane() == WAVE - 1) ws[w] = x;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / WAVE; ++i) {
+        const unsigned long long t = ws[i];
+        pre += (i < w) ? t : 0ull;
+        tot += t;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
+// one workgroup: exclusive scan of the block sums in place
+__global__ __launch_bounds__(1024) void k_scan64_single(unsigned long long *a, size_t n) {
+    __shared__ unsigned long long ws[1024 / WAVE];
+    unsigned long long carry = 0;
+    for (size_t c0 = 0; c0 < n; c0 += 1024) {
+        const size_t i = c0 + threadIdx.x;
+        const unsigned long long v = i < n ? a[i] : 0ull;
+        unsigned long long tot;
+        const unsigned long long e = block_excl_scan64<1024>(v, ws, tot);
+        if (i < n) a[i] = e + carry;
+        carry += tot;
+        __syncthreads();
+    }
+}
+
+// exclusive scan, split: lo[i] = low words, hi[i] = high words
+__global__ __launch_bounds__(SC_T) void k_scan64_down(const unsigned long long *__restrict__ in, size_t n,
+                                                      const unsigned long long *__restrict__ block_off, uint32_t *lo,
+                                                      uint32_t *hi) {
+    __shared__ unsigned long long ws[SC_T / WAVE];
+    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I;
+    unsigned long long v[SC_I];
+    unsigned long long s = 0;
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q) {
+        v[q] = base + q < n ? in[base + q] : 0ull;
+        s += v[q];
+    }
+    unsigned long long tot;
+    unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot) + block_off[blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q)
+        if (base + q < n) {
+            lo[base + q] = (uint32_t)run;
+            hi[base + q] = (uint32_t)(run >> 32);
+            run += v[q];
+        }
+}
+
+// Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
+// of cell c and ends as that of cell c+1.
+__global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
+                         const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t key = keys[i];
+    if (key == sentinel || (i < n_prev && p_key[i] == key)) return;
+    arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
+}
+
+// One lane per cell c: the stayers are the entries of c's previous run whose
+// new key is still c (S' index order), the arrivals arr_idx[arr_pos[c-1],
+// arr_pos[c]) are sorted by S' index (insertion sort: a cell rarely gets
+// more than a few) and merged in.  Writes the frame's permutation and keys.
+__global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const uint32_t *__restrict__ cell_start,
+                             const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
+                             uint32_t *arr_idx, uint32_t total_cells, uint32_t n_new, uint32_t n_total,
+                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && n_new < n_total) skeys[n_new] = sentinel;
+    if (c >= total_cells) return;
+    uint32_t o = cell_start[c];
+    const uint32_t oe = cell_start[c + 1];
+    if (o == oe) return;
+    const uint32_t ab = c ? arr_pos[c - 1] : 0u, ae = arr_pos[c];
+    for (uint32_t k = ab + 1; k < ae; ++k) {  // insertion sort of the arrivals
+        const uint32_t v = arr_idx[k];
+        uint32_t j = k;
+        while (j > ab && arr_idx[j - 1] > v) {
+            arr_idx[j] = arr_idx[j - 1];
+            --j;
+        }
+        arr_idx[j] = v;
+    }
+    uint32_t i = p_cell_start[c];
+    const uint32_t ie = p_cell_start[c + 1];
+    uint32_t a = ab;
+    uint32_t nxt = a < ae ? arr_idx[a] : 0xFFFFFFFFu;
+    while (o < oe) {
+        while (i < ie && keys[i] != c) ++i;  // skip the entries that left
+        const uint32_t st = i < ie ? i : 0xFFFFFFFFu;
+        uint32_t v;
+        if (st < nxt) {
+            v = st;
+            ++i;
+        } else {
+            v = nxt;
+            ++a;
+            nxt = a < ae ? arr_idx[a] : 0xFFFFFFFFu;
+        }
+        perm[o] = v;
+        skeys[o] = c;
+        ++o;
+    }
+}
+
 // --------------------------------------------------------------- gather ------
 
 __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
@@ -533,12 +756,18 @@ __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
                          SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
                          unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
-                         uint32_t sentinel, uint32_t n_total, TickScalars *sc) {
+                         uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     if (k >= n_new) return;
-    if (sorted_keys[k] == sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
+    const uint32_t key = sorted_keys[k];
+    if (key == sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
+    f_key[k] = key;
     const uint32_t i = perm[k];
+    if (i >= n_total) {  // bug guard: a broken permutation must not read out of bounds
+        atomicOr(&sc->err, ERR_COUNT_MISMATCH);
+        return;
+    }
     const SlotSp ss = ld_ss(s_ss, i);
     const Rec16 now = ld_rec(s_rec, i);
     st_rec(f_rec, k, now);
@@ -1465,6 +1694,17 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_rec, s_ss, info);
 }
 
+void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+                  uint64_t seq_floor, Rec16 *s_rec, const Rec16 *p_rec, uint32_t n_prev, TickScalars *sc,
+                  uint32_t *coll, hipStream_t st) {
+    for (uint32_t q = 0; q < RS.count; ++q)
+        if (RS.r[q].n)
+            k_moves_apply<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id, n_total, seq_floor,
+                                                                s_rec, sc, coll);
+    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, p_rec, n_prev, sc,
+                                      coll);
+}
+
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info,
                       uint32_t tick_id, TickScalars *sc, hipStream_t st) {
     if (!n) return;
@@ -1482,11 +1722,33 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
 
 void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
-                   const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, hipStream_t st) {
+                   const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
+                   unsigned long long *cnt64, hipStream_t st) {
     if (!n_total) return;  // the prologue left d_rel = bmax = 0
     const uint32_t nb = cdiv(n_total, 256);
-    k_keygen<<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid, n_prev, blk);
+    if (cnt64)
+        k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
+                                           n_prev, blk, p_key, cnt64);
+    else
+        k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
+                                            n_prev, blk, nullptr, nullptr);
     k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
+}
+
+size_t incr_sort_tmp_elems(size_t cells) { return (size_t)cdiv(cells + 1, SC_TILE) + 1; }
+
+void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
+                      const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
+                      uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
+                      unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, hipStream_t st) {
+    const size_t m = (size_t)total_cells + 1;
+    const uint32_t nb = cdiv(m, SC_TILE);
+    k_scan64_reduce<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
+    k_scan64_single<<<1, 1024, 0, st>>>(tmp, nb);
+    k_scan64_down<<<nb, SC_T, 0, st>>>(cnt64, m, tmp, cell_start, arr_pos);
+    if (n_total) k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx);
+    k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
+                                                         n_new, n_total, sentinel, perm, skeys);
 }
 
 size_t scan_tmp_elems(size_t n) {
@@ -1534,10 +1796,10 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
-                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, hipStream_t st) {
+                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
     k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand,
-                                            grid, seq_base, info, sorted_keys, sentinel, n_total, sc);
+                                            grid, seq_base, info, sorted_keys, sentinel, n_total, sc, f_key);
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <new>
@@ -35,6 +36,7 @@ const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",    "gather", "ce
 struct DevFrame {
     gw::Rec16 *rec = nullptr;
     gw::SlotSp *ss = nullptr;
+    uint32_t *key = nullptr;  // cell key of every entry (the next flush's "previous cell")
     uint32_t *cell_start = nullptr;
     size_t cell_cap = 0;  // entries allocated in cell_start
     SpaceGrid *grid = nullptr;
@@ -94,6 +96,12 @@ struct gwaoi_world {
     uint32_t *scan_tmp = nullptr;
     size_t scan_tmp_cap = 0;
     gw::SlotInfo *sinfo = nullptr;  // per slot: last op claim, S' index, space
+    // incremental frame sort (grid unchanged): per-cell counts, arrival lists
+    unsigned long long *cnt64 = nullptr, *scan64_tmp = nullptr;
+    uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
+    uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
+    size_t cnt64_cap = 0;
+    bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
@@ -300,6 +308,23 @@ int ensure_ops(gwaoi_world *w, size_t n) {
         return rc;
     }
     w->op_cap = cap;
+    return GWAOI_OK;
+}
+
+int ensure_incr(gwaoi_world *w, size_t cells) {
+    const size_t need = cells + 1;
+    if (need <= w->cnt64_cap) return GWAOI_OK;
+    const size_t cap = std::max(need + need / 4, (size_t)1024);
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    dfree(w->cnt64);
+    dfree(w->scan64_tmp);
+    dfree(w->arr_pos);
+    w->cnt64_cap = 0;
+    int rc;
+    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, cap)) ||
+        (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
+        return rc;
+    w->cnt64_cap = cap;
     return GWAOI_OK;
 }
 
@@ -524,12 +549,20 @@ int run_tick(gwaoi_world *w) {
 
     const uint32_t ns = std::max(1u, w->n_space_ids);
     const bool grid_same = Fn.hgrid.size() == ns && !std::memcmp(Fn.hgrid.data(), w->h_grid, ns * sizeof(SpaceGrid));
+    // the previous frame was cut with the same grid: its cells and keys are this flush's
+    const bool incr = !w->force_radix && n_prev > 0 && P.total_cells == total_cells && P.hgrid.size() == ns &&
+                      !std::memcmp(P.hgrid.data(), w->h_grid, ns * sizeof(SpaceGrid));
+    if (incr && (rc = ensure_incr(w, total_cells))) return rc;
     if (!grid_same) {
         HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * ns, hipMemcpyHostToDevice, st));
         Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
     }
-    gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
-                        w->n_space_ids, st);
+    if (incr)
+        gw::launch_prologue(w->sc, reinterpret_cast<uint32_t *>(w->cnt64), 2 * ((size_t)total_cells + 1), w->tile_total,
+                            entries + 1, dev_bbox(w), w->n_space_ids, st);
+    else
+        gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
+                            w->n_space_ids, st);
 
     // ---- apply queued ops onto S' = copy of the previous frame
     stage_begin(w, ST_APPLY);
@@ -539,7 +572,19 @@ int run_tick(gwaoi_world *w) {
                                hipMemcpyHostToDevice, st));
         gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->sinfo, st);
     }
-    if (n_ops) {
+    const bool moves_only = n_ops && host_ops == 0 && w->runs.size() <= gw::MAX_MOVE_RUNS && n_ops <= w->max_slots;
+    if (moves_only) {  // the per-tick position sync: one pass + fixup of repeated slots
+        gw::MoveRuns RS{};
+        uint32_t j0 = 0;
+        for (const Run &r : w->runs) {
+            gw::MoveRun &m = RS.r[RS.count++];
+            m.ds = r.ds; m.dx = r.dx; m.dz = r.dz; m.dseq = r.dseq; m.seq0 = r.seq0;
+            m.j0 = j0; m.n = (uint32_t)r.dn;
+            j0 += (uint32_t)r.dn;
+        }
+        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, w->srec, P.rec, n_prev, w->sc,
+                         w->coll, st);
+    } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
         for (const Run &r : w->runs) {
@@ -584,17 +629,24 @@ int run_tick(gwaoi_world *w) {
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, ST_KEYGEN);
     gw::launch_keygen(w->srec, w->sss, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, w->sc, st);
+                      n_prev, w->blk, w->sc, P.key, incr ? w->cnt64 : nullptr, st);
     stage_end(w, ST_KEYGEN);
     stage_begin(w, ST_SORT);
-    gw::SortBuffers sb;
-    sb.keys[0] = w->keys[0];
-    sb.keys[1] = w->keys[1];
-    sb.vals[0] = w->vals[0];
-    sb.vals[1] = w->vals[1];
-    sb.hist = w->hist;
-    sb.scan_tmp = w->scan_tmp;
-    const int which = gw::radix_sort(sb, n_total, bitlen(total_cells), st);
+    int which = 1;
+    if (incr) {
+        gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
+                             total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
+                             w->keys[1], st);
+    } else {
+        gw::SortBuffers sb;
+        sb.keys[0] = w->keys[0];
+        sb.keys[1] = w->keys[1];
+        sb.vals[0] = w->vals[0];
+        sb.vals[1] = w->vals[1];
+        sb.hist = w->hist;
+        sb.scan_tmp = w->scan_tmp;
+        which = gw::radix_sort(sb, n_total, bitlen(total_cells), st);
+    }
     stage_end(w, ST_SORT);
     const uint32_t *skeys = w->keys[which];
     const uint32_t *perm = w->vals[which];
@@ -603,14 +655,17 @@ int run_tick(gwaoi_world *w) {
     stage_begin(w, ST_GATHER);
     gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
-                      total_cells, n_total, w->sc, st);
+                      total_cells, n_total, w->sc, Fn.key, st);
     stage_end(w, ST_GATHER);
 
-    // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue)
-    stage_begin(w, ST_CELLS);
-    gw::launch_cell_count(skeys, n_new, Fn.cell_start, st);
-    gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
-    stage_end(w, ST_CELLS);
+    // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
+    // the incremental sort has written it already)
+    if (!incr) {
+        stage_begin(w, ST_CELLS);
+        gw::launch_cell_count(skeys, n_new, Fn.cell_start, st);
+        gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
+        stage_end(w, ST_CELLS);
+    }
     stage_begin(w, ST_TILES);
     gw::build_tiles(view_of(Fn), grid_same ? 0u : w->n_space_ids, total_rows, Fn.row_space, Fn.row_ntiles, Fn.tiles,
                     w->scan_tmp, st);
@@ -728,12 +783,13 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     for (DevFrame &f : w->fr) {
-        dfree(f.rec); dfree(f.ss); dfree(f.cell_start); dfree(f.grid);
+        dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.grid);
         dfree(f.row_space); dfree(f.row_ntiles); dfree(f.tiles);
     }
     dfree(w->srec); dfree(w->sss); dfree(w->orec); dfree(w->cand);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
+    dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
     dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
@@ -760,6 +816,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->max_spaces = cfg->max_spaces;
     w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 4.0f;
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
+    if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
     int rc = GWAOI_OK;
     auto fail = [&](int code) {
         gwaoi_world_destroy(w);
@@ -782,7 +839,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     }
     const size_t N = w->max_slots;
     for (DevFrame &f : w->fr) {
-        if ((rc = dalloc(w, &f.rec, N)) || (rc = dalloc(w, &f.ss, N)) || (rc = dalloc(w, &f.grid, w->max_spaces)))
+        if ((rc = dalloc(w, &f.rec, N)) || (rc = dalloc(w, &f.ss, N)) || (rc = dalloc(w, &f.key, N)) ||
+            (rc = dalloc(w, &f.grid, w->max_spaces)))
             return fail(rc);
         if ((rc = ensure_cells(w, f, 1))) return fail(rc);
     }
@@ -790,7 +848,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if ((rc = dalloc(w, &w->srec, N)) || (rc = dalloc(w, &w->sss, N)) || (rc = dalloc(w, &w->orec, N)) || (rc = dalloc(w, &w->cand, N)) ||
         (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
-        (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) ||
+        (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
+        (rc = dalloc(w, &w->coll, N)) ||
         (rc = dalloc(w, &w->sc, 1)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, (char **)&w->bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
         (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)))

@@ -292,6 +292,44 @@ def test_device_batch_matches_host_batch_gpu():
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
 
 
+def test_device_batch_repeated_slots_gpu():
+    """Slots moved several times in one flush, inside one device batch and
+    across two (the single-pass apply's collision fixup): the last call wins,
+    exactly as with host calls."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(5)
+    wl = make_workload("cfg2", n=6000)
+    slots, x0, z0, _ = wl.initial()
+    with World(wl.n) as wa, World(wl.n) as wb:
+        for w in (wa, wb):
+            s = w.space_create(wl.D)
+            w.enter_batch(s, slots, x0, z0)
+            w.tick()
+        x, z = x0.copy(), z0.copy()
+        for t in range(4):
+            runs = []
+            for r in range(2):
+                sl = rng.integers(0, 300 if r else wl.n, 5000).astype(np.uint32)  # many repeats
+                nx = (x[sl] + rng.uniform(-30, 30, sl.size)).astype(np.float32)
+                nz = (z[sl] + rng.uniform(-30, 30, sl.size)).astype(np.float32)
+                runs.append((sl, nx, nz))
+            dev = []
+            for sl, nx, nz in runs:
+                wa.moved_batch(sl, nx, nz)
+                d = [torch.from_numpy(v).cuda() for v in (sl.astype(np.int32), nx, nz)]
+                dev.append(d)
+                wb.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sl.size)
+            torch.cuda.synchronize()
+            ea, la = wa.tick()
+            eb, lb = wb.tick()
+            np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
+            for sl, nx, nz in runs:  # last write wins
+                x[sl], z[sl] = nx, nz
+        for i in (0, 1, 7, 299, 5999):
+            np.testing.assert_array_equal(wa.neighbors(i), wb.neighbors(i))
+
+
 def test_device_batch_errors_reported_gpu():
     torch = pytest.importorskip("torch")
     with World(8) as w:
@@ -383,3 +421,51 @@ def test_mixed_churn_vs_closed_form_gpu(oracle_mod, seed, spaces):
             np.testing.assert_array_equal(ge, ab(np.setdiff1d(cur, prev)))
             np.testing.assert_array_equal(gl, ab(np.setdiff1d(prev, cur)))
             prev = cur
+
+
+@pytest.mark.parametrize("cfg,n", [("cfg3", 60000), ("cfg2", 30000)])
+def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
+    """The incremental frame sort (grid unchanged) is the stable sort by cell
+    key: the flush's event arrays -- order included -- equal those of the
+    full radix-sort path (GWAOI_FORCE_RADIX=1), with churn in every flush."""
+    rng = np.random.default_rng(9)
+    wl = make_workload(cfg, n=n)
+    slots, x0, z0, _ = wl.initial()
+    monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
+    wr = World(n + 500)
+    monkeypatch.delenv("GWAOI_FORCE_RADIX")
+    wi = World(n + 500)
+    try:
+        for w in (wr, wi):
+            s = w.space_create(wl.D)
+            w.enter_batch(s, slots, x0, z0)
+            w.tick()
+        live = set(range(n))
+        spare = list(range(n, n + 500))
+        for t in range(5):
+            sl, nx, nz = wl.tick(t)
+            keep = np.array([int(v) in live for v in sl])
+            sl, nx, nz = sl[keep], nx[keep], nz[keep]
+            jump = rng.choice(sl.size, 200, replace=False)
+            nx[jump] += rng.uniform(-300, 300, 200).astype(np.float32)
+            leavers = rng.choice(sorted(live), 50, replace=False)
+            enter = [spare.pop() for _ in range(40)]
+            ex = rng.uniform(-wl.L / 2, wl.L / 2, 40).astype(np.float32)
+            ez = rng.uniform(-wl.L / 2, wl.L / 2, 40).astype(np.float32)
+            mv = ~np.isin(sl, leavers)
+            outs = []
+            for w in (wr, wi):
+                w.moved_batch(sl[mv], nx[mv], nz[mv])
+                w.leave_batch(leavers)
+                w.enter_batch(0, np.array(enter, np.uint32), ex, ez)
+                outs.append(w.tick())
+            live -= set(int(v) for v in leavers)
+            live |= set(enter)
+            spare.extend(int(v) for v in leavers)
+            (er, lr), (ei, li) = outs
+            np.testing.assert_array_equal(er, ei)
+            np.testing.assert_array_equal(lr, li)
+            assert er.size + lr.size > 0
+    finally:
+        wr.close()
+        wi.close()
