@@ -1178,8 +1178,9 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t nb) {
 
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
-constexpr int QCAP = 256;  // per-wave queue of filter survivors
-constexpr int EVW = 128;   // events buffered per wave
+constexpr int QCAP = 640;  // per-wave queue of filter survivors (>= SW_U * WAVE + a drain batch)
+constexpr int SW_U = 8;    // candidates per lane per sweep iteration on long rows
+constexpr int EVW = 192;   // events buffered per wave
 
 struct CombinedLds {
     uint2 q[CW][QCAP];  // queued pairs of a wave: (A frame index, B frame index)
@@ -1211,12 +1212,11 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // Full test of the queued pairs of wave w; appends events (deterministic order).
-// REPLAY: count only, and write events number >= EVW straight to the output.
-template <bool REPLAY>
+// replay: count only, and write events number >= EVW straight to the output.
 __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, const FrameView &F,
                                          const Rec16 *__restrict__ O_rec, const PairCtx &proto, float thr,
                                          uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap, unsigned long long pe,
-                                         unsigned long long pl) {
+                                         unsigned long long pl, bool replay) {
     const uint32_t ln = lane();
     for (uint32_t q0 = 0; q0 < qn; q0 += WAVE) {
         const uint32_t e = q0 + ln;
@@ -1238,7 +1238,7 @@ __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, 
         const uint32_t pos = ne + nl + (uint32_t)__popcll((em | lm) & lanemask_lt());
         if (kind) {
             const uint32_t a_slot = ld_ss(F.ss, a).slot, b_slot = ld_ss(F.ss, b).slot;
-            if (!REPLAY) {
+            if (!replay) {
                 if (pos < EVW) L.ev[w][pos] = make_uint2(a_slot, b_slot | (kind == 2 ? KIND_LEAVE : 0u));
             } else if (pos >= EVW) {
                 const uint32_t kidx = kind == 1 ? ne + (uint32_t)__popcll(em & lanemask_lt())
@@ -1267,61 +1267,86 @@ __device__ __forceinline__ void qpush(CombinedLds &L, int w, WaveQueue &Q, bool 
     Q.qn += (uint32_t)__popcll(m);
 }
 
-// Sweep the cell range [c0, c1] of grid row `row` for every lane (bounds are
-// per lane, loop trip count is the wave maximum).  MODE 0: Z strip, 1: X'
-// strip, 2: whole window of a jumper.
-template <int MODE, bool REPLAY>
-__device__ __forceinline__ void sweep_row(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int row,
-                                          int c0, int c1, const uint4 *__restrict__ cand, const FrameView &F,
-                                          const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
-                                          uint64_t cap, unsigned long long pe, unsigned long long pl) {
-    uint32_t jb = 0, len = 0;
-    if (on) {
-        const uint32_t rb = C.g.base + (uint32_t)row * C.g.gx;
-        jb = F.cell_start[rb + (uint32_t)c0];
-        len = F.cell_start[rb + (uint32_t)c1 + 1u] - jb;
-    }
-    const uint32_t mx = wave_max_u32(len);
+// Sweep candidates [jb, jb + len) of one grid row for every lane (ranges are
+// per lane; the loop runs to the wave maximum mx).  MODE 0: Z strip, 1: X'
+// strip, 2: whole window of a jumper.  U candidates per lane per iteration,
+// all U loads issued before the first is used (one L2 round trip per U).
+template <int MODE, int U>
+__device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, uint32_t jb,
+                                            uint32_t len, uint32_t mx, const uint4 *__restrict__ cand,
+                                            const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
+                                            uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
+                                            bool replay) {
     const float lo = C.lo, hi = C.hi;
-    for (uint32_t t = 0; t < mx; t += 2) {
-        const bool v0 = t < len, v1 = t + 1 < len;
-        const uint32_t b0 = jb + t, b1 = jb + t + 1;
-        const uint4 k0 = cand[v0 ? b0 : 0u], k1 = cand[v1 ? b1 : 0u];
-        bool keep0, keep1;
-        {
-            const float dx0 = __uint_as_float(k0.x) - A.x, dz0 = __uint_as_float(k0.y) - A.z;
-            const float dx1 = __uint_as_float(k1.x) - A.x, dz1 = __uint_as_float(k1.y) - A.z;
-            if (MODE == 0) {
-                keep0 = (int)(dz0 >= lo) & (int)(dz0 <= hi) & (int)(fabsf(dx0) <= hi) & (int)((k0.z & FL_JUMP) == 0u);
-                keep1 = (int)(dz1 >= lo) & (int)(dz1 <= hi) & (int)(fabsf(dx1) <= hi) & (int)((k1.z & FL_JUMP) == 0u);
-            } else if (MODE == 1) {
-                keep0 = (int)(dx0 >= lo) & (int)(dx0 <= hi) & (int)(fabsf(dz0) <= C.lo_in) &
-                        (int)((k0.z & FL_JUMP) == 0u);
-                keep1 = (int)(dx1 >= lo) & (int)(dx1 <= hi) & (int)(fabsf(dz1) <= C.lo_in) &
-                        (int)((k1.z & FL_JUMP) == 0u);
-            } else {
-                keep0 = (int)(fabsf(dx0) <= hi) & (int)(fabsf(dz0) <= hi) & (int)(b0 != A.a) &
-                        ((int)((k0.z & FL_JUMP) == 0u) | (int)(A.a < b0));
-                keep1 = (int)(fabsf(dx1) <= hi) & (int)(fabsf(dz1) <= hi) & (int)(b1 != A.a) &
-                        ((int)((k1.z & FL_JUMP) == 0u) | (int)(A.a < b1));
-            }
-            keep0 = keep0 & v0 & (int)(((k0.z | A.fl) & FL_CHG) != 0u);
-            keep1 = keep1 & v1 & (int)(((k1.z | A.fl) & FL_CHG) != 0u);
+    for (uint32_t t = 0; t < mx; t += U) {
+        uint3 k[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint4 v = cand[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
+            k[u] = make_uint3(v.x, v.y, v.z);
         }
-        qpush(L, w, Q, keep0, A.a, b0);
-        qpush(L, w, Q, keep1, A.a, b1);
-        if (Q.qn > QCAP - 2 * WAVE) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t b = jb + t + (uint32_t)u;
+            const float dx = __uint_as_float(k[u].x) - A.x, dz = __uint_as_float(k[u].y) - A.z;
+            bool keep;
+            if (MODE == 0)
+                keep = (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi) & (int)((k[u].z & FL_JUMP) == 0u);
+            else if (MODE == 1)
+                keep = (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in) &
+                       (int)((k[u].z & FL_JUMP) == 0u);
+            else
+                keep = (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi) & (int)(b != A.a) &
+                       ((int)((k[u].z & FL_JUMP) == 0u) | (int)(A.a < b));
+            keep = keep & (int)(t + (uint32_t)u < len) & (int)(((k[u].z | A.fl) & FL_CHG) != 0u);
+            qpush(L, w, Q, keep, A.a, b);
+        }
+        if (Q.qn > QCAP - U * WAVE) {
             __builtin_amdgcn_wave_barrier();
-            drain_queue<REPLAY>(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl);
+            drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
             Q.qn = 0;
         }
     }
 }
 
-template <bool REPLAY>
+// Rows r0..r1 (per lane; `on` = the lane takes part), cells c0..c1 of each row.
+// The next row's candidate range is loaded while the current one is swept.
+template <int MODE>
+__device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int r0,
+                                           int r1, int c0, int c1, const uint4 *__restrict__ cand, const FrameView &F,
+                                           const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
+                                           uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
+    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
+    const uint32_t nrw = wave_max_u32(nr);
+    const uint32_t *cs = F.cell_start;
+    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
+    uint32_t jb = 0, je = 0;
+    if (nr) {
+        const uint32_t rb = rb0 + (uint32_t)r0 * gx;
+        jb = cs[rb];
+        je = cs[rb + span];
+    }
+    for (uint32_t k = 0; k < nrw; ++k) {
+        uint32_t nb = 0, ne = 0;
+        if (k + 1 < nr) {  // prefetch the next row's range
+            const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + 1) * gx;
+            nb = cs[rb];
+            ne = cs[rb + span];
+        }
+        const uint32_t len = je - jb;
+        const uint32_t mx = wave_max_u32(len);
+        if (MODE != 2 && mx > 2)
+            sweep_range<MODE, SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        else if (mx)
+            sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        jb = nb;
+        je = ne;
+    }
+}
+
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
-                               uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl) {
+                               uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const int w = threadIdx.x / WAVE;
     const SpaceGrid &g = C.g;
     WaveQueue Q{0u, ne, nl};
@@ -1337,20 +1362,16 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c0 = cell_of(A.x - hi - M, g.ox, g.inv, g.gx);
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
-        const int nr = (int)wave_max_u32((uint32_t)(r1 - r0 + 1));
-        for (int k = 0; k < nr; ++k)
-            sweep_row<0, REPLAY>(L, w, Q, A, r0 + k <= r1, r0 + k, c0, c1, cand, F, O_rec, C, out, cap, pe, pl);
+        sweep_rows<0>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
         // X' strip: rows holding z in [z-lo, z+lo], cells holding x in [x+lo, x+hi]
-        r0 = 0, r1 = -1;
+        r0 = 0, r1 = -1, c0 = 0, c1 = -1;
         if (strip) {
             r0 = cell_of(A.z - lo - M, g.oz, g.inv, g.gz);
             r1 = cell_of(A.z + lo + M, g.oz, g.inv, g.gz);
             c0 = cell_of(A.x + lo - M, g.ox, g.inv, g.gx);
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
-        const int nx = (int)wave_max_u32((uint32_t)(r1 - r0 + 1));
-        for (int k = 0; k < nx; ++k)
-            sweep_row<1, REPLAY>(L, w, Q, A, r0 + k <= r1, r0 + k, c0, c1, cand, F, O_rec, C, out, cap, pe, pl);
+        sweep_rows<1>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
     }
     if (__ballot(whole)) {
         const float r = hi + M;
@@ -1361,13 +1382,11 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c0 = cell_of(A.x - r, g.ox, g.inv, g.gx);
             c1 = cell_of(A.x + r, g.ox, g.inv, g.gx);
         }
-        const int nr = (int)wave_max_u32((uint32_t)(r1 - r0 + 1));
-        for (int k = 0; k < nr; ++k)
-            sweep_row<2, REPLAY>(L, w, Q, A, r0 + k <= r1, r0 + k, c0, c1, cand, F, O_rec, C, out, cap, pe, pl);
+        sweep_rows<2>(L, w, Q, A, whole, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
     }
     if (Q.qn) {
         __builtin_amdgcn_wave_barrier();
-        drain_queue<REPLAY>(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl);
+        drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
     }
     ne = Q.ne;
     nl = Q.nl;
@@ -1401,9 +1420,8 @@ __global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__res
 
     uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform)
     // sweep once per distinct space in this wave (almost always one)
-    auto run = [&](auto replay_tag, uint2 *o, unsigned long long pe, unsigned long long pl, uint32_t &e,
+    auto run = [&](bool replay, uint2 *o, unsigned long long pe, unsigned long long pl, uint32_t &e,
                    uint32_t &l) {
-        constexpr bool RP = decltype(replay_tag)::value;
         unsigned long long pending = __ballot(A.valid);
         while (pending) {
             const uint32_t lead = (uint32_t)__ffsll((long long)pending) - 1u;
@@ -1426,10 +1444,10 @@ __global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__res
             C.proto.chg = false;
             LaneA B = A;
             B.valid = mine;
-            combined_sweep<RP>(L, B, cand, F, O_rec, C, e, l, o, cap, pe, pl);
+            combined_sweep(L, B, cand, F, O_rec, C, e, l, o, cap, pe, pl, replay);
         }
     };
-    run(std::false_type{}, nullptr, 0ull, 0ull, ne, nl);
+    run(false, nullptr, 0ull, 0ull, ne, nl);
     if (ln == 0) {
         L.wcnt[w][0] = ne;
         L.wcnt[w][1] = nl;
@@ -1482,7 +1500,7 @@ __global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__res
     }
     if (ne + nl > (uint32_t)EVW) {  // replay: this wave writes the events past its buffer directly
         uint32_t re = 0, rl = 0;
-        run(std::true_type{}, out, pe, pl, re, rl);
+        run(true, out, pe, pl, re, rl);
     }
 }
 
