@@ -102,11 +102,11 @@ struct TickOut {
 };
 
 // ---- launchers (gwaoi_kernels.hip) ------------------------------------------
-// Zero the per-tick counters and two ranges; bbox entries get the fold identity.
+// Zero the per-tick counters and two ranges; bbox entries get the fold
+// identity; S' <- the previous frame's first n_copy entries.
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
-                     uint32_t n_spaces, hipStream_t st);
-void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec, SlotSp *s_ss,
-                       hipStream_t st);
+                     uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
+                     SlotSp *s_ss, hipStream_t st);
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
                           SlotInfo *info, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
@@ -153,7 +153,8 @@ size_t incr_sort_tmp_elems(size_t cells);
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
-                      unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, hipStream_t st);
+                      unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
+                      TickScalars *sc, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {

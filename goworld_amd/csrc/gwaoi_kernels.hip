@@ -76,9 +76,16 @@ __device__ __forceinline__ float qnan() { return __int_as_float(0x7FC00000); }
 
 // ------------------------------------------------------------- prologue ------
 
+// Per-flush start: zero the counters and two ranges, reset the bbox fold,
+// and copy the previous frame into S' (n_copy entries).
 __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t *z1, uint32_t n1, int4 *bbox,
-                           uint32_t n_spaces) {
+                           uint32_t n_spaces, uint32_t n_copy, const Rec16 *__restrict__ p_rec,
+                           const SlotSp *__restrict__ p_ss, Rec16 *s_rec, SlotSp *s_ss) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_copy) {
+        reinterpret_cast<uint4 *>(s_rec)[i] = reinterpret_cast<const uint4 *>(p_rec)[i];
+        reinterpret_cast<uint2 *>(s_ss)[i] = reinterpret_cast<const uint2 *>(p_ss)[i];
+    }
     if (i == 0) {
         sc->err = 0;
         sc->counter = 0;
@@ -344,8 +351,8 @@ __global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec,
     }
 }
 
-__global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict__ blk, uint32_t nb,
-                                                        TickScalars *sc) {
+// Fold keygen's per-block partials into sc->d_rel / sc->bmax (1024 threads).
+__device__ __forceinline__ void keygen_fold(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
     __shared__ float s_m[2][1024 / WAVE];
     float a = 0.0f, b = 0.0f;
     for (uint32_t i = threadIdx.x; i < nb; i += 1024) {
@@ -370,6 +377,11 @@ __global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict_
         sc->d_rel = a;
         sc->bmax = b;
     }
+}
+
+__global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict__ blk, uint32_t nb,
+                                                        TickScalars *sc) {
+    keygen_fold(blk, nb, sc);
 }
 
 // ----------------------------------------------------------------- scan ------
@@ -611,10 +623,13 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 __global__ __launch_bounds__(SC_T) void k_scan64_reduce(const unsigned long long *__restrict__ in, size_t n,
                                                         unsigned long long *sums) {
     __shared__ unsigned long long ws[SC_T / WAVE];
-    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I;
+    const size_t base = (size_t)blockIdx.x * SC_TILE + threadIdx.x;  // coalesced: a sum needs no order
     unsigned long long s = 0;
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q) s += base + q < n ? in[base + q] : 0ull;
+    for (int q = 0; q < SC_I; ++q) {
+        const size_t i = base + (size_t)q * SC_T;
+        s += i < n ? in[i] : 0ull;
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     if (lane() == 0) ws[threadIdx.x / WAVE] = s;
@@ -653,8 +668,14 @@ __device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long lo
     return pre + x - v;
 }
 
-// one workgroup: exclusive scan of the block sums in place
-__global__ __launch_bounds__(1024) void k_scan64_single(unsigned long long *a, size_t n) {
+// one workgroup: exclusive scan of the block sums in place (and, in the same
+// launch, the fold of keygen's d_rel / bmax partials)
+__global__ __launch_bounds__(1024) void k_scan64_single(unsigned long long *a, size_t n, const float *blk,
+                                                        uint32_t nbk, TickScalars *sc) {
+    if (blk) {
+        keygen_fold(blk, nbk, sc);
+        __syncthreads();
+    }
     __shared__ unsigned long long ws[1024 / WAVE];
     unsigned long long carry = 0;
     for (size_t c0 = 0; c0 < n; c0 += 1024) {
@@ -668,28 +689,49 @@ __global__ __launch_bounds__(1024) void k_scan64_single(unsigned long long *a, s
     }
 }
 
-// exclusive scan, split: lo[i] = low words, hi[i] = high words
+// LDS tile index with one pad word per 16: a thread's 16 consecutive words
+// (stride 17) and a wave's coalesced row (stride 1) are both conflict-free.
+__device__ __forceinline__ uint32_t p64(uint32_t i) { return i + (i >> 4); }
+
+// exclusive scan, split: lo[i] = low words, hi[i] = high words.  Global
+// loads and stores are coalesced; the per-thread runs go through LDS.
 __global__ __launch_bounds__(SC_T) void k_scan64_down(const unsigned long long *__restrict__ in, size_t n,
                                                       const unsigned long long *__restrict__ block_off, uint32_t *lo,
                                                       uint32_t *hi) {
+    __shared__ unsigned long long tile[SC_TILE + SC_TILE / 16];
     __shared__ unsigned long long ws[SC_T / WAVE];
-    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_I;
+    const size_t base = (size_t)blockIdx.x * SC_TILE;
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q) {
+        const uint32_t j = (uint32_t)q * SC_T + tid;
+        tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
+    }
+    __syncthreads();
     unsigned long long v[SC_I];
     unsigned long long s = 0;
 #pragma unroll
     for (int q = 0; q < SC_I; ++q) {
-        v[q] = base + q < n ? in[base + q] : 0ull;
+        v[q] = tile[p64(tid * SC_I + (uint32_t)q)];
         s += v[q];
     }
     unsigned long long tot;
     unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot) + block_off[blockIdx.x];
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q)
-        if (base + q < n) {
-            lo[base + q] = (uint32_t)run;
-            hi[base + q] = (uint32_t)(run >> 32);
-            run += v[q];
+    for (int q = 0; q < SC_I; ++q) {  // a thread rewrites only the words it read
+        tile[p64(tid * SC_I + (uint32_t)q)] = run;
+        run += v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < SC_I; ++q) {
+        const uint32_t j = (uint32_t)q * SC_T + tid;
+        if (base + j < n) {
+            const unsigned long long e = tile[p64(j)];
+            lo[base + j] = (uint32_t)e;
+            hi[base + j] = (uint32_t)(e >> 32);
         }
+    }
 }
 
 // Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
@@ -1691,9 +1733,11 @@ __global__ __launch_bounds__(256) void k_neighbors(FrameView F, const SlotInfo *
 // ============================================================ launchers ======
 
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
-                     uint32_t n_spaces, hipStream_t st) {
-    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, 1});
-    k_prologue<<<cdiv(m, 256), 256, 0, st>>>(sc, z0, (uint32_t)n0, z1, (uint32_t)n1, bbox, n_spaces);
+                     uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
+                     SlotSp *s_ss, hipStream_t st) {
+    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, (size_t)n_copy, 1});
+    k_prologue<<<cdiv(m, 256), 256, 0, st>>>(sc, z0, (uint32_t)n0, z1, (uint32_t)n1, bbox, n_spaces, n_copy, p_rec,
+                                             p_ss, s_rec, s_ss);
 }
 
 void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
@@ -1746,11 +1790,12 @@ void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, con
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64);
-    else
+                                           n_prev, blk, p_key, cnt64);  // folded by incremental_sort
+    else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
                                             n_prev, blk, nullptr, nullptr);
-    k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
+        k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
+    }
 }
 
 size_t incr_sort_tmp_elems(size_t cells) { return (size_t)cdiv(cells + 1, SC_TILE) + 1; }
@@ -1758,11 +1803,12 @@ size_t incr_sort_tmp_elems(size_t cells) { return (size_t)cdiv(cells + 1, SC_TIL
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
-                      unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, hipStream_t st) {
+                      unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
+                      TickScalars *sc, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, SC_TILE);
     k_scan64_reduce<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
-    k_scan64_single<<<1, 1024, 0, st>>>(tmp, nb);
+    k_scan64_single<<<1, 1024, 0, st>>>(tmp, nb, blk, cdiv(n_total, 256), sc);
     k_scan64_down<<<nb, SC_T, 0, st>>>(cnt64, m, tmp, cell_start, arr_pos);
     if (n_total) k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,

@@ -557,16 +557,16 @@ int run_tick(gwaoi_world *w) {
         HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * ns, hipMemcpyHostToDevice, st));
         Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
     }
+    // counters, tile totals, bbox fold; S' <- the previous frame (the ops apply onto it)
     if (incr)
         gw::launch_prologue(w->sc, reinterpret_cast<uint32_t *>(w->cnt64), 2 * ((size_t)total_cells + 1), w->tile_total,
-                            entries + 1, dev_bbox(w), w->n_space_ids, st);
+                            entries + 1, dev_bbox(w), w->n_space_ids, n_prev, P.rec, P.ss, w->srec, w->sss, st);
     else
         gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
-                            w->n_space_ids, st);
+                            w->n_space_ids, n_prev, P.rec, P.ss, w->srec, w->sss, st);
 
     // ---- apply queued ops onto S' = copy of the previous frame
     stage_begin(w, ST_APPLY);
-    gw::launch_copy_state(n_prev, P.rec, P.ss, w->srec, w->sss, st);
     if (n_app) {
         HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
@@ -636,7 +636,7 @@ int run_tick(gwaoi_world *w) {
     if (incr) {
         gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             w->keys[1], st);
+                             w->keys[1], w->blk, w->sc, st);
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
