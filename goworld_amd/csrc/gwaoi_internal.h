@@ -54,11 +54,6 @@ struct SpaceGrid {
     uint32_t row_base;
 };
 
-// A pair-pass work unit: entities [e0, e1) of one grid row (at most TILE_A).
-struct Tile {
-    uint32_t e0, e1, row, pad;
-};
-
 // One flush's sorted state: entries [0, n) are the live entities ordered by
 // cell key (space-major, then cz, cx), stable in the previous order.
 struct FrameView {
@@ -70,12 +65,6 @@ struct FrameView {
     uint32_t total_cells;
 };
 
-struct TileSet {  // the pair-pass tiles of one frame
-    const Tile *tiles;
-    const uint32_t *n_tiles;    // device count
-    const uint32_t *row_space;  // space id of every global grid row
-    uint32_t bound;             // host upper bound on *n_tiles (launch size)
-};
 
 // Per-tick scalars written by device kernels.
 struct TickScalars {
@@ -174,14 +163,9 @@ size_t scan_tmp_elems(size_t n);
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
-                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, hipStream_t st);
+                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
+                   uint32_t n_spaces, void *bbox_parts, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
-
-// Tiles of a frame: rows split into runs of <= TILE_A entities.
-// row_ntiles needs n_rows + 1 entries; tiles needs tile_bound(n, n_rows).
-void build_tiles(FrameView F, uint32_t n_space_ids, uint32_t n_rows, uint32_t *row_space, uint32_t *row_ntiles,
-                 Tile *tiles, uint32_t *scan_tmp, hipStream_t st);
-inline uint32_t tile_bound(uint32_t n, uint32_t n_rows) { return (n + TILE_A - 1) / TILE_A + n_rows; }
 
 // Combined pass over the new frame: blocks of TILE_A consecutive entries
 // (O = previous state in the new order, NaN where not live in the same space).
@@ -191,21 +175,21 @@ inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, hipStream_t st);
-// Special-entity pass (mode 1) over the previous frame's tiles (O = S', the
-// new state in the previous order, with O_ss giving its space); tile t's
-// totals/bases at [tile_off + t] and [leave_off + tile_off + t].
-void launch_pairs(int mode, FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, TileSet T, uint64_t seq_base,
-                  TickScalars *sc, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
-                  unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st);
-// Copy every tile's events from tmp into tile order (dest = scanned tile_total).
+// Special-entity pass over the previous frame in blocks of TILE_A entries
+// (O = S', the new state in the previous order, with O_ss giving its space);
+// block t's totals/bases at [tile_off + t] and [leave_off + tile_off + t].
+void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t seq_base, TickScalars *sc,
+                  uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
+                  uint32_t tile_off, uint32_t leave_off, hipStream_t st);
+// Copy every tile's events from tmp into tile order (dest = scanned
+// tile_total) and write the flush's TickOut.
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
                     uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
-                    hipStream_t st);
-void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const TickScalars *sc,
-                   TickOut *out, hipStream_t st);
-// Per-space bounding box into the int4 array that follows TickOut.
+                    uint32_t n_enter_entries, const TickScalars *sc, TickOut *out, hipStream_t st);
+// Per-space bounding box into the int4 array that follows TickOut: k_gather
+// writes the level-1 parts, this folds them.
 size_t bbox_part_bytes(uint32_t n);
-void launch_bbox(FrameView F, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st);
+void launch_bbox(uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);
 // Zero `n` uint32 (rare re-run path).

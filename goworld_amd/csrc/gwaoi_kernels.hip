@@ -106,13 +106,6 @@ __global__ void k_zero(uint32_t *p, size_t n) {
 
 // ------------------------------------------------------------ op apply ------
 
-__global__ void k_copy_state(uint32_t n, const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
-                             Rec16 *s_rec, SlotSp *s_ss) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    reinterpret_cast<uint4 *>(s_rec)[i] = reinterpret_cast<const uint4 *>(p_rec)[i];
-    reinterpret_cast<uint2 *>(s_ss)[i] = reinterpret_cast<const uint2 *>(p_ss)[i];
-}
 
 __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t n_prev,
                                 Rec16 *s_rec, SlotSp *s_ss, SlotInfo *info) {
@@ -791,17 +784,121 @@ __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const ui
     }
 }
 
+// ----------------------------------------------------------------- bbox ------
+
+__device__ __forceinline__ int f2o(float f) {
+    int i = __float_as_int(f);
+    return i ^ ((i >> 31) & 0x7FFFFFFF);
+}
+
+__device__ __forceinline__ void bbox_flush(int4 *bbox, uint32_t ns, uint32_t sp, const int (&v)[4]) {
+    if (sp >= ns) return;
+    int *p = reinterpret_cast<int *>(bbox + sp);
+    atomicMin(p + 0, v[0]);
+    atomicMin(p + 1, v[1]);
+    atomicMax(p + 2, v[2]);
+    atomicMax(p + 3, v[3]);
+}
+
+constexpr uint32_t BB_T = 256;
+
+struct BBoxPart {  // one workgroup's fold: space id (SP_DEAD = nothing left) + ordered-int bbox
+    uint32_t sp;
+    int v[4];
+};
+
+// Fold per-thread (space, bbox) over a workgroup: when every thread ends on
+// the same space the block reduces to one part; otherwise each thread flushes
+// its own run with atomics (only at space boundaries).
+__device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], int4 *bbox, uint32_t ns,
+                                           BBoxPart *out) {
+    __shared__ uint32_t s_sp[BB_T / WAVE];
+    __shared__ int s_v[BB_T / WAVE][4];
+    __shared__ int s_uni;
+    const uint32_t first = __shfl(cur, 0);
+    const bool wuni = __all(cur == first || cur == SP_DEAD);
+    int v[4] = {own[0], own[1], own[2], own[3]};
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        v[0] = min(v[0], __shfl_xor(v[0], o));
+        v[1] = min(v[1], __shfl_xor(v[1], o));
+        v[2] = max(v[2], __shfl_xor(v[2], o));
+        v[3] = max(v[3], __shfl_xor(v[3], o));
+    }
+    const int w = threadIdx.x / WAVE;
+    if (threadIdx.x == 0) s_uni = 1;
+    __syncthreads();
+    if (lane() == 0) {
+        s_sp[w] = wuni ? first : SP_KEEP;
+        s_v[w][0] = v[0];
+        s_v[w][1] = v[1];
+        s_v[w][2] = v[2];
+        s_v[w][3] = v[3];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t bsp = SP_DEAD;
+        int r[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+        for (int q = 0; q < (int)(BB_T / WAVE); ++q) {
+            const uint32_t ws = s_sp[q];
+            if (ws == SP_DEAD) continue;
+            if (ws == SP_KEEP || (bsp != SP_DEAD && ws != bsp)) {
+                s_uni = 0;
+                break;
+            }
+            bsp = ws;
+            r[0] = min(r[0], s_v[q][0]);
+            r[1] = min(r[1], s_v[q][1]);
+            r[2] = max(r[2], s_v[q][2]);
+            r[3] = max(r[3], s_v[q][3]);
+        }
+        out->sp = s_uni ? bsp : SP_DEAD;
+        out->v[0] = r[0];
+        out->v[1] = r[1];
+        out->v[2] = r[2];
+        out->v[3] = r[3];
+    }
+    __syncthreads();
+    if (!s_uni && cur != SP_DEAD) bbox_flush(bbox, ns, cur, own);  // mixed spaces: every run flushes
+}
+
 // --------------------------------------------------------------- gather ------
 
-__global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
+__device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
+                                           const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
+                                           const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
+                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                                           const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
+                                           SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
+                                           uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
+                                           int (&bv)[4]);
+
+// One thread per new-frame entry; the block also folds its entries' bbox
+// (level 1 of the per-space bounding box, k_bbox_parts is level 2).
+__global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
                          SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
                          unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
-                         uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key) {
+                         uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
+                         uint32_t n_spaces, BBoxPart *parts) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
-    if (k >= n_new) return;
+    uint32_t cur = SP_DEAD;
+    int bv[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+    if (k < n_new) gather_one(k, perm, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand, grid, seq_base,
+                              info, sorted_keys, sentinel, n_total, sc, f_key, cur, bv);
+    bbox_block(cur, bv, bbox, n_spaces, &parts[blockIdx.x]);
+}
+
+__device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
+                                           const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
+                                           const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
+                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                                           const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
+                                           SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
+                                           uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
+                                           int (&bv)[4]) {
     const uint32_t key = sorted_keys[k];
     if (key == sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     f_key[k] = key;
@@ -823,6 +920,9 @@ __global__ void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint
     st_rec(o_rec, k, o);
     const float thr = FAR_FRAC * grid[ss.sp].D;
     cand[k] = make_uint4(__float_as_uint(now.x), __float_as_uint(now.z), flags_of(now, o, seq_base, thr), 0u);
+    cur = ss.sp;
+    bv[0] = bv[2] = f2o(now.x);
+    bv[1] = bv[3] = f2o(now.z);
 }
 
 // Entities per cell from the sorted keys: one atomic per run of equal keys
@@ -840,46 +940,6 @@ __global__ void k_cell_count(const uint32_t *__restrict__ keys, uint32_t n, uint
         const uint32_t next = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
         const uint32_t end = next < nvalid ? next : nvalid;
         atomicAdd(&cnt[key], end - l);
-    }
-}
-
-// ---------------------------------------------------------------- tiles ------
-
-__global__ void k_row_space(const SpaceGrid *__restrict__ grid, uint32_t n_spaces, uint32_t *row_space) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_spaces) return;
-    const SpaceGrid g = grid[s];
-    for (uint32_t cz = 0; cz < g.gz; ++cz) row_space[g.row_base + cz] = s;
-}
-
-__global__ void k_row_tiles(FrameView F, const uint32_t *__restrict__ row_space, uint32_t n_rows, uint32_t *cnt) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r > n_rows) return;
-    if (r == n_rows) {
-        cnt[r] = 0;
-        return;
-    }
-    const SpaceGrid g = F.grid[row_space[r]];
-    const uint32_t c0 = g.base + (r - g.row_base) * g.gx;
-    const uint32_t n_row = F.cell_start[c0 + g.gx] - F.cell_start[c0];
-    cnt[r] = (n_row + TILE_A - 1) / TILE_A;
-}
-
-__global__ void k_fill_tiles(FrameView F, const uint32_t *__restrict__ row_space, uint32_t n_rows,
-                             const uint32_t *__restrict__ off, Tile *tiles) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rows) return;
-    const SpaceGrid g = F.grid[row_space[r]];
-    const uint32_t c0 = g.base + (r - g.row_base) * g.gx;
-    const uint32_t b = F.cell_start[c0], e = F.cell_start[c0 + g.gx];
-    uint32_t t = off[r];
-    for (uint32_t k = b; k < e; k += TILE_A, ++t) {
-        Tile T;
-        T.e0 = k;
-        T.e1 = min(k + TILE_A, e);
-        T.row = r;
-        T.pad = 0;
-        tiles[t] = T;
     }
 }
 
@@ -994,8 +1054,7 @@ __device__ void enum_global(const FrameView &F, const Rec16 *O_rec, const SlotSp
 
 template <int MODE>
 __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restrict__ O_rec,
-                                              const SlotSp *__restrict__ O_ss, TileSet TS,
-                                              unsigned long long seq_base, const TickScalars *__restrict__ sc,
+                                              const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
                                               unsigned long long *counter, uint2 *tmp, uint64_t cap,
                                               uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
                                               uint32_t leave_off) {
@@ -1009,21 +1068,23 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
     __shared__ uint32_t s_ws[PT / WAVE];
     __shared__ unsigned long long s_base;
 
-    const uint32_t t = blockIdx.x;
-    if (t >= *TS.n_tiles) return;  // uniform per workgroup
-    const Tile T = TS.tiles[t];
+    __shared__ uint32_t s_spr[2];  // smallest / largest space among the active lanes
+    const uint32_t t = blockIdx.x;  // entries [t*PT, t*PT + PT) of the frame
     const uint32_t tid = threadIdx.x;
-    const SpaceGrid g = F.grid[TS.row_space[T.row]];
-    const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f;
-    const float thr = FAR_FRAC * g.D;
     PairCtx A;
-    A.D = g.D;
-    A.HM = g.D * (1.0f + 2.0f * sc->d_rel) + M;
     A.seq_base = seq_base;
-    A.a = T.e0 + tid;
-    bool active = A.a < T.e1;
+    A.a = t * PT + tid;
+    bool active = A.a < F.n;
+    const uint32_t my_sp = active ? ld_ss(F.ss, A.a).sp : SP_DEAD;
+    SpaceGrid g{};
+    float M = 0.0f, thr = 0.0f;
     int cx0 = 0, cx1 = -1, cz0 = 0, cz1 = -1;
     if (active) {
+        g = F.grid[my_sp];
+        M = (sc->bmax + 3.0f * g.D) * 0x1p-20f;
+        thr = FAR_FRAC * g.D;
+        A.D = g.D;
+        A.HM = g.D * (1.0f + 2.0f * sc->d_rel) + M;
         A.now = ld_rec(F.rec, A.a);
         A.oth = other_rec<MODE>(F, O_rec, O_ss, A.a);
         if (MODE == 2) {
@@ -1046,6 +1107,15 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
         }
     }
     if (MODE == 1 && !__syncthreads_or(active)) return;  // no special entity: totals stay 0
+    if (tid == 0) {
+        s_spr[0] = 0xFFFFFFFFu;
+        s_spr[1] = 0u;
+    }
+    __syncthreads();
+    if (active) {
+        atomicMin(&s_spr[0], my_sp);
+        atomicMax(&s_spr[1], my_sp);
+    }
     // tile box = union of the active entities' query cells
     {
         int v0 = active ? cx0 : INT_MAX, v1 = active ? cx1 : INT_MIN;
@@ -1074,11 +1144,14 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
     }
     const int CX0 = s_box[0], CX1 = s_box[1], CZ0 = s_box[2], CZ1 = s_box[3];
     const int nrows = CZ1 - CZ0 + 1;
-    const bool staged = nrows <= PMAXR;
+    // the LDS path indexes the rows of one grid: all active lanes in one space
+    const bool one_space = s_spr[0] == s_spr[1];
+    const SpaceGrid gb = F.grid[one_space ? s_spr[0] : 0u];
+    const bool staged = one_space && nrows <= PMAXR;
     uint32_t ne = 0, nl = 0, nk = 0;  // enters, leaves, buffered
     if (staged) {
         if ((int)tid < nrows) {
-            const uint32_t row = g.base + (uint32_t)(CZ0 + (int)tid) * g.gx;
+            const uint32_t row = gb.base + (uint32_t)(CZ0 + (int)tid) * gb.gx;
             const uint32_t b = F.cell_start[row + (uint32_t)CX0];
             s_seg[tid] = b;
             s_pre[tid + 1] = F.cell_start[row + (uint32_t)CX1 + 1u] - b;
@@ -1551,7 +1624,15 @@ __global__ __launch_bounds__(256) void k_reorder(const uint32_t *__restrict__ de
                                                  const uint32_t *__restrict__ tile_total,
                                                  const unsigned long long *__restrict__ tile_base,
                                                  uint32_t n_entries, const uint2 *__restrict__ tmp, uint2 *out,
-                                                 uint64_t cap) {
+                                                 uint64_t cap, uint32_t n_enter_entries,
+                                                 const TickScalars *__restrict__ sc, TickOut *res) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the flush's totals (dest is the finished scan)
+        res->n_enter = dest[n_enter_entries];
+        res->n_total = dest[n_entries];
+        res->err = sc->err;
+        res->total64 = sc->counter;
+        res->seq_max = sc->seq_max;
+    }
     const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
     for (uint32_t e = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; e < n_entries; e += waves) {
         const uint32_t cnt = tile_total[e];
@@ -1563,118 +1644,6 @@ __global__ __launch_bounds__(256) void k_reorder(const uint32_t *__restrict__ de
     }
 }
 
-__global__ void k_finish(const uint32_t *__restrict__ dest, uint32_t n_enter_entries, uint32_t n_entries,
-                         const TickScalars *__restrict__ sc, TickOut *res) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    res->n_enter = dest[n_enter_entries];
-    res->n_total = dest[n_entries];
-    res->err = sc->err;
-    res->total64 = sc->counter;
-    res->seq_max = sc->seq_max;
-}
-
-// ----------------------------------------------------------------- bbox ------
-
-__device__ __forceinline__ int f2o(float f) {
-    int i = __float_as_int(f);
-    return i ^ ((i >> 31) & 0x7FFFFFFF);
-}
-
-__device__ __forceinline__ void bbox_flush(int4 *bbox, uint32_t ns, uint32_t sp, const int (&v)[4]) {
-    if (sp >= ns) return;
-    int *p = reinterpret_cast<int *>(bbox + sp);
-    atomicMin(p + 0, v[0]);
-    atomicMin(p + 1, v[1]);
-    atomicMax(p + 2, v[2]);
-    atomicMax(p + 3, v[3]);
-}
-
-constexpr uint32_t BB_PER_THREAD = 16;
-constexpr uint32_t BB_T = 256;
-
-struct BBoxPart {  // one workgroup's fold: space id (SP_DEAD = nothing left) + ordered-int bbox
-    uint32_t sp;
-    int v[4];
-};
-
-// Fold per-thread (space, bbox) over a workgroup: when every thread ends on
-// the same space the block reduces to one part; otherwise each thread flushes
-// its own run with atomics (only at space boundaries).
-__device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], int4 *bbox, uint32_t ns,
-                                           BBoxPart *out) {
-    __shared__ uint32_t s_sp[BB_T / WAVE];
-    __shared__ int s_v[BB_T / WAVE][4];
-    __shared__ int s_uni;
-    const uint32_t first = __shfl(cur, 0);
-    const bool wuni = __all(cur == first || cur == SP_DEAD);
-    int v[4] = {own[0], own[1], own[2], own[3]};
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        v[0] = min(v[0], __shfl_xor(v[0], o));
-        v[1] = min(v[1], __shfl_xor(v[1], o));
-        v[2] = max(v[2], __shfl_xor(v[2], o));
-        v[3] = max(v[3], __shfl_xor(v[3], o));
-    }
-    const int w = threadIdx.x / WAVE;
-    if (threadIdx.x == 0) s_uni = 1;
-    __syncthreads();
-    if (lane() == 0) {
-        s_sp[w] = wuni ? first : SP_KEEP;
-        s_v[w][0] = v[0];
-        s_v[w][1] = v[1];
-        s_v[w][2] = v[2];
-        s_v[w][3] = v[3];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t bsp = SP_DEAD;
-        int r[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
-        for (int q = 0; q < (int)(BB_T / WAVE); ++q) {
-            const uint32_t ws = s_sp[q];
-            if (ws == SP_DEAD) continue;
-            if (ws == SP_KEEP || (bsp != SP_DEAD && ws != bsp)) {
-                s_uni = 0;
-                break;
-            }
-            bsp = ws;
-            r[0] = min(r[0], s_v[q][0]);
-            r[1] = min(r[1], s_v[q][1]);
-            r[2] = max(r[2], s_v[q][2]);
-            r[3] = max(r[3], s_v[q][3]);
-        }
-        out->sp = s_uni ? bsp : SP_DEAD;
-        out->v[0] = r[0];
-        out->v[1] = r[1];
-        out->v[2] = r[2];
-        out->v[3] = r[3];
-    }
-    __syncthreads();
-    if (!s_uni && cur != SP_DEAD) bbox_flush(bbox, ns, cur, own);  // mixed spaces: every run flushes
-}
-
-// Level 1: 16 consecutive entries per thread, runs of one space folded.
-__global__ __launch_bounds__(BB_T) void k_bbox(FrameView F, int4 *bbox, uint32_t ns, BBoxPart *parts) {
-    const uint32_t k0 = (blockIdx.x * BB_T + threadIdx.x) * BB_PER_THREAD;
-    const uint32_t k1 = min(k0 + BB_PER_THREAD, F.n);
-    uint32_t cur = SP_DEAD;
-    int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
-    for (uint32_t k = k0; k < k1; ++k) {
-        const uint32_t sp = ld_ss(F.ss, k).sp;
-        if (sp != cur) {
-            if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
-            cur = sp;
-            v[0] = v[1] = INT_MAX;
-            v[2] = v[3] = INT_MIN;
-        }
-        const Rec16 r = ld_rec(F.rec, k);
-        const int ix = f2o(r.x), iz = f2o(r.z);
-        v[0] = min(v[0], ix);
-        v[1] = min(v[1], iz);
-        v[2] = max(v[2], ix);
-        v[3] = max(v[3], iz);
-    }
-    bbox_block(cur, v, bbox, ns, &parts[blockIdx.x]);
-}
 
 // Level 2: one workgroup folds the level-1 parts (space-sorted).
 __global__ __launch_bounds__(BB_T) void k_bbox_parts(const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
@@ -1744,11 +1713,6 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
     if (n) k_zero<<<cdiv(n, 256), 256, 0, st>>>(p, n);
 }
 
-void launch_copy_state(uint32_t n, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec, SlotSp *s_ss,
-                       hipStream_t st) {
-    if (!n) return;
-    k_copy_state<<<cdiv(n, 256), 256, 0, st>>>(n, p_rec, p_ss, s_rec, s_ss);
-}
 
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
                           SlotInfo *info, hipStream_t st) {
@@ -1860,10 +1824,12 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
-                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, hipStream_t st) {
+                   uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
+                   uint32_t n_spaces, void *bbox_parts, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
     k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand,
-                                            grid, seq_base, info, sorted_keys, sentinel, n_total, sc, f_key);
+                                            grid, seq_base, info, sorted_keys, sentinel, n_total, sc, f_key, bbox,
+                                            n_spaces, reinterpret_cast<BBoxPart *>(bbox_parts));
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {
@@ -1871,22 +1837,14 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
     k_cell_count<<<cdiv(n, 256), 256, 0, st>>>(sorted_keys, n, cnt);
 }
 
-void build_tiles(FrameView F, uint32_t n_space_ids, uint32_t n_rows, uint32_t *row_space, uint32_t *row_ntiles,
-                 Tile *tiles, uint32_t *scan_tmp, hipStream_t st) {
-    if (n_space_ids) k_row_space<<<cdiv(n_space_ids, 256), 256, 0, st>>>(F.grid, n_space_ids, row_space);
-    k_row_tiles<<<cdiv((size_t)n_rows + 1, 256), 256, 0, st>>>(F, row_space, n_rows, row_ntiles);
-    scan_exclusive(row_ntiles, row_ntiles, (size_t)n_rows + 1, scan_tmp, st);
-    if (n_rows) k_fill_tiles<<<cdiv(n_rows, 256), 256, 0, st>>>(F, row_space, n_rows, row_ntiles, tiles);
-}
 
-void launch_pairs(int mode, FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, TileSet T, uint64_t seq_base,
-                  TickScalars *sc, uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total,
-                  unsigned long long *tile_base, uint32_t tile_off, uint32_t leave_off, hipStream_t st) {
-    if (!F.n || !T.bound) return;
+void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t seq_base, TickScalars *sc,
+                  uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
+                  uint32_t tile_off, uint32_t leave_off, hipStream_t st) {
+    if (!F.n) return;
     uint2 *tmp = reinterpret_cast<uint2 *>(tmp_pairs);
-    (void)mode;
-    k_pairs<1><<<T.bound, PT, 0, st>>>(F, O_rec, O_ss, T, seq_base, sc, &sc->counter, tmp, cap, tile_total, tile_base,
-                                       tile_off, leave_off);
+    k_pairs<1><<<combined_blocks(F.n), PT, 0, st>>>(F, O_rec, O_ss, seq_base, sc, &sc->counter, tmp, cap, tile_total,
+                                                    tile_base, tile_off, leave_off);
 }
 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
@@ -1900,27 +1858,20 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
 
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
                     uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
-                    hipStream_t st) {
-    if (!n_entries) return;
-    const uint32_t blocks = std::min<uint32_t>(cdiv(n_entries, 256 / WAVE), 2048);
+                    uint32_t n_enter_entries, const TickScalars *sc, TickOut *out, hipStream_t st) {
+    const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>(cdiv(n_entries, 256 / WAVE), 2048));
     k_reorder<<<blocks, 256, 0, st>>>(dest, tile_total, tile_base, n_entries,
                                       reinterpret_cast<const uint2 *>(tmp_pairs),
-                                      reinterpret_cast<uint2 *>(out_pairs), cap);
+                                      reinterpret_cast<uint2 *>(out_pairs), cap, n_enter_entries, sc, out);
 }
 
-void launch_finish(const uint32_t *dest, uint32_t n_enter_entries, uint32_t n_entries, const TickScalars *sc,
-                   TickOut *out, hipStream_t st) {
-    k_finish<<<1, 64, 0, st>>>(dest, n_enter_entries, n_entries, sc, out);
-}
 
-size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(cdiv(n, BB_PER_THREAD), BB_T) + 1); }
+size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }
 
-void launch_bbox(FrameView F, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st) {
-    if (!F.n) return;
+void launch_bbox(uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st) {
     BBoxPart *parts = reinterpret_cast<BBoxPart *>(parts_mem);
-    const uint32_t nb = cdiv(cdiv(F.n, BB_PER_THREAD), BB_T);
-    k_bbox<<<nb, BB_T, 0, st>>>(F, bbox, n_spaces, parts);
-    k_bbox_parts<<<1, BB_T, 0, st>>>(parts, nb, bbox, n_spaces, parts + nb);
+    const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
+    k_bbox_parts<<<1, BB_T, 0, st>>>(parts, np, bbox, n_spaces, parts + np);
 }
 
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,

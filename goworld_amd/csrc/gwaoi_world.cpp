@@ -28,9 +28,9 @@ using gw::SpaceGrid;
 
 namespace {
 
-enum Stage { ST_APPLY, ST_KEYGEN, ST_SORT, ST_GATHER, ST_CELLS, ST_TILES, ST_COMBINED, ST_SPECIAL, ST_REORDER,
-             ST_BBOX, ST_D2H, ST_N };
-const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",    "gather", "cells", "tiles",
+enum Stage { ST_APPLY, ST_KEYGEN, ST_SORT, ST_GATHER, ST_CELLS, ST_COMBINED, ST_SPECIAL, ST_REORDER, ST_BBOX,
+             ST_D2H, ST_N };
+const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",    "gather", "cells",
                                  "combined", "special", "reorder", "bbox",   "d2h"};
 
 struct DevFrame {
@@ -43,13 +43,6 @@ struct DevFrame {
     std::vector<SpaceGrid> hgrid;  // host mirror of `grid` (upload only on change)
     uint32_t n = 0;
     uint32_t total_cells = 0;
-    // pair-pass tiles of this frame
-    uint32_t *row_space = nullptr, *row_ntiles = nullptr;
-    size_t row_cap = 0;
-    gw::Tile *tiles = nullptr;
-    size_t tile_cap = 0;
-    uint32_t n_rows = 0;
-    uint32_t tile_bound = 0;
 };
 
 struct SpaceHost {
@@ -237,32 +230,6 @@ int ensure_events(gwaoi_world *w, uint64_t pairs) {
     return GWAOI_OK;
 }
 
-int ensure_tiles(gwaoi_world *w, DevFrame &f, uint32_t n_rows, uint32_t bound) {
-    if ((size_t)n_rows + 1 > f.row_cap) {
-        size_t cap = std::max<size_t>((size_t)n_rows + 1 + n_rows / 4, 256);
-        HIP_TRY(hipStreamSynchronize(w->stream));
-        dfree(f.row_space);
-        dfree(f.row_ntiles);
-        int rc;
-        if ((rc = dalloc(w, &f.row_space, cap)) || (rc = dalloc(w, &f.row_ntiles, cap))) {
-            f.row_cap = 0;
-            return rc;
-        }
-        f.row_cap = cap;
-    }
-    if (bound > f.tile_cap) {
-        size_t cap = std::max<size_t>(bound + bound / 4, 256);
-        HIP_TRY(hipStreamSynchronize(w->stream));
-        dfree(f.tiles);
-        int rc = dalloc(w, &f.tiles, cap);
-        if (rc) {
-            f.tile_cap = 0;
-            return rc;
-        }
-        f.tile_cap = cap;
-    }
-    return GWAOI_OK;
-}
 
 int ensure_tile_entries(gwaoi_world *w, size_t entries) {
     if (entries + 1 <= w->tile_entries_cap) return GWAOI_OK;
@@ -487,27 +454,26 @@ gw::TickOut *tick_out(gwaoi_world *w) { return reinterpret_cast<gw::TickOut *>(w
 const int4 *tick_bbox(gwaoi_world *w) { return reinterpret_cast<const int4 *>(w->h_out + sizeof(gw::TickOut)); }
 int4 *dev_bbox(gwaoi_world *w) { return reinterpret_cast<int4 *>(w->dev_out + sizeof(gw::TickOut)); }
 
-// Pair passes + deterministic reorder.  Tile-total entries: [enter totals:
-// new-frame tiles | previous-frame tiles] then [leave totals: same order];
-// their exclusive scan is the final layout [enters | leaves] in tile order.
+// Pair passes + deterministic reorder.  Block-total entries: [enter totals:
+// new-frame blocks | previous-frame blocks] then [leave totals: same order];
+// their exclusive scan is the final layout [enters | leaves] in block order.
 void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_base) {
     hipStream_t st = w->stream;
-    const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = P.n ? P.tile_bound : 0;
+    const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
-    gw::TileSet Tp{P.tiles, P.row_ntiles + P.n_rows, P.row_space, TBp};
     stage_begin(w, ST_COMBINED);
     gw::launch_combined(Vn, w->cand, w->orec, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
                         half, st);
     stage_end(w, ST_COMBINED);
     stage_begin(w, ST_SPECIAL);
-    gw::launch_pairs(1, Vp, w->srec, w->sss, Tp, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total,
-                     w->tile_base, TBn, half, st);
+    gw::launch_pairs(Vp, w->srec, w->sss, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
+                     TBn, half, st);
     stage_end(w, ST_SPECIAL);
     stage_begin(w, ST_REORDER);
     gw::scan_exclusive(w->tile_total, w->tile_dest, (size_t)entries + 1, w->scan_tmp, st);
-    gw::launch_reorder(w->tile_dest, w->tile_total, w->tile_base, entries, w->events_tmp, w->events, w->ev_cap, st);
-    gw::launch_finish(w->tile_dest, half, entries, w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), st);
+    gw::launch_reorder(w->tile_dest, w->tile_total, w->tile_base, entries, w->events_tmp, w->events, w->ev_cap, half,
+                       w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), st);
     stage_end(w, ST_REORDER);
 }
 
@@ -526,14 +492,11 @@ int run_tick(gwaoi_world *w) {
     const uint32_t n_total = n_prev + n_app;
     const uint32_t n_new = w->n_alive;
 
-    // grid + tiles for this flush
+    // grid for this flush
     uint32_t total_cells = 0, total_rows = 0;
     choose_grids(w, total_cells, total_rows);
-    const uint32_t tbound = gw::tile_bound(n_new, total_rows);
-    const uint32_t TBp = P.n ? P.tile_bound : 0;
-    const size_t entries = 2 * ((size_t)gw::combined_blocks(n_new) + TBp);
+    const size_t entries = 2 * ((size_t)gw::combined_blocks(n_new) + gw::combined_blocks(n_prev));
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
-    if ((rc = ensure_tiles(w, Fn, total_rows, tbound))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
     size_t host_ops = 0;
     for (const Run &r : w->runs)
@@ -544,8 +507,6 @@ int run_tick(gwaoi_world *w) {
     if ((rc = ensure_scan_tmp(w, scan_need))) return rc;
     Fn.total_cells = total_cells;
     Fn.n = n_new;
-    Fn.n_rows = total_rows;
-    Fn.tile_bound = tbound;
 
     const uint32_t ns = std::max(1u, w->n_space_ids);
     const bool grid_same = Fn.hgrid.size() == ns && !std::memcmp(Fn.hgrid.data(), w->h_grid, ns * sizeof(SpaceGrid));
@@ -655,7 +616,7 @@ int run_tick(gwaoi_world *w) {
     stage_begin(w, ST_GATHER);
     gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
-                      total_cells, n_total, w->sc, Fn.key, st);
+                      total_cells, n_total, w->sc, Fn.key, dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
     stage_end(w, ST_GATHER);
 
     // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
@@ -666,17 +627,13 @@ int run_tick(gwaoi_world *w) {
         gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
         stage_end(w, ST_CELLS);
     }
-    stage_begin(w, ST_TILES);
-    gw::build_tiles(view_of(Fn), grid_same ? 0u : w->n_space_ids, total_rows, Fn.row_space, Fn.row_ntiles, Fn.tiles,
-                    w->scan_tmp, st);
-    stage_end(w, ST_TILES);
 
     // ---- pair passes: combined over the new grid, special entities over the previous one
     launch_pair_passes(w, Fn, P, seq_base);
 
     // ---- per-space bounding boxes for the next flush's grid
     stage_begin(w, ST_BBOX);
-    gw::launch_bbox(view_of(Fn), dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
+    gw::launch_bbox(n_new, dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
     stage_end(w, ST_BBOX);
     HIP_TRY(hipGetLastError());
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
@@ -784,7 +741,6 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     for (DevFrame &f : w->fr) {
         dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.grid);
-        dfree(f.row_space); dfree(f.row_ntiles); dfree(f.tiles);
     }
     dfree(w->srec); dfree(w->sss); dfree(w->orec); dfree(w->cand);
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
@@ -859,7 +815,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
-    if ((rc = ensure_tile_entries(w, 2 * (size_t)gw::tile_bound((uint32_t)N, 1024)))) return fail(rc);
+    if ((rc = ensure_tile_entries(w, 4 * (size_t)gw::combined_blocks((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     if ((rc = ensure_events(w, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
         return fail(rc);
