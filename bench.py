@@ -76,6 +76,68 @@ def pmc_traffic(workload: str):
     return d.get("hbm_bytes_per_launch")
 
 
+SYNC_REC = np.dtype([("id", "V16"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("yaw", "<f4")])
+
+
+def entity_ids(slots: np.ndarray) -> np.ndarray:
+    """16-byte entity ids (common.ENTITYID_LENGTH) for slots: b"E" + 15 decimal digits."""
+    ids = np.char.add(b"E", np.char.zfill(slots.astype(np.int64).astype("S15"), 15))
+    return np.frombuffer(ids.astype("S16").tobytes(), np.uint8).reshape(-1, 16)
+
+
+def sync_leg(w, n: int, batches, client_frac: float):
+    """The per-tick position-sync path around the AOI flush (include/gwaoi_sync.h):
+    HandleSyncPositionYawFromClient packets (32-B records, every entity once, seeded
+    order) already in HBM -> GPU decode into the move batch -> flush ->
+    CollectEntitySyncInfos fan-out into per-gate 48-B records left in HBM.
+    Entities 0..n-1 get ids; a `client_frac` share has a client on one of 8 gates."""
+    import torch
+    slots = np.arange(n, dtype=np.uint32)
+    w.entity_bind(slots, entity_ids(slots))
+    rng = np.random.default_rng(0x5EED5C)
+    has_client = rng.random(n) < client_frac
+    for s in np.nonzero(has_client)[0]:
+        w.entity_set_client(int(s), 1 + int(s) % 8, b"C" + b"%015d" % int(s))
+    for s in range(n):
+        w.entity_set_syncing(s, True)
+    pays = []
+    for sl, nx, nz in batches:
+        r = np.zeros(sl.size, SYNC_REC)
+        r["id"] = entity_ids(sl).view("V16").reshape(-1)
+        r["x"], r["z"] = nx, nz
+        r["y"] = 1.0
+        r["yaw"] = rng.uniform(-3.1, 3.1, sl.size).astype(np.float32)
+        pays.append(torch.from_numpy(r.view(np.uint8).copy()).to(f"cuda:{torch.cuda.current_device()}"))
+    torch.cuda.synchronize()
+    # first packet + flush + collect untimed (clears the flags that entity binding left)
+    w.sync_from_clients_device(pays[0].data_ptr(), batches[0][0].size)
+    w.tick_device()
+    w.collect_sync_infos_device()
+    w.sync()
+    t_tick = t_col = 0.0
+    recs = moves = 0
+    for k in range(1, len(pays)):
+        a = time.perf_counter()
+        w.sync_from_clients_device(pays[k].data_ptr(), batches[k][0].size)
+        w.tick_device()
+        w.sync()
+        b = time.perf_counter()
+        ids, off, _ = w.collect_sync_infos_device()
+        w.sync()
+        c = time.perf_counter()
+        t_tick += b - a
+        t_col += c - b
+        recs += off[-1]
+        moves += batches[k][0].size
+    k = max(1, len(pays) - 1)
+    return {"steps": k, "clients": int(has_client.sum()), "gates": 8,
+            "decode_flush_ms": t_tick / k * 1e3, "moves_per_s": moves / t_tick,
+            "collect_ms": t_col / k * 1e3, "records_per_tick": recs / k,
+            "records_per_s": recs / t_col, "record_write_GBps": recs * 48 / t_col / 1e9,
+            "note": "client packets decoded on the GPU (hash lookup of 16-B ids), flush, then "
+                    "CollectEntitySyncInfos into per-gate 48-B records in HBM; wall clock per phase"}
+
+
 def cpu_baseline(args, wl_factory, target_s: float):
     """go-aoi XZListAOIManager restatement (oracle/xzlist.c), one core, timed on
     a prefix of tick 0's move batch of the same workload."""
@@ -236,6 +298,11 @@ def main():
     ap.add_argument("--breakdown-steps", type=int, default=10,
                     help="extra ticks after the timed region with every stage timed by HIP events")
     ap.add_argument("--cells-per-dist", type=float, default=0.0)
+    ap.add_argument("--sync-steps", type=int, default=5,
+                    help="extra ticks through the entity-sync path: client packets decoded in HBM, flush, "
+                         "CollectEntitySyncInfos fan-out (0 = off)")
+    ap.add_argument("--sync-clients", type=float, default=0.5,
+                    help="fraction of entities with a client (players) in the sync leg")
     ap.add_argument("--host-io-steps", type=int, default=10,
                     help="extra ticks timed with host move batches in and host event arrays out (PCIe-inclusive)")
     args = ap.parse_args()
@@ -286,6 +353,8 @@ def main():
         sl, nx, nz = wl.tick(t)
         batches.append((sl, nx, nz))
     host_batches = [wl.tick(ticks + t) for t in range(hio)]  # PCIe-inclusive leg (host memory)
+    sync_steps = max(0, args.sync_steps) if ws == 1 or args.workload != "cfg4" else 0
+    sync_batches = [wl.tick(ticks + hio + t) for t in range(sync_steps + 1 if sync_steps else 0)]
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
     d_x = torch.from_numpy(np.stack([b[1] for b in batches])).to(f"cuda:{device}")
     d_z = torch.from_numpy(np.stack([b[2] for b in batches])).to(f"cuda:{device}")
@@ -371,6 +440,7 @@ def main():
                    "events_per_s": h_evs / h_el, "steps": hio,
                    "note": "moves from host memory (H2D) + events copied to host arrays (D2H) per tick; "
                            "not the headline value"}
+    sync = sync_leg(w, n, sync_batches, args.sync_clients) if sync_batches else None
     elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], red_dev)
 
     if rank == 0:
@@ -427,6 +497,7 @@ def main():
             "setup_s": round(setup_s, 2),
             "roofline": roofline,
             "pcie_inclusive": host_io,
+            "sync_leg": sync,
             "stages_ms_per_tick": {k: round(v, 4) for k, v in stage_ms.items()},
             "stages_note": f"separate {bd} ticks after the timed region, every stage bracketed by HIP events "
                            "(the events add ~0.07 ms per tick, so these sum above ms_per_step)",

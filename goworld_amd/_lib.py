@@ -42,6 +42,18 @@ STRIP_EXPORTS = [
     "gwaoi_strips_last_error",
 ]
 
+# every function include/gwaoi_sync.h declares
+SYNC_EXPORTS = [
+    "gwaoi_entity_bind", "gwaoi_entity_bind_batch", "gwaoi_entity_unbind", "gwaoi_entity_set_client",
+    "gwaoi_entity_set_syncing", "gwaoi_entity_set_position_yaw", "gwaoi_set_position_yaw",
+    "gwaoi_sync_from_clients", "gwaoi_sync_from_clients_device", "gwaoi_collect_sync_infos",
+    "gwaoi_collect_sync_infos_device", "gwaoi_collect_client_events",
+]
+
+SYNC_OUT_REC = 48  # ClientID[16] + EntityID[16] + x,y,z,yaw float32 (Entity.go:1233-1251)
+DESTROY_REC = 32   # ClientID[16] + EntityID[16]
+SIF_OWN_CLIENT, SIF_NEIGHBOR_CLIENTS = 1, 2
+
 
 class Config(C.Structure):
     _fields_ = [("max_slots", C.c_uint32), ("max_spaces", C.c_uint32), ("device", C.c_int32),
@@ -62,6 +74,11 @@ class Info(C.Structure):
 class StripsConfig(C.Structure):
     _fields_ = [("n_strips", C.c_uint32), ("rank", C.c_uint32), ("edges", C.c_void_p),
                 ("aoi_distance", C.c_float), ("teleport", C.c_float)]
+
+
+class GateRecords(C.Structure):
+    _fields_ = [("n_gates", C.c_uint32), ("gate_ids", C.POINTER(C.c_uint16)),
+                ("offsets", C.POINTER(C.c_uint64)), ("records", C.c_void_p)]
 
 
 class StageTime(C.Structure):
@@ -128,6 +145,18 @@ def load():
         "gwaoi_strips_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_strips_events": ([vp, P(Events)], C.c_int),
         "gwaoi_strips_last_error": ([vp], C.c_char_p),
+        "gwaoi_entity_bind": ([vp, u32, vp], C.c_int),
+        "gwaoi_entity_bind_batch": ([vp, vp, vp, sz], C.c_int),
+        "gwaoi_entity_unbind": ([vp, u32], C.c_int),
+        "gwaoi_entity_set_client": ([vp, u32, C.c_uint16, vp], C.c_int),
+        "gwaoi_entity_set_syncing": ([vp, u32, C.c_int], C.c_int),
+        "gwaoi_entity_set_position_yaw": ([vp, u32, f, f, f, f], C.c_int),
+        "gwaoi_set_position_yaw": ([vp, u32, f, f, f, f], C.c_int),
+        "gwaoi_sync_from_clients": ([vp, vp, sz], C.c_int),
+        "gwaoi_sync_from_clients_device": ([vp, vp, sz], C.c_int),
+        "gwaoi_collect_sync_infos": ([vp, P(GateRecords)], C.c_int),
+        "gwaoi_collect_sync_infos_device": ([vp, P(GateRecords)], C.c_int),
+        "gwaoi_collect_client_events": ([vp, P(GateRecords), P(GateRecords)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -287,6 +316,88 @@ class World:
 
     def stream(self) -> int:
         return self._L.gwaoi_stream(self._w) or 0
+
+    # ---- entity position sync (include/gwaoi_sync.h)
+    def entity_bind(self, slots, eids):
+        """Bind slots to 16-byte entity ids: eids is (n,16) uint8 or a list of 16-byte bytes."""
+        s = np.ascontiguousarray(np.atleast_1d(slots), np.uint32)
+        e = _ids(eids, s.size)
+        self._check(self._L.gwaoi_entity_bind_batch(self._w, _p(s), _p(e), s.size))
+
+    def entity_unbind(self, slot):
+        self._check(self._L.gwaoi_entity_unbind(self._w, slot))
+
+    def entity_set_client(self, slot, gate_id=0, clientid=None):
+        if clientid is None:
+            self._check(self._L.gwaoi_entity_set_client(self._w, slot, 0, None))
+        else:
+            c = _ids([clientid], 1)
+            self._check(self._L.gwaoi_entity_set_client(self._w, slot, gate_id, _p(c)))
+
+    def entity_set_syncing(self, slot, syncing=True):
+        self._check(self._L.gwaoi_entity_set_syncing(self._w, slot, 1 if syncing else 0))
+
+    def entity_set_position_yaw(self, slot, x, y, z, yaw):
+        self._check(self._L.gwaoi_entity_set_position_yaw(self._w, slot, C.c_float(x), C.c_float(y),
+                                                          C.c_float(z), C.c_float(yaw)))
+
+    def set_position_yaw(self, slot, x, y, z, yaw):
+        self._check(self._L.gwaoi_set_position_yaw(self._w, slot, C.c_float(x), C.c_float(y), C.c_float(z),
+                                                   C.c_float(yaw)))
+
+    def sync_from_clients(self, payload):
+        """Decode a HandleSyncPositionYawFromClient payload (bytes / uint8 array, 32 B per record)."""
+        b = np.frombuffer(bytes(payload), np.uint8) if not isinstance(payload, np.ndarray) else \
+            np.ascontiguousarray(payload, np.uint8).reshape(-1)
+        if b.size % 32:
+            raise ValueError("payload is not a whole number of 32-byte records")
+        self._check(self._L.gwaoi_sync_from_clients(self._w, _p(b), b.size // 32))
+
+    def sync_from_clients_device(self, d_payload: int, n_rec: int):
+        self._check(self._L.gwaoi_sync_from_clients_device(self._w, C.c_void_p(d_payload), n_rec))
+
+    def collect_sync_infos(self) -> dict:
+        """CollectEntitySyncInfos: {gate_id: (n,48) uint8 records}."""
+        g = GateRecords()
+        self._check(self._L.gwaoi_collect_sync_infos(self._w, C.byref(g)))
+        return _gate_dict(g, SYNC_OUT_REC)
+
+    def collect_sync_infos_device(self):
+        """Records stay in HBM: (gate_ids, offsets (records), device pointer)."""
+        g = GateRecords()
+        self._check(self._L.gwaoi_collect_sync_infos_device(self._w, C.byref(g)))
+        ids = [g.gate_ids[i] for i in range(g.n_gates)]
+        off = [g.offsets[i] for i in range(g.n_gates + 1)] if g.n_gates else [0]
+        return ids, off, g.records or 0
+
+    def collect_client_events(self):
+        """Events routed to clients: ({gate: (n,48) create records}, {gate: (n,32) destroy records})."""
+        c, d = GateRecords(), GateRecords()
+        self._check(self._L.gwaoi_collect_client_events(self._w, C.byref(c), C.byref(d)))
+        return _gate_dict(c, SYNC_OUT_REC), _gate_dict(d, DESTROY_REC)
+
+
+def _ids(ids, n) -> np.ndarray:
+    if isinstance(ids, np.ndarray):
+        a = np.ascontiguousarray(ids, np.uint8).reshape(-1, 16)
+    else:
+        a = np.frombuffer(b"".join(bytes(i) for i in ids), np.uint8).reshape(-1, 16)
+    if a.shape[0] != n:
+        raise ValueError(f"expected {n} ids of 16 bytes")
+    return np.ascontiguousarray(a)
+
+
+def _gate_dict(g: GateRecords, rec: int) -> dict:
+    out = {}
+    if not g.n_gates:
+        return out
+    total = g.offsets[g.n_gates]
+    buf = np.ctypeslib.as_array(C.cast(g.records, C.POINTER(C.c_uint8)), shape=(total * rec,)).copy() \
+        if total else np.empty(0, np.uint8)
+    for i in range(g.n_gates):
+        a, b = g.offsets[i], g.offsets[i + 1]
+        out[g.gate_ids[i]] = buf[a * rec:b * rec].reshape(-1, rec)
+    return out
 
 
 def pair_keys(pairs: np.ndarray) -> np.ndarray:

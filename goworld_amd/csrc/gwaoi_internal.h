@@ -5,10 +5,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct gwaoi_world;  // include/gwaoi.h
+
 namespace gw {
 
 constexpr uint32_t SP_DEAD = 0xFFFFFFFFu;  // slot not live (or left this tick)
 constexpr uint32_t SP_KEEP = 0xFFFFFFFEu;  // device move: keep the space of the previous flush
+constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // op placeholder (skipped decoded sync record): no op
 
 // Device-side validation flags (bit set = problem seen during the tick).
 constexpr uint32_t ERR_NONFINITE = 1u;
@@ -115,6 +118,7 @@ struct MoveRun {
     const uint32_t *ds;
     const float *dx, *dz;
     const unsigned long long *dseq;  // explicit seqs (nullptr: seq0 + i)
+    const uint32_t *dsp;             // explicit space per op (nullptr: keep the slot's space)
     unsigned long long seq0;
     uint32_t j0, n;  // first op index in the flush, ops
 };
@@ -123,8 +127,8 @@ struct MoveRuns {
     uint32_t count;
 };
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
-                  uint64_t seq_floor, Rec16 *s_rec, const Rec16 *p_rec, uint32_t n_prev, TickScalars *sc,
-                  uint32_t *coll, hipStream_t st);
+                  uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
+                  TickScalars *sc, uint32_t *coll, hipStream_t st);
 
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
 // partials in blk, 2 * cdiv(n, 256) floats).  cnt64 != nullptr (grid
@@ -194,5 +198,29 @@ void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t
                       uint32_t *count, hipStream_t st);
 // Zero `n` uint32 (rare re-run path).
 void launch_zero(uint32_t *p, size_t n, hipStream_t st);
+
+// ---- world accessors for the entity-sync layer (gwaoi_sync.cpp) -------------
+struct SyncState;
+struct WorldView {
+    FrameView F;           // frame of the last flush
+    const SlotInfo *info;  // per slot: .rank = index in F for slots in F
+    hipStream_t st;
+    uint32_t max_slots;
+    size_t pending_ops;     // calls queued since the last flush
+    const uint32_t *events; // last flush's events (device): [enters | leaves] as (a,b) pairs
+    uint64_t n_enter, n_leave;
+};
+WorldView world_view(gwaoi_world *w);
+SyncState *&world_sync(gwaoi_world *w);
+void world_set_error(gwaoi_world *w, const char *msg);
+// Queue a device Moved batch whose ops carry their space (a decoded position
+// packet): op i moves d_slots[i] in space d_sp[i]; SLOT_NONE ops are no-ops.
+int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
+                        const uint32_t *d_sp, size_t n);
+// Space of a slot in call order (as queued so far), SP_DEAD if not in one.
+uint32_t world_slot_space(gwaoi_world *w, uint32_t slot);
+// Hooks the world calls when a sync layer is attached.
+void sync_note_slot(SyncState *s, uint32_t slot, uint32_t space_or_dead);
+void sync_destroy(SyncState *s);
 
 }  // namespace gw

@@ -24,6 +24,7 @@
 // window bounds must be plain float32 sums as in go-aoi (`coord - aoidist`).
 
 #include "gwaoi_internal.h"
+#include "gwaoi_device.h"
 
 #include <algorithm>
 
@@ -37,42 +38,6 @@ __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << la
 
 inline uint32_t cdiv(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 
-// Monotone non-decreasing in v (IEEE sub/mul round monotonically; clamp is
-// monotone).  keygen and every query use this one function.
-__device__ __forceinline__ int cell_of(float v, float o, float inv, uint32_t g) {
-    float t = (v - o) * inv;
-    t = fmaxf(t, 0.0f);
-    t = fminf(t, (float)(g - 1));
-    return (int)t;
-}
-
-__device__ __forceinline__ Rec16 ld_rec(const Rec16 *p, uint32_t i) {
-    const uint4 q = reinterpret_cast<const uint4 *>(p)[i];
-    Rec16 r;
-    r.x = __uint_as_float(q.x);
-    r.z = __uint_as_float(q.y);
-    r.s = ((unsigned long long)q.w << 32) | q.z;
-    return r;
-}
-
-__device__ __forceinline__ void st_rec(Rec16 *p, uint32_t i, const Rec16 &r) {
-    reinterpret_cast<uint4 *>(p)[i] =
-        make_uint4(__float_as_uint(r.x), __float_as_uint(r.z), (uint32_t)r.s, (uint32_t)(r.s >> 32));
-}
-
-__device__ __forceinline__ SlotSp ld_ss(const SlotSp *p, uint32_t i) {
-    const uint2 q = reinterpret_cast<const uint2 *>(p)[i];
-    SlotSp r;
-    r.slot = q.x;
-    r.sp = q.y;
-    return r;
-}
-
-__device__ __forceinline__ void st_ss(SlotSp *p, uint32_t i, uint32_t slot, uint32_t sp) {
-    reinterpret_cast<uint2 *>(p)[i] = make_uint2(slot, sp);
-}
-
-__device__ __forceinline__ float qnan() { return __int_as_float(0x7FC00000); }
 
 // ------------------------------------------------------------- prologue ------
 
@@ -126,6 +91,7 @@ __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slots[i];
+    if (s == SLOT_NONE) return;  // placeholder of a skipped decoded record
     if (s >= max_slots) {
         atomicOr(&sc->err, ERR_BAD_SLOT);
         return;
@@ -211,20 +177,23 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
 // `coll` (by whichever op sees the other's claim) and k_moves_fixup rewrites
 // it from the final winner after this kernel has drained.
 __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                              unsigned long long seq_floor, Rec16 *s_rec, TickScalars *sc, uint32_t *coll) {
+                              unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc,
+                              uint32_t *coll) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long smax = 0;
     if (i < R.n) {
         const uint32_t s = R.ds[i];
-        if (s >= max_slots) {
+        if (s == SLOT_NONE) {
+            // placeholder of a skipped decoded record: no op
+        } else if (s >= max_slots) {
             atomicOr(&sc->err, ERR_BAD_SLOT);
         } else {
             const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
             const unsigned long long old = atomicMax(&info[s].lastop, mine);
             if ((uint32_t)(old >> 32) == tick) coll[atomicAdd(&sc->ncoll, 1u)] = s;
             if (old < mine)
-                smax = op_apply_one(R.ds, R.dx, R.dz, nullptr, i, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
-                                    seq_floor, s_rec, nullptr, sc, false);
+                smax = op_apply_one(R.ds, R.dx, R.dz, R.dsp, i, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
+                                    seq_floor, s_rec, s_ss, sc, false);
         }
     }
     if (R.dseq) {  // one atomic per wave, not per op
@@ -237,7 +206,7 @@ __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uin
 }
 
 __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                              unsigned long long seq_floor, Rec16 *s_rec, const Rec16 *__restrict__ p_rec,
+                              unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
                               uint32_t n_prev, TickScalars *sc, const uint32_t *__restrict__ coll) {
     const uint32_t nc = sc->ncoll;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
@@ -249,8 +218,8 @@ __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, u
         const MoveRun &R = RS.r[q];
         // start from the previous state so that a dropped (invalid) winner leaves it unchanged
         if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
-        op_apply_one(R.ds, R.dx, R.dz, nullptr, j - R.j0, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
-                     seq_floor, s_rec, nullptr, sc, true);
+        op_apply_one(R.ds, R.dx, R.dz, R.dsp, j - R.j0, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
+                     seq_floor, s_rec, s_ss, sc, true);
     }
 }
 
@@ -969,14 +938,6 @@ constexpr int PS = 4;            // events buffered in LDS per thread
 constexpr int PMAXR = 32;        // candidate rows a tile may span (else global path)
 constexpr uint32_t KIND_LEAVE = 0x80000000u;
 
-// go-aoi relation: the owner (larger seq) W's window [fl32(w-D), fl32(w+D)]^2 contains the other
-__device__ __forceinline__ bool rel(float xa, float za, unsigned long long sa, float xb, float zb,
-                                    unsigned long long sb, float D) {
-    const bool own = sa > sb;
-    const float wx = own ? xa : xb, wz = own ? za : zb;
-    const float px = own ? xb : xa, pz = own ? zb : za;
-    return (int)(px >= wx - D) & (int)(px <= wx + D) & (int)(pz >= wz - D) & (int)(pz <= wz + D);
-}
 
 struct PairCtx {
     Rec16 now, oth;  // MODE 2: t, t-1 (NaN if absent);  MODE 1: t-1, t (NaN if absent)
@@ -1280,16 +1241,6 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 // go-aoi test (pair_kind<2>) with lanes over queue entries.  Events are
 // buffered per wave in processing order (deterministic); a wave whose buffer
 // overflows replays its sweep and writes the rest straight to the output.
-
-// Workgroups are dispatched round-robin over the 8 XCDs, each with its own
-// L2.  Neighbouring blocks read the same candidate rows, so give every XCD a
-// contiguous run of blocks: XCD x (bid % 8 == x) takes blocks
-// [x*q + min(x, r), ...) in order, q = nb / 8, r = nb % 8.
-constexpr uint32_t N_XCD = 8;
-__device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t nb) {
-    const uint32_t x = bid % N_XCD, k = bid / N_XCD, q = nb / N_XCD, r = nb % N_XCD;
-    return x * q + min(x, r) + k;
-}
 
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
@@ -1721,14 +1672,14 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_
 }
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
-                  uint64_t seq_floor, Rec16 *s_rec, const Rec16 *p_rec, uint32_t n_prev, TickScalars *sc,
-                  uint32_t *coll, hipStream_t st) {
+                  uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
+                  TickScalars *sc, uint32_t *coll, hipStream_t st) {
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
             k_moves_apply<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id, n_total, seq_floor,
-                                                                s_rec, sc, coll);
-    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, p_rec, n_prev, sc,
-                                      coll);
+                                                                s_rec, s_ss, sc, coll);
+    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
+                                      sc, coll);
 }
 
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info,

@@ -1,0 +1,1022 @@
+// gwaoi_sync.hip -- entity position sync around the AOI path (include/gwaoi_sync.h).
+//
+// Three device passes, all on the world's stream:
+//   decode    HandleSyncPositionYawFromClient (GameService.go:392-404): one
+//             lane per 32-B record, entity-id hash lookup, the record becomes
+//             op i of a device Moved batch (SLOT_NONE = skipped), Y/yaw by
+//             last-writer claim, sifSyncNeighborClients.
+//   fan-out   CollectEntitySyncInfos (Entity.go:1221-1267): one lane per
+//             frame entity A with flags; a record to A's own client and one
+//             to the client of every B with rel(A,B) (the go-aoi relation of
+//             the last flush == A.InterestedBy), grouped by gate.
+//   route     Entity.interest/uninterest -> sendCreateEntity/sendDestroyEntity
+//             (Entity.go:236-246, GameClient.go:37-59): the flush's events
+//             whose first entity has a client, grouped by gate.
+// Grouping by gate is a two-pass multisplit: pass 0 counts records per
+// (gate, block) in LDS, an exclusive scan gives every (gate, block) its
+// base, pass 1 recomputes and writes through LDS cursors.  The output is HBM
+// write bound (48 B per record); the fan-out enumerates each flagged
+// entity's window twice (count, write), like the reference's map walk.
+
+#include "gwaoi_device.h"
+#include "gwaoi_internal.h"
+#include "../../include/gwaoi_sync.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace gw {
+namespace {
+
+constexpr uint32_t NO_GATE = 0xFFFFFFFFu;
+constexpr uint32_t H_EMPTY = 0xFFFFFFFFu;  // hash bucket never used
+constexpr uint32_t H_TOMB = 0xFFFFFFFEu;   // hash bucket freed
+constexpr int ST = 256;                    // threads per workgroup of the sync kernels
+
+inline uint32_t cdivu(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Hash of a 16-byte id (host and device agree).
+__host__ __device__ inline uint32_t id_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    unsigned long long h = (((unsigned long long)b << 32) | a) * 0x9E3779B97F4A7C15ull;
+    h ^= (((unsigned long long)d << 32) | c) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    return (uint32_t)h;
+}
+
+__device__ __forceinline__ bool eq4(uint4 a, uint4 b) {
+    return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+
+// ------------------------------------------------------------ scatter ------
+// Host-side state changes reach the device as (array, index, value) writes.
+constexpr int MAX_ARR = 8;
+struct ArrTable {
+    void *p[MAX_ARR];
+};
+struct W32 {
+    uint32_t arr, idx, val, pad;
+};
+struct W128 {
+    uint32_t arr, idx, pad0, pad1;
+    uint4 val;
+};
+
+__global__ void k_scatter32(const W32 *__restrict__ w, uint32_t n, ArrTable T) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const W32 e = w[i];
+    static_cast<uint32_t *>(T.p[e.arr])[e.idx] = e.val;
+}
+
+__global__ void k_scatter128(const W128 *__restrict__ w, uint32_t n, ArrTable T) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const W128 e = w[i];
+    static_cast<uint4 *>(T.p[e.arr])[e.idx] = e.val;
+}
+
+// Host position/yaw writes (set_position_yaw, entity_set_position_yaw) and
+// flag-only ops (Space.enter): claim, then the winner writes.
+struct SideOp {
+    uint32_t slot, bits;
+    unsigned long long claim;
+    float4 pos;  // x, y, z, yaw
+};
+
+__global__ void k_side_claim(const SideOp *__restrict__ ops, uint32_t n, unsigned long long *sclaim,
+                             uint32_t *sflags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SideOp o = ops[i];
+    atomicMax(&sclaim[o.slot], o.claim);
+    if (o.bits) atomicOr(&sflags[o.slot], o.bits);
+}
+
+__global__ void k_side_write(const SideOp *__restrict__ ops, uint32_t n, const unsigned long long *sclaim,
+                             float4 *pos) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SideOp o = ops[i];
+    if (o.claim && sclaim[o.slot] == o.claim) pos[o.slot] = o.pos;  // claim 0: flags only
+}
+
+// ------------------------------------------------------------- decode ------
+struct DecodeArgs {
+    const uint4 *pay;  // 2 uint4 per record: id, (x, y, z, yaw) bits
+    uint32_t n;
+    const uint4 *hkey;
+    const uint32_t *hval;
+    uint32_t hmask;
+    const uint32_t *qspace, *syncing;
+    uint32_t *o_slot, *o_sp;
+    float *o_x, *o_z;
+    unsigned long long claim0;
+    unsigned long long *sclaim;
+    uint32_t *sflags;
+    float4 *pos;
+};
+
+__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ hkey, const uint32_t *__restrict__ hval,
+                                           uint32_t hmask, uint4 id) {
+    uint32_t h = id_hash(id.x, id.y, id.z, id.w) & hmask;
+    for (uint32_t probe = 0; probe <= hmask; ++probe, h = (h + 1) & hmask) {
+        const uint32_t v = hval[h];
+        if (v == H_EMPTY) return SLOT_NONE;
+        if (v != H_TOMB && eq4(hkey[h], id)) return v;
+    }
+    return SLOT_NONE;
+}
+
+// OnSyncPositionYawFromClient: unknown id -> skip (EntityManager.go:486-490);
+// syncPositionYawFromClient: only if syncing (Entity.go:432); setPositionYaw:
+// space nil -> skip (Entity.go:1190-1194).
+__global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint4 id = A.pay[2 * (size_t)i];
+    const uint4 pv = A.pay[2 * (size_t)i + 1];
+    uint32_t s = lookup(A.hkey, A.hval, A.hmask, id);
+    uint32_t sp = SP_DEAD;
+    if (s != SLOT_NONE) {
+        sp = A.qspace[s];
+        if (!A.syncing[s] || sp == SP_DEAD) s = SLOT_NONE;
+    }
+    A.o_slot[i] = s;
+    A.o_x[i] = __uint_as_float(pv.x);
+    A.o_z[i] = __uint_as_float(pv.z);
+    A.o_sp[i] = sp;
+    if (s != SLOT_NONE) {
+        atomicMax(&A.sclaim[s], A.claim0 + i);
+        atomicOr(&A.sflags[s], (uint32_t)GWAOI_SIF_NEIGHBOR_CLIENTS);
+    }
+}
+
+__global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint32_t s = A.o_slot[i];
+    if (s == SLOT_NONE || A.sclaim[s] != A.claim0 + i) return;
+    const uint4 pv = A.pay[2 * (size_t)i + 1];
+    A.pos[s] = make_float4(__uint_as_float(pv.x), __uint_as_float(pv.y), __uint_as_float(pv.z),
+                           __uint_as_float(pv.w));
+}
+
+// ------------------------------------------------------------ fan-out ------
+struct FanArgs {
+    FrameView F;
+    const uint32_t *left;  // slots that left since the last collect (own-client records only)
+    uint32_t n_left;
+    const uint4 *eid, *cid;
+    const uint32_t *cgate;
+    uint32_t *sflags;
+    const float4 *pos;
+    uint32_t G, nb;
+    uint32_t *blk_cnt;      // [G][nb] (pass 0 writes, the scan turns it into bases)
+    uint4 *out;             // 3 uint4 per record (pass 1)
+};
+
+template <int PASS>
+__device__ __forceinline__ void fan_emit(const FanArgs &A, uint32_t *lds, uint32_t g, const uint4 &client,
+                                         const uint4 &rec1, const uint4 &rec2) {
+    const uint32_t p = atomicAdd(&lds[g], 1u);
+    if (PASS == 1) {
+        uint4 *o = A.out + 3 * (size_t)p;
+        o[0] = client;
+        o[1] = rec1;
+        o[2] = rec2;
+    }
+}
+
+template <int PASS>
+__global__ __launch_bounds__(ST) void k_fanout(FanArgs A) {
+    extern __shared__ uint32_t lds[];  // per gate: count (pass 0) / cursor (pass 1)
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
+        lds[g] = PASS == 0 ? 0u : A.blk_cnt[(size_t)g * A.nb + blk];
+    __syncthreads();
+    const uint32_t i = blk * ST + threadIdx.x;
+    const uint32_t nf = A.F.n;
+    if (i < nf + A.n_left) {
+        const bool in_frame = i < nf;
+        Rec16 R;
+        uint32_t sA, sp = SP_DEAD;
+        if (in_frame) {
+            R = ld_rec(A.F.rec, i);
+            const SlotSp q = ld_ss(A.F.ss, i);
+            sA = q.slot;
+            sp = q.sp;
+        } else {
+            sA = A.left[i - nf];
+        }
+        const uint32_t fl = A.sflags[sA];
+        if (fl) {
+            if (PASS == 1) A.sflags[sA] = 0u;
+            const uint4 rec1 = A.eid[sA];
+            // the frame holds the AOI position; an entity that left uses its last sync position
+            const float4 P = A.pos[sA];
+            const uint4 rec2 = make_uint4(__float_as_uint(in_frame ? R.x : P.x), __float_as_uint(P.y),
+                                          __float_as_uint(in_frame ? R.z : P.z), __float_as_uint(P.w));
+            if (fl & GWAOI_SIF_OWN_CLIENT) {
+                const uint32_t g = A.cgate[sA];
+                if (g != NO_GATE) fan_emit<PASS>(A, lds, g, A.cid[sA], rec1, rec2);
+            }
+            if ((fl & GWAOI_SIF_NEIGHBOR_CLIENTS) && in_frame) {
+                const SpaceGrid gr = A.F.grid[sp];
+                const float D = gr.D;
+                const float mx = (fabsf(R.x) + 3.0f * D) * 0x1p-20f, mz = (fabsf(R.z) + 3.0f * D) * 0x1p-20f;
+                const int cx0 = cell_of(R.x - D - mx, gr.ox, gr.inv, gr.gx);
+                const int cx1 = cell_of(R.x + D + mx, gr.ox, gr.inv, gr.gx);
+                const int cz0 = cell_of(R.z - D - mz, gr.oz, gr.inv, gr.gz);
+                const int cz1 = cell_of(R.z + D + mz, gr.oz, gr.inv, gr.gz);
+                for (int cz = cz0; cz <= cz1; ++cz) {
+                    const uint32_t row = gr.base + (uint32_t)cz * gr.gx;
+                    const uint32_t jb = A.F.cell_start[row + (uint32_t)cx0];
+                    const uint32_t je = A.F.cell_start[row + (uint32_t)cx1 + 1u];
+                    for (uint32_t b = jb; b < je; ++b) {
+                        if (b == i) continue;
+                        const Rec16 B = ld_rec(A.F.rec, b);
+                        if (!rel(R.x, R.z, R.s, B.x, B.z, B.s, D)) continue;
+                        const uint32_t sB = ld_ss(A.F.ss, b).slot;
+                        const uint32_t g = A.cgate[sB];
+                        if (g != NO_GATE) fan_emit<PASS>(A, lds, g, A.cid[sB], rec1, rec2);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (PASS == 0)
+        for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) A.blk_cnt[(size_t)g * A.nb + blk] = lds[g];
+}
+
+// -------------------------------------------------------------- route ------
+struct RouteArgs {
+    const uint32_t *ev;  // (a,b) pairs: [enters | leaves]
+    uint32_t n_enter, n_total;
+    FrameView F;
+    const SlotInfo *info;
+    const uint4 *eid, *cid;
+    const uint32_t *cgate;
+    const float4 *pos;
+    uint32_t G, nb;
+    uint32_t *blk_cnt;  // [2][G][nb]: creates then destroys
+    uint4 *out_c;       // 3 uint4 per create record
+    uint4 *out_d;       // 2 uint4 per destroy record
+    uint32_t split;     // destroy bases start at split (one scan over both parts)
+};
+
+template <int PASS>
+__global__ __launch_bounds__(ST) void k_route(RouteArgs A) {
+    extern __shared__ uint32_t lds[];  // [2][G]
+    const uint32_t blk = blockIdx.x;
+    for (uint32_t g = threadIdx.x; g < 2 * A.G; g += blockDim.x)
+        lds[g] = PASS == 0 ? 0u : A.blk_cnt[(size_t)g * A.nb + blk];
+    __syncthreads();
+    const uint32_t e = blk * ST + threadIdx.x;
+    if (e < A.n_total) {
+        const uint2 ab = reinterpret_cast<const uint2 *>(A.ev)[e];
+        const uint32_t g = A.cgate[ab.x];
+        if (g != NO_GATE) {
+            const bool create = e < A.n_enter;
+            const uint32_t p = atomicAdd(&lds[(create ? 0u : A.G) + g], 1u);
+            if (PASS == 1) {
+                if (create) {
+                    const uint32_t r = A.info[ab.y].rank;  // b is live after the flush
+                    const Rec16 B = ld_rec(A.F.rec, r);
+                    const float4 P = A.pos[ab.y];
+                    uint4 *o = A.out_c + 3 * (size_t)p;
+                    o[0] = A.cid[ab.x];
+                    o[1] = A.eid[ab.y];
+                    o[2] = make_uint4(__float_as_uint(B.x), __float_as_uint(P.y), __float_as_uint(B.z),
+                                      __float_as_uint(P.w));
+                } else {
+                    uint4 *o = A.out_d + 2 * (size_t)(p - A.split);
+                    o[0] = A.cid[ab.x];
+                    o[1] = A.eid[ab.y];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (PASS == 0)
+        for (uint32_t g = threadIdx.x; g < 2 * A.G; g += blockDim.x) A.blk_cnt[(size_t)g * A.nb + blk] = lds[g];
+}
+
+// offsets[k] = scanned[k * nb] for k in [0, parts]; scanned has parts*nb + 1 entries
+__global__ void k_part_offsets(const uint32_t *__restrict__ scanned, uint32_t parts, uint32_t nb,
+                               unsigned long long *off) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k <= parts) off[k] = scanned[(size_t)k * nb];
+}
+
+}  // namespace
+
+// ======================================================== host state ======
+
+struct SyncState {
+    gwaoi_world *w = nullptr;
+    hipStream_t st = nullptr;
+    uint32_t max_slots = 0;
+    // device, per slot
+    uint4 *eid = nullptr, *cid = nullptr;
+    uint32_t *cgate = nullptr, *qspace = nullptr, *syncing = nullptr, *sflags = nullptr;
+    float4 *pos = nullptr;
+    unsigned long long *sclaim = nullptr;
+    // id -> slot hash table (device, host mirror)
+    uint4 *hkey = nullptr;
+    uint32_t *hval = nullptr;
+    uint32_t hcap = 0, hused = 0;  // buckets, live + tombstones
+    std::vector<uint4> h_hkey;
+    std::vector<uint32_t> h_hval;
+    // host mirrors
+    std::vector<uint4> h_eid;
+    std::vector<uint8_t> h_bound, h_client;
+    std::vector<uint32_t> h_bucket;  // slot -> its hash bucket (if bound)
+    std::unordered_map<uint32_t, uint32_t> gate_idx;  // gate id -> dense index
+    std::vector<uint16_t> gate_ids;
+    // pending device writes
+    std::vector<W32> w32;
+    std::vector<W128> w128;
+    std::vector<SideOp> side;
+    std::vector<uint32_t> left;  // slots that left since the last collect
+    unsigned long long claim_next = 1;
+    // staging (pinned host + device), reused once the previous upload has landed
+    void *h_stage = nullptr, *d_stage = nullptr;
+    size_t stage_cap = 0;
+    hipEvent_t stage_ev = nullptr;
+    bool stage_pending = false;
+    // decode arenas: alive until the flush that consumes them
+    struct Chunk {
+        char *p;
+        size_t cap, used;
+    };
+    std::vector<Chunk> arena;
+    uint64_t arena_tick = ~0ull;
+    // collect scratch / outputs
+    uint32_t *blk_cnt = nullptr, *scan_tmp = nullptr;
+    size_t blk_cap = 0, scan_cap = 0;
+    unsigned long long *d_off = nullptr;
+    size_t off_cap = 0;
+    uint32_t *d_left = nullptr;
+    size_t left_cap = 0;
+    uint4 *out = nullptr, *out_d = nullptr;
+    size_t out_cap = 0, outd_cap = 0;  // in uint4
+    std::vector<unsigned long long> h_off_raw;
+    std::vector<uint64_t> h_off, h_off_c, h_off_d;
+    uint8_t *h_rec = nullptr, *h_rec_d = nullptr;
+    size_t h_rec_cap = 0, h_recd_cap = 0;
+};
+
+namespace {
+
+template <class T>
+int salloc(SyncState *S, T **p, size_t n) {
+    *p = nullptr;
+    if (hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        world_set_error(S->w, "sync: hipMalloc failed");
+        return GWAOI_ENOMEM;
+    }
+    return GWAOI_OK;
+}
+template <class T>
+void sfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+#define SY_TRY(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            world_set_error(S->w, (std::string(#expr) + ": " + hipGetErrorString(e_)).c_str()); \
+            return GWAOI_EDEVICE;                                                        \
+        }                                                                                \
+    } while (0)
+
+enum Arr { A_CGATE, A_QSPACE, A_SYNCING, A_SFLAGS, A_HVAL, A_N32 };
+enum Arr128 { B_EID, B_CID, B_HKEY, B_N128 };
+
+ArrTable table32(SyncState *S) {
+    ArrTable T{};
+    T.p[A_CGATE] = S->cgate;
+    T.p[A_QSPACE] = S->qspace;
+    T.p[A_SYNCING] = S->syncing;
+    T.p[A_SFLAGS] = S->sflags;
+    T.p[A_HVAL] = S->hval;
+    return T;
+}
+ArrTable table128(SyncState *S) {
+    ArrTable T{};
+    T.p[B_EID] = S->eid;
+    T.p[B_CID] = S->cid;
+    T.p[B_HKEY] = S->hkey;
+    return T;
+}
+
+void put32(SyncState *S, Arr a, uint32_t idx, uint32_t v) { S->w32.push_back(W32{(uint32_t)a, idx, v, 0}); }
+void put128(SyncState *S, Arr128 a, uint32_t idx, uint4 v) { S->w128.push_back(W128{(uint32_t)a, idx, 0, 0, v}); }
+
+int ensure_stage(SyncState *S, size_t bytes) {
+    if (S->stage_pending) {
+        SY_TRY(hipEventSynchronize(S->stage_ev));
+        S->stage_pending = false;
+    }
+    if (bytes <= S->stage_cap) return GWAOI_OK;
+    if (S->h_stage) (void)hipHostFree(S->h_stage);
+    sfree(S->d_stage);
+    S->h_stage = nullptr;
+    S->stage_cap = 0;
+    const size_t cap = std::max<size_t>(bytes + bytes / 2, 1 << 16);
+    SY_TRY(hipHostMalloc(&S->h_stage, cap, hipHostMallocDefault));
+    if (int rc = salloc(S, (char **)&S->d_stage, cap)) return rc;
+    S->stage_cap = cap;
+    return GWAOI_OK;
+}
+
+// Keep the last write per (array, index): one scatter launch has no order.
+template <class T>
+void last_wins(std::vector<T> &v) {
+    if (v.size() < 2) return;
+    std::vector<uint32_t> ord(v.size());
+    for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    auto key = [&](uint32_t i) { return ((unsigned long long)v[i].arr << 32) | v[i].idx; };
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+    std::vector<T> out;
+    out.reserve(v.size());
+    for (size_t k = 0; k < ord.size(); ++k)
+        if (k + 1 == ord.size() || key(ord[k + 1]) != key(ord[k])) out.push_back(v[ord[k]]);
+    v.swap(out);
+}
+
+// Upload the pending host-side writes and Y/yaw ops (stream order).
+int push(SyncState *S) {
+    last_wins(S->w32);
+    last_wins(S->w128);
+    const size_t b32 = S->w32.size() * sizeof(W32), b128 = S->w128.size() * sizeof(W128);
+    const size_t bside = S->side.size() * sizeof(SideOp);
+    const size_t total = b128 + b32 + bside;
+    if (!total) return GWAOI_OK;
+    if (int rc = ensure_stage(S, total)) return rc;
+    char *h = static_cast<char *>(S->h_stage);
+    char *d = static_cast<char *>(S->d_stage);
+    std::memcpy(h, S->w128.data(), b128);
+    std::memcpy(h + b128, S->w32.data(), b32);
+    std::memcpy(h + b128 + b32, S->side.data(), bside);
+    SY_TRY(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, S->st));
+    SY_TRY(hipEventRecord(S->stage_ev, S->st));
+    S->stage_pending = true;
+    // 128-bit writes first (hash keys before the values that publish them)
+    if (!S->w128.empty())
+        k_scatter128<<<cdivu(S->w128.size(), ST), ST, 0, S->st>>>(reinterpret_cast<const W128 *>(d),
+                                                                   (uint32_t)S->w128.size(), table128(S));
+    if (!S->w32.empty())
+        k_scatter32<<<cdivu(S->w32.size(), ST), ST, 0, S->st>>>(reinterpret_cast<const W32 *>(d + b128),
+                                                                 (uint32_t)S->w32.size(), table32(S));
+    if (!S->side.empty()) {
+        const SideOp *o = reinterpret_cast<const SideOp *>(d + b128 + b32);
+        const uint32_t n = (uint32_t)S->side.size();
+        k_side_claim<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->sflags);
+        k_side_write<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->pos);
+    }
+    SY_TRY(hipGetLastError());
+    S->w32.clear();
+    S->w128.clear();
+    S->side.clear();
+    return GWAOI_OK;
+}
+
+int create(gwaoi_world *w, SyncState **out) {
+    SyncState *S = new (std::nothrow) SyncState();
+    if (!S) return GWAOI_ENOMEM;
+    const WorldView v = world_view(w);
+    S->w = w;
+    S->st = v.st;
+    S->max_slots = v.max_slots;
+    uint32_t cap = 1024;
+    while (cap < 2ull * v.max_slots) cap <<= 1;
+    S->hcap = cap;
+    const size_t N = v.max_slots;
+    int rc;
+    if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->cgate, N)) ||
+        (rc = salloc(S, &S->qspace, N)) || (rc = salloc(S, &S->syncing, N)) || (rc = salloc(S, &S->sflags, N)) ||
+        (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->sclaim, N)) || (rc = salloc(S, &S->hkey, cap)) ||
+        (rc = salloc(S, &S->hval, cap))) {
+        sync_destroy(S);
+        return rc;
+    }
+    bool ok = hipMemsetAsync(S->cgate, 0xFF, N * 4, S->st) == hipSuccess &&
+              hipMemsetAsync(S->syncing, 0, N * 4, S->st) == hipSuccess &&
+              hipMemsetAsync(S->sflags, 0, N * 4, S->st) == hipSuccess &&
+              hipMemsetAsync(S->pos, 0, N * 16, S->st) == hipSuccess &&
+              hipMemsetAsync(S->sclaim, 0, N * 8, S->st) == hipSuccess &&
+              hipMemsetAsync(S->eid, 0, N * 16, S->st) == hipSuccess &&
+              hipMemsetAsync(S->cid, 0, N * 16, S->st) == hipSuccess &&
+              hipMemsetAsync(S->hval, 0xFF, (size_t)cap * 4, S->st) == hipSuccess &&
+              hipEventCreateWithFlags(&S->stage_ev, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        sync_destroy(S);
+        return GWAOI_EDEVICE;
+    }
+    // space of every slot in call order (the world may hold entities already)
+    std::vector<uint32_t> qs(N);
+    for (uint32_t s = 0; s < N; ++s) qs[s] = world_slot_space(w, s);
+    if (hipMemcpyAsync(S->qspace, qs.data(), N * 4, hipMemcpyHostToDevice, S->st) != hipSuccess ||
+        hipStreamSynchronize(S->st) != hipSuccess) {
+        sync_destroy(S);
+        return GWAOI_EDEVICE;
+    }
+    S->h_hkey.assign(cap, make_uint4(0, 0, 0, 0));
+    S->h_hval.assign(cap, H_EMPTY);
+    S->h_eid.assign(N, make_uint4(0, 0, 0, 0));
+    S->h_bound.assign(N, 0);
+    S->h_client.assign(N, 0);
+    S->h_bucket.assign(N, H_EMPTY);
+    *out = S;
+    return GWAOI_OK;
+}
+
+int state(gwaoi_world *w, SyncState **out) {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *&S = world_sync(w);
+    if (!S) {
+        if (int rc = create(w, &S)) return rc;
+    }
+    *out = S;
+    return GWAOI_OK;
+}
+
+uint4 load_id(const uint8_t *p) {
+    uint4 v;
+    std::memcpy(&v, p, 16);
+    return v;
+}
+
+bool same(const uint4 &a, const uint4 &b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
+
+// bucket of id, or H_EMPTY
+uint32_t h_find(const SyncState *S, const uint4 &id) {
+    const uint32_t mask = S->hcap - 1;
+    uint32_t h = id_hash(id.x, id.y, id.z, id.w) & mask;
+    for (uint32_t p = 0; p < S->hcap; ++p, h = (h + 1) & mask) {
+        const uint32_t v = S->h_hval[h];
+        if (v == H_EMPTY) return H_EMPTY;
+        if (v != H_TOMB && same(S->h_hkey[h], id)) return h;
+    }
+    return H_EMPTY;
+}
+
+// Rebuild the table without tombstones and upload it whole.
+int h_rehash(SyncState *S) {
+    std::fill(S->h_hval.begin(), S->h_hval.end(), H_EMPTY);
+    S->hused = 0;
+    const uint32_t mask = S->hcap - 1;
+    for (uint32_t s = 0; s < S->max_slots; ++s) {
+        if (!S->h_bound[s]) continue;
+        const uint4 id = S->h_eid[s];
+        uint32_t h = id_hash(id.x, id.y, id.z, id.w) & mask;
+        while (S->h_hval[h] != H_EMPTY) h = (h + 1) & mask;
+        S->h_hkey[h] = id;
+        S->h_hval[h] = s;
+        S->h_bucket[s] = h;
+        S->hused++;
+    }
+    // drop pending table writes: the whole table goes up now (after the other pending writes)
+    std::vector<W32> k32;
+    for (const W32 &e : S->w32)
+        if (e.arr != A_HVAL) k32.push_back(e);
+    S->w32.swap(k32);
+    std::vector<W128> k128;
+    for (const W128 &e : S->w128)
+        if (e.arr != B_HKEY) k128.push_back(e);
+    S->w128.swap(k128);
+    if (int rc = push(S)) return rc;
+    SY_TRY(hipMemcpyAsync(S->hkey, S->h_hkey.data(), (size_t)S->hcap * 16, hipMemcpyHostToDevice, S->st));
+    SY_TRY(hipMemcpyAsync(S->hval, S->h_hval.data(), (size_t)S->hcap * 4, hipMemcpyHostToDevice, S->st));
+    return GWAOI_OK;
+}
+
+int bind_one(SyncState *S, uint32_t slot, const uint4 &id) {
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    const uint32_t hb = h_find(S, id);
+    if (S->h_bound[slot]) return (hb != H_EMPTY && S->h_hval[hb] == slot) ? GWAOI_OK : GWAOI_ESTATE;
+    if (hb != H_EMPTY) return GWAOI_ESTATE;  // id bound to another slot
+    if (S->hused + 1 > S->hcap / 4 * 3) {
+        // too many tombstones (live entries are <= max_slots <= hcap/2)
+        if (int rc = h_rehash(S)) return rc;
+    }
+    const uint32_t mask = S->hcap - 1;
+    uint32_t h = id_hash(id.x, id.y, id.z, id.w) & mask;
+    while (S->h_hval[h] != H_EMPTY && S->h_hval[h] != H_TOMB) h = (h + 1) & mask;
+    if (S->h_hval[h] == H_EMPTY) S->hused++;
+    S->h_hkey[h] = id;
+    S->h_hval[h] = slot;
+    S->h_bucket[slot] = h;
+    S->h_bound[slot] = 1;
+    S->h_eid[slot] = id;
+    put128(S, B_HKEY, h, id);
+    put32(S, A_HVAL, h, slot);
+    put128(S, B_EID, slot, id);
+    return GWAOI_OK;
+}
+
+int ensure_u32(SyncState *S, uint32_t **p, size_t *cap, size_t n) {
+    if (n <= *cap) return GWAOI_OK;
+    sfree(*p);
+    *cap = 0;
+    const size_t c = std::max<size_t>(n + n / 4, 1024);
+    if (int rc = salloc(S, p, c)) return rc;
+    *cap = c;
+    return GWAOI_OK;
+}
+
+// (device) records, grown to n uint4
+int ensure_out(SyncState *S, uint4 **p, size_t *cap, size_t n) {
+    if (n <= *cap) return GWAOI_OK;
+    sfree(*p);
+    *cap = 0;
+    const size_t c = std::max<size_t>(n + n / 8, 3 * 1024);
+    if (int rc = salloc(S, p, c)) return rc;
+    *cap = c;
+    return GWAOI_OK;
+}
+
+int ensure_host(SyncState *S, uint8_t **p, size_t *cap, size_t bytes) {
+    if (bytes <= *cap) return GWAOI_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t c = std::max<size_t>(bytes + bytes / 8, 1 << 16);
+    SY_TRY(hipHostMalloc((void **)p, c, hipHostMallocDefault));
+    *cap = c;
+    return GWAOI_OK;
+}
+
+// Multisplit bases: blk_cnt [parts][nb] -> exclusive scan (parts*nb + 1
+// entries, the last is the total) -> h_off_raw[0..parts].
+int part_bases(SyncState *S, uint32_t parts, uint32_t nb) {
+    const size_t n = (size_t)parts * nb + 1;
+    if (int rc = ensure_u32(S, &S->scan_tmp, &S->scan_cap, scan_tmp_elems(n) + 4)) return rc;
+    if (parts + 1 > S->off_cap) {
+        sfree(S->d_off);
+        if (int rc = salloc(S, &S->d_off, parts + 1)) return rc;
+        S->off_cap = parts + 1;
+    }
+    scan_exclusive(S->blk_cnt, S->blk_cnt, n, S->scan_tmp, S->st);
+    k_part_offsets<<<cdivu(parts + 1, ST), ST, 0, S->st>>>(S->blk_cnt, parts, nb, S->d_off);
+    SY_TRY(hipGetLastError());
+    S->h_off_raw.resize(parts + 1);
+    SY_TRY(hipMemcpyAsync(S->h_off_raw.data(), S->d_off, (parts + 1) * 8, hipMemcpyDeviceToHost, S->st));
+    SY_TRY(hipStreamSynchronize(S->st));
+    return GWAOI_OK;
+}
+
+void fill_out(SyncState *S, gwaoi_gate_records *o, const std::vector<uint64_t> &off, const uint8_t *rec) {
+    o->n_gates = (uint32_t)S->gate_ids.size();
+    o->gate_ids = S->gate_ids.data();
+    o->offsets = off.data();
+    o->records = rec;
+}
+
+int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
+    if (!w || !out) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = state(w, &S)) return rc;
+    const WorldView v = world_view(w);
+    if (v.pending_ops) return GWAOI_ESTATE;
+    if (int rc = push(S)) return rc;
+    // own-client records of flagged entities that left (deduplicated, still out of every space)
+    std::vector<uint32_t> left;
+    std::sort(S->left.begin(), S->left.end());
+    S->left.erase(std::unique(S->left.begin(), S->left.end()), S->left.end());
+    for (uint32_t s : S->left)
+        if (world_slot_space(w, s) == SP_DEAD) left.push_back(s);
+    S->left.clear();
+    if (!left.empty()) {
+        if (int rc = ensure_u32(S, &S->d_left, &S->left_cap, left.size())) return rc;
+        SY_TRY(hipMemcpyAsync(S->d_left, left.data(), left.size() * 4, hipMemcpyHostToDevice, S->st));
+    }
+    const uint32_t G = (uint32_t)S->gate_ids.size();
+    const uint32_t n_ent = v.F.n + (uint32_t)left.size();
+    const uint32_t nb = std::max(1u, cdivu(n_ent, ST));
+    FanArgs A{};
+    A.F = v.F;
+    A.left = S->d_left;
+    A.n_left = (uint32_t)left.size();
+    A.eid = S->eid;
+    A.cid = S->cid;
+    A.cgate = S->cgate;
+    A.sflags = S->sflags;
+    A.pos = S->pos;
+    A.G = G;
+    A.nb = nb;
+    if (int rc = ensure_u32(S, &S->blk_cnt, &S->blk_cap, (size_t)G * nb + 1)) return rc;
+    A.blk_cnt = S->blk_cnt;
+    const size_t lds = std::max<size_t>(G, 1) * 4;
+    uint64_t total = 0;
+    S->h_off_raw.assign(1, 0);
+    if (G) {
+        SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
+        k_fanout<0><<<nb, ST, lds, S->st>>>(A);
+        SY_TRY(hipGetLastError());
+        if (int rc = part_bases(S, G, nb)) return rc;
+        total = S->h_off_raw[G];
+    }
+    if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;
+    A.out = S->out;
+    k_fanout<1><<<nb, ST, lds, S->st>>>(A);  // also clears the flags
+    SY_TRY(hipGetLastError());
+    S->h_off.assign(S->h_off_raw.begin(), S->h_off_raw.end());
+    if (to_host) {
+        if (int rc = ensure_host(S, &S->h_rec, &S->h_rec_cap, std::max<uint64_t>(total, 1) * 48)) return rc;
+        if (total) SY_TRY(hipMemcpyAsync(S->h_rec, S->out, total * 48, hipMemcpyDeviceToHost, S->st));
+        SY_TRY(hipStreamSynchronize(S->st));
+        fill_out(S, out, S->h_off, S->h_rec);
+    } else {
+        fill_out(S, out, S->h_off, reinterpret_cast<const uint8_t *>(S->out));
+    }
+    return GWAOI_OK;
+}
+
+int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
+    if (!w || (n && !payload)) return GWAOI_EINVAL;
+    if (on_device && (reinterpret_cast<uintptr_t>(payload) & 15u)) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = state(w, &S)) return rc;
+    if (!n) return GWAOI_OK;
+    if (n > 0x7FFFFFFFull) return GWAOI_EINVAL;
+    // arena of the current flush (older chunks were consumed by earlier flushes)
+    uint64_t ticks_now;
+    {
+        gwaoi_info inf;
+        gwaoi_world_info(w, &inf);
+        ticks_now = inf.ticks;
+    }
+    if (S->arena_tick != ticks_now) {
+        if (S->arena.size() > 1) {  // keep the largest chunk only
+            SY_TRY(hipStreamSynchronize(S->st));
+            std::sort(S->arena.begin(), S->arena.end(),
+                      [](const SyncState::Chunk &a, const SyncState::Chunk &b) { return a.cap > b.cap; });
+            for (size_t k = 1; k < S->arena.size(); ++k) (void)hipFree(S->arena[k].p);
+            S->arena.resize(1);
+        }
+        for (auto &c : S->arena) c.used = 0;
+        S->arena_tick = ticks_now;
+    }
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t need = 4 * al(n * 4) + (on_device ? 0 : al(n * 32));
+    SyncState::Chunk *ch = nullptr;
+    for (auto &c : S->arena)
+        if (c.cap - c.used >= need) {
+            ch = &c;
+            break;
+        }
+    if (!ch) {
+        SyncState::Chunk c{nullptr, std::max<size_t>(need, 1 << 20), 0};
+        SY_TRY(hipMalloc((void **)&c.p, c.cap));
+        S->arena.push_back(c);
+        ch = &S->arena.back();
+    }
+    char *base = ch->p + ch->used;
+    ch->used += need;
+    uint32_t *o_slot = reinterpret_cast<uint32_t *>(base);
+    float *o_x = reinterpret_cast<float *>(base + al(n * 4));
+    float *o_z = reinterpret_cast<float *>(base + 2 * al(n * 4));
+    uint32_t *o_sp = reinterpret_cast<uint32_t *>(base + 3 * al(n * 4));
+    const uint4 *pay;
+    if (on_device) {
+        pay = reinterpret_cast<const uint4 *>(payload);
+    } else {
+        char *dp = base + 4 * al(n * 4);
+        SY_TRY(hipMemcpyAsync(dp, payload, n * 32, hipMemcpyHostToDevice, S->st));
+        pay = reinterpret_cast<const uint4 *>(dp);
+    }
+    if (int rc = push(S)) return rc;
+    DecodeArgs A{};
+    A.pay = pay;
+    A.n = (uint32_t)n;
+    A.hkey = S->hkey;
+    A.hval = S->hval;
+    A.hmask = S->hcap - 1;
+    A.qspace = S->qspace;
+    A.syncing = S->syncing;
+    A.o_slot = o_slot;
+    A.o_sp = o_sp;
+    A.o_x = o_x;
+    A.o_z = o_z;
+    A.claim0 = S->claim_next;
+    A.sclaim = S->sclaim;
+    A.sflags = S->sflags;
+    A.pos = S->pos;
+    S->claim_next += n;
+    k_decode<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+    k_decode_yaw<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+    SY_TRY(hipGetLastError());
+    return world_queue_decoded(w, o_slot, o_x, o_z, o_sp, n);
+}
+
+}  // namespace
+
+void sync_note_slot(SyncState *S, uint32_t slot, uint32_t space_or_dead) {
+    put32(S, A_QSPACE, slot, space_or_dead);
+    if (space_or_dead == SP_DEAD)
+        S->left.push_back(slot);
+    else  // Space.enter: syncInfoFlag |= sifSyncOwnClient | sifSyncNeighborClients (Space.go:205)
+        S->side.push_back(SideOp{slot, GWAOI_SIF_OWN_CLIENT | GWAOI_SIF_NEIGHBOR_CLIENTS, 0ull,
+                                 make_float4(0.f, 0.f, 0.f, 0.f)});
+}
+
+void sync_destroy(SyncState *S) {
+    if (!S) return;
+    if (S->st) (void)hipStreamSynchronize(S->st);
+    sfree(S->eid); sfree(S->cid); sfree(S->cgate); sfree(S->qspace); sfree(S->syncing); sfree(S->sflags);
+    sfree(S->pos); sfree(S->sclaim); sfree(S->hkey); sfree(S->hval);
+    sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
+    sfree(S->d_stage);
+    for (auto &c : S->arena) (void)hipFree(c.p);
+    if (S->h_stage) (void)hipHostFree(S->h_stage);
+    if (S->h_rec) (void)hipHostFree(S->h_rec);
+    if (S->h_rec_d) (void)hipHostFree(S->h_rec_d);
+    if (S->stage_ev) (void)hipEventDestroy(S->stage_ev);
+    delete S;
+}
+
+}  // namespace gw
+
+// =============================================================== C ABI =======
+
+using gw::SyncState;
+
+extern "C" {
+
+int gwaoi_entity_bind(gwaoi_world *w, uint32_t slot, const uint8_t eid[GWAOI_ID_LEN]) {
+    if (!w || !eid) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    return gw::bind_one(S, slot, gw::load_id(eid));
+}
+
+int gwaoi_entity_bind_batch(gwaoi_world *w, const uint32_t *slots, const uint8_t *eids, size_t n) {
+    if (!w || (n && (!slots || !eids))) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    for (size_t i = 0; i < n; ++i)
+        if (int rc = gw::bind_one(S, slots[i], gw::load_id(eids + 16 * i))) return rc;
+    return GWAOI_OK;
+}
+
+int gwaoi_entity_unbind(gwaoi_world *w, uint32_t slot) {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    if (!S->h_bound[slot]) return GWAOI_ESTATE;
+    const uint32_t h = S->h_bucket[slot];
+    S->h_hval[h] = gw::H_TOMB;
+    gw::put32(S, gw::A_HVAL, h, gw::H_TOMB);
+    S->h_bound[slot] = 0;
+    S->h_bucket[slot] = gw::H_EMPTY;
+    if (S->h_client[slot]) {
+        S->h_client[slot] = 0;
+        gw::put32(S, gw::A_CGATE, slot, gw::NO_GATE);
+    }
+    gw::put32(S, gw::A_SYNCING, slot, 0);
+    return GWAOI_OK;
+}
+
+int gwaoi_entity_set_client(gwaoi_world *w, uint32_t slot, uint16_t gate_id, const uint8_t *clientid) {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    if (!clientid) {
+        S->h_client[slot] = 0;
+        gw::put32(S, gw::A_CGATE, slot, gw::NO_GATE);
+        return GWAOI_OK;
+    }
+    auto it = S->gate_idx.find(gate_id);
+    uint32_t g;
+    if (it == S->gate_idx.end()) {
+        if (S->gate_ids.size() >= GWAOI_MAX_GATES) return GWAOI_ECAPACITY;
+        g = (uint32_t)S->gate_ids.size();
+        S->gate_idx.emplace(gate_id, g);
+        S->gate_ids.push_back(gate_id);
+    } else {
+        g = it->second;
+    }
+    S->h_client[slot] = 1;
+    gw::put128(S, gw::B_CID, slot, gw::load_id(clientid));
+    gw::put32(S, gw::A_CGATE, slot, g);
+    return GWAOI_OK;
+}
+
+int gwaoi_entity_set_syncing(gwaoi_world *w, uint32_t slot, int syncing) {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    gw::put32(S, gw::A_SYNCING, slot, syncing ? 1u : 0u);
+    return GWAOI_OK;
+}
+
+int gwaoi_entity_set_position_yaw(gwaoi_world *w, uint32_t slot, float x, float y, float z, float yaw) {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    S->side.push_back(gw::SideOp{slot, 0u, S->claim_next++, make_float4(x, y, z, yaw)});
+    return GWAOI_OK;
+}
+
+int gwaoi_set_position_yaw(gwaoi_world *w, uint32_t slot, float x, float y, float z, float yaw) {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    if (int rc = gwaoi_moved(w, slot, x, z)) return rc;  // ESTATE: not in a space
+    S->side.push_back(gw::SideOp{slot, GWAOI_SIF_OWN_CLIENT | GWAOI_SIF_NEIGHBOR_CLIENTS, S->claim_next++,
+                                 make_float4(x, y, z, yaw)});
+    return GWAOI_OK;
+}
+
+int gwaoi_sync_from_clients(gwaoi_world *w, const uint8_t *payload, size_t n_rec) {
+    return gw::decode(w, payload, n_rec, false);
+}
+
+int gwaoi_sync_from_clients_device(gwaoi_world *w, const uint8_t *d_payload, size_t n_rec) {
+    return gw::decode(w, d_payload, n_rec, true);
+}
+
+int gwaoi_collect_sync_infos(gwaoi_world *w, gwaoi_gate_records *out) { return gw::collect_sync(w, out, true); }
+
+int gwaoi_collect_sync_infos_device(gwaoi_world *w, gwaoi_gate_records *out) {
+    return gw::collect_sync(w, out, false);
+}
+
+int gwaoi_collect_client_events(gwaoi_world *w, gwaoi_gate_records *creates, gwaoi_gate_records *destroys) {
+    using namespace gw;
+    if (!w || !creates || !destroys) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = state(w, &S)) return rc;
+    const WorldView v = world_view(w);
+    if (v.pending_ops) return GWAOI_ESTATE;
+    if (int rc = push(S)) return rc;
+    const uint32_t G = (uint32_t)S->gate_ids.size();
+    const uint64_t n_total = v.n_enter + v.n_leave;
+    S->h_off_c.assign(G + 1, 0);
+    S->h_off_d.assign(G + 1, 0);
+    uint64_t nc = 0, nd = 0;
+    if (G && n_total) {
+        const uint32_t nb = cdivu(n_total, ST);
+        if (int rc = ensure_u32(S, &S->blk_cnt, &S->blk_cap, 2 * (size_t)G * nb + 1)) return rc;
+        RouteArgs A{};
+        A.ev = v.events;
+        A.n_enter = (uint32_t)v.n_enter;
+        A.n_total = (uint32_t)n_total;
+        A.F = v.F;
+        A.info = v.info;
+        A.eid = S->eid;
+        A.cid = S->cid;
+        A.cgate = S->cgate;
+        A.pos = S->pos;
+        A.G = G;
+        A.nb = nb;
+        A.blk_cnt = S->blk_cnt;
+        const size_t lds = 2 * (size_t)G * 4;
+        SY_TRY(hipMemsetAsync(S->blk_cnt + 2 * (size_t)G * nb, 0, 4, S->st));
+        k_route<0><<<nb, ST, lds, S->st>>>(A);
+        SY_TRY(hipGetLastError());
+        if (int rc = part_bases(S, 2 * G, nb)) return rc;
+        const uint64_t split = S->h_off_raw[G];  // creates occupy [0, split) of one index space
+        nc = split;
+        nd = S->h_off_raw[2 * G] - split;
+        if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(nc, 1))) return rc;
+        if (int rc = ensure_out(S, &S->out_d, &S->outd_cap, 2 * std::max<uint64_t>(nd, 1))) return rc;
+        A.out_c = S->out;
+        A.out_d = S->out_d;
+        A.split = (uint32_t)split;
+        k_route<1><<<nb, ST, lds, S->st>>>(A);
+        SY_TRY(hipGetLastError());
+        for (uint32_t g = 0; g <= G; ++g) {
+            S->h_off_c[g] = S->h_off_raw[g];
+            S->h_off_d[g] = S->h_off_raw[G + g] - split;
+        }
+    }
+    if (int rc = ensure_host(S, &S->h_rec, &S->h_rec_cap, std::max<uint64_t>(nc, 1) * 48)) return rc;
+    if (int rc = ensure_host(S, &S->h_rec_d, &S->h_recd_cap, std::max<uint64_t>(nd, 1) * 32)) return rc;
+    if (nc) SY_TRY(hipMemcpyAsync(S->h_rec, S->out, nc * 48, hipMemcpyDeviceToHost, S->st));
+    if (nd) SY_TRY(hipMemcpyAsync(S->h_rec_d, S->out_d, nd * 32, hipMemcpyDeviceToHost, S->st));
+    SY_TRY(hipStreamSynchronize(S->st));
+    fill_out(S, creates, S->h_off_c, S->h_rec);
+    fill_out(S, destroys, S->h_off_d, S->h_rec_d);
+    return GWAOI_OK;
+}
+
+}  // extern "C"

@@ -63,6 +63,7 @@ struct Run {  // a stretch of the op queue: host ops [hbegin, hend) or a device 
     const uint32_t *ds;
     const float *dx, *dz;
     const unsigned long long *dseq;  // explicit device seqs (nullptr: seq0 + i)
+    const uint32_t *dsp;             // explicit space per op (nullptr: keep the slot's space)
     uint64_t seq0;
     size_t dn;
 };
@@ -149,6 +150,7 @@ struct gwaoi_world {
     uint64_t stage_calls[ST_N] = {};
 
     std::string last_error;
+    gw::SyncState *sync = nullptr;  // entity position-sync layer (gwaoi_sync.h), created on first use
 };
 
 namespace {
@@ -539,12 +541,12 @@ int run_tick(gwaoi_world *w) {
         uint32_t j0 = 0;
         for (const Run &r : w->runs) {
             gw::MoveRun &m = RS.r[RS.count++];
-            m.ds = r.ds; m.dx = r.dx; m.dz = r.dz; m.dseq = r.dseq; m.seq0 = r.seq0;
+            m.ds = r.ds; m.dx = r.dx; m.dz = r.dz; m.dseq = r.dseq; m.dsp = r.dsp; m.seq0 = r.seq0;
             m.j0 = j0; m.n = (uint32_t)r.dn;
             j0 += (uint32_t)r.dn;
         }
-        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, w->srec, P.rec, n_prev, w->sc,
-                         w->coll, st);
+        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, w->srec, w->sss, P.rec, n_prev,
+                         w->sc, w->coll, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -569,7 +571,7 @@ int run_tick(gwaoi_world *w) {
                 uint64_t seq0 = 0;
                 uint32_t k;
                 if (r.device) {
-                    sl = r.ds; xs = r.dx; zs = r.dz; sps = nullptr; sq = r.dseq; seq0 = r.seq0; k = (uint32_t)r.dn;
+                    sl = r.ds; xs = r.dx; zs = r.dz; sps = r.dsp; sq = r.dseq; seq0 = r.seq0; k = (uint32_t)r.dn;
                 } else {
                     k = (uint32_t)(r.hend - r.hbegin);
                     sl = w->op_slot + hoff; xs = w->op_x + hoff; zs = w->op_z + hoff; sps = w->op_sp + hoff;
@@ -739,6 +741,8 @@ const char *gwaoi_last_error(gwaoi_world *w) { return w ? w->last_error.c_str() 
 int gwaoi_world_destroy(gwaoi_world *w) {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
+    if (w->sync) gw::sync_destroy(w->sync);
+    w->sync = nullptr;
     for (DevFrame &f : w->fr) {
         dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.grid);
     }
@@ -888,6 +892,7 @@ int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, 
     w->alive[slot] = 1;
     w->space_of[slot] = space;
     w->n_alive++;
+    if (w->sync) gw::sync_note_slot(w->sync, slot, space);
     SpaceHost &S = w->spaces[space];
     S.alive++;
     note_pending_bbox(S, x, z);
@@ -927,6 +932,7 @@ int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
     w->spaces[w->space_of[slot]].alive--;
     w->space_of[slot] = gw::SP_DEAD;
     w->n_alive--;
+    if (w->sync) gw::sync_note_slot(w->sync, slot, gw::SP_DEAD);
     w->touched.push_back(slot);
     push_host_op(w, slot, 0.f, 0.f, gw::SP_DEAD, w->seq_next);  // a Leave's seq is never compared
     return GWAOI_OK;
@@ -1022,6 +1028,54 @@ int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const 
     w->dev_seq_pending = true;
     return GWAOI_OK;
 }
+
+}  // extern "C"
+
+namespace gw {
+
+WorldView world_view(gwaoi_world *w) {
+    WorldView v{};
+    v.F = view_of(w->fr[w->cur]);
+    v.info = w->sinfo;
+    v.st = w->stream;
+    v.max_slots = w->max_slots;
+    v.pending_ops = w->n_ops;
+    v.events = w->events;
+    v.n_enter = w->last_n_enter;
+    v.n_leave = w->last_n_leave;
+    return v;
+}
+
+SyncState *&world_sync(gwaoi_world *w) { return w->sync; }
+
+void world_set_error(gwaoi_world *w, const char *msg) { w->last_error = msg; }
+
+uint32_t world_slot_space(gwaoi_world *w, uint32_t slot) {
+    return slot < w->max_slots && w->alive[slot] ? w->space_of[slot] : SP_DEAD;
+}
+
+int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
+                        const uint32_t *d_sp, size_t n) {
+    if (!n) return GWAOI_OK;
+    if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
+    if (w->dev_seq_pending) return GWAOI_ESTATE;
+    Run r{};
+    r.device = true;
+    r.ds = d_slots;
+    r.dx = d_x;
+    r.dz = d_z;
+    r.dsp = d_sp;
+    r.seq0 = w->seq_next;
+    r.dn = n;
+    w->runs.push_back(r);
+    w->n_ops += n;
+    w->seq_next += n;
+    return GWAOI_OK;
+}
+
+}  // namespace gw
+
+extern "C" {
 
 int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
     if (!w) return GWAOI_EINVAL;

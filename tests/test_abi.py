@@ -27,10 +27,11 @@ def lib():
 def test_header_lists_match_binding():
     assert header_functions() == sorted(_lib.EXPORTS)
     assert header_functions("gwaoi_strips.h") == sorted(_lib.STRIP_EXPORTS)
+    assert header_functions("gwaoi_sync.h") == sorted(_lib.SYNC_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol(lib):
-    for name in header_functions() + header_functions("gwaoi_strips.h"):
+    for name in header_functions() + header_functions("gwaoi_strips.h") + header_functions("gwaoi_sync.h"):
         assert hasattr(lib, name), name
         assert C.cast(getattr(lib, name), C.c_void_p).value
 

@@ -1,0 +1,176 @@
+"""Entity position sync around the AOI path (include/gwaoi_sync.h): client
+packet decode (GameService.go:392-404), CollectEntitySyncInfos fan-out
+(Entity.go:1221-1267) and the routing of AOI events to client create/destroy
+messages (Entity.go:236-246, GameClient.go:37-59).
+
+CPU tests pin the restatement (oracle/entity_sync.py) on hand-built cases;
+GPU tests run the seeded scenario of tests/sync_scenario.py through the
+C ABI and compare every flush with the restatement: enter/leave pairs
+bit-exact, sync records and client messages as exact multisets per gate.
+Parity unpinned against GoWorld itself (Go is absent; the reference holds
+no fixture for these packets) -- the record layouts follow the reference's
+Packet.Append* order (Entity.go:1233-1251) and its little-endian floats.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import sync_scenario as SS
+from oracle import oracle
+from oracle.entity_sync import SIF_NEIGHBOR, SIF_OWN, GameEntities, records_by_gate
+
+EID = [bytes([65 + i]) * 16 for i in range(6)]
+CID = [bytes([97 + i]) * 16 for i in range(6)]
+
+
+def rec(eid, x, y, z, yaw):
+    return eid + struct.pack("<4f", x, y, z, yaw)
+
+
+# ------------------------------------------------------------------ CPU ------
+
+def small_world():
+    g = GameEntities({0: 100.0}, 8)
+    for i in range(4):
+        g.create(EID[i], i, 10.0 * i, 1.0, 0.0, 0.5)
+    g.set_client(0, 1, CID[0])
+    g.set_client(1, 2, CID[1])
+    g.set_syncing(0, True)
+    g.set_syncing(1, False)
+    g.set_syncing(2, True)
+    for i in range(3):  # entity 3 never enters a space
+        g.enter_space(i, 0, 10.0 * i, 1.0, 0.0)
+    return g
+
+
+def test_enter_sets_both_flags_and_interest_is_symmetric():
+    g = small_world()
+    for e in g.by_slot.values():
+        assert e.In == e.By
+    assert g.by_slot[0].flags == SIF_OWN | SIF_NEIGHBOR
+    assert g.by_slot[3].flags == 0
+    out = g.collect()
+    # own records of 0 and 1, plus one per (entity, interested neighbour with a client)
+    assert sorted(out) == [1, 2]
+    assert len(out[1]) == 1 + 2 and len(out[2]) == 1 + 2
+    assert g.collect() == {}  # flags cleared
+
+
+def test_packet_decode_rules():
+    g = small_world()
+    g.collect()
+    pkt = rec(EID[0], 5.0, 2.0, 0.0, 1.0) + rec(EID[1], 7.0, 2.0, 0.0, 1.0) + rec(b"?" * 16, 0, 0, 0, 0) \
+        + rec(EID[3], 1.0, 1.0, 1.0, 1.0) + rec(EID[2], 30.0, 3.0, 0.0, 2.0) + rec(EID[0], 6.0, 4.0, 0.0, 2.5)
+    g.handle_sync_packet(pkt)
+    e0, e1, e2, e3 = (g.by_slot[i] for i in range(4))
+    assert (e0.x, e0.y, e0.yaw) == (6.0, 4.0, 2.5)         # last record wins
+    assert e1.x == 10.0 and e1.flags == 0                  # not syncing from its client
+    assert e3.x == 30.0 and e3.flags == 0                  # no space: setPositionYaw returns
+    assert e0.flags == SIF_NEIGHBOR and e2.flags == SIF_NEIGHBOR  # fromClient: no own-client record
+    out = g.collect()
+    # e0 and e2 moved; interested clients: e0 <- {1 (gate 2)}, e2 <- {0 (gate 1), 1 (gate 2)}
+    assert out == {1: sorted([CID[0] + EID[2] + struct.pack("<4f", 30, 3, 0, 2)]),
+                   2: sorted([CID[1] + EID[0] + struct.pack("<4f", 6, 4, 0, 2.5),
+                              CID[1] + EID[2] + struct.pack("<4f", 30, 3, 0, 2)])}
+
+
+def test_left_entity_keeps_own_record():
+    g = small_world()
+    g.collect()
+    g.set_position_yaw(0, 1.0, 1.0, 1.0, 1.0)
+    g.leave_space(0)
+    assert g.by_slot[0].By == set()
+    out = g.collect()
+    assert out == {1: [CID[0] + EID[0] + struct.pack("<4f", 1, 1, 1, 1)]}
+
+
+def test_scenario_oracle_consistency():
+    sc = SS.make(n=200, flushes=3)
+
+    def check(i, g):
+        for e in g.by_slot.values():
+            assert e.In == e.By
+            if e.space is not None:
+                assert sorted(e.By) == g.aoi.neighbors(e.slot).tolist()
+        g.collect()
+
+    SS.run_oracle(sc, check)
+
+
+# ------------------------------------------------------------------ GPU ------
+
+def expected(sc):
+    exp = []
+
+    def on_flush(i, g):
+        t, a, b = g.take_raw()
+        ent, lev = oracle.net_events(t, a, b)
+        cre, des = g.net_client_events(t, a, b)
+        exp.append({"sync": g.collect(), "enter": ent, "leave": lev, "create": cre, "destroy": des})
+
+    SS.run_oracle(sc, on_flush)
+    return exp
+
+
+def check_run(sc, device_payload=None):
+    from goworld_amd import World, pair_keys
+    exp = expected(sc)
+    seen = []
+
+    def on_flush(i, w, ent=None, lev=None):
+        e = exp[i]
+        if ent is not None:
+            assert np.array_equal(pair_keys(ent), e["enter"]), f"flush {i}: enter pairs"
+            assert np.array_equal(pair_keys(lev), e["leave"]), f"flush {i}: leave pairs"
+            cre, des = w.collect_client_events()
+            assert records_by_gate(cre) == e["create"], f"flush {i}: create messages"
+            assert records_by_gate(des) == e["destroy"], f"flush {i}: destroy messages"
+        got = records_by_gate(w.collect_sync_infos())
+        assert got == e["sync"], f"flush {i}: sync records"
+        seen.append(sum(len(v) for v in got.values()))
+
+    with World(sc["n"], max_spaces=4, device=0) as w:
+        SS.run_gpu(sc, w, on_flush, device_payload)
+    assert len(seen) == len(sc["flushes"]) + 1 and min(seen) > 0
+
+
+@pytest.mark.gpu
+def test_sync_host_packets_match_oracle():
+    check_run(SS.make(seed=11))
+
+
+@pytest.mark.gpu
+def test_sync_device_packets_match_oracle():
+    import torch
+
+    def dev(b):
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8).to("cuda:0")
+        torch.cuda.synchronize()
+        return t.data_ptr(), t
+
+    check_run(SS.make(seed=12, n=900, flushes=4), device_payload=dev)
+
+
+@pytest.mark.gpu
+def test_sync_errors():
+    from goworld_amd import GwaoiError, World
+    with World(16, device=0) as w:
+        sp = w.space_create(100.0)
+        w.entity_bind([0, 1], [EID[0], EID[1]])
+        w.entity_bind([0], [EID[0]])  # same binding again: no-op
+        with pytest.raises(GwaoiError):
+            w.entity_bind([2], [EID[0]])  # id taken
+        with pytest.raises(GwaoiError):
+            w.entity_bind([0], [EID[2]])  # slot taken
+        with pytest.raises(GwaoiError):
+            w.set_position_yaw(0, 1, 2, 3, 4)  # not in a space
+        w.enter(sp, 0, 0.0, 0.0)
+        with pytest.raises(GwaoiError):
+            w.collect_sync_infos()  # ops queued since the last flush
+        w.tick()
+        w.entity_unbind(1)
+        w.entity_bind([2], [EID[1]])  # the id is free again
+        with pytest.raises(GwaoiError):
+            w.entity_unbind(1)
+        assert w.collect_sync_infos() == {}  # no client anywhere
