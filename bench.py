@@ -56,9 +56,30 @@ def combined_pass_bytes(n: int, total_cells: int, events: float) -> float:
     """Algorithmic HBM bytes of one k_combined launch (Roofline):
     every frame entry once as the tile's own entity -- new record (x, z, seq:
     16 B) + previous-flush record (16 B) -- the cell_start index (4 B per
-    cell) and two directed (slot, slot) pairs per event (16 B).  Candidate
-    re-reads of neighbouring rows are L2/LDS reuse, not algorithmic traffic."""
-    return n * 32.0 + (total_cells + 1) * 4.0 + 16.0 * events
+    cell) and one (slot, slot) pair of 8 B per directed event (`events` is
+    the directed count).  Candidate re-reads of neighbouring rows are L2/LDS
+    reuse, not algorithmic traffic."""
+    return n * 32.0 + (total_cells + 1) * 4.0 + 8.0 * events
+
+
+def stage_bytes(n: int, moves: float, cells: int, events: float) -> dict:
+    """Algorithmic HBM bytes per flush of each pipeline stage:
+    the bytes a stage must move at least, at its own data layout.
+      apply    move (slot, x, z) 12 B read, slot rank 4 B read, claim 8 B and
+               record 16 B written: 40 B per move
+      keygen   S' record + slot/space 24 B and the previous key 4 B read, key
+               4 B written per entity; per-cell entity/arrival counts 8 B
+      sort     (incremental merge) counts 8 B/cell read, cell_start 4 B/cell
+               written, previous cell_start 4 B/cell and keys 4 B/entity read,
+               permutation + sorted key 8 B/entity written
+      gather   permutation 4 B, S' 24 B, previous frame 24 B read; frame 24 B,
+               previous-in-new-order 16 B, candidate 16 B, slot rank 8 B, key
+               4 B written: 120 B per entity
+      combined see combined_pass_bytes
+      reorder  each directed event pair (8 B) read and written once
+    """
+    return {"apply": 40.0 * moves, "keygen": 32.0 * n + 8.0 * cells, "sort": 12.0 * n + 16.0 * cells,
+            "gather": 120.0 * n, "combined": combined_pass_bytes(n, cells, events), "reorder": 16.0 * events}
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_k_combined.json")
@@ -138,9 +159,66 @@ def sync_leg(w, n: int, batches, client_frac: float):
                     "CollectEntitySyncInfos into per-gate 48-B records in HBM; wall clock per phase"}
 
 
+def cpu_cores() -> int:
+    """Host cores this process may use (the GPU box gives a 16-core share)."""
+    try:
+        c = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        c = os.cpu_count() or 1
+    return max(1, min(16, c))
+
+
+def cpu_baseline_spaces(args, target_s: float):
+    """cfg4: independent 2000-entity spaces, one sequential XZ-list restatement
+    per space, spaces run in parallel on all host cores (one thread per core;
+    the C oracle runs with the GIL released).  Move batches are generated
+    before timing."""
+    import threading
+    from goworld_amd.workload import make_workload
+    from oracle import oracle
+    cores = cpu_cores()
+    work = []
+    for k in range(cores):
+        wl = make_workload("cfg4", seed=0x5EED0004 + 7919 * k, n_spaces=1)
+        m = oracle.XZList(wl.D, wl.n, record=False)
+        slots, x0, z0, _ = wl.initial()
+        m.bulk_enter(slots.astype(np.int32), x0, z0)
+        work.append((m, wl))
+    done = [0] * cores
+    stop = [False]
+
+    def run(k):
+        m, wl = work[k]
+        t = 0
+        while not stop[0]:
+            sl, nx, nz = wl.tick(t)  # ~0.1 ms of numpy per ~10 ms of C (GIL released there)
+            m.moved_batch(sl, nx, nz)
+            done[k] += sl.size
+            t += 1
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(cores)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    timer = threading.Timer(target_s, lambda: stop.__setitem__(0, True))
+    timer.start()
+    for x in th:
+        x.join()
+    timer.cancel()
+    dt = time.perf_counter() - t0
+    ev = sum(sum(w[0].counts()) for w in work)
+    return {"value": sum(done) / dt, "unit": "entity-moves/s", "events_per_s": ev / dt, "cores": cores,
+            "kind": "port",
+            "sample": f"{cores} independent cfg4 spaces (2000 entities each), one per core, every entity "
+                      f"moving each tick ({sum(done)} Moved calls), sequential XZ-list restatement, {dt:.1f} s"}
+
+
 def cpu_baseline(args, wl_factory, target_s: float):
     """go-aoi XZListAOIManager restatement (oracle/xzlist.c), one core, timed on
-    a prefix of tick 0's move batch of the same workload."""
+    a prefix of tick 0's move batch of the same workload (cfg4: one space per
+    core, cpu_baseline_spaces)."""
+    if args.workload == "cfg4":
+        return cpu_baseline_spaces(args, target_s)
     from oracle import oracle
     wl = wl_factory()
     m = oracle.XZList(wl.D, wl.n, record=False)
@@ -464,6 +542,14 @@ def main():
                 roofline = {"bound": "hbm", "kernel": dom, "achieved": None, "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": None, "traffic": None,
                             "avg_launch_ms": round(stage_ms.get(dom, 0.0), 4)}
+        stage_roof = {}
+        if stage_ms:
+            sb = stage_bytes(n, moves / max(args.steps, 1), info["total_cells"], events / max(args.steps, 1))
+            for k, b in sb.items():
+                if stage_ms.get(k):
+                    gbs = b / (stage_ms[k] * 1e-3) / 1e9
+                    stage_roof[k] = {"ms": round(stage_ms[k], 4), "alg_MB": round(b / 1e6, 2),
+                                     "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
         cpu = None
         if not args.no_cpu_baseline:
             try:
@@ -499,6 +585,7 @@ def main():
             "pcie_inclusive": host_io,
             "sync_leg": sync,
             "stages_ms_per_tick": {k: round(v, 4) for k, v in stage_ms.items()},
+            "stage_roofline": stage_roof,
             "stages_note": f"separate {bd} ticks after the timed region, every stage bracketed by HIP events "
                            "(the events add ~0.07 ms per tick, so these sum above ms_per_step)",
             "cpu_baseline": cpu,
