@@ -33,6 +33,7 @@ EXPORTS = [
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
+    "gwaoi_snapshot", "gwaoi_restore",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -145,6 +146,8 @@ def load():
         "gwaoi_strips_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_strips_events": ([vp, P(Events)], C.c_int),
         "gwaoi_strips_last_error": ([vp], C.c_char_p),
+        "gwaoi_snapshot": ([vp, vp, vp, vp, vp, vp, sz, P(sz)], C.c_int),
+        "gwaoi_restore": ([vp, vp, vp, vp, vp, vp, sz], C.c_int),
         "gwaoi_entity_bind": ([vp, u32, vp], C.c_int),
         "gwaoi_entity_bind_batch": ([vp, vp, vp, sz], C.c_int),
         "gwaoi_entity_unbind": ([vp, u32], C.c_int),
@@ -316,6 +319,25 @@ class World:
 
     def stream(self) -> int:
         return self._L.gwaoi_stream(self._w) or 0
+
+    # ---- freeze / restore
+    def snapshot(self) -> dict:
+        """AOI state of the last flush in frame order: slot, space, x, z, seq arrays."""
+        n = C.c_size_t()
+        self._check(self._L.gwaoi_snapshot(self._w, None, None, None, None, None, 0, C.byref(n)))
+        k = n.value
+        out = {"slot": np.empty(k, np.uint32), "space": np.empty(k, np.uint32), "x": np.empty(k, np.float32),
+               "z": np.empty(k, np.float32), "seq": np.empty(k, np.uint64)}
+        if k:
+            self._check(self._L.gwaoi_snapshot(self._w, _p(out["slot"]), _p(out["space"]), _p(out["x"]),
+                                               _p(out["z"]), _p(out["seq"]), k, C.byref(n)))
+        return out
+
+    def restore(self, snap: dict):
+        a = {k: np.ascontiguousarray(snap[k], t) for k, t in
+             (("slot", np.uint32), ("space", np.uint32), ("x", np.float32), ("z", np.float32), ("seq", np.uint64))}
+        self._check(self._L.gwaoi_restore(self._w, _p(a["slot"]), _p(a["space"]), _p(a["x"]), _p(a["z"]),
+                                          _p(a["seq"]), a["slot"].size))
 
     # ---- entity position sync (include/gwaoi_sync.h)
     def entity_bind(self, slots, eids):

@@ -1152,6 +1152,55 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
     return GWAOI_OK;
 }
 
+int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, float *z, uint64_t *seq,
+                   size_t cap, size_t *n_out) {
+    if (!w || !n_out) return GWAOI_EINVAL;
+    const DevFrame &F = w->fr[w->cur];
+    *n_out = F.n;
+    if (F.n > cap || !F.n) return GWAOI_OK;
+    if (!slots || !spaces || !x || !z || !seq) return GWAOI_EINVAL;
+    std::vector<gw::Rec16> rec(F.n);
+    std::vector<gw::SlotSp> ss(F.n);
+    HIP_TRY(hipMemcpyAsync(rec.data(), F.rec, F.n * sizeof(gw::Rec16), hipMemcpyDeviceToHost, w->stream));
+    HIP_TRY(hipMemcpyAsync(ss.data(), F.ss, F.n * sizeof(gw::SlotSp), hipMemcpyDeviceToHost, w->stream));
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    for (uint32_t i = 0; i < F.n; ++i) {
+        slots[i] = ss[i].slot;
+        spaces[i] = ss[i].sp;
+        x[i] = rec[i].x;
+        z[i] = rec[i].z;
+        seq[i] = rec[i].s;
+    }
+    return GWAOI_OK;
+}
+
+int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces, const float *x, const float *z,
+                  const uint64_t *seq, size_t n) {
+    if (!w || (n && (!slots || !spaces || !x || !z || !seq))) return GWAOI_EINVAL;
+    if (w->n_ops || w->dev_seq_pending) return GWAOI_ESTATE;
+    std::vector<size_t> ord(n);
+    for (size_t i = 0; i < n; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return seq[a] < seq[b]; });
+    // validate everything before queueing anything
+    std::vector<uint32_t> seen(slots, slots + n);
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return GWAOI_ESTATE;
+    for (size_t k = 0; k < n; ++k) {
+        const size_t i = ord[k];
+        if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
+        if (w->alive[slots[i]]) return GWAOI_ESTATE;
+        if (spaces[i] >= w->n_space_ids || !w->spaces[spaces[i]].used) return GWAOI_EBADSPACE;
+        if (!finite2(x[i], z[i])) return GWAOI_ENONFINITE;
+        if (k && seq[i] == seq[ord[k - 1]]) return GWAOI_EINVAL;
+    }
+    // fresh seqs in the frozen order: the relation only compares seqs
+    for (size_t k = 0; k < n; ++k) {
+        const size_t i = ord[k];
+        if (int rc = enter_impl(w, spaces[i], slots[i], x[i], z[i], nullptr)) return rc;
+    }
+    return GWAOI_OK;
+}
+
 int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
     if (!w || !info) return GWAOI_EINVAL;
     info->ticks = w->ticks;

@@ -159,6 +159,20 @@ int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
 /* Device pointers of the last tick's events (same layout as gwaoi_events). */
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave);
 
+/* ---- freeze / restore (EntityManager.go:554-656, Space.go:118-125) ----------
+ * gwaoi_snapshot copies the AOI state of the last flush in frame order:
+ * slot, space, x, z and the seq of the entity's last Enter/Moved.  *n_out =
+ * live entities (also when it exceeds cap; nothing is copied then).
+ * gwaoi_restore re-enters such a state into a world with no queued op, in
+ * seq order with the original seqs, so the restored relation is the frozen
+ * one bit for bit (the reference re-enters in Go map order, Appendix D.6 of
+ * SURVEY.md, which may flip ownership-dependent pairs).  Spaces must exist;
+ * the next gwaoi_tick reports every restored pair as an enter. */
+int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, float *z, uint64_t *seq,
+                   size_t cap, size_t *n_out);
+int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces, const float *x, const float *z,
+                  const uint64_t *seq, size_t n);
+
 /* ---- queries ----------------------------------------------------------------- */
 /* Neighbours of `slot` at the last flush (unsorted).  *n_out = total count even
  * when it exceeds cap. */

@@ -44,6 +44,11 @@ def test_pure_host_entry_points(lib):
     assert lib.gwaoi_world_create(None, None) == -1
     assert lib.gwaoi_tick(None, None) == -1
     assert lib.gwaoi_world_destroy(None) == -1
+    # entity-sync entry points validate before any device work
+    assert lib.gwaoi_entity_bind(None, 0, None) == -1
+    assert lib.gwaoi_sync_from_clients(None, None, 0) == -1
+    assert lib.gwaoi_collect_sync_infos(None, None) == -1
+    assert lib.gwaoi_collect_client_events(None, None, None) == -1
 
 
 def test_library_is_gfx950_code_object():

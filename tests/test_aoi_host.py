@@ -149,3 +149,11 @@ def test_entity_interest_symmetry_rules():
     e1.on_leave_aoi(e2.aoi)
     e2.on_leave_aoi(e1.aoi)
     assert not (e1.interested_in or e1.interested_by or e2.interested_in or e2.interested_by)
+
+
+def test_restore_and_snapshot_validate_without_a_gpu():
+    """Null-argument paths of the freeze/restore ABI never touch the device."""
+    from goworld_amd import _lib
+    L = _lib.load()
+    assert L.gwaoi_snapshot(None, None, None, None, None, None, 0, None) == -1
+    assert L.gwaoi_restore(None, None, None, None, None, None, 0) == -1

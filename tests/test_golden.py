@@ -116,3 +116,43 @@ def test_gpu_replays_fixture(name):
                 got.append((np.uint64(s) << np.uint64(32)) | nb.astype(np.uint64))
         got = np.sort(np.concatenate(got)) if got else np.empty(0, np.uint64)
         np.testing.assert_array_equal(got, fx["final_pairs"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["lattice64", "multispace16x128", "cfg1_1k_50t"])
+def test_gpu_freeze_restore_keeps_relation(name):
+    """f4: freeze (gwaoi_snapshot) after the whole fixture, restore into a fresh
+    world (gwaoi_restore, original seq order): the first flush enters exactly
+    the frozen relation, bit for bit (EntityManager.go:554-656)."""
+    from goworld_amd import World, pair_keys
+    fx = G.load(name)
+    nsp = len(fx["space_D"])
+    with World(int(fx["max_slots"]), max_spaces=nsp) as w:
+        ids = [w.space_create(d) for d in fx["space_D"]]
+
+        def apply_op(kind, slot, x, z, sp):
+            if kind == G.ENTER:
+                w.enter(ids[sp], slot, x, z)
+            elif kind == G.LEAVE:
+                w.leave(slot)
+            else:
+                w.moved(slot, x, z)
+
+        for _ in G.replay(fx, apply_op, lambda: w.tick()):
+            pass
+        snap = w.snapshot()
+    x, z, seq, sp = G.final_state(fx)
+    live = np.nonzero(sp != 0xFFFFFFFF)[0]
+    assert np.array_equal(np.sort(snap["slot"]), live)
+    o = np.argsort(snap["slot"])
+    assert np.array_equal(snap["x"][o], x[live]) and np.array_equal(snap["z"][o], z[live])
+    # the frozen seqs order the entities exactly as the call stream did
+    assert np.array_equal(np.argsort(snap["seq"][o], kind="stable"), np.argsort(seq[live], kind="stable"))
+    perm = np.random.default_rng(5).permutation(snap["slot"].size)  # any input order (Go map order)
+    with World(int(fx["max_slots"]), max_spaces=nsp) as w2:
+        for d in fx["space_D"]:
+            w2.space_create(d)
+        w2.restore({k: v[perm] for k, v in snap.items()})
+        e, l = w2.tick()
+        assert l.size == 0
+        np.testing.assert_array_equal(pair_keys(e), fx["final_pairs"])
