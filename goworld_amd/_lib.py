@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libgwaoi.so")
+# GWAOI_LIB: an alternative in-tree build (tools/variants.sh, A/B tuning runs)
+LIB_PATH = os.environ.get("GWAOI_LIB") or os.path.join(HERE, "lib", "libgwaoi.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "gwaoi.h")
 
 GWAOI_F_TIMING = 1

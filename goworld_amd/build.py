@@ -32,17 +32,18 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Compile libgwaoi.so (or a tuning variant: `out` + -D `defines`)."""
+    if out == OUT and not defines and not force and not _stale():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "aoi_manager_test.cpp")

@@ -1255,9 +1255,19 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
-constexpr int QCAP = 640;  // per-wave queue of filter survivors (>= SW_U * WAVE + a drain batch)
-constexpr int SW_U = 8;    // candidates per lane per sweep iteration on long rows
-constexpr int EVW = 192;   // events buffered per wave
+#ifndef GWAOI_SW_U
+#define GWAOI_SW_U 8
+#endif
+#ifndef GWAOI_QCAP
+#define GWAOI_QCAP 640
+#endif
+#ifndef GWAOI_EVW
+#define GWAOI_EVW 192
+#endif
+constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= SW_U * WAVE + a drain batch)
+constexpr int SW_U = GWAOI_SW_U;  // candidates per lane per sweep iteration on long rows
+constexpr int EVW = GWAOI_EVW;    // events buffered per wave
+static_assert(QCAP >= SW_U * WAVE + WAVE, "queue must hold one sweep iteration beyond the drain mark");
 
 struct CombinedLds {
     uint2 q[CW][QCAP];  // queued pairs of a wave: (A frame index, B frame index)
