@@ -5,18 +5,17 @@
 //             lane per 32-B record, entity-id hash lookup, the record becomes
 //             op i of a device Moved batch (SLOT_NONE = skipped), Y/yaw by
 //             last-writer claim, sifSyncNeighborClients.
-//   fan-out   CollectEntitySyncInfos (Entity.go:1221-1267): one lane per
-//             frame entity A with flags; a record to A's own client and one
-//             to the client of every B with rel(A,B) (the go-aoi relation of
-//             the last flush == A.InterestedBy), grouped by gate.
+//   fan-out   CollectEntitySyncInfos (Entity.go:1221-1267), receiver side:
+//             one lane per frame entity B with a client; its records are its
+//             own (sifSyncOwnClient) and one per flagged A with rel(A,B) (the
+//             go-aoi relation of the last flush: B in A.InterestedBy).
 //   route     Entity.interest/uninterest -> sendCreateEntity/sendDestroyEntity
 //             (Entity.go:236-246, GameClient.go:37-59): the flush's events
 //             whose first entity has a client, grouped by gate.
 // Grouping by gate is a two-pass multisplit: pass 0 counts records per
 // (gate, block) in LDS, an exclusive scan gives every (gate, block) its
-// base, pass 1 recomputes and writes through LDS cursors.  The output is HBM
-// write bound (48 B per record); the fan-out enumerates each flagged
-// entity's window twice (count, write), like the reference's map walk.
+// base, pass 1 reserves each lane's run through an LDS cursor and writes it.
+// The output is HBM write bound (48 B per record).
 
 #include "gwaoi_device.h"
 #include "gwaoi_internal.h"
@@ -169,6 +168,15 @@ __global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
 }
 
 // ------------------------------------------------------------ fan-out ------
+// Receiver side: CollectEntitySyncInfos sends entity A's record to the client
+// of every B in A.InterestedBy, i.e. every B with rel(A,B).  One lane per
+// frame entity B with a client (gate g): its records are its own one (if B's
+// sifSyncOwnClient is set) plus one per A in B's window with rel(A,B) and
+// sifSyncNeighborClients set on A.  All of a lane's records go to one gate,
+// so a lane reserves its whole run with one LDS atomic and writes it
+// contiguously.  k_fan_prep first lays the senders out in frame order
+// (flags, id, position/yaw) so that the window walk reads them next to the
+// frame records, and clears the flags.
 struct FanArgs {
     FrameView F;
     const uint32_t *left;  // slots that left since the last collect (own-client records only)
@@ -177,83 +185,167 @@ struct FanArgs {
     const uint32_t *cgate;
     uint32_t *sflags;
     const float4 *pos;
+    // frame-ordered (n + n_left entries), written by k_fan_prep
+    uint32_t *snd;    // sender flags
+    uint32_t *rg;     // receiver gate (NO_GATE: no client)
+    uint32_t *rslot;  // slot
+    uint4 *srec1;     // sender id
+    uint4 *srec2;     // sender x, y, z, yaw
     uint32_t G, nb;
-    uint32_t *blk_cnt;      // [G][nb] (pass 0 writes, the scan turns it into bases)
-    uint4 *out;             // 3 uint4 per record (pass 1)
+    uint32_t *blk_cnt;  // [G][nb] (pass 0 writes, the scan turns it into bases)
+    uint4 *out;         // 3 uint4 per record (pass 1)
 };
 
-template <int PASS>
-__device__ __forceinline__ void fan_emit(const FanArgs &A, uint32_t *lds, uint32_t g, const uint4 &client,
-                                         const uint4 &rec1, const uint4 &rec2) {
-    const uint32_t p = atomicAdd(&lds[g], 1u);
-    if (PASS == 1) {
-        uint4 *o = A.out + 3 * (size_t)p;
-        o[0] = client;
-        o[1] = rec1;
-        o[2] = rec2;
+__global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nf = A.F.n;
+    if (i >= nf + A.n_left) return;
+    const bool in_frame = i < nf;
+    const uint32_t s = in_frame ? ld_ss(A.F.ss, i).slot : A.left[i - nf];
+    const uint32_t fl = A.sflags[s];
+    A.snd[i] = fl;
+    A.rg[i] = A.cgate[s];
+    A.rslot[i] = s;
+    if (fl) {
+        A.sflags[s] = 0u;
+        // the frame holds the AOI position; an entity that left uses its last sync position
+        const float4 P = A.pos[s];
+        float x = P.x, z = P.z;
+        if (in_frame) {
+            const Rec16 R = ld_rec(A.F.rec, i);
+            x = R.x;
+            z = R.z;
+        }
+        A.srec1[i] = A.eid[s];
+        A.srec2[i] = make_uint4(__float_as_uint(x), __float_as_uint(P.y), __float_as_uint(z), __float_as_uint(P.w));
     }
+}
+
+__device__ __forceinline__ uint32_t s_lane() { return __lane_id(); }
+__device__ __forceinline__ unsigned long long s_lt() { return (1ull << s_lane()) - 1ull; }
+
+// Exclusive scan of n (<= ST * k) LDS words in place by one workgroup.
+__device__ void lds_excl_scan(uint32_t *a, uint32_t n, uint32_t *ws) {
+    const uint32_t k = (n + ST - 1) / ST, b = threadIdx.x * k;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < k && b + q < n; ++q) sum += a[b + q];
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if ((int)s_lane() >= o) x += y;
+    }
+    const uint32_t w = threadIdx.x / 64;
+    if (s_lane() == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t pre = x - sum;
+    for (uint32_t q = 0; q < w; ++q) pre += ws[q];
+    for (uint32_t q = 0; q < k && b + q < n; ++q) {
+        const uint32_t v = a[b + q];
+        a[b + q] = pre;
+        pre += v;
+    }
+    __syncthreads();
+}
+
+// Records of one emission point: the emitting lanes of one gate group (lanes
+// sorted by gate, so a group is a contiguous lane range `grp`) take
+// consecutive slots from the block's cursor of that gate: stores of a group
+// land side by side.
+__device__ __forceinline__ size_t group_slot(bool emit, unsigned long long grp, uint32_t *cur, uint32_t g) {
+    const unsigned long long m = __ballot(emit) & grp;
+    if (!m) return 0;  // no record in this lane's group (its leader, if any, is active below)
+    uint32_t base = 0;
+    const uint32_t rank = (uint32_t)__popcll(m & s_lt());
+    if (emit && rank == 0) base = atomicAdd(&cur[g], (uint32_t)__popcll(m));
+    base = __shfl(base, m ? __ffsll((long long)m) - 1 : 0);
+    return (size_t)base + rank;
 }
 
 template <int PASS>
 __global__ __launch_bounds__(ST) void k_fanout(FanArgs A) {
-    extern __shared__ uint32_t lds[];  // per gate: count (pass 0) / cursor (pass 1)
+    extern __shared__ uint32_t lds[];  // cur[G]: count (pass 0) / cursor (pass 1); bin[G + 1]
+    __shared__ uint32_t s_perm[ST];
+    __shared__ uint32_t s_ws[ST / 64];
+    uint32_t *cur = lds, *bin = lds + A.G;
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t nf = A.F.n, ne = nf + A.n_left;
     for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
-        lds[g] = PASS == 0 ? 0u : A.blk_cnt[(size_t)g * A.nb + blk];
+        cur[g] = PASS == 0 ? 0u : A.blk_cnt[(size_t)g * A.nb + blk];
+    for (uint32_t g = threadIdx.x; g <= A.G; g += blockDim.x) bin[g] = 0u;
     __syncthreads();
-    const uint32_t i = blk * ST + threadIdx.x;
-    const uint32_t nf = A.F.n;
-    if (i < nf + A.n_left) {
-        const bool in_frame = i < nf;
-        Rec16 R;
-        uint32_t sA, sp = SP_DEAD;
-        if (in_frame) {
-            R = ld_rec(A.F.rec, i);
-            const SlotSp q = ld_ss(A.F.ss, i);
-            sA = q.slot;
-            sp = q.sp;
-        } else {
-            sA = A.left[i - nf];
-        }
-        const uint32_t fl = A.sflags[sA];
-        if (fl) {
-            if (PASS == 1) A.sflags[sA] = 0u;
-            const uint4 rec1 = A.eid[sA];
-            // the frame holds the AOI position; an entity that left uses its last sync position
-            const float4 P = A.pos[sA];
-            const uint4 rec2 = make_uint4(__float_as_uint(in_frame ? R.x : P.x), __float_as_uint(P.y),
-                                          __float_as_uint(in_frame ? R.z : P.z), __float_as_uint(P.w));
-            if (fl & GWAOI_SIF_OWN_CLIENT) {
-                const uint32_t g = A.cgate[sA];
-                if (g != NO_GATE) fan_emit<PASS>(A, lds, g, A.cid[sA], rec1, rec2);
+    // lanes sorted by receiver gate (no client last): same-gate lanes are neighbours
+    const uint32_t i0 = blk * ST + threadIdx.x;
+    const uint32_t g0 = i0 < ne ? A.rg[i0] : NO_GATE;
+    const uint32_t key = g0 == NO_GATE ? A.G : g0;
+    const uint32_t r0 = atomicAdd(&bin[key], 1u);
+    __syncthreads();
+    lds_excl_scan(bin, A.G + 1, s_ws);
+    s_perm[bin[key] + r0] = i0;
+    __syncthreads();
+    const uint32_t i = s_perm[threadIdx.x];
+    const uint32_t g = i < ne ? A.rg[i] : NO_GATE;
+    const bool on = g != NO_GATE;
+    // this lane's gate group within the wave
+    const uint32_t gprev = __shfl_up(g, 1);
+    const unsigned long long heads = __ballot(s_lane() == 0 || gprev != g);
+    const unsigned long long upto = heads & (s_lt() | (1ull << s_lane()));
+    const uint32_t gstart = 63 - __clzll(upto);
+    const unsigned long long above = heads & ~(s_lt() | (1ull << s_lane()));
+    const uint32_t gend = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
+    const unsigned long long grp = (gend == 64 ? ~0ull : ((1ull << gend) - 1ull)) & ~((1ull << gstart) - 1ull);
+    if (__ballot(on)) {
+        uint32_t c = 0;
+        uint4 client{};
+        if (PASS == 1 && on) client = A.cid[A.rslot[i]];
+        const bool own = on && (A.snd[i] & GWAOI_SIF_OWN_CLIENT);
+        if (PASS == 1) {
+            const size_t p = group_slot(own, grp, cur, g);
+            if (own) {
+                uint4 *o = A.out + 3 * p;
+                o[0] = client;
+                o[1] = A.srec1[i];
+                o[2] = A.srec2[i];
             }
-            if ((fl & GWAOI_SIF_NEIGHBOR_CLIENTS) && in_frame) {
-                const SpaceGrid gr = A.F.grid[sp];
-                const float D = gr.D;
-                const float mx = (fabsf(R.x) + 3.0f * D) * 0x1p-20f, mz = (fabsf(R.z) + 3.0f * D) * 0x1p-20f;
-                const int cx0 = cell_of(R.x - D - mx, gr.ox, gr.inv, gr.gx);
-                const int cx1 = cell_of(R.x + D + mx, gr.ox, gr.inv, gr.gx);
-                const int cz0 = cell_of(R.z - D - mz, gr.oz, gr.inv, gr.gz);
-                const int cz1 = cell_of(R.z + D + mz, gr.oz, gr.inv, gr.gz);
-                for (int cz = cz0; cz <= cz1; ++cz) {
-                    const uint32_t row = gr.base + (uint32_t)cz * gr.gx;
-                    const uint32_t jb = A.F.cell_start[row + (uint32_t)cx0];
-                    const uint32_t je = A.F.cell_start[row + (uint32_t)cx1 + 1u];
-                    for (uint32_t b = jb; b < je; ++b) {
-                        if (b == i) continue;
-                        const Rec16 B = ld_rec(A.F.rec, b);
-                        if (!rel(R.x, R.z, R.s, B.x, B.z, B.s, D)) continue;
-                        const uint32_t sB = ld_ss(A.F.ss, b).slot;
-                        const uint32_t g = A.cgate[sB];
-                        if (g != NO_GATE) fan_emit<PASS>(A, lds, g, A.cid[sB], rec1, rec2);
+        } else {
+            c += own;
+        }
+        if (on && i < nf) {
+            const Rec16 R = ld_rec(A.F.rec, i);
+            const SpaceGrid gr = A.F.grid[ld_ss(A.F.ss, i).sp];
+            const float D = gr.D;
+            const float mx = (fabsf(R.x) + 3.0f * D) * 0x1p-20f, mz = (fabsf(R.z) + 3.0f * D) * 0x1p-20f;
+            const int cx0 = cell_of(R.x - D - mx, gr.ox, gr.inv, gr.gx);
+            const int cx1 = cell_of(R.x + D + mx, gr.ox, gr.inv, gr.gx);
+            const int cz0 = cell_of(R.z - D - mz, gr.oz, gr.inv, gr.gz);
+            const int cz1 = cell_of(R.z + D + mz, gr.oz, gr.inv, gr.gz);
+            for (int cz = cz0; cz <= cz1; ++cz) {
+                const uint32_t row = gr.base + (uint32_t)cz * gr.gx;
+                const uint32_t jb = A.F.cell_start[row + (uint32_t)cx0];
+                const uint32_t je = A.F.cell_start[row + (uint32_t)cx1 + 1u];
+                for (uint32_t b = jb; b < je; ++b) {
+                    const Rec16 B = ld_rec(A.F.rec, b);
+                    const bool hit = b != i && (A.snd[b] & GWAOI_SIF_NEIGHBOR_CLIENTS) &&
+                                     rel(R.x, R.z, R.s, B.x, B.z, B.s, D);
+                    if (PASS == 1) {
+                        const size_t p = group_slot(hit, grp, cur, g);
+                        if (hit) {
+                            uint4 *o = A.out + 3 * p;
+                            o[0] = client;
+                            o[1] = A.srec1[b];
+                            o[2] = A.srec2[b];
+                        }
+                    } else {
+                        c += hit;
                     }
                 }
             }
         }
+        if (PASS == 0 && c) atomicAdd(&cur[g], c);
     }
     __syncthreads();
     if (PASS == 0)
-        for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) A.blk_cnt[(size_t)g * A.nb + blk] = lds[g];
+        for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) A.blk_cnt[(size_t)q * A.nb + blk] = cur[q];
 }
 
 // -------------------------------------------------------------- route ------
@@ -366,6 +458,10 @@ struct SyncState {
     size_t off_cap = 0;
     uint32_t *d_left = nullptr;
     size_t left_cap = 0;
+    // fan-out scratch, frame order (fan_cap entries each)
+    uint32_t *f_snd = nullptr, *f_rg = nullptr, *f_slot = nullptr;
+    uint4 *f_rec1 = nullptr, *f_rec2 = nullptr;
+    size_t fan_cap = 0;
     uint4 *out = nullptr, *out_d = nullptr;
     size_t out_cap = 0, outd_cap = 0;  // in uint4
     std::vector<unsigned long long> h_off_raw;
@@ -719,10 +815,26 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     A.nb = nb;
     if (int rc = ensure_u32(S, &S->blk_cnt, &S->blk_cap, (size_t)G * nb + 1)) return rc;
     A.blk_cnt = S->blk_cnt;
-    const size_t lds = std::max<size_t>(G, 1) * 4;
+    if (n_ent > S->fan_cap) {
+        sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec1); sfree(S->f_rec2);
+        S->fan_cap = 0;
+        const size_t c = std::max<size_t>(n_ent + n_ent / 8, 1024);
+        int rc;
+        if ((rc = salloc(S, &S->f_snd, c)) || (rc = salloc(S, &S->f_rg, c)) || (rc = salloc(S, &S->f_slot, c)) ||
+            (rc = salloc(S, &S->f_rec1, c)) || (rc = salloc(S, &S->f_rec2, c)))
+            return rc;
+        S->fan_cap = c;
+    }
+    A.snd = S->f_snd;
+    A.rg = S->f_rg;
+    A.rslot = S->f_slot;
+    A.srec1 = S->f_rec1;
+    A.srec2 = S->f_rec2;
+    if (n_ent) k_fan_prep<<<cdivu(n_ent, ST), ST, 0, S->st>>>(A);  // also clears the flags
+    const size_t lds = (2 * (size_t)G + 1) * 4;  // cursors + gate bins
     uint64_t total = 0;
     S->h_off_raw.assign(1, 0);
-    if (G) {
+    if (G && n_ent) {
         SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
         k_fanout<0><<<nb, ST, lds, S->st>>>(A);
         SY_TRY(hipGetLastError());
@@ -731,7 +843,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     }
     if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;
     A.out = S->out;
-    k_fanout<1><<<nb, ST, lds, S->st>>>(A);  // also clears the flags
+    if (total) k_fanout<1><<<nb, ST, lds, S->st>>>(A);
     SY_TRY(hipGetLastError());
     S->h_off.assign(S->h_off_raw.begin(), S->h_off_raw.end());
     if (to_host) {
@@ -838,6 +950,7 @@ void sync_destroy(SyncState *S) {
     if (S->st) (void)hipStreamSynchronize(S->st);
     sfree(S->eid); sfree(S->cid); sfree(S->cgate); sfree(S->qspace); sfree(S->syncing); sfree(S->sflags);
     sfree(S->pos); sfree(S->sclaim); sfree(S->hkey); sfree(S->hval);
+    sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec1); sfree(S->f_rec2);
     sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
     sfree(S->d_stage);
     for (auto &c : S->arena) (void)hipFree(c.p);
