@@ -1354,6 +1354,23 @@ __device__ __forceinline__ void qpush(CombinedLds &L, int w, WaveQueue &Q, bool 
     Q.qn += (uint32_t)__popcll(m);
 }
 
+// Cheap filter of candidate b (k = cand[b]: x, z, flags) for lane A.
+// MODE 0: Z strip, 1: X' strip, 2: whole window of a jumper.
+template <int MODE>
+__device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint3 &k, uint32_t b) {
+    const float lo = C.lo, hi = C.hi;
+    const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
+    bool keep;
+    if (MODE == 0)
+        keep = (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi) & (int)((k.z & FL_JUMP) == 0u);
+    else if (MODE == 1)
+        keep = (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in) & (int)((k.z & FL_JUMP) == 0u);
+    else
+        keep = (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi) & (int)(b != A.a) &
+               ((int)((k.z & FL_JUMP) == 0u) | (int)(A.a < b));
+    return keep & (((k.z | A.fl) & FL_CHG) != 0u);
+}
+
 // Sweep candidates [jb, jb + len) of one grid row for every lane (ranges are
 // per lane; the loop runs to the wave maximum mx).  MODE 0: Z strip, 1: X'
 // strip, 2: whole window of a jumper.  U candidates per lane per iteration,
@@ -1364,7 +1381,6 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                                             const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
-    const float lo = C.lo, hi = C.hi;
     for (uint32_t t = 0; t < mx; t += U) {
         uint3 k[U];
 #pragma unroll
@@ -1375,17 +1391,7 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t b = jb + t + (uint32_t)u;
-            const float dx = __uint_as_float(k[u].x) - A.x, dz = __uint_as_float(k[u].y) - A.z;
-            bool keep;
-            if (MODE == 0)
-                keep = (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi) & (int)((k[u].z & FL_JUMP) == 0u);
-            else if (MODE == 1)
-                keep = (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in) &
-                       (int)((k[u].z & FL_JUMP) == 0u);
-            else
-                keep = (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi) & (int)(b != A.a) &
-                       ((int)((k[u].z & FL_JUMP) == 0u) | (int)(A.a < b));
-            keep = keep & (int)(t + (uint32_t)u < len) & (int)(((k[u].z | A.fl) & FL_CHG) != 0u);
+            const bool keep = band_keep<MODE>(A, C, k[u], b) & (t + (uint32_t)u < len);
             qpush(L, w, Q, keep, A.a, b);
         }
         if (Q.qn > QCAP - U * WAVE) {
