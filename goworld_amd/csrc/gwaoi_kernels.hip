@@ -107,22 +107,13 @@ __device__ __forceinline__ unsigned long long op_apply_one(
     const uint32_t *__restrict__ slots, const float *__restrict__ xs, const float *__restrict__ zs,
     const uint32_t *__restrict__ sps, uint32_t i, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick,
     uint32_t n_total, const unsigned long long *__restrict__ seqs, unsigned long long seq0,
-    unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, bool check_claim = true,
-    const uint2 *pre = nullptr) {
+    unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, bool check_claim = true) {
     const uint32_t j = j0 + i;
     const uint32_t s = slots[i];
     if (s >= max_slots) return 0;
-    uint32_t idx, cur_sp;
-    if (pre) {  // rank, sp loaded by the caller (alongside its claim)
-        idx = pre->x;
-        cur_sp = pre->y;
-    } else {
-        const uint4 si = reinterpret_cast<const uint4 *>(info)[s];  // lastop, rank, sp: one line
-        if (check_claim && (((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j))
-            return 0;
-        idx = si.z;
-        cur_sp = si.w;
-    }
+    const uint4 si = reinterpret_cast<const uint4 *>(info)[s];  // lastop, rank, sp: one line
+    if (check_claim && (((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return 0;
+    const uint32_t idx = si.z, cur_sp = si.w;
     if (idx >= n_total) {
         atomicOr(&sc->err, ERR_MOVE_DEAD);
         return 0;
@@ -198,13 +189,11 @@ __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uin
             atomicOr(&sc->err, ERR_BAD_SLOT);
         } else {
             const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
-            // rank/sp (not written during apply) load in parallel with the claim
-            const uint2 rs = reinterpret_cast<const uint2 *>(info + s)[1];
             const unsigned long long old = atomicMax(&info[s].lastop, mine);
             if ((uint32_t)(old >> 32) == tick) coll[atomicAdd(&sc->ncoll, 1u)] = s;
             if (old < mine)
                 smax = op_apply_one(R.ds, R.dx, R.dz, R.dsp, i, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
-                                    seq_floor, s_rec, s_ss, sc, false, &rs);
+                                    seq_floor, s_rec, s_ss, sc, false);
         }
     }
     if (R.dseq) {  // one atomic per wave, not per op
