@@ -178,7 +178,7 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
 inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; }
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, hipStream_t st);
+                     uint32_t leave_off, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // Special-entity pass over the previous frame in blocks of TILE_A entries
 // (O = S', the new state in the previous order, with O_ss giving its space);
 // block t's totals/bases at [tile_off + t] and [leave_off + tile_off + t].

@@ -26,6 +26,8 @@
 #include "gwaoi_internal.h"
 #include "gwaoi_device.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 
 namespace gw {
@@ -1816,11 +1818,13 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, hipStream_t st) {
+                     uint32_t leave_off, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (!F.n) return;
-    k_combined<<<combined_blocks(F.n), CT, 0, st>>>(F, cand, O_rec, seq_base, sc, &sc->counter,
-                                                    reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base,
-                                                    leave_off);
+    // hipExtLaunchKernelGGL records the events at the kernel's own start and
+    // end: no marker packets between kernels when the stage is timed
+    hipExtLaunchKernelGGL(k_combined, dim3(combined_blocks(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
+                          (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
+                          reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off);
 }
 
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,

@@ -464,10 +464,11 @@ void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_
     const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
-    stage_begin(w, ST_COMBINED);
+    // timed with the launch's own start/end events (no marker packets)
+    const bool tc = w->timing_mask >> ST_COMBINED & 1u;
+    if (tc) w->ev_used[ST_COMBINED] = true;
     gw::launch_combined(Vn, w->cand, w->orec, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
-                        half, st);
-    stage_end(w, ST_COMBINED);
+                        half, st, tc ? w->ev[ST_COMBINED][0] : nullptr, tc ? w->ev[ST_COMBINED][1] : nullptr);
     stage_begin(w, ST_SPECIAL);
     gw::launch_pairs(Vp, w->srec, w->sss, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
                      TBn, half, st);
