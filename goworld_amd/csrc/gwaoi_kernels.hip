@@ -1258,7 +1258,7 @@ constexpr int CW = CT / WAVE;
 constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= SW_U * WAVE + a drain batch)
 constexpr int SW_U = GWAOI_SW_U;  // candidates per lane per sweep iteration on long rows
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
-static_assert(QCAP >= SW_U * WAVE + WAVE, "queue must hold one sweep iteration beyond the drain mark");
+static_assert(QCAP >= SW_U * WAVE, "queue must hold one sweep iteration");
 
 struct CombinedLds {
     uint2 q[CW][QCAP];  // queued pairs of a wave: (A frame index, B frame index)
@@ -1373,6 +1373,11 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
     for (uint32_t t = 0; t < mx; t += U) {
+        if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
+            __builtin_amdgcn_wave_barrier();
+            drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
+            Q.qn = 0;
+        }
         uint3 k[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1385,13 +1390,9 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
             const bool keep = band_keep<MODE>(A, C, k[u], b) & (t + (uint32_t)u < len);
             qpush(L, w, Q, keep, A.a, b);
         }
-        if (Q.qn > QCAP - U * WAVE) {
-            __builtin_amdgcn_wave_barrier();
-            drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
-            Q.qn = 0;
-        }
     }
 }
+
 
 // Rows r0..r1 (per lane; `on` = the lane takes part), cells c0..c1 of each row.
 // The next row's candidate range is loaded while the current one is swept.
