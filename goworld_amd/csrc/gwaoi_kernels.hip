@@ -172,15 +172,24 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
     }
 }
 
-// Device Moved batches only (the per-tick position sync): one pass instead of
-// claim + apply.  Each op claims its slot with a returning atomicMax and, if
-// it is the highest claim so far, writes its state.  Two ops of one slot in
-// one flush both may write, in any order: every such slot is listed in
-// `coll` (by whichever op sees the other's claim) and k_moves_fixup rewrites
-// it from the final winner after this kernel has drained.
+// Device Moved batches only (the per-tick position sync), without an atomic
+// per move (a device-scope atomic is performed memory-side on gfx950).
+// Pass 1 (k_moves_mark) stores every op's claim with a plain 8-byte store:
+// ops of one slot race and some claim of this tick survives the kernel
+// boundary.  Pass 2 (k_moves_apply): the op whose claim survived applies; an
+// op that finds another op's claim folds its own in with atomicMax
+// (repeated slots only, rare) and lists the slot, so that k_moves_fixup
+// re-applies the true last op once this kernel has drained.
+__global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R.n) return;
+    const uint32_t s = R.ds[i];
+    if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (R.j0 + i);
+}
+
 __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                              unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc,
-                              uint32_t *coll) {
+                               unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc,
+                               uint32_t *coll) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long smax = 0;
     if (i < R.n) {
@@ -191,11 +200,14 @@ __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uin
             atomicOr(&sc->err, ERR_BAD_SLOT);
         } else {
             const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
-            const unsigned long long old = atomicMax(&info[s].lastop, mine);
-            if ((uint32_t)(old >> 32) == tick) coll[atomicAdd(&sc->ncoll, 1u)] = s;
-            if (old < mine)
+            const unsigned long long seen = info[s].lastop;
+            if (seen == mine) {
                 smax = op_apply_one(R.ds, R.dx, R.dz, R.dsp, i, R.j0, max_slots, info, tick, n_total, R.dseq, R.seq0,
                                     seq_floor, s_rec, s_ss, sc, false);
+            } else {
+                atomicMax(&info[s].lastop, mine);
+                coll[atomicAdd(&sc->ncoll, 1u)] = s;
+            }
         }
     }
     if (R.dseq) {  // one atomic per wave, not per op
@@ -1693,10 +1705,12 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, hipStream_t st) {
+    for (uint32_t q = 0; q < RS.count; ++q)  // every run's claims before any apply
+        if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
-            k_moves_apply<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id, n_total, seq_floor,
-                                                                s_rec, s_ss, sc, coll);
+            k_moves_apply<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id, n_total,
+                                                                seq_floor, s_rec, s_ss, sc, coll);
     k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
                                       sc, coll);
 }
