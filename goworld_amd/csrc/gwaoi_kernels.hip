@@ -248,14 +248,15 @@ __device__ __forceinline__ bool is_near(float xn, float zn, float xo, float zo, 
     return (int)(fabsf(xn - xo) <= thr) & (int)(fabsf(zn - zo) <= thr);
 }
 
-constexpr uint32_t FL_JUMP = 1u, FL_CHG = 2u;  // candidate flags (k_gather -> k_combined)
-
-// FL_JUMP: not "near" (new in this space, changed space, or moved > FAR_FRAC*D
-// on an axis; an absent previous state has NaN coordinates and fails
-// is_near).  FL_CHG: Enter/Moved called this flush.
-__device__ __forceinline__ uint32_t flags_of(const Rec16 &now, const Rec16 &old, unsigned long long seq_base,
-                                             float thr) {
-    return (is_near(now.x, now.z, old.x, old.z, thr) ? 0u : FL_JUMP) | (now.s >= seq_base ? FL_CHG : 0u);
+// Candidate record of the combined pass (k_gather -> k_combined), 8 B per
+// frame entry: the exact (x, z) of a "near" entity, (NaN, NaN) for a jumper
+// -- not near: new in this space, changed space, or moved > FAR_FRAC*D on an
+// axis (an absent previous state has NaN coordinates and fails is_near).
+// NaN fails every band compare, so the strip filters drop jumper partners
+// without a flag load.
+__device__ __forceinline__ uint2 cand_of(const Rec16 &now, const Rec16 &old, float thr) {
+    return is_near(now.x, now.z, old.x, old.z, thr) ? make_uint2(__float_as_uint(now.x), __float_as_uint(now.z))
+                                                    : make_uint2(0x7FC00000u, 0x7FC00000u);
 }
 
 // INCR (the grid is the previous frame's): also count, per cell, the
@@ -850,7 +851,7 @@ __device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], in
 __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
                                            const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
-                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
                                            const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
                                            SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
@@ -861,7 +862,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
 __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
-                         SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
+                         SlotSp *f_ss, Rec16 *o_rec, uint2 *cand, const SpaceGrid *__restrict__ grid,
                          unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                          uint32_t n_spaces, BBoxPart *parts) {
@@ -877,7 +878,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
 __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
                                            const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
-                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
                                            const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
                                            SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
@@ -902,7 +903,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     if (i < n_prev && ld_ss(p_ss, i).sp == ss.sp) o = ld_rec(p_rec, i);
     st_rec(o_rec, k, o);
     const float thr = FAR_FRAC * grid[ss.sp].D;
-    cand[k] = make_uint4(__float_as_uint(now.x), __float_as_uint(now.z), flags_of(now, o, seq_base, thr), 0u);
+    cand[k] = cand_of(now, o, thr);
     cur = ss.sp;
     bv[0] = bv[2] = f2o(now.x);
     bv[1] = bv[3] = f2o(now.z);
@@ -1239,7 +1240,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 // by one of its members A, in the new frame (sorted by cell).  One lane per A,
 // fixed blocks of 256 consecutive frame entries.
 //
-// Both members "near" (FL_JUMP clear: live in the same space at t-1 and moved
+// Both members "near" (not a jumper: live in the same space at t-1 and moved
 // at most d_rel*D <= D/4 per axis): N_t != N_t-1 needs the pair in the band
 // (BW = 2 d_rel D + M covers both displacements plus the float32 rounding of
 // the window bounds; lo = D - BW, hi = D + BW, all differences fl(b - a)):
@@ -1247,7 +1248,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 //   X': dx in [lo, hi] and |dz| <  lo      (B right of A, not in Z either way)
 // Z and X' are disjoint and every band pair is in exactly one of them from
 // exactly one side, so A queries two thin strips of cells instead of the
-// whole window.  Pairs where neither member changed are skipped.
+// whole window.  Pairs where neither member changed yield no event.
 // A "jumper" A (new, changed space, moved > D/4) tests its whole window
 // (|d| <= hi + M) instead; a pair of two jumpers is visited by the lower
 // frame index, and near entities skip jumper partners.
@@ -1291,7 +1292,6 @@ struct CombinedCtx {  // block-uniform
 struct LaneA {
     uint32_t a;  // frame index
     float x, z;
-    uint32_t fl;
     bool valid, jump;
 };
 
@@ -1357,21 +1357,20 @@ __device__ __forceinline__ void qpush(CombinedLds &L, int w, WaveQueue &Q, bool 
     Q.qn += (uint32_t)__popcll(m);
 }
 
-// Cheap filter of candidate b (k = cand[b]: x, z, flags) for lane A.
-// MODE 0: Z strip, 1: X' strip, 2: whole window of a jumper.
+// Cheap filter of candidate b (k = cand[b]: x, z; NaN for a jumper) for lane A.
+// MODE 0: Z strip, 1: X' strip (jumper partners fail the NaN compares), 2:
+// whole window of a jumper A -- a jumper partner is kept unfiltered by the
+// lower frame index (the full test in drain_queue has the window box).
+// Pairs where neither member changed are not filtered here: their relation
+// is unchanged and the full test finds no event.
 template <int MODE>
-__device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint3 &k, uint32_t b) {
+__device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint2 &k, uint32_t b) {
     const float lo = C.lo, hi = C.hi;
     const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
-    bool keep;
-    if (MODE == 0)
-        keep = (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi) & (int)((k.z & FL_JUMP) == 0u);
-    else if (MODE == 1)
-        keep = (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in) & (int)((k.z & FL_JUMP) == 0u);
-    else
-        keep = (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi) & (int)(b != A.a) &
-               ((int)((k.z & FL_JUMP) == 0u) | (int)(A.a < b));
-    return keep & (((k.z | A.fl) & FL_CHG) != 0u);
+    if (MODE == 0) return (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi);
+    if (MODE == 1) return (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
+    const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
+    return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
 }
 
 // Sweep candidates [jb, jb + len) of one grid row for every lane (ranges are
@@ -1380,7 +1379,7 @@ __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, 
 // all U loads issued before the first is used (one L2 round trip per U).
 template <int MODE, int U>
 __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, uint32_t jb,
-                                            uint32_t len, uint32_t mx, const uint4 *__restrict__ cand,
+                                            uint32_t len, uint32_t mx, const uint2 *__restrict__ cand,
                                             const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
@@ -1390,12 +1389,9 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
             drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
             Q.qn = 0;
         }
-        uint3 k[U];
+        uint2 k[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint4 v = cand[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
-            k[u] = make_uint3(v.x, v.y, v.z);
-        }
+        for (int u = 0; u < U; ++u) k[u] = cand[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t b = jb + t + (uint32_t)u;
@@ -1410,7 +1406,7 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
 // The next row's candidate range is loaded while the current one is swept.
 template <int MODE>
 __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int r0,
-                                           int r1, int c0, int c1, const uint4 *__restrict__ cand, const FrameView &F,
+                                           int r1, int c0, int c1, const uint2 *__restrict__ cand, const FrameView &F,
                                            const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
                                            uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
@@ -1441,7 +1437,7 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
     }
 }
 
-__device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
+__device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
                                uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const int w = threadIdx.x / WAVE;
@@ -1491,7 +1487,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
 // spaces (small spaces) sweeps once per distinct space among a wave's lanes.
-__global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__restrict__ cand,
+__global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint2 *__restrict__ cand,
                                                  const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
                                                  const TickScalars *__restrict__ sc, unsigned long long *counter,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
@@ -1507,11 +1503,11 @@ __global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint4 *__res
     A.a = e0 + tid;
     A.valid = A.a < F.n;
     const uint32_t ia = A.valid ? A.a : 0u;
-    const uint4 ca = cand[ia];
-    A.x = __uint_as_float(ca.x);
-    A.z = __uint_as_float(ca.y);
-    A.fl = ca.z;
-    A.jump = (ca.z & FL_JUMP) != 0u;
+    const uint2 ca = cand[ia];
+    const Rec16 ra = ld_rec(F.rec, ia);  // exact position (a jumper's candidate record is NaN)
+    A.x = ra.x;
+    A.z = ra.z;
+    A.jump = __uint_as_float(ca.x) != __uint_as_float(ca.x);
     // spaces of the block: first and last entry (frame is space-major)
     const uint32_t my_sp = ld_ss(F.ss, ia).sp;
 
@@ -1806,7 +1802,7 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 }
 
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
-                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                    uint32_t n_spaces, void *bbox_parts, hipStream_t st) {
@@ -1831,7 +1827,7 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
                                                     tile_base, tile_off, leave_off);
 }
 
-void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
+void launch_combined(FrameView F, const uint2 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (!F.n) return;
