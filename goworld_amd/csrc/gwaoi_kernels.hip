@@ -1273,9 +1273,13 @@ constexpr int SW_U = GWAOI_SW_U;  // candidates per lane per sweep iteration on 
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
 static_assert(QCAP >= SW_U * WAVE, "queue must hold one sweep iteration");
 
+// A queued pair is (A, B): A is one of the block's own entries, so it is kept
+// as its offset in the block (1 B) next to B's frame index (4 B).  5 B per
+// entry keeps the block under 20 KB of LDS (8 blocks per CU).
 struct CombinedLds {
-    uint2 q[CW][QCAP];  // queued pairs of a wave: (A frame index, B frame index)
-    uint2 ev[CW][EVW];  // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
+    uint32_t qb[CW][QCAP];  // queued pairs of a wave: B frame index
+    uint8_t qa[CW][QCAP];   //   ... A frame index - block start
+    uint2 ev[CW][EVW];      // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
     uint32_t wcnt[CW][2];
     unsigned long long base;
     uint32_t te, tl;
@@ -1303,7 +1307,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // Full test of the queued pairs of wave w; appends events (deterministic order).
 // replay: count only, and write events number >= EVW straight to the output.
-__device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, const FrameView &F,
+__device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, uint32_t e0, const FrameView &F,
                                          const Rec16 *__restrict__ O_rec, const PairCtx &proto, float thr,
                                          uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap, unsigned long long pe,
                                          unsigned long long pl, bool replay) {
@@ -1313,9 +1317,8 @@ __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, 
         int kind = 0;
         uint32_t a = 0, b = 0;
         if (e < qn) {
-            const uint2 q = L.q[w][e];
-            a = q.x;
-            b = q.y;
+            a = e0 | (uint32_t)L.qa[w][e];
+            b = L.qb[w][e];
             PairCtx A = proto;
             A.a = a;
             A.now = ld_rec(F.rec, a);
@@ -1353,7 +1356,11 @@ struct WaveQueue {
 // Append (a, b) for the lanes with keep set.  Wave-uniform.
 __device__ __forceinline__ void qpush(CombinedLds &L, int w, WaveQueue &Q, bool keep, uint32_t a, uint32_t b) {
     const unsigned long long m = __ballot(keep);
-    if (keep) L.q[w][Q.qn + (uint32_t)__popcll(m & lanemask_lt())] = make_uint2(a, b);
+    if (keep) {
+        const uint32_t i = Q.qn + (uint32_t)__popcll(m & lanemask_lt());
+        L.qb[w][i] = b;
+        L.qa[w][i] = (uint8_t)(a & (uint32_t)(CT - 1));
+    }
     Q.qn += (uint32_t)__popcll(m);
 }
 
@@ -1386,7 +1393,8 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
     for (uint32_t t = 0; t < mx; t += U) {
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
             __builtin_amdgcn_wave_barrier();
-            drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
+            drain_queue(L, w, Q.qn, A.a & ~(uint32_t)(CT - 1), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl,
+                        replay);
             Q.qn = 0;
         }
         uint2 k[U];
@@ -1479,7 +1487,8 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__re
     }
     if (Q.qn) {
         __builtin_amdgcn_wave_barrier();
-        drain_queue(L, w, Q.qn, F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
+        drain_queue(L, w, Q.qn, A.a & ~(uint32_t)(CT - 1), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl,
+                        replay);
     }
     ne = Q.ne;
     nl = Q.nl;
@@ -1487,7 +1496,15 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__re
 
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
 // spaces (small spaces) sweeps once per distinct space among a wave's lanes.
-__global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint2 *__restrict__ cand,
+#ifndef GWAOI_COMBINED_WPE
+#define GWAOI_COMBINED_WPE 0
+#endif
+#if GWAOI_COMBINED_WPE
+#define COMBINED_ATTR __attribute__((amdgpu_waves_per_eu(GWAOI_COMBINED_WPE)))
+#else
+#define COMBINED_ATTR
+#endif
+__global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, const uint2 *__restrict__ cand,
                                                  const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
                                                  const TickScalars *__restrict__ sc, unsigned long long *counter,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
@@ -1518,7 +1535,7 @@ __global__ __launch_bounds__(CT) void k_combined(FrameView F, const uint2 *__res
         unsigned long long pending = __ballot(A.valid);
         while (pending) {
             const uint32_t lead = (uint32_t)__ffsll((long long)pending) - 1u;
-            const uint32_t sp = __shfl(my_sp, (int)lead);
+            const uint32_t sp = __builtin_amdgcn_readfirstlane(__shfl(my_sp, (int)lead));  // wave-uniform: scalar grid loads
             const bool mine = A.valid && my_sp == sp;
             pending &= ~__ballot(mine);
             CombinedCtx C;
