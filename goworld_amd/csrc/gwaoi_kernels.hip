@@ -1348,6 +1348,16 @@ __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, 
     }
 }
 
+// First frame entry of A's block, as a scalar (blocks are CT-aligned).
+__device__ __forceinline__ uint32_t block_start(const LaneA &A) {
+    return __builtin_amdgcn_readfirstlane(A.a & ~(uint32_t)(CT - 1));
+}
+
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 struct WaveQueue {
     uint32_t qn;
     uint32_t ne, nl;
@@ -1393,8 +1403,7 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
     for (uint32_t t = 0; t < mx; t += U) {
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
             __builtin_amdgcn_wave_barrier();
-            drain_queue(L, w, Q.qn, A.a & ~(uint32_t)(CT - 1), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl,
-                        replay);
+            drain_queue(L, w, Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
             Q.qn = 0;
         }
         uint2 k[U];
@@ -1487,8 +1496,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__re
     }
     if (Q.qn) {
         __builtin_amdgcn_wave_barrier();
-        drain_queue(L, w, Q.qn, A.a & ~(uint32_t)(CT - 1), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl,
-                        replay);
+        drain_queue(L, w, Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
     }
     ne = Q.ne;
     nl = Q.nl;
@@ -1586,7 +1594,8 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     }
     __syncthreads();
     const uint32_t pre_e = L.wcnt[w][0], pre_l = L.wcnt[w][1];
-    const unsigned long long pe = L.base + 2ull * pre_e, pl = L.base + 2ull * L.te + 2ull * pre_l;
+    const unsigned long long pe = uniform_u64(L.base + 2ull * pre_e),
+                             pl = uniform_u64(L.base + 2ull * L.te + 2ull * pre_l);
     // buffered events of this wave, in order, split by kind
     const uint32_t nbuf = min(ne + nl, (uint32_t)EVW);
     uint32_t ie = 0, il = 0;
