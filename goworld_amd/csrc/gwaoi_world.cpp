@@ -22,6 +22,7 @@
 #include <limits>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 using gw::SpaceGrid;
@@ -131,6 +132,10 @@ struct gwaoi_world {
     std::vector<unsigned long long> h_op_seq;
     std::vector<Run> runs;
     size_t n_ops = 0;
+    // host move batches (gwaoi_moved_batch) staged as [slots | x | z | space] in pinned memory and sent
+    // with one async H2D each; they then run as device batches.  Words in use until the flush.
+    uint32_t *h_stage = nullptr, *d_stage = nullptr;
+    size_t stage_cap = 0, stage_used = 0;
     std::vector<uint32_t> new_slots;
     std::vector<uint32_t> touched;  // slots whose liveness changed since the last flush
     // seq_next: the seq the next implicit call gets (advanced at queue time);
@@ -689,6 +694,7 @@ int run_tick(gwaoi_world *w) {
     w->h_op_seq.clear();
     w->runs.clear();
     w->n_ops = 0;
+    w->stage_used = 0;  // the flush synchronised the stream: every staged H2D has landed
     if (w->dev_seq_pending && r.seq_max >= w->seq_next) w->seq_next = r.seq_max + 1;
     w->dev_seq_pending = false;
     w->seq_floor = w->seq_next;
@@ -758,6 +764,8 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->h_out) (void)hipHostFree(w->h_out);
     if (w->h_events) (void)hipHostFree(w->h_events);
     if (w->h_grid) (void)hipHostFree(w->h_grid);
+    if (w->h_stage) (void)hipHostFree(w->h_stage);
+    dfree(w->d_stage);
     for (int s = 0; s < ST_N; ++s)
         for (int q = 0; q < 2; ++q)
             if (w->ev[s][q]) (void)hipEventDestroy(w->ev[s][q]);
@@ -914,6 +922,108 @@ int moved_impl(gwaoi_world *w, uint32_t slot, float x, float z, const uint64_t *
     return GWAOI_OK;
 }
 
+constexpr size_t kStageMinBatch = 64;  // smaller host batches queue as host ops
+
+// Room for `words` more staged words.  1: no room without moving a buffer that a queued
+// batch still points into (the caller then queues the batch as host ops).
+int ensure_stage(gwaoi_world *w, size_t words) {
+    if (w->stage_used + words <= w->stage_cap) return GWAOI_OK;
+    if (w->stage_used) return 1;
+    const size_t cap = std::max<size_t>({words, 2 * w->stage_cap, (size_t)4 << 16});
+    if (w->h_stage) (void)hipHostFree(w->h_stage);
+    w->h_stage = nullptr;
+    dfree(w->d_stage);
+    w->stage_cap = 0;
+    HIP_TRY(hipHostMalloc((void **)&w->h_stage, cap * sizeof(uint32_t), hipHostMallocDefault));
+    if (int rc = dalloc(w, &w->d_stage, cap)) return rc;
+    w->stage_cap = cap;
+    return GWAOI_OK;
+}
+
+struct StageBox {  // positions of one space seen by one staging chunk
+    float x0, z0, x1, z1;
+    bool any;
+};
+
+// Validate moves [lo, hi) in call order (the checks and their order of gwaoi_moved) and write them
+// into the staging words h = [slots | x | z | space] (n each).  Returns the first bad index (hi if
+// none) with its status in *st; boxes[space] gathers the chunk's positions.
+size_t stage_chunk(const gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n,
+                   size_t lo, size_t hi, uint32_t *h, StageBox *boxes, int *st) {
+    uint32_t *hs = h, *hsp = h + 3 * n;
+    float *hx = reinterpret_cast<float *>(h + n), *hz = reinterpret_cast<float *>(h + 2 * n);
+    const uint8_t *alive = w->alive.data();
+    const uint32_t *space_of = w->space_of.data();
+    for (size_t i = lo; i < hi; ++i) {
+        const uint32_t sl = slots[i];
+        const float xi = x[i], zi = z[i];
+        if (sl >= w->max_slots) { *st = GWAOI_EBADSLOT; return i; }
+        if (!alive[sl]) { *st = GWAOI_ESTATE; return i; }
+        if (!finite2(xi, zi)) { *st = GWAOI_ENONFINITE; return i; }
+        const uint32_t sp = space_of[sl];
+        hs[i] = sl; hx[i] = xi; hz[i] = zi; hsp[i] = sp;
+        StageBox &b = boxes[sp];
+        if (!b.any) {
+            b = StageBox{xi, zi, xi, zi, true};
+        } else {
+            b.x0 = std::min(b.x0, xi); b.x1 = std::max(b.x1, xi);
+            b.z0 = std::min(b.z0, zi); b.z1 = std::max(b.z1, zi);
+        }
+    }
+    *st = GWAOI_OK;
+    return hi;
+}
+
+// A host move batch with room in the staging area (ensure_stage): validate + stage it on up to
+// kStageThreads host threads, send it with one async H2D and queue it as a device batch with seqs
+// seq_next.. and the slot's space at call time (explicit, so a slot that entered earlier in this
+// flush moves exactly as a host op would).  Nothing is queued if any move is rejected.
+constexpr size_t kStageThreadMin = 1 << 17;  // moves per extra thread
+constexpr unsigned kStageThreads = 8;
+
+int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
+    uint32_t *h = w->h_stage + w->stage_used, *d = w->d_stage + w->stage_used;
+    const size_t nsp = std::max(1u, w->n_space_ids);
+    unsigned T = (unsigned)std::min<size_t>(kStageThreads, std::max<size_t>(1, n / kStageThreadMin));
+    T = std::min(T, std::max(1u, std::thread::hardware_concurrency()));
+    const size_t stride = nsp + 4;  // >= 64 B between the threads' boxes: no false sharing
+    std::vector<StageBox> boxes((size_t)T * stride, StageBox{0, 0, 0, 0, false});
+    std::vector<size_t> bad(T);
+    std::vector<int> st(T, GWAOI_OK);
+    const size_t chunk = (n + T - 1) / T;
+    auto run = [&](unsigned t) {
+        const size_t lo = std::min(n, t * chunk), hi = std::min(n, lo + chunk);
+        bad[t] = stage_chunk(w, slots, x, z, n, lo, hi, h, boxes.data() + (size_t)t * stride, &st[t]);
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < T; ++t) pool.emplace_back(run, t);
+    run(0);
+    for (std::thread &th : pool) th.join();
+    for (unsigned t = 0; t < T; ++t)  // chunks are in call order: the first bad chunk has the first bad move
+        if (st[t] != GWAOI_OK) return st[t];
+    for (unsigned t = 0; t < T; ++t)
+        for (size_t sp = 0; sp < nsp; ++sp) {
+            const StageBox &b = boxes[(size_t)t * stride + sp];
+            if (!b.any) continue;
+            note_pending_bbox(w->spaces[sp], b.x0, b.z0);
+            note_pending_bbox(w->spaces[sp], b.x1, b.z1);
+        }
+    HIP_TRY(hipMemcpyAsync(d, h, 4 * n * sizeof(uint32_t), hipMemcpyHostToDevice, w->stream));
+    w->stage_used += 4 * n;
+    Run r{};
+    r.device = true;
+    r.ds = d;
+    r.dx = reinterpret_cast<const float *>(d + n);
+    r.dz = reinterpret_cast<const float *>(d + 2 * n);
+    r.dsp = d + 3 * n;
+    r.seq0 = w->seq_next;
+    r.dn = n;
+    w->runs.push_back(r);
+    w->n_ops += n;
+    w->seq_next += n;
+    return GWAOI_OK;
+}
+
 }  // namespace
 
 int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z) {
@@ -982,6 +1092,10 @@ int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
 int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
     if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
+    // Batches of kStageMinBatch+ moves go through pinned staging as one device batch (single-pass
+    // move apply); without room (or if the staging allocation failed) they queue as host ops.
+    if (n >= kStageMinBatch && n <= 0xFFFFFFFFull - w->n_ops && ensure_stage(w, 4 * n) == GWAOI_OK)
+        return stage_moves(w, slots, x, z, n);
     for (size_t i = 0; i < n; ++i) {
         if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
         if (!w->alive[slots[i]]) return GWAOI_ESTATE;

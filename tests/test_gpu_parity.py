@@ -267,6 +267,88 @@ def test_scaled_configs_vs_closed_form_gpu(oracle_mod, cfg, n, ticks):
             np.testing.assert_array_equal(w.neighbors(i), want)
 
 
+def test_staged_host_batches_mixed_with_calls_gpu(oracle_mod):
+    """Host move batches go through pinned staging + one H2D each (>= 64 moves) and run as
+    device batches.  Interleave them in one flush with single Moved/Enter/Leave calls, small
+    batches (host ops), a batch past the staging capacity (falls back to host ops) and repeated
+    slots; the sequential XZ-list oracle decides every event."""
+    rng = np.random.default_rng(11)
+    n = 90000
+    wl = make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wl.initial()
+    live = np.zeros(n, bool)
+    m = oracle_mod.XZList(wl.D, n)
+    with World(n) as w:
+        s = w.space_create(wl.D)
+        k0 = n - 2000  # the last 2000 slots enter and leave along the way
+        w.enter_batch(s, slots[:k0], x0[:k0], z0[:k0])
+        m.bulk_enter(slots[:k0], x0[:k0], z0[:k0])
+        live[slots[:k0]] = True
+        flush(w)
+        m.take_events()
+        x, z = x0.copy(), z0.copy()
+
+        def batch(k, span=None):
+            pool = np.nonzero(live)[0] if span is None else np.nonzero(live)[0][:span]
+            sl = rng.choice(pool, k).astype(np.uint32)  # with repeats
+            nx = (x[sl] + rng.uniform(-40, 40, k)).astype(np.float32)
+            nz = (z[sl] + rng.uniform(-40, 40, k)).astype(np.float32)
+            w.moved_batch(sl, nx, nz)
+            m.moved_batch(sl, nx, nz)
+            x[sl], z[sl] = nx, nz
+
+        for t in range(3):
+            batch(5000)
+            for i in rng.choice(np.nonzero(~live)[0], 300, replace=False):  # Enter between batches
+                w.enter(s, int(i), x[i], z[i])
+                m.enter(int(i), x[i], z[i])
+                live[i] = True
+            batch(70)
+            batch(40)  # below the staging threshold: host ops
+            for i in rng.choice(np.nonzero(live)[0], 200, replace=False):
+                w.leave(int(i))
+                m.leave(int(i))
+                live[i] = False
+            j = int(np.nonzero(live)[0][0])
+            w.moved(j, x[j] + np.float32(3), z[j])
+            m.moved(j, x[j] + np.float32(3), z[j])
+            x[j] += np.float32(3)
+            batch(64000 if t == 1 else 3000, span=500 if t == 2 else None)  # t=1: past capacity
+            ge, gl = flush(w)
+            oe, ol = oracle_mod.net_events(*m.take_events())
+            np.testing.assert_array_equal(ge, oe)
+            np.testing.assert_array_equal(gl, ol)
+        for i in np.nonzero(live)[0][::997]:
+            np.testing.assert_array_equal(w.neighbors(int(i)), np.asarray(m.neighbors(int(i)), np.uint32))
+
+
+@pytest.mark.parametrize("bad", ["slot", "dead", "nan"])
+def test_staged_host_batch_rejects_whole_batch_gpu(bad):
+    """A staged host batch (>= 64 moves, validated on several host threads when large) with one bad
+    move is rejected as a whole with the same status as per-call Moved, and queues nothing."""
+    n = 300000
+    rng = np.random.default_rng(3)
+    with World(n + 1) as w:
+        s = w.space_create(D)
+        x0 = rng.uniform(-3000, 3000, n).astype(np.float32)
+        z0 = rng.uniform(-3000, 3000, n).astype(np.float32)
+        w.enter_batch(s, np.arange(n, dtype=np.uint32), x0, z0)
+        flush(w)
+        sl = np.arange(n, dtype=np.uint32)
+        nx = (x0 + np.float32(500)).astype(np.float32)  # would change most relations
+        k = n - 12345  # in the last host thread's chunk
+        if bad == "slot":
+            sl[k] = n + 7
+        elif bad == "dead":
+            sl[k] = n  # never entered
+        else:
+            nx[k] = np.float32("nan")
+        with pytest.raises(GwaoiError):
+            w.moved_batch(sl, nx, z0)
+        ent, lev = flush(w)
+        assert ent.size == 0 and lev.size == 0
+
+
 def test_device_batch_matches_host_batch_gpu():
     torch = pytest.importorskip("torch")
     wl_a = make_workload("cfg2", n=8000)
