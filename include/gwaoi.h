@@ -118,7 +118,9 @@ int gwaoi_leave(gwaoi_world *w, uint32_t slot);
 int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z);
 
 /* Batched forms (array order = call order).  Validated as a whole: on error
- * nothing is queued. */
+ * nothing is queued.  gwaoi_moved_batch copies the arrays before it returns
+ * (batches of 64+ moves into pinned staging, sent with one async H2D), so the
+ * caller may reuse them at once. */
 int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, const float *x,
                       const float *z, size_t n);
 int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n);
