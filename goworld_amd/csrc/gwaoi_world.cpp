@@ -97,6 +97,10 @@ struct gwaoi_world {
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
     size_t cnt64_cap = 0;
     bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
+    // End-of-flush wait: poll an event (default) or block in hipStreamSynchronize
+    // (GWAOI_BLOCKING_SYNC=1, A/B check).
+    hipEvent_t done_ev = nullptr;
+    bool blocking_sync = false;
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
@@ -209,6 +213,22 @@ void stage_collect(gwaoi_world *w) {
         }
         w->ev_used[s] = false;
     }
+}
+
+// Wait until the world's stream has drained.  The flush ends with a small D2H
+// that the host needs at once; polling an event returns as soon as it lands,
+// where the blocking wait of hipStreamSynchronize adds tens of microseconds of
+// wake-up latency to every tick.
+int wait_stream(gwaoi_world *w) {
+    if (w->blocking_sync || !w->done_ev) {
+        HIP_TRY(hipStreamSynchronize(w->stream));
+        return GWAOI_OK;
+    }
+    HIP_TRY(hipEventRecord(w->done_ev, w->stream));
+    hipError_t e;
+    while ((e = hipEventQuery(w->done_ev)) == hipErrorNotReady) __builtin_ia32_pause();
+    HIP_TRY(e);
+    return GWAOI_OK;
 }
 
 int ensure_scan_tmp(gwaoi_world *w, size_t n) {
@@ -646,7 +666,7 @@ int run_tick(gwaoi_world *w) {
     HIP_TRY(hipGetLastError());
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
     HIP_TRY(hipMemcpyAsync(w->h_out, w->dev_out, out_bytes, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = wait_stream(w))) return rc;
 
     gw::TickOut r = *tick_out(w);
     if (r.total64 > 0xFFFFFFFFull) {
@@ -661,7 +681,7 @@ int run_tick(gwaoi_world *w) {
         launch_pair_passes(w, Fn, P, seq_base);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(w->h_out, w->dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        if ((rc = wait_stream(w))) return rc;
         r = *tick_out(w);
     }
     stage_collect(w);
@@ -769,6 +789,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     for (int s = 0; s < ST_N; ++s)
         for (int q = 0; q < 2; ++q)
             if (w->ev[s][q]) (void)hipEventDestroy(w->ev[s][q]);
+    if (w->done_ev) (void)hipEventDestroy(w->done_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return GWAOI_OK;
@@ -838,6 +859,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     for (int s = 0; s < ST_N; ++s)
         for (int q = 0; q < 2; ++q)
             if (hipEventCreate(&w->ev[s][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
+    if (hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming) != hipSuccess) return fail(GWAOI_EDEVICE);
+    if (const char *e = std::getenv("GWAOI_BLOCKING_SYNC")) w->blocking_sync = e[0] == '1';
     w->alive.assign(N, 0);
     w->in_frame.assign(N, 0);
     w->appended.assign(N, 0);
@@ -1220,11 +1243,11 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
     if (tot) {
         hipError_t e = hipMemcpyAsync(w->h_events, w->events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       w->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
         if (e != hipSuccess) {
             w->last_error = std::string("event D2H: ") + hipGetErrorString(e);
             return GWAOI_EDEVICE;
         }
+        if (int rw = wait_stream(w)) return rw;
     }
     stage_end(w, ST_D2H);
     if (w->timing_mask) {
