@@ -458,10 +458,13 @@ def main():
     ne0, nl0 = w.tick_device()  # populate: every pair is an enter event
     setup_s = time.perf_counter() - t_setup
 
+    # device addresses of each tick's batch, taken once (torch row views cost microseconds of host time
+    # per call, during which the GPU would sit idle between ticks)
+    row_ptrs = [(d_slots[t].data_ptr(), d_x[t].data_ptr(), d_z[t].data_ptr()) for t in range(ticks)]
+
     def step(t):
-        row = t
-        w.moved_batch_device(d_slots[row].data_ptr(), d_x[row].data_ptr(), d_z[row].data_ptr(),
-                             moves_per_tick[row])
+        ps, px, pz = row_ptrs[t]
+        w.moved_batch_device(ps, px, pz, moves_per_tick[t])
         return w.tick_device()
 
     # warmup; its last ticks time every stage to find the dominant one
