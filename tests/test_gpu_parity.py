@@ -322,6 +322,38 @@ def test_staged_host_batches_mixed_with_calls_gpu(oracle_mod):
             np.testing.assert_array_equal(w.neighbors(int(i)), np.asarray(m.neighbors(int(i)), np.uint32))
 
 
+def test_staged_batch_many_spaces_gpu(oracle_mod):
+    """cfg4-style world (160 spaces x 2000): each tick is one host batch of 320k moves interleaved
+    over all spaces, staged on two host threads with per-space boxes.  Events == the diff of the
+    closed-form relation, tick by tick."""
+    nsp = 160
+    wl = make_workload("cfg4", n_spaces=nsp)
+    slots, x0, z0, sp = wl.initial()
+    seq = np.zeros(wl.n, np.uint64)
+    dmap = {s: wl.D for s in range(nsp)}
+    with World(wl.n, max_spaces=nsp) as w:
+        ids = [w.space_create(wl.D) for _ in range(nsp)]
+        nxt = 1
+        for s in range(nsp):
+            sel = np.nonzero(sp == s)[0]
+            w.enter_batch(ids[s], slots[sel], x0[sel], z0[sel])
+            seq[slots[sel]] = nxt + np.arange(sel.size, dtype=np.uint64)
+            nxt += sel.size
+        flush(w)
+        prev = oracle_mod.closed_form_pairs(wl.x, wl.z, seq, sp, dmap)
+        for t in range(2):
+            sl, nx, nz = wl.tick(t)
+            assert sl.size >= 2 * (1 << 17)  # two staging threads
+            w.moved_batch(sl, nx, nz)
+            seq[sl] = nxt + np.arange(sl.size, dtype=np.uint64)
+            nxt += sl.size
+            ge, gl = flush(w)
+            cur = oracle_mod.closed_form_pairs(wl.x, wl.z, seq, sp, dmap)
+            np.testing.assert_array_equal(ge, np.setdiff1d(cur, prev))
+            np.testing.assert_array_equal(gl, np.setdiff1d(prev, cur))
+            prev = cur
+
+
 @pytest.mark.parametrize("bad", ["slot", "dead", "nan"])
 def test_staged_host_batch_rejects_whole_batch_gpu(bad):
     """A staged host batch (>= 64 moves, validated on several host threads when large) with one bad
