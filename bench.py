@@ -376,6 +376,9 @@ def main():
     ap.add_argument("--spaces", type=int, default=None, help="cfg4: total spaces (default 8192)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="bracket the dominant kernel with HIP events on every k-th timed tick (the events "
+                         "stall the queue for ~10 us around the launch)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: exchange through host memory (multi-rank rehearsal on one GPU)")
     ap.add_argument("--no-timing", action="store_true", help="no HIP events at all (no roofline / breakdown)")
@@ -491,8 +494,11 @@ def main():
     events = 0
     moves = 0
     t0 = time.perf_counter()
+    every = max(1, args.time_every)
     for t in range(args.warmup, timed_end):
         a = time.perf_counter()
+        if not args.no_timing:
+            w.set_stage_timing([dom] if (t - args.warmup) % every == 0 else [])
         ne, nl = step(t)
         lat.append(time.perf_counter() - a)
         events += ne + nl
@@ -557,7 +563,8 @@ def main():
             roofline = {"bound": "hbm", "kernel": STAGE_KERNEL[dom], "achieved": round(ach, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
                         "traffic": pmc_traffic(args.workload) if dom == "combined" else None,
-                        "alg_bytes_per_launch": alg, "avg_launch_ms": round(timed_ms[dom], 4)}
+                        "alg_bytes_per_launch": alg, "avg_launch_ms": round(timed_ms[dom], 4),
+                        "timed_launches": int(timed_stages[dom][1])}
         stage_roof = {}
         if stage_ms:
             sb = stage_bytes(n, moves / max(args.steps, 1), info["total_cells"], events / max(args.steps, 1))

@@ -308,7 +308,8 @@ class World:
 
     def set_stage_timing(self, stages=None):
         """Time the named stages with HIP events (None = all, [] = none)."""
-        names = self.stage_names()
+        names = getattr(self, "_stage_names", None) or self.stage_names()
+        self._stage_names = names
         mask = (1 << len(names)) - 1 if stages is None else sum(1 << names.index(s) for s in stages)
         self._check(self._L.gwaoi_set_stage_timing(self._w, mask))
 
