@@ -1010,16 +1010,30 @@ int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const flo
     unsigned T = (unsigned)std::min<size_t>(kStageThreads, std::max<size_t>(1, n / kStageThreadMin));
     T = std::min(T, std::max(1u, std::thread::hardware_concurrency()));
     const size_t stride = nsp + 4;  // >= 64 B between the threads' boxes: no false sharing
-    std::vector<StageBox> boxes((size_t)T * stride, StageBox{0, 0, 0, 0, false});
-    std::vector<size_t> bad(T);
-    std::vector<int> st(T, GWAOI_OK);
+    std::vector<StageBox> boxes;
+    std::vector<size_t> bad;
+    std::vector<int> st;
+    std::vector<std::thread> pool;
+    try {  // no C++ exception may cross the C ABI
+        boxes.assign((size_t)T * stride, StageBox{0, 0, 0, 0, false});
+        bad.assign(T, 0);
+        st.assign(T, GWAOI_OK);
+        pool.reserve(T);
+    } catch (...) {
+        w->last_error = "moved_batch: host allocation failed";
+        return GWAOI_ENOMEM;
+    }
     const size_t chunk = (n + T - 1) / T;
     auto run = [&](unsigned t) {
         const size_t lo = std::min(n, t * chunk), hi = std::min(n, lo + chunk);
         bad[t] = stage_chunk(w, slots, x, z, n, lo, hi, h, boxes.data() + (size_t)t * stride, &st[t]);
     };
-    std::vector<std::thread> pool;
-    for (unsigned t = 1; t < T; ++t) pool.emplace_back(run, t);
+    unsigned started = 1;
+    try {
+        for (; started < T; ++started) pool.emplace_back(run, started);
+    } catch (...) {  // a thread that cannot start: its chunks run here
+    }
+    for (unsigned t = started; t < T; ++t) run(t);
     run(0);
     for (std::thread &th : pool) th.join();
     for (unsigned t = 0; t < T; ++t)  // chunks are in call order: the first bad chunk has the first bad move
