@@ -34,7 +34,7 @@ EXPORTS = [
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
-    "gwaoi_snapshot", "gwaoi_restore",
+    "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -49,7 +49,8 @@ SYNC_EXPORTS = [
     "gwaoi_entity_bind", "gwaoi_entity_bind_batch", "gwaoi_entity_unbind", "gwaoi_entity_set_client",
     "gwaoi_entity_set_syncing", "gwaoi_entity_set_position_yaw", "gwaoi_set_position_yaw",
     "gwaoi_sync_from_clients", "gwaoi_sync_from_clients_device", "gwaoi_collect_sync_infos",
-    "gwaoi_collect_sync_infos_device", "gwaoi_collect_client_events",
+    "gwaoi_collect_sync_infos_device", "gwaoi_collect_client_events", "gwaoi_entity_enter_plain",
+    "gwaoi_entity_leave_plain",
 ]
 
 SYNC_OUT_REC = 48  # ClientID[16] + EntityID[16] + x,y,z,yaw float32 (Entity.go:1233-1251)
@@ -83,6 +84,11 @@ class GateRecords(C.Structure):
                 ("offsets", C.POINTER(C.c_uint64)), ("records", C.c_void_p)]
 
 
+class Debug(C.Structure):
+    _fields_ = [("flushes", C.c_uint64), ("combined_replays", C.c_uint64), ("combined_queue_drains", C.c_uint64),
+                ("special_global", C.c_uint64), ("event_regrows", C.c_uint64)]
+
+
 class StageTime(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("ms", C.c_double), ("calls", C.c_uint64)]
 
@@ -91,6 +97,7 @@ class GwaoiError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"{STATUS.get(code, code)}: {msg}")
         self.code = code
+        self.events = None  # tick(): the committed flush's (enter, leave) pairs, still to replay
 
 
 _lib = None
@@ -127,6 +134,7 @@ def load():
         "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_neighbors": ([vp, u32, vp, sz, P(sz)], C.c_int),
         "gwaoi_world_info": ([vp, P(Info)], C.c_int),
+        "gwaoi_debug_counters": ([vp, P(Debug)], C.c_int),
         "gwaoi_stage_times": ([vp, P(StageTime), sz, P(sz)], C.c_int),
         "gwaoi_reset_stage_times": ([vp], C.c_int),
         "gwaoi_set_stage_timing": ([vp, C.c_uint32], C.c_int),
@@ -156,6 +164,8 @@ def load():
         "gwaoi_entity_set_syncing": ([vp, u32, C.c_int], C.c_int),
         "gwaoi_entity_set_position_yaw": ([vp, u32, f, f, f, f], C.c_int),
         "gwaoi_set_position_yaw": ([vp, u32, f, f, f, f], C.c_int),
+        "gwaoi_entity_enter_plain": ([vp, u32, f, f, f], C.c_int),
+        "gwaoi_entity_leave_plain": ([vp, u32], C.c_int),
         "gwaoi_sync_from_clients": ([vp, vp, sz], C.c_int),
         "gwaoi_sync_from_clients_device": ([vp, vp, sz], C.c_int),
         "gwaoi_collect_sync_infos": ([vp, P(GateRecords)], C.c_int),
@@ -261,17 +271,35 @@ class World:
 
     # ---- flush
     def tick(self):
-        """Flush; returns (enter_pairs, leave_pairs) as (n,2) uint32 arrays [a, b]."""
+        """Flush; returns (enter_pairs, leave_pairs) as (n,2) uint32 arrays [a, b].
+
+        When the flush committed but the device reported a problem in the queued
+        ops (a dropped move: ESTATE / ENONFINITE / EINVAL), the GwaoiError carries
+        the flush's events as ``.events``: they must still be replayed."""
         ev = Events()
-        self._check(self._L.gwaoi_tick(self._w, C.byref(ev)))
+        rc = self._L.gwaoi_tick(self._w, C.byref(ev))
         ne, nl = ev.n_enter, ev.n_leave
         ent = np.ctypeslib.as_array(ev.enter, shape=(2 * ne,)).reshape(ne, 2).copy() if ne else np.empty((0, 2), np.uint32)
         lev = np.ctypeslib.as_array(ev.leave, shape=(2 * nl,)).reshape(nl, 2).copy() if nl else np.empty((0, 2), np.uint32)
+        if rc != 0:
+            try:
+                self._check(rc)
+            except GwaoiError as e:
+                e.events = (ent, lev) if (ev.enter or ev.leave) else None
+                raise
         return ent, lev
 
     def tick_device(self):
+        """Flush; events stay in HBM.  Returns (n_enter, n_leave); on a committed flush
+        with a device-reported problem the GwaoiError carries them as ``.counts``."""
         ne, nl = C.c_uint64(), C.c_uint64()
-        self._check(self._L.gwaoi_tick_device(self._w, C.byref(ne), C.byref(nl)))
+        rc = self._L.gwaoi_tick_device(self._w, C.byref(ne), C.byref(nl))
+        if rc != 0:
+            try:
+                self._check(rc)
+            except GwaoiError as e:
+                e.counts = (ne.value, nl.value)
+                raise
         return ne.value, nl.value
 
     def events_device(self):
@@ -293,6 +321,12 @@ class World:
         i = Info()
         self._check(self._L.gwaoi_world_info(self._w, C.byref(i)))
         return {k: getattr(i, k) for k, _ in Info._fields_}
+
+    def debug_counters(self) -> dict:
+        """Rare-path counters summed over flushes (gwaoi_debug_counters)."""
+        d = Debug()
+        self._check(self._L.gwaoi_debug_counters(self._w, C.byref(d)))
+        return {k: getattr(d, k) for k, _ in Debug._fields_}
 
     def stage_times(self) -> dict:
         arr = (StageTime * 32)()
@@ -364,6 +398,13 @@ class World:
     def entity_set_position_yaw(self, slot, x, y, z, yaw):
         self._check(self._L.gwaoi_entity_set_position_yaw(self._w, slot, C.c_float(x), C.c_float(y),
                                                           C.c_float(z), C.c_float(yaw)))
+
+    def entity_enter_plain(self, slot, x, y, z):
+        """Space.enter of a space without AOI (or an entity type without AOI)."""
+        self._check(self._L.gwaoi_entity_enter_plain(self._w, slot, C.c_float(x), C.c_float(y), C.c_float(z)))
+
+    def entity_leave_plain(self, slot):
+        self._check(self._L.gwaoi_entity_leave_plain(self._w, slot))
 
     def set_position_yaw(self, slot, x, y, z, yaw):
         self._check(self._L.gwaoi_set_position_yaw(self._w, slot, C.c_float(x), C.c_float(y), C.c_float(z),

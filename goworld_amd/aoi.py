@@ -144,7 +144,14 @@ class AOIWorld:
         """Run the tick and replay the net callbacks.  Returns (n_enter, n_leave)
         directed events."""
         self._submit()
-        ent, lev = self.world.tick()
+        err = None
+        try:
+            ent, lev = self.world.tick()
+        except GwaoiError as e:  # committed with a dropped op: replay the events, then report
+            if e.events is None:
+                raise
+            ent, lev = e.events
+            err = e
         by = self._by_slot
         for a, b in lev.tolist():
             A = by[a]
@@ -159,6 +166,8 @@ class AOIWorld:
                 by[s] = None
                 self._free.append(s)
         self._quarantine = []
+        if err is not None:
+            raise err
         return len(ent), len(lev)
 
     def neighbors(self, aoi: AOI) -> List[AOI]:

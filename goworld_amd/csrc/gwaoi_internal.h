@@ -5,9 +5,25 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <new>
+
 struct gwaoi_world;  // include/gwaoi.h
 
 namespace gw {
+
+// Every extern "C" entry point runs its body through api_guard: no C++
+// exception (std::bad_alloc from a vector, a thread that cannot start, ...)
+// may cross the C ABI into a cgo host, where it would end in std::terminate.
+template <class F>
+inline int api_guard(F &&f) noexcept {
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        return -4;  // GWAOI_ENOMEM
+    } catch (...) {
+        return -5;  // GWAOI_EDEVICE
+    }
+}
 
 constexpr uint32_t SP_DEAD = 0xFFFFFFFFu;  // slot not live (or left this tick)
 constexpr uint32_t SP_KEEP = 0xFFFFFFFEu;  // device move: keep the space of the previous flush
@@ -79,6 +95,15 @@ struct TickScalars {
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply)
     uint32_t pad2;
+    uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
+};
+
+// Rare-path counters of one flush (gwaoi_debug_counters accumulates them).
+enum : uint32_t {
+    DBG_COMBINED_REPLAY = 0,  // k_combined waves whose event buffer (EVW) overflowed: sweep replayed
+    DBG_COMBINED_DRAIN = 1,   // k_combined survivor-queue drains in the middle of a sweep (QCAP full)
+    DBG_SPECIAL_GLOBAL = 2,   // special-pass lanes with more events than their LDS slots (global path)
+    DBG_N = 4
 };
 
 // Device -> host block copied once per tick: result + per-space bbox.
@@ -90,6 +115,7 @@ struct TickOut {
     unsigned long long total64;
     unsigned long long seq_max;
     unsigned long long pad2;
+    uint32_t dbg[4];  // TickScalars::dbg
     // followed by int4 bbox[n_spaces] (ordered-int min x, min z, max x, max z)
 };
 
@@ -221,6 +247,7 @@ int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_
 uint32_t world_slot_space(gwaoi_world *w, uint32_t slot);
 // Hooks the world calls when a sync layer is attached.
 void sync_note_slot(SyncState *s, uint32_t slot, uint32_t space_or_dead);
+bool sync_slot_plain(const SyncState *s, uint32_t slot);  // in a space without AOI
 void sync_destroy(SyncState *s);
 
 }  // namespace gw

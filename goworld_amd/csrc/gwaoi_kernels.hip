@@ -60,6 +60,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->bmax = 0.0f;
         sc->seq_max = 0;
         sc->ncoll = 0;
+        for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
     if (i < n0) z0[i] = 0;
     if (i < n1) z1[i] = 0;
@@ -1033,7 +1034,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
                                               const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
                                               unsigned long long *counter, uint2 *tmp, uint64_t cap,
                                               uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
-                                              uint32_t leave_off) {
+                                              uint32_t leave_off, uint32_t *dbg) {
     __shared__ uint4 s_now[PCAP];
     __shared__ uint4 s_oth[PCAP];
     __shared__ uint32_t s_slot[PCAP];
@@ -1224,6 +1225,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
                 }
             }
             if (nk > PS) {
+                atomicAdd(dbg + DBG_SPECIAL_GLOBAL, 1u);
                 uint32_t we = 0, wl = 0;  // continue after the buffered events, in order
                 enum_global<MODE, true>(F, O_rec, O_ss, g, A, thr, cx0, cx1, cz0, cz1, PS, tmp, pe + 2ull * ie,
                                         pl + 2ull * il, cap, we, wl);
@@ -1361,6 +1363,7 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) 
 struct WaveQueue {
     uint32_t qn;
     uint32_t ne, nl;
+    uint32_t drains;  // queue drains forced in the middle of a sweep (DBG_COMBINED_DRAIN)
 };
 
 // Append (a, b) for the lanes with keep set.  Wave-uniform.
@@ -1402,6 +1405,7 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                                             bool replay) {
     for (uint32_t t = 0; t < mx; t += U) {
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
+            ++Q.drains;
             __builtin_amdgcn_wave_barrier();
             drain_queue(L, w, Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
             Q.qn = 0;
@@ -1456,10 +1460,11 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
 
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
-                               uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
+                               uint32_t &drains, uint2 *out, uint64_t cap, unsigned long long pe,
+                               unsigned long long pl, bool replay) {
     const int w = threadIdx.x / WAVE;
     const SpaceGrid &g = C.g;
-    WaveQueue Q{0u, ne, nl};
+    WaveQueue Q{0u, ne, nl, 0u};
     const float lo = C.lo, hi = C.hi, M = C.M;
     const bool strip = A.valid && !A.jump && C.band_ok;
     const bool whole = A.valid && (A.jump || !C.band_ok);
@@ -1500,6 +1505,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__re
     }
     ne = Q.ne;
     nl = Q.nl;
+    drains += Q.drains;
 }
 
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
@@ -1516,7 +1522,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
                                                  const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
                                                  const TickScalars *__restrict__ sc, unsigned long long *counter,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
-                                                 unsigned long long *tile_base, uint32_t leave_off) {
+                                                 unsigned long long *tile_base, uint32_t leave_off, uint32_t *dbg) {
     __shared__ CombinedLds L;
     const uint32_t t = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t tid = threadIdx.x, ln = lane();
@@ -1537,6 +1543,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     const uint32_t my_sp = ld_ss(F.ss, ia).sp;
 
     uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform)
+    uint32_t drains = 0;
     // sweep once per distinct space in this wave (almost always one)
     auto run = [&](bool replay, uint2 *o, unsigned long long pe, unsigned long long pl, uint32_t &e,
                    uint32_t &l) {
@@ -1562,13 +1569,15 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.proto.chg = false;
             LaneA B = A;
             B.valid = mine;
-            combined_sweep(L, B, cand, F, O_rec, C, e, l, o, cap, pe, pl, replay);
+            combined_sweep(L, B, cand, F, O_rec, C, e, l, drains, o, cap, pe, pl, replay);
         }
     };
     run(false, nullptr, 0ull, 0ull, ne, nl);
     if (ln == 0) {
         L.wcnt[w][0] = ne;
         L.wcnt[w][1] = nl;
+        if (drains) atomicAdd(dbg + DBG_COMBINED_DRAIN, drains);
+        if (ne + nl > (uint32_t)EVW) atomicAdd(dbg + DBG_COMBINED_REPLAY, 1u);
     }
     // ---- offsets: 2 directed pairs per event; the block's enters, then its leaves
     __syncthreads();
@@ -1636,6 +1645,7 @@ __global__ __launch_bounds__(256) void k_reorder(const uint32_t *__restrict__ de
         res->err = sc->err;
         res->total64 = sc->counter;
         res->seq_max = sc->seq_max;
+        for (int q = 0; q < (int)DBG_N; ++q) res->dbg[q] = sc->dbg[q];
     }
     const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
     for (uint32_t e = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; e < n_entries; e += waves) {
@@ -1850,7 +1860,7 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
     if (!F.n) return;
     uint2 *tmp = reinterpret_cast<uint2 *>(tmp_pairs);
     k_pairs<1><<<combined_blocks(F.n), PT, 0, st>>>(F, O_rec, O_ss, seq_base, sc, &sc->counter, tmp, cap, tile_total,
-                                                    tile_base, tile_off, leave_off);
+                                                    tile_base, tile_off, leave_off, sc->dbg);
 }
 
 void launch_combined(FrameView F, const uint2 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
@@ -1861,7 +1871,7 @@ void launch_combined(FrameView F, const uint2 *cand, const Rec16 *O_rec, uint64_
     // end: no marker packets between kernels when the stage is timed
     hipExtLaunchKernelGGL(k_combined, dim3(combined_blocks(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
                           (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
-                          reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off);
+                          reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg);
 }
 
 void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,

@@ -445,6 +445,7 @@ int strip_err(gwaoi_strips *s, uint32_t e, const char *where) {
 extern "C" {
 
 int gwaoi_strips_destroy(gwaoi_strips *s) {
+    return gw::api_guard([&]() -> int {
     if (!s) return GWAOI_EINVAL;
     if (s->st) (void)hipStreamSynchronize(s->st);
     void *dev[] = {s->cur, s->prv, s->ptick, s->ttick, s->counts, s->scan_tmp, s->err, s->small_d, s->m_slot,
@@ -455,9 +456,11 @@ int gwaoi_strips_destroy(gwaoi_strips *s) {
     if (s->h_events) (void)hipHostFree(s->h_events);
     delete s;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_create(gwaoi_world *w, uint32_t space, const gwaoi_strips_config *cfg, gwaoi_strips **out) {
+    return gw::api_guard([&]() -> int {
     if (!w || !cfg || !out || cfg->n_strips == 0 || cfg->n_strips > GWAOI_MAX_STRIPS || cfg->rank >= cfg->n_strips ||
         (cfg->n_strips > 1 && !cfg->edges) || !(cfg->aoi_distance > 0.f) || !std::isfinite(cfg->aoi_distance))
         return GWAOI_EINVAL;
@@ -517,15 +520,19 @@ int gwaoi_strips_create(gwaoi_world *w, uint32_t space, const gwaoi_strips_confi
         return fail(GWAOI_EDEVICE);
     *out = s;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_halo(const gwaoi_strips *s, float *halo) {
+    return gw::api_guard([&]() -> int {
     if (!s || !halo) return GWAOI_EINVAL;
     *halo = s->geo.H;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint64_t *counts) {
+    return gw::api_guard([&]() -> int {
     if (!s || !counts || (n && !d_ops) || n > 0x7FFFFFFFu) return GWAOI_EINVAL;
     const uint32_t K = s->geo.S + 1;
     const uint32_t nb = std::max(1u, cdivu(n, BT));
@@ -541,9 +548,11 @@ int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, u
     s->r_nb = nb;
     s->routed = true;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_tele_rec *d_tele) {
+    return gw::api_guard([&]() -> int {
     if (!s || !s->routed) return GWAOI_EINVAL;
     s->routed = false;
     k_route<<<s->r_nb, BT, 0, s->st>>>(1, s->r_ops, s->r_n, s->cur, s->geo, s->counts, s->counts, s->r_nb, s->err,
@@ -551,11 +560,13 @@ int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_te
     S_TRY(hipGetLastError());
     S_TRY(hipStreamSynchronize(s->st));
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local, const gwaoi_halo_rec *d_recv,
                       size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele, uint64_t *n_enter,
                       uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
     if (!s || (n_local && !d_local) || (n_recv && !d_recv) || (n_tele && !d_tele) || n_tele > 0x7FFFFFFFu ||
         n_local + n_recv > 0x7FFFFFFFu)
         return GWAOI_EINVAL;
@@ -656,16 +667,20 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_l
     if (n_enter) *n_enter = s->n_enter;
     if (n_leave) *n_leave = s->n_leave;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const uint32_t **d_leave) {
+    return gw::api_guard([&]() -> int {
     if (!s) return GWAOI_EINVAL;
     if (d_enter) *d_enter = reinterpret_cast<const uint32_t *>(s->out);
     if (d_leave) *d_leave = reinterpret_cast<const uint32_t *>(s->out + s->n_enter);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_strips_events(gwaoi_strips *s, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
     if (!s || !out) return GWAOI_EINVAL;
     const uint64_t tot = s->n_enter + s->n_leave;
     if (tot > s->h_cap || !s->h_events) {
@@ -685,6 +700,7 @@ int gwaoi_strips_events(gwaoi_strips *s, gwaoi_events *out) {
     out->enter = s->h_events;
     out->leave = s->h_events + 2 * s->n_enter;
     return GWAOI_OK;
+    });
 }
 
 const char *gwaoi_strips_last_error(gwaoi_strips *s) { return s ? s->last_error.c_str() : "null strips"; }

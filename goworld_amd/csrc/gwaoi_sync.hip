@@ -81,29 +81,42 @@ __global__ void k_scatter128(const W128 *__restrict__ w, uint32_t n, ArrTable T)
     static_cast<uint4 *>(T.p[e.arr])[e.idx] = e.val;
 }
 
-// Host position/yaw writes (set_position_yaw, entity_set_position_yaw) and
-// flag-only ops (Space.enter): claim, then the winner writes.
+// Host position/yaw writes (set_position_yaw, entity_set_position_yaw,
+// entity_enter_plain) and flag-only ops (Space.enter): claim, then the winner
+// writes.  Position (x, y, z) and yaw have claims of their own: outside an AOI
+// space setPositionYaw changes yaw but not Position (Space.go:253-257), so the
+// last write of each may come from different calls.
+constexpr uint32_t SIDE_POS = 0x100u;  // op writes Position (x, y, z)
+constexpr uint32_t SIDE_YAW = 0x200u;  // op writes yaw
+constexpr uint32_t SIDE_SIF = GWAOI_SIF_OWN_CLIENT | GWAOI_SIF_NEIGHBOR_CLIENTS;
 struct SideOp {
-    uint32_t slot, bits;
+    uint32_t slot, bits;  // bits: SIDE_POS | SIDE_YAW | sync flags
     unsigned long long claim;
     float4 pos;  // x, y, z, yaw
 };
 
 __global__ void k_side_claim(const SideOp *__restrict__ ops, uint32_t n, unsigned long long *sclaim,
-                             uint32_t *sflags) {
+                             unsigned long long *yclaim, uint32_t *sflags) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const SideOp o = ops[i];
-    atomicMax(&sclaim[o.slot], o.claim);
-    if (o.bits) atomicOr(&sflags[o.slot], o.bits);
+    if (o.bits & SIDE_POS) atomicMax(&sclaim[o.slot], o.claim);
+    if (o.bits & SIDE_YAW) atomicMax(&yclaim[o.slot], o.claim);
+    if (o.bits & SIDE_SIF) atomicOr(&sflags[o.slot], o.bits & SIDE_SIF);
 }
 
 __global__ void k_side_write(const SideOp *__restrict__ ops, uint32_t n, const unsigned long long *sclaim,
-                             float4 *pos) {
+                             const unsigned long long *yclaim, float4 *pos) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const SideOp o = ops[i];
-    if (o.claim && sclaim[o.slot] == o.claim) pos[o.slot] = o.pos;  // claim 0: flags only
+    float *p = reinterpret_cast<float *>(pos + o.slot);
+    if ((o.bits & SIDE_POS) && sclaim[o.slot] == o.claim) {
+        p[0] = o.pos.x;
+        p[1] = o.pos.y;
+        p[2] = o.pos.z;
+    }
+    if ((o.bits & SIDE_YAW) && yclaim[o.slot] == o.claim) p[3] = o.pos.w;
 }
 
 // ------------------------------------------------------------- decode ------
@@ -114,12 +127,14 @@ struct DecodeArgs {
     const uint32_t *hval;
     uint32_t hmask;
     const uint32_t *qspace, *syncing;
-    uint32_t *o_slot, *o_sp;
+    uint32_t *o_slot, *o_sp;  // the device Moved batch (SLOT_NONE: no move)
     float *o_x, *o_z;
+    uint32_t *o_ys;  // slot of an applied record (SLOT_NONE: skipped), for k_decode_yaw
     unsigned long long claim0;
-    unsigned long long *sclaim;
+    unsigned long long *sclaim, *yclaim;
     uint32_t *sflags;
     float4 *pos;
+    uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
 };
 
 __device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ hkey, const uint32_t *__restrict__ hval,
@@ -134,8 +149,11 @@ __device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ hkey, const
 }
 
 // OnSyncPositionYawFromClient: unknown id -> skip (EntityManager.go:486-490);
-// syncPositionYawFromClient: only if syncing (Entity.go:432); setPositionYaw:
-// space nil -> skip (Entity.go:1190-1194).
+// syncPositionYawFromClient: only if syncing (Entity.go:432).  setPositionYaw
+// (Entity.go:1189-1205) then runs for every entity: e.Space is nilSpace, not
+// nil, outside every space.  In an AOI space it is a Moved (op i of the
+// batch) plus Position; elsewhere Space.move returns before Position
+// (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
 __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.n) return;
@@ -145,26 +163,38 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     uint32_t sp = SP_DEAD;
     if (s != SLOT_NONE) {
         sp = A.qspace[s];
-        if (!A.syncing[s] || sp == SP_DEAD) s = SLOT_NONE;
+        if (!A.syncing[s]) s = SLOT_NONE;
     }
-    A.o_slot[i] = s;
+    const bool move = s != SLOT_NONE && sp != SP_DEAD;
+    A.o_slot[i] = move ? s : SLOT_NONE;
     A.o_x[i] = __uint_as_float(pv.x);
     A.o_z[i] = __uint_as_float(pv.z);
     A.o_sp[i] = sp;
+    A.o_ys[i] = s;
     if (s != SLOT_NONE) {
-        atomicMax(&A.sclaim[s], A.claim0 + i);
-        atomicOr(&A.sflags[s], (uint32_t)GWAOI_SIF_NEIGHBOR_CLIENTS);
+        const unsigned long long c = A.claim0 + i;
+        atomicMax(&A.yclaim[s], c);
+        if (move) atomicMax(&A.sclaim[s], c);
+        const uint32_t old = atomicOr(&A.sflags[s], (uint32_t)GWAOI_SIF_NEIGHBOR_CLIENTS);
+        // first flag of a slot outside the frame since the last collect: list it once
+        if (!move && old == 0u) A.oflag[atomicAdd(A.oflag_n, 1u)] = s;
     }
 }
 
 __global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.n) return;
-    const uint32_t s = A.o_slot[i];
-    if (s == SLOT_NONE || A.sclaim[s] != A.claim0 + i) return;
+    const uint32_t s = A.o_ys[i];
+    if (s == SLOT_NONE) return;
+    const unsigned long long c = A.claim0 + i;
     const uint4 pv = A.pay[2 * (size_t)i + 1];
-    A.pos[s] = make_float4(__uint_as_float(pv.x), __uint_as_float(pv.y), __uint_as_float(pv.z),
-                           __uint_as_float(pv.w));
+    float *p = reinterpret_cast<float *>(A.pos + s);
+    if (A.o_sp[i] != SP_DEAD && A.sclaim[s] == c) {
+        p[0] = __uint_as_float(pv.x);
+        p[1] = __uint_as_float(pv.y);
+        p[2] = __uint_as_float(pv.z);
+    }
+    if (A.yclaim[s] == c) p[3] = __uint_as_float(pv.w);
 }
 
 // ------------------------------------------------------------ fan-out ------
@@ -179,7 +209,8 @@ __global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
 // frame records, and clears the flags.
 struct FanArgs {
     FrameView F;
-    const uint32_t *left;  // slots that left since the last collect (own-client records only)
+    const SlotInfo *info;  // slot -> frame index (rank) of the world
+    const uint32_t *left;  // flagged slots outside the frame (own-client records only), may repeat
     uint32_t n_left;
     const uint4 *eid, *cid;
     const uint32_t *cgate;
@@ -202,13 +233,20 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     if (i >= nf + A.n_left) return;
     const bool in_frame = i < nf;
     const uint32_t s = in_frame ? ld_ss(A.F.ss, i).slot : A.left[i - nf];
-    const uint32_t fl = A.sflags[s];
+    uint32_t fl;
+    if (in_frame) {
+        fl = A.sflags[s];
+        if (fl) A.sflags[s] = 0u;
+    } else {
+        // a listed slot back in the frame is its frame entry's; a slot listed twice is sent once
+        const uint32_t r = A.info[s].rank;
+        fl = (r < nf && ld_ss(A.F.ss, r).slot == s) ? 0u : atomicExch(&A.sflags[s], 0u);
+    }
     A.snd[i] = fl;
     A.rg[i] = A.cgate[s];
     A.rslot[i] = s;
     if (fl) {
-        A.sflags[s] = 0u;
-        // the frame holds the AOI position; an entity that left uses its last sync position
+        // the frame holds the AOI position; outside the frame, the last Position written
         const float4 P = A.pos[s];
         float x = P.x, z = P.z;
         if (in_frame) {
@@ -420,7 +458,9 @@ struct SyncState {
     uint4 *eid = nullptr, *cid = nullptr;
     uint32_t *cgate = nullptr, *qspace = nullptr, *syncing = nullptr, *sflags = nullptr;
     float4 *pos = nullptr;
-    unsigned long long *sclaim = nullptr;
+    unsigned long long *sclaim = nullptr, *yclaim = nullptr;  // Position / yaw last-writer claims
+    uint32_t *oflag = nullptr, *oflag_n = nullptr;  // decode: slots flagged outside every AOI space
+    bool decoded = false;                           // a decode ran since the last collect
     // id -> slot hash table (device, host mirror)
     uint4 *hkey = nullptr;
     uint32_t *hval = nullptr;
@@ -430,6 +470,7 @@ struct SyncState {
     // host mirrors
     std::vector<uint4> h_eid;
     std::vector<uint8_t> h_bound, h_client;
+    std::vector<uint8_t> h_plain;  // in a space without AOI (gwaoi_entity_enter_plain)
     std::vector<uint32_t> h_bucket;  // slot -> its hash bucket (if bound)
     std::unordered_map<uint32_t, uint32_t> gate_idx;  // gate id -> dense index
     std::vector<uint16_t> gate_ids;
@@ -437,7 +478,7 @@ struct SyncState {
     std::vector<W32> w32;
     std::vector<W128> w128;
     std::vector<SideOp> side;
-    std::vector<uint32_t> left;  // slots that left since the last collect
+    std::vector<uint32_t> left;  // slots flagged outside the frame since the last collect (host ops)
     unsigned long long claim_next = 1;
     // staging (pinned host + device), reused once the previous upload has landed
     void *h_stage = nullptr, *d_stage = nullptr;
@@ -579,8 +620,8 @@ int push(SyncState *S) {
     if (!S->side.empty()) {
         const SideOp *o = reinterpret_cast<const SideOp *>(d + b128 + b32);
         const uint32_t n = (uint32_t)S->side.size();
-        k_side_claim<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->sflags);
-        k_side_write<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->pos);
+        k_side_claim<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->yclaim, S->sflags);
+        k_side_write<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->yclaim, S->pos);
     }
     SY_TRY(hipGetLastError());
     S->w32.clear();
@@ -603,7 +644,8 @@ int create(gwaoi_world *w, SyncState **out) {
     int rc;
     if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->cgate, N)) ||
         (rc = salloc(S, &S->qspace, N)) || (rc = salloc(S, &S->syncing, N)) || (rc = salloc(S, &S->sflags, N)) ||
-        (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->sclaim, N)) || (rc = salloc(S, &S->hkey, cap)) ||
+        (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->sclaim, N)) || (rc = salloc(S, &S->yclaim, N)) ||
+        (rc = salloc(S, &S->oflag, N)) || (rc = salloc(S, &S->oflag_n, 1)) || (rc = salloc(S, &S->hkey, cap)) ||
         (rc = salloc(S, &S->hval, cap))) {
         sync_destroy(S);
         return rc;
@@ -613,6 +655,8 @@ int create(gwaoi_world *w, SyncState **out) {
               hipMemsetAsync(S->sflags, 0, N * 4, S->st) == hipSuccess &&
               hipMemsetAsync(S->pos, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->sclaim, 0, N * 8, S->st) == hipSuccess &&
+              hipMemsetAsync(S->yclaim, 0, N * 8, S->st) == hipSuccess &&
+              hipMemsetAsync(S->oflag_n, 0, 4, S->st) == hipSuccess &&
               hipMemsetAsync(S->eid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->cid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->hval, 0xFF, (size_t)cap * 4, S->st) == hipSuccess &&
@@ -634,6 +678,7 @@ int create(gwaoi_world *w, SyncState **out) {
     S->h_eid.assign(N, make_uint4(0, 0, 0, 0));
     S->h_bound.assign(N, 0);
     S->h_client.assign(N, 0);
+    S->h_plain.assign(N, 0);
     S->h_bucket.assign(N, H_EMPTY);
     *out = S;
     return GWAOI_OK;
@@ -788,24 +833,39 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     const WorldView v = world_view(w);
     if (v.pending_ops) return GWAOI_ESTATE;
     if (int rc = push(S)) return rc;
-    // own-client records of flagged entities that left (deduplicated, still out of every space)
+    // flagged slots outside the frame get their own-client record only (InterestedBy is empty
+    // outside an AOI space): the host ops' list, then the slots k_decode listed
     std::vector<uint32_t> left;
     std::sort(S->left.begin(), S->left.end());
     S->left.erase(std::unique(S->left.begin(), S->left.end()), S->left.end());
     for (uint32_t s : S->left)
         if (world_slot_space(w, s) == SP_DEAD) left.push_back(s);
     S->left.clear();
-    if (!left.empty()) {
-        if (int rc = ensure_u32(S, &S->d_left, &S->left_cap, left.size())) return rc;
-        SY_TRY(hipMemcpyAsync(S->d_left, left.data(), left.size() * 4, hipMemcpyHostToDevice, S->st));
+    uint32_t n_dec = 0;
+    if (S->decoded) {
+        SY_TRY(hipMemcpyAsync(&n_dec, S->oflag_n, 4, hipMemcpyDeviceToHost, S->st));
+        SY_TRY(hipStreamSynchronize(S->st));
+        S->decoded = false;
+    }
+    const size_t n_left = left.size() + n_dec;
+    if (n_left) {
+        if (int rc = ensure_u32(S, &S->d_left, &S->left_cap, n_left)) return rc;
+        if (!left.empty())
+            SY_TRY(hipMemcpyAsync(S->d_left, left.data(), left.size() * 4, hipMemcpyHostToDevice, S->st));
+        if (n_dec) {
+            SY_TRY(hipMemcpyAsync(S->d_left + left.size(), S->oflag, (size_t)n_dec * 4, hipMemcpyDeviceToDevice,
+                                  S->st));
+            SY_TRY(hipMemsetAsync(S->oflag_n, 0, 4, S->st));
+        }
     }
     const uint32_t G = (uint32_t)S->gate_ids.size();
-    const uint32_t n_ent = v.F.n + (uint32_t)left.size();
+    const uint32_t n_ent = v.F.n + (uint32_t)n_left;
     const uint32_t nb = std::max(1u, cdivu(n_ent, ST));
     FanArgs A{};
     A.F = v.F;
+    A.info = v.info;
     A.left = S->d_left;
-    A.n_left = (uint32_t)left.size();
+    A.n_left = (uint32_t)n_left;
     A.eid = S->eid;
     A.cid = S->cid;
     A.cgate = S->cgate;
@@ -883,7 +943,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
         S->arena_tick = ticks_now;
     }
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t need = 4 * al(n * 4) + (on_device ? 0 : al(n * 32));
+    const size_t need = 5 * al(n * 4) + (on_device ? 0 : al(n * 32));
     SyncState::Chunk *ch = nullptr;
     for (auto &c : S->arena)
         if (c.cap - c.used >= need) {
@@ -902,11 +962,12 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     float *o_x = reinterpret_cast<float *>(base + al(n * 4));
     float *o_z = reinterpret_cast<float *>(base + 2 * al(n * 4));
     uint32_t *o_sp = reinterpret_cast<uint32_t *>(base + 3 * al(n * 4));
+    uint32_t *o_ys = reinterpret_cast<uint32_t *>(base + 4 * al(n * 4));
     const uint4 *pay;
     if (on_device) {
         pay = reinterpret_cast<const uint4 *>(payload);
     } else {
-        char *dp = base + 4 * al(n * 4);
+        char *dp = base + 5 * al(n * 4);
         SY_TRY(hipMemcpyAsync(dp, payload, n * 32, hipMemcpyHostToDevice, S->st));
         pay = reinterpret_cast<const uint4 *>(dp);
     }
@@ -923,11 +984,16 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.o_sp = o_sp;
     A.o_x = o_x;
     A.o_z = o_z;
+    A.o_ys = o_ys;
     A.claim0 = S->claim_next;
     A.sclaim = S->sclaim;
+    A.yclaim = S->yclaim;
     A.sflags = S->sflags;
     A.pos = S->pos;
+    A.oflag = S->oflag;
+    A.oflag_n = S->oflag_n;
     S->claim_next += n;
+    S->decoded = true;
     k_decode<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_yaw<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     SY_TRY(hipGetLastError());
@@ -941,15 +1007,17 @@ void sync_note_slot(SyncState *S, uint32_t slot, uint32_t space_or_dead) {
     if (space_or_dead == SP_DEAD)
         S->left.push_back(slot);
     else  // Space.enter: syncInfoFlag |= sifSyncOwnClient | sifSyncNeighborClients (Space.go:205)
-        S->side.push_back(SideOp{slot, GWAOI_SIF_OWN_CLIENT | GWAOI_SIF_NEIGHBOR_CLIENTS, 0ull,
-                                 make_float4(0.f, 0.f, 0.f, 0.f)});
+        S->side.push_back(SideOp{slot, SIDE_SIF, 0ull, make_float4(0.f, 0.f, 0.f, 0.f)});
 }
+
+bool sync_slot_plain(const SyncState *S, uint32_t slot) { return slot < S->max_slots && S->h_plain[slot]; }
 
 void sync_destroy(SyncState *S) {
     if (!S) return;
     if (S->st) (void)hipStreamSynchronize(S->st);
     sfree(S->eid); sfree(S->cid); sfree(S->cgate); sfree(S->qspace); sfree(S->syncing); sfree(S->sflags);
-    sfree(S->pos); sfree(S->sclaim); sfree(S->hkey); sfree(S->hval);
+    sfree(S->pos); sfree(S->sclaim); sfree(S->yclaim); sfree(S->oflag); sfree(S->oflag_n);
+    sfree(S->hkey); sfree(S->hval);
     sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec1); sfree(S->f_rec2);
     sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
     sfree(S->d_stage);
@@ -970,22 +1038,27 @@ using gw::SyncState;
 extern "C" {
 
 int gwaoi_entity_bind(gwaoi_world *w, uint32_t slot, const uint8_t eid[GWAOI_ID_LEN]) {
+    return gw::api_guard([&]() -> int {
     if (!w || !eid) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
     return gw::bind_one(S, slot, gw::load_id(eid));
+    });
 }
 
 int gwaoi_entity_bind_batch(gwaoi_world *w, const uint32_t *slots, const uint8_t *eids, size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && (!slots || !eids))) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
     for (size_t i = 0; i < n; ++i)
         if (int rc = gw::bind_one(S, slots[i], gw::load_id(eids + 16 * i))) return rc;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_entity_unbind(gwaoi_world *w, uint32_t slot) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
@@ -1002,9 +1075,11 @@ int gwaoi_entity_unbind(gwaoi_world *w, uint32_t slot) {
     }
     gw::put32(S, gw::A_SYNCING, slot, 0);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_entity_set_client(gwaoi_world *w, uint32_t slot, uint16_t gate_id, const uint8_t *clientid) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
@@ -1028,52 +1103,100 @@ int gwaoi_entity_set_client(gwaoi_world *w, uint32_t slot, uint16_t gate_id, con
     gw::put128(S, gw::B_CID, slot, gw::load_id(clientid));
     gw::put32(S, gw::A_CGATE, slot, g);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_entity_set_syncing(gwaoi_world *w, uint32_t slot, int syncing) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
     if (slot >= S->max_slots) return GWAOI_EBADSLOT;
     gw::put32(S, gw::A_SYNCING, slot, syncing ? 1u : 0u);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_entity_set_position_yaw(gwaoi_world *w, uint32_t slot, float x, float y, float z, float yaw) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
     if (slot >= S->max_slots) return GWAOI_EBADSLOT;
-    S->side.push_back(gw::SideOp{slot, 0u, S->claim_next++, make_float4(x, y, z, yaw)});
+    S->side.push_back(gw::SideOp{slot, gw::SIDE_POS | gw::SIDE_YAW, S->claim_next++, make_float4(x, y, z, yaw)});
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_set_position_yaw(gwaoi_world *w, uint32_t slot, float x, float y, float z, float yaw) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = gw::state(w, &S)) return rc;
     if (slot >= S->max_slots) return GWAOI_EBADSLOT;
-    if (int rc = gwaoi_moved(w, slot, x, z)) return rc;  // ESTATE: not in a space
-    S->side.push_back(gw::SideOp{slot, GWAOI_SIF_OWN_CLIENT | GWAOI_SIF_NEIGHBOR_CLIENTS, S->claim_next++,
-                                 make_float4(x, y, z, yaw)});
+    if (gw::world_slot_space(w, slot) != gw::SP_DEAD) {  // Space.move of an AOI space: Position + Moved
+        if (int rc = gwaoi_moved(w, slot, x, z)) return rc;
+        S->side.push_back(gw::SideOp{slot, gw::SIDE_POS | gw::SIDE_YAW | gw::SIDE_SIF, S->claim_next++,
+                                     make_float4(x, y, z, yaw)});
+        return GWAOI_OK;
+    }
+    // nilSpace or a space without AOI: Space.move returns before Position (Space.go:253-257); yaw
+    // and both flags are still set (Entity.go:1196-1204)
+    S->side.push_back(gw::SideOp{slot, gw::SIDE_YAW | gw::SIDE_SIF, S->claim_next++, make_float4(x, y, z, yaw)});
+    S->left.push_back(slot);
     return GWAOI_OK;
+    });
+}
+
+int gwaoi_entity_enter_plain(gwaoi_world *w, uint32_t slot, float x, float y, float z) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    // Space.enter panics unless the entity is in nilSpace (Space.go:193-195)
+    if (S->h_plain[slot] || gw::world_slot_space(w, slot) != gw::SP_DEAD) return GWAOI_ESTATE;
+    S->h_plain[slot] = 1;
+    S->side.push_back(gw::SideOp{slot, gw::SIDE_POS | gw::SIDE_SIF, S->claim_next++, make_float4(x, y, z, 0.f)});
+    S->left.push_back(slot);
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_entity_leave_plain(gwaoi_world *w, uint32_t slot) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    SyncState *S;
+    if (int rc = gw::state(w, &S)) return rc;
+    if (slot >= S->max_slots) return GWAOI_EBADSLOT;
+    if (!S->h_plain[slot]) return GWAOI_ESTATE;  // Space.leave panics for another space (Space.go:229-231)
+    S->h_plain[slot] = 0;
+    return GWAOI_OK;
+    });
 }
 
 int gwaoi_sync_from_clients(gwaoi_world *w, const uint8_t *payload, size_t n_rec) {
+    return gw::api_guard([&]() -> int {
     return gw::decode(w, payload, n_rec, false);
+    });
 }
 
 int gwaoi_sync_from_clients_device(gwaoi_world *w, const uint8_t *d_payload, size_t n_rec) {
+    return gw::api_guard([&]() -> int {
     return gw::decode(w, d_payload, n_rec, true);
+    });
 }
 
-int gwaoi_collect_sync_infos(gwaoi_world *w, gwaoi_gate_records *out) { return gw::collect_sync(w, out, true); }
+int gwaoi_collect_sync_infos(gwaoi_world *w, gwaoi_gate_records *out) { return gw::api_guard([&]() -> int { return gw::collect_sync(w, out, true); }); }
 
 int gwaoi_collect_sync_infos_device(gwaoi_world *w, gwaoi_gate_records *out) {
+    return gw::api_guard([&]() -> int {
     return gw::collect_sync(w, out, false);
+    });
 }
 
 int gwaoi_collect_client_events(gwaoi_world *w, gwaoi_gate_records *creates, gwaoi_gate_records *destroys) {
+    return gw::api_guard([&]() -> int {
     using namespace gw;
     if (!w || !creates || !destroys) return GWAOI_EINVAL;
     SyncState *S;
@@ -1130,6 +1253,7 @@ int gwaoi_collect_client_events(gwaoi_world *w, gwaoi_gate_records *creates, gwa
     fill_out(S, creates, S->h_off_c, S->h_rec);
     fill_out(S, destroys, S->h_off_d, S->h_rec_d);
     return GWAOI_OK;
+    });
 }
 
 }  // extern "C"

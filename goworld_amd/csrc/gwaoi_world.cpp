@@ -97,6 +97,7 @@ struct gwaoi_world {
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
     size_t cnt64_cap = 0;
     bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
+    bool inject_regrow_fail = false;  // GWAOI_INJECT_REGROW_FAIL=1 (tests): the event regrow fails
     // End-of-flush wait: poll an event (default) or block in hipStreamSynchronize
     // (GWAOI_BLOCKING_SYNC=1, A/B check).
     hipEvent_t done_ev = nullptr;
@@ -150,6 +151,7 @@ struct gwaoi_world {
     uint64_t ticks = 0;
     uint32_t n_alive = 0;
     uint64_t last_n_enter = 0, last_n_leave = 0;
+    gwaoi_debug dbg{};  // rare-path counters, accumulated over flushes
 
     // stage timing: bit s of timing_mask = time stage s with HIP events
     uint32_t timing_mask = 0;
@@ -159,10 +161,23 @@ struct gwaoi_world {
     uint64_t stage_calls[ST_N] = {};
 
     std::string last_error;
+    // A flush that failed after its kernels rewrote the per-slot records (SlotInfo) for a frame it
+    // could not commit leaves host and device state apart: every later call returns GWAOI_EDEVICE.
+    bool poisoned = false;
+    std::string poison_msg;
     gw::SyncState *sync = nullptr;  // entity position-sync layer (gwaoi_sync.h), created on first use
 };
 
 namespace {
+
+// A poisoned world refuses every call (see gwaoi_world::poisoned).
+#define GW_LIVE(w)                                 \
+    do {                                           \
+        if ((w)->poisoned) {                       \
+            (w)->last_error = (w)->poison_msg;     \
+            return GWAOI_EDEVICE;                  \
+        }                                          \
+    } while (0)
 
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
@@ -505,8 +520,20 @@ void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_
     stage_end(w, ST_REORDER);
 }
 
+int poison(gwaoi_world *w, int rc) {
+    w->poisoned = true;
+    w->poison_msg = "world unusable after a failed flush: " + w->last_error;
+    w->last_error = w->poison_msg;
+    return rc;
+}
+
 // The flush.  On return the events of this tick are in w->events (device).
-int run_tick(gwaoi_world *w) {
+// *committed: the new frame became the world's state (the events are valid
+// and must be delivered, even when the returned status reports a problem the
+// device found in the queued ops).  A failure after the device kernels have
+// rewritten the per-slot records but before the commit poisons the world.
+int run_tick(gwaoi_world *w, bool *committed) {
+    *committed = false;
     hipStream_t st = w->stream;
     int rc;
     const uint32_t tick_id = ++w->tick_id;
@@ -663,30 +690,51 @@ int run_tick(gwaoi_world *w) {
     stage_begin(w, ST_BBOX);
     gw::launch_bbox(n_new, dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
     stage_end(w, ST_BBOX);
-    HIP_TRY(hipGetLastError());
+    // from here on the device has rewritten SlotInfo for the new frame: any failure before the
+    // commit below leaves the world inconsistent (poisoned)
+    if (hipGetLastError() != hipSuccess) {
+        w->last_error = "kernel launch failed";
+        return poison(w, GWAOI_EDEVICE);
+    }
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
-    HIP_TRY(hipMemcpyAsync(w->h_out, w->dev_out, out_bytes, hipMemcpyDeviceToHost, st));
-    if ((rc = wait_stream(w))) return rc;
+    if (hipMemcpyAsync(w->h_out, w->dev_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        wait_stream(w) != GWAOI_OK) {
+        w->last_error = "flush did not complete: " + w->last_error;
+        return poison(w, GWAOI_EDEVICE);
+    }
 
     gw::TickOut r = *tick_out(w);
     if (r.total64 > 0xFFFFFFFFull) {
         w->last_error = "more than 2^32-1 events in one flush";
-        return GWAOI_ECAPACITY;
+        return poison(w, GWAOI_ECAPACITY);
     }
     if (r.total64 > w->ev_cap) {  // grow and re-run the pair passes
         stage_collect(w);
-        if ((rc = ensure_events(w, r.total64))) return rc;
+        if (w->inject_regrow_fail) {
+            w->last_error = "event buffer regrow failed (injected)";
+            return poison(w, GWAOI_ENOMEM);
+        }
+        if ((rc = ensure_events(w, r.total64))) return poison(w, rc);
         gw::launch_zero(w->tile_total, entries + 1, st);
         gw::launch_zero(reinterpret_cast<uint32_t *>(&w->sc->counter), 2, st);
+        gw::launch_zero(w->sc->dbg, gw::DBG_N, st);
         launch_pair_passes(w, Fn, P, seq_base);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(w->h_out, w->dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st));
-        if ((rc = wait_stream(w))) return rc;
+        w->dbg.event_regrows++;
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(w->h_out, w->dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            wait_stream(w) != GWAOI_OK) {
+            w->last_error = "pair passes re-run failed: " + w->last_error;
+            return poison(w, GWAOI_EDEVICE);
+        }
         r = *tick_out(w);
     }
     stage_collect(w);
 
     // ---- commit host bookkeeping
+    w->dbg.flushes++;
+    w->dbg.combined_replays += r.dbg[gw::DBG_COMBINED_REPLAY];
+    w->dbg.combined_queue_drains += r.dbg[gw::DBG_COMBINED_DRAIN];
+    w->dbg.special_global += r.dbg[gw::DBG_SPECIAL_GLOBAL];
     w->last_n_enter = r.n_enter;
     w->last_n_leave = (uint64_t)r.n_total - r.n_enter;
     const int4 *bb = tick_bbox(w);
@@ -720,9 +768,12 @@ int run_tick(gwaoi_world *w) {
     w->seq_floor = w->seq_next;
     w->cur ^= 1;
     w->ticks++;
+    *committed = true;
+    // problems the device found in the queued ops: the frame is committed (the offending ops were
+    // dropped), so the flush's events are valid and the caller still receives them
     if (r.err & gw::ERR_COUNT_MISMATCH) {
         w->last_error = "internal: live-count mismatch between host and device";
-        return GWAOI_EDEVICE;
+        return poison(w, GWAOI_EDEVICE);
     }
     if (r.err & gw::ERR_NONFINITE) {
         w->last_error = "device batch held a non-finite coordinate (move dropped)";
@@ -766,6 +817,7 @@ const char *gwaoi_strerror(int s) {
 const char *gwaoi_last_error(gwaoi_world *w) { return w ? w->last_error.c_str() : "null world"; }
 
 int gwaoi_world_destroy(gwaoi_world *w) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     if (w->sync) gw::sync_destroy(w->sync);
@@ -793,9 +845,11 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
+    return gw::api_guard([&]() -> int {
     if (!cfg || !out || cfg->max_slots == 0 || cfg->max_spaces == 0 || cfg->max_slots > 0x7FFFFFF0u)
         return GWAOI_EINVAL;
     *out = nullptr;
@@ -807,6 +861,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 4.0f;
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
+    if (const char *e = std::getenv("GWAOI_INJECT_REGROW_FAIL")) w->inject_regrow_fail = e[0] == '1';
     int rc = GWAOI_OK;
     auto fail = [&](int code) {
         gwaoi_world_destroy(w);
@@ -868,9 +923,11 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->spaces.resize(w->max_spaces);
     *out = w;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_space_create(gwaoi_world *w, float d, uint32_t *space_out) {
+    return gw::api_guard([&]() -> int {
     if (!w || !space_out) return GWAOI_EINVAL;
     if (!(d > 0.f) || !std::isfinite(d)) return GWAOI_EINVAL;  // "defaultAOIDistance < 0" panic, Space.go:92-94
     for (uint32_t s = 0; s < w->max_spaces; ++s) {
@@ -887,15 +944,18 @@ int gwaoi_space_create(gwaoi_world *w, float d, uint32_t *space_out) {
         return GWAOI_OK;
     }
     return GWAOI_EBADSPACE;
+    });
 }
 
 int gwaoi_space_destroy(gwaoi_world *w, uint32_t space) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
     if (w->spaces[space].alive) return GWAOI_EBUSY;
     w->spaces[space].used = false;
     w->n_spaces_live--;
     return GWAOI_OK;
+    });
 }
 
 namespace {
@@ -916,9 +976,11 @@ uint64_t take_seq(gwaoi_world *w, const uint64_t *seq) {
 
 int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, const uint64_t *seq) {
     if (!w) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
     if (w->alive[slot]) return GWAOI_ESTATE;
+    if (w->sync && gw::sync_slot_plain(w->sync, slot)) return GWAOI_ESTATE;  // in a space without AOI
     if (!finite2(x, z)) return GWAOI_ENONFINITE;
     if (int rc = check_seq(w, seq)) return rc;
     w->alive[slot] = 1;
@@ -936,6 +998,7 @@ int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, 
 
 int moved_impl(gwaoi_world *w, uint32_t slot, float x, float z, const uint64_t *seq) {
     if (!w) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (!w->alive[slot]) return GWAOI_ESTATE;
     if (!finite2(x, z)) return GWAOI_ENONFINITE;
@@ -1064,15 +1127,21 @@ int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const flo
 }  // namespace
 
 int gwaoi_enter(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z) {
+    return gw::api_guard([&]() -> int {
     return enter_impl(w, space, slot, x, z, nullptr);
+    });
 }
 
 int gwaoi_enter_seq(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, uint64_t seq) {
+    return gw::api_guard([&]() -> int {
     return enter_impl(w, space, slot, x, z, &seq);
+    });
 }
 
 int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (!w->alive[slot]) return GWAOI_ESTATE;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
@@ -1084,17 +1153,22 @@ int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
     w->touched.push_back(slot);
     push_host_op(w, slot, 0.f, 0.f, gw::SP_DEAD, w->seq_next);  // a Leave's seq is never compared
     return GWAOI_OK;
+    });
 }
 
-int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z) { return moved_impl(w, slot, x, z, nullptr); }
+int gwaoi_moved(gwaoi_world *w, uint32_t slot, float x, float z) { return gw::api_guard([&]() -> int { return moved_impl(w, slot, x, z, nullptr); }); }
 
 int gwaoi_moved_seq(gwaoi_world *w, uint32_t slot, float x, float z, uint64_t seq) {
+    return gw::api_guard([&]() -> int {
     return moved_impl(w, slot, x, z, &seq);
+    });
 }
 
 int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, const float *x, const float *z,
                       size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
     // validate the whole batch first (duplicates inside the batch are Enter-twice)
@@ -1110,10 +1184,13 @@ int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, con
     if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return GWAOI_ESTATE;
     for (size_t i = 0; i < n; ++i) gwaoi_enter(w, space, slots[i], x[i], z[i]);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && !slots)) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (w->dev_seq_pending) return GWAOI_ESTATE;
     std::vector<uint32_t> seen(slots, slots + n);
     for (size_t i = 0; i < n; ++i) {
@@ -1124,10 +1201,13 @@ int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
     if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return GWAOI_ESTATE;
     for (size_t i = 0; i < n; ++i) gwaoi_leave(w, slots[i]);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (w->dev_seq_pending) return GWAOI_ESTATE;
     // Batches of kStageMinBatch+ moves go through pinned staging as one device batch (single-pass
     // move apply); without room (or if the staging allocation failed) they queue as host ops.
@@ -1140,11 +1220,14 @@ int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, con
     }
     for (size_t i = 0; i < n; ++i) gwaoi_moved(w, slots[i], x[i], z[i]);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
                              size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && (!d_slots || !d_x || !d_z))) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (!n) return GWAOI_OK;
     if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
@@ -1160,11 +1243,14 @@ int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const floa
     w->n_ops += n;
     w->seq_next += n;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
                                  const uint64_t *d_seq, size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && (!d_slots || !d_x || !d_z || !d_seq))) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (!n) return GWAOI_OK;
     if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
     Run r{};
@@ -1179,6 +1265,7 @@ int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const 
     w->n_ops += n;
     w->dev_seq_pending = true;
     return GWAOI_OK;
+    });
 }
 
 }  // extern "C"
@@ -1208,6 +1295,7 @@ uint32_t world_slot_space(gwaoi_world *w, uint32_t slot) {
 
 int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
                         const uint32_t *d_sp, size_t n) {
+    GW_LIVE(w);
     if (!n) return GWAOI_OK;
     if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
@@ -1230,27 +1318,41 @@ int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_
 extern "C" {
 
 int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
-    int rc = run_tick(w);
-    if (n_enter) *n_enter = w->last_n_enter;
-    if (n_leave) *n_leave = w->last_n_leave;
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    GW_LIVE(w);
+    bool committed;
+    int rc = run_tick(w, &committed);
+    if (committed) {
+        if (n_enter) *n_enter = w->last_n_enter;
+        if (n_leave) *n_leave = w->last_n_leave;
+    }
     return rc;
+    });
 }
 
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     if (d_enter) *d_enter = w->events;
     if (d_leave) *d_leave = w->events + 2 * w->last_n_enter;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
     if (!w || !out) return GWAOI_EINVAL;
-    int rc = run_tick(w);
-    const uint64_t tot = w->last_n_enter + w->last_n_leave;
     out->n_enter = out->n_leave = 0;
     out->enter = out->leave = nullptr;
-    if (rc != GWAOI_OK && rc != GWAOI_ESTATE && rc != GWAOI_ENONFINITE) return rc;
+    GW_LIVE(w);
+    bool committed;
+    int rc = run_tick(w, &committed);
+    if (!committed) return rc;
+    // committed: deliver the events whatever the status (InterestedIn/By must follow the frame)
+    const uint64_t tot = w->last_n_enter + w->last_n_leave;
     int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1));
     if (rc2) return rc2;
     stage_begin(w, ST_D2H);
@@ -1259,9 +1361,9 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
                                       w->stream);
         if (e != hipSuccess) {
             w->last_error = std::string("event D2H: ") + hipGetErrorString(e);
-            return GWAOI_EDEVICE;
+            return poison(w, GWAOI_EDEVICE);  // the committed events cannot reach the caller
         }
-        if (int rw = wait_stream(w)) return rw;
+        if (int rw = wait_stream(w)) return poison(w, rw);
     }
     stage_end(w, ST_D2H);
     if (w->timing_mask) {
@@ -1273,10 +1375,13 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
     out->enter = w->h_events;
     out->leave = w->h_events + 2 * w->last_n_enter;
     return rc;
+    });
 }
 
 int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, size_t *n_out) {
+    return gw::api_guard([&]() -> int {
     if (!w || (cap && !out)) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (n_out) *n_out = 0;
     if (!w->in_frame[slot]) return GWAOI_ESTATE;
@@ -1302,11 +1407,14 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
     }
     if (n_out) *n_out = cnt;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, float *z, uint64_t *seq,
                    size_t cap, size_t *n_out) {
+    return gw::api_guard([&]() -> int {
     if (!w || !n_out) return GWAOI_EINVAL;
+    GW_LIVE(w);
     const DevFrame &F = w->fr[w->cur];
     *n_out = F.n;
     if (F.n > cap || !F.n) return GWAOI_OK;
@@ -1324,11 +1432,14 @@ int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, 
         seq[i] = rec[i].s;
     }
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces, const float *x, const float *z,
                   const uint64_t *seq, size_t n) {
+    return gw::api_guard([&]() -> int {
     if (!w || (n && (!slots || !spaces || !x || !z || !seq))) return GWAOI_EINVAL;
+    GW_LIVE(w);
     if (w->n_ops || w->dev_seq_pending) return GWAOI_ESTATE;
     std::vector<size_t> ord(n);
     for (size_t i = 0; i < n; ++i) ord[i] = i;
@@ -1345,15 +1456,22 @@ int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces,
         if (!finite2(x[i], z[i])) return GWAOI_ENONFINITE;
         if (k && seq[i] == seq[ord[k - 1]]) return GWAOI_EINVAL;
     }
-    // fresh seqs in the frozen order: the relation only compares seqs
+    // The original seqs when they all lie at or above the world's next seq (a fresh world, or one
+    // whose counter is below the snapshot's): then gwaoi_snapshot after the restore returns them
+    // unchanged, which strip worlds (halo records carry global seqs) rely on.  Otherwise fresh seqs
+    // in the frozen order: the relation inside the world only compares seqs, so it is the frozen
+    // one either way.
+    const bool keep = n == 0 || seq[ord[0]] >= w->seq_next;
     for (size_t k = 0; k < n; ++k) {
         const size_t i = ord[k];
-        if (int rc = enter_impl(w, spaces[i], slots[i], x[i], z[i], nullptr)) return rc;
+        if (int rc = enter_impl(w, spaces[i], slots[i], x[i], z[i], keep ? &seq[i] : nullptr)) return rc;
     }
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
+    return gw::api_guard([&]() -> int {
     if (!w || !info) return GWAOI_EINVAL;
     info->ticks = w->ticks;
     info->next_seq = w->seq_next;
@@ -1365,9 +1483,19 @@ int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
     info->max_slots = w->max_slots;
     info->max_spaces = w->max_spaces;
     return GWAOI_OK;
+    });
+}
+
+int gwaoi_debug_counters(gwaoi_world *w, gwaoi_debug *out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out) return GWAOI_EINVAL;
+    *out = w->dbg;
+    return GWAOI_OK;
+    });
 }
 
 int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t *n_out) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     size_t k = std::min<size_t>(cap, ST_N);
     for (size_t i = 0; i < k; ++i) {
@@ -1377,27 +1505,34 @@ int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t 
     }
     if (n_out) *n_out = ST_N;
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_set_stage_timing(gwaoi_world *w, uint32_t stage_mask) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     w->timing_mask = stage_mask & ((1u << ST_N) - 1u);
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_reset_stage_times(gwaoi_world *w) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     for (int s = 0; s < ST_N; ++s) {
         w->stage_ms[s] = 0;
         w->stage_calls[s] = 0;
     }
     return GWAOI_OK;
+    });
 }
 
 int gwaoi_sync(gwaoi_world *w) {
+    return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     HIP_TRY(hipStreamSynchronize(w->stream));
     return GWAOI_OK;
+    });
 }
 
 void *gwaoi_stream(gwaoi_world *w) { return w ? (void *)w->stream : nullptr; }

@@ -140,6 +140,9 @@ class StripShard:
         tele (k,10) int32)."""
         torch = self.torch
         n = int(ops.shape[0])
+        # the world's stream does not wait for torch's: `ops` (and the caching allocator's reuse of
+        # the blocks written below) must be complete before the route kernels read them
+        torch.cuda.current_stream(self.dev).synchronize()
         counts = (C.c_uint64 * (self.n_strips + 1))()
         self._check(self._L.gwaoi_strips_route(self._s, C.c_void_p(ops.data_ptr() if n else 0), n, counts))
         c = np.array(counts[:], np.int64)

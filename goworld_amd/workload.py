@@ -12,6 +12,9 @@ the committed golden fixtures all consume bit-identical float32 inputs.
   every entity moves by U(-1,1) per axis per tick.
 * ``cfg3`` -- one space, N=1M, half uniform, half in 256 Gaussian hotspots
   (sigma 250, centres uniform in [-0.4L,0.4L]^2): skewed cell occupancy.
+  Scaled to another N, the hotspot count scales with N (256 N / 1M, at least
+  1) so that every hotspot keeps ~1953 entities at sigma 250: the crowd
+  density -- and the long cell rows it produces -- is the same at every N.
 * ``cfg4`` -- 8192 independent spaces x 2000 entities, per-space L=1581.1.
 * ``cfg5`` -- one 2^24-entity world, L=sqrt(N*1250).
 
@@ -148,7 +151,7 @@ def make_workload(cfg: str, n: int | None = None, seed: int | None = None,
         nu = n // 2
         xu, zu = _uniform_xy(subseed(seed, 1), nu, L)
         nh = n - nu
-        hot = 256
+        hot = max(1, round(256 * n / 1_000_000))  # density-preserving: ~1953 entities per hotspot
         rc = splitmix(subseed(seed, 2), 2 * hot)
         cx = (unit_f64(rc[0:hot]) * 0.8 - 0.4) * L
         cz = (unit_f64(rc[hot:]) * 0.8 - 0.4) * L

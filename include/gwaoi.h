@@ -98,6 +98,16 @@ typedef struct {
     uint32_t max_spaces;
 } gwaoi_info;
 
+/* Counters of the rare paths of the flush pipeline, summed over flushes
+ * since the world was created (tests assert that a workload reached them). */
+typedef struct {
+    uint64_t flushes;
+    uint64_t combined_replays;      /* combined-pass waves whose LDS event buffer overflowed (sweep replayed) */
+    uint64_t combined_queue_drains; /* combined-pass survivor queues drained in the middle of a sweep         */
+    uint64_t special_global;        /* special-pass lanes whose events spilled past their LDS slots          */
+    uint64_t event_regrows;         /* flushes that grew the device event buffer and re-ran the pair passes  */
+} gwaoi_debug;
+
 typedef struct {
     char name[32];
     double ms;             /* accumulated device time (HIP events)     */
@@ -180,6 +190,7 @@ int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces,
  * when it exceeds cap. */
 int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, size_t *n_out);
 int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info);
+int gwaoi_debug_counters(gwaoi_world *w, gwaoi_debug *out);
 int gwaoi_stage_times(gwaoi_world *w, gwaoi_stage_time *out, size_t cap, size_t *n_out);
 int gwaoi_reset_stage_times(gwaoi_world *w);
 /* Time only the stages whose bit is set (bit i = entry i of gwaoi_stage_times);

@@ -83,7 +83,9 @@ int gwaoi_strips_halo(const gwaoi_strips *s, float *halo);
 
 /* 1. Route this tick's ops of the entities this strip owned after the last
  * tick (Moved / Leave) or that enter the space inside it (Enter).  d_ops is
- * device memory, one op per entity at most, in any order.  counts[0..n_strips-1]
+ * device memory, one op per entity at most, in any order; it must be complete
+ * before the call (the world's stream does not wait for the producer's
+ * stream).  counts[0..n_strips-1]
  * = records for each destination rank, counts[n_strips] = teleport records.
  * Returns GWAOI_ESTATE if an op names an entity this strip does not own. */
 int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint64_t *counts);

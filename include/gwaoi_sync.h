@@ -12,6 +12,8 @@
  *   Entity.syncPositionYawFromClient    Entity.go:430-435       (only if SetClientSyncing(true))
  *   Entity.SetClientSyncing             Entity.go:437-440       gwaoi_entity_set_syncing
  *   Entity.setPositionYaw / SetPosition Entity.go:1185-1205     gwaoi_set_position_yaw
+ *   Space.enter / Space.leave without AOI (no EnableAOI, or IsUseAOI false)
+ *     Space.go:188-251                                        gwaoi_entity_enter_plain / _leave_plain
  *   CollectEntitySyncInfos              Entity.go:1221-1267     gwaoi_collect_sync_infos(_device)
  *     (per-gate MT_SYNC_POSITION_YAW_ON_CLIENTS payloads of 48-B records:
  *      ClientID[16] + EntityID[16] + x,y,z,yaw float32)
@@ -85,17 +87,32 @@ int gwaoi_entity_set_syncing(gwaoi_world *w, uint32_t slot, int syncing);
  * both sync flags as Space.enter does, Space.go:203-205). */
 int gwaoi_entity_set_position_yaw(gwaoi_world *w, uint32_t slot, float x, float y, float z, float yaw);
 
+/* Space.enter of a space without AOI (EnableAOI never called), or of an
+ * entity type without AOI (IsUseAOI false, Space.go:210): Position = (x,y,z)
+ * and both sync flags (Space.go:201-205), no AOI call; the entity has no AOI
+ * neighbours there.  GWAOI_ESTATE unless the slot is in nilSpace (neither in
+ * an AOI space nor in another space without AOI: Space.go:193-195 panics).
+ * gwaoi_enter of a slot in such a space is GWAOI_ESTATE too. */
+int gwaoi_entity_enter_plain(gwaoi_world *w, uint32_t slot, float x, float y, float z);
+/* Space.leave of that space: back to nilSpace (GWAOI_ESTATE if not in one). */
+int gwaoi_entity_leave_plain(gwaoi_world *w, uint32_t slot);
+
 /* ---- moves ---------------------------------------------------------------- */
-/* Entity.setPositionYaw(pos, yaw, fromClient=false) (server-side move): a
- * Moved(x, z) plus Y/yaw, and both sync flags.  GWAOI_ESTATE if the slot is
- * not in a space (the reference warns and returns, Entity.go:1190-1194). */
+/* Entity.setPositionYaw(pos, yaw, fromClient=false) (server-side move).  A
+ * created entity is never in a nil space: outside every space it is in
+ * nilSpace (EntityManager.go:250,293; Space.go:240), so Space.move always
+ * runs.  In an AOI space: a Moved(x, z) plus Position and yaw.  In nilSpace
+ * or a space without AOI, Space.move returns before Position
+ * (Space.go:253-257): only yaw changes.  Both sync flags either way; the
+ * own-client record then carries the stale Position with the new yaw. */
 int gwaoi_set_position_yaw(gwaoi_world *w, uint32_t slot, float x, float y, float z, float yaw);
 
 /* HandleSyncPositionYawFromClient: decode n_rec 32-B records (host memory)
  * on the GPU into one device Moved batch, in record order.  Records whose
- * id is unknown, whose entity is not syncing from its client or is not in a
- * space are skipped silently, as in the reference.  Applied records set
- * Y/yaw and sifSyncNeighborClients. */
+ * id is unknown or whose entity is not syncing from its client are skipped
+ * silently, as in the reference.  The others are setPositionYaw(fromClient):
+ * in an AOI space a Moved plus Position and yaw, elsewhere yaw only (as
+ * above); every applied record raises sifSyncNeighborClients. */
 int gwaoi_sync_from_clients(gwaoi_world *w, const uint8_t *payload, size_t n_rec);
 /* Same, payload already in device memory of the world's GPU (16-B aligned);
  * it must stay valid until the next gwaoi_tick*. */

@@ -13,8 +13,16 @@ restates, in plain Python:
   unknown id -> skipped; ``Entity.syncPositionYawFromClient`` (Entity.go:430-435):
   only while syncing from the client.
 * ``set_position_yaw``      Entity.setPositionYaw (Entity.go:1189-1205):
-  space nil -> return; Space.move (Space.go:253-261) -> Moved; yaw; flags
-  sifSyncNeighborClients, plus sifSyncOwnClient unless from the client.
+  Space.move (Space.go:253-261) -> Position + Moved only in a space with an
+  AOI manager; yaw and the flags sifSyncNeighborClients (+ sifSyncOwnClient
+  unless from the client) in every case.  An entity outside every space is in
+  nilSpace (``entity.Space = nilSpace``, EntityManager.go:250,293 and
+  Space.go:240), never nil, so the early return of Entity.go:1191-1194 is not
+  taken: in nilSpace and in a space without AOI, Position stays stale while
+  yaw and the flags change.
+* ``enter_plain_space``     Space.enter (Space.go:188-226) of a space without
+  AOI (EnableAOI never called) or of an entity type without AOI
+  (IsUseAOI false): Position and both flags, no AOI call.
 * ``collect``               CollectEntitySyncInfos (Entity.go:1221-1267): per
   flagged entity, a 48-byte record ``ClientID + EntityID + x,y,z,yaw`` to its
   own client (sifSyncOwnClient) and to the client of every entity in its
@@ -39,12 +47,13 @@ SIF_OWN, SIF_NEIGHBOR = 1, 2
 
 
 class Ent:
-    __slots__ = ("eid", "slot", "space", "x", "y", "z", "yaw", "gate", "cid", "syncing", "flags", "In", "By")
+    __slots__ = ("eid", "slot", "space", "aoi", "x", "y", "z", "yaw", "gate", "cid", "syncing", "flags", "In", "By")
 
     def __init__(self, eid: bytes, slot: int):
         self.eid, self.slot = eid, slot
         self.space = None
         self.x = self.y = self.z = self.yaw = np.float32(0)
+        self.aoi = False  # space (if any) has an AOI manager and the entity uses AOI
         self.gate, self.cid = None, None
         self.syncing = False
         self.flags = 0
@@ -108,27 +117,40 @@ class GameEntities:
     def enter_space(self, slot, sp, x, y, z):
         """Space.enter (Space.go:188-226): Position, both sync flags, Enter."""
         e = self.by_slot[slot]
-        e.space = sp
+        assert e.space is None, "Space.enter: entity not in nilSpace (Space.go:193-195 panics)"
+        e.space, e.aoi = sp, True
         e.x, e.y, e.z = f32(x), f32(y), f32(z)
         e.flags |= SIF_OWN | SIF_NEIGHBOR
         self.aoi.enter(sp, slot, e.x, e.z)
         self._replay()
 
-    def leave_space(self, slot):
-        """Space.leave (Space.go:228-251)."""
+    def enter_plain_space(self, slot, sp, x, y, z):
+        """Space.enter (Space.go:188-226) without an AOI call: the space has no
+        AOI manager, or the entity type does not use AOI (Space.go:210)."""
         e = self.by_slot[slot]
-        self.aoi.leave(slot)
-        e.space = None
+        assert e.space is None, "Space.enter: entity not in nilSpace (Space.go:193-195 panics)"
+        e.space, e.aoi = ("plain", sp), False
+        e.x, e.y, e.z = f32(x), f32(y), f32(z)
+        e.flags |= SIF_OWN | SIF_NEIGHBOR
+
+    def leave_space(self, slot):
+        """Space.leave (Space.go:228-251): back to nilSpace; Leave only with AOI (Space.go:242)."""
+        e = self.by_slot[slot]
+        if e.aoi:
+            self.aoi.leave(slot)
+        e.space, e.aoi = None, False
         self._replay()
 
     def set_position_yaw(self, slot, x, y, z, yaw, from_client=False):
-        """Entity.setPositionYaw (Entity.go:1189-1205)."""
+        """Entity.setPositionYaw (Entity.go:1189-1205).  e.Space is never nil
+        for a created entity (nilSpace), so every call reaches Space.move, which
+        returns before touching Position when the space has no AOI manager
+        (Space.go:253-257): only then are Position and the AOI relation updated."""
         e = self.by_slot[slot]
-        if e.space is None:
-            return False
-        e.x, e.y, e.z = f32(x), f32(y), f32(z)
-        self.aoi.moved(slot, e.x, e.z)
-        self._replay()
+        if e.aoi:
+            e.x, e.y, e.z = f32(x), f32(y), f32(z)
+            self.aoi.moved(slot, e.x, e.z)
+            self._replay()
         e.yaw = f32(yaw)
         e.flags |= SIF_NEIGHBOR
         if not from_client:

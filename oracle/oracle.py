@@ -74,6 +74,11 @@ def lib():
         L.cf_free.argtypes = [vp]
         L.cf_pred.argtypes = [f, f, f, f, f]
         L.cf_pred.restype = C.c_int
+        L.cf_diff.argtypes = [i64] + [vp] * 9 + [C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(i64),
+                                                 C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(i64), C.c_int]
+        L.cf_diff.restype = C.c_int
+        L.cf_rows.argtypes = [i64, vp, vp, vp, vp, vp, i64, vp, vp, C.POINTER(C.POINTER(C.c_uint32))]
+        L.cf_rows.restype = i64
         _lib = L
     return _lib
 
@@ -247,6 +252,73 @@ def closed_form_pairs(x, z, seq, sp, D_by_space):
     res = np.ctypeslib.as_array(out, shape=(n,)).copy() if n else np.empty(0, np.uint64)
     L.cf_free(C.cast(out, C.c_void_p))
     return res
+
+
+def _space_d(sp_arrays, D_by_space):
+    nsp = 1
+    for sp in sp_arrays:
+        live = sp[sp != DEAD]
+        if live.size:
+            nsp = max(nsp, int(live.max()) + 1)
+    D = np.zeros(nsp, np.float32)
+    for k, v in D_by_space.items():
+        if int(k) < nsp:
+            D[int(k)] = v
+    return D
+
+
+def _state(x, z, seq, sp):
+    return (np.ascontiguousarray(x, np.float32), np.ascontiguousarray(z, np.float32),
+            np.ascontiguousarray(seq, np.uint64), np.ascontiguousarray(sp, np.uint32))
+
+
+def closed_form_diff(before, after, D_by_space, threads=None):
+    """Net events of one flush from the closed form at two states (Appendix B,
+    per-tick recipe): ``before``/``after`` = (x, z, seq, space) per entity, space
+    DEAD when not live.  Returns sorted uint64 keys (enter, leave), both
+    directions.  An entity that changed space leaves every old pair and enters
+    every new one.  Multithreaded C (oracle/closed_form.c cf_diff)."""
+    L = lib()
+    b = _state(*before)
+    a = _state(*after)
+    n = b[0].size
+    D = _space_d([b[3], a[3]], D_by_space)
+    threads = threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    pe, pl = C.POINTER(C.c_uint64)(), C.POINTER(C.c_uint64)()
+    ne, nl = C.c_int64(), C.c_int64()
+    L.cf_diff(n, *[_p(v) for v in b], *[_p(v) for v in a], _p(D), C.byref(pe), C.byref(ne), C.byref(pl),
+              C.byref(nl), threads)
+    ent = np.ctypeslib.as_array(pe, shape=(ne.value,)).copy() if ne.value else np.empty(0, np.uint64)
+    lev = np.ctypeslib.as_array(pl, shape=(nl.value,)).copy() if nl.value else np.empty(0, np.uint64)
+    L.cf_free(C.cast(pe, C.c_void_p))
+    L.cf_free(C.cast(pl, C.c_void_p))
+    return ent, lev
+
+
+def closed_form_rows(x, z, seq, sp, D_by_space, query):
+    """Sorted closed-form neighbour list of every entity in ``query``: list of uint32 arrays."""
+    L = lib()
+    st = _state(x, z, seq, sp)
+    D = _space_d([st[3]], D_by_space)
+    q = np.ascontiguousarray(query, np.int32)
+    off = np.zeros(q.size + 1, np.int64)
+    out = C.POINTER(C.c_uint32)()
+    tot = L.cf_rows(st[0].size, *[_p(v) for v in st], _p(D), q.size, _p(q), _p(off), C.byref(out))
+    flat = np.ctypeslib.as_array(out, shape=(tot,)).copy() if tot else np.empty(0, np.uint32)
+    L.cf_free(C.cast(out, C.c_void_p))
+    return [flat[off[k]:off[k + 1]] for k in range(q.size)]
+
+
+def key_checksum(keys: np.ndarray) -> tuple:
+    """(count, sum of SplitMix64(key) mod 2^64) of a uint64 key multiset: an
+    order-independent fingerprint for relations too large to sort in a test."""
+    k = np.asarray(keys, np.uint64)
+    with np.errstate(over="ignore"):
+        z = k + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return int(k.size), int(np.sum(z, dtype=np.uint64))
 
 
 def pred(wx, wz, lx, lz, D):

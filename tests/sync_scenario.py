@@ -1,9 +1,12 @@
 """Seeded entity-sync scenario shared by the CPU and GPU sync tests.
 
-A game process with entities over two spaces: clients on several gates,
-some entities not syncing from their client, some never in a space, some
-unknown ids in the client packets, duplicated records, server-side moves,
-leaves and re-enters (space changes) between packets.  Each flush is a list
+A game process with entities over two AOI spaces and one space without AOI:
+clients on several gates, some entities not syncing from their client, some
+never in a space (nilSpace), some in the space without AOI, some unknown ids
+in the client packets, duplicated records, server-side moves (also of
+entities outside every AOI space: Position stays, yaw and flags change,
+Entity.go:1189-1205 with Space.go:253-257), leaves and re-enters (space
+changes) between packets.  Each flush is a list
 of ops in call order; `run_oracle` / `run_gpu` apply them to the sequential
 restatement (oracle/entity_sync.py) and to libgwaoi.
 """
@@ -36,14 +39,17 @@ def make(seed=7, n=600, n_outside=40, flushes=6, L=700.0):
         })
     spaces = {0: 100.0, 1: 60.0}
     in_space = {e["slot"]: (e["slot"] % 2) for e in ent[: n - n_outside]}
+    plain = {e["slot"] for e in ent[n - n_outside:] if e["slot"] % 2 == 0}  # in the space without AOI
     setup = [("set_pos", e["slot"], *e["pos"]) for e in ent]
     setup += [("enter", s, sp) for s, sp in in_space.items()]
+    setup += [("enter_plain", s) for s in sorted(plain)]
     cur = {e["slot"]: list(e["pos"]) for e in ent}
     space_of = dict(in_space)
     flush_ops = []
     for f in range(flushes):
         ops = []
         live = sorted(space_of)
+        outside = sorted(set(range(n)) - set(space_of))  # nilSpace or the space without AOI
 
         def step(s, big=False):
             p = cur[s]
@@ -57,7 +63,21 @@ def make(seed=7, n=600, n_outside=40, flushes=6, L=700.0):
         for s in rng.choice(live, size=min(25, len(live)), replace=False):
             p = step(int(s))
             ops.append(("server_move", int(s), *p))
+        for s in rng.choice(outside, size=min(6, len(outside)), replace=False):
+            p = step(int(s))  # Position stays stale in the reference: only yaw and the flags change
+            ops.append(("server_move", int(s), *p))
         ops.append(("packet", packet(rng, ent, cur, step, 0.6)))
+        # the space without AOI: leave to nilSpace, or enter it from nilSpace
+        for s in rng.choice(outside, size=min(4, len(outside)), replace=False):
+            s = int(s)
+            if s in plain:
+                ops.append(("leave_plain", s))
+                plain.discard(s)
+            else:
+                p = step(s, big=True)
+                ops.append(("set_pos", s, *p))
+                ops.append(("enter_plain", s))
+                plain.add(s)
         # leaves / re-enters / space changes
         for s in rng.choice(live, size=8, replace=False):
             s = int(s)
@@ -109,7 +129,10 @@ def run_oracle(sc, on_flush):
         elif k == "enter":
             x, y, z, _ = pend.pop(op[1])
             g.enter_space(op[1], op[2], x, y, z)
-        elif k == "leave":
+        elif k == "enter_plain":
+            x, y, z, _ = pend.pop(op[1])
+            g.enter_plain_space(op[1], 9, x, y, z)
+        elif k in ("leave", "leave_plain"):
             g.leave_space(op[1])
         elif k == "server_move":
             assert g.set_position_yaw(op[1], *op[2:], from_client=False)
@@ -145,8 +168,13 @@ def run_gpu(sc, w, on_flush, device_payload=None):
         elif k == "enter":
             x, _, z, _ = apply.last[op[1]]
             w.enter(sp_ids[op[2]], op[1], x, z)
+        elif k == "enter_plain":
+            x, y, z, _ = apply.last[op[1]]
+            w.entity_enter_plain(op[1], x, y, z)
         elif k == "leave":
             w.leave(op[1])
+        elif k == "leave_plain":
+            w.entity_leave_plain(op[1])
         elif k == "server_move":
             w.set_position_yaw(op[1], *op[2:])
         elif k == "packet":

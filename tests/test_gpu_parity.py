@@ -583,3 +583,56 @@ def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
     finally:
         wr.close()
         wi.close()
+
+
+def test_committed_events_delivered_on_device_error_gpu():
+    """A flush whose device batch held a bad op (here an explicit seq below the
+    flush's floor) commits without that op and reports the problem; its other
+    events must still reach the caller (GwaoiError.events), or the callers'
+    InterestedIn/By would drift from the engine for good."""
+    torch = pytest.importorskip("torch")
+    with World(16) as w:
+        s = w.space_create(D)
+        for i in range(10):
+            w.enter(s, i, 0.0, 0.0)
+        assert flush(w)[0].size == 90
+        floor = w.info()["next_seq"]
+        ds = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+        dx = torch.tensor([5000.0, 7000.0], device="cuda")
+        dz = torch.tensor([0.0, 0.0], device="cuda")
+        dq = torch.tensor([floor + 5, floor - 3], dtype=torch.int64, device="cuda")  # op 1 is stale: dropped
+        torch.cuda.synchronize()
+        w.moved_batch_device(ds.data_ptr(), dx.data_ptr(), dz.data_ptr(), 2, d_seq=dq.data_ptr())
+        with pytest.raises(GwaoiError) as ei:
+            w.tick()
+        assert ei.value.code == -1 and ei.value.events is not None
+        ent, lev = ei.value.events
+        assert ent.shape[0] == 0
+        assert sorted(map(tuple, lev.tolist())) == sorted([(0, i) for i in range(1, 10)] + [(i, 0) for i in range(1, 10)])
+        assert w.neighbors(0).size == 0 and w.neighbors(1).tolist() == [2, 3, 4, 5, 6, 7, 8, 9]
+        w.moved(1, 5000.0, 0.0)  # the world goes on
+        ent, lev = flush(w)
+        assert ent.size == 2 and lev.size == 16
+
+
+def test_failed_event_regrow_poisons_world_gpu(monkeypatch):
+    """A failure after the flush's kernels rewrote the per-slot records but
+    before the commit (here an injected failure of the event-buffer regrow)
+    leaves host and device apart: the world refuses every later call."""
+    monkeypatch.setenv("GWAOI_INJECT_REGROW_FAIL", "1")
+    w = World(64, event_capacity=16)
+    monkeypatch.delenv("GWAOI_INJECT_REGROW_FAIL")
+    try:
+        s = w.space_create(D)
+        for i in range(20):
+            w.enter(s, i, 0.0, 0.0)  # 380 directed enters > 16
+        with pytest.raises(GwaoiError) as ei:
+            w.tick()
+        assert ei.value.code == -4
+        for call in (lambda: w.enter(s, 30, 1.0, 1.0), lambda: w.moved(0, 1.0, 1.0), w.tick,
+                     lambda: w.neighbors(0)):
+            with pytest.raises(GwaoiError) as ej:
+                call()
+            assert ej.value.code == -5 and "failed flush" in str(ej.value)
+    finally:
+        w.close()

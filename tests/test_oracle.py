@@ -234,3 +234,43 @@ def test_bulk_enter_equals_sequential_enters(oracle_mod):
     a.moved_batch(sl, nx, nz)
     b.moved_batch(sl, nx, nz)
     np.testing.assert_array_equal(a.pairs(), b.pairs())
+
+
+def test_closed_form_diff_matches_setdiff(oracle_mod):
+    """cf_diff (the multithreaded tick diff used at full cfg3 size) == set
+    difference of two cf_pairs relations, with leaves, enters and space changes."""
+    rng = np.random.default_rng(17)
+    n = 4000
+    x0 = rng.uniform(-1500, 1500, n).astype(np.float32)
+    z0 = rng.uniform(-1500, 1500, n).astype(np.float32)
+    sp0 = rng.integers(0, 2, n).astype(np.uint32)
+    s0 = rng.permutation(n).astype(np.uint64) + 1
+    sp0[rng.random(n) < 0.05] = oracle_mod.DEAD
+    x1 = (x0 + rng.uniform(-30, 30, n)).astype(np.float32)
+    z1 = (z0 + rng.uniform(-30, 30, n)).astype(np.float32)
+    sp1 = sp0.copy()
+    ch = rng.random(n) < 0.05
+    sp1[ch] = rng.integers(0, 2, ch.sum()).astype(np.uint32)
+    sp1[rng.random(n) < 0.05] = oracle_mod.DEAD
+    s1 = s0.copy()
+    mv = rng.random(n) < 0.7
+    s1[mv] = n + 1 + rng.permutation(mv.sum()).astype(np.uint64)
+    Ds = {0: np.float32(100.0), 1: np.float32(60.0)}
+    ent, lev = oracle_mod.closed_form_diff((x0, z0, s0, sp0), (x1, z1, s1, sp1), Ds, threads=3)
+
+    def rel(x, z, s, sp):  # space-qualified keys (each space its own manager)
+        k = oracle_mod.closed_form_pairs(x, z, s, sp, Ds)
+        a = (k >> np.uint64(32)).astype(np.int64)
+        return set(zip(sp[a].tolist(), k.tolist()))
+
+    r0, r1 = rel(x0, z0, s0, sp0), rel(x1, z1, s1, sp1)
+    want_e = np.array(sorted(k for _, k in r1 - r0), np.uint64)
+    want_l = np.array(sorted(k for _, k in r0 - r1), np.uint64)
+    np.testing.assert_array_equal(ent, want_e)
+    np.testing.assert_array_equal(lev, want_l)
+    assert ent.size > 100 and lev.size > 100
+    rows = oracle_mod.closed_form_rows(x1, z1, s1, sp1, Ds, [0, 5, 17])
+    k1 = oracle_mod.closed_form_pairs(x1, z1, s1, sp1, Ds)
+    for q, r in zip([0, 5, 17], rows):
+        np.testing.assert_array_equal(r, (k1[(k1 >> np.uint64(32)) == q] & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+    assert oracle_mod.key_checksum(ent) == oracle_mod.key_checksum(ent[::-1].copy())

@@ -66,7 +66,7 @@ def test_packet_decode_rules():
     e0, e1, e2, e3 = (g.by_slot[i] for i in range(4))
     assert (e0.x, e0.y, e0.yaw) == (6.0, 4.0, 2.5)         # last record wins
     assert e1.x == 10.0 and e1.flags == 0                  # not syncing from its client
-    assert e3.x == 30.0 and e3.flags == 0                  # no space: setPositionYaw returns
+    assert e3.x == 30.0 and e3.flags == 0                  # not syncing from its client
     assert e0.flags == SIF_NEIGHBOR and e2.flags == SIF_NEIGHBOR  # fromClient: no own-client record
     out = g.collect()
     # e0 and e2 moved; interested clients: e0 <- {1 (gate 2)}, e2 <- {0 (gate 1), 1 (gate 2)}
@@ -85,14 +85,69 @@ def test_left_entity_keeps_own_record():
     assert out == {1: [CID[0] + EID[0] + struct.pack("<4f", 1, 1, 1, 1)]}
 
 
+def test_nilspace_entity_keeps_position_gets_yaw_and_flags():
+    """Entity.setPositionYaw of an entity outside every space: e.Space is
+    nilSpace (EntityManager.go:250, Space.go:240), not nil, so the call goes on
+    to nilSpace.move, which returns before `entity.Position = newPos` because
+    nilSpace has no AOI manager (Space.go:253-257); yaw and the sync flags are
+    still set (Entity.go:1196-1204).  CollectEntitySyncInfos then sends the own
+    client the STALE position with the NEW yaw (Entity.go:1228-1239)."""
+    g = small_world()
+    g.set_client(3, 1, CID[3])
+    g.set_syncing(3, True)
+    g.collect()
+    e3 = g.by_slot[3]
+    g.handle_sync_packet(rec(EID[3], 50.0, 9.0, 50.0, 1.25))  # from the client: neighbour flag only
+    assert (e3.x, e3.y, e3.z) == (30.0, 1.0, 0.0) and e3.yaw == np.float32(1.25)
+    assert e3.flags == SIF_NEIGHBOR and e3.By == set()
+    assert g.collect() == {}  # no own-client flag, nobody interested
+    assert g.set_position_yaw(3, 60.0, 8.0, 60.0, -2.0)  # server side: both flags
+    assert e3.x == 30.0 and e3.flags == SIF_OWN | SIF_NEIGHBOR
+    assert g.collect() == {1: [CID[3] + EID[3] + struct.pack("<4f", 30.0, 1.0, 0.0, -2.0)]}
+
+
+def test_space_without_aoi_enter_move_leave():
+    """Space.enter of a space without AOI (or of an entity type without AOI,
+    Space.go:210) sets Position and both flags but calls no AOI manager;
+    moves inside it keep Position (Space.go:254-256) and change yaw."""
+    g = small_world()
+    g.set_client(3, 2, CID[3])
+    g.collect()
+    e3 = g.by_slot[3]
+    g.enter_plain_space(3, 9, 5.0, 6.0, 7.0)
+    assert (e3.x, e3.y, e3.z) == (5.0, 6.0, 7.0) and e3.flags == SIF_OWN | SIF_NEIGHBOR
+    assert g.collect() == {2: [CID[3] + EID[3] + struct.pack("<4f", 5.0, 6.0, 7.0, 0.5)]}
+    g.set_position_yaw(3, 0.0, 0.0, 0.0, 3.0)
+    assert (e3.x, e3.z, e3.yaw) == (5.0, 7.0, np.float32(3.0))
+    assert g.collect() == {2: [CID[3] + EID[3] + struct.pack("<4f", 5.0, 6.0, 7.0, 3.0)]}
+    # the entity is 5 units from entity 0 of the AOI space, yet no AOI relation exists
+    assert g.by_slot[0].In == {1, 2} and 3 not in g.by_slot[0].By
+    g.leave_space(3)
+    assert e3.space is None and g.collect() == {}
+
+
+def test_left_aoi_entity_moves_keep_last_aoi_position():
+    """After Space.leave the entity is in nilSpace: a server move sends its own
+    client the position it had when it left, with the new yaw."""
+    g = small_world()
+    g.collect()
+    g.set_position_yaw(0, 3.0, 4.0, 5.0, 0.25)
+    g.leave_space(0)
+    g.collect()
+    g.set_position_yaw(0, 100.0, 100.0, 100.0, -1.0)
+    assert g.collect() == {1: [CID[0] + EID[0] + struct.pack("<4f", 3.0, 4.0, 5.0, -1.0)]}
+
+
 def test_scenario_oracle_consistency():
     sc = SS.make(n=200, flushes=3)
 
     def check(i, g):
         for e in g.by_slot.values():
             assert e.In == e.By
-            if e.space is not None:
+            if e.aoi:
                 assert sorted(e.By) == g.aoi.neighbors(e.slot).tolist()
+            else:
+                assert not e.By and not e.In
         g.collect()
 
     SS.run_oracle(sc, check)
@@ -163,9 +218,20 @@ def test_sync_errors():
             w.entity_bind([2], [EID[0]])  # id taken
         with pytest.raises(GwaoiError):
             w.entity_bind([0], [EID[2]])  # slot taken
+        w.set_position_yaw(0, 1, 2, 3, 4)  # nilSpace: yaw + flags, Position stays (Space.go:253-257)
         with pytest.raises(GwaoiError):
-            w.set_position_yaw(0, 1, 2, 3, 4)  # not in a space
+            w.set_position_yaw(99, 1, 2, 3, 4)  # slot out of range
+        w.entity_enter_plain(1, 1.0, 2.0, 3.0)  # a space without AOI
+        with pytest.raises(GwaoiError):
+            w.entity_enter_plain(1, 1.0, 2.0, 3.0)  # already in a space without AOI
+        with pytest.raises(GwaoiError):
+            w.enter(sp, 1, 0.0, 0.0)  # in a space already (Space.enter panics, Space.go:193-195)
+        w.entity_leave_plain(1)
+        with pytest.raises(GwaoiError):
+            w.entity_leave_plain(1)  # not in a space without AOI
         w.enter(sp, 0, 0.0, 0.0)
+        with pytest.raises(GwaoiError):
+            w.entity_enter_plain(0, 1.0, 2.0, 3.0)  # in an AOI space (Space.enter panics, Space.go:193-195)
         with pytest.raises(GwaoiError):
             w.collect_sync_infos()  # ops queued since the last flush
         w.tick()
