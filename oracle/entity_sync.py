@@ -73,7 +73,7 @@ class GameEntities:
         self.by_slot: dict[int, Ent] = {}
         self.creates: dict[int, list] = {}   # gate -> [48-byte create records], callback order
         self.destroys: dict[int, list] = {}  # gate -> [32-byte destroy records]
-        self.raw: list = []                  # (type, a, b) callbacks since take_raw()
+        self.raw: list = []                  # (type, a, b, space) callbacks since take_raw()
 
     # ---- entity table
     def create(self, eid: bytes, slot: int, x=0.0, y=0.0, z=0.0, yaw=0.0):
@@ -96,9 +96,9 @@ class GameEntities:
 
     # ---- AOI callbacks (Entity.go:227-246)
     def _replay(self):
-        t, a, b = self.aoi.take_events()
+        t, a, b, sp = self.aoi.take_events(with_space=True)
         if t.size:
-            self.raw.append((t, a, b))
+            self.raw.append((t, a, b, sp))
         for k in range(t.size):
             ea, eb = self.by_slot[int(a[k])], self.by_slot[int(b[k])]
             if t[k] == EV_ENTER:
@@ -186,17 +186,18 @@ class GameEntities:
         return {g: sorted(v) for g, v in out.items()}
 
     def take_raw(self):
-        """(type, a, b) arrays of every callback since the last call."""
+        """(type, a, b, space) arrays of every callback since the last call."""
         r, self.raw = self.raw, []
         if not r:
-            return np.empty(0, np.uint8), np.empty(0, np.int32), np.empty(0, np.int32)
-        return tuple(np.concatenate([x[i] for x in r]) for i in range(3))
+            return (np.empty(0, np.uint8), np.empty(0, np.int32), np.empty(0, np.int32),
+                    np.empty(0, np.int64))
+        return tuple(np.concatenate([x[i] for x in r]) for i in range(4))
 
-    def net_client_events(self, t, a, b):
+    def net_client_events(self, t, a, b, sp=None):
         """Client messages of a flush's NET diff at the flush's final state (the GPU
         path's granularity): ({gate: sorted create records}, {gate: sorted destroy records})."""
         from .oracle import net_events
-        ent, lev = net_events(t, a, b)
+        ent, lev = net_events(t, a, b, sp)
         cre, des = {}, {}
         for k in ent:
             ea, eb = self.by_slot[int(k >> np.uint64(32))], self.by_slot[int(k & np.uint64(0xFFFFFFFF))]

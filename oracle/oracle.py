@@ -214,14 +214,19 @@ class SpacesOracle:
         sp = sps.pop()
         self.mgr[sp].moved_batch(slots, xs, zs)
 
-    def take_events(self):
-        ts, as_, bs = [], [], []
+    def take_events(self, with_space: bool = False):
+        """(type, a, b) of every callback since the last call, manager by
+        manager (call order within a space); with_space: also the space of
+        each event, so that a net diff can keep every space its own manager."""
+        ts, as_, bs, ss = [], [], [], []
         for sp, m in self.mgr.items():
             t, a, b = m.take_events()
-            ts.append(t); as_.append(a); bs.append(b)
+            ts.append(t); as_.append(a); bs.append(b); ss.append(np.full(t.size, sp, np.int64))
         if not ts:
-            return np.empty(0, np.uint8), np.empty(0, np.int32), np.empty(0, np.int32)
-        return np.concatenate(ts), np.concatenate(as_), np.concatenate(bs)
+            e = (np.empty(0, np.uint8), np.empty(0, np.int32), np.empty(0, np.int32))
+            return e + (np.empty(0, np.int64),) if with_space else e
+        out = (np.concatenate(ts), np.concatenate(as_), np.concatenate(bs))
+        return out + (np.concatenate(ss),) if with_space else out
 
     def pairs(self):
         keys = [m.pairs() for m in self.mgr.values()]
@@ -334,21 +339,26 @@ def events_to_keys(t, a, b):
     return np.sort(k[t == EV_ENTER]), np.sort(k[t == EV_LEAVE])
 
 
-def net_events(t, a, b):
+def net_events(t, a, b, sp=None):
     """Net per-flush diff of a sequential event stream: (enter keys, leave keys).
 
     The sequential manager can emit a transient enter+leave of one pair within
     a flush; the batch engine reports only the net change.
+    With ``sp`` (the space of each event) every space is its own manager: a
+    pair that leaves in one space and enters in another inside the flush
+    (both entities changed space) keeps both events, as the GPU path reports
+    them.
     """
     a = np.asarray(a).astype(np.int64)
     b = np.asarray(b).astype(np.int64)
+    s = np.zeros(a.size, np.int64) if sp is None else np.asarray(sp).astype(np.int64)
     state = {}
-    for ti, ai, bi in zip(t.tolist(), a.tolist(), b.tolist()):
-        k = (ai << 32) | bi
+    for ti, ai, bi, si in zip(t.tolist(), a.tolist(), b.tolist(), s.tolist()):
+        k = (si, (ai << 32) | bi)
         d = 1 if ti == EV_ENTER else -1
         state[k] = state.get(k, 0) + d
-    ent = np.array(sorted(k for k, v in state.items() if v > 0), np.uint64)
-    lev = np.array(sorted(k for k, v in state.items() if v < 0), np.uint64)
+    ent = np.array(sorted(k for (_, k), v in state.items() if v > 0), np.uint64)
+    lev = np.array(sorted(k for (_, k), v in state.items() if v < 0), np.uint64)
     for v in state.values():
         assert v in (-1, 0, 1), "unbalanced event stream"
     return ent, lev

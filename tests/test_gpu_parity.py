@@ -134,7 +134,7 @@ def run_stream_vs_oracle(oracle_mod, ops, n, flush_every, D_by_space=None, check
                 orc.leave(op[1])
             if k % flush_every == flush_every - 1 or k == len(ops) - 1:
                 ge, gl = flush(w)
-                oe, ol = oracle_mod.net_events(*orc.take_events())
+                oe, ol = oracle_mod.net_events(*orc.take_events(with_space=True))
                 np.testing.assert_array_equal(ge, oe)
                 np.testing.assert_array_equal(gl, ol)
                 if check_neighbors:

@@ -159,9 +159,9 @@ def expected(sc):
     exp = []
 
     def on_flush(i, g):
-        t, a, b = g.take_raw()
-        ent, lev = oracle.net_events(t, a, b)
-        cre, des = g.net_client_events(t, a, b)
+        raw = g.take_raw()  # every space its own manager (a pair may leave in one and enter in another)
+        ent, lev = oracle.net_events(*raw)
+        cre, des = g.net_client_events(*raw)
         exp.append({"sync": g.collect(), "enter": ent, "leave": lev, "create": cre, "destroy": des})
 
     SS.run_oracle(sc, on_flush)
