@@ -189,9 +189,9 @@ void scan_exclusive(const uint32_t *in, uint32_t *out, size_t n, uint32_t *tmp, 
 size_t scan_tmp_elems(size_t n);
 
 // New frame (f_rec/f_ss), previous state in the new order (o_rec), and the
-// combined pass's candidate records cand = {x, z} (NaN, NaN for a jumper).
+// combined pass's candidate records cand = {x, z, old x, old z} (x, z NaN for a jumper).
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
-                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                    uint32_t n_spaces, void *bbox_parts, hipStream_t st);
@@ -202,7 +202,7 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
 // Directed event pairs go to tmp at an atomically reserved offset per block;
 // block t's enter total/base are at [t], its leave total/base at [leave_off + t].
 inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; }
-void launch_combined(FrameView F, const uint2 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
+void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // Special-entity pass over the previous frame in blocks of TILE_A entries

@@ -249,15 +249,18 @@ __device__ __forceinline__ bool is_near(float xn, float zn, float xo, float zo, 
     return (int)(fabsf(xn - xo) <= thr) & (int)(fabsf(zn - zo) <= thr);
 }
 
-// Candidate record of the combined pass (k_gather -> k_combined), 8 B per
-// frame entry: the exact (x, z) of a "near" entity, (NaN, NaN) for a jumper
-// -- not near: new in this space, changed space, or moved > FAR_FRAC*D on an
-// axis (an absent previous state has NaN coordinates and fails is_near).
-// NaN fails every band compare, so the strip filters drop jumper partners
-// without a flag load.
-__device__ __forceinline__ uint2 cand_of(const Rec16 &now, const Rec16 &old, float thr) {
-    return is_near(now.x, now.z, old.x, old.z, thr) ? make_uint2(__float_as_uint(now.x), __float_as_uint(now.z))
-                                                    : make_uint2(0x7FC00000u, 0x7FC00000u);
+// Candidate record of the combined pass (k_gather -> k_combined), 16 B per
+// frame entry: the exact (x, z) of a "near" entity and its previous-flush
+// (x, z); (NaN, NaN, ...) for a jumper -- not near: new in this space,
+// changed space, or moved > FAR_FRAC*D on an axis (an absent previous state
+// has NaN coordinates and fails is_near).  NaN fails every band compare, so
+// the strip filters drop jumper partners without a flag load; the previous
+// position lets the filter drop pairs whose relation certainly did not change.
+__device__ __forceinline__ uint4 cand_of(const Rec16 &now, const Rec16 &old, float thr) {
+    return is_near(now.x, now.z, old.x, old.z, thr)
+               ? make_uint4(__float_as_uint(now.x), __float_as_uint(now.z), __float_as_uint(old.x),
+                            __float_as_uint(old.z))
+               : make_uint4(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u);
 }
 
 // INCR (the grid is the previous frame's): also count, per cell, the
@@ -852,7 +855,7 @@ __device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], in
 __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
                                            const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
-                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
+                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                                            const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
                                            SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
@@ -863,7 +866,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
 __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
-                         SlotSp *f_ss, Rec16 *o_rec, uint2 *cand, const SpaceGrid *__restrict__ grid,
+                         SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
                          unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                          uint32_t n_spaces, BBoxPart *parts) {
@@ -879,7 +882,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
 __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
                                            const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
-                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
+                                           Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                                            const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
                                            SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
@@ -1046,6 +1049,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
     __shared__ unsigned long long s_base;
 
     __shared__ uint32_t s_spr[2];  // smallest / largest space among the active lanes
+    __shared__ uint32_t s_nglob;   // lanes taking the global write path (DBG_SPECIAL_GLOBAL)
     const uint32_t t = blockIdx.x;  // entries [t*PT, t*PT + PT) of the frame
     const uint32_t tid = threadIdx.x;
     PairCtx A;
@@ -1087,6 +1091,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
     if (tid == 0) {
         s_spr[0] = 0xFFFFFFFFu;
         s_spr[1] = 0u;
+        s_nglob = 0u;
     }
     __syncthreads();
     if (active) {
@@ -1225,7 +1230,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
                 }
             }
             if (nk > PS) {
-                atomicAdd(dbg + DBG_SPECIAL_GLOBAL, 1u);
+                atomicAdd(&s_nglob, 1u);
                 uint32_t we = 0, wl = 0;  // continue after the buffered events, in order
                 enum_global<MODE, true>(F, O_rec, O_ss, g, A, thr, cx0, cx1, cz0, cz1, PS, tmp, pe + 2ull * ie,
                                         pl + 2ull * il, cap, we, wl);
@@ -1235,6 +1240,8 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
             enum_global<MODE, true>(F, O_rec, O_ss, g, A, thr, cx0, cx1, cz0, cz1, 0, tmp, pe, pl, cap, we, wl);
         }
     }
+    __syncthreads();
+    if (tid == 0 && s_nglob) atomicAdd(dbg + DBG_SPECIAL_GLOBAL, s_nglob);
 }
 
 // ------------------------------------------------------- combined pass ------
@@ -1261,24 +1268,24 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
-#ifndef GWAOI_SW_U
-#define GWAOI_SW_U 8
-#endif
 #ifndef GWAOI_QCAP
 #define GWAOI_QCAP 640
 #endif
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
-constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= SW_U * WAVE + a drain batch)
-constexpr int SW_U = GWAOI_SW_U;  // candidates per lane per sweep iteration on long rows
+#ifndef GWAOI_SW_U
+#define GWAOI_SW_U 4  // candidates per lane per sweep iteration on long rows
+#endif
+constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= one sweep iteration + a drain batch)
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
-static_assert(QCAP >= SW_U * WAVE, "queue must hold one sweep iteration");
+static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
 
 // A queued pair is (A, B): A is one of the block's own entries, so it is kept
 // as its offset in the block (1 B) next to B's frame index (4 B).  5 B per
 // entry keeps the block under 20 KB of LDS (8 blocks per CU).
 struct CombinedLds {
+    uint32_t ndrain;        // mid-sweep queue drains of the block (DBG_COMBINED_DRAIN)
     uint32_t qb[CW][QCAP];  // queued pairs of a wave: B frame index
     uint8_t qa[CW][QCAP];   //   ... A frame index - block start
     uint2 ev[CW][EVW];      // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
@@ -1289,15 +1296,18 @@ struct CombinedLds {
 };
 
 struct CombinedCtx {  // block-uniform
+    uint32_t *dbg;  // TickScalars::dbg (rare-path counters)
     SpaceGrid g;
     PairCtx proto;
     float thr, lo, hi, lo_in, M;
+    float in_max, out_min;  // Chebyshev distance certainly inside (<=) / outside (>) every owner's window
     bool band_ok;  // lo > 0 (else every lane sweeps its whole window)
 };
 
 struct LaneA {
     uint32_t a;  // frame index
     float x, z;
+    float xo, zo;  // previous-flush position (near lanes)
     bool valid, jump;
 };
 
@@ -1309,18 +1319,21 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // Full test of the queued pairs of wave w; appends events (deterministic order).
 // replay: count only, and write events number >= EVW straight to the output.
-__device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, uint32_t e0, const FrameView &F,
-                                         const Rec16 *__restrict__ O_rec, const PairCtx &proto, float thr,
-                                         uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap, unsigned long long pe,
-                                         unsigned long long pl, bool replay) {
+__device__ __forceinline__ void drain_queue(const uint32_t *qb, const uint8_t *qa, uint2 *evb, uint32_t qn, uint32_t e0,
+                                         const FrameView &F, const Rec16 *__restrict__ O_rec, const PairCtx &proto,
+                                         float thr, uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap,
+                                         unsigned long long pe, unsigned long long pl, bool replay) {
     const uint32_t ln = lane();
+#ifdef GWAOI_EXP_NODRAIN  // timing experiment only: survivors are dropped (events wrong)
+    return;
+#endif
     for (uint32_t q0 = 0; q0 < qn; q0 += WAVE) {
         const uint32_t e = q0 + ln;
         int kind = 0;
         uint32_t a = 0, b = 0;
         if (e < qn) {
-            a = e0 | (uint32_t)L.qa[w][e];
-            b = L.qb[w][e];
+            a = e0 + (uint32_t)qa[e];
+            b = qb[e];
             PairCtx A = proto;
             A.a = a;
             A.now = ld_rec(F.rec, a);
@@ -1334,7 +1347,7 @@ __device__ __forceinline__ void drain_queue(CombinedLds &L, int w, uint32_t qn, 
         if (kind) {
             const uint32_t a_slot = ld_ss(F.ss, a).slot, b_slot = ld_ss(F.ss, b).slot;
             if (!replay) {
-                if (pos < EVW) L.ev[w][pos] = make_uint2(a_slot, b_slot | (kind == 2 ? KIND_LEAVE : 0u));
+                if (pos < EVW) evb[pos] = make_uint2(a_slot, b_slot | (kind == 2 ? KIND_LEAVE : 0u));
             } else if (pos >= EVW) {
                 const uint32_t kidx = kind == 1 ? ne + (uint32_t)__popcll(em & lanemask_lt())
                                                 : nl + (uint32_t)__popcll(lm & lanemask_lt());
@@ -1363,61 +1376,78 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) 
 struct WaveQueue {
     uint32_t qn;
     uint32_t ne, nl;
-    uint32_t drains;  // queue drains forced in the middle of a sweep (DBG_COMBINED_DRAIN)
 };
 
 // Append (a, b) for the lanes with keep set.  Wave-uniform.
-__device__ __forceinline__ void qpush(CombinedLds &L, int w, WaveQueue &Q, bool keep, uint32_t a, uint32_t b) {
+// a_off = A's offset in its block (the block's first frame entry is e0).
+__device__ __forceinline__ void qpush(uint32_t *qb, uint8_t *qa, WaveQueue &Q, bool keep, uint32_t a_off, uint32_t b) {
     const unsigned long long m = __ballot(keep);
     if (keep) {
         const uint32_t i = Q.qn + (uint32_t)__popcll(m & lanemask_lt());
-        L.qb[w][i] = b;
-        L.qa[w][i] = (uint8_t)(a & (uint32_t)(CT - 1));
+        qb[i] = b;
+        qa[i] = (uint8_t)a_off;
     }
     Q.qn += (uint32_t)__popcll(m);
 }
 
-// Cheap filter of candidate b (k = cand[b]: x, z; NaN for a jumper) for lane A.
-// MODE 0: Z strip, 1: X' strip (jumper partners fail the NaN compares), 2:
-// whole window of a jumper A -- a jumper partner is kept unfiltered by the
-// lower frame index (the full test in drain_queue has the window box).
-// Pairs where neither member changed are not filtered here: their relation
-// is unchanged and the full test finds no event.
+// Cheap filter of candidate b (k = cand[b]: x, z, old x, old z; NaN for a
+// jumper) for lane A.  MODE 0: Z strip, 1: X' strip (jumper partners fail
+// the NaN compares), 2: whole window of a jumper A -- a jumper partner is kept
+// unfiltered by the lower frame index (the full test in drain_queue has the
+// window box).
+// The strips also drop a pair whose relation certainly did not change: with
+// both members near, the pair is related at t-1 and at t when its Chebyshev
+// distance is <= D - M both times, and unrelated both times when it is
+// > D + M both times, whichever member owns the window (M covers the float32
+// rounding of the window bounds and of the differences).
 template <int MODE>
-__device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint2 &k, uint32_t b) {
+__device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint4 &k, uint32_t b) {
     const float lo = C.lo, hi = C.hi;
     const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
-    if (MODE == 0) return (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi);
-    if (MODE == 1) return (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
-    const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
-    return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
+    if (MODE == 2) {
+        const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
+        return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
+    }
+    const bool band = MODE == 0 ? (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi)
+                                : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
+    const float dn = fmaxf(fabsf(dx), fabsf(dz));
+    const float dxo = __uint_as_float(k.z) - A.xo, dzo = __uint_as_float(k.w) - A.zo;
+    const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
+    const bool same =
+        ((int)(dn <= C.in_max) & (int)(dold <= C.in_max)) | ((int)(dn > C.out_min) & (int)(dold > C.out_min));
+    return band & !same;
 }
 
 // Sweep candidates [jb, jb + len) of one grid row for every lane (ranges are
 // per lane; the loop runs to the wave maximum mx).  MODE 0: Z strip, 1: X'
-// strip, 2: whole window of a jumper.  U candidates per lane per iteration,
-// all U loads issued before the first is used (one L2 round trip per U).
+// strip, 2: whole window of a jumper.  U candidates (16-B records) per lane
+// per iteration, all U loads issued before the first is used.
 template <int MODE, int U>
 __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, uint32_t jb,
-                                            uint32_t len, uint32_t mx, const uint2 *__restrict__ cand,
+                                            uint32_t len, uint32_t mx, const uint4 *__restrict__ cand,
                                             const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
     for (uint32_t t = 0; t < mx; t += U) {
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
-            ++Q.drains;
+            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);  // LDS; one global add per block
             __builtin_amdgcn_wave_barrier();
-            drain_queue(L, w, Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
+            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
+                        cap, pe, pl, replay);
             Q.qn = 0;
         }
-        uint2 k[U];
+        uint4 k[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) k[u] = cand[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t b = jb + t + (uint32_t)u;
             const bool keep = band_keep<MODE>(A, C, k[u], b) & (t + (uint32_t)u < len);
-            qpush(L, w, Q, keep, A.a, b);
+#ifdef GWAOI_EXP_NOPUSH  // timing experiment only: the filter runs, nothing is queued (events wrong)
+            if (keep && k[u].w == 0x7FFFFFFFu) Q.ne += 1000;
+            continue;
+#endif
+            qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), b);
         }
     }
 }
@@ -1427,7 +1457,7 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
 // The next row's candidate range is loaded while the current one is swept.
 template <int MODE>
 __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int r0,
-                                           int r1, int c0, int c1, const uint2 *__restrict__ cand, const FrameView &F,
+                                           int r1, int c0, int c1, const uint4 *__restrict__ cand, const FrameView &F,
                                            const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
                                            uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
@@ -1450,7 +1480,7 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
         const uint32_t len = je - jb;
         const uint32_t mx = wave_max_u32(len);
         if (MODE != 2 && mx > 2)
-            sweep_range<MODE, SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+            sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
         else if (mx)
             sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
         jb = nb;
@@ -1458,13 +1488,12 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
     }
 }
 
-__device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__restrict__ cand, const FrameView &F,
+__device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
-                               uint32_t &drains, uint2 *out, uint64_t cap, unsigned long long pe,
-                               unsigned long long pl, bool replay) {
+                               uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const int w = threadIdx.x / WAVE;
     const SpaceGrid &g = C.g;
-    WaveQueue Q{0u, ne, nl, 0u};
+    WaveQueue Q{0u, ne, nl};
     const float lo = C.lo, hi = C.hi, M = C.M;
     const bool strip = A.valid && !A.jump && C.band_ok;
     const bool whole = A.valid && (A.jump || !C.band_ok);
@@ -1501,24 +1530,24 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint2 *__re
     }
     if (Q.qn) {
         __builtin_amdgcn_wave_barrier();
-        drain_queue(L, w, Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap, pe, pl, replay);
+        drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out, cap,
+                    pe, pl, replay);
     }
     ne = Q.ne;
     nl = Q.nl;
-    drains += Q.drains;
 }
 
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
 // spaces (small spaces) sweeps once per distinct space among a wave's lanes.
 #ifndef GWAOI_COMBINED_WPE
-#define GWAOI_COMBINED_WPE 0
+#define GWAOI_COMBINED_WPE 6  // waves_per_eu: caps k_combined at 80 VGPRs (6 waves per SIMD; measured 0.141 vs 0.145 ms)
 #endif
 #if GWAOI_COMBINED_WPE
 #define COMBINED_ATTR __attribute__((amdgpu_waves_per_eu(GWAOI_COMBINED_WPE)))
 #else
 #define COMBINED_ATTR
 #endif
-__global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, const uint2 *__restrict__ cand,
+__global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, const uint4 *__restrict__ cand,
                                                  const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
                                                  const TickScalars *__restrict__ sc, unsigned long long *counter,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
@@ -1528,22 +1557,27 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
     const uint32_t e0 = t * CT;
-    if (tid == 0) L.overflow = 0;
+    if (tid == 0) {
+        L.overflow = 0;
+        L.ndrain = 0;
+    }
+    __syncthreads();
 
     LaneA A;
     A.a = e0 + tid;
     A.valid = A.a < F.n;
     const uint32_t ia = A.valid ? A.a : 0u;
-    const uint2 ca = cand[ia];
+    const uint4 ca = cand[ia];
     const Rec16 ra = ld_rec(F.rec, ia);  // exact position (a jumper's candidate record is NaN)
     A.x = ra.x;
     A.z = ra.z;
+    A.xo = __uint_as_float(ca.z);
+    A.zo = __uint_as_float(ca.w);
     A.jump = __uint_as_float(ca.x) != __uint_as_float(ca.x);
     // spaces of the block: first and last entry (frame is space-major)
     const uint32_t my_sp = ld_ss(F.ss, ia).sp;
 
     uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform)
-    uint32_t drains = 0;
     // sweep once per distinct space in this wave (almost always one)
     auto run = [&](bool replay, uint2 *o, unsigned long long pe, unsigned long long pl, uint32_t &e,
                    uint32_t &l) {
@@ -1554,6 +1588,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             const bool mine = A.valid && my_sp == sp;
             pending &= ~__ballot(mine);
             CombinedCtx C;
+            C.dbg = dbg;
             C.g = F.grid[sp];
             C.M = (sc->bmax + 3.0f * C.g.D) * 0x1p-20f;
             C.thr = FAR_FRAC * C.g.D;
@@ -1562,6 +1597,8 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.hi = C.g.D + BW;
             C.lo_in = C.lo > 0.f ? __uint_as_float(__float_as_uint(C.lo) - 1u) : 0.f;
             C.band_ok = C.lo > 0.f;
+            C.in_max = C.g.D - C.M;
+            C.out_min = C.g.D + C.M;
             C.proto.D = C.g.D;
             C.proto.HM = C.hi;
             C.proto.seq_base = seq_base;
@@ -1569,14 +1606,13 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.proto.chg = false;
             LaneA B = A;
             B.valid = mine;
-            combined_sweep(L, B, cand, F, O_rec, C, e, l, drains, o, cap, pe, pl, replay);
+            combined_sweep(L, B, cand, F, O_rec, C, e, l, o, cap, pe, pl, replay);
         }
     };
     run(false, nullptr, 0ull, 0ull, ne, nl);
     if (ln == 0) {
         L.wcnt[w][0] = ne;
         L.wcnt[w][1] = nl;
-        if (drains) atomicAdd(dbg + DBG_COMBINED_DRAIN, drains);
         if (ne + nl > (uint32_t)EVW) atomicAdd(dbg + DBG_COMBINED_REPLAY, 1u);
     }
     // ---- offsets: 2 directed pairs per event; the block's enters, then its leaves
@@ -1593,6 +1629,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         }
         L.te = se;
         L.tl = sl;
+        if (L.ndrain) atomicAdd(dbg + DBG_COMBINED_DRAIN, L.ndrain);
         const uint32_t tot = 2 * (se + sl);
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
         L.base = b;
@@ -1838,7 +1875,7 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 }
 
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
-                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint2 *cand,
+                   const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                    uint32_t n_spaces, void *bbox_parts, hipStream_t st) {
@@ -1863,7 +1900,7 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
                                                     tile_base, tile_off, leave_off, sc->dbg);
 }
 
-void launch_combined(FrameView F, const uint2 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
+void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (!F.n) return;

@@ -85,7 +85,7 @@ struct gwaoi_world {
     gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
     gw::SlotSp *sss = nullptr;
     gw::Rec16 *orec = nullptr;  // previous state in the new frame's order (NaN if absent)
-    uint2 *cand = nullptr;      // combined-pass candidate records of the new frame (x, z; NaN = jumper)
+    uint4 *cand = nullptr;      // combined-pass candidate records of the new frame (x, z, old x, old z; NaN = jumper)
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;

