@@ -219,6 +219,119 @@ def cpu_baseline_spaces(args, target_s: float):
                       f"moving each tick ({sum(done)} Moved calls), sequential XZ-list restatement, {dt:.1f} s"}
 
 
+def cpu_grid_baseline(args, target_s: float):
+    """CPU-grid comparator: the same tick on all host cores --
+    every tick the relation of config 3 recomputed with a cell grid and diffed
+    against the last (oracle/cpu_grid.c, OpenMP).  Untimed populate, then
+    whole ticks until target_s."""
+    from goworld_amd.workload import make_workload
+    from oracle import oracle
+    cores = cpu_cores()
+    wl = make_workload("cfg3", n=args.n)
+    g = oracle.CpuGrid(wl.x, wl.z, wl.D, cores)
+    batches = [wl.tick(t) for t in range(3)]
+    done, ev, t = 0, 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < target_s or t == 0:
+        sl, nx, nz = batches[t % len(batches)] if t < len(batches) else wl.tick(t)
+        ne, nl = g.tick(sl, nx, nz)
+        done += sl.size
+        ev += ne + nl
+        t += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "entity-moves/s", "ms_per_tick": dt / t * 1e3, "events_per_s": ev / dt,
+            "cores": cores, "kind": "port",
+            "sample": f"{t} whole cfg3 ticks ({wl.n} entities, every entity moving), relation recomputed on a cell "
+                      f"grid and diffed per tick on {cores} threads, {dt:.1f} s"}
+
+
+def host_tick_bench(ticks: int, threads: int):
+    """The C++ host tick (tools/tick_bench.cpp, built in-tree): cfg3 from host
+    arrays through gwaoi_moved_batch to events in pinned host memory, serial and
+    pipelined (gwaoi_tick_begin/_end), plus the callback replay into per-entity
+    InterestedIn / InterestedBy sets (Entity.go:236-246) on 1 and T threads."""
+    import subprocess
+    exe = os.path.join(ROOT, "goworld_amd", "lib", "gwaoi_tick_bench")
+    if not os.path.exists(exe):
+        return {"error": "gwaoi_tick_bench not built"}
+    r = subprocess.run([exe, str(ticks), str(threads)], capture_output=True, text=True, timeout=300)
+    try:
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception:
+        return {"error": (r.stderr or r.stdout)[-500:]}
+
+
+def cfg4_leg(args, ws, rank, device, dist, red_dev):
+    """Config 4 as a strong-scaling sub-record of every line: 8192 independent
+    spaces x 2000 entities in total, sharded over the ranks in contiguous
+    blocks balanced by entity count (goworld_amd.shard.assign_spaces), one
+    world per rank covering all of its spaces with one launch sequence.  Move
+    batches (every entity, U(-1,1), random call order) are generated on the
+    GPU before timing; value = all ranks' moves / max time over ranks."""
+    import torch
+    from goworld_amd import World
+    from goworld_amd.shard import assign_spaces, reduce_over_ranks
+    per, total = 2000, args.cfg4_spaces
+    lo, hi = assign_spaces([per] * total, ws)[rank]
+    ns = max(0, hi - lo)
+    n = ns * per
+    L = float(np.sqrt(per * 1250.0))
+    dev = torch.device(f"cuda:{device}")
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0004 + lo)
+    t_setup = time.perf_counter()
+    ticks = args.cfg4_warmup + args.cfg4_steps
+    x = (torch.rand(n, generator=g, device=dev, dtype=torch.float64) * L - L / 2).to(torch.float32)
+    z = (torch.rand(n, generator=g, device=dev, dtype=torch.float64) * L - L / 2).to(torch.float32)
+    batches = []
+    for _ in range(ticks):
+        order = torch.randperm(n, generator=g, device=dev).to(torch.int32)
+        x = x + (2 * torch.rand(n, generator=g, device=dev, dtype=torch.float64) - 1).to(torch.float32)
+        z = z + (2 * torch.rand(n, generator=g, device=dev, dtype=torch.float64) - 1).to(torch.float32)
+        batches.append((order, x[order.long()].contiguous(), z[order.long()].contiguous()))
+    x0h = batches[0][1].new_empty(n)
+    x0h[batches[0][0].long()] = batches[0][1]
+    z0h = batches[0][2].new_empty(n)
+    z0h[batches[0][0].long()] = batches[0][2]
+    x0h, z0h = x0h.cpu().numpy(), z0h.cpu().numpy()
+    torch.cuda.synchronize(dev)
+    w = World(max(n, 1), max_spaces=max(ns, 1), device=device)
+    sp = [w.space_create(100.0) for _ in range(ns)]
+    slots = np.arange(n, dtype=np.uint32)
+    for k in range(ns):
+        a, b = k * per, (k + 1) * per
+        w.enter_batch(sp[k], slots[a:b], x0h[a:b], z0h[a:b])
+    w.tick_device()  # populate at batch 0's positions
+    setup_s = time.perf_counter() - t_setup
+    ptrs = [(o.data_ptr(), bx.data_ptr(), bz.data_ptr()) for o, bx, bz in batches]
+    for t in range(1, args.cfg4_warmup):
+        w.moved_batch_device(*ptrs[t], n)
+        w.tick_device()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    w.sync()
+    ev = 0
+    t0 = time.perf_counter()
+    for t in range(max(1, args.cfg4_warmup), ticks):
+        w.moved_batch_device(*ptrs[t], n)
+        ne, nl = w.tick_device()
+        ev += ne + nl
+    w.sync()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    steps = ticks - max(1, args.cfg4_warmup)
+    el_max, (moves_all, ev_all) = reduce_over_ranks(dist, el, [n * steps, ev], red_dev)
+    w.close()
+    return {"metric": "AOI entity-moves/sec, config 4 (strong scaling: fixed total work over the ranks)",
+            "value": moves_all / el_max, "unit": "entity-moves/s", "ms_per_step": el_max / steps * 1e3,
+            "steps": steps, "n_gpus": ws, "scaling": "strong", "events_per_s": ev_all / el_max,
+            "spaces_total": total, "entities_total": total * per, "entities_rank0": n, "setup_s_rank0": round(setup_s, 2),
+            "data": "synthetic (torch Philox on the GPU, generated before timing, resident in HBM)"}
+
+
 def cpu_baseline(args, wl_factory, target_s: float):
     """go-aoi XZListAOIManager restatement (oracle/xzlist.c), one core, timed on
     a prefix of tick 0's move batch of the same workload (cfg4: one space per
@@ -391,7 +504,14 @@ def main():
     ap.add_argument("--sync-clients", type=float, default=0.5,
                     help="fraction of entities with a client (players) in the sync leg")
     ap.add_argument("--host-io-steps", type=int, default=10,
-                    help="extra ticks timed with host move batches in and host event arrays out (PCIe-inclusive)")
+                    help="extra ticks timed with host move batches in and host event arrays out (PCIe-inclusive), "
+                         "serial and pipelined")
+    ap.add_argument("--host-tick-steps", type=int, default=10,
+                    help="ticks of the C++ host tick bench (tools/tick_bench.cpp; 0 = off)")
+    ap.add_argument("--cfg4-steps", type=int, default=5,
+                    help="cfg3 runs: timed ticks of the config-4 strong-scaling sub-record (0 = off)")
+    ap.add_argument("--cfg4-warmup", type=int, default=2)
+    ap.add_argument("--cfg4-spaces", type=int, default=8192)
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -440,7 +560,7 @@ def main():
         sl, nx, nz = wl.tick(t)
         batches.append((sl, nx, nz))
     # PCIe-inclusive leg (host memory): one untimed warmup tick (allocates the pinned staging) + hio timed
-    host_batches = [wl.tick(ticks + t) for t in range(hio + 1 if hio else 0)]
+    host_batches = [wl.tick(ticks + t) for t in range(2 * hio + 2 if hio else 0)]
     sync_steps = max(0, args.sync_steps) if ws == 1 or args.workload != "cfg4" else 0
     sync_batches = [wl.tick(ticks + len(host_batches) + t) for t in range(sync_steps + 1 if sync_steps else 0)]
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
@@ -522,32 +642,58 @@ def main():
         stages = w.stage_times()
         w.set_stage_timing([])
 
-    # ---- PCIe-inclusive leg: host move arrays -> H2D -> tick -> events D2H into host arrays
+    # ---- PCIe-inclusive leg (SURVEY.md §8d's tick): host move arrays -> validation + pinned staging + H2D
+    # -> flush -> events in pinned host memory (views, no copy).  Serial: per-tick latency.  Pipelined:
+    # gwaoi_tick_begin(t), the host batch of t+1 staged while the GPU runs t, gwaoi_tick_end(t).
     host_io = None
     if hio:
         w.moved_batch(*host_batches[0])  # warmup: sizes the pinned staging and host event buffers
-        w.tick()
+        w.tick(copy=False)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
-        h_ev = 0
+        h_ev, s_lat = 0, []
         h0 = time.perf_counter()
-        for sl, nx, nz in host_batches[1:]:
+        for sl, nx, nz in host_batches[1:hio + 1]:
+            a = time.perf_counter()
             w.moved_batch(sl, nx, nz)
-            ent, lev = w.tick()
+            ent, lev = w.tick(copy=False)
+            s_lat.append(time.perf_counter() - a)
             h_ev += len(ent) + len(lev)
+        s_el = time.perf_counter() - h0
+        pb = host_batches[hio + 1:]
+        p_lat = []
+        w.moved_batch(*pb[0])
+        p0 = issue = time.perf_counter()
+        for k in range(len(pb)):
+            w.tick_begin()
+            nxt = time.perf_counter()
+            if k + 1 < len(pb):
+                w.moved_batch(*pb[k + 1])  # staged while the flush of tick k runs
+            ent, lev = w.tick_end(copy=False)
+            p_lat.append(time.perf_counter() - issue)
+            issue = nxt
+        p_el = time.perf_counter() - p0
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        h_el = time.perf_counter() - h0
-        h_el, (h_moves, h_evs) = reduce_over_ranks(dist, h_el, [sum(b[0].size for b in host_batches[1:]), h_ev],
-                                                   red_dev)
-        host_io = {"value": h_moves / h_el, "unit": "entity-moves/s", "ms_per_step": h_el / hio * 1e3,
-                   "events_per_s": h_evs / h_el, "steps": hio,
-                   "note": "moves from host memory (H2D) + events copied to host arrays (D2H) per tick, after "
-                           "one untimed warmup tick; not the headline value"}
+        p_el, (h_moves, h_evs) = reduce_over_ranks(dist, p_el, [sum(b[0].size for b in pb), h_ev], red_dev)
+        sl_ms, pl_ms = np.array(s_lat) * 1e3, np.array(p_lat) * 1e3
+        host_io = {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
+                   "p50_tick_ms": float(np.percentile(pl_ms, 50)), "p99_tick_ms": float(np.percentile(pl_ms, 99)),
+                   "steps": len(pb),
+                   "serial": {"ms_per_step": s_el / hio * 1e3, "p50_tick_ms": float(np.percentile(sl_ms, 50)),
+                              "p99_tick_ms": float(np.percentile(sl_ms, 99)), "steps": hio,
+                              "events_per_s": h_evs / max(s_el, 1e-9)},
+                   "note": "pipelined: the moved_batch of tick t+1 (validation, pinned staging, H2D on a copy "
+                           "stream) overlaps the flush of tick t; p50/p99 = from the batch call to the events in "
+                           "pinned host memory; serial = moved_batch + tick back to back. Not the headline value"}
     sync = sync_leg(w, n, sync_batches, args.sync_clients) if sync_batches else None
     elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], red_dev)
+    w.close()
+    cfg4 = None
+    if args.workload == "cfg3" and args.cfg4_steps > 0:
+        cfg4 = cfg4_leg(args, ws, rank, device, dist, red_dev)
 
     if rank == 0:
         lat_ms = np.array(lat) * 1e3
@@ -579,6 +725,14 @@ def main():
                 cpu = cpu_baseline(args, wl_factory, args.cpu_seconds)
             except Exception as e:  # the baseline must not take the GPU number down with it
                 cpu = {"error": repr(e)}
+            if args.workload == "cfg3" and ws == 1 and isinstance(cpu, dict):
+                try:
+                    cpu["cpu_grid"] = cpu_grid_baseline(args, args.cpu_seconds)
+                except Exception as e:
+                    cpu["cpu_grid"] = {"error": repr(e)}
+        host_tick = None
+        if args.workload == "cfg3" and ws == 1 and args.host_tick_steps > 0 and not args.n:
+            host_tick = host_tick_bench(args.host_tick_steps, cpu_cores())
         out = {
             "metric": METRIC,
             "value": moves_all / elapsed_max,
@@ -612,11 +766,12 @@ def main():
             "stages_note": f"separate {bd} ticks after the timed region, every stage bracketed by HIP events "
                            "(the events add ~0.07 ms per tick, so these sum above ms_per_step)",
             "cpu_baseline": cpu,
+            "host_tick": host_tick,
+            "cfg4_strong": cfg4,
         }
         if cpu and "value" in cpu:
             out["speedup_vs_cpu"] = out["value"] / ws / cpu["value"]
         print(json.dumps(out), flush=True)
-    w.close()
     if dist is not None:
         dist.destroy_process_group()
 

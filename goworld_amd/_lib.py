@@ -34,7 +34,8 @@ EXPORTS = [
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
-    "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters",
+    "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
+    "gwaoi_tick_end_device",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -131,6 +132,9 @@ def load():
         "gwaoi_moved_batch_device": ([vp, vp, vp, vp, sz], C.c_int),
         "gwaoi_tick": ([vp, P(Events)], C.c_int),
         "gwaoi_tick_device": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_tick_begin": ([vp], C.c_int),
+        "gwaoi_tick_end": ([vp, P(Events)], C.c_int),
+        "gwaoi_tick_end_device": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_neighbors": ([vp, u32, vp, sz, P(sz)], C.c_int),
         "gwaoi_world_info": ([vp, P(Info)], C.c_int),
@@ -270,17 +274,36 @@ class World:
                                                              C.c_void_p(d_z), C.c_void_p(d_seq), n))
 
     # ---- flush
-    def tick(self):
+    def tick(self, copy: bool = True):
         """Flush; returns (enter_pairs, leave_pairs) as (n,2) uint32 arrays [a, b].
 
         When the flush committed but the device reported a problem in the queued
         ops (a dropped move: ESTATE / ENONFINITE / EINVAL), the GwaoiError carries
-        the flush's events as ``.events``: they must still be replayed."""
+        the flush's events as ``.events``: they must still be replayed.
+        copy=False: views of the world's pinned buffer, valid until the next flush."""
         ev = Events()
-        rc = self._L.gwaoi_tick(self._w, C.byref(ev))
+        return self._events(self._L.gwaoi_tick(self._w, C.byref(ev)), ev, copy)
+
+    def tick_begin(self):
+        """Start the flush (gwaoi_tick_begin); AOIManager calls made before tick_end
+        are queued for the next flush."""
+        self._check(self._L.gwaoi_tick_begin(self._w))
+
+    def tick_end(self, copy: bool = True):
+        """Finish the flush started by tick_begin: (enter_pairs, leave_pairs) as tick()."""
+        ev = Events()
+        return self._events(self._L.gwaoi_tick_end(self._w, C.byref(ev)), ev, copy)
+
+    def tick_end_device(self):
+        ne, nl = C.c_uint64(), C.c_uint64()
+        self._check(self._L.gwaoi_tick_end_device(self._w, C.byref(ne), C.byref(nl)))
+        return ne.value, nl.value
+
+    def _events(self, rc, ev, copy):
         ne, nl = ev.n_enter, ev.n_leave
-        ent = np.ctypeslib.as_array(ev.enter, shape=(2 * ne,)).reshape(ne, 2).copy() if ne else np.empty((0, 2), np.uint32)
-        lev = np.ctypeslib.as_array(ev.leave, shape=(2 * nl,)).reshape(nl, 2).copy() if nl else np.empty((0, 2), np.uint32)
+        cp = (lambda a: a.copy()) if copy else (lambda a: a)
+        ent = cp(np.ctypeslib.as_array(ev.enter, shape=(2 * ne,)).reshape(ne, 2)) if ne else np.empty((0, 2), np.uint32)
+        lev = cp(np.ctypeslib.as_array(ev.leave, shape=(2 * nl,)).reshape(nl, 2)) if nl else np.empty((0, 2), np.uint32)
         if rc != 0:
             try:
                 self._check(rc)

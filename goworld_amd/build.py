@@ -67,6 +67,28 @@ def build_cpp_tests(force: bool = False, verbose: bool = False) -> str:
     return CPP_TEST_OUT
 
 
+TICK_BENCH_SRC = os.path.join(ROOT, "tools", "tick_bench.cpp")
+TICK_BENCH_OUT = os.path.join(HERE, "lib", "gwaoi_tick_bench")
+
+
+def build_tick_bench(force: bool = False, verbose: bool = False) -> str:
+    """C++ host tick bench (tools/tick_bench.cpp): the cgo-like end-to-end tick + callback replay."""
+    lib = build(force=force, verbose=verbose)
+    deps = [TICK_BENCH_SRC, lib, os.path.join(ROOT, "include", "gwaoi.h")]
+    if (not force and os.path.exists(TICK_BENCH_OUT)
+            and all(os.path.getmtime(d) <= os.path.getmtime(TICK_BENCH_OUT) for d in deps)):
+        return TICK_BENCH_OUT
+    tmp = TICK_BENCH_OUT + ".tmp"
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"), TICK_BENCH_SRC,
+           "-o", tmp, "-L", os.path.dirname(lib), "-lgwaoi", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, TICK_BENCH_OUT)
+    return TICK_BENCH_OUT
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
     print(build_cpp_tests(verbose=True))
+    print(build_tick_bench(verbose=True))

@@ -232,7 +232,8 @@ struct WorldView {
     const SlotInfo *info;  // per slot: .rank = index in F for slots in F
     hipStream_t st;
     uint32_t max_slots;
-    size_t pending_ops;     // calls queued since the last flush
+    size_t pending_ops;     // calls queued since the last flush (or a flush in flight)
+    bool in_flight;         // gwaoi_tick_begin without its gwaoi_tick_end yet
     const uint32_t *events; // last flush's events (device): [enters | leaves] as (a,b) pairs
     uint64_t n_enter, n_leave;
 };

@@ -922,6 +922,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     if (on_device && (reinterpret_cast<uintptr_t>(payload) & 15u)) return GWAOI_EINVAL;
     SyncState *S;
     if (int rc = state(w, &S)) return rc;
+    if (world_view(w).in_flight) return GWAOI_ESTATE;  // a flush in flight reads the sync state's stream
     if (!n) return GWAOI_OK;
     if (n > 0x7FFFFFFFull) return GWAOI_EINVAL;
     // arena of the current flush (older chunks were consumed by earlier flushes)

@@ -16,6 +16,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -67,6 +70,86 @@ struct Run {  // a stretch of the op queue: host ops [hbegin, hend) or a device 
     const uint32_t *dsp;             // explicit space per op (nullptr: keep the slot's space)
     uint64_t seq0;
     size_t dn;
+};
+
+// Persistent host threads for the validation + staging of big move batches
+// (a thread start per call costs ~20 us each; a tick stages 1M moves).
+class StagePool {
+  public:
+    ~StagePool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread &t : th_) t.join();
+    }
+    // f(0) .. f(T-1), f(0) on the calling thread.  Falls back to running on the
+    // caller when threads cannot be started.
+    void run(unsigned T, const std::function<void(unsigned)> &f) {
+        while (th_.size() + 1 < T) {
+            try {
+                const unsigned id = (unsigned)th_.size() + 1;
+                th_.emplace_back([this, id] { loop(id); });
+            } catch (...) {
+                break;
+            }
+        }
+        const unsigned Tw = std::min<unsigned>(T, (unsigned)th_.size() + 1);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &f;
+            T_ = Tw;
+            left_ = Tw - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        for (unsigned t = Tw; t < T; ++t) f(t);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)> *job;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= T_) continue;
+                job = job_;
+            }
+            (*job)(id);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)> *job_ = nullptr;
+    unsigned T_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// A call made while a flush is in flight (gwaoi_tick_begin .. _end): validated
+// and given its seq at call time, queued for the next flush at the commit.
+struct Deferred {
+    enum Kind : uint8_t { MOVED, ENTER, LEAVE, RUN } kind;
+    uint32_t slot, space;
+    float x, z;
+    uint64_t seq;
+    Run run;  // RUN: a staged or device batch
+};
+struct DeferredBox {  // Enter/Moved positions of a deferred staged batch, per space
+    uint32_t space;
+    float x0, z0, x1, z1;
 };
 
 }  // namespace
@@ -138,18 +221,38 @@ struct gwaoi_world {
     std::vector<Run> runs;
     size_t n_ops = 0;
     // host move batches (gwaoi_moved_batch) staged as [slots | x | z | space] in pinned memory and sent
-    // with one async H2D each; they then run as device batches.  Words in use until the flush.
-    uint32_t *h_stage = nullptr, *d_stage = nullptr;
-    size_t stage_cap = 0, stage_used = 0;
+    // with one async H2D each (copy stream); they then run as device batches.  Two halves: the calls
+    // queued while a flush is in flight stage into the half that flush does not read.
+    uint32_t *h_stage[2] = {nullptr, nullptr}, *d_stage[2] = {nullptr, nullptr};
+    size_t stage_cap[2] = {0, 0}, stage_used[2] = {0, 0};
+    int stage_cur = 0;
+    hipStream_t copy_st = nullptr;  // staging H2D copies
+    hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
+    bool copy_pending = false;      // the flush must wait for copy_ev
+    StagePool pool;
     std::vector<uint32_t> new_slots;
     std::vector<uint32_t> touched;  // slots whose liveness changed since the last flush
     // seq_next: the seq the next implicit call gets (advanced at queue time);
     // seq_floor: seq_next at the last flush = lower bound of this flush's seqs.
     uint64_t seq_next = 1, seq_floor = 1;
+    bool space_ops_queued = false;  // an Enter or Leave is queued for the next flush
     bool dev_seq_pending = false;  // an explicit-seq device batch is queued (its max is known after the flush)
     uint32_t tick_id = 0;
     uint64_t ticks = 0;
     uint32_t n_alive = 0;
+    // ---- flush in flight (gwaoi_tick_begin -> gwaoi_tick_end).  The op queue (runs, host op
+    // arrays, new_slots, touched) stays frozen until the commit: calls made meanwhile are
+    // deferred, then queued for the next flush.
+    bool in_flight = false;
+    struct {
+        uint32_t tick_id;
+        size_t entries;
+        uint64_t seq_next;  // seq_next when the flush's queue was closed (the next flush's floor)
+        bool dev_seq;       // it held an explicit-seq device batch
+        std::vector<uint8_t> touched_alive;  // liveness of touched[i] when the queue was closed
+    } fl;
+    std::vector<Deferred> deferred;
+    std::vector<DeferredBox> deferred_boxes;
     uint64_t last_n_enter = 0, last_n_leave = 0;
     gwaoi_debug dbg{};  // rare-path counters, accumulated over flushes
 
@@ -388,6 +491,52 @@ void mark_appended(gwaoi_world *w, uint32_t slot) {
     }
 }
 
+// Queue the calls deferred while a flush was in flight, in call order, as if
+// they had been made now (their seqs were taken at call time).
+void replay_deferred(gwaoi_world *w) {
+    for (const Deferred &q : w->deferred) {
+        switch (q.kind) {
+            case Deferred::ENTER:
+                note_pending_bbox(w->spaces[q.space], q.x, q.z);
+                mark_appended(w, q.slot);
+                w->touched.push_back(q.slot);
+                push_host_op(w, q.slot, q.x, q.z, q.space, q.seq);
+                w->space_ops_queued = true;
+                break;
+            case Deferred::LEAVE:
+                w->touched.push_back(q.slot);
+                push_host_op(w, q.slot, 0.f, 0.f, gw::SP_DEAD, q.seq);
+                w->space_ops_queued = true;
+                break;
+            case Deferred::MOVED:
+                note_pending_bbox(w->spaces[q.space], q.x, q.z);
+                push_host_op(w, q.slot, q.x, q.z, q.space, q.seq);
+                break;
+            case Deferred::RUN:
+                w->runs.push_back(q.run);
+                w->n_ops += q.run.dn;
+                break;
+        }
+    }
+    for (const DeferredBox &b : w->deferred_boxes) {
+        note_pending_bbox(w->spaces[b.space], b.x0, b.z0);
+        note_pending_bbox(w->spaces[b.space], b.x1, b.z1);
+    }
+    w->deferred.clear();
+    w->deferred_boxes.clear();
+}
+
+void defer(gwaoi_world *w, Deferred::Kind k, uint32_t slot, uint32_t space, float x, float z, uint64_t seq) {
+    Deferred q{};
+    q.kind = k;
+    q.slot = slot;
+    q.space = space;
+    q.x = x;
+    q.z = z;
+    q.seq = seq;
+    w->deferred.push_back(q);
+}
+
 float o2f(int i) {
     int b = i ^ ((i >> 31) & 0x7FFFFFFF);
     float f;
@@ -527,13 +676,14 @@ int poison(gwaoi_world *w, int rc) {
     return rc;
 }
 
-// The flush.  On return the events of this tick are in w->events (device).
-// *committed: the new frame became the world's state (the events are valid
-// and must be delivered, even when the returned status reports a problem the
-// device found in the queued ops).  A failure after the device kernels have
-// rewritten the per-slot records but before the commit poisons the world.
-int run_tick(gwaoi_world *w, bool *committed) {
-    *committed = false;
+void replay_deferred(gwaoi_world *w);
+
+// The flush, first half: close the op queue and launch the whole pipeline on
+// the world's stream, ending with the D2H of the flush's summary (TickOut);
+// returns without waiting.  Calls made until tick_finish are deferred (see
+// Deferred).  A failure before any kernel was queued returns with nothing in
+// flight.
+int tick_launch(gwaoi_world *w) {
     hipStream_t st = w->stream;
     int rc;
     const uint32_t tick_id = ++w->tick_id;
@@ -550,6 +700,7 @@ int run_tick(gwaoi_world *w, bool *committed) {
     // grid for this flush
     uint32_t total_cells = 0, total_rows = 0;
     choose_grids(w, total_cells, total_rows);
+    for (uint32_t s = 0; s < w->n_space_ids; ++s) w->spaces[s].pend = false;  // consumed by this grid
     const size_t entries = 2 * ((size_t)gw::combined_blocks(n_new) + gw::combined_blocks(n_prev));
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
@@ -572,6 +723,11 @@ int run_tick(gwaoi_world *w, bool *committed) {
     if (!grid_same) {
         HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * ns, hipMemcpyHostToDevice, st));
         Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
+    }
+    // the staged move batches' H2D copies (copy stream) land before the flush reads them
+    if (w->copy_pending) {
+        HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
+        w->copy_pending = false;
     }
     // counters, tile totals, bbox fold; S' <- the previous frame (the ops apply onto it)
     if (incr)
@@ -698,7 +854,52 @@ int run_tick(gwaoi_world *w, bool *committed) {
     }
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
     if (hipMemcpyAsync(w->h_out, w->dev_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        wait_stream(w) != GWAOI_OK) {
+        (w->done_ev && hipEventRecord(w->done_ev, st) != hipSuccess)) {
+        w->last_error = "flush summary copy failed";
+        return poison(w, GWAOI_EDEVICE);
+    }
+    // the queue is closed: what the commit needs of it
+    w->in_flight = true;
+    w->fl.tick_id = tick_id;
+    w->fl.entries = entries;
+    w->fl.seq_next = w->seq_next;
+    w->fl.dev_seq = w->dev_seq_pending;
+    w->fl.touched_alive.resize(w->touched.size());
+    for (size_t i = 0; i < w->touched.size(); ++i) w->fl.touched_alive[i] = w->alive[w->touched[i]];
+    w->stage_cur ^= 1;  // calls made in flight stage into the other half (free: its flush has ended)
+    w->stage_used[w->stage_cur] = 0;
+    w->space_ops_queued = false;
+    return GWAOI_OK;
+}
+
+// Wait for the flush's summary: blocks on an event (GWAOI_BLOCKING_SYNC=1) or polls it.
+int wait_done(gwaoi_world *w) {
+    if (w->blocking_sync) {
+        HIP_TRY(hipEventSynchronize(w->done_ev));
+        return GWAOI_OK;
+    }
+    hipError_t e;
+    while ((e = hipEventQuery(w->done_ev)) == hipErrorNotReady) __builtin_ia32_pause();
+    HIP_TRY(e);
+    return GWAOI_OK;
+}
+
+// The flush, second half: wait for the summary, grow the event buffer and re-run
+// the pair passes if needed, commit the new frame and queue the deferred calls
+// for the next flush.  On return the events are in w->events (device).
+// *committed: the new frame became the world's state (the events are valid and
+// must be delivered, even when the returned status reports a problem the device
+// found in the queued ops).  A failure after the device kernels have rewritten
+// the per-slot records but before the commit poisons the world.
+int tick_finish(gwaoi_world *w, bool *committed) {
+    *committed = false;
+    hipStream_t st = w->stream;
+    int rc;
+    DevFrame &P = w->fr[w->cur];
+    DevFrame &Fn = w->fr[w->cur ^ 1];
+    const uint64_t seq_base = w->seq_floor;
+    const size_t entries = w->fl.entries;
+    if (wait_done(w) != GWAOI_OK) {
         w->last_error = "flush did not complete: " + w->last_error;
         return poison(w, GWAOI_EDEVICE);
     }
@@ -740,7 +941,6 @@ int run_tick(gwaoi_world *w, bool *committed) {
     const int4 *bb = tick_bbox(w);
     for (uint32_t s = 0; s < w->n_space_ids; ++s) {
         SpaceHost &S = w->spaces[s];
-        S.pend = false;
         if (S.used && S.alive && bb[s].x != 0x7FFFFFFF) {
             S.have_bbox = true;
             S.bx0 = o2f(bb[s].x);
@@ -753,7 +953,7 @@ int run_tick(gwaoi_world *w, bool *committed) {
     }
     for (uint32_t s : w->new_slots) w->appended[s] = 0;
     w->new_slots.clear();
-    for (uint32_t s : w->touched) w->in_frame[s] = w->alive[s];
+    for (size_t i = 0; i < w->touched.size(); ++i) w->in_frame[w->touched[i]] = w->fl.touched_alive[i];
     w->touched.clear();
     w->h_op_slot.clear();
     w->h_op_x.clear();
@@ -762,13 +962,14 @@ int run_tick(gwaoi_world *w, bool *committed) {
     w->h_op_seq.clear();
     w->runs.clear();
     w->n_ops = 0;
-    w->stage_used = 0;  // the flush synchronised the stream: every staged H2D has landed
-    if (w->dev_seq_pending && r.seq_max >= w->seq_next) w->seq_next = r.seq_max + 1;
+    if (w->fl.dev_seq && r.seq_max >= w->seq_next) w->seq_next = r.seq_max + 1;  // no call was made in flight
     w->dev_seq_pending = false;
-    w->seq_floor = w->seq_next;
+    w->seq_floor = w->fl.dev_seq ? w->seq_next : w->fl.seq_next;
     w->cur ^= 1;
     w->ticks++;
+    w->in_flight = false;
     *committed = true;
+    replay_deferred(w);
     // problems the device found in the queued ops: the frame is committed (the offending ops were
     // dropped), so the flush's events are valid and the caller still receives them
     if (r.err & gw::ERR_COUNT_MISMATCH) {
@@ -820,6 +1021,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
+    if (w->copy_st) (void)hipStreamSynchronize(w->copy_st);
     if (w->sync) gw::sync_destroy(w->sync);
     w->sync = nullptr;
     for (DevFrame &f : w->fr) {
@@ -836,8 +1038,12 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->h_out) (void)hipHostFree(w->h_out);
     if (w->h_events) (void)hipHostFree(w->h_events);
     if (w->h_grid) (void)hipHostFree(w->h_grid);
-    if (w->h_stage) (void)hipHostFree(w->h_stage);
-    dfree(w->d_stage);
+    for (int h = 0; h < 2; ++h) {
+        if (w->h_stage[h]) (void)hipHostFree(w->h_stage[h]);
+        dfree(w->d_stage[h]);
+    }
+    if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
+    if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
     for (int s = 0; s < ST_N; ++s)
         for (int q = 0; q < 2; ++q)
             if (w->ev[s][q]) (void)hipEventDestroy(w->ev[s][q]);
@@ -880,6 +1086,14 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     }
     if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
         w->stream = nullptr;
+        return fail(GWAOI_EDEVICE);
+    }
+    if (hipStreamCreateWithFlags(&w->copy_st, hipStreamNonBlocking) != hipSuccess) {
+        w->copy_st = nullptr;
+        return fail(GWAOI_EDEVICE);
+    }
+    if (hipEventCreateWithFlags(&w->copy_ev, hipEventDisableTiming) != hipSuccess) {
+        w->copy_ev = nullptr;
         return fail(GWAOI_EDEVICE);
     }
     const size_t N = w->max_slots;
@@ -989,10 +1203,16 @@ int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, 
     if (w->sync) gw::sync_note_slot(w->sync, slot, space);
     SpaceHost &S = w->spaces[space];
     S.alive++;
+    const uint64_t sq = take_seq(w, seq);
+    w->space_ops_queued = true;
+    if (w->in_flight) {
+        defer(w, Deferred::ENTER, slot, space, x, z, sq);
+        return GWAOI_OK;
+    }
     note_pending_bbox(S, x, z);
     mark_appended(w, slot);
     w->touched.push_back(slot);
-    push_host_op(w, slot, x, z, space, take_seq(w, seq));
+    push_host_op(w, slot, x, z, space, sq);
     return GWAOI_OK;
 }
 
@@ -1003,8 +1223,13 @@ int moved_impl(gwaoi_world *w, uint32_t slot, float x, float z, const uint64_t *
     if (!w->alive[slot]) return GWAOI_ESTATE;
     if (!finite2(x, z)) return GWAOI_ENONFINITE;
     if (int rc = check_seq(w, seq)) return rc;
+    const uint64_t sq = take_seq(w, seq);
+    if (w->in_flight) {
+        defer(w, Deferred::MOVED, slot, w->space_of[slot], x, z, sq);
+        return GWAOI_OK;
+    }
     note_pending_bbox(w->spaces[w->space_of[slot]], x, z);
-    push_host_op(w, slot, x, z, w->space_of[slot], take_seq(w, seq));
+    push_host_op(w, slot, x, z, w->space_of[slot], sq);
     return GWAOI_OK;
 }
 
@@ -1013,16 +1238,18 @@ constexpr size_t kStageMinBatch = 64;  // smaller host batches queue as host ops
 // Room for `words` more staged words.  1: no room without moving a buffer that a queued
 // batch still points into (the caller then queues the batch as host ops).
 int ensure_stage(gwaoi_world *w, size_t words) {
-    if (w->stage_used + words <= w->stage_cap) return GWAOI_OK;
-    if (w->stage_used) return 1;
-    const size_t cap = std::max<size_t>({words, 2 * w->stage_cap, (size_t)4 << 16});
-    if (w->h_stage) (void)hipHostFree(w->h_stage);
-    w->h_stage = nullptr;
-    dfree(w->d_stage);
-    w->stage_cap = 0;
-    HIP_TRY(hipHostMalloc((void **)&w->h_stage, cap * sizeof(uint32_t), hipHostMallocDefault));
-    if (int rc = dalloc(w, &w->d_stage, cap)) return rc;
-    w->stage_cap = cap;
+    const int h = w->stage_cur;
+    if (w->stage_used[h] + words <= w->stage_cap[h]) return GWAOI_OK;
+    if (w->stage_used[h]) return 1;
+    const size_t cap = std::max<size_t>({words, 2 * w->stage_cap[h], (size_t)4 << 16});
+    HIP_TRY(hipStreamSynchronize(w->copy_st));  // no staging copy may still read the old buffer
+    if (w->h_stage[h]) (void)hipHostFree(w->h_stage[h]);
+    w->h_stage[h] = nullptr;
+    dfree(w->d_stage[h]);
+    w->stage_cap[h] = 0;
+    HIP_TRY(hipHostMalloc((void **)&w->h_stage[h], cap * sizeof(uint32_t), hipHostMallocDefault));
+    if (int rc = dalloc(w, &w->d_stage[h], cap)) return rc;
+    w->stage_cap[h] = cap;
     return GWAOI_OK;
 }
 
@@ -1035,7 +1262,7 @@ struct StageBox {  // positions of one space seen by one staging chunk
 // into the staging words h = [slots | x | z | space] (n each).  Returns the first bad index (hi if
 // none) with its status in *st; boxes[space] gathers the chunk's positions.
 size_t stage_chunk(const gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n,
-                   size_t lo, size_t hi, uint32_t *h, StageBox *boxes, int *st) {
+                   size_t lo, size_t hi, uint32_t *h, bool with_space, StageBox *boxes, int *st) {
     uint32_t *hs = h, *hsp = h + 3 * n;
     float *hx = reinterpret_cast<float *>(h + n), *hz = reinterpret_cast<float *>(h + 2 * n);
     const uint8_t *alive = w->alive.data();
@@ -1047,7 +1274,8 @@ size_t stage_chunk(const gwaoi_world *w, const uint32_t *slots, const float *x, 
         if (!alive[sl]) { *st = GWAOI_ESTATE; return i; }
         if (!finite2(xi, zi)) { *st = GWAOI_ENONFINITE; return i; }
         const uint32_t sp = space_of[sl];
-        hs[i] = sl; hx[i] = xi; hz[i] = zi; hsp[i] = sp;
+        hs[i] = sl; hx[i] = xi; hz[i] = zi;
+        if (with_space) hsp[i] = sp;
         StageBox &b = boxes[sp];
         if (!b.any) {
             b = StageBox{xi, zi, xi, zi, true};
@@ -1068,59 +1296,59 @@ constexpr size_t kStageThreadMin = 1 << 17;  // moves per extra thread
 constexpr unsigned kStageThreads = 8;
 
 int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
-    uint32_t *h = w->h_stage + w->stage_used, *d = w->d_stage + w->stage_used;
+    const int half = w->stage_cur;
+    // the space column is needed only when an Enter/Leave of this flush precedes the batch (a slot
+    // that entered in this flush must move in its new space); otherwise every slot keeps its space
+    const bool with_space = w->space_ops_queued;
+    const size_t words = (with_space ? 4 : 3) * n;
+    uint32_t *h = w->h_stage[half] + w->stage_used[half], *d = w->d_stage[half] + w->stage_used[half];
     const size_t nsp = std::max(1u, w->n_space_ids);
     unsigned T = (unsigned)std::min<size_t>(kStageThreads, std::max<size_t>(1, n / kStageThreadMin));
     T = std::min(T, std::max(1u, std::thread::hardware_concurrency()));
     const size_t stride = nsp + 4;  // >= 64 B between the threads' boxes: no false sharing
-    std::vector<StageBox> boxes;
-    std::vector<size_t> bad;
-    std::vector<int> st;
-    std::vector<std::thread> pool;
-    try {  // no C++ exception may cross the C ABI
-        boxes.assign((size_t)T * stride, StageBox{0, 0, 0, 0, false});
-        bad.assign(T, 0);
-        st.assign(T, GWAOI_OK);
-        pool.reserve(T);
-    } catch (...) {
-        w->last_error = "moved_batch: host allocation failed";
-        return GWAOI_ENOMEM;
-    }
+    std::vector<StageBox> boxes((size_t)T * stride, StageBox{0, 0, 0, 0, false});
+    std::vector<size_t> bad(T, 0);
+    std::vector<int> st(T, GWAOI_OK);
     const size_t chunk = (n + T - 1) / T;
-    auto run = [&](unsigned t) {
+    w->pool.run(T, [&](unsigned t) {
         const size_t lo = std::min(n, t * chunk), hi = std::min(n, lo + chunk);
-        bad[t] = stage_chunk(w, slots, x, z, n, lo, hi, h, boxes.data() + (size_t)t * stride, &st[t]);
-    };
-    unsigned started = 1;
-    try {
-        for (; started < T; ++started) pool.emplace_back(run, started);
-    } catch (...) {  // a thread that cannot start: its chunks run here
-    }
-    for (unsigned t = started; t < T; ++t) run(t);
-    run(0);
-    for (std::thread &th : pool) th.join();
+        bad[t] = stage_chunk(w, slots, x, z, n, lo, hi, h, with_space, boxes.data() + (size_t)t * stride, &st[t]);
+    });
     for (unsigned t = 0; t < T; ++t)  // chunks are in call order: the first bad chunk has the first bad move
         if (st[t] != GWAOI_OK) return st[t];
-    for (unsigned t = 0; t < T; ++t)
-        for (size_t sp = 0; sp < nsp; ++sp) {
-            const StageBox &b = boxes[(size_t)t * stride + sp];
-            if (!b.any) continue;
-            note_pending_bbox(w->spaces[sp], b.x0, b.z0);
-            note_pending_bbox(w->spaces[sp], b.x1, b.z1);
-        }
-    HIP_TRY(hipMemcpyAsync(d, h, 4 * n * sizeof(uint32_t), hipMemcpyHostToDevice, w->stream));
-    w->stage_used += 4 * n;
+    HIP_TRY(hipMemcpyAsync(d, h, words * sizeof(uint32_t), hipMemcpyHostToDevice, w->copy_st));
+    HIP_TRY(hipEventRecord(w->copy_ev, w->copy_st));
+    w->copy_pending = true;
+    w->stage_used[half] += words;
     Run r{};
     r.device = true;
     r.ds = d;
     r.dx = reinterpret_cast<const float *>(d + n);
     r.dz = reinterpret_cast<const float *>(d + 2 * n);
-    r.dsp = d + 3 * n;
+    r.dsp = with_space ? d + 3 * n : nullptr;
     r.seq0 = w->seq_next;
     r.dn = n;
-    w->runs.push_back(r);
-    w->n_ops += n;
     w->seq_next += n;
+    for (unsigned t = 0; t < T; ++t)
+        for (size_t sp = 0; sp < nsp; ++sp) {
+            const StageBox &b = boxes[(size_t)t * stride + sp];
+            if (!b.any) continue;
+            if (w->in_flight) {
+                w->deferred_boxes.push_back(DeferredBox{(uint32_t)sp, b.x0, b.z0, b.x1, b.z1});
+            } else {
+                note_pending_bbox(w->spaces[sp], b.x0, b.z0);
+                note_pending_bbox(w->spaces[sp], b.x1, b.z1);
+            }
+        }
+    if (w->in_flight) {
+        Deferred q{};
+        q.kind = Deferred::RUN;
+        q.run = r;
+        w->deferred.push_back(q);
+    } else {
+        w->runs.push_back(r);
+        w->n_ops += n;
+    }
     return GWAOI_OK;
 }
 
@@ -1150,6 +1378,11 @@ int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
     w->space_of[slot] = gw::SP_DEAD;
     w->n_alive--;
     if (w->sync) gw::sync_note_slot(w->sync, slot, gw::SP_DEAD);
+    w->space_ops_queued = true;
+    if (w->in_flight) {
+        defer(w, Deferred::LEAVE, slot, gw::SP_DEAD, 0.f, 0.f, w->seq_next);
+        return GWAOI_OK;
+    }
     w->touched.push_back(slot);
     push_host_op(w, slot, 0.f, 0.f, gw::SP_DEAD, w->seq_next);  // a Leave's seq is never compared
     return GWAOI_OK;
@@ -1239,9 +1472,16 @@ int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const floa
     r.dseq = nullptr;
     r.seq0 = w->seq_next;
     r.dn = n;
+    w->seq_next += n;
+    if (w->in_flight) {
+        Deferred q{};
+        q.kind = Deferred::RUN;
+        q.run = r;
+        w->deferred.push_back(q);
+        return GWAOI_OK;
+    }
     w->runs.push_back(r);
     w->n_ops += n;
-    w->seq_next += n;
     return GWAOI_OK;
     });
 }
@@ -1251,6 +1491,7 @@ int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const 
     return gw::api_guard([&]() -> int {
     if (!w || (n && (!d_slots || !d_x || !d_z || !d_seq))) return GWAOI_EINVAL;
     GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
     if (!n) return GWAOI_OK;
     if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
     Run r{};
@@ -1278,7 +1519,8 @@ WorldView world_view(gwaoi_world *w) {
     v.info = w->sinfo;
     v.st = w->stream;
     v.max_slots = w->max_slots;
-    v.pending_ops = w->n_ops;
+    v.pending_ops = w->n_ops + w->deferred.size() + (w->in_flight ? 1 : 0);
+    v.in_flight = w->in_flight;
     v.events = w->events;
     v.n_enter = w->last_n_enter;
     v.n_leave = w->last_n_leave;
@@ -1296,6 +1538,7 @@ uint32_t world_slot_space(gwaoi_world *w, uint32_t slot) {
 int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
                         const uint32_t *d_sp, size_t n) {
     GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
     if (!n) return GWAOI_OK;
     if (n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
@@ -1317,14 +1560,24 @@ int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_
 
 extern "C" {
 
-int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+int gwaoi_tick_begin(gwaoi_world *w) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
+    return tick_launch(w);
+    });
+}
+
+int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     if (n_enter) *n_enter = 0;
     if (n_leave) *n_leave = 0;
     GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
     bool committed;
-    int rc = run_tick(w, &committed);
+    int rc = tick_finish(w, &committed);
     if (committed) {
         if (n_enter) *n_enter = w->last_n_enter;
         if (n_leave) *n_leave = w->last_n_leave;
@@ -1333,35 +1586,27 @@ int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
     });
 }
 
-int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
-    if (d_enter) *d_enter = w->events;
-    if (d_leave) *d_leave = w->events + 2 * w->last_n_enter;
-    return GWAOI_OK;
-    });
-}
-
-int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
+int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
     return gw::api_guard([&]() -> int {
     if (!w || !out) return GWAOI_EINVAL;
     out->n_enter = out->n_leave = 0;
     out->enter = out->leave = nullptr;
     GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
     bool committed;
-    int rc = run_tick(w, &committed);
+    int rc = tick_finish(w, &committed);
     if (!committed) return rc;
     // committed: deliver the events whatever the status (InterestedIn/By must follow the frame)
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1));
-    if (rc2) return rc2;
+    if (rc2) return poison(w, rc2);  // the committed events cannot reach the caller
     stage_begin(w, ST_D2H);
     if (tot) {
         hipError_t e = hipMemcpyAsync(w->h_events, w->events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       w->stream);
         if (e != hipSuccess) {
             w->last_error = std::string("event D2H: ") + hipGetErrorString(e);
-            return poison(w, GWAOI_EDEVICE);  // the committed events cannot reach the caller
+            return poison(w, GWAOI_EDEVICE);
         }
         if (int rw = wait_stream(w)) return poison(w, rw);
     }
@@ -1378,10 +1623,38 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
     });
 }
 
+int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    if (int rc = gwaoi_tick_begin(w)) {
+        if (n_enter) *n_enter = 0;
+        if (n_leave) *n_leave = 0;
+        return rc;
+    }
+    return gwaoi_tick_end_device(w, n_enter, n_leave);
+}
+
+int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    if (w->in_flight) return GWAOI_ESTATE;
+    if (d_enter) *d_enter = w->events;
+    if (d_leave) *d_leave = w->events + 2 * w->last_n_enter;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
+    if (!w || !out) return GWAOI_EINVAL;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    if (int rc = gwaoi_tick_begin(w)) return rc;
+    return gwaoi_tick_end(w, out);
+}
+
 int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, size_t *n_out) {
     return gw::api_guard([&]() -> int {
     if (!w || (cap && !out)) return GWAOI_EINVAL;
     GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (n_out) *n_out = 0;
     if (!w->in_frame[slot]) return GWAOI_ESTATE;
@@ -1415,6 +1688,7 @@ int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, 
     return gw::api_guard([&]() -> int {
     if (!w || !n_out) return GWAOI_EINVAL;
     GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
     const DevFrame &F = w->fr[w->cur];
     *n_out = F.n;
     if (F.n > cap || !F.n) return GWAOI_OK;
@@ -1440,7 +1714,7 @@ int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces,
     return gw::api_guard([&]() -> int {
     if (!w || (n && (!slots || !spaces || !x || !z || !seq))) return GWAOI_EINVAL;
     GW_LIVE(w);
-    if (w->n_ops || w->dev_seq_pending) return GWAOI_ESTATE;
+    if (w->n_ops || w->dev_seq_pending || w->in_flight) return GWAOI_ESTATE;
     std::vector<size_t> ord(n);
     for (size_t i = 0; i < n; ++i) ord[i] = i;
     std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return seq[a] < seq[b]; });

@@ -164,10 +164,27 @@ int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const 
                                  const uint64_t *d_seq, size_t n);
 
 /* ---- flush ------------------------------------------------------------------ */
-/* Run the tick and copy its events to host memory. */
+/* Run the tick and copy its events to host memory.  If the device found a bad
+ * op in a device batch (dropped; GWAOI_ESTATE / GWAOI_ENONFINITE /
+ * GWAOI_EINVAL) the flush still commits and *out holds its events: replay
+ * them.  Other failures leave *out empty. */
 int gwaoi_tick(gwaoi_world *w, gwaoi_events *out);
 /* Run the tick; events stay in device memory (see gwaoi_events_device). */
 int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
+
+/* Asynchronous flush: gwaoi_tick == gwaoi_tick_begin + gwaoi_tick_end.
+ * _begin closes the op queue, queues the whole pipeline on the GPU and returns
+ * at once.  Until _end, the AOIManager calls (enter / leave / moved and their
+ * batch forms, except explicit-seq device batches) stay available: they are
+ * validated and numbered at the call -- a gwaoi_moved_batch is also staged
+ * and sent to the GPU on a copy stream, overlapping the flush -- and queued
+ * for the NEXT flush when _end commits this one.  Everything else
+ * (neighbours, snapshot/restore, the sync layer, another _begin) returns
+ * GWAOI_ESTATE while a flush is in flight.  _end waits, commits and returns
+ * the events as gwaoi_tick / gwaoi_tick_device do. */
+int gwaoi_tick_begin(gwaoi_world *w);
+int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out);
+int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
 /* Device pointers of the last tick's events (same layout as gwaoi_events). */
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave);
 
@@ -176,10 +193,14 @@ int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t
  * slot, space, x, z and the seq of the entity's last Enter/Moved.  *n_out =
  * live entities (also when it exceeds cap; nothing is copied then).
  * gwaoi_restore re-enters such a state into a world with no queued op, in
- * seq order with the original seqs, so the restored relation is the frozen
- * one bit for bit (the reference re-enters in Go map order, Appendix D.6 of
- * SURVEY.md, which may flip ownership-dependent pairs).  Spaces must exist;
- * the next gwaoi_tick reports every restored pair as an enter. */
+ * seq order, so the restored relation is the frozen one bit for bit (the
+ * reference re-enters in Go map order, Appendix D.6 of SURVEY.md, which may
+ * flip ownership-dependent pairs).  The entities keep their original seqs
+ * when every one of them is >= the world's next seq (a fresh world, or one
+ * whose counter is below the snapshot's -- required for a strip world,
+ * gwaoi_strips.h, whose halo records carry global seqs); otherwise they get
+ * fresh seqs in the frozen order.  Spaces must exist; the next gwaoi_tick
+ * reports every restored pair as an enter. */
 int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, float *z, uint64_t *seq,
                    size_t cap, size_t *n_out);
 int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces, const float *x, const float *z,

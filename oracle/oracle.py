@@ -79,6 +79,12 @@ def lib():
         L.cf_diff.restype = C.c_int
         L.cf_rows.argtypes = [i64, vp, vp, vp, vp, vp, i64, vp, vp, C.POINTER(C.POINTER(C.c_uint32))]
         L.cf_rows.restype = i64
+        L.cg_new.argtypes = [i64, f, C.c_int]
+        L.cg_new.restype = vp
+        L.cg_free.argtypes = [vp]
+        L.cg_init.argtypes = [vp, vp, vp]
+        L.cg_init.restype = i64
+        L.cg_tick.argtypes = [vp, i64, vp, vp, vp, C.POINTER(i64), C.POINTER(i64)]
         _lib = L
     return _lib
 
@@ -257,6 +263,31 @@ def closed_form_pairs(x, z, seq, sp, D_by_space):
     res = np.ctypeslib.as_array(out, shape=(n,)).copy() if n else np.empty(0, np.uint64)
     L.cf_free(C.cast(out, C.c_void_p))
     return res
+
+
+class CpuGrid:
+    """CPU-grid comparator (oracle/cpu_grid.c): one space, every tick the relation
+    recomputed on all host cores with a cell grid and diffed against the last."""
+
+    def __init__(self, x, z, D, threads):
+        self._L = lib()
+        x = np.ascontiguousarray(x, np.float32)
+        z = np.ascontiguousarray(z, np.float32)
+        self._g = self._L.cg_new(x.size, C.c_float(D), int(threads))
+        self.pairs = self._L.cg_init(self._g, _p(x), _p(z))
+
+    def tick(self, slots, x, z):
+        s = np.ascontiguousarray(slots, np.int32)
+        x = np.ascontiguousarray(x, np.float32)
+        z = np.ascontiguousarray(z, np.float32)
+        ne, nl = C.c_int64(), C.c_int64()
+        self._L.cg_tick(self._g, s.size, _p(s), _p(x), _p(z), C.byref(ne), C.byref(nl))
+        return ne.value, nl.value
+
+    def __del__(self):
+        if getattr(self, "_g", None):
+            self._L.cg_free(self._g)
+            self._g = None
 
 
 def _space_d(sp_arrays, D_by_space):

@@ -636,3 +636,83 @@ def test_failed_event_regrow_poisons_world_gpu(monkeypatch):
             assert ej.value.code == -5 and "failed flush" in str(ej.value)
     finally:
         w.close()
+
+
+def test_async_tick_overlaps_next_calls_gpu():
+    """gwaoi_tick_begin / _end: the calls made while a flush is in flight (a staged
+    host batch with repeats, Enters, Leaves, single Moves, a device batch) are
+    validated at once and queued for the NEXT flush.  Every flush's events equal
+    those of a world driven with blocking ticks and the same call order."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(23)
+    n = 30000
+    wl = make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wl.initial()
+    k0 = n - 3000
+    live = np.zeros(n, bool)
+    live[:k0] = True
+    x, z = x0.copy(), z0.copy()
+    keep = []
+
+    def calls(t):
+        """This tick's calls as closures over a world."""
+        out = []
+        pool = np.nonzero(live)[0]
+        sl = rng.choice(pool, 20000).astype(np.uint32)  # repeats included
+        nx = (x[sl] + rng.uniform(-3, 3, sl.size)).astype(np.float32)
+        nz = (z[sl] + rng.uniform(-3, 3, sl.size)).astype(np.float32)
+        out.append(lambda w, a=sl, b=nx, c=nz: w.moved_batch(a, b, c))
+        x[sl], z[sl] = nx, nz
+        for i in rng.choice(np.nonzero(~live)[0], 200, replace=False):
+            xi, zi = np.float32(x[i]), np.float32(z[i])
+            out.append(lambda w, i=int(i), xi=xi, zi=zi: w.enter(0, i, xi, zi))
+            live[i] = True
+        for i in rng.choice(np.nonzero(live)[0], 150, replace=False):
+            out.append(lambda w, i=int(i): w.leave(i))
+            live[i] = False
+        j = int(np.nonzero(live)[0][t])
+        xj = np.float32(x[j] + 60)
+        out.append(lambda w, j=j, xj=xj: w.moved(j, xj, z[j]))
+        x[j] = xj
+        ds = rng.choice(np.nonzero(live)[0], 5000, replace=False).astype(np.uint32)
+        dx = (x[ds] + rng.uniform(-2, 2, ds.size)).astype(np.float32)
+        dz = (z[ds] + rng.uniform(-2, 2, ds.size)).astype(np.float32)
+        x[ds], z[ds] = dx, dz
+        tens = [torch.from_numpy(v).cuda() for v in (ds.astype(np.int32), dx, dz)]
+        torch.cuda.synchronize()
+        keep.append(tens)
+        out.append(lambda w, tt=tens: w.moved_batch_device(tt[0].data_ptr(), tt[1].data_ptr(), tt[2].data_ptr(),
+                                                           tt[0].numel()))
+        return out
+
+    with World(n) as wa, World(n) as wb:
+        for w in (wa, wb):
+            w.space_create(wl.D)
+            w.enter_batch(0, slots[:k0], x0[:k0], z0[:k0])
+        wa.tick()
+        wb.tick()
+        ticks = [calls(t) for t in range(5)]
+        for c in ticks[0]:
+            c(wa)
+        wa.tick_begin()
+        with pytest.raises(GwaoiError):
+            wa.tick_begin()  # one flush at a time
+        with pytest.raises(GwaoiError):
+            wa.neighbors(0)  # not while a flush is in flight
+        for t in range(5):
+            for c in ticks[t]:
+                c(wb)
+            eb, lb = wb.tick()
+            if t + 1 < 5:
+                for c in ticks[t + 1]:
+                    c(wa)  # queued while flush t is in flight
+            ea, la = wa.tick_end()
+            np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb), err_msg=f"flush {t}: enters")
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"flush {t}: leaves")
+            assert ea.shape[0] > 0 and la.shape[0] > 0
+            if t + 1 < 5:
+                wa.tick_begin()
+        with pytest.raises(GwaoiError):
+            wa.tick_end()  # nothing in flight
+        for i in np.nonzero(live)[0][::2003]:
+            np.testing.assert_array_equal(wa.neighbors(int(i)), wb.neighbors(int(i)))

@@ -274,3 +274,25 @@ def test_closed_form_diff_matches_setdiff(oracle_mod):
     for q, r in zip([0, 5, 17], rows):
         np.testing.assert_array_equal(r, (k1[(k1 >> np.uint64(32)) == q] & np.uint64(0xFFFFFFFF)).astype(np.uint32))
     assert oracle_mod.key_checksum(ent) == oracle_mod.key_checksum(ent[::-1].copy())
+
+
+def test_cpu_grid_comparator_counts(oracle_mod):
+    """The CPU-grid comparator of bench.py (oracle/cpu_grid.c) reports, tick by tick,
+    the enter/leave counts of the closed-form diff (it computes the same relation)."""
+    from goworld_amd.workload import make_workload
+    wl = make_workload("cfg3", n=20000)
+    n = wl.n
+    seq = 1 + np.arange(n, dtype=np.uint64)
+    sp = np.zeros(n, np.uint32)
+    g = oracle_mod.CpuGrid(wl.x, wl.z, wl.D, threads=3)
+    want = oracle_mod.closed_form_pairs(wl.x, wl.z, seq, sp, {0: wl.D})
+    assert g.pairs == want.size
+    nxt = n + 1
+    for t in range(3):
+        before = (wl.x.copy(), wl.z.copy(), seq.copy(), sp)
+        sl, nx, nz = wl.tick(t)
+        seq[sl] = nxt + np.arange(sl.size, dtype=np.uint64)
+        nxt += sl.size
+        ne, nl = g.tick(sl, nx, nz)
+        e, l = oracle_mod.closed_form_diff(before, (wl.x, wl.z, seq, sp), {0: wl.D}, threads=3)
+        assert (ne, nl) == (e.size, l.size) and ne > 0

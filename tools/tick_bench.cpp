@@ -1,0 +1,240 @@
+// gwaoi_tick_bench -- SURVEY.md §8(d)'s end-to-end tick from a C++ host, the
+// view a cgo caller has: config 3 (1M entities, 256 Gaussian crowd hotspots +
+// uniform background, D = 100, every entity moves by U(-1,1) per axis per tick
+// in a seeded random call order), host move arrays -> gwaoi_moved_batch
+// (validation + pinned staging + H2D) -> flush -> events in pinned host memory,
+// then the callback replay of Entity.go:236-246 (interest / uninterest: a.In
+// += b, b.By += a per directed event) into per-entity InterestedIn /
+// InterestedBy sets, the part SURVEY.md §7 (hard part 6) expects to dominate.
+//
+// Three measurements, one JSON line:
+//   serial     gwaoi_moved_batch + gwaoi_tick per tick (latency p50 / p99)
+//   pipelined  gwaoi_tick_begin(t); gwaoi_moved_batch(t+1) while the GPU runs;
+//              gwaoi_tick_end(t)  (period = host staging overlapped with the flush)
+//   replay     the tick's events into the sets: one thread, and T threads that
+//              each own the sets of a slot range (every thread scans all events)
+//
+// The workload mirrors goworld_amd/workload.py (SplitMix64, Box-Muller in
+// double); only its shape matters here, not bit-identity with the Python one.
+//
+// usage: gwaoi_tick_bench [ticks=20] [threads=16] [n=1000000]
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <numeric>
+#include <thread>
+#include <vector>
+
+#include "gwaoi.h"
+
+namespace {
+
+constexpr uint64_t GAMMA = 0x9E3779B97F4A7C15ull;
+
+uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+uint64_t subseed(uint64_t seed, uint64_t a, uint64_t b = ~0ull) {
+    uint64_t h = mix64(seed ^ (a * GAMMA));
+    if (b != ~0ull) h = mix64(h ^ (b * GAMMA));
+    return h;
+}
+struct Stream {  // consecutive SplitMix64 outputs of a seed
+    uint64_t s;
+    uint64_t next() { return mix64(s += GAMMA); }
+    double unit() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+double pct(std::vector<double> v, double p) {
+    std::sort(v.begin(), v.end());
+    if (v.empty()) return 0;
+    return v[std::min(v.size() - 1, (size_t)(p / 100.0 * (v.size() - 1) + 0.5))];
+}
+
+void check(int rc, const char *what, gwaoi_world *w) {
+    if (rc) {
+        std::fprintf(stderr, "%s: %s (%s)\n", what, gwaoi_strerror(rc), w ? gwaoi_last_error(w) : "");
+        std::exit(1);
+    }
+}
+
+// Per-entity sets: the event stream never adds a present member or removes an
+// absent one, so a vector with swap-remove is an exact set.
+struct Sets {
+    std::vector<std::vector<uint32_t>> in, by;
+    explicit Sets(size_t n) : in(n), by(n) {}
+};
+
+void erase_one(std::vector<uint32_t> &v, uint32_t x) {
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i] == x) {
+            v[i] = v.back();
+            v.pop_back();
+            return;
+        }
+}
+
+// Entity.go:236-246 for the flush's events (leaves first, then enters), for
+// the slots in [lo, hi) only (In of a, By of b).
+void replay(Sets &S, const gwaoi_events &ev, uint32_t lo, uint32_t hi) {
+    for (uint64_t k = 0; k < ev.n_leave; ++k) {
+        const uint32_t a = ev.leave[2 * k], b = ev.leave[2 * k + 1];
+        if (a >= lo && a < hi) erase_one(S.in[a], b);
+        if (b >= lo && b < hi) erase_one(S.by[b], a);
+    }
+    for (uint64_t k = 0; k < ev.n_enter; ++k) {
+        const uint32_t a = ev.enter[2 * k], b = ev.enter[2 * k + 1];
+        if (a >= lo && a < hi) S.in[a].push_back(b);
+        if (b >= lo && b < hi) S.by[b].push_back(a);
+    }
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const int ticks = argc > 1 ? std::atoi(argv[1]) : 20;
+    const unsigned T = argc > 2 ? (unsigned)std::atoi(argv[2]) : 16;
+    const uint32_t n = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 1000000;
+    const uint64_t seed = 0x5EED0003ull;
+    const double L = std::sqrt((double)n * 1250.0);
+    // ---- config 3 positions: half uniform, half in hotspots of ~1953 entities (sigma 250)
+    std::vector<float> x(n), z(n);
+    {
+        const uint32_t nu = n / 2, nh = n - nu, hot = std::max(1u, (uint32_t)std::lround(256.0 * n / 1e6));
+        Stream su{subseed(seed, 1)};
+        for (uint32_t i = 0; i < nu; ++i) x[i] = (float)(su.unit() * L - L / 2);
+        for (uint32_t i = 0; i < nu; ++i) z[i] = (float)(su.unit() * L - L / 2);
+        std::vector<double> cx(hot), cz(hot);
+        Stream sc{subseed(seed, 2)};
+        for (auto &c : cx) c = (sc.unit() * 0.8 - 0.4) * L;
+        for (auto &c : cz) c = (sc.unit() * 0.8 - 0.4) * L;
+        Stream sh{subseed(seed, 3)};
+        for (uint32_t i = 0; i < nh; ++i) {
+            const uint32_t h = (uint32_t)(sh.next() % hot);
+            const double u1 = 1.0 - sh.unit(), u2 = sh.unit(), u3 = 1.0 - sh.unit(), u4 = sh.unit();
+            x[nu + i] = (float)(cx[h] + 250.0 * std::sqrt(-2.0 * std::log(u1)) * std::cos(2.0 * M_PI * u2));
+            z[nu + i] = (float)(cz[h] + 250.0 * std::sqrt(-2.0 * std::log(u3)) * std::cos(2.0 * M_PI * u4));
+        }
+    }
+    // ---- move batches: 2 * ticks + 2 of them (serial + pipelined legs, one warmup each)
+    const int nb = 2 * ticks + 2;
+    std::vector<std::vector<uint32_t>> bs(nb);
+    std::vector<std::vector<float>> bx(nb), bz(nb);
+    {
+        std::vector<std::pair<uint64_t, uint32_t>> ord(n);
+        for (int t = 0; t < nb; ++t) {
+            Stream so{subseed(seed, 0x0D3, (uint64_t)t)}, sm{subseed(seed, 0x71C, (uint64_t)t)};
+            for (uint32_t i = 0; i < n; ++i) ord[i] = {so.next(), i};
+            std::sort(ord.begin(), ord.end());
+            bs[t].resize(n);
+            bx[t].resize(n);
+            bz[t].resize(n);
+            std::vector<float> sx(n), sz(n);
+            for (uint32_t i = 0; i < n; ++i) sx[i] = (float)(2.0 * sm.unit() - 1.0);
+            for (uint32_t i = 0; i < n; ++i) sz[i] = (float)(2.0 * sm.unit() - 1.0);
+            for (uint32_t k = 0; k < n; ++k) {
+                const uint32_t s = ord[k].second;
+                x[s] = x[s] + sx[s];
+                z[s] = z[s] + sz[s];
+                bs[t][k] = s;
+                bx[t][k] = x[s];
+                bz[t][k] = z[s];
+            }
+        }
+    }
+    // Enter at batch 0's positions (in its order) and move from batch 1 on.
+    gwaoi_config cfg{};
+    cfg.max_slots = n;
+    cfg.max_spaces = 1;
+    cfg.device = 0;
+    gwaoi_world *w = nullptr;
+    check(gwaoi_world_create(&cfg, &w), "world_create", nullptr);
+    uint32_t sp = 0;
+    check(gwaoi_space_create(w, 100.0f, &sp), "space_create", w);
+    check(gwaoi_enter_batch(w, sp, bs[0].data(), bx[0].data(), bz[0].data(), n), "enter_batch", w);
+    gwaoi_events ev{};
+    check(gwaoi_tick(w, &ev), "populate", w);
+    Sets S(n);
+    replay(S, ev, 0, n);
+    const uint64_t populate = ev.n_enter;
+
+    // ---- serial leg: moved_batch + tick, then replay (one thread)
+    std::vector<double> t_stage, t_tick, t_lat, t_rep1;
+    uint64_t events = 0;
+    for (int t = 1; t <= ticks; ++t) {
+        const double a = now();
+        check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
+        const double b = now();
+        check(gwaoi_tick(w, &ev), "tick", w);
+        const double c = now();
+        replay(S, ev, 0, n);
+        const double d = now();
+        if (t > 1) {  // the first tick sizes the pinned buffers
+            t_stage.push_back(b - a);
+            t_tick.push_back(c - b);
+            t_lat.push_back(c - a);
+            t_rep1.push_back(d - c);
+            events += ev.n_enter + ev.n_leave;
+        }
+    }
+    // ---- pipelined leg: stage t+1 while the flush of t runs; replay on T threads
+    std::vector<double> p_lat, t_repT;
+    int t = ticks + 1;
+    check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
+    double t_issue = now();
+    const double p0 = now();
+    int done = 0;
+    for (; t < nb; ++t) {
+        check(gwaoi_tick_begin(w), "tick_begin", w);
+        const double issued_next = now();
+        if (t + 1 < nb) check(gwaoi_moved_batch(w, bs[t + 1].data(), bx[t + 1].data(), bz[t + 1].data(), n), "moved_batch", w);
+        check(gwaoi_tick_end(w, &ev), "tick_end", w);
+        const double e = now();
+        p_lat.push_back(e - t_issue);  // from this tick's batch call to its events in host memory
+        t_issue = issued_next;
+        const double r0 = now();
+        std::vector<std::thread> th;
+        for (unsigned k = 1; k < T; ++k)
+            th.emplace_back([&, k] { replay(S, ev, (uint32_t)((uint64_t)n * k / T), (uint32_t)((uint64_t)n * (k + 1) / T)); });
+        replay(S, ev, 0, (uint32_t)((uint64_t)n / T));
+        for (auto &x : th) x.join();
+        t_repT.push_back(now() - r0);
+        ++done;
+    }
+    const double p_total = now() - p0;
+    const double p_flush = p_total - std::accumulate(t_repT.begin(), t_repT.end(), 0.0);
+    // sanity: In == By in size, and the sets hold the last flush's relation size
+    uint64_t sin = 0, sby = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        sin += S.in[i].size();
+        sby += S.by[i].size();
+    }
+    gwaoi_world_destroy(w);
+    const double ms = 1e3;
+    std::printf(
+        "{\"entities\": %u, \"ticks\": %d, \"populate_enters\": %llu, \"events_per_tick\": %.1f, "
+        "\"serial\": {\"stage_ms_p50\": %.4f, \"tick_ms_p50\": %.4f, \"latency_ms_mean\": %.4f, "
+        "\"latency_ms_p50\": %.4f, \"latency_ms_p99\": %.4f}, "
+        "\"pipelined\": {\"ms_per_tick\": %.4f, \"moves_per_s\": %.4g, \"latency_ms_p50\": %.4f, "
+        "\"latency_ms_p99\": %.4f, \"ms_per_tick_with_replay\": %.4f, "
+        "\"note\": \"period = wall time per tick minus the T-thread replay (timed separately)\"}, "
+        "\"replay\": {\"ms_1thread_p50\": %.4f, \"ms_%uthreads_p50\": %.4f, \"threads\": %u}, "
+        "\"relation_pairs\": %llu, \"in_eq_by\": %s}\n",
+        n, ticks, (unsigned long long)populate, (double)events / std::max<size_t>(1, t_lat.size()),
+        pct(t_stage, 50) * ms, pct(t_tick, 50) * ms,
+        std::accumulate(t_lat.begin(), t_lat.end(), 0.0) / std::max<size_t>(1, t_lat.size()) * ms,
+        pct(t_lat, 50) * ms, pct(t_lat, 99) * ms, p_flush / done * ms, (double)n * done / p_flush,
+        pct(p_lat, 50) * ms, pct(p_lat, 99) * ms, p_total / done * ms, pct(t_rep1, 50) * ms, T,
+        pct(t_repT, 50) * ms, T,
+        (unsigned long long)sin, sin == sby ? "true" : "false");
+    return 0;
+}
