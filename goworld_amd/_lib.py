@@ -35,7 +35,7 @@ EXPORTS = [
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
     "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
-    "gwaoi_tick_end_device",
+    "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -133,6 +133,8 @@ def load():
         "gwaoi_tick": ([vp, P(Events)], C.c_int),
         "gwaoi_tick_device": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_tick_begin": ([vp], C.c_int),
+        "gwaoi_events_csr": ([vp, P(vp), P(vp), P(u64)], C.c_int),
+        "gwaoi_events_csr_device": ([vp, P(vp), P(vp), P(u64)], C.c_int),
         "gwaoi_tick_end": ([vp, P(Events)], C.c_int),
         "gwaoi_tick_end_device": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
@@ -324,6 +326,16 @@ class World:
                 e.counts = (ne.value, nl.value)
                 raise
         return ne.value, nl.value
+
+    def events_csr(self):
+        """The last flush's events by entity (gwaoi_events_csr): (offsets[max_slots+1], items)
+        uint32 copies; item = b | 0x80000000 for an enter (s, b), b for a leave."""
+        o, it, n = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        self._check(self._L.gwaoi_events_csr(self._w, C.byref(o), C.byref(it), C.byref(n)))
+        off = np.ctypeslib.as_array(C.cast(o, C.POINTER(C.c_uint32)), shape=(self.max_slots + 1,)).copy()
+        items = (np.ctypeslib.as_array(C.cast(it, C.POINTER(C.c_uint32)), shape=(n.value,)).copy() if n.value
+                 else np.empty(0, np.uint32))
+        return off, items
 
     def events_device(self):
         e, l = C.c_void_p(), C.c_void_p()

@@ -1748,9 +1748,56 @@ __global__ __launch_bounds__(256) void k_neighbors(FrameView F, const SlotInfo *
     }
 }
 
+// ------------------------------------------------------------ event CSR ------
+// The flush's directed events regrouped by their first entity (gwaoi_events_csr):
+// row a = items[off[a] .. off[a+1]), an item is b (leave) or b | CSR_ENTER
+// (enter), so sorting a row puts its leaves first, each part by b.
+constexpr uint32_t CSR_ENTER = 0x80000000u;
+
+__global__ void k_csr_count(const uint2 *__restrict__ ev, uint32_t n_total, uint32_t *cnt) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n_total) atomicAdd(&cnt[ev[e].x], 1u);
+}
+
+__global__ void k_csr_fill(const uint2 *__restrict__ ev, uint32_t n_enter, uint32_t n_total,
+                           const uint32_t *__restrict__ off, uint32_t *cur, uint32_t *items) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_total) return;
+    const uint2 p = ev[e];
+    items[off[p.x] + atomicAdd(&cur[p.x], 1u)] = p.y | (e < n_enter ? CSR_ENTER : 0u);
+}
+
+// one lane per row: rows are short (a few events per entity per tick)
+__global__ void k_csr_sort(const uint32_t *__restrict__ off, uint32_t n_rows, uint32_t *items) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    const uint32_t b = off[r], e = off[r + 1];
+    for (uint32_t k = b + 1; k < e; ++k) {
+        const uint32_t v = items[k];
+        uint32_t j = k;
+        while (j > b && items[j - 1] > v) {
+            items[j] = items[j - 1];
+            --j;
+        }
+        items[j] = v;
+    }
+}
+
 }  // namespace
 
 // ============================================================ launchers ======
+
+void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_total, uint32_t n_rows, uint32_t *cnt,
+                       uint32_t *off, uint32_t *scan_tmp, uint32_t *items, hipStream_t st) {
+    const uint2 *ev = reinterpret_cast<const uint2 *>(ev_pairs);
+    k_zero<<<cdiv((size_t)n_rows + 1, 256), 256, 0, st>>>(cnt, (size_t)n_rows + 1);
+    if (n_total) k_csr_count<<<cdiv(n_total, 256), 256, 0, st>>>(ev, (uint32_t)n_total, cnt);
+    scan_exclusive(cnt, off, (size_t)n_rows + 1, scan_tmp, st);
+    if (!n_total) return;
+    k_zero<<<cdiv((size_t)n_rows, 256), 256, 0, st>>>(cnt, (size_t)n_rows);
+    k_csr_fill<<<cdiv(n_total, 256), 256, 0, st>>>(ev, (uint32_t)n_enter, (uint32_t)n_total, off, cnt, items);
+    k_csr_sort<<<cdiv(n_rows, 256), 256, 0, st>>>(off, n_rows, items);
+}
 
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
                      uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,

@@ -202,6 +202,12 @@ struct gwaoi_world {
     char *dev_out = nullptr;     // TickOut + int4 bbox[max_spaces]
     uint32_t *nb_out = nullptr, *nb_count = nullptr;
     size_t nb_cap = 0;
+    // per-slot rows of the last flush's events (gwaoi_events_csr), built on request
+    uint32_t *csr_cnt = nullptr, *csr_off = nullptr, *csr_items = nullptr;
+    uint64_t csr_items_cap = 0;
+    uint32_t *h_csr_off = nullptr, *h_csr_items = nullptr;
+    uint64_t h_csr_items_cap = 0;
+    uint64_t csr_tick = ~0ull;  // flush the device CSR belongs to
 
     // pinned host mirrors
     char *h_out = nullptr;  // TickOut + int4 bbox[max_spaces]
@@ -230,6 +236,7 @@ struct gwaoi_world {
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
     StagePool pool;
+    unsigned stage_threads = 8;  // host threads validating + staging one big batch (GWAOI_STAGE_THREADS)
     std::vector<uint32_t> new_slots;
     std::vector<uint32_t> touched;  // slots whose liveness changed since the last flush
     // seq_next: the seq the next implicit call gets (advanced at queue time);
@@ -1035,6 +1042,9 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
     dfree(w->nb_out); dfree(w->nb_count);
+    dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items);
+    if (w->h_csr_off) (void)hipHostFree(w->h_csr_off);
+    if (w->h_csr_items) (void)hipHostFree(w->h_csr_items);
     if (w->h_out) (void)hipHostFree(w->h_out);
     if (w->h_events) (void)hipHostFree(w->h_events);
     if (w->h_grid) (void)hipHostFree(w->h_grid);
@@ -1068,6 +1078,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_INJECT_REGROW_FAIL")) w->inject_regrow_fail = e[0] == '1';
+    if (const char *e = std::getenv("GWAOI_STAGE_THREADS")) w->stage_threads = (unsigned)std::max(1, std::atoi(e));
     int rc = GWAOI_OK;
     auto fail = [&](int code) {
         gwaoi_world_destroy(w);
@@ -1292,8 +1303,7 @@ size_t stage_chunk(const gwaoi_world *w, const uint32_t *slots, const float *x, 
 // kStageThreads host threads, send it with one async H2D and queue it as a device batch with seqs
 // seq_next.. and the slot's space at call time (explicit, so a slot that entered earlier in this
 // flush moves exactly as a host op would).  Nothing is queued if any move is rejected.
-constexpr size_t kStageThreadMin = 1 << 17;  // moves per extra thread
-constexpr unsigned kStageThreads = 8;
+constexpr size_t kStageThreadMin = 1 << 16;  // moves per extra thread
 
 int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
     const int half = w->stage_cur;
@@ -1303,7 +1313,7 @@ int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const flo
     const size_t words = (with_space ? 4 : 3) * n;
     uint32_t *h = w->h_stage[half] + w->stage_used[half], *d = w->d_stage[half] + w->stage_used[half];
     const size_t nsp = std::max(1u, w->n_space_ids);
-    unsigned T = (unsigned)std::min<size_t>(kStageThreads, std::max<size_t>(1, n / kStageThreadMin));
+    unsigned T = (unsigned)std::min<size_t>(w->stage_threads, std::max<size_t>(1, n / kStageThreadMin));
     T = std::min(T, std::max(1u, std::thread::hardware_concurrency()));
     const size_t stride = nsp + 4;  // >= 64 B between the threads' boxes: no false sharing
     std::vector<StageBox> boxes((size_t)T * stride, StageBox{0, 0, 0, 0, false});
@@ -1648,6 +1658,74 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
     out->enter = out->leave = nullptr;
     if (int rc = gwaoi_tick_begin(w)) return rc;
     return gwaoi_tick_end(w, out);
+}
+
+namespace {
+
+// Build the last flush's event rows on the device (once per flush).
+int build_csr(gwaoi_world *w) {
+    const uint64_t tot = w->last_n_enter + w->last_n_leave;
+    if (w->csr_tick == w->ticks) return GWAOI_OK;
+    const size_t rows = w->max_slots;
+    if (!w->csr_cnt) {
+        int rc;
+        if ((rc = dalloc(w, &w->csr_cnt, rows + 1)) || (rc = dalloc(w, &w->csr_off, rows + 1))) return rc;
+    }
+    if (tot > w->csr_items_cap) {
+        HIP_TRY(hipStreamSynchronize(w->stream));
+        dfree(w->csr_items);
+        w->csr_items_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(tot + tot / 4, 1 << 16);
+        if (int rc = dalloc(w, &w->csr_items, cap)) return rc;
+        w->csr_items_cap = cap;
+    }
+    if (int rc = ensure_scan_tmp(w, rows + 1)) return rc;
+    gw::launch_events_csr(w->events, w->last_n_enter, tot, (uint32_t)rows, w->csr_cnt, w->csr_off, w->scan_tmp,
+                          w->csr_items, w->stream);
+    HIP_TRY(hipGetLastError());
+    w->csr_tick = w->ticks;
+    return GWAOI_OK;
+}
+
+}  // namespace
+
+int gwaoi_events_csr_device(gwaoi_world *w, const uint32_t **d_offsets, const uint32_t **d_items, uint64_t *n_items) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !d_offsets || !d_items) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
+    if (int rc = build_csr(w)) return rc;
+    *d_offsets = w->csr_off;
+    *d_items = w->csr_items;
+    if (n_items) *n_items = w->last_n_enter + w->last_n_leave;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_events_csr(gwaoi_world *w, const uint32_t **offsets, const uint32_t **items, uint64_t *n_items) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !offsets || !items) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (w->in_flight) return GWAOI_ESTATE;
+    if (int rc = build_csr(w)) return rc;
+    const uint64_t tot = w->last_n_enter + w->last_n_leave;
+    if (!w->h_csr_off) HIP_TRY(hipHostMalloc((void **)&w->h_csr_off, ((size_t)w->max_slots + 1) * 4, hipHostMallocDefault));
+    if (tot > w->h_csr_items_cap) {
+        if (w->h_csr_items) (void)hipHostFree(w->h_csr_items);
+        w->h_csr_items = nullptr;
+        w->h_csr_items_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(tot + tot / 4, 1 << 16);
+        HIP_TRY(hipHostMalloc((void **)&w->h_csr_items, cap * 4, hipHostMallocDefault));
+        w->h_csr_items_cap = cap;
+    }
+    HIP_TRY(hipMemcpyAsync(w->h_csr_off, w->csr_off, ((size_t)w->max_slots + 1) * 4, hipMemcpyDeviceToHost, w->stream));
+    if (tot) HIP_TRY(hipMemcpyAsync(w->h_csr_items, w->csr_items, tot * 4, hipMemcpyDeviceToHost, w->stream));
+    if (int rc = wait_stream(w)) return rc;
+    *offsets = w->h_csr_off;
+    *items = w->h_csr_items;
+    if (n_items) *n_items = tot;
+    return GWAOI_OK;
+    });
 }
 
 int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, size_t *n_out) {

@@ -188,6 +188,21 @@ int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
 /* Device pointers of the last tick's events (same layout as gwaoi_events). */
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave);
 
+/* The last tick's events regrouped by entity (built on the GPU on request), for
+ * a replay entity by entity -- Entity.go:236-246 touches a's InterestedIn and
+ * b's InterestedBy per event (a,b); events come in pairs, so row s lists every
+ * change of s's InterestedIn AND of s's InterestedBy:
+ *   row s = items[offsets[s] .. offsets[s+1]),  offsets has max_slots + 1 entries,
+ *   item  = b               : leave (s, b)
+ *         = b | 0x80000000  : enter (s, b)
+ * sorted ascending within the row, so its leaves come first (an entity that
+ * changed space may leave and re-enter the same partner in one flush), each
+ * part by b.  Host memory (world-owned, valid until the next flush) or device
+ * memory.  GWAOI_ESTATE while a flush is in flight. */
+#define GWAOI_CSR_ENTER 0x80000000u
+int gwaoi_events_csr(gwaoi_world *w, const uint32_t **offsets, const uint32_t **items, uint64_t *n_items);
+int gwaoi_events_csr_device(gwaoi_world *w, const uint32_t **d_offsets, const uint32_t **d_items, uint64_t *n_items);
+
 /* ---- freeze / restore (EntityManager.go:554-656, Space.go:118-125) ----------
  * gwaoi_snapshot copies the AOI state of the last flush in frame order:
  * slot, space, x, z and the seq of the entity's last Enter/Moved.  *n_out =

@@ -657,6 +657,7 @@ def test_async_tick_overlaps_next_calls_gpu():
     def calls(t):
         """This tick's calls as closures over a world."""
         out = []
+        live_prev = live.copy()  # device batches may only move slots live at the previous flush
         pool = np.nonzero(live)[0]
         sl = rng.choice(pool, 20000).astype(np.uint32)  # repeats included
         nx = (x[sl] + rng.uniform(-3, 3, sl.size)).astype(np.float32)
@@ -674,7 +675,7 @@ def test_async_tick_overlaps_next_calls_gpu():
         xj = np.float32(x[j] + 60)
         out.append(lambda w, j=j, xj=xj: w.moved(j, xj, z[j]))
         x[j] = xj
-        ds = rng.choice(np.nonzero(live)[0], 5000, replace=False).astype(np.uint32)
+        ds = rng.choice(np.nonzero(live & live_prev)[0], 5000, replace=False).astype(np.uint32)
         dx = (x[ds] + rng.uniform(-2, 2, ds.size)).astype(np.float32)
         dz = (z[ds] + rng.uniform(-2, 2, ds.size)).astype(np.float32)
         x[ds], z[ds] = dx, dz
@@ -716,3 +717,36 @@ def test_async_tick_overlaps_next_calls_gpu():
             wa.tick_end()  # nothing in flight
         for i in np.nonzero(live)[0][::2003]:
             np.testing.assert_array_equal(wa.neighbors(int(i)), wb.neighbors(int(i)))
+
+
+def test_events_csr_regroups_events_gpu():
+    """gwaoi_events_csr: the flush's directed events regrouped by their first entity,
+    each row sorted with its leaves first; the same multiset as the event pairs,
+    including a pair that leaves one space and enters another in the same flush."""
+    rng = np.random.default_rng(41)
+    n = 20000
+    wl = make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wl.initial()
+    with World(n, max_spaces=2) as w:
+        s0 = w.space_create(wl.D)
+        s1 = w.space_create(wl.D)
+        w.enter_batch(s0, slots, x0, z0)
+        w.tick()
+        for t in range(3):
+            sl, nx, nz = wl.tick(t)
+            w.moved_batch(sl, nx, nz)
+            for i in rng.choice(n, 300, replace=False):  # space changes of neighbours at the same spot
+                w.leave(int(i))
+                w.enter(s1 if t % 2 == 0 else s0, int(i), wl.x[i], wl.z[i])
+            ent, lev = w.tick()
+            off, items = w.events_csr()
+            assert off.size == n + 1 and off[-1] == items.size == ent.shape[0] + lev.shape[0]
+            rows = np.repeat(np.arange(n, dtype=np.uint64), np.diff(off).astype(np.int64))
+            b = (items & np.uint32(0x7FFFFFFF)).astype(np.uint64)
+            is_enter = (items & np.uint32(0x80000000)) != 0
+            keys = (rows << np.uint64(32)) | b
+            np.testing.assert_array_equal(np.sort(keys[is_enter]), pair_keys(ent))
+            np.testing.assert_array_equal(np.sort(keys[~is_enter]), pair_keys(lev))
+            for r in range(0, n, 97):  # each row sorted: leaves (bit 31 clear) first, each part by b
+                row = items[off[r]:off[r + 1]]
+                assert np.all(row[:-1] <= row[1:])

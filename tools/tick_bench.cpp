@@ -11,8 +11,9 @@
 //   serial     gwaoi_moved_batch + gwaoi_tick per tick (latency p50 / p99)
 //   pipelined  gwaoi_tick_begin(t); gwaoi_moved_batch(t+1) while the GPU runs;
 //              gwaoi_tick_end(t)  (period = host staging overlapped with the flush)
-//   replay     the tick's events into the sets: one thread, and T threads that
-//              each own the sets of a slot range (every thread scans all events)
+//   replay     the tick's events into the sets: the event pairs on one thread;
+//              the per-entity rows of gwaoi_events_csr on one and on T threads
+//              (each thread owns the sets of a slot range)
 //
 // The workload mirrors goworld_amd/workload.py (SplitMix64, Box-Muller in
 // double); only its shape matters here, not bit-identity with the Python one.
@@ -98,6 +99,24 @@ void replay(Sets &S, const gwaoi_events &ev, uint32_t lo, uint32_t hi) {
     }
 }
 
+// The same with the events regrouped by entity (gwaoi_events_csr): row s lists
+// every change of s's InterestedIn and, events coming in pairs, of its
+// InterestedBy -- one pass per entity, no scan of the whole event list.
+void replay_csr(Sets &S, const uint32_t *off, const uint32_t *items, uint32_t lo, uint32_t hi) {
+    for (uint32_t s = lo; s < hi; ++s) {
+        for (uint32_t k = off[s]; k < off[s + 1]; ++k) {
+            const uint32_t it = items[k], b = it & ~GWAOI_CSR_ENTER;
+            if (it & GWAOI_CSR_ENTER) {
+                S.in[s].push_back(b);
+                S.by[s].push_back(b);
+            } else {
+                erase_one(S.in[s], b);
+                erase_one(S.by[s], b);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -167,51 +186,79 @@ int main(int argc, char **argv) {
     replay(S, ev, 0, n);
     const uint64_t populate = ev.n_enter;
 
-    // ---- serial leg: moved_batch + tick, then replay (one thread)
-    std::vector<double> t_stage, t_tick, t_lat, t_rep1;
+    // ---- serial leg: moved_batch + tick, then replay (one thread); odd ticks replay the event
+    // pairs, even ticks the per-entity rows (gwaoi_events_csr, built on the GPU and copied)
+    std::vector<double> t_stage, t_tick, t_lat, t_rep1, t_csr, t_repc1;
     uint64_t events = 0;
+    const uint32_t *coff = nullptr, *citems = nullptr;
+    uint64_t cn = 0;
     for (int t = 1; t <= ticks; ++t) {
         const double a = now();
         check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
         const double b = now();
         check(gwaoi_tick(w, &ev), "tick", w);
         const double c = now();
-        replay(S, ev, 0, n);
-        const double d = now();
-        if (t > 1) {  // the first tick sizes the pinned buffers
+        double d, e = 0;
+        if (t % 2) {
+            replay(S, ev, 0, n);
+            d = now();
+        } else {
+            check(gwaoi_events_csr(w, &coff, &citems, &cn), "events_csr", w);
+            e = now();
+            replay_csr(S, coff, citems, 0, n);
+            d = now();
+        }
+        if (t > 2) {  // the first ticks size the pinned buffers
             t_stage.push_back(b - a);
             t_tick.push_back(c - b);
             t_lat.push_back(c - a);
-            t_rep1.push_back(d - c);
+            if (t % 2) {
+                t_rep1.push_back(d - c);
+            } else {
+                t_csr.push_back(e - c);
+                t_repc1.push_back(d - e);
+            }
             events += ev.n_enter + ev.n_leave;
         }
     }
-    // ---- pipelined leg: stage t+1 while the flush of t runs; replay on T threads
-    std::vector<double> p_lat, t_repT;
-    int t = ticks + 1;
-    check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
-    double t_issue = now();
-    const double p0 = now();
-    int done = 0;
-    for (; t < nb; ++t) {
-        check(gwaoi_tick_begin(w), "tick_begin", w);
-        const double issued_next = now();
-        if (t + 1 < nb) check(gwaoi_moved_batch(w, bs[t + 1].data(), bx[t + 1].data(), bz[t + 1].data(), n), "moved_batch", w);
-        check(gwaoi_tick_end(w, &ev), "tick_end", w);
-        const double e = now();
-        p_lat.push_back(e - t_issue);  // from this tick's batch call to its events in host memory
-        t_issue = issued_next;
+    // ---- pipelined leg: while the GPU runs the flush of tick t, the host stages the batch of
+    // t+1 and replays the callbacks of t-1 on T threads (the events of t-1 stay in the pinned
+    // buffer until gwaoi_tick_end(t) replaces them)
+    std::vector<double> p_lat, t_repT, p_host;
+    auto replay_T = [&]() {  // the rows of the last gwaoi_events_csr, T threads over slot ranges
         const double r0 = now();
         std::vector<std::thread> th;
         for (unsigned k = 1; k < T; ++k)
-            th.emplace_back([&, k] { replay(S, ev, (uint32_t)((uint64_t)n * k / T), (uint32_t)((uint64_t)n * (k + 1) / T)); });
-        replay(S, ev, 0, (uint32_t)((uint64_t)n / T));
+            th.emplace_back([&, k] {
+                replay_csr(S, coff, citems, (uint32_t)((uint64_t)n * k / T), (uint32_t)((uint64_t)n * (k + 1) / T));
+            });
+        replay_csr(S, coff, citems, 0, (uint32_t)((uint64_t)n / T));
         for (auto &x : th) x.join();
         t_repT.push_back(now() - r0);
+    };
+    int t = ticks + 1;
+    double t_issue = now();
+    check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
+    const double p0 = now();
+    int done = 0;
+    bool have_prev = false;
+    for (; t < nb; ++t) {
+        check(gwaoi_tick_begin(w), "tick_begin", w);
+        const double h0 = now(), issued_next = h0;
+        if (t + 1 < nb) check(gwaoi_moved_batch(w, bs[t + 1].data(), bx[t + 1].data(), bz[t + 1].data(), n), "moved_batch", w);
+        if (have_prev) replay_T();  // tick t-1's callbacks, overlapping the flush of t
+        p_host.push_back(now() - h0);
+        uint64_t ne_, nl_;
+        check(gwaoi_tick_end_device(w, &ne_, &nl_), "tick_end", w);
+        check(gwaoi_events_csr(w, &coff, &citems, &cn), "events_csr", w);
+        p_lat.push_back(now() - t_issue);  // from this tick's batch call to its rows in host memory
+        have_prev = true;
+        t_issue = issued_next;
         ++done;
     }
+    replay_T();
     const double p_total = now() - p0;
-    const double p_flush = p_total - std::accumulate(t_repT.begin(), t_repT.end(), 0.0);
+    const double p_flush = p_total;
     // sanity: In == By in size, and the sets hold the last flush's relation size
     uint64_t sin = 0, sby = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -225,16 +272,18 @@ int main(int argc, char **argv) {
         "\"serial\": {\"stage_ms_p50\": %.4f, \"tick_ms_p50\": %.4f, \"latency_ms_mean\": %.4f, "
         "\"latency_ms_p50\": %.4f, \"latency_ms_p99\": %.4f}, "
         "\"pipelined\": {\"ms_per_tick\": %.4f, \"moves_per_s\": %.4g, \"latency_ms_p50\": %.4f, "
-        "\"latency_ms_p99\": %.4f, \"ms_per_tick_with_replay\": %.4f, "
-        "\"note\": \"period = wall time per tick minus the T-thread replay (timed separately)\"}, "
-        "\"replay\": {\"ms_1thread_p50\": %.4f, \"ms_%uthreads_p50\": %.4f, \"threads\": %u}, "
+        "\"latency_ms_p99\": %.4f, \"host_ms_p50\": %.4f, "
+        "\"note\": \"per tick: staging of t+1 and the T-thread replay of t-1 (per-entity rows) overlap the flush "
+        "of t; latency = batch call to the rows in pinned host memory\"}, "
+        "\"replay\": {\"pairs_ms_1thread_p50\": %.4f, \"csr_build_copy_ms_p50\": %.4f, "
+        "\"csr_ms_1thread_p50\": %.4f, \"csr_ms_%uthreads_p50\": %.4f, \"threads\": %u}, "
         "\"relation_pairs\": %llu, \"in_eq_by\": %s}\n",
         n, ticks, (unsigned long long)populate, (double)events / std::max<size_t>(1, t_lat.size()),
         pct(t_stage, 50) * ms, pct(t_tick, 50) * ms,
         std::accumulate(t_lat.begin(), t_lat.end(), 0.0) / std::max<size_t>(1, t_lat.size()) * ms,
         pct(t_lat, 50) * ms, pct(t_lat, 99) * ms, p_flush / done * ms, (double)n * done / p_flush,
-        pct(p_lat, 50) * ms, pct(p_lat, 99) * ms, p_total / done * ms, pct(t_rep1, 50) * ms, T,
-        pct(t_repT, 50) * ms, T,
+        pct(p_lat, 50) * ms, pct(p_lat, 99) * ms, pct(p_host, 50) * ms, pct(t_rep1, 50) * ms,
+        pct(t_csr, 50) * ms, pct(t_repc1, 50) * ms, T, pct(t_repT, 50) * ms, T,
         (unsigned long long)sin, sin == sby ? "true" : "false");
     return 0;
 }
