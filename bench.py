@@ -88,15 +88,19 @@ def stage_bytes(n: int, moves: float, cells: int, events: float) -> dict:
             "gather": 120.0 * n, "combined": combined_pass_bytes(n, cells, events), "reorder": 16.0 * events}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_k_combined.json")
+def pmc_file():
+    """the latest round's committed k_combined PMC summary (profiles/rNN_pmc_k_combined.json)"""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_k_combined.json")))
+    return fs[-1] if fs else None
 
 
 def pmc_traffic(workload: str):
     """HBM bytes per k_combined launch from the committed PMC pass
     (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), if one matches."""
     try:
-        d = json.load(open(PMC_FILE))
-    except (OSError, ValueError):
+        d = json.load(open(pmc_file()))
+    except (OSError, ValueError, TypeError):
         return None
     if d.get("workload") != workload:
         return None
@@ -663,6 +667,8 @@ def main():
         s_el = time.perf_counter() - h0
         pb = host_batches[hio + 1:]
         p_lat = []
+        import gc
+        gc.disable()  # no collector pauses inside the timed ticks
         w.moved_batch(*pb[0])
         p0 = issue = time.perf_counter()
         for k in range(len(pb)):
@@ -674,6 +680,7 @@ def main():
             p_lat.append(time.perf_counter() - issue)
             issue = nxt
         p_el = time.perf_counter() - p0
+        gc.enable()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()

@@ -1261,6 +1261,18 @@ int ensure_stage(gwaoi_world *w, size_t words) {
     HIP_TRY(hipHostMalloc((void **)&w->h_stage[h], cap * sizeof(uint32_t), hipHostMallocDefault));
     if (int rc = dalloc(w, &w->d_stage[h], cap)) return rc;
     w->stage_cap[h] = cap;
+    // grow the other half alike while no flush reads it, so that the first flush that stages
+    // into it (the next one begun with gwaoi_tick_begin) does not pay the pinned allocation
+    const int o = h ^ 1;
+    if (!w->in_flight && w->stage_used[o] == 0 && w->stage_cap[o] < cap) {
+        if (w->h_stage[o]) (void)hipHostFree(w->h_stage[o]);
+        w->h_stage[o] = nullptr;
+        dfree(w->d_stage[o]);
+        w->stage_cap[o] = 0;
+        if (hipHostMalloc((void **)&w->h_stage[o], cap * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+            dalloc(w, &w->d_stage[o], cap) == GWAOI_OK)
+            w->stage_cap[o] = cap;
+    }
     return GWAOI_OK;
 }
 

@@ -126,7 +126,8 @@ def main():
               "hbm_read_bytes_per_launch": kc["hbm_read_bytes"], "hbm_write_bytes_per_launch": kc["hbm_write_bytes"],
               "hbm_bytes_per_launch": kc["hbm_bytes"], "steady_median_us": kc.get("steady_median_us"),
               "note": "median over steady-state dispatches; read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE"}
-        with open(os.path.join(os.path.dirname(dst), "r01_pmc_k_combined.json"), "w") as fh:
+        rnd = os.path.basename(dst).split("_")[0]  # profiles/<round>_pmc_k_combined.json
+        with open(os.path.join(os.path.dirname(dst), f"{rnd}_pmc_k_combined.json"), "w") as fh:
             json.dump(pm, fh, indent=1)
     print("\n".join(lines))
 
