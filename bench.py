@@ -65,7 +65,7 @@ def combined_pass_bytes(n: int, total_cells: int, events: float) -> float:
 # the kernels behind each timed stage (the roofline's "kernel")
 STAGE_KERNEL = {"apply": "k_moves_apply+k_moves_fixup", "keygen": "k_keygen",
                 "sort": "k_scan64_reduce/single/down+k_arrive+k_cell_merge", "gather": "k_gather",
-                "combined": "k_combined", "reorder": "k_scan_single+k_reorder"}
+                "combined": "k_combined", "finish": "k_finish"}
 
 
 def stage_bytes(n: int, moves: float, cells: int, events: float) -> dict:
@@ -82,10 +82,10 @@ def stage_bytes(n: int, moves: float, cells: int, events: float) -> dict:
                previous-in-new-order 16 B, candidate 16 B, slot rank 8 B, key
                4 B written: 120 B per entity
       combined see combined_pass_bytes
-      reorder  each directed event pair (8 B) read and written once
+      finish   each directed event pair (8 B) read and written once
     """
     return {"apply": 40.0 * moves, "keygen": 32.0 * n + 8.0 * cells, "sort": 12.0 * n + 16.0 * cells,
-            "gather": 120.0 * n, "combined": combined_pass_bytes(n, cells, events), "reorder": 16.0 * events}
+            "gather": 120.0 * n, "combined": combined_pass_bytes(n, cells, events), "finish": 16.0 * events}
 
 
 def pmc_file():

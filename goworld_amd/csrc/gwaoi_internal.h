@@ -120,11 +120,6 @@ struct TickOut {
 };
 
 // ---- launchers (gwaoi_kernels.hip) ------------------------------------------
-// Zero the per-tick counters and two ranges; bbox entries get the fold
-// identity; S' <- the previous frame's first n_copy entries.
-void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
-                     uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
-                     SlotSp *s_ss, hipStream_t st);
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
                           SlotInfo *info, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
@@ -152,28 +147,43 @@ struct MoveRuns {
     MoveRun r[MAX_MOVE_RUNS];
     uint32_t count;
 };
+// s_ss == nullptr: a moves-only flush without the prologue's copy ("virtual S'":
+// the spaces are the previous frame's, and an entry of S' not written by an op
+// holds an older seq than seq_floor, so k_keygen takes the previous frame's
+// record for it and writes it back).  first_marked: the prologue stored run 0's
+// claims.
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, hipStream_t st);
+                  TickScalars *sc, uint32_t *coll, bool first_marked, hipStream_t st);
+// Zero the per-tick counters and two ranges; bbox entries get the fold
+// identity; S' <- the previous frame's first n_copy entries; and (mark != nullptr)
+// the claims of a moves-only flush's first run.
+void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
+                     uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
+                     SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+                     hipStream_t st);
 
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
 // partials in blk, 2 * cdiv(n, 256) floats).  cnt64 != nullptr (grid
 // unchanged): also per-cell entity counts (low word) and arrival counts
 // (high word; arrival = cell differs from p_key[i], or i >= n_prev).
-void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
+// S' entries i < n_prev whose seq is below seq_base (not written by this flush's
+// ops) take the previous frame's record, written back into s_rec (see launch_moves).
+void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, hipStream_t st);
+                   unsigned long long *cnt64, uint64_t seq_base, hipStream_t st);
 // The stable sort of S' by key when the grid is the previous frame's: the
 // new cell_start (from cnt64) plus, per cell, a merge of the entities that
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
-// frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems.
+// frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
+// look-back status words (zeroed once when allocated); tag: fresh per launch.
 size_t incr_sort_tmp_elems(size_t cells);
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, hipStream_t st);
+                      TickScalars *sc, uint32_t tag, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
@@ -211,15 +221,17 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
 void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t seq_base, TickScalars *sc,
                   uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                   uint32_t tile_off, uint32_t leave_off, hipStream_t st);
-// Copy every tile's events from tmp into tile order (dest = scanned
-// tile_total) and write the flush's TickOut.
-void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
-                    uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
-                    uint32_t n_enter_entries, const TickScalars *sc, TickOut *out, hipStream_t st);
-// Per-space bounding box into the int4 array that follows TickOut: k_gather
-// writes the level-1 parts, this folds them.
+// The flush's tail in one launch: every tile's events from tmp into tile order
+// (offsets by a decoupled look-back; lb: finish_lb_elems(n_entries) status
+// words, tag: a value not used by an earlier launch on the same lb, != 0 mod
+// 2^30), the scalars of TickOut, and the per-space bbox fold (k_gather's parts).
+size_t finish_lb_elems(size_t n_entries);
+void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
+                   uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
+                   uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
+                   uint32_t n_spaces, void *parts_mem, hipStream_t st);
+// Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
-void launch_bbox(uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);
 // Zero `n` uint32 (rare re-run path).

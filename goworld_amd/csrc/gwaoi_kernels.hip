@@ -45,10 +45,17 @@ inline uint32_t cdiv(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 
 // Per-flush start: zero the counters and two ranges, reset the bbox fold,
 // and copy the previous frame into S' (n_copy entries).
+// The claims of a moves-only flush's first Moved run (k_moves_mark) are stored
+// by the same launch (mark.n = 0: none).
 __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t *z1, uint32_t n1, int4 *bbox,
                            uint32_t n_spaces, uint32_t n_copy, const Rec16 *__restrict__ p_rec,
-                           const SlotSp *__restrict__ p_ss, Rec16 *s_rec, SlotSp *s_ss) {
+                           const SlotSp *__restrict__ p_ss, Rec16 *s_rec, SlotSp *s_ss, MoveRun mark,
+                           uint32_t max_slots, SlotInfo *info, uint32_t tick) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < mark.n) {
+        const uint32_t s = mark.ds[i];
+        if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (mark.j0 + i);
+    }
     if (i < n_copy) {
         reinterpret_cast<uint4 *>(s_rec)[i] = reinterpret_cast<const uint4 *>(p_rec)[i];
         reinterpret_cast<uint2 *>(s_ss)[i] = reinterpret_cast<const uint2 *>(p_ss)[i];
@@ -150,7 +157,10 @@ __device__ __forceinline__ unsigned long long op_apply_one(
         return 0;
     }
     st_rec(s_rec, idx, r);
-    if (!keep && sp != cur_sp) st_ss(s_ss, idx, s, sp);
+    if (!keep && sp != cur_sp) {
+        if (s_ss) st_ss(s_ss, idx, s, sp);
+        else atomicOr(&sc->err, ERR_COUNT_MISMATCH);  // moves-only flush (S' spaces = previous frame): bug guard
+    }
     return r.s;
 }
 
@@ -269,12 +279,13 @@ __device__ __forceinline__ uint4 cand_of(const Rec16 &now, const Rec16 &old, flo
 // S' is the previous frame (sorted by the same keys) plus appended entries,
 // so equal keys come in runs and one atomic per run and wave suffices.
 template <bool INCR>
-__global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
+__global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__restrict__ s_ss,
                                                 uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
                                                 uint32_t *keys, uint32_t *vals, const Rec16 *__restrict__ p_rec,
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
-                                                const uint32_t *__restrict__ p_key, unsigned long long *cnt64) {
+                                                const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
+                                                unsigned long long seq_base) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     float dr = 0.0f, bm = 0.0f;
@@ -282,17 +293,23 @@ __global__ __launch_bounds__(256) void k_keygen(const Rec16 *__restrict__ s_rec,
     if (i < n) {
         const uint32_t s = ld_ss(s_ss, i).sp;
         if (s != SP_DEAD) {
-            const Rec16 r = ld_rec(s_rec, i);
+            Rec16 r = ld_rec(s_rec, i);
+            const bool same = i < n_prev && ld_ss(p_ss, i).sp == s;
+            if (same || (i < n_prev && r.s < seq_base)) {
+                const Rec16 p = ld_rec(p_rec, i);
+                if (r.s < seq_base && i < n_prev) {  // not written by this flush's ops: the previous state
+                    if (r.x != p.x || r.z != p.z || r.s != p.s) st_rec(s_rec, i, p);  // (virtual S': no prologue copy)
+                    r = p;
+                }
+                const float D = p_grid[s].D;
+                if (same && is_near(r.x, r.z, p.x, p.z, FAR_FRAC * D))
+                    dr = fmaxf(fabsf(r.x - p.x), fabsf(r.z - p.z)) / D;
+            }
             const SpaceGrid g = grid[s];
             const int cx = cell_of(r.x, g.ox, g.inv, g.gx);
             const int cz = cell_of(r.z, g.oz, g.inv, g.gz);
             key = g.base + (uint32_t)cz * g.gx + (uint32_t)cx;
             bm = fmaxf(fabsf(r.x), fabsf(r.z));
-            if (i < n_prev && ld_ss(p_ss, i).sp == s) {
-                const Rec16 p = ld_rec(p_rec, i);
-                const float D = p_grid[s].D;
-                if (is_near(r.x, r.z, p.x, p.z, FAR_FRAC * D)) dr = fmaxf(fabsf(r.x - p.x), fabsf(r.z - p.z)) / D;
-            }
         }
         keys[i] = key;
         if (!INCR) vals[i] = i;
@@ -601,26 +618,83 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 //   k_arrive         arrivals into per-cell lists (atomic order, fixed later)
 //   k_cell_merge     one lane per cell: sort its arrivals, merge with the stayers
 
-__global__ __launch_bounds__(SC_T) void k_scan64_reduce(const unsigned long long *__restrict__ in, size_t n,
-                                                        unsigned long long *sums) {
-    __shared__ unsigned long long ws[SC_T / WAVE];
-    const size_t base = (size_t)blockIdx.x * SC_TILE + threadIdx.x;  // coalesced: a sum needs no order
-    unsigned long long s = 0;
+// ------------------------------------------------------ look-back scans ------
+// Single-pass scans (decoupled look-back): block b publishes its aggregate,
+// looks back over the status words of the blocks before it until it meets an
+// inclusive prefix, then publishes its own inclusive prefix.  A status word is
+// (tag << 2 | kind) << 32 | value: the tag is fresh per launch (the words are
+// never zeroed per flush; tag 0 = never written), kind 1 = aggregate,
+// 2 = inclusive.  The words are read and written with device-scope atomics.
+// Blocks are dispatched in index order, so the lowest unfinished block always
+// runs and never waits: the walk terminates.
+constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
+
+__device__ __forceinline__ unsigned long long lb_word(uint32_t tag, uint32_t kind, uint32_t v) {
+    return ((unsigned long long)((tag << 2) | kind) << 32) | v;
+}
+
+__device__ __forceinline__ void lb_store(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q) {
-        const size_t i = base + (size_t)q * SC_T;
-        s += i < n ? in[i] : 0ull;
-    }
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+// Sum of the values of blocks 0..b-1 over NW parallel status arrays
+// lb[q * stride + block] (one scan per array; the arrays of one block are
+// published together and read as a unit: a block counts as inclusive only
+// when all its words are).  Called by all 256 threads of the block: thread t
+// reads block j - t of a window, so a walk takes one window per 256 blocks
+// (the predecessors' aggregates are published at once, so a window is ready
+// after about one poll).  excl is valid in every thread.
+template <int NW>
+__device__ void lookback(const unsigned long long *lb, size_t stride, uint32_t b, uint32_t tag, uint32_t (&excl)[NW]) {
+    constexpr int NT = 256;
+    __shared__ int s_near;
+    __shared__ uint32_t s_part[NW][NT / WAVE];
+    const int t = (int)threadIdx.x, w = t / WAVE;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane() == 0) ws[threadIdx.x / WAVE] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < SC_T / WAVE; ++w) t += ws[w];
-        sums[blockIdx.x] = t;
+    for (int q = 0; q < NW; ++q) excl[q] = 0;
+    for (int j = (int)b - 1; j >= 0; j -= NT) {
+        const int idx = j - t;
+        unsigned long long wd[NW];
+        uint32_t kind = LB_INCL;
+        if (t == 0) s_near = NT;
+        for (;;) {
+            bool ok = true;
+            kind = LB_INCL;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                wd[q] = idx >= 0 ? __hip_atomic_load(lb + q * stride + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : lb_word(tag, LB_INCL, 0u);
+                const uint32_t hi = (uint32_t)(wd[q] >> 32);
+                ok = ok && (hi >> 2) == tag && (hi & 3u) != 0u;
+                if (q == 0) kind = hi & 3u;
+                else ok = ok && (hi & 3u) == kind;  // aggregate and inclusive words never mixed
+            }
+            if (__syncthreads_and(ok)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (kind == LB_INCL) atomicMin(&s_near, t);  // LDS: the nearest inclusive prefix ends the walk
+        __syncthreads();
+        const int m = s_near;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            const uint32_t v = wave_sum_u32(t <= m ? (uint32_t)wd[q] : 0u);
+            if (lane() == 0) s_part[q][w] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+            for (int i = 0; i < NT / WAVE; ++i) excl[q] += s_part[q][i];
+        __syncthreads();  // s_near / s_part are reused by the next window
+        if (m < NT) return;
     }
 }
+
 
 __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long x) {
 #pragma unroll
@@ -649,39 +723,54 @@ __device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long lo
     return pre + x - v;
 }
 
-// one workgroup: exclusive scan of the block sums in place (and, in the same
-// launch, the fold of keygen's d_rel / bmax partials)
-__global__ __launch_bounds__(1024) void k_scan64_single(unsigned long long *a, size_t n, const float *blk,
-                                                        uint32_t nbk, TickScalars *sc) {
-    if (blk) {
-        keygen_fold(blk, nbk, sc);
-        __syncthreads();
-    }
-    __shared__ unsigned long long ws[1024 / WAVE];
-    unsigned long long carry = 0;
-    for (size_t c0 = 0; c0 < n; c0 += 1024) {
-        const size_t i = c0 + threadIdx.x;
-        const unsigned long long v = i < n ? a[i] : 0ull;
-        unsigned long long tot;
-        const unsigned long long e = block_excl_scan64<1024>(v, ws, tot);
-        if (i < n) a[i] = e + carry;
-        carry += tot;
-        __syncthreads();
-    }
-}
 
 // LDS tile index with one pad word per 16: a thread's 16 consecutive words
 // (stride 17) and a wave's coalesced row (stride 1) are both conflict-free.
 __device__ __forceinline__ uint32_t p64(uint32_t i) { return i + (i >> 4); }
 
-// exclusive scan, split: lo[i] = low words, hi[i] = high words.  Global
-// loads and stores are coalesced; the per-thread runs go through LDS.
-__global__ __launch_bounds__(SC_T) void k_scan64_down(const unsigned long long *__restrict__ in, size_t n,
-                                                      const unsigned long long *__restrict__ block_off, uint32_t *lo,
-                                                      uint32_t *hi) {
+
+// Single-pass form of reduce + single + down (one launch): exclusive scan of
+// the packed (lo = entities, hi = arrivals) cell counts into lo[] / hi[]; the
+// block offsets come from a look-back over lb[0 .. nb) (lo) and lb[nb .. 2nb)
+// (hi).  The extra block nb folds keygen's d_rel / bmax partials.
+__device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
+    __shared__ float s_m[2][SC_T / WAVE];
+    float a = 0.0f, b = 0.0f;
+    for (uint32_t i = threadIdx.x; i < nb; i += SC_T) {
+        a = fmaxf(a, blk[2 * i]);
+        b = fmaxf(b, blk[2 * i + 1]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a = fmaxf(a, __shfl_xor(a, o));
+        b = fmaxf(b, __shfl_xor(b, o));
+    }
+    if (lane() == 0) {
+        s_m[0][threadIdx.x / WAVE] = a;
+        s_m[1][threadIdx.x / WAVE] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < SC_T / WAVE; ++q) {
+            a = fmaxf(a, s_m[0][q]);
+            b = fmaxf(b, s_m[1][q]);
+        }
+        sc->d_rel = a;
+        sc->bmax = b;
+    }
+}
+
+__global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
+                                                    unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
+                                                    const float *__restrict__ blk, uint32_t nbk, TickScalars *sc) {
+    if (blockIdx.x == nb) {
+        keygen_fold256(blk, nbk, sc);
+        return;
+    }
     __shared__ unsigned long long tile[SC_TILE + SC_TILE / 16];
     __shared__ unsigned long long ws[SC_T / WAVE];
-    const size_t base = (size_t)blockIdx.x * SC_TILE;
+    const uint32_t b = blockIdx.x;
+    const size_t base = (size_t)b * SC_TILE;
     const uint32_t tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < SC_I; ++q) {
@@ -697,7 +786,21 @@ __global__ __launch_bounds__(SC_T) void k_scan64_down(const unsigned long long *
         s += v[q];
     }
     unsigned long long tot;
-    unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot) + block_off[blockIdx.x];
+    unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot);
+    if (tid == 0) {
+        const uint32_t k = b == 0 ? LB_INCL : LB_AGG;
+        lb_store(lb + b, lb_word(tag, k, (uint32_t)tot));
+        lb_store(lb + nb + b, lb_word(tag, k, (uint32_t)(tot >> 32)));
+    }
+    uint32_t ex[2] = {0u, 0u};
+    if (b) lookback<2>(lb, nb, b, tag, ex);
+    const unsigned long long e = ((unsigned long long)ex[1] << 32) | ex[0];
+    if (tid == 0 && b) {
+        const unsigned long long t = e + tot;
+        lb_store(lb + b, lb_word(tag, LB_INCL, (uint32_t)t));
+        lb_store(lb + nb + b, lb_word(tag, LB_INCL, (uint32_t)(t >> 32)));
+    }
+    run += e;
 #pragma unroll
     for (int q = 0; q < SC_I; ++q) {  // a thread rewrites only the words it read
         tile[p64(tid * SC_I + (uint32_t)q)] = run;
@@ -862,7 +965,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            int (&bv)[4]);
 
 // One thread per new-frame entry; the block also folds its entries' bbox
-// (level 1 of the per-space bounding box, k_bbox_parts is level 2).
+// (level 1 of the per-space bounding box, k_finish folds level 2).
 __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
@@ -1506,7 +1609,9 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c0 = cell_of(A.x - hi - M, g.ox, g.inv, g.gx);
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
+#ifndef GWAOI_EXP_NOZ  // timing experiment only: skip the Z strip (events wrong)
         sweep_rows<0>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#endif
         // X' strip: rows holding z in [z-lo, z+lo], cells holding x in [x+lo, x+hi]
         r0 = 0, r1 = -1, c0 = 0, c1 = -1;
         if (strip) {
@@ -1515,7 +1620,9 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c0 = cell_of(A.x + lo - M, g.ox, g.inv, g.gx);
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
+#ifndef GWAOI_EXP_NOX  // timing experiment only: skip the X' strip (events wrong)
         sweep_rows<1>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#endif
     }
     if (__ballot(whole)) {
         const float r = hi + M;
@@ -1669,57 +1776,116 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     }
 }
 
-// one wave per tile entry, grid-strided
-__global__ __launch_bounds__(256) void k_reorder(const uint32_t *__restrict__ dest,
-                                                 const uint32_t *__restrict__ tile_total,
-                                                 const unsigned long long *__restrict__ tile_base,
-                                                 uint32_t n_entries, const uint2 *__restrict__ tmp, uint2 *out,
-                                                 uint64_t cap, uint32_t n_enter_entries,
-                                                 const TickScalars *__restrict__ sc, TickOut *res) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the flush's totals (dest is the finished scan)
-        res->n_enter = dest[n_enter_entries];
-        res->n_total = dest[n_entries];
-        res->err = sc->err;
-        res->total64 = sc->counter;
-        res->seq_max = sc->seq_max;
-        for (int q = 0; q < (int)DBG_N; ++q) res->dbg[q] = sc->dbg[q];
-    }
-    const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
-    for (uint32_t e = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; e < n_entries; e += waves) {
-        const uint32_t cnt = tile_total[e];
-        if (!cnt) continue;
-        const unsigned long long src = tile_base[e];
-        const uint64_t dst = dest[e];
-        for (uint32_t k = lane(); k < cnt; k += WAVE)
-            if (src + k < cap && dst + k < cap) out[dst + k] = tmp[src + k];
-    }
-}
+// ------------------------------------------------------------- finish ------
+// The flush's tail in one launch (it was three: a scan of the tile totals,
+// the tile copy and the bbox fold).  Blocks 0..R-1 take FT consecutive tile
+// entries each; a block's output offset is the sum of the tile totals before
+// it, found by a decoupled look-back over the blocks before it: each block
+// publishes its aggregate, then its inclusive prefix, in a 64-bit status
+// word tagged with the launch (so nothing is zeroed per flush).  Block R
+// folds the bbox parts and writes the scalars of TickOut.
+#ifndef GWAOI_FT
+#define GWAOI_FT 16  // measured: 16 -> 15.6 us, 32 -> 19.0, 64 -> 25.3 (cfg3)
+#endif
+constexpr int FT = GWAOI_FT;  // tile entries per finish block (<= 64: one wave scans them)
+static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 
-
-// Level 2: one workgroup folds the level-1 parts (space-sorted).
-__global__ __launch_bounds__(BB_T) void k_bbox_parts(const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
-                                                     uint32_t ns, BBoxPart *out) {
-    const uint32_t per = (np + BB_T - 1) / BB_T;
-    const uint32_t p0 = threadIdx.x * per, p1 = min(p0 + per, np);
-    uint32_t cur = SP_DEAD;
-    int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
-    for (uint32_t p = p0; p < p1; ++p) {
-        const BBoxPart q = parts[p];
-        if (q.sp == SP_DEAD) continue;
-        if (q.sp != cur) {
-            if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
-            cur = q.sp;
-            v[0] = v[1] = INT_MAX;
-            v[2] = v[3] = INT_MIN;
+__global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ tile_total,
+                                                const unsigned long long *__restrict__ tile_base, uint32_t n_entries,
+                                                uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag,
+                                                const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap,
+                                                const TickScalars *__restrict__ sc, TickOut *res,
+                                                const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
+                                                uint32_t ns) {
+    const uint32_t b = blockIdx.x, R = gridDim.x - 1;
+    if (b == R) {  // scalars + bbox fold (level 2 of the per-space bounding box)
+        if (threadIdx.x == 0) {
+            res->err = sc->err;
+            res->total64 = sc->counter;
+            res->seq_max = sc->seq_max;
+            for (int q = 0; q < (int)DBG_N; ++q) res->dbg[q] = sc->dbg[q];
+            if (n_entries == 0) res->n_enter = res->n_total = 0;
         }
-        v[0] = min(v[0], q.v[0]);
-        v[1] = min(v[1], q.v[1]);
-        v[2] = max(v[2], q.v[2]);
-        v[3] = max(v[3], q.v[3]);
+        const uint32_t per = (np + BB_T - 1) / BB_T;
+        const uint32_t p0 = threadIdx.x * per, p1 = min(p0 + per, np);
+        uint32_t cur = SP_DEAD;
+        int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+        for (uint32_t p = p0; p < p1; ++p) {
+            const BBoxPart q = parts[p];
+            if (q.sp == SP_DEAD) continue;
+            if (q.sp != cur) {
+                if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
+                cur = q.sp;
+                v[0] = v[1] = INT_MAX;
+                v[2] = v[3] = INT_MIN;
+            }
+            v[0] = min(v[0], q.v[0]);
+            v[1] = min(v[1], q.v[1]);
+            v[2] = max(v[2], q.v[2]);
+            v[3] = max(v[3], q.v[3]);
+        }
+        BBoxPart *fold = const_cast<BBoxPart *>(parts) + np;
+        bbox_block(cur, v, bbox, ns, fold);
+        __syncthreads();
+        if (threadIdx.x == 0 && fold->sp != SP_DEAD) bbox_flush(bbox, ns, fold->sp, fold->v);
+        return;
     }
-    bbox_block(cur, v, bbox, ns, out);
+    __shared__ uint32_t s_off[FT + 1];
+    __shared__ unsigned long long s_src[FT];
+    const uint32_t e0 = b * FT;
+    __shared__ uint32_t s_agg;
+    uint32_t cnt = 0, incl = 0;
+    if (threadIdx.x < WAVE) {
+        const uint32_t l = lane(), e = e0 + l;
+        cnt = l < (uint32_t)FT && e < n_entries ? tile_total[e] : 0u;
+        incl = wave_incl_scan(cnt);
+        const uint32_t agg = __shfl(incl, WAVE - 1);
+        if (l == 0) {
+            lb_store(lb + b, lb_word(tag, b == 0 ? LB_INCL : LB_AGG, agg));
+            s_agg = agg;
+        }
+    }
+    uint32_t ex[1] = {0u};
+    if (b) lookback<1>(lb, 0, b, tag, ex);  // (its barriers also publish s_agg)
     __syncthreads();
-    if (threadIdx.x == 0 && out->sp != SP_DEAD) bbox_flush(bbox, ns, out->sp, out->v);
+    const uint32_t excl = ex[0], agg = s_agg;
+    if (threadIdx.x == 0 && b != 0) lb_store(lb + b, lb_word(tag, LB_INCL, excl + agg));
+    if (threadIdx.x < WAVE) {
+        const uint32_t l = lane(), e = e0 + l;
+        const uint32_t off = excl + incl - cnt;
+        if (l < (uint32_t)FT) {
+            s_off[l] = off;
+            s_src[l] = e < n_entries ? tile_base[e] : 0ull;
+            if (e == n_enter_entries) res->n_enter = off;
+        }
+        if (l == 0) s_off[FT] = excl + agg;
+        if (b == R - 1 && l == 0) res->n_total = excl + agg;
+    }
+    __syncthreads();
+    // the block's tiles fill one contiguous output range: every thread takes
+    // positions tid, tid + 256, ... (increasing, so its tile index only moves
+    // forward); FU positions per thread in flight: the loads before the stores
+    constexpr int FU = 8;
+    const uint32_t o0 = s_off[0], o1 = s_off[FT];
+    uint32_t t = 0;
+    for (uint32_t p0 = o0 + threadIdx.x; p0 < o1; p0 += FU * blockDim.x) {
+        uint2 v[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const uint32_t p = p0 + (uint32_t)u * blockDim.x;
+            v[u] = make_uint2(0u, 0u);
+            if (p < o1) {
+                while (s_off[t + 1] <= p) ++t;  // last tile t with s_off[t] <= p (s_off[FT] = o1 > p)
+                const unsigned long long src = s_src[t] + (p - s_off[t]);
+                if (src < cap) v[u] = tmp[src];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const uint32_t p = p0 + (uint32_t)u * blockDim.x;
+            if (p < o1 && p < cap) out[p] = v[u];
+        }
+    }
 }
 
 // ------------------------------------------------------------ neighbors ------
@@ -1801,10 +1967,13 @@ void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_to
 
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
                      uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
-                     SlotSp *s_ss, hipStream_t st) {
-    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, (size_t)n_copy, 1});
+                     SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+                     hipStream_t st) {
+    MoveRun mk{};
+    if (mark) mk = *mark;
+    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, (size_t)n_copy, (size_t)mk.n, 1});
     k_prologue<<<cdiv(m, 256), 256, 0, st>>>(sc, z0, (uint32_t)n0, z1, (uint32_t)n1, bbox, n_spaces, n_copy, p_rec,
-                                             p_ss, s_rec, s_ss);
+                                             p_ss, s_rec, s_ss, mk, max_slots, info, tick_id);
 }
 
 void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
@@ -1820,8 +1989,8 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, hipStream_t st) {
-    for (uint32_t q = 0; q < RS.count; ++q)  // every run's claims before any apply
+                  TickScalars *sc, uint32_t *coll, bool first_marked, hipStream_t st) {
+    for (uint32_t q = first_marked ? 1u : 0u; q < RS.count; ++q)  // every run's claims before any apply
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
@@ -1846,34 +2015,34 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
                                               seq_floor, track_max ? 1 : 0, s_rec, s_ss, sc);
 }
 
-void launch_keygen(const Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
+void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, hipStream_t st) {
+                   unsigned long long *cnt64, uint64_t seq_base, hipStream_t st) {
     if (!n_total) return;  // the prologue left d_rel = bmax = 0
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64);  // folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr);
+                                            n_prev, blk, nullptr, nullptr, seq_base);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }
 
-size_t incr_sort_tmp_elems(size_t cells) { return (size_t)cdiv(cells + 1, SC_TILE) + 1; }
+// look-back status words: lo and hi per block
+size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, SC_TILE) + 1); }
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, hipStream_t st) {
+                      TickScalars *sc, uint32_t tag, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, SC_TILE);
-    k_scan64_reduce<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
-    k_scan64_single<<<1, 1024, 0, st>>>(tmp, nb, blk, cdiv(n_total, 256), sc);
-    k_scan64_down<<<nb, SC_T, 0, st>>>(cnt64, m, tmp, cell_start, arr_pos);
+    k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
+                                         cdiv(n_total, 256), sc);
     if (n_total) k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
                                                          n_new, n_total, sentinel, perm, skeys);
@@ -1958,23 +2127,20 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg);
 }
 
-void launch_reorder(const uint32_t *dest, const uint32_t *tile_total, const unsigned long long *tile_base,
-                    uint32_t n_entries, const uint32_t *tmp_pairs, uint32_t *out_pairs, uint64_t cap,
-                    uint32_t n_enter_entries, const TickScalars *sc, TickOut *out, hipStream_t st) {
-    const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>(cdiv(n_entries, 256 / WAVE), 2048));
-    k_reorder<<<blocks, 256, 0, st>>>(dest, tile_total, tile_base, n_entries,
-                                      reinterpret_cast<const uint2 *>(tmp_pairs),
-                                      reinterpret_cast<uint2 *>(out_pairs), cap, n_enter_entries, sc, out);
-}
+size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }
 
+void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
+                   uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
+                   uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
+                   uint32_t n_spaces, void *parts_mem, hipStream_t st) {
+    const uint32_t R = cdiv(n_entries, FT);
+    const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
+    k_finish<<<R + 1, 256, 0, st>>>(tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu,
+                                    reinterpret_cast<const uint2 *>(tmp_pairs), reinterpret_cast<uint2 *>(out_pairs),
+                                    cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox, n_spaces);
+}
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }
-
-void launch_bbox(uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, hipStream_t st) {
-    BBoxPart *parts = reinterpret_cast<BBoxPart *>(parts_mem);
-    const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
-    k_bbox_parts<<<1, BB_T, 0, st>>>(parts, np, bbox, n_spaces, parts + np);
-}
 
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st) {

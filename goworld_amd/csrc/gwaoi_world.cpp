@@ -32,10 +32,9 @@ using gw::SpaceGrid;
 
 namespace {
 
-enum Stage { ST_APPLY, ST_KEYGEN, ST_SORT, ST_GATHER, ST_CELLS, ST_COMBINED, ST_SPECIAL, ST_REORDER, ST_BBOX,
-             ST_D2H, ST_N };
-const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",    "gather", "cells",
-                                 "combined", "special", "reorder", "bbox",   "d2h"};
+enum Stage { ST_APPLY, ST_KEYGEN, ST_SORT, ST_GATHER, ST_CELLS, ST_COMBINED, ST_SPECIAL, ST_FINISH, ST_D2H, ST_N };
+const char *kStageNames[ST_N] = {"apply",    "keygen",  "sort",   "gather", "cells",
+                                 "combined", "special", "finish", "d2h"};
 
 struct DevFrame {
     gw::Rec16 *rec = nullptr;
@@ -167,6 +166,7 @@ struct gwaoi_world {
     // working set (max_slots entries each)
     gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
     gw::SlotSp *sss = nullptr;
+    const gw::SlotSp *s_ss_view = nullptr;  // this flush's S' spaces: sss, or the previous frame's (virtual S')
     gw::Rec16 *orec = nullptr;  // previous state in the new frame's order (NaN if absent)
     uint4 *cand = nullptr;      // combined-pass candidate records of the new frame (x, z, old x, old z; NaN = jumper)
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
@@ -180,6 +180,7 @@ struct gwaoi_world {
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
     size_t cnt64_cap = 0;
     bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
+    bool force_copy = false;   // GWAOI_FORCE_COPY=1: S' always copied by the prologue (A/B check of virtual S')
     bool inject_regrow_fail = false;  // GWAOI_INJECT_REGROW_FAIL=1 (tests): the event regrow fails
     // End-of-flush wait: poll an event (default) or block in hipStreamSynchronize
     // (GWAOI_BLOCKING_SYNC=1, A/B check).
@@ -193,7 +194,9 @@ struct gwaoi_world {
     uint32_t *events = nullptr;      // ev_cap (a,b) pairs: [enters | leaves] in tile order
     uint32_t *events_tmp = nullptr;  // ev_cap pairs: per-tile chunks at reserved offsets
     uint64_t ev_cap = 0;             // capacity in directed pairs
-    uint32_t *tile_total = nullptr, *tile_dest = nullptr;
+    uint32_t *tile_total = nullptr;
+    unsigned long long *tile_lb = nullptr;  // k_finish look-back status words
+    uint32_t lb_tag = 0;  // look-back launches so far (tags: k_finish, the incremental sort's scan)
     unsigned long long *tile_base = nullptr;
     size_t tile_entries_cap = 0;
     gw::TickScalars *sc = nullptr;
@@ -388,14 +391,15 @@ int ensure_tile_entries(gwaoi_world *w, size_t entries) {
     size_t cap = std::max<size_t>(entries + 1 + entries / 4, 1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->tile_total);
-    dfree(w->tile_dest);
+    dfree(w->tile_lb);
     dfree(w->tile_base);
     int rc;
-    if ((rc = dalloc(w, &w->tile_total, cap)) || (rc = dalloc(w, &w->tile_dest, cap)) ||
+    if ((rc = dalloc(w, &w->tile_total, cap)) || (rc = dalloc(w, &w->tile_lb, gw::finish_lb_elems(cap))) ||
         (rc = dalloc(w, &w->tile_base, cap))) {
         w->tile_entries_cap = 0;
         return rc;
     }
+    HIP_TRY(hipMemsetAsync(w->tile_lb, 0, gw::finish_lb_elems(cap) * sizeof(unsigned long long), w->stream));  // tag 0: never current
     w->tile_entries_cap = cap;
     return GWAOI_OK;
 }
@@ -443,6 +447,7 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, cap)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
+    HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
     w->cnt64_cap = cap;
     return GWAOI_OK;
 }
@@ -655,6 +660,12 @@ int4 *dev_bbox(gwaoi_world *w) { return reinterpret_cast<int4 *>(w->dev_out + si
 // Pair passes + deterministic reorder.  Block-total entries: [enter totals:
 // new-frame blocks | previous-frame blocks] then [leave totals: same order];
 // their exclusive scan is the final layout [enters | leaves] in block order.
+// A look-back tag not used by an earlier launch (tags are 30 bits; 0 = never written).
+uint32_t next_lb_tag(gwaoi_world *w) {
+    if (++w->lb_tag % 0x40000000u == 0) ++w->lb_tag;
+    return w->lb_tag;
+}
+
 void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_base) {
     hipStream_t st = w->stream;
     const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = gw::combined_blocks(P.n);
@@ -666,14 +677,15 @@ void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_
     gw::launch_combined(Vn, w->cand, w->orec, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
                         half, st, tc ? w->ev[ST_COMBINED][0] : nullptr, tc ? w->ev[ST_COMBINED][1] : nullptr);
     stage_begin(w, ST_SPECIAL);
-    gw::launch_pairs(Vp, w->srec, w->sss, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
+    gw::launch_pairs(Vp, w->srec, w->s_ss_view, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
                      TBn, half, st);
     stage_end(w, ST_SPECIAL);
-    stage_begin(w, ST_REORDER);
-    gw::scan_exclusive(w->tile_total, w->tile_dest, (size_t)entries + 1, w->scan_tmp, st);
-    gw::launch_reorder(w->tile_dest, w->tile_total, w->tile_base, entries, w->events_tmp, w->events, w->ev_cap, half,
-                       w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), st);
-    stage_end(w, ST_REORDER);
+    // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
+    stage_begin(w, ST_FINISH);
+    gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, w->events,
+                      w->ev_cap, w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), Fn.n, dev_bbox(w),
+                      w->n_space_ids, w->bbox_parts, st);
+    stage_end(w, ST_FINISH);
 }
 
 int poison(gwaoi_world *w, int rc) {
@@ -736,24 +748,14 @@ int tick_launch(gwaoi_world *w) {
         HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
         w->copy_pending = false;
     }
-    // counters, tile totals, bbox fold; S' <- the previous frame (the ops apply onto it)
-    if (incr)
-        gw::launch_prologue(w->sc, reinterpret_cast<uint32_t *>(w->cnt64), 2 * ((size_t)total_cells + 1), w->tile_total,
-                            entries + 1, dev_bbox(w), w->n_space_ids, n_prev, P.rec, P.ss, w->srec, w->sss, st);
-    else
-        gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
-                            w->n_space_ids, n_prev, P.rec, P.ss, w->srec, w->sss, st);
-
-    // ---- apply queued ops onto S' = copy of the previous frame
-    stage_begin(w, ST_APPLY);
-    if (n_app) {
-        HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
-                               hipMemcpyHostToDevice, st));
-        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->sinfo, st);
-    }
     const bool moves_only = n_ops && host_ops == 0 && w->runs.size() <= gw::MAX_MOVE_RUNS && n_ops <= w->max_slots;
-    if (moves_only) {  // the per-tick position sync: one pass + fixup of repeated slots
-        gw::MoveRuns RS{};
+    // Virtual S': a flush of Moved batches only (or of nothing) changes no space and appends
+    // no entry, so S' needs no copy of the previous frame: its spaces ARE the previous frame's,
+    // and the records no op wrote are taken from the previous frame by k_keygen (seq check).
+    const bool virt = n_app == 0 && host_ops == 0 && (moves_only || n_ops == 0) && !w->force_copy;
+    w->s_ss_view = virt ? P.ss : w->sss;
+    gw::MoveRuns RS{};
+    if (moves_only) {
         uint32_t j0 = 0;
         for (const Run &r : w->runs) {
             gw::MoveRun &m = RS.r[RS.count++];
@@ -761,8 +763,30 @@ int tick_launch(gwaoi_world *w) {
             m.j0 = j0; m.n = (uint32_t)r.dn;
             j0 += (uint32_t)r.dn;
         }
-        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, w->srec, w->sss, P.rec, n_prev,
-                         w->sc, w->coll, st);
+    }
+    // counters, tile totals, bbox fold identity; S' <- the previous frame unless virtual; the
+    // first Moved run's claims
+    const gw::MoveRun *mark = moves_only ? &RS.r[0] : nullptr;
+    const uint32_t n_copy = virt ? 0u : n_prev;
+    if (incr)
+        gw::launch_prologue(w->sc, reinterpret_cast<uint32_t *>(w->cnt64), 2 * ((size_t)total_cells + 1), w->tile_total,
+                            entries + 1, dev_bbox(w), w->n_space_ids, n_copy, P.rec, P.ss, w->srec, w->sss, mark,
+                            w->max_slots, w->sinfo, tick_id, st);
+    else
+        gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
+                            w->n_space_ids, n_copy, P.rec, P.ss, w->srec, w->sss, mark, w->max_slots, w->sinfo,
+                            tick_id, st);
+
+    // ---- apply queued ops onto S'
+    stage_begin(w, ST_APPLY);
+    if (n_app) {
+        HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, st));
+        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->sinfo, st);
+    }
+    if (moves_only) {  // the per-tick position sync: one pass + fixup of repeated slots
+        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, w->srec, virt ? nullptr : w->sss,
+                         P.rec, n_prev, w->sc, w->coll, true, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -807,15 +831,15 @@ int tick_launch(gwaoi_world *w) {
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, ST_KEYGEN);
-    gw::launch_keygen(w->srec, w->sss, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, w->sc, P.key, incr ? w->cnt64 : nullptr, st);
+    gw::launch_keygen(w->srec, w->s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
+                      n_prev, w->blk, w->sc, P.key, incr ? w->cnt64 : nullptr, seq_base, st);
     stage_end(w, ST_KEYGEN);
     stage_begin(w, ST_SORT);
     int which = 1;
     if (incr) {
         gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             w->keys[1], w->blk, w->sc, st);
+                             w->keys[1], w->blk, w->sc, next_lb_tag(w), st);
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -832,7 +856,7 @@ int tick_launch(gwaoi_world *w) {
 
     // ---- new frame + previous state in the new order
     stage_begin(w, ST_GATHER);
-    gw::launch_gather(perm, n_new, n_prev, w->srec, w->sss, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
+    gw::launch_gather(perm, n_new, n_prev, w->srec, w->s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
                       total_cells, n_total, w->sc, Fn.key, dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
     stage_end(w, ST_GATHER);
@@ -849,10 +873,6 @@ int tick_launch(gwaoi_world *w) {
     // ---- pair passes: combined over the new grid, special entities over the previous one
     launch_pair_passes(w, Fn, P, seq_base);
 
-    // ---- per-space bounding boxes for the next flush's grid
-    stage_begin(w, ST_BBOX);
-    gw::launch_bbox(n_new, dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
-    stage_end(w, ST_BBOX);
     // from here on the device has rewritten SlotInfo for the new frame: any failure before the
     // commit below leaves the world inconsistent (poisoned)
     if (hipGetLastError() != hipSuccess) {
@@ -1039,7 +1059,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_dest); dfree(w->tile_base);
+    dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items);
@@ -1077,6 +1097,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 4.0f;
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
+    if (const char *e = std::getenv("GWAOI_FORCE_COPY")) w->force_copy = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_INJECT_REGROW_FAIL")) w->inject_regrow_fail = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_STAGE_THREADS")) w->stage_threads = (unsigned)std::max(1, std::atoi(e));
     int rc = GWAOI_OK;
@@ -1124,8 +1145,9 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, (char **)&w->bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
         (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
-    // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
-    if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
+    // lastop = 0, rank = sp = 0xFFFFFFFF (not live); S' records seq 0 (virtual S': never "written")
+    if (hipMemset(w->srec, 0, N * sizeof(gw::Rec16)) != hipSuccess ||
+        hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
         hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);

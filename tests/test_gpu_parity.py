@@ -585,6 +585,115 @@ def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
         wi.close()
 
 
+def test_virtual_sprime_equals_copied_sprime_gpu(monkeypatch):
+    """A flush of Moved batches only skips the prologue's copy of the previous
+    frame (k_keygen takes the records no op wrote from the previous frame, by
+    their seq).  Its event arrays -- order included -- and neighbour rows equal
+    those of the copying path (GWAOI_FORCE_COPY=1) over: partial batches (most
+    entities unmoved), repeated slots across two batches (fixup), an empty
+    flush, a batch with a stale explicit seq (op dropped, flush reports it),
+    and host Enter/Leave flushes (which copy) between moves-only ones."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(77)
+    wl = make_workload("cfg3", n=30000)
+    slots, x0, z0, _ = wl.initial()
+    n = wl.n
+    monkeypatch.setenv("GWAOI_FORCE_COPY", "1")
+    wc = World(n + 200)
+    monkeypatch.delenv("GWAOI_FORCE_COPY")
+    wv = World(n + 200)
+
+    def both(fn):
+        outs = []
+        for w in (wc, wv):
+            fn(w)
+            try:
+                outs.append((w.tick(), None))
+            except GwaoiError as e:
+                outs.append((e.events, e.code))
+        ((ec, lc), cc), ((ev, lv), cv) = outs
+        assert cc == cv
+        np.testing.assert_array_equal(ec, ev)
+        np.testing.assert_array_equal(lc, lv)
+        return ec.shape[0] + lc.shape[0]
+
+    def dev(*arrs):
+        t = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+        torch.cuda.synchronize()
+        keep.append(t)
+        return t
+
+    keep = []
+    try:
+        for w in (wc, wv):
+            s = w.space_create(wl.D)
+            w.enter_batch(s, slots, x0, z0)
+            w.tick()
+        x, z = x0.copy(), z0.copy()
+        live = np.ones(n + 200, bool)
+        live[n:] = False
+        total = 0
+        for t in range(8):
+            kind = t % 4
+            if kind == 0:  # a third of the live entities move, in a device batch
+                sl = rng.choice(np.nonzero(live)[0], int(live.sum()) // 3, replace=False).astype(np.uint32)
+                nx = (x[sl] + rng.uniform(-1, 1, sl.size)).astype(np.float32)
+                nz = (z[sl] + rng.uniform(-1, 1, sl.size)).astype(np.float32)
+                d = dev(sl.astype(np.int32), nx, nz)
+                total += both(lambda w: w.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                                                             sl.size))
+                x[sl], z[sl] = nx, nz
+            elif kind == 1:  # two batches with repeated slots (collision fixup), then an empty flush
+                pool = np.nonzero(live)[0]
+                runs = []
+                for r in range(2):
+                    sl = rng.choice(pool[:400] if r else pool, 3000).astype(np.uint32)
+                    nx = (x[sl] + rng.uniform(-40, 40, sl.size)).astype(np.float32)
+                    nz = (z[sl] + rng.uniform(-40, 40, sl.size)).astype(np.float32)
+                    runs.append((sl, dev(sl.astype(np.int32), nx, nz)))
+                    x[sl], z[sl] = nx, nz
+
+                def issue(w):
+                    for sl, d in runs:
+                        w.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sl.size)
+                total += both(issue)
+                assert both(lambda w: None) == 0
+            elif kind == 2:  # explicit seqs, one of them stale: that op is dropped, the flush reports it
+                floors = {wc.info()["next_seq"], wv.info()["next_seq"]}
+                assert len(floors) == 1
+                floor = floors.pop()
+                sl = rng.choice(np.nonzero(live)[0], 2000, replace=False).astype(np.uint32)
+                nx = (x[sl] + rng.uniform(-2, 2, sl.size)).astype(np.float32)
+                nz = (z[sl] + rng.uniform(-2, 2, sl.size)).astype(np.float32)
+                sq = (floor + np.arange(sl.size)).astype(np.int64)
+                sq[7] = floor - 1
+                d = dev(sl.astype(np.int32), nx, nz, sq)
+                total += both(lambda w: w.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                                                             sl.size, d_seq=d[3].data_ptr()))
+                keep_op = np.ones(sl.size, bool)
+                keep_op[7] = False
+                x[sl[keep_op]], z[sl[keep_op]] = nx[keep_op], nz[keep_op]
+            else:  # host Leaves and Enters (the copying path) plus plain moves
+                out = rng.choice(np.nonzero(live)[0], 100, replace=False)
+                inn = rng.choice(np.nonzero(~live)[0], 100, replace=False)
+                ex = rng.uniform(-wl.L / 4, wl.L / 4, 100).astype(np.float32)
+                ez = rng.uniform(-wl.L / 4, wl.L / 4, 100).astype(np.float32)
+
+                def churn(w):
+                    w.leave_batch(out)
+                    w.enter_batch(0, inn.astype(np.uint32), ex, ez)
+                total += both(churn)
+                live[out] = False
+                live[inn] = True
+                x[inn], z[inn] = ex, ez
+        assert total > 0
+        for i in rng.choice(np.nonzero(live)[0], 50, replace=False):
+            np.testing.assert_array_equal(wc.neighbors(int(i)), wv.neighbors(int(i)))
+    finally:
+        wc.close()
+        wv.close()
+
+
 def test_committed_events_delivered_on_device_error_gpu():
     """A flush whose device batch held a bad op (here an explicit seq below the
     flush's floor) commits without that op and reports the problem; its other
