@@ -629,7 +629,8 @@ def test_virtual_sprime_equals_copied_sprime_gpu(monkeypatch):
             s = w.space_create(wl.D)
             w.enter_batch(s, slots, x0, z0)
             w.tick()
-        x, z = x0.copy(), z0.copy()
+        x = np.concatenate([x0, np.zeros(200, np.float32)])
+        z = np.concatenate([z0, np.zeros(200, np.float32)])
         live = np.ones(n + 200, bool)
         live[n:] = False
         total = 0
