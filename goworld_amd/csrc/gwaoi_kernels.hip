@@ -1409,6 +1409,9 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_BALLOT_LOOPS
+#define GWAOI_BALLOT_LOOPS 1  // sweep loops end on a ballot of the lanes' own bounds, not a wave max (6 bpermutes)
+#endif
 #ifndef GWAOI_SW_U
 #define GWAOI_SW_U 4  // candidates per lane per sweep iteration on long rows
 #endif
@@ -1450,7 +1453,7 @@ struct LaneA {
     bool valid, jump;
 };
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
     return v;
@@ -1567,7 +1570,12 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                                             const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
+#if GWAOI_BALLOT_LOOPS
+    (void)mx;
+    for (uint32_t t = 0; __ballot(t < len); t += U) {  // to the wave's longest range (scalar mask test)
+#else
     for (uint32_t t = 0; t < mx; t += U) {
+#endif
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
             if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);  // LDS; one global add per block
             __builtin_amdgcn_wave_barrier();
@@ -1576,8 +1584,16 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
             Q.qn = 0;
         }
         uint4 k[U];
+#ifdef GWAOI_EXP_8B  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint2 h = reinterpret_cast<const uint2 *>(cand)[2 * (t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u)];
+            k[u] = make_uint4(h.x, h.y, h.x, h.y);
+        }
+#else
 #pragma unroll
         for (int u = 0; u < U; ++u) k[u] = cand[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t b = jb + t + (uint32_t)u;
@@ -1600,7 +1616,9 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
                                            const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
                                            uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
+#if !GWAOI_BALLOT_LOOPS
     const uint32_t nrw = wave_max_u32(nr);
+#endif
     const uint32_t *cs = F.cell_start;
     const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
     uint32_t jb = 0, je = 0;
@@ -1609,7 +1627,11 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
         jb = cs[rb];
         je = cs[rb + span];
     }
+#if GWAOI_BALLOT_LOOPS
+    for (uint32_t k = 0; __ballot(k < nr); ++k) {
+#else
     for (uint32_t k = 0; k < nrw; ++k) {
+#endif
         uint32_t nb = 0, ne = 0;
         if (k + 1 < nr) {  // prefetch the next row's range
             const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + 1) * gx;
@@ -1617,15 +1639,108 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
             ne = cs[rb + span];
         }
         const uint32_t len = je - jb;
+#if GWAOI_BALLOT_LOOPS
+        const uint32_t mx = 0;
+        if (MODE != 2 && __ballot(len > 2))
+            sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        else if (__ballot(len != 0))
+            sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#else
         const uint32_t mx = wave_max_u32(len);
         if (MODE != 2 && mx > 2)
             sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
         else if (mx)
             sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#endif
         jb = nb;
         je = ne;
     }
 }
+
+// Rows r0..r1 as above, RB rows at a time: the first H candidates of each of
+// the RB rows are loaded together (RB*H loads in flight, one memory round trip
+// for RB short rows), then each row's rest, if any lane has more, is swept as
+// in sweep_rows.  For the X' strip: ~9 rows of 1-2 cells each, mostly 0-3
+// candidates per row, where one round trip per row was the cost.
+template <int MODE, int RB, int H>
+__device__ __forceinline__ void sweep_rows_batched(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
+                                                   int r0, int r1, int c0, int c1, const uint4 *__restrict__ cand,
+                                                   const FrameView &F, const Rec16 *__restrict__ O_rec,
+                                                   const CombinedCtx &C, uint2 *out, uint64_t cap,
+                                                   unsigned long long pe, unsigned long long pl, bool replay) {
+    static_assert(QCAP >= RB * H * WAVE, "queue must hold one batch of row heads");
+    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
+    const uint32_t nrw = wave_max_u32(nr);
+    const uint32_t *cs = F.cell_start;
+    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
+    uint32_t jb[RB], je[RB];
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+        jb[q] = je[q] = 0;
+        if ((uint32_t)q < nr) {
+            const uint32_t rb = rb0 + (uint32_t)(r0 + q) * gx;
+            jb[q] = cs[rb];
+            je[q] = cs[rb + span];
+        }
+    }
+    for (uint32_t k = 0; k < nrw; k += RB) {
+        uint32_t nb[RB], nn[RB];
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {  // prefetch the next batch's ranges
+            nb[q] = nn[q] = 0;
+            if (k + RB + (uint32_t)q < nr) {
+                const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + RB + q) * gx;
+                nb[q] = cs[rb];
+                nn[q] = cs[rb + span];
+            }
+        }
+        if (Q.qn > QCAP - RB * H * WAVE) {
+            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);
+            __builtin_amdgcn_wave_barrier();
+            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
+                        cap, pe, pl, replay);
+            Q.qn = 0;
+        }
+        uint4 kc[RB][H];
+#pragma unroll
+        for (int q = 0; q < RB; ++q)
+#pragma unroll
+            for (int h = 0; h < H; ++h) kc[q][h] = cand[jb[q] + (uint32_t)h < je[q] ? jb[q] + (uint32_t)h : 0u];
+#pragma unroll
+        for (int q = 0; q < RB; ++q)
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const uint32_t b = jb[q] + (uint32_t)h;
+                const bool keep = band_keep<MODE>(A, C, kc[q][h], b) & (b < je[q]);
+                qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), b);
+            }
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {  // rows longer than H
+            const uint32_t len = je[q] - jb[q] > (uint32_t)H ? je[q] - jb[q] - (uint32_t)H : 0u;
+            const uint32_t mx = wave_max_u32(len);
+            if (mx > 2)
+                sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb[q] + H, len, mx, cand, F, O_rec, C, out, cap, pe, pl,
+                                              replay);
+            else if (mx)
+                sweep_range<MODE, 2>(L, w, Q, A, jb[q] + H, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+            jb[q] = nb[q];
+            je[q] = nn[q];
+        }
+    }
+}
+
+#ifndef GWAOI_XB
+#define GWAOI_XB 0  // X' strip rows per batch (0: one row at a time; 2-4 measured slower: profiles/r02_variants_xbatch.log)
+#endif
+#ifndef GWAOI_XH
+#define GWAOI_XH 2  // candidates per row loaded with the batch
+#endif
+#ifndef GWAOI_ZB
+#define GWAOI_ZB 0  // Z strip rows per batch (0: one row at a time)
+#endif
+#ifndef GWAOI_ZH
+#define GWAOI_ZH 4
+#endif
 
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
@@ -1646,7 +1761,12 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
 #ifndef GWAOI_EXP_NOZ  // timing experiment only: skip the Z strip (events wrong)
+#if GWAOI_ZB > 0
+        sweep_rows_batched<0, GWAOI_ZB, GWAOI_ZH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
+                                                  pl, replay);
+#else
         sweep_rows<0>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#endif
 #endif
         // X' strip: rows holding z in [z-lo, z+lo], cells holding x in [x+lo, x+hi]
         r0 = 0, r1 = -1, c0 = 0, c1 = -1;
@@ -1657,7 +1777,12 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
 #ifndef GWAOI_EXP_NOX  // timing experiment only: skip the X' strip (events wrong)
+#if GWAOI_XB > 0
+        sweep_rows_batched<1, GWAOI_XB, GWAOI_XH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
+                                                  pl, replay);
+#else
         sweep_rows<1>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#endif
 #endif
     }
     if (__ballot(whole)) {

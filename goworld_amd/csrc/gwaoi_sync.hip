@@ -12,9 +12,10 @@
 //   route     Entity.interest/uninterest -> sendCreateEntity/sendDestroyEntity
 //             (Entity.go:236-246, GameClient.go:37-59): the flush's events
 //             whose first entity has a client, grouped by gate.
-// Grouping by gate is a two-pass multisplit: pass 0 counts records per
+// Grouping by gate is a multisplit: a first pass counts records per
 // (gate, block) in LDS, an exclusive scan gives every (gate, block) its
-// base, pass 1 reserves each lane's run through an LDS cursor and writes it.
+// base, a second pass writes each block's runs (the fan-out's first pass
+// also lists every record's sender, so the AOI window is walked once).
 // The output is HBM write bound (48 B per record).
 
 #include "gwaoi_device.h"
@@ -36,6 +37,7 @@ constexpr uint32_t NO_GATE = 0xFFFFFFFFu;
 constexpr uint32_t H_EMPTY = 0xFFFFFFFFu;  // hash bucket never used
 constexpr uint32_t H_TOMB = 0xFFFFFFFEu;   // hash bucket freed
 constexpr int ST = 256;                    // threads per workgroup of the sync kernels
+constexpr uint32_t SCR_FULL = 0xFFFFFFFFu; // fan-out: the block's hits did not fit the scratch
 
 inline uint32_t cdivu(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 
@@ -58,6 +60,7 @@ __device__ __forceinline__ bool eq4(uint4 a, uint4 b) {
 constexpr int MAX_ARR = 8;
 struct ArrTable {
     void *p[MAX_ARR];
+    uint32_t stride[MAX_ARR];  // elements between consecutive indices (fields of packed per-slot records)
 };
 struct W32 {
     uint32_t arr, idx, val, pad;
@@ -71,15 +74,22 @@ __global__ void k_scatter32(const W32 *__restrict__ w, uint32_t n, ArrTable T) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const W32 e = w[i];
-    static_cast<uint32_t *>(T.p[e.arr])[e.idx] = e.val;
+    static_cast<uint32_t *>(T.p[e.arr])[(size_t)e.idx * T.stride[e.arr]] = e.val;
 }
 
 __global__ void k_scatter128(const W128 *__restrict__ w, uint32_t n, ArrTable T) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const W128 e = w[i];
-    static_cast<uint4 *>(T.p[e.arr])[e.idx] = e.val;
+    static_cast<uint4 *>(T.p[e.arr])[(size_t)e.idx * T.stride[e.arr]] = e.val;
 }
+
+// Per-slot sync state is packed so that one pass touches one line per slot:
+//   sst[s]  uint4 {gate index, space in call order, syncing, sync flags}
+//   cl[s]   ulonglong2 {Position claim, yaw claim}
+//   htab[h] 2 x uint4 {entity id; slot, -, -, -}: an id-table bucket is one 32-B
+//           entry, so a probe reads key and value from the same line.
+enum SstField { SST_GATE = 0, SST_SPACE = 1, SST_SYNCING = 2, SST_FLAGS = 3 };
 
 // Host position/yaw writes (set_position_yaw, entity_set_position_yaw,
 // entity_enter_plain) and flag-only ops (Space.enter): claim, then the winner
@@ -95,55 +105,51 @@ struct SideOp {
     float4 pos;  // x, y, z, yaw
 };
 
-__global__ void k_side_claim(const SideOp *__restrict__ ops, uint32_t n, unsigned long long *sclaim,
-                             unsigned long long *yclaim, uint32_t *sflags) {
+__global__ void k_side_claim(const SideOp *__restrict__ ops, uint32_t n, unsigned long long *cl, uint32_t *sst) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const SideOp o = ops[i];
-    if (o.bits & SIDE_POS) atomicMax(&sclaim[o.slot], o.claim);
-    if (o.bits & SIDE_YAW) atomicMax(&yclaim[o.slot], o.claim);
-    if (o.bits & SIDE_SIF) atomicOr(&sflags[o.slot], o.bits & SIDE_SIF);
+    if (o.bits & SIDE_POS) atomicMax(&cl[2 * (size_t)o.slot], o.claim);
+    if (o.bits & SIDE_YAW) atomicMax(&cl[2 * (size_t)o.slot + 1], o.claim);
+    if (o.bits & SIDE_SIF) atomicOr(&sst[4 * (size_t)o.slot + SST_FLAGS], o.bits & SIDE_SIF);
 }
 
-__global__ void k_side_write(const SideOp *__restrict__ ops, uint32_t n, const unsigned long long *sclaim,
-                             const unsigned long long *yclaim, float4 *pos) {
+__global__ void k_side_write(const SideOp *__restrict__ ops, uint32_t n, const unsigned long long *cl, float4 *pos) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const SideOp o = ops[i];
     float *p = reinterpret_cast<float *>(pos + o.slot);
-    if ((o.bits & SIDE_POS) && sclaim[o.slot] == o.claim) {
+    if ((o.bits & SIDE_POS) && cl[2 * (size_t)o.slot] == o.claim) {
         p[0] = o.pos.x;
         p[1] = o.pos.y;
         p[2] = o.pos.z;
     }
-    if ((o.bits & SIDE_YAW) && yclaim[o.slot] == o.claim) p[3] = o.pos.w;
+    if ((o.bits & SIDE_YAW) && cl[2 * (size_t)o.slot + 1] == o.claim) p[3] = o.pos.w;
 }
 
 // ------------------------------------------------------------- decode ------
 struct DecodeArgs {
     const uint4 *pay;  // 2 uint4 per record: id, (x, y, z, yaw) bits
     uint32_t n;
-    const uint4 *hkey;
-    const uint32_t *hval;
+    const uint4 *htab;
     uint32_t hmask;
-    const uint32_t *qspace, *syncing;
+    uint32_t *sst;
     uint32_t *o_slot, *o_sp;  // the device Moved batch (SLOT_NONE: no move)
     float *o_x, *o_z;
     uint32_t *o_ys;  // slot of an applied record (SLOT_NONE: skipped), for k_decode_yaw
     unsigned long long claim0;
-    unsigned long long *sclaim, *yclaim;
-    uint32_t *sflags;
+    unsigned long long *cl;
     float4 *pos;
     uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
 };
 
-__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ hkey, const uint32_t *__restrict__ hval,
-                                           uint32_t hmask, uint4 id) {
+__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t hmask, uint4 id) {
     uint32_t h = id_hash(id.x, id.y, id.z, id.w) & hmask;
     for (uint32_t probe = 0; probe <= hmask; ++probe, h = (h + 1) & hmask) {
-        const uint32_t v = hval[h];
+        const uint4 k = htab[2 * (size_t)h];  // key and value: one 32-B bucket
+        const uint32_t v = htab[2 * (size_t)h + 1].x;
         if (v == H_EMPTY) return SLOT_NONE;
-        if (v != H_TOMB && eq4(hkey[h], id)) return v;
+        if (v != H_TOMB && eq4(k, id)) return v;
     }
     return SLOT_NONE;
 }
@@ -159,11 +165,12 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     if (i >= A.n) return;
     const uint4 id = A.pay[2 * (size_t)i];
     const uint4 pv = A.pay[2 * (size_t)i + 1];
-    uint32_t s = lookup(A.hkey, A.hval, A.hmask, id);
+    uint32_t s = lookup(A.htab, A.hmask, id);
     uint32_t sp = SP_DEAD;
     if (s != SLOT_NONE) {
-        sp = A.qspace[s];
-        if (!A.syncing[s]) s = SLOT_NONE;
+        const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[s];
+        sp = st.y;  // SST_SPACE
+        if (!st.z) s = SLOT_NONE;  // SST_SYNCING
     }
     const bool move = s != SLOT_NONE && sp != SP_DEAD;
     A.o_slot[i] = move ? s : SLOT_NONE;
@@ -172,13 +179,34 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     A.o_sp[i] = sp;
     A.o_ys[i] = s;
     if (s != SLOT_NONE) {
+        // Plain stores, no atomics (a device-scope atomic is performed memory-side
+        // on gfx950, ~17x slower than a store for 64 lanes on 64 lines): the
+        // claims of this batch are larger than every claim already applied, so a
+        // store replaces them; among records of one slot in this batch a random
+        // store survives, and k_decode_fix folds the others in.
         const unsigned long long c = A.claim0 + i;
-        atomicMax(&A.yclaim[s], c);
-        if (move) atomicMax(&A.sclaim[s], c);
-        const uint32_t old = atomicOr(&A.sflags[s], (uint32_t)GWAOI_SIF_NEIGHBOR_CLIENTS);
-        // first flag of a slot outside the frame since the last collect: list it once
+        if (move) reinterpret_cast<ulonglong2 *>(A.cl)[s] = make_ulonglong2(c, c);
+        else A.cl[2 * (size_t)s + 1] = c;
+        uint32_t *f = &A.sst[4 * (size_t)s + SST_FLAGS];
+        const uint32_t old = *f;  // records of one slot all set the same bit
+        if (!(old & GWAOI_SIF_NEIGHBOR_CLIENTS)) *f = old | GWAOI_SIF_NEIGHBOR_CLIENTS;
+        // first flag of a slot outside the frame since the last collect: listed (a
+        // slot with several records may be listed twice; k_fan_prep sends it once)
         if (!move && old == 0u) A.oflag[atomicAdd(A.oflag_n, 1u)] = s;
     }
+}
+
+// Records whose claim store did not survive (another record of the same slot
+// in this batch) fold it in with atomicMax: only repeated slots pay an atomic.
+__global__ __launch_bounds__(ST) void k_decode_fix(DecodeArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint32_t s = A.o_ys[i];
+    if (s == SLOT_NONE) return;
+    const unsigned long long c = A.claim0 + i;
+    const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
+    if (A.o_sp[i] != SP_DEAD && cs.x != c) atomicMax(&A.cl[2 * (size_t)s], c);
+    if (cs.y != c) atomicMax(&A.cl[2 * (size_t)s + 1], c);
 }
 
 __global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
@@ -189,12 +217,13 @@ __global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
     const unsigned long long c = A.claim0 + i;
     const uint4 pv = A.pay[2 * (size_t)i + 1];
     float *p = reinterpret_cast<float *>(A.pos + s);
-    if (A.o_sp[i] != SP_DEAD && A.sclaim[s] == c) {
+    const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
+    if (A.o_sp[i] != SP_DEAD && cs.x == c) {
         p[0] = __uint_as_float(pv.x);
         p[1] = __uint_as_float(pv.y);
         p[2] = __uint_as_float(pv.z);
     }
-    if (A.yclaim[s] == c) p[3] = __uint_as_float(pv.w);
+    if (cs.y == c) p[3] = __uint_as_float(pv.w);
 }
 
 // ------------------------------------------------------------ fan-out ------
@@ -213,18 +242,21 @@ struct FanArgs {
     const uint32_t *left;  // flagged slots outside the frame (own-client records only), may repeat
     uint32_t n_left;
     const uint4 *eid, *cid;
-    const uint32_t *cgate;
-    uint32_t *sflags;
+    uint32_t *sst;
     const float4 *pos;
     // frame-ordered (n + n_left entries), written by k_fan_prep
     uint32_t *snd;    // sender flags
     uint32_t *rg;     // receiver gate (NO_GATE: no client)
     uint32_t *rslot;  // slot
-    uint4 *srec1;     // sender id
-    uint4 *srec2;     // sender x, y, z, yaw
+    uint4 *srec;      // 2 per entry: sender id, then x, y, z, yaw (one 32-B load per record)
+    uint4 *frec;      // frame records (x, z, seq) with sifSyncNeighborClients in bit 63
+    uint32_t *fcnt, *fsb;  // records of each entry, its run in the scratch
+    uint32_t *scr;         // hits: sender entry of each record, receiver-contiguous runs
+    unsigned long long *scr_cursor;
+    unsigned long long scr_cap;  // < SCR_FULL
     uint32_t G, nb;
-    uint32_t *blk_cnt;  // [G][nb] (pass 0 writes, the scan turns it into bases)
-    uint4 *out;         // 3 uint4 per record (pass 1)
+    uint32_t *blk_cnt;  // [G][nb] (pass 1 writes, the scan turns it into bases)
+    uint4 *out;         // 3 uint4 per record (pass 2)
 };
 
 __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
@@ -233,34 +265,40 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     if (i >= nf + A.n_left) return;
     const bool in_frame = i < nf;
     const uint32_t s = in_frame ? ld_ss(A.F.ss, i).slot : A.left[i - nf];
+    const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[s];  // gate, space, syncing, flags
     uint32_t fl;
     if (in_frame) {
-        fl = A.sflags[s];
-        if (fl) A.sflags[s] = 0u;
+        fl = st.w;
+        if (fl) A.sst[4 * (size_t)s + SST_FLAGS] = 0u;
     } else {
         // a listed slot back in the frame is its frame entry's; a slot listed twice is sent once
         const uint32_t r = A.info[s].rank;
-        fl = (r < nf && ld_ss(A.F.ss, r).slot == s) ? 0u : atomicExch(&A.sflags[s], 0u);
+        fl = (r < nf && ld_ss(A.F.ss, r).slot == s) ? 0u : atomicExch(&A.sst[4 * (size_t)s + SST_FLAGS], 0u);
     }
     A.snd[i] = fl;
-    A.rg[i] = A.cgate[s];
+    A.rg[i] = st.x;
     A.rslot[i] = s;
+    uint4 q = make_uint4(0, 0, 0, 0);
+    if (in_frame) {  // the walk's candidate record: x, z, seq with the sender flag in bit 63
+        q = reinterpret_cast<const uint4 *>(A.F.rec)[i];
+        uint4 f = q;
+        if (fl & GWAOI_SIF_NEIGHBOR_CLIENTS) f.w |= 0x80000000u;
+        A.frec[i] = f;
+    }
     if (fl) {
         // the frame holds the AOI position; outside the frame, the last Position written
         const float4 P = A.pos[s];
         float x = P.x, z = P.z;
         if (in_frame) {
-            const Rec16 R = ld_rec(A.F.rec, i);
-            x = R.x;
-            z = R.z;
+            x = __uint_as_float(q.x);
+            z = __uint_as_float(q.y);
         }
-        A.srec1[i] = A.eid[s];
-        A.srec2[i] = make_uint4(__float_as_uint(x), __float_as_uint(P.y), __float_as_uint(z), __float_as_uint(P.w));
+        A.srec[2 * (size_t)i] = A.eid[s];
+        A.srec[2 * (size_t)i + 1] = make_uint4(__float_as_uint(x), __float_as_uint(P.y), __float_as_uint(z), __float_as_uint(P.w));
     }
 }
 
 __device__ __forceinline__ uint32_t s_lane() { return __lane_id(); }
-__device__ __forceinline__ unsigned long long s_lt() { return (1ull << s_lane()) - 1ull; }
 
 // Exclusive scan of n (<= ST * k) LDS words in place by one workgroup.
 __device__ void lds_excl_scan(uint32_t *a, uint32_t n, uint32_t *ws) {
@@ -286,104 +324,267 @@ __device__ void lds_excl_scan(uint32_t *a, uint32_t n, uint32_t *ws) {
     __syncthreads();
 }
 
-// Records of one emission point: the emitting lanes of one gate group (lanes
-// sorted by gate, so a group is a contiguous lane range `grp`) take
-// consecutive slots from the block's cursor of that gate: stores of a group
-// land side by side.
-__device__ __forceinline__ size_t group_slot(bool emit, unsigned long long grp, uint32_t *cur, uint32_t g) {
-    const unsigned long long m = __ballot(emit) & grp;
-    if (!m) return 0;  // no record in this lane's group (its leader, if any, is active below)
-    uint32_t base = 0;
-    const uint32_t rank = (uint32_t)__popcll(m & s_lt());
-    if (emit && rank == 0) base = atomicAdd(&cur[g], (uint32_t)__popcll(m));
-    base = __shfl(base, m ? __ffsll((long long)m) - 1 : 0);
-    return (size_t)base + rank;
+// Block-wide exclusive scan of one value per thread (ST threads).
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *ws, uint32_t &total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if ((int)s_lane() >= o) x += y;
+    }
+    const uint32_t w = threadIdx.x / 64;
+    if (s_lane() == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t pre = x - v;
+    total = 0;
+    for (uint32_t q = 0; q < ST / 64; ++q) {
+        if (q < w) pre += ws[q];
+        total += ws[q];
+    }
+    __syncthreads();
+    return pre;
 }
 
-template <int PASS>
-__global__ __launch_bounds__(ST) void k_fanout(FanArgs A) {
-    extern __shared__ uint32_t lds[];  // cur[G]: count (pass 0) / cursor (pass 1); bin[G + 1]
-    __shared__ uint32_t s_perm[ST];
+// The go-aoi window of receiver entry i (cells), widened by the float32
+// rounding margin of the window bounds.
+struct FanWin {
+    Rec16 R;
+    float D;
+    uint32_t row0, gx;  // cell index of (cx0, cz0), grid row length
+    int cx0, cx1, cz0, cz1;
+};
+__device__ __forceinline__ FanWin fan_window(const FrameView &F, uint32_t i) {
+    FanWin W;
+    W.R = ld_rec(F.rec, i);
+    const SpaceGrid gr = F.grid[ld_ss(F.ss, i).sp];
+    W.D = gr.D;
+    const float mx = (fabsf(W.R.x) + 3.0f * W.D) * 0x1p-20f, mz = (fabsf(W.R.z) + 3.0f * W.D) * 0x1p-20f;
+    W.cx0 = cell_of(W.R.x - W.D - mx, gr.ox, gr.inv, gr.gx);
+    W.cx1 = cell_of(W.R.x + W.D + mx, gr.ox, gr.inv, gr.gx);
+    W.cz0 = cell_of(W.R.z - W.D - mz, gr.oz, gr.inv, gr.gz);
+    W.cz1 = cell_of(W.R.z + W.D + mz, gr.oz, gr.inv, gr.gz);
+    W.gx = gr.gx;
+    W.row0 = gr.base + (uint32_t)W.cz0 * gr.gx + (uint32_t)W.cx0;
+    return W;
+}
+
+// Fan-out pass 1 (hits): one lane per entry i (frame order, then the listed
+// slots outside the frame).  A receiver (an entry with a client) lists the
+// senders of its records in the scratch: itself first if sifSyncOwnClient,
+// then every A in its go-aoi window with sifSyncNeighborClients and rel(A,B).
+// Its scratch run is sized by the window's candidate count (cell_start
+// loads only) and placed by one atomic per block, so the window is walked
+// once.  A block past the scratch capacity writes no hits (the host regrows
+// the scratch and reruns this pass; it has no other side effect).
+constexpr int FAN_U = 4;  // window candidates loaded together per lane
+
+__global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
+    extern __shared__ uint32_t gcnt[];  // [G] records per gate of the block
     __shared__ uint32_t s_ws[ST / 64];
-    uint32_t *cur = lds, *bin = lds + A.G;
+    __shared__ uint32_t s_base;
+    __shared__ uint16_t s_n[2][ST / 64];
+    __shared__ uint8_t s_perm[ST];
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t nf = A.F.n, ne = nf + A.n_left;
-    for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
-        cur[g] = PASS == 0 ? 0u : A.blk_cnt[(size_t)g * A.nb + blk];
-    for (uint32_t g = threadIdx.x; g <= A.G; g += blockDim.x) bin[g] = 0u;
-    __syncthreads();
-    // lanes sorted by receiver gate (no client last): same-gate lanes are neighbours
-    const uint32_t i0 = blk * ST + threadIdx.x;
-    const uint32_t g0 = i0 < ne ? A.rg[i0] : NO_GATE;
-    const uint32_t key = g0 == NO_GATE ? A.G : g0;
-    const uint32_t r0 = atomicAdd(&bin[key], 1u);
-    __syncthreads();
-    lds_excl_scan(bin, A.G + 1, s_ws);
-    s_perm[bin[key] + r0] = i0;
-    __syncthreads();
-    const uint32_t i = s_perm[threadIdx.x];
+    const uint32_t w = threadIdx.x / 64, ln = s_lane();
+    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) gcnt[q] = 0u;
+    // receivers that walk a window first (stable), so that whole waves idle instead of half lanes
+    {
+        const uint32_t i0 = blk * ST + threadIdx.x;
+        const bool wk = i0 < nf && A.rg[i0] != NO_GATE;
+        const unsigned long long m = __ballot(wk);
+        if (ln == 0) {
+            s_n[0][w] = (uint16_t)__popcll(m);
+            s_n[1][w] = (uint16_t)(64 - __popcll(m));
+        }
+        __syncthreads();
+        const unsigned long long lt = (1ull << ln) - 1ull;
+        uint32_t pos = wk ? (uint32_t)__popcll(m & lt) : (uint32_t)__popcll(~m & lt);
+        for (uint32_t q = 0; q < ST / 64; ++q) {
+            if (!wk) pos += s_n[0][q];
+            if (q < w) pos += s_n[wk ? 0 : 1][q];
+        }
+        s_perm[pos] = (uint8_t)threadIdx.x;
+        __syncthreads();
+    }
+    const uint32_t i = blk * ST + s_perm[threadIdx.x];
     const uint32_t g = i < ne ? A.rg[i] : NO_GATE;
     const bool on = g != NO_GATE;
-    // this lane's gate group within the wave
-    const uint32_t gprev = __shfl_up(g, 1);
-    const unsigned long long heads = __ballot(s_lane() == 0 || gprev != g);
-    const unsigned long long upto = heads & (s_lt() | (1ull << s_lane()));
-    const uint32_t gstart = 63 - __clzll(upto);
-    const unsigned long long above = heads & ~(s_lt() | (1ull << s_lane()));
-    const uint32_t gend = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
-    const unsigned long long grp = (gend == 64 ? ~0ull : ((1ull << gend) - 1ull)) & ~((1ull << gstart) - 1ull);
-    if (__ballot(on)) {
-        uint32_t c = 0;
-        uint4 client{};
-        if (PASS == 1 && on) client = A.cid[A.rslot[i]];
-        const bool own = on && (A.snd[i] & GWAOI_SIF_OWN_CLIENT);
-        if (PASS == 1) {
-            const size_t p = group_slot(own, grp, cur, g);
-            if (own) {
-                uint4 *o = A.out + 3 * p;
-                o[0] = client;
-                o[1] = A.srec1[i];
-                o[2] = A.srec2[i];
-            }
-        } else {
-            c += own;
+    const bool own = on && (A.snd[i] & GWAOI_SIF_OWN_CLIENT);
+    const bool walk = on && i < nf;
+    const uint32_t *cs = A.F.cell_start;
+    FanWin W{};
+    uint32_t ub = own ? 1u : 0u;
+    if (walk) {
+        W = fan_window(A.F, i);
+        const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
+        for (int cz = W.cz0; cz <= W.cz1; ++cz) {
+            const uint32_t rb = W.row0 + (uint32_t)(cz - W.cz0) * W.gx;
+            ub += cs[rb + span] - cs[rb];
         }
-        if (on && i < nf) {
-            const Rec16 R = ld_rec(A.F.rec, i);
-            const SpaceGrid gr = A.F.grid[ld_ss(A.F.ss, i).sp];
-            const float D = gr.D;
-            const float mx = (fabsf(R.x) + 3.0f * D) * 0x1p-20f, mz = (fabsf(R.z) + 3.0f * D) * 0x1p-20f;
-            const int cx0 = cell_of(R.x - D - mx, gr.ox, gr.inv, gr.gx);
-            const int cx1 = cell_of(R.x + D + mx, gr.ox, gr.inv, gr.gx);
-            const int cz0 = cell_of(R.z - D - mz, gr.oz, gr.inv, gr.gz);
-            const int cz1 = cell_of(R.z + D + mz, gr.oz, gr.inv, gr.gz);
-            for (int cz = cz0; cz <= cz1; ++cz) {
-                const uint32_t row = gr.base + (uint32_t)cz * gr.gx;
-                const uint32_t jb = A.F.cell_start[row + (uint32_t)cx0];
-                const uint32_t je = A.F.cell_start[row + (uint32_t)cx1 + 1u];
-                for (uint32_t b = jb; b < je; ++b) {
-                    const Rec16 B = ld_rec(A.F.rec, b);
-                    const bool hit = b != i && (A.snd[b] & GWAOI_SIF_NEIGHBOR_CLIENTS) &&
-                                     rel(R.x, R.z, R.s, B.x, B.z, B.s, D);
-                    if (PASS == 1) {
-                        const size_t p = group_slot(hit, grp, cur, g);
-                        if (hit) {
-                            uint4 *o = A.out + 3 * p;
-                            o[0] = client;
-                            o[1] = A.srec1[b];
-                            o[2] = A.srec2[b];
+    }
+    ub = (ub + 3u) & ~3u;  // runs start 16-B aligned: hits are stored four at a time
+    uint32_t tot;
+    const uint32_t off = block_excl(ub, s_ws, tot);
+    if (threadIdx.x == 0) {
+        const unsigned long long b = tot ? atomicAdd(A.scr_cursor, (unsigned long long)tot) : 0ull;
+        s_base = b + tot <= A.scr_cap ? (uint32_t)b : SCR_FULL;
+    }
+    __syncthreads();
+    const uint32_t base = s_base;
+    const bool fits = base != SCR_FULL;
+    const uint32_t sb = base + off;
+    uint4 *run = reinterpret_cast<uint4 *>(A.scr + sb);
+    uint32_t c = 0;
+    uint4 buf = make_uint4(i, 0u, 0u, 0u);
+    if (own) c = 1;
+    if (walk) {
+        const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
+        const unsigned long long rs = W.R.s;
+        for (int cz = W.cz0; cz <= W.cz1; ++cz) {
+            const uint32_t rb = W.row0 + (uint32_t)(cz - W.cz0) * W.gx;
+            const uint32_t jb = cs[rb], je = cs[rb + span];
+            for (uint32_t b0 = jb; b0 < je; b0 += FAN_U) {
+                uint4 q[FAN_U];
+#pragma unroll
+                for (int u = 0; u < FAN_U; ++u) q[u] = A.frec[b0 + u < je ? b0 + u : b0];
+#pragma unroll
+                for (int u = 0; u < FAN_U; ++u) {
+                    const uint32_t b = b0 + (uint32_t)u;
+                    const unsigned long long bs = ((unsigned long long)(q[u].w & 0x7FFFFFFFu) << 32) | q[u].z;
+                    const bool hit = b < je && b != i && (q[u].w >> 31) &&
+                                     rel(W.R.x, W.R.z, rs, __uint_as_float(q[u].x), __uint_as_float(q[u].y), bs, W.D);
+                    if (hit) {
+                        switch (c & 3u) {
+                            case 0: buf.x = b; break;
+                            case 1: buf.y = b; break;
+                            case 2: buf.z = b; break;
+                            default: buf.w = b; break;
                         }
-                    } else {
-                        c += hit;
+                        ++c;
+                        if (!(c & 3u) && fits) run[(c >> 2) - 1u] = buf;
                     }
                 }
             }
         }
-        if (PASS == 0 && c) atomicAdd(&cur[g], c);
     }
+    if ((c & 3u) && fits) run[c >> 2] = buf;
+    if (i < ne) {
+        A.fcnt[i] = c;
+        A.fsb[i] = sb;
+    }
+    if (c) atomicAdd(&gcnt[g], c);
     __syncthreads();
-    if (PASS == 0)
-        for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) A.blk_cnt[(size_t)q * A.nb + blk] = cur[q];
+    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) A.blk_cnt[(size_t)q * A.nb + blk] = gcnt[q];
+}
+
+// Fan-out pass 2 (write): block blk expands the hits of its receivers into
+// 48-B records (receiver's ClientID, sender's EntityID, x, y, z, yaw).  The
+// receivers are regrouped by gate (stable), so the block's records of gate g
+// form one run starting at the scanned base of (g, blk).  Thread t writes
+// records t, t + ST, ... of the block: consecutive threads write consecutive
+// records of a run (coalesced stores), each finding its receiver by a binary
+// search of the inclusive record prefix in LDS.  (GoWorld's own per-gate
+// order is Go map order, EntityManager.go's entity loop: the order of
+// records inside a gate is not part of the contract.)
+#ifndef GWAOI_FW_G
+#define GWAOI_FW_G 4
+#endif
+constexpr int FW_G = GWAOI_FW_G;  // record groups of 64 per wave with their loads in flight together
+
+__global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
+    extern __shared__ uint32_t lds[];  // bin[G + 1] | gbase[G] | seg[G]
+    __shared__ uint32_t s_pre[ST], s_sb[ST], s_gate[ST];
+    __shared__ uint4 s_cli[ST];
+    __shared__ uint4 s_rec[ST / 64][3 * 64];  // a wave's 64 records, staged for contiguous stores
+    __shared__ uint32_t s_pos[ST / 64][64];
+    __shared__ uint32_t s_ws[ST / 64];
+    uint32_t *bin = lds, *gbase = lds + A.G + 1, *seg = gbase + A.G;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t ne = A.F.n + A.n_left;
+    const uint32_t w = threadIdx.x / 64, ln = s_lane();
+    for (uint32_t q = threadIdx.x; q <= A.G; q += blockDim.x) bin[q] = 0u;
+    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) gbase[q] = A.blk_cnt[(size_t)q * A.nb + blk];
+    __syncthreads();
+    const uint32_t i = blk * ST + threadIdx.x;
+    const uint32_t g = i < ne ? A.rg[i] : NO_GATE;
+    const uint32_t key = g == NO_GATE ? A.G : g;
+    const uint32_t r0 = atomicAdd(&bin[key], 1u);
+    __syncthreads();
+    lds_excl_scan(bin, A.G + 1, s_ws);
+    const uint32_t p = bin[key] + r0;  // (the order inside a gate's run is not part of the contract)
+    const uint32_t c = g != NO_GATE ? A.fcnt[i] : 0u;
+    s_pre[p] = c;
+    s_sb[p] = c ? A.fsb[i] : 0u;
+    s_gate[p] = key;
+    if (c) s_cli[p] = A.cid[A.rslot[i]];
+    __syncthreads();
+    uint32_t R;
+    const uint32_t mine = s_pre[threadIdx.x];
+    const uint32_t ex = block_excl(mine, s_ws, R);
+    s_pre[threadIdx.x] = ex + mine;  // inclusive
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) seg[q] = bin[q] ? s_pre[bin[q] - 1] : 0u;
+    __syncthreads();
+    const uint4 *srec = A.srec;
+    // record r -> (receiver perm position, its scratch entry, output position)
+    auto locate = [&](uint32_t r, uint32_t &q, uint32_t &sidx, uint32_t &pos) {
+        uint32_t lo = 0, hi = ST - 1;  // first receiver q with s_pre[q] > r
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s_pre[m] > r) hi = m;
+            else lo = m + 1;
+        }
+        q = lo;
+        const uint32_t gq = s_gate[q];
+        sidx = s_sb[q] + r - (q ? s_pre[q - 1] : 0u);
+        pos = gbase[gq] + (r - seg[gq]);
+    };
+    // stage a wave's 64 records in LDS, then store them as 3 x 64 consecutive 16-B words
+    auto emit = [&](uint32_t rw, bool ok, uint32_t q, uint32_t pos, const uint4 &id, const uint4 &pv) {
+        if (ok) {
+            s_pos[w][ln] = pos;
+            s_rec[w][3 * ln] = s_cli[q];
+            s_rec[w][3 * ln + 1] = id;
+            s_rec[w][3 * ln + 2] = pv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        const uint32_t nrec = min(64u, R - rw);
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) {
+            const uint32_t e = ln + 64u * j, rr = e / 3u;
+            if (rr < nrec) A.out[3 * (size_t)s_pos[w][rr] + (e - 3u * rr)] = s_rec[w][e];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    };
+    // wave w: records [rw + k*ST, rw + k*ST + 64) for k < FW_G per step, all groups' loads in flight
+    for (uint32_t rw = w * 64; rw < R; rw += FW_G * ST) {
+        uint32_t q[FW_G], pos[FW_G], h[FW_G];
+        bool ok[FW_G];
+#pragma unroll
+        for (int k = 0; k < FW_G; ++k) {
+            const uint32_t r = rw + (uint32_t)k * ST + ln;
+            ok[k] = r < R;
+            uint32_t sidx = 0;
+            q[k] = pos[k] = 0;
+            if (ok[k]) locate(r, q[k], sidx, pos[k]);
+            h[k] = ok[k] ? A.scr[sidx] : 0u;
+        }
+        uint4 id[FW_G], pv[FW_G];
+#pragma unroll
+        for (int k = 0; k < FW_G; ++k) {
+            id[k] = pv[k] = make_uint4(0, 0, 0, 0);
+            if (ok[k]) {
+                id[k] = srec[2 * (size_t)h[k]];
+                pv[k] = srec[2 * (size_t)h[k] + 1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < FW_G; ++k)
+            if (rw + (uint32_t)k * ST < R) emit(rw + (uint32_t)k * ST, ok[k], q[k], pos[k], id[k], pv[k]);
+    }
 }
 
 // -------------------------------------------------------------- route ------
@@ -393,7 +594,7 @@ struct RouteArgs {
     FrameView F;
     const SlotInfo *info;
     const uint4 *eid, *cid;
-    const uint32_t *cgate;
+    const uint32_t *sst;
     const float4 *pos;
     uint32_t G, nb;
     uint32_t *blk_cnt;  // [2][G][nb]: creates then destroys
@@ -412,7 +613,7 @@ __global__ __launch_bounds__(ST) void k_route(RouteArgs A) {
     const uint32_t e = blk * ST + threadIdx.x;
     if (e < A.n_total) {
         const uint2 ab = reinterpret_cast<const uint2 *>(A.ev)[e];
-        const uint32_t g = A.cgate[ab.x];
+        const uint32_t g = A.sst[4 * (size_t)ab.x + SST_GATE];
         if (g != NO_GATE) {
             const bool create = e < A.n_enter;
             const uint32_t p = atomicAdd(&lds[(create ? 0u : A.G) + g], 1u);
@@ -456,17 +657,17 @@ struct SyncState {
     uint32_t max_slots = 0;
     // device, per slot
     uint4 *eid = nullptr, *cid = nullptr;
-    uint32_t *cgate = nullptr, *qspace = nullptr, *syncing = nullptr, *sflags = nullptr;
+    uint32_t *sst = nullptr;  // 4 per slot: gate, space, syncing, flags
     float4 *pos = nullptr;
-    unsigned long long *sclaim = nullptr, *yclaim = nullptr;  // Position / yaw last-writer claims
+    unsigned long long *cl = nullptr;  // 2 per slot: Position / yaw last-writer claims
     uint32_t *oflag = nullptr, *oflag_n = nullptr;  // decode: slots flagged outside every AOI space
     bool decoded = false;                           // a decode ran since the last collect
     // id -> slot hash table (device, host mirror)
-    uint4 *hkey = nullptr;
-    uint32_t *hval = nullptr;
+    uint4 *htab = nullptr;  // 2 per bucket: key, (slot, -, -, -)
     uint32_t hcap = 0, hused = 0;  // buckets, live + tombstones
     std::vector<uint4> h_hkey;
     std::vector<uint32_t> h_hval;
+    std::vector<uint4> h_tab;  // rehash upload staging
     // host mirrors
     std::vector<uint4> h_eid;
     std::vector<uint8_t> h_bound, h_client;
@@ -500,8 +701,12 @@ struct SyncState {
     uint32_t *d_left = nullptr;
     size_t left_cap = 0;
     // fan-out scratch, frame order (fan_cap entries each)
-    uint32_t *f_snd = nullptr, *f_rg = nullptr, *f_slot = nullptr;
-    uint4 *f_rec1 = nullptr, *f_rec2 = nullptr;
+    uint32_t *f_snd = nullptr, *f_rg = nullptr, *f_slot = nullptr, *f_cnt = nullptr, *f_sb = nullptr;
+    uint32_t *scr = nullptr;  // fan-out hits (sender entries), receiver runs
+    size_t scr_cap = 0;
+    unsigned long long *scr_cursor = nullptr;
+    uint4 *f_rec = nullptr;  // 2 per entry
+    uint4 *f_frec = nullptr;
     size_t fan_cap = 0;
     uint4 *out = nullptr, *out_d = nullptr;
     size_t out_cap = 0, outd_cap = 0;  // in uint4
@@ -543,18 +748,23 @@ enum Arr128 { B_EID, B_CID, B_HKEY, B_N128 };
 
 ArrTable table32(SyncState *S) {
     ArrTable T{};
-    T.p[A_CGATE] = S->cgate;
-    T.p[A_QSPACE] = S->qspace;
-    T.p[A_SYNCING] = S->syncing;
-    T.p[A_SFLAGS] = S->sflags;
-    T.p[A_HVAL] = S->hval;
+    T.p[A_CGATE] = S->sst + SST_GATE;
+    T.p[A_QSPACE] = S->sst + SST_SPACE;
+    T.p[A_SYNCING] = S->sst + SST_SYNCING;
+    T.p[A_SFLAGS] = S->sst + SST_FLAGS;
+    for (int a = A_CGATE; a <= A_SFLAGS; ++a) T.stride[a] = 4;
+    T.p[A_HVAL] = reinterpret_cast<uint32_t *>(S->htab + 1);
+    T.stride[A_HVAL] = 8;
     return T;
 }
 ArrTable table128(SyncState *S) {
     ArrTable T{};
     T.p[B_EID] = S->eid;
+    T.stride[B_EID] = 1;
     T.p[B_CID] = S->cid;
-    T.p[B_HKEY] = S->hkey;
+    T.stride[B_CID] = 1;
+    T.p[B_HKEY] = S->htab;
+    T.stride[B_HKEY] = 2;
     return T;
 }
 
@@ -620,8 +830,8 @@ int push(SyncState *S) {
     if (!S->side.empty()) {
         const SideOp *o = reinterpret_cast<const SideOp *>(d + b128 + b32);
         const uint32_t n = (uint32_t)S->side.size();
-        k_side_claim<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->yclaim, S->sflags);
-        k_side_write<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->sclaim, S->yclaim, S->pos);
+        k_side_claim<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->cl, S->sst);
+        k_side_write<<<cdivu(n, ST), ST, 0, S->st>>>(o, n, S->cl, S->pos);
     }
     SY_TRY(hipGetLastError());
     S->w32.clear();
@@ -642,33 +852,27 @@ int create(gwaoi_world *w, SyncState **out) {
     S->hcap = cap;
     const size_t N = v.max_slots;
     int rc;
-    if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->cgate, N)) ||
-        (rc = salloc(S, &S->qspace, N)) || (rc = salloc(S, &S->syncing, N)) || (rc = salloc(S, &S->sflags, N)) ||
-        (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->sclaim, N)) || (rc = salloc(S, &S->yclaim, N)) ||
-        (rc = salloc(S, &S->oflag, N)) || (rc = salloc(S, &S->oflag_n, 1)) || (rc = salloc(S, &S->hkey, cap)) ||
-        (rc = salloc(S, &S->hval, cap))) {
+    if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->sst, 4 * N)) ||
+        (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->cl, 2 * N)) || (rc = salloc(S, &S->oflag, N)) ||
+        (rc = salloc(S, &S->oflag_n, 1)) || (rc = salloc(S, &S->htab, 2 * (size_t)cap))) {
         sync_destroy(S);
         return rc;
     }
-    bool ok = hipMemsetAsync(S->cgate, 0xFF, N * 4, S->st) == hipSuccess &&
-              hipMemsetAsync(S->syncing, 0, N * 4, S->st) == hipSuccess &&
-              hipMemsetAsync(S->sflags, 0, N * 4, S->st) == hipSuccess &&
-              hipMemsetAsync(S->pos, 0, N * 16, S->st) == hipSuccess &&
-              hipMemsetAsync(S->sclaim, 0, N * 8, S->st) == hipSuccess &&
-              hipMemsetAsync(S->yclaim, 0, N * 8, S->st) == hipSuccess &&
+    bool ok = hipMemsetAsync(S->pos, 0, N * 16, S->st) == hipSuccess &&
+              hipMemsetAsync(S->cl, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->oflag_n, 0, 4, S->st) == hipSuccess &&
               hipMemsetAsync(S->eid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->cid, 0, N * 16, S->st) == hipSuccess &&
-              hipMemsetAsync(S->hval, 0xFF, (size_t)cap * 4, S->st) == hipSuccess &&
+              hipMemsetAsync(S->htab, 0xFF, (size_t)cap * 32, S->st) == hipSuccess &&  // every slot H_EMPTY
               hipEventCreateWithFlags(&S->stage_ev, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         sync_destroy(S);
         return GWAOI_EDEVICE;
     }
     // space of every slot in call order (the world may hold entities already)
-    std::vector<uint32_t> qs(N);
-    for (uint32_t s = 0; s < N; ++s) qs[s] = world_slot_space(w, s);
-    if (hipMemcpyAsync(S->qspace, qs.data(), N * 4, hipMemcpyHostToDevice, S->st) != hipSuccess ||
+    std::vector<uint4> qs(N);
+    for (uint32_t s = 0; s < N; ++s) qs[s] = make_uint4(NO_GATE, world_slot_space(w, s), 0u, 0u);
+    if (hipMemcpyAsync(S->sst, qs.data(), N * 16, hipMemcpyHostToDevice, S->st) != hipSuccess ||
         hipStreamSynchronize(S->st) != hipSuccess) {
         sync_destroy(S);
         return GWAOI_EDEVICE;
@@ -739,8 +943,13 @@ int h_rehash(SyncState *S) {
         if (e.arr != B_HKEY) k128.push_back(e);
     S->w128.swap(k128);
     if (int rc = push(S)) return rc;
-    SY_TRY(hipMemcpyAsync(S->hkey, S->h_hkey.data(), (size_t)S->hcap * 16, hipMemcpyHostToDevice, S->st));
-    SY_TRY(hipMemcpyAsync(S->hval, S->h_hval.data(), (size_t)S->hcap * 4, hipMemcpyHostToDevice, S->st));
+    S->h_tab.resize(2 * (size_t)S->hcap);
+    for (size_t h = 0; h < S->hcap; ++h) {
+        S->h_tab[2 * h] = S->h_hkey[h];
+        S->h_tab[2 * h + 1] = make_uint4(S->h_hval[h], 0u, 0u, 0u);
+    }
+    SY_TRY(hipMemcpyAsync(S->htab, S->h_tab.data(), S->h_tab.size() * 16, hipMemcpyHostToDevice, S->st));
+    SY_TRY(hipStreamSynchronize(S->st));  // h_tab is pageable staging
     return GWAOI_OK;
 }
 
@@ -868,42 +1077,63 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     A.n_left = (uint32_t)n_left;
     A.eid = S->eid;
     A.cid = S->cid;
-    A.cgate = S->cgate;
-    A.sflags = S->sflags;
+    A.sst = S->sst;
     A.pos = S->pos;
     A.G = G;
     A.nb = nb;
     if (int rc = ensure_u32(S, &S->blk_cnt, &S->blk_cap, (size_t)G * nb + 1)) return rc;
     A.blk_cnt = S->blk_cnt;
     if (n_ent > S->fan_cap) {
-        sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec1); sfree(S->f_rec2);
+        sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec); sfree(S->f_frec);
+        sfree(S->f_cnt); sfree(S->f_sb);
         S->fan_cap = 0;
         const size_t c = std::max<size_t>(n_ent + n_ent / 8, 1024);
         int rc;
         if ((rc = salloc(S, &S->f_snd, c)) || (rc = salloc(S, &S->f_rg, c)) || (rc = salloc(S, &S->f_slot, c)) ||
-            (rc = salloc(S, &S->f_rec1, c)) || (rc = salloc(S, &S->f_rec2, c)))
+            (rc = salloc(S, &S->f_rec, 2 * c)) || (rc = salloc(S, &S->f_frec, c)) || (rc = salloc(S, &S->f_cnt, c)) ||
+            (rc = salloc(S, &S->f_sb, c)))
             return rc;
         S->fan_cap = c;
     }
+    int rc_scr = GWAOI_OK;
+    if (!S->scr_cursor && (rc_scr = salloc(S, &S->scr_cursor, 1))) return rc_scr;
+    A.fcnt = S->f_cnt;
+    A.fsb = S->f_sb;
     A.snd = S->f_snd;
     A.rg = S->f_rg;
     A.rslot = S->f_slot;
-    A.srec1 = S->f_rec1;
-    A.srec2 = S->f_rec2;
+    A.srec = S->f_rec;
+    A.frec = S->f_frec;
     if (n_ent) k_fan_prep<<<cdivu(n_ent, ST), ST, 0, S->st>>>(A);  // also clears the flags
-    const size_t lds = (2 * (size_t)G + 1) * 4;  // cursors + gate bins
     uint64_t total = 0;
     S->h_off_raw.assign(1, 0);
     if (G && n_ent) {
-        SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
-        k_fanout<0><<<nb, ST, lds, S->st>>>(A);
-        SY_TRY(hipGetLastError());
+        // pass 1: hits into the scratch; a run past the capacity is redone after a regrow
+        for (int attempt = 0;; ++attempt) {
+            if (S->scr_cap == 0 && (rc_scr = ensure_u32(S, &S->scr, &S->scr_cap, 32 * (size_t)n_ent))) return rc_scr;
+            A.scr = S->scr;
+            A.scr_cap = std::min<unsigned long long>(S->scr_cap, SCR_FULL - 1ull);
+            A.scr_cursor = S->scr_cursor;
+            SY_TRY(hipMemsetAsync(S->scr_cursor, 0, 8, S->st));
+            SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
+            k_fan_hits<<<nb, ST, (size_t)G * 4, S->st>>>(A);
+            SY_TRY(hipGetLastError());
+            unsigned long long used = 0;
+            SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
+            SY_TRY(hipStreamSynchronize(S->st));
+            if (used <= A.scr_cap) break;
+            if (attempt || used >= SCR_FULL) {
+                world_set_error(w, "sync: fan-out scratch exceeds 2^32 entries");
+                return GWAOI_ENOMEM;
+            }
+            if ((rc_scr = ensure_u32(S, &S->scr, &S->scr_cap, (size_t)used))) return rc_scr;
+        }
         if (int rc = part_bases(S, G, nb)) return rc;
         total = S->h_off_raw[G];
     }
     if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;
     A.out = S->out;
-    if (total) k_fanout<1><<<nb, ST, lds, S->st>>>(A);
+    if (total) k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
     SY_TRY(hipGetLastError());
     S->h_off.assign(S->h_off_raw.begin(), S->h_off_raw.end());
     if (to_host) {
@@ -976,26 +1206,23 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     DecodeArgs A{};
     A.pay = pay;
     A.n = (uint32_t)n;
-    A.hkey = S->hkey;
-    A.hval = S->hval;
+    A.htab = S->htab;
     A.hmask = S->hcap - 1;
-    A.qspace = S->qspace;
-    A.syncing = S->syncing;
+    A.sst = S->sst;
     A.o_slot = o_slot;
     A.o_sp = o_sp;
     A.o_x = o_x;
     A.o_z = o_z;
     A.o_ys = o_ys;
     A.claim0 = S->claim_next;
-    A.sclaim = S->sclaim;
-    A.yclaim = S->yclaim;
-    A.sflags = S->sflags;
+    A.cl = S->cl;
     A.pos = S->pos;
     A.oflag = S->oflag;
     A.oflag_n = S->oflag_n;
     S->claim_next += n;
     S->decoded = true;
     k_decode<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+    k_decode_fix<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_yaw<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     SY_TRY(hipGetLastError());
     return world_queue_decoded(w, o_slot, o_x, o_z, o_sp, n);
@@ -1016,11 +1243,11 @@ bool sync_slot_plain(const SyncState *S, uint32_t slot) { return slot < S->max_s
 void sync_destroy(SyncState *S) {
     if (!S) return;
     if (S->st) (void)hipStreamSynchronize(S->st);
-    sfree(S->eid); sfree(S->cid); sfree(S->cgate); sfree(S->qspace); sfree(S->syncing); sfree(S->sflags);
-    sfree(S->pos); sfree(S->sclaim); sfree(S->yclaim); sfree(S->oflag); sfree(S->oflag_n);
-    sfree(S->hkey); sfree(S->hval);
-    sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec1); sfree(S->f_rec2);
-    sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
+    sfree(S->eid); sfree(S->cid); sfree(S->sst);
+    sfree(S->pos); sfree(S->cl); sfree(S->oflag); sfree(S->oflag_n);
+    sfree(S->htab);
+    sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec); sfree(S->f_frec);
+    sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->scr); sfree(S->scr_cursor); sfree(S->f_cnt); sfree(S->f_sb); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
     sfree(S->d_stage);
     for (auto &c : S->arena) (void)hipFree(c.p);
     if (S->h_stage) (void)hipHostFree(S->h_stage);
@@ -1221,7 +1448,7 @@ int gwaoi_collect_client_events(gwaoi_world *w, gwaoi_gate_records *creates, gwa
         A.info = v.info;
         A.eid = S->eid;
         A.cid = S->cid;
-        A.cgate = S->cgate;
+        A.sst = S->sst;
         A.pos = S->pos;
         A.G = G;
         A.nb = nb;
