@@ -547,6 +547,7 @@ constexpr int RS_I = 16;
 constexpr int RS_TILE = RS_T * RS_I;
 constexpr int RS_WAVES = RS_T / WAVE;
 constexpr int RS_WSEG = WAVE * RS_I;
+static_assert(RS_T == 256, "the downsweep gives one thread per digit (<= 8-bit digits)");
 
 __global__ __launch_bounds__(RS_T) void k_rs_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
                                                      int nbits, uint32_t *hist, uint32_t ntiles) {
@@ -576,11 +577,25 @@ __global__ __launch_bounds__(RS_T) void k_rs_upsweep(const uint32_t *__restrict_
         hist[(size_t)d * ntiles + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
+#ifndef GWAOI_RS_LDS
+#define GWAOI_RS_LDS 1  // downsweep: tile regrouped by digit in LDS, then coalesced runs out (0: direct scatter)
+#endif
+
+// Stable scatter of one tile by digit.  Ranks come from wave multisplits
+// (per-wave digit counts in LDS).  With GWAOI_RS_LDS the tile is first
+// regrouped by digit in LDS, so that consecutive threads write consecutive
+// positions of a digit's run (coalesced stores) instead of scattering every key
+// to its own line.
 __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restrict__ keys_in,
                                                        const uint32_t *__restrict__ vals_in, uint32_t *keys_out,
                                                        uint32_t *vals_out, uint32_t n, int shift, int nbits,
                                                        const uint32_t *__restrict__ hist_scanned, uint32_t ntiles) {
     __shared__ uint32_t wcnt[RS_WAVES][256];
+#if GWAOI_RS_LDS
+    __shared__ uint32_t lkey[RS_TILE], lval[RS_TILE];
+    __shared__ uint32_t dstart[256], dglob[256];
+    __shared__ uint32_t s_ws[RS_WAVES];
+#endif
     const int bins = 1 << nbits;
     const uint32_t mask = (uint32_t)bins - 1u;
     const int w = threadIdx.x / WAVE;
@@ -618,6 +633,59 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
         rk[j] = base + (uint32_t)__popcll(peers & lt);
     }
     __syncthreads();
+#if GWAOI_RS_LDS
+    // tile-local layout: digit d's run starts at dstart[d]; wave w's keys of digit d follow the
+    // lower waves' (stability); the run goes to hist_scanned[d][tile] onwards
+    {
+        const int d = threadIdx.x;  // RS_T == 256 >= bins
+        uint32_t c[RS_WAVES], tot = 0;
+#pragma unroll
+        for (int ww = 0; ww < RS_WAVES; ++ww) {
+            c[ww] = d < bins ? wcnt[ww][d] : 0u;
+            tot += c[ww];
+        }
+        uint32_t x = tot;  // block exclusive scan of the digit totals
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (l >= o) x += y;
+        }
+        if (l == WAVE - 1) s_ws[w] = x;
+        __syncthreads();
+        uint32_t pre = x - tot;
+        for (int q = 0; q < w; ++q) pre += s_ws[q];
+        if (d < bins) {
+            dstart[d] = pre;
+            dglob[d] = hist_scanned[(size_t)d * ntiles + blockIdx.x];
+            uint32_t run = pre;
+#pragma unroll
+            for (int ww = 0; ww < RS_WAVES; ++ww) {
+                wcnt[ww][d] = run;
+                run += c[ww];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_I; ++j) {
+        const size_t idx = wbase + (size_t)j * WAVE + l;
+        if (idx < n) {
+            const uint32_t d = (k[j] >> shift) & mask;
+            const uint32_t p = wcnt[w][d] + rk[j];
+            lkey[p] = k[j];
+            lval[p] = v[j];
+        }
+    }
+    __syncthreads();
+    const size_t t0 = (size_t)blockIdx.x * RS_TILE;
+    const uint32_t tn = (uint32_t)min((size_t)RS_TILE, (size_t)n - t0);
+    for (uint32_t t = threadIdx.x; t < tn; t += RS_T) {
+        const uint32_t key = lkey[t], d = (key >> shift) & mask;
+        const uint32_t pos = dglob[d] + (t - dstart[d]);
+        keys_out[pos] = key;
+        vals_out[pos] = lval[t];
+    }
+#else
     for (int d = threadIdx.x; d < bins; d += RS_T) {
         uint32_t run = hist_scanned[(size_t)d * ntiles + blockIdx.x];
 #pragma unroll
@@ -638,6 +706,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
             vals_out[pos] = v[j];
         }
     }
+#endif
 }
 
 // ------------------------------------------------- incremental frame sort ------
