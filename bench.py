@@ -507,7 +507,7 @@ def main():
                          "CollectEntitySyncInfos fan-out (0 = off)")
     ap.add_argument("--sync-clients", type=float, default=0.5,
                     help="fraction of entities with a client (players) in the sync leg")
-    ap.add_argument("--host-io-steps", type=int, default=10,
+    ap.add_argument("--host-io-steps", type=int, default=30,
                     help="extra ticks timed with host move batches in and host event arrays out (PCIe-inclusive), "
                          "serial and pipelined")
     ap.add_argument("--host-tick-steps", type=int, default=10,
@@ -681,6 +681,10 @@ def main():
             issue = nxt
         p_el = time.perf_counter() - p0
         gc.enable()
+        # the first pipelined tick has no flush before it to hide its staging behind: it is the
+        # pipeline's fill, reported apart from the steady percentiles
+        p_first = p_lat[0]
+        p_lat = p_lat[1:] if len(p_lat) > 1 else p_lat
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -688,13 +692,14 @@ def main():
         sl_ms, pl_ms = np.array(s_lat) * 1e3, np.array(p_lat) * 1e3
         host_io = {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
                    "p50_tick_ms": float(np.percentile(pl_ms, 50)), "p99_tick_ms": float(np.percentile(pl_ms, 99)),
-                   "steps": len(pb),
+                   "steps": len(pb), "first_tick_ms": p_first * 1e3,
                    "serial": {"ms_per_step": s_el / hio * 1e3, "p50_tick_ms": float(np.percentile(sl_ms, 50)),
                               "p99_tick_ms": float(np.percentile(sl_ms, 99)), "steps": hio,
                               "events_per_s": h_evs / max(s_el, 1e-9)},
                    "note": "pipelined: the moved_batch of tick t+1 (validation, pinned staging, H2D on a copy "
                            "stream) overlaps the flush of tick t; p50/p99 = from the batch call to the events in "
-                           "pinned host memory; serial = moved_batch + tick back to back. Not the headline value"}
+                           "pinned host memory, over the ticks after the first (the pipeline fill, first_tick_ms); "
+                           "serial = moved_batch + tick back to back. Not the headline value"}
     sync = sync_leg(w, n, sync_batches, args.sync_clients) if sync_batches else None
     elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], red_dev)
     w.close()

@@ -7,6 +7,6 @@ this package holds its ctypes binding (``_lib``), the host-side mirror of the
 go-aoi interface (``aoi``), the seeded workloads (``workload``) and the
 in-tree build (``build``).
 """
-from ._lib import GwaoiError, World, load, pair_keys  # noqa: F401
+from ._lib import GwaoiError, Wire, World, load, pair_keys  # noqa: F401
 
-__all__ = ["World", "GwaoiError", "load", "pair_keys"]
+__all__ = ["World", "Wire", "GwaoiError", "load", "pair_keys"]

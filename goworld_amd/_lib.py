@@ -54,6 +54,14 @@ SYNC_EXPORTS = [
     "gwaoi_entity_leave_plain",
 ]
 
+# every function include/gwaoi_wire.h declares
+WIRE_EXPORTS = [
+    "gwaoi_wire_create", "gwaoi_wire_destroy", "gwaoi_wire_last_error", "gwaoi_wire_set_entity_games",
+    "gwaoi_wire_remove_entities", "gwaoi_wire_set_clients", "gwaoi_wire_remove_clients",
+    "gwaoi_wire_gate_from_clients", "gwaoi_wire_gate_from_clients_device", "gwaoi_wire_dispatcher_to_games",
+    "gwaoi_wire_dispatcher_to_games_device", "gwaoi_wire_gate_to_clients", "gwaoi_wire_gate_to_clients_device",
+]
+
 SYNC_OUT_REC = 48  # ClientID[16] + EntityID[16] + x,y,z,yaw float32 (Entity.go:1233-1251)
 DESTROY_REC = 32   # ClientID[16] + EntityID[16]
 SIF_OWN_CLIENT, SIF_NEIGHBOR_CLIENTS = 1, 2
@@ -83,6 +91,11 @@ class StripsConfig(C.Structure):
 class GateRecords(C.Structure):
     _fields_ = [("n_gates", C.c_uint32), ("gate_ids", C.POINTER(C.c_uint16)),
                 ("offsets", C.POINTER(C.c_uint64)), ("records", C.c_void_p)]
+
+
+class WireGroups(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("keys", C.POINTER(C.c_uint32)), ("offsets", C.POINTER(C.c_uint64)),
+                ("records", C.c_void_p), ("rec_bytes", C.c_uint32), ("n_dropped", C.c_uint64)]
 
 
 class Debug(C.Structure):
@@ -177,6 +190,19 @@ def load():
         "gwaoi_collect_sync_infos": ([vp, P(GateRecords)], C.c_int),
         "gwaoi_collect_sync_infos_device": ([vp, P(GateRecords)], C.c_int),
         "gwaoi_collect_client_events": ([vp, P(GateRecords), P(GateRecords)], C.c_int),
+        "gwaoi_wire_create": ([C.c_int, P(vp)], C.c_int),
+        "gwaoi_wire_destroy": ([vp], None),
+        "gwaoi_wire_last_error": ([vp], C.c_char_p),
+        "gwaoi_wire_set_entity_games": ([vp, vp, vp, sz], C.c_int),
+        "gwaoi_wire_remove_entities": ([vp, vp, sz], C.c_int),
+        "gwaoi_wire_set_clients": ([vp, vp, vp, sz], C.c_int),
+        "gwaoi_wire_remove_clients": ([vp, vp, sz], C.c_int),
+        "gwaoi_wire_gate_from_clients": ([vp, vp, sz, u32, P(WireGroups)], C.c_int),
+        "gwaoi_wire_gate_from_clients_device": ([vp, vp, sz, u32, P(WireGroups)], C.c_int),
+        "gwaoi_wire_dispatcher_to_games": ([vp, vp, sz, P(WireGroups)], C.c_int),
+        "gwaoi_wire_dispatcher_to_games_device": ([vp, vp, sz, P(WireGroups)], C.c_int),
+        "gwaoi_wire_gate_to_clients": ([vp, vp, sz, P(WireGroups)], C.c_int),
+        "gwaoi_wire_gate_to_clients_device": ([vp, vp, sz, P(WireGroups)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -506,3 +532,104 @@ def pair_keys(pairs: np.ndarray) -> np.ndarray:
         return np.empty(0, np.uint64)
     k = (pairs[:, 0].astype(np.uint64) << np.uint64(32)) | pairs[:, 1].astype(np.uint64)
     return np.sort(k)
+
+
+class Wire:
+    """The position-sync wire regroups of a gate or a dispatcher on the GPU
+    (include/gwaoi_wire.h): GateService.handleSyncPositionYawFromClient +
+    tryFlushPendingSyncPackets, DispatcherService.handleSyncPositionYawFromClient
+    + sendEntitySyncInfosToGames, GateService.handleSyncPositionYawOnClients.
+    Each regroup returns ``{destination key: bytes}`` (host) in key order."""
+
+    def __init__(self, device: int = 0):
+        self._L = load()
+        h = C.c_void_p()
+        rc = self._L.gwaoi_wire_create(device, C.byref(h))
+        if rc != 0:
+            raise GwaoiError(rc, self._L.gwaoi_strerror(rc).decode())
+        self._w = h
+
+    def close(self):
+        if getattr(self, "_w", None):
+            self._L.gwaoi_wire_destroy(self._w)
+            self._w = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise GwaoiError(rc, self._L.gwaoi_strerror(rc).decode() + " (" +
+                             self._L.gwaoi_wire_last_error(self._w).decode() + ")")
+
+    @staticmethod
+    def _ids(ids) -> np.ndarray:
+        a = np.ascontiguousarray(np.frombuffer(b"".join(ids), np.uint8) if isinstance(ids, (list, tuple))
+                                 else np.asarray(ids, np.uint8))
+        assert a.size % 16 == 0
+        return a
+
+    def set_entity_games(self, ids, games):
+        a, g = self._ids(ids), np.ascontiguousarray(games, np.uint16)
+        self._check(self._L.gwaoi_wire_set_entity_games(self._w, _p(a), _p(g), g.size))
+
+    def remove_entities(self, ids):
+        a = self._ids(ids)
+        self._check(self._L.gwaoi_wire_remove_entities(self._w, _p(a), a.size // 16))
+
+    def set_clients(self, ids, index):
+        a, x = self._ids(ids), np.ascontiguousarray(index, np.uint32)
+        self._check(self._L.gwaoi_wire_set_clients(self._w, _p(a), _p(x), x.size))
+
+    def remove_clients(self, ids):
+        a = self._ids(ids)
+        self._check(self._L.gwaoi_wire_remove_clients(self._w, _p(a), a.size // 16))
+
+    @staticmethod
+    def _groups(g: WireGroups, on_device: bool):
+        n = g.n_groups
+        keys = np.ctypeslib.as_array(g.keys, shape=(n,)).copy() if n else np.empty(0, np.uint32)
+        off = np.ctypeslib.as_array(g.offsets, shape=(n + 1,)).copy()
+        if on_device:
+            return keys, off, g.records, int(g.n_dropped)
+        total = int(off[-1]) * g.rec_bytes
+        buf = C.string_at(g.records, total) if total else b""
+        return {int(k): buf[int(off[i]) * g.rec_bytes:int(off[i + 1]) * g.rec_bytes] for i, k in enumerate(keys)}, \
+            int(g.n_dropped)
+
+    def _call(self, fn, data, *extra, rec=32):
+        buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(data)
+        assert buf.size % rec == 0
+        g = WireGroups()
+        self._check(fn(self._w, _p(buf) if buf.size else None, buf.size // rec, *extra, C.byref(g)))
+        return self._groups(g, False)
+
+    def gate_from_clients(self, records: bytes, n_dispatchers: int):
+        return self._call(self._L.gwaoi_wire_gate_from_clients, records, n_dispatchers)
+
+    def dispatcher_to_games(self, records: bytes):
+        return self._call(self._L.gwaoi_wire_dispatcher_to_games, records)
+
+    def gate_to_clients(self, records: bytes):
+        return self._call(self._L.gwaoi_wire_gate_to_clients, records, rec=48)
+
+    def _call_device(self, fn, d_ptr: int, n: int, *extra):
+        g = WireGroups()
+        self._check(fn(self._w, C.c_void_p(d_ptr) if n else None, n, *extra, C.byref(g)))
+        return self._groups(g, True)
+
+    def gate_from_clients_device(self, d_ptr: int, n: int, n_dispatchers: int):
+        """(keys, offsets, device records pointer, n_dropped)."""
+        return self._call_device(self._L.gwaoi_wire_gate_from_clients_device, d_ptr, n, n_dispatchers)
+
+    def dispatcher_to_games_device(self, d_ptr: int, n: int):
+        return self._call_device(self._L.gwaoi_wire_dispatcher_to_games_device, d_ptr, n)
+
+    def gate_to_clients_device(self, d_ptr: int, n: int):
+        return self._call_device(self._L.gwaoi_wire_gate_to_clients_device, d_ptr, n)

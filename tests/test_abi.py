@@ -28,10 +28,12 @@ def test_header_lists_match_binding():
     assert header_functions() == sorted(_lib.EXPORTS)
     assert header_functions("gwaoi_strips.h") == sorted(_lib.STRIP_EXPORTS)
     assert header_functions("gwaoi_sync.h") == sorted(_lib.SYNC_EXPORTS)
+    assert header_functions("gwaoi_wire.h") == sorted(_lib.WIRE_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol(lib):
-    for name in header_functions() + header_functions("gwaoi_strips.h") + header_functions("gwaoi_sync.h"):
+    for name in (header_functions() + header_functions("gwaoi_strips.h") + header_functions("gwaoi_sync.h") +
+                 header_functions("gwaoi_wire.h")):
         assert hasattr(lib, name), name
         assert C.cast(getattr(lib, name), C.c_void_p).value
 
@@ -49,6 +51,11 @@ def test_pure_host_entry_points(lib):
     assert lib.gwaoi_sync_from_clients(None, None, 0) == -1
     assert lib.gwaoi_collect_sync_infos(None, None) == -1
     assert lib.gwaoi_collect_client_events(None, None, None) == -1
+    # wire regroups validate the handle first
+    assert lib.gwaoi_wire_create(0, None) == -1
+    assert lib.gwaoi_wire_gate_from_clients(None, None, 0, 4, None) == -1
+    assert lib.gwaoi_wire_gate_to_clients(None, None, 0, None) == -1
+    assert lib.gwaoi_wire_set_clients(None, None, None, 0) == -1
 
 
 def test_library_is_gfx950_code_object():
