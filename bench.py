@@ -379,7 +379,8 @@ def cpu_baseline(args, wl_factory, target_s: float):
 def run_strips(args, ws, rank, local, dist):
     """Config 5: one 2^24-entity space cut into one x-strip per rank; every
     tick routes the owned moves, exchanges halo records over RCCL
-    (all_gather of counts + all_to_all of records) and flushes each strip's
+    (counts all-gathered on the host over gloo, records point to point to the
+    neighbour strips in one RCCL send/recv group) and flushes each strip's
     world (goworld_amd/strips.py).  Inputs are generated on the GPU before
     timing (DeviceUniformWorkload); value = all N moves per tick / max time."""
     import torch
@@ -388,6 +389,8 @@ def run_strips(args, ws, rank, local, dist):
     from goworld_amd.workload import DeviceUniformWorkload
 
     dev = torch.device(f"cuda:{local}")
+    if dist is not None:
+        dist.barrier()  # RCCL's communicator exists before the first batched send/recv
     n = args.n or (1 << 24)
     t_setup = time.perf_counter()
     wl = DeviceUniformWorkload(n, 0x5EED0005, dev)
@@ -464,7 +467,8 @@ def run_strips(args, ws, rank, local, dist):
             "data": "synthetic (torch Philox on the GPU, generated before timing, resident in HBM)",
             "config": {"workload": f"cfg5: {WORKLOAD_DESC['cfg5']}", "entities": n, "strips": ws,
                        "aoi_distance": float(D_CFG5), "halo": sh.halo,
-                       "parallelism": f"one x-strip per rank x{ws}, halo records all_to_all over RCCL"},
+                       "parallelism": f"one x-strip per rank x{ws}, halo records point to point (RCCL send/recv) "
+                                              "to the neighbour strips"},
             "events_per_s": events_all / el_max,
             "p50_tick_ms": float(np.percentile(lat_ms, 50)), "p99_tick_ms": float(np.percentile(lat_ms, 99)),
             "events_per_tick": events_all / max(args.steps, 1), "initial_enter_events_rank0": ne0,
@@ -657,6 +661,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         h_ev, s_lat = 0, []
+        import gc
+        gc.disable()  # no collector pauses inside the timed ticks
         h0 = time.perf_counter()
         for sl, nx, nz in host_batches[1:hio + 1]:
             a = time.perf_counter()
@@ -667,8 +673,6 @@ def main():
         s_el = time.perf_counter() - h0
         pb = host_batches[hio + 1:]
         p_lat = []
-        import gc
-        gc.disable()  # no collector pauses inside the timed ticks
         w.moved_batch(*pb[0])
         p0 = issue = time.perf_counter()
         for k in range(len(pb)):

@@ -1310,25 +1310,44 @@ size_t stage_chunk(const gwaoi_world *w, const uint32_t *slots, const float *x, 
                    size_t lo, size_t hi, uint32_t *h, bool with_space, StageBox *boxes, int *st) {
     uint32_t *hs = h, *hsp = h + 3 * n;
     float *hx = reinterpret_cast<float *>(h + n), *hz = reinterpret_cast<float *>(h + 2 * n);
-    const uint8_t *alive = w->alive.data();
+    // a live slot has a space (space_of == SP_DEAD <=> !alive): one random lookup per move
     const uint32_t *space_of = w->space_of.data();
+    const uint32_t ms = w->max_slots;
+    // The running box of the current space stays in registers: updated through a StageBox in
+    // memory, every float store to hx/hz may alias it and the loop became a load-store chain.
+    uint32_t bsp = gw::SP_DEAD;
+    float bx0 = 0.f, bz0 = 0.f, bx1 = 0.f, bz1 = 0.f;
+    auto fold = [&]() {
+        if (bsp == gw::SP_DEAD) return;
+        StageBox &b = boxes[bsp];
+        if (!b.any) {
+            b = StageBox{bx0, bz0, bx1, bz1, true};
+        } else {
+            b.x0 = std::min(b.x0, bx0); b.x1 = std::max(b.x1, bx1);
+            b.z0 = std::min(b.z0, bz0); b.z1 = std::max(b.z1, bz1);
+        }
+    };
     for (size_t i = lo; i < hi; ++i) {
+        if (i + 16 < hi) __builtin_prefetch(space_of + std::min(slots[i + 16], ms - 1));
         const uint32_t sl = slots[i];
         const float xi = x[i], zi = z[i];
-        if (sl >= w->max_slots) { *st = GWAOI_EBADSLOT; return i; }
-        if (!alive[sl]) { *st = GWAOI_ESTATE; return i; }
-        if (!finite2(xi, zi)) { *st = GWAOI_ENONFINITE; return i; }
+        if (sl >= ms) { *st = GWAOI_EBADSLOT; return i; }
         const uint32_t sp = space_of[sl];
+        if (sp == gw::SP_DEAD) { *st = GWAOI_ESTATE; return i; }
+        if (!finite2(xi, zi)) { *st = GWAOI_ENONFINITE; return i; }
         hs[i] = sl; hx[i] = xi; hz[i] = zi;
         if (with_space) hsp[i] = sp;
-        StageBox &b = boxes[sp];
-        if (!b.any) {
-            b = StageBox{xi, zi, xi, zi, true};
+        if (sp != bsp) {
+            fold();
+            bsp = sp;
+            bx0 = bx1 = xi;
+            bz0 = bz1 = zi;
         } else {
-            b.x0 = std::min(b.x0, xi); b.x1 = std::max(b.x1, xi);
-            b.z0 = std::min(b.z0, zi); b.z1 = std::max(b.z1, zi);
+            bx0 = std::min(bx0, xi); bx1 = std::max(bx1, xi);
+            bz0 = std::min(bz0, zi); bz1 = std::max(bz1, zi);
         }
     }
+    fold();
     *st = GWAOI_OK;
     return hi;
 }

@@ -10,9 +10,12 @@ halo H of its strip.  Each tick:
    entities the rank owned before it (Moved / Leave) or that enter the space
    inside its strip (Enter) become halo records per destination rank, plus
    teleport records (HIP kernels, ``k_route``).
-2. ``exchange``: one ``all_to_all_single`` of the records over RCCL (xGMI),
-   after an ``all_gather`` of the per-destination counts; teleport records
-   are all-gathered.  This is the path's one real data exchange.
+2. ``exchange``: the per-destination counts (already on the host) are
+   all-gathered over gloo, then the records go point to point in one
+   ``batch_isend_irecv`` group over RCCL (xGMI) -- to the two neighbour
+   strips only, when strips are at least H + teleport wide; teleport records
+   are all-gathered only when some rank has any.  This is the path's one real
+   data exchange.
 3. ``StripShard.finish(recv, tele)``: the records become ops of the rank's
    gwaoi world (explicit global seqs), the world flushes, and only the events
    this strip owns are kept (enter: owner after the tick; leave: owner
@@ -187,12 +190,33 @@ def local_slice(send, counts, rank):
     return send[int(c[rank]):int(c[rank + 1])]
 
 
+_COUNT_GROUPS = {}
+
+
+def count_group(dist, group=None):
+    """The process group that carries the per-destination counts: gloo, on
+    host tensors.  route() has the counts on the host already (its scatter is
+    sized by them), so exchanging them over gloo costs no device sync; with a
+    gloo job it is the job's own group.  Created once per job (collective:
+    every rank calls exchange the same way)."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group)
+    if key not in _COUNT_GROUPS:
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        _COUNT_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _COUNT_GROUPS[key]
+
+
 def exchange(dist, send, counts, tele, group=None, via_cpu=False):
-    """The halo exchange of one tick over torch.distributed (RCCL on GPU
-    tensors, gloo on CPU ones): counts all-gathered, the records for other
-    ranks all-to-all'd (a rank's own slice stays put: ``local_slice``),
-    teleport records all-gathered.  Returns (records from the other ranks,
-    all teleports).
+    """The halo exchange of one tick over torch.distributed: the count matrix
+    is all-gathered on the host (gloo, ``count_group``), then every record
+    travels point to point, batched in one group (``batch_isend_irecv``:
+    RCCL send/recv over xGMI for GPU tensors) from its source to its
+    destination only -- for strips at least H + teleport wide these are the
+    two neighbours -- and a rank's own slice stays put (``local_slice``).
+    Teleport records are all-gathered only when some rank has any.  Returns
+    (records from the other ranks in source-rank order, all teleports).
     via_cpu: GPU tensors go through host memory (gloo rehearsal of several
     ranks sharing one GPU; RCCL allows one rank per device)."""
     import torch
@@ -204,28 +228,35 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     S = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = send.device
-    mine = torch.tensor(list(np.asarray(counts, np.int64)) + [int(tele.shape[0])], dtype=torch.int64, device=dev)
+    mine = torch.tensor(list(np.asarray(counts, np.int64)) + [int(tele.shape[0])], dtype=torch.int64)
     rows = [torch.empty_like(mine) for _ in range(S)]
-    dist.all_gather(rows, mine, group=group)
-    M = torch.stack(rows).cpu().numpy()  # M[src, dst]; column S = teleports of src
-    in_splits = [int(v) for v in M[rank, :S]]
-    out_splits = [int(v) for v in M[:, rank]]
-    # the own slice is cut out on both sides: send without it, receive without it
-    lo = sum(in_splits[:rank])
-    if in_splits[rank]:
-        send = torch.cat([send[:lo], send[lo + in_splits[rank]:]])
-    in_splits[rank] = out_splits[rank] = 0
-    recv = torch.empty((sum(out_splits), send.shape[1]), dtype=send.dtype, device=dev)
-    dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
+    dist.all_gather(rows, mine, group=count_group(dist, group))
+    M = torch.stack(rows).numpy()  # M[src, dst]; column S = teleports of src (host tensors: no device sync)
+    off = np.concatenate([[0], np.cumsum(M[rank, :S])]).astype(np.int64)
+    peer = (lambda q: q) if group is None else (lambda q: dist.get_global_rank(group, q))
+    ops, parts = [], []
+    for q in range(S):
+        if q == rank:
+            continue
+        if M[rank, q]:
+            ops.append(dist.P2POp(dist.isend, send[int(off[q]):int(off[q + 1])], peer(q), group))
+        if M[q, rank]:
+            buf = torch.empty((int(M[q, rank]), send.shape[1]), dtype=send.dtype, device=dev)
+            parts.append(buf)
+            ops.append(dist.P2POp(dist.irecv, buf, peer(q), group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    recv = torch.cat(parts) if parts else send[:0]
     T = M[:, S]
     if T.sum() == 0:
         return recv, tele[:0]
     pad = int(T.max())
     buf = torch.zeros((pad, tele.shape[1]), dtype=tele.dtype, device=dev)
     buf[:tele.shape[0]] = tele
-    parts = [torch.empty_like(buf) for _ in range(S)]
-    dist.all_gather(parts, buf, group=group)
-    return recv, torch.cat([parts[r][:int(T[r])] for r in range(S)])
+    gathered = [torch.empty_like(buf) for _ in range(S)]
+    dist.all_gather(gathered, buf, group=group)
+    return recv, torch.cat([gathered[r][:int(T[r])] for r in range(S)])
 
 
 def exchange_local(outs: List[Tuple]):

@@ -99,8 +99,12 @@ def _worker(rank, ws, port, seed, ticks, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_strip_exchange(oracle_mod):
-    ws, seed, ticks = 2, 5, 4
+@pytest.mark.parametrize("ws", [2, 3])
+def test_gloo_strip_exchange(oracle_mod, ws):
+    """ws ranks over gloo: counts all-gathered on the host, records point to
+    point (3 ranks: the middle strip talks to both neighbours, the outer ones
+    reach each other only through teleports)."""
+    seed, ticks = 5, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -111,6 +115,7 @@ def test_two_rank_gloo_strip_exchange(oracle_mod):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    got = [tuple(np.array(parts[0][t][i] + parts[1][t][i], np.uint64) for i in (0, 1)) for t in range(ticks)]
+    got = [tuple(np.array(sum((parts[r][t][i] for r in range(ws)), []), np.uint64) for i in (0, 1))
+           for t in range(ticks)]
     ref = reference_ticks(oracle_mod, Scenario(n0=3000, n_strips=ws, seed=seed), ticks)
     assert_same(got, ref)
