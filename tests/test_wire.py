@@ -4,7 +4,7 @@ oracle/wire.py (GateService.go:346-371, 398-425; DispatcherService.go:786-825).
 
 CPU tests pin the restatement on hand-derived cases read off the Go source
 (the reference holds no test or fixture for these handlers: parity for this
-row is against the restatement, DESIGN.md §3d).  GPU tests compare the
+row is against the restatement, DESIGN.md §3c).  GPU tests compare the
 libgwaoi regroups with the restatement byte for byte, per destination.
 """
 import struct
