@@ -282,6 +282,9 @@ __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, u
 
 // --------------------------------------------------------------- keygen ------
 
+#ifndef GWAOI_CAND_SPLIT
+#define GWAOI_CAND_SPLIT 0  // 1: candidates as two 8-B arrays {x, z} | {old x, old z}, old read by band hits only (measured 0.170 vs 0.124 ms: the dependent second load costs more than the bytes it saves)
+#endif
 constexpr float FAR_FRAC = 0.25f;  // displacement > FAR_FRAC * D per axis => "special"
 
 // "near" = live at t-1 and at t in the same space and moved at most
@@ -1056,7 +1059,7 @@ __device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], in
 
 // --------------------------------------------------------------- gather ------
 
-__device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
+__device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev, uint32_t n_new,
                                            const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
                                            Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
@@ -1078,12 +1081,12 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     uint32_t cur = SP_DEAD;
     int bv[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
-    if (k < n_new) gather_one(k, perm, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand, grid, seq_base,
+    if (k < n_new) gather_one(k, perm, n_prev, n_new, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand, grid, seq_base,
                               info, sorted_keys, sentinel, n_total, sc, f_key, cur, bv);
     bbox_block(cur, bv, bbox, n_spaces, &parts[blockIdx.x]);
 }
 
-__device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev,
+__device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev, uint32_t n_new,
                                            const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
                                            Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
@@ -1111,7 +1114,14 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     if (i < n_prev && ld_ss(p_ss, i).sp == ss.sp) o = ld_rec(p_rec, i);
     st_rec(o_rec, k, o);
     const float thr = FAR_FRAC * grid[ss.sp].D;
-    cand[k] = cand_of(now, o, thr);
+    const uint4 c = cand_of(now, o, thr);
+#if GWAOI_CAND_SPLIT
+    reinterpret_cast<uint2 *>(cand)[k] = make_uint2(c.x, c.y);           // {x, z}: what every sweep streams
+    reinterpret_cast<uint2 *>(cand)[n_new + k] = make_uint2(c.z, c.w);   // {old x, old z}: band hits only
+#else
+    (void)n_new;
+    cand[k] = c;
+#endif
     cur = ss.sp;
     bv[0] = bv[2] = f2o(now.x);
     bv[1] = bv[3] = f2o(now.z);
@@ -1611,6 +1621,27 @@ __device__ __forceinline__ void qpush(uint32_t *qb, uint8_t *qa, WaveQueue &Q, b
 // distance is <= D - M both times, and unrelated both times when it is
 // > D + M both times, whichever member owns the window (M covers the float32
 // rounding of the window bounds and of the differences).
+// Split layout: the band test on {x, z} ...
+template <int MODE>
+__device__ __forceinline__ bool band_xz(const LaneA &A, const CombinedCtx &C, const uint2 &k, uint32_t b) {
+    const float lo = C.lo, hi = C.hi;
+    const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
+    if (MODE == 2) {
+        const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
+        return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
+    }
+    return MODE == 0 ? (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi)
+                     : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
+}
+// ... then, for band hits only, the unchanged-relation test with {old x, old z}.
+__device__ __forceinline__ bool same_rel(const LaneA &A, const CombinedCtx &C, const uint2 &k, const uint2 &o) {
+    const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
+    const float dn = fmaxf(fabsf(dx), fabsf(dz));
+    const float dxo = __uint_as_float(o.x) - A.xo, dzo = __uint_as_float(o.y) - A.zo;
+    const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
+    return ((int)(dn <= C.in_max) & (int)(dold <= C.in_max)) | ((int)(dn > C.out_min) & (int)(dold > C.out_min));
+}
+
 template <int MODE>
 __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint4 &k, uint32_t b) {
     const float lo = C.lo, hi = C.hi;
@@ -1652,6 +1683,31 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                         cap, pe, pl, replay);
             Q.qn = 0;
         }
+#if GWAOI_CAND_SPLIT
+        {
+            const uint2 *c2 = reinterpret_cast<const uint2 *>(cand);
+            uint2 k[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) k[u] = c2[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
+            bool bd[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) bd[u] = band_xz<MODE>(A, C, k[u], jb + t + (uint32_t)u) & (t + (uint32_t)u < len);
+            uint2 o[U];
+            if (MODE != 2) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {  // only band hits read the old positions
+                    o[u] = make_uint2(0u, 0u);
+                    if (bd[u]) o[u] = c2[F.n + jb + t + (uint32_t)u];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool keep = MODE == 2 ? bd[u] : (bd[u] && !same_rel(A, C, k[u], o[u]));
+                qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), jb + t + (uint32_t)u);
+            }
+            continue;
+        }
+#endif
         uint4 k[U];
 #ifdef GWAOI_EXP_8B  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
 #pragma unroll
@@ -1911,7 +1967,11 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         const uint32_t a = e0 + tid;
         uint32_t cls = NCLS - 1;  // past the frame
         if (a < F.n) {
+#if GWAOI_CAND_SPLIT
+            const uint2 c0 = reinterpret_cast<const uint2 *>(cand)[a];
+#else
             const uint4 c0 = cand[a];
+#endif
             const Rec16 r0 = ld_rec(F.rec, a);
             const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
             const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f, BW = 2.0f * sc->d_rel * g.D + M;
@@ -1944,7 +2004,13 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     A.a = e0 + off;
     A.valid = A.a < F.n;
     const uint32_t ia = A.valid ? A.a : 0u;
+#if GWAOI_CAND_SPLIT
+    const uint2 cxz = reinterpret_cast<const uint2 *>(cand)[ia];
+    const uint2 cold = reinterpret_cast<const uint2 *>(cand)[F.n + ia];
+    const uint4 ca = make_uint4(cxz.x, cxz.y, cold.x, cold.y);
+#else
     const uint4 ca = cand[ia];
+#endif
     const Rec16 ra = ld_rec(F.rec, ia);  // exact position (a jumper's candidate record is NaN)
     A.x = ra.x;
     A.z = ra.z;

@@ -51,6 +51,26 @@ __host__ __device__ inline uint32_t id_hash(uint32_t a, uint32_t b, uint32_t c, 
     return (uint32_t)h;
 }
 
+// Streaming 16-B store (GWAOI_NT_STORES): the fan-out's output and scratch are
+// written once and read by another kernel, so they need not take L2 lines
+// from the sender records the record gathers re-read.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+#ifndef GWAOI_NT_STORES
+#define GWAOI_NT_STORES 0  // 1: nontemporal stores (measured collect 1.49 vs 1.39 ms: slower)
+#endif
+__device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
+#if GWAOI_NT_STORES
+    u32x4_t t;
+    t.x = v.x;
+    t.y = v.y;
+    t.z = v.z;
+    t.w = v.w;
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x4_t *>(p));
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ bool eq4(uint4 a, uint4 b) {
     return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
 }
@@ -462,13 +482,13 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
                             default: buf.w = b; break;
                         }
                         ++c;
-                        if (!(c & 3u) && fits) run[(c >> 2) - 1u] = buf;
+                        if (!(c & 3u) && fits) st_stream(run + (c >> 2) - 1u, buf);
                     }
                 }
             }
         }
     }
-    if ((c & 3u) && fits) run[c >> 2] = buf;
+    if ((c & 3u) && fits) st_stream(run + (c >> 2), buf);
     if (i < ne) {
         A.fcnt[i] = c;
         A.fsb[i] = sb;
@@ -554,7 +574,7 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
 #pragma unroll
         for (uint32_t j = 0; j < 3; ++j) {
             const uint32_t e = ln + 64u * j, rr = e / 3u;
-            if (rr < nrec) A.out[3 * (size_t)s_pos[w][rr] + (e - 3u * rr)] = s_rec[w][e];
+            if (rr < nrec) st_stream(A.out + 3 * (size_t)s_pos[w][rr] + (e - 3u * rr), s_rec[w][e]);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
