@@ -1488,6 +1488,9 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_SW_PIPE
+#define GWAOI_SW_PIPE 0  // 1: sweep loads of iteration t+1 issued before iteration t's filter
+#endif
 #ifndef GWAOI_BALLOT_LOOPS
 #define GWAOI_BALLOT_LOOPS 1  // sweep loops end on a ballot of the lanes' own bounds, not a wave max (6 bpermutes)
 #endif
@@ -1634,7 +1637,7 @@ __device__ __forceinline__ bool band_xz(const LaneA &A, const CombinedCtx &C, co
                      : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
 }
 // ... then, for band hits only, the unchanged-relation test with {old x, old z}.
-__device__ __forceinline__ bool same_rel(const LaneA &A, const CombinedCtx &C, const uint2 &k, const uint2 &o) {
+[[maybe_unused]] __device__ __forceinline__ bool same_rel(const LaneA &A, const CombinedCtx &C, const uint2 &k, const uint2 &o) {
     const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
     const float dn = fmaxf(fabsf(dx), fabsf(dz));
     const float dxo = __uint_as_float(o.x) - A.xo, dzo = __uint_as_float(o.y) - A.zo;
@@ -1670,6 +1673,11 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                                             const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
+#if GWAOI_SW_PIPE
+    uint4 kn[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) kn[u] = cand[(uint32_t)u < len ? jb + (uint32_t)u : 0u];
+#endif
 #if GWAOI_BALLOT_LOOPS
     (void)mx;
     for (uint32_t t = 0; __ballot(t < len); t += U) {  // to the wave's longest range (scalar mask test)
@@ -1709,7 +1717,16 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
         }
 #endif
         uint4 k[U];
-#ifdef GWAOI_EXP_8B  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
+#if GWAOI_SW_PIPE
+        // software pipeline: this iteration's candidates were loaded by the previous one
+        // (or before the loop); the next iteration's loads go out before this one's filter
+#pragma unroll
+        for (int u = 0; u < U; ++u) k[u] = kn[u];
+        if (__ballot(t + U < len)) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) kn[u] = cand[t + U + (uint32_t)u < len ? jb + t + U + (uint32_t)u : 0u];
+        }
+#elif defined(GWAOI_EXP_8B)  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint2 h = reinterpret_cast<const uint2 *>(cand)[2 * (t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u)];
