@@ -519,6 +519,9 @@ def main():
     ap.add_argument("--cfg4-steps", type=int, default=5,
                     help="cfg3 runs: timed ticks of the config-4 strong-scaling sub-record (0 = off)")
     ap.add_argument("--cfg4-warmup", type=int, default=2)
+    ap.add_argument("--serial-issue", action="store_true",
+                    help="register tick t+1's move batch only after tick t's flush returned (default: registered "
+                         "while the flush of tick t runs, gwaoi_tick_begin/_end, as a game loop receives moves)")
     ap.add_argument("--cfg4-spaces", type=int, default=8192)
     args = ap.parse_args()
 
@@ -621,13 +624,25 @@ def main():
     lat = []
     events = 0
     moves = 0
-    t0 = time.perf_counter()
     every = max(1, args.time_every)
+    overlap = not args.serial_issue
+    if overlap:  # tick t's batch is registered before the timed loop, like the later ones during a flush
+        ps, px, pz = row_ptrs[args.warmup]
+        w.moved_batch_device(ps, px, pz, moves_per_tick[args.warmup])
+    t0 = time.perf_counter()
     for t in range(args.warmup, timed_end):
         a = time.perf_counter()
         if not args.no_timing:
             w.set_stage_timing([dom] if (t - args.warmup) % every == 0 else [])
-        ne, nl = step(t)
+        if overlap:
+            # flush t on the GPU; tick t+1's batch is registered (queued for the next flush) meanwhile
+            w.tick_begin()
+            if t + 1 < timed_end:
+                ps, px, pz = row_ptrs[t + 1]
+                w.moved_batch_device(ps, px, pz, moves_per_tick[t + 1])
+            ne, nl = w.tick_end_device()
+        else:
+            ne, nl = step(t)
         lat.append(time.perf_counter() - a)
         events += ne + nl
         moves += moves_per_tick[t]
@@ -697,6 +712,7 @@ def main():
         host_io = {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
                    "p50_tick_ms": float(np.percentile(pl_ms, 50)), "p99_tick_ms": float(np.percentile(pl_ms, 99)),
                    "steps": len(pb), "first_tick_ms": p_first * 1e3,
+                   "ticks_ms": [round(v, 3) for v in pl_ms.tolist()],
                    "serial": {"ms_per_step": s_el / hio * 1e3, "p50_tick_ms": float(np.percentile(sl_ms, 50)),
                               "p99_tick_ms": float(np.percentile(sl_ms, 99)), "steps": hio,
                               "events_per_s": h_evs / max(s_el, 1e-9)},
