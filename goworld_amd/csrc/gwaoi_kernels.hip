@@ -1488,6 +1488,9 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_UNIFORM_CTX
+#define GWAOI_UNIFORM_CTX 1
+#endif
 #ifndef GWAOI_SW_PIPE
 #define GWAOI_SW_PIPE 0  // 1: sweep loads of iteration t+1 issued before iteration t's filter
 #endif
@@ -1590,6 +1593,10 @@ __device__ __forceinline__ void drain_queue(const uint32_t *qb, const uint8_t *q
 // First frame entry of A's block, as a scalar (blocks are CT-aligned).
 __device__ __forceinline__ uint32_t block_start(const LaneA &A) {
     return __builtin_amdgcn_readfirstlane(A.a & ~(uint32_t)(CT - 1));
+}
+
+__device__ __forceinline__ float uniform_f32(float v) {
+    return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(v)));
 }
 
 __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
@@ -1950,7 +1957,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
 // spaces (small spaces) sweeps once per distinct space among a wave's lanes.
 #ifndef GWAOI_COMBINED_WPE
-#define GWAOI_COMBINED_WPE 6  // waves_per_eu: caps k_combined at 80 VGPRs (6 waves per SIMD; measured 0.141 vs 0.145 ms)
+#define GWAOI_COMBINED_WPE 8  // waves_per_eu: 62 VGPRs, 8 waves per SIMD with the context in SGPRs (0.120 vs 0.123 ms at 7 waves)
 #endif
 #if GWAOI_COMBINED_WPE
 #define COMBINED_ATTR __attribute__((amdgpu_waves_per_eu(GWAOI_COMBINED_WPE)))
@@ -2058,6 +2065,16 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.band_ok = C.lo > 0.f;
             C.in_max = C.g.D - C.M;
             C.out_min = C.g.D + C.M;
+#if GWAOI_UNIFORM_CTX
+            // wave-uniform by construction: keep them in SGPRs (they were VALU results in VGPRs)
+            C.M = uniform_f32(C.M);
+            C.thr = uniform_f32(C.thr);
+            C.lo = uniform_f32(C.lo);
+            C.hi = uniform_f32(C.hi);
+            C.lo_in = uniform_f32(C.lo_in);
+            C.in_max = uniform_f32(C.in_max);
+            C.out_min = uniform_f32(C.out_min);
+#endif
             C.proto.D = C.g.D;
             C.proto.HM = C.hi;
             C.proto.seq_base = seq_base;
