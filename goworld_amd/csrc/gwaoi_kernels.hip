@@ -1488,6 +1488,9 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_BAND_LEAN
+#define GWAOI_BAND_LEAN 1
+#endif
 #ifndef GWAOI_UNIFORM_CTX
 #define GWAOI_UNIFORM_CTX 1
 #endif
@@ -1660,13 +1663,28 @@ __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, 
         const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
         return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
     }
+#if GWAOI_BAND_LEAN
+    // Only the lower bounds that split the band between the Z and X' strips: a pair past the
+    // band's outer bound (dz or dx > hi = D + 2 d_rel D + M) has Chebyshev distance > D + M at t
+    // and at t-1 (both members near: each moved <= d_rel D per axis), so the unchanged-relation
+    // test below drops it anyway.
+    (void)hi;
+    const bool band = MODE == 0 ? (int)(dz >= lo) : (int)(dx >= lo) & (int)(fabsf(dz) <= C.lo_in);
+#else
     const bool band = MODE == 0 ? (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi)
                                 : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
+#endif
     const float dn = fmaxf(fabsf(dx), fabsf(dz));
     const float dxo = __uint_as_float(k.z) - A.xo, dzo = __uint_as_float(k.w) - A.zo;
     const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
+    // (dn <= in_max && dold <= in_max) || (dn > out_min && dold > out_min), as one max and one min
+    // (a band hit is near at t and t-1: finite positions, no NaN operand)
+#if GWAOI_SAME_4CMP
     const bool same =
         ((int)(dn <= C.in_max) & (int)(dold <= C.in_max)) | ((int)(dn > C.out_min) & (int)(dold > C.out_min));
+#else
+    const bool same = (int)(fmaxf(dn, dold) <= C.in_max) | (int)(fminf(dn, dold) > C.out_min);
+#endif
     return band & !same;
 }
 
