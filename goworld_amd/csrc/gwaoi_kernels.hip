@@ -1488,6 +1488,9 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_BALLOT_I1
+#define GWAOI_BALLOT_I1 1
+#endif
 #ifndef GWAOI_BAND_LEAN
 #define GWAOI_BAND_LEAN 1
 #endif
@@ -1615,12 +1618,24 @@ struct WaveQueue {
 // Append (a, b) for the lanes with keep set.  Wave-uniform.
 // a_off = A's offset in its block (the block's first frame entry is e0).
 __device__ __forceinline__ void qpush(uint32_t *qb, uint8_t *qa, WaveQueue &Q, bool keep, uint32_t a_off, uint32_t b) {
+#if GWAOI_BALLOT_I1
+    // the lane predicate stays an SGPR mask: the i1 ballot builtin, and the lane's rank by
+    // v_mbcnt on the mask's halves (an SGPR operand) instead of an AND with a VGPR lane mask
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(keep);
+    if (keep) {
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t i = Q.qn + r;
+        qb[i] = b;
+        qa[i] = (uint8_t)a_off;
+    }
+#else
     const unsigned long long m = __ballot(keep);
     if (keep) {
         const uint32_t i = Q.qn + (uint32_t)__popcll(m & lanemask_lt());
         qb[i] = b;
         qa[i] = (uint8_t)a_off;
     }
+#endif
     Q.qn += (uint32_t)__popcll(m);
 }
 
