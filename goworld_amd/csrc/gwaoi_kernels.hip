@@ -1488,6 +1488,9 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_PK_SUB
+#define GWAOI_PK_SUB 0  // 1: the filter's differences as packed f32 subtractions (measured neutral: 0.1124-0.1130 vs 0.1112-0.1121 ms)
+#endif
 #ifndef GWAOI_BALLOT_I1
 #define GWAOI_BALLOT_I1 1
 #endif
@@ -1670,10 +1673,18 @@ __device__ __forceinline__ bool band_xz(const LaneA &A, const CombinedCtx &C, co
     return ((int)(dn <= C.in_max) & (int)(dold <= C.in_max)) | ((int)(dn > C.out_min) & (int)(dold > C.out_min));
 }
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
 template <int MODE>
 __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint4 &k, uint32_t b) {
     const float lo = C.lo, hi = C.hi;
+#if GWAOI_PK_SUB
+    // the four differences as two packed (2 x f32) subtractions: IEEE per component, same bits
+    const f32x2_t dn2 = f32x2_t{__uint_as_float(k.x), __uint_as_float(k.y)} - f32x2_t{A.x, A.z};
+    const float dx = dn2.x, dz = dn2.y;
+#else
     const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
+#endif
     if (MODE == 2) {
         const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
         return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
@@ -1690,7 +1701,12 @@ __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, 
                                 : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
 #endif
     const float dn = fmaxf(fabsf(dx), fabsf(dz));
+#if GWAOI_PK_SUB
+    const f32x2_t do2 = f32x2_t{__uint_as_float(k.z), __uint_as_float(k.w)} - f32x2_t{A.xo, A.zo};
+    const float dxo = do2.x, dzo = do2.y;
+#else
     const float dxo = __uint_as_float(k.z) - A.xo, dzo = __uint_as_float(k.w) - A.zo;
+#endif
     const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
     // (dn <= in_max && dold <= in_max) || (dn > out_min && dold > out_min), as one max and one min
     // (a band hit is near at t and t-1: finite positions, no NaN operand)
