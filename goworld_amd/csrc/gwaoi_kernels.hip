@@ -1488,6 +1488,10 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
+#ifndef GWAOI_BUF_LOADS
+#define GWAOI_BUF_LOADS 0  // 1: sweep loads as raw buffer loads, no index select (measured slower, 0.120 vs 0.112 ms: lanes past their range then read distinct lines instead of one shared record)
+#endif
+typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
 #ifndef GWAOI_PK_SUB
 #define GWAOI_PK_SUB 0  // 1: the filter's differences as packed f32 subtractions (measured neutral: 0.1124-0.1130 vs 0.1112-0.1121 ms)
 #endif
@@ -1787,6 +1791,20 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
         for (int u = 0; u < U; ++u) {
             const uint2 h = reinterpret_cast<const uint2 *>(cand)[2 * (t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u)];
             k[u] = make_uint4(h.x, h.y, h.x, h.y);
+        }
+#elif GWAOI_BUF_LOADS
+        {
+            // raw buffer loads: one per-lane offset per iteration (the u-th record by the
+            // instruction's immediate offset), no per-candidate index select -- a record past the
+            // lane's range is ignored by the (t + u < len) mask, one past the frame reads as 0
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4 *>(cand), 0, (int)(F.n * 16u), 0x00020000);
+            const int vo = (int)((jb + t) * 16u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const cand_v4_t q = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 16 * u, 0);  // u by soffset
+                k[u] = make_uint4(q.x, q.y, q.z, q.w);
+            }
         }
 #else
 #pragma unroll
