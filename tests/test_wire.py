@@ -158,3 +158,23 @@ def test_gpu_gate_to_clients_matches_oracle_host_and_device():
             del connected[c]
         got, _ = w.gate_to_clients(pay)
         assert got == W.gate_to_clients(pay, connected)
+
+
+@pytest.mark.gpu
+def test_gpu_wire_error_paths():
+    import ctypes
+    from goworld_amd import GwaoiError, Wire
+    from goworld_amd._lib import WireGroups
+    with Wire(0) as w:
+        with pytest.raises(GwaoiError):
+            w.gate_from_clients(_rec(bytes(16)), 0)  # no dispatcher
+        with pytest.raises(GwaoiError):
+            w.set_clients([bytes(16)], [0xFFFFFFFE])  # reserved index
+        g = WireGroups()
+        L = w._L
+        assert L.gwaoi_wire_gate_to_clients_device(w._w, ctypes.c_void_p(8), 1, ctypes.byref(g)) == -1  # misaligned
+        assert L.gwaoi_wire_dispatcher_to_games(w._w, None, 3, ctypes.byref(g)) == -1  # records missing
+        # an empty table drops everything; removing an unknown id is a no-op
+        w.remove_entities([bytes(16)])
+        got, dropped = w.dispatcher_to_games(_rec(_id(1)) * 5)
+        assert got == {} and dropped == 5
