@@ -1492,6 +1492,9 @@ constexpr int CW = CT / WAVE;
 #define GWAOI_BUF_LOADS 0  // 1: sweep loads as raw buffer loads, no index select (measured slower, 0.120 vs 0.112 ms: lanes past their range then read distinct lines instead of one shared record)
 #endif
 typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
+#ifndef GWAOI_SW_U1
+#define GWAOI_SW_U1 0  // 1: rows where no lane has more than one candidate take one load per lane (measured neutral)
+#endif
 #ifndef GWAOI_PK_SUB
 #define GWAOI_PK_SUB 0  // 1: the filter's differences as packed f32 subtractions (measured neutral: 0.1124-0.1130 vs 0.1112-0.1121 ms)
 #endif
@@ -1859,8 +1862,15 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
         const uint32_t mx = 0;
         if (MODE != 2 && __ballot(len > 2))
             sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#if GWAOI_SW_U1
+        else if (__ballot(len > 1))
+            sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        else if (__ballot(len != 0))  // every lane has at most one candidate in this row (sparse X' rows)
+            sweep_range<MODE, 1>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#else
         else if (__ballot(len != 0))
             sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#endif
 #else
         const uint32_t mx = wave_max_u32(len);
         if (MODE != 2 && mx > 2)
