@@ -163,14 +163,38 @@ struct DecodeArgs {
     uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
 };
 
+#ifndef GWAOI_PROBE4
+#define GWAOI_PROBE4 1
+#endif
 __device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t hmask, uint4 id) {
     uint32_t h = id_hash(id.x, id.y, id.z, id.w) & hmask;
+#if GWAOI_PROBE4
+    // Four buckets per step, loaded together: a wave waits for its longest probe sequence,
+    // and with one dependent load per bucket that tail (not the mean of ~1.5) set the time.
+    for (uint32_t probe = 0; probe <= hmask; probe += 4) {
+        uint4 k[4];
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t hq = (h + (uint32_t)q) & hmask;
+            k[q] = htab[2 * (size_t)hq];
+            v[q] = htab[2 * (size_t)hq + 1].x;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (v[q] == H_EMPTY) return SLOT_NONE;
+            if (v[q] != H_TOMB && eq4(k[q], id)) return v[q];
+        }
+        h = (h + 4u) & hmask;
+    }
+#else
     for (uint32_t probe = 0; probe <= hmask; ++probe, h = (h + 1) & hmask) {
         const uint4 k = htab[2 * (size_t)h];  // key and value: one 32-B bucket
         const uint32_t v = htab[2 * (size_t)h + 1].x;
         if (v == H_EMPTY) return SLOT_NONE;
         if (v != H_TOMB && eq4(k, id)) return v;
     }
+#endif
     return SLOT_NONE;
 }
 
