@@ -534,6 +534,13 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
 #ifndef GWAOI_FW_G
 #define GWAOI_FW_G 4
 #endif
+#ifndef GWAOI_FW_EXP
+#define GWAOI_FW_EXP 0  // A/B decomposition only (1: no sender gathers, 2: no hit or gathers, 3: no stores, 4: neither,
+                        // 5: 4 without the receiver search, with GWAOI_FW_SCAN=0)
+#endif
+#ifndef GWAOI_FW_SCAN
+#define GWAOI_FW_SCAN 1
+#endif
 constexpr int FW_G = GWAOI_FW_G;  // record groups of 64 per wave with their loads in flight together
 
 __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
@@ -571,21 +578,23 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
     for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) seg[q] = bin[q] ? s_pre[bin[q] - 1] : 0u;
     __syncthreads();
     const uint4 *srec = A.srec;
-    // record r -> (receiver perm position, its scratch entry, output position)
-    auto locate = [&](uint32_t r, uint32_t &q, uint32_t &sidx, uint32_t &pos) {
-        uint32_t lo = 0, hi = ST - 1;  // first receiver q with s_pre[q] > r
+    // record r of receiver q -> (its scratch entry, output position)
+    auto place = [&](uint32_t r, uint32_t q, uint32_t &sidx, uint32_t &pos) {
+        const uint32_t gq = s_gate[q];
+        sidx = s_sb[q] + r - (q ? s_pre[q - 1] : 0u);
+        pos = gbase[gq] + (r - seg[gq]);
+    };
+    auto search = [&](uint32_t r) {  // first receiver q with s_pre[q] > r
+        uint32_t lo = 0, hi = ST - 1;
         while (lo < hi) {
             const uint32_t m = (lo + hi) >> 1;
             if (s_pre[m] > r) hi = m;
             else lo = m + 1;
         }
-        q = lo;
-        const uint32_t gq = s_gate[q];
-        sidx = s_sb[q] + r - (q ? s_pre[q - 1] : 0u);
-        pos = gbase[gq] + (r - seg[gq]);
+        return lo;
     };
     // stage a wave's 64 records in LDS, then store them as 3 x 64 consecutive 16-B words
-    auto emit = [&](uint32_t rw, bool ok, uint32_t q, uint32_t pos, const uint4 &id, const uint4 &pv) {
+    auto emit = [&](uint32_t nrec, bool ok, uint32_t q, uint32_t pos, const uint4 &id, const uint4 &pv) {
         if (ok) {
             s_pos[w][ln] = pos;
             s_rec[w][3 * ln] = s_cli[q];
@@ -594,15 +603,42 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        const uint32_t nrec = min(64u, R - rw);
 #pragma unroll
         for (uint32_t j = 0; j < 3; ++j) {
             const uint32_t e = ln + 64u * j, rr = e / 3u;
-            if (rr < nrec) st_stream(A.out + 3 * (size_t)s_pos[w][rr] + (e - 3u * rr), s_rec[w][e]);
+#if GWAOI_FW_EXP == 3 || GWAOI_FW_EXP == 4 || GWAOI_FW_EXP == 5
+            if (rr < nrec && s_rec[w][e].x == 0xFFFFFFF1u && s_rec[w][e].y == 0x5u)  // timing experiment only: no stores
+#else
+            if (rr < nrec)
+#endif
+                st_stream(A.out + 3 * (size_t)s_pos[w][rr] + (e - 3u * rr), s_rec[w][e]);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     };
+#if GWAOI_FW_SCAN
+    // wave w: one contiguous chunk [c0, c1) of the block's records, FW_G consecutive groups of 64
+    // per step with all groups' loads in flight.  A lane's records are then exactly 64 apart
+    // (under one receiver on average), so its receiver is found by a forward scan from the last
+    // one instead of a binary search over the block per record.
+    const uint32_t per = (R + ST - 1u) / ST * 64u;  // ST / 64 waves
+    const uint32_t c0 = min(R, w * per), c1 = min(R, c0 + per);
+    uint32_t qc = c0 + ln < c1 ? search(c0 + ln) : 0u;
+    for (uint32_t rw = c0; rw < c1; rw += FW_G * 64) {
+        uint32_t q[FW_G], pos[FW_G], h[FW_G];
+        bool ok[FW_G];
+#pragma unroll
+        for (int k = 0; k < FW_G; ++k) {
+            const uint32_t r = rw + (uint32_t)k * 64u + ln;
+            ok[k] = r < c1;
+            uint32_t sidx = 0;
+            q[k] = pos[k] = 0;
+            if (ok[k]) {
+                while (s_pre[qc] <= r) ++qc;  // ends: s_pre[ST - 1] = R > r
+                q[k] = qc;
+                place(r, qc, sidx, pos[k]);
+            }
+#else
     // wave w: records [rw + k*ST, rw + k*ST + 64) for k < FW_G per step, all groups' loads in flight
     for (uint32_t rw = w * 64; rw < R; rw += FW_G * ST) {
         uint32_t q[FW_G], pos[FW_G], h[FW_G];
@@ -613,21 +649,51 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
             ok[k] = r < R;
             uint32_t sidx = 0;
             q[k] = pos[k] = 0;
-            if (ok[k]) locate(r, q[k], sidx, pos[k]);
+#if GWAOI_FW_EXP == 5
+            if (ok[k]) {  // timing experiment only: no receiver search
+                q[k] = ln;
+                sidx = r;
+                pos[k] = r;
+            }
+#else
+            if (ok[k]) {
+                q[k] = search(r);
+                place(r, q[k], sidx, pos[k]);
+            }
+#endif
+#endif
+#if GWAOI_FW_EXP == 2 || GWAOI_FW_EXP == 4 || GWAOI_FW_EXP == 5
+            h[k] = sidx;  // timing experiment only: no hit loads
+#else
             h[k] = ok[k] ? A.scr[sidx] : 0u;
+#endif
         }
         uint4 id[FW_G], pv[FW_G];
 #pragma unroll
         for (int k = 0; k < FW_G; ++k) {
             id[k] = pv[k] = make_uint4(0, 0, 0, 0);
             if (ok[k]) {
+#if GWAOI_FW_EXP == 1 || GWAOI_FW_EXP == 2 || GWAOI_FW_EXP == 4 || GWAOI_FW_EXP == 5
+                id[k] = pv[k] = make_uint4(h[k], h[k], h[k], h[k]);  // timing experiment only: no sender gathers
+#else
                 id[k] = srec[2 * (size_t)h[k]];
                 pv[k] = srec[2 * (size_t)h[k] + 1];
+#endif
             }
         }
+#if GWAOI_FW_SCAN
 #pragma unroll
-        for (int k = 0; k < FW_G; ++k)
-            if (rw + (uint32_t)k * ST < R) emit(rw + (uint32_t)k * ST, ok[k], q[k], pos[k], id[k], pv[k]);
+        for (int k = 0; k < FW_G; ++k) {
+            const uint32_t rk = rw + (uint32_t)k * 64u;
+            if (rk < c1) emit(min(64u, c1 - rk), ok[k], q[k], pos[k], id[k], pv[k]);
+        }
+#else
+#pragma unroll
+        for (int k = 0; k < FW_G; ++k) {
+            const uint32_t rk = rw + (uint32_t)k * ST;
+            if (rk < R) emit(min(64u, R - rk), ok[k], q[k], pos[k], id[k], pv[k]);
+        }
+#endif
     }
 }
 
