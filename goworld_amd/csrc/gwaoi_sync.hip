@@ -420,7 +420,27 @@ __device__ __forceinline__ FanWin fan_window(const FrameView &F, uint32_t i) {
 // loads only) and placed by one atomic per block, so the window is walked
 // once.  A block past the scratch capacity writes no hits (the host regrows
 // the scratch and reruns this pass; it has no other side effect).
-constexpr int FAN_U = 4;  // window candidates loaded together per lane
+#ifndef GWAOI_FAN_U
+#define GWAOI_FAN_U 6  // A/B: 6 -0.03 ms collect vs 4; 8 and 2 no better (profiles/r02_variants_fan_hits.log)
+#endif
+#ifndef GWAOI_FH_EXP
+#define GWAOI_FH_EXP 0  // A/B only (1: no hit stores, timing only; 2: nontemporal hit stores)
+#endif
+constexpr int FAN_U = GWAOI_FAN_U;  // window candidates loaded together per lane
+__device__ __forceinline__ void st_hits(uint4 *p, const uint4 &v) {
+#if GWAOI_FH_EXP == 1
+    if (v.x == 0xFFFFFFF7u && v.y == 0xFFFFFFF7u) st_stream(p, v);
+#elif GWAOI_FH_EXP == 2
+    u32x4_t t;
+    t.x = v.x;
+    t.y = v.y;
+    t.z = v.z;
+    t.w = v.w;
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x4_t *>(p));
+#else
+    st_stream(p, v);
+#endif
+}
 
 __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
     extern __shared__ uint32_t gcnt[];  // [G] records per gate of the block
@@ -506,13 +526,13 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
                             default: buf.w = b; break;
                         }
                         ++c;
-                        if (!(c & 3u) && fits) st_stream(run + (c >> 2) - 1u, buf);
+                        if (!(c & 3u) && fits) st_hits(run + (c >> 2) - 1u, buf);
                     }
                 }
             }
         }
     }
-    if ((c & 3u) && fits) st_stream(run + (c >> 2), buf);
+    if ((c & 3u) && fits) st_hits(run + (c >> 2), buf);
     if (i < ne) {
         A.fcnt[i] = c;
         A.fsb[i] = sb;
