@@ -570,8 +570,9 @@ def main():
     for t in range(ticks):
         sl, nx, nz = wl.tick(t)
         batches.append((sl, nx, nz))
-    # PCIe-inclusive leg (host memory): one untimed warmup tick (allocates the pinned staging) + hio timed
-    host_batches = [wl.tick(ticks + t) for t in range(2 * hio + 2 if hio else 0)]
+    # PCIe-inclusive leg (host memory): three untimed warmup ticks (one serial, two pipelined: they
+    # allocate both pinned staging buffers) + hio serial + hio + 1 pipelined
+    host_batches = [wl.tick(ticks + t) for t in range(2 * hio + 4 if hio else 0)]
     sync_steps = max(0, args.sync_steps) if ws == 1 or args.workload != "cfg4" else 0
     sync_batches = [wl.tick(ticks + len(host_batches) + t) for t in range(sync_steps + 1 if sync_steps else 0)]
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
@@ -672,6 +673,12 @@ def main():
     if hio:
         w.moved_batch(*host_batches[0])  # warmup: sizes the pinned staging and host event buffers
         w.tick(copy=False)
+        w.moved_batch(*host_batches[1])  # pipelined warmup: the second staging buffer
+        w.tick_begin()
+        w.moved_batch(*host_batches[2])
+        w.tick_end(copy=False)
+        w.tick_begin()
+        w.tick_end(copy=False)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -679,14 +686,14 @@ def main():
         import gc
         gc.disable()  # no collector pauses inside the timed ticks
         h0 = time.perf_counter()
-        for sl, nx, nz in host_batches[1:hio + 1]:
+        for sl, nx, nz in host_batches[3:hio + 3]:
             a = time.perf_counter()
             w.moved_batch(sl, nx, nz)
             ent, lev = w.tick(copy=False)
             s_lat.append(time.perf_counter() - a)
             h_ev += len(ent) + len(lev)
         s_el = time.perf_counter() - h0
-        pb = host_batches[hio + 1:]
+        pb = host_batches[hio + 3:]
         p_lat = []
         w.moved_batch(*pb[0])
         p0 = issue = time.perf_counter()
