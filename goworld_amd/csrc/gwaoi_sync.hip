@@ -161,7 +161,11 @@ struct DecodeArgs {
     unsigned long long *cl;
     float4 *pos;
     uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
+    uint32_t *dups, *ndup;      // slots with a record whose claim store did not survive (GWAOI_DECODE_FUSE)
 };
+#ifndef GWAOI_DECODE_FUSE
+#define GWAOI_DECODE_FUSE 1
+#endif
 
 #ifndef GWAOI_PROBE4
 #define GWAOI_PROBE4 1
@@ -206,6 +210,9 @@ __device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint3
 // (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
 __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+#if GWAOI_DECODE_FUSE
+    if (i == 0) *A.ndup = 0u;  // read by k_decode_apply, the next launch on the stream
+#endif
     if (i >= A.n) return;
     const uint4 id = A.pay[2 * (size_t)i];
     const uint4 pv = A.pay[2 * (size_t)i + 1];
@@ -240,6 +247,7 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     }
 }
 
+#if !GWAOI_DECODE_FUSE
 // Records whose claim store did not survive (another record of the same slot
 // in this batch) fold it in with atomicMax: only repeated slots pay an atomic.
 __global__ __launch_bounds__(ST) void k_decode_fix(DecodeArgs A) {
@@ -269,6 +277,63 @@ __global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
     }
     if (cs.y == c) p[3] = __uint_as_float(pv.w);
 }
+#endif
+
+#if GWAOI_DECODE_FUSE
+// The claim fold and the apply in one pass.  A record whose claim store survived
+// (cs == c) applies its position / yaw; one whose store was overwritten by another
+// record of the same slot folds its claim in with atomicMax and lists the slot.
+// Whatever the interleaving, every slot with two or more records in the batch is
+// listed by one of them, and k_decode_dups then applies the record that holds the
+// final (largest) claim.  A batch without repeated slots pays no atomic and
+// lists nothing: the separate read-only fold pass (k_decode_fix) is gone.
+__global__ __launch_bounds__(ST) void k_decode_apply(DecodeArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint32_t s = A.o_ys[i];
+    if (s == SLOT_NONE) return;
+    const unsigned long long c = A.claim0 + i;
+    const uint4 pv = A.pay[2 * (size_t)i + 1];
+    float *p = reinterpret_cast<float *>(A.pos + s);
+    const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
+    bool lost = false;
+    if (A.o_sp[i] != SP_DEAD) {
+        if (cs.x == c) {
+            p[0] = __uint_as_float(pv.x);
+            p[1] = __uint_as_float(pv.y);
+            p[2] = __uint_as_float(pv.z);
+        } else {
+            atomicMax(&A.cl[2 * (size_t)s], c);
+            lost = true;
+        }
+    }
+    if (cs.y == c) {
+        p[3] = __uint_as_float(pv.w);
+    } else {
+        atomicMax(&A.cl[2 * (size_t)s + 1], c);
+        lost = true;
+    }
+    if (lost) A.dups[atomicAdd(A.ndup, 1u)] = s;
+}
+
+// Listed slots (rare; may repeat): apply the records holding the final claims.
+__global__ __launch_bounds__(ST) void k_decode_dups(DecodeArgs A) {
+    const uint32_t nd = *A.ndup;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
+        const uint32_t s = A.dups[k];
+        const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
+        float *p = reinterpret_cast<float *>(A.pos + s);
+        const unsigned long long ix = cs.x - A.claim0, iy = cs.y - A.claim0;  // claims of older batches wrap
+        if (ix < A.n && A.o_ys[ix] == s && A.o_sp[ix] != SP_DEAD) {
+            const uint4 pv = A.pay[2 * (size_t)ix + 1];
+            p[0] = __uint_as_float(pv.x);
+            p[1] = __uint_as_float(pv.y);
+            p[2] = __uint_as_float(pv.z);
+        }
+        if (iy < A.n && A.o_ys[iy] == s) p[3] = __uint_as_float(A.pay[2 * (size_t)iy + 1].w);
+    }
+}
+#endif
 
 // ------------------------------------------------------------ fan-out ------
 // Receiver side: CollectEntitySyncInfos sends entity A's record to the client
@@ -1304,7 +1369,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
         S->arena_tick = ticks_now;
     }
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t need = 5 * al(n * 4) + (on_device ? 0 : al(n * 32));
+    const size_t need = 6 * al(n * 4) + al(4) + (on_device ? 0 : al(n * 32));
     SyncState::Chunk *ch = nullptr;
     for (auto &c : S->arena)
         if (c.cap - c.used >= need) {
@@ -1328,7 +1393,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     if (on_device) {
         pay = reinterpret_cast<const uint4 *>(payload);
     } else {
-        char *dp = base + 5 * al(n * 4);
+        char *dp = base + 6 * al(n * 4) + al(4);
         SY_TRY(hipMemcpyAsync(dp, payload, n * 32, hipMemcpyHostToDevice, S->st));
         pay = reinterpret_cast<const uint4 *>(dp);
     }
@@ -1349,11 +1414,18 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.pos = S->pos;
     A.oflag = S->oflag;
     A.oflag_n = S->oflag_n;
+    A.dups = reinterpret_cast<uint32_t *>(base + 5 * al(n * 4));
+    A.ndup = reinterpret_cast<uint32_t *>(base + 6 * al(n * 4));
     S->claim_next += n;
     S->decoded = true;
     k_decode<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+#if GWAOI_DECODE_FUSE
+    k_decode_apply<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+    k_decode_dups<<<std::min<uint32_t>(cdivu(n, ST), 64u), ST, 0, S->st>>>(A);
+#else
     k_decode_fix<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_yaw<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+#endif
     SY_TRY(hipGetLastError());
     return world_queue_decoded(w, o_slot, o_x, o_z, o_sp, n);
 }
