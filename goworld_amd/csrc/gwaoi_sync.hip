@@ -1206,7 +1206,10 @@ int ensure_host(SyncState *S, uint8_t **p, size_t *cap, size_t bytes) {
 
 // Multisplit bases: blk_cnt [parts][nb] -> exclusive scan (parts*nb + 1
 // entries, the last is the total) -> h_off_raw[0..parts].
-int part_bases(SyncState *S, uint32_t parts, uint32_t nb) {
+#ifndef GWAOI_COLLECT_ONESYNC
+#define GWAOI_COLLECT_ONESYNC 1
+#endif
+int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true) {
     const size_t n = (size_t)parts * nb + 1;
     if (int rc = ensure_u32(S, &S->scan_tmp, &S->scan_cap, scan_tmp_elems(n) + 4)) return rc;
     if (parts + 1 > S->off_cap) {
@@ -1219,7 +1222,7 @@ int part_bases(SyncState *S, uint32_t parts, uint32_t nb) {
     SY_TRY(hipGetLastError());
     S->h_off_raw.resize(parts + 1);
     SY_TRY(hipMemcpyAsync(S->h_off_raw.data(), S->d_off, (parts + 1) * 8, hipMemcpyDeviceToHost, S->st));
-    SY_TRY(hipStreamSynchronize(S->st));
+    if (sync) SY_TRY(hipStreamSynchronize(S->st));
     return GWAOI_OK;
 }
 
@@ -1313,6 +1316,11 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
             k_fan_hits<<<nb, ST, (size_t)G * 4, S->st>>>(A);
             SY_TRY(hipGetLastError());
+            // the per-gate bases are scanned before the capacity check: one host round trip
+            // for both (a rerun rewrites every count the scan read)
+#if GWAOI_COLLECT_ONESYNC
+            if (int rc = part_bases(S, G, nb, false)) return rc;
+#endif
             unsigned long long used = 0;
             SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
             SY_TRY(hipStreamSynchronize(S->st));
@@ -1323,7 +1331,9 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             }
             if ((rc_scr = ensure_u32(S, &S->scr, &S->scr_cap, (size_t)used))) return rc_scr;
         }
+#if !GWAOI_COLLECT_ONESYNC
         if (int rc = part_bases(S, G, nb)) return rc;
+#endif
         total = S->h_off_raw[G];
     }
     if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;

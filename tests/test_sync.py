@@ -208,6 +208,14 @@ def test_sync_device_packets_match_oracle():
 
 
 @pytest.mark.gpu
+def test_sync_dense_crowd_regrows_fanout_scratch():
+    """Every entity inside everyone's window (a 60 x 60 square, D = 100 / 60):
+    ~250 records per receiver, past the fan-out scratch's first size (32 words
+    per entry), so the first collect regrows it and reruns the hits pass."""
+    check_run(SS.make(seed=13, n=600, n_outside=20, flushes=2, L=60.0))
+
+
+@pytest.mark.gpu
 def test_sync_errors():
     from goworld_amd import GwaoiError, World
     with World(16, device=0) as w:
