@@ -371,6 +371,10 @@ struct FanArgs {
 __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nf = A.F.n;
+    if (i == 0) {  // the hits pass's scratch cursor and the scan's extra count (first attempt)
+        *A.scr_cursor = 0ull;
+        A.blk_cnt[(size_t)A.G * A.nb] = 0u;
+    }
     if (i >= nf + A.n_left) return;
     const bool in_frame = i < nf;
     const uint32_t s = in_frame ? ld_ss(A.F.ss, i).slot : A.left[i - nf];
@@ -1302,6 +1306,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     A.rslot = S->f_slot;
     A.srec = S->f_rec;
     A.frec = S->f_frec;
+    A.scr_cursor = S->scr_cursor;
     if (n_ent) k_fan_prep<<<cdivu(n_ent, ST), ST, 0, S->st>>>(A);  // also clears the flags
     uint64_t total = 0;
     S->h_off_raw.assign(1, 0);
@@ -1311,9 +1316,10 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             if (S->scr_cap == 0 && (rc_scr = ensure_u32(S, &S->scr, &S->scr_cap, 32 * (size_t)n_ent))) return rc_scr;
             A.scr = S->scr;
             A.scr_cap = std::min<unsigned long long>(S->scr_cap, SCR_FULL - 1ull);
-            A.scr_cursor = S->scr_cursor;
-            SY_TRY(hipMemsetAsync(S->scr_cursor, 0, 8, S->st));
-            SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
+            if (attempt) {  // (k_fan_prep zeroed them for the first)
+                SY_TRY(hipMemsetAsync(S->scr_cursor, 0, 8, S->st));
+                SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
+            }
             k_fan_hits<<<nb, ST, (size_t)G * 4, S->st>>>(A);
             SY_TRY(hipGetLastError());
             // the per-gate bases are scanned before the capacity check: one host round trip
