@@ -168,11 +168,33 @@ struct DecodeArgs {
 #endif
 
 #ifndef GWAOI_PROBE4
-#define GWAOI_PROBE4 1
+#define GWAOI_PROBE4 2
 #endif
 __device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t hmask, uint4 id) {
     uint32_t h = id_hash(id.x, id.y, id.z, id.w) & hmask;
-#if GWAOI_PROBE4
+#if GWAOI_PROBE4 == 2
+    // One 128-B line (four 32-B buckets, the table is 256-B aligned) per step, the line that
+    // holds h: a match anywhere in it is the key (ids are unique in the table), while an
+    // empty bucket ends the probe sequence only at or after h.
+    uint32_t first = h & 3u;
+    h &= ~3u;
+    for (uint32_t probe = 0; probe <= hmask; probe += 4) {
+        uint4 k[4];
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            k[q] = htab[2 * (size_t)(h + (uint32_t)q)];
+            v[q] = htab[2 * (size_t)(h + (uint32_t)q) + 1].x;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (v[q] != H_EMPTY && v[q] != H_TOMB && eq4(k[q], id)) return v[q];
+            if ((uint32_t)q >= first && v[q] == H_EMPTY) return SLOT_NONE;
+        }
+        first = 0;
+        h = (h + 4u) & hmask;
+    }
+#elif GWAOI_PROBE4
     // Four buckets per step, loaded together: a wave waits for its longest probe sequence,
     // and with one dependent load per bucket that tail (not the mean of ~1.5) set the time.
     for (uint32_t probe = 0; probe <= hmask; probe += 4) {
