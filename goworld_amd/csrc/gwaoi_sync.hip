@@ -239,10 +239,11 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     const uint4 id = A.pay[2 * (size_t)i];
     const uint4 pv = A.pay[2 * (size_t)i + 1];
     uint32_t s = lookup(A.htab, A.hmask, id);
-    uint32_t sp = SP_DEAD;
+    uint32_t sp = SP_DEAD, old = 0;
     if (s != SLOT_NONE) {
         const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[s];
         sp = st.y;  // SST_SPACE
+        old = st.w;  // SST_FLAGS
         if (!st.z) s = SLOT_NONE;  // SST_SYNCING
     }
     const bool move = s != SLOT_NONE && sp != SP_DEAD;
@@ -260,9 +261,8 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
         const unsigned long long c = A.claim0 + i;
         if (move) reinterpret_cast<ulonglong2 *>(A.cl)[s] = make_ulonglong2(c, c);
         else A.cl[2 * (size_t)s + 1] = c;
-        uint32_t *f = &A.sst[4 * (size_t)s + SST_FLAGS];
-        const uint32_t old = *f;  // records of one slot all set the same bit
-        if (!(old & GWAOI_SIF_NEIGHBOR_CLIENTS)) *f = old | GWAOI_SIF_NEIGHBOR_CLIENTS;
+        // (the flags word came with the slot's record; records of one slot all set the same bit)
+        if (!(old & GWAOI_SIF_NEIGHBOR_CLIENTS)) A.sst[4 * (size_t)s + SST_FLAGS] = old | GWAOI_SIF_NEIGHBOR_CLIENTS;
         // first flag of a slot outside the frame since the last collect: listed (a
         // slot with several records may be listed twice; k_fan_prep sends it once)
         if (!move && old == 0u) A.oflag[atomicAdd(A.oflag_n, 1u)] = s;
