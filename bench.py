@@ -52,6 +52,49 @@ def dist_env():
     return ws, rank, local
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus: int, env) -> list | None:
+    """How `bench.py --gpus N` runs.  None: this process is the whole job (N=1, or
+    a rank started by torch.distributed.run with WORLD_SIZE == N).  A list: the
+    environments of the N rank processes to spawn (WORLD_SIZE unset, N > 1), one
+    per GPU, rendezvous on 127.0.0.1.  Raises ValueError when an outside
+    launcher's WORLD_SIZE disagrees with --gpus."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: need at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise ValueError(f"--gpus {gpus} but WORLD_SIZE={ws} (the launcher started {ws} ranks)")
+        return None
+    if gpus == 1:
+        return None
+    port = str(_free_port())
+    plan = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        plan.append(e)
+    return plan
+
+
+def spawn_ranks(plan) -> int:
+    """Run the rank processes of `plan` (children of this process, which has not
+    touched the GPU) and return the job's exit code: the first failing rank's,
+    else 0.  Rank 0 prints the JSON line."""
+    import subprocess
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e) for e in plan]
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
 def combined_pass_bytes(n: int, total_cells: int, events: float) -> float:
     """Algorithmic HBM bytes of one k_combined launch (Roofline):
     every frame entry once as the tile's own entity -- new record (x, z, seq:
@@ -385,11 +428,12 @@ def run_strips(args, ws, rank, local, dist):
     timing (DeviceUniformWorkload); value = all N moves per tick / max time."""
     import torch
     from goworld_amd.shard import reduce_over_ranks
-    from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local, local_slice
+    from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local, local_slice, setup_count_group
     from goworld_amd.workload import DeviceUniformWorkload
 
     dev = torch.device(f"cuda:{local}")
     if dist is not None:
+        setup_count_group(dist)  # collective over every rank: the host count all-gather's gloo group
         dist.barrier()  # RCCL's communicator exists before the first batched send/recv
     n = args.n or (1 << 24)
     t_setup = time.perf_counter()
@@ -525,11 +569,24 @@ def main():
     ap.add_argument("--cfg4-spaces", type=int, default=8192)
     args = ap.parse_args()
 
+    # --gpus N without an outside launcher: spawn the N ranks here, before anything touches the GPU
+    try:
+        plan = launch_plan(args.gpus, os.environ)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(2)
+    if plan is not None:
+        sys.exit(spawn_ranks(plan))
     ws, rank, local = dist_env()
     dist = None
     if ws > 1:
         import torch
         import torch.distributed as dist
+        if args.dist_backend == "nccl" and torch.cuda.device_count() < ws:
+            print(f"bench.py: {ws} ranks over RCCL need {ws} GPUs, {torch.cuda.device_count()} visible "
+                  "(RCCL allows one rank per device; --dist-backend gloo rehearses several ranks on one GPU)",
+                  file=sys.stderr)
+            sys.exit(2)
         if args.dist_backend == "gloo":  # rehearsal: several ranks may share a GPU
             local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)

@@ -577,6 +577,8 @@ class Wire:
 
     def set_entity_games(self, ids, games):
         a, g = self._ids(ids), np.ascontiguousarray(games, np.uint16)
+        if a.size // 16 != g.size:
+            raise ValueError(f"{a.size // 16} ids but {g.size} games")
         self._check(self._L.gwaoi_wire_set_entity_games(self._w, _p(a), _p(g), g.size))
 
     def remove_entities(self, ids):
@@ -585,6 +587,8 @@ class Wire:
 
     def set_clients(self, ids, index):
         a, x = self._ids(ids), np.ascontiguousarray(index, np.uint32)
+        if a.size // 16 != x.size:
+            raise ValueError(f"{a.size // 16} ids but {x.size} client indices")
         self._check(self._L.gwaoi_wire_set_clients(self._w, _p(a), _p(x), x.size))
 
     def remove_clients(self, ids):

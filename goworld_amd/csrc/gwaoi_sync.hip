@@ -161,6 +161,7 @@ struct DecodeArgs {
     unsigned long long *cl;
     float4 *pos;
     uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
+    uint32_t oflag_cap;         // entries oflag holds (max_slots: one per slot, see k_decode)
     uint32_t *dups, *ndup;      // slots with a record whose claim store did not survive (GWAOI_DECODE_FUSE)
 };
 #ifndef GWAOI_DECODE_FUSE
@@ -262,10 +263,19 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
         if (move) reinterpret_cast<ulonglong2 *>(A.cl)[s] = make_ulonglong2(c, c);
         else A.cl[2 * (size_t)s + 1] = c;
         // (the flags word came with the slot's record; records of one slot all set the same bit)
-        if (!(old & GWAOI_SIF_NEIGHBOR_CLIENTS)) A.sst[4 * (size_t)s + SST_FLAGS] = old | GWAOI_SIF_NEIGHBOR_CLIENTS;
-        // first flag of a slot outside the frame since the last collect: listed (a
-        // slot with several records may be listed twice; k_fan_prep sends it once)
-        if (!move && old == 0u) A.oflag[atomicAdd(A.oflag_n, 1u)] = s;
+        uint32_t *fl = A.sst + 4 * (size_t)s + SST_FLAGS;
+        if (!move && old == 0u) {
+            // first flag of a slot outside the frame since the last collect: the flag is
+            // claimed atomically, so a slot with several records in the batch is listed
+            // once and the list never holds more than one entry per slot (rare path: only
+            // entities outside every AOI space get here)
+            if (atomicOr(fl, GWAOI_SIF_NEIGHBOR_CLIENTS) == 0u) {
+                const uint32_t k = atomicAdd(A.oflag_n, 1u);
+                if (k < A.oflag_cap) A.oflag[k] = s;
+            }
+        } else if (!(old & GWAOI_SIF_NEIGHBOR_CLIENTS)) {
+            *fl = old | GWAOI_SIF_NEIGHBOR_CLIENTS;
+        }
     }
 }
 
@@ -882,6 +892,7 @@ struct SyncState {
     float4 *pos = nullptr;
     unsigned long long *cl = nullptr;  // 2 per slot: Position / yaw last-writer claims
     uint32_t *oflag = nullptr, *oflag_n = nullptr;  // decode: slots flagged outside every AOI space
+    uint32_t oflag_cap = 0;                           // entries of oflag (max_slots)
     bool decoded = false;                           // a decode ran since the last collect
     // id -> slot hash table (device, host mirror)
     uint4 *htab = nullptr;  // 2 per bucket: key, (slot, -, -, -)
@@ -1072,6 +1083,7 @@ int create(gwaoi_world *w, SyncState **out) {
     while (cap < 2ull * v.max_slots) cap <<= 1;
     S->hcap = cap;
     const size_t N = v.max_slots;
+    S->oflag_cap = (uint32_t)N;
     int rc;
     if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->sst, 4 * N)) ||
         (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->cl, 2 * N)) || (rc = salloc(S, &S->oflag, N)) ||
@@ -1279,6 +1291,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
         SY_TRY(hipMemcpyAsync(&n_dec, S->oflag_n, 4, hipMemcpyDeviceToHost, S->st));
         SY_TRY(hipStreamSynchronize(S->st));
         S->decoded = false;
+        n_dec = std::min(n_dec, S->oflag_cap);  // k_decode lists a slot at most once (atomicOr claim)
     }
     const size_t n_left = left.size() + n_dec;
     if (n_left) {
@@ -1452,6 +1465,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.pos = S->pos;
     A.oflag = S->oflag;
     A.oflag_n = S->oflag_n;
+    A.oflag_cap = S->oflag_cap;
     A.dups = reinterpret_cast<uint32_t *>(base + 5 * al(n * 4));
     A.ndup = reinterpret_cast<uint32_t *>(base + 6 * al(n * 4));
     S->claim_next += n;

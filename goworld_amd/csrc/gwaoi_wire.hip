@@ -255,6 +255,9 @@ int table_grow(gwaoi_wire *w, IdTable &t) {
 int table_set(gwaoi_wire *w, IdTable &t, const uint8_t *ids, const uint32_t *vals, size_t n, bool remove) {
     if (n && !ids) return GWAOI_EINVAL;
     if (!remove && n && !vals) return GWAOI_EINVAL;
+    if (!remove)  // validate the whole batch before touching the table: a rejected call changes nothing
+        for (size_t i = 0; i < n; ++i)
+            if (vals[i] >= H_TOMB) return GWAOI_EINVAL;
     for (size_t i = 0; i < n; ++i) {
         uint4 id;
         std::memcpy(&id, ids + 16 * i, 16);
@@ -266,7 +269,6 @@ int table_set(gwaoi_wire *w, IdTable &t, const uint8_t *ids, const uint32_t *val
             t.dirty.push_back(at);
             continue;
         }
-        if (vals[i] >= H_TOMB) return GWAOI_EINVAL;
         if (at != H_EMPTY) {
             t.val[at] = vals[i];
             t.dirty.push_back(at);

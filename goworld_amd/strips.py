@@ -193,18 +193,35 @@ def local_slice(send, counts, rank):
 _COUNT_GROUPS = {}
 
 
-def count_group(dist, group=None):
-    """The process group that carries the per-destination counts: gloo, on
-    host tensors.  route() has the counts on the host already (its scatter is
-    sized by them), so exchanging them over gloo costs no device sync; with a
-    gloo job it is the job's own group.  Created once per job (collective:
-    every rank calls exchange the same way)."""
+def _group_key(dist, group):
+    return tuple(range(dist.get_world_size())) if group is None else tuple(dist.get_process_group_ranks(group))
+
+
+def setup_count_group(dist, group=None):
+    """Create the process group that carries the per-destination counts: gloo,
+    on host tensors.  route() has the counts on the host already (its scatter
+    is sized by them), so exchanging them over gloo costs no device sync; with
+    a gloo job it is the job's own group.  ``new_group`` is collective over the
+    whole default group, so EVERY rank of the job calls this once at setup
+    (tile_tick's callers, bench.py's strip run), before the first exchange --
+    not lazily inside exchange, where ranks outside ``group`` would never join.
+    Cached on the group's rank tuple."""
     if dist.get_backend(group) == "gloo":
         return group
-    key = id(group)
+    key = _group_key(dist, group)
     if key not in _COUNT_GROUPS:
-        ranks = None if group is None else dist.get_process_group_ranks(group)
-        _COUNT_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+        _COUNT_GROUPS[key] = dist.new_group(ranks=list(key), backend="gloo")
+    return _COUNT_GROUPS[key]
+
+
+def count_group(dist, group=None):
+    """The count group set up by ``setup_count_group`` (gloo jobs: the group itself)."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = _group_key(dist, group)
+    if key not in _COUNT_GROUPS:
+        raise RuntimeError("strips.exchange over a non-gloo group needs setup_count_group(dist, group) on every "
+                           "rank at setup (dist.new_group is collective)")
     return _COUNT_GROUPS[key]
 
 

@@ -236,10 +236,11 @@ def test_cfg1_vs_sequential_oracle_gpu(oracle_mod):
             np.testing.assert_array_equal(gl, ol)
 
 
-@pytest.mark.parametrize("cfg,n,ticks", [("cfg2", 20000, 4), ("cfg3", 40000, 3)])
+@pytest.mark.parametrize("cfg,n,ticks", [("cfg2", 20000, 4), ("cfg2", 100000, 4), ("cfg3", 40000, 3)])
 def test_scaled_configs_vs_closed_form_gpu(oracle_mod, cfg, n, ticks):
-    """cfg2/cfg3 at reduced N (same density): GPU events == diff of the
-    closed-form relation, and the GPU relation == the closed form."""
+    """cfg2 at its own size (100k) and reduced, cfg3 reduced (same density): GPU
+    events == diff of the closed-form relation, and the GPU relation == the
+    closed form."""
     wl = make_workload(cfg, n=n)
     seq = np.zeros(wl.n, np.uint64)
     sp = np.zeros(wl.n, np.uint32)

@@ -295,3 +295,38 @@ def test_sync_fanout_full_size_sampled():
             cid = b"C%015d" % b
             exp = sorted(cid + bytes(eids[a]) + struct.pack("<4f", *pos[int(a)]) for a in w.neighbors(b))
             assert sorted(by_client.get(cid, [])) == exp, f"receiver {b}"
+
+
+@pytest.mark.gpu
+def test_sync_repeated_records_outside_spaces_list_each_slot_once():
+    """More client records than max_slots, all for syncing entities outside every
+    AOI space (nilSpace): k_decode lists such a slot for its own-client record at
+    most once (atomic flag claim), so its per-slot list cannot overflow; the
+    collects match the restatement (GameService.go:392-404, Entity.go:1221-1267)."""
+    from goworld_amd import World
+    n, reps = 8, 5
+    eids = [bytes([70 + i]) * 16 for i in range(n)]
+    cids = [bytes([110 + i]) * 16 for i in range(n)]
+    g = GameEntities({0: 100.0}, n)
+    with World(n, device=0) as w:
+        w.entity_bind(list(range(n)), eids)
+        for i in range(n):
+            g.create(eids[i], i, 0.0, 0.0, 0.0, 0.0)
+            w.entity_set_client(i, 1 + i % 2, cids[i])
+            g.set_client(i, 1 + i % 2, cids[i])
+            w.entity_set_syncing(i, True)
+            g.set_syncing(i, True)
+        assert records_by_gate(w.collect_sync_infos()) == g.collect()
+        pkt = b"".join(rec(eids[i], float(k), 1.0, float(i), 0.25 * k) for k in range(reps) for i in range(n))
+        w.sync_from_clients(pkt)
+        g.handle_sync_packet(pkt)
+        w.tick()
+        assert records_by_gate(w.collect_sync_infos()) == g.collect() == {}
+        for i in range(0, n, 2):  # server-side moves: own-client records with the stale position
+            w.set_position_yaw(i, 9.0, 9.0, 9.0, -1.0)
+            g.set_position_yaw(i, 9.0, 9.0, 9.0, -1.0)
+        w.sync_from_clients(pkt)
+        g.handle_sync_packet(pkt)
+        w.tick()
+        got = records_by_gate(w.collect_sync_infos())
+        assert got == g.collect() and sum(len(v) for v in got.values()) == n // 2
