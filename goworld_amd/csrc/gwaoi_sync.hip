@@ -1344,7 +1344,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     A.scr_cursor = S->scr_cursor;
     if (n_ent) k_fan_prep<<<cdivu(n_ent, ST), ST, 0, S->st>>>(A);  // also clears the flags
     uint64_t total = 0;
-    S->h_off_raw.assign(1, 0);
+    S->h_off_raw.assign((size_t)G + 1, 0);  // G gates, all empty unless the passes below run
     if (G && n_ent) {
         // pass 1: hits into the scratch; a run past the capacity is redone after a regrow
         for (int attempt = 0;; ++attempt) {
