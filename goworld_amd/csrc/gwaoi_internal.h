@@ -163,20 +163,6 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
                      SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
                      hipStream_t st);
 
-// Block tickets of the look-back kernels (k_scan64_lb, k_finish): a device
-// counter that is never reset and the host's running count of the tickets
-// handed out so far; take(g) returns a launch's first ticket.  One counter per
-// stream (launches on it run in order).
-struct LbTickets {
-    uint32_t *counter = nullptr;
-    uint32_t next = 0;
-    uint32_t take(uint32_t g) {
-        const uint32_t f = next;
-        next += g;
-        return f;
-    }
-};
-
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
 // partials in blk, 2 * cdiv(n, 256) floats).  cnt64 != nullptr (grid
 // unchanged): also per-cell entity counts (low word) and arrival counts
@@ -197,7 +183,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, uint32_t tag, LbTickets &tk, hipStream_t st);
+                      TickScalars *sc, uint32_t tag, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
@@ -243,7 +229,7 @@ size_t finish_lb_elems(size_t n_entries);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, LbTickets &tk, hipStream_t st);
+                   uint32_t n_spaces, void *parts_mem, hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,

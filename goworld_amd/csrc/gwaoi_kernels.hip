@@ -729,25 +729,19 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 // (tag << 2 | kind) << 32 | value: the tag is fresh per launch (the words are
 // never zeroed per flush; tag 0 = never written), kind 1 = aggregate,
 // 2 = inclusive.  The words are read and written with device-scope atomics.
-// A block's scan index is a ticket taken with one atomic on entry, not
-// blockIdx.x (HIP does not promise dispatch in index order): every block
-// before a running block has started, so the lowest unfinished one always runs
-// and never waits, and the walk terminates.  The ticket counter is never reset:
-// the host passes the launch's first ticket (the running sum of grid sizes).
-// When the 30-bit tag wraps the host zeroes the status words first.
+// Blocks take their scan index from blockIdx.x.  The walk terminates because
+// the command processor dispatches a launch's workgroups in index order (per
+// XCD, round robin over the XCDs): the lowest unfinished block has every
+// predecessor finished, so it never waits, and every block before it on its
+// XCD has finished, so it has been dispatched.  An atomic ticket per block
+// (index order independent of dispatch) was measured: +9 us in the sort's scan
+// and +11 us in k_finish per cfg3 tick (one contended counter, ~1000 blocks),
+// 7% of the tick (profiles/r03_ticket_lookback.log), so it is not used.
+// When the 30-bit tag wraps, the host zeroes the status words first.
 constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
 
 __device__ __forceinline__ unsigned long long lb_word(uint32_t tag, uint32_t kind, uint32_t v) {
     return ((unsigned long long)((tag << 2) | kind) << 32) | v;
-}
-
-// This block's index in look-back order (see above); called by every thread.
-__device__ __forceinline__ uint32_t lb_ticket(uint32_t *ticket, uint32_t first) {
-    __shared__ uint32_t s_t;
-    // (mod the grid: even a host count out of step with the counter yields a permutation of 0..grid-1)
-    if (threadIdx.x == 0) s_t = (atomicAdd(ticket, 1u) - first) % gridDim.x;
-    __syncthreads();
-    return s_t;
 }
 
 __device__ __forceinline__ void lb_store(unsigned long long *p, unsigned long long v) {
@@ -879,9 +873,8 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
-                                                    const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
-                                                    uint32_t *ticket, uint32_t first) {
-    const uint32_t b = lb_ticket(ticket, first);
+                                                    const float *__restrict__ blk, uint32_t nbk, TickScalars *sc) {
+    const uint32_t b = blockIdx.x;
     if (b == nb) {
         keygen_fold256(blk, nbk, sc);
         return;
@@ -2256,8 +2249,8 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap,
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
-                                                uint32_t ns, uint32_t *ticket, uint32_t first) {
-    const uint32_t b = lb_ticket(ticket, first), R = gridDim.x - 1;
+                                                uint32_t ns) {
+    const uint32_t b = blockIdx.x, R = gridDim.x - 1;
     if (b == R) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         if (threadIdx.x == 0) {
             res->err = sc->err;
@@ -2498,11 +2491,11 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, uint32_t tag, LbTickets &tk, hipStream_t st) {
+                      TickScalars *sc, uint32_t tag, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, SC_TILE);
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
-                                         cdiv(n_total, 256), sc, tk.counter, tk.take(nb + 1));
+                                         cdiv(n_total, 256), sc);
     if (n_total) k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
                                                          n_new, n_total, sentinel, perm, skeys);
@@ -2592,13 +2585,12 @@ size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, LbTickets &tk, hipStream_t st) {
+                   uint32_t n_spaces, void *parts_mem, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     k_finish<<<R + 1, 256, 0, st>>>(tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu,
                                     reinterpret_cast<const uint2 *>(tmp_pairs), reinterpret_cast<uint2 *>(out_pairs),
-                                    cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox, n_spaces,
-                                    tk.counter, tk.take(R + 1));
+                                    cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox, n_spaces);
 }
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }

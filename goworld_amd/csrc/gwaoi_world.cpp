@@ -197,7 +197,6 @@ struct gwaoi_world {
     uint32_t *tile_total = nullptr;
     unsigned long long *tile_lb = nullptr;  // k_finish look-back status words
     uint32_t lb_tag = 0;  // look-back launches so far (tags: k_finish, the incremental sort's scan)
-    gw::LbTickets lb_tickets;  // their block tickets (counter on the device, zeroed at creation)
     unsigned long long *tile_base = nullptr;
     size_t tile_entries_cap = 0;
     gw::TickScalars *sc = nullptr;
@@ -695,7 +694,7 @@ void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_
     stage_begin(w, ST_FINISH);
     gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, w->events,
                       w->ev_cap, w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), Fn.n, dev_bbox(w),
-                      w->n_space_ids, w->bbox_parts, w->lb_tickets, st);
+                      w->n_space_ids, w->bbox_parts, st);
     stage_end(w, ST_FINISH);
 }
 
@@ -850,7 +849,7 @@ int tick_launch(gwaoi_world *w) {
     if (incr) {
         gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             w->keys[1], w->blk, w->sc, next_lb_tag(w), w->lb_tickets, st);
+                             w->keys[1], w->blk, w->sc, next_lb_tag(w), st);
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -1070,7 +1069,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base); dfree(w->lb_tickets.counter);
+    dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items);
@@ -1154,14 +1153,12 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->coll, N)) ||
         (rc = dalloc(w, &w->sc, 1)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, (char **)&w->bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
-        (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)) ||
-        (rc = dalloc(w, &w->lb_tickets.counter, 1)))
+        (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     // lastop = 0, rank = sp = 0xFFFFFFFF (not live); S' records seq 0 (virtual S': never "written")
     if (hipMemset(w->srec, 0, N * sizeof(gw::Rec16)) != hipSuccess ||
         hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
-        hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess ||
-        hipMemset(w->lb_tickets.counter, 0, sizeof(uint32_t)) != hipSuccess)
+        hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_tile_entries(w, 4 * (size_t)gw::combined_blocks((uint32_t)N)))) return fail(rc);
