@@ -74,12 +74,13 @@ TICK_BENCH_OUT = os.path.join(HERE, "lib", "gwaoi_tick_bench")
 def build_tick_bench(force: bool = False, verbose: bool = False) -> str:
     """C++ host tick bench (tools/tick_bench.cpp): the cgo-like end-to-end tick + callback replay."""
     lib = build(force=force, verbose=verbose)
-    deps = [TICK_BENCH_SRC, lib, os.path.join(ROOT, "include", "gwaoi.h")]
+    deps = [TICK_BENCH_SRC, lib, os.path.join(ROOT, "include", "gwaoi.h"), os.path.join(ROOT, "tools", "interest_sets.hpp")]
     if (not force and os.path.exists(TICK_BENCH_OUT)
             and all(os.path.getmtime(d) <= os.path.getmtime(TICK_BENCH_OUT) for d in deps)):
         return TICK_BENCH_OUT
     tmp = TICK_BENCH_OUT + ".tmp"
-    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"), TICK_BENCH_SRC,
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"), "-I",
+           os.path.join(ROOT, "tools"), TICK_BENCH_SRC,
            "-o", tmp, "-L", os.path.dirname(lib), "-lgwaoi", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -240,7 +240,8 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st);
 // off[n_rows + 1] (exclusive scan of the counts, cnt is scratch), items[n_total]
 // = b | 0x80000000 for an enter, each row sorted (leaves first).
 void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_total, uint32_t n_rows, uint32_t *cnt,
-                       uint32_t *off, uint32_t *scan_tmp, uint32_t *items, hipStream_t st);
+                       uint32_t *off, uint32_t *scan_tmp, uint32_t *items, uint32_t *scratch, uint32_t *long_rows,
+                       hipStream_t st);
 
 // ---- world accessors for the entity-sync layer (gwaoi_sync.cpp) -------------
 struct SyncState;

@@ -2386,11 +2386,22 @@ __global__ void k_csr_fill(const uint2 *__restrict__ ev, uint32_t n_enter, uint3
     items[off[p.x] + atomicAdd(&cur[p.x], 1u)] = p.y | (e < n_enter ? CSR_ENTER : 0u);
 }
 
-// one lane per row: rows are short (a few events per entity per tick)
-__global__ void k_csr_sort(const uint32_t *__restrict__ off, uint32_t n_rows, uint32_t *items) {
+// Rows are short in a steady tick (about one event per entity): one lane sorts
+// a row of up to CSR_SHORT items by insertion.  Longer rows (a populate or
+// teleport burst: 85-460 items at config 3, the whole crowd for co-located
+// entities) are listed and sorted by a block each (k_csr_sort_long).
+constexpr uint32_t CSR_SHORT = 32;
+constexpr uint32_t CSR_LDS = 4096;  // items a block sorts in LDS at once (16 KB)
+
+__global__ void k_csr_sort(const uint32_t *__restrict__ off, uint32_t n_rows, uint32_t *items, uint32_t *long_rows,
+                           uint32_t *n_long) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_rows) return;
     const uint32_t b = off[r], e = off[r + 1];
+    if (e - b > CSR_SHORT) {
+        long_rows[atomicAdd(n_long, 1u)] = r;
+        return;
+    }
     for (uint32_t k = b + 1; k < e; ++k) {
         const uint32_t v = items[k];
         uint32_t j = k;
@@ -2402,20 +2413,90 @@ __global__ void k_csr_sort(const uint32_t *__restrict__ off, uint32_t n_rows, ui
     }
 }
 
+// Block-wide merge of the sorted runs a[0, na) and b[0, nb) into out: thread t
+// writes outputs [t * per, (t + 1) * per), its split found on the merge path.
+__device__ void block_merge(const uint32_t *__restrict__ a, uint32_t na, const uint32_t *__restrict__ b, uint32_t nb,
+                            uint32_t *__restrict__ out) {
+    const uint32_t n = na + nb, per = (n + blockDim.x - 1) / blockDim.x;
+    const uint32_t d0 = min(threadIdx.x * per, n), d1 = min(d0 + per, n);
+    if (d0 >= d1) return;
+    // i = items taken from a among the first d0 outputs (a wins ties: stable)
+    uint32_t lo = d0 > nb ? d0 - nb : 0u, hi = min(d0, na);
+    while (lo < hi) {
+        const uint32_t i = (lo + hi) / 2;
+        if (a[i] <= b[d0 - i - 1]) lo = i + 1;
+        else hi = i;
+    }
+    uint32_t i = lo, j = d0 - lo;
+    for (uint32_t d = d0; d < d1; ++d) out[d] = (j >= nb || (i < na && a[i] <= b[j])) ? a[i++] : b[j++];
+}
+
+__global__ __launch_bounds__(256) void k_csr_sort_long(const uint32_t *__restrict__ off, uint32_t *items,
+                                                       uint32_t *scratch, const uint32_t *__restrict__ long_rows,
+                                                       const uint32_t *__restrict__ n_long) {
+    __shared__ uint32_t s[CSR_LDS];
+    const uint32_t nl = *n_long, tid = threadIdx.x, T = blockDim.x;
+    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
+        const uint32_t r = long_rows[q], b = off[r], len = off[r + 1] - b;
+        // runs of CSR_LDS sorted in LDS (bitonic over the next power of two, padded with ~0)
+        for (uint32_t c0 = 0; c0 < len; c0 += CSR_LDS) {
+            const uint32_t m = min(CSR_LDS, len - c0);
+            uint32_t p = 1;
+            while (p < m) p <<= 1;
+            for (uint32_t i = tid; i < p; i += T) s[i] = i < m ? items[b + c0 + i] : 0xFFFFFFFFu;
+            __syncthreads();
+            for (uint32_t k = 2; k <= p; k <<= 1)
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t i = tid; i < p; i += T) {
+                        const uint32_t ixj = i ^ j;
+                        if (ixj > i) {
+                            const uint32_t x = s[i], y = s[ixj];
+                            if ((x > y) == ((i & k) == 0)) {
+                                s[i] = y;
+                                s[ixj] = x;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            for (uint32_t i = tid; i < m; i += T) items[b + c0 + i] = s[i];
+            __syncthreads();
+        }
+        // merge passes, ping-pong with the scratch
+        uint32_t *src = items + b, *dst = scratch + b;
+        for (uint32_t w = CSR_LDS; w < len; w <<= 1) {
+            for (uint32_t lo = 0; lo < len; lo += 2 * w) {
+                const uint32_t na = min(w, len - lo), nb = len - lo > w ? min(w, len - lo - w) : 0u;
+                block_merge(src + lo, na, src + lo + na, nb, dst + lo);
+            }
+            __syncthreads();
+            uint32_t *t = src;
+            src = dst;
+            dst = t;
+        }
+        if (src != items + b) {
+            for (uint32_t i = tid; i < len; i += T) items[b + i] = src[i];
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 // ============================================================ launchers ======
 
 void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_total, uint32_t n_rows, uint32_t *cnt,
-                       uint32_t *off, uint32_t *scan_tmp, uint32_t *items, hipStream_t st) {
+                       uint32_t *off, uint32_t *scan_tmp, uint32_t *items, uint32_t *scratch, uint32_t *long_rows,
+                       hipStream_t st) {
     const uint2 *ev = reinterpret_cast<const uint2 *>(ev_pairs);
     k_zero<<<cdiv((size_t)n_rows + 1, 256), 256, 0, st>>>(cnt, (size_t)n_rows + 1);
     if (n_total) k_csr_count<<<cdiv(n_total, 256), 256, 0, st>>>(ev, (uint32_t)n_total, cnt);
     scan_exclusive(cnt, off, (size_t)n_rows + 1, scan_tmp, st);
     if (!n_total) return;
-    k_zero<<<cdiv((size_t)n_rows, 256), 256, 0, st>>>(cnt, (size_t)n_rows);
+    k_zero<<<cdiv((size_t)n_rows + 1, 256), 256, 0, st>>>(cnt, (size_t)n_rows + 1);  // cursors + long-row count
     k_csr_fill<<<cdiv(n_total, 256), 256, 0, st>>>(ev, (uint32_t)n_enter, (uint32_t)n_total, off, cnt, items);
-    k_csr_sort<<<cdiv(n_rows, 256), 256, 0, st>>>(off, n_rows, items);
+    k_csr_sort<<<cdiv(n_rows, 256), 256, 0, st>>>(off, n_rows, items, long_rows, cnt + n_rows);
+    k_csr_sort_long<<<512, 256, 0, st>>>(off, items, scratch, long_rows, cnt + n_rows);
 }
 
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,

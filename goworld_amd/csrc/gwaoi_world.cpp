@@ -206,7 +206,7 @@ struct gwaoi_world {
     uint32_t *nb_out = nullptr, *nb_count = nullptr;
     size_t nb_cap = 0;
     // per-slot rows of the last flush's events (gwaoi_events_csr), built on request
-    uint32_t *csr_cnt = nullptr, *csr_off = nullptr, *csr_items = nullptr;
+    uint32_t *csr_cnt = nullptr, *csr_off = nullptr, *csr_items = nullptr, *csr_long = nullptr;
     uint64_t csr_items_cap = 0;
     uint32_t *h_csr_off = nullptr, *h_csr_items = nullptr;
     uint64_t h_csr_items_cap = 0;
@@ -1072,7 +1072,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
     dfree(w->nb_out); dfree(w->nb_count);
-    dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items);
+    dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);
     if (w->h_csr_off) (void)hipHostFree(w->h_csr_off);
     if (w->h_csr_items) (void)hipHostFree(w->h_csr_items);
     if (w->h_out) (void)hipHostFree(w->h_out);
@@ -1732,19 +1732,21 @@ int build_csr(gwaoi_world *w) {
     const size_t rows = w->max_slots;
     if (!w->csr_cnt) {
         int rc;
-        if ((rc = dalloc(w, &w->csr_cnt, rows + 1)) || (rc = dalloc(w, &w->csr_off, rows + 1))) return rc;
+        if ((rc = dalloc(w, &w->csr_cnt, rows + 1)) || (rc = dalloc(w, &w->csr_off, rows + 1)) ||
+            (rc = dalloc(w, &w->csr_long, rows)))
+            return rc;
     }
     if (tot > w->csr_items_cap) {
         HIP_TRY(hipStreamSynchronize(w->stream));
         dfree(w->csr_items);
         w->csr_items_cap = 0;
         const uint64_t cap = std::max<uint64_t>(tot + tot / 4, 1 << 16);
-        if (int rc = dalloc(w, &w->csr_items, cap)) return rc;
+        if (int rc = dalloc(w, &w->csr_items, 2 * cap)) return rc;  // items | merge scratch of long rows
         w->csr_items_cap = cap;
     }
     if (int rc = ensure_scan_tmp(w, rows + 1)) return rc;
     gw::launch_events_csr(w->events, w->last_n_enter, tot, (uint32_t)rows, w->csr_cnt, w->csr_off, w->scan_tmp,
-                          w->csr_items, w->stream);
+                          w->csr_items, w->csr_items + w->csr_items_cap, w->csr_long, w->stream);
     HIP_TRY(hipGetLastError());
     w->csr_tick = w->ticks;
     return GWAOI_OK;

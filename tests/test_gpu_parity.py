@@ -861,3 +861,43 @@ def test_events_csr_regroups_events_gpu():
             for r in range(0, n, 97):  # each row sorted: leaves (bit 31 clear) first, each part by b
                 row = items[off[r]:off[r + 1]]
                 assert np.all(row[:-1] <= row[1:])
+
+
+def test_events_csr_long_rows_gpu():
+    """Rows past one lane's insertion sort: a populate flush with a co-located crowd of
+    5000 (rows of 4999 items: LDS-sorted runs + block merge) and a 60-entity crowd
+    beside a 1500-entity one (rows of 59 .. 1559: one LDS run), then a flush where
+    the big crowd leaves -- every row sorted and the CSR equal to the event pairs."""
+    rng = np.random.default_rng(43)
+    n = 5000 + 1500 + 60 + 3000
+    x = np.zeros(n, np.float32)
+    z = np.zeros(n, np.float32)
+    x[5000:6500] = rng.uniform(1000, 1100, 1500)
+    z[5000:6500] = rng.uniform(1000, 1100, 1500)
+    x[6500:6560] = rng.uniform(1050, 1150, 60)
+    z[6500:6560] = rng.uniform(1000, 1100, 60)
+    x[6560:] = rng.uniform(-50000, 50000, n - 6560)  # sparse background: short rows
+    z[6560:] = rng.uniform(-50000, 50000, n - 6560)
+    order = rng.permutation(n).astype(np.uint32)
+    with World(n) as w:
+        s = w.space_create(100.0)
+        w.enter_batch(s, order, x[order], z[order])
+        for flush in range(2):
+            ent, lev = w.tick()
+            off, items = w.events_csr()
+            assert off[-1] == items.size == ent.shape[0] + lev.shape[0]
+            lens = np.diff(off)
+            if flush == 0:
+                assert lens.max() == 4999 and np.sum((lens > 32) & (lens < 4096)) > 1000
+            rows = np.repeat(np.arange(n, dtype=np.uint64), lens.astype(np.int64))
+            b = (items & np.uint32(0x7FFFFFFF)).astype(np.uint64)
+            is_enter = (items & np.uint32(0x80000000)) != 0
+            keys = (rows << np.uint64(32)) | b
+            np.testing.assert_array_equal(np.sort(keys[is_enter]), pair_keys(ent))
+            np.testing.assert_array_equal(np.sort(keys[~is_enter]), pair_keys(lev))
+            starts = off[:-1][lens > 1]
+            for r in np.nonzero(lens > 1)[0]:
+                row = items[off[r]:off[r + 1]]
+                assert np.all(row[:-1] <= row[1:]), f"flush {flush} row {r} ({row.size} items) not sorted"
+            assert starts.size > 0
+            w.leave_batch(np.arange(5000, dtype=np.uint32))  # next flush: 5000 rows of 4999 leaves

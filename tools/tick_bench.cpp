@@ -13,15 +13,24 @@
 //              gwaoi_tick_end(t)  (period = host staging overlapped with the flush)
 //   replay     the tick's events into the sets: the event pairs on one thread;
 //              the per-entity rows of gwaoi_events_csr on one and on T threads
-//              (each thread owns the sets of a slot range)
+//              (each thread owns the sets of a slot range; persistent pool)
+//
+// The sets are flat open-addressing tables in slot order (tools/interest_sets.hpp),
+// so a replay of the rows moves forward through memory, about one cache line per
+// set operation.  At the end 1,000 sampled entities' InterestedIn sets are
+// compared with gwaoi_neighbors (the replay is exact, not just timed).
 //
 // The workload mirrors goworld_amd/workload.py (SplitMix64, Box-Muller in
 // double); only its shape matters here, not bit-identity with the Python one.
 //
 // usage: gwaoi_tick_bench [ticks=20] [threads=16] [n=1000000]
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +39,7 @@
 #include <vector>
 
 #include "gwaoi.h"
+#include "interest_sets.hpp"
 
 namespace {
 
@@ -68,54 +78,98 @@ void check(int rc, const char *what, gwaoi_world *w) {
     }
 }
 
-// Per-entity sets: the event stream never adds a present member or removes an
-// absent one, so a vector with swap-remove is an exact set.
+// InterestedIn / InterestedBy of every entity, split into T slot ranges (one
+// owner thread each).
 struct Sets {
-    std::vector<std::vector<uint32_t>> in, by;
-    explicit Sets(size_t n) : in(n), by(n) {}
+    uint32_t n, T;
+    std::vector<gwsets::Range> in, by;
+    Sets(uint32_t n_, uint32_t T_, const uint32_t *sizes) : n(n_), T(T_), in(T_), by(T_) {
+        for (uint32_t k = 0; k < T; ++k) {
+            const uint32_t lo = lo_of(k), hi = lo_of(k + 1);
+            in[k].init(lo, hi, sizes ? sizes + lo : nullptr);
+            by[k].init(lo, hi, sizes ? sizes + lo : nullptr);
+        }
+    }
+    uint32_t lo_of(uint32_t k) const { return (uint32_t)((uint64_t)n * k / T); }
+    uint32_t owner(uint32_t s) const {  // range holding slot s
+        uint32_t k = (uint32_t)((uint64_t)s * T / n);
+        while (k + 1 < T && s >= lo_of(k + 1)) ++k;
+        while (k > 0 && s < lo_of(k)) --k;
+        return k;
+    }
 };
 
-void erase_one(std::vector<uint32_t> &v, uint32_t x) {
-    for (size_t i = 0; i < v.size(); ++i)
-        if (v[i] == x) {
-            v[i] = v.back();
-            v.pop_back();
-            return;
-        }
-}
-
-// Entity.go:236-246 for the flush's events (leaves first, then enters), for
-// the slots in [lo, hi) only (In of a, By of b).
-void replay(Sets &S, const gwaoi_events &ev, uint32_t lo, uint32_t hi) {
+// Entity.go:236-246 for the flush's event pairs on one thread (leaves first, then
+// enters): uninterest / interest = a.In -/+= b, b.By -/+= a.
+void replay_pairs(Sets &S, const gwaoi_events &ev) {
     for (uint64_t k = 0; k < ev.n_leave; ++k) {
         const uint32_t a = ev.leave[2 * k], b = ev.leave[2 * k + 1];
-        if (a >= lo && a < hi) erase_one(S.in[a], b);
-        if (b >= lo && b < hi) erase_one(S.by[b], a);
+        S.in[S.owner(a)].del(a, b);
+        S.by[S.owner(b)].del(b, a);
     }
     for (uint64_t k = 0; k < ev.n_enter; ++k) {
         const uint32_t a = ev.enter[2 * k], b = ev.enter[2 * k + 1];
-        if (a >= lo && a < hi) S.in[a].push_back(b);
-        if (b >= lo && b < hi) S.by[b].push_back(a);
+        S.in[S.owner(a)].add(a, b);
+        S.by[S.owner(b)].add(b, a);
     }
 }
 
-// The same with the events regrouped by entity (gwaoi_events_csr): row s lists
-// every change of s's InterestedIn and, events coming in pairs, of its
-// InterestedBy -- one pass per entity, no scan of the whole event list.
-void replay_csr(Sets &S, const uint32_t *off, const uint32_t *items, uint32_t lo, uint32_t hi) {
-    for (uint32_t s = lo; s < hi; ++s) {
-        for (uint32_t k = off[s]; k < off[s + 1]; ++k) {
-            const uint32_t it = items[k], b = it & ~GWAOI_CSR_ENTER;
-            if (it & GWAOI_CSR_ENTER) {
-                S.in[s].push_back(b);
-                S.by[s].push_back(b);
-            } else {
-                erase_one(S.in[s], b);
-                erase_one(S.by[s], b);
+// Persistent workers: run(f) calls f(k) for k = 0..T-1 (k = 0 on the caller) and waits.
+class Pool {
+  public:
+    explicit Pool(unsigned T) : T_(T) {
+        for (unsigned k = 1; k < T; ++k) th_.emplace_back([this, k] { loop(k); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void run(const std::function<void(unsigned)> &f) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            f_ = &f;
+            left_ = T_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+    }
+
+  private:
+    void loop(unsigned k) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)> *f;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                f = f_;
+            }
+            (*f)(k);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (--left_ == 0) done_.notify_one();
             }
         }
     }
-}
+    unsigned T_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)> *f_ = nullptr;
+    uint64_t gen_ = 0;
+    unsigned left_ = 0;
+    bool stop_ = false;
+};
 
 }  // namespace
 
@@ -182,16 +236,21 @@ int main(int argc, char **argv) {
     check(gwaoi_enter_batch(w, sp, bs[0].data(), bx[0].data(), bz[0].data(), n), "enter_batch", w);
     gwaoi_events ev{};
     check(gwaoi_tick(w, &ev), "populate", w);
-    Sets S(n);
-    replay(S, ev, 0, n);
     const uint64_t populate = ev.n_enter;
+    // the sets start from the populate flush's rows (tables sized 2x the first relation)
+    const uint32_t *coff = nullptr, *citems = nullptr;
+    uint64_t cn = 0;
+    check(gwaoi_events_csr(w, &coff, &citems, &cn), "events_csr (populate)", w);
+    std::vector<uint32_t> sizes(n);
+    for (uint32_t i = 0; i < n; ++i) sizes[i] = coff[i + 1] - coff[i];
+    Sets S(n, T, sizes.data());
+    Pool pool(T);
+    pool.run([&](unsigned k) { gwsets::replay_rows(S.in[k], S.by[k], coff, citems, GWAOI_CSR_ENTER); });
 
     // ---- serial leg: moved_batch + tick, then replay (one thread); odd ticks replay the event
     // pairs, even ticks the per-entity rows (gwaoi_events_csr, built on the GPU and copied)
     std::vector<double> t_stage, t_tick, t_lat, t_rep1, t_csr, t_repc1;
     uint64_t events = 0;
-    const uint32_t *coff = nullptr, *citems = nullptr;
-    uint64_t cn = 0;
     for (int t = 1; t <= ticks; ++t) {
         const double a = now();
         check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
@@ -200,12 +259,12 @@ int main(int argc, char **argv) {
         const double c = now();
         double d, e = 0;
         if (t % 2) {
-            replay(S, ev, 0, n);
+            replay_pairs(S, ev);
             d = now();
         } else {
             check(gwaoi_events_csr(w, &coff, &citems, &cn), "events_csr", w);
             e = now();
-            replay_csr(S, coff, citems, 0, n);
+            for (unsigned k = 0; k < T; ++k) gwsets::replay_rows(S.in[k], S.by[k], coff, citems, GWAOI_CSR_ENTER);
             d = now();
         }
         if (t > 2) {  // the first ticks size the pinned buffers
@@ -225,15 +284,9 @@ int main(int argc, char **argv) {
     // t+1 and replays the callbacks of t-1 on T threads (the events of t-1 stay in the pinned
     // buffer until gwaoi_tick_end(t) replaces them)
     std::vector<double> p_lat, t_repT, p_host;
-    auto replay_T = [&]() {  // the rows of the last gwaoi_events_csr, T threads over slot ranges
+    auto replay_T = [&]() {  // the rows of the last gwaoi_events_csr, T pool threads over slot ranges
         const double r0 = now();
-        std::vector<std::thread> th;
-        for (unsigned k = 1; k < T; ++k)
-            th.emplace_back([&, k] {
-                replay_csr(S, coff, citems, (uint32_t)((uint64_t)n * k / T), (uint32_t)((uint64_t)n * (k + 1) / T));
-            });
-        replay_csr(S, coff, citems, 0, (uint32_t)((uint64_t)n / T));
-        for (auto &x : th) x.join();
+        pool.run([&](unsigned k) { gwsets::replay_rows(S.in[k], S.by[k], coff, citems, GWAOI_CSR_ENTER); });
         t_repT.push_back(now() - r0);
     };
     int t = ticks + 1;
@@ -259,11 +312,25 @@ int main(int argc, char **argv) {
     replay_T();
     const double p_total = now() - p0;
     const double p_flush = p_total;
-    // sanity: In == By in size, and the sets hold the last flush's relation size
+    // exactness: In == By in size, the sets hold the last flush's relation, and 1,000 sampled
+    // InterestedIn sets equal the world's neighbour rows
     uint64_t sin = 0, sby = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        sin += S.in[i].size();
-        sby += S.by[i].size();
+        sin += S.in[S.owner(i)].size(i);
+        sby += S.by[S.owner(i)].size(i);
+    }
+    uint32_t sample_bad = 0;
+    {
+        std::vector<uint32_t> nb(1 << 16);
+        Stream sq{subseed(seed, 0x5A)};
+        for (int q = 0; q < 1000; ++q) {
+            const uint32_t s = (uint32_t)(sq.next() % n);
+            size_t cnt = 0;
+            check(gwaoi_neighbors(w, s, nb.data(), nb.size(), &cnt), "neighbors", w);
+            std::vector<uint32_t> want(nb.begin(), nb.begin() + (long)std::min(cnt, nb.size()));
+            std::sort(want.begin(), want.end());
+            if (S.in[S.owner(s)].members(s) != want || S.by[S.owner(s)].members(s) != want) ++sample_bad;
+        }
     }
     gwaoi_world_destroy(w);
     const double ms = 1e3;
@@ -277,13 +344,13 @@ int main(int argc, char **argv) {
         "of t; latency = batch call to the rows in pinned host memory\"}, "
         "\"replay\": {\"pairs_ms_1thread_p50\": %.4f, \"csr_build_copy_ms_p50\": %.4f, "
         "\"csr_ms_1thread_p50\": %.4f, \"csr_ms_%uthreads_p50\": %.4f, \"threads\": %u}, "
-        "\"relation_pairs\": %llu, \"in_eq_by\": %s}\n",
+        "\"relation_pairs\": %llu, \"in_eq_by\": %s, \"sampled_sets_vs_neighbors_mismatches\": %u}\n",
         n, ticks, (unsigned long long)populate, (double)events / std::max<size_t>(1, t_lat.size()),
         pct(t_stage, 50) * ms, pct(t_tick, 50) * ms,
         std::accumulate(t_lat.begin(), t_lat.end(), 0.0) / std::max<size_t>(1, t_lat.size()) * ms,
         pct(t_lat, 50) * ms, pct(t_lat, 99) * ms, p_flush / done * ms, (double)n * done / p_flush,
         pct(p_lat, 50) * ms, pct(p_lat, 99) * ms, pct(p_host, 50) * ms, pct(t_rep1, 50) * ms,
         pct(t_csr, 50) * ms, pct(t_repc1, 50) * ms, T, pct(t_repT, 50) * ms, T,
-        (unsigned long long)sin, sin == sby ? "true" : "false");
+        (unsigned long long)sin, sin == sby ? "true" : "false", sample_bad);
     return 0;
 }
