@@ -212,6 +212,97 @@ def sync_leg(w, n: int, batches, client_frac: float):
                     "CollectEntitySyncInfos into per-gate 48-B records in HBM; wall clock per phase"}
 
 
+def wire_leg(steps: int, n_rec: int, n_out_rec: int, device: int):
+    """The gate / dispatcher position-sync regroups (include/gwaoi_wire.h) on the GPU
+    beside the host C regroup of the same records (oracle/wire_host.c, one thread --
+    the reference appends records to per-destination packets on one goroutine):
+      gate_from_clients   n_rec 32-B client records -> 8 dispatchers (GateService.go:398-425)
+      dispatcher_to_games n_rec 32-B records, n_rec entities in the table -> 8 games
+                          (DispatcherService.go:786-825)
+      gate_to_clients     n_out_rec 48-B records of one gate's share of a collect over
+                          n_out_rec / 64 connected clients (GateService.go:346-371)
+    GPU forms: host records in (pageable numpy: H2D + regroup + grouped records back in
+    pinned host memory) and device-resident (records in HBM, groups left in HBM).
+    Wall clock per call, median over `steps` after one warmup call."""
+    import ctypes as C
+    import torch
+    from goworld_amd import Wire
+    from goworld_amd._lib import WireGroups
+    from oracle import oracle
+    rng = np.random.default_rng(0x5EED57)
+    slots = np.arange(n_rec, dtype=np.uint32)
+    eids = entity_ids(slots)
+    pos = rng.uniform(-1000, 1000, (n_rec, 4)).astype(np.float32)
+    rec = np.ascontiguousarray(np.concatenate([eids[rng.permutation(n_rec)], pos.view(np.uint8)], axis=1))
+    games = (1 + slots % 8).astype(np.uint16)
+    n_cli = max(1, n_out_rec // 64)
+    cids = np.frombuffer(b"".join(b"C%015d" % c for c in range(n_cli)), np.uint8).reshape(n_cli, 16)
+    cidx = np.arange(n_cli, dtype=np.uint32)
+    who = rng.integers(0, n_cli, n_out_rec)
+    rec48 = np.ascontiguousarray(np.concatenate(
+        [cids[who], eids[rng.integers(0, n_rec, n_out_rec)], rng.uniform(-1, 1, (n_out_rec, 4)).astype(np.float32)
+         .view(np.uint8)], axis=1))
+    dev = f"cuda:{device}"
+    d_rec = torch.from_numpy(rec).to(dev)
+    d_rec48 = torch.from_numpy(rec48).to(dev)
+    torch.cuda.synchronize()
+    out = {}
+    with Wire(device) as W:
+        W.set_entity_games(eids, games)
+        W.set_clients(cids, cidx)
+        L = W._L
+        H = oracle.WireHost(eids, games.astype(np.uint32), cids, cidx)
+        legs = {
+            "gate_from_clients": (n_rec, 32, lambda g: L.gwaoi_wire_gate_from_clients(W._w, _ptr(rec), n_rec, 8, g),
+                                  lambda g: L.gwaoi_wire_gate_from_clients_device(W._w, C.c_void_p(d_rec.data_ptr()),
+                                                                                  n_rec, 8, g),
+                                  lambda: H.gate_from_clients(rec, 8)),
+            "dispatcher_to_games": (n_rec, 32, lambda g: L.gwaoi_wire_dispatcher_to_games(W._w, _ptr(rec), n_rec, g),
+                                    lambda g: L.gwaoi_wire_dispatcher_to_games_device(
+                                        W._w, C.c_void_p(d_rec.data_ptr()), n_rec, g),
+                                    lambda: H.dispatcher_to_games(rec)),
+            "gate_to_clients": (n_out_rec, 48, lambda g: L.gwaoi_wire_gate_to_clients(W._w, _ptr(rec48), n_out_rec, g),
+                                lambda g: L.gwaoi_wire_gate_to_clients_device(W._w, C.c_void_p(d_rec48.data_ptr()),
+                                                                              n_out_rec, g),
+                                lambda: H.gate_to_clients(rec48)),
+        }
+        for name, (n, rb, host_fn, dev_fn, cpu_fn) in legs.items():
+            res = {"records": n, "record_bytes": rb}
+            for form, fn in (("gpu_host_records", host_fn), ("gpu_device_records", dev_fn)):
+                g = WireGroups()
+                ts = []
+                for k in range(steps + 1):
+                    a = time.perf_counter()
+                    rc = fn(C.byref(g))
+                    if rc:
+                        raise RuntimeError(f"wire {name}: rc {rc}")
+                    if form == "gpu_device_records":
+                        torch.cuda.synchronize()
+                    if k:
+                        ts.append(time.perf_counter() - a)
+                t = float(np.median(ts))
+                res[form] = {"ms": round(t * 1e3, 4), "records_per_s": n / t, "groups": int(g.n_groups)}
+            ts = []
+            for k in range(max(2, steps // 2)):
+                a = time.perf_counter()
+                cpu_fn()
+                ts.append(time.perf_counter() - a)
+            t = float(np.median(ts))
+            res["cpu_host_c_1thread"] = {"ms": round(t * 1e3, 3), "records_per_s": n / t}
+            res["gpu_device_vs_cpu"] = round(t / (res["gpu_device_records"]["ms"] * 1e-3), 2)
+            res["gpu_host_vs_cpu"] = round(t / (res["gpu_host_records"]["ms"] * 1e-3), 2)
+            out[name] = res
+    out["note"] = ("wall clock per call (median); gpu_host_records = pageable host records in, grouped records in "
+                   "pinned host memory out (PCIe both ways); gpu_device_records = records and groups in HBM; "
+                   "cpu = oracle/wire_host.c, the reference's append-per-destination loop in C, one thread")
+    return out
+
+
+def _ptr(a):
+    import ctypes as C
+    return a.ctypes.data_as(C.c_void_p)
+
+
 def cpu_cores() -> int:
     """Host cores this process may use (the GPU box gives a 16-core share)."""
     try:
@@ -567,6 +658,11 @@ def main():
                     help="register tick t+1's move batch only after tick t's flush returned (default: registered "
                          "while the flush of tick t runs, gwaoi_tick_begin/_end, as a game loop receives moves)")
     ap.add_argument("--cfg4-spaces", type=int, default=8192)
+    ap.add_argument("--wire-steps", type=int, default=5,
+                    help="timed calls per gate/dispatcher regroup in the wire leg (0 = off)")
+    ap.add_argument("--wire-records", type=int, default=1_000_000, help="32-B client records per wire regroup call")
+    ap.add_argument("--wire-out-records", type=int, default=4_000_000,
+                    help="48-B game records per gate_to_clients call (one gate's share of a cfg3 collect)")
     args = ap.parse_args()
 
     # --gpus N without an outside launcher: spawn the N ranks here, before anything touches the GPU
@@ -785,6 +881,12 @@ def main():
                            "pinned host memory, over the ticks after the first (the pipeline fill, first_tick_ms); "
                            "serial = moved_batch + tick back to back. Not the headline value"}
     sync = sync_leg(w, n, sync_batches, args.sync_clients) if sync_batches else None
+    wire = None
+    if args.wire_steps > 0 and ws == 1 and args.workload == "cfg3":
+        try:
+            wire = wire_leg(args.wire_steps, args.wire_records, args.wire_out_records, device)
+        except Exception as e:  # a side leg must not take the headline down with it
+            wire = {"error": repr(e)}
     elapsed_max, (moves_all, events_all) = reduce_over_ranks(dist, elapsed, [moves, events], red_dev)
     w.close()
     cfg4 = None
@@ -857,6 +959,7 @@ def main():
             "roofline": roofline,
             "pcie_inclusive": host_io,
             "sync_leg": sync,
+            "wire_leg": wire,
             "stages_ms_per_tick": {k: round(v, 4) for k, v in stage_ms.items()},
             "stage_roofline": stage_roof,
             "stages_note": f"separate {bd} ticks after the timed region, every stage bracketed by HIP events "

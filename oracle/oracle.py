@@ -9,6 +9,8 @@ this module, and only as the checker / CPU baseline, never as a product path.
   GoWorld gives every Space its own manager (engine/entity/Space.go:33,105).
 * ``closed_form_pairs`` -- the batch relation of SURVEY.md Appendix B
   (oracle/closed_form.c).
+* ``WireHost`` -- the gate / dispatcher sync regroups as a host C loop
+  (oracle/wire_host.c), bench.py's wire_leg comparator.
 
 PARITY UNPINNED: go-aoi (go.mod:29) is absent and the reference holds no AOI
 fixture; see DESIGN.md §Oracle.
@@ -85,6 +87,14 @@ def lib():
         L.cg_init.argtypes = [vp, vp, vp]
         L.cg_init.restype = i64
         L.cg_tick.argtypes = [vp, i64, vp, vp, vp, C.POINTER(i64), C.POINTER(i64)]
+        L.wh_map_new.argtypes = [i64, vp, vp]
+        L.wh_map_new.restype = vp
+        L.wh_map_free.argtypes = [vp]
+        L.wh_gate_from_clients.argtypes = [vp, i64, C.c_uint32, vp, vp, vp]
+        L.wh_gate_from_clients.restype = i64
+        for name in ("wh_dispatcher_to_games", "wh_gate_to_clients"):
+            getattr(L, name).argtypes = [vp, i64, vp, C.c_uint32, vp, vp, vp]
+            getattr(L, name).restype = i64
         _lib = L
     return _lib
 
@@ -393,3 +403,54 @@ def net_events(t, a, b, sp=None):
     for v in state.values():
         assert v in (-1, 0, 1), "unbalanced event stream"
     return ent, lev
+
+
+class WireHost:
+    """Host C restatement of the gate / dispatcher sync regroups (oracle/wire_host.c):
+    the CPU comparator of bench.py's wire_leg.  Tables: entity id -> game, client
+    id -> proxy index.  Each call returns (keys, offsets, records bytes array) like
+    the GPU regroups of include/gwaoi_wire.h."""
+
+    def __init__(self, entity_ids=None, games=None, client_ids=None, client_index=None):
+        self._L = lib()
+        self._g = self._c = None
+        self.max_game = self.max_client = 0
+        if entity_ids is not None:
+            ids = np.ascontiguousarray(entity_ids, np.uint8).reshape(-1)
+            v = np.ascontiguousarray(games, np.uint32)
+            self._g = self._L.wh_map_new(v.size, _p(ids), _p(v))
+            self.max_game = int(v.max()) if v.size else 0
+        if client_ids is not None:
+            ids = np.ascontiguousarray(client_ids, np.uint8).reshape(-1)
+            v = np.ascontiguousarray(client_index, np.uint32)
+            self._c = self._L.wh_map_new(v.size, _p(ids), _p(v))
+            self.max_client = int(v.max()) if v.size else 0
+
+    def __del__(self):
+        for h in (getattr(self, "_g", None), getattr(self, "_c", None)):
+            if h:
+                self._L.wh_map_free(h)
+
+    def _out(self, n, max_key, rec):
+        return (np.empty(max_key + 2, np.uint32), np.empty(max_key + 3, np.uint64), np.empty(max(n, 1) * rec, np.uint8))
+
+    def gate_from_clients(self, rec, n_disp):
+        rec = np.ascontiguousarray(rec, np.uint8).reshape(-1)
+        n = rec.size // 32
+        k, o, out = self._out(n, n_disp, 32)
+        g = self._L.wh_gate_from_clients(_p(rec), n, n_disp, _p(k), _p(o), _p(out))
+        return k[:g], o[:g + 1], out[:int(o[g]) * 32]
+
+    def dispatcher_to_games(self, rec):
+        rec = np.ascontiguousarray(rec, np.uint8).reshape(-1)
+        n = rec.size // 32
+        k, o, out = self._out(n, self.max_game, 32)
+        g = self._L.wh_dispatcher_to_games(_p(rec), n, self._g, self.max_game, _p(k), _p(o), _p(out))
+        return k[:g], o[:g + 1], out[:int(o[g]) * 32]
+
+    def gate_to_clients(self, rec):
+        rec = np.ascontiguousarray(rec, np.uint8).reshape(-1)
+        n = rec.size // 48
+        k, o, out = self._out(n, self.max_client, 32)
+        g = self._L.wh_gate_to_clients(_p(rec), n, self._c, self.max_client, _p(k), _p(o), _p(out))
+        return k[:g], o[:g + 1], out[:int(o[g]) * 32]

@@ -178,3 +178,26 @@ def test_gpu_wire_error_paths():
         w.remove_entities([bytes(16)])
         got, dropped = w.dispatcher_to_games(_rec(_id(1)) * 5)
         assert got == {} and dropped == 5
+
+
+def test_host_c_comparator_matches_restatement():
+    """oracle/wire_host.c (bench.py's wire_leg CPU comparator) == the Python restatement."""
+    from oracle import oracle
+    rng = np.random.default_rng(5)
+    n = 3000
+    ids = rng.integers(0, 256, (400, 16), dtype=np.uint8)
+    rec = np.concatenate([ids[rng.integers(0, 400, n)], rng.integers(0, 256, (n, 16), dtype=np.uint8)], axis=1)
+    games = rng.integers(1, 9, 300).astype(np.uint32)  # the last 100 ids have no game: dropped
+    clients = rng.integers(0, 256, (50, 16), dtype=np.uint8)
+    cidx = rng.permutation(1000)[:40].astype(np.uint32)  # 10 clients not connected
+    rec48 = np.concatenate([clients[rng.integers(0, 50, n)], rec], axis=1)
+    H = oracle.WireHost(ids[:300], games, clients[:40], cidx)
+
+    def as_dict(k, o, out):
+        return {int(key): out[int(o[i]) * 32:int(o[i + 1]) * 32].tobytes() for i, key in enumerate(k)}
+
+    assert as_dict(*H.gate_from_clients(rec, 5)) == W.gate_from_clients(rec.tobytes(), 5)
+    game_of = {bytes(ids[i]): int(games[i]) for i in range(300)}
+    assert as_dict(*H.dispatcher_to_games(rec)) == W.dispatcher_to_games(rec.tobytes(), game_of)
+    connected = {bytes(clients[i]): int(cidx[i]) for i in range(40)}
+    assert as_dict(*H.gate_to_clients(rec48)) == W.gate_to_clients(rec48.tobytes(), connected)
