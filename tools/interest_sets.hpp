@@ -110,6 +110,12 @@ class Range {
     }
     uint32_t lo() const { return lo_; }
     uint32_t hi() const { return hi_; }
+    // prefetch the line where a lookup of k in s's table starts (the replay runs this some
+    // rows ahead: one random line per operation is the whole cost, and it is latency)
+    void prefetch(uint32_t s, uint32_t k) const {
+        const Table &t = t_[s - lo_];
+        if (t.cap) __builtin_prefetch(arena_.data() + t.off + slot_hash(k, t.cap - 1), 1, 1);
+    }
 
   private:
     static uint32_t cap_for(uint32_t n) {
@@ -143,10 +149,24 @@ class Range {
 // flush's events come in pairs (s, b) and (b, s), so row s holds every change
 // of s.InterestedIn and of s.InterestedBy.  Returns the set operations done.
 inline uint64_t replay_rows(Range &in, Range &by, const uint32_t *off, const uint32_t *items, uint32_t enter_bit) {
+    constexpr uint32_t AHEAD = 16;  // items prefetched ahead of the one applied
     uint64_t ops = 0;
+    // the item stream of the range, with its row, runs AHEAD items in front of the replay
+    uint32_t ps = in.lo(), pk = off[in.lo()];
+    const uint32_t kend = off[in.hi()];
+    auto advance = [&]() {
+        if (pk >= kend) return;
+        while (off[ps + 1] <= pk) ++ps;
+        const uint32_t b = items[pk] & ~enter_bit;
+        in.prefetch(ps, b);
+        by.prefetch(ps, b);
+        ++pk;
+    };
+    for (uint32_t q = 0; q < AHEAD; ++q) advance();
     for (uint32_t s = in.lo(); s < in.hi(); ++s) {
         const uint32_t e = off[s + 1];
         for (uint32_t k = off[s]; k < e; ++k) {
+            advance();
             const uint32_t it = items[k], b = it & ~enter_bit;
             if (it & enter_bit) {
                 in.add(s, b);
