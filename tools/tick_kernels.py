@@ -34,9 +34,12 @@ def main():
         for k, v in seen.items():
             per.setdefault(k, []).append(v / 1e3)
     span = statistics.median([(t[-1][2] - t[0][1]) / 1e3 for t in steady])
+    busy = statistics.median([sum(e - s for _, s, e in t) / 1e3 for t in steady])
+    inner = statistics.median([sum(max(0, b[1] - a[2]) for a, b in zip(t, t[1:])) / 1e3 for t in steady])
     gaps = statistics.median([(b[0][1] - a[-1][2]) / 1e3 for a, b in zip(steady, steady[1:])])
     label = sys.argv[2] if len(sys.argv) > 2 else ""
-    print(f"== {label}: {len(steady)} ticks, median span {span:.1f} us, gap to next tick {gaps:.1f} us")
+    print(f"== {label}: {len(steady)} ticks, median span {span:.1f} us (kernels {busy:.1f}, gaps between them "
+          f"{inner:.1f}), gap to next tick {gaps:.1f} us")
     for k, v in per.items():
         print(f"   {k:28s} {statistics.median(v):7.1f}")
 
