@@ -658,6 +658,9 @@ def main():
                     help="register tick t+1's move batch only after tick t's flush returned (default: registered "
                          "while the flush of tick t runs, gwaoi_tick_begin/_end, as a game loop receives moves)")
     ap.add_argument("--cfg4-spaces", type=int, default=8192)
+    ap.add_argument("--no-speculative", action="store_true",
+                    help="overlap mode without gwaoi_tick_end_begin_device: each flush is queued after the commit "
+                         "of the previous one (A/B of the speculative launch)")
     ap.add_argument("--wire-steps", type=int, default=5,
                     help="timed calls per gate/dispatcher regroup in the wire leg (0 = off)")
     ap.add_argument("--wire-records", type=int, default=1_000_000, help="32-B client records per wire regroup call")
@@ -780,15 +783,33 @@ def main():
     moves = 0
     every = max(1, args.time_every)
     overlap = not args.serial_issue
+    spec = overlap and not args.no_speculative
+
+    def timing_for(t):
+        if not args.no_timing:
+            w.set_stage_timing([dom] if (t - args.warmup) % every == 0 else [])
+
     if overlap:  # tick t's batch is registered before the timed loop, like the later ones during a flush
         ps, px, pz = row_ptrs[args.warmup]
         w.moved_batch_device(ps, px, pz, moves_per_tick[args.warmup])
     t0 = time.perf_counter()
+    if spec:
+        timing_for(args.warmup)
+        w.tick_begin()
     for t in range(args.warmup, timed_end):
         a = time.perf_counter()
-        if not args.no_timing:
-            w.set_stage_timing([dom] if (t - args.warmup) % every == 0 else [])
-        if overlap:
+        if spec:
+            # flush t is in flight; tick t+1's batch is registered meanwhile, then one call finishes t and
+            # queues t+1 on the GPU before t's summary is waited for (gwaoi_tick_end_begin_device)
+            if t + 1 < timed_end:
+                ps, px, pz = row_ptrs[t + 1]
+                w.moved_batch_device(ps, px, pz, moves_per_tick[t + 1])
+                timing_for(t + 1)
+                ne, nl = w.tick_end_begin_device()
+            else:
+                ne, nl = w.tick_end_device()
+        elif overlap:
+            timing_for(t)
             # flush t on the GPU; tick t+1's batch is registered (queued for the next flush) meanwhile
             w.tick_begin()
             if t + 1 < timed_end:
@@ -796,6 +817,7 @@ def main():
                 w.moved_batch_device(ps, px, pz, moves_per_tick[t + 1])
             ne, nl = w.tick_end_device()
         else:
+            timing_for(t)
             ne, nl = step(t)
         lat.append(time.perf_counter() - a)
         events += ne + nl
@@ -808,6 +830,7 @@ def main():
 
     timed_stages = w.stage_times() if not args.no_timing else {}
     info = w.info()
+    spec_launches = w.debug_counters()["speculative_launches"]
     # ---- per-stage breakdown: separate ticks, every stage bracketed by HIP events
     stages = {}
     if bd:
@@ -956,6 +979,9 @@ def main():
             "events_per_tick": events / max(args.steps, 1),
             "initial_enter_events": ne0,
             "setup_s": round(setup_s, 2),
+            "tick_loop": ("speculative: gwaoi_tick_end_begin_device queues flush t+1 before flush t's summary "
+                          f"({spec_launches} of {args.steps} timed flushes)" if spec else
+                          "overlap: batch t+1 registered while flush t runs" if overlap else "serial"),
             "roofline": roofline,
             "pcie_inclusive": host_io,
             "sync_leg": sync,

@@ -35,7 +35,7 @@ EXPORTS = [
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
     "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
-    "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device",
+    "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -100,7 +100,7 @@ class WireGroups(C.Structure):
 
 class Debug(C.Structure):
     _fields_ = [("flushes", C.c_uint64), ("combined_replays", C.c_uint64), ("combined_queue_drains", C.c_uint64),
-                ("special_global", C.c_uint64), ("event_regrows", C.c_uint64)]
+                ("special_global", C.c_uint64), ("event_regrows", C.c_uint64), ("speculative_launches", C.c_uint64)]
 
 
 class StageTime(C.Structure):
@@ -150,6 +150,7 @@ def load():
         "gwaoi_events_csr_device": ([vp, P(vp), P(vp), P(u64)], C.c_int),
         "gwaoi_tick_end": ([vp, P(Events)], C.c_int),
         "gwaoi_tick_end_device": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_tick_end_begin_device": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_neighbors": ([vp, u32, vp, sz, P(sz)], C.c_int),
         "gwaoi_world_info": ([vp, P(Info)], C.c_int),
@@ -325,6 +326,21 @@ class World:
     def tick_end_device(self):
         ne, nl = C.c_uint64(), C.c_uint64()
         self._check(self._L.gwaoi_tick_end_device(self._w, C.byref(ne), C.byref(nl)))
+        return ne.value, nl.value
+
+    def tick_end_begin_device(self):
+        """gwaoi_tick_end_begin_device: finish the flush in flight and begin the next one
+        (queued on the GPU before this one's commit when only device Moved batches were
+        queued).  Returns the finished flush's (n_enter, n_leave); its events stay
+        readable through events_device() while the next flush runs."""
+        ne, nl = C.c_uint64(), C.c_uint64()
+        rc = self._L.gwaoi_tick_end_begin_device(self._w, C.byref(ne), C.byref(nl))
+        if rc != 0:
+            try:
+                self._check(rc)
+            except GwaoiError as e:
+                e.counts = (ne.value, nl.value)
+                raise
         return ne.value, nl.value
 
     def _events(self, rc, ev, copy):

@@ -179,6 +179,8 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
 // look-back status words (zeroed once when allocated); tag: fresh per launch.
 size_t incr_sort_tmp_elems(size_t cells);
+// true: the sort's scan zeroes cnt64 as it reads it (zeroed once when allocated)
+bool scan_rezeroes_counts();
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
@@ -222,6 +224,8 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
                   uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                   uint32_t tile_off, uint32_t leave_off, hipStream_t st);
 // The flush's tail in one launch: every tile's events from tmp into tile order
+// (`out` may be host-mapped pinned memory, and hbbox, when given, receives the
+// folded per-space boxes there: the flush summary needs no copy)
 // (offsets by a decoupled look-back; lb: finish_lb_elems(n_entries) status
 // words, tag: a value not used by an earlier launch on the same lb, != 0 mod
 // 2^30), the scalars of TickOut, and the per-space bbox fold (k_gather's parts).
@@ -229,7 +233,7 @@ size_t finish_lb_elems(size_t n_entries);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, hipStream_t st);
+                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,

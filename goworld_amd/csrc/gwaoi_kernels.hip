@@ -871,7 +871,13 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
     }
 }
 
-__global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
+// The counts are zeroed as they are read (GWAOI_SCAN_REZERO): the next flush's
+// k_keygen<true> finds them zero, so the prologue no longer clears 2 words per
+// cell (16 MB of 4-B stores at config 3).
+#ifndef GWAOI_SCAN_REZERO
+#define GWAOI_SCAN_REZERO 1
+#endif
+__global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc) {
     const uint32_t b = blockIdx.x;
@@ -887,6 +893,9 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
     for (int q = 0; q < SC_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
+#if GWAOI_SCAN_REZERO
+        if (base + j < n) in[base + j] = 0ull;
+#endif
     }
     __syncthreads();
     unsigned long long v[SC_I];
@@ -2249,7 +2258,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap,
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
-                                                uint32_t ns) {
+                                                uint32_t ns, int4 *hbbox) {
     const uint32_t b = blockIdx.x, R = gridDim.x - 1;
     if (b == R) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         if (threadIdx.x == 0) {
@@ -2281,6 +2290,17 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         bbox_block(cur, v, bbox, ns, fold);
         __syncthreads();
         if (threadIdx.x == 0 && fold->sp != SP_DEAD) bbox_flush(bbox, ns, fold->sp, fold->v);
+        if (hbbox) {  // the folded boxes straight into the host's summary (read past L1: atomics land in L2)
+            __threadfence();
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
+                const int *q = reinterpret_cast<const int *>(bbox + i);
+                hbbox[i] = make_int4(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+        }
         return;
     }
     __shared__ uint32_t s_off[FT + 1];
@@ -2566,6 +2586,8 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 }
 
 // look-back status words: lo and hi per block
+bool scan_rezeroes_counts() { return GWAOI_SCAN_REZERO != 0; }
+
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, SC_TILE) + 1); }
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
@@ -2666,12 +2688,12 @@ size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, hipStream_t st) {
+                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     k_finish<<<R + 1, 256, 0, st>>>(tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu,
                                     reinterpret_cast<const uint2 *>(tmp_pairs), reinterpret_cast<uint2 *>(out_pairs),
-                                    cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox, n_spaces);
+                                    cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox, n_spaces, hbbox);
 }
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }

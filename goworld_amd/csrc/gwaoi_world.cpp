@@ -30,6 +30,13 @@
 
 using gw::SpaceGrid;
 
+// 1: k_finish writes the flush summary (TickOut + per-space boxes) straight into
+// pinned host memory; 0: it writes device memory and a copy follows (a blit
+// kernel of ~4 us per flush at config 3, profiles/r03_trace_base.txt)
+#ifndef GWAOI_DIRECT_SUMMARY
+#define GWAOI_DIRECT_SUMMARY 1
+#endif
+
 namespace {
 
 enum Stage { ST_APPLY, ST_KEYGEN, ST_SORT, ST_GATHER, ST_CELLS, ST_COMBINED, ST_SPECIAL, ST_FINISH, ST_D2H, ST_N };
@@ -151,6 +158,27 @@ struct DeferredBox {  // Enter/Moved positions of a deferred staged batch, per s
     float x0, z0, x1, z1;
 };
 
+// The buffers one flush writes that the flush after it must leave alone while the
+// first may still be re-run (event buffer regrow) or read by the caller: two
+// sets, alternated per launch, so that flush t+1 can be launched before flush
+// t's summary has reached the host (gwaoi_tick_end_begin_device).
+struct FlushSet {
+    gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
+    gw::SlotSp *sss = nullptr;
+    gw::Rec16 *orec = nullptr;  // previous state in the new frame's order (NaN if absent)
+    uint4 *cand = nullptr;      // combined-pass candidate records of the new frame (x, z, old x, old z; NaN = jumper)
+    gw::TickScalars *sc = nullptr;
+    uint32_t *events = nullptr;  // ev_cap (a,b) pairs: [enters | leaves] in tile order
+    uint64_t ev_cap = 0;         // capacity in directed pairs
+    void *bbox_parts = nullptr;  // bbox level-1 partials
+    char *dev_out = nullptr;     // TickOut + int4 bbox[max_spaces] (device: the bbox fold)
+    char *h_out = nullptr;       // pinned: the flush summary (TickOut + bbox)
+    char *d_hout = nullptr;      // h_out as the device sees it: k_finish writes the summary there
+    hipEvent_t done_ev = nullptr;  // recorded after the flush's last kernel
+    hipEvent_t ev[ST_N][2] = {};   // stage timing
+    bool ev_used[ST_N] = {};
+};
+
 }  // namespace
 
 struct gwaoi_world {
@@ -160,15 +188,15 @@ struct gwaoi_world {
     uint32_t max_slots = 0, max_spaces = 0;
     float cells_per_dist = 1.0f;
 
-    DevFrame fr[2];
-    int cur = 0;  // fr[cur] = frame of the last flush
+    // three frames: the last committed one, the one a flush in flight writes, and (while a
+    // flush launched before the commit of the one in flight runs) the one that flush writes
+    DevFrame fr[3];
+    int cur = 0;  // fr[cur] = frame of the last committed flush
+    FlushSet fs[2];
+    int launch_set = 0;  // set the next launch uses (alternates)
+    int last_set = 0;    // set of the last committed flush (its events)
 
     // working set (max_slots entries each)
-    gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
-    gw::SlotSp *sss = nullptr;
-    const gw::SlotSp *s_ss_view = nullptr;  // this flush's S' spaces: sss, or the previous frame's (virtual S')
-    gw::Rec16 *orec = nullptr;  // previous state in the new frame's order (NaN if absent)
-    uint4 *cand = nullptr;      // combined-pass candidate records of the new frame (x, z, old x, old z; NaN = jumper)
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;
@@ -184,25 +212,21 @@ struct gwaoi_world {
     bool inject_regrow_fail = false;  // GWAOI_INJECT_REGROW_FAIL=1 (tests): the event regrow fails
     // End-of-flush wait: poll an event (default) or block in hipStreamSynchronize
     // (GWAOI_BLOCKING_SYNC=1, A/B check).
-    hipEvent_t done_ev = nullptr;
+    hipEvent_t done_ev = nullptr;  // wait_stream's marker
     bool blocking_sync = false;
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
     unsigned long long *op_seq = nullptr;
     size_t op_cap = 0;
-    uint32_t *events = nullptr;      // ev_cap (a,b) pairs: [enters | leaves] in tile order
-    uint32_t *events_tmp = nullptr;  // ev_cap pairs: per-tile chunks at reserved offsets
-    uint64_t ev_cap = 0;             // capacity in directed pairs
+    uint32_t *events_tmp = nullptr;  // evtmp_cap pairs: per-tile chunks at reserved offsets (shared by the sets)
+    uint64_t evtmp_cap = 0;
     uint32_t *tile_total = nullptr;
     unsigned long long *tile_lb = nullptr;  // k_finish look-back status words
     uint32_t lb_tag = 0;  // look-back launches so far (tags: k_finish, the incremental sort's scan)
     unsigned long long *tile_base = nullptr;
     size_t tile_entries_cap = 0;
-    gw::TickScalars *sc = nullptr;
     float *blk = nullptr;        // keygen per-block partials
-    void *bbox_parts = nullptr;  // bbox level-1 partials
-    char *dev_out = nullptr;     // TickOut + int4 bbox[max_spaces]
     uint32_t *nb_out = nullptr, *nb_count = nullptr;
     size_t nb_cap = 0;
     // per-slot rows of the last flush's events (gwaoi_events_csr), built on request
@@ -213,7 +237,6 @@ struct gwaoi_world {
     uint64_t csr_tick = ~0ull;  // flush the device CSR belongs to
 
     // pinned host mirrors
-    char *h_out = nullptr;  // TickOut + int4 bbox[max_spaces]
     uint32_t *h_events = nullptr;
     uint64_t h_ev_cap = 0;
     SpaceGrid *h_grid = nullptr;
@@ -254,13 +277,18 @@ struct gwaoi_world {
     // arrays, new_slots, touched) stays frozen until the commit: calls made meanwhile are
     // deferred, then queued for the next flush.
     bool in_flight = false;
-    struct {
+    struct Flight {
         uint32_t tick_id;
         size_t entries;
         uint64_t seq_next;  // seq_next when the flush's queue was closed (the next flush's floor)
+        uint64_t seq_base;  // the flush's seq floor (every seq of it is >= seq_base)
         bool dev_seq;       // it held an explicit-seq device batch
+        int set;            // FlushSet it writes
+        int p_idx, n_idx;   // previous / new frame
+        const gw::SlotSp *s_ss_view;  // its S' spaces: the set's sss, or the previous frame's (virtual S')
         std::vector<uint8_t> touched_alive;  // liveness of touched[i] when the queue was closed
     } fl;
+
     std::vector<Deferred> deferred;
     std::vector<DeferredBox> deferred_boxes;
     uint64_t last_n_enter = 0, last_n_leave = 0;
@@ -268,8 +296,6 @@ struct gwaoi_world {
 
     // stage timing: bit s of timing_mask = time stage s with HIP events
     uint32_t timing_mask = 0;
-    hipEvent_t ev[ST_N][2] = {};
-    bool ev_used[ST_N] = {};
     double stage_ms[ST_N] = {};
     uint64_t stage_calls[ST_N] = {};
 
@@ -322,24 +348,24 @@ void dfree(T *&p) {
 
 inline bool finite2(float x, float z) { return std::isfinite(x) && std::isfinite(z); }
 
-void stage_begin(gwaoi_world *w, Stage s) {
+void stage_begin(gwaoi_world *w, FlushSet &S, Stage s) {
     if (!(w->timing_mask >> s & 1u)) return;
-    (void)hipEventRecord(w->ev[s][0], w->stream);
-    w->ev_used[s] = true;
+    (void)hipEventRecord(S.ev[s][0], w->stream);
+    S.ev_used[s] = true;
 }
-void stage_end(gwaoi_world *w, Stage s) {
+void stage_end(gwaoi_world *w, FlushSet &S, Stage s) {
     if (!(w->timing_mask >> s & 1u)) return;
-    (void)hipEventRecord(w->ev[s][1], w->stream);
+    (void)hipEventRecord(S.ev[s][1], w->stream);
 }
-void stage_collect(gwaoi_world *w) {
+void stage_collect(gwaoi_world *w, FlushSet &S) {
     for (int s = 0; s < ST_N; ++s) {
-        if (!w->ev_used[s]) continue;
+        if (!S.ev_used[s]) continue;
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, w->ev[s][0], w->ev[s][1]) == hipSuccess) {
+        if (hipEventElapsedTime(&ms, S.ev[s][0], S.ev[s][1]) == hipSuccess) {
             w->stage_ms[s] += ms;
             w->stage_calls[s] += 1;
         }
-        w->ev_used[s] = false;
+        S.ev_used[s] = false;
     }
 }
 
@@ -370,18 +396,26 @@ int ensure_scan_tmp(gwaoi_world *w, size_t n) {
     return GWAOI_OK;
 }
 
-int ensure_events(gwaoi_world *w, uint64_t pairs) {
-    if (pairs <= w->ev_cap) return GWAOI_OK;
-    uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, w->ev_cap * 2);
+// Room for `pairs` directed events in set S's event buffer and in the shared scratch.  Grows only
+// S's buffer: the other set may hold the events of a committed flush the caller has not read yet.
+int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs) {
+    if (pairs <= S.ev_cap && pairs <= w->evtmp_cap) return GWAOI_OK;
     HIP_TRY(hipStreamSynchronize(w->stream));
-    dfree(w->events);
-    dfree(w->events_tmp);
     int rc;
-    if ((rc = dalloc(w, &w->events, 2 * cap)) || (rc = dalloc(w, &w->events_tmp, 2 * cap))) {
-        w->ev_cap = 0;
-        return rc;
+    if (pairs > S.ev_cap) {
+        const uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, S.ev_cap * 2);
+        dfree(S.events);
+        S.ev_cap = 0;
+        if ((rc = dalloc(w, &S.events, 2 * cap))) return rc;
+        S.ev_cap = cap;
     }
-    w->ev_cap = cap;
+    if (pairs > w->evtmp_cap) {
+        const uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, w->evtmp_cap * 2);
+        dfree(w->events_tmp);
+        w->evtmp_cap = 0;
+        if ((rc = dalloc(w, &w->events_tmp, 2 * cap))) return rc;
+        w->evtmp_cap = cap;
+    }
     return GWAOI_OK;
 }
 
@@ -448,6 +482,7 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
+    HIP_TRY(hipMemsetAsync(w->cnt64, 0, cap * sizeof(unsigned long long), w->stream));  // then kept zero by the scan
     w->cnt64_cap = cap;
     return GWAOI_OK;
 }
@@ -653,9 +688,11 @@ int bitlen(uint32_t v) {
     return b;
 }
 
-gw::TickOut *tick_out(gwaoi_world *w) { return reinterpret_cast<gw::TickOut *>(w->h_out); }
-const int4 *tick_bbox(gwaoi_world *w) { return reinterpret_cast<const int4 *>(w->h_out + sizeof(gw::TickOut)); }
-int4 *dev_bbox(gwaoi_world *w) { return reinterpret_cast<int4 *>(w->dev_out + sizeof(gw::TickOut)); }
+gw::TickOut *tick_out(FlushSet &S) { return reinterpret_cast<gw::TickOut *>(S.h_out); }
+const int4 *tick_bbox(FlushSet &S) { return reinterpret_cast<const int4 *>(S.h_out + sizeof(gw::TickOut)); }
+int4 *dev_bbox(FlushSet &S) { return reinterpret_cast<int4 *>(S.dev_out + sizeof(gw::TickOut)); }
+// the events of the last committed flush
+uint32_t *last_events(gwaoi_world *w) { return w->fs[w->last_set].events; }
 
 // Pair passes + deterministic reorder.  Block-total entries: [enter totals:
 // new-frame blocks | previous-frame blocks] then [leave totals: same order];
@@ -676,26 +713,30 @@ uint32_t next_lb_tag(gwaoi_world *w) {
     return w->lb_tag;
 }
 
-void launch_pair_passes(gwaoi_world *w, DevFrame &Fn, DevFrame &P, uint64_t seq_base) {
+void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
+                        const gw::SlotSp *s_ss_view) {
     hipStream_t st = w->stream;
     const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
+    // the pair passes may emit min(set capacity, scratch capacity) pairs; more is an overflow (re-run)
+    const uint64_t cap = std::min(S.ev_cap, w->evtmp_cap);
     // timed with the launch's own start/end events (no marker packets)
     const bool tc = w->timing_mask >> ST_COMBINED & 1u;
-    if (tc) w->ev_used[ST_COMBINED] = true;
-    gw::launch_combined(Vn, w->cand, w->orec, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
-                        half, st, tc ? w->ev[ST_COMBINED][0] : nullptr, tc ? w->ev[ST_COMBINED][1] : nullptr);
-    stage_begin(w, ST_SPECIAL);
-    gw::launch_pairs(Vp, w->srec, w->s_ss_view, seq_base, w->sc, w->events_tmp, w->ev_cap, w->tile_total, w->tile_base,
-                     TBn, half, st);
-    stage_end(w, ST_SPECIAL);
+    if (tc) S.ev_used[ST_COMBINED] = true;
+    gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, half, st,
+                        tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
+    stage_begin(w, S, ST_SPECIAL);
+    gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn, half,
+                     st);
+    stage_end(w, S, ST_SPECIAL);
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
-    stage_begin(w, ST_FINISH);
-    gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, w->events,
-                      w->ev_cap, w->sc, reinterpret_cast<gw::TickOut *>(w->dev_out), Fn.n, dev_bbox(w),
-                      w->n_space_ids, w->bbox_parts, st);
-    stage_end(w, ST_FINISH);
+    stage_begin(w, S, ST_FINISH);
+    gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, S.events,
+                      cap, S.sc, reinterpret_cast<gw::TickOut *>(GWAOI_DIRECT_SUMMARY ? S.d_hout : S.dev_out), Fn.n,
+                      dev_bbox(S), w->n_space_ids, S.bbox_parts,
+                      GWAOI_DIRECT_SUMMARY ? reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)) : nullptr, st);
+    stage_end(w, S, ST_FINISH);
 }
 
 int poison(gwaoi_world *w, int rc) {
@@ -719,8 +760,12 @@ int tick_launch(gwaoi_world *w) {
     const uint64_t seq_base = w->seq_floor;  // every seq of this flush is >= seq_base > every earlier one
     const uint32_t n_ops = (uint32_t)w->n_ops;
 
-    DevFrame &P = w->fr[w->cur];       // previous flush
-    DevFrame &Fn = w->fr[w->cur ^ 1];  // this flush
+    // the previous flush's frame, and one no flush that may still be re-run reads
+    const int p_idx = w->cur, n_idx = (w->cur + 1) % 3;
+    DevFrame &P = w->fr[p_idx];   // previous flush
+    DevFrame &Fn = w->fr[n_idx];  // this flush
+    const int set = w->launch_set;
+    FlushSet &S = w->fs[set];
     const uint32_t n_prev = P.n;
     const uint32_t n_app = (uint32_t)w->new_slots.size();
     const uint32_t n_total = n_prev + n_app;
@@ -733,6 +778,8 @@ int tick_launch(gwaoi_world *w) {
     const size_t entries = 2 * ((size_t)gw::combined_blocks(n_new) + gw::combined_blocks(n_prev));
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
+    // a set whose twin grew on an overflow grows alike before its next flush (one re-run, not two)
+    if (S.ev_cap < w->fs[set ^ 1].ev_cap && (rc = ensure_events(w, S, w->fs[set ^ 1].ev_cap))) return rc;
     size_t host_ops = 0;
     for (const Run &r : w->runs)
         if (!r.device) host_ops += r.hend - r.hbegin;
@@ -763,7 +810,7 @@ int tick_launch(gwaoi_world *w) {
     // no entry, so S' needs no copy of the previous frame: its spaces ARE the previous frame's,
     // and the records no op wrote are taken from the previous frame by k_keygen (seq check).
     const bool virt = n_app == 0 && host_ops == 0 && (moves_only || n_ops == 0) && !w->force_copy;
-    w->s_ss_view = virt ? P.ss : w->sss;
+    const gw::SlotSp *s_ss_view = virt ? P.ss : S.sss;
     gw::MoveRuns RS{};
     if (moves_only) {
         uint32_t j0 = 0;
@@ -779,24 +826,25 @@ int tick_launch(gwaoi_world *w) {
     const gw::MoveRun *mark = moves_only ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
-        gw::launch_prologue(w->sc, reinterpret_cast<uint32_t *>(w->cnt64), 2 * ((size_t)total_cells + 1), w->tile_total,
-                            entries + 1, dev_bbox(w), w->n_space_ids, n_copy, P.rec, P.ss, w->srec, w->sss, mark,
+        gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
+                            gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
+                            entries + 1, dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
                             w->max_slots, w->sinfo, tick_id, st);
     else
-        gw::launch_prologue(w->sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(w),
-                            w->n_space_ids, n_copy, P.rec, P.ss, w->srec, w->sss, mark, w->max_slots, w->sinfo,
+        gw::launch_prologue(S.sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(S),
+                            w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark, w->max_slots, w->sinfo,
                             tick_id, st);
 
     // ---- apply queued ops onto S'
-    stage_begin(w, ST_APPLY);
+    stage_begin(w, S, ST_APPLY);
     if (n_app) {
         HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
-        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, w->srec, w->sss, w->sinfo, st);
+        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, S.srec, S.sss, w->sinfo, st);
     }
     if (moves_only) {  // the per-tick position sync: one pass + fixup of repeated slots
-        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, w->srec, virt ? nullptr : w->sss,
-                         P.rec, n_prev, w->sc, w->coll, true, st);
+        gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
+                         P.rec, n_prev, S.sc, w->coll, true, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -829,27 +877,27 @@ int tick_launch(gwaoi_world *w) {
                     hoff += k;
                 }
                 if (pass == 0)
-                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->sinfo, tick_id, w->sc, st);
+                    gw::launch_ops_claim(sl, k, j0, w->max_slots, w->sinfo, tick_id, S.sc, st);
                 else
                     gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->sinfo, tick_id, n_total, sq, seq0,
-                                         seq_base, r.device && r.dseq, w->srec, w->sss, w->sc, st);
+                                         seq_base, r.device && r.dseq, S.srec, S.sss, S.sc, st);
                 j0 += k;
             }
         }
     }
-    stage_end(w, ST_APPLY);
+    stage_end(w, S, ST_APPLY);
 
     // ---- keys (+ d_rel, bmax) and stable sort
-    stage_begin(w, ST_KEYGEN);
-    gw::launch_keygen(w->srec, w->s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, w->sc, P.key, incr ? w->cnt64 : nullptr, seq_base, st);
-    stage_end(w, ST_KEYGEN);
-    stage_begin(w, ST_SORT);
+    stage_begin(w, S, ST_KEYGEN);
+    gw::launch_keygen(S.srec, s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
+                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, st);
+    stage_end(w, S, ST_KEYGEN);
+    stage_begin(w, S, ST_SORT);
     int which = 1;
     if (incr) {
         gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             w->keys[1], w->blk, w->sc, next_lb_tag(w), st);
+                             w->keys[1], w->blk, S.sc, next_lb_tag(w), st);
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -860,28 +908,28 @@ int tick_launch(gwaoi_world *w) {
         sb.scan_tmp = w->scan_tmp;
         which = gw::radix_sort(sb, n_total, bitlen(total_cells), st);
     }
-    stage_end(w, ST_SORT);
+    stage_end(w, S, ST_SORT);
     const uint32_t *skeys = w->keys[which];
     const uint32_t *perm = w->vals[which];
 
     // ---- new frame + previous state in the new order
-    stage_begin(w, ST_GATHER);
-    gw::launch_gather(perm, n_new, n_prev, w->srec, w->s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, w->orec, w->cand, Fn.grid,
+    stage_begin(w, S, ST_GATHER);
+    gw::launch_gather(perm, n_new, n_prev, S.srec, s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, S.orec, S.cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
-                      total_cells, n_total, w->sc, Fn.key, dev_bbox(w), w->n_space_ids, w->bbox_parts, st);
-    stage_end(w, ST_GATHER);
+                      total_cells, n_total, S.sc, Fn.key, dev_bbox(S), w->n_space_ids, S.bbox_parts, st);
+    stage_end(w, S, ST_GATHER);
 
     // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
     // the incremental sort has written it already)
     if (!incr) {
-        stage_begin(w, ST_CELLS);
+        stage_begin(w, S, ST_CELLS);
         gw::launch_cell_count(skeys, n_new, Fn.cell_start, st);
         gw::scan_exclusive(Fn.cell_start, Fn.cell_start, (size_t)total_cells + 1, w->scan_tmp, st);
-        stage_end(w, ST_CELLS);
+        stage_end(w, S, ST_CELLS);
     }
 
     // ---- pair passes: combined over the new grid, special entities over the previous one
-    launch_pair_passes(w, Fn, P, seq_base);
+    launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view);
 
     // from here on the device has rewritten SlotInfo for the new frame: any failure before the
     // commit below leaves the world inconsistent (poisoned)
@@ -890,8 +938,8 @@ int tick_launch(gwaoi_world *w) {
         return poison(w, GWAOI_EDEVICE);
     }
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
-    if (hipMemcpyAsync(w->h_out, w->dev_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        (w->done_ev && hipEventRecord(w->done_ev, st) != hipSuccess)) {
+    if ((!GWAOI_DIRECT_SUMMARY && hipMemcpyAsync(S.h_out, S.dev_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipEventRecord(S.done_ev, st) != hipSuccess) {
         w->last_error = "flush summary copy failed";
         return poison(w, GWAOI_EDEVICE);
     }
@@ -900,7 +948,13 @@ int tick_launch(gwaoi_world *w) {
     w->fl.tick_id = tick_id;
     w->fl.entries = entries;
     w->fl.seq_next = w->seq_next;
+    w->fl.seq_base = seq_base;
     w->fl.dev_seq = w->dev_seq_pending;
+    w->fl.set = set;
+    w->fl.p_idx = p_idx;
+    w->fl.n_idx = n_idx;
+    w->fl.s_ss_view = s_ss_view;
+    w->launch_set ^= 1;
     w->fl.touched_alive.resize(w->touched.size());
     for (size_t i = 0; i < w->touched.size(); ++i) w->fl.touched_alive[i] = w->alive[w->touched[i]];
     w->stage_cur ^= 1;  // calls made in flight stage into the other half (free: its flush has ended)
@@ -909,85 +963,25 @@ int tick_launch(gwaoi_world *w) {
     return GWAOI_OK;
 }
 
-// Wait for the flush's summary: blocks on an event (GWAOI_BLOCKING_SYNC=1) or polls it.
-int wait_done(gwaoi_world *w) {
+// Wait for a flush's summary: blocks on its event (GWAOI_BLOCKING_SYNC=1) or polls it.
+int wait_done(gwaoi_world *w, hipEvent_t ev) {
     if (w->blocking_sync) {
-        HIP_TRY(hipEventSynchronize(w->done_ev));
+        HIP_TRY(hipEventSynchronize(ev));
         return GWAOI_OK;
     }
     hipError_t e;
-    while ((e = hipEventQuery(w->done_ev)) == hipErrorNotReady) __builtin_ia32_pause();
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
     HIP_TRY(e);
     return GWAOI_OK;
 }
 
-// The flush, second half: wait for the summary, grow the event buffer and re-run
-// the pair passes if needed, commit the new frame and queue the deferred calls
-// for the next flush.  On return the events are in w->events (device).
-// *committed: the new frame became the world's state (the events are valid and
-// must be delivered, even when the returned status reports a problem the device
-// found in the queued ops).  A failure after the device kernels have rewritten
-// the per-slot records but before the commit poisons the world.
-int tick_finish(gwaoi_world *w, bool *committed) {
-    *committed = false;
-    hipStream_t st = w->stream;
-    int rc;
-    DevFrame &P = w->fr[w->cur];
-    DevFrame &Fn = w->fr[w->cur ^ 1];
-    const uint64_t seq_base = w->seq_floor;
-    const size_t entries = w->fl.entries;
-    if (wait_done(w) != GWAOI_OK) {
-        w->last_error = "flush did not complete: " + w->last_error;
-        return poison(w, GWAOI_EDEVICE);
-    }
+using Flight = decltype(gwaoi_world::fl);
 
-    gw::TickOut r = *tick_out(w);
-    if (r.total64 > 0xFFFFFFFFull) {
-        w->last_error = "more than 2^32-1 events in one flush";
-        return poison(w, GWAOI_ECAPACITY);
-    }
-    if (r.total64 > w->ev_cap) {  // grow and re-run the pair passes
-        stage_collect(w);
-        if (w->inject_regrow_fail) {
-            w->last_error = "event buffer regrow failed (injected)";
-            return poison(w, GWAOI_ENOMEM);
-        }
-        if ((rc = ensure_events(w, r.total64))) return poison(w, rc);
-        gw::launch_zero(w->tile_total, entries + 1, st);
-        gw::launch_zero(reinterpret_cast<uint32_t *>(&w->sc->counter), 2, st);
-        gw::launch_zero(w->sc->dbg, gw::DBG_N, st);
-        launch_pair_passes(w, Fn, P, seq_base);
-        w->dbg.event_regrows++;
-        if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(w->h_out, w->dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            wait_stream(w) != GWAOI_OK) {
-            w->last_error = "pair passes re-run failed: " + w->last_error;
-            return poison(w, GWAOI_EDEVICE);
-        }
-        r = *tick_out(w);
-    }
-    stage_collect(w);
-
-    // ---- commit host bookkeeping
-    w->dbg.flushes++;
-    w->dbg.combined_replays += r.dbg[gw::DBG_COMBINED_REPLAY];
-    w->dbg.combined_queue_drains += r.dbg[gw::DBG_COMBINED_DRAIN];
-    w->dbg.special_global += r.dbg[gw::DBG_SPECIAL_GLOBAL];
-    w->last_n_enter = r.n_enter;
-    w->last_n_leave = (uint64_t)r.n_total - r.n_enter;
-    const int4 *bb = tick_bbox(w);
-    for (uint32_t s = 0; s < w->n_space_ids; ++s) {
-        SpaceHost &S = w->spaces[s];
-        if (S.used && S.alive && bb[s].x != 0x7FFFFFFF) {
-            S.have_bbox = true;
-            S.bx0 = o2f(bb[s].x);
-            S.bz0 = o2f(bb[s].y);
-            S.bx1 = o2f(bb[s].z);
-            S.bz1 = o2f(bb[s].w);
-        } else {
-            S.have_bbox = false;
-        }
-    }
+// The host half of a flush's commit: its op queue becomes the world's state and
+// the calls deferred while it was in flight are queued for the next flush.  r:
+// the flush's summary (needed only after explicit-seq device batches; a
+// speculative launch commits before the summary and never has those).
+void commit_host(gwaoi_world *w, const gw::TickOut *r) {
     for (uint32_t s : w->new_slots) w->appended[s] = 0;
     w->new_slots.clear();
     for (size_t i = 0; i < w->touched.size(); ++i) w->in_frame[w->touched[i]] = w->fl.touched_alive[i];
@@ -999,14 +993,88 @@ int tick_finish(gwaoi_world *w, bool *committed) {
     w->h_op_seq.clear();
     w->runs.clear();
     w->n_ops = 0;
-    if (w->fl.dev_seq && r.seq_max >= w->seq_next) w->seq_next = r.seq_max + 1;  // no call was made in flight
+    if (r && w->fl.dev_seq && r->seq_max >= w->seq_next) w->seq_next = r->seq_max + 1;  // no call was made in flight
     w->dev_seq_pending = false;
     w->seq_floor = w->fl.dev_seq ? w->seq_next : w->fl.seq_next;
-    w->cur ^= 1;
-    w->ticks++;
+    w->cur = w->fl.n_idx;
     w->in_flight = false;
-    *committed = true;
     replay_deferred(w);
+}
+
+// The flush, second half, for flight f: wait for the summary, grow the event
+// buffer and re-run the pair passes if needed, commit.  host_done: the host half
+// was committed ahead (a speculative launch of the next flush followed it; that
+// flush writes the other FlushSet and the third frame, so f's pair-pass inputs
+// are intact for a re-run, which then runs after it on the stream).  On return
+// the events are in the set's buffer (last_events).  *committed: the new frame
+// became the world's state (the events are valid and must be delivered, even
+// when the returned status reports a problem the device found in the queued
+// ops).  A failure after the device kernels have rewritten the per-slot records
+// but before the commit poisons the world.
+int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committed) {
+    *committed = false;
+    hipStream_t st = w->stream;
+    int rc;
+    FlushSet &S = w->fs[f.set];
+    DevFrame &P = w->fr[f.p_idx];
+    DevFrame &Fn = w->fr[f.n_idx];
+    if (wait_done(w, S.done_ev) != GWAOI_OK) {
+        w->last_error = "flush did not complete: " + w->last_error;
+        return poison(w, GWAOI_EDEVICE);
+    }
+
+    gw::TickOut r = *tick_out(S);
+    if (r.total64 > 0xFFFFFFFFull) {
+        w->last_error = "more than 2^32-1 events in one flush";
+        return poison(w, GWAOI_ECAPACITY);
+    }
+    if (r.total64 > std::min(S.ev_cap, w->evtmp_cap)) {  // grow and re-run the pair passes
+        stage_collect(w, S);
+        if (w->inject_regrow_fail) {
+            w->last_error = "event buffer regrow failed (injected)";
+            return poison(w, GWAOI_ENOMEM);
+        }
+        if ((rc = ensure_events(w, S, r.total64))) return poison(w, rc);
+        gw::launch_zero(w->tile_total, f.entries + 1, st);
+        gw::launch_zero(reinterpret_cast<uint32_t *>(&S.sc->counter), 2, st);
+        gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
+        launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view);
+        w->dbg.event_regrows++;
+        if (hipGetLastError() != hipSuccess ||
+            (!GWAOI_DIRECT_SUMMARY &&
+             hipMemcpyAsync(S.h_out, S.dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            wait_stream(w) != GWAOI_OK) {
+            w->last_error = "pair passes re-run failed: " + w->last_error;
+            return poison(w, GWAOI_EDEVICE);
+        }
+        r = *tick_out(S);
+    }
+    stage_collect(w, S);
+
+    // ---- commit
+    w->dbg.flushes++;
+    w->dbg.combined_replays += r.dbg[gw::DBG_COMBINED_REPLAY];
+    w->dbg.combined_queue_drains += r.dbg[gw::DBG_COMBINED_DRAIN];
+    w->dbg.special_global += r.dbg[gw::DBG_SPECIAL_GLOBAL];
+    w->last_n_enter = r.n_enter;
+    w->last_n_leave = (uint64_t)r.n_total - r.n_enter;
+    w->last_set = f.set;
+    const int4 *bb = tick_bbox(S);
+    for (uint32_t s = 0; s < w->n_space_ids; ++s) {
+        SpaceHost &SH = w->spaces[s];
+        if (SH.used && SH.alive && bb[s].x != 0x7FFFFFFF) {
+            SH.have_bbox = true;
+            SH.bx0 = o2f(bb[s].x);
+            SH.bz0 = o2f(bb[s].y);
+            SH.bx1 = o2f(bb[s].z);
+            SH.bz1 = o2f(bb[s].w);
+        } else {
+            SH.have_bbox = false;
+        }
+    }
+    if (!host_done) commit_host(w, &r);
+    w->ticks++;
+    *committed = true;
     // problems the device found in the queued ops: the frame is committed (the offending ops were
     // dropped), so the flush's events are valid and the caller still receives them
     if (r.err & gw::ERR_COUNT_MISMATCH) {
@@ -1026,6 +1094,23 @@ int tick_finish(gwaoi_world *w, bool *committed) {
         return GWAOI_ESTATE;
     }
     return GWAOI_OK;
+}
+
+int tick_finish(gwaoi_world *w, bool *committed) { return finish_flight(w, w->fl, false, committed); }
+
+// Whether the calls queued during the flush in flight allow launching the next
+// flush before the one in flight has committed: device Moved batches only
+// (implicit seqs, the space of every slot unchanged, no host op), and the flush
+// in flight has no explicit-seq batch (its successor's seq floor is then known).
+bool speculative_ok(gwaoi_world *w) {
+    if (!w->in_flight || w->fl.dev_seq || !w->deferred_boxes.empty() || w->deferred.size() > gw::MAX_MOVE_RUNS)
+        return false;
+    size_t n = 0;
+    for (const Deferred &q : w->deferred) {
+        if (q.kind != Deferred::RUN || !q.run.device || q.run.dseq || q.run.dsp) return false;
+        n += q.run.dn;
+    }
+    return n <= w->max_slots;
 }
 
 }  // namespace
@@ -1064,18 +1149,26 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     for (DevFrame &f : w->fr) {
         dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.grid);
     }
-    dfree(w->srec); dfree(w->sss); dfree(w->orec); dfree(w->cand);
+    for (FlushSet &S : w->fs) {
+        dfree(S.srec); dfree(S.sss); dfree(S.orec); dfree(S.cand); dfree(S.sc); dfree(S.events);
+        dfree(S.bbox_parts); dfree(S.dev_out);
+        if (S.h_out) (void)hipHostFree(S.h_out);
+        S.h_out = nullptr;
+        for (int st = 0; st < ST_N; ++st)
+            for (int q = 0; q < 2; ++q)
+                if (S.ev[st][q]) (void)hipEventDestroy(S.ev[st][q]);
+        if (S.done_ev) (void)hipEventDestroy(S.done_ev);
+    }
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events); dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
-    dfree(w->sc); dfree(w->blk); dfree(w->bbox_parts); dfree(w->dev_out);
+    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
+    dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);
     if (w->h_csr_off) (void)hipHostFree(w->h_csr_off);
     if (w->h_csr_items) (void)hipHostFree(w->h_csr_items);
-    if (w->h_out) (void)hipHostFree(w->h_out);
     if (w->h_events) (void)hipHostFree(w->h_events);
     if (w->h_grid) (void)hipHostFree(w->h_grid);
     for (int h = 0; h < 2; ++h) {
@@ -1084,9 +1177,6 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     }
     if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
     if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
-    for (int s = 0; s < ST_N; ++s)
-        for (int q = 0; q < 2; ++q)
-            if (w->ev[s][q]) (void)hipEventDestroy(w->ev[s][q]);
     if (w->done_ev) (void)hipEventDestroy(w->done_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
@@ -1146,31 +1236,41 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         if ((rc = ensure_cells(w, f, 1))) return fail(rc);
     }
     const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * (size_t)w->max_spaces;
-    if ((rc = dalloc(w, &w->srec, N)) || (rc = dalloc(w, &w->sss, N)) || (rc = dalloc(w, &w->orec, N)) || (rc = dalloc(w, &w->cand, N)) ||
-        (rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
+    for (FlushSet &S : w->fs) {
+        if ((rc = dalloc(w, &S.srec, N)) || (rc = dalloc(w, &S.sss, N)) || (rc = dalloc(w, &S.orec, N)) ||
+            (rc = dalloc(w, &S.cand, N)) || (rc = dalloc(w, &S.sc, 1)) ||
+            (rc = dalloc(w, (char **)&S.bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
+            (rc = dalloc(w, &S.dev_out, out_bytes)))
+            return fail(rc);
+        // S' records seq 0 (virtual S': never "written")
+        if (hipMemset(S.srec, 0, N * sizeof(gw::Rec16)) != hipSuccess) return fail(GWAOI_EDEVICE);
+        if (hipHostMalloc((void **)&S.h_out, out_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&S.d_hout, S.h_out, 0) != hipSuccess)
+            return fail(GWAOI_ENOMEM);
+        std::memset(S.h_out, 0, out_bytes);
+        for (int st = 0; st < ST_N; ++st)
+            for (int q = 0; q < 2; ++q)
+                if (hipEventCreate(&S.ev[st][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
+        if (hipEventCreateWithFlags(&S.done_ev, hipEventDisableTiming) != hipSuccess) return fail(GWAOI_EDEVICE);
+    }
+    if ((rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
-        (rc = dalloc(w, &w->coll, N)) ||
-        (rc = dalloc(w, &w->sc, 1)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
-        (rc = dalloc(w, (char **)&w->bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
-        (rc = dalloc(w, &w->dev_out, out_bytes)) || (rc = dalloc(w, &w->nb_count, 1)))
+        (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
+        (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
-    // lastop = 0, rank = sp = 0xFFFFFFFF (not live); S' records seq 0 (virtual S': never "written")
-    if (hipMemset(w->srec, 0, N * sizeof(gw::Rec16)) != hipSuccess ||
-        hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
+    // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
+    if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
         hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_tile_entries(w, 4 * (size_t)gw::combined_blocks((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
-    if ((rc = ensure_events(w, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
-        return fail(rc);
-    if (hipHostMalloc((void **)&w->h_out, out_bytes, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
+    for (FlushSet &S : w->fs)
+        if ((rc = ensure_events(w, S, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
+            return fail(rc);
+    if (hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
         return fail(GWAOI_ENOMEM);
-    for (int s = 0; s < ST_N; ++s)
-        for (int q = 0; q < 2; ++q)
-            if (hipEventCreate(&w->ev[s][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
     if (hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming) != hipSuccess) return fail(GWAOI_EDEVICE);
     if (const char *e = std::getenv("GWAOI_BLOCKING_SYNC")) w->blocking_sync = e[0] == '1';
     w->alive.assign(N, 0);
@@ -1594,7 +1694,7 @@ WorldView world_view(gwaoi_world *w) {
     v.max_slots = w->max_slots;
     v.pending_ops = w->n_ops + w->deferred.size() + (w->in_flight ? 1 : 0);
     v.in_flight = w->in_flight;
-    v.events = w->events;
+    v.events = last_events(w);
     v.n_enter = w->last_n_enter;
     v.n_leave = w->last_n_leave;
     return v;
@@ -1659,6 +1759,35 @@ int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) 
     });
 }
 
+int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
+    bool committed = false;
+    int rc, lrc = GWAOI_OK;
+    if (speculative_ok(w)) {
+        // the next flush goes on the stream first, then the host waits for the one in flight:
+        // no idle gap on the GPU between the two
+        const Flight f = w->fl;
+        commit_host(w, nullptr);
+        lrc = tick_launch(w);
+        if (lrc == GWAOI_OK) w->dbg.speculative_launches++;
+        rc = finish_flight(w, f, true, &committed);
+    } else {
+        rc = tick_finish(w, &committed);
+        if (committed && !w->poisoned) lrc = tick_launch(w);
+    }
+    if (committed) {
+        if (n_enter) *n_enter = w->last_n_enter;
+        if (n_leave) *n_leave = w->last_n_leave;
+    }
+    return rc != GWAOI_OK ? rc : lrc;
+    });
+}
+
 int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
     return gw::api_guard([&]() -> int {
     if (!w || !out) return GWAOI_EINVAL;
@@ -1673,9 +1802,10 @@ int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1));
     if (rc2) return poison(w, rc2);  // the committed events cannot reach the caller
-    stage_begin(w, ST_D2H);
+    FlushSet &S = w->fs[w->last_set];
+    stage_begin(w, S, ST_D2H);
     if (tot) {
-        hipError_t e = hipMemcpyAsync(w->h_events, w->events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        hipError_t e = hipMemcpyAsync(w->h_events, S.events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       w->stream);
         if (e != hipSuccess) {
             w->last_error = std::string("event D2H: ") + hipGetErrorString(e);
@@ -1683,10 +1813,10 @@ int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
         }
         if (int rw = wait_stream(w)) return poison(w, rw);
     }
-    stage_end(w, ST_D2H);
+    stage_end(w, S, ST_D2H);
     if (w->timing_mask) {
         (void)hipStreamSynchronize(w->stream);
-        stage_collect(w);
+        stage_collect(w, S);
     }
     out->n_enter = w->last_n_enter;
     out->n_leave = w->last_n_leave;
@@ -1708,9 +1838,8 @@ int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
-    if (w->in_flight) return GWAOI_ESTATE;
-    if (d_enter) *d_enter = w->events;
-    if (d_leave) *d_leave = w->events + 2 * w->last_n_enter;
+    if (d_enter) *d_enter = last_events(w);
+    if (d_leave) *d_leave = last_events(w) + 2 * w->last_n_enter;
     return GWAOI_OK;
     });
 }
@@ -1745,7 +1874,7 @@ int build_csr(gwaoi_world *w) {
         w->csr_items_cap = cap;
     }
     if (int rc = ensure_scan_tmp(w, rows + 1)) return rc;
-    gw::launch_events_csr(w->events, w->last_n_enter, tot, (uint32_t)rows, w->csr_cnt, w->csr_off, w->scan_tmp,
+    gw::launch_events_csr(last_events(w), w->last_n_enter, tot, (uint32_t)rows, w->csr_cnt, w->csr_off, w->scan_tmp,
                           w->csr_items, w->csr_items + w->csr_items_cap, w->csr_long, w->stream);
     HIP_TRY(hipGetLastError());
     w->csr_tick = w->ticks;
@@ -1896,7 +2025,7 @@ int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
     info->spaces = w->n_spaces_live;
     info->total_cells = w->fr[w->cur].total_cells;
     info->pending_ops = (uint32_t)w->n_ops;
-    info->event_capacity = w->ev_cap;
+    info->event_capacity = std::min(w->fs[w->launch_set].ev_cap, w->evtmp_cap);
     info->max_slots = w->max_slots;
     info->max_spaces = w->max_spaces;
     return GWAOI_OK;

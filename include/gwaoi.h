@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GWAOI_ABI_VERSION 1
+#define GWAOI_ABI_VERSION 2
 
 typedef struct gwaoi_world gwaoi_world;
 
@@ -106,6 +106,8 @@ typedef struct {
     uint64_t combined_queue_drains; /* combined-pass survivor queues drained in the middle of a sweep         */
     uint64_t special_global;        /* special-pass lanes whose events spilled past their LDS slots          */
     uint64_t event_regrows;         /* flushes that grew the device event buffer and re-ran the pair passes  */
+    uint64_t speculative_launches;  /* flushes gwaoi_tick_end_begin_device queued before the commit of the  */
+                                    /* one in flight                                                         */
 } gwaoi_debug;
 
 typedef struct {
@@ -185,7 +187,22 @@ int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
 int gwaoi_tick_begin(gwaoi_world *w);
 int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out);
 int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
-/* Device pointers of the last tick's events (same layout as gwaoi_events). */
+/* The steady game loop's flush: _end_device of the flush in flight, then
+ * _begin of the next one with the calls queued meanwhile -- one call per tick,
+ * the next flush in flight on return.  When those calls are device Moved
+ * batches only (gwaoi_moved_batch_device: implicit seqs, no Enter / Leave /
+ * space change, no host op) and the flush in flight has no explicit-seq batch,
+ * the next flush is queued on the GPU BEFORE this one's summary is waited for,
+ * so the GPU runs the two back to back (its frame, S', candidates and events
+ * live in a second buffer set; an event-buffer overflow of the first is still
+ * re-run exactly).  Otherwise the next flush starts after the commit.  Returns
+ * the finished flush's status and counts; its events stay readable through
+ * gwaoi_events_device until the next commit.  The next flush is in flight on
+ * return whenever the finished one committed. */
+int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
+/* Device pointers of the last committed tick's events (same layout as
+ * gwaoi_events); valid until the next commit, also while a later flush is in
+ * flight (it writes the other event buffer). */
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave);
 
 /* The last tick's events regrouped by entity (built on the GPU on request), for

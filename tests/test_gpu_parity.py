@@ -902,3 +902,65 @@ def test_events_csr_long_rows_gpu():
             assert starts.size > 0
             if flush == 0:
                 w.leave_batch(np.arange(5000, dtype=np.uint32))  # next flush: 5000 rows of 4999 leaves
+
+
+def _device_events(w, ne, nl):
+    """Copy the last committed flush's device events (gwaoi_events_device) to the host."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    e, l = w.events_device()
+    out = []
+    for ptr, n in ((e, ne), (l, nl)):
+        a = np.empty((n, 2), np.uint32)
+        if n:
+            assert hip.hipMemcpy(a.ctypes.data, ptr, a.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+        out.append(a)
+    return out
+
+
+@pytest.mark.parametrize("event_capacity", [0, 3000])
+def test_speculative_next_flush_matches_serial_gpu(event_capacity):
+    """gwaoi_tick_end_begin_device: the next flush queued before the commit of the one in
+    flight (device Moved batches only) gives every flush the events of the serial path --
+    also when the flush in flight overflows its event buffer and is re-run after its
+    successor (event_capacity=3000), and when a host call in flight forces the fallback."""
+    torch = pytest.importorskip("torch")
+    n = 20000
+    wa, wb = make_workload("cfg2", n=n), make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wa.initial()
+    ticks = 8
+    batches = []
+    for t in range(ticks):
+        sl, nx, nz = wa.tick(t)
+        batches.append([torch.from_numpy(a).to("cuda:0") for a in (sl.astype(np.int32), nx, nz)])
+    torch.cuda.synchronize()
+    with World(n, event_capacity=event_capacity) as A, World(n) as B:
+        for w in (A, B):
+            s = w.space_create(wa.D)
+            w.enter_batch(s, slots, x0, z0)
+            w.tick()
+        A.moved_batch_device(*(b.data_ptr() for b in batches[0]), n)
+        A.tick_begin()
+        for t in range(ticks):
+            if t + 1 < ticks:
+                A.moved_batch_device(*(b.data_ptr() for b in batches[t + 1]), n)
+                if t == 4:  # a host call queued in flight: this tick takes the fallback path
+                    A.moved(7, 123.0, 456.0)
+                ne, nl = A.tick_end_begin_device()
+            else:
+                ne, nl = A.tick_end_device()
+            ga, la = _device_events(A, ne, nl)
+            sl, nx, nz = wb.tick(t)
+            B.moved_batch(sl, nx, nz)
+            if t == 5:
+                B.moved(7, 123.0, 456.0)
+            gb, lb = B.tick()
+            np.testing.assert_array_equal(pair_keys(ga), pair_keys(gb), err_msg=f"tick {t}: enters")
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"tick {t}: leaves")
+        d = A.debug_counters()
+        assert d["speculative_launches"] >= ticks - 3
+        if event_capacity:
+            assert d["event_regrows"] > 0
+        for i in range(0, n, 997):
+            np.testing.assert_array_equal(A.neighbors(i), B.neighbors(i))
