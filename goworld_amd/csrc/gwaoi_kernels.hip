@@ -280,6 +280,168 @@ __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, u
     }
 }
 
+// Bucketed form of the same apply (a moves-only flush, every slot < MV_NB_MAX
+// * MV_R).  The ops arrive in the caller's order, which is random against the
+// slot-indexed SlotInfo: the form above pays a random 8-B claim store
+// (prologue), a random SlotInfo line and the record store per op, plus atomics
+// for repeated slots.  Here
+//   k_mv_count    per-block LDS histogram of bucket = slot >> MV_R_LOG, added to
+//                 the bucket totals (one atomic per non-empty bucket and block);
+//   k_mv_scatter  the bucket starts (every block scans the <= MV_NB_MAX totals),
+//                 block ranks by LDS atomics, one atomic per bucket and block for
+//                 the block's run inside the bucket, then {slot, x, z, op index}
+//                 written into the bucket (order inside a bucket is irrelevant);
+//   k_mv_apply    one workgroup per bucket (<= MV_R distinct slots: a bucket is
+//                 big only through repeated slots): the last op of each slot by
+//                 LDS atomicMax on the op index, then the winners apply -- their
+//                 SlotInfo lines are one contiguous 64 KB range of the bucket.
+// No global claim, no fixup; the totals and cursors are re-zeroed by k_mv_apply.
+constexpr uint32_t MV_R_LOG = 12, MV_R = 1u << MV_R_LOG;  // slots per bucket (LDS claim array: 16 KB)
+constexpr int MV_T = 256, MV_PER = 16, MV_OPB = MV_T * MV_PER;  // ops per count/scatter workgroup
+
+struct alignas(16) MvOp {
+    uint32_t slot;
+    float x, z;
+    uint32_t j;  // op index in the flush
+};
+
+__device__ __forceinline__ uint32_t run_of(const MoveRuns &RS, uint32_t j) {
+    uint32_t q = 0;
+    while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
+    return q;
+}
+
+// Slot of op j (SLOT_NONE: no op; >= max_slots: flagged once, by k_mv_count).
+__device__ __forceinline__ uint32_t mv_slot(const MoveRuns &RS, uint32_t j) {
+    const MoveRun &R = RS.r[run_of(RS, j)];
+    return R.ds[j - R.j0];
+}
+
+__global__ __launch_bounds__(MV_T) void k_mv_count(MoveRuns RS, uint32_t n, uint32_t max_slots, uint32_t nb,
+                                                  uint32_t *total, TickScalars *sc) {
+    extern __shared__ uint32_t mv_h[];  // nb
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = 0;
+    __syncthreads();
+    const uint32_t j0 = blockIdx.x * MV_OPB;
+#pragma unroll 4
+    for (int k = 0; k < MV_PER; ++k) {
+        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
+        if (j >= n) break;
+        const uint32_t s = mv_slot(RS, j);
+        if (s == SLOT_NONE) continue;  // placeholder of a skipped decoded record
+        if (s >= max_slots) {
+            atomicOr(&sc->err, ERR_BAD_SLOT);
+            continue;
+        }
+        atomicAdd(&mv_h[s >> MV_R_LOG], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T)
+        if (mv_h[b]) atomicAdd(&total[b], mv_h[b]);
+}
+
+__global__ __launch_bounds__(MV_T) void k_mv_scatter(MoveRuns RS, uint32_t n, uint32_t max_slots, uint32_t nb,
+                                                    const uint32_t *__restrict__ total, uint32_t *cursor,
+                                                    uint32_t *start, MvOp *binned) {
+    extern __shared__ uint32_t mv_h[];  // nb: the block's count per bucket, then its base in the bucket
+    __shared__ uint32_t wsum[MV_T / WAVE];
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = 0;
+    // bucket starts: exclusive scan of the totals, thread t owns buckets [b0, b1)
+    const uint32_t per = (nb + MV_T - 1) / MV_T, b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
+    uint32_t run = 0;
+    for (uint32_t b = b0; b < b1; ++b) run += total[b];
+    uint32_t incl = run;  // inclusive scan of the chunk sums across the block
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, WAVE);
+        if ((int)lane() >= o) incl += v;
+    }
+    const int w = threadIdx.x / WAVE;
+    if (lane() == WAVE - 1) wsum[w] = incl;
+    __syncthreads();
+    uint32_t before = incl - run;  // start of bucket b0
+    for (int q = 0; q < w; ++q) before += wsum[q];
+    // this block's ops: LDS rank inside the bucket
+    const uint32_t j0 = blockIdx.x * MV_OPB;
+    uint32_t bk[MV_PER], rk[MV_PER];
+#pragma unroll
+    for (int k = 0; k < MV_PER; ++k) {
+        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
+        bk[k] = 0xFFFFFFFFu;
+        if (j < n) {
+            const uint32_t s = mv_slot(RS, j);
+            if (s < max_slots) {
+                bk[k] = s >> MV_R_LOG;
+                rk[k] = atomicAdd(&mv_h[bk[k]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = b0; b < b1; ++b) {  // the block's run in each bucket (block 0 publishes the starts)
+        if (mv_h[b]) mv_h[b] = before + atomicAdd(&cursor[b], mv_h[b]);
+        if (blockIdx.x == 0) start[b] = before;
+        before += total[b];
+    }
+    if (blockIdx.x == 0 && b1 == nb && b0 < b1) start[nb] = before;  // every bucketed op
+    if (blockIdx.x == 0 && nb == 0 && threadIdx.x == 0) start[0] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MV_PER; ++k) {
+        if (bk[k] == 0xFFFFFFFFu) continue;
+        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
+        const MoveRun &R = RS.r[run_of(RS, j)];
+        const uint32_t i = j - R.j0;
+        MvOp o;
+        o.slot = R.ds[i];
+        o.x = R.dx[i];
+        o.z = R.dz[i];
+        o.j = j;
+        binned[mv_h[bk[k]] + rk[k]] = o;
+    }
+}
+
+__global__ __launch_bounds__(MV_T) void k_mv_apply(MoveRuns RS, const uint32_t *__restrict__ start, uint32_t *total,
+                                                  uint32_t *cursor, const MvOp *__restrict__ binned,
+                                                  uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
+                                                  SlotSp *s_ss, SlotInfo *info, TickScalars *sc, int track_max) {
+    __shared__ uint32_t claim[MV_R];
+    const uint32_t b = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < MV_R; i += MV_T) claim[i] = 0;
+    const uint32_t s0 = start[b], s1 = start[b + 1];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // consumed: zero for the next flush
+        total[b] = 0;
+        cursor[b] = 0;
+    }
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += MV_T) {
+        const MvOp o = binned[i];
+        atomicMax(&claim[o.slot & (MV_R - 1)], o.j + 1u);
+    }
+    __syncthreads();
+    unsigned long long smax = 0;
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += MV_T) {
+        const MvOp m = binned[i];
+        if (claim[m.slot & (MV_R - 1)] != m.j + 1u) continue;  // a later op of this slot wins
+        const MoveRun &R = RS.r[run_of(RS, m.j)];
+        const uint32_t k = m.j - R.j0;
+        OpIn o;
+        o.slot = m.slot;
+        o.x = m.x;
+        o.z = m.z;
+        o.sp = R.dsp ? R.dsp[k] : SP_KEEP;
+        o.seq = R.dseq ? R.dseq[k] : R.seq0 + k;
+        const unsigned long long q =
+            op_apply_one(o, m.j, slot_info(info, m.slot), info, 0u, n_total, seq_floor, s_rec, s_ss, sc, false);
+        smax = q > smax ? q : smax;
+    }
+    if (track_max) {  // one atomic per wave
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(smax, o, WAVE);
+            smax = v > smax ? v : smax;
+        }
+        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
+    }
+}
+
 // --------------------------------------------------------------- keygen ------
 
 #ifndef GWAOI_CAND_SPLIT
@@ -2552,6 +2714,27 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
                                                                 seq_floor, s_rec, s_ss, sc, coll);
     k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
                                       sc, coll);
+}
+
+uint32_t moves_buckets(uint32_t max_slots) { return cdiv(max_slots, MV_R); }
+
+void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t n_total,
+                           uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *mv_tab,
+                           void *binned, hipStream_t st) {
+    const uint32_t n = RS.count ? RS.r[RS.count - 1].j0 + RS.r[RS.count - 1].n : 0u;
+    const uint32_t nb = moves_buckets(max_slots);
+    uint32_t *total = mv_tab, *cursor = mv_tab + MV_NB_MAX, *start = mv_tab + 2 * MV_NB_MAX;
+    bool track = false;
+    for (uint32_t q = 0; q < RS.count; ++q) track |= RS.r[q].dseq != nullptr;
+    MvOp *bo = reinterpret_cast<MvOp *>(binned);
+    if (n) {
+        const uint32_t g = cdiv(n, MV_OPB);
+        k_mv_count<<<g, MV_T, nb * sizeof(uint32_t), st>>>(RS, n, max_slots, nb, total, sc);
+        k_mv_scatter<<<g, MV_T, nb * sizeof(uint32_t), st>>>(RS, n, max_slots, nb, total, cursor, start,
+                                                                        bo);
+        k_mv_apply<<<nb, MV_T, 0, st>>>(RS, start, total, cursor, bo, n_total, seq_floor, s_rec, s_ss, info, sc,
+                                        track ? 1 : 0);
+    }
 }
 
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info,

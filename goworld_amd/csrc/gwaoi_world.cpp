@@ -206,6 +206,9 @@ struct gwaoi_world {
     unsigned long long *cnt64 = nullptr, *scan64_tmp = nullptr;
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
+    uint32_t *mv_tab = nullptr;  // bucketed apply: totals | cursors | starts (gw::launch_moves_bucketed)
+    uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
+    bool moves_legacy = false;   // GWAOI_MOVES_LEGACY=1: claim + apply + fixup (A/B)
     size_t cnt64_cap = 0;
     bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
     bool force_copy = false;   // GWAOI_FORCE_COPY=1: S' always copied by the prologue (A/B check of virtual S')
@@ -398,12 +401,14 @@ int ensure_scan_tmp(gwaoi_world *w, size_t n) {
 
 // Room for `pairs` directed events in set S's event buffer and in the shared scratch.  Grows only
 // S's buffer: the other set may hold the events of a committed flush the caller has not read yet.
-int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs) {
+// exact: grow to `pairs` and no more (matching the twin set's capacity: with slack, the two sets
+// would outgrow each other on every flush).
+int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs, bool exact = false) {
     if (pairs <= S.ev_cap && pairs <= w->evtmp_cap) return GWAOI_OK;
     HIP_TRY(hipStreamSynchronize(w->stream));
     int rc;
     if (pairs > S.ev_cap) {
-        const uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, S.ev_cap * 2);
+        const uint64_t cap = exact ? pairs : std::max<uint64_t>(pairs + pairs / 4, S.ev_cap * 2);
         dfree(S.events);
         S.ev_cap = 0;
         if ((rc = dalloc(w, &S.events, 2 * cap))) return rc;
@@ -771,6 +776,7 @@ int tick_launch(gwaoi_world *w) {
     const uint32_t n_total = n_prev + n_app;
     const uint32_t n_new = w->n_alive;
 
+    (void)hipGetLastError();  // the launch check below must see this flush's launches only
     // grid for this flush
     uint32_t total_cells = 0, total_rows = 0;
     choose_grids(w, total_cells, total_rows);
@@ -779,7 +785,7 @@ int tick_launch(gwaoi_world *w) {
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
     // a set whose twin grew on an overflow grows alike before its next flush (one re-run, not two)
-    if (S.ev_cap < w->fs[set ^ 1].ev_cap && (rc = ensure_events(w, S, w->fs[set ^ 1].ev_cap))) return rc;
+    if (S.ev_cap < w->fs[set ^ 1].ev_cap && (rc = ensure_events(w, S, w->fs[set ^ 1].ev_cap, true))) return rc;
     size_t host_ops = 0;
     for (const Run &r : w->runs)
         if (!r.device) host_ops += r.hend - r.hbegin;
@@ -823,7 +829,8 @@ int tick_launch(gwaoi_world *w) {
     }
     // counters, tile totals, bbox fold identity; S' <- the previous frame unless virtual; the
     // first Moved run's claims
-    const gw::MoveRun *mark = moves_only ? &RS.r[0] : nullptr;
+    const bool bucketed = moves_only && w->mv_binned && !w->moves_legacy;
+    const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
@@ -842,7 +849,10 @@ int tick_launch(gwaoi_world *w) {
                                hipMemcpyHostToDevice, st));
         gw::launch_init_appended(w->new_slots_d, n_app, n_prev, S.srec, S.sss, w->sinfo, st);
     }
-    if (moves_only) {  // the per-tick position sync: one pass + fixup of repeated slots
+    if (bucketed) {  // the per-tick position sync: ops regrouped by slot bucket, last op per slot in LDS
+        gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
+                                  S.sc, w->mv_tab, w->mv_binned, st);
+    } else if (moves_only) {  // one pass + fixup of repeated slots
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                          P.rec, n_prev, S.sc, w->coll, true, st);
     } else if (n_ops) {
@@ -1035,6 +1045,7 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
             return poison(w, GWAOI_ENOMEM);
         }
         if ((rc = ensure_events(w, S, r.total64))) return poison(w, rc);
+        (void)hipGetLastError();  // a failure of an unrelated earlier call is not this re-run's
         gw::launch_zero(w->tile_total, f.entries + 1, st);
         gw::launch_zero(reinterpret_cast<uint32_t *>(&S.sc->counter), 2, st);
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
@@ -1162,6 +1173,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
+    dfree(w->mv_tab); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
     dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->blk);
@@ -1263,6 +1275,13 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
         hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
+    if (gw::moves_buckets((uint32_t)N) <= gw::MV_NB_MAX) {
+        if ((rc = dalloc(w, &w->mv_tab, 3 * (size_t)gw::MV_NB_MAX + 1)) || (rc = dalloc(w, &w->mv_binned, N)))
+            return fail(rc);
+        if (hipMemset(w->mv_tab, 0, (3 * (size_t)gw::MV_NB_MAX + 1) * sizeof(uint32_t)) != hipSuccess)
+            return fail(GWAOI_EDEVICE);
+    }
+    if (const char *e = std::getenv("GWAOI_MOVES_LEGACY")) w->moves_legacy = e[0] == '1';
     if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_tile_entries(w, 4 * (size_t)gw::combined_blocks((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);

@@ -445,6 +445,68 @@ def test_device_batch_repeated_slots_gpu():
             np.testing.assert_array_equal(wa.neighbors(i), wb.neighbors(i))
 
 
+@pytest.mark.parametrize("legacy", ["0", "1"])
+def test_device_batches_many_buckets_vs_closed_form_gpu(oracle_mod, monkeypatch, legacy):
+    """Moves-only flushes through the bucketed apply (slots regrouped by 4096-slot
+    bucket, last op per slot by LDS claim; GWAOI_MOVES_LEGACY=1: the global-claim
+    apply): live slots scattered over 14 buckets, three device batches per flush
+    with slots repeated inside a batch and across batches, one batch with
+    explicit seqs.  Last call wins (Space.go:259 in call order); events vs the
+    closed form."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("GWAOI_MOVES_LEGACY", legacy)
+    O = oracle_mod
+    rng = np.random.default_rng(77)
+    N = 57000
+    live = np.sort(rng.choice(N, 20000, replace=False)).astype(np.uint32)
+    L = float(np.sqrt(live.size * 1250.0))
+    x = np.zeros(N, np.float32)
+    z = np.zeros(N, np.float32)
+    seq = np.zeros(N, np.uint64)
+    sp = np.full(N, O.DEAD, np.uint32)
+    x[live] = rng.uniform(-L / 2, L / 2, live.size).astype(np.float32)
+    z[live] = rng.uniform(-L / 2, L / 2, live.size).astype(np.float32)
+    with World(N) as w:
+        s = w.space_create(D)
+        w.enter_batch(s, live, x[live], z[live])
+        seq[live] = 1 + np.arange(live.size, dtype=np.uint64)
+        sp[live] = s
+        nxt = live.size + 1
+        w.tick()
+        for t in range(4):
+            before = (x.copy(), z.copy(), seq.copy(), sp.copy())
+            keep = []
+            for r in range(3):
+                k = 9000 if r != 1 else 3000
+                sl = (live[rng.integers(0, live.size, k)] if r != 1 else
+                      live[rng.integers(0, 50, k)]).astype(np.uint32)  # run 1: 50 slots, ~60 moves each
+                nx = (x[sl] + rng.uniform(-40, 40, k)).astype(np.float32)
+                nz = (z[sl] + rng.uniform(-40, 40, k)).astype(np.float32)
+                d = [torch.from_numpy(v).cuda() for v in (sl.astype(np.int32), nx, nz)]
+                if r == 2 and t % 2:  # explicit seqs, above every earlier one
+                    q = nxt + np.arange(k, dtype=np.uint64)
+                    d.append(torch.from_numpy(q.astype(np.int64)).cuda())
+                    torch.cuda.synchronize()
+                    w.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), k, d_seq=d[3].data_ptr())
+                else:
+                    torch.cuda.synchronize()
+                    w.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), k)
+                keep.append(d)
+                u, first_rev = np.unique(sl[::-1], return_index=True)
+                lastpos = k - 1 - first_rev  # each slot's last call in the batch
+                x[u], z[u] = nx[lastpos], nz[lastpos]
+                seq[u] = nxt + lastpos.astype(np.uint64)
+                nxt += k
+            ge, gl = w.tick()
+            want_e, want_l = O.closed_form_diff(before, (x, z, seq, sp), {s: D})
+            assert want_e.size > 1000 and want_l.size > 1000
+            np.testing.assert_array_equal(pair_keys(ge), want_e, err_msg=f"flush {t}: enters")
+            np.testing.assert_array_equal(pair_keys(gl), want_l, err_msg=f"flush {t}: leaves")
+        for i in live[rng.integers(0, live.size, 200)]:
+            np.testing.assert_array_equal(
+                w.neighbors(int(i)), O.closed_form_rows(x, z, seq, sp, {s: D}, np.array([i]))[0])
+
+
 def test_device_batch_errors_reported_gpu():
     torch = pytest.importorskip("torch")
     with World(8) as w:
@@ -929,7 +991,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity):
     n = 20000
     wa, wb = make_workload("cfg2", n=n), make_workload("cfg2", n=n)
     slots, x0, z0, _ = wa.initial()
-    ticks = 8
+    ticks = 24
     batches = []
     for t in range(ticks):
         sl, nx, nz = wa.tick(t)
@@ -942,6 +1004,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity):
             w.tick()
         A.moved_batch_device(*(b.data_ptr() for b in batches[0]), n)
         A.tick_begin()
+        caps = []
         for t in range(ticks):
             if t + 1 < ticks:
                 A.moved_batch_device(*(b.data_ptr() for b in batches[t + 1]), n)
@@ -951,6 +1014,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity):
             else:
                 ne, nl = A.tick_end_device()
             ga, la = _device_events(A, ne, nl)
+            caps.append(A.info()["event_capacity"])
             sl, nx, nz = wb.tick(t)
             B.moved_batch(sl, nx, nz)
             if t == 5:
@@ -960,6 +1024,8 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity):
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"tick {t}: leaves")
         d = A.debug_counters()
         assert d["speculative_launches"] >= ticks - 3
+        # the two event sets match each other's capacity without outgrowing it (was: x1.25 per flush)
+        assert caps[-1] == caps[ticks // 2], caps
         if event_capacity:
             assert d["event_regrows"] > 0
         for i in range(0, n, 997):

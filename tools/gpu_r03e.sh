@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_r03e.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_r03e.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_r03e.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_r03e.log; exit 1; }
 tail -2 gpurun_out/pytest_r03e.log
 B="--no-cpu-baseline --host-io-steps 0 --sync-steps 0 --cfg4-steps 0 --host-tick-steps 0 --wire-steps 0"
 for k in 1 2; do
