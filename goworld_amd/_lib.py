@@ -32,7 +32,7 @@ EXPORTS = [
     "gwaoi_enter", "gwaoi_leave", "gwaoi_moved", "gwaoi_enter_batch", "gwaoi_leave_batch",
     "gwaoi_moved_batch", "gwaoi_moved_batch_device", "gwaoi_tick", "gwaoi_tick_device",
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
-    "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_strerror", "gwaoi_last_error",
+    "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_stream_after", "gwaoi_stream_before", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
     "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
     "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
@@ -160,6 +160,8 @@ def load():
         "gwaoi_set_stage_timing": ([vp, C.c_uint32], C.c_int),
         "gwaoi_sync": ([vp], C.c_int),
         "gwaoi_stream": ([vp], vp),
+        "gwaoi_stream_after": ([vp, vp], C.c_int),
+        "gwaoi_stream_before": ([vp, vp], C.c_int),
         "gwaoi_strerror": ([C.c_int], C.c_char_p),
         "gwaoi_last_error": ([vp], C.c_char_p),
         "gwaoi_abi_version": ([], C.c_int),
@@ -432,6 +434,14 @@ class World:
 
     def stream(self) -> int:
         return self._L.gwaoi_stream(self._w) or 0
+
+    def stream_after(self, other: int):
+        """The world's stream runs what it is given next after everything queued on `other` (a hipStream_t)."""
+        self._check(self._L.gwaoi_stream_after(self._w, C.c_void_p(other)))
+
+    def stream_before(self, other: int):
+        """`other` runs what it is given next after everything queued on the world's stream."""
+        self._check(self._L.gwaoi_stream_before(self._w, C.c_void_p(other)))
 
     # ---- freeze / restore
     def snapshot(self) -> dict:

@@ -155,15 +155,17 @@ struct MoveRuns {
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, bool first_marked, hipStream_t st);
-// The same flush through slot buckets (gwaoi_kernels.hip k_mv_*): usable when
-// moves_buckets(max_slots) <= MV_NB_MAX.  mv_tab: 3 * MV_NB_MAX + 1 uint32
-// (totals, cursors, starts), zeroed when allocated and kept zeroed by the kernels;
-// binned: 16 B per op (<= max_slots ops).
+// The same flush through slot buckets (gwaoi_kernels.hip k_mv_*), for worlds whose
+// SlotInfo outgrows the MALL (max_slots > MV_MIN_SLOTS; moves_buckets(max_slots) <=
+// MV_NB_MAX).  hist: moves_hist_elems(n ops, max_slots) uint32; scan_tmp:
+// scan_tmp_elems of that; binned: 16 B per op (<= max_slots ops).
 constexpr uint32_t MV_NB_MAX = 8192;
+constexpr uint32_t MV_MIN_SLOTS = 1u << 22;
 uint32_t moves_buckets(uint32_t max_slots);
+size_t moves_hist_elems(uint32_t n, uint32_t max_slots);
 void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t n_total,
-                           uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *mv_tab,
-                           void *binned, hipStream_t st);
+                           uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *hist,
+                           uint32_t *scan_tmp, void *binned, hipStream_t st);
 // Zero the per-tick counters and two ranges; bbox entries get the fold
 // identity; S' <- the previous frame's first n_copy entries; and (mark != nullptr)
 // the claims of a moves-only flush's first run.

@@ -280,168 +280,6 @@ __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, u
     }
 }
 
-// Bucketed form of the same apply (a moves-only flush, every slot < MV_NB_MAX
-// * MV_R).  The ops arrive in the caller's order, which is random against the
-// slot-indexed SlotInfo: the form above pays a random 8-B claim store
-// (prologue), a random SlotInfo line and the record store per op, plus atomics
-// for repeated slots.  Here
-//   k_mv_count    per-block LDS histogram of bucket = slot >> MV_R_LOG, added to
-//                 the bucket totals (one atomic per non-empty bucket and block);
-//   k_mv_scatter  the bucket starts (every block scans the <= MV_NB_MAX totals),
-//                 block ranks by LDS atomics, one atomic per bucket and block for
-//                 the block's run inside the bucket, then {slot, x, z, op index}
-//                 written into the bucket (order inside a bucket is irrelevant);
-//   k_mv_apply    one workgroup per bucket (<= MV_R distinct slots: a bucket is
-//                 big only through repeated slots): the last op of each slot by
-//                 LDS atomicMax on the op index, then the winners apply -- their
-//                 SlotInfo lines are one contiguous 64 KB range of the bucket.
-// No global claim, no fixup; the totals and cursors are re-zeroed by k_mv_apply.
-constexpr uint32_t MV_R_LOG = 12, MV_R = 1u << MV_R_LOG;  // slots per bucket (LDS claim array: 16 KB)
-constexpr int MV_T = 256, MV_PER = 16, MV_OPB = MV_T * MV_PER;  // ops per count/scatter workgroup
-
-struct alignas(16) MvOp {
-    uint32_t slot;
-    float x, z;
-    uint32_t j;  // op index in the flush
-};
-
-__device__ __forceinline__ uint32_t run_of(const MoveRuns &RS, uint32_t j) {
-    uint32_t q = 0;
-    while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
-    return q;
-}
-
-// Slot of op j (SLOT_NONE: no op; >= max_slots: flagged once, by k_mv_count).
-__device__ __forceinline__ uint32_t mv_slot(const MoveRuns &RS, uint32_t j) {
-    const MoveRun &R = RS.r[run_of(RS, j)];
-    return R.ds[j - R.j0];
-}
-
-__global__ __launch_bounds__(MV_T) void k_mv_count(MoveRuns RS, uint32_t n, uint32_t max_slots, uint32_t nb,
-                                                  uint32_t *total, TickScalars *sc) {
-    extern __shared__ uint32_t mv_h[];  // nb
-    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = 0;
-    __syncthreads();
-    const uint32_t j0 = blockIdx.x * MV_OPB;
-#pragma unroll 4
-    for (int k = 0; k < MV_PER; ++k) {
-        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
-        if (j >= n) break;
-        const uint32_t s = mv_slot(RS, j);
-        if (s == SLOT_NONE) continue;  // placeholder of a skipped decoded record
-        if (s >= max_slots) {
-            atomicOr(&sc->err, ERR_BAD_SLOT);
-            continue;
-        }
-        atomicAdd(&mv_h[s >> MV_R_LOG], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nb; b += MV_T)
-        if (mv_h[b]) atomicAdd(&total[b], mv_h[b]);
-}
-
-__global__ __launch_bounds__(MV_T) void k_mv_scatter(MoveRuns RS, uint32_t n, uint32_t max_slots, uint32_t nb,
-                                                    const uint32_t *__restrict__ total, uint32_t *cursor,
-                                                    uint32_t *start, MvOp *binned) {
-    extern __shared__ uint32_t mv_h[];  // nb: the block's count per bucket, then its base in the bucket
-    __shared__ uint32_t wsum[MV_T / WAVE];
-    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = 0;
-    // bucket starts: exclusive scan of the totals, thread t owns buckets [b0, b1)
-    const uint32_t per = (nb + MV_T - 1) / MV_T, b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
-    uint32_t run = 0;
-    for (uint32_t b = b0; b < b1; ++b) run += total[b];
-    uint32_t incl = run;  // inclusive scan of the chunk sums across the block
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, WAVE);
-        if ((int)lane() >= o) incl += v;
-    }
-    const int w = threadIdx.x / WAVE;
-    if (lane() == WAVE - 1) wsum[w] = incl;
-    __syncthreads();
-    uint32_t before = incl - run;  // start of bucket b0
-    for (int q = 0; q < w; ++q) before += wsum[q];
-    // this block's ops: LDS rank inside the bucket
-    const uint32_t j0 = blockIdx.x * MV_OPB;
-    uint32_t bk[MV_PER], rk[MV_PER];
-#pragma unroll
-    for (int k = 0; k < MV_PER; ++k) {
-        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
-        bk[k] = 0xFFFFFFFFu;
-        if (j < n) {
-            const uint32_t s = mv_slot(RS, j);
-            if (s < max_slots) {
-                bk[k] = s >> MV_R_LOG;
-                rk[k] = atomicAdd(&mv_h[bk[k]], 1u);
-            }
-        }
-    }
-    __syncthreads();
-    for (uint32_t b = b0; b < b1; ++b) {  // the block's run in each bucket (block 0 publishes the starts)
-        if (mv_h[b]) mv_h[b] = before + atomicAdd(&cursor[b], mv_h[b]);
-        if (blockIdx.x == 0) start[b] = before;
-        before += total[b];
-    }
-    if (blockIdx.x == 0 && b1 == nb && b0 < b1) start[nb] = before;  // every bucketed op
-    if (blockIdx.x == 0 && nb == 0 && threadIdx.x == 0) start[0] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < MV_PER; ++k) {
-        if (bk[k] == 0xFFFFFFFFu) continue;
-        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
-        const MoveRun &R = RS.r[run_of(RS, j)];
-        const uint32_t i = j - R.j0;
-        MvOp o;
-        o.slot = R.ds[i];
-        o.x = R.dx[i];
-        o.z = R.dz[i];
-        o.j = j;
-        binned[mv_h[bk[k]] + rk[k]] = o;
-    }
-}
-
-__global__ __launch_bounds__(MV_T) void k_mv_apply(MoveRuns RS, const uint32_t *__restrict__ start, uint32_t *total,
-                                                  uint32_t *cursor, const MvOp *__restrict__ binned,
-                                                  uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
-                                                  SlotSp *s_ss, SlotInfo *info, TickScalars *sc, int track_max) {
-    __shared__ uint32_t claim[MV_R];
-    const uint32_t b = blockIdx.x;
-    for (uint32_t i = threadIdx.x; i < MV_R; i += MV_T) claim[i] = 0;
-    const uint32_t s0 = start[b], s1 = start[b + 1];
-    __syncthreads();
-    if (threadIdx.x == 0) {  // consumed: zero for the next flush
-        total[b] = 0;
-        cursor[b] = 0;
-    }
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += MV_T) {
-        const MvOp o = binned[i];
-        atomicMax(&claim[o.slot & (MV_R - 1)], o.j + 1u);
-    }
-    __syncthreads();
-    unsigned long long smax = 0;
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += MV_T) {
-        const MvOp m = binned[i];
-        if (claim[m.slot & (MV_R - 1)] != m.j + 1u) continue;  // a later op of this slot wins
-        const MoveRun &R = RS.r[run_of(RS, m.j)];
-        const uint32_t k = m.j - R.j0;
-        OpIn o;
-        o.slot = m.slot;
-        o.x = m.x;
-        o.z = m.z;
-        o.sp = R.dsp ? R.dsp[k] : SP_KEEP;
-        o.seq = R.dseq ? R.dseq[k] : R.seq0 + k;
-        const unsigned long long q =
-            op_apply_one(o, m.j, slot_info(info, m.slot), info, 0u, n_total, seq_floor, s_rec, s_ss, sc, false);
-        smax = q > smax ? q : smax;
-    }
-    if (track_max) {  // one atomic per wave
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long v = __shfl_xor(smax, o, WAVE);
-            smax = v > smax ? v : smax;
-        }
-        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
-    }
-}
-
 // --------------------------------------------------------------- keygen ------
 
 #ifndef GWAOI_CAND_SPLIT
@@ -699,6 +537,150 @@ __global__ __launch_bounds__(SC1_T) void k_scan_single(const uint32_t *in, uint3
         storeN_excl<SC1_I>(out, base, n, v, run);
         carry += tot;
         __syncthreads();
+    }
+}
+
+// ------------------------------------------------------- bucketed apply ------
+// Bucketed form of the moves-only apply (k_moves_*) for large worlds.  The ops
+// arrive in the caller's order, which is random against the slot-indexed
+// SlotInfo: k_moves_* pay a random 8-B claim store (prologue), a random SlotInfo
+// line and the record store per op, plus atomics for repeated slots.  While
+// SlotInfo stays in the 256 MB MALL (1M slots: 16 MB) that is the faster form;
+// at 16M slots (256 MB) every random line comes from HBM and this one wins
+// (cfg5 one strip: 5.9 vs 7.7 ms per tick).
+//   k_mv_count    per-workgroup LDS histogram of bucket = slot >> MV_R_LOG,
+//                 written bucket-major (hist[b * G + g]); an exclusive scan of it
+//                 gives every workgroup its run inside every bucket (no atomics:
+//                 a device-scope atomic on one address serialises memory-side);
+//   k_mv_scatter  LDS ranks, then {slot, x, z, op index} into the bucket runs;
+//   k_mv_apply    one workgroup per bucket (<= MV_R distinct slots: a bucket is
+//                 big only through repeated slots): the last op of each slot by
+//                 LDS atomicMax on the op index, then the winners apply -- their
+//                 SlotInfo lines are one contiguous 64 KB range of the bucket.
+// No global claim, no fixup.
+constexpr uint32_t MV_R_LOG = 12, MV_R = 1u << MV_R_LOG;  // slots per bucket (LDS claim array: 16 KB)
+constexpr int MV_T = 1024;                                 // threads per workgroup (all three kernels)
+
+struct alignas(16) MvOp {
+    uint32_t slot;
+    float x, z;
+    uint32_t j;  // op index in the flush
+};
+
+__device__ __forceinline__ uint32_t run_of(const MoveRuns &RS, uint32_t j) {
+    uint32_t q = 0;
+    while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
+    return q;
+}
+
+// Slot of op j (SLOT_NONE: no op; >= max_slots: flagged once, by k_mv_count).
+__device__ __forceinline__ uint32_t mv_slot(const MoveRuns &RS, uint32_t j) {
+    const MoveRun &R = RS.r[run_of(RS, j)];
+    return R.ds[j - R.j0];
+}
+
+template <int PER>
+__global__ __launch_bounds__(MV_T) void k_mv_count(MoveRuns RS, uint32_t n, uint32_t max_slots, uint32_t nb,
+                                                  uint32_t *hist, TickScalars *sc) {
+    extern __shared__ uint32_t mv_h[];  // nb
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = 0;
+    __syncthreads();
+    const uint32_t j0 = blockIdx.x * (uint32_t)(MV_T * PER);
+    uint32_t s[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {  // every load first
+        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
+        s[k] = j < n ? mv_slot(RS, j) : SLOT_NONE;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (s[k] == SLOT_NONE) continue;  // past the ops, or the placeholder of a skipped decoded record
+        if (s[k] >= max_slots) {
+            atomicOr(&sc->err, ERR_BAD_SLOT);
+            continue;
+        }
+        atomicAdd(&mv_h[s[k] >> MV_R_LOG], 1u);
+    }
+    __syncthreads();
+    const uint32_t G = gridDim.x;
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) hist[(size_t)b * G + blockIdx.x] = mv_h[b];
+    if (blockIdx.x == 0 && threadIdx.x == 0) hist[(size_t)nb * G] = 0;  // -> total after the scan
+}
+
+template <int PER>
+__global__ __launch_bounds__(MV_T) void k_mv_scatter(MoveRuns RS, uint32_t n, uint32_t max_slots, uint32_t nb,
+                                                    const uint32_t *__restrict__ hist, MvOp *binned) {
+    extern __shared__ uint32_t mv_h[];  // nb: ranks, then this workgroup's base in each bucket
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = 0;
+    __syncthreads();
+    const uint32_t j0 = blockIdx.x * (uint32_t)(MV_T * PER);
+    uint32_t bk[PER], rk[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
+        bk[k] = 0xFFFFFFFFu;
+        const uint32_t sl = j < n ? mv_slot(RS, j) : SLOT_NONE;
+        if (sl < max_slots) {
+            bk[k] = sl >> MV_R_LOG;
+            rk[k] = atomicAdd(&mv_h[bk[k]], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t G = gridDim.x;
+    for (uint32_t b = threadIdx.x; b < nb; b += MV_T) mv_h[b] = hist[(size_t)b * G + blockIdx.x];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (bk[k] == 0xFFFFFFFFu) continue;
+        const uint32_t j = j0 + (uint32_t)k * MV_T + threadIdx.x;
+        const MoveRun &R = RS.r[run_of(RS, j)];
+        const uint32_t i = j - R.j0;
+        MvOp o;
+        o.slot = R.ds[i];
+        o.x = R.dx[i];
+        o.z = R.dz[i];
+        o.j = j;
+        binned[mv_h[bk[k]] + rk[k]] = o;
+    }
+}
+
+// hist: the scanned histogram (bucket b starts at hist[b * G], the last one ends at hist[nb * G]).
+__global__ __launch_bounds__(MV_T) void k_mv_apply(MoveRuns RS, const uint32_t *__restrict__ hist, uint32_t G,
+                                                  const MvOp *__restrict__ binned, uint32_t n_total,
+                                                  unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss,
+                                                  SlotInfo *info, TickScalars *sc, int track_max) {
+    __shared__ uint32_t claim[MV_R];
+    const uint32_t b = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < MV_R; i += MV_T) claim[i] = 0;
+    const uint32_t s0 = hist[(size_t)b * G], s1 = hist[(size_t)(b + 1) * G];
+    __syncthreads();
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += MV_T) {
+        const MvOp o = binned[i];
+        atomicMax(&claim[o.slot & (MV_R - 1)], o.j + 1u);
+    }
+    __syncthreads();
+    unsigned long long smax = 0;
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += MV_T) {
+        const MvOp m = binned[i];
+        if (claim[m.slot & (MV_R - 1)] != m.j + 1u) continue;  // a later op of this slot wins
+        const MoveRun &R = RS.r[run_of(RS, m.j)];
+        const uint32_t k = m.j - R.j0;
+        OpIn o;
+        o.slot = m.slot;
+        o.x = m.x;
+        o.z = m.z;
+        o.sp = R.dsp ? R.dsp[k] : SP_KEEP;
+        o.seq = R.dseq ? R.dseq[k] : R.seq0 + k;
+        const unsigned long long q =
+            op_apply_one(o, m.j, slot_info(info, m.slot), info, 0u, n_total, seq_floor, s_rec, s_ss, sc, false);
+        smax = q > smax ? q : smax;
+    }
+    if (track_max) {  // one atomic per wave
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(smax, o, WAVE);
+            smax = v > smax ? v : smax;
+        }
+        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
     }
 }
 
@@ -1694,6 +1676,12 @@ typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
 #ifndef GWAOI_SW_U
 #define GWAOI_SW_U 4  // candidates per lane per sweep iteration on long rows
 #endif
+#ifndef GWAOI_ZLDS
+#define GWAOI_ZLDS 0  // 1: the Z strip's rows staged in LDS per wave (union of the lanes' ranges, coalesced loads)
+#endif
+#ifndef GWAOI_ZCAP
+#define GWAOI_ZCAP 192  // candidates per wave in the Z-strip stage (wider unions take the direct loads)
+#endif
 constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= one sweep iteration + a drain batch)
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
 static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
@@ -1710,6 +1698,9 @@ struct CombinedLds {
     uint32_t qb[CW][QCAP];  // queued pairs of a wave: B frame index
     uint8_t qa[CW][QCAP];   //   ... A frame index - block start
     uint2 ev[CW][EVW];      // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
+#if GWAOI_ZLDS
+    uint4 zl[CW][GWAOI_ZCAP];  // Z strip: the union of a wave's candidate ranges of one grid row
+#endif
     uint32_t wcnt[CW][2];
     unsigned long long base;
     uint32_t te, tl;
@@ -2005,6 +1996,89 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
 }
 
 
+#if GWAOI_ZLDS
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+// sweep_range over a range staged in LDS: lane's candidates zl[off, off + len), frame index base + i.
+template <int U>
+__device__ __forceinline__ void sweep_range_lds(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, const uint4 *zl,
+                                                uint32_t base, uint32_t off, uint32_t len, const FrameView &F,
+                                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
+                                                uint64_t cap, unsigned long long pe, unsigned long long pl,
+                                                bool replay) {
+    for (uint32_t t = 0; __ballot(t < len); t += U) {
+        if (Q.qn > QCAP - U * WAVE) {
+            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);
+            __builtin_amdgcn_wave_barrier();
+            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
+                        cap, pe, pl, replay);
+            Q.qn = 0;
+        }
+        uint4 k[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) k[u] = zl[t + (uint32_t)u < len ? off + t + (uint32_t)u : 0u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t b = base + off + t + (uint32_t)u;
+            const bool keep = band_keep<0>(A, C, k[u], b) & (t + (uint32_t)u < len);
+            qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), b);
+        }
+    }
+}
+
+// The Z strip's rows with the wave's candidate union staged in LDS (coalesced loads, each
+// candidate line read once per wave instead of once per lane that sweeps it).
+__device__ __forceinline__ void sweep_rows_zlds(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int r0,
+                                                int r1, int c0, int c1, const uint4 *__restrict__ cand,
+                                                const FrameView &F, const Rec16 *__restrict__ O_rec,
+                                                const CombinedCtx &C, uint2 *out, uint64_t cap, unsigned long long pe,
+                                                unsigned long long pl, bool replay) {
+    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
+    const uint32_t *cs = F.cell_start;
+    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
+    uint4 *zl = L.zl[w];
+    for (uint32_t k = 0; __ballot(k < nr); ++k) {
+        uint32_t jb = 0, je = 0;
+        if (k < nr) {
+            const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k) * gx;
+            jb = cs[rb];
+            je = cs[rb + span];
+        }
+        const uint32_t len = je - jb;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(wave_min_u32(len ? jb : 0xFFFFFFFFu));
+        const uint32_t hi = __builtin_amdgcn_readfirstlane(wave_max_u32(len ? je : 0u));
+        if (lo >= hi) continue;  // no lane has a candidate in this row
+        if (hi - lo <= (uint32_t)GWAOI_ZCAP) {
+            uint4 v[(GWAOI_ZCAP + WAVE - 1) / WAVE];
+#pragma unroll
+            for (int q = 0; q < (GWAOI_ZCAP + WAVE - 1) / WAVE; ++q) {  // every load first
+                const uint32_t i = (uint32_t)q * WAVE + lane();
+                if (i < hi - lo) v[q] = cand[lo + i];
+            }
+#pragma unroll
+            for (int q = 0; q < (GWAOI_ZCAP + WAVE - 1) / WAVE; ++q) {
+                const uint32_t i = (uint32_t)q * WAVE + lane();
+                if (i < hi - lo) zl[i] = v[q];
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (__ballot(len > 2))
+                sweep_range_lds<GWAOI_SW_U>(L, w, Q, A, zl, lo, jb - lo, len, F, O_rec, C, out, cap, pe, pl, replay);
+            else
+                sweep_range_lds<2>(L, w, Q, A, zl, lo, jb - lo, len, F, O_rec, C, out, cap, pe, pl, replay);
+            __builtin_amdgcn_wave_barrier();  // every lane is done with the stage before the next row's
+        } else if (__ballot(len > 2)) {
+            sweep_range<0, GWAOI_SW_U>(L, w, Q, A, jb, len, 0, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        } else {
+            sweep_range<0, 2>(L, w, Q, A, jb, len, 0, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        }
+    }
+}
+#endif
+
 // Rows r0..r1 (per lane; `on` = the lane takes part), cells c0..c1 of each row.
 // The next row's candidate range is loaded while the current one is swept.
 template <int MODE>
@@ -2165,7 +2239,9 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
 #ifndef GWAOI_EXP_NOZ  // timing experiment only: skip the Z strip (events wrong)
-#if GWAOI_ZB > 0
+#if GWAOI_ZLDS
+        sweep_rows_zlds(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#elif GWAOI_ZB > 0
         sweep_rows_batched<0, GWAOI_ZB, GWAOI_ZH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
                                                   pl, replay);
 #else
@@ -2718,23 +2794,35 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
 
 uint32_t moves_buckets(uint32_t max_slots) { return cdiv(max_slots, MV_R); }
 
-void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t n_total,
-                           uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *mv_tab,
-                           void *binned, hipStream_t st) {
-    const uint32_t n = RS.count ? RS.r[RS.count - 1].j0 + RS.r[RS.count - 1].n : 0u;
+// ops per workgroup of k_mv_count / k_mv_scatter: 4 per thread, 16 once the bucket-major
+// histogram (buckets x workgroups) would pass 2^20 entries
+static int mv_per(uint32_t n, uint32_t nb) {
+    return (size_t)nb * cdiv(std::max(n, 1u), (size_t)MV_T * 4) > (1u << 20) ? 16 : 4;
+}
+
+size_t moves_hist_elems(uint32_t n, uint32_t max_slots) {
     const uint32_t nb = moves_buckets(max_slots);
-    uint32_t *total = mv_tab, *cursor = mv_tab + MV_NB_MAX, *start = mv_tab + 2 * MV_NB_MAX;
+    return (size_t)nb * cdiv(std::max(n, 1u), (size_t)MV_T * mv_per(n, nb)) + 1;
+}
+
+void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t n_total,
+                           uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *hist,
+                           uint32_t *scan_tmp, void *binned, hipStream_t st) {
+    const uint32_t n = RS.count ? RS.r[RS.count - 1].j0 + RS.r[RS.count - 1].n : 0u;
+    if (!n) return;
+    const uint32_t nb = moves_buckets(max_slots);
     bool track = false;
     for (uint32_t q = 0; q < RS.count; ++q) track |= RS.r[q].dseq != nullptr;
     MvOp *bo = reinterpret_cast<MvOp *>(binned);
-    if (n) {
-        const uint32_t g = cdiv(n, MV_OPB);
-        k_mv_count<<<g, MV_T, nb * sizeof(uint32_t), st>>>(RS, n, max_slots, nb, total, sc);
-        k_mv_scatter<<<g, MV_T, nb * sizeof(uint32_t), st>>>(RS, n, max_slots, nb, total, cursor, start,
-                                                                        bo);
-        k_mv_apply<<<nb, MV_T, 0, st>>>(RS, start, total, cursor, bo, n_total, seq_floor, s_rec, s_ss, info, sc,
-                                        track ? 1 : 0);
-    }
+    const int per = mv_per(n, nb);
+    const uint32_t G = cdiv(n, (size_t)MV_T * per);
+    const size_t lds = nb * sizeof(uint32_t);
+    if (per == 4) k_mv_count<4><<<G, MV_T, lds, st>>>(RS, n, max_slots, nb, hist, sc);
+    else k_mv_count<16><<<G, MV_T, lds, st>>>(RS, n, max_slots, nb, hist, sc);
+    scan_exclusive(hist, hist, (size_t)nb * G + 1, scan_tmp, st);
+    if (per == 4) k_mv_scatter<4><<<G, MV_T, lds, st>>>(RS, n, max_slots, nb, hist, bo);
+    else k_mv_scatter<16><<<G, MV_T, lds, st>>>(RS, n, max_slots, nb, hist, bo);
+    k_mv_apply<<<nb, MV_T, 0, st>>>(RS, hist, G, bo, n_total, seq_floor, s_rec, s_ss, info, sc, track ? 1 : 0);
 }
 
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info,

@@ -202,6 +202,7 @@ __global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__
                                              uint32_t *counts, const uint32_t *__restrict__ offs, uint32_t nb,
                                              uint32_t *err, uint32_t *m_slot, float *m_x, float *m_z,
                                              unsigned long long *m_seq, gwaoi_halo_rec *el) {
+    if (phase == 1 && *err) return;  // phase 0 found a bad record: the tick fails with the state untouched
     const uint32_t i = blockIdx.x * BT + threadIdx.x;
     unsigned long long m = 0;
     gwaoi_halo_rec r{};
@@ -264,8 +265,8 @@ __global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restric
                                                const Rec16 *__restrict__ cur, const Rec16 *__restrict__ prv,
                                                const uint32_t *__restrict__ ptick, const uint32_t *__restrict__ ttick,
                                                uint32_t tick, StripGeo g, uint32_t *counts,
-                                               const uint32_t *__restrict__ offs, uint32_t nb, uint32_t leave_gap,
-                                               uint2 *out) {
+                                               const uint32_t *__restrict__ offs, uint32_t nb,
+                                               const unsigned long long *__restrict__ tcnt, uint2 *out) {
     const uint32_t i = blockIdx.x * BT + threadIdx.x;
     unsigned long long m = 0;
     uint2 p = make_uint2(0, 0);
@@ -279,6 +280,7 @@ __global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restric
         }
     }
     if (phase == 0 && i == 0) counts[2 * nb] = 0;
+    const uint32_t leave_gap = phase == 1 && tcnt ? (uint32_t)tcnt[0] : 0u;  // teleporter enters go between
     multisplit(phase, m, false, 0xFFFFFFFFu, 2, counts, offs, nb,
                [&](uint32_t q, uint32_t pos) { out[pos + (q ? leave_gap : 0u)] = p; });
 }
@@ -286,7 +288,7 @@ __global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restric
 // ---- teleporter x teleporter: phase 0 counts, phase 1 writes (atomic slots;
 // the pairs are few and their order is not part of the contract).
 __global__ void k_tele_pairs(int phase, const gwaoi_tele_rec *__restrict__ t, uint32_t n, StripGeo g,
-                             unsigned long long *cnt, uint2 *ent, uint2 *lev) {
+                             unsigned long long *cnt, uint2 *ent, uint2 *lev, unsigned long long cap) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const gwaoi_tele_rec A = t[i];
@@ -306,17 +308,49 @@ __global__ void k_tele_pairs(int phase, const gwaoi_tele_rec *__restrict__ t, ui
         const bool was = (A.flags & 1u) && (B.flags & 1u) && rel(ap, bp, g.D);
         const bool is = (A.flags & 2u) && (B.flags & 2u) && rel(an, bn, g.D);
         if (own_now && is && !was) {
-            if (phase == 1) ent[atomicAdd(&cnt[0], 1ull)] = make_uint2(A.slot, B.slot);
+            if (phase == 1) {
+                const unsigned long long k = atomicAdd(&cnt[0], 1ull);
+                if (k < cap) ent[k] = make_uint2(A.slot, B.slot);
+            }
             else ++ce;
         }
         if (own_before && was && !is) {
-            if (phase == 1) lev[atomicAdd(&cnt[1], 1ull)] = make_uint2(A.slot, B.slot);
+            if (phase == 1) {
+                const unsigned long long k = atomicAdd(&cnt[1], 1ull);
+                if (k < cap) lev[k] = make_uint2(A.slot, B.slot);
+            }
             else ++cl;
         }
     }
     if (phase == 0) {
         if (ce) atomicAdd(&cnt[0], (unsigned long long)ce);
         if (cl) atomicAdd(&cnt[1], (unsigned long long)cl);
+    }
+}
+
+// The teleporter pairs next to the filtered events, all offsets read on the device:
+// out = [filter enters (fe) | tele enters (te) | filter leaves (fl) | tele leaves (tl)],
+// fe = offs[nb], fe + fl = offs[2 nb] (the filter's scanned counts).
+__global__ void k_tele_place(const uint32_t *__restrict__ offs, uint32_t nb, const unsigned long long *__restrict__ tcnt,
+                             const uint2 *__restrict__ tent, const uint2 *__restrict__ tlev, uint2 *out) {
+    const uint32_t fe = offs[nb], fl = offs[2 * nb] - fe;
+    const uint32_t te = (uint32_t)tcnt[0], tl = (uint32_t)tcnt[1];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < max(te, tl); i += gridDim.x * blockDim.x) {
+        if (i < te) out[fe + i] = tent[i];
+        if (i < tl) out[fe + te + fl + i] = tlev[i];
+    }
+}
+
+// The tick's result for the host: small[0] = filter enters, [1] = filter leaves,
+// [2] = tele enters, [3] = tele leaves, [4] = err.
+__global__ void k_tick_totals(const uint32_t *__restrict__ offs, uint32_t nb, const unsigned long long *__restrict__ tcnt,
+                              const uint32_t *__restrict__ err, uint32_t *small) {
+    if (threadIdx.x == 0) {
+        small[0] = offs[nb];
+        small[1] = offs[2 * nb] - offs[nb];
+        small[2] = (uint32_t)tcnt[0];
+        small[3] = (uint32_t)tcnt[1];
+        small[4] = *err;
     }
 }
 
@@ -328,6 +362,9 @@ __global__ void k_totals(const uint32_t *offs, uint32_t K, uint32_t nb, const ui
 }
 
 inline uint32_t cdivu(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
+
+constexpr size_t EL_PREFETCH = 1u << 16;          // enter/leave records copied with the recv counts
+constexpr uint64_t TELE_PAIRS_MAX = 1ull << 22;  // bound n (n-1) per kind sized without a count (n_tele <= 2048)
 
 }  // namespace
 
@@ -557,8 +594,7 @@ int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_te
     s->routed = false;
     k_route<<<s->r_nb, BT, 0, s->st>>>(1, s->r_ops, s->r_n, s->cur, s->geo, s->counts, s->counts, s->r_nb, s->err,
                                        d_send, d_tele);
-    S_TRY(hipGetLastError());
-    S_TRY(hipStreamSynchronize(s->st));
+    S_TRY(hipGetLastError());  // complete in stream order on the world's stream (gwaoi_stream): no host wait
     return GWAOI_OK;
     });
 }
@@ -576,31 +612,39 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_l
     s->n_enter = s->n_leave = 0;
     const uint32_t tick = ++s->tick;
     hipStream_t st = s->st;
-    // ---- received records -> world ops + state
+    // ---- received records -> world ops + state.  Both multisplit phases run back to back into
+    // buffers sized for every record; ONE host wait brings the counts and (up to EL_PREFETCH of)
+    // the enter/leave records the host-side Enter/Leave calls need.
     const uint32_t nb = std::max(1u, cdivu(n_all, BT));
     if (int rc = ensure_split(s, 3, nb)) return rc;
     if (int rc = ensure_moves(s, n_all)) return rc;
+    if (int rc = grow(s, &s->el_d, s->el_cap, n_all + 1)) return rc;
     S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
-    k_recv<<<nb, BT, 0, st>>>(0, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
-                              nullptr, nb, s->err, nullptr, nullptr, nullptr, nullptr, nullptr);
-    if (int rc = split_totals(s, 3, nb)) return rc;
+    k_recv<<<nb, BT, 0, st>>>(0, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick,
+                              s->max_slots, s->counts, nullptr, nb, s->err, nullptr, nullptr, nullptr, nullptr, nullptr);
+    gw::scan_exclusive(s->counts, s->counts, (size_t)3 * nb + 1, s->scan_tmp, st);
+    k_recv<<<nb, BT, 0, st>>>(1, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick,
+                              s->max_slots, s->counts, s->counts, nb, s->err, s->m_slot, s->m_x, s->m_z, s->m_seq,
+                              s->el_d);
+    k_totals<<<1, 128, 0, st>>>(s->counts, 3, nb, s->err, s->small_d);
+    if (n_tele) k_tele_mark<<<cdivu(n_tele, 256), 256, 0, st>>>(d_tele, (uint32_t)n_tele, s->ttick, tick, s->max_slots);
+    S_TRY(hipGetLastError());
+    const size_t pre = std::min<size_t>(n_all, EL_PREFETCH);
+    if (s->el_h.size() < EL_PREFETCH) s->el_h.resize(EL_PREFETCH);
+    S_TRY(hipMemcpyAsync(s->small_h, s->small_d, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (pre) S_TRY(hipMemcpyAsync(s->el_h.data(), s->el_d, pre * sizeof(gwaoi_halo_rec), hipMemcpyDeviceToHost, st));
+    S_TRY(hipStreamSynchronize(st));
     if (int rc = strip_err(s, s->small_h[4], "recv")) return rc;
     const uint32_t n_move = s->small_h[1] - s->small_h[0];
     const uint32_t n_ent = s->small_h[2] - s->small_h[1];
     const uint32_t n_lev = s->small_h[3] - s->small_h[2];
-    if (int rc = grow(s, &s->el_d, s->el_cap, (size_t)n_ent + n_lev + 1)) return rc;
-    k_recv<<<nb, BT, 0, st>>>(1, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick, s->max_slots, s->counts,
-                              s->counts, nb, s->err, s->m_slot, s->m_x, s->m_z, s->m_seq, s->el_d);
-    S_TRY(hipGetLastError());
-    s->el_h.resize((size_t)n_ent + n_lev);
-    if (n_ent + n_lev)
-        S_TRY(hipMemcpyAsync(s->el_h.data(), s->el_d, ((size_t)n_ent + n_lev) * sizeof(gwaoi_halo_rec),
+    const size_t n_el = (size_t)n_ent + n_lev;
+    if (n_el > pre) {  // more boundary crossings than the prefetch: one more copy
+        s->el_h.resize(n_el);
+        S_TRY(hipMemcpyAsync(s->el_h.data() + pre, s->el_d + pre, (n_el - pre) * sizeof(gwaoi_halo_rec),
                              hipMemcpyDeviceToHost, st));
-    if (n_tele) {
-        k_tele_mark<<<cdivu(n_tele, 256), 256, 0, st>>>(d_tele, (uint32_t)n_tele, s->ttick, tick, s->max_slots);
-        S_TRY(hipGetLastError());
+        S_TRY(hipStreamSynchronize(st));
     }
-    S_TRY(hipStreamSynchronize(st));
     // leaves (no seq), then enters in seq order, then the device moves
     for (uint32_t k = 0; k < n_lev; ++k)
         if (int rc = gwaoi_leave(s->w, s->el_h[n_ent + k].slot)) {
@@ -628,40 +672,41 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_l
     }
     const uint32_t *wev = nullptr;
     if (int rc = gwaoi_events_device(s->w, &wev, nullptr)) return rc;
-    // ---- teleporter pairs (counted first so the output can be laid out)
-    uint64_t te = 0, tl = 0;
-    if (n_tele > 1) {
-        S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
+    // ---- teleporter pairs: one pass into buffers that hold every possible pair (n (n-1) per kind)
+    S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
+    uint64_t tcap = n_tele > 1 ? (uint64_t)n_tele * (n_tele - 1) : 0;
+    if (tcap > TELE_PAIRS_MAX) {  // a teleport storm: count first (one more host wait), then size exactly
         k_tele_pairs<<<cdivu(n_tele, 256), 256, 0, st>>>(0, d_tele, (uint32_t)n_tele, s->geo, s->tcnt, nullptr,
-                                                         nullptr);
+                                                         nullptr, 0);
         unsigned long long hc[2];
         S_TRY(hipMemcpyAsync(hc, s->tcnt, sizeof(hc), hipMemcpyDeviceToHost, st));
         S_TRY(hipStreamSynchronize(st));
-        te = hc[0];
-        tl = hc[1];
-        if (int rc = grow(s, &s->tpairs, s->tpairs_cap, te + tl + 1)) return rc;
+        tcap = std::max<uint64_t>(std::max(hc[0], hc[1]), 1);
         S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
-        k_tele_pairs<<<cdivu(n_tele, 256), 256, 0, st>>>(1, d_tele, (uint32_t)n_tele, s->geo, s->tcnt, s->tpairs,
-                                                         s->tpairs + te);
-        S_TRY(hipGetLastError());
     }
-    // ---- filter the world's events to this strip's
+    if (int rc = grow(s, &s->tpairs, s->tpairs_cap, 2 * tcap + 1)) return rc;
+    if (n_tele > 1)
+        k_tele_pairs<<<cdivu(n_tele, 256), 256, 0, st>>>(1, d_tele, (uint32_t)n_tele, s->geo, s->tcnt, s->tpairs,
+                                                         s->tpairs + tcap, tcap);
+    // ---- filter the world's events to this strip's: [filter enters | tele enters | filter leaves | tele leaves]
     const uint64_t nev = wne + wnl;
     if (nev > 0x7FFFFFFFull) return GWAOI_ECAPACITY;
     const uint32_t fb = std::max(1u, cdivu(nev, BT));
     if (int rc = ensure_split(s, 2, fb)) return rc;
+    if (int rc = grow(s, &s->out, s->out_cap, nev + 2 * tcap + 1)) return rc;
     k_filter<<<fb, BT, 0, st>>>(0, reinterpret_cast<const uint2 *>(wev), (uint32_t)wne, (uint32_t)wnl, s->cur, s->prv,
-                                s->ptick, s->ttick, tick, s->geo, s->counts, nullptr, fb, 0, nullptr);
-    if (int rc = split_totals(s, 2, fb)) return rc;
-    const uint64_t fe = s->small_h[1] - s->small_h[0], fl = s->small_h[2] - s->small_h[1];
-    const uint64_t tot = fe + te + fl + tl;
-    if (int rc = grow(s, &s->out, s->out_cap, tot + 1)) return rc;
+                                s->ptick, s->ttick, tick, s->geo, s->counts, nullptr, fb, nullptr, nullptr);
+    gw::scan_exclusive(s->counts, s->counts, (size_t)2 * fb + 1, s->scan_tmp, st);
     k_filter<<<fb, BT, 0, st>>>(1, reinterpret_cast<const uint2 *>(wev), (uint32_t)wne, (uint32_t)wnl, s->cur, s->prv,
-                                s->ptick, s->ttick, tick, s->geo, s->counts, s->counts, fb, (uint32_t)te, s->out);
+                                s->ptick, s->ttick, tick, s->geo, s->counts, s->counts, fb, s->tcnt, s->out);
+    if (tcap)
+        k_tele_place<<<std::min<uint32_t>(cdivu(tcap, 256), 1024), 256, 0, st>>>(s->counts, fb, s->tcnt, s->tpairs,
+                                                                                 s->tpairs + tcap, s->out);
+    k_tick_totals<<<1, 64, 0, st>>>(s->counts, fb, s->tcnt, s->err, s->small_d);
     S_TRY(hipGetLastError());
-    if (te) S_TRY(hipMemcpyAsync(s->out + fe, s->tpairs, te * sizeof(uint2), hipMemcpyDeviceToDevice, st));
-    if (tl) S_TRY(hipMemcpyAsync(s->out + fe + te + fl, s->tpairs + te, tl * sizeof(uint2), hipMemcpyDeviceToDevice, st));
+    S_TRY(hipMemcpyAsync(s->small_h, s->small_d, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     S_TRY(hipStreamSynchronize(st));
+    const uint64_t fe = s->small_h[0], fl = s->small_h[1], te = s->small_h[2], tl = s->small_h[3];
     s->n_enter = fe + te;
     s->n_leave = fl + tl;
     if (n_enter) *n_enter = s->n_enter;

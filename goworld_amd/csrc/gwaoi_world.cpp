@@ -206,9 +206,9 @@ struct gwaoi_world {
     unsigned long long *cnt64 = nullptr, *scan64_tmp = nullptr;
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
-    uint32_t *mv_tab = nullptr;  // bucketed apply: totals | cursors | starts (gw::launch_moves_bucketed)
+    uint32_t *mv_hist = nullptr;  // bucketed apply: the bucket-major histogram, scanned (gw::launch_moves_bucketed)
     uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
-    bool moves_legacy = false;   // GWAOI_MOVES_LEGACY=1: claim + apply + fixup (A/B)
+    bool moves_bucketed = false;   // the bucketed apply (max_slots > MV_MIN_SLOTS; GWAOI_MOVES_BUCKETED forces it)
     size_t cnt64_cap = 0;
     bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
     bool force_copy = false;   // GWAOI_FORCE_COPY=1: S' always copied by the prologue (A/B check of virtual S')
@@ -216,6 +216,7 @@ struct gwaoi_world {
     // End-of-flush wait: poll an event (default) or block in hipStreamSynchronize
     // (GWAOI_BLOCKING_SYNC=1, A/B check).
     hipEvent_t done_ev = nullptr;  // wait_stream's marker
+    hipEvent_t order_ev = nullptr;  // gwaoi_stream_after / _before
     bool blocking_sync = false;
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
@@ -829,7 +830,7 @@ int tick_launch(gwaoi_world *w) {
     }
     // counters, tile totals, bbox fold identity; S' <- the previous frame unless virtual; the
     // first Moved run's claims
-    const bool bucketed = moves_only && w->mv_binned && !w->moves_legacy;
+    const bool bucketed = moves_only && w->mv_binned;
     const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
@@ -851,7 +852,7 @@ int tick_launch(gwaoi_world *w) {
     }
     if (bucketed) {  // the per-tick position sync: ops regrouped by slot bucket, last op per slot in LDS
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
-                                  S.sc, w->mv_tab, w->mv_binned, st);
+                                  S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
     } else if (moves_only) {  // one pass + fixup of repeated slots
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                          P.rec, n_prev, S.sc, w->coll, true, st);
@@ -1173,7 +1174,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
-    dfree(w->mv_tab); dfree(w->mv_binned);
+    dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
     dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->blk);
@@ -1190,6 +1191,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
     if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
     if (w->done_ev) (void)hipEventDestroy(w->done_ev);
+    if (w->order_ev) (void)hipEventDestroy(w->order_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return GWAOI_OK;
@@ -1275,14 +1277,16 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
         hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
-    if (gw::moves_buckets((uint32_t)N) <= gw::MV_NB_MAX) {
-        if ((rc = dalloc(w, &w->mv_tab, 3 * (size_t)gw::MV_NB_MAX + 1)) || (rc = dalloc(w, &w->mv_binned, N)))
-            return fail(rc);
-        if (hipMemset(w->mv_tab, 0, (3 * (size_t)gw::MV_NB_MAX + 1) * sizeof(uint32_t)) != hipSuccess)
-            return fail(GWAOI_EDEVICE);
+    // the bucketed apply for worlds whose SlotInfo outgrows the MALL (GWAOI_MOVES_BUCKETED=0/1 forces it)
+    w->moves_bucketed = N > gw::MV_MIN_SLOTS;
+    if (const char *e = std::getenv("GWAOI_MOVES_BUCKETED")) w->moves_bucketed = e[0] == '1';
+    size_t mv_hist_n = 0;
+    if (w->moves_bucketed && gw::moves_buckets((uint32_t)N) <= gw::MV_NB_MAX) {
+        mv_hist_n = std::max(gw::moves_hist_elems((uint32_t)N, (uint32_t)N),
+                             ((size_t)1 << 20) + 2 * (size_t)gw::moves_buckets((uint32_t)N) + 2);
+        if ((rc = dalloc(w, &w->mv_hist, mv_hist_n)) || (rc = dalloc(w, &w->mv_binned, N))) return fail(rc);
     }
-    if (const char *e = std::getenv("GWAOI_MOVES_LEGACY")) w->moves_legacy = e[0] == '1';
-    if ((rc = ensure_scan_tmp(w, gw::radix_hist_elems((uint32_t)N)))) return fail(rc);
+    if ((rc = ensure_scan_tmp(w, std::max(gw::radix_hist_elems((uint32_t)N), mv_hist_n)))) return fail(rc);
     if ((rc = ensure_tile_entries(w, 4 * (size_t)gw::combined_blocks((uint32_t)N)))) return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     for (FlushSet &S : w->fs)
@@ -1290,7 +1294,9 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
             return fail(rc);
     if (hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
         return fail(GWAOI_ENOMEM);
-    if (hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming) != hipSuccess) return fail(GWAOI_EDEVICE);
+    if (hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->order_ev, hipEventDisableTiming) != hipSuccess)
+        return fail(GWAOI_EDEVICE);
     if (const char *e = std::getenv("GWAOI_BLOCKING_SYNC")) w->blocking_sync = e[0] == '1';
     w->alive.assign(N, 0);
     w->in_frame.assign(N, 0);
@@ -2101,5 +2107,23 @@ int gwaoi_sync(gwaoi_world *w) {
 }
 
 void *gwaoi_stream(gwaoi_world *w) { return w ? (void *)w->stream : nullptr; }
+
+int gwaoi_stream_after(gwaoi_world *w, void *other) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    HIP_TRY(hipEventRecord(w->order_ev, (hipStream_t)other));
+    HIP_TRY(hipStreamWaitEvent(w->stream, w->order_ev, 0));
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_stream_before(gwaoi_world *w, void *other) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    HIP_TRY(hipEventRecord(w->order_ev, w->stream));
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)other, w->order_ev, 0));
+    return GWAOI_OK;
+    });
+}
 
 }  // extern "C"

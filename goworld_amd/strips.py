@@ -28,6 +28,7 @@ used by the single-GPU parity tests).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -118,6 +119,30 @@ class StripShard:
         hf = C.c_float()
         self._check(self._L.gwaoi_strips_halo(self._s, C.byref(hf)))
         self.halo = hf.value
+        # the world's HIP stream as a torch stream: the strip's kernels and torch's producers /
+        # consumers of its buffers are ordered by stream waits, not host synchronisation
+        self._host_sync = os.environ.get("GWAOI_STRIPS_HOSTSYNC", "0") == "1"  # A/B: host waits instead
+        self._inflight = []  # tensors the world's stream may still read (released by finish's host wait)
+
+    def _cur(self) -> int:
+        return self.torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _after_torch(self, *tensors):
+        """The world's stream waits for torch's current stream (the producers of `tensors`); the
+        tensors are kept referenced until finish() has waited for the world's stream, so the
+        caching allocator cannot hand their blocks out while the strip kernels read them."""
+        if self._host_sync:
+            self.torch.cuda.current_stream(self.dev).synchronize()
+            return
+        self.world.stream_after(self._cur())
+        self._inflight.extend(t for t in tensors if t is not None)
+
+    def _torch_after(self):
+        """torch's current stream waits for the world's stream (consumers of the strip's writes)."""
+        if self._host_sync:
+            self.torch.cuda.synchronize(self.dev)
+        else:
+            self.world.stream_before(self._cur())
 
     def close(self):
         if getattr(self, "_s", None):
@@ -143,16 +168,16 @@ class StripShard:
         tele (k,10) int32)."""
         torch = self.torch
         n = int(ops.shape[0])
-        # the world's stream does not wait for torch's: `ops` (and the caching allocator's reuse of
-        # the blocks written below) must be complete before the route kernels read them
-        torch.cuda.current_stream(self.dev).synchronize()
-        counts = (C.c_uint64 * (self.n_strips + 1))()
+        self._after_torch(ops)
+        counts = (C.c_uint64 * (self.n_strips + 1))()  # the one host wait of the route: the counts
         self._check(self._L.gwaoi_strips_route(self._s, C.c_void_p(ops.data_ptr() if n else 0), n, counts))
         c = np.array(counts[:], np.int64)
         send = torch.empty((int(c[:-1].sum()), HALO_WORDS), dtype=torch.int32, device=self.dev)
         tele = torch.empty((int(c[-1]), TELE_WORDS), dtype=torch.int32, device=self.dev)
+        self._after_torch(send, tele)
         self._check(self._L.gwaoi_strips_route_scatter(self._s, C.c_void_p(send.data_ptr() if send.numel() else 0),
                                                        C.c_void_p(tele.data_ptr() if tele.numel() else 0)))
+        self._torch_after()  # the transport reads them after the scatter
         return send, c[:-1], tele
 
     # ---- step 3: apply the exchanged records, flush, keep this strip's events
@@ -161,10 +186,12 @@ class StripShard:
         from the other strips; tele: all teleport records."""
         ne, nl = C.c_uint64(), C.c_uint64()
         nlo, nr, nt = int(local.shape[0]), int(recv.shape[0]), int(tele.shape[0])
+        self._after_torch(local, recv, tele)  # the exchange's writes land before the tick reads them
         self._check(self._L.gwaoi_strips_tick(self._s, C.c_void_p(local.data_ptr() if nlo else 0), nlo,
                                               C.c_void_p(recv.data_ptr() if nr else 0), nr,
                                               C.c_void_p(tele.data_ptr() if nt else 0), nt, C.byref(ne),
                                               C.byref(nl)))
+        self._inflight.clear()  # gwaoi_strips_tick returned after its last host wait: nothing in flight
         return ne.value, nl.value
 
     def events(self):
@@ -232,7 +259,8 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     RCCL send/recv over xGMI for GPU tensors) from its source to its
     destination only -- for strips at least H + teleport wide these are the
     two neighbours -- and a rank's own slice stays put (``local_slice``).
-    Teleport records are all-gathered only when some rank has any.  Returns
+    Teleport records go point to point to every rank, at their exact sizes
+    (the count matrix carries them), in the same batch.  Returns
     (records from the other ranks in source-rank order, all teleports).
     via_cpu: GPU tensors go through host memory (gloo rehearsal of several
     ranks sharing one GPU; RCCL allows one rank per device)."""
@@ -251,7 +279,8 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     M = torch.stack(rows).numpy()  # M[src, dst]; column S = teleports of src (host tensors: no device sync)
     off = np.concatenate([[0], np.cumsum(M[rank, :S])]).astype(np.int64)
     peer = (lambda q: q) if group is None else (lambda q: dist.get_global_rank(group, q))
-    ops, parts = [], []
+    T = M[:, S]  # teleport records per source rank
+    ops, parts, tparts = [], [], {rank: tele}
     for q in range(S):
         if q == rank:
             continue
@@ -261,19 +290,20 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
             buf = torch.empty((int(M[q, rank]), send.shape[1]), dtype=send.dtype, device=dev)
             parts.append(buf)
             ops.append(dist.P2POp(dist.irecv, buf, peer(q), group))
+        # teleport records travel to every rank, exact sizes (the count matrix has them): no padding
+        if T[rank]:
+            ops.append(dist.P2POp(dist.isend, tele, peer(q), group))
+        if T[q]:
+            tb = torch.empty((int(T[q]), tele.shape[1]), dtype=tele.dtype, device=dev)
+            tparts[q] = tb
+            ops.append(dist.P2POp(dist.irecv, tb, peer(q), group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     recv = torch.cat(parts) if parts else send[:0]
-    T = M[:, S]
     if T.sum() == 0:
         return recv, tele[:0]
-    pad = int(T.max())
-    buf = torch.zeros((pad, tele.shape[1]), dtype=tele.dtype, device=dev)
-    buf[:tele.shape[0]] = tele
-    gathered = [torch.empty_like(buf) for _ in range(S)]
-    dist.all_gather(gathered, buf, group=group)
-    return recv, torch.cat([gathered[r][:int(T[r])] for r in range(S)])
+    return recv, torch.cat([tparts[r] for r in range(S) if T[r]])
 
 
 def exchange_local(outs: List[Tuple]):
@@ -300,7 +330,6 @@ def tile_tick(shard: StripShard, dist, ops, group=None) -> Tuple[int, int]:
     """One tick of this rank's strip in a torch.distributed job."""
     send, counts, tele = shard.route(ops)
     recv, tele_all = exchange(dist, send, counts, tele, group=group)
-    shard.torch.cuda.current_stream(shard.dev).synchronize()
     return shard.finish(local_slice(send, counts, dist.get_rank(group)), recv, tele_all)
 
 
@@ -308,5 +337,4 @@ def local_tick(shards: Sequence[StripShard], ops_per_strip) -> List[Tuple[int, i
     """One tick of several strips in one process (loopback exchange)."""
     outs = [sh.route(o) for sh, o in zip(shards, ops_per_strip)]
     ex = exchange_local(outs)
-    shards[0].torch.cuda.synchronize()
     return [sh.finish(local_slice(o[0], o[1], q), r, t) for q, (sh, o, (r, t)) in enumerate(zip(shards, outs, ex))]

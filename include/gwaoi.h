@@ -251,6 +251,13 @@ int gwaoi_reset_stage_times(gwaoi_world *w);
 int gwaoi_set_stage_timing(gwaoi_world *w, uint32_t stage_mask);
 int gwaoi_sync(gwaoi_world *w);
 void *gwaoi_stream(gwaoi_world *w); /* the world's hipStream_t */
+/* Stream ordering without a host wait (a caller whose producers / consumers of
+ * the world's device buffers run on another hipStream_t `other`):
+ * gwaoi_stream_after: work queued on the world's stream from now on runs after
+ * everything queued on `other` so far; gwaoi_stream_before: work queued on
+ * `other` from now on runs after everything queued on the world's stream so far. */
+int gwaoi_stream_after(gwaoi_world *w, void *other);
+int gwaoi_stream_before(gwaoi_world *w, void *other);
 
 const char *gwaoi_strerror(int status);
 const char *gwaoi_last_error(gwaoi_world *w);

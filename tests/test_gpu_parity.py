@@ -445,16 +445,16 @@ def test_device_batch_repeated_slots_gpu():
             np.testing.assert_array_equal(wa.neighbors(i), wb.neighbors(i))
 
 
-@pytest.mark.parametrize("legacy", ["0", "1"])
-def test_device_batches_many_buckets_vs_closed_form_gpu(oracle_mod, monkeypatch, legacy):
-    """Moves-only flushes through the bucketed apply (slots regrouped by 4096-slot
-    bucket, last op per slot by LDS claim; GWAOI_MOVES_LEGACY=1: the global-claim
-    apply): live slots scattered over 14 buckets, three device batches per flush
+@pytest.mark.parametrize("bucketed", ["0", "1"])
+def test_device_batches_many_buckets_vs_closed_form_gpu(oracle_mod, monkeypatch, bucketed):
+    """Moves-only flushes through the global-claim apply and (GWAOI_MOVES_BUCKETED=1)
+    the bucketed one (slots regrouped by 4096-slot bucket, last op per slot by LDS
+    claim): live slots scattered over 14 buckets, three device batches per flush
     with slots repeated inside a batch and across batches, one batch with
     explicit seqs.  Last call wins (Space.go:259 in call order); events vs the
     closed form."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("GWAOI_MOVES_LEGACY", legacy)
+    monkeypatch.setenv("GWAOI_MOVES_BUCKETED", bucketed)
     O = oracle_mod
     rng = np.random.default_rng(77)
     N = 57000
