@@ -14,6 +14,11 @@
 // The event stream never adds a present member or removes an absent one (the
 // flush reports net changes), but add/del here are exact
 // set operations anyway and report whether they changed the set.
+//
+// An entity's two sets share one table: an entry is the member's slot (< 2^30)
+// with a bit for InterestedIn and a bit for InterestedBy, so one probe serves
+// both sets of a row item (interest(s, b) and the mirrored interest(b, s) both
+// change row s) and an entry leaves the table when neither bit is left.
 #pragma once
 
 #include <algorithm>
@@ -33,6 +38,8 @@ struct Table {  // one entity's set: keys at arena[off .. off + cap)
 
 inline uint32_t slot_hash(uint32_t k, uint32_t mask) { return (k * 0x9E3779B1u >> 7) & mask; }
 
+constexpr uint32_t IN = 1u << 30, BY = 1u << 31, KEY = IN - 1;  // entry = slot | membership bits
+
 // The sets of entities [lo, hi): one owner thread.
 class Range {
   public:
@@ -50,21 +57,27 @@ class Range {
         }
         arena_.assign(total, EMPTY);
     }
-    bool add(uint32_t s, uint32_t k) {
+    // add k to the sets of s named by bits (IN, BY or both); true if some set changed
+    bool add(uint32_t s, uint32_t k, uint32_t bits) {
         Table &t = t_[s - lo_];
         if (2 * (t.size + 1) > t.cap) grow(t);
         uint32_t *a = arena_.data() + t.off;
         const uint32_t mask = t.cap - 1;
         for (uint32_t h = slot_hash(k, mask);; h = (h + 1) & mask) {
-            if (a[h] == k) return false;
             if (a[h] == EMPTY) {
-                a[h] = k;
+                a[h] = k | bits;
                 ++t.size;
                 return true;
             }
+            if ((a[h] & KEY) == k) {
+                const bool changed = (a[h] & bits) != bits;
+                a[h] |= bits;
+                return changed;
+            }
         }
     }
-    bool del(uint32_t s, uint32_t k) {
+    // remove k from the sets of s named by bits; true if some set changed
+    bool del(uint32_t s, uint32_t k, uint32_t bits) {
         Table &t = t_[s - lo_];
         if (!t.size) return false;
         uint32_t *a = arena_.data() + t.off;
@@ -72,12 +85,16 @@ class Range {
         uint32_t h = slot_hash(k, mask);
         for (;; h = (h + 1) & mask) {
             if (a[h] == EMPTY) return false;
-            if (a[h] == k) break;
+            if ((a[h] & KEY) == k) break;
         }
-        // backward-shift delete: pull later members of the probe cluster into the hole
+        const bool changed = (a[h] & bits) != 0;
+        a[h] &= ~bits;
+        if (a[h] & (IN | BY)) return changed;
+        // neither set holds k: backward-shift delete, pulling later members of the probe
+        // cluster into the hole
         uint32_t hole = h;
         for (uint32_t j = (h + 1) & mask; a[j] != EMPTY; j = (j + 1) & mask) {
-            const uint32_t home = slot_hash(a[j], mask);
+            const uint32_t home = slot_hash(a[j] & KEY, mask);
             // a[j] may move to the hole iff the hole lies on its probe path [home, j)
             if (((j - home) & mask) >= ((j - hole) & mask)) {
                 a[hole] = a[j];
@@ -86,27 +103,37 @@ class Range {
         }
         a[hole] = EMPTY;
         --t.size;
-        return true;
+        return changed;
     }
-    bool has(uint32_t s, uint32_t k) const {
+    bool has(uint32_t s, uint32_t k, uint32_t bit) const {
         const Table &t = t_[s - lo_];
         if (!t.cap) return false;
         const uint32_t *a = arena_.data() + t.off;
         const uint32_t mask = t.cap - 1;
         for (uint32_t h = slot_hash(k, mask);; h = (h + 1) & mask) {
-            if (a[h] == k) return true;
             if (a[h] == EMPTY) return false;
+            if ((a[h] & KEY) == k) return (a[h] & bit) != 0;
         }
     }
-    uint32_t size(uint32_t s) const { return t_[s - lo_].size; }
-    // the members of s, sorted
-    std::vector<uint32_t> members(uint32_t s) const {
+    // the members of one set (IN or BY) of s, sorted
+    std::vector<uint32_t> members(uint32_t s, uint32_t bit) const {
         const Table &t = t_[s - lo_];
         std::vector<uint32_t> m;
-        for (uint32_t i = 0; i < t.cap; ++i)
-            if (arena_[t.off + i] != EMPTY) m.push_back(arena_[t.off + i]);
+        for (uint32_t i = 0; i < t.cap; ++i) {
+            const uint32_t e = arena_[t.off + i];
+            if (e != EMPTY && (e & bit)) m.push_back(e & KEY);
+        }
         std::sort(m.begin(), m.end());
         return m;
+    }
+    uint32_t size(uint32_t s, uint32_t bit) const {
+        const Table &t = t_[s - lo_];
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < t.cap; ++i) {
+            const uint32_t e = arena_[t.off + i];
+            c += e != EMPTY && (e & bit) ? 1u : 0u;
+        }
+        return c;
     }
     uint32_t lo() const { return lo_; }
     uint32_t hi() const { return hi_; }
@@ -130,11 +157,11 @@ class Range {
         uint32_t *na = arena_.data() + noff;
         const uint32_t mask = nc - 1;
         for (uint32_t i = 0; i < t.cap; ++i) {
-            const uint32_t k = arena_[t.off + i];
-            if (k == EMPTY) continue;
-            uint32_t h = slot_hash(k, mask);
+            const uint32_t e = arena_[t.off + i];
+            if (e == EMPTY) continue;
+            uint32_t h = slot_hash(e & KEY, mask);
             while (na[h] != EMPTY) h = (h + 1) & mask;
-            na[h] = k;
+            na[h] = e;
         }
         t.off = noff;
         t.cap = nc;
@@ -147,34 +174,28 @@ class Range {
 // The replay of one flush for the slots of one Range from the per-entity rows
 // of gwaoi_events_csr (row s: items b | enter_bit for the events (s, b)).  The
 // flush's events come in pairs (s, b) and (b, s), so row s holds every change
-// of s.InterestedIn and of s.InterestedBy.  Returns the set operations done.
-inline uint64_t replay_rows(Range &in, Range &by, const uint32_t *off, const uint32_t *items, uint32_t enter_bit) {
+// of s.InterestedIn (event (s, b)) and of s.InterestedBy (event (b, s)): one
+// probe per item updates both.  Returns the set operations done.
+inline uint64_t replay_rows(Range &r, const uint32_t *off, const uint32_t *items, uint32_t enter_bit) {
     constexpr uint32_t AHEAD = 16;  // items prefetched ahead of the one applied
     uint64_t ops = 0;
     // the item stream of the range, with its row, runs AHEAD items in front of the replay
-    uint32_t ps = in.lo(), pk = off[in.lo()];
-    const uint32_t kend = off[in.hi()];
+    uint32_t ps = r.lo(), pk = off[r.lo()];
+    const uint32_t kend = off[r.hi()];
     auto advance = [&]() {
         if (pk >= kend) return;
         while (off[ps + 1] <= pk) ++ps;
-        const uint32_t b = items[pk] & ~enter_bit;
-        in.prefetch(ps, b);
-        by.prefetch(ps, b);
+        r.prefetch(ps, items[pk] & ~enter_bit);
         ++pk;
     };
     for (uint32_t q = 0; q < AHEAD; ++q) advance();
-    for (uint32_t s = in.lo(); s < in.hi(); ++s) {
+    for (uint32_t s = r.lo(); s < r.hi(); ++s) {
         const uint32_t e = off[s + 1];
         for (uint32_t k = off[s]; k < e; ++k) {
             advance();
             const uint32_t it = items[k], b = it & ~enter_bit;
-            if (it & enter_bit) {
-                in.add(s, b);
-                by.add(s, b);
-            } else {
-                in.del(s, b);
-                by.del(s, b);
-            }
+            if (it & enter_bit) r.add(s, b, IN | BY);
+            else r.del(s, b, IN | BY);
         }
         ops += 2ull * (e - off[s]);
     }

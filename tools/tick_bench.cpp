@@ -78,16 +78,15 @@ void check(int rc, const char *what, gwaoi_world *w) {
     }
 }
 
-// InterestedIn / InterestedBy of every entity, split into T slot ranges (one
-// owner thread each).
+// InterestedIn / InterestedBy of every entity (one table per entity, a bit per
+// set: tools/interest_sets.hpp), split into T slot ranges (one owner thread each).
 struct Sets {
     uint32_t n, T;
-    std::vector<gwsets::Range> in, by;
-    Sets(uint32_t n_, uint32_t T_, const uint32_t *sizes) : n(n_), T(T_), in(T_), by(T_) {
+    std::vector<gwsets::Range> r;
+    Sets(uint32_t n_, uint32_t T_, const uint32_t *sizes) : n(n_), T(T_), r(T_) {
         for (uint32_t k = 0; k < T; ++k) {
             const uint32_t lo = lo_of(k), hi = lo_of(k + 1);
-            in[k].init(lo, hi, sizes ? sizes + lo : nullptr);
-            by[k].init(lo, hi, sizes ? sizes + lo : nullptr);
+            r[k].init(lo, hi, sizes ? sizes + lo : nullptr);
         }
     }
     uint32_t lo_of(uint32_t k) const { return (uint32_t)((uint64_t)n * k / T); }
@@ -104,13 +103,13 @@ struct Sets {
 void replay_pairs(Sets &S, const gwaoi_events &ev) {
     for (uint64_t k = 0; k < ev.n_leave; ++k) {
         const uint32_t a = ev.leave[2 * k], b = ev.leave[2 * k + 1];
-        S.in[S.owner(a)].del(a, b);
-        S.by[S.owner(b)].del(b, a);
+        S.r[S.owner(a)].del(a, b, gwsets::IN);
+        S.r[S.owner(b)].del(b, a, gwsets::BY);
     }
     for (uint64_t k = 0; k < ev.n_enter; ++k) {
         const uint32_t a = ev.enter[2 * k], b = ev.enter[2 * k + 1];
-        S.in[S.owner(a)].add(a, b);
-        S.by[S.owner(b)].add(b, a);
+        S.r[S.owner(a)].add(a, b, gwsets::IN);
+        S.r[S.owner(b)].add(b, a, gwsets::BY);
     }
 }
 
@@ -245,7 +244,7 @@ int main(int argc, char **argv) {
     for (uint32_t i = 0; i < n; ++i) sizes[i] = coff[i + 1] - coff[i];
     Sets S(n, T, sizes.data());
     Pool pool(T);
-    pool.run([&](unsigned k) { gwsets::replay_rows(S.in[k], S.by[k], coff, citems, GWAOI_CSR_ENTER); });
+    pool.run([&](unsigned k) { gwsets::replay_rows(S.r[k], coff, citems, GWAOI_CSR_ENTER); });
 
     // ---- serial leg: moved_batch + tick, then replay (one thread); odd ticks replay the event
     // pairs, even ticks the per-entity rows (gwaoi_events_csr, built on the GPU and copied)
@@ -264,7 +263,7 @@ int main(int argc, char **argv) {
         } else {
             check(gwaoi_events_csr(w, &coff, &citems, &cn), "events_csr", w);
             e = now();
-            for (unsigned k = 0; k < T; ++k) gwsets::replay_rows(S.in[k], S.by[k], coff, citems, GWAOI_CSR_ENTER);
+            for (unsigned k = 0; k < T; ++k) gwsets::replay_rows(S.r[k], coff, citems, GWAOI_CSR_ENTER);
             d = now();
         }
         if (t > 2) {  // the first ticks size the pinned buffers
@@ -286,7 +285,7 @@ int main(int argc, char **argv) {
     std::vector<double> p_lat, t_repT, p_host;
     auto replay_T = [&]() {  // the rows of the last gwaoi_events_csr, T pool threads over slot ranges
         const double r0 = now();
-        pool.run([&](unsigned k) { gwsets::replay_rows(S.in[k], S.by[k], coff, citems, GWAOI_CSR_ENTER); });
+        pool.run([&](unsigned k) { gwsets::replay_rows(S.r[k], coff, citems, GWAOI_CSR_ENTER); });
         t_repT.push_back(now() - r0);
     };
     int t = ticks + 1;
@@ -316,8 +315,8 @@ int main(int argc, char **argv) {
     // InterestedIn sets equal the world's neighbour rows
     uint64_t sin = 0, sby = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        sin += S.in[S.owner(i)].size(i);
-        sby += S.by[S.owner(i)].size(i);
+        sin += S.r[S.owner(i)].size(i, gwsets::IN);
+        sby += S.r[S.owner(i)].size(i, gwsets::BY);
     }
     uint32_t sample_bad = 0;
     {
@@ -329,7 +328,7 @@ int main(int argc, char **argv) {
             check(gwaoi_neighbors(w, s, nb.data(), nb.size(), &cnt), "neighbors", w);
             std::vector<uint32_t> want(nb.begin(), nb.begin() + (long)std::min(cnt, nb.size()));
             std::sort(want.begin(), want.end());
-            if (S.in[S.owner(s)].members(s) != want || S.by[S.owner(s)].members(s) != want) ++sample_bad;
+            if (S.r[S.owner(s)].members(s, gwsets::IN) != want || S.r[S.owner(s)].members(s, gwsets::BY) != want) ++sample_bad;
         }
     }
     gwaoi_world_destroy(w);
