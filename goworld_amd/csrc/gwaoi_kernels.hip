@@ -2079,6 +2079,99 @@ __device__ __forceinline__ void sweep_rows_zlds(CombinedLds &L, int w, WaveQueue
 }
 #endif
 
+#ifndef GWAOI_XPAIR
+#define GWAOI_XPAIR 2  // the X' strip's rows swept P at a time as one virtual range per lane (0: one row at a time; 2: combined 0.1095/0.1081 vs 0.1123/0.1120 ms, 3: 0.128, profiles/r03_variants_xpair.log)
+#endif
+#if GWAOI_XPAIR
+// sweep_range over P row ranges of a lane taken as one sequence (index select per candidate):
+// the short X' rows share sweep iterations instead of paying one each.
+template <int MODE, int U, int P>
+__device__ __forceinline__ void sweep_segs(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A,
+                                           const uint32_t (&jb)[P], const uint32_t (&ln)[P],
+                                           const uint4 *__restrict__ cand, const FrameView &F,
+                                           const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
+                                           uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
+    uint32_t cum[P], tot = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        tot += ln[q];
+        cum[q] = tot;
+    }
+    for (uint32_t t = 0; __ballot(t < tot); t += U) {
+        if (Q.qn > QCAP - U * WAVE) {
+            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);
+            __builtin_amdgcn_wave_barrier();
+            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
+                        cap, pe, pl, replay);
+            Q.qn = 0;
+        }
+        uint4 k[U];
+        uint32_t bi[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = t + (uint32_t)u;
+            uint32_t idx = jb[0] + v;
+#pragma unroll
+            for (int q = 1; q < P; ++q)
+                if (v >= cum[q - 1]) idx = jb[q] + (v - cum[q - 1]);
+            bi[u] = v < tot ? idx : 0u;
+            k[u] = cand[bi[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool keep = band_keep<MODE>(A, C, k[u], bi[u]) & (t + (uint32_t)u < tot);
+            qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), bi[u]);
+        }
+    }
+}
+
+// The X' strip's rows, P at a time (sweep_segs); the next group's ranges are loaded first.
+template <int P>
+__device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
+                                                   int r0, int r1, int c0, int c1, const uint4 *__restrict__ cand,
+                                                   const FrameView &F, const Rec16 *__restrict__ O_rec,
+                                                   const CombinedCtx &C, uint2 *out, uint64_t cap,
+                                                   unsigned long long pe, unsigned long long pl, bool replay) {
+    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
+    const uint32_t *cs = F.cell_start;
+    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
+    uint32_t jb[P], ln[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        jb[q] = ln[q] = 0;
+        if ((uint32_t)q < nr) {
+            const uint32_t rb = rb0 + (uint32_t)(r0 + q) * gx;
+            jb[q] = cs[rb];
+            ln[q] = cs[rb + span] - jb[q];
+        }
+    }
+    for (uint32_t k = 0; __ballot(k < nr); k += P) {
+        uint32_t nb[P], nl[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {  // prefetch the next group's ranges
+            nb[q] = nl[q] = 0;
+            if (k + P + (uint32_t)q < nr) {
+                const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + P + q) * gx;
+                nb[q] = cs[rb];
+                nl[q] = cs[rb + span] - nb[q];
+            }
+        }
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) tot += ln[q];
+        if (__ballot(tot > 2))
+            sweep_segs<1, GWAOI_SW_U, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        else if (__ballot(tot != 0))
+            sweep_segs<1, 2, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            jb[q] = nb[q];
+            ln[q] = nl[q];
+        }
+    }
+}
+#endif
+
 // Rows r0..r1 (per lane; `on` = the lane takes part), cells c0..c1 of each row.
 // The next row's candidate range is loaded while the current one is swept.
 template <int MODE>
@@ -2257,7 +2350,10 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
 #ifndef GWAOI_EXP_NOX  // timing experiment only: skip the X' strip (events wrong)
-#if GWAOI_XB > 0
+#if GWAOI_XPAIR
+        sweep_rows_grouped<GWAOI_XPAIR>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl,
+                                        replay);
+#elif GWAOI_XB > 0
         sweep_rows_batched<1, GWAOI_XB, GWAOI_XH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
                                                   pl, replay);
 #else
