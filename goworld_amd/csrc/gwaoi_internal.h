@@ -150,11 +150,13 @@ struct MoveRuns {
 // s_ss == nullptr: a moves-only flush without the prologue's copy ("virtual S'":
 // the spaces are the previous frame's, and an entry of S' not written by an op
 // holds an older seq than seq_floor, so k_keygen takes the previous frame's
-// record for it and writes it back).  first_marked: the prologue stored run 0's
-// claims.
+// record for it and writes it back).  n_marked: runs whose claims are stored
+// already (by the prologue: run 0; by launch_moves_mark: every run).
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, bool first_marked, hipStream_t st);
+                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st);
+// The claims of every run (k_moves_mark), on a stream of the caller's choice.
+void launch_moves_mark(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st);
 // The same flush through slot buckets (gwaoi_kernels.hip k_mv_*), for worlds whose
 // SlotInfo outgrows the MALL (max_slots > MV_MIN_SLOTS; moves_buckets(max_slots) <=
 // MV_NB_MAX).  hist: moves_hist_elems(n ops, max_slots) uint32; scan_tmp:

@@ -2875,10 +2875,15 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_rec, s_ss, info);
 }
 
+void launch_moves_mark(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st) {
+    for (uint32_t q = 0; q < RS.count; ++q)
+        if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
+}
+
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, bool first_marked, hipStream_t st) {
-    for (uint32_t q = first_marked ? 1u : 0u; q < RS.count; ++q)  // every run's claims before any apply
+                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st) {
+    for (uint32_t q = n_marked; q < RS.count; ++q)  // every run's claims before any apply
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)

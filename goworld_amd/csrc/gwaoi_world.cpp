@@ -262,6 +262,14 @@ struct gwaoi_world {
     uint32_t *h_stage[2] = {nullptr, nullptr}, *d_stage[2] = {nullptr, nullptr};
     size_t stage_cap[2] = {0, 0}, stage_used[2] = {0, 0};
     int stage_cur = 0;
+    // A speculative launch stores its claims on a side stream, beside the flush in flight
+    // (after that flush's apply: applied_ev), and its apply waits for them (claimed_ev).
+    hipStream_t claim_st = nullptr;
+    hipEvent_t applied_ev = nullptr, claimed_ev = nullptr;
+    bool spec_launch = false;     // tick_launch called by gwaoi_tick_end_begin_device's speculative path
+    // GWAOI_SIDE_CLAIMS=1 (A/B, off): measured slower, 0.303-0.305 vs 0.292-0.294 ms per tick -- the
+    // side kernel's random claim stores ran 30 us beside k_keygen and stretched it from 20 to 37 us
+    bool side_claims = false;
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
@@ -808,6 +816,7 @@ int tick_launch(gwaoi_world *w) {
         Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
     }
     // the staged move batches' H2D copies (copy stream) land before the flush reads them
+    const bool copy_wait = w->copy_pending;
     if (w->copy_pending) {
         HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
         w->copy_pending = false;
@@ -831,7 +840,16 @@ int tick_launch(gwaoi_world *w) {
     // counters, tile totals, bbox fold identity; S' <- the previous frame unless virtual; the
     // first Moved run's claims
     const bool bucketed = moves_only && w->mv_binned;
-    const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
+    // a speculative launch: the flush in flight is still on the stream; its successor's claims need
+    // only that flush's apply to be done, so they run beside the rest of it on the side stream
+    const bool side = moves_only && !bucketed && w->spec_launch && w->side_claims;
+    if (side) {
+        HIP_TRY(hipStreamWaitEvent(w->claim_st, w->applied_ev, 0));
+        if (copy_wait) HIP_TRY(hipStreamWaitEvent(w->claim_st, w->copy_ev, 0));
+        gw::launch_moves_mark(RS, w->max_slots, w->sinfo, tick_id, w->claim_st);
+        HIP_TRY(hipEventRecord(w->claimed_ev, w->claim_st));
+    }
+    const gw::MoveRun *mark = moves_only && !bucketed && !side ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
@@ -854,8 +872,9 @@ int tick_launch(gwaoi_world *w) {
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
     } else if (moves_only) {  // one pass + fixup of repeated slots
+        if (side) HIP_TRY(hipStreamWaitEvent(st, w->claimed_ev, 0));
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
-                         P.rec, n_prev, S.sc, w->coll, true, st);
+                         P.rec, n_prev, S.sc, w->coll, side ? RS.count : 1u, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -897,6 +916,7 @@ int tick_launch(gwaoi_world *w) {
         }
     }
     stage_end(w, S, ST_APPLY);
+    HIP_TRY(hipEventRecord(w->applied_ev, st));  // a speculative successor's claims may start from here
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
@@ -1190,6 +1210,10 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     }
     if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
     if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
+    if (w->claim_st) (void)hipStreamSynchronize(w->claim_st);
+    if (w->applied_ev) (void)hipEventDestroy(w->applied_ev);
+    if (w->claimed_ev) (void)hipEventDestroy(w->claimed_ev);
+    if (w->claim_st) (void)hipStreamDestroy(w->claim_st);
     if (w->done_ev) (void)hipEventDestroy(w->done_ev);
     if (w->order_ev) (void)hipEventDestroy(w->order_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
@@ -1238,6 +1262,14 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         w->copy_st = nullptr;
         return fail(GWAOI_EDEVICE);
     }
+    if (hipStreamCreateWithFlags(&w->claim_st, hipStreamNonBlocking) != hipSuccess) {
+        w->claim_st = nullptr;
+        return fail(GWAOI_EDEVICE);
+    }
+    if (hipEventCreateWithFlags(&w->applied_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->claimed_ev, hipEventDisableTiming) != hipSuccess)
+        return fail(GWAOI_EDEVICE);
+    if (const char *e = std::getenv("GWAOI_SIDE_CLAIMS")) w->side_claims = e[0] == '1';
     if (hipEventCreateWithFlags(&w->copy_ev, hipEventDisableTiming) != hipSuccess) {
         w->copy_ev = nullptr;
         return fail(GWAOI_EDEVICE);
@@ -1798,7 +1830,9 @@ int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_l
         // no idle gap on the GPU between the two
         const Flight f = w->fl;
         commit_host(w, nullptr);
+        w->spec_launch = true;
         lrc = tick_launch(w);
+        w->spec_launch = false;
         if (lrc == GWAOI_OK) w->dbg.speculative_launches++;
         rc = finish_flight(w, f, true, &committed);
     } else {

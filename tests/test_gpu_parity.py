@@ -981,33 +981,46 @@ def _device_events(w, ne, nl):
     return out
 
 
-@pytest.mark.parametrize("event_capacity", [0, 3000])
-def test_speculative_next_flush_matches_serial_gpu(event_capacity):
+@pytest.mark.parametrize("event_capacity,repeats", [(0, False), (3000, False), (0, True)])
+def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
     """gwaoi_tick_end_begin_device: the next flush queued before the commit of the one in
-    flight (device Moved batches only) gives every flush the events of the serial path --
-    also when the flush in flight overflows its event buffer and is re-run after its
-    successor (event_capacity=3000), and when a host call in flight forces the fallback."""
+    flight (device Moved batches only; its claims stored on a side stream beside the
+    flush in flight) gives every flush the events of the serial path -- also when the
+    flush in flight overflows its event buffer and is re-run after its successor
+    (event_capacity=3000), when a batch moves slots more than once (repeats: the last
+    call wins), and when a host call in flight forces the fallback."""
     torch = pytest.importorskip("torch")
     n = 20000
     wa, wb = make_workload("cfg2", n=n), make_workload("cfg2", n=n)
     slots, x0, z0, _ = wa.initial()
     ticks = 24
-    batches = []
+    batches, host = [], []
+    rng = np.random.default_rng(99)
     for t in range(ticks):
         sl, nx, nz = wa.tick(t)
+        if repeats:  # 2,000 extra moves of 300 slots, after and before their regular move
+            extra = rng.integers(0, 300, 2000).astype(sl.dtype)
+            ex = (x0[extra] + rng.uniform(-20, 20, extra.size)).astype(np.float32)
+            ez = (z0[extra] + rng.uniform(-20, 20, extra.size)).astype(np.float32)
+            cut = sl.size // 2
+            sl = np.concatenate([sl[:cut], extra, sl[cut:]])
+            nx = np.concatenate([nx[:cut], ex, nx[cut:]])
+            nz = np.concatenate([nz[:cut], ez, nz[cut:]])
+        host.append((sl, nx, nz))
         batches.append([torch.from_numpy(a).to("cuda:0") for a in (sl.astype(np.int32), nx, nz)])
     torch.cuda.synchronize()
-    with World(n, event_capacity=event_capacity) as A, World(n) as B:
+    cap = 2 * n if repeats else n  # a speculative launch takes at most max_slots ops
+    with World(cap, event_capacity=event_capacity) as A, World(cap) as B:
         for w in (A, B):
             s = w.space_create(wa.D)
             w.enter_batch(s, slots, x0, z0)
             w.tick()
-        A.moved_batch_device(*(b.data_ptr() for b in batches[0]), n)
+        A.moved_batch_device(*(b.data_ptr() for b in batches[0]), host[0][0].size)
         A.tick_begin()
         caps = []
         for t in range(ticks):
             if t + 1 < ticks:
-                A.moved_batch_device(*(b.data_ptr() for b in batches[t + 1]), n)
+                A.moved_batch_device(*(b.data_ptr() for b in batches[t + 1]), host[t + 1][0].size)
                 if t == 4:  # a host call queued in flight: this tick takes the fallback path
                     A.moved(7, 123.0, 456.0)
                 ne, nl = A.tick_end_begin_device()
@@ -1015,7 +1028,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity):
                 ne, nl = A.tick_end_device()
             ga, la = _device_events(A, ne, nl)
             caps.append(A.info()["event_capacity"])
-            sl, nx, nz = wb.tick(t)
+            sl, nx, nz = host[t]
             B.moved_batch(sl, nx, nz)
             if t == 5:
                 B.moved(7, 123.0, 456.0)
