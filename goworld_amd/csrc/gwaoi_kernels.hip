@@ -313,6 +313,9 @@ __device__ __forceinline__ uint4 cand_of(const Rec16 &now, const Rec16 &old, flo
 // differs from their previous-frame cell, or new in the frame (high word).
 // S' is the previous frame (sorted by the same keys) plus appended entries,
 // so equal keys come in runs and one atomic per run and wave suffices.
+#ifndef GWAOI_DELTA_COUNTS
+#define GWAOI_DELTA_COUNTS 1  // incremental keygen counts only the cell changers (0: every entity, one atomic per run)
+#endif
 template <bool INCR>
 __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__restrict__ s_ss,
                                                 uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
@@ -350,6 +353,18 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         if (!INCR) vals[i] = i;
     }
     if (INCR) {
+#if GWAOI_DELTA_COUNTS
+        // only the entities that changed cell count: an arrival in the new cell (low word), a
+        // departure from the old one (high word); a cell's stayers are its previous count minus
+        // its departures, which k_scan64_lb takes from the previous cell_start
+        if (i < n) {
+            const uint32_t old = i < n_prev ? p_key[i] : sentinel;
+            if (key != old) {
+                if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
+                if (old != sentinel) atomicAdd(&cnt64[old], 1ull << 32);
+            }
+        }
+#else
         const bool live = i < n && key != sentinel;
         const uint32_t l = lane();
         const uint32_t prev_key = __shfl_up(key, 1);
@@ -362,6 +377,7 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
             atomicAdd(&cnt64[key], (unsigned long long)(next - l));
         }
         if (live && (i >= n_prev || p_key[i] != key)) atomicAdd(&cnt64[key], 1ull << 32);
+#endif
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1023,7 +1039,8 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 #endif
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
-                                                    const float *__restrict__ blk, uint32_t nbk, TickScalars *sc) {
+                                                    const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
+                                                    const uint32_t *__restrict__ p_cs) {
     const uint32_t b = blockIdx.x;
     if (b == nb) {
         keygen_fold256(blk, nbk, sc);
@@ -1076,8 +1093,15 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
         const uint32_t j = (uint32_t)q * SC_T + tid;
         if (base + j < n) {
             const unsigned long long e = tile[p64(j)];
+#if GWAOI_DELTA_COUNTS
+            // e = (departures before c) << 32 | (arrivals before c): cell c starts at its previous
+            // start plus the arrivals minus the departures of the cells before it
+            lo[base + j] = p_cs[base + j] + (uint32_t)e - (uint32_t)(e >> 32);
+            hi[base + j] = (uint32_t)e;
+#else
             lo[base + j] = (uint32_t)e;
             hi[base + j] = (uint32_t)(e >> 32);
+#endif
         }
     }
 }
@@ -2970,7 +2994,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, SC_TILE);
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
-                                         cdiv(n_total, 256), sc);
+                                         cdiv(n_total, 256), sc, p_cell_start);
     if (n_total) k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
                                                          n_new, n_total, sentinel, perm, skeys);
