@@ -262,6 +262,57 @@ __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uin
     }
 }
 
+#ifndef GWAOI_APPLY_PER
+#define GWAOI_APPLY_PER 4  // ops per thread in k_moves_apply, their SlotInfo lines loaded together (1: 38.5, 2: 33.9, 4: 33.0 us; profiles/r03_variants_apply_per.log)
+#endif
+#if GWAOI_APPLY_PER > 1
+template <int PER>
+__global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
+                                                       uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
+                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
+    const uint32_t i0 = blockIdx.x * (256u * PER) + threadIdx.x;
+    OpIn o[PER];
+    uint4 si[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * 256u;
+        o[u].slot = SLOT_NONE;
+        if (i < R.n) o[u] = op_in(R.ds, R.dx, R.dz, R.dsp, R.dseq, R.seq0, i);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u)  // every SlotInfo line in flight at once
+        si[u] = o[u].slot < max_slots ? slot_info(info, o[u].slot) : make_uint4(0, 0, 0, 0);
+    unsigned long long smax = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * 256u;
+        const uint32_t s = o[u].slot;
+        if (i >= R.n || s == SLOT_NONE) continue;
+        if (s >= max_slots) {
+            atomicOr(&sc->err, ERR_BAD_SLOT);
+            continue;
+        }
+        const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
+        const unsigned long long seen = ((unsigned long long)si[u].y << 32) | si[u].x;
+        if (seen == mine) {
+            const unsigned long long q =
+                op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false);
+            smax = q > smax ? q : smax;
+        } else {
+            atomicMax(&info[s].lastop, mine);
+            coll[atomicAdd(&sc->ncoll, 1u)] = s;
+        }
+    }
+    if (R.dseq) {
+        for (int q = 32; q > 0; q >>= 1) {
+            const unsigned long long v = __shfl_xor(smax, q, WAVE);
+            smax = v > smax ? v : smax;
+        }
+        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
+    }
+}
+#endif
+
 __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
                               unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
                               uint32_t n_prev, TickScalars *sc, const uint32_t *__restrict__ coll) {
@@ -2911,8 +2962,13 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
+#if GWAOI_APPLY_PER > 1
+            k_moves_apply_n<GWAOI_APPLY_PER><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
+#else
             k_moves_apply<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id, n_total,
                                                                 seq_floor, s_rec, s_ss, sc, coll);
+#endif
     k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
                                       sc, coll);
 }

@@ -231,18 +231,12 @@ __device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint3
 // nil, outside every space.  In an AOI space it is a Moved (op i of the
 // batch) plus Position; elsewhere Space.move returns before Position
 // (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
-__global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-#if GWAOI_DECODE_FUSE
-    if (i == 0) *A.ndup = 0u;  // read by k_decode_apply, the next launch on the stream
-#endif
-    if (i >= A.n) return;
-    const uint4 id = A.pay[2 * (size_t)i];
-    const uint4 pv = A.pay[2 * (size_t)i + 1];
-    uint32_t s = lookup(A.htab, A.hmask, id);
+// The record's effects once its slot is known (s: the looked-up slot or SLOT_NONE; st: its
+// slot record when s != SLOT_NONE).
+__device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, const uint4 &pv, uint32_t s,
+                                            const uint4 &st) {
     uint32_t sp = SP_DEAD, old = 0;
     if (s != SLOT_NONE) {
-        const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[s];
         sp = st.y;  // SST_SPACE
         old = st.w;  // SST_FLAGS
         if (!st.z) s = SLOT_NONE;  // SST_SYNCING
@@ -276,6 +270,75 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
         } else if (!(old & GWAOI_SIF_NEIGHBOR_CLIENTS)) {
             *fl = old | GWAOI_SIF_NEIGHBOR_CLIENTS;
         }
+    }
+}
+
+#ifndef GWAOI_DECODE_PER
+#define GWAOI_DECODE_PER 1  // records per thread in k_decode (their probe lines and slot records in flight together)
+#endif
+
+// OnSyncPositionYawFromClient: unknown id -> skip (EntityManager.go:486-490);
+// syncPositionYawFromClient: only if syncing (Entity.go:432).  setPositionYaw
+// (Entity.go:1189-1205) then runs for every entity: e.Space is nilSpace, not
+// nil, outside every space.  In an AOI space it is a Moved (op i of the
+// batch) plus Position; elsewhere Space.move returns before Position
+// (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
+// PER records per thread, strided by the block: every record's first probe line
+// (four 32-B buckets) and then every slot record are loaded before any is used.
+template <int PER>
+__global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
+    const uint32_t i0 = blockIdx.x * (ST * PER) + threadIdx.x;
+#if GWAOI_DECODE_FUSE
+    if (i0 == 0) *A.ndup = 0u;  // read by k_decode_apply, the next launch on the stream
+#endif
+    uint4 id[PER], pv[PER];
+    uint32_t s[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * ST;
+        id[u] = pv[u] = make_uint4(0, 0, 0, 0);
+        if (i < A.n) {
+            id[u] = A.pay[2 * (size_t)i];
+            pv[u] = A.pay[2 * (size_t)i + 1];
+        }
+    }
+    if (PER == 1) {
+        s[0] = i0 < A.n ? lookup(A.htab, A.hmask, id[0]) : SLOT_NONE;
+    } else {
+        uint4 k[PER][4];
+        uint32_t v[PER][4], h[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {  // the first probe line of every record
+            h[u] = id_hash(id[u].x, id[u].y, id[u].z, id[u].w) & A.hmask;
+            const uint32_t hb = h[u] & ~3u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                k[u][q] = A.htab[2 * (size_t)(hb + (uint32_t)q)];
+                v[u][q] = A.htab[2 * (size_t)(hb + (uint32_t)q) + 1].x;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t first = h[u] & 3u;
+            uint32_t r = 0xFFFFFFFEu;  // not decided by the first line
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (r != 0xFFFFFFFEu) continue;
+                if (v[u][q] != H_EMPTY && v[u][q] != H_TOMB && eq4(k[u][q], id[u])) r = v[u][q];
+                else if ((uint32_t)q >= first && v[u][q] == H_EMPTY) r = SLOT_NONE;
+            }
+            if (r == 0xFFFFFFFEu) r = lookup(A.htab, A.hmask, id[u]);  // the probe runs past the line (rare)
+            s[u] = i0 + (uint32_t)u * ST < A.n ? r : SLOT_NONE;
+        }
+    }
+    uint4 st[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u)  // every slot record in flight together
+        st[u] = s[u] != SLOT_NONE ? reinterpret_cast<const uint4 *>(A.sst)[s[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * ST;
+        if (i < A.n) decode_rest(A, i, pv[u], s[u], st[u]);
     }
 }
 
@@ -1470,7 +1533,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.ndup = reinterpret_cast<uint32_t *>(base + 6 * al(n * 4));
     S->claim_next += n;
     S->decoded = true;
-    k_decode<<<cdivu(n, ST), ST, 0, S->st>>>(A);
+    k_decode<GWAOI_DECODE_PER><<<cdivu(n, ST * GWAOI_DECODE_PER), ST, 0, S->st>>>(A);
 #if GWAOI_DECODE_FUSE
     k_decode_apply<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_dups<<<std::min<uint32_t>(cdivu(n, ST), 64u), ST, 0, S->st>>>(A);
