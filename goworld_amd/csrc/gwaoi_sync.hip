@@ -107,8 +107,8 @@ __global__ void k_scatter128(const W128 *__restrict__ w, uint32_t n, ArrTable T)
 // Per-slot sync state is packed so that one pass touches one line per slot:
 //   sst[s]  uint4 {gate index, space in call order, syncing, sync flags}
 //   cl[s]   ulonglong2 {Position claim, yaw claim}
-//   htab[h] 2 x uint4 {entity id; slot, -, -, -}: an id-table bucket is one 32-B
-//           entry, so a probe reads key and value from the same line.
+//   htab    64-B buckets {3 entity ids; their 3 slots}: a probe reads keys and
+//           values from one line (see lookup).
 enum SstField { SST_GATE = 0, SST_SPACE = 1, SST_SYNCING = 2, SST_FLAGS = 3 };
 
 // Host position/yaw writes (set_position_yaw, entity_set_position_yaw,
@@ -152,7 +152,7 @@ struct DecodeArgs {
     const uint4 *pay;  // 2 uint4 per record: id, (x, y, z, yaw) bits
     uint32_t n;
     const uint4 *htab;
-    uint32_t hmask;
+    uint32_t hmask;  // buckets - 1 (power of two)
     uint32_t *sst;
     uint32_t *o_slot, *o_sp;  // the device Moved batch (SLOT_NONE: no move)
     float *o_x, *o_z;
@@ -168,69 +168,27 @@ struct DecodeArgs {
 #define GWAOI_DECODE_FUSE 1
 #endif
 
-#ifndef GWAOI_PROBE4
-#define GWAOI_PROBE4 2
-#endif
-__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t hmask, uint4 id) {
-    uint32_t h = id_hash(id.x, id.y, id.z, id.w) & hmask;
-#if GWAOI_PROBE4 == 2
-    // One 128-B line (four 32-B buckets, the table is 256-B aligned) per step, the line that
-    // holds h: a match anywhere in it is the key (ids are unique in the table), while an
-    // empty bucket ends the probe sequence only at or after h.
-    uint32_t first = h & 3u;
-    h &= ~3u;
-    for (uint32_t probe = 0; probe <= hmask; probe += 4) {
-        uint4 k[4];
-        uint32_t v[4];
+// The id table: 64-B buckets (one line), three entries each: keys in words 0..11,
+// the three slots in words 12..14 (H_EMPTY never used, H_TOMB freed).  Linear
+// probing over entries e = 3 b + way, so a probe reads one line per step and
+// almost always stops in the first (half the bytes of the 32-B bucket layout).
+__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t bmask, uint4 id) {
+    uint32_t b = id_hash(id.x, id.y, id.z, id.w) & bmask;
+    for (uint32_t probe = 0; probe <= bmask; ++probe, b = (b + 1) & bmask) {
+        uint4 k[3];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            k[q] = htab[2 * (size_t)(h + (uint32_t)q)];
-            v[q] = htab[2 * (size_t)(h + (uint32_t)q) + 1].x;
-        }
+        for (int q = 0; q < 3; ++q) k[q] = htab[4 * (size_t)b + (uint32_t)q];
+        const uint4 m = htab[4 * (size_t)b + 3];
+        const uint32_t v[3] = {m.x, m.y, m.z};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (v[q] != H_EMPTY && v[q] != H_TOMB && eq4(k[q], id)) return v[q];
-            if ((uint32_t)q >= first && v[q] == H_EMPTY) return SLOT_NONE;
-        }
-        first = 0;
-        h = (h + 4u) & hmask;
-    }
-#elif GWAOI_PROBE4
-    // Four buckets per step, loaded together: a wave waits for its longest probe sequence,
-    // and with one dependent load per bucket that tail (not the mean of ~1.5) set the time.
-    for (uint32_t probe = 0; probe <= hmask; probe += 4) {
-        uint4 k[4];
-        uint32_t v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t hq = (h + (uint32_t)q) & hmask;
-            k[q] = htab[2 * (size_t)hq];
-            v[q] = htab[2 * (size_t)hq + 1].x;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < 3; ++q) {
             if (v[q] == H_EMPTY) return SLOT_NONE;
             if (v[q] != H_TOMB && eq4(k[q], id)) return v[q];
         }
-        h = (h + 4u) & hmask;
     }
-#else
-    for (uint32_t probe = 0; probe <= hmask; ++probe, h = (h + 1) & hmask) {
-        const uint4 k = htab[2 * (size_t)h];  // key and value: one 32-B bucket
-        const uint32_t v = htab[2 * (size_t)h + 1].x;
-        if (v == H_EMPTY) return SLOT_NONE;
-        if (v != H_TOMB && eq4(k, id)) return v;
-    }
-#endif
     return SLOT_NONE;
 }
 
-// OnSyncPositionYawFromClient: unknown id -> skip (EntityManager.go:486-490);
-// syncPositionYawFromClient: only if syncing (Entity.go:432).  setPositionYaw
-// (Entity.go:1189-1205) then runs for every entity: e.Space is nilSpace, not
-// nil, outside every space.  In an AOI space it is a Moved (op i of the
-// batch) plus Position; elsewhere Space.move returns before Position
-// (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
 // The record's effects once its slot is known (s: the looked-up slot or SLOT_NONE; st: its
 // slot record when s != SLOT_NONE).
 __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, const uint4 &pv, uint32_t s,
@@ -283,8 +241,7 @@ __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, con
 // nil, outside every space.  In an AOI space it is a Moved (op i of the
 // batch) plus Position; elsewhere Space.move returns before Position
 // (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
-// PER records per thread, strided by the block: every record's first probe line
-// (four 32-B buckets) and then every slot record are loaded before any is used.
+// PER records per thread, strided by the block: every slot record is loaded before any is used.
 template <int PER>
 __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     const uint32_t i0 = blockIdx.x * (ST * PER) + threadIdx.x;
@@ -302,35 +259,8 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
             pv[u] = A.pay[2 * (size_t)i + 1];
         }
     }
-    if (PER == 1) {
-        s[0] = i0 < A.n ? lookup(A.htab, A.hmask, id[0]) : SLOT_NONE;
-    } else {
-        uint4 k[PER][4];
-        uint32_t v[PER][4], h[PER];
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {  // the first probe line of every record
-            h[u] = id_hash(id[u].x, id[u].y, id[u].z, id[u].w) & A.hmask;
-            const uint32_t hb = h[u] & ~3u;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                k[u][q] = A.htab[2 * (size_t)(hb + (uint32_t)q)];
-                v[u][q] = A.htab[2 * (size_t)(hb + (uint32_t)q) + 1].x;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t first = h[u] & 3u;
-            uint32_t r = 0xFFFFFFFEu;  // not decided by the first line
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (r != 0xFFFFFFFEu) continue;
-                if (v[u][q] != H_EMPTY && v[u][q] != H_TOMB && eq4(k[u][q], id[u])) r = v[u][q];
-                else if ((uint32_t)q >= first && v[u][q] == H_EMPTY) r = SLOT_NONE;
-            }
-            if (r == 0xFFFFFFFEu) r = lookup(A.htab, A.hmask, id[u]);  // the probe runs past the line (rare)
-            s[u] = i0 + (uint32_t)u * ST < A.n ? r : SLOT_NONE;
-        }
-    }
+    for (int u = 0; u < PER; ++u) s[u] = i0 + (uint32_t)u * ST < A.n ? lookup(A.htab, A.hmask, id[u]) : SLOT_NONE;
     uint4 st[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u)  // every slot record in flight together
@@ -391,8 +321,14 @@ __global__ __launch_bounds__(ST) void k_decode_apply(DecodeArgs A) {
     const uint4 pv = A.pay[2 * (size_t)i + 1];
     float *p = reinterpret_cast<float *>(A.pos + s);
     const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
+    const bool moves = A.o_sp[i] != SP_DEAD;
+    if (moves && cs.x == c && cs.y == c) {  // the common case: one 16-B store of position and yaw
+        A.pos[s] = make_float4(__uint_as_float(pv.x), __uint_as_float(pv.y), __uint_as_float(pv.z),
+                               __uint_as_float(pv.w));
+        return;
+    }
     bool lost = false;
-    if (A.o_sp[i] != SP_DEAD) {
+    if (moves) {
         if (cs.x == c) {
             p[0] = __uint_as_float(pv.x);
             p[1] = __uint_as_float(pv.y);
@@ -958,8 +894,9 @@ struct SyncState {
     uint32_t oflag_cap = 0;                           // entries of oflag (max_slots)
     bool decoded = false;                           // a decode ran since the last collect
     // id -> slot hash table (device, host mirror)
-    uint4 *htab = nullptr;  // 2 per bucket: key, (slot, -, -, -)
-    uint32_t hcap = 0, hused = 0;  // buckets, live + tombstones
+    uint4 *htab = nullptr;  // 4 per bucket: 3 keys, (slot, slot, slot, -)
+    uint32_t hcap = 0, hused = 0;  // entries (3 per 64-B bucket), live + tombstones
+    uint32_t hbuckets = 0;         // power of two
     std::vector<uint4> h_hkey;
     std::vector<uint32_t> h_hval;
     std::vector<uint4> h_tab;  // rehash upload staging
@@ -1048,8 +985,8 @@ ArrTable table32(SyncState *S) {
     T.p[A_SYNCING] = S->sst + SST_SYNCING;
     T.p[A_SFLAGS] = S->sst + SST_FLAGS;
     for (int a = A_CGATE; a <= A_SFLAGS; ++a) T.stride[a] = 4;
-    T.p[A_HVAL] = reinterpret_cast<uint32_t *>(S->htab + 1);
-    T.stride[A_HVAL] = 8;
+    T.p[A_HVAL] = reinterpret_cast<uint32_t *>(S->htab);  // index: the slot word of an entry (hval_word)
+    T.stride[A_HVAL] = 1;
     return T;
 }
 ArrTable table128(SyncState *S) {
@@ -1058,8 +995,8 @@ ArrTable table128(SyncState *S) {
     T.stride[B_EID] = 1;
     T.p[B_CID] = S->cid;
     T.stride[B_CID] = 1;
-    T.p[B_HKEY] = S->htab;
-    T.stride[B_HKEY] = 2;
+    T.p[B_HKEY] = S->htab;  // index: the key of an entry (hkey_vec)
+    T.stride[B_HKEY] = 1;
     return T;
 }
 
@@ -1142,15 +1079,17 @@ int create(gwaoi_world *w, SyncState **out) {
     S->w = w;
     S->st = v.st;
     S->max_slots = v.max_slots;
-    uint32_t cap = 1024;
-    while (cap < 2ull * v.max_slots) cap <<= 1;
+    uint32_t nbk = 512;  // buckets of three: at least 2 entries per slot
+    while (3ull * nbk < 2ull * v.max_slots) nbk <<= 1;
+    const uint32_t cap = 3 * nbk;
+    S->hbuckets = nbk;
     S->hcap = cap;
     const size_t N = v.max_slots;
     S->oflag_cap = (uint32_t)N;
     int rc;
     if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->sst, 4 * N)) ||
         (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->cl, 2 * N)) || (rc = salloc(S, &S->oflag, N)) ||
-        (rc = salloc(S, &S->oflag_n, 1)) || (rc = salloc(S, &S->htab, 2 * (size_t)cap))) {
+        (rc = salloc(S, &S->oflag_n, 1)) || (rc = salloc(S, &S->htab, 4 * (size_t)nbk))) {
         sync_destroy(S);
         return rc;
     }
@@ -1159,7 +1098,7 @@ int create(gwaoi_world *w, SyncState **out) {
               hipMemsetAsync(S->oflag_n, 0, 4, S->st) == hipSuccess &&
               hipMemsetAsync(S->eid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->cid, 0, N * 16, S->st) == hipSuccess &&
-              hipMemsetAsync(S->htab, 0xFF, (size_t)cap * 32, S->st) == hipSuccess &&  // every slot H_EMPTY
+              hipMemsetAsync(S->htab, 0xFF, (size_t)nbk * 64, S->st) == hipSuccess &&  // every entry H_EMPTY
               hipEventCreateWithFlags(&S->stage_ev, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         sync_destroy(S);
@@ -1202,11 +1141,18 @@ uint4 load_id(const uint8_t *p) {
 
 bool same(const uint4 &a, const uint4 &b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
 
-// bucket of id, or H_EMPTY
+// Entry e of the id table: bucket e / 3, way e % 3 (see lookup).
+uint32_t hkey_vec(uint32_t e) { return 4 * (e / 3) + e % 3; }        // uint4 index of its key
+uint32_t hval_word(uint32_t e) { return 16 * (e / 3) + 12 + e % 3; }  // uint32 index of its slot
+uint32_t h_first(const SyncState *S, const uint4 &id) {  // the probe's first entry
+    return 3 * (id_hash(id.x, id.y, id.z, id.w) & (S->hbuckets - 1));
+}
+uint32_t h_next(const SyncState *S, uint32_t e) { return e + 1 == S->hcap ? 0 : e + 1; }
+
+// entry of id, or H_EMPTY
 uint32_t h_find(const SyncState *S, const uint4 &id) {
-    const uint32_t mask = S->hcap - 1;
-    uint32_t h = id_hash(id.x, id.y, id.z, id.w) & mask;
-    for (uint32_t p = 0; p < S->hcap; ++p, h = (h + 1) & mask) {
+    uint32_t h = h_first(S, id);
+    for (uint32_t p = 0; p < S->hcap; ++p, h = h_next(S, h)) {
         const uint32_t v = S->h_hval[h];
         if (v == H_EMPTY) return H_EMPTY;
         if (v != H_TOMB && same(S->h_hkey[h], id)) return h;
@@ -1218,12 +1164,11 @@ uint32_t h_find(const SyncState *S, const uint4 &id) {
 int h_rehash(SyncState *S) {
     std::fill(S->h_hval.begin(), S->h_hval.end(), H_EMPTY);
     S->hused = 0;
-    const uint32_t mask = S->hcap - 1;
     for (uint32_t s = 0; s < S->max_slots; ++s) {
         if (!S->h_bound[s]) continue;
         const uint4 id = S->h_eid[s];
-        uint32_t h = id_hash(id.x, id.y, id.z, id.w) & mask;
-        while (S->h_hval[h] != H_EMPTY) h = (h + 1) & mask;
+        uint32_t h = h_first(S, id);
+        while (S->h_hval[h] != H_EMPTY) h = h_next(S, h);
         S->h_hkey[h] = id;
         S->h_hval[h] = s;
         S->h_bucket[s] = h;
@@ -1239,10 +1184,10 @@ int h_rehash(SyncState *S) {
         if (e.arr != B_HKEY) k128.push_back(e);
     S->w128.swap(k128);
     if (int rc = push(S)) return rc;
-    S->h_tab.resize(2 * (size_t)S->hcap);
-    for (size_t h = 0; h < S->hcap; ++h) {
-        S->h_tab[2 * h] = S->h_hkey[h];
-        S->h_tab[2 * h + 1] = make_uint4(S->h_hval[h], 0u, 0u, 0u);
+    S->h_tab.assign(4 * (size_t)S->hbuckets, make_uint4(H_EMPTY, H_EMPTY, H_EMPTY, H_EMPTY));
+    for (uint32_t h = 0; h < S->hcap; ++h) {
+        S->h_tab[hkey_vec(h)] = S->h_hkey[h];
+        reinterpret_cast<uint32_t *>(S->h_tab.data())[hval_word(h)] = S->h_hval[h];
     }
     SY_TRY(hipMemcpyAsync(S->htab, S->h_tab.data(), S->h_tab.size() * 16, hipMemcpyHostToDevice, S->st));
     SY_TRY(hipStreamSynchronize(S->st));  // h_tab is pageable staging
@@ -1258,17 +1203,16 @@ int bind_one(SyncState *S, uint32_t slot, const uint4 &id) {
         // too many tombstones (live entries are <= max_slots <= hcap/2)
         if (int rc = h_rehash(S)) return rc;
     }
-    const uint32_t mask = S->hcap - 1;
-    uint32_t h = id_hash(id.x, id.y, id.z, id.w) & mask;
-    while (S->h_hval[h] != H_EMPTY && S->h_hval[h] != H_TOMB) h = (h + 1) & mask;
+    uint32_t h = h_first(S, id);
+    while (S->h_hval[h] != H_EMPTY && S->h_hval[h] != H_TOMB) h = h_next(S, h);
     if (S->h_hval[h] == H_EMPTY) S->hused++;
     S->h_hkey[h] = id;
     S->h_hval[h] = slot;
     S->h_bucket[slot] = h;
     S->h_bound[slot] = 1;
     S->h_eid[slot] = id;
-    put128(S, B_HKEY, h, id);
-    put32(S, A_HVAL, h, slot);
+    put128(S, B_HKEY, hkey_vec(h), id);
+    put32(S, A_HVAL, hval_word(h), slot);
     put128(S, B_EID, slot, id);
     return GWAOI_OK;
 }
@@ -1516,7 +1460,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.pay = pay;
     A.n = (uint32_t)n;
     A.htab = S->htab;
-    A.hmask = S->hcap - 1;
+    A.hmask = S->hbuckets - 1;
     A.sst = S->sst;
     A.o_slot = o_slot;
     A.o_sp = o_sp;
@@ -1611,7 +1555,7 @@ int gwaoi_entity_unbind(gwaoi_world *w, uint32_t slot) {
     if (!S->h_bound[slot]) return GWAOI_ESTATE;
     const uint32_t h = S->h_bucket[slot];
     S->h_hval[h] = gw::H_TOMB;
-    gw::put32(S, gw::A_HVAL, h, gw::H_TOMB);
+    gw::put32(S, gw::A_HVAL, gw::hval_word(h), gw::H_TOMB);
     S->h_bound[slot] = 0;
     S->h_bucket[slot] = gw::H_EMPTY;
     if (S->h_client[slot]) {
