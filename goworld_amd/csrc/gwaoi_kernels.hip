@@ -1085,6 +1085,13 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 // The counts are zeroed as they are read (GWAOI_SCAN_REZERO): the next flush's
 // k_keygen<true> finds them zero, so the prologue no longer clears 2 words per
 // cell (16 MB of 4-B stores at config 3).
+#ifndef GWAOI_ARRIVE_REZERO
+#define GWAOI_ARRIVE_REZERO 0  // 1 (with GWAOI_DELTA_COUNTS): k_arrive re-zeroes the counts of the cells the
+                               // cell changers touched, instead of the scan re-zeroing every cell
+#endif
+#if GWAOI_ARRIVE_REZERO && !GWAOI_DELTA_COUNTS
+#error "GWAOI_ARRIVE_REZERO needs GWAOI_DELTA_COUNTS"
+#endif
 #ifndef GWAOI_SCAN_REZERO
 #define GWAOI_SCAN_REZERO 1
 #endif
@@ -1105,7 +1112,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
     for (int q = 0; q < SC_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
-#if GWAOI_SCAN_REZERO
+#if GWAOI_SCAN_REZERO && !GWAOI_ARRIVE_REZERO
         if (base + j < n) in[base + j] = 0ull;
 #endif
     }
@@ -1160,11 +1167,22 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
 // Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
 // of cell c and ends as that of cell c+1.
 __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
-                         const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx) {
+                         const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
+                         unsigned long long *cnt64) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t key = keys[i];
+#if GWAOI_ARRIVE_REZERO
+    const uint32_t old = i < n_prev ? p_key[i] : sentinel;
+    if (key == old) return;
+    // the cells k_keygen counted this entity in, read by the scan already: zero for the next flush
+    if (key != sentinel) cnt64[key] = 0ull;
+    if (old != sentinel) cnt64[old] = 0ull;
+    if (key == sentinel) return;
+#else
+    (void)cnt64;
     if (key == sentinel || (i < n_prev && p_key[i] == key)) return;
+#endif
     arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
 }
 
@@ -2154,6 +2172,9 @@ __device__ __forceinline__ void sweep_rows_zlds(CombinedLds &L, int w, WaveQueue
 }
 #endif
 
+#ifndef GWAOI_ZPAIR
+#define GWAOI_ZPAIR 0  // 1: the Z strip's (one or two) rows swept as one range per lane too
+#endif
 #ifndef GWAOI_XPAIR
 #define GWAOI_XPAIR 2  // the X' strip's rows swept P at a time as one virtual range per lane (0: one row at a time; 2: combined 0.1095/0.1081 vs 0.1123/0.1120 ms, 3: 0.128, profiles/r03_variants_xpair.log)
 #endif
@@ -2200,8 +2221,8 @@ __device__ __forceinline__ void sweep_segs(CombinedLds &L, int w, WaveQueue &Q, 
     }
 }
 
-// The X' strip's rows, P at a time (sweep_segs); the next group's ranges are loaded first.
-template <int P>
+// A strip's rows, P at a time (sweep_segs); the next group's ranges are loaded first.
+template <int MODE, int P>
 __device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
                                                    int r0, int r1, int c0, int c1, const uint4 *__restrict__ cand,
                                                    const FrameView &F, const Rec16 *__restrict__ O_rec,
@@ -2235,9 +2256,9 @@ __device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQu
 #pragma unroll
         for (int q = 0; q < P; ++q) tot += ln[q];
         if (__ballot(tot > 2))
-            sweep_segs<1, GWAOI_SW_U, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+            sweep_segs<MODE, GWAOI_SW_U, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
         else if (__ballot(tot != 0))
-            sweep_segs<1, 2, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+            sweep_segs<MODE, 2, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             jb[q] = nb[q];
@@ -2409,6 +2430,8 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 #ifndef GWAOI_EXP_NOZ  // timing experiment only: skip the Z strip (events wrong)
 #if GWAOI_ZLDS
         sweep_rows_zlds(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#elif GWAOI_ZPAIR && GWAOI_XPAIR
+        sweep_rows_grouped<0, 2>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
 #elif GWAOI_ZB > 0
         sweep_rows_batched<0, GWAOI_ZB, GWAOI_ZH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
                                                   pl, replay);
@@ -2426,8 +2449,8 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
         }
 #ifndef GWAOI_EXP_NOX  // timing experiment only: skip the X' strip (events wrong)
 #if GWAOI_XPAIR
-        sweep_rows_grouped<GWAOI_XPAIR>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl,
-                                        replay);
+        sweep_rows_grouped<1, GWAOI_XPAIR>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl,
+                                           replay);
 #elif GWAOI_XB > 0
         sweep_rows_batched<1, GWAOI_XB, GWAOI_XH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
                                                   pl, replay);
@@ -3038,7 +3061,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 }
 
 // look-back status words: lo and hi per block
-bool scan_rezeroes_counts() { return GWAOI_SCAN_REZERO != 0; }
+bool scan_rezeroes_counts() { return GWAOI_SCAN_REZERO != 0 || GWAOI_ARRIVE_REZERO != 0; }
 
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, SC_TILE) + 1); }
 
@@ -3051,7 +3074,8 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
     const uint32_t nb = cdiv(m, SC_TILE);
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
                                          cdiv(n_total, 256), sc, p_cell_start);
-    if (n_total) k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx);
+    if (n_total)
+        k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
                                                          n_new, n_total, sentinel, perm, skeys);
 }
