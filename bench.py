@@ -652,7 +652,7 @@ def main():
                     help="ticks of the C++ host tick bench (tools/tick_bench.cpp; 0 = off)")
     ap.add_argument("--cfg4-steps", type=int, default=5,
                     help="cfg3 runs: timed ticks of the config-4 strong-scaling sub-record (0 = off)")
-    ap.add_argument("--cfg4-warmup", type=int, default=2)
+    ap.add_argument("--cfg4-warmup", type=int, default=3)
     ap.add_argument("--serial-issue", action="store_true",
                     help="register tick t+1's move batch only after tick t's flush returned (default: registered "
                          "while the flush of tick t runs, gwaoi_tick_begin/_end, as a game loop receives moves)")
