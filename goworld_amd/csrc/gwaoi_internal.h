@@ -185,7 +185,9 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, hipStream_t st);
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st);
+// special (optional, cdiv(n_prev, TILE_A) words): keygen marks the previous-frame tiles that hold an
+// entity the special pass must look at; launch_pairs skips the others.
 // The stable sort of S' by key when the grid is the previous frame's: the
 // new cell_start (from cnt64) plus, per cell, a merge of the entities that
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
@@ -235,7 +237,7 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
 // block t's totals/bases at [tile_off + t] and [leave_off + tile_off + t].
 void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t seq_base, TickScalars *sc,
                   uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                  uint32_t tile_off, uint32_t leave_off, hipStream_t st);
+                  uint32_t tile_off, uint32_t leave_off, const uint32_t *special, hipStream_t st);
 // The flush's tail in one launch: every tile's events from tmp into tile order
 // (`out` may be host-mapped pinned memory, and hbbox, when given, receives the
 // folded per-space boxes there: the flush summary needs no copy)

@@ -374,11 +374,12 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
-                                                unsigned long long seq_base) {
+                                                unsigned long long seq_base, uint32_t *special) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     float dr = 0.0f, bm = 0.0f;
     uint32_t key = sentinel;
+    bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
     if (i < n) {
         const uint32_t s = ld_ss(s_ss, i).sp;
         if (s != SP_DEAD) {
@@ -391,8 +392,10 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                     r = p;
                 }
                 const float D = p_grid[s].D;
-                if (same && is_near(r.x, r.z, p.x, p.z, FAR_FRAC * D))
+                if (same && is_near(r.x, r.z, p.x, p.z, FAR_FRAC * D)) {
                     dr = fmaxf(fabsf(r.x - p.x), fabsf(r.z - p.z)) / D;
+                    near = true;
+                }
             }
             const SpaceGrid g = grid[s];
             const int cx = cell_of(r.x, g.ox, g.inv, g.gx);
@@ -439,7 +442,10 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         s_m[0][threadIdx.x / WAVE] = dr;
         s_m[1][threadIdx.x / WAVE] = bm;
     }
-    __syncthreads();
+    // the special pass's tile of this block (previous-frame entries [256 b, 256 b + 256)): does it hold
+    // an entity that is not near (left, changed space, jumped)?  k_pairs<1> skips the tiles without
+    const bool sp_any = __syncthreads_or(i < n_prev && !near);
+    if (special && threadIdx.x == 0 && blockIdx.x * 256u < n_prev) special[blockIdx.x] = sp_any ? 1u : 0u;
     if (threadIdx.x == 0) {
         float a = s_m[0][0], b = s_m[1][0];
         for (int q = 1; q < 256 / WAVE; ++q) {
@@ -1504,7 +1510,8 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
                                               const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
                                               unsigned long long *counter, uint2 *tmp, uint64_t cap,
                                               uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
-                                              uint32_t leave_off, uint32_t *dbg) {
+                                              uint32_t leave_off, uint32_t *dbg, const uint32_t *__restrict__ special) {
+    if (MODE == 1 && special && !special[blockIdx.x]) return;  // keygen saw no special entity in this tile
     __shared__ uint4 s_now[PCAP];
     __shared__ uint4 s_oth[PCAP];
     __shared__ uint32_t s_slot[PCAP];
@@ -3047,15 +3054,15 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, hipStream_t st) {
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st) {
     if (!n_total) return;  // the prologue left d_rel = bmax = 0
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64, seq_base);  // folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base, special);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr, seq_base);
+                                            n_prev, blk, nullptr, nullptr, seq_base, special);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }
@@ -3141,11 +3148,11 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
 
 void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t seq_base, TickScalars *sc,
                   uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                  uint32_t tile_off, uint32_t leave_off, hipStream_t st) {
+                  uint32_t tile_off, uint32_t leave_off, const uint32_t *special, hipStream_t st) {
     if (!F.n) return;
     uint2 *tmp = reinterpret_cast<uint2 *>(tmp_pairs);
     k_pairs<1><<<combined_blocks(F.n), PT, 0, st>>>(F, O_rec, O_ss, seq_base, sc, &sc->counter, tmp, cap, tile_total,
-                                                    tile_base, tile_off, leave_off, sc->dbg);
+                                                    tile_base, tile_off, leave_off, sc->dbg, special);
 }
 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,

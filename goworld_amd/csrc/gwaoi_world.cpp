@@ -214,6 +214,7 @@ struct gwaoi_world {
     unsigned long long *cnt64 = nullptr, *scan64_tmp = nullptr;
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
+    uint32_t *special = nullptr;  // per previous-frame tile: keygen saw a special entity (the special pass's skip list)
     uint32_t *mv_hist = nullptr;  // bucketed apply: the bucket-major histogram, scanned (gw::launch_moves_bucketed)
     uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
     bool moves_bucketed = false;   // the bucketed apply (max_slots > MV_MIN_SLOTS; GWAOI_MOVES_BUCKETED forces it)
@@ -749,8 +750,10 @@ uint32_t next_lb_tag(gwaoi_world *w) {
     return w->lb_tag;
 }
 
+// rerun: the flush's pair passes again after an event-buffer overflow; keygen's special-tile
+// flags may belong to a later (speculatively launched) flush by then, so every tile is visited.
 void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
-                        const gw::SlotSp *s_ss_view) {
+                        const gw::SlotSp *s_ss_view, bool rerun = false) {
     hipStream_t st = w->stream;
     const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
@@ -764,7 +767,7 @@ void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, 
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
     stage_begin(w, S, ST_SPECIAL);
     gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn, half,
-                     st);
+                     rerun ? nullptr : w->special, st);
     stage_end(w, S, ST_SPECIAL);
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
     stage_begin(w, S, ST_FINISH);
@@ -943,7 +946,7 @@ int tick_launch(gwaoi_world *w) {
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
     gw::launch_keygen(S.srec, s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, st);
+                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, st);
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;
@@ -1092,7 +1095,7 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
         gw::launch_zero(w->tile_total, f.entries + 1, st);
         gw::launch_zero(reinterpret_cast<uint32_t *>(&S.sc->counter), 2, st);
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
-        launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view);
+        launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true);
         w->dbg.event_regrows++;
         if (hipGetLastError() != hipSuccess ||
             (!GWAOI_DIRECT_SUMMARY &&
@@ -1226,7 +1229,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     }
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
-    dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll);
+    dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll); dfree(w->special);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
     dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
@@ -1337,6 +1340,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
+        (rc = dalloc(w, &w->special, N / 256 + 2)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
