@@ -231,7 +231,11 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
 inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; }
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, hipStream_t st,
+                     hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// tile_order[1 + i] = the tile k_combined's i-th block (xcd_block index) runs, heaviest first per
+// XCD range by tile_work; tile_order[0] = the tile count it was built for (k_combined ignores it otherwise)
+void launch_tile_order(const uint32_t *tile_work, uint32_t n, uint32_t *tile_order, hipStream_t st);
 // Special-entity pass over the previous frame in blocks of TILE_A entries
 // (O = S', the new state in the previous order, with O_ss giving its space);
 // block t's totals/bases at [tile_off + t] and [leave_off + tile_off + t].

@@ -1742,8 +1742,11 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 
 constexpr int CT = 256;
 constexpr int CW = CT / WAVE;
+#ifndef GWAOI_FLAT
+#define GWAOI_FLAT 1  // 1: a row group's candidates of all lanes dealt out evenly over the wave (sweep_flat); 0: lock-step
+#endif
 #ifndef GWAOI_QCAP
-#define GWAOI_QCAP 640
+#define GWAOI_QCAP (GWAOI_FLAT ? 384 : 640)
 #endif
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
@@ -1782,6 +1785,18 @@ typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
 #ifndef GWAOI_ZCAP
 #define GWAOI_ZCAP 192  // candidates per wave in the Z-strip stage (wider unions take the direct loads)
 #endif
+#ifndef GWAOI_FLAT_U
+#define GWAOI_FLAT_U 2  // flat sweep: 64-candidate chunks per iteration
+#endif
+#ifndef GWAOI_XPAIR
+#define GWAOI_XPAIR 2  // the X' strip's rows swept P at a time as one virtual range per lane (0: one row at a time; 2: combined 0.1095/0.1081 vs 0.1123/0.1120 ms, 3: 0.128, profiles/r03_variants_xpair.log)
+#endif
+#ifndef GWAOI_FLAT_NOPERM
+#define GWAOI_FLAT_NOPERM 0  // flat sweep: lanes keep frame order (no work-class regrouping)
+#endif
+#ifndef GWAOI_FLAT_ATAB
+#define GWAOI_FLAT_ATAB 1  // flat sweep: the owner's position from an LDS table (1) or by ds_bpermute (0)
+#endif
 constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= one sweep iteration + a drain batch)
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
 static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
@@ -1789,6 +1804,7 @@ static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
 // A queued pair is (A, B): A is one of the block's own entries, so it is kept
 // as its offset in the block (1 B) next to B's frame index (4 B).  5 B per
 // entry keeps the block under 20 KB of LDS (8 blocks per CU).
+static_assert(CW == 4, "tile work sums four waves");
 constexpr int NCLS = 6;  // lane work classes of k_combined (see lane_class)
 
 struct CombinedLds {
@@ -1801,7 +1817,18 @@ struct CombinedLds {
 #if GWAOI_ZLDS
     uint4 zl[CW][GWAOI_ZCAP];  // Z strip: the union of a wave's candidate ranges of one grid row
 #endif
+#if GWAOI_FLAT
+    uint4 seg[CW][WAVE];                   // flat sweep: a lane's row ranges of the current group (sweep_flat)
+#if GWAOI_XPAIR > 2
+    uint4 seg2[CW][WAVE];                  //   ... rows 3-4 of a group
+#endif
+#if GWAOI_FLAT_ATAB
+    float4 atab[CW][WAVE];                 //   ... the lanes' own positions (x, z, old x, old z)
+#endif
+    uint8_t mark[CW][WAVE * GWAOI_FLAT_U];  //   ... lane + 1 at the flat position where its items start
+#endif
     uint32_t wcnt[CW][2];
+    uint32_t wwork[CW];  // flat sweep: candidates dealt out by each wave (the tile's work, for the next flush's order)
     unsigned long long base;
     uint32_t te, tl;
     int overflow;
@@ -2182,9 +2209,6 @@ __device__ __forceinline__ void sweep_rows_zlds(CombinedLds &L, int w, WaveQueue
 #ifndef GWAOI_ZPAIR
 #define GWAOI_ZPAIR 0  // 1: the Z strip's (one or two) rows swept as one range per lane too
 #endif
-#ifndef GWAOI_XPAIR
-#define GWAOI_XPAIR 2  // the X' strip's rows swept P at a time as one virtual range per lane (0: one row at a time; 2: combined 0.1095/0.1081 vs 0.1123/0.1120 ms, 3: 0.128, profiles/r03_variants_xpair.log)
-#endif
 #if GWAOI_XPAIR
 // sweep_range over P row ranges of a lane taken as one sequence (index select per candidate):
 // the short X' rows share sweep iterations instead of paying one each.
@@ -2228,6 +2252,153 @@ __device__ __forceinline__ void sweep_segs(CombinedLds &L, int w, WaveQueue &Q, 
     }
 }
 
+#if GWAOI_FLAT
+// Inclusive wave-wide scans by DPP (rows of 16 lanes, then the row broadcasts).
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
+    switch (n) {
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    case 4: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    }
+}
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += dpp_shr(v, 1);
+    v += dpp_shr(v, 2);
+    v += dpp_shr(v, 4);
+    v += dpp_shr(v, 8);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, dpp_shr(v, 1));
+    v = max(v, dpp_shr(v, 2));
+    v = max(v, dpp_shr(v, 4));
+    v = max(v, dpp_shr(v, 8));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
+// The candidates of P row ranges per lane, dealt out evenly: the wave's lanes
+// lay their ranges end to end (lane order, then row order) and every lane
+// takes one position of each 64-position chunk.  A position's owner is the
+// last lane whose items start at or before it: each lane with items marks its
+// start (lane + 1) in LDS, and a max-scan over the chunk fills the gaps.  The
+// owner's ranges and its offset come from the wave's table in LDS, its
+// position by ds_bpermute.  Lock-step sweeps pay for the busiest lane of every
+// row (29% of the loaded slots were a lane's own candidates at config 3);
+// here only the last chunk of a group is partial.
+template <int MODE, int P>
+__device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A,
+                                           const uint32_t (&jb)[P], const uint32_t (&ln)[P],
+                                           const uint4 *__restrict__ cand, const FrameView &F,
+                                           const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
+                                           uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
+    static_assert(P >= 1 && P <= 4, "one to four row ranges per lane");
+    constexpr int U = GWAOI_FLAT_U;
+    const uint32_t me = lane();
+    uint32_t cum[P], tot = 0;  // items before row q of this lane
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        cum[q] = tot;
+        tot += ln[q];
+    }
+    const uint32_t inc = wave_scan_add(tot);
+    const uint32_t T = __builtin_amdgcn_readlane(inc, WAVE - 1);
+    if (T == 0) return;
+    if (me == 0 && !replay) L.wwork[w] += T;
+    const uint32_t off = inc - tot;
+    const uint32_t offa = off | ((A.a & (uint32_t)(CT - 1)) << 24);
+    // row q's candidate of lane-local item kk is (jb[q] - cum[q]) + kk, for the last q with cum[q] <= kk
+    if (P <= 2) {
+        L.seg[w][me] = make_uint4(jb[0], P == 2 ? jb[P - 1] - cum[P - 1] : 0u, P == 2 ? cum[P - 1] : 0xFFFFFFFFu, offa);
+    } else {
+#if GWAOI_XPAIR > 2
+        L.seg[w][me] = make_uint4(jb[0], jb[1] - cum[1], jb[2] - cum[2], P > 3 ? jb[P - 1] - cum[P - 1] : 0u);
+        L.seg2[w][me] = make_uint4(cum[1], cum[2], P > 3 ? cum[P - 1] : 0xFFFFFFFFu, offa);
+#endif
+    }
+#if GWAOI_FLAT_ATAB
+    L.atab[w][me] = make_float4(A.x, A.z, A.xo, A.zo);
+#endif
+    uint8_t *mk = L.mark[w];
+    uint32_t carry = 0;  // owner + 1 of the position before this chunk
+    for (uint32_t g0 = 0; g0 < T; g0 += U * WAVE) {
+        if (Q.qn > QCAP - U * WAVE) {
+            if (!replay && me == 0) atomicAdd(&L.ndrain, 1u);
+            __builtin_amdgcn_wave_barrier();
+            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
+                        cap, pe, pl, replay);
+            Q.qn = 0;
+        }
+        if (me < (uint32_t)(U * WAVE / 4)) reinterpret_cast<uint32_t *>(mk)[me] = 0u;
+        if (tot != 0 && off >= g0 && off < g0 + (uint32_t)(U * WAVE)) mk[off - g0] = (uint8_t)(me + 1u);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t own[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) own[u] = wave_scan_max(mk[u * WAVE + me]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            own[u] = max(own[u], carry);
+            carry = __builtin_amdgcn_readlane(own[u], WAVE - 1);
+        }
+        __builtin_amdgcn_wave_barrier();  // the marks are read before the next chunk clears them
+        uint4 k[U];
+        uint32_t bi[U], ao[U];
+        float ax[U], az[U], axo[U], azo[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t p = g0 + (uint32_t)(u * WAVE) + me;
+            const uint32_t o = (own[u] - 1u) & (uint32_t)(WAVE - 1);
+            const uint4 s = L.seg[w][o];
+            uint32_t idx;
+            if (P <= 2) {
+                const uint32_t kk = p - (s.w & 0xFFFFFFu);
+                idx = (kk >= s.z ? s.y : s.x) + kk;
+                ao[u] = s.w >> 24;
+            } else {
+#if GWAOI_XPAIR > 2
+                const uint4 s2 = L.seg2[w][o];
+                const uint32_t kk = p - (s2.w & 0xFFFFFFu);
+                uint32_t base = kk >= s2.x ? s.y : s.x;
+                base = kk >= s2.y ? s.z : base;
+                base = kk >= s2.z ? s.w : base;
+                idx = base + kk;
+                ao[u] = s2.w >> 24;
+#endif
+            }
+            bi[u] = p < T ? idx : 0u;
+#if GWAOI_FLAT_ATAB
+            const float4 ap = L.atab[w][o];
+            ax[u] = ap.x;
+            az[u] = ap.y;
+            axo[u] = ap.z;
+            azo[u] = ap.w;
+#else
+            ax[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.x)));
+            az[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.z)));
+            axo[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.xo)));
+            azo[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.zo)));
+#endif
+            k[u] = cand[bi[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            LaneA B;
+            B.a = 0;
+            B.x = ax[u];
+            B.z = az[u];
+            B.xo = axo[u];
+            B.zo = azo[u];
+            const bool keep = band_keep<MODE>(B, C, k[u], bi[u]) & (g0 + (uint32_t)(u * WAVE) + me < T);
+            qpush(L.qb[w], L.qa[w], Q, keep, ao[u], bi[u]);
+        }
+    }
+}
+#endif
+
 // A strip's rows, P at a time (sweep_segs); the next group's ranges are loaded first.
 template <int MODE, int P>
 __device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
@@ -2259,6 +2430,12 @@ __device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQu
                 nl[q] = cs[rb + span] - nb[q];
             }
         }
+#if GWAOI_FLAT
+        if (MODE != 2) {
+            sweep_flat<MODE, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        } else
+#endif
+        {
         uint32_t tot = 0;
 #pragma unroll
         for (int q = 0; q < P; ++q) tot += ln[q];
@@ -2266,6 +2443,7 @@ __device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQu
             sweep_segs<MODE, GWAOI_SW_U, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
         else if (__ballot(tot != 0))
             sweep_segs<MODE, 2, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+        }
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             jb[q] = nb[q];
@@ -2437,7 +2615,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 #ifndef GWAOI_EXP_NOZ  // timing experiment only: skip the Z strip (events wrong)
 #if GWAOI_ZLDS
         sweep_rows_zlds(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#elif GWAOI_ZPAIR && GWAOI_XPAIR
+#elif (GWAOI_ZPAIR || GWAOI_FLAT) && GWAOI_XPAIR
         sweep_rows_grouped<0, 2>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
 #elif GWAOI_ZB > 0
         sweep_rows_batched<0, GWAOI_ZB, GWAOI_ZH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
@@ -2489,23 +2667,35 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
 // spaces (small spaces) sweeps once per distinct space among a wave's lanes.
 #ifndef GWAOI_COMBINED_WPE
-#define GWAOI_COMBINED_WPE 8  // waves_per_eu: 62 VGPRs, 8 waves per SIMD with the context in SGPRs (0.120 vs 0.123 ms at 7 waves)
+#define GWAOI_COMBINED_WPE (GWAOI_FLAT ? 7 : 8)  // flat: 68 VGPRs without spills; lock-step: waves_per_eu: 62 VGPRs, 8 waves per SIMD with the context in SGPRs (0.120 vs 0.123 ms at 7 waves)
 #endif
 #if GWAOI_COMBINED_WPE
 #define COMBINED_ATTR __attribute__((amdgpu_waves_per_eu(GWAOI_COMBINED_WPE)))
 #else
 #define COMBINED_ATTR
 #endif
+#ifdef GWAOI_EXP_BLOCKTIME
+constexpr uint32_t BT_MAX = 65536;
+__device__ unsigned long long gw_blocktime[3 * BT_MAX];
+#endif
 __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, const uint4 *__restrict__ cand,
                                                  const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
                                                  const TickScalars *__restrict__ sc, unsigned long long *counter,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
-                                                 unsigned long long *tile_base, uint32_t leave_off, uint32_t *dbg) {
+                                                 unsigned long long *tile_base, uint32_t leave_off, uint32_t *dbg,
+                                                 const uint32_t *__restrict__ tile_order, uint32_t *tile_work) {
     __shared__ CombinedLds L;
-    const uint32_t t = xcd_block(blockIdx.x, gridDim.x);
+#ifdef GWAOI_EXP_BLOCKTIME
+    const unsigned long long bt0 = wall_clock64();
+#endif
+    // Tiles run heaviest first within each XCD's range when the previous flush left an order for
+    // this tile count (k_tile_order); any order gives the same events.
+    uint32_t t = xcd_block(blockIdx.x, gridDim.x);
+    if (tile_order && tile_order[0] == gridDim.x) t = tile_order[1 + t];
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
     const uint32_t e0 = t * CT;
+    if (tid < CW) L.wwork[tid] = 0;
     if (tid == 0) {
         L.overflow = 0;
         L.ndrain = 0;
@@ -2519,6 +2709,9 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     // cells per row (either happens to ~1 entity in 6, so a wave of mixed
     // lanes would pay the longer shape for all), or a whole-window sweep.
     uint32_t off = tid;
+#if GWAOI_FLAT_NOPERM  // the flat sweeps deal a wave's candidates out evenly: lane order does not matter to them
+    if (false)
+#endif
     {
         const uint32_t a = e0 + tid;
         uint32_t cls = NCLS - 1;  // past the frame
@@ -2638,6 +2831,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         L.te = se;
         L.tl = sl;
         if (L.ndrain) atomicAdd(dbg + DBG_COMBINED_DRAIN, L.ndrain);
+        if (tile_work) tile_work[t] = L.wwork[0] + L.wwork[1] + L.wwork[2] + L.wwork[3] + CT;
         const uint32_t tot = 2 * (se + sl);
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
         L.base = b;
@@ -2675,6 +2869,15 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         uint32_t re = 0, rl = 0;
         run(true, out, pe, pl, re, rl);
     }
+#ifdef GWAOI_EXP_BLOCKTIME  // diagnostics build only: per-block start/end (wall clock) and hardware ids
+    __syncthreads();
+    if (tid == 0 && t < BT_MAX) {
+        gw_blocktime[3 * t] = bt0;
+        gw_blocktime[3 * t + 1] = wall_clock64();
+        gw_blocktime[3 * t + 2] = (unsigned long long)__smid() | ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32) |
+                                  ((unsigned long long)blockIdx.x << 40);
+    }
+#endif
 }
 
 // ------------------------------------------------------------- finish ------
@@ -3157,13 +3360,51 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, hipStream_t st,
+                     hipEvent_t ev0, hipEvent_t ev1) {
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and
     // end: no marker packets between kernels when the stage is timed
     hipExtLaunchKernelGGL(k_combined, dim3(combined_blocks(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
                           (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
-                          reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg);
+                          reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,
+                          tile_order, tile_work);
+}
+
+// The next flush's tile order: within each XCD's range of tiles (xcd_block), heaviest first by
+// this flush's work per tile, as a counting sort over 64 log-spaced work classes.  Only the
+// schedule changes; k_combined's events do not depend on it.
+constexpr int TO_T = 1024, TO_NB = 64;
+__global__ __launch_bounds__(TO_T) void k_tile_order(const uint32_t *__restrict__ tile_work, uint32_t nb,
+                                                     uint32_t *tile_order) {
+    __shared__ uint32_t hist[TO_NB];
+    const uint32_t x = blockIdx.x, q = nb / N_XCD, r = nb % N_XCD;
+    const uint32_t lo = x * q + min(x, r), hi = lo + q + (x < r ? 1u : 0u);
+    if (threadIdx.x < TO_NB) hist[threadIdx.x] = 0;
+    __syncthreads();
+    auto cls = [&](uint32_t v) {  // descending: class 0 = heaviest
+        const int c = (int)(8.0f * __log2f((float)v + 1.0f)) - 40;
+        return (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
+    };
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += TO_T) atomicAdd(&hist[cls(tile_work[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int c = 0; c < TO_NB; ++c) {
+            const uint32_t v = hist[c];
+            hist[c] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += TO_T)
+        tile_order[1 + lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
+    if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
+}
+
+void launch_tile_order(const uint32_t *tile_work, uint32_t n, uint32_t *tile_order, hipStream_t st) {
+    if (!n) return;
+    k_tile_order<<<N_XCD, TO_T, 0, st>>>(tile_work, combined_blocks(n), tile_order);
 }
 
 size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }
@@ -3187,3 +3428,9 @@ void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t
 }
 
 }  // namespace gw
+
+#ifdef GWAOI_EXP_BLOCKTIME
+extern "C" __attribute__((visibility("default"))) int gwaoi_debug_blocktime(unsigned long long *host, size_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gw::gw_blocktime), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
