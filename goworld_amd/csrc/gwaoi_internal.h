@@ -229,6 +229,12 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
 // Directed event pairs go to tmp at an atomically reserved offset per block;
 // block t's enter total/base are at [t], its leave total/base at [leave_off + t].
 inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; }
+#ifndef GWAOI_CT
+#define GWAOI_CT 256
+#endif
+// entities per k_combined tile (= threads per workgroup; the special pass keeps TILE_A)
+constexpr uint32_t COMBINED_TILE = GWAOI_CT;
+inline uint32_t combined_tiles(uint32_t n) { return (n + COMBINED_TILE - 1) / COMBINED_TILE; }
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, hipStream_t st,

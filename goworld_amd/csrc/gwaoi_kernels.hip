@@ -1740,7 +1740,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 // buffered per wave in processing order (deterministic); a wave whose buffer
 // overflows replays its sweep and writes the rest straight to the output.
 
-constexpr int CT = 256;
+constexpr int CT = (int)COMBINED_TILE;
 constexpr int CW = CT / WAVE;
 #ifndef GWAOI_FLAT
 #define GWAOI_FLAT 1  // 1: a row group's candidates of all lanes dealt out evenly over the wave (sweep_flat); 0: lock-step
@@ -1791,6 +1791,9 @@ typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
 #ifndef GWAOI_XPAIR
 #define GWAOI_XPAIR 2  // the X' strip's rows swept P at a time as one virtual range per lane (0: one row at a time; 2: combined 0.1095/0.1081 vs 0.1123/0.1120 ms, 3: 0.128, profiles/r03_variants_xpair.log)
 #endif
+#ifndef GWAOI_FLAT_MERGE
+#define GWAOI_FLAT_MERGE 1  // flat sweep: both strips' rows in one list (union band, MODE 3)
+#endif
 #ifndef GWAOI_FLAT_NOPERM
 #define GWAOI_FLAT_NOPERM 0  // flat sweep: lanes keep frame order (no work-class regrouping)
 #endif
@@ -1804,7 +1807,6 @@ static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
 // A queued pair is (A, B): A is one of the block's own entries, so it is kept
 // as its offset in the block (1 B) next to B's frame index (4 B).  5 B per
 // entry keeps the block under 20 KB of LDS (8 blocks per CU).
-static_assert(CW == 4, "tile work sums four waves");
 constexpr int NCLS = 6;  // lane work classes of k_combined (see lane_class)
 
 struct CombinedLds {
@@ -1998,11 +2000,13 @@ __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, 
     // and at t-1 (both members near: each moved <= d_rel D per axis), so the unchanged-relation
     // test below drops it anyway.
     (void)hi;
-    const bool band = MODE == 0 ? (int)(dz >= lo) : (int)(dx >= lo) & (int)(fabsf(dz) <= C.lo_in);
+    const bool bz = (int)(dz >= lo), bx = (int)(dx >= lo) & (int)(fabsf(dz) <= C.lo_in);
 #else
-    const bool band = MODE == 0 ? (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi)
-                                : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
+    const bool bz = (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi),
+               bx = (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
 #endif
+    // MODE 3: the rows of both strips in one sweep, either band (the strips stay disjoint)
+    const bool band = MODE == 0 ? bz : MODE == 1 ? bx : (bool)((int)bz | (int)bx);
     const float dn = fmaxf(fabsf(dx), fabsf(dz));
 #if GWAOI_PK_SUB
     const f32x2_t do2 = f32x2_t{__uint_as_float(k.z), __uint_as_float(k.w)} - f32x2_t{A.xo, A.zo};
@@ -2594,6 +2598,49 @@ __device__ __forceinline__ void sweep_rows_batched(CombinedLds &L, int w, WaveQu
 #define GWAOI_ZH 4
 #endif
 
+#if GWAOI_FLAT_MERGE
+// Both strips as one list of rows per lane, swept flat P rows at a time with the union band
+// (MODE 3): the X' rows below the Z strip's first row, then the Z rows.  The row the two strips
+// share is swept once, over the Z strip's wider cells, where the union band finds both kinds.
+template <int P>
+__device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
+                                                  int zr0, int zr1, int zc0, int zc1, int xr0, int xr1, int xc0,
+                                                  int xc1, const uint4 *__restrict__ cand, const FrameView &F,
+                                                  const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
+                                                  uint64_t cap, unsigned long long pe, unsigned long long pl,
+                                                  bool replay) {
+    const int xe = min(xr1, zr0 - 1);
+    const uint32_t nx = on && xe >= xr0 ? (uint32_t)(xe - xr0 + 1) : 0u;
+    const uint32_t nr = on ? nx + (uint32_t)(zr1 - zr0 + 1) : 0u;
+    const uint32_t *cs = F.cell_start;
+    const uint32_t gx = C.g.gx;
+    const uint32_t xb = C.g.base + (uint32_t)xr0 * gx + (uint32_t)xc0, xs = (uint32_t)(xc1 - xc0) + 1u;
+    const uint32_t zb = C.g.base + (uint32_t)zr0 * gx + (uint32_t)zc0, zs = (uint32_t)(zc1 - zc0) + 1u;
+    auto range = [&](uint32_t q, uint32_t &b, uint32_t &l) {
+        b = l = 0;
+        if (q < nr) {
+            const uint32_t rb = q < nx ? xb + q * gx : zb + (q - nx) * gx;
+            b = cs[rb];
+            l = cs[rb + (q < nx ? xs : zs)] - b;
+        }
+    };
+    uint32_t jb[P], ln[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) range((uint32_t)q, jb[q], ln[q]);
+    for (uint32_t k = 0; __ballot(k < nr); k += P) {
+        uint32_t nb[P], nl[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) range(k + P + (uint32_t)q, nb[q], nl[q]);  // the next group's ranges
+        sweep_flat<3, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            jb[q] = nb[q];
+            ln[q] = nl[q];
+        }
+    }
+}
+#endif
+
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
                                uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
@@ -2603,6 +2650,23 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
     const float lo = C.lo, hi = C.hi, M = C.M;
     const bool strip = A.valid && !A.jump && C.band_ok;
     const bool whole = A.valid && (A.jump || !C.band_ok);
+#if GWAOI_FLAT_MERGE
+    if (__ballot(strip)) {
+        int zr0 = 0, zr1 = -1, zc0 = 0, zc1 = -1, xr0 = 0, xr1 = -1, xc0 = 0, xc1 = -1;
+        if (strip) {
+            zr0 = cell_of(A.z + lo - M, g.oz, g.inv, g.gz);
+            zr1 = cell_of(A.z + hi + M, g.oz, g.inv, g.gz);
+            zc0 = cell_of(A.x - hi - M, g.ox, g.inv, g.gx);
+            zc1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
+            xr0 = cell_of(A.z - lo - M, g.oz, g.inv, g.gz);
+            xr1 = cell_of(A.z + lo + M, g.oz, g.inv, g.gz);
+            xc0 = cell_of(A.x + lo - M, g.ox, g.inv, g.gx);
+            xc1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
+        }
+        sweep_rows_merged<GWAOI_XPAIR>(L, w, Q, A, strip, zr0, zr1, zc0, zc1, xr0, xr1, xc0, xc1, cand, F, O_rec, C,
+                                       out, cap, pe, pl, replay);
+    }
+#else
     if (__ballot(strip)) {
         // Z strip: rows holding z in [z+lo, z+hi], cells holding x in [x-hi, x+hi]
         int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
@@ -2644,6 +2708,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 #endif
 #endif
     }
+#endif
     if (__ballot(whole)) {
         const float r = hi + M;
         int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
@@ -2831,7 +2896,11 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         L.te = se;
         L.tl = sl;
         if (L.ndrain) atomicAdd(dbg + DBG_COMBINED_DRAIN, L.ndrain);
-        if (tile_work) tile_work[t] = L.wwork[0] + L.wwork[1] + L.wwork[2] + L.wwork[3] + CT;
+        if (tile_work) {
+            uint32_t wk = CT;
+            for (int q = 0; q < CW; ++q) wk += L.wwork[q];
+            tile_work[t] = wk;
+        }
         const uint32_t tot = 2 * (se + sl);
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
         L.base = b;
@@ -3365,7 +3434,7 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and
     // end: no marker packets between kernels when the stage is timed
-    hipExtLaunchKernelGGL(k_combined, dim3(combined_blocks(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
+    hipExtLaunchKernelGGL(k_combined, dim3(combined_tiles(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
                           (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,
                           tile_order, tile_work);
@@ -3404,7 +3473,7 @@ __global__ __launch_bounds__(TO_T) void k_tile_order(const uint32_t *__restrict_
 
 void launch_tile_order(const uint32_t *tile_work, uint32_t n, uint32_t *tile_order, hipStream_t st) {
     if (!n) return;
-    k_tile_order<<<N_XCD, TO_T, 0, st>>>(tile_work, combined_blocks(n), tile_order);
+    k_tile_order<<<N_XCD, TO_T, 0, st>>>(tile_work, combined_tiles(n), tile_order);
 }
 
 size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }

@@ -758,7 +758,7 @@ uint32_t next_lb_tag(gwaoi_world *w) {
 void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
                         const gw::SlotSp *s_ss_view, bool rerun = false) {
     hipStream_t st = w->stream;
-    const uint32_t TBn = gw::combined_blocks(Fn.n), TBp = gw::combined_blocks(P.n);
+    const uint32_t TBn = gw::combined_tiles(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
     // the pair passes may emit min(set capacity, scratch capacity) pairs; more is an overflow (re-run)
@@ -820,7 +820,7 @@ int tick_launch(gwaoi_world *w) {
     uint32_t total_cells = 0, total_rows = 0;
     choose_grids(w, total_cells, total_rows);
     for (uint32_t s = 0; s < w->n_space_ids; ++s) w->spaces[s].pend = false;  // consumed by this grid
-    const size_t entries = 2 * ((size_t)gw::combined_blocks(n_new) + gw::combined_blocks(n_prev));
+    const size_t entries = 2 * ((size_t)gw::combined_tiles(n_new) + gw::combined_blocks(n_prev));
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
     // a set whose twin grew on an overflow grows alike before its next flush (one re-run, not two)
@@ -1346,8 +1346,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
-        (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / 256 + 2)) ||
-        (rc = dalloc(w, &w->tile_order, N / 256 + 3)) ||
+        (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / gw::COMBINED_TILE + 2)) ||
+        (rc = dalloc(w, &w->tile_order, N / gw::COMBINED_TILE + 3)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess) return fail(GWAOI_EDEVICE);  // no order yet
@@ -1366,7 +1366,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         if ((rc = dalloc(w, &w->mv_hist, mv_hist_n)) || (rc = dalloc(w, &w->mv_binned, N))) return fail(rc);
     }
     if ((rc = ensure_scan_tmp(w, std::max(gw::radix_hist_elems((uint32_t)N), mv_hist_n)))) return fail(rc);
-    if ((rc = ensure_tile_entries(w, 4 * (size_t)gw::combined_blocks((uint32_t)N)))) return fail(rc);
+    if ((rc = ensure_tile_entries(w, 2 * ((size_t)gw::combined_tiles((uint32_t)N) + gw::combined_blocks((uint32_t)N)))))
+        return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     for (FlushSet &S : w->fs)
         if ((rc = ensure_events(w, S, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
