@@ -237,7 +237,8 @@ constexpr uint32_t COMBINED_TILE = GWAOI_CT;
 inline uint32_t combined_tiles(uint32_t n) { return (n + COMBINED_TILE - 1) / COMBINED_TILE; }
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, hipStream_t st,
+                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,
+                     hipStream_t st,
                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // tile_order[1 + i] = the tile k_combined's i-th block (xcd_block index) runs, heaviest first per
 // XCD range by tile_work; tile_order[0] = the tile count it was built for (k_combined ignores it otherwise)

@@ -1794,6 +1794,9 @@ typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
 #ifndef GWAOI_FLAT_MERGE
 #define GWAOI_FLAT_MERGE 1  // flat sweep: both strips' rows in one list (union band, MODE 3)
 #endif
+#ifndef GWAOI_DEAL
+#define GWAOI_DEAL GWAOI_FLAT  // a block's entries ranked by last flush's work and dealt round-robin to its waves (flat: combined 0.091 -> 0.080 ms)
+#endif
 #ifndef GWAOI_FLAT_NOPERM
 #define GWAOI_FLAT_NOPERM 0  // flat sweep: lanes keep frame order (no work-class regrouping)
 #endif
@@ -1807,7 +1810,7 @@ static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
 // A queued pair is (A, B): A is one of the block's own entries, so it is kept
 // as its offset in the block (1 B) next to B's frame index (4 B).  5 B per
 // entry keeps the block under 20 KB of LDS (8 blocks per CU).
-constexpr int NCLS = 6;  // lane work classes of k_combined (see lane_class)
+constexpr int NCLS = GWAOI_DEAL ? 14 : 6;  // lane work classes of k_combined
 
 struct CombinedLds {
     uint32_t ndrain;        // mid-sweep queue drains of the block (DBG_COMBINED_DRAIN)
@@ -1921,6 +1924,7 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) 
 struct WaveQueue {
     uint32_t qn;
     uint32_t ne, nl;
+    uint32_t lw;  // per lane: candidates of this lane's ranges (flat sweep; the next flush's deal)
 };
 
 // Append (a, b) for the lanes with keep set.  Wave-uniform.
@@ -2313,6 +2317,7 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
     const uint32_t T = __builtin_amdgcn_readlane(inc, WAVE - 1);
     if (T == 0) return;
     if (me == 0 && !replay) L.wwork[w] += T;
+    Q.lw += tot;
     const uint32_t off = inc - tot;
     const uint32_t offa = off | ((A.a & (uint32_t)(CT - 1)) << 24);
     // row q's candidate of lane-local item kk is (jb[q] - cum[q]) + kk, for the last q with cum[q] <= kk
@@ -2643,10 +2648,11 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
 
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
-                               uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
+                               uint32_t &lw, uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
+                               bool replay) {
     const int w = threadIdx.x / WAVE;
     const SpaceGrid &g = C.g;
-    WaveQueue Q{0u, ne, nl};
+    WaveQueue Q{0u, ne, nl, lw};
     const float lo = C.lo, hi = C.hi, M = C.M;
     const bool strip = A.valid && !A.jump && C.band_ok;
     const bool whole = A.valid && (A.jump || !C.band_ok);
@@ -2727,6 +2733,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
     }
     ne = Q.ne;
     nl = Q.nl;
+    lw = Q.lw;
 }
 
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
@@ -2748,7 +2755,8 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
                                                  const TickScalars *__restrict__ sc, unsigned long long *counter,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
                                                  unsigned long long *tile_base, uint32_t leave_off, uint32_t *dbg,
-                                                 const uint32_t *__restrict__ tile_order, uint32_t *tile_work) {
+                                                 const uint32_t *__restrict__ tile_order, uint32_t *tile_work,
+                                                 uint32_t *ework) {
     __shared__ CombinedLds L;
 #ifdef GWAOI_EXP_BLOCKTIME
     const unsigned long long bt0 = wall_clock64();
@@ -2767,12 +2775,14 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     }
     __syncthreads();
 
-    // Lanes sweep in lock-step, so a wave runs as long as its busiest lane: the
-    // block's entries are regrouped by work class (stable), and lane tid takes
-    // entry e0 + perm[tid].  The class is the shape of the entity's strips:
-    // whether the Z strip spans two grid rows and whether the X' strip spans two
-    // cells per row (either happens to ~1 entity in 6, so a wave of mixed
-    // lanes would pay the longer shape for all), or a whole-window sweep.
+    // A block holds its LDS until its slowest wave ends, so the waves get equal
+    // work: the block's entries are ranked by the candidates their lanes swept
+    // last flush (stable, by ballots over log2 classes) and dealt round-robin,
+    // rank r to wave r mod 4; lane tid takes entry e0 + perm[tid] (GWAOI_DEAL).
+    // Lock-step sweeps (GWAOI_FLAT=0) run a wave as long as its busiest lane
+    // instead, so there the class is the shape of the entity's strips: whether
+    // the Z strip spans two grid rows and whether the X' strip spans two cells
+    // per row (either happens to ~1 entity in 6), or a whole-window sweep.
     uint32_t off = tid;
 #if GWAOI_FLAT_NOPERM  // the flat sweeps deal a wave's candidates out evenly: lane order does not matter to them
     if (false)
@@ -2780,7 +2790,17 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     {
         const uint32_t a = e0 + tid;
         uint32_t cls = NCLS - 1;  // past the frame
+#if GWAOI_DEAL
+        // by the work this entry's lane had last flush (the frame index then held about the same
+        // entity), heaviest first, dealt round-robin to the waves below
         if (a < F.n) {
+            const uint32_t wk = ework ? ework[a] : 0u;
+            cls = (uint32_t)(NCLS - 2) - min((uint32_t)(NCLS - 2), (uint32_t)(31 - __clz((int)(wk | 1u))));
+        }
+        if (false) {
+#else
+        if (a < F.n) {
+#endif
 #if GWAOI_CAND_SPLIT
             const uint2 c0 = reinterpret_cast<const uint2 *>(cand)[a];
 #else
@@ -2810,6 +2830,9 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         for (int c = 0; c < NCLS; ++c)
             for (int q = 0; q < CW; ++q)
                 if ((uint32_t)c < cls || ((uint32_t)c == cls && q < w)) pos += L.ccnt[c][q];
+#if GWAOI_DEAL
+        pos = (pos & (uint32_t)(CW - 1)) * WAVE + pos / CW;  // rank r goes to wave r mod CW
+#endif
         L.perm[pos] = (uint8_t)tid;
         __syncthreads();
         off = L.perm[tid];  // (measured: combined 0.135 ms vs 0.148 in frame order)
@@ -2834,6 +2857,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     const uint32_t my_sp = ld_ss(F.ss, ia).sp;
 
     uint32_t ne = 0, nl = 0;  // wave totals (wave-uniform)
+    uint32_t lw = 0;          // this lane's candidates
     // sweep once per distinct space in this wave (almost always one)
     auto run = [&](bool replay, uint2 *o, unsigned long long pe, unsigned long long pl, uint32_t &e,
                    uint32_t &l) {
@@ -2872,10 +2896,13 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.proto.chg = false;
             LaneA B = A;
             B.valid = mine;
-            combined_sweep(L, B, cand, F, O_rec, C, e, l, o, cap, pe, pl, replay);
+            combined_sweep(L, B, cand, F, O_rec, C, e, l, lw, o, cap, pe, pl, replay);
         }
     };
     run(false, nullptr, 0ull, 0ull, ne, nl);
+#if GWAOI_DEAL
+    if (ework && A.valid) ework[A.a] = lw;
+#endif
     if (ln == 0) {
         L.wcnt[w][0] = ne;
         L.wcnt[w][1] = nl;
@@ -3429,15 +3456,15 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, hipStream_t st,
-                     hipEvent_t ev0, hipEvent_t ev1) {
+                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,
+                     hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and
     // end: no marker packets between kernels when the stage is timed
     hipExtLaunchKernelGGL(k_combined, dim3(combined_tiles(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
                           (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,
-                          tile_order, tile_work);
+                          tile_order, tile_work, ework);
 }
 
 // The next flush's tile order: within each XCD's range of tiles (xcd_block), heaviest first by

@@ -217,6 +217,7 @@ struct gwaoi_world {
     uint32_t *special = nullptr;  // per previous-frame tile: keygen saw a special entity (the special pass's skip list)
     uint32_t *tile_work = nullptr;   // per combined tile: candidates swept this flush (k_combined)
     uint32_t *tile_order = nullptr;  // the next flush's combined tile order, heaviest first (k_tile_order)
+    uint32_t *ework = nullptr;       // per frame entry: candidates its lane swept (the next flush's deal to waves)
     bool tile_order_on = true;       // GWAOI_TILE_ORDER=0: tiles in xcd_block order
     uint32_t *mv_hist = nullptr;  // bucketed apply: the bucket-major histogram, scanned (gw::launch_moves_bucketed)
     uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
@@ -767,7 +768,8 @@ void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, 
     const bool tc = w->timing_mask >> ST_COMBINED & 1u;
     if (tc) S.ev_used[ST_COMBINED] = true;
     gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, half,
-                        w->tile_order_on ? w->tile_order : nullptr, w->tile_order_on ? w->tile_work : nullptr, st,
+                        w->tile_order_on ? w->tile_order : nullptr, w->tile_order_on ? w->tile_work : nullptr, w->ework,
+                        st,
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
     if (w->tile_order_on) gw::launch_tile_order(w->tile_work, Fn.n, w->tile_order, st);
     stage_begin(w, S, ST_SPECIAL);
@@ -1235,7 +1237,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
     dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll); dfree(w->special);
-    dfree(w->tile_work); dfree(w->tile_order);
+    dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
     dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
@@ -1347,10 +1349,12 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / gw::COMBINED_TILE + 2)) ||
-        (rc = dalloc(w, &w->tile_order, N / gw::COMBINED_TILE + 3)) ||
+        (rc = dalloc(w, &w->tile_order, N / gw::COMBINED_TILE + 3)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
-    if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess) return fail(GWAOI_EDEVICE);  // no order yet
+    if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess ||  // no order yet
+        hipMemset(w->ework, 0, N * sizeof(uint32_t)) != hipSuccess)
+        return fail(GWAOI_EDEVICE);
     if (const char *e = std::getenv("GWAOI_TILE_ORDER")) w->tile_order_on = e[0] != '0';
     // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
     if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
