@@ -241,8 +241,8 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
                      hipStream_t st,
                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // tile_order[1 + i] = the tile k_combined's i-th block (xcd_block index) runs, heaviest first per
-// XCD range by tile_work; tile_order[0] = the tile count it was built for (k_combined ignores it otherwise)
-void launch_tile_order(const uint32_t *tile_work, uint32_t n, uint32_t *tile_order, hipStream_t st);
+// XCD range by tile_work; tile_order[0] = the tile count it was built for (k_combined ignores it
+// otherwise).  launch_finish builds it for the next flush when given the buffers.
 // Special-entity pass over the previous frame in blocks of TILE_A entries
 // (O = S', the new state in the previous order, with O_ss giving its space);
 // block t's totals/bases at [tile_off + t] and [leave_off + tile_off + t].
@@ -259,7 +259,8 @@ size_t finish_lb_elems(size_t n_entries);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, hipStream_t st);
+                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
+                   hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,

@@ -2990,14 +2990,52 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 constexpr int FT = GWAOI_FT;  // tile entries per finish block (<= 64: one wave scans them)
 static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 
+// The next flush's combined tile order (k_finish's last N_XCD blocks, one per XCD range): within
+// each XCD's range of tiles (xcd_block), heaviest first by this flush's work per tile, as a counting
+// sort over 64 log-spaced work classes.  Only the schedule changes; k_combined's events do not
+// depend on it.
+constexpr int TO_NB = 64;
+__device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
+    __shared__ uint32_t hist[TO_NB];
+    const uint32_t q = nb / N_XCD, r = nb % N_XCD;
+    const uint32_t lo = x * q + min(x, r), hi = lo + q + (x < r ? 1u : 0u);
+    if (threadIdx.x < TO_NB) hist[threadIdx.x] = 0;
+    __syncthreads();
+    auto cls = [&](uint32_t v) {  // descending: class 0 = heaviest
+        const int c = (int)(8.0f * __log2f((float)v + 1.0f)) - 40;
+        return (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
+    };
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(tile_work[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < WAVE) {  // exclusive scan of the 64 class counts by one wave
+        const uint32_t v = hist[threadIdx.x];
+        uint32_t incl = v;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+            if ((int)threadIdx.x >= o) incl += t;
+        }
+        hist[threadIdx.x] = incl - v;
+    }
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+        tile_order[1 + lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
+    if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
+}
+
 __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ tile_total,
                                                 const unsigned long long *__restrict__ tile_base, uint32_t n_entries,
                                                 uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag,
                                                 const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap,
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
-                                                uint32_t ns, int4 *hbbox) {
-    const uint32_t b = blockIdx.x, R = gridDim.x - 1;
+                                                uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
+                                                uint32_t n_tiles, uint32_t *tile_order) {
+    const uint32_t b = blockIdx.x, R = gridDim.x - 1 - (tile_order ? N_XCD : 0u);
+    if (b > R) {
+        tile_order_block(b - R - 1, tile_work, n_tiles, tile_order);
+        return;
+    }
     if (b == R) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         if (threadIdx.x == 0) {
             res->err = sc->err;
@@ -3467,53 +3505,21 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
                           tile_order, tile_work, ework);
 }
 
-// The next flush's tile order: within each XCD's range of tiles (xcd_block), heaviest first by
-// this flush's work per tile, as a counting sort over 64 log-spaced work classes.  Only the
-// schedule changes; k_combined's events do not depend on it.
-constexpr int TO_T = 1024, TO_NB = 64;
-__global__ __launch_bounds__(TO_T) void k_tile_order(const uint32_t *__restrict__ tile_work, uint32_t nb,
-                                                     uint32_t *tile_order) {
-    __shared__ uint32_t hist[TO_NB];
-    const uint32_t x = blockIdx.x, q = nb / N_XCD, r = nb % N_XCD;
-    const uint32_t lo = x * q + min(x, r), hi = lo + q + (x < r ? 1u : 0u);
-    if (threadIdx.x < TO_NB) hist[threadIdx.x] = 0;
-    __syncthreads();
-    auto cls = [&](uint32_t v) {  // descending: class 0 = heaviest
-        const int c = (int)(8.0f * __log2f((float)v + 1.0f)) - 40;
-        return (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
-    };
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += TO_T) atomicAdd(&hist[cls(tile_work[i])], 1u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int c = 0; c < TO_NB; ++c) {
-            const uint32_t v = hist[c];
-            hist[c] = acc;
-            acc += v;
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += TO_T)
-        tile_order[1 + lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
-    if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
-}
-
-void launch_tile_order(const uint32_t *tile_work, uint32_t n, uint32_t *tile_order, hipStream_t st) {
-    if (!n) return;
-    k_tile_order<<<N_XCD, TO_T, 0, st>>>(tile_work, combined_tiles(n), tile_order);
-}
 
 size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }
 
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, hipStream_t st) {
+                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
+                   hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
-    k_finish<<<R + 1, 256, 0, st>>>(tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu,
-                                    reinterpret_cast<const uint2 *>(tmp_pairs), reinterpret_cast<uint2 *>(out_pairs),
-                                    cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox, n_spaces, hbbox);
+    if (!n_new) tile_order = nullptr;
+    k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
+        tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu, reinterpret_cast<const uint2 *>(tmp_pairs),
+        reinterpret_cast<uint2 *>(out_pairs), cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox,
+        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order);
 }
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }

@@ -771,7 +771,6 @@ void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, 
                         w->tile_order_on ? w->tile_order : nullptr, w->tile_order_on ? w->tile_work : nullptr, w->ework,
                         st,
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
-    if (w->tile_order_on) gw::launch_tile_order(w->tile_work, Fn.n, w->tile_order, st);
     stage_begin(w, S, ST_SPECIAL);
     gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn, half,
                      rerun ? nullptr : w->special, st);
@@ -781,7 +780,8 @@ void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, 
     gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, S.events,
                       cap, S.sc, reinterpret_cast<gw::TickOut *>(GWAOI_DIRECT_SUMMARY ? S.d_hout : S.dev_out), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
-                      GWAOI_DIRECT_SUMMARY ? reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)) : nullptr, st);
+                      GWAOI_DIRECT_SUMMARY ? reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)) : nullptr,
+                      w->tile_order_on ? w->tile_work : nullptr, w->tile_order_on ? w->tile_order : nullptr, st);
     stage_end(w, S, ST_FINISH);
 }
 
