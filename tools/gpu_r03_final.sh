@@ -8,7 +8,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -2 gpurun_out/pytest_final.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_final.log 2>&1 || { tail -20 gpurun_out/smoke_final.log; exit 1; }
 tail -1 gpurun_out/smoke_final.log
-bash tools/gpu_r03_prof.sh r03final
-timeout -k 10 400 python -u tools/variants.py run base base > gpurun_out/variants_final_order.log 2>&1 && \
-GWAOI_TILE_ORDER=0 timeout -k 10 400 python -u tools/variants.py run base base >> gpurun_out/variants_final_order.log 2>&1
-cat gpurun_out/variants_final_order.log
+bash tools/gpu_r03_prof.sh ${1:-r03final}
