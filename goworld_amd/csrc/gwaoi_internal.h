@@ -234,7 +234,14 @@ inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; 
 #endif
 // entities per k_combined tile (= threads per workgroup; the special pass keeps TILE_A)
 constexpr uint32_t COMBINED_TILE = GWAOI_CT;
-inline uint32_t combined_tiles(uint32_t n) { return (n + COMBINED_TILE - 1) / COMBINED_TILE; }
+__host__ __device__ inline uint32_t combined_tiles(uint32_t n) { return (n + COMBINED_TILE - 1) / COMBINED_TILE; }
+#ifndef GWAOI_XCD_BALANCE
+#define GWAOI_XCD_BALANCE 0  // 1: the XCDs' tile ranges split by work, not by count (k_combined's grid: 8 x stride)
+#endif
+// tiles one XCD's range may hold when the ranges are split by work (tile_order lists; blocks past a
+// list's end exit at once)
+__host__ __device__ inline uint32_t xcd_stride(uint32_t nb) { return (nb + 7) / 8 + (nb + 15) / 16 + 1; }
+constexpr uint32_t TO_HDR = 10;  // tile_order: nb, stride, 8 list lengths, then the lists
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,

@@ -495,6 +495,11 @@ __global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict_
 constexpr int SC_T = 256;
 constexpr int SC_I = 16;
 constexpr int SC_TILE = SC_T * SC_I;
+#ifndef GWAOI_S64_I
+#define GWAOI_S64_I 16  // cells per thread of the incremental sort's cell scan (k_scan64_lb)
+#endif
+constexpr int S64_I = GWAOI_S64_I;
+constexpr int S64_TILE = SC_T * S64_I;
 constexpr int SC1_T = 1024;  // single-workgroup scan
 constexpr int SC1_I = 16;
 constexpr size_t SC1_MAX = (size_t)SC1_T * SC1_I * 4;  // loops over chunks of SC1_T*SC1_I
@@ -1110,12 +1115,12 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
         keygen_fold256(blk, nbk, sc);
         return;
     }
-    __shared__ unsigned long long tile[SC_TILE + SC_TILE / 16];
+    __shared__ unsigned long long tile[S64_TILE + S64_TILE / 16];
     __shared__ unsigned long long ws[SC_T / WAVE];
-    const size_t base = (size_t)b * SC_TILE;
+    const size_t base = (size_t)b * S64_TILE;
     const uint32_t tid = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q) {
+    for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
 #if GWAOI_SCAN_REZERO && !GWAOI_ARRIVE_REZERO
@@ -1123,11 +1128,11 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
 #endif
     }
     __syncthreads();
-    unsigned long long v[SC_I];
+    unsigned long long v[S64_I];
     unsigned long long s = 0;
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q) {
-        v[q] = tile[p64(tid * SC_I + (uint32_t)q)];
+    for (int q = 0; q < S64_I; ++q) {
+        v[q] = tile[p64(tid * S64_I + (uint32_t)q)];
         s += v[q];
     }
     unsigned long long tot;
@@ -1147,13 +1152,13 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
     }
     run += e;
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q) {  // a thread rewrites only the words it read
-        tile[p64(tid * SC_I + (uint32_t)q)] = run;
+    for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read
+        tile[p64(tid * S64_I + (uint32_t)q)] = run;
         run += v[q];
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < SC_I; ++q) {
+    for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         if (base + j < n) {
             const unsigned long long e = tile[p64(j)];
@@ -2763,8 +2768,24 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 #endif
     // Tiles run heaviest first within each XCD's range when the previous flush left an order for
     // this tile count (k_tile_order); any order gives the same events.
+#if GWAOI_XCD_BALANCE
+    // XCD x's k-th block runs the k-th tile of x's list; the lists split the tiles by work (k_finish)
+    uint32_t t;
+    {
+        const uint32_t nb = combined_tiles(F.n), x = blockIdx.x % N_XCD, k = blockIdx.x / N_XCD;
+        if (tile_order && tile_order[0] == nb) {
+            if (k >= tile_order[2 + x]) return;
+            t = tile_order[TO_HDR + x * xcd_stride(nb) + k];
+        } else {
+            const uint32_t q = nb / N_XCD, r = nb % N_XCD;
+            if (k >= q + (x < r ? 1u : 0u)) return;
+            t = x * q + min(x, r) + k;
+        }
+    }
+#else
     uint32_t t = xcd_block(blockIdx.x, gridDim.x);
     if (tile_order && tile_order[0] == gridDim.x) t = tile_order[1 + t];
+#endif
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
     const uint32_t e0 = t * CT;
@@ -2997,8 +3018,65 @@ static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 constexpr int TO_NB = 64;
 __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
     __shared__ uint32_t hist[TO_NB];
+#if GWAOI_XCD_BALANCE
+    // The XCD ranges split the tiles by work: range x starts at the first tile whose work prefix
+    // reaches x/8 of the total, kept within xcd_stride(nb) tiles per range (every tile in one range).
+    __shared__ unsigned long long part[256];
+    __shared__ uint32_t bnd[N_XCD + 1];
+    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x, c0 = min(threadIdx.x * per, nb), c1 = min(c0 + per, nb);
+    unsigned long long my = 0;
+    for (uint32_t i = c0; i < c1; ++i) my += tile_work[i];
+    part[threadIdx.x] = my;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive prefix of the 256 chunk sums
+        unsigned long long acc = 0;
+        for (uint32_t i = 0; i < blockDim.x; ++i) {
+            const unsigned long long v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+        bnd[0] = 0;
+        bnd[N_XCD] = nb;
+        for (uint32_t y = 1; y < N_XCD; ++y) bnd[y] = 0xFFFFFFFFu;
+        hist[0] = (uint32_t)(acc >> 32);  // the total work, passed through LDS (hist is cleared below)
+        hist[1] = (uint32_t)acc;
+    }
+    __syncthreads();
+    const unsigned long long W = ((unsigned long long)hist[0] << 32) | hist[1];
+    {
+        unsigned long long pre = part[threadIdx.x];
+        for (uint32_t i = c0; i < c1; ++i) {  // the chunk holding target y/8 finds the tile
+            const unsigned long long nxt = pre + tile_work[i];
+            for (uint32_t y = 1; y < N_XCD; ++y) {
+                const unsigned long long tgt = W * y / N_XCD;
+                if (pre < tgt && nxt >= tgt) atomicMin(&bnd[y], i + 1);
+            }
+            pre = nxt;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t S = xcd_stride(nb);
+        for (uint32_t y = 1; y < N_XCD; ++y) {
+            uint32_t v = bnd[y] == 0xFFFFFFFFu ? bnd[y - 1] : bnd[y];
+            const uint32_t room = (N_XCD - y) * S;  // the ranges after y must hold the rest
+            v = max(v, bnd[y - 1]);
+            if (nb > room) v = max(v, nb - room);
+            v = min(v, bnd[y - 1] + S);
+            v = min(v, nb);
+            bnd[y] = v;
+        }
+    }
+    __syncthreads();
+    const uint32_t lo = bnd[x], hi = bnd[x + 1];
+    uint32_t *dst = tile_order + TO_HDR + x * xcd_stride(nb);
+    if (threadIdx.x == 0) tile_order[2 + x] = hi - lo;
+    __syncthreads();
+#else
     const uint32_t q = nb / N_XCD, r = nb % N_XCD;
     const uint32_t lo = x * q + min(x, r), hi = lo + q + (x < r ? 1u : 0u);
+    uint32_t *dst = tile_order + 1;
+#endif
     if (threadIdx.x < TO_NB) hist[threadIdx.x] = 0;
     __syncthreads();
     auto cls = [&](uint32_t v) {  // descending: class 0 = heaviest
@@ -3019,7 +3097,11 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
     }
     __syncthreads();
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-        tile_order[1 + lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
+#if GWAOI_XCD_BALANCE
+        dst[atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
+#else
+        dst[lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
+#endif
     if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
 }
 
@@ -3407,7 +3489,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // look-back status words: lo and hi per block
 bool scan_rezeroes_counts() { return GWAOI_SCAN_REZERO != 0 || GWAOI_ARRIVE_REZERO != 0; }
 
-size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, SC_TILE) + 1); }
+size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
@@ -3415,7 +3497,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
                       TickScalars *sc, uint32_t tag, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
-    const uint32_t nb = cdiv(m, SC_TILE);
+    const uint32_t nb = cdiv(m, S64_TILE);
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
                                          cdiv(n_total, 256), sc, p_cell_start);
     if (n_total)
@@ -3499,7 +3581,8 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and
     // end: no marker packets between kernels when the stage is timed
-    hipExtLaunchKernelGGL(k_combined, dim3(combined_tiles(F.n)), dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
+    hipExtLaunchKernelGGL(k_combined, dim3(GWAOI_XCD_BALANCE ? N_XCD * xcd_stride(combined_tiles(F.n)) : combined_tiles(F.n)),
+                          dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
                           (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,
                           tile_order, tile_work, ework);

@@ -1349,7 +1349,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / gw::COMBINED_TILE + 2)) ||
-        (rc = dalloc(w, &w->tile_order, N / gw::COMBINED_TILE + 3)) || (rc = dalloc(w, &w->ework, N)) ||
+        (rc = dalloc(w, &w->tile_order, gw::TO_HDR + 8 * (size_t)gw::xcd_stride(gw::combined_tiles((uint32_t)N)) + 8)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess ||  // no order yet
