@@ -3177,6 +3177,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         }
     }
     uint32_t ex[1] = {0u};
+    // relies on in-order workgroup dispatch to terminate (see the look-back scans' comment above)
     if (b) lookback<1>(lb, 0, b, tag, ex);  // (its barriers also publish s_agg)
     __syncthreads();
     const uint32_t excl = ex[0], agg = s_agg;

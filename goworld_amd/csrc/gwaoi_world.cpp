@@ -311,6 +311,7 @@ struct gwaoi_world {
         int set;            // FlushSet it writes
         int p_idx, n_idx;   // previous / new frame
         const gw::SlotSp *s_ss_view;  // its S' spaces: the set's sss, or the previous frame's (virtual S')
+        uint64_t cap;       // event capacity its pair passes were launched with (writes clipped to it)
         std::vector<uint8_t> touched_alive;  // liveness of touched[i] when the queue was closed
     } fl;
 
@@ -623,9 +624,8 @@ float o2f(int i) {
 // cell count bounded by the population.
 // The cell size for a mean of K neighbours per entity: entities per cell ~ (K / 4) / c^2 held
 // near 1.3 (config 3: K = 85 -> D/4; configs 4 and 5: K = 30-32 -> D/2).
-float recommend_cells_per_dist(double K) {
-    return (float)std::min(4.0, std::max(2.0, std::floor(std::sqrt(K / 5.33) + 0.25)));
-}
+// Only D/2 and D/4 are used (the measured sizes; D/3 ties D/4 at config 3): D/4 from K = 5.33 * 3^2 = 48.
+float recommend_cells_per_dist(double K) { return std::sqrt(K / 5.33) >= 3.0 ? 4.0f : 2.0f; }
 
 void choose_grids(gwaoi_world *w, uint32_t &total_cells, uint32_t &total_rows) {
     uint32_t base = 0, rows = 0;
@@ -636,6 +636,7 @@ void choose_grids(gwaoi_world *w, uint32_t &total_cells, uint32_t &total_rows) {
         w->cells_per_dist = w->cpd_rec;
         w->cpd_streak = 0;
         rebuild = true;
+        w->dbg.cell_size_switches++;
     }
     for (uint32_t s = 0; s < w->n_space_ids; ++s) {
         SpaceHost &S = w->spaces[s];
@@ -754,10 +755,14 @@ uint32_t next_lb_tag(gwaoi_world *w) {
     return w->lb_tag;
 }
 
-// rerun: the flush's pair passes again after an event-buffer overflow; keygen's special-tile
-// flags may belong to a later (speculatively launched) flush by then, so every tile is visited.
-void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
-                        const gw::SlotSp *s_ss_view, bool rerun = false) {
+// Returns the event capacity the passes were given (what the flush's finish must compare the total
+// against: the set's buffer or the shared scratch may grow later, by another flush's regrow).
+// rerun: the flush's pair passes again after an event-buffer overflow.  By then a speculatively
+// launched successor may have rebuilt the shared scheduling buffers (tile order, tile work, per-entry
+// work) for the flush after it, so a re-run neither reads nor writes them, and keygen's special-tile
+// flags may be the successor's too, so every tile is visited.
+uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
+                            const gw::SlotSp *s_ss_view, bool rerun = false) {
     hipStream_t st = w->stream;
     const uint32_t TBn = gw::combined_tiles(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
@@ -767,8 +772,9 @@ void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, 
     // timed with the launch's own start/end events (no marker packets)
     const bool tc = w->timing_mask >> ST_COMBINED & 1u;
     if (tc) S.ev_used[ST_COMBINED] = true;
+    const bool order = w->tile_order_on && !rerun;
     gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, half,
-                        w->tile_order_on ? w->tile_order : nullptr, w->tile_order_on ? w->tile_work : nullptr, w->ework,
+                        order ? w->tile_order : nullptr, order ? w->tile_work : nullptr, rerun ? nullptr : w->ework,
                         st,
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
     stage_begin(w, S, ST_SPECIAL);
@@ -781,8 +787,9 @@ void launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, 
                       cap, S.sc, reinterpret_cast<gw::TickOut *>(GWAOI_DIRECT_SUMMARY ? S.d_hout : S.dev_out), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
                       GWAOI_DIRECT_SUMMARY ? reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)) : nullptr,
-                      w->tile_order_on ? w->tile_work : nullptr, w->tile_order_on ? w->tile_order : nullptr, st);
+                      order ? w->tile_work : nullptr, order ? w->tile_order : nullptr, st);
     stage_end(w, S, ST_FINISH);
+    return cap;
 }
 
 int poison(gwaoi_world *w, int rc) {
@@ -992,7 +999,7 @@ int tick_launch(gwaoi_world *w) {
     }
 
     // ---- pair passes: combined over the new grid, special entities over the previous one
-    launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view);
+    const uint64_t ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view);
 
     // from here on the device has rewritten SlotInfo for the new frame: any failure before the
     // commit below leaves the world inconsistent (poisoned)
@@ -1017,6 +1024,7 @@ int tick_launch(gwaoi_world *w) {
     w->fl.p_idx = p_idx;
     w->fl.n_idx = n_idx;
     w->fl.s_ss_view = s_ss_view;
+    w->fl.cap = ev_cap;
     w->launch_set ^= 1;
     w->fl.touched_alive.resize(w->touched.size());
     for (size_t i = 0; i < w->touched.size(); ++i) w->fl.touched_alive[i] = w->alive[w->touched[i]];
@@ -1091,7 +1099,9 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
         w->last_error = "more than 2^32-1 events in one flush";
         return poison(w, GWAOI_ECAPACITY);
     }
-    if (r.total64 > std::min(S.ev_cap, w->evtmp_cap)) {  // grow and re-run the pair passes
+    // compared with the capacity the passes had at launch: a regrow by another flush since then
+    // (shared scratch, or the twin set's catch-up) does not make the clipped events complete
+    if (r.total64 > f.cap) {  // grow and re-run the pair passes
         stage_collect(w, S);
         if (w->inject_regrow_fail) {
             w->last_error = "event buffer regrow failed (injected)";
@@ -1102,7 +1112,10 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
         gw::launch_zero(w->tile_total, f.entries + 1, st);
         gw::launch_zero(reinterpret_cast<uint32_t *>(&S.sc->counter), 2, st);
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
-        launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true);
+        if (launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true) < r.total64) {
+            w->last_error = "pair passes re-run: event buffers did not grow";
+            return poison(w, GWAOI_EDEVICE);
+        }
         w->dbg.event_regrows++;
         if (hipGetLastError() != hipSuccess ||
             (!GWAOI_DIRECT_SUMMARY &&
@@ -1335,7 +1348,10 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
             return fail(rc);
         // S' records seq 0 (virtual S': never "written")
         if (hipMemset(S.srec, 0, N * sizeof(gw::Rec16)) != hipSuccess) return fail(GWAOI_EDEVICE);
-        if (hipHostMalloc((void **)&S.h_out, out_bytes, hipHostMallocDefault) != hipSuccess ||
+        // k_finish writes the summary here while the host polls done_ev: coherent (uncached, system
+        // scope) memory, so that the writes are visible once the event is seen whatever the runtime's
+        // default coherence of pinned allocations
+        if (hipHostMalloc((void **)&S.h_out, out_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&S.d_hout, S.h_out, 0) != hipSuccess)
             return fail(GWAOI_ENOMEM);
         std::memset(S.h_out, 0, out_bytes);
@@ -2147,6 +2163,7 @@ int gwaoi_debug_counters(gwaoi_world *w, gwaoi_debug *out) {
     return gw::api_guard([&]() -> int {
     if (!w || !out) return GWAOI_EINVAL;
     *out = w->dbg;
+    out->cells_per_dist = (uint32_t)w->cells_per_dist;
     return GWAOI_OK;
     });
 }

@@ -108,6 +108,9 @@ typedef struct {
     uint64_t event_regrows;         /* flushes that grew the device event buffer and re-ran the pair passes  */
     uint64_t speculative_launches;  /* flushes gwaoi_tick_end_begin_device queued before the commit of the  */
                                     /* one in flight                                                         */
+    uint64_t cell_size_switches;    /* flushes that rebuilt every grid with another automatic cell size      */
+    uint32_t cells_per_dist;        /* cells per AOI distance of the grids in use (2 or 4 when automatic)    */
+    uint32_t pad;
 } gwaoi_debug;
 
 typedef struct {

@@ -1043,3 +1043,104 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
             assert d["event_regrows"] > 0
         for i in range(0, n, 997):
             np.testing.assert_array_equal(A.neighbors(i), B.neighbors(i))
+
+
+def test_speculative_regrows_with_growing_crowd_gpu():
+    """Event counts that rise flush after flush (the space contracts every tick) with a
+    small event capacity: the speculative pipeline overflows and regrows its event sets
+    several times back to back, while the twin set and the shared scratch drift apart.
+    Every flush must still deliver the serial path's events: a flush compares its total
+    with the capacity its pair passes were launched with, not with a buffer another
+    flush grew since (finish_flight)."""
+    torch = pytest.importorskip("torch")
+    n, ticks = 20000, 14
+    rng = np.random.default_rng(7)
+    L = float(np.sqrt(n * 1250.0))
+    x = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
+    z = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
+    slots = np.arange(n, dtype=np.uint32)
+    host, dev = [], []
+    px, pz = x, z
+    for t in range(ticks):
+        order = rng.permutation(n).astype(np.uint32)
+        px = (px * np.float32(0.8) + rng.uniform(-1, 1, n).astype(np.float32)).astype(np.float32)
+        pz = (pz * np.float32(0.8) + rng.uniform(-1, 1, n).astype(np.float32)).astype(np.float32)
+        host.append((order, px[order], pz[order]))
+        dev.append([torch.from_numpy(a).to("cuda:0") for a in (order.astype(np.int32), px[order], pz[order])])
+    torch.cuda.synchronize()
+    with World(n, event_capacity=2000) as A, World(n) as B:
+        for w in (A, B):
+            s = w.space_create(D)
+            w.enter_batch(s, slots, x, z)
+            w.tick()
+        A.moved_batch_device(*(b.data_ptr() for b in dev[0]), n)
+        A.tick_begin()
+        totals = []
+        for t in range(ticks):
+            if t + 1 < ticks:
+                A.moved_batch_device(*(b.data_ptr() for b in dev[t + 1]), n)
+                ne, nl = A.tick_end_begin_device()
+            else:
+                ne, nl = A.tick_end_device()
+            ga, la = _device_events(A, ne, nl)
+            B.moved_batch(*host[t])
+            gb, lb = B.tick()
+            totals.append(ne + nl)
+            np.testing.assert_array_equal(pair_keys(ga), pair_keys(gb), err_msg=f"tick {t}: enters")
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"tick {t}: leaves")
+        d = A.debug_counters()
+        assert d["event_regrows"] >= 2, (d, totals)
+        assert d["speculative_launches"] >= ticks - 2
+        assert totals[-1] > 4 * totals[1], totals
+        for i in range(0, n, 1999):
+            np.testing.assert_array_equal(A.neighbors(i), B.neighbors(i))
+
+
+def test_cell_size_switch_keeps_parity_gpu(oracle_mod):
+    """Automatic cell size (gwaoi_config.cells_per_dist = 0): a sparse uniform space
+    switches the grids to D/2, a contracted one back to D/4 (two flushes recommending
+    the other size rebuild every grid; that flush takes the radix sort, the others the
+    incremental merge).  Events equal a world with a fixed D/4 grid and the closed form
+    at every flush, across both switches."""
+    n = 20000
+    rng = np.random.default_rng(5)
+    L = float(np.sqrt(n * 1250.0))
+    x = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
+    z = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
+    slots = np.arange(n, dtype=np.uint32)
+    seq = np.zeros(n, np.uint64)
+    sp = np.zeros(n, np.uint32)
+    with World(n) as A, World(n, cells_per_dist=4.0) as B:
+        for w in (A, B):
+            s = w.space_create(D)
+            w.enter_batch(s, slots, x, z)
+        seq[:] = 1 + np.arange(n, dtype=np.uint64)
+        nxt = n + 1
+        ea, _ = flush(A)
+        eb, _ = flush(B)
+        np.testing.assert_array_equal(ea, eb)
+        prev = oracle_mod.closed_form_pairs(x, z, seq, sp, {0: D})
+        np.testing.assert_array_equal(ea, prev)
+        cpd = [A.debug_counters()["cells_per_dist"]]
+        for t in range(12):
+            order = rng.permutation(n).astype(np.uint32)
+            shrink = np.float32(0.88) if 4 <= t < 8 else np.float32(1.0)  # ticks 4-7: the crowd thickens
+            x = (x * shrink + rng.uniform(-1, 1, n).astype(np.float32)).astype(np.float32)
+            z = (z * shrink + rng.uniform(-1, 1, n).astype(np.float32)).astype(np.float32)
+            for w in (A, B):
+                w.moved_batch(order, x[order], z[order])
+            seq[order] = nxt + np.arange(n, dtype=np.uint64)
+            nxt += n
+            ea, la = flush(A)
+            eb, lb = flush(B)
+            cur = oracle_mod.closed_form_pairs(x, z, seq, sp, {0: D})
+            np.testing.assert_array_equal(ea, eb, err_msg=f"tick {t}: enters vs fixed grid")
+            np.testing.assert_array_equal(la, lb, err_msg=f"tick {t}: leaves vs fixed grid")
+            np.testing.assert_array_equal(ea, np.setdiff1d(cur, prev), err_msg=f"tick {t}: enters vs closed form")
+            np.testing.assert_array_equal(la, np.setdiff1d(prev, cur), err_msg=f"tick {t}: leaves vs closed form")
+            prev = cur
+            cpd.append(A.debug_counters()["cells_per_dist"])
+        # sparse start (about 32 neighbours each): D/2; crowded end (about 90): back to D/4
+        assert cpd[0] == 4 and 2 in cpd[1:5] and cpd[-1] == 4, cpd
+        assert A.debug_counters()["cell_size_switches"] == 2, cpd
+        assert B.debug_counters()["cell_size_switches"] == 0

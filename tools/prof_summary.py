@@ -19,8 +19,10 @@ import sys
 
 
 def short(name):
-    m = re.search(r"(k_[a-z_0-9]+|__amd_[a-zA-Z_]+)", name)
-    return m.group(1) if m else name[:40]
+    """Kernel name without namespace and parameters, template arguments kept:
+    k_keygen<true> (steady flush) and k_keygen<false> (populate) are different kernels."""
+    m = re.search(r"(k_[a-z_0-9]+(?:<[^<>()]*>)?|__amd_[a-zA-Z_]+)", name)
+    return m.group(1).replace(" ", "") if m else name[:40]
 
 
 def kernel_stats(d):
