@@ -352,7 +352,7 @@ def cpu_baseline_spaces(args, target_s: float):
     dt = time.perf_counter() - t0
     ev = sum(sum(w[0].counts()) for w in work)
     return {"value": sum(done) / dt, "unit": "entity-moves/s", "events_per_s": ev / dt, "cores": cores,
-            "kind": "port",
+            "nproc": os.cpu_count(), "kind": "port",
             "sample": f"{cores} independent cfg4 spaces (2000 entities each), one per core, every entity "
                       f"moving each tick ({sum(done)} Moved calls), sequential XZ-list restatement, {dt:.1f} s"}
 
@@ -463,11 +463,18 @@ def cfg4_leg(args, ws, rank, device, dist, red_dev):
     steps = ticks - max(1, args.cfg4_warmup)
     el_max, (moves_all, ev_all) = reduce_over_ranks(dist, el, [n * steps, ev], red_dev)
     w.close()
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.cfg4_cpu_seconds > 0:
+        try:
+            cpu = cpu_baseline_spaces(args, args.cfg4_cpu_seconds)
+        except Exception as e:  # the baseline must not take the GPU number down with it
+            cpu = {"error": repr(e)}
     return {"metric": "AOI entity-moves/sec, config 4 (strong scaling: fixed total work over the ranks)",
             "value": moves_all / el_max, "unit": "entity-moves/s", "ms_per_step": el_max / steps * 1e3,
             "steps": steps, "n_gpus": ws, "scaling": "strong", "events_per_s": ev_all / el_max,
             "spaces_total": total, "entities_total": total * per, "entities_rank0": n, "setup_s_rank0": round(setup_s, 2),
-            "data": "synthetic (torch Philox on the GPU, generated before timing, resident in HBM)"}
+            "data": "synthetic (torch Philox on the GPU, generated before timing, resident in HBM)",
+            "cpu_baseline": cpu}
 
 
 def cpu_baseline(args, wl_factory, target_s: float):
@@ -510,13 +517,53 @@ def cpu_baseline(args, wl_factory, target_s: float):
     }
 
 
+def cfg5_cpu_baseline(x0, z0, ops0, target_s: float):
+    """CPU-XZ at config 5 (BASELINE.md:49): the go-aoi restatement (oracle/xzlist.c), one
+    core, populated with the 2^24 entities (bulk populate, untimed), then timed on the
+    first Moved calls of tick 0 in call order until target_s; the per-move cost is
+    extrapolated to the whole tick (every entity moves once)."""
+    from oracle import oracle
+    n = x0.size
+    t0 = time.perf_counter()
+    m = oracle.XZList(D_CFG5, n, record=False)
+    m.bulk_enter(np.arange(n, dtype=np.int32), x0, z0)
+    pop_s = time.perf_counter() - t0
+    rec = np.ascontiguousarray(ops0).view(np.uint8)
+    rec = np.frombuffer(rec.tobytes(), np.dtype([("slot", "<u4"), ("x", "<f4"), ("z", "<f4"), ("kind", "<u4"),
+                                                 ("seq", "<u8")]))
+    rec = rec[np.argsort(rec["seq"], kind="stable")]  # call order
+    sl = rec["slot"].astype(np.int32)
+    nx, nz = rec["x"].astype(np.float32), rec["z"].astype(np.float32)
+    done, chunk = 0, 16
+    t0 = time.perf_counter()
+    while done < sl.size and time.perf_counter() - t0 < target_s:
+        k = min(chunk, sl.size - done)
+        m.moved_batch(sl[done:done + k], nx[done:done + k], nz[done:done + k])
+        done += k
+        chunk = min(chunk * 2, 256)
+    dt = time.perf_counter() - t0
+    ne, nl = m.counts()
+    rate = done / dt
+    return {"value": rate, "unit": "entity-moves/s", "events_per_s": (ne + nl) / dt, "cores": 1, "kind": "port",
+            "extrapolated_tick_s": n / rate,
+            "sample": f"first {done} Moved calls of tick 0 of cfg5 ({n} entities in one space, populated in "
+                      f"{pop_s:.1f} s untimed), sequential XZ-list restatement, {dt:.1f} s; the tick "
+                      f"(every entity moving once) extrapolated from the per-move cost",
+            "note": "BASELINE.md asks for a 65,536-move prefix: at ~50 moves/s (each Moved walks ~23k x-list and "
+                    "~23k z-list nodes at this size) that is ~20 min, so the prefix is time-bounded instead"}
+
+
 def run_strips(args, ws, rank, local, dist):
     """Config 5: one 2^24-entity space cut into one x-strip per rank; every
-    tick routes the owned moves, exchanges halo records over RCCL
-    (counts all-gathered on the host over gloo, records point to point to the
-    neighbour strips in one RCCL send/recv group) and flushes each strip's
-    world (goworld_amd/strips.py).  Inputs are generated on the GPU before
-    timing (DeviceUniformWorkload); value = all N moves per tick / max time."""
+    tick routes the owned moves, exchanges halo records over RCCL (counts,
+    with the ENTER / LEAVE statistics, all-gathered on the host over gloo;
+    records point to point to the neighbour strips in one RCCL send/recv
+    group) and queues each strip's tick on the GPU (the strip records become
+    device Leave / Enter / Moved batches of its world, which flushes; the
+    filter keeps the strip's events).  The next tick's route waits once for
+    its counts and completes the previous tick with that same wait
+    (goworld_amd/strips.py).  Inputs are generated on the GPU before timing
+    (DeviceUniformWorkload); value = all N moves per tick / max time."""
     import torch
     from goworld_amd.shard import reduce_over_ranks
     from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local, local_slice, setup_count_group
@@ -532,32 +579,39 @@ def run_strips(args, ws, rank, local, dist):
     edges = even_edges(ws, -wl.L / 2, wl.L / 2)
     edges_t = torch.from_numpy(edges).to(dev)
     ticks = args.warmup + args.steps
+    cpu_here = rank == 0 and ws == 1 and not args.no_cpu_baseline
+    x0h = wl.x.cpu().numpy() if cpu_here else None
+    z0h = wl.z.cpu().numpy() if cpu_here else None
     init_ops = wl.initial_ops(edges_t, rank)
     ops = [wl.tick_ops(edges_t, rank) for _ in range(ticks)]
+    ops0h = ops[0].cpu().numpy() if cpu_here else None
     del wl
     torch.cuda.synchronize()
     sh = StripShard(n, float(D_CFG5), edges, rank, device=local, cells_per_dist=args.cells_per_dist)
+    via_cpu = args.dist_backend == "gloo"
 
     def one(o, phases=None):
         a = time.perf_counter()
-        send, counts, tele = sh.route(o)
+        send, counts, tele = sh.route(o)  # the tick's one host wait; it completes the previous tick
         b = time.perf_counter()
         if dist is not None:
-            recv, tele_all = exchange(dist, send, counts, tele, via_cpu=args.dist_backend == "gloo")
+            recv, tele_all, kinds = exchange(dist, send, counts, tele, via_cpu=via_cpu, kinds=sh.kinds)
         else:
-            recv, tele_all = exchange_local([(send, counts, tele)])[0]
-        c = time.perf_counter()  # finish() orders the world's stream after the exchange (no host wait)
-        r = sh.finish(local_slice(send, counts, rank), recv, tele_all)
+            recv, tele_all, kinds = exchange_local([(send, counts, tele)], kinds=[sh.kinds])[0]
+        c = time.perf_counter()
+        sh.finish(local_slice(send, counts, rank), recv, tele_all, kinds=kinds)  # queued, no wait
         if phases is not None:
             phases[0] += b - a
             phases[1] += c - b
             phases[2] += time.perf_counter() - c
-        return r, int(counts.sum() - counts[rank]), int(recv.shape[0])
+        return int(counts.sum() - counts[rank]), int(recv.shape[0])
 
-    (ne0, nl0), _, _ = one(init_ops)
+    one(init_ops)
+    ne0, nl0 = sh.wait()
     setup_s = time.perf_counter() - t_setup
     for t in range(args.warmup):
         one(ops[t])
+    sh.wait()
     w = sh.world
     w.set_stage_timing([] if args.no_timing else ["combined"])
     w.reset_stage_times()
@@ -566,23 +620,35 @@ def run_strips(args, ws, rank, local, dist):
     torch.cuda.synchronize()
     lat, events, sent, recvd = [], 0, 0, 0
     phases = [0.0, 0.0, 0.0]
+    waits0 = sh.host_waits()
     t0 = time.perf_counter()
     for t in range(args.warmup, ticks):
         a = time.perf_counter()
-        (ne, nl), ns, nr = one(ops[t], phases)
+        ns, nr = one(ops[t], phases)
+        if t > args.warmup:
+            ne, nl = sh.wait()  # the previous tick's counts: completed by this route, no wait here
+            events += ne + nl
         lat.append(time.perf_counter() - a)
-        events += ne + nl
         sent += ns
         recvd += nr
+    ne, nl = sh.wait()  # the last tick
+    events += ne + nl
+    waits = sh.host_waits() - waits0
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timed = w.stage_times() if not args.no_timing else {}
     info = w.info()
-    el_max, (moves_all, events_all, halo_all, live_all) = reduce_over_ranks(
-        dist, elapsed, [n * args.steps / ws, events, sent, info["live"]],
+    el_max, (moves_all, events_all, halo_all, live_all, waits_all) = reduce_over_ranks(
+        dist, elapsed, [n * args.steps / ws, events, sent, info["live"], waits],
         "cpu" if args.dist_backend == "gloo" else dev)
+    cpu = None
+    if cpu_here:
+        try:
+            cpu = cfg5_cpu_baseline(x0h, z0h, ops0h, args.cpu_seconds)
+        except Exception as e:  # the baseline must not take the GPU number down with it
+            cpu = {"error": repr(e)}
     if rank == 0:
         lat_ms = np.array(lat) * 1e3
         tm = {k: v[0] / max(v[1], 1) for k, v in timed.items() if v[1]}
@@ -608,14 +674,69 @@ def run_strips(args, ws, rank, local, dist):
             "events_per_tick": events_all / max(args.steps, 1), "initial_enter_events_rank0": ne0,
             "halo_records_per_tick": halo_all / max(args.steps, 1),
             "halo_note": "records sent to other ranks (24 B each), all ranks",
+            "host_waits_per_tick": waits_all / ws / max(args.steps, 1),
             "strip_world_entities_sum": live_all, "setup_s": round(setup_s, 2),
-            "rank0_phase_ms_per_tick": {"route": round(phases[0] / args.steps * 1e3, 4),
+            "rank0_phase_ms_per_tick": {"route_and_previous_tick_wait": round(phases[0] / args.steps * 1e3, 4),
                                         "exchange": round(phases[1] / args.steps * 1e3, 4),
-                                        "tick_filter": round(phases[2] / args.steps * 1e3, 4)},
-            "roofline": roofline, "cpu_baseline": None,
+                                        "tick_queue": round(phases[2] / args.steps * 1e3, 4)},
+            "tick_note": "asynchronous strip tick: route's one host wait brings its counts and completes the "
+                         "previous tick (receive, world Leave/Enter/Moved device batches, flush, filter); "
+                         "p50/p99 = route + exchange + queue per tick",
+            "roofline": roofline, "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        line = json.dumps(out)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+        else:
+            print(line, flush=True)
     sh.close()
+
+
+def cfg5_job(args, ws, rank, local):
+    """The config-5 strip run as a sub-record of the default line (`cfg5_strips`): one child
+    job of ws ranks (`bench.py --workload cfg5`), started here before this process touches
+    the GPU and waited for with a time limit, so that the strip / RCCL path runs on the
+    driver's own multi-GPU launches while a hang or crash in it cannot take the headline
+    down.  Returns the child's JSON (rank 0) or an error record."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"gwaoi_cfg5_{os.getpid()}_{rank}.json")
+    env = dict(os.environ)
+    port = int(os.environ.get("MASTER_PORT", "0") or 0)
+    env.update(RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(ws), LOCAL_WORLD_SIZE=str(ws),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port + 1 if port else _free_port()))
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "cfg5", "--gpus", str(ws), "--steps",
+           str(args.cfg5_steps), "--warmup", str(args.cfg5_warmup), "--dist-backend", args.dist_backend,
+           "--json-out", out, "--cpu-seconds", str(args.cfg5_cpu_seconds)]
+    if args.cfg5_entities:
+        cmd += ["--entities", str(args.cfg5_entities)]
+    if args.no_cpu_baseline or args.cfg5_cpu_seconds <= 0:
+        cmd.append("--no-cpu-baseline")
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL)
+    try:
+        rc = p.wait(timeout=args.cfg5_timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+        rc = "timeout"
+    wall = round(time.perf_counter() - t0, 1)
+    if rank != 0:
+        return None
+    res = None
+    try:
+        with open(out) as fh:
+            res = json.loads(fh.read().strip().splitlines()[-1])
+        os.unlink(out)
+    except (OSError, ValueError, IndexError):
+        pass
+    if res is None:
+        return {"error": f"cfg5 child job: exit {rc} after {wall} s, no result"}
+    res["job"] = {"wall_s": wall, "exit": rc, "note": "child job of the default bench (bench.py --workload cfg5), "
+                                                      "one rank per GPU, run before the cfg3 line's own ranks "
+                                                      "touch the GPU"}
+    return res
 
 
 D_CFG5 = np.float32(100.0)
@@ -665,6 +786,16 @@ def main():
     ap.add_argument("--wire-records", type=int, default=1_000_000, help="32-B client records per wire regroup call")
     ap.add_argument("--wire-out-records", type=int, default=4_000_000,
                     help="48-B game records per gate_to_clients call (one gate's share of a cfg3 collect)")
+    ap.add_argument("--cfg5-steps", type=int, default=5,
+                    help="cfg3 runs: timed ticks of the config-5 strip sub-record (child job; 0 = off)")
+    ap.add_argument("--cfg5-warmup", type=int, default=3)
+    ap.add_argument("--cfg5-entities", type=int, default=0, help="cfg5 sub-record entities (default 2^24)")
+    ap.add_argument("--cfg5-timeout", type=float, default=420.0, help="seconds before the cfg5 child job is killed")
+    ap.add_argument("--cfg5-cpu-seconds", type=float, default=10.0,
+                    help="CPU-XZ sample of the cfg5 sub-record (rank 0 at N=1; 0 = off)")
+    ap.add_argument("--cfg4-cpu-seconds", type=float, default=10.0,
+                    help="CPU-XZ of the cfg4 sub-record on all cores (rank 0 at N=1; 0 = off)")
+    ap.add_argument("--json-out", default=None, help="write the JSON line to this file instead of stdout")
     args = ap.parse_args()
 
     # --gpus N without an outside launcher: spawn the N ranks here, before anything touches the GPU
@@ -676,6 +807,8 @@ def main():
     if plan is not None:
         sys.exit(spawn_ranks(plan))
     ws, rank, local = dist_env()
+    # the config-5 strip sub-record runs first, as a child job, while this process has not touched the GPU
+    cfg5 = cfg5_job(args, ws, rank, local) if args.workload == "cfg3" and args.cfg5_steps > 0 else None
     dist = None
     if ws > 1:
         import torch
@@ -992,6 +1125,7 @@ def main():
             "cpu_baseline": cpu,
             "host_tick": host_tick,
             "cfg4_strong": cfg4,
+            "cfg5_strips": cfg5,
         }
         if cpu and "value" in cpu:
             out["speedup_vs_cpu"] = out["value"] / ws / cpu["value"]

@@ -36,13 +36,15 @@ EXPORTS = [
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
     "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
     "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
+    "gwaoi_enter_batch_device", "gwaoi_leave_batch_device",
 ]
 
 # every function include/gwaoi_strips.h declares
 STRIP_EXPORTS = [
     "gwaoi_strips_create", "gwaoi_strips_destroy", "gwaoi_strips_halo", "gwaoi_strips_route",
     "gwaoi_strips_route_scatter", "gwaoi_strips_tick", "gwaoi_strips_events_device", "gwaoi_strips_events",
-    "gwaoi_strips_last_error",
+    "gwaoi_strips_last_error", "gwaoi_strips_route_kinds", "gwaoi_strips_tick_async", "gwaoi_strips_wait",
+    "gwaoi_strips_host_waits",
 ]
 
 # every function include/gwaoi_sync.h declares
@@ -169,12 +171,18 @@ def load():
         "gwaoi_enter_seq": ([vp, u32, u32, f, f, u64], C.c_int),
         "gwaoi_moved_seq": ([vp, u32, f, f, u64], C.c_int),
         "gwaoi_moved_batch_device_seq": ([vp, vp, vp, vp, vp, sz], C.c_int),
+        "gwaoi_enter_batch_device": ([vp, u32, vp, vp, vp, vp, sz, vp], C.c_int),
+        "gwaoi_leave_batch_device": ([vp, u32, vp, sz], C.c_int),
         "gwaoi_strips_create": ([vp, u32, P(StripsConfig), P(vp)], C.c_int),
         "gwaoi_strips_destroy": ([vp], C.c_int),
         "gwaoi_strips_halo": ([vp, P(f)], C.c_int),
         "gwaoi_strips_route": ([vp, vp, sz, P(u64)], C.c_int),
         "gwaoi_strips_route_scatter": ([vp, vp, vp], C.c_int),
         "gwaoi_strips_tick": ([vp, vp, sz, vp, sz, vp, sz, P(u64), P(u64)], C.c_int),
+        "gwaoi_strips_route_kinds": ([vp, vp, vp, vp], C.c_int),
+        "gwaoi_strips_tick_async": ([vp, vp, sz, vp, sz, vp, sz, u64, u64, vp], C.c_int),
+        "gwaoi_strips_wait": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_strips_host_waits": ([vp, P(u64)], C.c_int),
         "gwaoi_strips_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_strips_events": ([vp, P(Events)], C.c_int),
         "gwaoi_strips_last_error": ([vp], C.c_char_p),
@@ -304,6 +312,18 @@ class World:
         else:
             self._check(self._L.gwaoi_moved_batch_device_seq(self._w, C.c_void_p(d_slots), C.c_void_p(d_x),
                                                              C.c_void_p(d_z), C.c_void_p(d_seq), n))
+
+    def enter_batch_device(self, space, d_slots: int, d_x: int, d_z: int, n: int, d_seq: int | None = None,
+                           box=None):
+        """gwaoi_enter_batch_device: Enter calls whose arrays live in device memory (slots
+        not live; box = (x0, z0, x1, z1) around the positions, or None)."""
+        b = np.ascontiguousarray(box, np.float32) if box is not None else None
+        self._check(self._L.gwaoi_enter_batch_device(self._w, space, C.c_void_p(d_slots), C.c_void_p(d_x),
+                                                     C.c_void_p(d_z), C.c_void_p(d_seq) if d_seq else None, n,
+                                                     _p(b) if b is not None else None))
+
+    def leave_batch_device(self, space, d_slots: int, n: int):
+        self._check(self._L.gwaoi_leave_batch_device(self._w, space, C.c_void_p(d_slots), n))
 
     # ---- flush
     def tick(self, copy: bool = True):

@@ -35,6 +35,7 @@ constexpr uint32_t ERR_MOVE_DEAD = 2u;       // device move of a slot that is no
 constexpr uint32_t ERR_BAD_SLOT = 4u;
 constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreement (bug guard)
 constexpr uint32_t ERR_SEQ = 16u;            // explicit device seq below the flush's floor
+constexpr uint32_t ERR_ENTER_LIVE = 32u;     // device Enter of a slot live when the flush began
 
 constexpr uint32_t TILE_A = 256;  // entities per pair-pass tile (= threads per workgroup)
 
@@ -120,16 +121,20 @@ struct TickOut {
 };
 
 // ---- launchers (gwaoi_kernels.hip) ------------------------------------------
-void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
-                          SlotInfo *info, hipStream_t st);
+// S' entries base .. base+n_app-1 for the entering slots new_slots[] (host-checked, or a device
+// Enter batch: slots out of range or live when the flush began are flagged and left dead).
+void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t base, Rec16 *s_rec, SlotSp *s_ss,
+                          SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
 // means a device-resident Moved batch (keep the space).  Op i gets seq
 // seqs[i] when seqs is given (explicit: checked >= seq_floor, the largest
 // folded into sc->seq_max when track_max), else seq0 + i.
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots,
                       SlotInfo *info, uint32_t tick_id, TickScalars *sc, hipStream_t st);
-void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
-                      uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+// sp == nullptr: every op has space sp_def (SP_KEEP: Moved; a space: Enter; SP_DEAD: Leave, whose
+// x / z may be nullptr).
+void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t sp_def,
+                      uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
                       uint32_t n_total, const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor,
                       bool track_max, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st);
 // A flush whose queue is only device Moved batches (<= MAX_MOVE_RUNS of them):
@@ -139,9 +144,10 @@ struct MoveRun {
     const uint32_t *ds;
     const float *dx, *dz;
     const unsigned long long *dseq;  // explicit seqs (nullptr: seq0 + i)
-    const uint32_t *dsp;             // explicit space per op (nullptr: keep the slot's space)
+    const uint32_t *dsp;             // explicit space per op (nullptr: sp_def for every op)
     unsigned long long seq0;
     uint32_t j0, n;  // first op index in the flush, ops
+    uint32_t sp_def; // SP_KEEP: Moved (keep the slot's space); a space: Enter; SP_DEAD: Leave
 };
 struct MoveRuns {
     MoveRun r[MAX_MOVE_RUNS];
@@ -267,7 +273,7 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   hipStream_t st);
+                   uint32_t *dcount, hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
@@ -300,6 +306,11 @@ void world_set_error(gwaoi_world *w, const char *msg);
 // packet): op i moves d_slots[i] in space d_sp[i]; SLOT_NONE ops are no-ops.
 int world_queue_decoded(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
                         const uint32_t *d_sp, size_t n);
+// The event buffer, device counts {n_enter, n_total} (written by the flush's k_finish) and event
+// capacity of the flush in flight (gwaoi_tick_begin .. _end) or, when none is, of the last
+// committed one: for work queued on the world's stream behind the flush (the strip filter).
+// Events past the capacity were not written (the flush re-runs them at its end).
+void world_flush_events(gwaoi_world *w, const uint32_t **events, const uint32_t **dcount, uint64_t *cap);
 // Space of a slot in call order (as queued so far), SP_DEAD if not in one.
 uint32_t world_slot_space(gwaoi_world *w, uint32_t slot);
 // Hooks the world calls when a sync layer is attached.

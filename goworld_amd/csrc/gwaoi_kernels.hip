@@ -82,17 +82,26 @@ __global__ void k_zero(uint32_t *p, size_t n) {
 // ------------------------------------------------------------ op apply ------
 
 
-__global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t n_prev,
-                                Rec16 *s_rec, SlotSp *s_ss, SlotInfo *info) {
+__global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t base,
+                                Rec16 *s_rec, SlotSp *s_ss, SlotInfo *info, uint32_t max_slots, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_app) return;
     const uint32_t s = new_slots[i];
-    const uint32_t idx = n_prev + i;
+    const uint32_t idx = base + i;
     Rec16 r;
     r.x = r.z = 0.0f;
     r.s = 0;
     st_rec(s_rec, idx, r);
-    st_ss(s_ss, idx, s, SP_DEAD);
+    st_ss(s_ss, idx, s, SP_DEAD);  // dead until its Enter applies
+    if (s >= max_slots) {
+        atomicOr(&sc->err, ERR_BAD_SLOT);
+        return;
+    }
+    // a slot live when the flush began keeps its entry (a device Enter batch breaking the rules)
+    if (reinterpret_cast<const uint2 *>(info + s)[1].y != SP_DEAD) {
+        atomicOr(&sc->err, ERR_ENTER_LIVE);
+        return;
+    }
     reinterpret_cast<uint2 *>(info + s)[1] = make_uint2(idx, SP_DEAD);
 }
 
@@ -121,13 +130,13 @@ struct OpIn {
 
 __device__ __forceinline__ OpIn op_in(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
                                       const float *__restrict__ zs, const uint32_t *__restrict__ sps,
-                                      const unsigned long long *__restrict__ seqs, unsigned long long seq0,
-                                      uint32_t i) {
+                                      uint32_t sp_def, const unsigned long long *__restrict__ seqs,
+                                      unsigned long long seq0, uint32_t i) {
     OpIn o;
     o.slot = slots[i];
     o.x = xs[i];
     o.z = zs[i];
-    o.sp = sps ? sps[i] : SP_KEEP;
+    o.sp = sps ? sps[i] : sp_def;
     o.seq = seqs ? seqs[i] : seq0 + i;
     return o;
 }
@@ -192,15 +201,20 @@ __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32
 }
 
 __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
-                            const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t n, uint32_t j0,
-                            uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                            const unsigned long long *__restrict__ seqs, unsigned long long seq0,
+                            const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t sp_def,
+                            uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick,
+                            uint32_t n_total, const unsigned long long *__restrict__ seqs, unsigned long long seq0,
                             unsigned long long seq_floor, int track_max, Rec16 *s_rec, SlotSp *s_ss,
                             TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long smax = 0;
     if (i < n) {
-        const OpIn o = op_in(slots, xs, zs, sps, seqs, seq0, i);
+        OpIn o;
+        o.slot = slots[i];
+        o.x = xs ? xs[i] : 0.0f;  // a Leave run has no positions
+        o.z = zs ? zs[i] : 0.0f;
+        o.sp = sps ? sps[i] : sp_def;
+        o.seq = seqs ? seqs[i] : seq0 + i;
         if (o.slot < max_slots)
             smax = op_apply_one(o, j0 + i, slot_info(info, o.slot), info, tick, n_total, seq_floor, s_rec, s_ss, sc,
                                 true);
@@ -235,7 +249,7 @@ __global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uin
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long smax = 0;
     if (i < R.n) {
-        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.dseq, R.seq0, i);
+        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, i);
         const uint32_t s = o.slot;
         if (s == SLOT_NONE) {
             // placeholder of a skipped decoded record: no op
@@ -277,7 +291,7 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
     for (int u = 0; u < PER; ++u) {
         const uint32_t i = i0 + (uint32_t)u * 256u;
         o[u].slot = SLOT_NONE;
-        if (i < R.n) o[u] = op_in(R.ds, R.dx, R.dz, R.dsp, R.dseq, R.seq0, i);
+        if (i < R.n) o[u] = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, i);
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u)  // every SlotInfo line in flight at once
@@ -326,7 +340,7 @@ __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, u
         const MoveRun &R = RS.r[q];
         // start from the previous state so that a dropped (invalid) winner leaves it unchanged
         if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
-        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.dseq, R.seq0, j - R.j0);
+        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
         op_apply_one(o, j, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, true);
     }
 }
@@ -747,7 +761,7 @@ __global__ __launch_bounds__(MV_T) void k_mv_apply(MoveRuns RS, const uint32_t *
         o.slot = m.slot;
         o.x = m.x;
         o.z = m.z;
-        o.sp = R.dsp ? R.dsp[k] : SP_KEEP;
+        o.sp = R.dsp ? R.dsp[k] : R.sp_def;
         o.seq = R.dseq ? R.dseq[k] : R.seq0 + k;
         const unsigned long long q =
             op_apply_one(o, m.j, slot_info(info, m.slot), info, 0u, n_total, seq_floor, s_rec, s_ss, sc, false);
@@ -3112,7 +3126,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
                                                 uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
-                                                uint32_t n_tiles, uint32_t *tile_order) {
+                                                uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt) {
     const uint32_t b = blockIdx.x, R = gridDim.x - 1 - (tile_order ? N_XCD : 0u);
     if (b > R) {
         tile_order_block(b - R - 1, tile_work, n_tiles, tile_order);
@@ -3124,7 +3138,10 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
             res->total64 = sc->counter;
             res->seq_max = sc->seq_max;
             for (int q = 0; q < (int)DBG_N; ++q) res->dbg[q] = sc->dbg[q];
-            if (n_entries == 0) res->n_enter = res->n_total = 0;
+            if (n_entries == 0) {
+                res->n_enter = res->n_total = 0;
+                if (dcnt) dcnt[0] = dcnt[1] = 0;
+            }
         }
         const uint32_t per = (np + BB_T - 1) / BB_T;
         const uint32_t p0 = threadIdx.x * per, p1 = min(p0 + per, np);
@@ -3188,10 +3205,16 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         if (l < (uint32_t)FT) {
             s_off[l] = off;
             s_src[l] = e < n_entries ? tile_base[e] : 0ull;
-            if (e == n_enter_entries) res->n_enter = off;
+            if (e == n_enter_entries) {
+                res->n_enter = off;
+                if (dcnt) dcnt[0] = off;  // device copy of the counts (events read on the device before the host)
+            }
         }
         if (l == 0) s_off[FT] = excl + agg;
-        if (b == R - 1 && l == 0) res->n_total = excl + agg;
+        if (b == R - 1 && l == 0) {
+            res->n_total = excl + agg;
+            if (dcnt) dcnt[1] = excl + agg;
+        }
     }
     __syncthreads();
     // the block's tiles fill one contiguous output range: every thread takes
@@ -3394,10 +3417,10 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
 }
 
 
-void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t n_prev, Rec16 *s_rec, SlotSp *s_ss,
-                          SlotInfo *info, hipStream_t st) {
+void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t base, Rec16 *s_rec, SlotSp *s_ss,
+                          SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st) {
     if (!n_app) return;
-    k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, n_prev, s_rec, s_ss, info);
+    k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
 }
 
 void launch_moves_mark(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st) {
@@ -3462,13 +3485,13 @@ void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t m
     k_ops_claim<<<cdiv(n, 256), 256, 0, st>>>(slots, n, j0, max_slots, info, tick_id, sc);
 }
 
-void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t n,
-                      uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t sp_def,
+                      uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                       const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor, bool track_max,
                       Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st) {
     if (!n) return;
-    k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, n, j0, max_slots, info, tick_id, n_total, seqs, seq0,
-                                              seq_floor, track_max ? 1 : 0, s_rec, s_ss, sc);
+    k_ops_apply<<<cdiv(n, 256), 256, 0, st>>>(slots, x, z, sp, sp_def, n, j0, max_slots, info, tick_id, n_total, seqs,
+                                              seq0, seq_floor, track_max ? 1 : 0, s_rec, s_ss, sc);
 }
 
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
@@ -3596,14 +3619,14 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   hipStream_t st) {
+                   uint32_t *dcount, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     if (!n_new) tile_order = nullptr;
     k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
         tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu, reinterpret_cast<const uint2 *>(tmp_pairs),
         reinterpret_cast<uint2 *>(out_pairs), cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox,
-        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order);
+        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount);
 }
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }

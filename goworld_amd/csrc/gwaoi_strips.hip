@@ -8,14 +8,21 @@
 //
 // Kernels (all one-lane-per-record, 256-thread blocks, stable block-scan
 // compaction so that every output order is deterministic):
-//   k_route      owner side: op -> halo records per destination + teleports
-//   k_recv       receiver side: records -> world ops (device moves, host
-//                enters/leaves) + per-slot state update
+//   k_route      owner side: op -> halo records per destination + teleports,
+//                plus the ENTER / LEAVE counts and Enter box per destination
+//   k_recv       receiver side: records -> world ops [moves | enters | leaves]
+//                (device batches) + per-slot state update
 //   k_tele_mark  mark this tick's teleporters
-//   k_filter     keep the world events this strip owns
+//   k_filter     keep the world events this strip owns (count read on the
+//                device, so it is queued behind the world's flush)
 //   k_tele_pairs teleporter x teleporter pairs decided from before/after states
-// The exchange between ranks is the caller's (goworld_amd/strips.py: RCCL
-// all_to_all + all_gather).
+// The exchange between ranks is the caller's (goworld_amd/strips.py: counts
+// on the host, records point to point over RCCL).
+//
+// Host waits: one per tick.  gwaoi_strips_route waits for its counts, and the
+// same wait completes the previous tick (queued by gwaoi_strips_tick_async:
+// the receive, the world's device Enter/Leave/Moved batches, its flush, the
+// filter), whose results are then read from pinned memory.
 
 #include "gwaoi_internal.h"
 #include "../../include/gwaoi_strips.h"
@@ -23,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -41,6 +49,7 @@ constexpr uint32_t SE_STATE = 1u;     // op for an entity this strip does not ow
 constexpr uint32_t SE_NONFINITE = 2u;
 constexpr uint32_t SE_BADSLOT = 4u;
 constexpr uint32_t SE_KIND = 8u;
+constexpr uint32_t SE_COUNT = 16u;    // the records' kinds disagree with the announced counts
 
 struct StripGeo {
     uint32_t S, rank;
@@ -129,11 +138,77 @@ __device__ __forceinline__ void multisplit(int phase, unsigned long long mask, b
     }
 }
 
-// ---- owner side: classes 0..S-1 = destination ranks, S = teleports
+// Per-destination kind statistics of a route (and of a receiver's records): the
+// ENTER and LEAVE records and the box of the ENTER positions.  The host needs
+// them to queue its world's device Enter / Leave batches without reading the
+// records back (gwaoi_enter_batch_device sizes the grid from the box).
+constexpr int KS = 6;  // enters, leaves, box x0, z0, x1, z1 (ordered ints)
+
+__device__ __forceinline__ int f2o(float f) {
+    const int i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+
+__global__ void k_kstat_init(int *ks, uint32_t n) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    int *k = ks + (size_t)q * KS;
+    k[0] = k[1] = 0;
+    k[2] = k[3] = INT_MAX;
+    k[4] = k[5] = INT_MIN;
+}
+
+// Block-level accumulation of kind statistics over up to GWAOI_MAX_STRIPS classes: every lane
+// adds its few ENTER / LEAVE records (rare: entities crossing a region boundary) in LDS, then
+// one thread per class folds the block's figures into the global ones.
+struct KindLds {
+    int k[GWAOI_MAX_STRIPS][KS];
+};
+__device__ __forceinline__ void kind_init(KindLds &L, uint32_t K) {
+    for (uint32_t i = threadIdx.x; i < K * KS; i += blockDim.x) {
+        const uint32_t c = i % KS;
+        L.k[i / KS][c] = c < 2 ? 0 : (c < 4 ? INT_MAX : INT_MIN);
+    }
+}
+__device__ __forceinline__ void kind_add(KindLds &L, unsigned long long ent, unsigned long long lev, float x, float z) {
+    while (ent) {
+        const int q = __ffsll((long long)ent) - 1;
+        ent &= ent - 1;
+        atomicAdd(&L.k[q][0], 1);
+        atomicMin(&L.k[q][2], f2o(x));
+        atomicMin(&L.k[q][3], f2o(z));
+        atomicMax(&L.k[q][4], f2o(x));
+        atomicMax(&L.k[q][5], f2o(z));
+    }
+    while (lev) {
+        const int q = __ffsll((long long)lev) - 1;
+        lev &= lev - 1;
+        atomicAdd(&L.k[q][1], 1);
+    }
+}
+__device__ __forceinline__ void kind_flush(const KindLds &L, uint32_t K, int *ks) {
+    for (uint32_t q = threadIdx.x; q < K; q += blockDim.x) {
+        if (!L.k[q][0] && !L.k[q][1]) continue;
+        int *g = ks + (size_t)q * KS;
+        if (L.k[q][0]) {
+            atomicAdd(g + 0, L.k[q][0]);
+            atomicMin(g + 2, L.k[q][2]);
+            atomicMin(g + 3, L.k[q][3]);
+            atomicMax(g + 4, L.k[q][4]);
+            atomicMax(g + 5, L.k[q][5]);
+        }
+        if (L.k[q][1]) atomicAdd(g + 1, L.k[q][1]);
+    }
+}
+
+// ---- owner side: classes 0..S-1 = destination ranks, S = teleports.  Phase 0 also gathers the
+// kind statistics per destination (ks).
 __global__ void __launch_bounds__(BT) k_route(int phase, const gwaoi_halo_rec *__restrict__ ops, uint32_t n,
                                               const Rec16 *__restrict__ cur, StripGeo g, uint32_t *counts,
                                               const uint32_t *__restrict__ offs, uint32_t nb, uint32_t *err,
-                                              gwaoi_halo_rec *send, gwaoi_tele_rec *tele) {
+                                              gwaoi_halo_rec *send, gwaoi_tele_rec *tele, int *ks) {
+    __shared__ KindLds KL;
+    if (phase == 0) kind_init(KL, g.S);
     const uint32_t i = blockIdx.x * BT + threadIdx.x;
     unsigned long long mP = 0, mN = 0;
     bool tp = false;
@@ -168,6 +243,10 @@ __global__ void __launch_bounds__(BT) k_route(int phase, const gwaoi_halo_rec *_
             tp = op.kind == GWAOI_HALO_MOVE && fabsf(nw.x - pv.x) > g.tele;
         }
     }
+    if (phase == 0) {
+        __syncthreads();  // KL initialised
+        kind_add(KL, mN & ~mP, mP & ~mN, nw.x, nw.z);
+    }
     if (phase == 0 && i == 0) counts[(size_t)(g.S + 1) * nb] = 0;
     multisplit(phase, mP | mN, tp, g.S, g.S + 1, counts, offs, nb, [&](uint32_t q, uint32_t pos) {
         if (q < g.S) {
@@ -193,16 +272,26 @@ __global__ void __launch_bounds__(BT) k_route(int phase, const gwaoi_halo_rec *_
             tele[pos - offs[(size_t)g.S * nb]] = t;
         }
     });
+    if (phase == 0) {
+        __syncthreads();  // (multisplit's barrier orders the adds too; explicit for clarity)
+        kind_flush(KL, g.S, ks);
+    }
 }
 
-// ---- receiver side: classes 0 = world device moves, 1 = host enters, 2 = host leaves
+// ---- receiver side: classes 0 = world device moves, 1 = enters, 2 = leaves.  Every record is
+// emitted by its kind, so that the classes have exactly the sizes the senders' kind statistics
+// announced (the host queued the world batches with them); a record in the wrong state is
+// flagged (err), never dropped.  Output: one SoA array set [moves | enters | leaves].  Phase 0
+// also gathers the kind statistics (ks: one class) for gwaoi_strips_tick, which has no announced
+// counts.
 __global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__restrict__ lv, uint32_t n_local,
                                              const gwaoi_halo_rec *__restrict__ rv, uint32_t n, Rec16 *cur,
                                              Rec16 *prv, uint32_t *ptick, uint32_t tick, uint32_t max_slots,
                                              uint32_t *counts, const uint32_t *__restrict__ offs, uint32_t nb,
                                              uint32_t *err, uint32_t *m_slot, float *m_x, float *m_z,
-                                             unsigned long long *m_seq, gwaoi_halo_rec *el) {
-    if (phase == 1 && *err) return;  // phase 0 found a bad record: the tick fails with the state untouched
+                                             unsigned long long *m_seq, int *ks) {
+    __shared__ KindLds KL;
+    if (phase == 0 && ks) kind_init(KL, 1);
     const uint32_t i = blockIdx.x * BT + threadIdx.x;
     unsigned long long m = 0;
     gwaoi_halo_rec r{};
@@ -228,23 +317,32 @@ __global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__
                 st16(cur, r.slot, nw);
             }
         }
-        if (e) {
-            if (phase == 0) atomicOr(err, e);
-        } else {
-            m = 1ull << r.kind;
-        }
+        if (e && phase == 0) atomicOr(err, e);
+        if (r.kind <= GWAOI_HALO_LEAVE) m = 1ull << r.kind;
+    }
+    if (phase == 0 && ks) {
+        __syncthreads();
+        kind_add(KL, m >> 1 & 1ull, m >> 2 & 1ull, r.x, r.z);
     }
     if (phase == 0 && i == 0) counts[3 * nb] = 0;
-    multisplit(phase, m, false, 0xFFFFFFFFu, 3, counts, offs, nb, [&](uint32_t q, uint32_t pos) {
-        if (q == 0) {
-            m_slot[pos] = r.slot;
-            m_x[pos] = r.x;
-            m_z[pos] = r.z;
-            m_seq[pos] = r.seq;
-        } else {
-            el[pos - offs[nb]] = r;  // enters then leaves, contiguous
-        }
+    multisplit(phase, m, false, 0xFFFFFFFFu, 3, counts, offs, nb, [&](uint32_t, uint32_t pos) {
+        m_slot[pos] = r.slot;
+        m_x[pos] = r.x;
+        m_z[pos] = r.z;
+        m_seq[pos] = r.seq;
     });
+    if (phase == 0 && ks) {
+        __syncthreads();
+        kind_flush(KL, 1, ks);
+    }
+}
+
+// The receiver's class sizes against the counts the host queued the world batches with.
+__global__ void k_recv_check(const uint32_t *__restrict__ offs, uint32_t nb, uint32_t n_move, uint32_t n_ent,
+                             uint32_t n_lev, uint32_t *err) {
+    if (threadIdx.x == 0 && (offs[nb] != n_move || offs[2 * nb] - offs[nb] != n_ent ||
+                             offs[3 * nb] - offs[2 * nb] != n_lev))
+        atomicOr(err, SE_COUNT);
 }
 
 __global__ void k_tele_mark(const gwaoi_tele_rec *__restrict__ t, uint32_t n, uint32_t *ttick, uint32_t tick,
@@ -260,29 +358,70 @@ __device__ __forceinline__ Rec16 before(const Rec16 *cur, const Rec16 *prv, cons
 
 // ---- keep the world events this strip owns: class 0 enters (owner after the
 // tick), class 1 leaves (owner before the tick); teleporter pairs are dropped
-// here and decided by k_tele_pairs.
-__global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restrict__ ev, uint32_t ne, uint32_t nl,
+// here and decided by k_tele_pairs.  The event count is read on the device
+// (dcnt = {n_enter, n_total}, written by the world flush's k_finish, clipped to
+// cap): the filter is queued behind the flush without a host round trip.  Block
+// b takes one contiguous chunk of the events, BT at a time; phase 0 counts per
+// class, phase 1 writes at the scanned offsets (counts[q * G + b]).
+__global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restrict__ ev,
+                                               const uint32_t *__restrict__ dcnt, uint64_t cap,
                                                const Rec16 *__restrict__ cur, const Rec16 *__restrict__ prv,
                                                const uint32_t *__restrict__ ptick, const uint32_t *__restrict__ ttick,
                                                uint32_t tick, StripGeo g, uint32_t *counts,
-                                               const uint32_t *__restrict__ offs, uint32_t nb,
+                                               const uint32_t *__restrict__ offs,
                                                const unsigned long long *__restrict__ tcnt, uint2 *out) {
-    const uint32_t i = blockIdx.x * BT + threadIdx.x;
-    unsigned long long m = 0;
-    uint2 p = make_uint2(0, 0);
-    if (i < ne + nl) {
-        p = ev[i];
-        const bool is_enter = i < ne;
-        const bool tt = ttick[p.x] == tick && ttick[p.y] == tick;
-        if (!tt) {
-            const Rec16 a = is_enter ? ld16(cur, p.x) : before(cur, prv, ptick, p.x, tick);
-            if (present(a) && strip_of(g, a.x) == g.rank) m = is_enter ? 1ull : 2ull;
+    __shared__ uint32_t cnt[2][NW];
+    const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x / WV;
+    const uint32_t n = (uint32_t)min((uint64_t)dcnt[1], cap), ne = min(dcnt[0], n);
+    const uint32_t per = (uint32_t)(((uint64_t)n + (uint64_t)G * BT - 1) / ((uint64_t)G * BT)) * BT;
+    const uint32_t lo = (uint32_t)min((uint64_t)b * per, (uint64_t)n), hi = (uint32_t)min((uint64_t)lo + per, (uint64_t)n);
+    // phase 1: the teleporter enters go between the filter's enters and leaves
+    const uint32_t gap = phase == 1 && tcnt ? (uint32_t)tcnt[0] : 0u;
+    uint32_t base0 = phase == 1 ? offs[b] : 0u, base1 = phase == 1 ? offs[G + b] + gap : 0u;
+    for (uint32_t i0 = lo; i0 < hi; i0 += BT) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool k0 = false, k1 = false;
+        uint2 p = make_uint2(0, 0);
+        if (i < hi) {
+            p = ev[i];
+            const bool is_enter = i < ne;
+            const bool tt = ttick[p.x] == tick && ttick[p.y] == tick;
+            if (!tt) {
+                const Rec16 a = is_enter ? ld16(cur, p.x) : before(cur, prv, ptick, p.x, tick);
+                const bool own = present(a) && strip_of(g, a.x) == g.rank;
+                k0 = own && is_enter;
+                k1 = own && !is_enter;
+            }
         }
+        const unsigned long long b0 = __ballot(k0), b1 = __ballot(k1);
+        if (__lane_id() == 0) {
+            cnt[0][w] = (uint32_t)__popcll(b0);
+            cnt[1][w] = (uint32_t)__popcll(b1);
+        }
+        __syncthreads();
+        uint32_t t0 = 0, t1 = 0, p0 = 0, p1 = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)NW; ++k) {
+            if (k < w) {
+                p0 += cnt[0][k];
+                p1 += cnt[1][k];
+            }
+            t0 += cnt[0][k];
+            t1 += cnt[1][k];
+        }
+        if (phase == 1) {
+            if (k0) out[base0 + p0 + (uint32_t)__popcll(b0 & lanemask_lt())] = p;
+            if (k1) out[base1 + p1 + (uint32_t)__popcll(b1 & lanemask_lt())] = p;
+        }
+        base0 += t0;
+        base1 += t1;
+        __syncthreads();  // cnt is rewritten by the next step
     }
-    if (phase == 0 && i == 0) counts[2 * nb] = 0;
-    const uint32_t leave_gap = phase == 1 && tcnt ? (uint32_t)tcnt[0] : 0u;  // teleporter enters go between
-    multisplit(phase, m, false, 0xFFFFFFFFu, 2, counts, offs, nb,
-               [&](uint32_t q, uint32_t pos) { out[pos + (q ? leave_gap : 0u)] = p; });
+    if (phase == 0 && threadIdx.x == 0) {
+        counts[b] = base0;
+        counts[G + b] = base1;
+        if (b == 0) counts[2 * G] = 0;
+    }
 }
 
 // ---- teleporter x teleporter: phase 0 counts, phase 1 writes (atomic slots;
@@ -363,8 +502,21 @@ __global__ void k_totals(const uint32_t *offs, uint32_t K, uint32_t nb, const ui
 
 inline uint32_t cdivu(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 
-constexpr size_t EL_PREFETCH = 1u << 16;          // enter/leave records copied with the recv counts
+float o2f(int i) {
+    const int b = i >= 0 ? i : i ^ 0x7FFFFFFF;
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
+
 constexpr uint64_t TELE_PAIRS_MAX = 1ull << 22;  // bound n (n-1) per kind sized without a count (n_tele <= 2048)
+constexpr uint32_t FILTER_BLOCKS = 1024;         // k_filter's grid (chunks of the world's events)
+// pinned / device scalar regions (uint32 words)
+constexpr size_t SM_ROUTE = 0;                                  // route totals: K + 2
+constexpr size_t SM_KIND = 128;                                 // route kind statistics: KS per destination
+constexpr size_t SM_TICK = SM_KIND + KS * GWAOI_MAX_STRIPS;     // the tick's result (k_tick_totals): 5
+constexpr size_t SM_RECV = SM_TICK + 8;                         // gwaoi_strips_tick: receive totals 4 + kinds KS
+constexpr size_t SM_WORDS = SM_RECV + 16;
 
 }  // namespace
 
@@ -380,19 +532,18 @@ struct gwaoi_strips {
     // multisplit scratch
     uint32_t *counts = nullptr, *scan_tmp = nullptr, *err = nullptr, *small_d = nullptr;
     size_t counts_cap = 0, scan_cap = 0;
-    uint32_t *small_h = nullptr;  // pinned
+    uint32_t *small_h = nullptr;  // pinned, SM_WORDS
+    int *kstat = nullptr;         // device kind statistics: route (GWAOI_MAX_STRIPS x KS), receive (KS)
     // route state
     const gwaoi_halo_rec *r_ops = nullptr;
     uint32_t r_n = 0, r_nb = 0;
     bool routed = false;
-    // received world ops
+    bool kinds_valid = false;
+    // received records as world ops, SoA [moves | enters | leaves]
     uint32_t *m_slot = nullptr;
     float *m_x = nullptr, *m_z = nullptr;
     unsigned long long *m_seq = nullptr;
     size_t m_cap = 0;
-    gwaoi_halo_rec *el_d = nullptr;
-    size_t el_cap = 0;
-    std::vector<gwaoi_halo_rec> el_h;
     // teleporter pairs
     unsigned long long *tcnt = nullptr;
     uint2 *tpairs = nullptr;
@@ -403,6 +554,11 @@ struct gwaoi_strips {
     uint64_t n_enter = 0, n_leave = 0;
     uint32_t *h_events = nullptr;
     size_t h_cap = 0;
+    // a tick queued by gwaoi_strips_tick_async, completed by the next host wait
+    bool pending = false;
+    uint64_t pend_tcap = 0;     // its teleporter-pair buffers (for a filter re-run)
+    uint64_t pend_regrows = 0;  // the world's event regrows before its flush
+    uint64_t waits = 0;         // host waits (stream synchronisations) so far
     std::string last_error;
 };
 
@@ -417,11 +573,17 @@ namespace {
         }                                                                    \
     } while (0)
 
+int wait(gwaoi_strips *s) {
+    s->waits++;
+    S_TRY(hipStreamSynchronize(s->st));
+    return GWAOI_OK;
+}
+
 template <class T>
 int grow(gwaoi_strips *s, T **p, size_t &cap, size_t need) {
     if (need <= cap && *p) return GWAOI_OK;
     const size_t c = std::max<size_t>({need + need / 4, cap * 2, 256});
-    S_TRY(hipStreamSynchronize(s->st));
+    if (int rc = wait(s)) return rc;  // nothing queued may still use the old buffer
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     cap = 0;
@@ -435,20 +597,10 @@ int grow(gwaoi_strips *s, T **p, size_t &cap, size_t need) {
     return GWAOI_OK;
 }
 
-// counts (K*nb + 1) -> exclusive scan in place -> totals + err into small_h[0..K+1]
 int ensure_split(gwaoi_strips *s, uint32_t K, uint32_t nb) {
     const size_t n = (size_t)K * nb + 1;
     if (int rc = grow(s, &s->counts, s->counts_cap, n)) return rc;
     if (int rc = grow(s, &s->scan_tmp, s->scan_cap, gw::scan_tmp_elems(n) + 16)) return rc;
-    return GWAOI_OK;
-}
-
-int split_totals(gwaoi_strips *s, uint32_t K, uint32_t nb) {
-    gw::scan_exclusive(s->counts, s->counts, (size_t)K * nb + 1, s->scan_tmp, s->st);
-    k_totals<<<1, 128, 0, s->st>>>(s->counts, K, nb, s->err, s->small_d);
-    S_TRY(hipGetLastError());
-    S_TRY(hipMemcpyAsync(s->small_h, s->small_d, (K + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->st));
-    S_TRY(hipStreamSynchronize(s->st));
     return GWAOI_OK;
 }
 
@@ -472,9 +624,60 @@ int strip_err(gwaoi_strips *s, uint32_t e, const char *where) {
                     ((e & SE_BADSLOT) ? "slot out of range" :
                      (e & SE_KIND) ? "bad record kind" :
                      (e & SE_NONFINITE) ? "non-finite coordinate" :
+                     (e & SE_COUNT) ? "received records disagree with the announced enter / leave counts" :
                                           "entity not owned by / in the wrong state for this strip");
     return (e & SE_BADSLOT) ? GWAOI_EBADSLOT : (e & SE_NONFINITE) ? GWAOI_ENONFINITE :
-           (e & SE_KIND) ? GWAOI_EINVAL : GWAOI_ESTATE;
+           (e & SE_KIND) ? GWAOI_EINVAL : (e & SE_COUNT) ? GWAOI_EDEVICE : GWAOI_ESTATE;
+}
+
+// The filter of the world flush's events (in flight, or committed after a regrow), the teleporter
+// placement and the tick's totals (copied into small_h[SM_TICK..]), all queued on the stream.
+int launch_filter(gwaoi_strips *s, uint64_t tcap) {
+    const uint32_t *wev = nullptr, *dcnt = nullptr;
+    uint64_t cap = 0;
+    gw::world_flush_events(s->w, &wev, &dcnt, &cap);
+    if (int rc = grow(s, &s->out, s->out_cap, cap + 2 * tcap + 1)) return rc;
+    const uint32_t G = std::max(1u, std::min<uint32_t>(FILTER_BLOCKS, cdivu(std::max<uint64_t>(cap, 1), BT)));
+    if (int rc = ensure_split(s, 2, G)) return rc;
+    hipStream_t st = s->st;
+    const uint2 *ev = reinterpret_cast<const uint2 *>(wev);
+    k_filter<<<G, BT, 0, st>>>(0, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->counts,
+                               nullptr, nullptr, nullptr);
+    gw::scan_exclusive(s->counts, s->counts, (size_t)2 * G + 1, s->scan_tmp, st);
+    k_filter<<<G, BT, 0, st>>>(1, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->counts,
+                               s->counts, s->tcnt, s->out);
+    k_tele_place<<<64, 256, 0, st>>>(s->counts, G, s->tcnt, s->tpairs, s->tpairs + tcap, s->out);
+    k_tick_totals<<<1, 64, 0, st>>>(s->counts, G, s->tcnt, s->err, s->small_d + SM_TICK);
+    S_TRY(hipGetLastError());
+    S_TRY(hipMemcpyAsync(s->small_h + SM_TICK, s->small_d + SM_TICK, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    return GWAOI_OK;
+}
+
+// Complete the tick queued by gwaoi_strips_tick_async.  synced: the caller has just waited for
+// the stream (everything queued before has finished), so this adds no wait.  The world's flush
+// is committed (its summary is in pinned memory already); if it overflowed its event buffer,
+// it re-ran its pair passes on commit, and the filter runs again on the complete events.
+int complete(gwaoi_strips *s, bool synced) {
+    if (!s->pending) return GWAOI_OK;
+    if (!synced)
+        if (int rc = wait(s)) return rc;
+    s->pending = false;
+    uint64_t wne = 0, wnl = 0;
+    if (int rc = gwaoi_tick_end_device(s->w, &wne, &wnl)) {
+        s->last_error = std::string("world tick: ") + gwaoi_last_error(s->w);
+        return rc;
+    }
+    gwaoi_debug dbg{};
+    (void)gwaoi_debug_counters(s->w, &dbg);
+    if (dbg.event_regrows != s->pend_regrows) {
+        if (int rc = launch_filter(s, s->pend_tcap)) return rc;
+        if (int rc = wait(s)) return rc;
+    }
+    const uint32_t *t = s->small_h + SM_TICK;
+    s->n_enter = (uint64_t)t[0] + t[2];
+    s->n_leave = (uint64_t)t[1] + t[3];
+    if (wne + wnl > 0x7FFFFFFFull) return GWAOI_ECAPACITY;
+    return strip_err(s, t[4], "recv");
 }
 
 }  // namespace
@@ -484,9 +687,10 @@ extern "C" {
 int gwaoi_strips_destroy(gwaoi_strips *s) {
     return gw::api_guard([&]() -> int {
     if (!s) return GWAOI_EINVAL;
+    if (s->pending) (void)complete(s, false);
     if (s->st) (void)hipStreamSynchronize(s->st);
-    void *dev[] = {s->cur, s->prv, s->ptick, s->ttick, s->counts, s->scan_tmp, s->err, s->small_d, s->m_slot,
-                   s->m_x, s->m_z, s->m_seq, s->el_d, s->tcnt, s->tpairs, s->out};
+    void *dev[] = {s->cur, s->prv, s->ptick, s->ttick, s->counts, s->scan_tmp, s->err, s->small_d, s->kstat,
+                   s->m_slot, s->m_x, s->m_z, s->m_seq, s->tcnt, s->tpairs, s->out};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (s->small_h) (void)hipHostFree(s->small_h);
@@ -544,10 +748,12 @@ int gwaoi_strips_create(gwaoi_world *w, uint32_t space, const gwaoi_strips_confi
         hipMalloc((void **)&s->ptick, N * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&s->ttick, N * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&s->err, sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&s->small_d, 128 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->small_d, SM_WORDS * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->kstat, (GWAOI_MAX_STRIPS + 1) * KS * sizeof(int)) != hipSuccess ||
         hipMalloc((void **)&s->tcnt, 2 * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc((void **)&s->small_h, 128 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc((void **)&s->small_h, SM_WORDS * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(GWAOI_ENOMEM);
+    std::memset(s->small_h, 0, SM_WORDS * sizeof(uint32_t));
     if (hipMemsetAsync(s->cur, 0xFF, N * sizeof(Rec16), s->st) != hipSuccess ||  // x = NaN: absent
         hipMemsetAsync(s->prv, 0xFF, N * sizeof(Rec16), s->st) != hipSuccess ||
         hipMemsetAsync(s->ptick, 0, N * sizeof(uint32_t), s->st) != hipSuccess ||
@@ -573,17 +779,52 @@ int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, u
     if (!s || !counts || (n && !d_ops) || n > 0x7FFFFFFFu) return GWAOI_EINVAL;
     const uint32_t K = s->geo.S + 1;
     const uint32_t nb = std::max(1u, cdivu(n, BT));
+    s->kinds_valid = false;
     if (int rc = ensure_split(s, K, nb)) return rc;
-    S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), s->st));
-    k_route<<<nb, BT, 0, s->st>>>(0, d_ops, (uint32_t)n, s->cur, s->geo, s->counts, nullptr, nb, s->err, nullptr,
-                                  nullptr);
-    if (int rc = split_totals(s, K, nb)) return rc;
-    if (int rc = strip_err(s, s->small_h[K + 1], "route")) return rc;
-    for (uint32_t q = 0; q < K; ++q) counts[q] = s->small_h[q + 1] - s->small_h[q];
+    hipStream_t st = s->st;
+    // queued behind the previous tick (if one is pending): its filter and totals land before this
+    // route's totals, so the one wait below completes both
+    S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
+    k_kstat_init<<<1, 64, 0, st>>>(s->kstat, s->geo.S);
+    k_route<<<nb, BT, 0, st>>>(0, d_ops, (uint32_t)n, s->cur, s->geo, s->counts, nullptr, nb, s->err, nullptr,
+                               nullptr, s->kstat);
+    gw::scan_exclusive(s->counts, s->counts, (size_t)K * nb + 1, s->scan_tmp, st);
+    k_totals<<<1, 128, 0, st>>>(s->counts, K, nb, s->err, s->small_d + SM_ROUTE);
+    S_TRY(hipGetLastError());
+    S_TRY(hipMemcpyAsync(s->small_h + SM_ROUTE, s->small_d + SM_ROUTE, (K + 2) * sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, st));
+    S_TRY(hipMemcpyAsync(s->small_h + SM_KIND, s->kstat, (size_t)s->geo.S * KS * sizeof(int), hipMemcpyDeviceToHost,
+                         st));
+    if (int rc = wait(s)) return rc;  // the one host wait of a strip tick
+    if (int rc = complete(s, true)) return rc;
+    if (int rc = strip_err(s, s->small_h[SM_ROUTE + K + 1], "route")) return rc;
+    for (uint32_t q = 0; q < K; ++q) counts[q] = s->small_h[SM_ROUTE + q + 1] - s->small_h[SM_ROUTE + q];
     s->r_ops = d_ops;
     s->r_n = (uint32_t)n;
     s->r_nb = nb;
     s->routed = true;
+    s->kinds_valid = true;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_strips_route_kinds(const gwaoi_strips *s, uint64_t *enters, uint64_t *leaves, float *enter_boxes) {
+    return gw::api_guard([&]() -> int {
+    if (!s || !s->kinds_valid) return GWAOI_EINVAL;
+    for (uint32_t q = 0; q < s->geo.S; ++q) {
+        const int *k = reinterpret_cast<const int *>(s->small_h + SM_KIND) + (size_t)q * KS;
+        if (enters) enters[q] = (uint32_t)k[0];
+        if (leaves) leaves[q] = (uint32_t)k[1];
+        if (enter_boxes) {
+            float *b = enter_boxes + 4 * q;
+            if (k[0]) {
+                b[0] = o2f(k[2]); b[1] = o2f(k[3]); b[2] = o2f(k[4]); b[3] = o2f(k[5]);
+            } else {
+                b[0] = b[1] = INFINITY;
+                b[2] = b[3] = -INFINITY;
+            }
+        }
+    }
     return GWAOI_OK;
     });
 }
@@ -593,85 +834,60 @@ int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_te
     if (!s || !s->routed) return GWAOI_EINVAL;
     s->routed = false;
     k_route<<<s->r_nb, BT, 0, s->st>>>(1, s->r_ops, s->r_n, s->cur, s->geo, s->counts, s->counts, s->r_nb, s->err,
-                                       d_send, d_tele);
+                                       d_send, d_tele, nullptr);
     S_TRY(hipGetLastError());  // complete in stream order on the world's stream (gwaoi_stream): no host wait
     return GWAOI_OK;
     });
 }
 
-int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local, const gwaoi_halo_rec *d_recv,
-                      size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele, uint64_t *n_enter,
-                      uint64_t *n_leave) {
+int gwaoi_strips_tick_async(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local,
+                            const gwaoi_halo_rec *d_recv, size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele,
+                            uint64_t n_enter_recs, uint64_t n_leave_recs, const float *enter_box) {
     return gw::api_guard([&]() -> int {
     if (!s || (n_local && !d_local) || (n_recv && !d_recv) || (n_tele && !d_tele) || n_tele > 0x7FFFFFFFu ||
-        n_local + n_recv > 0x7FFFFFFFu)
+        n_local + n_recv > 0x7FFFFFFFu || n_enter_recs + n_leave_recs > n_local + n_recv)
         return GWAOI_EINVAL;
+    if (int rc = complete(s, false)) return rc;
     const size_t n_all = n_local + n_recv;
-    if (n_enter) *n_enter = 0;
-    if (n_leave) *n_leave = 0;
+    const uint32_t n_ent = (uint32_t)n_enter_recs, n_lev = (uint32_t)n_leave_recs;
+    const uint32_t n_move = (uint32_t)n_all - n_ent - n_lev;
     s->n_enter = s->n_leave = 0;
     const uint32_t tick = ++s->tick;
     hipStream_t st = s->st;
-    // ---- received records -> world ops + state.  Both multisplit phases run back to back into
-    // buffers sized for every record; ONE host wait brings the counts and (up to EL_PREFETCH of)
-    // the enter/leave records the host-side Enter/Leave calls need.
+    // ---- own + received records -> world ops [moves | enters | leaves] + per-slot state
     const uint32_t nb = std::max(1u, cdivu(n_all, BT));
     if (int rc = ensure_split(s, 3, nb)) return rc;
-    if (int rc = ensure_moves(s, n_all)) return rc;
-    if (int rc = grow(s, &s->el_d, s->el_cap, n_all + 1)) return rc;
+    if (int rc = ensure_moves(s, std::max<size_t>(n_all, 1))) return rc;
     S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
     k_recv<<<nb, BT, 0, st>>>(0, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick,
                               s->max_slots, s->counts, nullptr, nb, s->err, nullptr, nullptr, nullptr, nullptr, nullptr);
     gw::scan_exclusive(s->counts, s->counts, (size_t)3 * nb + 1, s->scan_tmp, st);
     k_recv<<<nb, BT, 0, st>>>(1, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick,
                               s->max_slots, s->counts, s->counts, nb, s->err, s->m_slot, s->m_x, s->m_z, s->m_seq,
-                              s->el_d);
-    k_totals<<<1, 128, 0, st>>>(s->counts, 3, nb, s->err, s->small_d);
+                              nullptr);
+    k_recv_check<<<1, 64, 0, st>>>(s->counts, nb, n_move, n_ent, n_lev, s->err);
     if (n_tele) k_tele_mark<<<cdivu(n_tele, 256), 256, 0, st>>>(d_tele, (uint32_t)n_tele, s->ttick, tick, s->max_slots);
     S_TRY(hipGetLastError());
-    const size_t pre = std::min<size_t>(n_all, EL_PREFETCH);
-    if (s->el_h.size() < EL_PREFETCH) s->el_h.resize(EL_PREFETCH);
-    S_TRY(hipMemcpyAsync(s->small_h, s->small_d, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    if (pre) S_TRY(hipMemcpyAsync(s->el_h.data(), s->el_d, pre * sizeof(gwaoi_halo_rec), hipMemcpyDeviceToHost, st));
-    S_TRY(hipStreamSynchronize(st));
-    if (int rc = strip_err(s, s->small_h[4], "recv")) return rc;
-    const uint32_t n_move = s->small_h[1] - s->small_h[0];
-    const uint32_t n_ent = s->small_h[2] - s->small_h[1];
-    const uint32_t n_lev = s->small_h[3] - s->small_h[2];
-    const size_t n_el = (size_t)n_ent + n_lev;
-    if (n_el > pre) {  // more boundary crossings than the prefetch: one more copy
-        s->el_h.resize(n_el);
-        S_TRY(hipMemcpyAsync(s->el_h.data() + pre, s->el_d + pre, (n_el - pre) * sizeof(gwaoi_halo_rec),
-                             hipMemcpyDeviceToHost, st));
-        S_TRY(hipStreamSynchronize(st));
-    }
-    // leaves (no seq), then enters in seq order, then the device moves
-    for (uint32_t k = 0; k < n_lev; ++k)
-        if (int rc = gwaoi_leave(s->w, s->el_h[n_ent + k].slot)) {
-            s->last_error = std::string("world leave: ") + gwaoi_last_error(s->w);
-            return rc;
-        }
-    std::sort(s->el_h.begin(), s->el_h.begin() + n_ent,
-              [](const gwaoi_halo_rec &a, const gwaoi_halo_rec &b) { return a.seq < b.seq; });
-    for (uint32_t k = 0; k < n_ent; ++k) {
-        const gwaoi_halo_rec &r = s->el_h[k];
-        if (int rc = gwaoi_enter_seq(s->w, s->space, r.slot, r.x, r.z, r.seq)) {
-            s->last_error = std::string("world enter: ") + gwaoi_last_error(s->w);
-            return rc;
-        }
-    }
-    if (int rc = gwaoi_moved_batch_device_seq(s->w, s->m_slot, s->m_x, s->m_z,
-                                              reinterpret_cast<const uint64_t *>(s->m_seq), n_move)) {
-        s->last_error = std::string("world moves: ") + gwaoi_last_error(s->w);
+    // ---- the world's ops, all device batches: Leaves, Enters, Moves (one record per slot)
+    auto wfail = [&](int rc, const char *what) {
+        s->last_error = std::string(what) + ": " + gwaoi_last_error(s->w);
         return rc;
-    }
-    uint64_t wne = 0, wnl = 0;
-    if (int rc = gwaoi_tick_device(s->w, &wne, &wnl)) {
-        s->last_error = std::string("world tick: ") + gwaoi_last_error(s->w);
-        return rc;
-    }
-    const uint32_t *wev = nullptr;
-    if (int rc = gwaoi_events_device(s->w, &wev, nullptr)) return rc;
+    };
+    const uint64_t *seqs = reinterpret_cast<const uint64_t *>(s->m_seq);
+    if (n_lev)
+        if (int rc = gwaoi_leave_batch_device(s->w, s->space, s->m_slot + n_move + n_ent, n_lev))
+            return wfail(rc, "world leaves");
+    if (n_ent)
+        if (int rc = gwaoi_enter_batch_device(s->w, s->space, s->m_slot + n_move, s->m_x + n_move, s->m_z + n_move,
+                                              seqs + n_move, n_ent, enter_box))
+            return wfail(rc, "world enters");
+    if (n_move)
+        if (int rc = gwaoi_moved_batch_device_seq(s->w, s->m_slot, s->m_x, s->m_z, seqs, n_move))
+            return wfail(rc, "world moves");
+    gwaoi_debug dbg{};
+    (void)gwaoi_debug_counters(s->w, &dbg);
+    s->pend_regrows = dbg.event_regrows;
+    if (int rc = gwaoi_tick_begin(s->w)) return wfail(rc, "world tick");
     // ---- teleporter pairs: one pass into buffers that hold every possible pair (n (n-1) per kind)
     S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
     uint64_t tcap = n_tele > 1 ? (uint64_t)n_tele * (n_tele - 1) : 0;
@@ -680,37 +896,72 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_l
                                                          nullptr, 0);
         unsigned long long hc[2];
         S_TRY(hipMemcpyAsync(hc, s->tcnt, sizeof(hc), hipMemcpyDeviceToHost, st));
-        S_TRY(hipStreamSynchronize(st));
+        if (int rc = wait(s)) return rc;
         tcap = std::max<uint64_t>(std::max(hc[0], hc[1]), 1);
         S_TRY(hipMemsetAsync(s->tcnt, 0, 2 * sizeof(unsigned long long), st));
     }
+    // the pair buffers hold at least 2^16 pairs per kind: a tick-to-tick change of the teleporter
+    // count does not reallocate them (a reallocation waits for the stream)
+    tcap = std::max<uint64_t>(tcap, 1u << 16);
     if (int rc = grow(s, &s->tpairs, s->tpairs_cap, 2 * tcap + 1)) return rc;
     if (n_tele > 1)
         k_tele_pairs<<<cdivu(n_tele, 256), 256, 0, st>>>(1, d_tele, (uint32_t)n_tele, s->geo, s->tcnt, s->tpairs,
                                                          s->tpairs + tcap, tcap);
     // ---- filter the world's events to this strip's: [filter enters | tele enters | filter leaves | tele leaves]
-    const uint64_t nev = wne + wnl;
-    if (nev > 0x7FFFFFFFull) return GWAOI_ECAPACITY;
-    const uint32_t fb = std::max(1u, cdivu(nev, BT));
-    if (int rc = ensure_split(s, 2, fb)) return rc;
-    if (int rc = grow(s, &s->out, s->out_cap, nev + 2 * tcap + 1)) return rc;
-    k_filter<<<fb, BT, 0, st>>>(0, reinterpret_cast<const uint2 *>(wev), (uint32_t)wne, (uint32_t)wnl, s->cur, s->prv,
-                                s->ptick, s->ttick, tick, s->geo, s->counts, nullptr, fb, nullptr, nullptr);
-    gw::scan_exclusive(s->counts, s->counts, (size_t)2 * fb + 1, s->scan_tmp, st);
-    k_filter<<<fb, BT, 0, st>>>(1, reinterpret_cast<const uint2 *>(wev), (uint32_t)wne, (uint32_t)wnl, s->cur, s->prv,
-                                s->ptick, s->ttick, tick, s->geo, s->counts, s->counts, fb, s->tcnt, s->out);
-    if (tcap)
-        k_tele_place<<<std::min<uint32_t>(cdivu(tcap, 256), 1024), 256, 0, st>>>(s->counts, fb, s->tcnt, s->tpairs,
-                                                                                 s->tpairs + tcap, s->out);
-    k_tick_totals<<<1, 64, 0, st>>>(s->counts, fb, s->tcnt, s->err, s->small_d);
-    S_TRY(hipGetLastError());
-    S_TRY(hipMemcpyAsync(s->small_h, s->small_d, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    S_TRY(hipStreamSynchronize(st));
-    const uint64_t fe = s->small_h[0], fl = s->small_h[1], te = s->small_h[2], tl = s->small_h[3];
-    s->n_enter = fe + te;
-    s->n_leave = fl + tl;
+    if (int rc = launch_filter(s, tcap)) return rc;
+    s->pend_tcap = tcap;
+    s->pending = true;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_strips_wait(gwaoi_strips *s, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!s) return GWAOI_EINVAL;
+    const int rc = complete(s, false);
     if (n_enter) *n_enter = s->n_enter;
     if (n_leave) *n_leave = s->n_leave;
+    return rc;
+    });
+}
+
+int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local, const gwaoi_halo_rec *d_recv,
+                      size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele, uint64_t *n_enter,
+                      uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    if (!s || (n_local && !d_local) || (n_recv && !d_recv) || n_local + n_recv > 0x7FFFFFFFu) return GWAOI_EINVAL;
+    if (int rc = complete(s, false)) return rc;
+    // no announced counts: the records' kinds and the box of their Enters are read here first
+    const size_t n_all = n_local + n_recv;
+    const uint32_t nb = std::max(1u, cdivu(n_all, BT));
+    if (int rc = ensure_split(s, 3, nb)) return rc;
+    hipStream_t st = s->st;
+    int *ks = s->kstat + (size_t)GWAOI_MAX_STRIPS * KS;
+    S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
+    k_kstat_init<<<1, 64, 0, st>>>(ks, 1);
+    k_recv<<<nb, BT, 0, st>>>(0, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick,
+                              s->tick + 1, s->max_slots, s->counts, nullptr, nb, s->err, nullptr, nullptr, nullptr,
+                              nullptr, ks);
+    S_TRY(hipGetLastError());
+    S_TRY(hipMemcpyAsync(s->small_h + SM_RECV, s->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    S_TRY(hipMemcpyAsync(s->small_h + SM_RECV + 2, ks, KS * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (int rc = wait(s)) return rc;
+    if (int rc = strip_err(s, s->small_h[SM_RECV], "recv")) return rc;
+    const int *k = reinterpret_cast<const int *>(s->small_h + SM_RECV + 2);
+    const float box[4] = {o2f(k[2]), o2f(k[3]), o2f(k[4]), o2f(k[5])};
+    if (int rc = gwaoi_strips_tick_async(s, d_local, n_local, d_recv, n_recv, d_tele, n_tele, (uint32_t)k[0],
+                                         (uint32_t)k[1], k[0] ? box : nullptr))
+        return rc;
+    return gwaoi_strips_wait(s, n_enter, n_leave);
+    });
+}
+
+int gwaoi_strips_host_waits(const gwaoi_strips *s, uint64_t *waits) {
+    return gw::api_guard([&]() -> int {
+    if (!s || !waits) return GWAOI_EINVAL;
+    *waits = s->waits;
     return GWAOI_OK;
     });
 }
@@ -718,6 +969,7 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_l
 int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const uint32_t **d_leave) {
     return gw::api_guard([&]() -> int {
     if (!s) return GWAOI_EINVAL;
+    if (int rc = complete(s, false)) return rc;
     if (d_enter) *d_enter = reinterpret_cast<const uint32_t *>(s->out);
     if (d_leave) *d_leave = reinterpret_cast<const uint32_t *>(s->out + s->n_enter);
     return GWAOI_OK;
@@ -727,6 +979,7 @@ int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const 
 int gwaoi_strips_events(gwaoi_strips *s, gwaoi_events *out) {
     return gw::api_guard([&]() -> int {
     if (!s || !out) return GWAOI_EINVAL;
+    if (int rc = complete(s, false)) return rc;
     const uint64_t tot = s->n_enter + s->n_leave;
     if (tot > s->h_cap || !s->h_events) {
         if (s->h_events) (void)hipHostFree(s->h_events);
@@ -738,7 +991,7 @@ int gwaoi_strips_events(gwaoi_strips *s, gwaoi_events *out) {
     }
     if (tot) {
         S_TRY(hipMemcpyAsync(s->h_events, s->out, tot * sizeof(uint2), hipMemcpyDeviceToHost, s->st));
-        S_TRY(hipStreamSynchronize(s->st));
+        if (int rc = wait(s)) return rc;
     }
     out->n_enter = s->n_enter;
     out->n_leave = s->n_leave;

@@ -67,8 +67,12 @@ struct SpaceHost {
     bool grid_valid = false;
 };
 
+enum RunKind : uint8_t { RUN_MOVE = 0, RUN_ENTER = 1, RUN_LEAVE = 2 };
+
 struct Run {  // a stretch of the op queue: host ops [hbegin, hend) or a device batch
     bool device;
+    uint8_t kind;    // device batch: RUN_MOVE, or a structural batch (gwaoi_enter/leave_batch_device)
+    uint32_t space;  // RUN_ENTER / RUN_LEAVE: the space
     size_t hbegin, hend;
     const uint32_t *ds;
     const float *dx, *dz;
@@ -269,6 +273,12 @@ struct gwaoi_world {
     std::vector<unsigned long long> h_op_seq;
     std::vector<Run> runs;
     size_t n_ops = 0;
+    // device Enter/Leave batches (gwaoi_enter/leave_batch_device) queued for the next flush: their
+    // slots are known on the device only, so the per-slot host mirror (alive, space_of, in_frame)
+    // goes stale and is rebuilt from the frame on demand (host_slots)
+    uint32_t dev_app = 0;     // entries the queued device Enter batches append to S'
+    bool dev_struct = false;  // a device Enter/Leave batch is queued
+    bool slots_stale = false; // the host mirror misses device Enter/Leave batches of committed flushes
     // host move batches (gwaoi_moved_batch) staged as [slots | x | z | space] in pinned memory and sent
     // with one async H2D each (copy stream); they then run as device batches.  Two halves: the calls
     // queued while a flush is in flight stage into the half that flush does not read.
@@ -787,7 +797,8 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
                       cap, S.sc, reinterpret_cast<gw::TickOut *>(GWAOI_DIRECT_SUMMARY ? S.d_hout : S.dev_out), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
                       GWAOI_DIRECT_SUMMARY ? reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)) : nullptr,
-                      order ? w->tile_work : nullptr, order ? w->tile_order : nullptr, st);
+                      order ? w->tile_work : nullptr, order ? w->tile_order : nullptr,
+                      reinterpret_cast<uint32_t *>(S.dev_out), st);
     stage_end(w, S, ST_FINISH);
     return cap;
 }
@@ -820,7 +831,8 @@ int tick_launch(gwaoi_world *w) {
     const int set = w->launch_set;
     FlushSet &S = w->fs[set];
     const uint32_t n_prev = P.n;
-    const uint32_t n_app = (uint32_t)w->new_slots.size();
+    const uint32_t n_app_host = (uint32_t)w->new_slots.size();
+    const uint32_t n_app = n_app_host + w->dev_app;
     const uint32_t n_total = n_prev + n_app;
     const uint32_t n_new = w->n_alive;
 
@@ -860,11 +872,13 @@ int tick_launch(gwaoi_world *w) {
         HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
         w->copy_pending = false;
     }
+    // device runs only (device Enter/Leave batches included: their ops carry the space, the appended
+    // entries are initialised first and S' is copied, so the single-pass apply handles them)
     const bool moves_only = n_ops && host_ops == 0 && w->runs.size() <= gw::MAX_MOVE_RUNS && n_ops <= w->max_slots;
     // Virtual S': a flush of Moved batches only (or of nothing) changes no space and appends
     // no entry, so S' needs no copy of the previous frame: its spaces ARE the previous frame's,
     // and the records no op wrote are taken from the previous frame by k_keygen (seq check).
-    const bool virt = n_app == 0 && host_ops == 0 && (moves_only || n_ops == 0) && !w->force_copy;
+    const bool virt = n_app == 0 && host_ops == 0 && !w->dev_struct && (moves_only || n_ops == 0) && !w->force_copy;
     const gw::SlotSp *s_ss_view = virt ? P.ss : S.sss;
     gw::MoveRuns RS{};
     if (moves_only) {
@@ -872,6 +886,7 @@ int tick_launch(gwaoi_world *w) {
         for (const Run &r : w->runs) {
             gw::MoveRun &m = RS.r[RS.count++];
             m.ds = r.ds; m.dx = r.dx; m.dz = r.dz; m.dseq = r.dseq; m.dsp = r.dsp; m.seq0 = r.seq0;
+            m.sp_def = r.kind == RUN_MOVE ? gw::SP_KEEP : r.kind == RUN_ENTER ? r.space : gw::SP_DEAD;
             m.j0 = j0; m.n = (uint32_t)r.dn;
             j0 += (uint32_t)r.dn;
         }
@@ -902,10 +917,18 @@ int tick_launch(gwaoi_world *w) {
 
     // ---- apply queued ops onto S'
     stage_begin(w, S, ST_APPLY);
-    if (n_app) {
-        HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app * sizeof(uint32_t),
+    if (n_app_host) {
+        HIP_TRY(hipMemcpyAsync(w->new_slots_d, w->new_slots.data(), n_app_host * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
-        gw::launch_init_appended(w->new_slots_d, n_app, n_prev, S.srec, S.sss, w->sinfo, st);
+        gw::launch_init_appended(w->new_slots_d, n_app_host, n_prev, S.srec, S.sss, w->sinfo, w->max_slots, S.sc, st);
+    }
+    if (w->dev_app) {  // device Enter batches: their slots are appended after the host ones, in queue order
+        uint32_t base = n_prev + n_app_host;
+        for (const Run &r : w->runs)
+            if (r.device && r.kind == RUN_ENTER) {
+                gw::launch_init_appended(r.ds, (uint32_t)r.dn, base, S.srec, S.sss, w->sinfo, w->max_slots, S.sc, st);
+                base += (uint32_t)r.dn;
+            }
     }
     if (bucketed) {  // the per-tick position sync: ops regrouped by slot bucket, last op per slot in LDS
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
@@ -937,6 +960,8 @@ int tick_launch(gwaoi_world *w) {
                 const unsigned long long *sq;
                 uint64_t seq0 = 0;
                 uint32_t k;
+                const uint32_t sp_def = !r.device || r.kind == RUN_MOVE ? gw::SP_KEEP
+                                        : r.kind == RUN_ENTER ? r.space : gw::SP_DEAD;
                 if (r.device) {
                     sl = r.ds; xs = r.dx; zs = r.dz; sps = r.dsp; sq = r.dseq; seq0 = r.seq0; k = (uint32_t)r.dn;
                 } else {
@@ -948,7 +973,7 @@ int tick_launch(gwaoi_world *w) {
                 if (pass == 0)
                     gw::launch_ops_claim(sl, k, j0, w->max_slots, w->sinfo, tick_id, S.sc, st);
                 else
-                    gw::launch_ops_apply(sl, xs, zs, sps, k, j0, w->max_slots, w->sinfo, tick_id, n_total, sq, seq0,
+                    gw::launch_ops_apply(sl, xs, zs, sps, sp_def, k, j0, w->max_slots, w->sinfo, tick_id, n_total, sq, seq0,
                                          seq_base, r.device && r.dseq, S.srec, S.sss, S.sc, st);
                 j0 += k;
             }
@@ -1064,6 +1089,9 @@ void commit_host(gwaoi_world *w, const gw::TickOut *r) {
     w->h_op_seq.clear();
     w->runs.clear();
     w->n_ops = 0;
+    if (w->dev_struct) w->slots_stale = true;
+    w->dev_app = 0;
+    w->dev_struct = false;
     if (r && w->fl.dev_seq && r->seq_max >= w->seq_next) w->seq_next = r->seq_max + 1;  // no call was made in flight
     w->dev_seq_pending = false;
     w->seq_floor = w->fl.dev_seq ? w->seq_next : w->fl.seq_next;
@@ -1165,8 +1193,11 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
     *committed = true;
     // problems the device found in the queued ops: the frame is committed (the offending ops were
     // dropped), so the flush's events are valid and the caller still receives them
-    if (r.err & gw::ERR_COUNT_MISMATCH) {
-        w->last_error = "internal: live-count mismatch between host and device";
+    if (r.err & (gw::ERR_COUNT_MISMATCH | gw::ERR_ENTER_LIVE)) {
+        w->last_error = (r.err & gw::ERR_ENTER_LIVE)
+                            ? "device Enter batch of a slot live when the flush began (frame count broken)"
+                            : "live-count mismatch between host and device (a device Enter/Leave batch broke its "
+                              "rules, or an internal error)";
         return poison(w, GWAOI_EDEVICE);
     }
     if (r.err & gw::ERR_NONFINITE) {
@@ -1442,6 +1473,34 @@ int gwaoi_space_destroy(gwaoi_world *w, uint32_t space) {
 
 namespace {
 
+// The per-slot host mirror for a host call that reads it: rebuilt from the last committed frame
+// after device Enter/Leave batches (the frame holds exactly the live slots); GWAOI_ESTATE while
+// such a batch is queued or in flight (its slots are not known on the host yet).
+int host_slots(gwaoi_world *w) {
+    if (w->dev_struct || (w->in_flight && w->slots_stale)) {
+        w->last_error = "a device Enter/Leave batch is queued or in flight: flush before host per-slot calls";
+        return GWAOI_ESTATE;
+    }
+    if (!w->slots_stale) return GWAOI_OK;
+    const DevFrame &F = w->fr[w->cur];
+    std::vector<gw::SlotSp> ss(F.n);
+    if (F.n) {
+        HIP_TRY(hipMemcpyAsync(ss.data(), F.ss, F.n * sizeof(gw::SlotSp), hipMemcpyDeviceToHost, w->stream));
+        HIP_TRY(hipStreamSynchronize(w->stream));
+    }
+    std::fill(w->alive.begin(), w->alive.end(), 0);
+    std::fill(w->in_frame.begin(), w->in_frame.end(), 0);
+    std::fill(w->space_of.begin(), w->space_of.end(), gw::SP_DEAD);
+    for (const gw::SlotSp &e : ss) {
+        if (e.slot >= w->max_slots) continue;
+        w->alive[e.slot] = 1;
+        w->in_frame[e.slot] = 1;
+        w->space_of[e.slot] = e.sp;
+    }
+    w->slots_stale = false;
+    return GWAOI_OK;
+}
+
 // Explicit seqs must keep call order: >= the next implicit seq, and nothing
 // host-side may follow an explicit device batch inside one flush (its
 // largest seq is only known after the flush).
@@ -1459,6 +1518,7 @@ uint64_t take_seq(gwaoi_world *w, const uint64_t *seq) {
 int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, const uint64_t *seq) {
     if (!w) return GWAOI_EINVAL;
     GW_LIVE(w);
+    if (int rc = host_slots(w)) return rc;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
     if (w->alive[slot]) return GWAOI_ESTATE;
@@ -1487,6 +1547,7 @@ int enter_impl(gwaoi_world *w, uint32_t space, uint32_t slot, float x, float z, 
 int moved_impl(gwaoi_world *w, uint32_t slot, float x, float z, const uint64_t *seq) {
     if (!w) return GWAOI_EINVAL;
     GW_LIVE(w);
+    if (int rc = host_slots(w)) return rc;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (!w->alive[slot]) return GWAOI_ESTATE;
     if (!finite2(x, z)) return GWAOI_ENONFINITE;
@@ -1668,6 +1729,7 @@ int gwaoi_leave(gwaoi_world *w, uint32_t slot) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     GW_LIVE(w);
+    if (int rc = host_slots(w)) return rc;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (!w->alive[slot]) return GWAOI_ESTATE;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
@@ -1702,6 +1764,7 @@ int gwaoi_enter_batch(gwaoi_world *w, uint32_t space, const uint32_t *slots, con
     GW_LIVE(w);
     if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
     if (w->dev_seq_pending) return GWAOI_ESTATE;
+    if (int rc = host_slots(w)) return rc;
     // validate the whole batch first (duplicates inside the batch are Enter-twice)
     std::vector<uint32_t> seen;
     seen.reserve(n);
@@ -1723,6 +1786,7 @@ int gwaoi_leave_batch(gwaoi_world *w, const uint32_t *slots, size_t n) {
     if (!w || (n && !slots)) return GWAOI_EINVAL;
     GW_LIVE(w);
     if (w->dev_seq_pending) return GWAOI_ESTATE;
+    if (int rc = host_slots(w)) return rc;
     std::vector<uint32_t> seen(slots, slots + n);
     for (size_t i = 0; i < n; ++i) {
         if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
@@ -1740,6 +1804,7 @@ int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, con
     if (!w || (n && (!slots || !x || !z))) return GWAOI_EINVAL;
     GW_LIVE(w);
     if (w->dev_seq_pending) return GWAOI_ESTATE;
+    if (int rc = host_slots(w)) return rc;
     // Batches of kStageMinBatch+ moves go through pinned staging as one device batch (single-pass
     // move apply); without room (or if the staging allocation failed) they queue as host ops.
     if (n >= kStageMinBatch && n <= 0xFFFFFFFFull - w->n_ops && ensure_stage(w, 4 * n) == GWAOI_OK)
@@ -1807,6 +1872,74 @@ int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const 
     });
 }
 
+int gwaoi_enter_batch_device(gwaoi_world *w, uint32_t space, const uint32_t *d_slots, const float *d_x,
+                             const float *d_z, const uint64_t *d_seq, size_t n, const float *box) {
+    return gw::api_guard([&]() -> int {
+    if (!w || (n && (!d_slots || !d_x || !d_z))) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
+    if (w->in_flight || w->sync) return GWAOI_ESTATE;
+    if (!d_seq && w->dev_seq_pending) return GWAOI_ESTATE;
+    if (!n) return GWAOI_OK;
+    if (n > (size_t)w->max_slots - w->n_alive || n > 0xFFFFFFFFull - w->n_ops) return GWAOI_ECAPACITY;
+    if (box && !(std::isfinite(box[0]) && std::isfinite(box[1]) && std::isfinite(box[2]) && std::isfinite(box[3]) &&
+                 box[0] <= box[2] && box[1] <= box[3]))
+        return GWAOI_EINVAL;
+    Run r{};
+    r.device = true;
+    r.kind = RUN_ENTER;
+    r.space = space;
+    r.ds = d_slots;
+    r.dx = d_x;
+    r.dz = d_z;
+    r.dseq = reinterpret_cast<const unsigned long long *>(d_seq);
+    r.seq0 = d_seq ? 0 : w->seq_next;
+    r.dn = n;
+    if (!d_seq) w->seq_next += n;
+    else w->dev_seq_pending = true;
+    w->runs.push_back(r);
+    w->n_ops += n;
+    w->dev_app += (uint32_t)n;
+    w->dev_struct = true;
+    w->space_ops_queued = true;
+    w->n_alive += (uint32_t)n;
+    SpaceHost &S = w->spaces[space];
+    S.alive += (uint32_t)n;
+    if (box) {
+        note_pending_bbox(S, box[0], box[1]);
+        note_pending_bbox(S, box[2], box[3]);
+    }
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_leave_batch_device(gwaoi_world *w, uint32_t space, const uint32_t *d_slots, size_t n) {
+    return gw::api_guard([&]() -> int {
+    if (!w || (n && !d_slots)) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (space >= w->n_space_ids || !w->spaces[space].used) return GWAOI_EBADSPACE;
+    if (w->in_flight || w->sync) return GWAOI_ESTATE;
+    if (!n) return GWAOI_OK;
+    if (n > w->spaces[space].alive || n > 0xFFFFFFFFull - w->n_ops) return GWAOI_ESTATE;
+    Run r{};
+    r.device = true;
+    r.kind = RUN_LEAVE;
+    r.space = space;
+    r.ds = d_slots;
+    // a Leave has no position: the slot array stands in for x and z (read, never used)
+    r.dx = r.dz = reinterpret_cast<const float *>(d_slots);
+    r.seq0 = w->seq_next;  // a Leave's seq is never compared
+    r.dn = n;
+    w->runs.push_back(r);
+    w->n_ops += n;
+    w->dev_struct = true;
+    w->space_ops_queued = true;
+    w->n_alive -= (uint32_t)n;
+    w->spaces[space].alive -= (uint32_t)n;
+    return GWAOI_OK;
+    });
+}
+
 }  // extern "C"
 
 namespace gw {
@@ -1829,7 +1962,15 @@ SyncState *&world_sync(gwaoi_world *w) { return w->sync; }
 
 void world_set_error(gwaoi_world *w, const char *msg) { w->last_error = msg; }
 
+void world_flush_events(gwaoi_world *w, const uint32_t **events, const uint32_t **dcount, uint64_t *cap) {
+    FlushSet &S = w->fs[w->in_flight ? w->fl.set : w->last_set];
+    *events = S.events;
+    *dcount = reinterpret_cast<const uint32_t *>(S.dev_out);
+    *cap = w->in_flight ? w->fl.cap : std::min(S.ev_cap, w->evtmp_cap);
+}
+
 uint32_t world_slot_space(gwaoi_world *w, uint32_t slot) {
+    if (host_slots(w) != GWAOI_OK) return SP_DEAD;
     return slot < w->max_slots && w->alive[slot] ? w->space_of[slot] : SP_DEAD;
 }
 
@@ -2056,6 +2197,7 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
     if (w->in_flight) return GWAOI_ESTATE;
     if (slot >= w->max_slots) return GWAOI_EBADSLOT;
     if (n_out) *n_out = 0;
+    if (int rc = host_slots(w)) return rc;
     if (!w->in_frame[slot]) return GWAOI_ESTATE;
     const size_t need = std::max<size_t>(cap, 1);
     if (need > w->nb_cap) {
@@ -2114,6 +2256,7 @@ int gwaoi_restore(gwaoi_world *w, const uint32_t *slots, const uint32_t *spaces,
     if (!w || (n && (!slots || !spaces || !x || !z || !seq))) return GWAOI_EINVAL;
     GW_LIVE(w);
     if (w->n_ops || w->dev_seq_pending || w->in_flight) return GWAOI_ESTATE;
+    if (int rc = host_slots(w)) return rc;
     std::vector<size_t> ord(n);
     for (size_t i = 0; i < n; ++i) ord[i] = i;
     std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return seq[a] < seq[b]; });

@@ -10,16 +10,20 @@ halo H of its strip.  Each tick:
    entities the rank owned before it (Moved / Leave) or that enter the space
    inside its strip (Enter) become halo records per destination rank, plus
    teleport records (HIP kernels, ``k_route``).
-2. ``exchange``: the per-destination counts (already on the host) are
+2. ``exchange``: the per-destination counts (already on the host, with how
+   many of them are ENTER / LEAVE records and the box of the ENTERs) are
    all-gathered over gloo, then the records go point to point in one
    ``batch_isend_irecv`` group over RCCL (xGMI) -- to the two neighbour
    strips only, when strips are at least H + teleport wide; teleport records
-   are all-gathered only when some rank has any.  This is the path's one real
+   go to every rank only when some rank has any.  This is the path's one real
    data exchange.
-3. ``StripShard.finish(recv, tele)``: the records become ops of the rank's
-   gwaoi world (explicit global seqs), the world flushes, and only the events
-   this strip owns are kept (enter: owner after the tick; leave: owner
-   before it).  The union over ranks is the whole space's net diff.
+3. ``StripShard.finish(recv, tele, kinds)``: queued on the GPU without a host
+   wait (gwaoi_strips_tick_async): the records become device Leave / Enter /
+   Moved batches of the rank's gwaoi world (explicit global seqs), the world
+   flushes, and only the events this strip owns are kept (enter: owner after
+   the tick; leave: owner before it).  The union over ranks is the whole
+   space's net diff.  The next ``route`` completes the tick with the same
+   host wait that brings its counts: one host wait per tick.
 
 ``tile_tick`` runs the three steps for one rank of a ``torch.distributed``
 job; ``local_tick`` runs several strips in one process (loopback exchange,
@@ -85,6 +89,37 @@ def make_ops(slots, x, z, seq, kind=HALO_MOVE) -> np.ndarray:
     a["kind"] = kind
     a["seq"] = np.asarray(seq, np.uint64)
     return a
+
+
+def kinds_of(send: np.ndarray, counts) -> tuple:
+    """Kind statistics of routed records (HALO_DTYPE, grouped by destination): per destination,
+    the ENTER and LEAVE records and the box (x0, z0, x1, z1) of the ENTER positions, as
+    gwaoi_strips_route_kinds reports them (CPU model and checks)."""
+    S = len(counts)
+    ent = np.zeros(S, np.int64)
+    lev = np.zeros(S, np.int64)
+    box = np.tile(np.array([np.inf, np.inf, -np.inf, -np.inf], np.float32), (S, 1))
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    for q in range(S):
+        r = send[off[q]:off[q + 1]]
+        e = r[r["kind"] == HALO_ENTER]
+        ent[q] = e.size
+        lev[q] = int(np.sum(r["kind"] == HALO_LEAVE))
+        if e.size:
+            box[q] = (e["x"].min(), e["z"].min(), e["x"].max(), e["z"].max())
+    return ent, lev, box
+
+
+def merge_kinds(parts) -> tuple:
+    """A receiver's (enters, leaves, box) from the senders' (enters, leaves, box) for it."""
+    ne = sum(int(p[0]) for p in parts)
+    nl = sum(int(p[1]) for p in parts)
+    b = np.array([np.inf, np.inf, -np.inf, -np.inf], np.float32)
+    for p in parts:
+        if int(p[0]):
+            b = np.array([min(b[0], p[2][0]), min(b[1], p[2][1]), max(b[2], p[2][2]), max(b[3], p[2][3])],
+                         np.float32)
+    return ne, nl, (b if ne else None)
 
 
 def as_words(rec: np.ndarray, words: int):
@@ -172,6 +207,12 @@ class StripShard:
         counts = (C.c_uint64 * (self.n_strips + 1))()  # the one host wait of the route: the counts
         self._check(self._L.gwaoi_strips_route(self._s, C.c_void_p(ops.data_ptr() if n else 0), n, counts))
         c = np.array(counts[:], np.int64)
+        S = self.n_strips
+        ent, lev = (C.c_uint64 * S)(), (C.c_uint64 * S)()
+        box = np.empty((S, 4), np.float32)
+        self._check(self._L.gwaoi_strips_route_kinds(self._s, ent, lev, _p(box)))
+        self.kinds = (np.array(ent[:], np.int64), np.array(lev[:], np.int64), box)
+        self._inflight = [ops]  # the route's host wait completed the previous tick; the scatter reads ops
         send = torch.empty((int(c[:-1].sum()), HALO_WORDS), dtype=torch.int32, device=self.dev)
         tele = torch.empty((int(c[-1]), TELE_WORDS), dtype=torch.int32, device=self.dev)
         self._after_torch(send, tele)
@@ -181,23 +222,46 @@ class StripShard:
         return send, c[:-1], tele
 
     # ---- step 3: apply the exchanged records, flush, keep this strip's events
-    def finish(self, local, recv, tele) -> Tuple[int, int]:
+    def finish(self, local, recv, tele, kinds=None):
         """local: this strip's own slice of its send buffer; recv: the records
-        from the other strips; tele: all teleport records."""
-        ne, nl = C.c_uint64(), C.c_uint64()
+        from the other strips; tele: all teleport records; kinds: this receiver's
+        (ENTER records, LEAVE records, box of the ENTERs or None) over local + recv,
+        from the senders' route statistics (``exchange(..., kinds=...)``).  With
+        kinds the tick is queued and nothing waits (complete it with ``wait`` /
+        ``events`` / the next ``route``); returns None.  Without, the strip layer
+        reads the kinds back first and waits for the tick: returns (n_enter, n_leave)."""
         nlo, nr, nt = int(local.shape[0]), int(recv.shape[0]), int(tele.shape[0])
         self._after_torch(local, recv, tele)  # the exchange's writes land before the tick reads them
-        self._check(self._L.gwaoi_strips_tick(self._s, C.c_void_p(local.data_ptr() if nlo else 0), nlo,
-                                              C.c_void_p(recv.data_ptr() if nr else 0), nr,
-                                              C.c_void_p(tele.data_ptr() if nt else 0), nt, C.byref(ne),
-                                              C.byref(nl)))
-        self._inflight.clear()  # gwaoi_strips_tick returned after its last host wait: nothing in flight
+        pl, pr, pt = (C.c_void_p(t.data_ptr() if k else 0) for t, k in ((local, nlo), (recv, nr), (tele, nt)))
+        if kinds is None:
+            ne, nl = C.c_uint64(), C.c_uint64()
+            self._check(self._L.gwaoi_strips_tick(self._s, pl, nlo, pr, nr, pt, nt, C.byref(ne), C.byref(nl)))
+            self._inflight.clear()  # gwaoi_strips_tick returned after its last host wait: nothing in flight
+            return ne.value, nl.value
+        n_ent, n_lev, box = kinds
+        b = np.ascontiguousarray(box, np.float32) if box is not None else None
+        self._check(self._L.gwaoi_strips_tick_async(self._s, pl, nlo, pr, nr, pt, nt, int(n_ent), int(n_lev),
+                                                    _p(b) if b is not None else None))
+        return None
+
+    def wait(self) -> Tuple[int, int]:
+        """Complete the queued tick: its (n_enter, n_leave)."""
+        ne, nl = C.c_uint64(), C.c_uint64()
+        self._check(self._L.gwaoi_strips_wait(self._s, C.byref(ne), C.byref(nl)))
+        self._inflight.clear()
         return ne.value, nl.value
 
+    def host_waits(self) -> int:
+        """Stream synchronisations of the strip layer so far (gwaoi_strips_host_waits)."""
+        n = C.c_uint64()
+        self._check(self._L.gwaoi_strips_host_waits(self._s, C.byref(n)))
+        return n.value
+
     def events(self):
-        """This strip's events of the last tick as (n,2) uint32 arrays [a, b]."""
+        """This strip's events of the last tick as (n,2) uint32 arrays [a, b] (completes a queued tick)."""
         ev = Events()
         self._check(self._L.gwaoi_strips_events(self._s, C.byref(ev)))
+        self._inflight.clear()
         ne, nl = ev.n_enter, ev.n_leave
         ent = np.ctypeslib.as_array(ev.enter, shape=(2 * ne,)).reshape(ne, 2).copy() if ne else np.empty((0, 2), np.uint32)
         lev = np.ctypeslib.as_array(ev.leave, shape=(2 * nl,)).reshape(nl, 2).copy() if nl else np.empty((0, 2), np.uint32)
@@ -206,6 +270,7 @@ class StripShard:
     def events_device(self):
         e, l = C.c_void_p(), C.c_void_p()
         self._check(self._L.gwaoi_strips_events_device(self._s, C.byref(e), C.byref(l)))
+        self._inflight.clear()
         return e.value, l.value
 
 
@@ -252,7 +317,7 @@ def count_group(dist, group=None):
     return _COUNT_GROUPS[key]
 
 
-def exchange(dist, send, counts, tele, group=None, via_cpu=False):
+def exchange(dist, send, counts, tele, group=None, via_cpu=False, kinds=None):
     """The halo exchange of one tick over torch.distributed: the count matrix
     is all-gathered on the host (gloo, ``count_group``), then every record
     travels point to point, batched in one group (``batch_isend_irecv``:
@@ -263,20 +328,32 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
     (the count matrix carries them), in the same batch.  Returns
     (records from the other ranks in source-rank order, all teleports).
     via_cpu: GPU tensors go through host memory (gloo rehearsal of several
-    ranks sharing one GPU; RCCL allows one rank per device)."""
+    ranks sharing one GPU; RCCL allows one rank per device).
+    kinds: this rank's route statistics (enters[S], leaves[S], boxes[S, 4]);
+    they travel in the same count row, and the receiver's merged
+    (enters, leaves, box) is returned third (for ``StripShard.finish``)."""
     import torch
     if via_cpu and send.is_cuda:
         dev = send.device
         torch.cuda.current_stream(dev).synchronize()
-        r, t = exchange(dist, send.cpu(), counts, tele.cpu(), group)
-        return r.to(dev), t.to(dev)
+        res = exchange(dist, send.cpu(), counts, tele.cpu(), group, kinds=kinds)
+        return (res[0].to(dev), res[1].to(dev)) + tuple(res[2:])
     S = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = send.device
-    mine = torch.tensor(list(np.asarray(counts, np.int64)) + [int(tele.shape[0])], dtype=torch.int64)
+    row = list(np.asarray(counts, np.int64)) + [int(tele.shape[0])]
+    if kinds is not None:
+        ent, lev, box = kinds
+        row += list(np.asarray(ent, np.int64)) + list(np.asarray(lev, np.int64))
+        row += list(np.ascontiguousarray(box, np.float32).reshape(-1).view(np.int32).astype(np.int64))
+    mine = torch.tensor(row, dtype=torch.int64)
     rows = [torch.empty_like(mine) for _ in range(S)]
     dist.all_gather(rows, mine, group=count_group(dist, group))
     M = torch.stack(rows).numpy()  # M[src, dst]; column S = teleports of src (host tensors: no device sync)
+    rk = None
+    if kinds is not None:  # the senders' statistics for this receiver
+        bx = M[:, 3 * S + 1:].astype(np.int32).view(np.float32).reshape(S, S, 4)
+        rk = merge_kinds([(M[q, S + 1 + rank], M[q, 2 * S + 1 + rank], bx[q, rank]) for q in range(S)])
     off = np.concatenate([[0], np.cumsum(M[rank, :S])]).astype(np.int64)
     peer = (lambda q: q) if group is None else (lambda q: dist.get_global_rank(group, q))
     T = M[:, S]  # teleport records per source rank
@@ -301,15 +378,16 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False):
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     recv = torch.cat(parts) if parts else send[:0]
-    if T.sum() == 0:
-        return recv, tele[:0]
-    return recv, torch.cat([tparts[r] for r in range(S) if T[r]])
+    tele_all = tele[:0] if T.sum() == 0 else torch.cat([tparts[r] for r in range(S) if T[r]])
+    return (recv, tele_all) if kinds is None else (recv, tele_all, rk)
 
 
-def exchange_local(outs: List[Tuple]):
+def exchange_local(outs: List[Tuple], kinds=None):
     """Loopback exchange for several strips in one process: outs[r] =
     (send, counts, tele) of strip r.  Returns [(recv, tele_all)] per strip
-    (records from the other strips in source rank order, like ``exchange``)."""
+    (records from the other strips in source rank order, like ``exchange``);
+    with kinds[r] = strip r's route statistics, [(recv, tele_all, kinds of the
+    receiver)]."""
     import torch
     S = len(outs)
     starts = []
@@ -322,19 +400,31 @@ def exchange_local(outs: List[Tuple]):
         parts = [outs[r][0][int(starts[r][q]):int(starts[r][q + 1])] for r in range(S) if r != q]
         if not parts:
             parts = [outs[q][0][:0]]
-        res.append((torch.cat(parts), tele_all))
+        r = (torch.cat(parts), tele_all)
+        if kinds is not None:
+            r += (merge_kinds([(kinds[src][0][q], kinds[src][1][q], kinds[src][2][q]) for src in range(S)]),)
+        res.append(r)
     return res
 
 
-def tile_tick(shard: StripShard, dist, ops, group=None) -> Tuple[int, int]:
-    """One tick of this rank's strip in a torch.distributed job."""
+def tile_tick(shard: StripShard, dist, ops, group=None, via_cpu=False):
+    """One tick of this rank's strip in a torch.distributed job: route (the tick's one host
+    wait, which also completes the previous tick), exchange, and the tick queued on the GPU
+    (``shard.wait()`` / ``shard.events()`` complete it)."""
     send, counts, tele = shard.route(ops)
-    recv, tele_all = exchange(dist, send, counts, tele, group=group)
-    return shard.finish(local_slice(send, counts, dist.get_rank(group)), recv, tele_all)
+    recv, tele_all, kinds = exchange(dist, send, counts, tele, group=group, via_cpu=via_cpu, kinds=shard.kinds)
+    shard.finish(local_slice(send, counts, dist.get_rank(group)), recv, tele_all, kinds=kinds)
+    return send, counts, recv
 
 
-def local_tick(shards: Sequence[StripShard], ops_per_strip) -> List[Tuple[int, int]]:
-    """One tick of several strips in one process (loopback exchange)."""
+def local_tick(shards: Sequence[StripShard], ops_per_strip, sync=False):
+    """One tick of several strips in one process (loopback exchange), queued on each
+    strip's stream; sync=True: gwaoi_strips_tick instead (reads the kinds back, waits)."""
     outs = [sh.route(o) for sh, o in zip(shards, ops_per_strip)]
-    ex = exchange_local(outs)
-    return [sh.finish(local_slice(o[0], o[1], q), r, t) for q, (sh, o, (r, t)) in enumerate(zip(shards, outs, ex))]
+    if sync:
+        ex = exchange_local(outs)
+        return [sh.finish(local_slice(o[0], o[1], q), r, t) for q, (sh, o, (r, t)) in enumerate(zip(shards, outs, ex))]
+    ex = exchange_local(outs, kinds=[sh.kinds for sh in shards])
+    for q, (sh, o, (r, t, k)) in enumerate(zip(shards, outs, ex)):
+        sh.finish(local_slice(o[0], o[1], q), r, t, kinds=k)
+    return None

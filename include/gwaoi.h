@@ -168,6 +168,25 @@ int gwaoi_moved_seq(gwaoi_world *w, uint32_t slot, float x, float z, uint64_t se
 int gwaoi_moved_batch_device_seq(gwaoi_world *w, const uint32_t *d_slots, const float *d_x, const float *d_z,
                                  const uint64_t *d_seq, size_t n);
 
+/* ---- structural device batches ----------------------------------------------
+ * Enter / Leave calls whose slots live in device memory (Space.go:211,243): the
+ * entities crossing into / out of a strip world (gwaoi_strips.h) without a host
+ * round trip.  The host learns only the counts, so the world's per-slot host
+ * mirror goes stale; it is rebuilt from the device on the next host call that
+ * needs it (a host Enter/Leave/Moved/batch, gwaoi_neighbors), which returns
+ * GWAOI_ESTATE while such a batch is queued and not yet flushed.  Rules, checked
+ * on the device: an entered slot is not live when the flush begins, a left slot
+ * is live (the host counts it out of `space`), each slot appears once in the
+ * flush.  A violation breaks
+ * the frame's live count: the flush fails and the world is poisoned.
+ * gwaoi_enter_batch_device: d_seq NULL = implicit seqs (call order), else
+ * explicit seqs (rules above); box = {x0, z0, x1, z1} holding every entered
+ * position (sizes the space's grid), or NULL.  Not while a flush is in flight,
+ * nor on a world with an entity-sync layer (gwaoi_sync.h). */
+int gwaoi_enter_batch_device(gwaoi_world *w, uint32_t space, const uint32_t *d_slots, const float *d_x,
+                             const float *d_z, const uint64_t *d_seq, size_t n, const float *box);
+int gwaoi_leave_batch_device(gwaoi_world *w, uint32_t space, const uint32_t *d_slots, size_t n);
+
 /* ---- flush ------------------------------------------------------------------ */
 /* Run the tick and copy its events to host memory.  If the device found a bad
  * op in a device batch (dropped; GWAOI_ESTATE / GWAOI_ENONFINITE /

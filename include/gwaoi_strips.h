@@ -22,14 +22,21 @@
  * Per tick, on every rank:
  *   1. gwaoi_strips_route(ops)  -- the owned entities' Enter/Moved/Leave of this
  *      tick (their owner before the tick receives them) become halo records
- *      per destination rank + teleport records; returns the counts.
+ *      per destination rank + teleport records; returns the counts, and
+ *      gwaoi_strips_route_kinds how many of each destination's records are
+ *      ENTER / LEAVE (and the box of the ENTER positions).
  *   2. gwaoi_strips_route_scatter(send, tele) -- writes them, grouped by
  *      destination rank, into caller device buffers.
- *   3. the caller exchanges them (all_to_all over RCCL / xGMI; teleports
- *      all-gathered) -- see goworld_amd/strips.py.
- *   4. gwaoi_strips_tick(local, recv, tele_all) -- applies its own and the
- *      received records to the world, flushes it, and filters its events to
- *      the ones this strip owns.
+ *   3. the caller exchanges them (counts on the host, records point to point
+ *      over RCCL / xGMI; teleports to every rank) -- see goworld_amd/strips.py.
+ *   4. gwaoi_strips_tick_async(local, recv, tele_all, enters, leaves, box) --
+ *      queues: its own and the received records become device Leave / Enter /
+ *      Moved batches of the world (gwaoi.h), the world flushes, and its events
+ *      are filtered to the ones this strip owns.  Nothing waits: the next
+ *      gwaoi_strips_route (or gwaoi_strips_wait / _events) completes the tick
+ *      with the same host wait that brings the route's counts, so a tick has
+ *      ONE host wait.  gwaoi_strips_tick does 4. and waits (two waits: it
+ *      reads the record kinds back first).
  *
  * Single-threaded per strip, on the world's stream.  All counts are records.
  */
@@ -100,6 +107,25 @@ int gwaoi_strips_route_scatter(gwaoi_strips *s, gwaoi_halo_rec *d_send, gwaoi_te
 int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local, const gwaoi_halo_rec *d_recv,
                       size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele, uint64_t *n_enter,
                       uint64_t *n_leave);
+/* After gwaoi_strips_route: per destination rank q (n_strips entries each),
+ * the ENTER and LEAVE records among counts[q] and the box {x0, z0, x1, z1} of
+ * the ENTER positions (+inf, +inf, -inf, -inf when none).  A receiver sums
+ * them over the senders for gwaoi_strips_tick_async. */
+int gwaoi_strips_route_kinds(const gwaoi_strips *s, uint64_t *enters, uint64_t *leaves, float *enter_boxes);
+/* 4. (asynchronous) As gwaoi_strips_tick, with the receiver's ENTER / LEAVE
+ * record counts over d_local + d_recv and the box of their positions (NULL:
+ * unknown) taken from the senders' gwaoi_strips_route_kinds.  Queues the tick
+ * on the world's stream and returns; the inputs must stay valid until it
+ * completes (the next gwaoi_strips_route, gwaoi_strips_wait, _events,
+ * _events_device or _destroy).  Problems found on the device are reported
+ * by the call that completes it. */
+int gwaoi_strips_tick_async(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local,
+                            const gwaoi_halo_rec *d_recv, size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele,
+                            uint64_t n_enter_recs, uint64_t n_leave_recs, const float *enter_box);
+/* Complete the queued tick (host wait if needed); its event counts. */
+int gwaoi_strips_wait(gwaoi_strips *s, uint64_t *n_enter, uint64_t *n_leave);
+/* Host waits (stream synchronisations) of the strip layer so far (tests, bench). */
+int gwaoi_strips_host_waits(const gwaoi_strips *s, uint64_t *waits);
 /* Device pointers of this strip's events of the last tick (layout of
  * gwaoi_events: enter pairs, then leave pairs, a0,b0,a1,b1,...). */
 int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const uint32_t **d_leave);

@@ -29,6 +29,8 @@
  *
  * Node ids are manager-local dense integers in [0, cap).
  */
+#include <limits.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -356,17 +358,38 @@ int64_t xz_apply(xzmgr *m, int64_t n, const uint8_t *op, const int32_t *id, cons
 
 /* Bulk equivalent of Enter(id[0..n)) in array order on an empty manager: the
  * same sorted lists and the same neighbour sets (closed form with seq = array
- * position) in O(n log n + E) instead of go-aoi's O(n^2)
+ * position) in O(n + E) instead of go-aoi's O(n^2)
  * head-scan inserts.  No events are emitted.  Used only to populate the
- * bench's cpu_baseline at 1M entities; tests check it against real Enters. */
-extern int64_t cf_pairs_ex(int64_t n, const float *x, const float *z, const uint64_t *seq, const uint32_t *sp,
-                           const float *D, uint64_t **out, int sort);
-static const float *g_sort_c;
-static int cmp_by_c(const void *pa, const void *pb) {
-    int32_t a = *(const int32_t *)pa, b = *(const int32_t *)pb;
-    float ca = g_sort_c[a], cb = g_sort_c[b];
-    return ca < cb ? -1 : (ca > cb);
+ * bench's cpu_baseline (1M entities at config 3, 2^24 at config 5); tests check
+ * it against real Enters.  The lists come from a stable LSD radix sort of the
+ * coordinates (equal coordinates keep array order); the neighbour sets from a
+ * grid of 2D cells, one thread per entity's own set (OpenMP). */
+static inline uint32_t fkey(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+
+/* positions 0..n-1 ordered stably by key[] (4 passes of 8 bits) */
+static void radix_order(int64_t n, const uint32_t *key, int32_t *ord) {
+    int32_t *tmp = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
+    for (int64_t i = 0; i < n; i++) ord[i] = (int32_t)i;
+    for (int sh = 0; sh < 32; sh += 8) {
+        int64_t cnt[257] = {0};
+        for (int64_t i = 0; i < n; i++) cnt[((key[ord[i]] >> sh) & 255u) + 1]++;
+        for (int b = 0; b < 256; b++) cnt[b + 1] += cnt[b];
+        for (int64_t i = 0; i < n; i++) tmp[cnt[(key[ord[i]] >> sh) & 255u]++] = ord[i];
+        int32_t *t = ord;
+        memcpy(t, tmp, sizeof(int32_t) * n);
+    }
+    free(tmp);
+}
+
+static inline int bulk_pred(float wx, float wz, float lx, float lz, float D) {
+    const float lox = wx - D, hix = wx + D, loz = wz - D, hiz = wz + D;
+    return lx >= lox && lx <= hix && lz >= loz && lz <= hiz;
+}
+
 int xz_bulk_enter(xzmgr *m, int64_t n, const int32_t *id, const float *x, const float *z) {
     if (m->xhead != NIL || m->zhead != NIL) return -1;
     for (int64_t i = 0; i < n; i++)
@@ -378,32 +401,77 @@ int xz_bulk_enter(xzmgr *m, int64_t n, const int32_t *id, const float *x, const 
         m->mark[id[i]] = 0;
     }
     int32_t *ord = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
+    uint32_t *key = (uint32_t *)malloc(sizeof(uint32_t) * (n ? n : 1));
     for (int a = 0; a < 2; a++) {
         axis A = a == 0 ? ax_x(m) : ax_z(m);
-        for (int64_t i = 0; i < n; i++) ord[i] = id[i];
-        g_sort_c = A.c;
-        qsort(ord, n, sizeof(int32_t), cmp_by_c);
-        for (int64_t i = 0; i < n; i++) {
-            A.prev[ord[i]] = i ? ord[i - 1] : NIL;
-            A.next[ord[i]] = i + 1 < n ? ord[i + 1] : NIL;
+        const float *c = a == 0 ? x : z;
+        for (int64_t i = 0; i < n; i++) key[i] = fkey(c[i]);
+        radix_order(n, key, ord);
+        for (int64_t k = 0; k < n; k++) {
+            const int32_t e = id[ord[k]];
+            A.prev[e] = k ? id[ord[k - 1]] : NIL;
+            A.next[e] = k + 1 < n ? id[ord[k + 1]] : NIL;
         }
-        *A.head = n ? ord[0] : NIL;
-        *A.tail = n ? ord[n - 1] : NIL;
+        *A.head = n ? id[ord[0]] : NIL;
+        *A.tail = n ? id[ord[n - 1]] : NIL;
     }
+    free(key);
     free(ord);
-    uint64_t *seq = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
-    uint32_t *sp = (uint32_t *)calloc(n ? n : 1, sizeof(uint32_t));
-    for (int64_t i = 0; i < n; i++) seq[i] = (uint64_t)i + 1;
-    uint64_t *pairs = NULL;
-    float D = m->D;
-    int64_t np = cf_pairs_ex(n, x, z, seq, sp, &D, &pairs, 0);
-    for (int64_t k = 0; k < np; k++) {
-        int64_t ia = (int64_t)(pairs[k] >> 32), ib = (int64_t)(pairs[k] & 0xFFFFFFFFu);
-        nset_add(&m->nb[id[ia]], id[ib]);
+    if (n < 2) return 0;
+    /* cells of side C = 2D: a window [fl32(w-D), fl32(w+D)] spans at most the 3x3 cells around w */
+    /* (wider cells for a sparse world: any side >= 2D keeps the 3x3 neighbourhood complete) */
+    const float D = m->D;
+    double x0 = INFINITY, z0 = INFINITY, x1 = -INFINITY, z1 = -INFINITY;
+    for (int64_t i = 0; i < n; i++) {
+        x0 = fmin(x0, x[i]); x1 = fmax(x1, x[i]);
+        z0 = fmin(z0, z[i]); z1 = fmax(z1, z[i]);
     }
-    free(pairs);
-    free(seq);
-    free(sp);
+    double C = 2.0 * (double)D;
+    while (((x1 - x0) / C + 2.0) * ((z1 - z0) / C + 2.0) > 4.0 * (double)n + 1024.0) C *= 2.0;
+    int64_t cx0 = INT64_MAX, cz0 = INT64_MAX, cx1 = INT64_MIN, cz1 = INT64_MIN;
+    int64_t *cxz = (int64_t *)malloc(sizeof(int64_t) * 2 * n);
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t cx = (int64_t)floor((double)x[i] / C), cz = (int64_t)floor((double)z[i] / C);
+        cxz[2 * i] = cx;
+        cxz[2 * i + 1] = cz;
+        if (cx < cx0) cx0 = cx;
+        if (cx > cx1) cx1 = cx;
+        if (cz < cz0) cz0 = cz;
+        if (cz > cz1) cz1 = cz;
+    }
+    const int64_t gx = cx1 - cx0 + 1, gz = cz1 - cz0 + 1;
+    int64_t *start = (int64_t *)calloc((size_t)(gx * gz + 1), sizeof(int64_t));
+    int32_t *cell = (int32_t *)malloc(sizeof(int32_t) * n);
+    for (int64_t i = 0; i < n; i++) start[(cxz[2 * i] - cx0) * gz + (cxz[2 * i + 1] - cz0) + 1]++;
+    for (int64_t c = 0; c < gx * gz; c++) start[c + 1] += start[c];
+    {
+        int64_t *fill = (int64_t *)malloc(sizeof(int64_t) * (size_t)(gx * gz));
+        memcpy(fill, start, sizeof(int64_t) * (size_t)(gx * gz));
+        for (int64_t i = 0; i < n; i++) cell[fill[(cxz[2 * i] - cx0) * gz + (cxz[2 * i + 1] - cz0)]++] = (int32_t)i;
+        free(fill);
+    }
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t cx = cxz[2 * i] - cx0, cz = cxz[2 * i + 1] - cz0;
+        nset *s = &m->nb[id[i]];
+        for (int64_t ux = cx - 1; ux <= cx + 1; ux++) {
+            if (ux < 0 || ux >= gx) continue;
+            for (int64_t uz = cz - 1; uz <= cz + 1; uz++) {
+                if (uz < 0 || uz >= gz) continue;
+                const int64_t c = ux * gz + uz;
+                for (int64_t k = start[c]; k < start[c + 1]; k++) {
+                    const int64_t j = cell[k];
+                    if (j == i) continue;
+                    /* the later of the two (larger array position = larger seq) owns the window */
+                    const int nb = j < i ? bulk_pred(x[i], z[i], x[j], z[j], D) : bulk_pred(x[j], z[j], x[i], z[i], D);
+                    if (nb) nset_add(s, id[j]);
+                }
+            }
+        }
+    }
+    free(start);
+    free(cell);
+    free(cxz);
     return 0;
 }
 

@@ -12,7 +12,7 @@ from __future__ import annotations
 import numpy as np
 
 from goworld_amd.strips import (HALO_DTYPE, HALO_ENTER, HALO_LEAVE, HALO_MOVE, HALO_WORDS, TELE_DTYPE, TELE_WORDS,
-                                as_words, default_teleport)
+                                as_words, default_teleport, kinds_of)
 
 
 def region_bounds(edges, D, teleport=0.0):
@@ -106,6 +106,7 @@ class ModelShard:
         allr = [r for v in sends for r in v]
         send = np.concatenate(allr) if allr else np.empty(0, HALO_DTYPE)
         tel = np.concatenate(tele) if tele else np.empty(0, TELE_DTYPE)
+        self.kinds = kinds_of(send, counts)  # what gwaoi_strips_route_kinds reports
         return as_words(send, HALO_WORDS), counts, as_words(tel, TELE_WORDS)
 
     def _before(self, s):
@@ -113,12 +114,16 @@ class ModelShard:
             return self.prv[s], self.pseq[s]
         return self.cur[s], self.cseq[s]
 
-    def finish(self, local, recv, tele):
+    def finish(self, local, recv, tele, kinds=None):
         O = self.oracle
         self.tick_id += 1
         t = self.tick_id
         recv = np.concatenate([np.frombuffer(local.numpy().tobytes(), HALO_DTYPE),
                                np.frombuffer(recv.numpy().tobytes(), HALO_DTYPE)])
+        if kinds is not None:  # the senders' statistics, as the exchange delivered them, match the records
+            e, l, b = kinds_of(recv, [recv.size])
+            assert (int(kinds[0]), int(kinds[1])) == (int(e[0]), int(l[0])), (kinds, e, l)
+            assert (kinds[2] is None) == (e[0] == 0) and (kinds[2] is None or np.array_equal(kinds[2], b[0]))
         tele = np.frombuffer(tele.numpy().tobytes(), TELE_DTYPE)
         leaves, rest = [], []
         for r in recv:

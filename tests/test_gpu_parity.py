@@ -1144,3 +1144,90 @@ def test_cell_size_switch_keeps_parity_gpu(oracle_mod):
         assert cpd[0] == 4 and 2 in cpd[1:5] and cpd[-1] == 4, cpd
         assert A.debug_counters()["cell_size_switches"] == 2, cpd
         assert B.debug_counters()["cell_size_switches"] == 0
+
+
+def test_device_enter_leave_batches_match_host_calls_gpu(oracle_mod):
+    """gwaoi_enter_batch_device / gwaoi_leave_batch_device (the strip worlds' boundary
+    crossers, Space.go:211,243) give the events of the same Enter/Leave calls made on the
+    host, with implicit and explicit seqs, mixed with a device Moved batch in one flush;
+    the host mirror is rebuilt from the frame for the next host call (neighbors, Leave)."""
+    torch = pytest.importorskip("torch")
+    n = 30000
+    wl = make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wl.initial()
+    half = n // 2
+    dev = "cuda:0"
+    with World(n) as A, World(n) as B:
+        for w in (A, B):
+            s = w.space_create(wl.D)
+            w.enter_batch(s, slots[:half], x0[:half], z0[:half])
+            w.tick()
+        # flush 1: device Enters of the second half (implicit seqs) + device moves of the first
+        sl, nx, nz = wl.tick(0)
+        keep = sl < half
+        msl, mx, mz = sl[keep], nx[keep], nz[keep]
+        d = [torch.from_numpy(a).to(dev) for a in (slots[half:].astype(np.int32), x0[half:], z0[half:],
+                                                   msl.astype(np.int32), mx, mz)]
+        torch.cuda.synchronize()
+        box = (float(x0[half:].min()), float(z0[half:].min()), float(x0[half:].max()), float(z0[half:].max()))
+        A.enter_batch_device(0, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), n - half, box=box)
+        with pytest.raises(GwaoiError):  # the host mirror is stale until the flush
+            A.moved(0, 1.0, 1.0)
+        A.moved_batch_device(d[3].data_ptr(), d[4].data_ptr(), d[5].data_ptr(), msl.size)
+        B.enter_batch(0, slots[half:], x0[half:], z0[half:])
+        B.moved_batch(msl, mx, mz)
+        ea, la = flush(A)
+        eb, lb = flush(B)
+        np.testing.assert_array_equal(ea, eb)
+        np.testing.assert_array_equal(la, lb)
+        assert A.info()["live"] == n
+        # flush 2: device Leaves of 5000 slots + explicit-seq device moves of the rest
+        gone = np.arange(0, n, 6, dtype=np.uint32)[:5000]
+        rest = np.setdiff1d(slots, gone)
+        rx = (wl.x[rest] + np.float32(0.5)).astype(np.float32)
+        rz = (wl.z[rest] - np.float32(0.5)).astype(np.float32)
+        base = A.info()["next_seq"]
+        sq = base + np.arange(rest.size, dtype=np.uint64)
+        d2 = [torch.from_numpy(a).to(dev) for a in (gone.astype(np.int32), rest.astype(np.int32), rx, rz,
+                                                    sq.view(np.int64))]
+        torch.cuda.synchronize()
+        A.leave_batch_device(0, d2[0].data_ptr(), gone.size)
+        A.moved_batch_device(d2[1].data_ptr(), d2[2].data_ptr(), d2[3].data_ptr(), rest.size, d_seq=d2[4].data_ptr())
+        B.leave_batch(gone)
+        B.moved_batch(rest, rx, rz)
+        ea, la = flush(A)
+        eb, lb = flush(B)
+        np.testing.assert_array_equal(ea, eb)
+        np.testing.assert_array_equal(la, lb)
+        assert A.info()["live"] == n - gone.size
+        # host calls again: the mirror is rebuilt from the frame
+        for i in (1, 2, 7, 12345, int(rest[-1])):
+            np.testing.assert_array_equal(A.neighbors(i), B.neighbors(i))
+        with pytest.raises(GwaoiError):
+            A.neighbors(int(gone[3]))  # left: not in the frame
+        for w in (A, B):
+            w.leave(int(rest[0]))
+            w.enter(0, int(gone[0]), 10.0, 20.0)
+        ea, la = flush(A)
+        eb, lb = flush(B)
+        np.testing.assert_array_equal(ea, eb)
+        np.testing.assert_array_equal(la, lb)
+
+
+def test_device_enter_of_live_slot_poisons_gpu():
+    """A device Enter batch naming a live slot breaks the frame's live count: the flush
+    fails and the world refuses further calls (the rules of gwaoi_enter_batch_device)."""
+    torch = pytest.importorskip("torch")
+    with World(64) as w:
+        w.space_create(D)
+        for i in range(4):
+            w.enter(0, i, float(i), 0.0)
+        w.tick()
+        d = [torch.tensor(a, device="cuda:0") for a in ([2, 9], [5.0, 6.0], [0.0, 0.0])]
+        torch.cuda.synchronize()
+        w.enter_batch_device(0, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 2)
+        with pytest.raises(GwaoiError) as ei:
+            w.tick()
+        assert "live" in str(ei.value)
+        with pytest.raises(GwaoiError):
+            w.moved(1, 0.0, 0.0)

@@ -123,3 +123,54 @@ def test_explicit_seq_world_matches_implicit():
         we.moved_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 4, d_seq=sq.data_ptr())
         with pytest.raises(GwaoiError):
             we.tick()
+
+
+def test_strips_sync_compat_path(oracle_mod):
+    """gwaoi_strips_tick (kinds read back on the device, then the queued tick, then a wait)
+    gives the same events as the asynchronous path."""
+    import torch
+    from goworld_amd.strips import local_tick as lt
+    sc = Scenario(n0=4000, n_strips=3, seed=23)
+    shards = [StripShard(sc.max_slots, D, sc.edges, r, device=0) for r in range(3)]
+    ref_w = World(sc.max_slots, 1, device=0)
+    ref_w.space_create(D)
+    for t in range(4):
+        kind, sl, nx, nz, seq, px = sc.tick()
+        per = split_by_owner(kind, sl, nx, nz, seq, px, sc.edges)
+        res = lt(shards, [as_words(o, HALO_WORDS).to("cuda:0") for o in per], sync=True)
+        evs = [sh.events() for sh in shards]
+        assert [(e.shape[0], l.shape[0]) for e, l in evs] == [tuple(r) for r in res]
+        re_, rl = world_reference(ref_w, kind, sl, nx, nz, seq)
+        assert np.array_equal(np.sort(np.concatenate([pair_keys(e) for e, _ in evs])), re_), f"tick {t}"
+        assert np.array_equal(np.sort(np.concatenate([pair_keys(l) for _, l in evs])), rl), f"tick {t}"
+    for sh in shards:
+        sh.close()
+    ref_w.close()
+
+
+def test_strip_tick_has_one_host_wait(oracle_mod):
+    """The asynchronous strip tick: route waits once for its counts, and that wait also
+    completes the previous tick (receive, world Enter/Leave/Moved device batches, flush,
+    filter).  Steady ticks add exactly one host wait per strip per tick, and the events
+    still match one unsplit world."""
+    import torch
+    sc = Scenario(n0=6000, n_strips=2, seed=29)
+    shards = [StripShard(sc.max_slots, D, sc.edges, r, device=0) for r in range(2)]
+    ref_w = World(sc.max_slots, 1, device=0)
+    ref_w.space_create(D)
+    waits = []
+    for t in range(6):
+        kind, sl, nx, nz, seq, px = sc.tick()
+        per = split_by_owner(kind, sl, nx, nz, seq, px, sc.edges)
+        local_tick(shards, [as_words(o, HALO_WORDS).to("cuda:0") for o in per])
+        waits.append([sh.host_waits() for sh in shards])
+        re_, rl = world_reference(ref_w, kind, sl, nx, nz, seq)
+        if t == 5:  # the last tick: completed by events() (one more wait, plus the copy's)
+            evs = [sh.events() for sh in shards]
+            assert np.array_equal(np.sort(np.concatenate([pair_keys(e) for e, _ in evs])), re_)
+            assert np.array_equal(np.sort(np.concatenate([pair_keys(l) for _, l in evs])), rl)
+    d = np.diff(np.array(waits), axis=0)
+    assert np.all(d[2:] == 1), waits  # after the buffers have grown: one wait per tick
+    for sh in shards:
+        sh.close()
+    ref_w.close()

@@ -38,8 +38,8 @@ def run_strips_local(oracle, sc: Scenario, ticks: int):
     for _ in range(ticks):
         per = split_by_owner(*sc.tick(), sc.edges)
         routed = [sh.route(as_words(o, HALO_WORDS)) for sh, o in zip(shards, per)]
-        for q, (sh, (recv, tele)) in enumerate(zip(shards, exchange_local(routed))):
-            sh.finish(local_slice(routed[q][0], routed[q][1], q), recv, tele)
+        for q, (sh, (recv, tele, k)) in enumerate(zip(shards, exchange_local(routed, [s.kinds for s in shards]))):
+            sh.finish(local_slice(routed[q][0], routed[q][1], q), recv, tele, kinds=k)
         out.append(tuple(np.concatenate([sh.last[i] for sh in shards]) for i in (0, 1)))
     return out
 
@@ -91,8 +91,8 @@ def _worker(rank, ws, port, seed, ticks, q):
     for _ in range(ticks):
         ops = split_by_owner(*sc.tick(), sc.edges)[rank]
         send, counts, tele = sh.route(as_words(ops, HALO_WORDS))
-        recv, tele_all = exchange(dist, send, counts, tele)
-        sh.finish(local_slice(send, counts, rank), recv, tele_all)
+        recv, tele_all, kinds = exchange(dist, send, counts, tele, kinds=sh.kinds)
+        sh.finish(local_slice(send, counts, rank), recv, tele_all, kinds=kinds)
         res.append((sh.last[0].tolist(), sh.last[1].tolist()))
     q.put((rank, res))
     dist.barrier()
@@ -101,7 +101,8 @@ def _worker(rank, ws, port, seed, ticks, q):
 
 @pytest.mark.parametrize("ws", [2, 3])
 def test_gloo_strip_exchange(oracle_mod, ws):
-    """ws ranks over gloo: counts all-gathered on the host, records point to
+    """ws ranks over gloo: counts (with the ENTER / LEAVE statistics the receivers
+    queue their world batches with) all-gathered on the host, records point to
     point (3 ranks: the middle strip talks to both neighbours, the outer ones
     reach each other only through teleports)."""
     seed, ticks = 5, 4
