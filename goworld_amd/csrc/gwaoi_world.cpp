@@ -293,6 +293,13 @@ struct gwaoi_world {
     // GWAOI_SIDE_CLAIMS=1 (A/B, off): measured slower, 0.303-0.305 vs 0.292-0.294 ms per tick -- the
     // side kernel's random claim stores ran 30 us beside k_keygen and stretched it from 20 to 37 us
     bool side_claims = false;
+    // zero-copy batch (gwaoi_moved_batch_stage / _commit): the caller fills [slots | x | z | space]
+    size_t resv_n = 0;        // moves reserved (0: no reservation)
+    uint32_t *resv_h = nullptr, *resv_d = nullptr;
+    int resv_half = 0;
+    // event copies to the host beside the next flush (gwaoi_tick_end_begin)
+    hipStream_t out_st = nullptr;
+    hipEvent_t out_ev = nullptr;
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
@@ -1298,6 +1305,9 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     }
     if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
     if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
+    if (w->out_st) (void)hipStreamSynchronize(w->out_st);
+    if (w->out_ev) (void)hipEventDestroy(w->out_ev);
+    if (w->out_st) (void)hipStreamDestroy(w->out_st);
     if (w->claim_st) (void)hipStreamSynchronize(w->claim_st);
     if (w->applied_ev) (void)hipEventDestroy(w->applied_ev);
     if (w->claimed_ev) (void)hipEventDestroy(w->claimed_ev);
@@ -1361,6 +1371,14 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (const char *e = std::getenv("GWAOI_SIDE_CLAIMS")) w->side_claims = e[0] == '1';
     if (hipEventCreateWithFlags(&w->copy_ev, hipEventDisableTiming) != hipSuccess) {
         w->copy_ev = nullptr;
+        return fail(GWAOI_EDEVICE);
+    }
+    if (hipStreamCreateWithFlags(&w->out_st, hipStreamNonBlocking) != hipSuccess) {
+        w->out_st = nullptr;
+        return fail(GWAOI_EDEVICE);
+    }
+    if (hipEventCreateWithFlags(&w->out_ev, hipEventDisableTiming) != hipSuccess) {
+        w->out_ev = nullptr;
         return fail(GWAOI_EDEVICE);
     }
     const size_t N = w->max_slots;
@@ -1570,7 +1588,7 @@ int ensure_stage(gwaoi_world *w, size_t words) {
     const int h = w->stage_cur;
     if (w->stage_used[h] + words <= w->stage_cap[h]) return GWAOI_OK;
     if (w->stage_used[h]) return 1;
-    const size_t cap = std::max<size_t>({words, 2 * w->stage_cap[h], (size_t)4 << 16});
+    const size_t cap = std::max<size_t>({2 * words, 2 * w->stage_cap[h], (size_t)4 << 16});
     HIP_TRY(hipStreamSynchronize(w->copy_st));  // no staging copy may still read the old buffer
     if (w->h_stage[h]) (void)hipHostFree(w->h_stage[h]);
     w->h_stage[h] = nullptr;
@@ -1940,6 +1958,87 @@ int gwaoi_leave_batch_device(gwaoi_world *w, uint32_t space, const uint32_t *d_s
     });
 }
 
+int gwaoi_moved_batch_stage(gwaoi_world *w, size_t n, uint32_t **slots, float **x, float **z) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !slots || !x || !z || n == 0 || n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (w->resv_n || w->dev_seq_pending) return GWAOI_ESTATE;
+    if (int rc = ensure_stage(w, 4 * n)) {
+        if (rc == 1) {
+            w->last_error = "staging memory holds this flush's batches: flush before staging more";
+            return GWAOI_ECAPACITY;
+        }
+        return rc;
+    }
+    const int h = w->stage_cur;
+    w->resv_half = h;
+    w->resv_n = n;
+    w->resv_h = w->h_stage[h] + w->stage_used[h];
+    w->resv_d = w->d_stage[h] + w->stage_used[h];
+    *slots = w->resv_h;
+    *x = reinterpret_cast<float *>(w->resv_h + n);
+    *z = reinterpret_cast<float *>(w->resv_h + 2 * n);
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_moved_batch_commit(gwaoi_world *w, size_t k) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    const size_t n = w->resv_n;
+    if (!n || k > n) return n ? GWAOI_EINVAL : GWAOI_ESTATE;
+    w->resv_n = 0;
+    if (w->resv_half != w->stage_cur) return GWAOI_ESTATE;  // a flush launched in between took that half
+    if (!k) return GWAOI_OK;
+    uint32_t *h = w->resv_h, *d = w->resv_d;
+    // After an Enter / Leave queued in this flush a slot's space may differ from its space at the
+    // flush's start: the space column is filled (and the batch checked) on the host then.
+    const bool with_space = w->space_ops_queued;
+    if (with_space) {
+        if (int rc = host_slots(w)) return rc;
+        std::vector<StageBox> boxes(std::max(1u, w->n_space_ids), StageBox{0, 0, 0, 0, false});
+        int st = GWAOI_OK;
+        const float *hx = reinterpret_cast<const float *>(h + n), *hz = reinterpret_cast<const float *>(h + 2 * n);
+        if (stage_chunk(w, h, hx, hz, n, 0, k, h, true, boxes.data(), &st) != k) return st;
+        for (size_t sp = 0; sp < boxes.size(); ++sp) {
+            const StageBox &b = boxes[sp];
+            if (!b.any) continue;
+            if (w->in_flight) {
+                w->deferred_boxes.push_back(DeferredBox{(uint32_t)sp, b.x0, b.z0, b.x1, b.z1});
+            } else {
+                note_pending_bbox(w->spaces[sp], b.x0, b.z0);
+                note_pending_bbox(w->spaces[sp], b.x1, b.z1);
+            }
+        }
+    }
+    const size_t words = (with_space ? 4 : 3) * n;
+    HIP_TRY(hipMemcpyAsync(d, h, words * sizeof(uint32_t), hipMemcpyHostToDevice, w->copy_st));
+    HIP_TRY(hipEventRecord(w->copy_ev, w->copy_st));
+    w->copy_pending = true;
+    w->stage_used[w->resv_half] += 4 * n;
+    Run r{};
+    r.device = true;
+    r.ds = d;
+    r.dx = reinterpret_cast<const float *>(d + n);
+    r.dz = reinterpret_cast<const float *>(d + 2 * n);
+    r.dsp = with_space ? d + 3 * n : nullptr;
+    r.seq0 = w->seq_next;
+    r.dn = k;
+    w->seq_next += k;
+    if (w->in_flight) {
+        Deferred q{};
+        q.kind = Deferred::RUN;
+        q.run = r;
+        w->deferred.push_back(q);
+    } else {
+        w->runs.push_back(r);
+        w->n_ops += k;
+    }
+    return GWAOI_OK;
+    });
+}
+
 }  // extern "C"
 
 namespace gw {
@@ -2025,13 +2124,13 @@ int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) 
     });
 }
 
-int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
-    if (n_enter) *n_enter = 0;
-    if (n_leave) *n_leave = 0;
-    GW_LIVE(w);
-    if (!w->in_flight) return GWAOI_ESTATE;
+}  // extern "C"
+
+namespace {
+
+// gwaoi_tick_end_begin(_device): finish the flush in flight, begin the next one (speculatively,
+// before the finished one's summary is read, when the queue allows it).
+int end_begin(gwaoi_world *w, bool *committed_out) {
     bool committed = false;
     int rc, lrc = GWAOI_OK;
     if (speculative_ok(w)) {
@@ -2048,11 +2147,59 @@ int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_l
         rc = tick_finish(w, &committed);
         if (committed && !w->poisoned) lrc = tick_launch(w);
     }
+    *committed_out = committed;
+    return rc != GWAOI_OK ? rc : lrc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
+    bool committed = false;
+    const int rc = end_begin(w, &committed);
     if (committed) {
         if (n_enter) *n_enter = w->last_n_enter;
         if (n_leave) *n_leave = w->last_n_leave;
     }
-    return rc != GWAOI_OK ? rc : lrc;
+    return rc;
+    });
+}
+
+int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out) return GWAOI_EINVAL;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
+    const uint64_t regrows = w->dbg.event_regrows;
+    bool committed = false;
+    const int rc = end_begin(w, &committed);
+    if (!committed) return rc;
+    // the finished flush's events to pinned host memory on the copy-out stream, beside the next flush
+    const uint64_t tot = w->last_n_enter + w->last_n_leave;
+    if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
+    FlushSet &S = w->fs[w->last_set];
+    if (tot) {
+        // ordered after the flush's last kernel (its event's release makes the writes visible to the
+        // copy engine); after a re-run of its pair passes, after the wait that followed the re-run
+        HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
+        HIP_TRY(hipMemcpyAsync(w->h_events, S.events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost, w->out_st));
+        HIP_TRY(hipEventRecord(w->out_ev, w->out_st));
+        if (int rw = wait_done(w, w->out_ev)) return poison(w, rw);
+    }
+    out->n_enter = w->last_n_enter;
+    out->n_leave = w->last_n_leave;
+    out->enter = w->h_events;
+    out->leave = w->h_events + 2 * w->last_n_enter;
+    return rc;
     });
 }
 

@@ -222,6 +222,29 @@ int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
  * gwaoi_events_device until the next commit.  The next flush is in flight on
  * return whenever the finished one committed. */
 int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
+/* The same with the finished flush's events copied to host memory (as
+ * gwaoi_tick_end; valid until the next call that returns events).  The copy
+ * runs on its own stream, beside the next flush. */
+int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out);
+
+/* ---- zero-copy host move batches ---------------------------------------------
+ * The per-tick position batch written straight into the world's pinned staging
+ * memory, as a cgo adapter appends each client's (slot, x, z) while it decodes
+ * the sync packets (GameService.go:392-404, HandleSyncPositionYawFromClient):
+ * _stage reserves room for up to n moves and returns the three arrays; the
+ * caller fills a prefix of them and _commit(k) queues those k moves as one
+ * Moved batch (array order = call order) and starts their one H2D copy on a
+ * copy stream.  Nothing is read on the host: a move of a slot that is not
+ * live, an out-of-range slot or a non-finite coordinate is dropped on the
+ * device and reported by the flush (as gwaoi_moved_batch_device).  When an
+ * Enter / Leave is queued in the same flush before it, the batch is checked
+ * on the host instead (a slot's space may have changed; errors as
+ * gwaoi_moved_batch: nothing is queued).  One reservation at a time;
+ * available while a flush is in flight (the batch joins the next flush).
+ * GWAOI_ECAPACITY: the staging memory holds this flush's batches already
+ * (commit, flush, then stage again). */
+int gwaoi_moved_batch_stage(gwaoi_world *w, size_t n, uint32_t **slots, float **x, float **z);
+int gwaoi_moved_batch_commit(gwaoi_world *w, size_t n);
 /* Device pointers of the last committed tick's events (same layout as
  * gwaoi_events); valid until the next commit, also while a later flush is in
  * flight (it writes the other event buffer). */
