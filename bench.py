@@ -399,6 +399,139 @@ def host_tick_bench(ticks: int, threads: int):
         return {"error": (r.stderr or r.stdout)[-500:]}
 
 
+class _Filler:
+    """The caller side of the zero-copy batch: the tick's (slot, x, z) arrays written into the
+    world's pinned staging views by 8 threads (numpy copies release the GIL), as a cgo adapter
+    would append the moves it decodes."""
+
+    def __init__(self, threads: int = 8):
+        from concurrent.futures import ThreadPoolExecutor
+        self.T = threads
+        self.pool = ThreadPoolExecutor(threads)
+
+    def fill(self, views, batch):
+        n = batch[0].size
+        cuts = np.linspace(0, n, self.T + 1).astype(np.int64)
+
+        def part(k):
+            a, b = cuts[k], cuts[k + 1]
+            for v, src in zip(views, batch):
+                v[a:b] = src[a:b]
+        list(self.pool.map(part, range(self.T)))
+
+    def close(self):
+        self.pool.shutdown()
+
+
+def host_io_leg(w, host_batches, hio, dist, red_dev):
+    """The host -> host tick (p50/p99 "end-to-end from H2D to event CSR in host
+    memory"), with host move arrays and the events delivered to pinned host memory.
+
+    zero-copy (the headline twin): the caller writes each tick's moves straight into the world's pinned
+      staging (gwaoi_moved_batch_stage; 8 filler threads), gwaoi_moved_batch_commit starts the one H2D on a
+      copy stream, and the moves are checked on the device.  Serial: commit + gwaoi_tick.  Pipelined:
+      the batch of t+1 is filled and committed while flush t runs, then gwaoi_tick_end_begin queues flush
+      t+1 before t's summary is read and copies t's events out beside it.  Latency = commit of the batch ->
+      its events in host memory (the fill is the caller's, before the H2D: reported apart).
+    staged (gwaoi_moved_batch: validation + copy into pinned staging on 8 library threads): the same ticks
+      through the copying API, for comparison."""
+    import gc
+    import torch
+    from goworld_amd.shard import reduce_over_ranks
+    F = _Filler()
+    nb = len(host_batches)
+    zc, st = host_batches[:nb // 2], host_batches[nb // 2:]
+
+    def zfill(b):
+        t = time.perf_counter()
+        F.fill(w.stage_moves(b[0].size), b)
+        return time.perf_counter() - t
+
+    # warmup (sizes the pinned staging halves and host event buffers; the pipeline's fill)
+    zfill(zc[0]); w.commit_moves(zc[0][0].size); w.tick(copy=False)
+    zfill(zc[1]); w.commit_moves(zc[1][0].size); w.tick_begin()
+    zfill(zc[2]); w.commit_moves(zc[2][0].size); w.tick_end_begin(copy=False)
+    w.tick_end(copy=False)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    gc.disable()  # no collector pauses inside the timed ticks
+    # serial
+    s_lat, s_fill, h_ev = [], [], 0
+    ser = zc[3:hio + 3]
+    s0 = time.perf_counter()
+    for b in ser:
+        s_fill.append(zfill(b))
+        a = time.perf_counter()
+        w.commit_moves(b[0].size)
+        ent, lev = w.tick(copy=False)
+        s_lat.append(time.perf_counter() - a)
+        h_ev += len(ent) + len(lev)
+    s_el = time.perf_counter() - s0
+    # pipelined
+    pb = zc[hio + 3:]
+    p_lat, p_fill = [], []
+    p_fill.append(zfill(pb[0]))
+    p0 = time.perf_counter()
+    w.commit_moves(pb[0][0].size)
+    commit_t = [p0]
+    w.tick_begin()
+    for k in range(len(pb)):
+        if k + 1 < len(pb):
+            p_fill.append(zfill(pb[k + 1]))  # the caller writes t+1 while flush t runs
+            commit_t.append(time.perf_counter())
+            w.commit_moves(pb[k + 1][0].size)
+            w.tick_end_begin(copy=False)
+        else:
+            w.tick_end(copy=False)
+        p_lat.append(time.perf_counter() - commit_t[k])
+    p_el = time.perf_counter() - p0
+    gc.enable()
+    torch.cuda.synchronize()
+    # staged (copying API): the same measurement through gwaoi_moved_batch
+    k = max(2, hio // 2)
+    w.moved_batch(*st[0]); w.tick(copy=False)
+    c_lat = []
+    for b in st[1:k + 1]:
+        a = time.perf_counter()
+        w.moved_batch(*b)
+        w.tick(copy=False)
+        c_lat.append(time.perf_counter() - a)
+    cp = st[k + 1:2 * k + 1]
+    cq_lat = []
+    w.moved_batch(*cp[0])
+    c0 = issue = time.perf_counter()
+    for j in range(len(cp)):
+        w.tick_begin()
+        nxt = time.perf_counter()
+        if j + 1 < len(cp):
+            w.moved_batch(*cp[j + 1])
+        w.tick_end(copy=False)
+        cq_lat.append(time.perf_counter() - issue)
+        issue = nxt
+    c_el = time.perf_counter() - c0
+    F.close()
+    if dist is not None:
+        dist.barrier()
+    p_el, (h_moves, h_evs) = reduce_over_ranks(dist, p_el, [sum(b[0].size for b in pb), h_ev], red_dev)
+    pct = lambda v, q: float(np.percentile(np.array(v) * 1e3, q))
+    return {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
+            "p50_tick_ms": pct(p_lat, 50), "p99_tick_ms": pct(p_lat, 99), "steps": len(pb),
+            "ticks_ms": [round(v * 1e3, 3) for v in p_lat],
+            "caller_fill_ms_p50": pct(p_fill, 50),
+            "serial": {"ms_per_step": s_el / len(ser) * 1e3, "p50_tick_ms": pct(s_lat, 50),
+                       "p99_tick_ms": pct(s_lat, 99), "steps": len(ser), "caller_fill_ms_p50": pct(s_fill, 50),
+                       "events_per_s": h_evs / max(s_el, 1e-9)},
+            "staged_copy_api": {"serial_p50_tick_ms": pct(c_lat, 50), "serial_p99_tick_ms": pct(c_lat, 99),
+                                "pipelined_ms_per_step": c_el / len(cp) * 1e3,
+                                "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(c_lat)},
+            "note": "zero-copy: moves written by the caller (8 threads) into pinned staging, one H2D per tick, "
+                    "checked on the device; pipelined = batch t+1 filled and committed while flush t runs, "
+                    "gwaoi_tick_end_begin (flush t+1 queued before t's summary, t's events copied out beside it); "
+                    "tick latency = commit -> events in pinned host memory (ms_per_step includes the caller's "
+                    "fill); staged_copy_api = the same ticks through gwaoi_moved_batch (library validation + copy)"}
+
+
 def cfg4_leg(args, ws, rank, device, dist, red_dev):
     """Config 4 as a strong-scaling sub-record of every line: 8192 independent
     spaces x 2000 entities in total, sharded over the ranks in contiguous
@@ -860,7 +993,7 @@ def main():
         batches.append((sl, nx, nz))
     # PCIe-inclusive leg (host memory): three untimed warmup ticks (one serial, two pipelined: they
     # allocate both pinned staging buffers) + hio serial + hio + 1 pipelined
-    host_batches = [wl.tick(ticks + t) for t in range(2 * hio + 4 if hio else 0)]
+    host_batches = [wl.tick(ticks + t) for t in range(2 * (2 * hio + 4) if hio else 0)]
     sync_steps = max(0, args.sync_steps) if ws == 1 or args.workload != "cfg4" else 0
     sync_batches = [wl.tick(ticks + len(host_batches) + t) for t in range(sync_steps + 1 if sync_steps else 0)]
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
@@ -974,67 +1107,9 @@ def main():
         stages = w.stage_times()
         w.set_stage_timing([])
 
-    # ---- PCIe-inclusive leg (SURVEY.md §8d's tick): host move arrays -> validation + pinned staging + H2D
-    # -> flush -> events in pinned host memory (views, no copy).  Serial: per-tick latency.  Pipelined:
-    # gwaoi_tick_begin(t), the host batch of t+1 staged while the GPU runs t, gwaoi_tick_end(t).
-    host_io = None
-    if hio:
-        w.moved_batch(*host_batches[0])  # warmup: sizes the pinned staging and host event buffers
-        w.tick(copy=False)
-        w.moved_batch(*host_batches[1])  # pipelined warmup: the second staging buffer
-        w.tick_begin()
-        w.moved_batch(*host_batches[2])
-        w.tick_end(copy=False)
-        w.tick_begin()
-        w.tick_end(copy=False)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        h_ev, s_lat = 0, []
-        import gc
-        gc.disable()  # no collector pauses inside the timed ticks
-        h0 = time.perf_counter()
-        for sl, nx, nz in host_batches[3:hio + 3]:
-            a = time.perf_counter()
-            w.moved_batch(sl, nx, nz)
-            ent, lev = w.tick(copy=False)
-            s_lat.append(time.perf_counter() - a)
-            h_ev += len(ent) + len(lev)
-        s_el = time.perf_counter() - h0
-        pb = host_batches[hio + 3:]
-        p_lat = []
-        w.moved_batch(*pb[0])
-        p0 = issue = time.perf_counter()
-        for k in range(len(pb)):
-            w.tick_begin()
-            nxt = time.perf_counter()
-            if k + 1 < len(pb):
-                w.moved_batch(*pb[k + 1])  # staged while the flush of tick k runs
-            ent, lev = w.tick_end(copy=False)
-            p_lat.append(time.perf_counter() - issue)
-            issue = nxt
-        p_el = time.perf_counter() - p0
-        gc.enable()
-        # the first pipelined tick has no flush before it to hide its staging behind: it is the
-        # pipeline's fill, reported apart from the steady percentiles
-        p_first = p_lat[0]
-        p_lat = p_lat[1:] if len(p_lat) > 1 else p_lat
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        p_el, (h_moves, h_evs) = reduce_over_ranks(dist, p_el, [sum(b[0].size for b in pb), h_ev], red_dev)
-        sl_ms, pl_ms = np.array(s_lat) * 1e3, np.array(p_lat) * 1e3
-        host_io = {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
-                   "p50_tick_ms": float(np.percentile(pl_ms, 50)), "p99_tick_ms": float(np.percentile(pl_ms, 99)),
-                   "steps": len(pb), "first_tick_ms": p_first * 1e3,
-                   "ticks_ms": [round(v, 3) for v in pl_ms.tolist()],
-                   "serial": {"ms_per_step": s_el / hio * 1e3, "p50_tick_ms": float(np.percentile(sl_ms, 50)),
-                              "p99_tick_ms": float(np.percentile(sl_ms, 99)), "steps": hio,
-                              "events_per_s": h_evs / max(s_el, 1e-9)},
-                   "note": "pipelined: the moved_batch of tick t+1 (validation, pinned staging, H2D on a copy "
-                           "stream) overlaps the flush of tick t; p50/p99 = from the batch call to the events in "
-                           "pinned host memory, over the ticks after the first (the pipeline fill, first_tick_ms); "
-                           "serial = moved_batch + tick back to back. Not the headline value"}
+    # ---- PCIe-inclusive leg (SURVEY.md §8d's tick, BASELINE.md's p50/p99 "end-to-end from H2D to event CSR in
+    # host memory"): host move arrays -> pinned staging -> H2D -> flush -> events in pinned host memory
+    host_io = host_io_leg(w, host_batches, hio, dist, red_dev) if hio else None
     sync = sync_leg(w, n, sync_batches, args.sync_clients) if sync_batches else None
     wire = None
     if args.wire_steps > 0 and ws == 1 and args.workload == "cfg3":
@@ -1115,6 +1190,12 @@ def main():
                           f"({spec_launches} of {args.steps} timed flushes)" if spec else
                           "overlap: batch t+1 registered while flush t runs" if overlap else "serial"),
             "roofline": roofline,
+            "host_to_host_tick": ({k: host_io[k] for k in ("value", "unit", "ms_per_step", "p50_tick_ms", "p99_tick_ms")}
+                                  | {"serial_p50_tick_ms": host_io["serial"]["p50_tick_ms"],
+                                     "serial_p99_tick_ms": host_io["serial"]["p99_tick_ms"],
+                                     "note": "headline twin: BASELINE.md's tick, host move arrays in (zero-copy "
+                                             "staging, one H2D) -> events in pinned host memory; details in "
+                                             "pcie_inclusive"} if host_io else None),
             "pcie_inclusive": host_io,
             "sync_leg": sync,
             "wire_leg": wire,

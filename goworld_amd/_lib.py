@@ -36,7 +36,8 @@ EXPORTS = [
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
     "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
     "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
-    "gwaoi_enter_batch_device", "gwaoi_leave_batch_device",
+    "gwaoi_enter_batch_device", "gwaoi_leave_batch_device", "gwaoi_tick_end_begin", "gwaoi_moved_batch_stage",
+    "gwaoi_moved_batch_commit",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -154,6 +155,9 @@ def load():
         "gwaoi_tick_end": ([vp, P(Events)], C.c_int),
         "gwaoi_tick_end_device": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_tick_end_begin_device": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_tick_end_begin": ([vp, P(Events)], C.c_int),
+        "gwaoi_moved_batch_stage": ([vp, sz, P(vp), P(vp), P(vp)], C.c_int),
+        "gwaoi_moved_batch_commit": ([vp, sz], C.c_int),
         "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_neighbors": ([vp, u32, vp, sz, P(sz)], C.c_int),
         "gwaoi_world_info": ([vp, P(Info)], C.c_int),
@@ -305,6 +309,19 @@ class World:
         z = np.ascontiguousarray(z, np.float32)
         self._check(self._L.gwaoi_moved_batch(self._w, _p(s), _p(x), _p(z), s.size))
 
+    def stage_moves(self, n: int):
+        """gwaoi_moved_batch_stage: (slots, x, z) numpy views of n moves in the world's pinned
+        staging memory, to be filled by the caller and queued with commit_moves(k)."""
+        ps, px, pz = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(self._L.gwaoi_moved_batch_stage(self._w, n, C.byref(ps), C.byref(px), C.byref(pz)))
+        u32, f32 = C.POINTER(C.c_uint32), C.POINTER(C.c_float)
+        return (np.ctypeslib.as_array(C.cast(ps, u32), shape=(n,)), np.ctypeslib.as_array(C.cast(px, f32), shape=(n,)),
+                np.ctypeslib.as_array(C.cast(pz, f32), shape=(n,)))
+
+    def commit_moves(self, k: int):
+        """gwaoi_moved_batch_commit: queue the first k staged moves (one H2D, checked on the device)."""
+        self._check(self._L.gwaoi_moved_batch_commit(self._w, k))
+
     def moved_batch_device(self, d_slots: int, d_x: int, d_z: int, n: int, d_seq: int | None = None):
         if d_seq is None:
             self._check(self._L.gwaoi_moved_batch_device(self._w, C.c_void_p(d_slots), C.c_void_p(d_x),
@@ -365,6 +382,12 @@ class World:
                 e.counts = (ne.value, nl.value)
                 raise
         return ne.value, nl.value
+
+    def tick_end_begin(self, copy: bool = True):
+        """gwaoi_tick_end_begin: finish the flush in flight (its events copied to host memory
+        beside the next flush) and begin the next one."""
+        ev = Events()
+        return self._events(self._L.gwaoi_tick_end_begin(self._w, C.byref(ev)), ev, copy)
 
     def _events(self, rc, ev, copy):
         ne, nl = ev.n_enter, ev.n_leave

@@ -532,6 +532,11 @@ struct gwaoi_strips {
     // multisplit scratch
     uint32_t *counts = nullptr, *scan_tmp = nullptr, *err = nullptr, *small_d = nullptr;
     size_t counts_cap = 0, scan_cap = 0;
+    // the filter's own multisplit scratch and the tick's error word: a filter re-run (after the
+    // world regrew its events) happens inside the next route, whose counts and error word it
+    // must leave alone
+    uint32_t *fcounts = nullptr, *fscan_tmp = nullptr, *terr = nullptr;
+    size_t fcounts_cap = 0, fscan_cap = 0;
     uint32_t *small_h = nullptr;  // pinned, SM_WORDS
     int *kstat = nullptr;         // device kind statistics: route (GWAOI_MAX_STRIPS x KS), receive (KS)
     // route state
@@ -604,6 +609,13 @@ int ensure_split(gwaoi_strips *s, uint32_t K, uint32_t nb) {
     return GWAOI_OK;
 }
 
+int ensure_fsplit(gwaoi_strips *s, uint32_t G) {
+    const size_t n = (size_t)2 * G + 1;
+    if (int rc = grow(s, &s->fcounts, s->fcounts_cap, n)) return rc;
+    if (int rc = grow(s, &s->fscan_tmp, s->fscan_cap, gw::scan_tmp_elems(n) + 16)) return rc;
+    return GWAOI_OK;
+}
+
 int ensure_moves(gwaoi_strips *s, size_t n) {
     if (n <= s->m_cap && s->m_slot) return GWAOI_OK;
     size_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
@@ -638,16 +650,16 @@ int launch_filter(gwaoi_strips *s, uint64_t tcap) {
     gw::world_flush_events(s->w, &wev, &dcnt, &cap);
     if (int rc = grow(s, &s->out, s->out_cap, cap + 2 * tcap + 1)) return rc;
     const uint32_t G = std::max(1u, std::min<uint32_t>(FILTER_BLOCKS, cdivu(std::max<uint64_t>(cap, 1), BT)));
-    if (int rc = ensure_split(s, 2, G)) return rc;
+    if (int rc = ensure_fsplit(s, G)) return rc;
     hipStream_t st = s->st;
     const uint2 *ev = reinterpret_cast<const uint2 *>(wev);
-    k_filter<<<G, BT, 0, st>>>(0, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->counts,
+    k_filter<<<G, BT, 0, st>>>(0, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->fcounts,
                                nullptr, nullptr, nullptr);
-    gw::scan_exclusive(s->counts, s->counts, (size_t)2 * G + 1, s->scan_tmp, st);
-    k_filter<<<G, BT, 0, st>>>(1, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->counts,
-                               s->counts, s->tcnt, s->out);
-    k_tele_place<<<64, 256, 0, st>>>(s->counts, G, s->tcnt, s->tpairs, s->tpairs + tcap, s->out);
-    k_tick_totals<<<1, 64, 0, st>>>(s->counts, G, s->tcnt, s->err, s->small_d + SM_TICK);
+    gw::scan_exclusive(s->fcounts, s->fcounts, (size_t)2 * G + 1, s->fscan_tmp, st);
+    k_filter<<<G, BT, 0, st>>>(1, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->fcounts,
+                               s->fcounts, s->tcnt, s->out);
+    k_tele_place<<<64, 256, 0, st>>>(s->fcounts, G, s->tcnt, s->tpairs, s->tpairs + tcap, s->out);
+    k_tick_totals<<<1, 64, 0, st>>>(s->fcounts, G, s->tcnt, s->terr, s->small_d + SM_TICK);
     S_TRY(hipGetLastError());
     S_TRY(hipMemcpyAsync(s->small_h + SM_TICK, s->small_d + SM_TICK, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     return GWAOI_OK;
@@ -690,7 +702,8 @@ int gwaoi_strips_destroy(gwaoi_strips *s) {
     if (s->pending) (void)complete(s, false);
     if (s->st) (void)hipStreamSynchronize(s->st);
     void *dev[] = {s->cur, s->prv, s->ptick, s->ttick, s->counts, s->scan_tmp, s->err, s->small_d, s->kstat,
-                   s->m_slot, s->m_x, s->m_z, s->m_seq, s->tcnt, s->tpairs, s->out};
+                   s->m_slot, s->m_x, s->m_z, s->m_seq, s->tcnt, s->tpairs, s->out, s->fcounts, s->fscan_tmp,
+                   s->terr};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (s->small_h) (void)hipHostFree(s->small_h);
@@ -748,6 +761,7 @@ int gwaoi_strips_create(gwaoi_world *w, uint32_t space, const gwaoi_strips_confi
         hipMalloc((void **)&s->ptick, N * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&s->ttick, N * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&s->err, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&s->terr, sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&s->small_d, SM_WORDS * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&s->kstat, (GWAOI_MAX_STRIPS + 1) * KS * sizeof(int)) != hipSuccess ||
         hipMalloc((void **)&s->tcnt, 2 * sizeof(unsigned long long)) != hipSuccess ||
@@ -759,6 +773,7 @@ int gwaoi_strips_create(gwaoi_world *w, uint32_t space, const gwaoi_strips_confi
         hipMemsetAsync(s->ptick, 0, N * sizeof(uint32_t), s->st) != hipSuccess ||
         hipMemsetAsync(s->ttick, 0, N * sizeof(uint32_t), s->st) != hipSuccess ||
         hipMemsetAsync(s->err, 0, sizeof(uint32_t), s->st) != hipSuccess ||
+        hipMemsetAsync(s->terr, 0, sizeof(uint32_t), s->st) != hipSuccess ||
         hipStreamSynchronize(s->st) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     *out = s;
@@ -858,14 +873,14 @@ int gwaoi_strips_tick_async(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size
     const uint32_t nb = std::max(1u, cdivu(n_all, BT));
     if (int rc = ensure_split(s, 3, nb)) return rc;
     if (int rc = ensure_moves(s, std::max<size_t>(n_all, 1))) return rc;
-    S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
+    S_TRY(hipMemsetAsync(s->terr, 0, sizeof(uint32_t), st));
     k_recv<<<nb, BT, 0, st>>>(0, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick,
-                              s->max_slots, s->counts, nullptr, nb, s->err, nullptr, nullptr, nullptr, nullptr, nullptr);
+                              s->max_slots, s->counts, nullptr, nb, s->terr, nullptr, nullptr, nullptr, nullptr, nullptr);
     gw::scan_exclusive(s->counts, s->counts, (size_t)3 * nb + 1, s->scan_tmp, st);
     k_recv<<<nb, BT, 0, st>>>(1, d_local, (uint32_t)n_local, d_recv, (uint32_t)n_all, s->cur, s->prv, s->ptick, tick,
-                              s->max_slots, s->counts, s->counts, nb, s->err, s->m_slot, s->m_x, s->m_z, s->m_seq,
+                              s->max_slots, s->counts, s->counts, nb, s->terr, s->m_slot, s->m_x, s->m_z, s->m_seq,
                               nullptr);
-    k_recv_check<<<1, 64, 0, st>>>(s->counts, nb, n_move, n_ent, n_lev, s->err);
+    k_recv_check<<<1, 64, 0, st>>>(s->counts, nb, n_move, n_ent, n_lev, s->terr);
     if (n_tele) k_tele_mark<<<cdivu(n_tele, 256), 256, 0, st>>>(d_tele, (uint32_t)n_tele, s->ttick, tick, s->max_slots);
     S_TRY(hipGetLastError());
     // ---- the world's ops, all device batches: Leaves, Enters, Moves (one record per slot)

@@ -1231,3 +1231,73 @@ def test_device_enter_of_live_slot_poisons_gpu():
         assert "live" in str(ei.value)
         with pytest.raises(GwaoiError):
             w.moved(1, 0.0, 0.0)
+
+
+def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
+    """gwaoi_moved_batch_stage / _commit (moves written straight into pinned staging, checked
+    on the device) == gwaoi_moved_batch, serial and pipelined with gwaoi_tick_end_begin (the
+    event copy beside the next flush); a partial commit, a batch after an Enter in the same
+    flush (host-checked, space column), and a dead slot dropped and reported by the flush."""
+    wl = make_workload("cfg3", n=40000)
+    slots, x0, z0, _ = wl.initial()
+    with World(wl.n) as A, World(wl.n) as B:
+        for w in (A, B):
+            s = w.space_create(wl.D)
+            w.enter_batch(s, slots[:-10], x0[:-10], z0[:-10])
+            w.tick()
+        # serial: stage 1.5x, fill and commit the tick's moves
+        for t in range(3):
+            sl, nx, nz = wl.tick(t)
+            keep = sl < wl.n - 10
+            sl, nx, nz = sl[keep], nx[keep], nz[keep]
+            vs, vx, vz = A.stage_moves(sl.size + sl.size // 2)
+            vs[:sl.size], vx[:sl.size], vz[:sl.size] = sl, nx, nz
+            A.commit_moves(sl.size)
+            B.moved_batch(sl, nx, nz)
+            ea, la = A.tick()
+            eb, lb = B.tick()
+            np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
+        # an Enter queued first: the staged batch then carries the space column (host-checked)
+        new = slots[-10:]
+        for w in (A, B):
+            w.enter_batch(0, new, x0[-10:], z0[-10:])
+        sl, nx, nz = wl.tick(3)
+        vs, vx, vz = A.stage_moves(sl.size)
+        vs[:], vx[:], vz[:] = sl, nx, nz
+        A.commit_moves(sl.size)
+        B.moved_batch(sl, nx, nz)
+        ea, la = A.tick()
+        eb, lb = B.tick()
+        np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
+        np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
+        # pipelined: batch t+1 staged while flush t runs, tick_end_begin returns t's events
+        host = [wl.tick(4 + t) for t in range(5)]
+        vs, vx, vz = A.stage_moves(host[0][0].size)
+        vs[:], vx[:], vz[:] = host[0]
+        A.commit_moves(host[0][0].size)
+        A.tick_begin()
+        for t in range(5):
+            if t + 1 < 5:
+                sl, nx, nz = host[t + 1]
+                vs, vx, vz = A.stage_moves(sl.size)
+                vs[:], vx[:], vz[:] = sl, nx, nz
+                A.commit_moves(sl.size)
+                ea, la = A.tick_end_begin()
+            else:
+                ea, la = A.tick_end()
+            B.moved_batch(*host[t])
+            eb, lb = B.tick()
+            np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb), err_msg=f"pipelined tick {t}")
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"pipelined tick {t}")
+        assert A.debug_counters()["speculative_launches"] >= 3
+        # a move of a slot that is not live: dropped on the device, reported by the flush
+        A.leave(5)
+        A.tick()
+        vs, vx, vz = A.stage_moves(2)
+        vs[:], vx[:], vz[:] = [5, 6], [1.0, 2.0], [3.0, 4.0]
+        A.commit_moves(2)
+        with pytest.raises(GwaoiError) as ei:
+            A.tick()
+        assert ei.value.code == -3  # GWAOI_ESTATE, the flush committed
+        np.testing.assert_array_equal(A.snapshot()["x"][A.snapshot()["slot"] == 6], [np.float32(2.0)])
