@@ -1254,11 +1254,21 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
                                            int (&bv)[4]) {
     const uint32_t key = sorted_keys[k];
-    if (key == sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     f_key[k] = key;
     const uint32_t i = perm[k];
-    if (i >= n_total) {  // bug guard: a broken permutation must not read out of bounds
+    if (key == sentinel || i >= n_total) {
+        // Fewer live entries than the host counted (a device Enter / Leave batch broke its rules, or a
+        // broken permutation): the flush fails and poisons the world, but it must not fault first.  The
+        // entry becomes an inert placeholder: slot 0 of space 0 at NaN (no relation, no slot-indexed
+        // write, no bbox).
         atomicOr(&sc->err, ERR_COUNT_MISMATCH);
+        Rec16 z;
+        z.x = z.z = qnan();
+        z.s = 0;
+        st_rec(f_rec, k, z);
+        st_rec(o_rec, k, z);
+        reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(0u, 0u);
+        cand[k] = make_uint4(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u);
         return;
     }
     const SlotSp ss = ld_ss(s_ss, i);
