@@ -66,6 +66,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->bmax = 0.0f;
         sc->seq_max = 0;
         sc->ncoll = 0;
+        sc->apply_done = 0;
         for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
     if (i < n0) z0[i] = 0;
@@ -241,10 +242,36 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint
     if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (R.j0 + i);
 }
 
+// The slots moved more than once: the op whose claim survived every atomicMax is applied again, on
+// the previous state (so that a dropped, invalid winner leaves it unchanged).  Run by the last
+// block of the last run's apply once every block has finished (k_moves_apply_n): the list and the
+// claims are read at agent scope, past this CU's L1 (which may hold lines read before the others'
+// atomicMax).
+__device__ void moves_fixup(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
+                            unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
+                            uint32_t n_prev, TickScalars *sc, const uint32_t *coll) {
+    const uint32_t nc = __hip_atomic_load(&sc->ncoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
+        const uint32_t s = __hip_atomic_load(coll + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long lo = __hip_atomic_load(&info[s].lastop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long rk = __hip_atomic_load(reinterpret_cast<unsigned long long *>(info + s) + 1,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint4 si = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)rk, (uint32_t)(rk >> 32));
+        const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
+        uint32_t q = 0;
+        while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
+        const MoveRun &R = RS.r[q];
+        if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
+        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
+        op_apply_one(o, j, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, true);
+    }
+}
+
 template <int PER>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
-                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
+                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll, int last,
+                                                       MoveRuns RS, const Rec16 *__restrict__ p_rec, uint32_t n_prev) {
     const uint32_t i0 = blockIdx.x * (256u * PER) + threadIdx.x;
     OpIn o[PER];
     uint4 si[PER];
@@ -285,25 +312,19 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
         }
         if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
     }
-}
-
-__global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                              unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
-                              uint32_t n_prev, TickScalars *sc, const uint32_t *__restrict__ coll) {
-    const uint32_t nc = sc->ncoll;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
-        const uint32_t s = coll[k];
-        const uint4 si = reinterpret_cast<const uint4 *>(info)[s];
-        const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
-        uint32_t q = 0;
-        while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
-        const MoveRun &R = RS.r[q];
-        // start from the previous state so that a dropped (invalid) winner leaves it unchanged
-        if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
-        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
-        op_apply_one(o, j, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, true);
+    if (last) {  // the last block to finish re-applies the slots moved more than once (no extra launch)
+        __shared__ uint32_t s_last;
+        __threadfence();  // this block's claims, list entries and S' writes before its count
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = atomicAdd(&sc->apply_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+        __syncthreads();
+        if (s_last) {
+            __threadfence();
+            moves_fixup(RS, max_slots, info, tick, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev, sc, coll);
+        }
     }
 }
+
 
 // --------------------------------------------------------------- keygen ------
 
@@ -2824,12 +2845,14 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st) {
     for (uint32_t q = n_marked; q < RS.count; ++q)  // every run's claims before any apply
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
+    uint32_t last = 0;
+    for (uint32_t q = 0; q < RS.count; ++q)
+        if (RS.r[q].n) last = q;
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
             k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
-                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
-    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
-                                      sc, coll);
+                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll, q == last ? 1 : 0, RS,
+                p_rec, n_prev);
 }
 
 uint32_t moves_buckets(uint32_t max_slots) { return cdiv(max_slots, MV_R); }

@@ -1257,6 +1257,19 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             eb, lb = B.tick()
             np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
+        # the caller's own pinned buffer (gwaoi_pinned_alloc + gwaoi_moved_batch_pinned)
+        sl, nx, nz = wl.tick(30)
+        keep = sl < wl.n - 10
+        sl, nx, nz = sl[keep], nx[keep], nz[keep]
+        ptr, views = A.pinned_batch(sl.size)
+        views[0][:], views[1][:], views[2][:] = sl, nx, nz
+        A.moved_batch_pinned(views, sl.size)
+        B.moved_batch(sl, nx, nz)
+        ea, la = A.tick()
+        eb, lb = B.tick()
+        A.free_pinned_batch(ptr)
+        np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
+        np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
         # an Enter queued first: the staged batch then carries the space column (host-checked)
         new = slots[-10:]
         for w in (A, B):

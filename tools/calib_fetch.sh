@@ -1,0 +1,12 @@
+#!/bin/bash
+# FETCH_SIZE calibration for k_combined's read shapes (tools/calib_fetch.hip), on the GPU box.
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export TMPDIR=/tmp
+OUT=$R/gpurun_out/calib_fetch
+mkdir -p $OUT
+cd /tmp
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $R/goworld_amd/lib/calib_fetch > $OUT/calib.json 2> $OUT/fetch.err
+timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o run -- $R/goworld_amd/lib/calib_fetch > /dev/null 2> $OUT/trace.err
+rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+ls -R $OUT | head

@@ -75,6 +75,7 @@ def main():
     ks = kernel_stats(d)
     steady = trace_steady(d)
     sq = pmc(d, "pmc_sq")
+    tc = pmc(d, "pmc_tcp")
     fe = pmc(d, "pmc_fetch")
     wr = pmc(d, "pmc_write")
     kern = {}
@@ -83,6 +84,16 @@ def main():
         e = dict(r)
         e["steady_median_us"] = steady.get(k)
         e["pmc"] = dict(sq.get(k, {}))
+        e["pmc"].update(tc.get(k, {}))
+        p = e["pmc"]
+        if p.get("SQ_WAVE_CYCLES"):
+            for c in ("SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY"):
+                if c in p:
+                    e.setdefault("derived", {})[c + "_frac"] = p[c] / p["SQ_WAVE_CYCLES"]
+        if p.get("TCP_TOTAL_CACHE_ACCESSES_sum") and "TCP_TCC_READ_REQ_sum" in p:
+            e.setdefault("derived", {})["tcp_hit_rate"] = 1.0 - p["TCP_TCC_READ_REQ_sum"] / p["TCP_TOTAL_CACHE_ACCESSES_sum"]
+        if p.get("TCC_HIT_sum") is not None and p.get("TCC_MISS_sum") is not None and p["TCC_HIT_sum"] + p["TCC_MISS_sum"]:
+            e.setdefault("derived", {})["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
         f = fe.get(k, {}).get("FETCH_SIZE")
         w = wr.get(k, {}).get("WRITE_SIZE")
         if f is not None:
@@ -99,7 +110,7 @@ def main():
         json.dump(js, fh, indent=1)
     lines = [f"# rocprofv3 summary ({os.path.basename(dst)})", "",
              "Command: `tools/profile.sh` = `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 8 --warmup 2`, "
-             "then separate `--pmc` passes (SQ block, FETCH_SIZE, WRITE_SIZE). "
+             "then separate `--pmc` passes (SQ block with SQ_WAIT_ANY / SQ_ACTIVE_INST_ANY, TCP/TCC hit counters, FETCH_SIZE, WRITE_SIZE). "
              "PMC values are medians over steady-state dispatches; HBM read bytes = 2 x FETCH_SIZE (gfx950 correction).", ""]
     if bench:
         lines += [f"bench under trace: ms_per_step {bench.get('ms_per_step'):.4f}, value {bench.get('value'):.4g} "
@@ -119,6 +130,8 @@ def main():
         lines += ["", f"## PMC, {top} (steady-state median per dispatch)", ""]
         for c, v in sorted(kern[top]["pmc"].items()):
             lines.append(f"- {c}: {v:.6g}")
+        for c, v in sorted(kern[top].get("derived", {}).items()):
+            lines.append(f"- {c}: {v:.4f}")
     open(dst + ".md", "w").write("\n".join(lines) + "\n")
     kc = kern.get("k_combined")
     if kc and "hbm_bytes" in kc:

@@ -1,16 +1,17 @@
 // gwaoi_tick_bench -- SURVEY.md §8(d)'s end-to-end tick from a C++ host, the
 // view a cgo caller has: config 3 (1M entities, 256 Gaussian crowd hotspots +
 // uniform background, D = 100, every entity moves by U(-1,1) per axis per tick
-// in a seeded random call order), host move arrays -> gwaoi_moved_batch
-// (validation + pinned staging + H2D) -> flush -> events in pinned host memory,
+// in a seeded random call order), host move arrays (the caller's pinned buffers,
+// gwaoi_moved_batch_pinned: one H2D, checked on the device) -> flush -> events
+// in pinned host memory,
 // then the callback replay of Entity.go:236-246 (interest / uninterest: a.In
 // += b, b.By += a per directed event) into per-entity InterestedIn /
 // InterestedBy sets, the part SURVEY.md §7 (hard part 6) expects to dominate.
 //
 // Three measurements, one JSON line:
-//   serial     gwaoi_moved_batch + gwaoi_tick per tick (latency p50 / p99)
-//   pipelined  gwaoi_tick_begin(t); gwaoi_moved_batch(t+1) while the GPU runs;
-//              gwaoi_tick_end(t)  (period = host staging overlapped with the flush)
+//   serial     gwaoi_moved_batch_pinned + gwaoi_tick per tick (latency p50 / p99)
+//   pipelined  gwaoi_tick_begin(t); gwaoi_moved_batch_pinned(t+1) while the GPU runs;
+//              gwaoi_tick_end(t)  (period = host replay overlapped with the flush)
 //   replay     the tick's events into the sets: the event pairs on one thread;
 //              the per-entity rows of gwaoi_events_csr on one and on T threads
 //              (each thread owns the sets of a slot range; persistent pool)
@@ -233,6 +234,23 @@ int main(int argc, char **argv) {
     uint32_t sp = 0;
     check(gwaoi_space_create(w, 100.0f, &sp), "space_create", w);
     check(gwaoi_enter_batch(w, sp, bs[0].data(), bx[0].data(), bz[0].data(), n), "enter_batch", w);
+    // the caller's per-tick move buffers in pinned memory (gwaoi_pinned_alloc), filled before timing:
+    // a game server appends the decoded moves there while the tick's packets arrive, and
+    // gwaoi_moved_batch_pinned sends a buffer with one H2D (checked on the device)
+    std::vector<uint32_t *> pin(nb, nullptr);
+    for (int t = 1; t < nb; ++t) {
+        void *p = nullptr;
+        check(gwaoi_pinned_alloc(w, 12 * (size_t)n, &p), "pinned_alloc", w);
+        pin[t] = static_cast<uint32_t *>(p);
+        std::copy(bs[t].begin(), bs[t].end(), pin[t]);
+        std::copy(bx[t].begin(), bx[t].end(), reinterpret_cast<float *>(pin[t] + n));
+        std::copy(bz[t].begin(), bz[t].end(), reinterpret_cast<float *>(pin[t] + 2 * (size_t)n));
+    }
+    auto batch = [&](int t) {
+        check(gwaoi_moved_batch_pinned(w, pin[t], reinterpret_cast<const float *>(pin[t] + n),
+                                       reinterpret_cast<const float *>(pin[t] + 2 * (size_t)n), n),
+              "moved_batch_pinned", w);
+    };
     gwaoi_events ev{};
     check(gwaoi_tick(w, &ev), "populate", w);
     const uint64_t populate = ev.n_enter;
@@ -252,7 +270,7 @@ int main(int argc, char **argv) {
     uint64_t events = 0;
     for (int t = 1; t <= ticks; ++t) {
         const double a = now();
-        check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
+        batch(t);
         const double b = now();
         check(gwaoi_tick(w, &ev), "tick", w);
         const double c = now();
@@ -290,14 +308,14 @@ int main(int argc, char **argv) {
     };
     int t = ticks + 1;
     double t_issue = now();
-    check(gwaoi_moved_batch(w, bs[t].data(), bx[t].data(), bz[t].data(), n), "moved_batch", w);
+    batch(t);
     const double p0 = now();
     int done = 0;
     bool have_prev = false;
     for (; t < nb; ++t) {
         check(gwaoi_tick_begin(w), "tick_begin", w);
         const double h0 = now(), issued_next = h0;
-        if (t + 1 < nb) check(gwaoi_moved_batch(w, bs[t + 1].data(), bx[t + 1].data(), bz[t + 1].data(), n), "moved_batch", w);
+        if (t + 1 < nb) batch(t + 1);
         if (have_prev) replay_T();  // tick t-1's callbacks, overlapping the flush of t
         p_host.push_back(now() - h0);
         uint64_t ne_, nl_;
@@ -331,6 +349,8 @@ int main(int argc, char **argv) {
             if (S.r[S.owner(s)].members(s, gwsets::IN) != want || S.r[S.owner(s)].members(s, gwsets::BY) != want) ++sample_bad;
         }
     }
+    for (uint32_t *p : pin)
+        if (p) gwaoi_pinned_free(w, p);
     gwaoi_world_destroy(w);
     const double ms = 1e3;
     std::printf(
