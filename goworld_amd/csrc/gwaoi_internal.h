@@ -80,6 +80,7 @@ struct FrameView {
     const Rec16 *rec;
     const SlotSp *ss;
     const uint32_t *cell_start;  // total_cells + 1 entries
+    const float2 *cbx;           // per cell: (min x, max x) of its entries (k_gather); stale while empty
     const SpaceGrid *grid;
     uint32_t n;
     uint32_t total_cells;
@@ -196,9 +197,10 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // new cell_start (from cnt64) plus, per cell, a merge of the entities that
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
 // frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
-// look-back status words (zeroed once when allocated); tag: fresh per launch.
+// look-back status words (zeroed once when allocated); tag: fresh per launch;
+// arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
 size_t incr_sort_tmp_elems(size_t cells);
-// true: the sort's scan zeroes cnt64 as it reads it (zeroed once when allocated)
+// true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
 bool scan_rezeroes_counts();
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
@@ -225,7 +227,7 @@ void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const 
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
-                   uint32_t n_spaces, void *bbox_parts, hipStream_t st);
+                   uint32_t n_spaces, void *bbox_parts, float2 *cbx, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
 // Combined pass over the new frame: blocks of TILE_A consecutive entries

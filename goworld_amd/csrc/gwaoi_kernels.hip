@@ -1035,13 +1035,15 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
     }
 }
 
-// The counts are zeroed as they are read (1): the next flush's
-// k_keygen<true> finds them zero, so the prologue no longer clears 2 words per
-// cell (16 MB of 4-B stores at config 3).
-__global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restrict__ in, size_t n, uint32_t nb,
+// The counts are not cleared here: k_arrive zeroes the two cells of every entity that changed
+// cell (the only cells k_keygen<true> counted into), so the next flush's keygen finds them zero
+// without a store per cell.  shift[c]: SHIFT_CHANGED for a cell with arrivals or departures, else
+// how far its run moved (new start - previous start): k_arrive places such a cell's stayers itself.
+constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
+__global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
-                                                    const uint32_t *__restrict__ p_cs) {
+                                                    const uint32_t *__restrict__ p_cs, uint32_t *shift) {
     const uint32_t b = blockIdx.x;
     if (b == nb) {
         keygen_fold256(blk, nbk, sc);
@@ -1055,7 +1057,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
     for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
-        if (base + j < n) in[base + j] = 0ull;
     }
     __syncthreads();
     unsigned long long v[S64_I];
@@ -1082,8 +1083,8 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
     }
     run += e;
 #pragma unroll
-    for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read
-        tile[p64(tid * S64_I + (uint32_t)q)] = run;
+    for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read; bit 31: c changed
+        tile[p64(tid * S64_I + (uint32_t)q)] = run | (v[q] ? (unsigned long long)SHIFT_CHANGED : 0ull);
         run += v[q];
     }
     __syncthreads();
@@ -1094,36 +1095,54 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(unsigned long long *__restri
             const unsigned long long e = tile[p64(j)];
             // e = (departures before c) << 32 | (arrivals before c): cell c starts at its previous
             // start plus the arrivals minus the departures of the cells before it
-            lo[base + j] = p_cs[base + j] + (uint32_t)e - (uint32_t)(e >> 32);
-            hi[base + j] = (uint32_t)e;
+            const uint32_t arr = (uint32_t)e & ~SHIFT_CHANGED, d = arr - (uint32_t)(e >> 32);
+            lo[base + j] = p_cs[base + j] + d;
+            hi[base + j] = arr;
+            shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
         }
     }
 }
 
 // Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
-// of cell c and ends as that of cell c+1.
+// of cell c and ends as that of cell c+1.  An entity that changed cell also
+// zeroes the counts of both its cells (k_scan64_lb has read them).  A stayer
+// of an unchanged cell (no arrival, no departure) keeps its rank in the run,
+// so its frame position is its S' index plus the cell's shift.
 __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
                          const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
-                         unsigned long long *cnt64) {
+                         unsigned long long *cnt64, const uint32_t *__restrict__ shift, uint32_t *perm,
+                         uint32_t *skeys) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t key = keys[i];
-    (void)cnt64;
-    if (key == sentinel || (i < n_prev && p_key[i] == key)) return;
+    const uint32_t old = i < n_prev ? p_key[i] : sentinel;
+    if (key == old) {
+        if (key == sentinel) return;
+        const uint32_t d = shift[key];
+        if (d != SHIFT_CHANGED) {
+            perm[i + d] = i;
+            skeys[i + d] = key;
+        }
+        return;
+    }
+    if (old != sentinel) cnt64[old] = 0ull;
+    if (key == sentinel) return;
+    cnt64[key] = 0ull;
     arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
 }
 
-// One lane per cell c: the stayers are the entries of c's previous run whose
-// new key is still c (S' index order), the arrivals arr_idx[arr_pos[c-1],
-// arr_pos[c]) are sorted by S' index (insertion sort: a cell rarely gets
-// more than a few) and merged in.  Writes the frame's permutation and keys.
+// One lane per changed cell c (shift[c] == SHIFT_CHANGED; k_arrive placed the
+// others): the stayers are the entries of c's previous run whose new key is
+// still c (S' index order), the arrivals arr_idx[arr_pos[c-1], arr_pos[c])
+// are sorted by S' index (insertion sort: a cell rarely gets more than a few)
+// and merged in.  Writes the frame's permutation and keys.
 __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const uint32_t *__restrict__ cell_start,
                              const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                              uint32_t *arr_idx, uint32_t total_cells, uint32_t n_new, uint32_t n_total,
-                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys) {
+                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ shift) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c == 0 && n_new < n_total) skeys[n_new] = sentinel;
-    if (c >= total_cells) return;
+    if (c >= total_cells || shift[c] != SHIFT_CHANGED) return;
     uint32_t o = cell_start[c];
     const uint32_t oe = cell_start[c + 1];
     if (o == oe) return;
@@ -1165,6 +1184,7 @@ __device__ __forceinline__ int f2o(float f) {
     int i = __float_as_int(f);
     return i ^ ((i >> 31) & 0x7FFFFFFF);
 }
+[[maybe_unused]] __device__ __forceinline__ float o2f(int i) { return __int_as_float(i ^ ((i >> 31) & 0x7FFFFFFF)); }  // f2o's inverse
 
 __device__ __forceinline__ void bbox_flush(int4 *bbox, uint32_t ns, uint32_t sp, const int (&v)[4]) {
     if (sp >= ns) return;
@@ -1237,6 +1257,10 @@ __device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], in
     if (!s_uni && cur != SP_DEAD) bbox_flush(bbox, ns, cur, own);  // mixed spaces: every run flushes
 }
 
+#ifndef GWAOI_CELL_BOUNDS
+#define GWAOI_CELL_BOUNDS 1  // k_gather folds per-cell x bounds; k_combined trims the X' rows' end cells by them
+#endif
+
 // --------------------------------------------------------------- gather ------
 
 __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restrict__ perm, uint32_t n_prev, uint32_t n_new,
@@ -1248,6 +1272,37 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
                                            int (&bv)[4]);
 
+// Per-cell x bounds of the new frame (k_combined trims the X' rows' end cells by them).  The
+// frame is sorted by cell, so a cell's entries are one run: a segmented fold inside the wave,
+// then the run's first lane writes.  A run that crosses a wave boundary gets (-inf, +inf) from the
+// wave holding its first entry (no trim); an empty cell keeps a stale pair, which trims nothing.
+#if GWAOI_CELL_BOUNDS
+__device__ __forceinline__ void cell_bounds(uint32_t k, uint32_t n_new, const uint32_t *__restrict__ keys,
+                                            uint32_t sentinel, int vlo, int vhi, float2 *cbx) {
+    const uint32_t l = lane();
+    const uint32_t key = k < n_new ? keys[k] : sentinel;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {  // lane l: fold over [l, l + 2o) of its run
+        const uint32_t ko = (uint32_t)__shfl_down((int)key, o);
+        const int lo2 = __shfl_down(vlo, o), hi2 = __shfl_down(vhi, o);
+        if (l + (uint32_t)o < WAVE && ko == key) {
+            vlo = min(vlo, lo2);
+            vhi = max(vhi, hi2);
+        }
+    }
+    const uint32_t kprev = (uint32_t)__shfl_up((int)key, 1);
+    const bool head = l ? kprev != key : (k == 0 || k >= n_new || keys[k - 1] != key);  // first entry of its run
+    // the wave's last run continues past the wave?
+    const bool cont_last = l == WAVE - 1 && k + 1 < n_new && keys[k + 1] == key;
+    const bool cont = __ballot(cont_last) != 0ull;
+    const uint32_t klast = (uint32_t)__builtin_amdgcn_readlane((int)key, WAVE - 1);
+    if (head && k < n_new && key != sentinel) {
+        cbx[key] = cont && key == klast ? make_float2(-INFINITY, INFINITY)
+                                        : make_float2(o2f(vlo), o2f(vhi));
+    }
+}
+#endif
+
 // One thread per new-frame entry; the block also folds its entries' bbox
 // (level 1 of the per-space bounding box, k_finish folds level 2).
 __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, uint32_t n_new, uint32_t n_prev,
@@ -1256,13 +1311,18 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
                          SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
                          unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
-                         uint32_t n_spaces, BBoxPart *parts) {
+                         uint32_t n_spaces, BBoxPart *parts, float2 *cbx) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     uint32_t cur = SP_DEAD;
     int bv[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
     if (k < n_new) gather_one(k, perm, n_prev, n_new, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand, grid, seq_base,
                               info, sorted_keys, sentinel, n_total, sc, f_key, cur, bv);
+#if GWAOI_CELL_BOUNDS
+    cell_bounds(k, n_new, sorted_keys, sentinel, bv[0], bv[2], cbx);
+#else
+    (void)cbx;
+#endif
     bbox_block(cur, bv, bbox, n_spaces, &parts[blockIdx.x]);
 }
 
@@ -1994,7 +2054,7 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
                                            const uint4 *__restrict__ cand, const FrameView &F,
                                            const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint2 *out,
                                            uint64_t cap, unsigned long long pe, unsigned long long pl, bool replay) {
-    static_assert(P >= 1 && P <= 4, "one to four row ranges per lane");
+    static_assert(P == 1 || P == 2, "one or two row ranges per lane");
     constexpr int U = GWAOI_FLAT_U;
     const uint32_t me = lane();
     uint32_t cum[P], tot = 0;  // items before row q of this lane
@@ -2011,10 +2071,7 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
     const uint32_t off = inc - tot;
     const uint32_t offa = off | ((A.a & (uint32_t)(CT - 1)) << 24);
     // row q's candidate of lane-local item kk is (jb[q] - cum[q]) + kk, for the last q with cum[q] <= kk
-    if (P <= 2) {
-        L.seg[w][me] = make_uint4(jb[0], P == 2 ? jb[P - 1] - cum[P - 1] : 0u, P == 2 ? cum[P - 1] : 0xFFFFFFFFu, offa);
-    } else {
-    }
+    L.seg[w][me] = make_uint4(jb[0], P == 2 ? jb[P - 1] - cum[P - 1] : 0u, P == 2 ? cum[P - 1] : 0xFFFFFFFFu, offa);
     L.atab[w][me] = make_float4(A.x, A.z, A.xo, A.zo);
     uint8_t *mk = L.mark[w];
     uint32_t carry = 0;  // owner + 1 of the position before this chunk
@@ -2046,13 +2103,9 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
             const uint32_t p = g0 + (uint32_t)(u * WAVE) + me;
             const uint32_t o = (own[u] - 1u) & (uint32_t)(WAVE - 1);
             const uint4 s = L.seg[w][o];
-            uint32_t idx;
-            if (P <= 2) {
-                const uint32_t kk = p - (s.w & 0xFFFFFFu);
-                idx = (kk >= s.z ? s.y : s.x) + kk;
-                ao[u] = s.w >> 24;
-            } else {
-            }
+            const uint32_t kk = p - (s.w & 0xFFFFFFu);
+            const uint32_t idx = (kk >= s.z ? s.y : s.x) + kk;
+            ao[u] = s.w >> 24;
             bi[u] = p < T ? idx : 0u;
             const float4 ap = L.atab[w][o];
             ax[u] = ap.x;
@@ -2126,6 +2179,26 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
     const uint32_t gx = C.g.gx;
     const uint32_t xb = C.g.base + (uint32_t)xr0 * gx + (uint32_t)xc0, xs = (uint32_t)(xc1 - xc0) + 1u;
     const uint32_t zb = C.g.base + (uint32_t)zr0 * gx + (uint32_t)zc0, zs = (uint32_t)(zc1 - zc0) + 1u;
+#if GWAOI_CELL_BOUNDS
+    // an X' row's end cells whose entries all lie left of the band (max x < x + lo - M) or past its
+    // outer bound (min x > x + hi + M: dropped by the unchanged-relation test) are not swept
+    const float xl = A.x + C.lo - C.M, xh = A.x + C.hi + C.M;
+    auto range = [&](uint32_t q, uint32_t &b, uint32_t &l) {
+        b = l = 0;
+        if (q < nx) {
+            const uint32_t rb = xb + q * gx;
+            const uint32_t c0 = rb + (F.cbx[rb].y < xl ? 1u : 0u);
+            const uint32_t c1 = rb + xs - 1u;
+            const uint32_t ce = c1 + (c1 >= c0 && F.cbx[c1].x > xh ? 0u : 1u);  // one past the last swept cell
+            b = cs[c0];
+            l = cs[ce] - b;
+        } else if (q < nr) {
+            const uint32_t rb = zb + (q - nx) * gx;
+            b = cs[rb];
+            l = cs[rb + zs] - b;
+        }
+    };
+#else
     auto range = [&](uint32_t q, uint32_t &b, uint32_t &l) {
         b = l = 0;
         if (q < nr) {
@@ -2134,6 +2207,7 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
             l = cs[rb + (q < nx ? xs : zs)] - b;
         }
     };
+#endif
     uint32_t jb[P], ln[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) range((uint32_t)q, jb[q], ln[q]);
@@ -2956,7 +3030,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 }
 
 // look-back status words: lo and hi per block
-bool scan_rezeroes_counts() { return 1 != 0 || 0 != 0; }
+bool scan_rezeroes_counts() { return true; }
 
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
 
@@ -2967,12 +3041,14 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       TickScalars *sc, uint32_t tag, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
+    uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 2 (total_cells + 1) words
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
-                                         cdiv(n_total, 256), sc, p_cell_start);
+                                         cdiv(n_total, 256), sc, p_cell_start, shift);
     if (n_total)
-        k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64);
+        k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
+                                                     shift, perm, skeys);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
-                                                         n_new, n_total, sentinel, perm, skeys);
+                                                         n_new, n_total, sentinel, perm, skeys, shift);
 }
 
 size_t scan_tmp_elems(size_t n) {
@@ -3021,11 +3097,11 @@ void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const 
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
-                   uint32_t n_spaces, void *bbox_parts, hipStream_t st) {
+                   uint32_t n_spaces, void *bbox_parts, float2 *cbx, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
     k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand,
                                             grid, seq_base, info, sorted_keys, sentinel, n_total, sc, f_key, bbox,
-                                            n_spaces, reinterpret_cast<BBoxPart *>(bbox_parts));
+                                            n_spaces, reinterpret_cast<BBoxPart *>(bbox_parts), cbx);
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {

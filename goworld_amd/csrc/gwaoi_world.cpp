@@ -45,6 +45,7 @@ struct DevFrame {
     gw::SlotSp *ss = nullptr;
     uint32_t *key = nullptr;  // cell key of every entry (the next flush's "previous cell")
     uint32_t *cell_start = nullptr;
+    float2 *cbx = nullptr;  // per-cell x bounds (cell_cap entries)
     size_t cell_cap = 0;  // entries allocated in cell_start
     SpaceGrid *grid = nullptr;
     std::vector<SpaceGrid> hgrid;  // host mirror of `grid` (upload only on change)
@@ -512,11 +513,12 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     dfree(w->arr_pos);
     w->cnt64_cap = 0;
     int rc;
-    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, cap)) ||
+    // arr_pos: the arrival cursors, then the per-cell stayer shifts (incremental_sort)
+    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
-    HIP_TRY(hipMemsetAsync(w->cnt64, 0, cap * sizeof(unsigned long long), w->stream));  // then kept zero by the scan
+    HIP_TRY(hipMemsetAsync(w->cnt64, 0, cap * sizeof(unsigned long long), w->stream));  // then kept zero by the sort
     w->cnt64_cap = cap;
     return GWAOI_OK;
 }
@@ -527,7 +529,10 @@ int ensure_cells(gwaoi_world *w, DevFrame &f, size_t cells) {
     size_t cap = std::max(need + need / 4, (size_t)1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(f.cell_start);
+    dfree(f.cbx);
+    f.cbx = nullptr;
     int rc = dalloc(w, &f.cell_start, cap);
+    if (!rc) rc = dalloc(w, &f.cbx, cap);
     if (rc) {
         f.cell_cap = 0;
         return rc;
@@ -721,6 +726,7 @@ gw::FrameView view_of(const DevFrame &f) {
     v.rec = f.rec;
     v.ss = f.ss;
     v.cell_start = f.cell_start;
+    v.cbx = f.cbx;
     v.grid = f.grid;
     v.n = f.n;
     v.total_cells = f.total_cells;
@@ -995,7 +1001,7 @@ int tick_launch(gwaoi_world *w) {
     stage_begin(w, S, ST_GATHER);
     gw::launch_gather(perm, n_new, n_prev, S.srec, s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, S.orec, S.cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
-                      total_cells, n_total, S.sc, Fn.key, dev_bbox(S), w->n_space_ids, S.bbox_parts, st);
+                      total_cells, n_total, S.sc, Fn.key, dev_bbox(S), w->n_space_ids, S.bbox_parts, Fn.cbx, st);
     stage_end(w, S, ST_GATHER);
 
     // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
@@ -1246,7 +1252,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->sync) gw::sync_destroy(w->sync);
     w->sync = nullptr;
     for (DevFrame &f : w->fr) {
-        dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.grid);
+        dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.cbx); dfree(f.grid);
     }
     for (FlushSet &S : w->fs) {
         dfree(S.srec); dfree(S.sss); dfree(S.orec); dfree(S.cand); dfree(S.sc); dfree(S.events);
