@@ -1141,7 +1141,14 @@ __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const ui
                              uint32_t *arr_idx, uint32_t total_cells, uint32_t n_new, uint32_t n_total,
                              uint32_t sentinel, uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ shift) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0 && n_new < n_total) skeys[n_new] = sentinel;
+    // entries past the live count are dead: sentinel keys, no source (so a host count that
+    // disagrees with the device's -- a device batch breaking its rules -- finds sentinels, not
+    // a previous flush's values, at [n_new, n_total))
+    for (uint32_t k = cell_start[total_cells] + c; k < n_total; k += gridDim.x * blockDim.x) {
+        skeys[k] = sentinel;
+        perm[k] = 0xFFFFFFFFu;
+    }
+    (void)n_new;
     if (c >= total_cells || shift[c] != SHIFT_CHANGED) return;
     uint32_t o = cell_start[c];
     const uint32_t oe = cell_start[c + 1];
@@ -1296,7 +1303,7 @@ __device__ __forceinline__ void cell_bounds(uint32_t k, uint32_t n_new, const ui
     const bool cont_last = l == WAVE - 1 && k + 1 < n_new && keys[k + 1] == key;
     const bool cont = __ballot(cont_last) != 0ull;
     const uint32_t klast = (uint32_t)__builtin_amdgcn_readlane((int)key, WAVE - 1);
-    if (head && k < n_new && key != sentinel) {
+    if (head && k < n_new && key < sentinel) {
         cbx[key] = cont && key == klast ? make_float2(-INFINITY, INFINITY)
                                         : make_float2(o2f(vlo), o2f(vhi));
     }
@@ -1337,7 +1344,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     const uint32_t key = sorted_keys[k];
     f_key[k] = key;
     const uint32_t i = perm[k];
-    if (key == sentinel || i >= n_total) {
+    if (key >= sentinel || i >= n_total) {
         // Fewer live entries than the host counted (a device Enter / Leave batch broke its rules, or a
         // broken permutation): the flush fails and poisons the world, but it must not fault first.  The
         // entry becomes an inert placeholder: slot 0 of space 0 at NaN (no relation, no slot-indexed

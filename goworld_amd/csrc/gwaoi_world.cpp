@@ -233,6 +233,9 @@ struct gwaoi_world {
     hipEvent_t done_ev = nullptr;  // wait_stream's marker
     hipEvent_t order_ev = nullptr;  // gwaoi_stream_after / _before
     bool blocking_sync = false;
+    bool check_stages = false;   // GWAOI_CHECK_STAGES=1: wait after every flush stage (fault diagnosis)
+    const char *fault_stage = nullptr;  // stage at the first failed wait
+    bool fault_before = false;          // ... the wait before it (else after it)
     uint32_t *new_slots_d = nullptr;
     uint32_t *op_slot = nullptr, *op_sp = nullptr;
     float *op_x = nullptr, *op_z = nullptr;
@@ -382,11 +385,17 @@ void dfree(T *&p) {
 inline bool finite2(float x, float z) { return std::isfinite(x) && std::isfinite(z); }
 
 void stage_begin(gwaoi_world *w, FlushSet &S, Stage s) {
+    if (w->check_stages && !w->fault_stage && hipStreamSynchronize(w->stream) != hipSuccess) {
+        w->fault_stage = kStageNames[s];
+        w->fault_before = true;
+    }
     if (!(w->timing_mask >> s & 1u)) return;
     (void)hipEventRecord(S.ev[s][0], w->stream);
     S.ev_used[s] = true;
 }
 void stage_end(gwaoi_world *w, FlushSet &S, Stage s) {
+    if (w->check_stages && !w->fault_stage && hipStreamSynchronize(w->stream) != hipSuccess)
+        w->fault_stage = kStageNames[s];
     if (!(w->timing_mask >> s & 1u)) return;
     (void)hipEventRecord(S.ev[s][1], w->stream);
 }
@@ -1108,6 +1117,9 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
     DevFrame &Fn = w->fr[f.n_idx];
     if (wait_done(w, S.done_ev) != GWAOI_OK) {
         w->last_error = "flush did not complete: " + w->last_error;
+        if (w->fault_stage)
+            w->last_error += std::string(" (first failed stage wait: ") + (w->fault_before ? "before " : "after ") +
+                             w->fault_stage + ")";
         return poison(w, GWAOI_EDEVICE);
     }
 
@@ -1414,6 +1426,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         hipEventCreateWithFlags(&w->order_ev, hipEventDisableTiming) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     if (const char *e = std::getenv("GWAOI_BLOCKING_SYNC")) w->blocking_sync = e[0] == '1';
+    if (const char *e = std::getenv("GWAOI_CHECK_STAGES")) w->check_stages = e[0] == '1';
     w->alive.assign(N, 0);
     w->in_frame.assign(N, 0);
     w->appended.assign(N, 0);

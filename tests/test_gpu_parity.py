@@ -1222,7 +1222,9 @@ def test_device_enter_of_live_slot_poisons_gpu():
         for i in range(4):
             w.enter(0, i, float(i), 0.0)
         w.tick()
-        d = [torch.tensor(a, device="cuda:0") for a in ([2, 9], [5.0, 6.0], [0.0, 0.0])]
+        d = [torch.tensor([2, 9], dtype=torch.int32, device="cuda:0"),
+             torch.tensor([5.0, 6.0], dtype=torch.float32, device="cuda:0"),
+             torch.tensor([0.0, 0.0], dtype=torch.float32, device="cuda:0")]
         torch.cuda.synchronize()
         w.enter_batch_device(0, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 2)
         with pytest.raises(GwaoiError) as ei:
