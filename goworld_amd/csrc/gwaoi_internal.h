@@ -96,7 +96,7 @@ struct TickScalars {
     float bmax;                  // largest |x|,|z| of live entities (new positions)
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
-    uint32_t apply_done;         // blocks of the last Moved run's apply that finished (the last one fixes up)
+    uint32_t pad2;
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
 };
 

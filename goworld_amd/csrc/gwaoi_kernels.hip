@@ -66,7 +66,6 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->bmax = 0.0f;
         sc->seq_max = 0;
         sc->ncoll = 0;
-        sc->apply_done = 0;
         for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
     if (i < n0) z0[i] = 0;
@@ -242,36 +241,10 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint
     if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (R.j0 + i);
 }
 
-// The slots moved more than once: the op whose claim survived every atomicMax is applied again, on
-// the previous state (so that a dropped, invalid winner leaves it unchanged).  Run by the last
-// block of the last run's apply once every block has finished (k_moves_apply_n): the list and the
-// claims are read at agent scope, past this CU's L1 (which may hold lines read before the others'
-// atomicMax).
-__device__ void moves_fixup(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                            unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
-                            uint32_t n_prev, TickScalars *sc, const uint32_t *coll) {
-    const uint32_t nc = __hip_atomic_load(&sc->ncoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
-        const uint32_t s = __hip_atomic_load(coll + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long lo = __hip_atomic_load(&info[s].lastop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long rk = __hip_atomic_load(reinterpret_cast<unsigned long long *>(info + s) + 1,
-                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint4 si = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)rk, (uint32_t)(rk >> 32));
-        const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
-        uint32_t q = 0;
-        while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
-        const MoveRun &R = RS.r[q];
-        if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
-        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
-        op_apply_one(o, j, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, true);
-    }
-}
-
 template <int PER>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
-                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll, int last,
-                                                       MoveRuns RS, const Rec16 *__restrict__ p_rec, uint32_t n_prev) {
+                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
     const uint32_t i0 = blockIdx.x * (256u * PER) + threadIdx.x;
     OpIn o[PER];
     uint4 si[PER];
@@ -312,16 +285,26 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
         }
         if (lane() == 0 && smax) atomicMax(&sc->seq_max, smax);
     }
-    if (last) {  // the last block to finish re-applies the slots moved more than once (no extra launch)
-        __shared__ uint32_t s_last;
-        __threadfence();  // this block's claims, list entries and S' writes before its count
-        __syncthreads();
-        if (threadIdx.x == 0) s_last = atomicAdd(&sc->apply_done, 1u) == gridDim.x - 1 ? 1u : 0u;
-        __syncthreads();
-        if (s_last) {
-            __threadfence();
-            moves_fixup(RS, max_slots, info, tick, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev, sc, coll);
-        }
+}
+
+// The slots moved more than once: the op whose claim survived every atomicMax is applied again.
+// A launch of its own: fusing it into the last apply block needed a release fence in every block
+// (at agent scope on gfx950, a write-back of the XCD's L2), measured at 162 against 33 us per apply.
+__global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
+                              unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
+                              uint32_t n_prev, TickScalars *sc, const uint32_t *__restrict__ coll) {
+    const uint32_t nc = sc->ncoll;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
+        const uint32_t s = coll[k];
+        const uint4 si = reinterpret_cast<const uint4 *>(info)[s];
+        const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
+        uint32_t q = 0;
+        while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
+        const MoveRun &R = RS.r[q];
+        // start from the previous state so that a dropped (invalid) winner leaves it unchanged
+        if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
+        const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
+        op_apply_one(o, j, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, true);
     }
 }
 
@@ -1040,6 +1023,9 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 // without a store per cell.  shift[c]: SHIFT_CHANGED for a cell with arrivals or departures, else
 // how far its run moved (new start - previous start): k_arrive places such a cell's stayers itself.
 constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
+#ifndef GWAOI_STAYER
+#define GWAOI_STAYER 1  // 0: every cell through k_cell_merge, counts zeroed by the scan (round-3 form, A/B)
+#endif
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
@@ -1057,6 +1043,9 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
     for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
+#if !GWAOI_STAYER
+        if (base + j < n) const_cast<unsigned long long *>(in)[base + j] = 0ull;
+#endif
     }
     __syncthreads();
     unsigned long long v[S64_I];
@@ -1098,7 +1087,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
             const uint32_t arr = (uint32_t)e & ~SHIFT_CHANGED, d = arr - (uint32_t)(e >> 32);
             lo[base + j] = p_cs[base + j] + d;
             hi[base + j] = arr;
-            shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
+            shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) || !GWAOI_STAYER ? SHIFT_CHANGED : d;
         }
     }
 }
@@ -1125,9 +1114,13 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
         }
         return;
     }
+#if GWAOI_STAYER
     if (old != sentinel) cnt64[old] = 0ull;
     if (key == sentinel) return;
     cnt64[key] = 0ull;
+#else
+    if (key == sentinel) return;
+#endif
     arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
 }
 
@@ -2962,14 +2955,12 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st) {
     for (uint32_t q = n_marked; q < RS.count; ++q)  // every run's claims before any apply
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
-    uint32_t last = 0;
-    for (uint32_t q = 0; q < RS.count; ++q)
-        if (RS.r[q].n) last = q;
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
             k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
-                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll, q == last ? 1 : 0, RS,
-                p_rec, n_prev);
+                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
+    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, p_rec, n_prev,
+                                      sc, coll);
 }
 
 uint32_t moves_buckets(uint32_t max_slots) { return cdiv(max_slots, MV_R); }
