@@ -739,6 +739,7 @@ def run_strips(args, ws, rank, local, dist):
     def one(o, phases=None):
         a = time.perf_counter()
         send, counts, tele = sh.route(o)  # the tick's one host wait; it completes the previous tick
+        prev = sh.wait()  # the previous tick's counts, completed by the route: no wait
         b = time.perf_counter()
         if dist is not None:
             recv, tele_all, kinds = exchange(dist, send, counts, tele, via_cpu=via_cpu, kinds=sh.kinds)
@@ -750,7 +751,7 @@ def run_strips(args, ws, rank, local, dist):
             phases[0] += b - a
             phases[1] += c - b
             phases[2] += time.perf_counter() - c
-        return int(counts.sum() - counts[rank]), int(recv.shape[0])
+        return int(counts.sum() - counts[rank]), int(recv.shape[0]), prev
 
     one(init_ops)
     ne0, nl0 = sh.wait()
@@ -770,9 +771,8 @@ def run_strips(args, ws, rank, local, dist):
     t0 = time.perf_counter()
     for t in range(args.warmup, ticks):
         a = time.perf_counter()
-        ns, nr = one(ops[t], phases)
-        if t > args.warmup:
-            ne, nl = sh.wait()  # the previous tick's counts: completed by this route, no wait here
+        ns, nr, (ne, nl) = one(ops[t], phases)
+        if t > args.warmup:  # the previous tick's events (the first timed route completes a warmup tick)
             events += ne + nl
         lat.append(time.perf_counter() - a)
         sent += ns

@@ -245,10 +245,14 @@ class StripShard:
         return None
 
     def wait(self) -> Tuple[int, int]:
-        """Complete the queued tick: its (n_enter, n_leave)."""
+        """Complete the queued tick: its (n_enter, n_leave).  Right after ``route`` (which
+        completed it) this reads the counts without a wait, and the route's scatter keeps its
+        inputs referenced."""
+        w0 = self.host_waits()
         ne, nl = C.c_uint64(), C.c_uint64()
         self._check(self._L.gwaoi_strips_wait(self._s, C.byref(ne), C.byref(nl)))
-        self._inflight.clear()
+        if self.host_waits() != w0:  # the stream drained: nothing queued still reads the held tensors
+            self._inflight.clear()
         return ne.value, nl.value
 
     def host_waits(self) -> int:
