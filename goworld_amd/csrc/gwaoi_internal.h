@@ -80,7 +80,6 @@ struct FrameView {
     const Rec16 *rec;
     const SlotSp *ss;
     const uint32_t *cell_start;  // total_cells + 1 entries
-    const float2 *cbx;           // per cell: (min x, max x) of its entries (k_gather); stale while empty
     const SpaceGrid *grid;
     uint32_t n;
     uint32_t total_cells;
@@ -227,7 +226,7 @@ void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const 
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
-                   uint32_t n_spaces, void *bbox_parts, float2 *cbx, hipStream_t st);
+                   uint32_t n_spaces, void *bbox_parts, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
 
 // Combined pass over the new frame: blocks of TILE_A consecutive entries
@@ -241,13 +240,6 @@ inline uint32_t combined_blocks(uint32_t n) { return (n + TILE_A - 1) / TILE_A; 
 // entities per k_combined tile (= threads per workgroup; the special pass keeps TILE_A)
 constexpr uint32_t COMBINED_TILE = GWAOI_CT;
 __host__ __device__ inline uint32_t combined_tiles(uint32_t n) { return (n + COMBINED_TILE - 1) / COMBINED_TILE; }
-#ifndef GWAOI_XCD_BALANCE
-#define GWAOI_XCD_BALANCE 0  // 1: the XCDs' tile ranges split by work, not by count (k_combined's grid: 8 x stride)
-#endif
-// tiles one XCD's range may hold when the ranges are split by work (tile_order lists; blocks past a
-// list's end exit at once)
-__host__ __device__ inline uint32_t xcd_stride(uint32_t nb) { return (nb + 7) / 8 + (nb + 15) / 16 + 1; }
-constexpr uint32_t TO_HDR = 10;  // tile_order: nb, stride, 8 list lengths, then the lists
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
                      uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,

@@ -1023,9 +1023,6 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 // without a store per cell.  shift[c]: SHIFT_CHANGED for a cell with arrivals or departures, else
 // how far its run moved (new start - previous start): k_arrive places such a cell's stayers itself.
 constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
-#ifndef GWAOI_STAYER
-#define GWAOI_STAYER 1  // 0: every cell through k_cell_merge, counts zeroed by the scan (round-3 form, A/B)
-#endif
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
@@ -1043,9 +1040,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
     for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
-#if !GWAOI_STAYER
-        if (base + j < n) const_cast<unsigned long long *>(in)[base + j] = 0ull;
-#endif
     }
     __syncthreads();
     unsigned long long v[S64_I];
@@ -1087,7 +1081,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
             const uint32_t arr = (uint32_t)e & ~SHIFT_CHANGED, d = arr - (uint32_t)(e >> 32);
             lo[base + j] = p_cs[base + j] + d;
             hi[base + j] = arr;
-            shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) || !GWAOI_STAYER ? SHIFT_CHANGED : d;
+            shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
         }
     }
 }
@@ -1114,13 +1108,9 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
         }
         return;
     }
-#if GWAOI_STAYER
     if (old != sentinel) cnt64[old] = 0ull;
     if (key == sentinel) return;
     cnt64[key] = 0ull;
-#else
-    if (key == sentinel) return;
-#endif
     arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
 }
 
@@ -1184,7 +1174,6 @@ __device__ __forceinline__ int f2o(float f) {
     int i = __float_as_int(f);
     return i ^ ((i >> 31) & 0x7FFFFFFF);
 }
-[[maybe_unused]] __device__ __forceinline__ float o2f(int i) { return __int_as_float(i ^ ((i >> 31) & 0x7FFFFFFF)); }  // f2o's inverse
 
 __device__ __forceinline__ void bbox_flush(int4 *bbox, uint32_t ns, uint32_t sp, const int (&v)[4]) {
     if (sp >= ns) return;
@@ -1257,9 +1246,6 @@ __device__ __forceinline__ void bbox_block(uint32_t cur, const int (&own)[4], in
     if (!s_uni && cur != SP_DEAD) bbox_flush(bbox, ns, cur, own);  // mixed spaces: every run flushes
 }
 
-#ifndef GWAOI_CELL_BOUNDS
-#define GWAOI_CELL_BOUNDS 1  // k_gather folds per-cell x bounds; k_combined trims the X' rows' end cells by them
-#endif
 
 // --------------------------------------------------------------- gather ------
 
@@ -1276,32 +1262,6 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
 // frame is sorted by cell, so a cell's entries are one run: a segmented fold inside the wave,
 // then the run's first lane writes.  A run that crosses a wave boundary gets (-inf, +inf) from the
 // wave holding its first entry (no trim); an empty cell keeps a stale pair, which trims nothing.
-#if GWAOI_CELL_BOUNDS
-__device__ __forceinline__ void cell_bounds(uint32_t k, uint32_t n_new, const uint32_t *__restrict__ keys,
-                                            uint32_t sentinel, int vlo, int vhi, float2 *cbx) {
-    const uint32_t l = lane();
-    const uint32_t key = k < n_new ? keys[k] : sentinel;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {  // lane l: fold over [l, l + 2o) of its run
-        const uint32_t ko = (uint32_t)__shfl_down((int)key, o);
-        const int lo2 = __shfl_down(vlo, o), hi2 = __shfl_down(vhi, o);
-        if (l + (uint32_t)o < WAVE && ko == key) {
-            vlo = min(vlo, lo2);
-            vhi = max(vhi, hi2);
-        }
-    }
-    const uint32_t kprev = (uint32_t)__shfl_up((int)key, 1);
-    const bool head = l ? kprev != key : (k == 0 || k >= n_new || keys[k - 1] != key);  // first entry of its run
-    // the wave's last run continues past the wave?
-    const bool cont_last = l == WAVE - 1 && k + 1 < n_new && keys[k + 1] == key;
-    const bool cont = __ballot(cont_last) != 0ull;
-    const uint32_t klast = (uint32_t)__builtin_amdgcn_readlane((int)key, WAVE - 1);
-    if (head && k < n_new && key < sentinel) {
-        cbx[key] = cont && key == klast ? make_float2(-INFINITY, INFINITY)
-                                        : make_float2(o2f(vlo), o2f(vhi));
-    }
-}
-#endif
 
 // One thread per new-frame entry; the block also folds its entries' bbox
 // (level 1 of the per-space bounding box, k_finish folds level 2).
@@ -1311,18 +1271,13 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
                          SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
                          unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
-                         uint32_t n_spaces, BBoxPart *parts, float2 *cbx) {
+                         uint32_t n_spaces, BBoxPart *parts) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0 && n_new < n_total && sorted_keys[n_new] != sentinel) atomicOr(&sc->err, ERR_COUNT_MISMATCH);
     uint32_t cur = SP_DEAD;
     int bv[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
     if (k < n_new) gather_one(k, perm, n_prev, n_new, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand, grid, seq_base,
                               info, sorted_keys, sentinel, n_total, sc, f_key, cur, bv);
-#if GWAOI_CELL_BOUNDS
-    cell_bounds(k, n_new, sorted_keys, sentinel, bv[0], bv[2], cbx);
-#else
-    (void)cbx;
-#endif
     bbox_block(cur, bv, bbox, n_spaces, &parts[blockIdx.x]);
 }
 
@@ -2179,26 +2134,6 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
     const uint32_t gx = C.g.gx;
     const uint32_t xb = C.g.base + (uint32_t)xr0 * gx + (uint32_t)xc0, xs = (uint32_t)(xc1 - xc0) + 1u;
     const uint32_t zb = C.g.base + (uint32_t)zr0 * gx + (uint32_t)zc0, zs = (uint32_t)(zc1 - zc0) + 1u;
-#if GWAOI_CELL_BOUNDS
-    // an X' row's end cells whose entries all lie left of the band (max x < x + lo - M) or past its
-    // outer bound (min x > x + hi + M: dropped by the unchanged-relation test) are not swept
-    const float xl = A.x + C.lo - C.M, xh = A.x + C.hi + C.M;
-    auto range = [&](uint32_t q, uint32_t &b, uint32_t &l) {
-        b = l = 0;
-        if (q < nx) {
-            const uint32_t rb = xb + q * gx;
-            const uint32_t c0 = rb + (F.cbx[rb].y < xl ? 1u : 0u);
-            const uint32_t c1 = rb + xs - 1u;
-            const uint32_t ce = c1 + (c1 >= c0 && F.cbx[c1].x > xh ? 0u : 1u);  // one past the last swept cell
-            b = cs[c0];
-            l = cs[ce] - b;
-        } else if (q < nr) {
-            const uint32_t rb = zb + (q - nx) * gx;
-            b = cs[rb];
-            l = cs[rb + zs] - b;
-        }
-    };
-#else
     auto range = [&](uint32_t q, uint32_t &b, uint32_t &l) {
         b = l = 0;
         if (q < nr) {
@@ -2207,7 +2142,6 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
             l = cs[rb + (q < nx ? xs : zs)] - b;
         }
     };
-#endif
     uint32_t jb[P], ln[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) range((uint32_t)q, jb[q], ln[q]);
@@ -2297,24 +2231,8 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 #endif
     // Tiles run heaviest first within each XCD's range when the previous flush left an order for
     // this tile count (k_tile_order); any order gives the same events.
-#if GWAOI_XCD_BALANCE
-    // XCD x's k-th block runs the k-th tile of x's list; the lists split the tiles by work (k_finish)
-    uint32_t t;
-    {
-        const uint32_t nb = combined_tiles(F.n), x = blockIdx.x % N_XCD, k = blockIdx.x / N_XCD;
-        if (tile_order && tile_order[0] == nb) {
-            if (k >= tile_order[2 + x]) return;
-            t = tile_order[TO_HDR + x * xcd_stride(nb) + k];
-        } else {
-            const uint32_t q = nb / N_XCD, r = nb % N_XCD;
-            if (k >= q + (x < r ? 1u : 0u)) return;
-            t = x * q + min(x, r) + k;
-        }
-    }
-#else
     uint32_t t = xcd_block(blockIdx.x, gridDim.x);
     if (tile_order && tile_order[0] == gridDim.x) t = tile_order[1 + t];
-#endif
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
     const uint32_t e0 = t * CT;
@@ -2512,7 +2430,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 // word tagged with the launch (so nothing is zeroed per flush).  Block R
 // folds the bbox parts and writes the scalars of TickOut.
 #ifndef GWAOI_ORDER_GROUP
-#define GWAOI_ORDER_GROUP 1  // tiles ordered heaviest first in groups of this many neighbours (1: each tile)
+#define GWAOI_ORDER_GROUP 8  // tiles ordered heaviest first in groups of this many neighbours (1: each tile)
 #endif
 #ifndef GWAOI_FT
 #define GWAOI_FT 16  // measured: 16 -> 15.6 us, 32 -> 19.0, 64 -> 25.3 (cfg3)
@@ -2527,65 +2445,9 @@ static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 constexpr int TO_NB = 64;
 __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
     __shared__ uint32_t hist[TO_NB];
-#if GWAOI_XCD_BALANCE
-    // The XCD ranges split the tiles by work: range x starts at the first tile whose work prefix
-    // reaches x/8 of the total, kept within xcd_stride(nb) tiles per range (every tile in one range).
-    __shared__ unsigned long long part[256];
-    __shared__ uint32_t bnd[N_XCD + 1];
-    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x, c0 = min(threadIdx.x * per, nb), c1 = min(c0 + per, nb);
-    unsigned long long my = 0;
-    for (uint32_t i = c0; i < c1; ++i) my += tile_work[i];
-    part[threadIdx.x] = my;
-    __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive prefix of the 256 chunk sums
-        unsigned long long acc = 0;
-        for (uint32_t i = 0; i < blockDim.x; ++i) {
-            const unsigned long long v = part[i];
-            part[i] = acc;
-            acc += v;
-        }
-        bnd[0] = 0;
-        bnd[N_XCD] = nb;
-        for (uint32_t y = 1; y < N_XCD; ++y) bnd[y] = 0xFFFFFFFFu;
-        hist[0] = (uint32_t)(acc >> 32);  // the total work, passed through LDS (hist is cleared below)
-        hist[1] = (uint32_t)acc;
-    }
-    __syncthreads();
-    const unsigned long long W = ((unsigned long long)hist[0] << 32) | hist[1];
-    {
-        unsigned long long pre = part[threadIdx.x];
-        for (uint32_t i = c0; i < c1; ++i) {  // the chunk holding target y/8 finds the tile
-            const unsigned long long nxt = pre + tile_work[i];
-            for (uint32_t y = 1; y < N_XCD; ++y) {
-                const unsigned long long tgt = W * y / N_XCD;
-                if (pre < tgt && nxt >= tgt) atomicMin(&bnd[y], i + 1);
-            }
-            pre = nxt;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t S = xcd_stride(nb);
-        for (uint32_t y = 1; y < N_XCD; ++y) {
-            uint32_t v = bnd[y] == 0xFFFFFFFFu ? bnd[y - 1] : bnd[y];
-            const uint32_t room = (N_XCD - y) * S;  // the ranges after y must hold the rest
-            v = max(v, bnd[y - 1]);
-            if (nb > room) v = max(v, nb - room);
-            v = min(v, bnd[y - 1] + S);
-            v = min(v, nb);
-            bnd[y] = v;
-        }
-    }
-    __syncthreads();
-    const uint32_t lo = bnd[x], hi = bnd[x + 1];
-    uint32_t *dst = tile_order + TO_HDR + x * xcd_stride(nb);
-    if (threadIdx.x == 0) tile_order[2 + x] = hi - lo;
-    __syncthreads();
-#else
     const uint32_t q = nb / N_XCD, r = nb % N_XCD;
     const uint32_t lo = x * q + min(x, r), hi = lo + q + (x < r ? 1u : 0u);
     uint32_t *dst = tile_order + 1;
-#endif
     if (threadIdx.x < TO_NB) hist[threadIdx.x] = 0;
     __syncthreads();
     auto cls = [&](uint32_t v) {  // descending: class 0 = heaviest
@@ -2622,27 +2484,15 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
     for (uint32_t g = threadIdx.x; g < ng; g += blockDim.x) {
         const uint32_t slot = atomicAdd(&hist[cls(gwork(g))], 1u);
         for (uint32_t k = 0; k < OG; ++k) {
-#if GWAOI_XCD_BALANCE
-            dst[slot * OG + k] = lo + g * OG + k;
-#else
             dst[lo + slot * OG + k] = lo + g * OG + k;
-#endif
         }
     }
     for (uint32_t i = lo + ng * OG + threadIdx.x; i < hi; i += blockDim.x) {
-#if GWAOI_XCD_BALANCE
-        dst[i - lo] = i;
-#else
         dst[i] = i;
-#endif
     }
 #else
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-#if GWAOI_XCD_BALANCE
-        dst[atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
-#else
         dst[lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
-#endif
 #endif
     if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
 }
@@ -3095,11 +2945,11 @@ void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const 
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                    const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
-                   uint32_t n_spaces, void *bbox_parts, float2 *cbx, hipStream_t st) {
+                   uint32_t n_spaces, void *bbox_parts, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
     k_gather<<<cdiv(nt, 256), 256, 0, st>>>(perm, n_new, n_prev, s_rec, s_ss, p_rec, p_ss, f_rec, f_ss, o_rec, cand,
                                             grid, seq_base, info, sorted_keys, sentinel, n_total, sc, f_key, bbox,
-                                            n_spaces, reinterpret_cast<BBoxPart *>(bbox_parts), cbx);
+                                            n_spaces, reinterpret_cast<BBoxPart *>(bbox_parts));
 }
 
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st) {
@@ -3123,7 +2973,7 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and
     // end: no marker packets between kernels when the stage is timed
-    hipExtLaunchKernelGGL(k_combined, dim3(GWAOI_XCD_BALANCE ? N_XCD * xcd_stride(combined_tiles(F.n)) : combined_tiles(F.n)),
+    hipExtLaunchKernelGGL(k_combined, dim3(combined_tiles(F.n)),
                           dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
                           (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,

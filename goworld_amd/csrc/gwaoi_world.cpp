@@ -45,7 +45,6 @@ struct DevFrame {
     gw::SlotSp *ss = nullptr;
     uint32_t *key = nullptr;  // cell key of every entry (the next flush's "previous cell")
     uint32_t *cell_start = nullptr;
-    float2 *cbx = nullptr;  // per-cell x bounds (cell_cap entries)
     size_t cell_cap = 0;  // entries allocated in cell_start
     SpaceGrid *grid = nullptr;
     std::vector<SpaceGrid> hgrid;  // host mirror of `grid` (upload only on change)
@@ -538,10 +537,7 @@ int ensure_cells(gwaoi_world *w, DevFrame &f, size_t cells) {
     size_t cap = std::max(need + need / 4, (size_t)1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(f.cell_start);
-    dfree(f.cbx);
-    f.cbx = nullptr;
     int rc = dalloc(w, &f.cell_start, cap);
-    if (!rc) rc = dalloc(w, &f.cbx, cap);
     if (rc) {
         f.cell_cap = 0;
         return rc;
@@ -735,7 +731,6 @@ gw::FrameView view_of(const DevFrame &f) {
     v.rec = f.rec;
     v.ss = f.ss;
     v.cell_start = f.cell_start;
-    v.cbx = f.cbx;
     v.grid = f.grid;
     v.n = f.n;
     v.total_cells = f.total_cells;
@@ -1010,7 +1005,7 @@ int tick_launch(gwaoi_world *w) {
     stage_begin(w, S, ST_GATHER);
     gw::launch_gather(perm, n_new, n_prev, S.srec, s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, S.orec, S.cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
-                      total_cells, n_total, S.sc, Fn.key, dev_bbox(S), w->n_space_ids, S.bbox_parts, Fn.cbx, st);
+                      total_cells, n_total, S.sc, Fn.key, dev_bbox(S), w->n_space_ids, S.bbox_parts, st);
     stage_end(w, S, ST_GATHER);
 
     // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
@@ -1264,7 +1259,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->sync) gw::sync_destroy(w->sync);
     w->sync = nullptr;
     for (DevFrame &f : w->fr) {
-        dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.cbx); dfree(f.grid);
+        dfree(f.rec); dfree(f.ss); dfree(f.key); dfree(f.cell_start); dfree(f.grid);
     }
     for (FlushSet &S : w->fs) {
         dfree(S.srec); dfree(S.sss); dfree(S.orec); dfree(S.cand); dfree(S.sc); dfree(S.events);
@@ -1393,7 +1388,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / gw::COMBINED_TILE + 2)) ||
-        (rc = dalloc(w, &w->tile_order, gw::TO_HDR + 8 * (size_t)gw::xcd_stride(gw::combined_tiles((uint32_t)N)) + 8)) || (rc = dalloc(w, &w->ework, N)) ||
+        (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 8)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess ||  // no order yet
