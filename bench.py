@@ -431,9 +431,10 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
       (gwaoi_pinned_alloc; a cgo adapter fills it as the sync packets arrive over the game tick, so the
       batch is in host memory when the tick starts, as the bench's device leg has it in HBM), and
       gwaoi_moved_batch_pinned queues one H2D of it on a copy stream; the moves are checked on the device.
-      Serial: batch + gwaoi_tick.  Pipelined: the batch of t+1 is queued while flush t runs, then
-      gwaoi_tick_end_begin queues flush t+1 before t's summary is read and copies t's events out beside
-      it.  Latency = the batch call -> its events in host memory.
+      Serial: batch + gwaoi_tick.  Pipelined: the batch of t+1 is queued while flush t runs (its H2D beside
+      the copy-out of t-1's events), gwaoi_events_host takes t-1's events, then gwaoi_tick_end_begin_async
+      queues flush t+1 before t's summary is read and starts t's copy-out without waiting for it.
+      Latency = the batch call -> its events in host memory.
     stage_commit: the caller writing the moves into the library's pinned staging (gwaoi_moved_batch_stage /
       _commit, 8 numpy threads here): the fill cost a caller pays per tick, and those ticks' latency.
     staged_copy_api (gwaoi_moved_batch: validation + copy into pinned staging on 8 library threads): the
@@ -478,11 +479,18 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
     for k in range(len(pb)):
         if k + 1 < len(pb):
             issue.append(time.perf_counter())
-            w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])  # batch t+1 queued while flush t runs
-            w.tick_end_begin(copy=False)
+            # batch t+1's H2D is queued while flush t runs and t-1's events are still being copied out
+            w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])
+            if k:
+                w.events_host(copy=False)  # tick t-1's events in host memory
+                p_lat.append(time.perf_counter() - issue[k - 1])
+            w.tick_end_begin_async()  # finish t, queue t+1, start t's copy-out (no wait for it)
         else:
+            if k:
+                w.events_host(copy=False)
+                p_lat.append(time.perf_counter() - issue[k - 1])
             w.tick_end(copy=False)
-        p_lat.append(time.perf_counter() - issue[k])
+            p_lat.append(time.perf_counter() - issue[k])
     p_el = time.perf_counter() - p0
     gc.enable()
     torch.cuda.synchronize()
@@ -539,10 +547,11 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
                                 "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(g_lat)},
             "note": "pinned: each tick's moves in a caller-owned pinned buffer (gwaoi_pinned_alloc, filled before "
                     "timing as a game server fills it while packets arrive), one H2D per tick, checked on the "
-                    "device; pipelined = batch t+1 queued while flush t runs, gwaoi_tick_end_begin (flush t+1 "
-                    "queued before t's summary, t's events copied out beside it); tick latency = batch call -> "
-                    "events in pinned host memory.  stage_commit = the caller writing the moves into the "
-                    "library's staging per tick (its fill cost); staged_copy_api = gwaoi_moved_batch"}
+                    "device; pipelined = batch t+1 queued while flush t runs (its H2D beside t-1's event "
+                    "copy-out), gwaoi_events_host(t-1), gwaoi_tick_end_begin_async (flush t+1 queued before t's "
+                    "summary, t's copy-out started); tick latency = batch call -> events in pinned host memory.  "
+                    "stage_commit = the caller writing the moves into the library's staging per tick (its fill "
+                    "cost); staged_copy_api = gwaoi_moved_batch"}
 
 
 def cfg4_leg(args, ws, rank, device, dist, red_dev):

@@ -2429,9 +2429,6 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 // publishes its aggregate, then its inclusive prefix, in a 64-bit status
 // word tagged with the launch (so nothing is zeroed per flush).  Block R
 // folds the bbox parts and writes the scalars of TickOut.
-#ifndef GWAOI_ORDER_GROUP
-#define GWAOI_ORDER_GROUP 8  // tiles ordered heaviest first in groups of this many neighbours (1: each tile)
-#endif
 #ifndef GWAOI_FT
 #define GWAOI_FT 16  // measured: 16 -> 15.6 us, 32 -> 19.0, 64 -> 25.3 (cfg3)
 #endif
@@ -2454,20 +2451,7 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
         const int c = (int)(8.0f * __log2f((float)v + 1.0f)) - 40;
         return (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
     };
-#if GWAOI_ORDER_GROUP > 1
-    // groups of GWAOI_ORDER_GROUP neighbouring tiles ordered by their summed work, each group's
-    // tiles kept together (they share candidate rows in L2 when they run side by side)
-    constexpr uint32_t OG = GWAOI_ORDER_GROUP;
-    const uint32_t ng = (hi - lo) / OG;  // whole groups; the range's last hi - lo - ng * OG tiles run last
-    auto gwork = [&](uint32_t g) {
-        uint32_t v = 0;
-        for (uint32_t i = lo + g * OG; i < lo + g * OG + OG; ++i) v += tile_work[i];
-        return v / OG;
-    };
-    for (uint32_t g = threadIdx.x; g < ng; g += blockDim.x) atomicAdd(&hist[cls(gwork(g))], 1u);
-#else
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(tile_work[i])], 1u);
-#endif
     __syncthreads();
     if (threadIdx.x < WAVE) {  // exclusive scan of the 64 class counts by one wave
         const uint32_t v = hist[threadIdx.x];
@@ -2480,20 +2464,8 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
         hist[threadIdx.x] = incl - v;
     }
     __syncthreads();
-#if GWAOI_ORDER_GROUP > 1
-    for (uint32_t g = threadIdx.x; g < ng; g += blockDim.x) {
-        const uint32_t slot = atomicAdd(&hist[cls(gwork(g))], 1u);
-        for (uint32_t k = 0; k < OG; ++k) {
-            dst[lo + slot * OG + k] = lo + g * OG + k;
-        }
-    }
-    for (uint32_t i = lo + ng * OG + threadIdx.x; i < hi; i += blockDim.x) {
-        dst[i] = i;
-    }
-#else
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
         dst[lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
-#endif
     if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
 }
 

@@ -292,6 +292,7 @@ struct gwaoi_world {
     // event copies to the host beside the next flush (gwaoi_tick_end_begin)
     hipStream_t out_st = nullptr;
     hipEvent_t out_ev = nullptr;
+    bool out_pending = false;  // a copy-out of events queued by gwaoi_tick_end_begin_async, not yet waited for
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
@@ -481,7 +482,16 @@ int ensure_tile_entries(gwaoi_world *w, size_t entries) {
     return GWAOI_OK;
 }
 
+int wait_done(gwaoi_world *w, hipEvent_t ev);
+// Waits for the copy-out gwaoi_tick_end_begin_async queued (before h_events is rewritten or freed).
+int finish_out(gwaoi_world *w) {
+    if (!w->out_pending) return GWAOI_OK;
+    w->out_pending = false;
+    return wait_done(w, w->out_ev);
+}
+
 int ensure_host_events(gwaoi_world *w, uint64_t pairs) {
+    if (int rc = finish_out(w)) return rc;
     if (pairs <= w->h_ev_cap) return GWAOI_OK;
     uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, 1024);
     if (w->h_events) (void)hipHostFree(w->h_events);
@@ -843,6 +853,9 @@ int tick_launch(gwaoi_world *w) {
     const uint32_t n_new = w->n_alive;
 
     (void)hipGetLastError();  // the launch check below must see this flush's launches only
+    // a copy-out still reading a flush set's events (gwaoi_tick_end_begin_async) ends before this
+    // flush writes into a set
+    if (w->out_pending) HIP_TRY(hipStreamWaitEvent(st, w->out_ev, 0));
     // grid for this flush
     uint32_t total_cells = 0, total_rows = 0;
     choose_grids(w, total_cells, total_rows);
@@ -1256,6 +1269,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     if (w->copy_st) (void)hipStreamSynchronize(w->copy_st);
+    if (w->out_st) (void)hipStreamSynchronize(w->out_st);
     if (w->sync) gw::sync_destroy(w->sync);
     w->sync = nullptr;
     for (DevFrame &f : w->fr) {
@@ -2237,6 +2251,48 @@ int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out) {
     out->enter = w->h_events;
     out->leave = w->h_events + 2 * w->last_n_enter;
     return rc;
+    });
+}
+
+int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
+    if (int rw = finish_out(w)) return poison(w, rw);
+    const uint64_t regrows = w->dbg.event_regrows;
+    bool committed = false;
+    const int rc = end_begin(w, &committed);
+    if (!committed) return rc;
+    const uint64_t tot = w->last_n_enter + w->last_n_leave;
+    if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
+    FlushSet &S = w->fs[w->last_set];
+    if (tot) {  // queued as in gwaoi_tick_end_begin; waited for by gwaoi_events_host (or the next copy-out)
+        HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
+        HIP_TRY(hipMemcpyAsync(w->h_events, S.events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost, w->out_st));
+        HIP_TRY(hipEventRecord(w->out_ev, w->out_st));
+        w->out_pending = true;
+    }
+    if (n_enter) *n_enter = w->last_n_enter;
+    if (n_leave) *n_leave = w->last_n_leave;
+    return rc;
+    });
+}
+
+int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out) return GWAOI_EINVAL;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    GW_LIVE(w);
+    if (int rw = finish_out(w)) return poison(w, rw);
+    out->n_enter = w->last_n_enter;
+    out->n_leave = w->last_n_leave;
+    out->enter = w->h_events;
+    out->leave = w->h_events ? w->h_events + 2 * w->last_n_enter : nullptr;
+    return GWAOI_OK;
     });
 }
 

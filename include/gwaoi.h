@@ -226,6 +226,16 @@ int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_l
  * gwaoi_tick_end; valid until the next call that returns events).  The copy
  * runs on its own stream, beside the next flush. */
 int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out);
+/* The same without waiting for the copy: the finished flush's events are on
+ * their way to host memory when this returns (counts in *n_enter / *n_leave),
+ * and gwaoi_events_host waits for them.  The caller queues the next tick's
+ * batch (e.g. gwaoi_moved_batch_pinned) in between, so that batch's H2D copy
+ * and this D2H copy run at the same time.  Any later call that returns events
+ * or starts another copy-out waits for this one first. */
+int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
+/* The events of the last gwaoi_tick_end_begin_async, in host memory (waits
+ * for their copy); valid until the next call that returns events. */
+int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out);
 
 /* ---- zero-copy host move batches ---------------------------------------------
  * The per-tick position batch written straight into the world's pinned staging

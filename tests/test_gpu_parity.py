@@ -1237,8 +1237,9 @@ def test_device_enter_of_live_slot_poisons_gpu():
 def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
     """gwaoi_moved_batch_stage / _commit (moves written straight into pinned staging, checked
     on the device) == gwaoi_moved_batch, serial and pipelined with gwaoi_tick_end_begin (the
-    event copy beside the next flush); a partial commit, a batch after an Enter in the same
-    flush (host-checked, space column), and a dead slot dropped and reported by the flush."""
+    event copy beside the next flush) and with gwaoi_tick_end_begin_async + gwaoi_events_host;
+    a partial commit, a batch after an Enter in the same flush (host-checked, space column),
+    and a dead slot dropped and reported by the flush."""
     wl = make_workload("cfg3", n=40000)
     slots, x0, z0, _ = wl.initial()
     with World(wl.n) as A, World(wl.n) as B:
@@ -1305,6 +1306,36 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb), err_msg=f"pipelined tick {t}")
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"pipelined tick {t}")
         assert A.debug_counters()["speculative_launches"] >= 3
+        # pipelined with the copy-out left running (gwaoi_tick_end_begin_async): batch t+1 queued from
+        # the caller's pinned buffer, tick t-1's events taken (gwaoi_events_host), then t finished
+        host = [wl.tick(9 + t) for t in range(5)]
+        ptrs, got = [], []
+
+        def put(b):
+            ptr, views = A.pinned_batch(b[0].size)
+            views[0][:], views[1][:], views[2][:] = b
+            ptrs.append(ptr)
+            A.moved_batch_pinned(views, b[0].size)
+
+        put(host[0])
+        A.tick_begin()
+        for t in range(5):
+            if t + 1 < 5:
+                put(host[t + 1])
+                if t:
+                    got.append(A.events_host())
+                counts = A.tick_end_begin_async()
+            else:
+                got.append(A.events_host())
+                got.append(A.tick_end())
+        assert counts == (len(got[3][0]), len(got[3][1]))
+        for t in range(5):
+            B.moved_batch(*host[t])
+            eb, lb = B.tick()
+            np.testing.assert_array_equal(pair_keys(got[t][0]), pair_keys(eb), err_msg=f"async tick {t}")
+            np.testing.assert_array_equal(pair_keys(got[t][1]), pair_keys(lb), err_msg=f"async tick {t}")
+        for p in ptrs:
+            A.free_pinned_batch(p)
         # a move of a slot that is not live: dropped on the device, reported by the flush
         A.leave(5)
         A.tick()
