@@ -261,6 +261,8 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 // words, tag: a value not used by an earlier launch on the same lb, != 0 mod
 // 2^30), the scalars of TickOut, and the per-space bbox fold (k_gather's parts).
 size_t finish_lb_elems(size_t n_entries);
+// bytes (a multiple of 8) from device memory to pinned host memory, written by a few workgroups
+void launch_copy_out(const void *src, void *dst, size_t bytes, hipStream_t st);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,

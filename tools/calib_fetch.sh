@@ -7,6 +7,6 @@ OUT=$R/gpurun_out/calib_fetch
 mkdir -p $OUT
 cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $R/goworld_amd/lib/calib_fetch > $OUT/calib.json 2> $OUT/fetch.err
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/rdreq -o run -- $R/goworld_amd/lib/calib_fetch > /dev/null 2> $OUT/rdreq.err
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o run -- $R/goworld_amd/lib/calib_fetch > /dev/null 2> $OUT/trace.err
-rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 ls -R $OUT | head

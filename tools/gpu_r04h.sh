@@ -1,6 +1,9 @@
 set -o pipefail
-# round-4: cell size D/3 against D/4 on the cfg3 tick (kernel traces), then the profile + FETCH calibration
+# round-4: async copy-out parity + the default bench line, cell size D/3 against D/4 (kernel traces),
+# then the rocprofv3 profile of the cfg3 tick and the FETCH_SIZE calibration
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $R/gpurun_out
+bash tools/gpu_run.sh r04h "zero_copy or speculative or device_enter" || exit 1
 export TMPDIR=/tmp
 ARGS="--steps 20 --warmup 3 --no-cpu-baseline --host-io-steps 0 --sync-steps 0 --cfg4-steps 0 --cfg5-steps 0 --host-tick-steps 0 --wire-steps 0"
 for c in 4 3; do

@@ -78,6 +78,8 @@ def main():
     tc = pmc(d, "pmc_tcp")
     fe = pmc(d, "pmc_fetch")
     wr = pmc(d, "pmc_write")
+    rq = pmc(d, "pmc_rdreq")  # L2 -> fabric read requests by size (exact read bytes, no FETCH_SIZE factor)
+    dr = pmc(d, "pmc_dram")   # ... of them, the ones that went to DRAM (the rest hit the Infinity Cache)
     kern = {}
     for r in ks:
         k = r["kernel"]
@@ -96,9 +98,17 @@ def main():
             e.setdefault("derived", {})["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
         f = fe.get(k, {}).get("FETCH_SIZE")
         w = wr.get(k, {}).get("WRITE_SIZE")
+        r = rq.get(k, {})
+        e["pmc"].update(r)
+        e["pmc"].update(dr.get(k, {}))
         if f is not None:
             e["pmc"]["FETCH_SIZE_KiB"] = f
             e["hbm_read_bytes"] = 2.0 * f * 1024.0
+        if all(c in r for c in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
+            # requests by size: the read bytes without FETCH_SIZE's factor (which holds for 128-B requests only)
+            e["read_bytes_by_request_size"] = (32.0 * r["TCC_EA0_RDREQ_32B_sum"] + 64.0 * r["TCC_EA0_RDREQ_64B_sum"] +
+                                               128.0 * r["TCC_EA0_RDREQ_128B_sum"])
+            e["hbm_read_bytes"] = e["read_bytes_by_request_size"]
         if w is not None:
             e["pmc"]["WRITE_SIZE_KiB"] = w
             e["hbm_write_bytes"] = w * 1024.0
@@ -111,7 +121,8 @@ def main():
     lines = [f"# rocprofv3 summary ({os.path.basename(dst)})", "",
              "Command: `tools/profile.sh` = `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 8 --warmup 2`, "
              "then separate `--pmc` passes (SQ block with SQ_WAIT_ANY / SQ_ACTIVE_INST_ANY, TCP/TCC hit counters, FETCH_SIZE, WRITE_SIZE). "
-             "PMC values are medians over steady-state dispatches; HBM read bytes = 2 x FETCH_SIZE (gfx950 correction).", ""]
+             "PMC values are medians over steady-state dispatches; read bytes = 32/64/128 B x TCC_EA0_RDREQ_{32B,64B,128B} "
+             "when that pass ran (else 2 x FETCH_SIZE, the gfx950 factor for 128-B streaming requests).", ""]
     if bench:
         lines += [f"bench under trace: ms_per_step {bench.get('ms_per_step'):.4f}, value {bench.get('value'):.4g} "
                   f"{bench.get('unit')}", ""]
@@ -140,7 +151,8 @@ def main():
               "kernel": "k_combined", "source": os.path.basename(dst),
               "hbm_read_bytes_per_launch": kc["hbm_read_bytes"], "hbm_write_bytes_per_launch": kc["hbm_write_bytes"],
               "hbm_bytes_per_launch": kc["hbm_bytes"], "steady_median_us": kc.get("steady_median_us"),
-              "note": "median over steady-state dispatches; read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE"}
+              "note": "median over steady-state dispatches; read = L2->fabric read requests x their size "
+                      "(TCC_EA0_RDREQ_32B/64B/128B; 2 x FETCH_SIZE without that pass), write = WRITE_SIZE"}
         rnd = os.path.basename(dst).split("_")[0]  # profiles/<round>_pmc_k_combined.json
         with open(os.path.join(os.path.dirname(dst), f"{rnd}_pmc_k_combined.json"), "w") as fh:
             json.dump(pm, fh, indent=1)
