@@ -199,6 +199,8 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // look-back status words (zeroed once when allocated); tag: fresh per launch;
 // arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
 size_t incr_sort_tmp_elems(size_t cells);
+// cnt64 words for `cells` counted cells: the cells, then one total per scan tile (GWAOI_SCAN_BT)
+size_t cnt64_elems(size_t cells);
 // true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
 bool scan_rezeroes_counts();
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,

@@ -533,11 +533,11 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     w->cnt64_cap = 0;
     int rc;
     // arr_pos: the arrival cursors, then the per-cell stayer shifts (incremental_sort)
-    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
+    if ((rc = dalloc(w, &w->cnt64, gw::cnt64_elems(cap))) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
-    HIP_TRY(hipMemsetAsync(w->cnt64, 0, cap * sizeof(unsigned long long), w->stream));  // then kept zero by the sort
+    HIP_TRY(hipMemsetAsync(w->cnt64, 0, gw::cnt64_elems(cap) * sizeof(unsigned long long), w->stream));  // then kept zero by the sort
     w->cnt64_cap = cap;
     return GWAOI_OK;
 }
