@@ -443,7 +443,7 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
     import torch
     from goworld_amd.shard import reduce_over_ranks
     n_ser, n_pip = hio, hio + 1
-    zc, rest = host_batches[:3 + n_ser + n_pip], host_batches[3 + n_ser + n_pip:]
+    zc, rest = host_batches[:3 + n_ser + 2 * n_pip], host_batches[3 + n_ser + 2 * n_pip:]
     # the caller's pinned batch buffers, filled before timing (untimed, like the device leg's HBM batches)
     bufs = []
     for b in zc:
@@ -470,28 +470,35 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
         s_lat.append(time.perf_counter() - a)
         h_ev += len(ent) + len(lev)
     s_el = time.perf_counter() - s0
-    pb = bufs[3 + n_ser:]
-    p_lat, issue = [], []
-    p0 = time.perf_counter()
-    issue.append(p0)
-    w.moved_batch_pinned(pb[0][1], pb[0][2])
-    w.tick_begin()
-    for k in range(len(pb)):
-        if k + 1 < len(pb):
-            issue.append(time.perf_counter())
-            # batch t+1's H2D is queued while flush t runs and t-1's events are still being copied out
-            w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])
-            if k:
-                w.events_host(copy=False)  # tick t-1's events in host memory
-                p_lat.append(time.perf_counter() - issue[k - 1])
-            w.tick_end_begin_async()  # finish t, queue t+1, start t's copy-out (no wait for it)
-        else:
-            if k:
-                w.events_host(copy=False)
-                p_lat.append(time.perf_counter() - issue[k - 1])
-            w.tick_end(copy=False)
-            p_lat.append(time.perf_counter() - issue[k])
-    p_el = time.perf_counter() - p0
+    def pipelined(pb, pairs):
+        lat, issue = [], []
+        end_begin = w.tick_end_begin_pairs_async if pairs else w.tick_end_begin_async
+        take = w.pairs_host if pairs else w.events_host
+        t0 = time.perf_counter()
+        issue.append(t0)
+        w.moved_batch_pinned(pb[0][1], pb[0][2])
+        w.tick_begin()
+        for k in range(len(pb)):
+            if k + 1 < len(pb):
+                issue.append(time.perf_counter())
+                # batch t+1's H2D is queued while flush t runs and t-1's events are still being copied out
+                w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])
+                if k:
+                    take(copy=False)  # tick t-1's events in host memory
+                    lat.append(time.perf_counter() - issue[k - 1])
+                end_begin()  # finish t, queue t+1, start t's copy-out (no wait for it)
+            else:
+                if k:
+                    take(copy=False)
+                    lat.append(time.perf_counter() - issue[k - 1])
+                w.tick_end(copy=False)
+                lat.append(time.perf_counter() - issue[k])
+        return time.perf_counter() - t0, lat
+
+    pb = bufs[3 + n_ser:3 + n_ser + n_pip]
+    d_el, d_lat = pipelined(pb, False)  # every directed event to host memory
+    pb = bufs[3 + n_ser + n_pip:]
+    p_el, p_lat = pipelined(pb, True)   # one event per mirrored pair: half the D2H bytes
     gc.enable()
     torch.cuda.synchronize()
     for ptr, _, _ in bufs:
@@ -534,10 +541,13 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
     if dist is not None:
         dist.barrier()
     p_el, (h_moves, h_evs) = reduce_over_ranks(dist, p_el, [sum(b[2] for b in pb), h_ev], red_dev)
+    d_el, _ = reduce_over_ranks(dist, d_el, [0.0], red_dev)
     pct = lambda v, q: float(np.percentile(np.array(v) * 1e3, q))
     return {"value": h_moves / p_el, "unit": "entity-moves/s", "ms_per_step": p_el / len(pb) * 1e3,
             "p50_tick_ms": pct(p_lat, 50), "p99_tick_ms": pct(p_lat, 99), "steps": len(pb),
             "ticks_ms": [round(v * 1e3, 3) for v in p_lat],
+            "directed_events_out": {"ms_per_step": d_el / n_pip * 1e3, "p50_tick_ms": pct(d_lat, 50),
+                                    "p99_tick_ms": pct(d_lat, 99), "steps": n_pip},
             "serial": {"ms_per_step": s_el / len(ser) * 1e3, "p50_tick_ms": pct(s_lat, 50),
                        "p99_tick_ms": pct(s_lat, 99), "steps": len(ser), "events_per_s": h_evs / max(s_el, 1e-9)},
             "stage_commit": {"caller_fill_ms_p50": pct(f_ms, 50), "serial_p50_tick_ms": pct(c_lat, 50),
@@ -547,11 +557,15 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
                                 "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(g_lat)},
             "note": "pinned: each tick's moves in a caller-owned pinned buffer (gwaoi_pinned_alloc, filled before "
                     "timing as a game server fills it while packets arrive), one H2D per tick, checked on the "
-                    "device; pipelined = batch t+1 queued while flush t runs (its H2D beside t-1's event "
-                    "copy-out), gwaoi_events_host(t-1), gwaoi_tick_end_begin_async (flush t+1 queued before t's "
-                    "summary, t's copy-out started); tick latency = batch call -> events in pinned host memory.  "
-                    "stage_commit = the caller writing the moves into the library's staging per tick (its fill "
-                    "cost); staged_copy_api = gwaoi_moved_batch"}
+                    "device; pipelined = batch t+1 queued while flush t runs, the events of t-1 taken, "
+                    "gwaoi_tick_end_begin_pairs_async (flush t+1 queued before t's summary, t's copy-out started: "
+                    "one event per mirrored pair (a,b)/(b,a), the pair list gwaoi_pairs_host returns, from which "
+                    "the callbacks of both entities follow); directed_events_out = the same ticks copying every "
+                    "directed event (gwaoi_tick_end_begin_async + gwaoi_events_host).  Tick latency = batch call "
+                    "-> events in pinned host memory.  PCIe here carries one direction at a time "
+                    "(tools/pcie_probe.py), so a pipelined tick costs H2D + D2H.  stage_commit = the caller "
+                    "writing the moves into the library's staging per tick (its fill cost); staged_copy_api = "
+                    "gwaoi_moved_batch"}
 
 
 def cfg4_leg(args, ws, rank, device, dist, red_dev):
@@ -1015,7 +1029,7 @@ def main():
         batches.append((sl, nx, nz))
     # PCIe-inclusive leg (host memory): three untimed warmup ticks (one serial, two pipelined: they
     # allocate both pinned staging buffers) + hio serial + hio + 1 pipelined
-    host_batches = [wl.tick(ticks + t) for t in range(3 * hio + 16 if hio else 0)]
+    host_batches = [wl.tick(ticks + t) for t in range(4 * hio + 17 if hio else 0)]
     sync_steps = max(0, args.sync_steps) if ws == 1 or args.workload != "cfg4" else 0
     sync_batches = [wl.tick(ticks + len(host_batches) + t) for t in range(sync_steps + 1 if sync_steps else 0)]
     d_slots = torch.from_numpy(np.stack([b[0] for b in batches]).astype(np.int32)).to(f"cuda:{device}")
@@ -1215,9 +1229,11 @@ def main():
             "host_to_host_tick": ({k: host_io[k] for k in ("value", "unit", "ms_per_step", "p50_tick_ms", "p99_tick_ms")}
                                   | {"serial_p50_tick_ms": host_io["serial"]["p50_tick_ms"],
                                      "serial_p99_tick_ms": host_io["serial"]["p99_tick_ms"],
+                                     "directed_events_out": host_io["directed_events_out"],
                                      "note": "headline twin: BASELINE.md's tick, the host move batch (caller's "
-                                             "pinned buffer, one H2D) -> events in pinned host memory; details in "
-                                             "pcie_inclusive"} if host_io else None),
+                                             "pinned buffer, one H2D) -> events in pinned host memory (pipelined: "
+                                             "one event per mirrored pair; serial and directed_events_out: every "
+                                             "directed event); details in pcie_inclusive"} if host_io else None),
             "pcie_inclusive": host_io,
             "sync_leg": sync,
             "wire_leg": wire,

@@ -38,7 +38,7 @@ EXPORTS = [
     "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
     "gwaoi_enter_batch_device", "gwaoi_leave_batch_device", "gwaoi_tick_end_begin", "gwaoi_moved_batch_stage",
     "gwaoi_moved_batch_commit", "gwaoi_moved_batch_pinned", "gwaoi_pinned_alloc", "gwaoi_pinned_free",
-    "gwaoi_tick_end_begin_async", "gwaoi_events_host",
+    "gwaoi_tick_end_begin_async", "gwaoi_events_host", "gwaoi_tick_end_begin_pairs_async", "gwaoi_pairs_host",
 ]
 
 # every function include/gwaoi_strips.h declares
@@ -159,6 +159,8 @@ def load():
         "gwaoi_tick_end_begin": ([vp, P(Events)], C.c_int),
         "gwaoi_tick_end_begin_async": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_events_host": ([vp, P(Events)], C.c_int),
+        "gwaoi_tick_end_begin_pairs_async": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_pairs_host": ([vp, P(Events)], C.c_int),
         "gwaoi_moved_batch_stage": ([vp, sz, P(vp), P(vp), P(vp)], C.c_int),
         "gwaoi_moved_batch_commit": ([vp, sz], C.c_int),
         "gwaoi_moved_batch_pinned": ([vp, vp, vp, vp, sz], C.c_int),
@@ -423,6 +425,24 @@ class World:
                 e.counts = (ne.value, nl.value)
                 raise
         return ne.value, nl.value
+
+    def tick_end_begin_pairs_async(self):
+        """gwaoi_tick_end_begin_pairs_async: as tick_end_begin_async, one event per mirrored pair
+        copied out; returns the directed (n_enter, n_leave).  pairs_host() waits for them."""
+        ne, nl = C.c_uint64(), C.c_uint64()
+        rc = self._L.gwaoi_tick_end_begin_pairs_async(self._w, C.byref(ne), C.byref(nl))
+        if rc != 0:
+            try:
+                self._check(rc)
+            except GwaoiError as e:
+                e.counts = (ne.value, nl.value)
+                raise
+        return ne.value, nl.value
+
+    def pairs_host(self, copy: bool = True):
+        """gwaoi_pairs_host: (enter pairs, leave pairs) as (n,2) arrays; (a,b) stands for (a,b) and (b,a)."""
+        ev = Events()
+        return self._events(self._L.gwaoi_pairs_host(self._w, C.byref(ev)), ev, copy)
 
     def events_host(self, copy: bool = True):
         """gwaoi_events_host: the events of the last tick_end_begin_async in host memory."""

@@ -199,8 +199,6 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // look-back status words (zeroed once when allocated); tag: fresh per launch;
 // arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
 size_t incr_sort_tmp_elems(size_t cells);
-// cnt64 words for `cells` counted cells: the cells, then one total per scan tile (GWAOI_SCAN_BT)
-size_t cnt64_elems(size_t cells);
 // true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
 bool scan_rezeroes_counts();
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
@@ -265,6 +263,8 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 size_t finish_lb_elems(size_t n_entries);
 // bytes (a multiple of 8) from device memory to pinned host memory, written by a few workgroups
 void launch_copy_out(const void *src, void *dst, size_t bytes, hipStream_t st);
+// the first event of each mirrored pair of a flush's [enters | leaves] (n_pairs of them) into pinned host memory
+void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream_t st);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,

@@ -342,23 +342,6 @@ constexpr int SC_TILE = SC_T * SC_I;
 #endif
 constexpr int S64_I = GWAOI_S64_I;
 constexpr int S64_TILE = SC_T * S64_I;
-#ifndef GWAOI_SCAN_BT
-#define GWAOI_SCAN_BT 0  // 1: keygen also totals the counts per scan tile; the scan adds its predecessors' totals (no look-back)
-#endif
-
-// Adds v * (lanes naming block b) to bt[b] for every b the wave's lanes name (NONE: no add),
-// one atomic per distinct b: S' is in cell order, so a wave's cells mostly share one scan tile.
-[[maybe_unused]] __device__ __forceinline__ void wave_block_add(unsigned long long *bt, uint32_t b, unsigned long long v) {
-    for (;;) {
-        const unsigned long long act = __ballot(b != 0xFFFFFFFFu);
-        if (!act) return;
-        const int first = __ffsll((long long)act) - 1;
-        const uint32_t lead = (uint32_t)__builtin_amdgcn_readlane((int)b, first);
-        const unsigned long long same = __ballot(b == lead);
-        if ((int)lane() == first) atomicAdd(&bt[lead], v * (unsigned long long)__popcll(same));
-        if (b == lead) b = 0xFFFFFFFFu;
-    }
-}
 
 // INCR (the grid is the previous frame's): also count, per cell, the
 // entities (low word of cnt64) and the "arrivals" -- entities whose cell
@@ -372,7 +355,7 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
-                                                unsigned long long seq_base, uint32_t *special, uint32_t bt_off) {
+                                                unsigned long long seq_base, uint32_t *special) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     float dr = 0.0f, bm = 0.0f;
@@ -408,29 +391,13 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         // only the entities that changed cell count: an arrival in the new cell (low word), a
         // departure from the old one (high word); a cell's stayers are its previous count minus
         // its departures, which k_scan64_lb takes from the previous cell_start
-        uint32_t ba = 0xFFFFFFFFu, bd = 0xFFFFFFFFu;
         if (i < n) {
             const uint32_t old = i < n_prev ? p_key[i] : sentinel;
             if (key != old) {
-                if (key != sentinel) {
-                    atomicAdd(&cnt64[key], 1ull);
-                    ba = key / (uint32_t)S64_TILE;
-                }
-                if (old != sentinel) {
-                    atomicAdd(&cnt64[old], 1ull << 32);
-                    bd = old / (uint32_t)S64_TILE;
-                }
+                if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
+                if (old != sentinel) atomicAdd(&cnt64[old], 1ull << 32);
             }
         }
-#if GWAOI_SCAN_BT
-        // the same counts totalled per scan tile (after the cells, at cnt64 + bt_off)
-        wave_block_add(cnt64 + bt_off, ba, 1ull);
-        wave_block_add(cnt64 + bt_off, bd, 1ull << 32);
-#else
-        (void)ba;
-        (void)bd;
-        (void)bt_off;
-#endif
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1085,21 +1052,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
     }
     unsigned long long tot;
     unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot);
-#if GWAOI_SCAN_BT
-    // the tile's offset: the totals keygen kept for the tiles before it (read by every block; no chain)
-    (void)lb;
-    (void)tag;
-    __shared__ unsigned long long s_pre[SC_T / WAVE];
-    unsigned long long pre = 0;
-    for (uint32_t j = tid; j < b; j += SC_T) pre += in[n + j];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
-    if (lane() == 0) s_pre[tid / WAVE] = pre;
-    __syncthreads();
-    unsigned long long e = 0;
-#pragma unroll
-    for (int q = 0; q < SC_T / WAVE; ++q) e += s_pre[q];
-#else
     if (tid == 0) {
         const uint32_t k = b == 0 ? LB_INCL : LB_AGG;
         lb_store(lb + b, lb_word(tag, k, (uint32_t)tot));
@@ -1113,7 +1065,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
         lb_store(lb + b, lb_word(tag, LB_INCL, (uint32_t)t));
         lb_store(lb + nb + b, lb_word(tag, LB_INCL, (uint32_t)(t >> 32)));
     }
-#endif
     run += e;
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read; bit 31: c changed
@@ -1144,15 +1095,8 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
 __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
                          const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
                          unsigned long long *cnt64, const uint32_t *__restrict__ shift, uint32_t *perm,
-                         uint32_t *skeys, uint32_t bt_off, uint32_t n_bt) {
+                         uint32_t *skeys) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-#if GWAOI_SCAN_BT
-    if (blockIdx.x == 0)  // the scan has read keygen's tile totals: zero for the next flush
-        for (uint32_t j = threadIdx.x; j < n_bt; j += blockDim.x) cnt64[bt_off + j] = 0ull;
-#else
-    (void)bt_off;
-    (void)n_bt;
-#endif
     if (i >= n) return;
     const uint32_t key = keys[i];
     const uint32_t old = i < n_prev ? p_key[i] : sentinel;
@@ -2838,10 +2782,7 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
         if (RS.r[q].n)
             k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
-#ifndef GWAOI_FIXUP_BLOCKS
-#define GWAOI_FIXUP_BLOCKS 64
-#endif
-    k_moves_fixup<<<GWAOI_FIXUP_BLOCKS, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss,
+    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss,
                                                       p_rec, n_prev, sc, coll);
 }
 
@@ -2901,11 +2842,10 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64, seq_base, special,
-                                           sentinel + 1);  // (sentinel = total_cells) folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base, special);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr, seq_base, special, 0u);
+                                            n_prev, blk, nullptr, nullptr, seq_base, special);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }
@@ -2914,7 +2854,6 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 bool scan_rezeroes_counts() { return true; }
 
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
-size_t cnt64_elems(size_t cells) { return cells + (size_t)cdiv(cells, S64_TILE) + 2; }
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
@@ -2928,7 +2867,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                                          cdiv(n_total, 256), sc, p_cell_start, shift);
     if (n_total)
         k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
-                                                     shift, perm, skeys, (uint32_t)m, nb);
+                                                     shift, perm, skeys);
     k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
                                                          n_new, n_total, sentinel, perm, skeys, shift);
 }
@@ -3031,6 +2970,26 @@ void launch_copy_out(const void *src, void *dst, size_t bytes, hipStream_t st) {
     k_copy_out<<<blocks, 256, 0, st>>>(static_cast<const uint4 *>(src), static_cast<uint4 *>(dst), n16,
                                        reinterpret_cast<const uint2 *>(static_cast<const char *>(src) + 16 * n16),
                                        reinterpret_cast<uint2 *>(static_cast<char *>(dst) + 16 * n16), tail8);
+}
+
+// One event of each mirrored pair ((a,b) at an even index, (b,a) after it) into pinned host memory:
+// dst[k] = ev[2k], half the bytes of the directed list over PCIe.
+__global__ __launch_bounds__(256) void k_pairs_out(const uint4 *__restrict__ ev4, uint64_t n2, uint4 *dst4,
+                                                   const uint2 *__restrict__ ev2, uint2 *dst2, uint64_t n_pairs) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n2; k += stride) {
+        const uint4 a = ev4[2 * k], b = ev4[2 * k + 1];  // ev[4k .. 4k+3]: two pairs
+        dst4[k] = make_uint4(a.x, a.y, b.x, b.y);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n_pairs & 1u)) dst2[n_pairs - 1] = ev2[2 * (n_pairs - 1)];
+}
+
+void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream_t st) {
+    if (!n_pairs) return;
+    const uint64_t n2 = n_pairs / 2;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cdiv(n2, 256 * 8), 1), 64);
+    k_pairs_out<<<blocks, 256, 0, st>>>(static_cast<const uint4 *>(events), n2, static_cast<uint4 *>(dst),
+                                        static_cast<const uint2 *>(events), static_cast<uint2 *>(dst), n_pairs);
 }
 
 size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }

@@ -188,14 +188,14 @@ struct gwaoi_world {
     hipStream_t stream = nullptr;
     uint32_t max_slots = 0, max_spaces = 0;
     float cells_per_dist = 1.0f;  // cells per AOI distance of the grids in use
-    // Cell size by density (gwaoi_config.cells_per_dist == 0): clustered crowds want D/4,
+    // Cell size by density (gwaoi_config.cells_per_dist == 0): clustered crowds want D/3,
     // sparse uniform worlds D/2 (fewer cells to scan and merge; config 5: 5.25 vs 5.91 ms,
     // config 4: 4.35 vs 4.95, config 3: 0.316 vs 0.283).  The measure is the mean number of
     // neighbours per entity, kept from the flushes' enter/leave counts.
     bool cells_auto = true;
     int64_t rel_pairs = 0;     // directed relation pairs after the last committed flush
     uint32_t cpd_streak = 0;   // consecutive flushes recommending another cell size
-    float cpd_rec = 4.0f;
+    float cpd_rec = 3.0f;
 
     // three frames: the last committed one, the one a flush in flight writes, and (while a
     // flush launched before the commit of the one in flight runs) the one that flush writes
@@ -293,6 +293,7 @@ struct gwaoi_world {
     hipStream_t out_st = nullptr;
     hipEvent_t out_ev = nullptr;
     bool out_pending = false;  // a copy-out of events queued by gwaoi_tick_end_begin_async, not yet waited for
+    bool out_pairs = false;    // ... of one event per mirrored pair (gwaoi_tick_end_begin_pairs_async)
     bool copyout_kernel = false;  // GWAOI_COPYOUT_KERNEL=1: event copy-outs by k_copy_out, not a DMA copy
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
@@ -533,11 +534,11 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     w->cnt64_cap = 0;
     int rc;
     // arr_pos: the arrival cursors, then the per-cell stayer shifts (incremental_sort)
-    if ((rc = dalloc(w, &w->cnt64, gw::cnt64_elems(cap))) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
+    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
-    HIP_TRY(hipMemsetAsync(w->cnt64, 0, gw::cnt64_elems(cap) * sizeof(unsigned long long), w->stream));  // then kept zero by the sort
+    HIP_TRY(hipMemsetAsync(w->cnt64, 0, cap * sizeof(unsigned long long), w->stream));  // then kept zero by the sort
     w->cnt64_cap = cap;
     return GWAOI_OK;
 }
@@ -650,9 +651,11 @@ float o2f(int i) {
 // (cellOf is monotone and clamped); this only keeps cells near D wide and the
 // cell count bounded by the population.
 // The cell size for a mean of K neighbours per entity: entities per cell ~ (K / 4) / c^2 held
-// near 1.3 (config 3: K = 85 -> D/4; configs 4 and 5: K = 30-32 -> D/2).
-// Only D/2 and D/4 are used (the measured sizes; D/3 ties D/4 at config 3): D/4 from K = 5.33 * 3^2 = 48.
-float recommend_cells_per_dist(double K) { return std::sqrt(K / 5.33) >= 3.0 ? 4.0f : 2.0f; }
+// near 1.3 (config 3: K = 85 -> D/3 or D/4; configs 4 and 5: K = 30-32 -> D/2).
+// Only D/2 and D/3 are used (the measured sizes): D/3 from K = 5.33 * 3^2 = 48.  At config 3, D/3 against
+// D/4 (round 4): the cell scan, merge and keygen shrink with the cell count, the combined pass grows,
+// and the tick is 4 us shorter (241.3 vs 245.4 us, kernel traces).
+float recommend_cells_per_dist(double K) { return std::sqrt(K / 5.33) >= 3.0 ? 3.0f : 2.0f; }
 
 void choose_grids(gwaoi_world *w, uint32_t &total_cells, uint32_t &total_rows) {
     uint32_t base = 0, rows = 0;
@@ -1327,7 +1330,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->cfg = *cfg;
     w->max_slots = cfg->max_slots;
     w->max_spaces = cfg->max_spaces;
-    w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 4.0f;
+    w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 3.0f;
     w->cells_auto = !(cfg->cells_per_dist > 0.f);
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
@@ -2239,6 +2242,7 @@ int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out) {
     // the finished flush's events to pinned host memory on the copy-out stream, beside the next flush
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
+    w->out_pairs = false;
     FlushSet &S = w->fs[w->last_set];
     if (tot) {
         // ordered after the flush's last kernel (its event's release makes the writes visible to the
@@ -2256,9 +2260,9 @@ int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out) {
     });
 }
 
-int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
+namespace {
+// gwaoi_tick_end_begin_async / _pairs_async: end_begin, then the copy-out queued and left running
+int end_begin_async(gwaoi_world *w, bool pairs, uint64_t *n_enter, uint64_t *n_leave) {
     if (n_enter) *n_enter = 0;
     if (n_leave) *n_leave = 0;
     GW_LIVE(w);
@@ -2271,9 +2275,13 @@ int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_le
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
     FlushSet &S = w->fs[w->last_set];
-    if (tot) {  // queued as in gwaoi_tick_end_begin; waited for by gwaoi_events_host (or the next copy-out)
+    w->out_pairs = pairs;
+    if (tot) {  // queued as in gwaoi_tick_end_begin; waited for by gwaoi_events_host / _pairs_host
         HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
-        if (w->copyout_kernel) {
+        if (pairs) {
+            gw::launch_pairs_out(S.events, tot / 2, w->h_events, w->out_st);
+            HIP_TRY(hipGetLastError());
+        } else if (w->copyout_kernel) {
             gw::launch_copy_out(S.events, w->h_events, 2 * tot * sizeof(uint32_t), w->out_st);
             HIP_TRY(hipGetLastError());
         } else {
@@ -2286,6 +2294,20 @@ int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_le
     if (n_enter) *n_enter = w->last_n_enter;
     if (n_leave) *n_leave = w->last_n_leave;
     return rc;
+}
+}  // namespace
+
+int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    return end_begin_async(w, false, n_enter, n_leave);
+    });
+}
+
+int gwaoi_tick_end_begin_pairs_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    return end_begin_async(w, true, n_enter, n_leave);
     });
 }
 
@@ -2295,11 +2317,28 @@ int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out) {
     out->n_enter = out->n_leave = 0;
     out->enter = out->leave = nullptr;
     GW_LIVE(w);
+    if (w->out_pairs) return GWAOI_ESTATE;  // the last copy-out holds pairs: gwaoi_pairs_host
     if (int rw = finish_out(w)) return poison(w, rw);
     out->n_enter = w->last_n_enter;
     out->n_leave = w->last_n_leave;
     out->enter = w->h_events;
     out->leave = w->h_events ? w->h_events + 2 * w->last_n_enter : nullptr;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_pairs_host(gwaoi_world *w, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out) return GWAOI_EINVAL;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    GW_LIVE(w);
+    if (!w->out_pairs) return GWAOI_ESTATE;
+    if (int rw = finish_out(w)) return poison(w, rw);
+    out->n_enter = w->last_n_enter / 2;
+    out->n_leave = w->last_n_leave / 2;
+    out->enter = w->h_events;
+    out->leave = w->h_events ? w->h_events + w->last_n_enter : nullptr;
     return GWAOI_OK;
     });
 }
@@ -2318,6 +2357,7 @@ int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1));
     if (rc2) return poison(w, rc2);  // the committed events cannot reach the caller
+    w->out_pairs = false;
     FlushSet &S = w->fs[w->last_set];
     stage_begin(w, S, ST_D2H);
     if (tot) {

@@ -74,7 +74,7 @@ typedef struct {
     int32_t device;          /* HIP device ordinal, -1 = the calling thread's current */
     uint32_t flags;          /* GWAOI_F_*                                             */
     uint64_t event_capacity; /* initial device event capacity in pairs (0 = default) */
-    float cells_per_dist;    /* grid cells per AOI distance (0 = default 4.0)         */
+    float cells_per_dist;    /* grid cells per AOI distance (0 = automatic, from 3.0) */
 } gwaoi_config;
 
 #define GWAOI_F_TIMING 1u /* time every pipeline stage with HIP events (gwaoi_stage_times) */
@@ -109,7 +109,7 @@ typedef struct {
     uint64_t speculative_launches;  /* flushes gwaoi_tick_end_begin_device queued before the commit of the  */
                                     /* one in flight                                                         */
     uint64_t cell_size_switches;    /* flushes that rebuilt every grid with another automatic cell size      */
-    uint32_t cells_per_dist;        /* cells per AOI distance of the grids in use (2 or 4 when automatic)    */
+    uint32_t cells_per_dist;        /* cells per AOI distance of the grids in use (2 or 3 when automatic)    */
     uint32_t pad;
 } gwaoi_debug;
 
@@ -236,6 +236,15 @@ int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_le
 /* The events of the last gwaoi_tick_end_begin_async, in host memory (waits
  * for their copy); valid until the next call that returns events. */
 int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out);
+/* gwaoi_tick_end_begin_async copying half the bytes: the flush reports every
+ * relation change as the mirrored pair (a,b),(b,a), and only (a,b) crosses
+ * PCIe.  gwaoi_pairs_host returns them: n_enter / n_leave pairs, each entry
+ * (a,b) standing for the two events (a,b) and (b,a) -- OnEnterAOI / OnLeaveAOI
+ * on both entities.  (The counts of _pairs_async are directed events, as
+ * elsewhere.)  gwaoi_events_host after a _pairs_async (and gwaoi_pairs_host
+ * after anything else) returns GWAOI_ESTATE. */
+int gwaoi_tick_end_begin_pairs_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
+int gwaoi_pairs_host(gwaoi_world *w, gwaoi_events *out);
 
 /* ---- zero-copy host move batches ---------------------------------------------
  * The per-tick position batch written straight into the world's pinned staging

@@ -1097,7 +1097,7 @@ def test_speculative_regrows_with_growing_crowd_gpu():
 
 def test_cell_size_switch_keeps_parity_gpu(oracle_mod):
     """Automatic cell size (gwaoi_config.cells_per_dist = 0): a sparse uniform space
-    switches the grids to D/2, a contracted one back to D/4 (two flushes recommending
+    switches the grids to D/2, a contracted one back to D/3 (two flushes recommending
     the other size rebuild every grid; that flush takes the radix sort, the others the
     incremental merge).  Events equal a world with a fixed D/4 grid and the closed form
     at every flush, across both switches."""
@@ -1139,8 +1139,8 @@ def test_cell_size_switch_keeps_parity_gpu(oracle_mod):
             np.testing.assert_array_equal(la, np.setdiff1d(prev, cur), err_msg=f"tick {t}: leaves vs closed form")
             prev = cur
             cpd.append(A.debug_counters()["cells_per_dist"])
-        # sparse start (about 32 neighbours each): D/2; crowded end (about 90): back to D/4
-        assert cpd[0] == 4 and 2 in cpd[1:5] and cpd[-1] == 4, cpd
+        # sparse start (about 32 neighbours each): D/2; crowded end (about 90): back to D/3
+        assert cpd[0] == 3 and 2 in cpd[1:5] and cpd[-1] == 3, cpd
         assert A.debug_counters()["cell_size_switches"] == 2, cpd
         assert B.debug_counters()["cell_size_switches"] == 0
 
@@ -1334,6 +1334,34 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             eb, lb = B.tick()
             np.testing.assert_array_equal(pair_keys(got[t][0]), pair_keys(eb), err_msg=f"async tick {t}")
             np.testing.assert_array_equal(pair_keys(got[t][1]), pair_keys(lb), err_msg=f"async tick {t}")
+        for p in ptrs:
+            A.free_pinned_batch(p)
+        # the same with one event per mirrored pair copied out (gwaoi_tick_end_begin_pairs_async):
+        # the pairs and their mirrors are the directed events
+        host = [wl.tick(14 + t) for t in range(4)]
+        ptrs, got = [], []
+        put(host[0])
+        A.tick_begin()
+        for t in range(4):
+            if t + 1 < 4:
+                put(host[t + 1])
+                if t:
+                    got.append(A.pairs_host())
+                ne, nl = A.tick_end_begin_pairs_async()
+            else:
+                got.append(A.pairs_host())
+                got.append(A.tick_end())
+        with pytest.raises(GwaoiError):
+            A.pairs_host()  # the last copy-out (tick_end) holds directed events
+        for t in range(4):
+            B.moved_batch(*host[t])
+            eb, lb = B.tick()
+            ea, la = got[t]
+            if t < 3:  # pairs: mirror them
+                assert ea.shape[0] * 2 == len(eb) and la.shape[0] * 2 == len(lb)
+                ea, la = np.concatenate([ea, ea[:, ::-1]]), np.concatenate([la, la[:, ::-1]])
+            np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb), err_msg=f"pairs tick {t}")
+            np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"pairs tick {t}")
         for p in ptrs:
             A.free_pinned_batch(p)
         # a move of a slot that is not live: dropped on the device, reported by the flush
