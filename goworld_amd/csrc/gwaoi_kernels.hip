@@ -1291,7 +1291,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
                                            int (&bv)[4]) {
     const uint32_t key = sorted_keys[k];
-    f_key[k] = key;
+    if (f_key) f_key[k] = key;  // (nullptr: the sort wrote the frame's keys in place)
     const uint32_t i = perm[k];
     if (key >= sentinel || i >= n_total) {
         // Fewer live entries than the host counted (a device Enter / Leave batch broke its rules, or a

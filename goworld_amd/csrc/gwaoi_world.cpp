@@ -1003,7 +1003,7 @@ int tick_launch(gwaoi_world *w) {
     if (incr) {
         gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             w->keys[1], w->blk, S.sc, next_lb_tag(w), st);
+                             Fn.key, w->blk, S.sc, next_lb_tag(w), st);  // the sorted keys ARE the frame's
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -1015,14 +1015,15 @@ int tick_launch(gwaoi_world *w) {
         which = gw::radix_sort(sb, n_total, bitlen(total_cells), st);
     }
     stage_end(w, S, ST_SORT);
-    const uint32_t *skeys = w->keys[which];
+    const uint32_t *skeys = incr ? Fn.key : w->keys[which];
     const uint32_t *perm = w->vals[which];
 
     // ---- new frame + previous state in the new order
     stage_begin(w, S, ST_GATHER);
     gw::launch_gather(perm, n_new, n_prev, S.srec, s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, S.orec, S.cand, Fn.grid,
                       seq_base, w->sinfo, skeys,
-                      total_cells, n_total, S.sc, Fn.key, dev_bbox(S), w->n_space_ids, S.bbox_parts, st);
+                      total_cells, n_total, S.sc, incr ? nullptr : Fn.key, dev_bbox(S), w->n_space_ids,
+                      S.bbox_parts, st);
     stage_end(w, S, ST_GATHER);
 
     // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
