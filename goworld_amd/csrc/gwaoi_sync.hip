@@ -467,9 +467,6 @@ __device__ __forceinline__ FanWin fan_window(const FrameView &F, uint32_t i) {
 // loads only) and placed by one atomic per block, so the window is walked
 // once.  A block past the scratch capacity writes no hits (the host regrows
 // the scratch and reruns this pass; it has no other side effect).
-#ifndef GWAOI_HITS64
-#define GWAOI_HITS64 0  // 1: a lane stores its hits 64 B (16 hits) at a time (A/B)
-#endif
 #ifndef GWAOI_FAN_U
 #define GWAOI_FAN_U 6  // A/B: 6 -0.03 ms collect vs 4; 8 and 2 no better (profiles/r02_variants_fan_hits.log)
 #endif
@@ -523,11 +520,7 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
             ub += cs[rb + span] - cs[rb];
         }
     }
-#if GWAOI_HITS64
-    ub = (ub + 15u) & ~15u;  // runs start 64-B aligned: hits are stored sixteen at a time
-#else
     ub = (ub + 3u) & ~3u;  // runs start 16-B aligned: hits are stored four at a time
-#endif
     uint32_t tot;
     const uint32_t off = block_excl(ub, s_ws, tot);
     if (threadIdx.x == 0) {
@@ -541,11 +534,6 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
     uint4 *run = reinterpret_cast<uint4 *>(A.scr + sb);
     uint32_t c = 0;
     uint4 buf = make_uint4(i, 0u, 0u, 0u);
-#if GWAOI_HITS64
-    // 64 B of hits per lane before a store: a lane's run is written one whole 64-B segment at a
-    // time, not one 16-B quarter at a time with the line evicted in between by the window reads
-    uint4 bq[3] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
-#endif
     if (own) c = 1;
     if (walk) {
         const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
@@ -571,40 +559,13 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
                             default: buf.w = b; break;
                         }
                         ++c;
-#if GWAOI_HITS64
-                        if (!(c & 3u)) {  // a full quarter: into the segment, or the segment out
-                            const uint32_t qtr = ((c >> 2) - 1u) & 3u;
-                            if (qtr == 0u) bq[0] = buf;
-                            else if (qtr == 1u) bq[1] = buf;
-                            else if (qtr == 2u) bq[2] = buf;
-                            else if (fits) {
-                                uint4 *seg = run + ((c >> 4) - 1u) * 4u;
-                                st_hits(seg, bq[0]);
-                                st_hits(seg + 1, bq[1]);
-                                st_hits(seg + 2, bq[2]);
-                                st_hits(seg + 3, buf);
-                            }
-                        }
-#else
                         if (!(c & 3u) && fits) st_hits(run + (c >> 2) - 1u, buf);
-#endif
                     }
                 }
             }
         }
     }
-#if GWAOI_HITS64
-    if ((c & 15u) && fits) {  // the last, partial segment: its whole quarters, then the partial one
-        uint4 *seg = run + (c >> 4) * 4u;
-        const uint32_t full = (c & 15u) >> 2;
-        if (full > 0u) st_hits(seg, bq[0]);
-        if (full > 1u) st_hits(seg + 1, bq[1]);
-        if (full > 2u) st_hits(seg + 2, bq[2]);
-        if (c & 3u) st_hits(seg + full, buf);
-    }
-#else
     if ((c & 3u) && fits) st_hits(run + (c >> 2), buf);
-#endif
     if (i < ne) {
         A.fcnt[i] = c;
         A.fsb[i] = sb;
