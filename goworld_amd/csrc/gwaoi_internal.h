@@ -197,10 +197,9 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
 // frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
 // look-back status words (zeroed once when allocated); tag: fresh per launch;
-// arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
+// arr_pos: 3 (total_cells + 1) + 1 words (arrival cursors, per-cell shifts, then the changed-cell
+// count -- zeroed by the prologue -- and list).
 size_t incr_sort_tmp_elems(size_t cells);
-// true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
-bool scan_rezeroes_counts();
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,

@@ -1027,7 +1027,8 @@ constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
-                                                    const uint32_t *__restrict__ p_cs, uint32_t *shift) {
+                                                    const uint32_t *__restrict__ p_cs, uint32_t *shift,
+                                                    uint32_t *chg_n, uint32_t *chg) {
     const uint32_t b = blockIdx.x;
     if (b == nb) {
         keygen_fold256(blk, nbk, sc);
@@ -1085,6 +1086,26 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
             shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
         }
     }
+    // the changed cells (arrivals or departures; not the end entry n - 1) listed for k_cell_merge, one
+    // atomic per block on the list's count
+    uint32_t nch = 0;
+#pragma unroll
+    for (int q = 0; q < S64_I; ++q) {
+        const uint32_t j = (uint32_t)q * SC_T + tid;
+        nch += base + j + 1 < n && (tile[p64(j)] & (unsigned long long)SHIFT_CHANGED) ? 1u : 0u;
+    }
+    __syncthreads();  // ws is reused
+    unsigned long long tch;
+    uint32_t at = (uint32_t)block_excl_scan64<SC_T>(nch, ws, tch);
+    __shared__ uint32_t s_at;
+    if (tid == 0) s_at = tch ? atomicAdd(chg_n, (uint32_t)tch) : 0u;
+    __syncthreads();
+    at += s_at;
+#pragma unroll
+    for (int q = 0; q < S64_I; ++q) {
+        const uint32_t j = (uint32_t)q * SC_T + tid;
+        if (base + j + 1 < n && (tile[p64(j)] & (unsigned long long)SHIFT_CHANGED)) chg[at++] = (uint32_t)(base + j);
+    }
 }
 
 // Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
@@ -1120,20 +1141,36 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
 // still c (S' index order), the arrivals arr_idx[arr_pos[c-1], arr_pos[c])
 // are sorted by S' index (insertion sort: a cell rarely gets more than a few)
 // and merged in.  Writes the frame's permutation and keys.
+__device__ __forceinline__ void merge_cell(uint32_t c, const uint32_t *__restrict__ p_cell_start,
+                                           const uint32_t *__restrict__ cell_start, const uint32_t *__restrict__ keys,
+                                           const uint32_t *__restrict__ arr_pos, uint32_t *arr_idx, uint32_t *perm,
+                                           uint32_t *skeys);
+
 __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const uint32_t *__restrict__ cell_start,
                              const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                              uint32_t *arr_idx, uint32_t total_cells, uint32_t n_new, uint32_t n_total,
-                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ shift) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ chg_n,
+                             const uint32_t *__restrict__ chg) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     // entries past the live count are dead: sentinel keys, no source (so a host count that
     // disagrees with the device's -- a device batch breaking its rules -- finds sentinels, not
     // a previous flush's values, at [n_new, n_total))
-    for (uint32_t k = cell_start[total_cells] + c; k < n_total; k += gridDim.x * blockDim.x) {
+    for (uint32_t k = cell_start[total_cells] + t; k < n_total; k += stride) {
         skeys[k] = sentinel;
         perm[k] = 0xFFFFFFFFu;
     }
     (void)n_new;
-    if (c >= total_cells || shift[c] != SHIFT_CHANGED) return;
+    const uint32_t nc = *chg_n;
+    for (uint32_t k = t; k < nc; k += stride) merge_cell(chg[k], p_cell_start, cell_start, keys, arr_pos, arr_idx, perm, skeys);
+}
+
+// One changed cell c: the stayers are the entries of c's previous run whose new key is still c (S' index
+// order), the arrivals arr_idx[arr_pos[c-1], arr_pos[c]) are sorted by S' index (insertion sort: a cell
+// rarely gets more than a few) and merged in.
+__device__ __forceinline__ void merge_cell(uint32_t c, const uint32_t *__restrict__ p_cell_start,
+                                           const uint32_t *__restrict__ cell_start, const uint32_t *__restrict__ keys,
+                                           const uint32_t *__restrict__ arr_pos, uint32_t *arr_idx, uint32_t *perm,
+                                           uint32_t *skeys) {
     uint32_t o = cell_start[c];
     const uint32_t oe = cell_start[c + 1];
     if (o == oe) return;
@@ -2851,7 +2888,6 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 }
 
 // look-back status words: lo and hi per block
-bool scan_rezeroes_counts() { return true; }
 
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
 
@@ -2862,14 +2898,17 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       TickScalars *sc, uint32_t tag, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
-    uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 2 (total_cells + 1) words
+    // the caller allocates arr_pos with 3 (total_cells + 1) + 1 words: cursors, shifts, changed-cell count + list
+    uint32_t *shift = arr_pos + m, *chg_n = arr_pos + 2 * m;
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
-                                         cdiv(n_total, 256), sc, p_cell_start, shift);
+                                         cdiv(n_total, 256), sc, p_cell_start, shift, chg_n, chg_n + 1);
     if (n_total)
         k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
                                                      shift, perm, skeys);
-    k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
-                                                         n_new, n_total, sentinel, perm, skeys, shift);
+    // the changed cells: a few percent of the cells per tick (grid-stride over the scan's list)
+    k_cell_merge<<<std::min<uint32_t>(cdiv(total_cells, 256), 1024), 256, 0, st>>>(
+        p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_new, n_total, sentinel, perm, skeys, chg_n,
+        chg_n + 1);
 }
 
 size_t scan_tmp_elems(size_t n) {

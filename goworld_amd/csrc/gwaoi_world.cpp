@@ -533,8 +533,8 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     dfree(w->arr_pos);
     w->cnt64_cap = 0;
     int rc;
-    // arr_pos: the arrival cursors, then the per-cell stayer shifts (incremental_sort)
-    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
+    // arr_pos: the arrival cursors, the per-cell stayer shifts, the changed-cell count and list (incremental_sort)
+    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 3 * cap + 1)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
@@ -918,9 +918,8 @@ int tick_launch(gwaoi_world *w) {
     const bool bucketed = moves_only && w->mv_binned;
     const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
-    if (incr)
-        gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
-                            gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
+    if (incr)  // (z0: the incremental sort's changed-cell count, arr_pos[3 (total_cells + 1)])
+        gw::launch_prologue(S.sc, w->arr_pos + 2 * ((size_t)total_cells + 1), 1, w->tile_total,
                             entries + 1, dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
                             w->max_slots, w->sinfo, tick_id, st);
     else
