@@ -2470,6 +2470,9 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 #ifndef GWAOI_FT
 #define GWAOI_FT 16  // measured: 16 -> 15.6 us, 32 -> 19.0, 64 -> 25.3 (cfg3)
 #endif
+#ifndef GWAOI_FIN2
+#define GWAOI_FIN2 0  // 1: the tile offsets by a separate scan launch, k_finish without look-back (A/B)
+#endif
 constexpr int FT = GWAOI_FT;  // tile entries per finish block (<= 64: one wave scans them)
 static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 
@@ -2514,7 +2517,8 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
                                                 uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
-                                                uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt) {
+                                                uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt,
+                                                const uint32_t *__restrict__ offs) {
     const uint32_t b = blockIdx.x, R = gridDim.x - 1 - (tile_order ? N_XCD : 0u);
     if (b > R) {
         tile_order_block(b - R - 1, tile_work, n_tiles, tile_order);
@@ -2569,6 +2573,31 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     __shared__ uint32_t s_off[FT + 1];
     __shared__ unsigned long long s_src[FT];
     const uint32_t e0 = b * FT;
+#if GWAOI_FIN2
+    // the tile offsets come from the exclusive scan launched before (offs[n_entries] = the total)
+    (void)lb;
+    (void)tag;
+    if (threadIdx.x < WAVE) {
+        const uint32_t l = lane(), e = e0 + l;
+        if (l <= (uint32_t)FT) {
+            const uint32_t off = offs[min(e, n_entries)];
+            s_off[l] = off;
+            if (l < (uint32_t)FT) {
+                s_src[l] = e < n_entries ? tile_base[e] : 0ull;
+                if (e == n_enter_entries) {
+                    res->n_enter = off;
+                    if (dcnt) dcnt[0] = off;  // device copy of the counts (events read on the device before the host)
+                }
+            }
+        }
+        if (b == R - 1 && l == 0) {
+            const uint32_t tot = offs[n_entries];
+            res->n_total = tot;
+            if (dcnt) dcnt[1] = tot;
+        }
+    }
+#else
+    (void)offs;
     __shared__ uint32_t s_agg;
     uint32_t cnt = 0, incl = 0;
     if (threadIdx.x < WAVE) {
@@ -2604,6 +2633,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
             if (dcnt) dcnt[1] = excl + agg;
         }
     }
+#endif
     __syncthreads();
     // the block's tiles fill one contiguous output range: every thread takes
     // positions tid, tid + 256, ... (increasing, so its tile index only moves
@@ -3037,14 +3067,19 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   uint32_t *dcount, hipStream_t st) {
+                   uint32_t *dcount, uint32_t *offs, uint32_t *scan_tmp, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
+#if GWAOI_FIN2
+    scan_exclusive(tile_total, offs, (size_t)n_entries + 1, scan_tmp, st);  // tile_total[n_entries] is 0
+#else
+    (void)scan_tmp;
+#endif
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     if (!n_new) tile_order = nullptr;
     k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
         tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu, reinterpret_cast<const uint2 *>(tmp_pairs),
         reinterpret_cast<uint2 *>(out_pairs), cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox,
-        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount);
+        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount, offs);
 }
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }

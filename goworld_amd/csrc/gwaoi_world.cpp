@@ -243,6 +243,7 @@ struct gwaoi_world {
     uint32_t *events_tmp = nullptr;  // evtmp_cap pairs: per-tile chunks at reserved offsets (shared by the sets)
     uint64_t evtmp_cap = 0;
     uint32_t *tile_total = nullptr;
+    uint32_t *tile_off = nullptr;  // exclusive scan of tile_total (k_finish's offsets, GWAOI_FIN2)
     unsigned long long *tile_lb = nullptr;  // k_finish look-back status words
     uint32_t lb_tag = 0;  // look-back launches so far (tags: k_finish, the incremental sort's scan)
     unsigned long long *tile_base = nullptr;
@@ -471,11 +472,12 @@ int ensure_tile_entries(gwaoi_world *w, size_t entries) {
     size_t cap = std::max<size_t>(entries + 1 + entries / 4, 1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->tile_total);
+    dfree(w->tile_off);
     dfree(w->tile_lb);
     dfree(w->tile_base);
     int rc;
     if ((rc = dalloc(w, &w->tile_total, cap)) || (rc = dalloc(w, &w->tile_lb, gw::finish_lb_elems(cap))) ||
-        (rc = dalloc(w, &w->tile_base, cap))) {
+        (rc = dalloc(w, &w->tile_base, cap)) || (rc = dalloc(w, &w->tile_off, cap))) {
         w->tile_entries_cap = 0;
         return rc;
     }
@@ -818,7 +820,7 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
                       reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
                       order ? w->tile_work : nullptr, order ? w->tile_order : nullptr,
-                      reinterpret_cast<uint32_t *>(S.dev_out), st);
+                      reinterpret_cast<uint32_t *>(S.dev_out), w->tile_off, w->scan_tmp, st);
     stage_end(w, S, ST_FINISH);
     return cap;
 }
@@ -1295,7 +1297,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
+    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_off); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);
