@@ -95,7 +95,7 @@ struct TickScalars {
     float bmax;                  // largest |x|,|z| of live entities (new positions)
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
-    uint32_t pad2;
+    uint32_t fix_done;           // keygen's block 0 finished the moves fixup (GWAOI_FIXUP_IN_KEYGEN)
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
 };
 
@@ -158,6 +158,20 @@ struct MoveRuns {
 // holds an older seq than seq_floor, so k_keygen takes the previous frame's
 // record for it and writes it back).  n_marked: runs whose claims are stored
 // already (by the prologue: run 0; by launch_moves_mark: every run).
+// The re-apply of the slots moved more than once (its own launch, or the start of keygen: FixupArgs).
+struct FixupArgs {
+    MoveRuns RS;
+    uint32_t max_slots, tick, n_total, n_prev;
+    unsigned long long seq_floor;
+    SlotInfo *info;
+    Rec16 *s_rec;
+    SlotSp *s_ss;
+    const Rec16 *p_rec;
+    TickScalars *sc;
+    const uint32_t *coll;
+};
+// true: launch_moves leaves the fixup to the flush's keygen (launch_keygen's fx)
+bool fixup_in_keygen();
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st);
@@ -189,7 +203,8 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st);
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const FixupArgs *fx,
+                   hipStream_t st);
 // special (optional, cdiv(n_prev, TILE_A) words): keygen marks the previous-frame tiles that hold an
 // entity the special pass must look at; launch_pairs skips the others.
 // The stable sort of S' by key when the grid is the previous frame's: the

@@ -66,6 +66,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->bmax = 0.0f;
         sc->seq_max = 0;
         sc->ncoll = 0;
+        sc->fix_done = 0;
         for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
     if (i < n0) z0[i] = 0;
@@ -290,24 +291,26 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
 // The slots moved more than once: the op whose claim survived every atomicMax is applied again.
 // A launch of its own: fusing it into the last apply block needed a release fence in every block
 // (at agent scope on gfx950, a write-back of the XCD's L2), measured at 162 against 33 us per apply.
-__global__ void k_moves_fixup(MoveRuns RS, uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_total,
-                              unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *__restrict__ p_rec,
-                              uint32_t n_prev, TickScalars *sc, const uint32_t *__restrict__ coll) {
-    const uint32_t nc = sc->ncoll;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
-        const uint32_t s = coll[k];
-        const uint4 si = reinterpret_cast<const uint4 *>(info)[s];
+#ifndef GWAOI_FIXUP_IN_KEYGEN
+#define GWAOI_FIXUP_IN_KEYGEN 0  // 1: the fixup runs in keygen's block 0 (no launch of its own), others wait if needed
+#endif
+__device__ __forceinline__ void moves_fixup(const FixupArgs &F, uint32_t t0, uint32_t stride) {
+    const uint32_t nc = F.sc->ncoll;
+    for (uint32_t k = t0; k < nc; k += stride) {
+        const uint32_t s = F.coll[k];
+        const uint4 si = reinterpret_cast<const uint4 *>(F.info)[s];
         const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
         uint32_t q = 0;
-        while (q + 1 < RS.count && j >= RS.r[q + 1].j0) ++q;
-        const MoveRun &R = RS.r[q];
+        while (q + 1 < F.RS.count && j >= F.RS.r[q + 1].j0) ++q;
+        const MoveRun &R = F.RS.r[q];
         // start from the previous state so that a dropped (invalid) winner leaves it unchanged
-        if (si.z < n_prev) st_rec(s_rec, si.z, ld_rec(p_rec, si.z));
+        if (si.z < F.n_prev) st_rec(F.s_rec, si.z, ld_rec(F.p_rec, si.z));
         const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
-        op_apply_one(o, j, si, info, tick, n_total, seq_floor, s_rec, s_ss, sc, true);
+        op_apply_one(o, j, si, F.info, F.tick, F.n_total, F.seq_floor, F.s_rec, F.s_ss, F.sc, true);
     }
 }
 
+__global__ void k_moves_fixup(FixupArgs F) { moves_fixup(F, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x); }
 
 // --------------------------------------------------------------- keygen ------
 
@@ -355,9 +358,23 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
-                                                unsigned long long seq_base, uint32_t *special) {
+                                                unsigned long long seq_base, uint32_t *special, FixupArgs fx,
+                                                int with_fix) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (with_fix && fx.sc->ncoll) {  // slots moved more than once: block 0 re-applies them, the others wait
+        if (blockIdx.x == 0) {
+            moves_fixup(fx, threadIdx.x, blockDim.x);
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(&fx.sc->fix_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (threadIdx.x == 0)  // block 0 was dispatched first (in-order dispatch, as the look-backs)
+                while (!__hip_atomic_load(&fx.sc->fix_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT))
+                    __builtin_amdgcn_s_sleep(2);
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+    }
     float dr = 0.0f, bm = 0.0f;
     uint32_t key = sentinel;
     bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
@@ -2840,6 +2857,8 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t ba
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
 }
 
+bool fixup_in_keygen() { return GWAOI_FIXUP_IN_KEYGEN != 0; }
+
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st) {
@@ -2849,8 +2868,22 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
         if (RS.r[q].n)
             k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
-    k_moves_fixup<<<64, 256, 0, st>>>(RS, max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss,
-                                                      p_rec, n_prev, sc, coll);
+    if (!fixup_in_keygen()) {
+        FixupArgs F;
+        F.RS = RS;
+        F.max_slots = max_slots;
+        F.tick = tick_id;
+        F.n_total = n_total;
+        F.n_prev = n_prev;
+        F.seq_floor = seq_floor;
+        F.info = info;
+        F.s_rec = s_rec;
+        F.s_ss = s_ss;
+        F.p_rec = p_rec;
+        F.sc = sc;
+        F.coll = coll;
+        k_moves_fixup<<<64, 256, 0, st>>>(F);
+    }
 }
 
 uint32_t moves_buckets(uint32_t max_slots) { return cdiv(max_slots, MV_R); }
@@ -2904,15 +2937,19 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st) {
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const FixupArgs *fx,
+                   hipStream_t st) {
+    FixupArgs F{};
+    const int wf = fx ? 1 : 0;
+    if (fx) F = *fx;
     if (!n_total) return;  // the prologue left d_rel = bmax = 0
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64, seq_base, special);  // folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base, special, F, wf);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr, seq_base, special);
+                                            n_prev, blk, nullptr, nullptr, seq_base, special, F, wf);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }

@@ -996,8 +996,25 @@ int tick_launch(gwaoi_world *w) {
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
+    gw::FixupArgs fx{};
+    const bool fx_on = moves_only && !bucketed && gw::fixup_in_keygen();
+    if (fx_on) {  // the single-pass apply's fixup, run by keygen's first block
+        fx.RS = RS;
+        fx.max_slots = w->max_slots;
+        fx.tick = tick_id;
+        fx.n_total = n_total;
+        fx.n_prev = n_prev;
+        fx.seq_floor = seq_base;
+        fx.info = w->sinfo;
+        fx.s_rec = S.srec;
+        fx.s_ss = virt ? nullptr : S.sss;
+        fx.p_rec = P.rec;
+        fx.sc = S.sc;
+        fx.coll = w->coll;
+    }
     gw::launch_keygen(S.srec, s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, st);
+                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special,
+                      fx_on ? &fx : nullptr, st);
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;

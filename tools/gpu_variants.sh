@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 for v in "$@"; do
   [ "$v" = base ] && continue
-  GWAOI_LIB=$R/goworld_amd/lib/variants/$v.so timeout -k 10 300 python -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread -k "scaled_configs or speculative or incremental_sort" > $R/gpurun_out/pytest_${TAG}_$v.log 2>&1 || { echo "parity $v failed"; tail -20 $R/gpurun_out/pytest_${TAG}_$v.log; exit 1; }
+  GWAOI_LIB=$R/goworld_amd/lib/variants/$v.so timeout -k 10 300 python -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread -k "scaled_configs or speculative or incremental_sort or repeated or device_batch or zero_copy" > $R/gpurun_out/pytest_${TAG}_$v.log 2>&1 || { echo "parity $v failed"; tail -20 $R/gpurun_out/pytest_${TAG}_$v.log; exit 1; }
   echo "parity $v: $(tail -1 $R/gpurun_out/pytest_${TAG}_$v.log)"
 done
 bash $R/tools/trace_variants.sh $TAG "$@"
