@@ -275,8 +275,6 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 // words, tag: a value not used by an earlier launch on the same lb, != 0 mod
 // 2^30), the scalars of TickOut, and the per-space bbox fold (k_gather's parts).
 size_t finish_lb_elems(size_t n_entries);
-// bytes (a multiple of 8) from device memory to pinned host memory, written by a few workgroups
-void launch_copy_out(const void *src, void *dst, size_t bytes, hipStream_t st);
 // the first event of each mirrored pair of a flush's [enters | leaves] (n_pairs of them) into pinned host memory
 void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream_t st);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,

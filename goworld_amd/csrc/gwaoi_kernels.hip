@@ -3059,25 +3059,6 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
                           tile_order, tile_work, ework);
 }
 
-// Events to pinned host memory by the CUs (PCIe writes from a few workgroups) instead of a DMA
-// engine, so that the copy-out of one tick and the H2D of the next batch do not queue on one engine.
-__global__ __launch_bounds__(256) void k_copy_out(const uint4 *__restrict__ src, uint4 *dst, size_t n16,
-                                                  const uint2 *__restrict__ src8, uint2 *dst8, uint32_t tail8) {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
-    if (blockIdx.x == 0 && threadIdx.x < tail8) dst8[threadIdx.x] = src8[threadIdx.x];
-}
-
-void launch_copy_out(const void *src, void *dst, size_t bytes, hipStream_t st) {
-    if (!bytes) return;
-    const size_t n16 = bytes / 16;
-    const uint32_t tail8 = (uint32_t)((bytes - 16 * n16) / 8);  // event buffers are whole 8-B pairs
-    const uint32_t blocks = (uint32_t)std::min<size_t>(std::max<size_t>(cdiv(n16, 256 * 8), 1), 64);
-    k_copy_out<<<blocks, 256, 0, st>>>(static_cast<const uint4 *>(src), static_cast<uint4 *>(dst), n16,
-                                       reinterpret_cast<const uint2 *>(static_cast<const char *>(src) + 16 * n16),
-                                       reinterpret_cast<uint2 *>(static_cast<char *>(dst) + 16 * n16), tail8);
-}
-
 // One event of each mirrored pair ((a,b) at an even index, (b,a) after it) into pinned host memory:
 // dst[k] = ev[2k], half the bytes of the directed list over PCIe.
 __global__ __launch_bounds__(256) void k_pairs_out(const uint4 *__restrict__ ev4, uint64_t n2, uint4 *dst4,

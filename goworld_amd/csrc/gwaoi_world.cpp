@@ -295,7 +295,6 @@ struct gwaoi_world {
     hipEvent_t out_ev = nullptr;
     bool out_pending = false;  // a copy-out of events queued by gwaoi_tick_end_begin_async, not yet waited for
     bool out_pairs = false;    // ... of one event per mirrored pair (gwaoi_tick_end_begin_pairs_async)
-    bool copyout_kernel = false;  // GWAOI_COPYOUT_KERNEL=1: event copy-outs by k_copy_out, not a DMA copy
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
@@ -501,7 +500,7 @@ int ensure_host_events(gwaoi_world *w, uint64_t pairs) {
     if (w->h_events) (void)hipHostFree(w->h_events);
     w->h_events = nullptr;
     w->h_ev_cap = 0;
-    HIP_TRY(hipHostMalloc((void **)&w->h_events, 2 * cap * sizeof(uint32_t), hipHostMallocMapped));  // (k_copy_out writes it)
+    HIP_TRY(hipHostMalloc((void **)&w->h_events, 2 * cap * sizeof(uint32_t), hipHostMallocMapped));  // (k_pairs_out writes it)
     w->h_ev_cap = cap;
     return GWAOI_OK;
 }
@@ -1459,7 +1458,6 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         return fail(GWAOI_EDEVICE);
     if (const char *e = std::getenv("GWAOI_BLOCKING_SYNC")) w->blocking_sync = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_CHECK_STAGES")) w->check_stages = e[0] == '1';
-    if (const char *e = std::getenv("GWAOI_COPYOUT_KERNEL")) w->copyout_kernel = e[0] == '1';
     w->alive.assign(N, 0);
     w->in_frame.assign(N, 0);
     w->appended.assign(N, 0);
@@ -2299,9 +2297,6 @@ int end_begin_async(gwaoi_world *w, bool pairs, uint64_t *n_enter, uint64_t *n_l
         HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
         if (pairs) {
             gw::launch_pairs_out(S.events, tot / 2, w->h_events, w->out_st);
-            HIP_TRY(hipGetLastError());
-        } else if (w->copyout_kernel) {
-            gw::launch_copy_out(S.events, w->h_events, 2 * tot * sizeof(uint32_t), w->out_st);
             HIP_TRY(hipGetLastError());
         } else {
             HIP_TRY(hipMemcpyAsync(w->h_events, S.events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
