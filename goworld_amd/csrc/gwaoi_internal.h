@@ -95,7 +95,7 @@ struct TickScalars {
     float bmax;                  // largest |x|,|z| of live entities (new positions)
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
-    uint32_t fix_done;           // keygen's block 0 finished the moves fixup (GWAOI_FIXUP_IN_KEYGEN)
+    uint32_t pad2;
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
 };
 
@@ -158,7 +158,7 @@ struct MoveRuns {
 // holds an older seq than seq_floor, so k_keygen takes the previous frame's
 // record for it and writes it back).  n_marked: runs whose claims are stored
 // already (by the prologue: run 0; by launch_moves_mark: every run).
-// The re-apply of the slots moved more than once (its own launch, or the start of keygen: FixupArgs).
+// The re-apply of the slots moved more than once (k_moves_fixup's arguments).
 struct FixupArgs {
     MoveRuns RS;
     uint32_t max_slots, tick, n_total, n_prev;
@@ -170,8 +170,6 @@ struct FixupArgs {
     TickScalars *sc;
     const uint32_t *coll;
 };
-// true: launch_moves leaves the fixup to the flush's keygen (launch_keygen's fx)
-bool fixup_in_keygen();
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st);
@@ -203,8 +201,7 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const FixupArgs *fx,
-                   hipStream_t st);
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st);
 // special (optional, cdiv(n_prev, TILE_A) words): keygen marks the previous-frame tiles that hold an
 // entity the special pass must look at; launch_pairs skips the others.
 // The stable sort of S' by key when the grid is the previous frame's: the
@@ -212,9 +209,10 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
 // frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
 // look-back status words (zeroed once when allocated); tag: fresh per launch;
-// arr_pos: 3 (total_cells + 1) + 1 words (arrival cursors, per-cell shifts, then the changed-cell
-// count -- zeroed by the prologue -- and list).
+// arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
 size_t incr_sort_tmp_elems(size_t cells);
+// true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
+bool scan_rezeroes_counts();
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
@@ -281,7 +279,7 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   uint32_t *dcount, uint32_t *offs, uint32_t *scan_tmp, hipStream_t st);
+                   uint32_t *dcount, hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
 void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,

@@ -66,7 +66,6 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->bmax = 0.0f;
         sc->seq_max = 0;
         sc->ncoll = 0;
-        sc->fix_done = 0;
         for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
     if (i < n0) z0[i] = 0;
@@ -291,9 +290,6 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
 // The slots moved more than once: the op whose claim survived every atomicMax is applied again.
 // A launch of its own: fusing it into the last apply block needed a release fence in every block
 // (at agent scope on gfx950, a write-back of the XCD's L2), measured at 162 against 33 us per apply.
-#ifndef GWAOI_FIXUP_IN_KEYGEN
-#define GWAOI_FIXUP_IN_KEYGEN 0  // 1: the fixup runs in keygen's block 0 (no launch of its own), others wait if needed
-#endif
 __device__ __forceinline__ void moves_fixup(const FixupArgs &F, uint32_t t0, uint32_t stride) {
     const uint32_t nc = F.sc->ncoll;
     for (uint32_t k = t0; k < nc; k += stride) {
@@ -358,23 +354,9 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
-                                                unsigned long long seq_base, uint32_t *special, FixupArgs fx,
-                                                int with_fix) {
+                                                unsigned long long seq_base, uint32_t *special) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (with_fix && fx.sc->ncoll) {  // slots moved more than once: block 0 re-applies them, the others wait
-        if (blockIdx.x == 0) {
-            moves_fixup(fx, threadIdx.x, blockDim.x);
-            __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_store(&fx.sc->fix_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (threadIdx.x == 0)  // block 0 was dispatched first (in-order dispatch, as the look-backs)
-                while (!__hip_atomic_load(&fx.sc->fix_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT))
-                    __builtin_amdgcn_s_sleep(2);
-            __syncthreads();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-    }
     float dr = 0.0f, bm = 0.0f;
     uint32_t key = sentinel;
     bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
@@ -1044,8 +1026,7 @@ constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
 __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
-                                                    const uint32_t *__restrict__ p_cs, uint32_t *shift,
-                                                    uint32_t *chg_n, uint32_t *chg) {
+                                                    const uint32_t *__restrict__ p_cs, uint32_t *shift) {
     const uint32_t b = blockIdx.x;
     if (b == nb) {
         keygen_fold256(blk, nbk, sc);
@@ -1103,26 +1084,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
             shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
         }
     }
-    // the changed cells (arrivals or departures; not the end entry n - 1) listed for k_cell_merge, one
-    // atomic per block on the list's count
-    uint32_t nch = 0;
-#pragma unroll
-    for (int q = 0; q < S64_I; ++q) {
-        const uint32_t j = (uint32_t)q * SC_T + tid;
-        nch += base + j + 1 < n && (tile[p64(j)] & (unsigned long long)SHIFT_CHANGED) ? 1u : 0u;
-    }
-    __syncthreads();  // ws is reused
-    unsigned long long tch;
-    uint32_t at = (uint32_t)block_excl_scan64<SC_T>(nch, ws, tch);
-    __shared__ uint32_t s_at;
-    if (tid == 0) s_at = tch ? atomicAdd(chg_n, (uint32_t)tch) : 0u;
-    __syncthreads();
-    at += s_at;
-#pragma unroll
-    for (int q = 0; q < S64_I; ++q) {
-        const uint32_t j = (uint32_t)q * SC_T + tid;
-        if (base + j + 1 < n && (tile[p64(j)] & (unsigned long long)SHIFT_CHANGED)) chg[at++] = (uint32_t)(base + j);
-    }
 }
 
 // Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
@@ -1158,36 +1119,20 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
 // still c (S' index order), the arrivals arr_idx[arr_pos[c-1], arr_pos[c])
 // are sorted by S' index (insertion sort: a cell rarely gets more than a few)
 // and merged in.  Writes the frame's permutation and keys.
-__device__ __forceinline__ void merge_cell(uint32_t c, const uint32_t *__restrict__ p_cell_start,
-                                           const uint32_t *__restrict__ cell_start, const uint32_t *__restrict__ keys,
-                                           const uint32_t *__restrict__ arr_pos, uint32_t *arr_idx, uint32_t *perm,
-                                           uint32_t *skeys);
-
 __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const uint32_t *__restrict__ cell_start,
                              const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                              uint32_t *arr_idx, uint32_t total_cells, uint32_t n_new, uint32_t n_total,
-                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ chg_n,
-                             const uint32_t *__restrict__ chg) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+                             uint32_t sentinel, uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ shift) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     // entries past the live count are dead: sentinel keys, no source (so a host count that
     // disagrees with the device's -- a device batch breaking its rules -- finds sentinels, not
     // a previous flush's values, at [n_new, n_total))
-    for (uint32_t k = cell_start[total_cells] + t; k < n_total; k += stride) {
+    for (uint32_t k = cell_start[total_cells] + c; k < n_total; k += gridDim.x * blockDim.x) {
         skeys[k] = sentinel;
         perm[k] = 0xFFFFFFFFu;
     }
     (void)n_new;
-    const uint32_t nc = *chg_n;
-    for (uint32_t k = t; k < nc; k += stride) merge_cell(chg[k], p_cell_start, cell_start, keys, arr_pos, arr_idx, perm, skeys);
-}
-
-// One changed cell c: the stayers are the entries of c's previous run whose new key is still c (S' index
-// order), the arrivals arr_idx[arr_pos[c-1], arr_pos[c]) are sorted by S' index (insertion sort: a cell
-// rarely gets more than a few) and merged in.
-__device__ __forceinline__ void merge_cell(uint32_t c, const uint32_t *__restrict__ p_cell_start,
-                                           const uint32_t *__restrict__ cell_start, const uint32_t *__restrict__ keys,
-                                           const uint32_t *__restrict__ arr_pos, uint32_t *arr_idx, uint32_t *perm,
-                                           uint32_t *skeys) {
+    if (c >= total_cells || shift[c] != SHIFT_CHANGED) return;
     uint32_t o = cell_start[c];
     const uint32_t oe = cell_start[c + 1];
     if (o == oe) return;
@@ -2487,9 +2432,6 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 #ifndef GWAOI_FT
 #define GWAOI_FT 16  // measured: 16 -> 15.6 us, 32 -> 19.0, 64 -> 25.3 (cfg3)
 #endif
-#ifndef GWAOI_FIN2
-#define GWAOI_FIN2 0  // 1: the tile offsets by a separate scan launch, k_finish without look-back (A/B)
-#endif
 constexpr int FT = GWAOI_FT;  // tile entries per finish block (<= 64: one wave scans them)
 static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 
@@ -2534,8 +2476,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
                                                 uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
-                                                uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt,
-                                                const uint32_t *__restrict__ offs) {
+                                                uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt) {
     const uint32_t b = blockIdx.x, R = gridDim.x - 1 - (tile_order ? N_XCD : 0u);
     if (b > R) {
         tile_order_block(b - R - 1, tile_work, n_tiles, tile_order);
@@ -2590,31 +2531,6 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     __shared__ uint32_t s_off[FT + 1];
     __shared__ unsigned long long s_src[FT];
     const uint32_t e0 = b * FT;
-#if GWAOI_FIN2
-    // the tile offsets come from the exclusive scan launched before (offs[n_entries] = the total)
-    (void)lb;
-    (void)tag;
-    if (threadIdx.x < WAVE) {
-        const uint32_t l = lane(), e = e0 + l;
-        if (l <= (uint32_t)FT) {
-            const uint32_t off = offs[min(e, n_entries)];
-            s_off[l] = off;
-            if (l < (uint32_t)FT) {
-                s_src[l] = e < n_entries ? tile_base[e] : 0ull;
-                if (e == n_enter_entries) {
-                    res->n_enter = off;
-                    if (dcnt) dcnt[0] = off;  // device copy of the counts (events read on the device before the host)
-                }
-            }
-        }
-        if (b == R - 1 && l == 0) {
-            const uint32_t tot = offs[n_entries];
-            res->n_total = tot;
-            if (dcnt) dcnt[1] = tot;
-        }
-    }
-#else
-    (void)offs;
     __shared__ uint32_t s_agg;
     uint32_t cnt = 0, incl = 0;
     if (threadIdx.x < WAVE) {
@@ -2650,7 +2566,6 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
             if (dcnt) dcnt[1] = excl + agg;
         }
     }
-#endif
     __syncthreads();
     // the block's tiles fill one contiguous output range: every thread takes
     // positions tid, tid + 256, ... (increasing, so its tile index only moves
@@ -2857,8 +2772,6 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t ba
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
 }
 
-bool fixup_in_keygen() { return GWAOI_FIXUP_IN_KEYGEN != 0; }
-
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st) {
@@ -2868,7 +2781,7 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
         if (RS.r[q].n)
             k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
-    if (!fixup_in_keygen()) {
+    {
         FixupArgs F;
         F.RS = RS;
         F.max_slots = max_slots;
@@ -2937,24 +2850,21 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const FixupArgs *fx,
-                   hipStream_t st) {
-    FixupArgs F{};
-    const int wf = fx ? 1 : 0;
-    if (fx) F = *fx;
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st) {
     if (!n_total) return;  // the prologue left d_rel = bmax = 0
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64, seq_base, special, F, wf);  // folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base, special);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr, seq_base, special, F, wf);
+                                            n_prev, blk, nullptr, nullptr, seq_base, special);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }
 
 // look-back status words: lo and hi per block
+bool scan_rezeroes_counts() { return true; }
 
 size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
 
@@ -2965,17 +2875,14 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       TickScalars *sc, uint32_t tag, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
-    // the caller allocates arr_pos with 3 (total_cells + 1) + 1 words: cursors, shifts, changed-cell count + list
-    uint32_t *shift = arr_pos + m, *chg_n = arr_pos + 2 * m;
+    uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 2 (total_cells + 1) words
     k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
-                                         cdiv(n_total, 256), sc, p_cell_start, shift, chg_n, chg_n + 1);
+                                         cdiv(n_total, 256), sc, p_cell_start, shift);
     if (n_total)
         k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
                                                      shift, perm, skeys);
-    // the changed cells: a few percent of the cells per tick (grid-stride over the scan's list)
-    k_cell_merge<<<std::min<uint32_t>(cdiv(total_cells, 256), 1024), 256, 0, st>>>(
-        p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_new, n_total, sentinel, perm, skeys, chg_n,
-        chg_n + 1);
+    k_cell_merge<<<cdiv(total_cells, 256), 256, 0, st>>>(p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells,
+                                                         n_new, n_total, sentinel, perm, skeys, shift);
 }
 
 size_t scan_tmp_elems(size_t n) {
@@ -3085,19 +2992,14 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
                    uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   uint32_t *dcount, uint32_t *offs, uint32_t *scan_tmp, hipStream_t st) {
+                   uint32_t *dcount, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
-#if GWAOI_FIN2
-    scan_exclusive(tile_total, offs, (size_t)n_entries + 1, scan_tmp, st);  // tile_total[n_entries] is 0
-#else
-    (void)scan_tmp;
-#endif
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     if (!n_new) tile_order = nullptr;
     k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
         tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu, reinterpret_cast<const uint2 *>(tmp_pairs),
         reinterpret_cast<uint2 *>(out_pairs), cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox,
-        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount, offs);
+        n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount);
 }
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }

@@ -243,7 +243,6 @@ struct gwaoi_world {
     uint32_t *events_tmp = nullptr;  // evtmp_cap pairs: per-tile chunks at reserved offsets (shared by the sets)
     uint64_t evtmp_cap = 0;
     uint32_t *tile_total = nullptr;
-    uint32_t *tile_off = nullptr;  // exclusive scan of tile_total (k_finish's offsets, GWAOI_FIN2)
     unsigned long long *tile_lb = nullptr;  // k_finish look-back status words
     uint32_t lb_tag = 0;  // look-back launches so far (tags: k_finish, the incremental sort's scan)
     unsigned long long *tile_base = nullptr;
@@ -471,12 +470,11 @@ int ensure_tile_entries(gwaoi_world *w, size_t entries) {
     size_t cap = std::max<size_t>(entries + 1 + entries / 4, 1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->tile_total);
-    dfree(w->tile_off);
     dfree(w->tile_lb);
     dfree(w->tile_base);
     int rc;
     if ((rc = dalloc(w, &w->tile_total, cap)) || (rc = dalloc(w, &w->tile_lb, gw::finish_lb_elems(cap))) ||
-        (rc = dalloc(w, &w->tile_base, cap)) || (rc = dalloc(w, &w->tile_off, cap))) {
+        (rc = dalloc(w, &w->tile_base, cap))) {
         w->tile_entries_cap = 0;
         return rc;
     }
@@ -534,8 +532,8 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     dfree(w->arr_pos);
     w->cnt64_cap = 0;
     int rc;
-    // arr_pos: the arrival cursors, the per-cell stayer shifts, the changed-cell count and list (incremental_sort)
-    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 3 * cap + 1)) ||
+    // arr_pos: the arrival cursors, then the per-cell stayer shifts (incremental_sort)
+    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
@@ -819,7 +817,7 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
                       reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
                       order ? w->tile_work : nullptr, order ? w->tile_order : nullptr,
-                      reinterpret_cast<uint32_t *>(S.dev_out), w->tile_off, w->scan_tmp, st);
+                      reinterpret_cast<uint32_t *>(S.dev_out), st);
     stage_end(w, S, ST_FINISH);
     return cap;
 }
@@ -919,8 +917,9 @@ int tick_launch(gwaoi_world *w) {
     const bool bucketed = moves_only && w->mv_binned;
     const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
     const uint32_t n_copy = virt ? 0u : n_prev;
-    if (incr)  // (z0: the incremental sort's changed-cell count, arr_pos[3 (total_cells + 1)])
-        gw::launch_prologue(S.sc, w->arr_pos + 2 * ((size_t)total_cells + 1), 1, w->tile_total,
+    if (incr)
+        gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
+                            gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
                             entries + 1, dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
                             w->max_slots, w->sinfo, tick_id, st);
     else
@@ -995,25 +994,8 @@ int tick_launch(gwaoi_world *w) {
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
-    gw::FixupArgs fx{};
-    const bool fx_on = moves_only && !bucketed && gw::fixup_in_keygen();
-    if (fx_on) {  // the single-pass apply's fixup, run by keygen's first block
-        fx.RS = RS;
-        fx.max_slots = w->max_slots;
-        fx.tick = tick_id;
-        fx.n_total = n_total;
-        fx.n_prev = n_prev;
-        fx.seq_floor = seq_base;
-        fx.info = w->sinfo;
-        fx.s_rec = S.srec;
-        fx.s_ss = virt ? nullptr : S.sss;
-        fx.p_rec = P.rec;
-        fx.sc = S.sc;
-        fx.coll = w->coll;
-    }
     gw::launch_keygen(S.srec, s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special,
-                      fx_on ? &fx : nullptr, st);
+                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, st);
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;
@@ -1313,7 +1295,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_off); dfree(w->tile_lb); dfree(w->tile_base);
+    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
     dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);
