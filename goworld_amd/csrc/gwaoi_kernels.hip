@@ -241,6 +241,9 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint
     if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (R.j0 + i);
 }
 
+#ifndef GWAOI_APPLY_PER
+#define GWAOI_APPLY_PER 4  // moves per thread of the single-pass apply (all SlotInfo lines in flight at once)
+#endif
 template <int PER>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
@@ -2779,7 +2782,7 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
-            k_moves_apply_n<4><<<cdiv(RS.r[q].n, 256 * 4), 256, 0, st>>>(
+            k_moves_apply_n<GWAOI_APPLY_PER><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
     {
         FixupArgs F;
