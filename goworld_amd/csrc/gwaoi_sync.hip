@@ -224,6 +224,9 @@ __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, con
 // batch) plus Position; elsewhere Space.move returns before Position
 // (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
 // PER records per thread, strided by the block: every slot record is loaded before any is used.
+#ifndef GWAOI_DEC_PER
+#define GWAOI_DEC_PER 1  // records per k_decode thread
+#endif
 template <int PER>
 __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     const uint32_t i0 = blockIdx.x * (ST * PER) + threadIdx.x;
@@ -1350,7 +1353,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.ndup = reinterpret_cast<uint32_t *>(base + 6 * al(n * 4));
     S->claim_next += n;
     S->decoded = true;
-    k_decode<1><<<cdivu(n, ST * 1), ST, 0, S->st>>>(A);
+    k_decode<GWAOI_DEC_PER><<<cdivu(n, ST * GWAOI_DEC_PER), ST, 0, S->st>>>(A);
     k_decode_apply<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_dups<<<std::min<uint32_t>(cdivu(n, ST), 64u), ST, 0, S->st>>>(A);
     SY_TRY(hipGetLastError());
