@@ -1,15 +1,16 @@
 set -o pipefail
-# round-4: k_decode records per thread (1 = base, 2, 4): sync parity, then the sync leg's decode + flush time
+# round-4: k_decode records per thread (1 = base, 2, 4) and k_fan_write record groups in flight (4 = base, 8, 2):
+# sync parity, then the sync leg's decode + flush and collect times
 # and the k_decode kernel time
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 export TMPDIR=/tmp
-for v in dec2 dec4; do
+for v in dec2 dec4 fw8 fw2; do
   GWAOI_LIB=$R/goworld_amd/lib/variants/$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "sync" > $R/gpurun_out/pytest_r04s_$v.log 2>&1 || { tail -30 $R/gpurun_out/pytest_r04s_$v.log; exit 1; }
   echo "parity $v: $(tail -1 $R/gpurun_out/pytest_r04s_$v.log)"
 done
 A="--steps 3 --warmup 2 --no-cpu-baseline --cfg4-steps 0 --cfg5-steps 0 --host-tick-steps 0 --host-io-steps 0 --wire-steps 0 --breakdown-steps 0 --sync-steps 5"
-for v in base dec2 dec4 base dec2 dec4; do
+for v in base dec2 dec4 fw8 fw2 base dec2 dec4 fw8 fw2; do
   if [ $v = base ]; then unset GWAOI_LIB; else export GWAOI_LIB=$R/goworld_amd/lib/variants/$v.so; fi
   OUT=$R/gpurun_out/ts_r04s_$v
   mkdir -p $OUT
