@@ -107,7 +107,7 @@ def combined_pass_bytes(n: int, total_cells: int, events: float) -> float:
 
 # the kernels behind each timed stage (the roofline's "kernel")
 STAGE_KERNEL = {"apply": "k_moves_apply+k_moves_fixup", "keygen": "k_keygen",
-                "sort": "k_scan64_reduce/single/down+k_arrive+k_cell_merge", "gather": "k_gather",
+                "sort": "k_scan64_agg+k_scan64+k_arrive+k_cell_merge", "gather": "k_gather",
                 "combined": "k_combined", "finish": "k_finish"}
 
 

@@ -208,7 +208,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // new cell_start (from cnt64) plus, per cell, a merge of the entities that
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
 // frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
-// look-back status words (zeroed once when allocated); tag: fresh per launch;
+// words (the cell scan's tile totals);
 // arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
 size_t incr_sort_tmp_elems(size_t cells);
 // true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
@@ -217,7 +217,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, u
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, uint32_t tag, hipStream_t st);
+                      TickScalars *sc, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
@@ -269,14 +269,15 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 // The flush's tail in one launch: every tile's events from tmp into tile order
 // (`out` may be host-mapped pinned memory, and hbbox, when given, receives the
 // folded per-space boxes there: the flush summary needs no copy)
-// (offsets by a decoupled look-back; lb: finish_lb_elems(n_entries) status
-// words, tag: a value not used by an earlier launch on the same lb, != 0 mod
-// 2^30), the scalars of TickOut, and the per-space bbox fold (k_gather's parts).
-size_t finish_lb_elems(size_t n_entries);
+// (a block's offset: the group totals the pair passes added, then its group's
+// tile totals before it), the scalars of TickOut, and the per-space bbox fold
+// (k_gather's parts).
+// tile_total words for n_entries entries: the totals, one spare, then any group totals (all zeroed per flush)
+size_t tile_total_elems(size_t n_entries);
 // the first event of each mirrored pair of a flush's [enters | leaves] (n_pairs of them) into pinned host memory
 void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream_t st);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
-                   uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
+                   uint32_t n_enter_entries, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
                    uint32_t *dcount, hipStream_t st);

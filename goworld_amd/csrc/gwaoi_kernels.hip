@@ -340,9 +340,16 @@ constexpr int SC_T = 256;
 constexpr int SC_I = 16;
 constexpr int SC_TILE = SC_T * SC_I;
 #ifndef GWAOI_S64_I
-#define GWAOI_S64_I 16  // cells per thread of the incremental sort's cell scan (k_scan64_lb)
+#define GWAOI_S64_I 16  // cells per thread of the incremental sort's cell scan (k_scan64)
 #endif
 constexpr int S64_I = GWAOI_S64_I;
+constexpr uint32_t FG = 256;  // measured (cfg3 k_finish): 128 -> 11.8 us, 256 -> 11.4, 512 -> 11.7
+// A pair pass's tile total, also added to its group's total, which follows the entries'
+// totals (tile_total[entries + 1 + e / FG], zeroed with them by the prologue).
+__device__ __forceinline__ void put_tile_total(uint32_t *tt, uint32_t leave_off, uint32_t e, uint32_t v) {
+    tt[e] = v;
+    if (v) atomicAdd(tt + 2 * leave_off + 1 + e / FG, v);
+}
 constexpr int S64_TILE = SC_T * S64_I;
 
 // INCR (the grid is the previous frame's): also count, per cell, the
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     if (INCR) {
         // only the entities that changed cell count: an arrival in the new cell (low word), a
         // departure from the old one (high word); a cell's stayers are its previous count minus
-        // its departures, which k_scan64_lb takes from the previous cell_start
+        // its departures, which k_scan64 takes from the previous cell_start
         if (i < n) {
             const uint32_t old = i < n_prev ? p_key[i] : sentinel;
             if (key != old) {
@@ -875,32 +882,12 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 //   k_arrive         arrivals into per-cell lists (atomic order, fixed later)
 //   k_cell_merge     one lane per cell: sort its arrivals, merge with the stayers
 
-// ------------------------------------------------------ look-back scans ------
-// Single-pass scans (decoupled look-back): block b publishes its aggregate,
-// looks back over the status words of the blocks before it until it meets an
-// inclusive prefix, then publishes its own inclusive prefix.  A status word is
-// (tag << 2 | kind) << 32 | value: the tag is fresh per launch (the words are
-// never zeroed per flush; tag 0 = never written), kind 1 = aggregate,
-// 2 = inclusive.  The words are read and written with device-scope atomics.
-// Blocks take their scan index from blockIdx.x.  The walk terminates because
-// the command processor dispatches a launch's workgroups in index order (per
-// XCD, round robin over the XCDs): the lowest unfinished block has every
-// predecessor finished, so it never waits, and every block before it on its
-// XCD has finished, so it has been dispatched.  An atomic ticket per block
-// (index order independent of dispatch) was measured: +9 us in the sort's scan
-// and +11 us in k_finish per cfg3 tick (one contended counter, ~1000 blocks),
-// 7% of the tick (profiles/r03_ticket_lookback.log), so it is not used.
-// When the 30-bit tag wraps, the host zeroes the status words first.
-constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
-
-__device__ __forceinline__ unsigned long long lb_word(uint32_t tag, uint32_t kind, uint32_t v) {
-    return ((unsigned long long)((tag << 2) | kind) << 32) | v;
-}
-
-__device__ __forceinline__ void lb_store(unsigned long long *p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
+// ------------------------------------------------------ block offsets ------
+// The two scans across blocks (the sort's cell counts, k_finish's tile totals) take a
+// block's offset from totals written by an earlier launch -- per scan tile (k_scan64_agg)
+// or per group of FG tile entries (the pair passes' atomics) -- summed by the whole block,
+// with no chain between blocks.  Rounds 2-4 used a decoupled look-back instead: its chain
+// cost 10 us in the cell scan and 3.5 us in k_finish per cfg3 tick (profiles/r04_variants_scan.log).
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
@@ -914,51 +901,6 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // reads block j - t of a window, so a walk takes one window per 256 blocks
 // (the predecessors' aggregates are published at once, so a window is ready
 // after about one poll).  excl is valid in every thread.
-template <int NW>
-__device__ void lookback(const unsigned long long *lb, size_t stride, uint32_t b, uint32_t tag, uint32_t (&excl)[NW]) {
-    constexpr int NT = 256;
-    __shared__ int s_near;
-    __shared__ uint32_t s_part[NW][NT / WAVE];
-    const int t = (int)threadIdx.x, w = t / WAVE;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) excl[q] = 0;
-    for (int j = (int)b - 1; j >= 0; j -= NT) {
-        const int idx = j - t;
-        unsigned long long wd[NW];
-        uint32_t kind = LB_INCL;
-        if (t == 0) s_near = NT;
-        for (;;) {
-            bool ok = true;
-            kind = LB_INCL;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) {
-                wd[q] = idx >= 0 ? __hip_atomic_load(lb + q * stride + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : lb_word(tag, LB_INCL, 0u);
-                const uint32_t hi = (uint32_t)(wd[q] >> 32);
-                ok = ok && (hi >> 2) == tag && (hi & 3u) != 0u;
-                if (q == 0) kind = hi & 3u;
-                else ok = ok && (hi & 3u) == kind;  // aggregate and inclusive words never mixed
-            }
-            if (__syncthreads_and(ok)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (kind == LB_INCL) atomicMin(&s_near, t);  // LDS: the nearest inclusive prefix ends the walk
-        __syncthreads();
-        const int m = s_near;
-#pragma unroll
-        for (int q = 0; q < NW; ++q) {
-            const uint32_t v = wave_sum_u32(t <= m ? (uint32_t)wd[q] : 0u);
-            if (lane() == 0) s_part[q][w] = v;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < NW; ++q)
-            for (int i = 0; i < NT / WAVE; ++i) excl[q] += s_part[q][i];
-        __syncthreads();  // s_near / s_part are reused by the next window
-        if (m < NT) return;
-    }
-}
-
 __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long x) {
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -990,10 +932,9 @@ __device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long lo
 // (stride 17) and a wave's coalesced row (stride 1) are both conflict-free.
 __device__ __forceinline__ uint32_t p64(uint32_t i) { return i + (i >> 4); }
 
-// Single-pass form of reduce + single + down (one launch): exclusive scan of
-// the packed (lo = entities, hi = arrivals) cell counts into lo[] / hi[]; the
-// block offsets come from a look-back over lb[0 .. nb) (lo) and lb[nb .. 2nb)
-// (hi).  The extra block nb folds keygen's d_rel / bmax partials.
+// Exclusive scan of the packed (lo = arrivals, hi = departures) cell counts, one
+// tile per block, the tile offsets from k_scan64_agg's totals.  The extra block nb
+// folds keygen's d_rel / bmax partials.
 __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
     __shared__ float s_m[2][SC_T / WAVE];
     float a = 0.0f, b = 0.0f;
@@ -1026,8 +967,30 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 // without a store per cell.  shift[c]: SHIFT_CHANGED for a cell with arrivals or departures, else
 // how far its run moved (new start - previous start): k_arrive places such a cell's stayers itself.
 constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
-__global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
-                                                    unsigned long long *lb, uint32_t tag, uint32_t *lo, uint32_t *hi,
+// The packed counts' total per scan tile (one block per tile).
+__global__ __launch_bounds__(SC_T) void k_scan64_agg(const unsigned long long *__restrict__ in, size_t n,
+                                                     unsigned long long *agg) {
+    __shared__ unsigned long long s_w[SC_T / WAVE];
+    const size_t base = (size_t)blockIdx.x * S64_TILE;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int q = 0; q < S64_I; ++q) {
+        const size_t j = base + (uint32_t)q * SC_T + threadIdx.x;
+        v += j < n ? in[j] : 0ull;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane() == 0) s_w[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int q = 0; q < SC_T / WAVE; ++q) t += s_w[q];
+        agg[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
+                                                    const unsigned long long *__restrict__ agg, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
                                                     const uint32_t *__restrict__ p_cs, uint32_t *shift) {
     const uint32_t b = blockIdx.x;
@@ -1054,19 +1017,18 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
     }
     unsigned long long tot;
     unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot);
-    if (tid == 0) {
-        const uint32_t k = b == 0 ? LB_INCL : LB_AGG;
-        lb_store(lb + b, lb_word(tag, k, (uint32_t)tot));
-        lb_store(lb + nb + b, lb_word(tag, k, (uint32_t)(tot >> 32)));
-    }
-    uint32_t ex[2] = {0u, 0u};
-    if (b) lookback<2>(lb, nb, b, tag, ex);
-    const unsigned long long e = ((unsigned long long)ex[1] << 32) | ex[0];
-    if (tid == 0 && b) {
-        const unsigned long long t = e + tot;
-        lb_store(lb + b, lb_word(tag, LB_INCL, (uint32_t)t));
-        lb_store(lb + nb + b, lb_word(tag, LB_INCL, (uint32_t)(t >> 32)));
-    }
+    // the tile's offset: the sum of the earlier tiles' totals (k_scan64_agg), no look-back chain:
+    // a chain serialises ~500 tiles at ~20 ns a hop, the block-wide sum of <= 1k words does not
+    __shared__ unsigned long long s_pre[SC_T / WAVE];
+    unsigned long long pre = 0;
+    for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    if (lane() == 0) s_pre[tid / WAVE] = pre;
+    __syncthreads();
+    unsigned long long e = 0;
+#pragma unroll
+    for (int q = 0; q < SC_T / WAVE; ++q) e += s_pre[q];
     run += e;
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read; bit 31: c changed
@@ -1091,7 +1053,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64_lb(const unsigned long long *__
 
 // Arrivals into per-cell lists.  arr_pos[c] starts as the exclusive offset
 // of cell c and ends as that of cell c+1.  An entity that changed cell also
-// zeroes the counts of both its cells (k_scan64_lb has read them).  A stayer
+// zeroes the counts of both its cells (k_scan64 has read them).  A stayer
 // of an unchanged cell (no arrival, no departure) keeps its rank in the run,
 // so its frame position is its S' index plus the cell's shift.
 __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
@@ -1622,9 +1584,9 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
         const uint32_t tot = te + tl;
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
         s_base = b;
-        tile_total[tile_off + t] = te;
+        put_tile_total(tile_total, leave_off, tile_off + t, te);
         tile_base[tile_off + t] = b;
-        tile_total[leave_off + tile_off + t] = tl;
+        put_tile_total(tile_total, leave_off, leave_off + tile_off + t, tl);
         tile_base[leave_off + tile_off + t] = b + te;
     }
     __syncthreads();
@@ -2379,9 +2341,9 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         const uint32_t tot = 2 * (se + sl);
         const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
         L.base = b;
-        tile_total[t] = 2 * se;
+        put_tile_total(tile_total, leave_off, t, 2 * se);
         tile_base[t] = b;
-        tile_total[leave_off + t] = 2 * sl;
+        put_tile_total(tile_total, leave_off, leave_off + t, 2 * sl);
         tile_base[leave_off + t] = b + 2ull * se;
     }
     __syncthreads();
@@ -2428,12 +2390,11 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 // The flush's tail in one launch (it was three: a scan of the tile totals,
 // the tile copy and the bbox fold).  Blocks 0..R-1 take FT consecutive tile
 // entries each; a block's output offset is the sum of the tile totals before
-// it, found by a decoupled look-back over the blocks before it: each block
-// publishes its aggregate, then its inclusive prefix, in a 64-bit status
-// word tagged with the launch (so nothing is zeroed per flush).  Block R
+// it: the group totals (FG entries each) before its group, added by the pair
+// passes, then its own group's entries before it.  Block R
 // folds the bbox parts and writes the scalars of TickOut.
 #ifndef GWAOI_FT
-#define GWAOI_FT 16  // measured: 16 -> 15.6 us, 32 -> 19.0, 64 -> 25.3 (cfg3)
+#define GWAOI_FT 16  // measured (cfg3, group totals): 8 -> 12.4 us, 16 -> 11.4, 32 -> 13.7
 #endif
 constexpr int FT = GWAOI_FT;  // tile entries per finish block (<= 64: one wave scans them)
 static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
@@ -2474,7 +2435,7 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
 
 __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ tile_total,
                                                 const unsigned long long *__restrict__ tile_base, uint32_t n_entries,
-                                                uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag,
+                                                uint32_t n_enter_entries,
                                                 const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap,
                                                 const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
@@ -2541,17 +2502,22 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         cnt = l < (uint32_t)FT && e < n_entries ? tile_total[e] : 0u;
         incl = wave_incl_scan(cnt);
         const uint32_t agg = __shfl(incl, WAVE - 1);
-        if (l == 0) {
-            lb_store(lb + b, lb_word(tag, b == 0 ? LB_INCL : LB_AGG, agg));
-            s_agg = agg;
-        }
+        if (l == 0) s_agg = agg;
     }
-    uint32_t ex[1] = {0u};
-    // relies on in-order workgroup dispatch to terminate (see the look-back scans' comment above)
-    if (b) lookback<1>(lb, 0, b, tag, ex);  // (its barriers also publish s_agg)
+    // the offset: the totals of the groups before e0's, then its group's entries before e0
+    __shared__ uint32_t s_pw[256 / WAVE];
+    {
+        const uint32_t *grp = tile_total + n_entries + 1, g = e0 / FG;
+        uint32_t p = 0;
+        for (uint32_t q = threadIdx.x; q < g; q += blockDim.x) p += grp[q];
+        for (uint32_t e = g * FG + threadIdx.x; e < e0; e += blockDim.x) p += tile_total[e];
+        p = wave_sum_u32(p);
+        if (lane() == 0) s_pw[threadIdx.x / WAVE] = p;
+    }
     __syncthreads();
-    const uint32_t excl = ex[0], agg = s_agg;
-    if (threadIdx.x == 0 && b != 0) lb_store(lb + b, lb_word(tag, LB_INCL, excl + agg));
+    uint32_t excl = 0;
+    for (uint32_t q = 0; q < blockDim.x / WAVE; ++q) excl += s_pw[q];
+    const uint32_t agg = s_agg;
     if (threadIdx.x < WAVE) {
         const uint32_t l = lane(), e = e0 + l;
         const uint32_t off = excl + incl - cnt;
@@ -2866,21 +2832,22 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
     }
 }
 
-// look-back status words: lo and hi per block
+// k_arrive re-zeroes the counted cells (no clearing pass over cnt64)
 bool scan_rezeroes_counts() { return true; }
 
-size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
+size_t incr_sort_tmp_elems(size_t cells) { return (size_t)cdiv(cells + 1, S64_TILE) + 1; }  // tile totals
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, uint32_t tag, hipStream_t st) {
+                      TickScalars *sc, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
     uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 2 (total_cells + 1) words
-    k_scan64_lb<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, tag & 0x3FFFFFFFu, cell_start, arr_pos, blk,
-                                         cdiv(n_total, 256), sc, p_cell_start, shift);
+    k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
+    k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
+                                      cdiv(n_total, 256), sc, p_cell_start, shift);
     if (n_total)
         k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
                                                      shift, perm, skeys);
@@ -2989,10 +2956,10 @@ void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream
                                         static_cast<const uint2 *>(events), static_cast<uint2 *>(dst), n_pairs);
 }
 
-size_t finish_lb_elems(size_t n_entries) { return (size_t)cdiv(n_entries, FT) + 1; }
+size_t tile_total_elems(size_t n_entries) { return n_entries + 1 + cdiv(n_entries, FG); }
 
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
-                   uint32_t n_enter_entries, unsigned long long *lb, uint32_t tag, const uint32_t *tmp_pairs,
+                   uint32_t n_enter_entries, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
                    uint32_t *dcount, hipStream_t st) {
@@ -3000,7 +2967,7 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
     const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     if (!n_new) tile_order = nullptr;
     k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
-        tile_total, tile_base, n_entries, n_enter_entries, lb, tag & 0x3FFFFFFFu, reinterpret_cast<const uint2 *>(tmp_pairs),
+        tile_total, tile_base, n_entries, n_enter_entries, reinterpret_cast<const uint2 *>(tmp_pairs),
         reinterpret_cast<uint2 *>(out_pairs), cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox,
         n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount);
 }

@@ -243,8 +243,6 @@ struct gwaoi_world {
     uint32_t *events_tmp = nullptr;  // evtmp_cap pairs: per-tile chunks at reserved offsets (shared by the sets)
     uint64_t evtmp_cap = 0;
     uint32_t *tile_total = nullptr;
-    unsigned long long *tile_lb = nullptr;  // k_finish look-back status words
-    uint32_t lb_tag = 0;  // look-back launches so far (tags: k_finish, the incremental sort's scan)
     unsigned long long *tile_base = nullptr;
     size_t tile_entries_cap = 0;
     float *blk = nullptr;        // keygen per-block partials
@@ -470,15 +468,13 @@ int ensure_tile_entries(gwaoi_world *w, size_t entries) {
     size_t cap = std::max<size_t>(entries + 1 + entries / 4, 1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->tile_total);
-    dfree(w->tile_lb);
     dfree(w->tile_base);
     int rc;
-    if ((rc = dalloc(w, &w->tile_total, cap)) || (rc = dalloc(w, &w->tile_lb, gw::finish_lb_elems(cap))) ||
+    if ((rc = dalloc(w, &w->tile_total, gw::tile_total_elems(cap))) ||
         (rc = dalloc(w, &w->tile_base, cap))) {
         w->tile_entries_cap = 0;
         return rc;
     }
-    HIP_TRY(hipMemsetAsync(w->tile_lb, 0, gw::finish_lb_elems(cap) * sizeof(unsigned long long), w->stream));  // tag 0: never current
     w->tile_entries_cap = cap;
     return GWAOI_OK;
 }
@@ -768,21 +764,6 @@ uint32_t *last_events(gwaoi_world *w) { return w->fs[w->last_set].events; }
 // Pair passes + deterministic reorder.  Block-total entries: [enter totals:
 // new-frame blocks | previous-frame blocks] then [leave totals: same order];
 // their exclusive scan is the final layout [enters | leaves] in block order.
-// A look-back tag not used by an earlier launch (tags are 30 bits; 0 = never written).
-// When the tag wraps, the status words are zeroed first, so that a word left by a launch
-// 2^30 tags ago (possibly of a larger grid) can never carry a current tag.
-uint32_t next_lb_tag(gwaoi_world *w) {
-    if (++w->lb_tag % 0x40000000u == 0) {
-        ++w->lb_tag;
-        if (w->tile_lb)
-            (void)hipMemsetAsync(w->tile_lb, 0, gw::finish_lb_elems(w->tile_entries_cap) * sizeof(unsigned long long),
-                                 w->stream);
-        if (w->scan64_tmp)
-            (void)hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(w->cnt64_cap) * sizeof(unsigned long long),
-                                 w->stream);
-    }
-    return w->lb_tag;
-}
 
 // Returns the event capacity the passes were given (what the flush's finish must compare the total
 // against: the set's buffer or the shared scratch may grow later, by another flush's regrow).
@@ -812,7 +793,7 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
     stage_end(w, S, ST_SPECIAL);
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
     stage_begin(w, S, ST_FINISH);
-    gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->tile_lb, next_lb_tag(w), w->events_tmp, S.events,
+    gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->events_tmp, S.events,
                       cap, S.sc, reinterpret_cast<gw::TickOut *>(S.d_hout), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
                       reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
@@ -920,10 +901,10 @@ int tick_launch(gwaoi_world *w) {
     if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
                             gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
-                            entries + 1, dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
+                            gw::tile_total_elems(entries), dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
                             w->max_slots, w->sinfo, tick_id, st);
     else
-        gw::launch_prologue(S.sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, entries + 1, dev_bbox(S),
+        gw::launch_prologue(S.sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, gw::tile_total_elems(entries), dev_bbox(S),
                             w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark, w->max_slots, w->sinfo,
                             tick_id, st);
 
@@ -1002,7 +983,7 @@ int tick_launch(gwaoi_world *w) {
     if (incr) {
         gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             Fn.key, w->blk, S.sc, next_lb_tag(w), st);  // the sorted keys ARE the frame's
+                             Fn.key, w->blk, S.sc, st);  // the sorted keys ARE the frame's
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -1150,7 +1131,7 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
         }
         if ((rc = ensure_events(w, S, r.total64))) return poison(w, rc);
         (void)hipGetLastError();  // a failure of an unrelated earlier call is not this re-run's
-        gw::launch_zero(w->tile_total, f.entries + 1, st);
+        gw::launch_zero(w->tile_total, gw::tile_total_elems(f.entries), st);
         gw::launch_zero(reinterpret_cast<uint32_t *>(&S.sc->counter), 2, st);
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
         if (launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true) < r.total64) {
@@ -1295,7 +1276,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_lb); dfree(w->tile_base);
+    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_base);
     dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);

@@ -1,4 +1,4 @@
-"""CPU model of the incremental frame sort (gwaoi_kernels.hip k_scan64_lb / k_arrive /
+"""CPU model of the incremental frame sort (gwaoi_kernels.hip k_scan64 / k_arrive /
 k_cell_merge): the per-cell shift rule for stayers of unchanged cells plus the merge of changed
 cells must equal the stable sort of S' by the new cell keys.  The GPU kernels are checked
 against the oracle by tests/test_gpu_parity.py; this test pins the rule they implement."""
@@ -15,7 +15,7 @@ def incremental_sort_model(p_key, key, n_cells, sentinel):
     dep = np.bincount(old[ch & (old != sentinel)], minlength=n_cells + 1)[:n_cells + 1]
     ea = np.concatenate([[0], np.cumsum(arr)])[:n_cells + 1]
     ed = np.concatenate([[0], np.cumsum(dep)])[:n_cells + 1]
-    start = pcs + ea - ed                     # k_scan64_lb: new cell_start
+    start = pcs + ea - ed                     # k_scan64: new cell_start
     changed = (arr | dep) != 0
     n_new = int((key != sentinel).sum())
     perm = np.full(n_new, -1)
