@@ -340,7 +340,7 @@ constexpr int SC_T = 256;
 constexpr int SC_I = 16;
 constexpr int SC_TILE = SC_T * SC_I;
 #ifndef GWAOI_S64_I
-#define GWAOI_S64_I 16  // cells per thread of the incremental sort's cell scan (k_scan64)
+#define GWAOI_S64_I 4  // cells per thread of the cell scan (k_scan64); measured (cfg3): 2 -> 10.3 us, 4 -> 8.2, 8 -> 8.7, 16 -> 13.6
 #endif
 constexpr int S64_I = GWAOI_S64_I;
 constexpr uint32_t FG = 256;  // measured (cfg3 k_finish): 128 -> 11.8 us, 256 -> 11.4, 512 -> 11.7
