@@ -1083,7 +1083,7 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
 // others): the stayers are the entries of c's previous run whose new key is
 // still c (S' index order), the arrivals arr_idx[arr_pos[c-1], arr_pos[c])
 // are sorted by S' index (insertion sort: a cell rarely gets more than a few)
-// and merged in.  Writes the frame's permutation and keys.
+// and placed around the stayers.  Writes the frame's permutation and keys.
 __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const uint32_t *__restrict__ cell_start,
                              const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                              uint32_t *arr_idx, uint32_t total_cells, uint32_t n_new, uint32_t n_total,
@@ -1111,23 +1111,33 @@ __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const ui
         }
         arr_idx[j] = v;
     }
-    uint32_t i = p_cell_start[c];
-    const uint32_t ie = p_cell_start[c + 1];
+    // An arrival is new to c, so its S' index lies outside c's previous run [ps, pe) (which
+    // holds exactly the entries whose previous key is c): the cell's order is the arrivals
+    // below ps, the stayers in run order, then the arrivals past pe -- no merge.
+    const uint32_t ps = p_cell_start[c], pe = p_cell_start[c + 1];
     uint32_t a = ab;
-    uint32_t nxt = a < ae ? arr_idx[a] : 0xFFFFFFFFu;
-    while (o < oe) {
-        while (i < ie && keys[i] != c) ++i;  // skip the entries that left
-        const uint32_t st = i < ie ? i : 0xFFFFFFFFu;
-        uint32_t v;
-        if (st < nxt) {
-            v = st;
-            ++i;
-        } else {
-            v = nxt;
-            ++a;
-            nxt = a < ae ? arr_idx[a] : 0xFFFFFFFFu;
-        }
+    for (; a < ae; ++a) {
+        const uint32_t v = arr_idx[a];
+        if (v >= ps || o >= oe) break;
         perm[o] = v;
+        skeys[o] = c;
+        ++o;
+    }
+    constexpr uint32_t MU = 4;  // run keys in flight per step; measured (cfg3 k_cell_merge): 1 -> 11.9 us, 4 -> 10.2, 8 -> 10.1; two-way merge 13.4
+    for (uint32_t i = ps; i < pe; i += MU) {
+        uint32_t k[MU];
+#pragma unroll
+        for (uint32_t u = 0; u < MU; ++u) k[u] = i + u < pe ? keys[i + u] : sentinel;
+#pragma unroll
+        for (uint32_t u = 0; u < MU; ++u)
+            if (k[u] == c && o < oe) {
+                perm[o] = i + u;
+                skeys[o] = c;
+                ++o;
+            }
+    }
+    for (; a < ae && o < oe; ++a) {
+        perm[o] = arr_idx[a];
         skeys[o] = c;
         ++o;
     }

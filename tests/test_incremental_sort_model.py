@@ -1,6 +1,6 @@
 """CPU model of the incremental frame sort (gwaoi_kernels.hip k_scan64 / k_arrive /
-k_cell_merge): the per-cell shift rule for stayers of unchanged cells plus the merge of changed
-cells must equal the stable sort of S' by the new cell keys.  The GPU kernels are checked
+k_cell_merge): the per-cell shift rule for stayers of unchanged cells plus the three-part layout
+of changed cells must equal the stable sort of S' by the new cell keys.  The GPU kernels are checked
 against the oracle by tests/test_gpu_parity.py; this test pins the rule they implement."""
 import numpy as np
 import pytest
@@ -24,11 +24,14 @@ def incremental_sort_model(p_key, key, n_cells, sentinel):
         c = key[i]
         if not changed[c]:
             perm[i + start[c] - pcs[c]] = i
-    # k_cell_merge: changed cells merge their stayers with the arrivals, by S' index
+    # k_cell_merge: a changed cell is [arrivals below its previous run] [stayers] [arrivals past
+    # it]: an arrival's S' index never lies inside the run (the run is exactly the entries whose
+    # previous key is c), so the three parts are already in S' index order
     for c in np.nonzero(changed[:n_cells])[0]:
         stay = [i for i in range(pcs[c], pcs[c + 1]) if key[i] == c]
-        arrivals = np.nonzero(ch & (key == c))[0].tolist()
-        run = sorted(stay + arrivals)
+        arrivals = sorted(np.nonzero(ch & (key == c))[0].tolist())
+        assert not any(pcs[c] <= v < pcs[c + 1] for v in arrivals)
+        run = [v for v in arrivals if v < pcs[c]] + stay + [v for v in arrivals if v >= pcs[c + 1]]
         assert start[c] + len(run) == start[c + 1]
         perm[start[c]:start[c] + len(run)] = run
     return perm, start
