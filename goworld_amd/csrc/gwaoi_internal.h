@@ -209,11 +209,11 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // stayed with the arrivals.  Writes perm / skeys like radix_sort and the
 // frame's cell_start (so no separate cell count).  tmp: incr_sort_tmp_elems
 // words (the cell scan's tile totals);
-// arr_pos: 2 (total_cells + 1) words (arrival cursors, then per-cell shifts).
+// arr_pos: 3 (total_cells + 1) words (arrival cursors, per-cell shifts, changed cells).
 size_t incr_sort_tmp_elems(size_t cells);
 // true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
 bool scan_rezeroes_counts();
-void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, uint32_t n_new, const uint32_t *p_key,
+void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,

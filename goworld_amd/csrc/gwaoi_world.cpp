@@ -528,8 +528,8 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
     dfree(w->arr_pos);
     w->cnt64_cap = 0;
     int rc;
-    // arr_pos: the arrival cursors, then the per-cell stayer shifts (incremental_sort)
-    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 2 * cap)) ||
+    // arr_pos: the arrival cursors, the per-cell stayer shifts, the changed cells (incremental_sort)
+    if ((rc = dalloc(w, &w->cnt64, cap)) || (rc = dalloc(w, &w->arr_pos, 3 * cap)) ||
         (rc = dalloc(w, &w->scan64_tmp, gw::incr_sort_tmp_elems(cap))))
         return rc;
     HIP_TRY(hipMemsetAsync(w->scan64_tmp, 0, gw::incr_sort_tmp_elems(cap) * sizeof(unsigned long long), w->stream));
@@ -981,7 +981,7 @@ int tick_launch(gwaoi_world *w) {
     stage_begin(w, S, ST_SORT);
     int which = 1;
     if (incr) {
-        gw::incremental_sort(w->keys[0], n_total, n_prev, n_new, P.key, P.cell_start, w->cnt64, total_cells,
+        gw::incremental_sort(w->keys[0], n_total, n_prev, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
                              Fn.key, w->blk, S.sc, st);  // the sorted keys ARE the frame's
     } else {
