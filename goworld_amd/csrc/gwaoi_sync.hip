@@ -51,10 +51,8 @@ __host__ __device__ inline uint32_t id_hash(uint32_t a, uint32_t b, uint32_t c, 
     return (uint32_t)h;
 }
 
-// Streaming 16-B store (0): the fan-out's output and scratch are
-// written once and read by another kernel, so they need not take L2 lines
-// from the sender records the record gathers re-read.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// The fan-out's 16-B output and scratch stores.  Plain stores: the non-temporal form was
+// slower.
 __device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
     *p = v;
 }
