@@ -1686,7 +1686,6 @@ constexpr int CW = CT / WAVE;
 #ifndef GWAOI_EVW
 #define GWAOI_EVW 192
 #endif
-typedef unsigned int cand_v4_t __attribute__((ext_vector_type(4)));
 #ifndef GWAOI_SW_U
 #define GWAOI_SW_U 4  // candidates per lane per sweep iteration on long rows
 #endif
@@ -1748,9 +1747,6 @@ __device__ __forceinline__ void drain_queue(const uint32_t *qb, const uint8_t *q
                                          float thr, uint32_t &ne, uint32_t &nl, uint2 *out, uint64_t cap,
                                          unsigned long long pe, unsigned long long pl, bool replay) {
     const uint32_t ln = lane();
-#ifdef GWAOI_EXP_NODRAIN  // timing experiment only: survivors are dropped (events wrong)
-    return;
-#endif
     for (uint32_t q0 = 0; q0 < qn; q0 += WAVE) {
         const uint32_t e = q0 + ln;
         int kind = 0;
@@ -1856,12 +1852,7 @@ __device__ __forceinline__ bool band_keep(const LaneA &A, const CombinedCtx &C, 
     const float dold = fmaxf(fabsf(dxo), fabsf(dzo));
     // (dn <= in_max && dold <= in_max) || (dn > out_min && dold > out_min), as one max and one min
     // (a band hit is near at t and t-1: finite positions, no NaN operand)
-#if GWAOI_SAME_4CMP
-    const bool same =
-        ((int)(dn <= C.in_max) & (int)(dold <= C.in_max)) | ((int)(dn > C.out_min) & (int)(dold > C.out_min));
-#else
     const bool same = (int)(fmaxf(dn, dold) <= C.in_max) | (int)(fminf(dn, dold) > C.out_min);
-#endif
     return band & !same;
 }
 
@@ -1885,38 +1876,12 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
             Q.qn = 0;
         }
         uint4 k[U];
-#if defined(GWAOI_EXP_8B)  // timing experiment only: 8-B candidate loads (old position = new; events wrong)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint2 h = reinterpret_cast<const uint2 *>(cand)[2 * (t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u)];
-            k[u] = make_uint4(h.x, h.y, h.x, h.y);
-        }
-#elif 0
-        {
-            // raw buffer loads: one per-lane offset per iteration (the u-th record by the
-            // instruction's immediate offset), no per-candidate index select -- a record past the
-            // lane's range is ignored by the (t + u < len) mask, one past the frame reads as 0
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4 *>(cand), 0, (int)(F.n * 16u), 0x00020000);
-            const int vo = (int)((jb + t) * 16u);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const cand_v4_t q = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 16 * u, 0);  // u by soffset
-                k[u] = make_uint4(q.x, q.y, q.z, q.w);
-            }
-        }
-#else
 #pragma unroll
         for (int u = 0; u < U; ++u) k[u] = cand[t + (uint32_t)u < len ? jb + t + (uint32_t)u : 0u];
-#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t b = jb + t + (uint32_t)u;
             const bool keep = band_keep<MODE>(A, C, k[u], b) & (t + (uint32_t)u < len);
-#ifdef GWAOI_EXP_NOPUSH  // timing experiment only: the filter runs, nothing is queued (events wrong)
-            if (keep && k[u].w == 0x7FFFFFFFu) Q.ne += 1000;
-            continue;
-#endif
             qpush(L.qb[w], L.qa[w], Q, keep, A.a & (uint32_t)(CT - 1), b);
         }
     }
