@@ -483,18 +483,12 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
         for k in range(len(pb)):
             if k + 1 < len(pb):
                 issue.append(time.perf_counter())
-                # batch t+1's H2D is queued while flush t runs and t-1's events are still being copied out
-                w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])
-                if k:
-                    take(copy=False)  # tick t-1's events in host memory
-                    lat.append(time.perf_counter() - issue[k - 1])
-                end_begin()  # finish t, queue t+1, start t's copy-out (no wait for it)
+                w.moved_batch_pinned(pb[k + 1][1], pb[k + 1][2])  # batch t+1's H2D, queued while flush t runs
+                end_begin()  # finish t, queue t+1, start t's copy-out
+                take(copy=False)  # tick t's events in host memory (flush t+1 keeps the GPU busy meanwhile)
             else:
-                if k:
-                    take(copy=False)
-                    lat.append(time.perf_counter() - issue[k - 1])
                 w.tick_end(copy=False)
-                lat.append(time.perf_counter() - issue[k])
+            lat.append(time.perf_counter() - issue[k])
         return time.perf_counter() - t0, lat
 
     pb = bufs[3 + n_ser:3 + n_ser + n_pip]
@@ -559,10 +553,10 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
                                 "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(g_lat)},
             "note": "pinned: each tick's moves in a caller-owned pinned buffer (gwaoi_pinned_alloc, filled before "
                     "timing as a game server fills it while packets arrive), one H2D per tick, checked on the "
-                    "device; pipelined = batch t+1 queued while flush t runs, the events of t-1 taken, then "
-                    "gwaoi_tick_end_begin_pairs_async (flush t+1 queued before t's summary, t's copy-out started: "
-                    "one event per mirrored pair (a,b)/(b,a), the pair list gwaoi_pairs_host returns, from which "
-                    "the callbacks of both entities follow); directed_events_out = the same ticks copying every "
+                    "device; pipelined = batch t+1 queued while flush t runs, then gwaoi_tick_end_begin_pairs_async "
+                    "(flush t+1 queued before t's summary, t's copy-out started: one event per mirrored pair "
+                    "(a,b)/(b,a), from which the callbacks of both entities follow), then t's pairs taken "
+                    "(gwaoi_pairs_host) while flush t+1 runs; directed_events_out = the same ticks copying every "
                     "directed event (gwaoi_tick_end_begin_async + gwaoi_events_host).  Tick latency = batch call "
                     "-> events in pinned host memory.  PCIe here carries one direction at a time "
                     "(tools/pcie_probe.py), so a pipelined tick costs H2D + D2H.  stage_commit = the caller "
