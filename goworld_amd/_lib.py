@@ -105,7 +105,8 @@ class WireGroups(C.Structure):
 class Debug(C.Structure):
     _fields_ = [("flushes", C.c_uint64), ("combined_replays", C.c_uint64), ("combined_queue_drains", C.c_uint64),
                 ("special_global", C.c_uint64), ("event_regrows", C.c_uint64), ("speculative_launches", C.c_uint64),
-                ("cell_size_switches", C.c_uint64), ("cells_per_dist", C.c_uint32), ("pad", C.c_uint32)]
+                ("cell_size_switches", C.c_uint64), ("cells_per_dist", C.c_uint32), ("pad", C.c_uint32),
+                ("incremental_sorts", C.c_uint64)]
 
 
 class StageTime(C.Structure):

@@ -981,6 +981,7 @@ int tick_launch(gwaoi_world *w) {
     stage_begin(w, S, ST_SORT);
     int which = 1;
     if (incr) {
+        w->dbg.incremental_sorts++;
         gw::incremental_sort(w->keys[0], n_total, n_prev, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
                              Fn.key, w->blk, S.sc, st);  // the sorted keys ARE the frame's

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GWAOI_ABI_VERSION 2
+#define GWAOI_ABI_VERSION 3
 
 typedef struct gwaoi_world gwaoi_world;
 
@@ -111,6 +111,7 @@ typedef struct {
     uint64_t cell_size_switches;    /* flushes that rebuilt every grid with another automatic cell size      */
     uint32_t cells_per_dist;        /* cells per AOI distance of the grids in use (2 or 3 when automatic)    */
     uint32_t pad;
+    uint64_t incremental_sorts;     /* flush launches whose frame sort was the per-cell merge (grid unchanged) */
 } gwaoi_debug;
 
 typedef struct {

@@ -648,6 +648,70 @@ def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
         wi.close()
 
 
+def test_incremental_sort_pileup_gpu(monkeypatch, oracle_mod):
+    """Crowds piling into and draining out of a few cells, grid unchanged: hot cells
+    get hundreds of arrivals a flush -- from below and above their previous run in S'
+    order, and appended entries -- while others lose most of their run.  k_cell_merge's
+    three-part layout and its per-tile changed-cell lists must still give the stable sort:
+    event arrays, order included, equal those of the radix-sort path, and the oracle's."""
+    rng = np.random.default_rng(21)
+    n, D, L = 4000, 100.0, 3000.0
+    x = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
+    z = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
+    x[:4], z[:4] = [-L / 2, L / 2, -L / 2, L / 2], [-L / 2, -L / 2, L / 2, L / 2]  # fixed corners: same grid
+    hot = np.array([[-700.0, 300.0], [0.0, 0.0], [650.0, -420.0]], np.float32)
+    monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
+    wr = World(n + 400, cells_per_dist=3.0)  # a fixed cell size: the grid stays the same all along
+    monkeypatch.delenv("GWAOI_FORCE_RADIX")
+    wi = World(n + 400, cells_per_dist=3.0)
+    ref = oracle_mod.SpacesOracle({0: D}, n + 400)
+    try:
+        slots = np.arange(n, dtype=np.uint32)
+        for w in (wr, wi):
+            sp = w.space_create(D)
+            w.enter_batch(sp, slots, x, z)
+            w.tick()
+        for i in range(n):
+            ref.enter(0, i, x[i], z[i])
+        ref.take_events(with_space=True)
+        live, spare = set(range(4, n)), list(range(n, n + 400))
+        for t in range(6):
+            mv = rng.choice(sorted(live), 500, replace=False).astype(np.uint32)
+            h = hot[rng.integers(0, 3, mv.size)] if t < 4 else rng.uniform(-L / 2, L / 2, (mv.size, 2)).astype(np.float32)
+            nx = (h[:, 0] + rng.uniform(-6, 6, mv.size)).astype(np.float32)  # into one or two cells
+            nz = (h[:, 1] + rng.uniform(-6, 6, mv.size)).astype(np.float32)
+            leavers = rng.choice(sorted(set(live) - set(int(v) for v in mv)), 30, replace=False)
+            enter = np.array([spare.pop() for _ in range(40)], np.uint32)
+            eh = hot[rng.integers(0, 3, enter.size)]
+            ex = (eh[:, 0] + rng.uniform(-6, 6, enter.size)).astype(np.float32)
+            ez = (eh[:, 1] + rng.uniform(-6, 6, enter.size)).astype(np.float32)
+            outs = []
+            for w in (wr, wi):
+                w.moved_batch(mv, nx, nz)
+                w.leave_batch(leavers)
+                w.enter_batch(0, enter, ex, ez)
+                outs.append(w.tick())
+            for i, a, b in zip(mv, nx, nz):
+                ref.moved(int(i), a, b)
+            for i in leavers:
+                ref.leave(int(i))
+            for i, a, b in zip(enter, ex, ez):
+                ref.enter(0, int(i), a, b)
+            oe, ol = oracle_mod.net_events(*ref.take_events(with_space=True))
+            live = (live - set(int(v) for v in leavers)) | set(int(v) for v in enter)
+            spare.extend(int(v) for v in leavers)
+            (er, lr), (ei, li) = outs
+            np.testing.assert_array_equal(er, ei)
+            np.testing.assert_array_equal(lr, li)
+            np.testing.assert_array_equal(pair_keys(ei), oe)
+            np.testing.assert_array_equal(pair_keys(li), ol)
+        assert wi.debug_counters()["incremental_sorts"] == 6
+        assert wr.debug_counters()["incremental_sorts"] == 0
+    finally:
+        wr.close()
+        wi.close()
+
+
 def test_virtual_sprime_equals_copied_sprime_gpu(monkeypatch):
     """A flush of Moved batches only skips the prologue's copy of the previous
     frame (k_keygen takes the records no op wrote from the previous frame, by
