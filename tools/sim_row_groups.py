@@ -3,8 +3,9 @@ wave, the groups of two rows of the merged strips and their 128-position chunks,
 runs them and with each lane's empty rows dropped first.
     python tools/sim_row_groups.py"""
 import numpy as np, sys, os
-sys.path.insert(0, '/root/repo')
-exec(open('/root/repo/tools/sim_sweep_slots.py').read().split("print(\"rows Z mean")[0].replace("float(sys.argv[1]) if len(sys.argv) > 1 else 4", "3.0"))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+exec(open(os.path.join(HERE, 'sim_sweep_slots.py')).read().split("print(\"rows Z mean")[0].replace("float(sys.argv[1]) if len(sys.argv) > 1 else 4", "3.0"))
 # merged list per lane: X' rows below zr0, then Z rows
 NXr = int(2 * c + 3)
 lists = []
