@@ -772,9 +772,13 @@ def run_strips(args, ws, rank, local, dist):
             phases[2] += time.perf_counter() - c
         return int(counts.sum() - counts[rank]), int(recv.shape[0]), prev
 
-    one(init_ops)
+    t_gen = time.perf_counter() - t_setup
+    ph0 = [0.0, 0.0, 0.0]
+    one(init_ops, ph0)
     ne0, nl0 = sh.wait()
     setup_s = time.perf_counter() - t_setup
+    print(f"[cfg5 rank {rank}] setup {setup_s:.2f} s: inputs {t_gen:.2f}, populate route {ph0[0]:.2f} / exchange "
+          f"{ph0[1]:.2f} / queue {ph0[2]:.2f}, flush wait {setup_s - t_gen - sum(ph0):.2f}", file=sys.stderr, flush=True)
     for t in range(args.warmup):
         one(ops[t])
     sh.wait()
