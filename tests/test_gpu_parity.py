@@ -648,6 +648,49 @@ def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
         wi.close()
 
 
+@pytest.mark.parametrize("n", [255, 257, 4095, 4097, 16383, 16385, 32769])
+def test_chain_free_offsets_at_tile_boundaries_gpu(monkeypatch, oracle_mod, n):
+    """Frame sizes either side of the block boundaries of the chain-free offsets (the cell scan's
+    tiles, k_finish's groups of 256 tile entries, the combined pass's tiles): three churned
+    flushes, incremental and radix paths equal (order included) and equal to the oracle."""
+    rng = np.random.default_rng(n)
+    wl = make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wl.initial()
+    monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
+    wr = World(n, cells_per_dist=3.0)
+    monkeypatch.delenv("GWAOI_FORCE_RADIX")
+    wi = World(n, cells_per_dist=3.0)
+    ref = oracle_mod.SpacesOracle({0: wl.D}, n)
+    try:
+        for w in (wr, wi):
+            sp = w.space_create(wl.D)
+            w.enter_batch(sp, slots, x0, z0)
+            w.tick()
+        for i in range(n):
+            ref.enter(0, int(slots[i]), x0[i], z0[i])
+        ref.take_events(with_space=True)
+        for t in range(3):
+            sl, nx, nz = wl.tick(t)
+            jump = rng.choice(sl.size, max(1, sl.size // 50), replace=False)
+            nx[jump] += rng.uniform(-400, 400, jump.size).astype(np.float32)
+            outs = []
+            for w in (wr, wi):
+                w.moved_batch(sl, nx, nz)
+                outs.append(w.tick())
+            for i, a, b in zip(sl, nx, nz):
+                ref.moved(int(i), a, b)
+            oe, ol = oracle_mod.net_events(*ref.take_events(with_space=True))
+            (er, lr), (ei, li) = outs
+            np.testing.assert_array_equal(er, ei)
+            np.testing.assert_array_equal(lr, li)
+            np.testing.assert_array_equal(pair_keys(ei), oe)
+            np.testing.assert_array_equal(pair_keys(li), ol)
+        assert wi.debug_counters()["incremental_sorts"] >= 1
+    finally:
+        wr.close()
+        wi.close()
+
+
 def test_incremental_sort_pileup_gpu(monkeypatch, oracle_mod):
     """Crowds piling into and draining out of a few cells, grid unchanged: hot cells
     get hundreds of arrivals a flush -- from below and above their previous run in S'
