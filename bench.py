@@ -32,6 +32,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+T_START = time.perf_counter()  # the process's start, for the child job's phase clock
 METRIC = "AOI entity-moves/sec + enter/leave events/sec at 1M entities; p99 tick ms"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -303,13 +304,35 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def cpu_cores() -> int:
-    """Host cores this process may use (the GPU box gives a 16-core share)."""
+def cpu_core_counts() -> dict:
+    """Host cores: the affinity mask's count, the cgroup CPU quota in cores (cgroup v2 cpu.max or
+    v1 cfs quota / period; None when unlimited), and the number used = the smaller of the two.
+    On the GPU box the affinity mask shows the whole machine while the quota is the box's share."""
     try:
-        c = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        c = os.cpu_count() or 1
-    return max(1, min(16, c))
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fq, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fp:
+                q, per = int(fq.read()), int(fp.read())
+                if q > 0:
+                    quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    used = max(1, min(aff, quota) if quota else aff)
+    return {"affinity": aff, "cgroup_quota": quota, "used": used}
+
+
+def cpu_cores() -> int:
+    """Host cores the CPU comparators use: the affinity count, bounded by the cgroup quota."""
+    return cpu_core_counts()["used"]
 
 
 def cpu_baseline_spaces(args, target_s: float):
@@ -352,7 +375,7 @@ def cpu_baseline_spaces(args, target_s: float):
     dt = time.perf_counter() - t0
     ev = sum(sum(w[0].counts()) for w in work)
     return {"value": sum(done) / dt, "unit": "entity-moves/s", "events_per_s": ev / dt, "cores": cores,
-            "nproc": os.cpu_count(), "kind": "port",
+            "nproc": os.cpu_count(), "core_counts": cpu_core_counts(), "kind": "port",
             "sample": f"{cores} independent cfg4 spaces (2000 entities each), one per core, every entity "
                       f"moving each tick ({sum(done)} Moved calls), sequential XZ-list restatement, {dt:.1f} s"}
 
@@ -378,7 +401,7 @@ def cpu_grid_baseline(args, target_s: float):
         t += 1
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "entity-moves/s", "ms_per_tick": dt / t * 1e3, "events_per_s": ev / dt,
-            "cores": cores, "kind": "port",
+            "cores": cores, "core_counts": cpu_core_counts(), "kind": "port",
             "sample": f"{t} whole cfg3 ticks ({wl.n} entities, every entity moving), relation recomputed on a cell "
                       f"grid and diffed per tick on {cores} threads, {dt:.1f} s"}
 
@@ -566,6 +589,74 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
                     "gwaoi_moved_batch"}
 
 
+def line_summary(out: dict) -> dict:
+    """The headline numbers of every leg, compact, at the end of the JSON line (a driver that keeps
+    the tail of stdout keeps these)."""
+    def g(d, *ks):
+        for k in ks:
+            if not isinstance(d, dict):
+                return None
+            d = d.get(k)
+        return round(d, 4) if isinstance(d, float) else d
+    cfg5 = out.get("cfg5_strips") or {}
+    return {
+        "ms_per_step": g(out, "ms_per_step"), "p99_tick_ms": g(out, "p99_tick_ms"),
+        "combined_ms": g(out, "roofline", "avg_launch_ms"), "roofline_frac": g(out, "roofline", "frac"),
+        "host_to_host_tick_ms": g(out, "host_to_host_tick", "ms_per_step"),
+        "host_to_host_p50_ms": g(out, "host_to_host_tick", "p50_tick_ms"),
+        "host_to_host_p99_ms": g(out, "host_to_host_tick", "p99_tick_ms"),
+        "host_to_host_serial_p99_ms": g(out, "host_to_host_tick", "serial_p99_tick_ms"),
+        "host_tick_with_replay_ms": g(out, "host_tick", "ms_per_tick"),
+        "small_flush_p50_ms": {k: g(v, "device", "p50_ms") for k, v in (out.get("small_flush") or {}).items()
+                               if isinstance(v, dict)},
+        "sync_decode_flush_ms": g(out, "sync_leg", "decode_flush_ms"), "sync_collect_ms": g(out, "sync_leg", "collect_ms"),
+        "cfg4_ms_per_step": g(out, "cfg4_strong", "ms_per_step"),
+        "cfg5_ms_per_step": g(cfg5, "ms_per_step"), "cfg5_error": cfg5.get("error"),
+        "cfg5_job_wall_s": g(cfg5, "job", "wall_s"),
+        "cpu_port_moves_per_s": g(out, "cpu_baseline", "value"),
+        "cpu_grid_ms_per_tick": g(out, "cpu_baseline", "cpu_grid", "ms_per_tick"),
+    }
+
+
+def small_flush_leg(w, last, reps: int, sizes=(1, 64, 4096, 65536)):
+    """What one flush of k Moved calls costs on the config-3 world (1M entities): the game
+    loop's price for read-after-write interest sets (a flush after each timer callback that
+    moves entities).  k random entities move U(-1,1) from their current
+    positions; the wall clock runs from the host batch call to the flush's events in HBM
+    (gwaoi_moved_batch + gwaoi_tick_device), and again with the events copied to host memory
+    (gwaoi_tick).  Events are checked for nothing here (the parity tests do that)."""
+    sl, x, z = (np.array(a) for a in last)
+    rng = np.random.default_rng(0x5EEDF1)
+    out = {}
+    for k in sizes:
+        res = {}
+        for mode in ("device", "host"):
+            ts, evs, sparse0 = [], [], w.debug_counters().get("sparse_flushes", 0)
+            for r in range(reps + 3):
+                idx = rng.choice(sl.size, k, replace=False)
+                x[idx] += rng.uniform(-1.0, 1.0, k).astype(np.float32)
+                z[idx] += rng.uniform(-1.0, 1.0, k).astype(np.float32)
+                bs, bx, bz = sl[idx], x[idx], z[idx]
+                a = time.perf_counter()
+                w.moved_batch(bs, bx, bz)
+                if mode == "device":
+                    ne, nl = w.tick_device()
+                else:
+                    e, l = w.tick()
+                    ne, nl = len(e), len(l)
+                if r >= 3:
+                    ts.append(time.perf_counter() - a)
+                    evs.append(ne + nl)
+            t = np.array(ts) * 1e3
+            res[mode] = {"p50_ms": round(float(np.percentile(t, 50)), 4), "p99_ms": round(float(np.percentile(t, 99)), 4),
+                         "mean_ms": round(float(t.mean()), 4), "events_mean": float(np.mean(evs)),
+                         "sparse_flushes": w.debug_counters().get("sparse_flushes", 0) - sparse0}
+        out[str(k)] = res
+    out["note"] = ("one flush of k Moved calls on the 1M-entity config-3 world, wall clock from the host batch call "
+                   "to the events (device: in HBM; host: in host memory); reps per size after 3 untimed")
+    return out
+
+
 def cfg4_leg(args, ws, rank, device, dist, red_dev):
     """Config 4 as a strong-scaling sub-record of every line: 8192 independent
     spaces x 2000 entities in total, sharded over the ranks in contiguous
@@ -720,6 +811,32 @@ def cfg5_cpu_baseline(x0, z0, ops0, target_s: float):
                     "~23k z-list nodes at this size) that is ~20 min, so the prefix is time-bounded instead"}
 
 
+class PhaseClock:
+    """Wall time of each phase of a (child) job, in seconds: kept for its JSON record and printed
+    to stderr as each phase ends, so that a run killed at its time limit still shows where its
+    time went.  t0: the process's start (perf_counter of main())."""
+
+    def __init__(self, tag: str, t0: float | None = None, pre: dict | None = None):
+        self.tag = tag
+        self.t0 = t0 if t0 is not None else time.perf_counter()
+        self.phases = dict(pre or {})
+        self.last = self.t0 + sum(self.phases.values())
+        self.mark("to_strip_setup")
+
+    def mark(self, name: str):
+        now = time.perf_counter()
+        self.phases[name] = round(now - self.last, 3)
+        self.last = now
+        print(f"[{self.tag}] {name} {self.phases[name]:.3f} s (at {now - self.t0:.2f} s)", file=sys.stderr, flush=True)
+
+    def note(self, **kv):
+        for k, v in kv.items():
+            self.phases[k] = round(v, 3)
+
+    def record(self) -> dict:
+        return dict(self.phases, total=round(time.perf_counter() - self.t0, 3))
+
+
 def run_strips(args, ws, rank, local, dist):
     """Config 5: one 2^24-entity space cut into one x-strip per rank; every
     tick routes the owned moves, exchanges halo records over RCCL (counts,
@@ -737,9 +854,11 @@ def run_strips(args, ws, rank, local, dist):
     from goworld_amd.workload import DeviceUniformWorkload
 
     dev = torch.device(f"cuda:{local}")
+    ph = PhaseClock(f"cfg5 rank {rank}", args.phases_t0, args.phases_pre)  # wall time per phase (JSON + stderr)
     if dist is not None:
         setup_count_group(dist)  # collective over every rank: the host count all-gather's gloo group
         dist.barrier()  # RCCL's communicator exists before the first batched send/recv
+        ph.mark("count_group_and_barrier")
     n = args.n or (1 << 24)
     t_setup = time.perf_counter()
     wl = DeviceUniformWorkload(n, 0x5EED0005, dev)
@@ -754,16 +873,23 @@ def run_strips(args, ws, rank, local, dist):
     ops0h = ops[0].cpu().numpy() if cpu_here else None
     del wl
     torch.cuda.synchronize()
+    ph.mark("inputs")
     sh = StripShard(n, float(D_CFG5), edges, rank, device=local, cells_per_dist=args.cells_per_dist)
+    ph.mark("strip_world_create")
     via_cpu = args.dist_backend == "gloo"
+
+    dev_counts = dist is not None and args.strip_counts == "device"
 
     def one(o, phases=None):
         a = time.perf_counter()
-        send, counts, tele = sh.route(o)  # the tick's one host wait; it completes the previous tick
+        # the tick's one host wait; it completes the previous tick.  Device counts: every strip's count
+        # row all-gathered on the world's stream before that wait (RCCL), no host collective per tick
+        send, counts, tele = sh.route(o, dist) if dev_counts else sh.route(o)
         prev = sh.wait()  # the previous tick's counts, completed by the route: no wait
         b = time.perf_counter()
         if dist is not None:
-            recv, tele_all, kinds = exchange(dist, send, counts, tele, via_cpu=via_cpu, kinds=sh.kinds)
+            recv, tele_all, kinds = exchange(dist, send, counts, tele, via_cpu=via_cpu, kinds=sh.kinds,
+                                             matrix=sh.matrix)
         else:
             recv, tele_all, kinds = exchange_local([(send, counts, tele)], kinds=[sh.kinds])[0]
         c = time.perf_counter()
@@ -774,16 +900,17 @@ def run_strips(args, ws, rank, local, dist):
             phases[2] += time.perf_counter() - c
         return int(counts.sum() - counts[rank]), int(recv.shape[0]), prev
 
-    t_gen = time.perf_counter() - t_setup
     ph0 = [0.0, 0.0, 0.0]
     one(init_ops, ph0)
+    ph.mark("populate_route_exchange_queue")
     ne0, nl0 = sh.wait()
+    ph.mark("populate_flush_wait")
     setup_s = time.perf_counter() - t_setup
-    print(f"[cfg5 rank {rank}] setup {setup_s:.2f} s: inputs {t_gen:.2f}, populate route {ph0[0]:.2f} / exchange "
-          f"{ph0[1]:.2f} / queue {ph0[2]:.2f}, flush wait {setup_s - t_gen - sum(ph0):.2f}", file=sys.stderr, flush=True)
+    ph.note(populate_route=ph0[0], populate_exchange=ph0[1], populate_queue=ph0[2])
     for t in range(args.warmup):
         one(ops[t])
     sh.wait()
+    ph.mark("warmup_ticks")
     w = sh.world
     w.set_stage_timing([] if args.no_timing else ["combined"])
     w.reset_stage_times()
@@ -809,17 +936,20 @@ def run_strips(args, ws, rank, local, dist):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ph.mark("timed_ticks")
     timed = w.stage_times() if not args.no_timing else {}
     info = w.info()
     el_max, (moves_all, events_all, halo_all, live_all, waits_all) = reduce_over_ranks(
         dist, elapsed, [n * args.steps / ws, events, sent, info["live"], waits],
         "cpu" if args.dist_backend == "gloo" else dev)
+    ph.mark("rank_reduction")
     cpu = None
     if cpu_here:
         try:
             cpu = cfg5_cpu_baseline(x0h, z0h, ops0h, args.cpu_seconds)
         except Exception as e:  # the baseline must not take the GPU number down with it
             cpu = {"error": repr(e)}
+        ph.mark("cpu_sample")
     if rank == 0:
         lat_ms = np.array(lat) * 1e3
         tm = {k: v[0] / max(v[1], 1) for k, v in timed.items() if v[1]}
@@ -846,7 +976,8 @@ def run_strips(args, ws, rank, local, dist):
             "halo_records_per_tick": halo_all / max(args.steps, 1),
             "halo_note": "records sent to other ranks (24 B each), all ranks",
             "host_waits_per_tick": waits_all / ws / max(args.steps, 1),
-            "strip_world_entities_sum": live_all, "setup_s": round(setup_s, 2),
+            "strip_world_entities_sum": live_all, "setup_s": round(setup_s, 2), "phases_s": ph.record(),
+            "strip_counts": args.strip_counts if dist is not None else "local",
             "rank0_phase_ms_per_tick": {"route_and_previous_tick_wait": round(phases[0] / args.steps * 1e3, 4),
                                         "exchange": round(phases[1] / args.steps * 1e3, 4),
                                         "tick_queue": round(phases[2] / args.steps * 1e3, 4)},
@@ -879,20 +1010,30 @@ def cfg5_job(args, ws, rank, local):
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port + 1 if port else _free_port()))
     cmd = [sys.executable, os.path.abspath(__file__), "--workload", "cfg5", "--gpus", str(ws), "--steps",
            str(args.cfg5_steps), "--warmup", str(args.cfg5_warmup), "--dist-backend", args.dist_backend,
-           "--json-out", out, "--cpu-seconds", str(args.cfg5_cpu_seconds)]
+           "--json-out", out, "--cpu-seconds", str(args.cfg5_cpu_seconds), "--strip-counts", args.strip_counts]
     if args.cfg5_entities:
         cmd += ["--entities", str(args.cfg5_entities)]
     if args.no_cpu_baseline or args.cfg5_cpu_seconds <= 0:
         cmd.append("--no-cpu-baseline")
     t0 = time.perf_counter()
-    p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL)
-    try:
-        rc = p.wait(timeout=args.cfg5_timeout)
-    except subprocess.TimeoutExpired:
-        p.kill()
-        p.wait()
-        rc = "timeout"
+    err_path = out + ".err"
+    with open(err_path, "w") as err_fh:
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=err_fh)
+        try:
+            rc = p.wait(timeout=args.cfg5_timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+            rc = "timeout"
     wall = round(time.perf_counter() - t0, 1)
+    try:  # the child's stderr, passed on, and its phase lines (where a slow or killed run spent its time)
+        with open(err_path) as fh:
+            err_text = fh.read()
+        os.unlink(err_path)
+    except OSError:
+        err_text = ""
+    sys.stderr.write(err_text)
+    phase_lines = [ln for ln in err_text.splitlines() if ln.startswith("[cfg5 rank")]
     if rank != 0:
         return None
     res = None
@@ -903,7 +1044,7 @@ def cfg5_job(args, ws, rank, local):
     except (OSError, ValueError, IndexError):
         pass
     if res is None:
-        return {"error": f"cfg5 child job: exit {rc} after {wall} s, no result"}
+        return {"error": f"cfg5 child job: exit {rc} after {wall} s, no result", "phase_lines": phase_lines[-24:]}
     res["job"] = {"wall_s": wall, "exit": rc, "note": "child job of the default bench (bench.py --workload cfg5), "
                                                       "one rank per GPU, run before the cfg3 line's own ranks "
                                                       "touch the GPU"}
@@ -957,6 +1098,14 @@ def main():
     ap.add_argument("--wire-records", type=int, default=1_000_000, help="32-B client records per wire regroup call")
     ap.add_argument("--wire-out-records", type=int, default=4_000_000,
                     help="48-B game records per gate_to_clients call (one gate's share of a cfg3 collect)")
+    ap.add_argument("--no-batch-ready", action="store_true",
+                    help="A/B: the next batch's claims stored by the next flush's prologue, not beside the flush "
+                         "in flight (GWAOI_F_BATCH_READY off)")
+    ap.add_argument("--small-flush-reps", type=int, default=20,
+                    help="cfg3: timed flushes per size of the small-flush leg (1/64/4096/65536 moves; 0 = off)")
+    ap.add_argument("--strip-counts", default="device", choices=["device", "host"],
+                    help="cfg5: the per-tick count exchange -- device: all-gathered on the GPU inside the route's "
+                         "one host wait (RCCL); host: gloo all-gather of host tensors after it")
     ap.add_argument("--cfg5-steps", type=int, default=5,
                     help="cfg3 runs: timed ticks of the config-5 strip sub-record (child job; 0 = off)")
     ap.add_argument("--cfg5-warmup", type=int, default=3)
@@ -981,6 +1130,8 @@ def main():
     # the config-5 strip sub-record runs first, as a child job, while this process has not touched the GPU
     cfg5 = cfg5_job(args, ws, rank, local) if args.workload == "cfg3" and args.cfg5_steps > 0 else None
     dist = None
+    args.phases_t0 = T_START
+    args.phases_pre = {}
     if ws > 1:
         import torch
         import torch.distributed as dist
@@ -992,7 +1143,12 @@ def main():
         if args.dist_backend == "gloo":  # rehearsal: several ranks may share a GPU
             local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
+        t_pg = time.perf_counter()
         dist.init_process_group(args.dist_backend)
+        args.phases_pre = {"start_to_process_group": round(t_pg - T_START, 3),
+                           "init_process_group": round(time.perf_counter() - t_pg, 3)}
+        if args.workload == "cfg5":
+            print(f"[cfg5 rank {rank}] {args.phases_pre}", file=sys.stderr, flush=True)
     device = local
     red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{device}"
     if args.workload == "cfg5":
@@ -1038,10 +1194,13 @@ def main():
     d_x = torch.from_numpy(np.stack([b[1] for b in batches])).to(f"cuda:{device}")
     d_z = torch.from_numpy(np.stack([b[2] for b in batches])).to(f"cuda:{device}")
     moves_per_tick = [b[0].size for b in batches]
+    last_batch = batches[-1]  # every entity's position after the last tick (the small-flush leg moves from there)
     del batches
     torch.cuda.synchronize()
 
-    w = World(n, max_spaces=wl.n_spaces, device=device, cells_per_dist=args.cells_per_dist)
+    # the move batches are in HBM before the timed region: complete when passed (GWAOI_F_BATCH_READY)
+    w = World(n, max_spaces=wl.n_spaces, device=device, cells_per_dist=args.cells_per_dist,
+              batch_ready=not args.no_batch_ready)
     spaces = [w.space_create(wl.D) for _ in range(wl.n_spaces)]
     wl0 = wl_factory()  # initial positions (wl has advanced through the batches)
     slots, x0, z0, sp = wl0.initial()
@@ -1145,6 +1304,9 @@ def main():
         stages = w.stage_times()
         w.set_stage_timing([])
 
+    small = None
+    if args.small_flush_reps > 0 and ws == 1 and args.workload == "cfg3":
+        small = small_flush_leg(w, last_batch, args.small_flush_reps)
     # ---- PCIe-inclusive leg (SURVEY.md §8d's tick, BASELINE.md's p50/p99 "end-to-end from H2D to event CSR in
     # host memory"): host move arrays -> pinned staging -> H2D -> flush -> events in pinned host memory
     host_io = host_io_leg(w, host_batches, hio, dist, red_dev) if hio else None
@@ -1237,6 +1399,7 @@ def main():
                                              "one event per mirrored pair; serial and directed_events_out: every "
                                              "directed event); details in pcie_inclusive"} if host_io else None),
             "pcie_inclusive": host_io,
+            "small_flush": small,
             "sync_leg": sync,
             "wire_leg": wire,
             "stages_ms_per_tick": {k: round(v, 4) for k, v in stage_ms.items()},
@@ -1250,6 +1413,7 @@ def main():
         }
         if cpu and "value" in cpu:
             out["speedup_vs_cpu"] = out["value"] / ws / cpu["value"]
+        out["summary"] = line_summary(out)  # last: the part of the line a tail of stdout keeps
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -19,6 +19,8 @@ LIB_PATH = os.environ.get("GWAOI_LIB") or os.path.join(HERE, "lib", "libgwaoi.so
 HEADER = os.path.join(os.path.dirname(HERE), "include", "gwaoi.h")
 
 GWAOI_F_TIMING = 1
+GWAOI_F_NO_SPARSE = 2  # never the sparse flush (include/gwaoi.h)
+GWAOI_F_BATCH_READY = 4  # device batches complete when passed: claims stored beside the flush before
 
 STATUS = {
     0: "GWAOI_OK", -1: "GWAOI_EINVAL", -2: "GWAOI_EBADSLOT", -3: "GWAOI_ESTATE", -4: "GWAOI_ENOMEM",
@@ -46,7 +48,7 @@ STRIP_EXPORTS = [
     "gwaoi_strips_create", "gwaoi_strips_destroy", "gwaoi_strips_halo", "gwaoi_strips_route",
     "gwaoi_strips_route_scatter", "gwaoi_strips_tick", "gwaoi_strips_events_device", "gwaoi_strips_events",
     "gwaoi_strips_last_error", "gwaoi_strips_route_kinds", "gwaoi_strips_tick_async", "gwaoi_strips_wait",
-    "gwaoi_strips_host_waits",
+    "gwaoi_strips_host_waits", "gwaoi_strips_route_row_words", "gwaoi_strips_route_begin", "gwaoi_strips_route_end",
 ]
 
 # every function include/gwaoi_sync.h declares
@@ -106,7 +108,8 @@ class Debug(C.Structure):
     _fields_ = [("flushes", C.c_uint64), ("combined_replays", C.c_uint64), ("combined_queue_drains", C.c_uint64),
                 ("special_global", C.c_uint64), ("event_regrows", C.c_uint64), ("speculative_launches", C.c_uint64),
                 ("cell_size_switches", C.c_uint64), ("cells_per_dist", C.c_uint32), ("pad", C.c_uint32),
-                ("incremental_sorts", C.c_uint64)]
+                ("incremental_sorts", C.c_uint64), ("sparse_flushes", C.c_uint64), ("sparse_declined", C.c_uint64),
+                ("premarked_runs", C.c_uint64)]
 
 
 class StageTime(C.Structure):
@@ -190,6 +193,9 @@ def load():
         "gwaoi_strips_destroy": ([vp], C.c_int),
         "gwaoi_strips_halo": ([vp, P(f)], C.c_int),
         "gwaoi_strips_route": ([vp, vp, sz, P(u64)], C.c_int),
+        "gwaoi_strips_route_row_words": ([vp, P(u32)], C.c_int),
+        "gwaoi_strips_route_begin": ([vp, vp, sz, vp], C.c_int),
+        "gwaoi_strips_route_end": ([vp, vp, P(vp), P(u64)], C.c_int),
         "gwaoi_strips_route_scatter": ([vp, vp, vp], C.c_int),
         "gwaoi_strips_tick": ([vp, vp, sz, vp, sz, vp, sz, P(u64), P(u64)], C.c_int),
         "gwaoi_strips_route_kinds": ([vp, vp, vp, vp], C.c_int),
@@ -245,10 +251,12 @@ class World:
     """One GPU AOI world: many spaces, one HIP stream (include/gwaoi.h)."""
 
     def __init__(self, max_slots: int, max_spaces: int = 1, device: int = -1, timing: bool = False,
-                 event_capacity: int = 0, cells_per_dist: float = 0.0):
+                 event_capacity: int = 0, cells_per_dist: float = 0.0, sparse: bool = True,
+                 batch_ready: bool = False):
         self._L = load()
-        cfg = Config(max_slots, max_spaces, device, GWAOI_F_TIMING if timing else 0, event_capacity,
-                     cells_per_dist)
+        flags = ((GWAOI_F_TIMING if timing else 0) | (0 if sparse else GWAOI_F_NO_SPARSE) |
+                 (GWAOI_F_BATCH_READY if batch_ready else 0))
+        cfg = Config(max_slots, max_spaces, device, flags, event_capacity, cells_per_dist)
         h = C.c_void_p()
         self._check(self._L.gwaoi_world_create(C.byref(cfg), C.byref(h)), world=False)
         self._w = h

@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libgwaoi.so")
-SOURCES = ["gwaoi_kernels.hip", "gwaoi_world.cpp", "gwaoi_strips.hip", "gwaoi_sync.hip", "gwaoi_wire.hip"]
+SOURCES = ["gwaoi_kernels.hip", "gwaoi_world.cpp", "gwaoi_strips.hip", "gwaoi_sync.hip", "gwaoi_wire.hip",
+           "gwaoi_sparse.hip"]
 HEADERS = ["gwaoi_internal.h", "gwaoi_device.h", os.path.join("..", "..", "include", "gwaoi.h"),
            os.path.join("..", "..", "include", "gwaoi_sync.h"),
            os.path.join("..", "..", "include", "gwaoi_strips.h"), os.path.join("..", "..", "include", "gwaoi_wire.h")]

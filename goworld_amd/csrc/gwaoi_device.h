@@ -63,4 +63,25 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t nb) {
     return x * q + min(x, r) + k;
 }
 
+// The XCD this wave runs on (s_getreg HW_REG_XCC_ID: id 20, offset 0, 4 bits), 0..7.  Placement
+// information, for speed only: nothing's correctness depends on it.
+__device__ __forceinline__ uint32_t xcc_id() {
+    return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & (N_XCD - 1u);
+}
+
+// n directed pairs from event stream q (one returning atomic on the shard's own line); the
+// encoded stream position of the first (ev_phys gives the scratch index).
+__device__ __forceinline__ unsigned long long ev_alloc(TickScalars *sc, uint32_t q, uint32_t n) {
+    return ev_enc(q, atomicAdd(reinterpret_cast<unsigned long long *>(&sc->shard[q][2]), (unsigned long long)n));
+}
+
+// The directed pair (a,b), (b,a) at stream position p (even: both in one chunk), if it fits.
+__device__ __forceinline__ void ev_put2(uint2 *out, uint64_t cap, unsigned long long p, uint32_t a, uint32_t b) {
+    const unsigned long long i = ev_phys(p);
+    if (i + 1 < cap) {
+        out[i] = make_uint2(a, b);
+        out[i + 1] = make_uint2(b, a);
+    }
+}
+
 }  // namespace gw

@@ -2,6 +2,8 @@
 // kernels (gwaoi_kernels.hip).  Not part of the public ABI.
 #pragma once
 
+#include <cstddef>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -97,7 +99,33 @@ struct TickScalars {
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
     uint32_t pad2;
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
+    uint32_t pad3[18];
+    // One 128-B line per XCD shard q (zeroed by the prologue): [q][2..3] = the u64 length of
+    // event stream q (the pair passes' event allocator: ev_phys).  Sharded because one device-scope atomic word saturates
+    // at ~88 returning atomics per us (MI355X_MICROARCH.md, dequeue).
+    uint32_t shard[8][32];
 };
+constexpr uint32_t EV_SHARDS = 8;
+static_assert(offsetof(TickScalars, shard) % 128 == 0, "one line per shard");
+
+// The pair passes' directed events go to EV_SHARDS virtual streams (one per XCD, allocated by
+// that XCD's waves with one atomic per tile on the shard's own word), interleaved over the
+// scratch buffer in chunks of EV_CHUNK pairs: stream q's chunk k is physical chunk k*8+q.  A
+// tile's events are contiguous in its stream; a stream position is encoded (q << 60) | v.
+constexpr uint32_t EV_CHUNK_LOG = 8;
+constexpr uint64_t EV_CHUNK = 1ull << EV_CHUNK_LOG;
+__host__ __device__ inline unsigned long long ev_phys(unsigned long long qv) {
+    const unsigned long long q = qv >> 60, v = qv & ((1ull << 60) - 1);
+    return (((v >> EV_CHUNK_LOG) * EV_SHARDS + q) << EV_CHUNK_LOG) | (v & (EV_CHUNK - 1));
+}
+__host__ __device__ inline unsigned long long ev_enc(uint32_t q, unsigned long long v) {
+    return ((unsigned long long)q << 60) | v;
+}
+// The scratch extent n pairs can need at most: all of them in one stream, whose chunks are every
+// EV_SHARDS-th physical chunk.
+inline uint64_t ev_worst_extent(uint64_t n) {
+    return ((n + EV_CHUNK - 1) >> EV_CHUNK_LOG) * EV_SHARDS * EV_CHUNK;
+}
 
 // Rare-path counters of one flush (gwaoi_debug_counters accumulates them).
 enum : uint32_t {
@@ -257,8 +285,9 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
                      uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,
                      hipStream_t st,
                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// tile_order[1 + i] = the tile k_combined's i-th block (xcd_block index) runs, heaviest first per
-// XCD range by tile_work; tile_order[0] = the tile count it was built for (k_combined ignores it
+// The schedule: tile_order[1 + i] = the i-th tile of the XCD ranges laid end to end, heaviest first
+// within each range; tile_order[2 + n_tiles + x] .. = the eight ranges' cuts (cumulative measured
+// time, tile_work); tile_order[0] = the tile count it was built for (k_combined ignores it
 // otherwise).  launch_finish builds it for the next flush when given the buffers.
 // Special-entity pass over the previous frame in blocks of TILE_A entries
 // (O = S', the new state in the previous order, with O_ss giving its space);
@@ -293,6 +322,19 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st);
 void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_total, uint32_t n_rows, uint32_t *cnt,
                        uint32_t *off, uint32_t *scan_tmp, uint32_t *items, uint32_t *scratch, uint32_t *long_rows,
                        hipStream_t st);
+
+// The claims (tick << 32 | j0 + i) of one Moved run (k_moves_mark), on any stream.
+void launch_moves_mark(const MoveRun &R, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st);
+
+// Sparse flush of k host Moved calls on a frame in place (gwaoi_sparse.hip): claims must be stored
+// first (launch_ops_claim, this tick).  cnt: sparse_cnt_elems(k) words.  The flush's summary goes to
+// res (TickOut.pad != 0: declined, nothing changed); its events [enters | leaves] to out (cap pairs).
+size_t sparse_cnt_elems(uint32_t k);
+// op_seq == nullptr: op j's seq is seq0 + j.
+void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
+                   SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                   const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t tick, uint32_t *cnt,
+                   uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st);
 
 // ---- world accessors for the entity-sync layer (gwaoi_sync.cpp) -------------
 struct SyncState;

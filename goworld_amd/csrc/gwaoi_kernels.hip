@@ -71,6 +71,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
     if (i < n0) z0[i] = 0;
     if (i < n1) z1[i] = 0;
     if (i < n_spaces) bbox[i] = make_int4(INT_MAX, INT_MAX, INT_MIN, INT_MIN);
+    if (i < EV_SHARDS * 32) (&sc->shard[0][0])[i] = 0;
 }
 
 __global__ void k_zero(uint32_t *p, size_t n) {
@@ -1428,11 +1429,7 @@ __device__ void enum_global(const FrameView &F, const Rec16 *O_rec, const SlotSp
             if (!kind) continue;
             if (WRITE && k >= skip) {
                 const uint32_t slot_b = ld_ss(F.ss, b).slot;
-                const unsigned long long p = kind == 1 ? pe + 2ull * ne : pl + 2ull * nl;
-                if (p + 1 < cap) {
-                    out[p] = make_uint2(slot_a, slot_b);
-                    out[p + 1] = make_uint2(slot_b, slot_a);
-                }
+                ev_put2(out, cap, kind == 1 ? pe + 2ull * ne : pl + 2ull * nl, slot_a, slot_b);
             }
             if (!WRITE || k >= skip) {
                 ne += (uint32_t)(kind == 1);
@@ -1446,7 +1443,7 @@ __device__ void enum_global(const FrameView &F, const Rec16 *O_rec, const SlotSp
 template <int MODE>
 __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restrict__ O_rec,
                                               const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
-                                              unsigned long long *counter, uint2 *tmp, uint64_t cap,
+                                              TickScalars *scw, uint2 *tmp, uint64_t cap,
                                               uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
                                               uint32_t leave_off, uint32_t *dbg, const uint32_t *__restrict__ special) {
     if (MODE == 1 && special && !special[blockIdx.x]) return;  // keygen saw no special entity in this tile
@@ -1614,8 +1611,8 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
     __syncthreads();
     const uint32_t ol = block_excl_scan<PT>(2 * nl, s_ws, tl);
     if (tid == 0) {
-        const uint32_t tot = te + tl;
-        const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+        const uint32_t tot = te + tl, q = xcc_id();
+        const unsigned long long b = tot ? ev_alloc(scw, q, tot) : ev_enc(q, 0ull);
         s_base = b;
         put_tile_total(tile_total, leave_off, tile_off + t, te);
         tile_base[tile_off + t] = b;
@@ -1636,10 +1633,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
                 const unsigned long long p = lv ? pl + 2ull * il : pe + 2ull * ie;
                 il += (uint32_t)lv;
                 ie += (uint32_t)!lv;
-                if (p + 1 < cap) {
-                    tmp[p] = make_uint2(slot_a, slot_b);
-                    tmp[p + 1] = make_uint2(slot_b, slot_a);
-                }
+                ev_put2(tmp, cap, p, slot_a, slot_b);
             }
             if (nk > PS) {
                 atomicAdd(&s_nglob, 1u);
@@ -1679,7 +1673,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 // overflows replays its sweep and writes the rest straight to the output.
 
 constexpr int CT = (int)COMBINED_TILE;
-constexpr int CW = CT / WAVE;
+constexpr int CW = CT / WAVE;  // waves per k_combined workgroup
 #ifndef GWAOI_QCAP
 #define GWAOI_QCAP 384
 #endif
@@ -1702,7 +1696,7 @@ static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
 constexpr int NCLS = 14;  // lane work classes of k_combined
 
 struct CombinedLds {
-    uint32_t ndrain;        // mid-sweep queue drains of the block (DBG_COMBINED_DRAIN)
+    uint32_t ndrain[CW];    // mid-sweep queue drains of each wave (DBG_COMBINED_DRAIN)
     uint16_t ccnt[NCLS][CW];  // entities per work class and wave
     uint8_t perm[CT];         // the block's entries regrouped by work class
     uint32_t qb[CW][QCAP];  // queued pairs of a wave: B frame index
@@ -1771,11 +1765,7 @@ __device__ __forceinline__ void drain_queue(const uint32_t *qb, const uint8_t *q
             } else if (pos >= EVW) {
                 const uint32_t kidx = kind == 1 ? ne + (uint32_t)__popcll(em & lanemask_lt())
                                                 : nl + (uint32_t)__popcll(lm & lanemask_lt());
-                const unsigned long long p = (kind == 1 ? pe : pl) + 2ull * kidx;
-                if (p + 1 < cap) {
-                    out[p] = make_uint2(a_slot, b_slot);
-                    out[p + 1] = make_uint2(b_slot, a_slot);
-                }
+                ev_put2(out, cap, (kind == 1 ? pe : pl) + 2ull * kidx, a_slot, b_slot);
             }
         }
         ne += (uint32_t)__popcll(em);
@@ -1869,7 +1859,7 @@ __device__ __forceinline__ void sweep_range(CombinedLds &L, int w, WaveQueue &Q,
     (void)mx;
     for (uint32_t t = 0; __ballot(t < len); t += U) {  // to the wave's longest range (scalar mask test)
         if (Q.qn > QCAP - U * WAVE) {  // room for this iteration's pushes (any earlier sweep may have filled it)
-            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);  // LDS; one global add per block
+            if (!replay && lane() == 0) atomicAdd(&L.ndrain[w], 1u);  // LDS; one global add per block
             __builtin_amdgcn_wave_barrier();
             drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
                         cap, pe, pl, replay);
@@ -1903,7 +1893,7 @@ __device__ __forceinline__ void sweep_segs(CombinedLds &L, int w, WaveQueue &Q, 
     }
     for (uint32_t t = 0; __ballot(t < tot); t += U) {
         if (Q.qn > QCAP - U * WAVE) {
-            if (!replay && lane() == 0) atomicAdd(&L.ndrain, 1u);
+            if (!replay && lane() == 0) atomicAdd(&L.ndrain[w], 1u);
             __builtin_amdgcn_wave_barrier();
             drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
                         cap, pe, pl, replay);
@@ -1995,7 +1985,7 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
     uint32_t carry = 0;  // owner + 1 of the position before this chunk
     for (uint32_t g0 = 0; g0 < T; g0 += U * WAVE) {
         if (Q.qn > QCAP - U * WAVE) {
-            if (!replay && me == 0) atomicAdd(&L.ndrain, 1u);
+            if (!replay && me == 0) atomicAdd(&L.ndrain[w], 1u);
             __builtin_amdgcn_wave_barrier();
             drain_queue(L.qb[w], L.qa[w], L.ev[w], Q.qn, block_start(A), F, O_rec, C.proto, C.thr, Q.ne, Q.nl, out,
                         cap, pe, pl, replay);
@@ -2181,29 +2171,51 @@ __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__re
 constexpr uint32_t BT_MAX = 65536;
 __device__ unsigned long long gw_blocktime[3 * BT_MAX];
 #endif
+// The schedule (tile_order, built by k_finish for the next flush from this flush's measured time
+// per tile; any schedule gives the same events): each XCD x gets a contiguous range of tiles, cut
+// where the cumulative time crosses x/8 of the total (the XCDs end together: an even split by
+// count left them 65-88 us apart at config 3), run heaviest first; workgroup b runs on XCD b % 8
+// (the round-robin dispatch, for speed only) as that range's (b / 8)-th tile, and the workgroups
+// past a range's end leave at once.
+__host__ __device__ inline uint32_t range_max(uint32_t n_tiles) {
+    const uint32_t even = (n_tiles + N_XCD - 1) / N_XCD;
+    return even + even / 4 + 64;
+}
+__host__ __device__ inline uint32_t order_meta(uint32_t n_tiles) { return 1 + n_tiles; }
+
 __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, const uint4 *__restrict__ cand,
                                                  const Rec16 *__restrict__ O_rec, unsigned long long seq_base,
-                                                 const TickScalars *__restrict__ sc, unsigned long long *counter,
+                                                 const TickScalars *__restrict__ sc, TickScalars *scw,
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
                                                  unsigned long long *tile_base, uint32_t leave_off, uint32_t *dbg,
                                                  const uint32_t *__restrict__ tile_order, uint32_t *tile_work,
-                                                 uint32_t *ework) {
+                                                 uint32_t *ework, uint32_t n_tiles) {
     __shared__ CombinedLds L;
+    uint32_t t;
+    {
+        const uint32_t x = blockIdx.x % N_XCD, k = blockIdx.x / N_XCD;
+        const bool ordered = tile_order && tile_order[0] == n_tiles;
+        uint32_t lo, hi;
+        if (ordered) {
+            lo = tile_order[order_meta(n_tiles) + x];
+            hi = tile_order[order_meta(n_tiles) + x + 1];
+        } else {
+            const uint32_t q = n_tiles / N_XCD, r = n_tiles % N_XCD;
+            lo = x * q + min(x, r);
+            hi = lo + q + (x < r ? 1u : 0u);
+        }
+        if (lo + k >= hi) return;  // past this XCD's range (block-uniform: before any barrier)
+        t = ordered ? tile_order[1 + lo + k] : lo + k;
+    }
+    const unsigned long long t_start = wall_clock64();
 #ifdef GWAOI_EXP_BLOCKTIME
-    const unsigned long long bt0 = wall_clock64();
+    const unsigned long long bt0 = t_start;
 #endif
-    // Tiles run heaviest first within each XCD's range when the previous flush left an order for
-    // this tile count (k_tile_order); any order gives the same events.
-    uint32_t t = xcd_block(blockIdx.x, gridDim.x);
-    if (tile_order && tile_order[0] == gridDim.x) t = tile_order[1 + t];
     const uint32_t tid = threadIdx.x, ln = lane();
     const int w = tid / WAVE;
     const uint32_t e0 = t * CT;
-    if (tid < CW) L.wwork[tid] = 0;
-    if (tid == 0) {
-        L.overflow = 0;
-        L.ndrain = 0;
-    }
+    if (tid < CW) L.wwork[tid] = L.ndrain[tid] = 0;
+    if (tid == 0) L.overflow = 0;
     __syncthreads();
 
     // A block holds its LDS until its slowest wave ends, so the waves get equal
@@ -2330,14 +2342,11 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         }
         L.te = se;
         L.tl = sl;
-        if (L.ndrain) atomicAdd(dbg + DBG_COMBINED_DRAIN, L.ndrain);
-        if (tile_work) {
-            uint32_t wk = CT;
-            for (int q = 0; q < CW; ++q) wk += L.wwork[q];
-            tile_work[t] = wk;
-        }
-        const uint32_t tot = 2 * (se + sl);
-        const unsigned long long b = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+        uint32_t nd = 0;
+        for (int q = 0; q < CW; ++q) nd += L.ndrain[q];
+        if (nd) atomicAdd(dbg + DBG_COMBINED_DRAIN, nd);
+        const uint32_t tot = 2 * (se + sl), q = xcc_id();
+        const unsigned long long b = tot ? ev_alloc(scw, q, tot) : ev_enc(q, 0ull);
         L.base = b;
         put_tile_total(tile_total, leave_off, t, 2 * se);
         tile_base[t] = b;
@@ -2361,10 +2370,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             const uint32_t b_slot = ev.y & ~KIND_LEAVE;
             const unsigned long long p = lv ? pl + 2ull * (il + (uint32_t)__popcll(lm & lanemask_lt()))
                                             : pe + 2ull * (ie + (uint32_t)__popcll(em & lanemask_lt()));
-            if (p + 1 < cap) {
-                out[p] = make_uint2(ev.x, b_slot);
-                out[p + 1] = make_uint2(b_slot, ev.x);
-            }
+            ev_put2(out, cap, p, ev.x, b_slot);
         }
         ie += (uint32_t)__popcll(em);
         il += (uint32_t)__popcll(lm);
@@ -2373,8 +2379,22 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         uint32_t re = 0, rl = 0;
         run(true, out, pe, pl, re, rl);
     }
-#ifdef GWAOI_EXP_BLOCKTIME  // diagnostics build only: per-block start/end (wall clock) and hardware ids
+    // the tile's cost for the next flush's schedule: its measured time (100 MHz ticks), which the
+    // candidate count predicted poorly (crowd tiles take longer per candidate)
     __syncthreads();
+#ifndef GWAOI_TILE_TIME
+#define GWAOI_TILE_TIME 1
+#endif
+    if (tile_work && tid == 0) {
+#if GWAOI_TILE_TIME
+        tile_work[t] = max(1u, (uint32_t)min(wall_clock64() - t_start, 0xFFFFFFFFull));
+#else
+        uint32_t wk = CT;
+        for (int q = 0; q < CW; ++q) wk += L.wwork[q];
+        tile_work[t] = wk;
+#endif
+    }
+#ifdef GWAOI_EXP_BLOCKTIME  // diagnostics build only: per-block start/end (wall clock) and hardware ids
     if (tid == 0 && t < BT_MAX) {
         gw_blocktime[3 * t] = bt0;
         gw_blocktime[3 * t + 1] = wall_clock64();
@@ -2383,6 +2403,8 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     }
 #endif
 }
+
+
 
 // ------------------------------------------------------------- finish ------
 // The flush's tail in one launch (it was three: a scan of the tile totals,
@@ -2397,39 +2419,99 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 constexpr int FT = GWAOI_FT;  // tile entries per finish block (<= 64: one wave scans them)
 static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 
-// The next flush's combined tile order (k_finish's last N_XCD blocks, one per XCD range): within
-// each XCD's range of tiles (xcd_block), heaviest first by this flush's work per tile, as a counting
-// sort over 64 log-spaced work classes.  Only the schedule changes; k_combined's events do not
-// depend on it.
+// The next flush's k_combined schedule is built by the finish from this flush's work per tile:
+// within each XCD's range, heaviest first, as a counting sort over 64 log-spaced work classes.
+// Only the schedule changes; k_combined's events do not depend on it.
+// Bands (GWAOI_ORDER_BANDS): the range is cut into that many consecutive bands, run one after the
+// other, heaviest first within each -- the tail of the launch gets the light units of the last
+// band, and the units in flight stay near one another in the frame.
+#ifndef GWAOI_ORDER_BANDS
+#define GWAOI_ORDER_BANDS 1
+#endif
 constexpr int TO_NB = 64;
-__device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
-    __shared__ uint32_t hist[TO_NB];
-    const uint32_t q = nb / N_XCD, r = nb % N_XCD;
-    const uint32_t lo = x * q + min(x, r), hi = lo + q + (x < r ? 1u : 0u);
+constexpr int TO_BANDS = GWAOI_ORDER_BANDS;
+static_assert(TO_NB * TO_BANDS <= 256, "one histogram bin per thread");
+
+// Counting sort of range [lo, hi) of tiles by (band, descending work class) into tile_order[1 + ...].
+__device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t lo, uint32_t hi, uint32_t *tile_order) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t ws[256 / WAVE];
+    const uint32_t len = hi - lo;
     uint32_t *dst = tile_order + 1;
-    if (threadIdx.x < TO_NB) hist[threadIdx.x] = 0;
+    hist[threadIdx.x] = 0;
     __syncthreads();
-    auto cls = [&](uint32_t v) {  // descending: class 0 = heaviest
-        const int c = (int)(8.0f * __log2f((float)v + 1.0f)) - 40;
-        return (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
+    auto cls = [&](uint32_t i) {  // band-major, then descending work: bin 0 = heaviest of band 0
+        const int c = (int)(8.0f * __log2f((float)tile_work[i] + 1.0f)) - 40;
+        const uint32_t band = (uint32_t)(((unsigned long long)(i - lo) * TO_BANDS) / max(len, 1u));
+        return band * TO_NB + (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
     };
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(tile_work[i])], 1u);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(i)], 1u);
     __syncthreads();
-    if (threadIdx.x < WAVE) {  // exclusive scan of the 64 class counts by one wave
-        const uint32_t v = hist[threadIdx.x];
-        uint32_t incl = v;
-#pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
-            if ((int)threadIdx.x >= o) incl += t;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan<256>(hist[threadIdx.x], ws, total);
+    __syncthreads();
+    hist[threadIdx.x] = ex;
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) dst[lo + atomicAdd(&hist[cls(i)], 1u)] = i;
+}
+
+
+// The next flush's tile schedule (k_finish's last N_XCD blocks, block x for XCD x; see k_combined):
+// the eight ranges cut at the eighths of the cumulative measured time (every block computes the
+// same cuts; each thread sums a contiguous segment, so one scan finds them), at most range_max
+// long; range x heaviest first; the cuts at tile_order[order_meta .. order_meta + 8].
+__device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
+    __shared__ uint32_t s_cut[N_XCD + 1];
+    __shared__ unsigned long long s_sum[256];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t seg = (nb + 255) / 256, s0 = min(nb, tid * seg), s1 = min(nb, s0 + seg);
+    unsigned long long my = 0;
+    for (uint32_t i = s0; i < s1; ++i) my += tile_work[i];
+    s_sum[tid] = my;
+    if (tid <= N_XCD) s_cut[tid] = tid == N_XCD ? nb : 0u;
+    __syncthreads();
+    if (tid < WAVE) {  // inclusive scan of the 256 segment sums by one wave (4 per lane)
+        unsigned long long v[4], tt = 0;
+        for (int q = 0; q < 4; ++q) {
+            tt += s_sum[4 * tid + q];
+            v[q] = tt;
         }
-        hist[threadIdx.x] = incl - v;
+        unsigned long long incl = tt;
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const unsigned long long y = __shfl_up(incl, o);
+            if ((int)tid >= o) incl += y;
+        }
+        const unsigned long long ex = incl - tt;
+        for (int q = 0; q < 4; ++q) s_sum[4 * tid + q] = ex + v[q];
     }
     __syncthreads();
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-        dst[lo + atomicAdd(&hist[cls(tile_work[i])], 1u)] = i;
-    if (x == 0 && threadIdx.x == 0) tile_order[0] = nb;
+    const unsigned long long W = s_sum[255];
+    unsigned long long e = tid ? s_sum[tid - 1] : 0ull;  // work before this segment
+    for (uint32_t i = s0; i < s1; ++i) {  // cut q: the first tile whose exclusive prefix reaches q W / 8
+        const unsigned long long in = e + tile_work[i];
+        for (uint32_t q = 1; q < N_XCD; ++q) {
+            const unsigned long long T = (W * q) / N_XCD;
+            if (e < T && in >= T) s_cut[q] = i + 1;
+        }
+        e = in;
+    }
+    __syncthreads();
+    if (tid == 0) {  // at most range_max per range (the launch grid's bound), in order
+        const uint32_t Lmax = range_max(nb);
+        for (uint32_t q = 1; q < N_XCD; ++q) {
+            const unsigned long long rest = (unsigned long long)(N_XCD - q) * Lmax;
+            uint32_t lo_b = s_cut[q - 1];
+            if (nb > rest) lo_b = max(lo_b, (uint32_t)(nb - rest));
+            const uint32_t hi_b = (uint32_t)min((unsigned long long)nb, (unsigned long long)s_cut[q - 1] + Lmax);
+            s_cut[q] = min(max(s_cut[q], lo_b), hi_b);
+        }
+    }
+    __syncthreads();
+    order_range(tile_work, s_cut[x], s_cut[x + 1], tile_order);
+    if (x == 0 && tid <= N_XCD) tile_order[order_meta(nb) + tid] = s_cut[tid];
+    if (x == 0 && tid == 0) tile_order[0] = nb;
 }
+
 
 __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ tile_total,
                                                 const unsigned long long *__restrict__ tile_base, uint32_t n_entries,
@@ -2447,7 +2529,13 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     if (b == R) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         if (threadIdx.x == 0) {
             res->err = sc->err;
-            res->total64 = sc->counter;
+            // the scratch extent the pair passes needed (each stream's last chunk), against the capacity
+            unsigned long long ext = 0;
+            for (uint32_t q = 0; q < EV_SHARDS; ++q) {
+                const unsigned long long len = *reinterpret_cast<const unsigned long long *>(&sc->shard[q][2]);
+                if (len) ext = max(ext, ev_phys(ev_enc(q, len - 1)) + 1);
+            }
+            res->total64 = ext;
             res->seq_max = sc->seq_max;
             for (int q = 0; q < (int)DBG_N; ++q) res->dbg[q] = sc->dbg[q];
             if (n_entries == 0) {
@@ -2548,7 +2636,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
             v[u] = make_uint2(0u, 0u);
             if (p < o1) {
                 while (s_off[t + 1] <= p) ++t;  // last tile t with s_off[t] <= p (s_off[FT] = o1 > p)
-                const unsigned long long src = s_src[t] + (p - s_off[t]);
+                const unsigned long long src = ev_phys(s_src[t] + (p - s_off[t]));
                 if (src < cap) v[u] = tmp[src];
             }
         }
@@ -2724,7 +2812,7 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
                      hipStream_t st) {
     MoveRun mk{};
     if (mark) mk = *mark;
-    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, (size_t)n_copy, (size_t)mk.n, 1});
+    const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, (size_t)n_copy, (size_t)mk.n, (size_t)EV_SHARDS * 32});
     k_prologue<<<cdiv(m, 256), 256, 0, st>>>(sc, z0, (uint32_t)n0, z1, (uint32_t)n1, bbox, n_spaces, n_copy, p_rec,
                                              p_ss, s_rec, s_ss, mk, max_slots, info, tick_id);
 }
@@ -2737,6 +2825,10 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t ba
                           SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st) {
     if (!n_app) return;
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
+}
+
+void launch_moves_mark(const MoveRun &R, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st) {
+    if (R.n) k_moves_mark<<<cdiv(R.n, 256), 256, 0, st>>>(R, max_slots, info, tick_id);
 }
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
@@ -2918,7 +3010,7 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
                   uint32_t tile_off, uint32_t leave_off, const uint32_t *special, hipStream_t st) {
     if (!F.n) return;
     uint2 *tmp = reinterpret_cast<uint2 *>(tmp_pairs);
-    k_pairs<1><<<combined_blocks(F.n), PT, 0, st>>>(F, O_rec, O_ss, seq_base, sc, &sc->counter, tmp, cap, tile_total,
+    k_pairs<1><<<combined_blocks(F.n), PT, 0, st>>>(F, O_rec, O_ss, seq_base, sc, sc, tmp, cap, tile_total,
                                                     tile_base, tile_off, leave_off, sc->dbg, special);
 }
 
@@ -2929,11 +3021,12 @@ void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and
     // end: no marker packets between kernels when the stage is timed
-    hipExtLaunchKernelGGL(k_combined, dim3(combined_tiles(F.n)),
+    const uint32_t tiles = combined_tiles(F.n);
+    hipExtLaunchKernelGGL(k_combined, dim3(N_XCD * range_max(tiles)),
                           dim3(CT), 0, st, ev0, ev1, 0, F, cand, O_rec,
-                          (unsigned long long)seq_base, (const TickScalars *)sc, &sc->counter,
+                          (unsigned long long)seq_base, (const TickScalars *)sc, sc,
                           reinterpret_cast<uint2 *>(tmp_pairs), cap, tile_total, tile_base, leave_off, sc->dbg,
-                          tile_order, tile_work, ework);
+                          tile_order, tile_work, ework, tiles);
 }
 
 // One event of each mirrored pair ((a,b) at an even index, (b,a) after it) into pinned host memory:

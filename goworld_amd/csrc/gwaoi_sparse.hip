@@ -1,0 +1,383 @@
+// Sparse flush: a flush of a few Moved calls (the game loop's read-after-write case: a timer
+// callback moves an entity, the next one reads interest sets) priced by its calls, not by the
+// world.  The full flush rebuilds the frame (keys, sort, gather, the band sweep of every entity:
+// ~0.2 ms at 1M entities whatever the call count).  Here, with the frame of the last flush in place:
+//
+//   1. k_ops_claim (gwaoi_kernels.hip): the last op of each slot wins, as in every flush;
+//   2. k_sp_events<0>: one workgroup per winning op A scans the grid cells around A's old and new
+//      positions; a partner B that is no mover keeps its frame state, so the pair's relation before
+//      is rel(A_old, B) and after rel(A_new, B) (go-aoi's window test with A's new, largest seq).
+//      Mover pairs are taken from the op list (the lower slot of the two), both states from the
+//      frame and the ops.  Counts enters / leaves per op;
+//   3. k_sp_scan: the per-op offsets, the flush summary, the capacity check;
+//   4. k_sp_events<1>: the same scan, writing the directed pairs [enters | leaves] in op order;
+//   5. k_sp_apply (one workgroup): the frame patched in place -- each winner's record, and a winner
+//      whose cell changed shifted into its new cell (the entries between move by one, cell starts
+//      by one, SlotInfo.rank follows).  The frame stays exactly the stable sort a full flush makes
+//      of it, up to the order inside a cell (which nothing depends on).
+//
+// Steps 3 and 5 decline (TickOut.pad != 0, nothing mutated) when the events outgrow the flush
+// set's buffer or the shifts are long; the host then runs the full flush over the same queue.
+// The pair relation between flushes is the closed form over the frame, so
+// the events are exactly those of the full flush of the same queue.
+#include "gwaoi_device.h"
+
+namespace gw {
+namespace {
+
+constexpr int WAVE = 64;
+constexpr uint32_t SP_T = 256;         // threads per op workgroup
+constexpr uint32_t SA_T = 1024;        // threads of the apply workgroup
+constexpr uint32_t SP_MAX_CHANGERS = 64;     // winners changing cell one sparse flush shifts
+constexpr uint32_t SP_MAX_SHIFT = 1u << 17;  // frame entries those shifts may move in total
+
+struct SparseArgs {
+    Rec16 *rec;
+    SlotSp *ss;
+    uint32_t *key;
+    uint32_t *cell_start;
+    const SpaceGrid *grid;
+    SlotInfo *info;
+    const uint32_t *op_slot;
+    const float *op_x, *op_z;
+    const unsigned long long *op_seq;  // nullptr: op j's seq is seq0 + j
+    unsigned long long seq0;
+    uint32_t k;
+    uint32_t tick;
+    uint32_t *cnt;  // [0, k): enters per op, [k, 2k): leaves, their exclusive scans [2k, 4k), totals [4k, 4k+2), declined [4k+2]
+    uint2 *out;
+    uint64_t cap;
+    TickOut *res;
+};
+
+__device__ __forceinline__ unsigned long long op_seq(const SparseArgs &A, uint32_t j) {
+    return A.op_seq ? A.op_seq[j] : A.seq0 + j;
+}
+
+__device__ __forceinline__ bool winner(const SparseArgs &A, uint32_t j, uint32_t slot) {
+    return A.info[slot].lastop == (((unsigned long long)A.tick << 32) | j);
+}
+
+// Block-wide exclusive scan of two flags, in thread order, and their block totals.
+__device__ __forceinline__ void scan2(bool e, bool l, uint32_t *ws, uint32_t &pe, uint32_t &pl, uint32_t &te,
+                                      uint32_t &tl) {
+    const unsigned long long me = __ballot(e), ml = __ballot(l);
+    const uint32_t w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const unsigned long long lt = (1ull << __lane_id()) - 1ull;
+    __syncthreads();
+    if (__lane_id() == 0) {
+        ws[w] = (uint32_t)__popcll(me);
+        ws[nw + w] = (uint32_t)__popcll(ml);
+    }
+    __syncthreads();
+    uint32_t be = 0, bl = 0;
+    te = tl = 0;
+    for (uint32_t q = 0; q < nw; ++q) {
+        if (q < w) {
+            be += ws[q];
+            bl += ws[nw + q];
+        }
+        te += ws[q];
+        tl += ws[nw + q];
+    }
+    pe = be + (uint32_t)__popcll(me & lt);
+    pl = bl + (uint32_t)__popcll(ml & lt);
+}
+
+template <int PHASE>
+__global__ __launch_bounds__(SP_T) void k_sp_events(SparseArgs A) {
+    __shared__ uint32_t ws[2 * SP_T / WAVE];
+    const uint32_t j = blockIdx.x, tid = threadIdx.x;
+    const uint32_t slot = A.op_slot[j];
+    if (!winner(A, j, slot)) {
+        if (PHASE == 0 && tid == 0) A.cnt[j] = A.cnt[A.k + j] = 0;
+        return;
+    }
+    const uint32_t ra = A.info[slot].rank;
+    const Rec16 ao = ld_rec(A.rec, ra);
+    const uint32_t sp = ld_ss(A.ss, ra).sp;
+    const SpaceGrid g = A.grid[sp];
+    const float D = g.D;
+    const float nx = A.op_x[j], nz = A.op_z[j];
+    const unsigned long long ns = op_seq(A, j);
+    // every B related to A before or after lies within D (+ the float32 rounding of fl32(w +- D))
+    // of A's old or new position
+    const float mx = (fmaxf(fabsf(ao.x), fabsf(nx)) + 3.0f * D) * 0x1p-20f;
+    const float mz = (fmaxf(fabsf(ao.z), fabsf(nz)) + 3.0f * D) * 0x1p-20f;
+    const int cx0 = cell_of(fminf(ao.x, nx) - D - mx, g.ox, g.inv, g.gx);
+    const int cx1 = cell_of(fmaxf(ao.x, nx) + D + mx, g.ox, g.inv, g.gx);
+    const int cz0 = cell_of(fminf(ao.z, nz) - D - mz, g.oz, g.inv, g.gz);
+    const int cz1 = cell_of(fmaxf(ao.z, nz) + D + mz, g.oz, g.inv, g.gz);
+    uint32_t ne = 0, nl = 0;
+    unsigned long long pe = 0, pl = 0;  // PHASE 1: this op's next enter / leave position (directed pairs)
+    if (PHASE == 1) {
+        pe = 2ull * A.cnt[2 * A.k + j];
+        pl = 2ull * ((unsigned long long)A.cnt[4 * A.k] + A.cnt[3 * A.k + j]);
+    }
+    auto emit = [&](bool valid, int kind, uint32_t b_slot) {
+        uint32_t oe, ol, te, tl;
+        scan2(valid && kind == 1, valid && kind == 2, ws, oe, ol, te, tl);
+        if (PHASE == 1 && valid && kind) {
+            const unsigned long long p = kind == 1 ? pe + 2ull * oe : pl + 2ull * ol;
+            if (p + 1 < A.cap) {
+                A.out[p] = make_uint2(slot, b_slot);
+                A.out[p + 1] = make_uint2(b_slot, slot);
+            }
+        }
+        ne += te;
+        nl += tl;
+        pe += 2ull * te;
+        pl += 2ull * tl;
+    };
+    // partners in the frame that are not movers of this flush (their state is the frame's)
+    for (int cz = cz0; cz <= cz1; ++cz) {
+        const uint32_t row = g.base + (uint32_t)cz * g.gx;
+        const uint32_t jb = A.cell_start[row + (uint32_t)cx0], je = A.cell_start[row + (uint32_t)cx1 + 1u];
+        for (uint32_t b0 = jb; b0 < je; b0 += SP_T) {
+            const uint32_t b = b0 + tid;
+            int kind = 0;
+            uint32_t b_slot = 0;
+            if (b < je && b != ra) {
+                b_slot = ld_ss(A.ss, b).slot;
+                if ((uint32_t)(A.info[b_slot].lastop >> 32) != A.tick) {
+                    const Rec16 br = ld_rec(A.rec, b);
+                    const bool was = rel(ao.x, ao.z, ao.s, br.x, br.z, br.s, D);
+                    const bool is = rel(nx, nz, ns, br.x, br.z, br.s, D);
+                    kind = was == is ? 0 : is ? 1 : 2;
+                }
+            }
+            emit(b < je, kind, b_slot);
+        }
+    }
+    // pairs of two movers, from the lower slot: both states from the frame and the ops
+    for (uint32_t q0 = 0; q0 < A.k; q0 += SP_T) {
+        const uint32_t q = q0 + tid;
+        int kind = 0;
+        uint32_t b_slot = 0;
+        if (q < A.k) {
+            b_slot = A.op_slot[q];
+            if (b_slot > slot && winner(A, q, b_slot)) {
+                const uint32_t rb = A.info[b_slot].rank;
+                if (ld_ss(A.ss, rb).sp == sp) {
+                    const Rec16 bo = ld_rec(A.rec, rb);
+                    const bool was = rel(ao.x, ao.z, ao.s, bo.x, bo.z, bo.s, D);
+                    const bool is = rel(nx, nz, ns, A.op_x[q], A.op_z[q], op_seq(A, q), D);
+                    kind = was == is ? 0 : is ? 1 : 2;
+                }
+            }
+        }
+        emit(q < A.k, kind, b_slot);
+    }
+    if (PHASE == 0 && tid == 0) {
+        A.cnt[j] = ne;
+        A.cnt[A.k + j] = nl;
+    }
+}
+
+// Per-op offsets (exclusive scans of the enter and leave counts), the summary, the capacity check.
+__global__ __launch_bounds__(SA_T) void k_sp_scan(SparseArgs A) {
+    __shared__ uint32_t ws[2 * SA_T / WAVE];
+    __shared__ uint32_t carry[2];
+    if (threadIdx.x == 0) carry[0] = carry[1] = 0;
+    for (uint32_t j0 = 0; j0 < A.k; j0 += SA_T) {
+        const uint32_t j = j0 + threadIdx.x;
+        const uint32_t e = j < A.k ? A.cnt[j] : 0u, l = j < A.k ? A.cnt[A.k + j] : 0u;
+        // exclusive scan of counts (not flags): wave scan, then the waves' totals
+        uint32_t ie = e, il = l;
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t te = (uint32_t)__shfl_up((int)ie, o), tl = (uint32_t)__shfl_up((int)il, o);
+            if ((int)__lane_id() >= o) {
+                ie += te;
+                il += tl;
+            }
+        }
+        const uint32_t w = threadIdx.x / WAVE, nw = SA_T / WAVE;
+        __syncthreads();
+        if (__lane_id() == WAVE - 1) {
+            ws[w] = ie;
+            ws[nw + w] = il;
+        }
+        __syncthreads();
+        uint32_t be = carry[0], bl = carry[1], te = 0, tl = 0;
+        for (uint32_t q = 0; q < nw; ++q) {
+            if (q < w) {
+                be += ws[q];
+                bl += ws[nw + q];
+            }
+            te += ws[q];
+            tl += ws[nw + q];
+        }
+        if (j < A.k) {
+            A.cnt[2 * A.k + j] = be + ie - e;
+            A.cnt[3 * A.k + j] = bl + il - l;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            carry[0] += te;
+            carry[1] += tl;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t E = carry[0], L = carry[1];
+        A.cnt[4 * A.k] = E;
+        A.cnt[4 * A.k + 1] = L;
+        const unsigned long long tot = 2ull * ((unsigned long long)E + L);
+        A.res->n_enter = 2 * E;
+        A.res->n_total = (uint32_t)tot;
+        A.res->err = 0;
+        const uint32_t declined = tot > A.cap ? 1u : 0u;  // the flush set's buffer is too small (the full flush grows it)
+        A.cnt[4 * A.k + 2] = declined;
+        A.res->pad = declined;
+        A.res->total64 = tot;
+        A.res->seq_max = 0;
+        for (int q = 0; q < (int)DBG_N; ++q) A.res->dbg[q] = 0;
+    }
+}
+
+// Shift one mover (now at frame index p, key k1, new key k2 != k1) into its new cell: the entries
+// between move by one (in place, in chunks ordered so that no entry is overwritten before it is
+// read), the cell starts between by one, and SlotInfo.rank of every moved entry follows.
+__device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t k2) {
+    __shared__ uint4 s_rec[SA_T];
+    __shared__ uint2 s_ss[SA_T];
+    __shared__ uint32_t s_key[SA_T];
+    __shared__ uint4 m_rec;
+    __shared__ uint2 m_ss;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        m_rec = reinterpret_cast<const uint4 *>(A.rec)[p];
+        m_ss = reinterpret_cast<const uint2 *>(A.ss)[p];
+    }
+    uint32_t dst;
+    if (k2 > k1) {  // entries p+1 .. e down by one, the mover to e
+        const uint32_t e = A.cell_start[k2 + 1] - 1u;
+        __syncthreads();
+        for (uint32_t c0 = p + 1; c0 <= e; c0 += SA_T) {
+            const uint32_t i = c0 + tid;
+            const bool v = i <= e;
+            if (v) {
+                s_rec[tid] = reinterpret_cast<const uint4 *>(A.rec)[i];
+                s_ss[tid] = reinterpret_cast<const uint2 *>(A.ss)[i];
+                s_key[tid] = A.key[i];
+            }
+            __syncthreads();
+            if (v) {
+                reinterpret_cast<uint4 *>(A.rec)[i - 1] = s_rec[tid];
+                reinterpret_cast<uint2 *>(A.ss)[i - 1] = s_ss[tid];
+                A.key[i - 1] = s_key[tid];
+                A.info[s_ss[tid].x].rank = i - 1;
+            }
+            __syncthreads();
+        }
+        for (uint32_t c = k1 + 1 + tid; c <= k2; c += SA_T) A.cell_start[c] -= 1u;
+        dst = e;
+    } else {  // entries s .. p-1 up by one, the mover to s
+        const uint32_t s = A.cell_start[k2 + 1];
+        __syncthreads();
+        for (uint32_t hi = p; hi > s;) {  // chunks from the top down
+            const uint32_t lo = hi - s > SA_T ? hi - SA_T : s;
+            const uint32_t i = lo + tid;
+            const bool v = i < hi;
+            if (v) {
+                s_rec[tid] = reinterpret_cast<const uint4 *>(A.rec)[i];
+                s_ss[tid] = reinterpret_cast<const uint2 *>(A.ss)[i];
+                s_key[tid] = A.key[i];
+            }
+            __syncthreads();
+            if (v) {
+                reinterpret_cast<uint4 *>(A.rec)[i + 1] = s_rec[tid];
+                reinterpret_cast<uint2 *>(A.ss)[i + 1] = s_ss[tid];
+                A.key[i + 1] = s_key[tid];
+                A.info[s_ss[tid].x].rank = i + 1;
+            }
+            __syncthreads();
+            hi = lo;
+        }
+        for (uint32_t c = k2 + 1 + tid; c <= k1; c += SA_T) A.cell_start[c] += 1u;
+        dst = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        reinterpret_cast<uint4 *>(A.rec)[dst] = m_rec;
+        reinterpret_cast<uint2 *>(A.ss)[dst] = m_ss;
+        A.key[dst] = k2;
+        A.info[m_ss.x].rank = dst;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t key_of(const SpaceGrid &g, float x, float z) {
+    return g.base + (uint32_t)cell_of(z, g.oz, g.inv, g.gz) * g.gx + (uint32_t)cell_of(x, g.ox, g.inv, g.gx);
+}
+
+// The frame patched in place (one workgroup): first decide (no write before the decision), then
+// the winners' records, then the cell changers one after another in op order.
+__global__ __launch_bounds__(SA_T) void k_sp_apply(SparseArgs A) {
+    __shared__ uint32_t n_chg, shift_sum;
+    __shared__ uint32_t chg[SP_MAX_CHANGERS];
+    const uint32_t tid = threadIdx.x;
+    if (A.cnt[4 * A.k + 2]) return;  // declined by the scan
+    if (tid == 0) n_chg = shift_sum = 0;
+    __syncthreads();
+    for (uint32_t j = tid; j < A.k; j += SA_T) {
+        const uint32_t slot = A.op_slot[j];
+        if (!winner(A, j, slot)) continue;
+        const uint32_t r = A.info[slot].rank;
+        const uint32_t k1 = A.key[r], k2 = key_of(A.grid[ld_ss(A.ss, r).sp], A.op_x[j], A.op_z[j]);
+        if (k1 == k2) continue;
+        const uint32_t c = atomicAdd(&n_chg, 1u);
+        if (c < SP_MAX_CHANGERS) chg[c] = j;
+        // entries this shift moves (against the starts before any shift: an estimate of the total)
+        const uint32_t d = k2 > k1 ? A.cell_start[k2 + 1] - 1u - r : r - A.cell_start[k2 + 1];
+        atomicAdd(&shift_sum, min(d, SP_MAX_SHIFT + 1u));
+    }
+    __syncthreads();
+    if (n_chg > SP_MAX_CHANGERS || shift_sum > SP_MAX_SHIFT) {
+        if (tid == 0) A.res->pad = 2u;  // declined: too much of the frame would move
+        return;
+    }
+    // the winners' records (a changer's record moves with it below)
+    for (uint32_t j = tid; j < A.k; j += SA_T) {
+        const uint32_t slot = A.op_slot[j];
+        if (!winner(A, j, slot)) continue;
+        Rec16 r;
+        r.x = A.op_x[j];
+        r.z = A.op_z[j];
+        r.s = op_seq(A, j);
+        st_rec(A.rec, A.info[slot].rank, r);
+    }
+    // changers in op order (deterministic frame): rank-sort the short list
+    __shared__ uint32_t ord[SP_MAX_CHANGERS];
+    const uint32_t nc = n_chg;
+    if (tid < nc) {
+        uint32_t pos = 0;
+        for (uint32_t q = 0; q < nc; ++q) pos += chg[q] < chg[tid];
+        ord[pos] = chg[tid];
+    }
+    __syncthreads();
+    for (uint32_t c = 0; c < nc; ++c) {
+        const uint32_t j = ord[c], slot = A.op_slot[j];
+        const uint32_t p = A.info[slot].rank;
+        const uint32_t k1 = A.key[p], k2 = key_of(A.grid[ld_ss(A.ss, p).sp], A.op_x[j], A.op_z[j]);
+        sp_shift(A, p, k1, k2);
+    }
+}
+
+}  // namespace
+
+size_t sparse_cnt_elems(uint32_t k) { return 4 * (size_t)k + 3; }
+
+void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
+                   SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                   const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t tick, uint32_t *cnt,
+                   uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st) {
+    SparseArgs A{rec, ss, key, cell_start, grid, info, op_slot, op_x, op_z, op_seq, seq0, k, tick, cnt,
+                 reinterpret_cast<uint2 *>(out), cap, res};
+    k_sp_events<0><<<k, SP_T, 0, st>>>(A);
+    k_sp_scan<<<1, SA_T, 0, st>>>(A);
+    k_sp_events<1><<<k, SP_T, 0, st>>>(A);
+    k_sp_apply<<<1, SA_T, 0, st>>>(A);
+}
+
+}  // namespace gw

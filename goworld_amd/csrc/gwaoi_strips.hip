@@ -318,7 +318,14 @@ __global__ void __launch_bounds__(BT) k_recv(int phase, const gwaoi_halo_rec *__
             }
         }
         if (e && phase == 0) atomicOr(err, e);
+        // a record of no known kind counts as a move on the host (n_move = all - enters - leaves):
+        // it goes into class 0 as a no-op placeholder (SLOT_NONE), so the world's move batch never
+        // reads a word this tick did not write
         if (r.kind <= GWAOI_HALO_LEAVE) m = 1ull << r.kind;
+        else {
+            m = 1ull;
+            r.slot = gw::SLOT_NONE;
+        }
     }
     if (phase == 0 && ks) {
         __syncthreads();
@@ -504,6 +511,19 @@ __global__ void k_totals(const uint32_t *offs, uint32_t K, uint32_t nb, const ui
 
 inline uint32_t cdivu(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// This strip's count row (gwaoi_strips_route_begin): [records to each strip (S) | teleports |
+// per destination: ENTER, LEAVE, ENTER box x0 z0 x1 z1 (KS ints each) | route error word].
+inline uint32_t row_words(uint32_t S) { return S + 1 + S * 6 + 1; }
+__global__ void k_route_row(const uint32_t *__restrict__ small, const int *__restrict__ kstat, uint32_t S,
+                            uint32_t *row) {
+    const uint32_t K = S + 1, words = K + S * 6 + 1;
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+        if (i < K) row[i] = small[i + 1] - small[i];
+        else if (i < K + S * 6) row[i] = (uint32_t)kstat[i - K];
+        else row[i] = small[K + 1];
+    }
+}
+
 float o2f(int i) {
     const int b = i >= 0 ? i : i ^ 0x7FFFFFFF;
     float f;
@@ -524,6 +544,8 @@ constexpr size_t SM_WORDS = SM_RECV + 16;
 
 struct gwaoi_strips {
     gwaoi_world *w = nullptr;
+    bool broken = false;  // a failed asynchronous tick (complete_or_break)
+    std::string broken_msg;
     uint32_t space = 0;
     hipStream_t st = nullptr;
     StripGeo geo{};
@@ -546,6 +568,8 @@ struct gwaoi_strips {
     uint32_t r_n = 0, r_nb = 0;
     bool routed = false;
     bool kinds_valid = false;
+    bool row_pending = false;     // gwaoi_strips_route_begin queued, its _end not called yet
+    uint32_t *row_h = nullptr;    // pinned: every strip's count row (gwaoi_strips_route_end)
     // received records as world ops, SoA [moves | enters | leaves]
     uint32_t *m_slot = nullptr;
     float *m_x = nullptr, *m_z = nullptr;
@@ -706,6 +730,22 @@ int complete(gwaoi_strips *s, bool synced) {
     return strip_err(s, t[4], "recv");
 }
 
+// An asynchronous tick that fails on completion has already changed the strip's per-slot state
+// and fed its world (which a record in the wrong state poisons): the strip is unusable from then
+// on, and every later call says so (gwaoi_strips.h).
+int complete_or_break(gwaoi_strips *s, bool synced) {
+    if (s->broken) {
+        s->last_error = s->broken_msg;
+        return GWAOI_ESTATE;
+    }
+    const int rc = complete(s, synced);
+    if (rc) {
+        s->broken = true;
+        s->broken_msg = "strip unusable after a failed tick: " + s->last_error;
+    }
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -721,6 +761,7 @@ int gwaoi_strips_destroy(gwaoi_strips *s) {
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (s->small_h) (void)hipHostFree(s->small_h);
+    if (s->row_h) (void)hipHostFree(s->row_h);
     if (s->h_events) (void)hipHostFree(s->h_events);
     delete s;
     return GWAOI_OK;
@@ -803,16 +844,18 @@ int gwaoi_strips_halo(const gwaoi_strips *s, float *halo) {
     });
 }
 
-int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint64_t *counts) {
-    return gw::api_guard([&]() -> int {
-    if (!s || !counts || (n && !d_ops) || n > 0x7FFFFFFFu) return GWAOI_EINVAL;
+}  // extern "C"
+
+namespace {
+// Route phase 0 and its totals, queued (no wait).  Behind the previous tick, if one is pending:
+// its filter and totals land before this route's totals, so the route's one wait completes both.
+int route_launch(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n) {
     const uint32_t K = s->geo.S + 1;
     const uint32_t nb = std::max(1u, cdivu(n, BT));
     s->kinds_valid = false;
+    s->routed = false;
     if (int rc = ensure_split(s, K, nb)) return rc;
     hipStream_t st = s->st;
-    // queued behind the previous tick (if one is pending): its filter and totals land before this
-    // route's totals, so the one wait below completes both
     S_TRY(hipMemsetAsync(s->err, 0, sizeof(uint32_t), st));
     k_kstat_init<<<1, 64, 0, st>>>(s->kstat, s->geo.S);
     k_route<<<nb, BT, 0, st>>>(0, d_ops, (uint32_t)n, s->cur, s->geo, s->counts, nullptr, nb, s->err, nullptr,
@@ -820,19 +863,82 @@ int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, u
     gw::scan_exclusive(s->counts, s->counts, (size_t)K * nb + 1, s->scan_tmp, st);
     k_totals<<<1, 128, 0, st>>>(s->counts, K, nb, s->err, s->small_d + SM_ROUTE);
     S_TRY(hipGetLastError());
+    s->r_ops = d_ops;
+    s->r_n = (uint32_t)n;
+    s->r_nb = nb;
+    return GWAOI_OK;
+}
+
+// The route's totals and kind statistics to the host (queued after whatever else the caller
+// queued), then the tick's one host wait; it also completes the previous tick.
+int route_finish(gwaoi_strips *s, uint64_t *counts) {
+    const uint32_t K = s->geo.S + 1;
+    hipStream_t st = s->st;
     S_TRY(hipMemcpyAsync(s->small_h + SM_ROUTE, s->small_d + SM_ROUTE, (K + 2) * sizeof(uint32_t),
                          hipMemcpyDeviceToHost, st));
     S_TRY(hipMemcpyAsync(s->small_h + SM_KIND, s->kstat, (size_t)s->geo.S * KS * sizeof(int), hipMemcpyDeviceToHost,
                          st));
     if (int rc = wait(s)) return rc;  // the one host wait of a strip tick
-    if (int rc = complete(s, true)) return rc;
+    if (int rc = complete_or_break(s, true)) return rc;
     if (int rc = strip_err(s, s->small_h[SM_ROUTE + K + 1], "route")) return rc;
     for (uint32_t q = 0; q < K; ++q) counts[q] = s->small_h[SM_ROUTE + q + 1] - s->small_h[SM_ROUTE + q];
-    s->r_ops = d_ops;
-    s->r_n = (uint32_t)n;
-    s->r_nb = nb;
     s->routed = true;
     s->kinds_valid = true;
+    return GWAOI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint64_t *counts) {
+    return gw::api_guard([&]() -> int {
+    if (!s || !counts || (n && !d_ops) || n > 0x7FFFFFFFu || s->row_pending) return GWAOI_EINVAL;
+    if (int rc = route_launch(s, d_ops, n)) return rc;
+    return route_finish(s, counts);
+    });
+}
+
+int gwaoi_strips_route_row_words(const gwaoi_strips *s, uint32_t *words) {
+    return gw::api_guard([&]() -> int {
+    if (!s || !words) return GWAOI_EINVAL;
+    *words = row_words(s->geo.S);
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_strips_route_begin(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint32_t *d_row) {
+    return gw::api_guard([&]() -> int {
+    if (!s || !d_row || (n && !d_ops) || n > 0x7FFFFFFFu || s->row_pending) return GWAOI_EINVAL;
+    if (s->broken) {
+        s->last_error = s->broken_msg;
+        return GWAOI_ESTATE;
+    }
+    if (int rc = route_launch(s, d_ops, n)) return rc;
+    k_route_row<<<1, 256, 0, s->st>>>(s->small_d + SM_ROUTE, s->kstat, s->geo.S, d_row);
+    S_TRY(hipGetLastError());
+    s->row_pending = true;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_strips_route_end(gwaoi_strips *s, const uint32_t *d_matrix, const uint32_t **h_matrix, uint64_t *counts) {
+    return gw::api_guard([&]() -> int {
+    if (!s || !d_matrix || !h_matrix || !counts || !s->row_pending) return GWAOI_EINVAL;
+    s->row_pending = false;
+    const size_t words = (size_t)s->geo.S * row_words(s->geo.S);
+    if (!s->row_h) {
+        S_TRY(hipHostMalloc((void **)&s->row_h, words * sizeof(uint32_t), hipHostMallocDefault));
+    }
+    S_TRY(hipMemcpyAsync(s->row_h, d_matrix, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->st));
+    if (int rc = route_finish(s, counts)) return rc;
+    // every strip's route error (its own was checked by route_finish)
+    const uint32_t W = row_words(s->geo.S);
+    for (uint32_t q = 0; q < s->geo.S; ++q)
+        if (uint32_t e = s->row_h[(size_t)q * W + W - 1]) {
+            s->routed = false;
+            return strip_err(s, e, "route of another strip");
+        }
+    *h_matrix = s->row_h;
     return GWAOI_OK;
     });
 }
@@ -876,7 +982,7 @@ int gwaoi_strips_tick_async(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size
     if (!s || (n_local && !d_local) || (n_recv && !d_recv) || (n_tele && !d_tele) || n_tele > 0x7FFFFFFFu ||
         n_local + n_recv > 0x7FFFFFFFu || n_enter_recs + n_leave_recs > n_local + n_recv)
         return GWAOI_EINVAL;
-    if (int rc = complete(s, false)) return rc;
+    if (int rc = complete_or_break(s, false)) return rc;
     const size_t n_all = n_local + n_recv;
     const uint32_t n_ent = (uint32_t)n_enter_recs, n_lev = (uint32_t)n_leave_recs;
     const uint32_t n_move = (uint32_t)n_all - n_ent - n_lev;
@@ -947,7 +1053,7 @@ int gwaoi_strips_tick_async(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size
 int gwaoi_strips_wait(gwaoi_strips *s, uint64_t *n_enter, uint64_t *n_leave) {
     return gw::api_guard([&]() -> int {
     if (!s) return GWAOI_EINVAL;
-    const int rc = complete(s, false);
+    const int rc = complete_or_break(s, false);
     if (n_enter) *n_enter = s->n_enter;
     if (n_leave) *n_leave = s->n_leave;
     return rc;
@@ -961,7 +1067,7 @@ int gwaoi_strips_tick(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_l
     if (n_enter) *n_enter = 0;
     if (n_leave) *n_leave = 0;
     if (!s || (n_local && !d_local) || (n_recv && !d_recv) || n_local + n_recv > 0x7FFFFFFFu) return GWAOI_EINVAL;
-    if (int rc = complete(s, false)) return rc;
+    if (int rc = complete_or_break(s, false)) return rc;
     // no announced counts: the records' kinds and the box of their Enters are read here first
     const size_t n_all = n_local + n_recv;
     const uint32_t nb = std::max(1u, cdivu(n_all, BT));
@@ -998,7 +1104,7 @@ int gwaoi_strips_host_waits(const gwaoi_strips *s, uint64_t *waits) {
 int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const uint32_t **d_leave) {
     return gw::api_guard([&]() -> int {
     if (!s) return GWAOI_EINVAL;
-    if (int rc = complete(s, false)) return rc;
+    if (int rc = complete_or_break(s, false)) return rc;
     if (d_enter) *d_enter = reinterpret_cast<const uint32_t *>(s->out);
     if (d_leave) *d_leave = reinterpret_cast<const uint32_t *>(s->out + s->n_enter);
     return GWAOI_OK;
@@ -1008,7 +1114,7 @@ int gwaoi_strips_events_device(gwaoi_strips *s, const uint32_t **d_enter, const 
 int gwaoi_strips_events(gwaoi_strips *s, gwaoi_events *out) {
     return gw::api_guard([&]() -> int {
     if (!s || !out) return GWAOI_EINVAL;
-    if (int rc = complete(s, false)) return rc;
+    if (int rc = complete_or_break(s, false)) return rc;
     const uint64_t tot = s->n_enter + s->n_leave;
     if (tot > s->h_cap || !s->h_events) {
         if (s->h_events) (void)hipHostFree(s->h_events);

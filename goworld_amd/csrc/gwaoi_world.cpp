@@ -77,6 +77,7 @@ struct Run {  // a stretch of the op queue: host ops [hbegin, hend) or a device 
     const uint32_t *dsp;             // explicit space per op (nullptr: keep the slot's space)
     uint64_t seq0;
     size_t dn;
+    bool checked;  // a host batch validated while staged (gwaoi_moved_batch): every slot live, finite positions
 };
 
 // Persistent host threads for the validation + staging of big move batches
@@ -216,7 +217,7 @@ struct gwaoi_world {
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
     uint32_t *special = nullptr;  // per previous-frame tile: keygen saw a special entity (the special pass's skip list)
-    uint32_t *tile_work = nullptr;   // per combined tile: candidates swept this flush (k_combined)
+    uint32_t *tile_work = nullptr;   // per combined tile: its measured time this flush (k_combined)
     uint32_t *tile_order = nullptr;  // the next flush's combined tile order, heaviest first (k_tile_order)
     uint32_t *ework = nullptr;       // per frame entry: candidates its lane swept (the next flush's deal to waves)
     bool tile_order_on = true;       // GWAOI_TILE_ORDER=0: tiles in xcd_block order
@@ -284,6 +285,9 @@ struct gwaoi_world {
     size_t stage_cap[2] = {0, 0}, stage_used[2] = {0, 0};
     int stage_cur = 0;
     // zero-copy batch (gwaoi_moved_batch_stage / _commit): the caller fills [slots | x | z | space]
+    // sparse flush (gwaoi_sparse.hip): per-op counts and offsets; off with GWAOI_F_NO_SPARSE
+    uint32_t *sp_cnt = nullptr;
+    bool sparse_on = true;
     size_t resv_n = 0;        // moves reserved (0: no reservation)
     uint32_t *resv_h = nullptr, *resv_d = nullptr;
     int resv_half = 0;
@@ -292,6 +296,23 @@ struct gwaoi_world {
     hipEvent_t out_ev = nullptr;
     bool out_pending = false;  // a copy-out of events queued by gwaoi_tick_end_begin_async, not yet waited for
     bool out_pairs = false;    // ... of one event per mirrored pair (gwaoi_tick_end_begin_pairs_async)
+    // GWAOI_F_BATCH_READY: the first device Moved batch queued while a flush is in flight gets its
+    // claims on mark_st once that flush's apply is done (apply_ev), beside the rest of the flush
+    bool batch_ready = false;
+    hipStream_t mark_st = nullptr;
+    hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
+    bool apply_ev_valid = false;
+    bool premark_late = false;  // the claims beside the pair passes rather than after the apply
+    // the special pass beside the combined pass (GWAOI_SPECIAL_SIDE=0: in line, A/B)
+    bool special_side = true;
+    hipStream_t side_st = nullptr;
+    hipEvent_t side_fork = nullptr, side_join = nullptr;
+    struct {
+        bool on;
+        uint32_t tick;
+        const uint32_t *ds;
+        size_t n;
+    } premark{};
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
@@ -783,14 +804,28 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
     const bool tc = w->timing_mask >> ST_COMBINED & 1u;
     if (tc) S.ev_used[ST_COMBINED] = true;
     const bool order = w->tile_order_on && !rerun;
+    // The special pass needs nothing of the combined pass: it runs beside it on a side stream (in
+    // the combined pass's tail, whose CUs empty as its last tiles drain), unless it is timed.
+    const bool side = w->special_side && !(w->timing_mask >> ST_SPECIAL & 1u);
+    if (side) {
+        HIP_TRY(hipEventRecord(w->side_fork, st));
+        HIP_TRY(hipStreamWaitEvent(w->side_st, w->side_fork, 0));
+        gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn,
+                         half, rerun ? nullptr : w->special, w->side_st);
+        HIP_TRY(hipEventRecord(w->side_join, w->side_st));
+    }
     gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, half,
                         order ? w->tile_order : nullptr, order ? w->tile_work : nullptr, rerun ? nullptr : w->ework,
                         st,
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
-    stage_begin(w, S, ST_SPECIAL);
-    gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn, half,
-                     rerun ? nullptr : w->special, st);
-    stage_end(w, S, ST_SPECIAL);
+    if (side) {
+        HIP_TRY(hipStreamWaitEvent(st, w->side_join, 0));
+    } else {
+        stage_begin(w, S, ST_SPECIAL);
+        gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn,
+                         half, rerun ? nullptr : w->special, st);
+        stage_end(w, S, ST_SPECIAL);
+    }
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
     stage_begin(w, S, ST_FINISH);
     gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->events_tmp, S.events,
@@ -897,6 +932,14 @@ int tick_launch(gwaoi_world *w) {
     // first Moved run's claims
     const bool bucketed = moves_only && w->mv_binned;
     const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
+    // the first run's claims stored already, beside the previous flush (GWAOI_F_BATCH_READY)
+    if (mark && w->premark.on && w->premark.tick == tick_id && w->premark.ds == RS.r[0].ds &&
+        w->premark.n == RS.r[0].n) {
+        HIP_TRY(hipStreamWaitEvent(st, w->mark_ev, 0));
+        mark = nullptr;
+        w->dbg.premarked_runs++;
+    }
+    w->premark.on = false;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
@@ -926,7 +969,7 @@ int tick_launch(gwaoi_world *w) {
     if (bucketed) {  // the per-tick position sync: ops regrouped by slot bucket, last op per slot in LDS
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
-    } else if (moves_only) {  // one pass + fixup of repeated slots
+    } else if (moves_only) {  // one pass + fixup of repeated slots (run 0's claims: prologue or premark)
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                          P.rec, n_prev, S.sc, w->coll, 1u, st);
     } else if (n_ops) {
@@ -972,6 +1015,10 @@ int tick_launch(gwaoi_world *w) {
         }
     }
     stage_end(w, S, ST_APPLY);
+    if (w->batch_ready && !w->premark_late) {  // from here on this flush no longer reads the claims
+        HIP_TRY(hipEventRecord(w->apply_ev, st));
+        w->apply_ev_valid = true;
+    }
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
@@ -1016,6 +1063,11 @@ int tick_launch(gwaoi_world *w) {
         stage_end(w, S, ST_CELLS);
     }
 
+    // the next batch's claims beside the pair passes instead (GWAOI_PREMARK_LATE=1: A/B)
+    if (w->batch_ready && w->premark_late) {
+        HIP_TRY(hipEventRecord(w->apply_ev, st));
+        w->apply_ev_valid = true;
+    }
     // ---- pair passes: combined over the new grid, special entities over the previous one
     const uint64_t ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view);
 
@@ -1124,18 +1176,28 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
     }
     // compared with the capacity the passes had at launch: a regrow by another flush since then
     // (shared scratch, or the twin set's catch-up) does not make the clipped events complete
-    if (r.total64 > f.cap) {  // grow and re-run the pair passes
+    // The scratch extent is not the event count: the pair passes deal their pairs to the event
+    // streams by the XCD each block lands on, so a re-run's extent may differ from the overflowed
+    // run's.  The first re-run is sized for the extent seen; a second one for the worst case (every
+    // pair in one stream), which cannot overflow.
+    uint64_t cap_used = f.cap;
+    for (int attempt = 0; r.total64 > cap_used; ++attempt) {  // grow and re-run the pair passes
         stage_collect(w, S);
         if (w->inject_regrow_fail) {
             w->last_error = "event buffer regrow failed (injected)";
             return poison(w, GWAOI_ENOMEM);
         }
-        if ((rc = ensure_events(w, S, r.total64))) return poison(w, rc);
+        if (attempt == 2) {
+            w->last_error = "pair passes re-run: the event extent exceeds its worst-case bound";
+            return poison(w, GWAOI_EDEVICE);
+        }
+        const uint64_t need = attempt == 0 ? r.total64 : std::max<uint64_t>(r.total64, gw::ev_worst_extent(r.n_total));
+        if ((rc = ensure_events(w, S, need))) return poison(w, rc);
         (void)hipGetLastError();  // a failure of an unrelated earlier call is not this re-run's
         gw::launch_zero(w->tile_total, gw::tile_total_elems(f.entries), st);
-        gw::launch_zero(reinterpret_cast<uint32_t *>(&S.sc->counter), 2, st);
+        gw::launch_zero(&S.sc->shard[0][0], gw::EV_SHARDS * 32, st);  // event streams
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
-        if (launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true) < r.total64) {
+        if ((cap_used = launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true)) < need) {
             w->last_error = "pair passes re-run: event buffers did not grow";
             return poison(w, GWAOI_EDEVICE);
         }
@@ -1145,6 +1207,10 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
             return poison(w, GWAOI_EDEVICE);
         }
         r = *tick_out(S);
+        if (r.total64 > 0xFFFFFFFFull) {
+            w->last_error = "more than 2^32-1 events in one flush";
+            return poison(w, GWAOI_ECAPACITY);
+        }
     }
     stage_collect(w, S);
 
@@ -1208,6 +1274,88 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
 }
 
 int tick_finish(gwaoi_world *w, bool *committed) { return finish_flight(w, w->fl, false, committed); }
+
+// The sparse flush (gwaoi_sparse.hip): a queue of a few host Moved calls, nothing in flight,
+// becomes events and an in-place patch of the committed frame, without the frame rebuild.
+// Returns GWAOI_OK when it committed, 1 when it was not taken or the device declined it (nothing
+// changed: the caller runs the full flush over the same queue), or an error.
+constexpr size_t kSparseMaxOps = 256;
+int sparse_try(gwaoi_world *w) {
+    if (!w->sparse_on || w->in_flight || w->n_ops == 0 || w->n_ops > kSparseMaxOps || !w->new_slots.empty() ||
+        w->space_ops_queued || w->dev_app || w->dev_struct || w->dev_seq_pending || !w->deferred.empty() ||
+        w->resv_n || w->ticks == 0 || w->runs.size() != 1)
+        return 1;
+    const Run &run = w->runs[0];
+    // one stretch of host calls, or one host batch staged as a device batch (validated on the host,
+    // implicit seqs, every slot in its own space); never a caller's device batch (checked on the device)
+    if (run.device && (run.kind != RUN_MOVE || !run.checked || run.dseq || run.dsp)) return 1;
+    DevFrame &P = w->fr[w->cur];
+    if (P.n == 0) return 1;
+    for (uint32_t sp : w->h_op_sp)
+        if (sp == gw::SP_DEAD) return 1;
+    const uint32_t k = (uint32_t)w->n_ops;
+    hipStream_t st = w->stream;
+    const int set = w->launch_set;
+    FlushSet &S = w->fs[set];
+    int rc;
+    if (!w->sp_cnt && (rc = dalloc(w, &w->sp_cnt, gw::sparse_cnt_elems((uint32_t)kSparseMaxOps)))) return rc;
+    if (w->out_pending) HIP_TRY(hipStreamWaitEvent(st, w->out_ev, 0));  // a copy-out still reads S's events
+    const uint32_t *d_slot = run.ds;
+    const float *d_x = run.dx, *d_z = run.dz;
+    const unsigned long long *d_seq = nullptr;
+    if (!run.device) {
+        if ((rc = ensure_ops(w, k))) return rc;
+        HIP_TRY(hipMemcpyAsync(w->op_slot, w->h_op_slot.data(), k * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->op_x, w->h_op_x.data(), k * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->op_z, w->h_op_z.data(), k * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(w->op_seq, w->h_op_seq.data(), k * 8, hipMemcpyHostToDevice, st));
+        d_slot = w->op_slot;
+        d_x = w->op_x;
+        d_z = w->op_z;
+        d_seq = w->op_seq;
+    } else if (w->copy_pending) {  // the staged batch's H2D lands first
+        HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
+        w->copy_pending = false;
+    }
+    const uint32_t tick_id = ++w->tick_id;
+    HIP_TRY(hipMemsetAsync(&S.sc->err, 0, sizeof(uint32_t), st));
+    gw::launch_ops_claim(d_slot, k, 0, w->max_slots, w->sinfo, tick_id, S.sc, st);
+    gw::launch_sparse(P.rec, P.ss, P.key, P.cell_start, P.grid, w->sinfo, d_slot, d_x, d_z, d_seq, run.seq0, k,
+                      tick_id, w->sp_cnt, S.events, S.ev_cap, reinterpret_cast<gw::TickOut *>(S.d_hout), st);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(S.done_ev, st) != hipSuccess) {
+        w->last_error = "sparse flush launch failed";
+        return poison(w, GWAOI_EDEVICE);  // the frame may be half patched
+    }
+    if (wait_done(w, S.done_ev) != GWAOI_OK) {
+        w->last_error = "sparse flush did not complete: " + w->last_error;
+        return poison(w, GWAOI_EDEVICE);
+    }
+    const gw::TickOut r = *tick_out(S);
+    if (r.pad) {  // declined on the device before any write to the frame
+        w->dbg.sparse_declined++;
+        return 1;
+    }
+    // ---- commit: the frame is patched in place (same frame index); the events are set S's
+    w->dbg.flushes++;
+    w->dbg.sparse_flushes++;
+    w->last_n_enter = r.n_enter;
+    w->last_n_leave = (uint64_t)r.n_total - r.n_enter;
+    w->rel_pairs += (int64_t)w->last_n_enter - (int64_t)w->last_n_leave;
+    w->last_set = set;
+    w->launch_set ^= 1;
+    w->h_op_slot.clear();
+    w->h_op_x.clear();
+    w->h_op_z.clear();
+    w->h_op_sp.clear();
+    w->h_op_seq.clear();
+    w->runs.clear();
+    w->n_ops = 0;
+    w->seq_floor = w->seq_next;
+    w->ticks++;
+    // the staged batch was read (the stream was waited for): its staging words are free again
+    if (run.device) w->stage_used[w->stage_cur] = 0;
+    return GWAOI_OK;
+}
 
 // Whether the calls queued during the flush in flight allow launching the next
 // flush before the one in flight has committed: device Moved batches only
@@ -1277,7 +1425,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_base);
+    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_base); dfree(w->sp_cnt);
     dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);
@@ -1289,6 +1437,14 @@ int gwaoi_world_destroy(gwaoi_world *w) {
         if (w->h_stage[h]) (void)hipHostFree(w->h_stage[h]);
         dfree(w->d_stage[h]);
     }
+    if (w->side_st) (void)hipStreamSynchronize(w->side_st);
+    if (w->side_fork) (void)hipEventDestroy(w->side_fork);
+    if (w->side_join) (void)hipEventDestroy(w->side_join);
+    if (w->side_st) (void)hipStreamDestroy(w->side_st);
+    if (w->mark_st) (void)hipStreamSynchronize(w->mark_st);
+    if (w->apply_ev) (void)hipEventDestroy(w->apply_ev);
+    if (w->mark_ev) (void)hipEventDestroy(w->mark_ev);
+    if (w->mark_st) (void)hipStreamDestroy(w->mark_st);
     if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
     if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
     if (w->out_st) (void)hipStreamSynchronize(w->out_st);
@@ -1315,6 +1471,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->cells_per_dist = cfg->cells_per_dist > 0.f ? cfg->cells_per_dist : 3.0f;
     w->cells_auto = !(cfg->cells_per_dist > 0.f);
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
+    w->sparse_on = !(cfg->flags & GWAOI_F_NO_SPARSE);
+    if (const char *e = std::getenv("GWAOI_SPARSE")) w->sparse_on = w->sparse_on && e[0] != '0';
     if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_FORCE_COPY")) w->force_copy = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_INJECT_REGROW_FAIL")) w->inject_regrow_fail = e[0] == '1';
@@ -1355,6 +1513,18 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         w->out_ev = nullptr;
         return fail(GWAOI_EDEVICE);
     }
+    if (hipStreamCreateWithFlags(&w->side_st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&w->side_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->side_join, hipEventDisableTiming) != hipSuccess)
+        return fail(GWAOI_EDEVICE);
+    if (const char *e = std::getenv("GWAOI_SPECIAL_SIDE")) w->special_side = e[0] != '0';
+    w->batch_ready = (cfg->flags & GWAOI_F_BATCH_READY) != 0;
+    if (const char *e = std::getenv("GWAOI_BATCH_READY")) w->batch_ready = w->batch_ready && e[0] != '0';  // A/B
+    if (const char *e = std::getenv("GWAOI_PREMARK_LATE")) w->premark_late = e[0] == '1';
+    if (w->batch_ready && (hipStreamCreateWithFlags(&w->mark_st, hipStreamNonBlocking) != hipSuccess ||
+                           hipEventCreateWithFlags(&w->apply_ev, hipEventDisableTiming) != hipSuccess ||
+                           hipEventCreateWithFlags(&w->mark_ev, hipEventDisableTiming) != hipSuccess))
+        return fail(GWAOI_EDEVICE);
     const size_t N = w->max_slots;
     for (DevFrame &f : w->fr) {
         if ((rc = dalloc(w, &f.rec, N)) || (rc = dalloc(w, &f.ss, N)) || (rc = dalloc(w, &f.key, N)) ||
@@ -1388,7 +1558,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / gw::COMBINED_TILE + 2)) ||
-        (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 8)) || (rc = dalloc(w, &w->ework, N)) ||
+        (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 16)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess ||  // no order yet
@@ -1561,6 +1731,9 @@ constexpr size_t kStageMinBatch = 64;  // smaller host batches queue as host ops
 // batch still points into (the caller then queues the batch as host ops).
 int ensure_stage(gwaoi_world *w, size_t words) {
     const int h = w->stage_cur;
+    // an open reservation (gwaoi_moved_batch_stage) owns the words past stage_used until its commit:
+    // nothing else may stage into them, and the buffer it points into must not move
+    if (w->resv_n) return 1;
     if (w->stage_used[h] + words <= w->stage_cap[h]) return GWAOI_OK;
     if (w->stage_used[h]) return 1;
     const size_t cap = std::max<size_t>({2 * words, 2 * w->stage_cap[h], (size_t)4 << 16});
@@ -1680,6 +1853,7 @@ int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const flo
     r.dsp = with_space ? d + 3 * n : nullptr;
     r.seq0 = w->seq_next;
     r.dn = n;
+    r.checked = true;
     w->seq_next += n;
     for (unsigned t = 0; t < T; ++t)
         for (size_t sp = 0; sp < nsp; ++sp) {
@@ -1830,6 +2004,21 @@ int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const floa
     r.dn = n;
     w->seq_next += n;
     if (w->in_flight) {
+        // the next flush's first run (nothing else deferred yet): its claims beside the flush in
+        // flight, once that flush's apply is done (the batch is complete: GWAOI_F_BATCH_READY)
+        if (w->batch_ready && w->deferred.empty() && w->apply_ev_valid && !w->mv_binned &&
+            w->fl.tick_id == w->tick_id) {
+            gw::MoveRun m{};
+            m.ds = d_slots; m.dx = d_x; m.dz = d_z; m.seq0 = r.seq0; m.sp_def = gw::SP_KEEP;
+            m.j0 = 0; m.n = (uint32_t)n;
+            HIP_TRY(hipStreamWaitEvent(w->mark_st, w->apply_ev, 0));
+            gw::launch_moves_mark(m, w->max_slots, w->sinfo, w->tick_id + 1, w->mark_st);
+            HIP_TRY(hipEventRecord(w->mark_ev, w->mark_st));
+            w->premark.on = true;
+            w->premark.tick = w->tick_id + 1;
+            w->premark.ds = d_slots;
+            w->premark.n = n;
+        }
         Deferred q{};
         q.kind = Deferred::RUN;
         q.run = r;
@@ -2361,6 +2550,15 @@ int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
 }
 
 int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
+    const int sp = w ? gw::api_guard([&]() -> int {
+        GW_LIVE(w);
+        return sparse_try(w);
+    }) : 1;
+    if (sp <= 0) {
+        if (n_enter) *n_enter = sp == GWAOI_OK ? w->last_n_enter : 0;
+        if (n_leave) *n_leave = sp == GWAOI_OK ? w->last_n_leave : 0;
+        return sp;
+    }
     if (int rc = gwaoi_tick_begin(w)) {
         if (n_enter) *n_enter = 0;
         if (n_leave) *n_leave = 0;
@@ -2382,6 +2580,26 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
     if (!w || !out) return GWAOI_EINVAL;
     out->n_enter = out->n_leave = 0;
     out->enter = out->leave = nullptr;
+    const int sp = gw::api_guard([&]() -> int {
+        GW_LIVE(w);
+        const int rc = sparse_try(w);
+        if (rc != GWAOI_OK) return rc;
+        // the sparse flush's events to host memory
+        const uint64_t tot = w->last_n_enter + w->last_n_leave;
+        if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
+        w->out_pairs = false;
+        if (tot) {
+            HIP_TRY(hipMemcpyAsync(w->h_events, w->fs[w->last_set].events, 2 * tot * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, w->stream));
+            if (int rw = wait_stream(w)) return poison(w, rw);
+        }
+        out->n_enter = w->last_n_enter;
+        out->n_leave = w->last_n_leave;
+        out->enter = w->h_events;
+        out->leave = w->h_events + 2 * w->last_n_enter;
+        return GWAOI_OK;
+    });
+    if (sp <= 0) return sp;  // committed sparse flush, or an error
     if (int rc = gwaoi_tick_begin(w)) return rc;
     return gwaoi_tick_end(w, out);
 }

@@ -10,9 +10,10 @@ halo H of its strip.  Each tick:
    entities the rank owned before it (Moved / Leave) or that enter the space
    inside its strip (Enter) become halo records per destination rank, plus
    teleport records (HIP kernels, ``k_route``).
-2. ``exchange``: the per-destination counts (already on the host, with how
-   many of them are ENTER / LEAVE records and the box of the ENTERs) are
-   all-gathered over gloo, then the records go point to point in one
+2. ``exchange``: the per-destination counts (with how many of them are
+   ENTER / LEAVE records and the box of the ENTERs) are all-gathered on the
+   device by the route itself (RCCL, between its kernels and its one host
+   wait; gloo on host tensors in a gloo job), then the records go point to point in one
    ``batch_isend_irecv`` group over RCCL (xGMI) -- to the two neighbour
    strips only, when strips are at least H + teleport wide; teleport records
    go to every rank only when some rank has any.  This is the path's one real
@@ -122,6 +123,56 @@ def merge_kinds(parts) -> tuple:
     return ne, nl, (b if ne else None)
 
 
+def row_words(S: int) -> int:
+    """Words of a strip's device count row (gwaoi_strips_route_begin)."""
+    return S + 1 + 6 * S + 1
+
+
+def _o2f(v) -> np.ndarray:
+    """Order-preserving int32 (the device's box words) -> float32."""
+    i = np.asarray(v, np.uint32).view(np.int32)
+    return np.where(i >= 0, i, i ^ np.int32(0x7FFFFFFF)).astype(np.int32).view(np.float32)
+
+
+def _f2o(v) -> np.ndarray:
+    """float32 -> order-preserving int32 bits (uint32), the device box words."""
+    i = np.asarray(v, np.float32).view(np.int32)
+    return np.where(i >= 0, i, i ^ np.int32(0x7FFFFFFF)).astype(np.int32).view(np.uint32)
+
+
+def count_row(counts, n_tele: int, kinds, err: int = 0) -> np.ndarray:
+    """The count row gwaoi_strips_route_begin writes on the device (k_route_row), built on the
+    host from a route's counts and kinds (CPU model, tests)."""
+    S = len(counts)
+    ent, lev, box = kinds
+    row = np.zeros(row_words(S), np.uint32)
+    row[:S] = np.asarray(counts, np.int64)
+    row[S] = n_tele
+    for d in range(S):
+        k = row[S + 1 + 6 * d:S + 7 + 6 * d]
+        k[0], k[1] = int(ent[d]), int(lev[d])
+        # an empty box is the device's fold identity (INT_MAX, INT_MAX, INT_MIN, INT_MIN)
+        k[2:6] = _f2o(box[d]) if int(ent[d]) else np.array([0x7FFFFFFF, 0x7FFFFFFF, 0x80000000, 0x80000000], np.uint32)
+    row[-1] = err
+    return row
+
+
+def matrix_counts(matrix: np.ndarray, S: int) -> np.ndarray:
+    """M[src, dst] (records) and M[src, S] (teleports) from the gathered device rows."""
+    return np.asarray(matrix[:, :S + 1], np.uint32).astype(np.int64)
+
+
+def matrix_kinds(matrix: np.ndarray, S: int, rank: int) -> tuple:
+    """This receiver's (enters, leaves, box) from the gathered device rows (merge_kinds)."""
+    parts = []
+    for q in range(S):
+        k = np.asarray(matrix[q, S + 1 + 6 * rank:S + 1 + 6 * rank + 6], np.uint32)
+        ent, lev = int(k[0]), int(k[1])
+        box = _o2f(k[2:6]) if ent else np.array([np.inf, np.inf, -np.inf, -np.inf], np.float32)
+        parts.append((ent, lev, box))
+    return merge_kinds(parts)
+
+
 def as_words(rec: np.ndarray, words: int):
     """Structured records -> torch int32 (n, words) view (CPU tensor)."""
     import torch
@@ -158,6 +209,11 @@ class StripShard:
         # consumers of its buffers are ordered by stream waits, not host synchronisation
         self._host_sync = os.environ.get("GWAOI_STRIPS_HOSTSYNC", "0") == "1"  # A/B: host waits instead
         self._inflight = []  # tensors the world's stream may still read (released by finish's host wait)
+        w = C.c_uint32()
+        self._check(self._L.gwaoi_strips_route_row_words(self._s, C.byref(w)))
+        self.row_words = w.value
+        self._row = self._mat = self._ext = None  # device count rows (route with dist)
+        self.matrix = None  # every strip's count row of the last route with dist (numpy, S x row_words)
 
     def _cur(self) -> int:
         return self.torch.cuda.current_stream(self.dev).cuda_stream
@@ -197,15 +253,41 @@ class StripShard:
         return rc
 
     # ---- step 1: route this tick's owned ops
-    def route(self, ops):
+    def route(self, ops, dist=None, group=None):
         """ops: device int32 (n, 6) tensor of HALO_DTYPE records.  Returns
         (send (m,6) int32 grouped by destination rank, counts[n_strips] int64,
-        tele (k,10) int32)."""
+        tele (k,10) int32).
+
+        dist: the count exchange happens here, on the device: this strip's
+        count row is all-gathered from every rank of ``group`` (RCCL over xGMI
+        with the nccl backend) on the world's stream, between the route's
+        kernels and its one host wait (gwaoi_strips_route_begin / _end);
+        ``self.matrix`` then holds every strip's row for ``exchange``, which
+        needs no host collective."""
         torch = self.torch
         n = int(ops.shape[0])
         self._after_torch(ops)
         counts = (C.c_uint64 * (self.n_strips + 1))()  # the one host wait of the route: the counts
-        self._check(self._L.gwaoi_strips_route(self._s, C.c_void_p(ops.data_ptr() if n else 0), n, counts))
+        pops = C.c_void_p(ops.data_ptr() if n else 0)
+        if dist is None:
+            self.matrix = None
+            self._check(self._L.gwaoi_strips_route(self._s, pops, n, counts))
+        else:
+            S, W = self.n_strips, self.row_words
+            if self._row is None:  # persistent: the world's stream and the collective reuse them every tick
+                self._row = torch.zeros(W, dtype=torch.int32, device=self.dev)
+                self._mat = torch.zeros(S * W, dtype=torch.int32, device=self.dev)
+                self._ext = torch.cuda.ExternalStream(self.world.stream(), device=self.dev)
+            self._check(self._L.gwaoi_strips_route_begin(self._s, pops, n, C.c_void_p(self._row.data_ptr())))
+            with torch.cuda.stream(self._ext):  # ordered after the route's kernels, before its D2H
+                if dist.get_backend(group) == "nccl":
+                    dist.all_gather_into_tensor(self._mat, self._row, group=group)
+                else:  # gloo rehearsal (CUDA tensors staged through the host by gloo)
+                    dist.all_gather([self._mat[q * W:(q + 1) * W] for q in range(S)], self._row, group=group)
+            hp = C.c_void_p()
+            self._check(self._L.gwaoi_strips_route_end(self._s, C.c_void_p(self._mat.data_ptr()), C.byref(hp),
+                                                      counts))
+            self.matrix = np.ctypeslib.as_array(C.cast(hp, C.POINTER(C.c_uint32)), shape=(S, W)).copy()
         c = np.array(counts[:], np.int64)
         S = self.n_strips
         ent, lev = (C.c_uint64 * S)(), (C.c_uint64 * S)()
@@ -321,7 +403,7 @@ def count_group(dist, group=None):
     return _COUNT_GROUPS[key]
 
 
-def exchange(dist, send, counts, tele, group=None, via_cpu=False, kinds=None):
+def exchange(dist, send, counts, tele, group=None, via_cpu=False, kinds=None, matrix=None):
     """The halo exchange of one tick over torch.distributed: the count matrix
     is all-gathered on the host (gloo, ``count_group``), then every record
     travels point to point, batched in one group (``batch_isend_irecv``:
@@ -335,29 +417,37 @@ def exchange(dist, send, counts, tele, group=None, via_cpu=False, kinds=None):
     ranks sharing one GPU; RCCL allows one rank per device).
     kinds: this rank's route statistics (enters[S], leaves[S], boxes[S, 4]);
     they travel in the same count row, and the receiver's merged
-    (enters, leaves, box) is returned third (for ``StripShard.finish``)."""
+    (enters, leaves, box) is returned third (for ``StripShard.finish``).
+    matrix: every strip's device count row, already gathered by
+    ``StripShard.route(ops, dist)`` (``shard.matrix``): no host collective
+    here; with kinds, the receiver's statistics come from it."""
     import torch
     if via_cpu and send.is_cuda:
         dev = send.device
         torch.cuda.current_stream(dev).synchronize()
-        res = exchange(dist, send.cpu(), counts, tele.cpu(), group, kinds=kinds)
+        res = exchange(dist, send.cpu(), counts, tele.cpu(), group, kinds=kinds, matrix=matrix)
         return (res[0].to(dev), res[1].to(dev)) + tuple(res[2:])
     S = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = send.device
-    row = list(np.asarray(counts, np.int64)) + [int(tele.shape[0])]
-    if kinds is not None:
-        ent, lev, box = kinds
-        row += list(np.asarray(ent, np.int64)) + list(np.asarray(lev, np.int64))
-        row += list(np.ascontiguousarray(box, np.float32).reshape(-1).view(np.int32).astype(np.int64))
-    mine = torch.tensor(row, dtype=torch.int64)
-    rows = [torch.empty_like(mine) for _ in range(S)]
-    dist.all_gather(rows, mine, group=count_group(dist, group))
-    M = torch.stack(rows).numpy()  # M[src, dst]; column S = teleports of src (host tensors: no device sync)
     rk = None
-    if kinds is not None:  # the senders' statistics for this receiver
-        bx = M[:, 3 * S + 1:].astype(np.int32).view(np.float32).reshape(S, S, 4)
-        rk = merge_kinds([(M[q, S + 1 + rank], M[q, 2 * S + 1 + rank], bx[q, rank]) for q in range(S)])
+    if matrix is not None:
+        M = matrix_counts(matrix, S)  # M[src, dst]; column S = teleports of src
+        if kinds is not None:
+            rk = matrix_kinds(matrix, S, rank)
+    else:
+        row = list(np.asarray(counts, np.int64)) + [int(tele.shape[0])]
+        if kinds is not None:
+            ent, lev, box = kinds
+            row += list(np.asarray(ent, np.int64)) + list(np.asarray(lev, np.int64))
+            row += list(np.ascontiguousarray(box, np.float32).reshape(-1).view(np.int32).astype(np.int64))
+        mine = torch.tensor(row, dtype=torch.int64)
+        rows = [torch.empty_like(mine) for _ in range(S)]
+        dist.all_gather(rows, mine, group=count_group(dist, group))
+        M = torch.stack(rows).numpy()  # M[src, dst]; column S = teleports of src (host tensors: no device sync)
+        if kinds is not None:  # the senders' statistics for this receiver
+            bx = M[:, 3 * S + 1:].astype(np.int32).view(np.float32).reshape(S, S, 4)
+            rk = merge_kinds([(M[q, S + 1 + rank], M[q, 2 * S + 1 + rank], bx[q, rank]) for q in range(S)])
     off = np.concatenate([[0], np.cumsum(M[rank, :S])]).astype(np.int64)
     peer = (lambda q: q) if group is None else (lambda q: dist.get_global_rank(group, q))
     T = M[:, S]  # teleport records per source rank
@@ -411,12 +501,16 @@ def exchange_local(outs: List[Tuple], kinds=None):
     return res
 
 
-def tile_tick(shard: StripShard, dist, ops, group=None, via_cpu=False):
+def tile_tick(shard: StripShard, dist, ops, group=None, via_cpu=False, device_counts=None):
     """One tick of this rank's strip in a torch.distributed job: route (the tick's one host
     wait, which also completes the previous tick), exchange, and the tick queued on the GPU
-    (``shard.wait()`` / ``shard.events()`` complete it)."""
-    send, counts, tele = shard.route(ops)
-    recv, tele_all, kinds = exchange(dist, send, counts, tele, group=group, via_cpu=via_cpu, kinds=shard.kinds)
+    (``shard.wait()`` / ``shard.events()`` complete it).  device_counts (default: the group's
+    backend is nccl): the count rows are all-gathered on the device inside the route."""
+    if device_counts is None:
+        device_counts = dist.get_backend(group) == "nccl"
+    send, counts, tele = shard.route(ops, dist, group) if device_counts else shard.route(ops)
+    recv, tele_all, kinds = exchange(dist, send, counts, tele, group=group, via_cpu=via_cpu, kinds=shard.kinds,
+                                     matrix=shard.matrix)
     shard.finish(local_slice(send, counts, dist.get_rank(group)), recv, tele_all, kinds=kinds)
     return send, counts, recv
 

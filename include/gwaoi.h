@@ -78,6 +78,11 @@ typedef struct {
 } gwaoi_config;
 
 #define GWAOI_F_TIMING 1u /* time every pipeline stage with HIP events (gwaoi_stage_times) */
+#define GWAOI_F_NO_SPARSE 2u /* never take the sparse flush (every flush rebuilds the frame; A/B, tests) */
+/* Device Moved batches (gwaoi_moved_batch_device) are complete in memory when passed, not
+ * produced on another stream behind gwaoi_stream_after: a batch queued while a flush is in
+ * flight then has its last-op claims stored beside that flush, off the next flush's path. */
+#define GWAOI_F_BATCH_READY 4u
 
 typedef struct {
     uint64_t n_enter;      /* directed enter events; replay pair (a,b) as a.OnEnterAOI(b) */
@@ -112,6 +117,9 @@ typedef struct {
     uint32_t cells_per_dist;        /* cells per AOI distance of the grids in use (2 or 3 when automatic)    */
     uint32_t pad;
     uint64_t incremental_sorts;     /* flush launches whose frame sort was the per-cell merge (grid unchanged) */
+    uint64_t sparse_flushes;        /* flushes of a few Moved calls done on the frame in place (gwaoi_tick*) */
+    uint64_t sparse_declined;       /* sparse flushes that fell back to the full one (long shifts, capacity)  */
+    uint64_t premarked_runs;        /* flushes whose first batch's claims were stored beside the flush before */
 } gwaoi_debug;
 
 typedef struct {

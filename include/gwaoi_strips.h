@@ -96,6 +96,22 @@ int gwaoi_strips_halo(const gwaoi_strips *s, float *halo);
  * = records for each destination rank, counts[n_strips] = teleport records.
  * Returns GWAOI_ESTATE if an op names an entity this strip does not own. */
 int gwaoi_strips_route(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint64_t *counts);
+/* 1'. The same route with the count exchange on the device (multi-GPU: no
+ * host collective per tick).  _begin queues the route and writes this
+ * strip's count row to d_row (device, gwaoi_strips_route_row_words words):
+ *   [records to each strip (n_strips) | teleport records |
+ *    per destination: ENTER, LEAVE, ENTER box x0 z0 x1 z1 (6 words each; the
+ *    box as order-preserving ints) | route error word];
+ * nothing waits.  The caller then gathers the rows of all strips, in rank
+ * order, into d_matrix (n_strips rows) on the world's stream (an RCCL
+ * all-gather over xGMI: goworld_amd/strips.py), and _end copies the matrix
+ * to host memory owned by the strip (*h_matrix, valid until the next _end)
+ * with the tick's one host wait, which also completes the previous tick.
+ * counts and gwaoi_strips_route_kinds as after gwaoi_strips_route; _end
+ * fails if any strip's row carries a route error. */
+int gwaoi_strips_route_row_words(const gwaoi_strips *s, uint32_t *words);
+int gwaoi_strips_route_begin(gwaoi_strips *s, const gwaoi_halo_rec *d_ops, size_t n, uint32_t *d_row);
+int gwaoi_strips_route_end(gwaoi_strips *s, const uint32_t *d_matrix, const uint32_t **h_matrix, uint64_t *counts);
 /* 2. Write the routed records: d_send holds sum(counts[0..n_strips-1])
  * records grouped by destination rank (rank order), d_tele counts[n_strips].
  * Returns after the writes completed (the caller's transport may read them). */
@@ -118,7 +134,14 @@ int gwaoi_strips_route_kinds(const gwaoi_strips *s, uint64_t *enters, uint64_t *
  * on the world's stream and returns; the inputs must stay valid until it
  * completes (the next gwaoi_strips_route, gwaoi_strips_wait, _events,
  * _events_device or _destroy).  Problems found on the device are reported
- * by the call that completes it. */
+ * by the call that completes it.  The records are not validated before the
+ * world consumes them: a bad record (slot out of range, a kind that is not
+ * MOVE / ENTER / LEAVE, an ENTER of a slot the strip holds, a MOVE / LEAVE of
+ * one it does not) fails that completing call, and the strip is unusable
+ * from then on -- every later call returns GWAOI_ESTATE, and its world is
+ * poisoned when a record reached it in the wrong state (gwaoi_tick).  An
+ * unknown kind reaches the world as a no-op.  gwaoi_strips_tick validates
+ * first and leaves the state untouched on such an error. */
 int gwaoi_strips_tick_async(gwaoi_strips *s, const gwaoi_halo_rec *d_local, size_t n_local,
                             const gwaoi_halo_rec *d_recv, size_t n_recv, const gwaoi_tele_rec *d_tele, size_t n_tele,
                             uint64_t n_enter_recs, uint64_t n_leave_recs, const float *enter_box);

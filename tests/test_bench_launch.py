@@ -53,3 +53,23 @@ def test_spawn_propagates_rank_failure(monkeypatch, tmp_path):
     assert bench.spawn_ranks(bench.launch_plan(2, dict(os.environ))) == 3
     script.write_text("import sys\nsys.exit(0)\n")
     assert bench.spawn_ranks(bench.launch_plan(3, dict(os.environ))) == 0
+
+
+def test_line_summary_is_last_and_compact():
+    """The headline numbers of every leg close the JSON line (a stdout tail keeps them)."""
+    out = {"ms_per_step": 0.21, "p99_tick_ms": 0.23, "roofline": {"avg_launch_ms": 0.07, "frac": 0.08},
+           "host_to_host_tick": {"ms_per_step": 0.35, "p50_tick_ms": 0.6, "p99_tick_ms": 0.7,
+                                 "serial_p99_tick_ms": 0.69},
+           "small_flush": {"1": {"device": {"p50_ms": 0.05}}, "note": "x"},
+           "cfg5_strips": {"error": "cfg5 child job: exit timeout"}, "cpu_baseline": None}
+    s = bench.line_summary(out)
+    assert s["host_to_host_p99_ms"] == 0.7 and s["combined_ms"] == 0.07
+    assert s["small_flush_p50_ms"] == {"1": 0.05}
+    assert s["cfg5_error"].startswith("cfg5 child job") and s["cpu_grid_ms_per_tick"] is None
+    assert len(__import__("json").dumps(s)) < 1200
+
+
+def test_cpu_core_counts_bounded_by_affinity():
+    c = bench.cpu_core_counts()
+    assert 1 <= c["used"] <= c["affinity"]
+    assert c["cgroup_quota"] is None or c["used"] <= c["cgroup_quota"]

@@ -657,9 +657,9 @@ def test_chain_free_offsets_at_tile_boundaries_gpu(monkeypatch, oracle_mod, n):
     wl = make_workload("cfg2", n=n)
     slots, x0, z0, _ = wl.initial()
     monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
-    wr = World(n, cells_per_dist=3.0)
+    wr = World(n, cells_per_dist=3.0, sparse=False)  # full flushes only: the sort paths are the subject
     monkeypatch.delenv("GWAOI_FORCE_RADIX")
-    wi = World(n, cells_per_dist=3.0)
+    wi = World(n, cells_per_dist=3.0, sparse=False)
     ref = oracle_mod.SpacesOracle({0: wl.D}, n)
     try:
         for w in (wr, wi):
@@ -1088,13 +1088,15 @@ def _device_events(w, ne, nl):
     return out
 
 
-@pytest.mark.parametrize("event_capacity,repeats", [(0, False), (3000, False), (0, True)])
-def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
+@pytest.mark.parametrize("event_capacity,repeats,ready", [(0, False, False), (3000, False, False), (0, True, False),
+                                                          (0, True, True), (3000, False, True)])
+def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats, ready):
     """gwaoi_tick_end_begin_device: the next flush queued before the commit of the one in
     flight (device Moved batches only) gives every flush the events of the serial path -- also when the
     flush in flight overflows its event buffer and is re-run after its successor
     (event_capacity=3000), when a batch moves slots more than once (repeats: the last
-    call wins), and when a host call in flight forces the fallback."""
+    call wins), and when a host call in flight forces the fallback.  ready
+    (GWAOI_F_BATCH_READY): the next batch's claims are stored beside the flush in flight."""
     torch = pytest.importorskip("torch")
     n = 20000
     wa, wb = make_workload("cfg2", n=n), make_workload("cfg2", n=n)
@@ -1116,7 +1118,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
         batches.append([torch.from_numpy(a).to("cuda:0") for a in (sl.astype(np.int32), nx, nz)])
     torch.cuda.synchronize()
     cap = 2 * n if repeats else n  # a speculative launch takes at most max_slots ops
-    with World(cap, event_capacity=event_capacity) as A, World(cap) as B:
+    with World(cap, event_capacity=event_capacity, batch_ready=ready) as A, World(cap) as B:
         for w in (A, B):
             s = w.space_create(wa.D)
             w.enter_batch(s, slots, x0, z0)
@@ -1143,6 +1145,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"tick {t}: leaves")
         d = A.debug_counters()
         assert d["speculative_launches"] >= ticks - 3
+        assert (d["premarked_runs"] >= ticks - 3) if ready else d["premarked_runs"] == 0
         # the two event sets match each other's capacity without outgrowing it (was: x1.25 per flush)
         assert caps[-1] == caps[ticks // 2], caps
         if event_capacity:
@@ -1393,6 +1396,21 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
         eb, lb = B.tick()
         np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
         np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
+        # a host batch between _stage and _commit stays out of the reservation (queued as host ops
+        # ahead of the committed batch: commit order is call order)
+        sl, nx, nz = wl.tick(20)
+        s2, x2, z2 = wl.tick(21)
+        vs, vx, vz = A.stage_moves(sl.size)
+        vs[:], vx[:], vz[:] = sl, nx, nz
+        A.moved_batch(s2, x2, z2)
+        np.testing.assert_array_equal(vs, sl)  # the reserved words were not overwritten
+        A.commit_moves(sl.size)
+        B.moved_batch(s2, x2, z2)
+        B.moved_batch(sl, nx, nz)
+        ea, la = A.tick()
+        eb, lb = B.tick()
+        np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb))
+        np.testing.assert_array_equal(pair_keys(la), pair_keys(lb))
         # pipelined: batch t+1 staged while flush t runs, tick_end_begin returns t's events
         host = [wl.tick(4 + t) for t in range(5)]
         vs, vx, vz = A.stage_moves(host[0][0].size)
@@ -1481,3 +1499,62 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             A.tick()
         assert ei.value.code == -3  # GWAOI_ESTATE, the flush committed
         np.testing.assert_array_equal(A.snapshot()["x"][A.snapshot()["slot"] == 6], [np.float32(2.0)])
+
+
+@pytest.mark.parametrize("cfg,n,seed", [("cfg3", 30000, 5), ("cfg2", 20000, 9)])
+def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, cfg, n, seed):
+    """The sparse flush (a few Moved calls: events against the frame in place, the frame patched
+    in place, a cell changer shifted into its new cell) gives exactly the events of the full
+    flush and of the sequential oracle, flush after flush; the full flushes in between start
+    from the patched frame.  Batches of 1-300 moves: host calls (< 64) and staged host batches
+    (64..256), repeated slots, steps across cells and rows, and teleports far enough that the
+    shifts are declined (the full flush runs instead)."""
+    wl = make_workload(cfg, n=n, seed=seed)
+    slots, x0, z0, _ = wl.initial()
+    m = oracle_mod.XZList(wl.D, n)
+    rng = np.random.default_rng(seed)
+    px, pz = x0.astype(np.float32).copy(), z0.astype(np.float32).copy()
+    lo, hi = float(min(px.min(), pz.min())), float(max(px.max(), pz.max()))
+    with World(n) as A, World(n, sparse=False) as B:
+        for w in (A, B):
+            s = w.space_create(wl.D)
+            w.enter_batch(s, slots, x0, z0)
+            w.tick()
+        for i in range(n):
+            m.enter(int(slots[i]), x0[i], z0[i])
+        m.take_events()
+        sizes = [1, 1, 2, 5, 17, 63, 64, 100, 256, 257, 1, 3]
+        for it in range(48):
+            k = sizes[it % len(sizes)]
+            if it % 16 == 15:
+                k = n  # a full flush of every entity, from the patched frame
+            sl = rng.choice(n, k, replace=k >= n or rng.random() < 0.5).astype(np.uint32)  # repeats
+            u = rng.random(k)
+            step = np.where(u < 0.75, rng.uniform(-1, 1, k), np.where(u < 0.97, rng.uniform(-45, 45, k), 0.0))
+            nx = (px[sl] + step.astype(np.float32)).astype(np.float32)
+            nz = (pz[sl] + rng.uniform(-1, 1, k).astype(np.float32) * np.where(u < 0.9, 1.0, 60.0)).astype(np.float32)
+            tele = u >= 0.97
+            nx[tele] = rng.uniform(lo, hi, int(tele.sum())).astype(np.float32)
+            nz[tele] = rng.uniform(lo, hi, int(tele.sum())).astype(np.float32)
+            if k < 64:
+                for s_, x_, z_ in zip(sl.tolist(), nx.tolist(), nz.tolist()):
+                    A.moved(s_, x_, z_)
+            else:
+                A.moved_batch(sl, nx, nz)
+            B.moved_batch(sl, nx, nz)
+            m.moved_batch(sl, nx, nz)
+            for s_, x_, z_ in zip(sl.tolist(), nx.tolist(), nz.tolist()):  # the last op of a slot wins
+                px[s_], pz[s_] = x_, z_
+            ea, la = (pair_keys(e) for e in A.tick())
+            eb, lb = (pair_keys(e) for e in B.tick())
+            oe, ol = oracle_mod.net_events(*m.take_events())
+            np.testing.assert_array_equal(ea, oe, err_msg=f"flush {it} ({k} moves): sparse-world enters")
+            np.testing.assert_array_equal(la, ol, err_msg=f"flush {it} ({k} moves): sparse-world leaves")
+            np.testing.assert_array_equal(eb, oe, err_msg=f"flush {it}: full-world enters")
+            np.testing.assert_array_equal(lb, ol, err_msg=f"flush {it}: full-world leaves")
+            if it % 6 == 5:  # the patched frame answers cell queries exactly
+                for i in rng.choice(n, 24, replace=False).tolist():
+                    np.testing.assert_array_equal(A.neighbors(i), m.neighbors(i).astype(np.uint32))
+        d = A.debug_counters()
+        assert d["sparse_flushes"] >= 20, d
+        assert B.debug_counters()["sparse_flushes"] == 0

@@ -93,6 +93,38 @@ def test_strip_route_rejects_foreign_entities():
     b.close()
 
 
+@pytest.mark.parametrize("bad", ["enter_live", "unknown_kind"])
+def test_async_tick_with_bad_record_breaks_strip(bad):
+    """gwaoi_strips_tick_async does not validate before the world consumes its records: a bad
+    received record fails the call that completes the tick, and the strip refuses every later
+    call (gwaoi_strips.h).  An ENTER of a slot the strip holds also poisons its world; a record
+    of unknown kind reaches the world as a no-op (the move batch never reads a stale word)."""
+    import torch
+    from goworld_amd.strips import TELE_WORDS
+    sh = StripShard(64, D, np.array([], np.float32), 0, device=0)
+    local_tick([sh], [as_words(make_ops([1, 2], [0.0, 10.0], [0.0, 0.0], [1, 2], kind=HALO_ENTER),
+                               HALO_WORDS).to("cuda:0")])
+    assert sorted(map(tuple, sh.events()[0].tolist())) == [(1, 2), (2, 1)]
+    if bad == "enter_live":
+        rec = make_ops([1], [5.0], [0.0], [3], kind=HALO_ENTER)
+        kinds = (1, 0, np.array([5.0, 0.0, 5.0, 0.0], np.float32))
+    else:
+        rec = make_ops([1], [5.0], [0.0], [3], kind=7)
+        kinds = (0, 0, None)
+    local = as_words(rec, HALO_WORDS).to("cuda:0")
+    empty = torch.empty((0, HALO_WORDS), dtype=torch.int32, device="cuda:0")
+    tele = torch.empty((0, TELE_WORDS), dtype=torch.int32, device="cuda:0")
+    sh.finish(local, empty, tele, kinds=kinds)
+    with pytest.raises(GwaoiError):
+        sh.wait()
+    with pytest.raises(GwaoiError) as ei:  # broken from then on
+        sh.wait()
+    assert ei.value.code == -3 and "unusable" in str(ei.value)
+    with pytest.raises(GwaoiError):
+        sh.route(as_words(make_ops([2], [11.0], [0.0], [4]), HALO_WORDS).to("cuda:0"))
+    sh.close()
+
+
 def test_explicit_seq_world_matches_implicit():
     """gwaoi_moved_batch_device_seq with the implicit order's seqs == gwaoi_moved_batch_device."""
     import torch

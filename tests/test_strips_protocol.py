@@ -16,7 +16,8 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from goworld_amd.strips import as_words, exchange, exchange_local, local_slice, HALO_WORDS, owner_of
+from goworld_amd.strips import (HALO_WORDS, as_words, count_row, exchange, exchange_local, kinds_of, local_slice,
+                                matrix_counts, matrix_kinds, merge_kinds, owner_of, row_words)
 from strip_model import ModelShard
 from strip_scenario import D, Scenario, split_by_owner
 
@@ -80,9 +81,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, seed, ticks, q):
+def _worker(rank, ws, port, seed, ticks, q, rows=False):
+    import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from oracle import oracle
     sc = Scenario(n0=3000, n_strips=ws, seed=seed)
@@ -91,7 +94,14 @@ def _worker(rank, ws, port, seed, ticks, q):
     for _ in range(ticks):
         ops = split_by_owner(*sc.tick(), sc.edges)[rank]
         send, counts, tele = sh.route(as_words(ops, HALO_WORDS))
-        recv, tele_all, kinds = exchange(dist, send, counts, tele, kinds=sh.kinds)
+        M = None
+        if rows:  # the device count rows (k_route_row's layout), gathered as StripShard.route(ops, dist) does
+            row = torch.from_numpy(count_row(counts, int(tele.shape[0]), sh.kinds).view(np.int32))
+            W = row.numel()
+            mat = torch.zeros(ws * W, dtype=torch.int32)
+            dist.all_gather([mat[r * W:(r + 1) * W] for r in range(ws)], row)
+            M = mat.numpy().view(np.uint32).reshape(ws, W)
+        recv, tele_all, kinds = exchange(dist, send, counts, tele, kinds=sh.kinds, matrix=M)
         sh.finish(local_slice(send, counts, rank), recv, tele_all, kinds=kinds)
         res.append((sh.last[0].tolist(), sh.last[1].tolist()))
     q.put((rank, res))
@@ -99,17 +109,18 @@ def _worker(rank, ws, port, seed, ticks, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 3])
-def test_gloo_strip_exchange(oracle_mod, ws):
+@pytest.mark.parametrize("ws,rows", [(2, False), (3, False), (2, True), (3, True), (8, True)])
+def test_gloo_strip_exchange(oracle_mod, ws, rows):
     """ws ranks over gloo: counts (with the ENTER / LEAVE statistics the receivers
-    queue their world batches with) all-gathered on the host, records point to
+    queue their world batches with) all-gathered -- as host rows, or (rows) as the
+    device count rows the RCCL path gathers inside the route -- records point to
     point (3 ranks: the middle strip talks to both neighbours, the outer ones
-    reach each other only through teleports)."""
+    reach each other only through teleports; 8 ranks: config 5's strip count)."""
     seed, ticks = 5, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, seed, ticks, q)) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, seed, ticks, q, rows)) for r in range(ws)]
     for p in procs:
         p.start()
     parts = dict(q.get(timeout=300) for _ in range(ws))
@@ -120,3 +131,31 @@ def test_gloo_strip_exchange(oracle_mod, ws):
            for t in range(ticks)]
     ref = reference_ticks(oracle_mod, Scenario(n0=3000, n_strips=ws, seed=seed), ticks)
     assert_same(got, ref)
+
+
+def test_count_row_round_trip():
+    """The device count row (k_route_row's layout, written by the host model here) parses back to
+    the same counts and the same receiver statistics as the host row (merge_kinds)."""
+    rng = np.random.default_rng(3)
+    S = 5
+    sends = []
+    for src in range(S):
+        counts = rng.integers(0, 40, S)
+        n = int(counts.sum())
+        rec = np.zeros(n, dtype=np.dtype([("slot", "<u4"), ("x", "<f4"), ("z", "<f4"), ("kind", "<u4"),
+                                          ("seq", "<u8")]))
+        rec["kind"] = rng.integers(0, 3, n)
+        rec["x"] = rng.normal(0, 1e4, n).astype(np.float32)
+        rec["z"] = rng.normal(0, 1e4, n).astype(np.float32)
+        sends.append((rec, counts, int(rng.integers(0, 9))))
+    M = np.stack([count_row(c, t, kinds_of(r, c)) for r, c, t in sends])
+    assert M.shape == (S, row_words(S))
+    assert np.array_equal(matrix_counts(M, S)[:, :S], np.stack([c for _, c, _ in sends]))
+    assert np.array_equal(matrix_counts(M, S)[:, S], [t for _, _, t in sends])
+    for rank in range(S):
+        want = merge_kinds([tuple(k[rank] for k in kinds_of(r, c)) for r, c, _ in sends])
+        got = matrix_kinds(M, S, rank)
+        assert got[0] == want[0] and got[1] == want[1]
+        assert (got[2] is None) == (want[2] is None)
+        if want[2] is not None:
+            assert np.array_equal(got[2], want[2])

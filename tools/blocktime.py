@@ -18,7 +18,8 @@ def main():
     wl = make_workload("cfg3")
     n = wl.n
     lib = ctypes.CDLL(os.environ["GWAOI_LIB"])
-    nb = (n + 255) // 256
+    unit = int(os.environ.get("BT_UNIT", "64"))  # entries per k_combined unit (64: one wave's, GWAOI_CQ; 256: a block's)
+    nb = (n + unit - 1) // unit
     buf = np.zeros(3 * 65536, np.uint64)
     with World(n, device=0) as w:
         s = w.space_create(wl.D)
@@ -48,8 +49,8 @@ def main():
     act = [int(((t0 * us <= g) & (t1 * us > g)).sum()) for g in grid]
     print("blocks running, 40 steps over the span:", act)
     starts = np.sort(t0 * us)
-    print("start time of block k (us): k=0 %.1f, 1792 %.1f, 3584 %.1f, last %.1f" %
-          (starts[0], starts[min(1792, nb - 1)], starts[min(3584, nb - 1)], starts[-1]))
+    print("start time of block k (us): k=0 %.1f, k=nb/2 %.1f, k=3nb/4 %.1f, last %.1f" %
+          (starts[0], starts[nb // 2], starts[3 * nb // 4], starts[-1]))
     xcc = (hw >> np.uint64(32)) & np.uint64(0xFF)
     for x in range(8):
         m = xcc == x
