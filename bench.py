@@ -455,7 +455,7 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
       batch is in host memory when the tick starts, as the bench's device leg has it in HBM), and
       gwaoi_moved_batch_pinned queues one H2D of it on a copy stream; the moves are checked on the device.
       Serial: batch + gwaoi_tick.  Pipelined: the batch of t+1 is queued while flush t runs (its H2D beside
-      the copy-out of t-1's events), gwaoi_pairs_host takes t-1's events, then gwaoi_tick_end_begin_pairs_async
+      the copy-out of t-1's events), gwaoi_pairs_host takes t-1's events, then gwaoi_tick_finish(NEXT|PAIRS)
       queues flush t+1 before t's summary is read and starts t's copy-out (one event per mirrored pair)
       without waiting for it.  (Taking t's events right after that call instead: 0.364 vs 0.341 ms per
       tick, p99 latency 0.86 vs 0.87 ms, r04n / r04m.)
@@ -577,11 +577,11 @@ def host_io_leg(w, host_batches, hio, dist, red_dev):
                                 "pipelined_p99_tick_ms": pct(cq_lat[1:], 99), "steps": len(g_lat)},
             "note": "pinned: each tick's moves in a caller-owned pinned buffer (gwaoi_pinned_alloc, filled before "
                     "timing as a game server fills it while packets arrive), one H2D per tick, checked on the "
-                    "device; pipelined = batch t+1 queued while flush t runs, then gwaoi_tick_end_begin_pairs_async "
+                    "device; pipelined = batch t+1 queued while flush t runs, then gwaoi_tick_finish(NEXT|PAIRS) "
                     "(flush t+1 queued before t's summary, t's copy-out started: one event per mirrored pair "
                     "(a,b)/(b,a), from which the callbacks of both entities follow), then t's pairs taken "
                     "(gwaoi_pairs_host) while flush t+1 runs; directed_events_out = the same ticks copying every "
-                    "directed event (gwaoi_tick_end_begin_async + gwaoi_events_host).  Tick latency = batch call "
+                    "directed event (gwaoi_tick_finish(NEXT|HOST) + gwaoi_events_host).  Tick latency = batch call "
                     "-> events in pinned host memory; pipelined percentiles over the ticks after the first "
                     "fill_ticks (every tick's latency in ticks_ms; ms_per_step counts them all).  PCIe here carries one direction at a time "
                     "(tools/pcie_probe.py), so a pipelined tick costs H2D + D2H.  stage_commit = the caller "
@@ -1091,16 +1091,16 @@ def main():
                          "while the flush of tick t runs, gwaoi_tick_begin/_end, as a game loop receives moves)")
     ap.add_argument("--cfg4-spaces", type=int, default=8192)
     ap.add_argument("--no-speculative", action="store_true",
-                    help="overlap mode without gwaoi_tick_end_begin_device: each flush is queued after the commit "
+                    help="overlap mode without gwaoi_tick_finish(NEXT): each flush is queued after the commit "
                          "of the previous one (A/B of the speculative launch)")
     ap.add_argument("--wire-steps", type=int, default=5,
                     help="timed calls per gate/dispatcher regroup in the wire leg (0 = off)")
     ap.add_argument("--wire-records", type=int, default=1_000_000, help="32-B client records per wire regroup call")
     ap.add_argument("--wire-out-records", type=int, default=4_000_000,
                     help="48-B game records per gate_to_clients call (one gate's share of a cfg3 collect)")
-    ap.add_argument("--no-batch-ready", action="store_true",
-                    help="A/B: the next batch's claims stored by the next flush's prologue, not beside the flush "
-                         "in flight (GWAOI_F_BATCH_READY off)")
+    ap.add_argument("--batch-ready", action="store_true",
+                    help="A/B: the next batch's claims stored beside the flush in flight (GWAOI_F_BATCH_READY), "
+                         "not by the next flush's prologue; slower at config 3 (DESIGN.md sec. 3 step 1)")
     ap.add_argument("--small-flush-reps", type=int, default=20,
                     help="cfg3: timed flushes per size of the small-flush leg (1/64/4096/65536 moves; 0 = off)")
     ap.add_argument("--strip-counts", default="device", choices=["device", "host"],
@@ -1200,7 +1200,7 @@ def main():
 
     # the move batches are in HBM before the timed region: complete when passed (GWAOI_F_BATCH_READY)
     w = World(n, max_spaces=wl.n_spaces, device=device, cells_per_dist=args.cells_per_dist,
-              batch_ready=not args.no_batch_ready)
+              batch_ready=args.batch_ready)
     spaces = [w.space_create(wl.D) for _ in range(wl.n_spaces)]
     wl0 = wl_factory()  # initial positions (wl has advanced through the batches)
     slots, x0, z0, sp = wl0.initial()
@@ -1262,7 +1262,7 @@ def main():
         a = time.perf_counter()
         if spec:
             # flush t is in flight; tick t+1's batch is registered meanwhile, then one call finishes t and
-            # queues t+1 on the GPU before t's summary is waited for (gwaoi_tick_end_begin_device)
+            # queues t+1 on the GPU before t's summary is waited for (gwaoi_tick_finish(NEXT))
             if t + 1 < timed_end:
                 ps, px, pz = row_ptrs[t + 1]
                 w.moved_batch_device(ps, px, pz, moves_per_tick[t + 1])
@@ -1386,7 +1386,7 @@ def main():
             "events_per_tick": events / max(args.steps, 1),
             "initial_enter_events": ne0,
             "setup_s": round(setup_s, 2),
-            "tick_loop": ("speculative: gwaoi_tick_end_begin_device queues flush t+1 before flush t's summary "
+            "tick_loop": ("speculative: gwaoi_tick_finish(NEXT) queues flush t+1 before flush t's summary "
                           f"({spec_launches} of {args.steps} timed flushes)" if spec else
                           "overlap: batch t+1 registered while flush t runs" if overlap else "serial"),
             "roofline": roofline,

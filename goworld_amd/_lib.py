@@ -36,12 +36,15 @@ EXPORTS = [
     "gwaoi_events_device", "gwaoi_neighbors", "gwaoi_world_info", "gwaoi_stage_times",
     "gwaoi_reset_stage_times", "gwaoi_set_stage_timing", "gwaoi_sync", "gwaoi_stream", "gwaoi_stream_after", "gwaoi_stream_before", "gwaoi_strerror", "gwaoi_last_error",
     "gwaoi_abi_version", "gwaoi_enter_seq", "gwaoi_moved_seq", "gwaoi_moved_batch_device_seq",
-    "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_end",
-    "gwaoi_tick_end_device", "gwaoi_events_csr", "gwaoi_events_csr_device", "gwaoi_tick_end_begin_device",
-    "gwaoi_enter_batch_device", "gwaoi_leave_batch_device", "gwaoi_tick_end_begin", "gwaoi_moved_batch_stage",
+    "gwaoi_snapshot", "gwaoi_restore", "gwaoi_debug_counters", "gwaoi_tick_begin", "gwaoi_tick_finish",
+    "gwaoi_events_csr", "gwaoi_events_csr_device",
+    "gwaoi_enter_batch_device", "gwaoi_leave_batch_device", "gwaoi_moved_batch_stage",
     "gwaoi_moved_batch_commit", "gwaoi_moved_batch_pinned", "gwaoi_pinned_alloc", "gwaoi_pinned_free",
-    "gwaoi_tick_end_begin_async", "gwaoi_events_host", "gwaoi_tick_end_begin_pairs_async", "gwaoi_pairs_host",
+    "gwaoi_events_host", "gwaoi_pairs_host",
 ]
+
+# gwaoi_tick_finish modes
+GWAOI_END_NEXT, GWAOI_END_HOST, GWAOI_END_PAIRS = 1, 2, 4
 
 # every function include/gwaoi_strips.h declares
 STRIP_EXPORTS = [
@@ -109,7 +112,7 @@ class Debug(C.Structure):
                 ("special_global", C.c_uint64), ("event_regrows", C.c_uint64), ("speculative_launches", C.c_uint64),
                 ("cell_size_switches", C.c_uint64), ("cells_per_dist", C.c_uint32), ("pad", C.c_uint32),
                 ("incremental_sorts", C.c_uint64), ("sparse_flushes", C.c_uint64), ("sparse_declined", C.c_uint64),
-                ("premarked_runs", C.c_uint64)]
+                ("premarked_runs", C.c_uint64), ("sparse_unfused", C.c_uint64)]
 
 
 class StageTime(C.Structure):
@@ -157,13 +160,8 @@ def load():
         "gwaoi_tick_begin": ([vp], C.c_int),
         "gwaoi_events_csr": ([vp, P(vp), P(vp), P(u64)], C.c_int),
         "gwaoi_events_csr_device": ([vp, P(vp), P(vp), P(u64)], C.c_int),
-        "gwaoi_tick_end": ([vp, P(Events)], C.c_int),
-        "gwaoi_tick_end_device": ([vp, P(u64), P(u64)], C.c_int),
-        "gwaoi_tick_end_begin_device": ([vp, P(u64), P(u64)], C.c_int),
-        "gwaoi_tick_end_begin": ([vp, P(Events)], C.c_int),
-        "gwaoi_tick_end_begin_async": ([vp, P(u64), P(u64)], C.c_int),
+        "gwaoi_tick_finish": ([vp, C.c_uint32, P(u64), P(u64)], C.c_int),
         "gwaoi_events_host": ([vp, P(Events)], C.c_int),
-        "gwaoi_tick_end_begin_pairs_async": ([vp, P(u64), P(u64)], C.c_int),
         "gwaoi_pairs_host": ([vp, P(Events)], C.c_int),
         "gwaoi_moved_batch_stage": ([vp, sz, P(vp), P(vp), P(vp)], C.c_int),
         "gwaoi_moved_batch_commit": ([vp, sz], C.c_int),
@@ -391,62 +389,69 @@ class World:
         are queued for the next flush."""
         self._check(self._L.gwaoi_tick_begin(self._w))
 
-    def tick_end(self, copy: bool = True):
-        """Finish the flush started by tick_begin: (enter_pairs, leave_pairs) as tick()."""
-        ev = Events()
-        return self._events(self._L.gwaoi_tick_end(self._w, C.byref(ev)), ev, copy)
-
-    def tick_end_device(self):
+    def finish(self, mode: int = 0):
+        """gwaoi_tick_finish(mode): commit the flush in flight; mode is an OR of GWAOI_END_NEXT
+        (begin the next flush), GWAOI_END_HOST (events to host memory: events_host) and
+        GWAOI_END_PAIRS (one event per mirrored pair: pairs_host).  Returns the finished flush's
+        (n_enter, n_leave); on a committed flush with a device-reported problem the GwaoiError
+        carries them as ``.counts``."""
         ne, nl = C.c_uint64(), C.c_uint64()
-        self._check(self._L.gwaoi_tick_end_device(self._w, C.byref(ne), C.byref(nl)))
+        rc = self._L.gwaoi_tick_finish(self._w, mode, C.byref(ne), C.byref(nl))
+        if rc != 0:
+            try:
+                self._check(rc)
+            except GwaoiError as e:
+                e.counts = (ne.value, nl.value)
+                raise
         return ne.value, nl.value
 
+    def _finish_events(self, mode, copy):
+        # the flush's host events with its status: a committed flush with a device-reported
+        # problem raises with them as ``.events`` (events_host describes the copy this call made,
+        # empty when the flush did not commit)
+        err = None
+        try:
+            self.finish(mode)
+        except GwaoiError as e:
+            err = e
+        ev = Events()
+        ok = self._L.gwaoi_events_host(self._w, C.byref(ev)) == 0
+        ent, lev = self._events(0, ev, copy) if ok else (None, None)
+        if err is not None:
+            err.events = (ent, lev) if ok else None
+            raise err
+        return ent, lev
+
+    def tick_end(self, copy: bool = True):
+        """Finish the flush started by tick_begin: (enter_pairs, leave_pairs) as tick()
+        (gwaoi_tick_finish(GWAOI_END_HOST))."""
+        return self._finish_events(GWAOI_END_HOST, copy)
+
+    def tick_end_device(self):
+        """gwaoi_tick_finish(0): events stay in HBM."""
+        return self.finish(0)
+
     def tick_end_begin_device(self):
-        """gwaoi_tick_end_begin_device: finish the flush in flight and begin the next one
+        """gwaoi_tick_finish(GWAOI_END_NEXT): finish the flush in flight and begin the next one
         (queued on the GPU before this one's commit when only device Moved batches were
         queued).  Returns the finished flush's (n_enter, n_leave); its events stay
         readable through events_device() while the next flush runs."""
-        ne, nl = C.c_uint64(), C.c_uint64()
-        rc = self._L.gwaoi_tick_end_begin_device(self._w, C.byref(ne), C.byref(nl))
-        if rc != 0:
-            try:
-                self._check(rc)
-            except GwaoiError as e:
-                e.counts = (ne.value, nl.value)
-                raise
-        return ne.value, nl.value
+        return self.finish(GWAOI_END_NEXT)
 
     def tick_end_begin(self, copy: bool = True):
-        """gwaoi_tick_end_begin: finish the flush in flight (its events copied to host memory
-        beside the next flush) and begin the next one."""
-        ev = Events()
-        return self._events(self._L.gwaoi_tick_end_begin(self._w, C.byref(ev)), ev, copy)
+        """gwaoi_tick_finish(GWAOI_END_NEXT | GWAOI_END_HOST) + events_host: finish the flush in
+        flight (its events copied to host memory beside the next flush) and begin the next one."""
+        return self._finish_events(GWAOI_END_NEXT | GWAOI_END_HOST, copy)
 
     def tick_end_begin_async(self):
-        """gwaoi_tick_end_begin_async: as tick_end_begin, but the events' copy to host memory
-        is left running; returns (n_enter, n_leave).  events_host() waits for it."""
-        ne, nl = C.c_uint64(), C.c_uint64()
-        rc = self._L.gwaoi_tick_end_begin_async(self._w, C.byref(ne), C.byref(nl))
-        if rc != 0:
-            try:
-                self._check(rc)
-            except GwaoiError as e:
-                e.counts = (ne.value, nl.value)
-                raise
-        return ne.value, nl.value
+        """gwaoi_tick_finish(GWAOI_END_NEXT | GWAOI_END_HOST): the events' copy to host memory is
+        left running; returns (n_enter, n_leave).  events_host() waits for it."""
+        return self.finish(GWAOI_END_NEXT | GWAOI_END_HOST)
 
     def tick_end_begin_pairs_async(self):
-        """gwaoi_tick_end_begin_pairs_async: as tick_end_begin_async, one event per mirrored pair
-        copied out; returns the directed (n_enter, n_leave).  pairs_host() waits for them."""
-        ne, nl = C.c_uint64(), C.c_uint64()
-        rc = self._L.gwaoi_tick_end_begin_pairs_async(self._w, C.byref(ne), C.byref(nl))
-        if rc != 0:
-            try:
-                self._check(rc)
-            except GwaoiError as e:
-                e.counts = (ne.value, nl.value)
-                raise
-        return ne.value, nl.value
+        """gwaoi_tick_finish(GWAOI_END_NEXT | GWAOI_END_PAIRS): one event per mirrored pair copied
+        out; returns the directed (n_enter, n_leave).  pairs_host() waits for them."""
+        return self.finish(GWAOI_END_NEXT | GWAOI_END_PAIRS)
 
     def pairs_host(self, copy: bool = True):
         """gwaoi_pairs_host: (enter pairs, leave pairs) as (n,2) arrays; (a,b) stands for (a,b) and (b,a)."""

@@ -335,6 +335,14 @@ void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, 
                    SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
                    const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t tick, uint32_t *cnt,
                    uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st);
+// The same flush in one launch for k <= sparse_fused_max() ops (no claims stored): scr holds
+// 2 * scr_cap words per op, done one zeroed word (re-armed by the kernel).  TickOut.pad 3: an op
+// outgrew its scratch row (nothing written; run launch_sparse instead).
+uint32_t sparse_fused_max();
+void launch_sparse_fused(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
+                         SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                         const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t *cnt, uint32_t *scr,
+                         uint32_t scr_cap, uint32_t *done, uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st);
 
 // ---- world accessors for the entity-sync layer (gwaoi_sync.cpp) -------------
 struct SyncState;
@@ -344,7 +352,7 @@ struct WorldView {
     hipStream_t st;
     uint32_t max_slots;
     size_t pending_ops;     // calls queued since the last flush (or a flush in flight)
-    bool in_flight;         // gwaoi_tick_begin without its gwaoi_tick_end yet
+    bool in_flight;         // gwaoi_tick_begin without its gwaoi_tick_finish yet
     const uint32_t *events; // last flush's events (device): [enters | leaves] as (a,b) pairs
     uint64_t n_enter, n_leave;
 };

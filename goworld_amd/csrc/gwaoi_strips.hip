@@ -709,7 +709,7 @@ int complete(gwaoi_strips *s, bool synced) {
         if (int rc = wait(s)) return rc;
     s->pending = false;
     uint64_t wne = 0, wnl = 0;
-    if (int rc = gwaoi_tick_end_device(s->w, &wne, &wnl)) {
+    if (int rc = gwaoi_tick_finish(s->w, 0u, &wne, &wnl)) {
         s->last_error = std::string("world tick: ") + gwaoi_last_error(s->w);
         return rc;
     }

@@ -95,6 +95,10 @@ class StagePool {
     // f(0) .. f(T-1), f(0) on the calling thread.  Falls back to running on the
     // caller when threads cannot be started.
     void run(unsigned T, const std::function<void(unsigned)> &f) {
+        if (T <= 1) {  // inline: no wake-up of the workers
+            if (T) f(0);
+            return;
+        }
         while (th_.size() + 1 < T) {
             try {
                 const unsigned id = (unsigned)th_.size() + 1;
@@ -163,7 +167,7 @@ struct DeferredBox {  // Enter/Moved positions of a deferred staged batch, per s
 // The buffers one flush writes that the flush after it must leave alone while the
 // first may still be re-run (event buffer regrow) or read by the caller: two
 // sets, alternated per launch, so that flush t+1 can be launched before flush
-// t's summary has reached the host (gwaoi_tick_end_begin_device).
+// t's summary has reached the host (gwaoi_tick_finish with GWAOI_END_NEXT).
 struct FlushSet {
     gw::Rec16 *srec = nullptr;  // S': previous frame + this flush's ops, previous order
     gw::SlotSp *sss = nullptr;
@@ -284,18 +288,30 @@ struct gwaoi_world {
     uint32_t *h_stage[2] = {nullptr, nullptr}, *d_stage[2] = {nullptr, nullptr};
     size_t stage_cap[2] = {0, 0}, stage_used[2] = {0, 0};
     int stage_cur = 0;
-    // zero-copy batch (gwaoi_moved_batch_stage / _commit): the caller fills [slots | x | z | space]
-    // sparse flush (gwaoi_sparse.hip): per-op counts and offsets; off with GWAOI_F_NO_SPARSE
+    // sparse flush (gwaoi_sparse.hip): per-op counts and offsets, and the host ops' upload buffer
+    // (sp_ops_layout: pinned -> device in one copy); off with GWAOI_F_NO_SPARSE
     uint32_t *sp_cnt = nullptr;
+    uint8_t *h_sp_ops = nullptr, *d_sp_ops = nullptr;
+    // the fused form (one launch; GWAOI_SPARSE_FUSED=0: the kernel sequence): per-op scratch rows of
+    // sp_scr_cap events per kind (GWAOI_SPARSE_SCR, tests), and its arrival counter
+    uint32_t *sp_scr = nullptr, *sp_done = nullptr;
+    uint32_t sp_scr_cap = 512;
+    size_t stage_min = 64;  // host move batches of this many moves or more are staged (GWAOI_STAGE_MIN: A/B)
+    bool sparse_fused = true;
     bool sparse_on = true;
+    // zero-copy batch (gwaoi_moved_batch_stage / _commit): the caller fills [slots | x | z | space]
     size_t resv_n = 0;        // moves reserved (0: no reservation)
     uint32_t *resv_h = nullptr, *resv_d = nullptr;
     int resv_half = 0;
-    // event copies to the host beside the next flush (gwaoi_tick_end_begin)
+    // event copies to the host beside the next flush (gwaoi_tick_finish, GWAOI_END_HOST / _PAIRS)
     hipStream_t out_st = nullptr;
     hipEvent_t out_ev = nullptr;
-    bool out_pending = false;  // a copy-out of events queued by gwaoi_tick_end_begin_async, not yet waited for
-    bool out_pairs = false;    // ... of one event per mirrored pair (gwaoi_tick_end_begin_pairs_async)
+    bool out_pending = false;  // a copy-out of events queued by gwaoi_tick_finish, not yet waited for
+    bool out_pairs = false;    // ... of one event per mirrored pair (GWAOI_END_PAIRS)
+    // the counts of the flush whose events h_events holds (a later commit without a copy-out, e.g.
+    // gwaoi_tick_finish without a host mode, changes last_n_* but not the host copy)
+    uint64_t out_n_enter = 0, out_n_leave = 0;
+    uint32_t *d_h_events = nullptr;  // h_events as the device sees it (k_pairs_out writes through it)
     // GWAOI_F_BATCH_READY: the first device Moved batch queued while a flush is in flight gets its
     // claims on mark_st once that flush's apply is done (apply_ev), beside the rest of the flush
     bool batch_ready = false;
@@ -303,8 +319,9 @@ struct gwaoi_world {
     hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
     bool apply_ev_valid = false;
     bool premark_late = false;  // the claims beside the pair passes rather than after the apply
-    // the special pass beside the combined pass (GWAOI_SPECIAL_SIDE=0: in line, A/B)
-    bool special_side = true;
+    // the special pass beside the combined pass on a side stream (GWAOI_SPECIAL_SIDE=1, A/B):
+    // measured slower at config 3 (0.2375 against 0.2202 ms per tick, profiles/r05_ab_side_premark.txt)
+    bool special_side = false;
     hipStream_t side_st = nullptr;
     hipEvent_t side_fork = nullptr, side_join = nullptr;
     struct {
@@ -328,7 +345,7 @@ struct gwaoi_world {
     uint32_t tick_id = 0;
     uint64_t ticks = 0;
     uint32_t n_alive = 0;
-    // ---- flush in flight (gwaoi_tick_begin -> gwaoi_tick_end).  The op queue (runs, host op
+    // ---- flush in flight (gwaoi_tick_begin -> gwaoi_tick_finish).  The op queue (runs, host op
     // arrays, new_slots, touched) stays frozen until the commit: calls made meanwhile are
     // deferred, then queued for the next flush.
     bool in_flight = false;
@@ -501,7 +518,7 @@ int ensure_tile_entries(gwaoi_world *w, size_t entries) {
 }
 
 int wait_done(gwaoi_world *w, hipEvent_t ev);
-// Waits for the copy-out gwaoi_tick_end_begin_async queued (before h_events is rewritten or freed).
+// Waits for the copy-out gwaoi_tick_finish queued (before h_events is rewritten or freed).
 int finish_out(gwaoi_world *w) {
     if (!w->out_pending) return GWAOI_OK;
     w->out_pending = false;
@@ -513,9 +530,11 @@ int ensure_host_events(gwaoi_world *w, uint64_t pairs) {
     if (pairs <= w->h_ev_cap) return GWAOI_OK;
     uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, 1024);
     if (w->h_events) (void)hipHostFree(w->h_events);
-    w->h_events = nullptr;
+    w->h_events = w->d_h_events = nullptr;
     w->h_ev_cap = 0;
-    HIP_TRY(hipHostMalloc((void **)&w->h_events, 2 * cap * sizeof(uint32_t), hipHostMallocMapped));  // (k_pairs_out writes it)
+    // mapped and coherent: k_pairs_out writes it from the device, through its device address
+    HIP_TRY(hipHostMalloc((void **)&w->h_events, 2 * cap * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostGetDevicePointer((void **)&w->d_h_events, w->h_events, 0));
     w->h_ev_cap = cap;
     return GWAOI_OK;
 }
@@ -872,7 +891,7 @@ int tick_launch(gwaoi_world *w) {
     const uint32_t n_new = w->n_alive;
 
     (void)hipGetLastError();  // the launch check below must see this flush's launches only
-    // a copy-out still reading a flush set's events (gwaoi_tick_end_begin_async) ends before this
+    // a copy-out still reading a flush set's events (gwaoi_tick_finish) ends before this
     // flush writes into a set
     if (w->out_pending) HIP_TRY(hipStreamWaitEvent(st, w->out_ev, 0));
     // grid for this flush
@@ -1280,6 +1299,9 @@ int tick_finish(gwaoi_world *w, bool *committed) { return finish_flight(w, w->fl
 // Returns GWAOI_OK when it committed, 1 when it was not taken or the device declined it (nothing
 // changed: the caller runs the full flush over the same queue), or an error.
 constexpr size_t kSparseMaxOps = 256;
+// the host ops of a sparse flush in one upload: [seq u64 x 256 | slot x 256 | x x 256 | z x 256]
+constexpr size_t kSpSeq = 0, kSpSlot = 8 * kSparseMaxOps, kSpX = 12 * kSparseMaxOps, kSpZ = 16 * kSparseMaxOps;
+constexpr size_t kSpOpsBytes = 20 * kSparseMaxOps;
 int sparse_try(gwaoi_world *w) {
     if (!w->sparse_on || w->in_flight || w->n_ops == 0 || w->n_ops > kSparseMaxOps || !w->new_slots.empty() ||
         w->space_ops_queued || w->dev_app || w->dev_struct || w->dev_seq_pending || !w->deferred.empty() ||
@@ -1303,32 +1325,57 @@ int sparse_try(gwaoi_world *w) {
     const uint32_t *d_slot = run.ds;
     const float *d_x = run.dx, *d_z = run.dz;
     const unsigned long long *d_seq = nullptr;
-    if (!run.device) {
-        if ((rc = ensure_ops(w, k))) return rc;
-        HIP_TRY(hipMemcpyAsync(w->op_slot, w->h_op_slot.data(), k * 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->op_x, w->h_op_x.data(), k * 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->op_z, w->h_op_z.data(), k * 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(w->op_seq, w->h_op_seq.data(), k * 8, hipMemcpyHostToDevice, st));
-        d_slot = w->op_slot;
-        d_x = w->op_x;
-        d_z = w->op_z;
-        d_seq = w->op_seq;
+    if (!run.device) {  // one pinned upload (four pageable copies cost ~8 us each)
+        if (!w->h_sp_ops) {
+            HIP_TRY(hipHostMalloc((void **)&w->h_sp_ops, kSpOpsBytes, hipHostMallocDefault));
+            if ((rc = dalloc(w, &w->d_sp_ops, kSpOpsBytes))) return rc;
+        }
+        std::memcpy(w->h_sp_ops + kSpSeq, w->h_op_seq.data(), k * 8);
+        std::memcpy(w->h_sp_ops + kSpSlot, w->h_op_slot.data(), k * 4);
+        std::memcpy(w->h_sp_ops + kSpX, w->h_op_x.data(), k * 4);
+        std::memcpy(w->h_sp_ops + kSpZ, w->h_op_z.data(), k * 4);
+        HIP_TRY(hipMemcpyAsync(w->d_sp_ops, w->h_sp_ops, kSpZ + k * 4, hipMemcpyHostToDevice, st));
+        d_slot = reinterpret_cast<const uint32_t *>(w->d_sp_ops + kSpSlot);
+        d_x = reinterpret_cast<const float *>(w->d_sp_ops + kSpX);
+        d_z = reinterpret_cast<const float *>(w->d_sp_ops + kSpZ);
+        d_seq = reinterpret_cast<const unsigned long long *>(w->d_sp_ops + kSpSeq);
     } else if (w->copy_pending) {  // the staged batch's H2D lands first
         HIP_TRY(hipStreamWaitEvent(st, w->copy_ev, 0));
         w->copy_pending = false;
     }
     const uint32_t tick_id = ++w->tick_id;
-    HIP_TRY(hipMemsetAsync(&S.sc->err, 0, sizeof(uint32_t), st));
-    gw::launch_ops_claim(d_slot, k, 0, w->max_slots, w->sinfo, tick_id, S.sc, st);
-    gw::launch_sparse(P.rec, P.ss, P.key, P.cell_start, P.grid, w->sinfo, d_slot, d_x, d_z, d_seq, run.seq0, k,
-                      tick_id, w->sp_cnt, S.events, S.ev_cap, reinterpret_cast<gw::TickOut *>(S.d_hout), st);
-    if (hipGetLastError() != hipSuccess || hipEventRecord(S.done_ev, st) != hipSuccess) {
-        w->last_error = "sparse flush launch failed";
-        return poison(w, GWAOI_EDEVICE);  // the frame may be half patched
+    gw::TickOut *res = reinterpret_cast<gw::TickOut *>(S.d_hout);
+    auto run_sparse = [&](bool fused) -> int {
+        if (fused) {
+            gw::launch_sparse_fused(P.rec, P.ss, P.key, P.cell_start, P.grid, w->sinfo, d_slot, d_x, d_z, d_seq,
+                                    run.seq0, k, w->sp_cnt, w->sp_scr, w->sp_scr_cap, w->sp_done, S.events,
+                                    S.ev_cap, res, st);
+        } else {
+            gw::launch_ops_claim(d_slot, k, 0, w->max_slots, w->sinfo, tick_id, S.sc, st);
+            gw::launch_sparse(P.rec, P.ss, P.key, P.cell_start, P.grid, w->sinfo, d_slot, d_x, d_z, d_seq, run.seq0,
+                              k, tick_id, w->sp_cnt, S.events, S.ev_cap, res, st);
+        }
+        if (hipGetLastError() != hipSuccess || hipEventRecord(S.done_ev, st) != hipSuccess) {
+            w->last_error = "sparse flush launch failed";
+            return poison(w, GWAOI_EDEVICE);  // the frame may be half patched
+        }
+        if (wait_done(w, S.done_ev) != GWAOI_OK) {
+            w->last_error = "sparse flush did not complete: " + w->last_error;
+            return poison(w, GWAOI_EDEVICE);
+        }
+        return GWAOI_OK;
+    };
+    const bool fused = w->sparse_fused && k <= gw::sparse_fused_max();
+    if (fused && !w->sp_scr) {
+        if ((rc = dalloc(w, &w->sp_scr, (size_t)gw::sparse_fused_max() * 2 * w->sp_scr_cap)) ||
+            (rc = dalloc(w, &w->sp_done, 1)))
+            return rc;
+        HIP_TRY(hipMemsetAsync(w->sp_done, 0, sizeof(uint32_t), st));
     }
-    if (wait_done(w, S.done_ev) != GWAOI_OK) {
-        w->last_error = "sparse flush did not complete: " + w->last_error;
-        return poison(w, GWAOI_EDEVICE);
+    if ((rc = run_sparse(fused))) return rc;
+    if (fused && tick_out(S)->pad == 3u) {  // an op outgrew its scratch row: the kernel sequence
+        w->dbg.sparse_unfused++;
+        if ((rc = run_sparse(false))) return rc;
     }
     const gw::TickOut r = *tick_out(S);
     if (r.pad) {  // declined on the device before any write to the frame
@@ -1425,7 +1472,8 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_base); dfree(w->sp_cnt);
+    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_base); dfree(w->sp_cnt); dfree(w->d_sp_ops); dfree(w->sp_scr); dfree(w->sp_done);
+    if (w->h_sp_ops) (void)hipHostFree(w->h_sp_ops);
     dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
     dfree(w->csr_cnt); dfree(w->csr_off); dfree(w->csr_items); dfree(w->csr_long);
@@ -1473,6 +1521,9 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     w->sparse_on = !(cfg->flags & GWAOI_F_NO_SPARSE);
     if (const char *e = std::getenv("GWAOI_SPARSE")) w->sparse_on = w->sparse_on && e[0] != '0';
+    if (const char *e = std::getenv("GWAOI_SPARSE_FUSED")) w->sparse_fused = e[0] != '0';
+    if (const char *e = std::getenv("GWAOI_STAGE_MIN")) w->stage_min = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+    if (const char *e = std::getenv("GWAOI_SPARSE_SCR")) w->sp_scr_cap = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_FORCE_COPY")) w->force_copy = e[0] == '1';
     if (const char *e = std::getenv("GWAOI_INJECT_REGROW_FAIL")) w->inject_regrow_fail = e[0] == '1';
@@ -1517,7 +1568,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         hipEventCreateWithFlags(&w->side_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&w->side_join, hipEventDisableTiming) != hipSuccess)
         return fail(GWAOI_EDEVICE);
-    if (const char *e = std::getenv("GWAOI_SPECIAL_SIDE")) w->special_side = e[0] != '0';
+    if (const char *e = std::getenv("GWAOI_SPECIAL_SIDE")) w->special_side = e[0] == '1';
     w->batch_ready = (cfg->flags & GWAOI_F_BATCH_READY) != 0;
     if (const char *e = std::getenv("GWAOI_BATCH_READY")) w->batch_ready = w->batch_ready && e[0] != '0';  // A/B
     if (const char *e = std::getenv("GWAOI_PREMARK_LATE")) w->premark_late = e[0] == '1';
@@ -1725,7 +1776,6 @@ int moved_impl(gwaoi_world *w, uint32_t slot, float x, float z, const uint64_t *
     return GWAOI_OK;
 }
 
-constexpr size_t kStageMinBatch = 64;  // smaller host batches queue as host ops
 
 // Room for `words` more staged words.  1: no room without moving a buffer that a queued
 // batch still points into (the caller then queues the batch as host ops).
@@ -1972,9 +2022,9 @@ int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, con
     GW_LIVE(w);
     if (w->dev_seq_pending) return GWAOI_ESTATE;
     if (int rc = host_slots(w)) return rc;
-    // Batches of kStageMinBatch+ moves go through pinned staging as one device batch (single-pass
+    // Batches of stage_min+ moves go through pinned staging as one device batch (single-pass
     // move apply); without room (or if the staging allocation failed) they queue as host ops.
-    if (n >= kStageMinBatch && n <= 0xFFFFFFFFull - w->n_ops && ensure_stage(w, 4 * n) == GWAOI_OK)
+    if (n >= w->stage_min && n <= 0xFFFFFFFFull - w->n_ops && ensure_stage(w, 4 * n) == GWAOI_OK)
         return stage_moves(w, slots, x, z, n);
     for (size_t i = 0; i < n; ++i) {
         if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
@@ -2335,28 +2385,11 @@ int gwaoi_tick_begin(gwaoi_world *w) {
     });
 }
 
-int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
-    if (n_enter) *n_enter = 0;
-    if (n_leave) *n_leave = 0;
-    GW_LIVE(w);
-    if (!w->in_flight) return GWAOI_ESTATE;
-    bool committed;
-    int rc = tick_finish(w, &committed);
-    if (committed) {
-        if (n_enter) *n_enter = w->last_n_enter;
-        if (n_leave) *n_leave = w->last_n_leave;
-    }
-    return rc;
-    });
-}
-
 }  // extern "C"
 
 namespace {
 
-// gwaoi_tick_end_begin(_device): finish the flush in flight, begin the next one (speculatively,
+// gwaoi_tick_finish(GWAOI_END_NEXT): finish the flush in flight, begin the next one (speculatively,
 // before the finished one's summary is read, when the queue allows it).
 int end_begin(gwaoi_world *w, bool *committed_out) {
     bool committed = false;
@@ -2377,79 +2410,23 @@ int end_begin(gwaoi_world *w, bool *committed_out) {
     return rc != GWAOI_OK ? rc : lrc;
 }
 
-}  // namespace
-
-extern "C" {
-
-int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
-    if (n_enter) *n_enter = 0;
-    if (n_leave) *n_leave = 0;
-    GW_LIVE(w);
-    if (!w->in_flight) return GWAOI_ESTATE;
-    bool committed = false;
-    const int rc = end_begin(w, &committed);
-    if (committed) {
-        if (n_enter) *n_enter = w->last_n_enter;
-        if (n_leave) *n_leave = w->last_n_leave;
-    }
-    return rc;
-    });
-}
-
-int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out) {
-    return gw::api_guard([&]() -> int {
-    if (!w || !out) return GWAOI_EINVAL;
-    out->n_enter = out->n_leave = 0;
-    out->enter = out->leave = nullptr;
-    GW_LIVE(w);
-    if (!w->in_flight) return GWAOI_ESTATE;
-    const uint64_t regrows = w->dbg.event_regrows;
-    bool committed = false;
-    const int rc = end_begin(w, &committed);
-    if (!committed) return rc;
-    // the finished flush's events to pinned host memory on the copy-out stream, beside the next flush
-    const uint64_t tot = w->last_n_enter + w->last_n_leave;
-    if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
-    w->out_pairs = false;
-    FlushSet &S = w->fs[w->last_set];
-    if (tot) {
-        // ordered after the flush's last kernel (its event's release makes the writes visible to the
-        // copy engine); after a re-run of its pair passes, after the wait that followed the re-run
-        HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
-        HIP_TRY(hipMemcpyAsync(w->h_events, S.events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost, w->out_st));
-        HIP_TRY(hipEventRecord(w->out_ev, w->out_st));
-        if (int rw = wait_done(w, w->out_ev)) return poison(w, rw);
-    }
-    out->n_enter = w->last_n_enter;
-    out->n_leave = w->last_n_leave;
-    out->enter = w->h_events;
-    out->leave = w->h_events + 2 * w->last_n_enter;
-    return rc;
-    });
-}
-
-namespace {
-// gwaoi_tick_end_begin_async / _pairs_async: end_begin, then the copy-out queued and left running
-int end_begin_async(gwaoi_world *w, bool pairs, uint64_t *n_enter, uint64_t *n_leave) {
-    if (n_enter) *n_enter = 0;
-    if (n_leave) *n_leave = 0;
-    GW_LIVE(w);
-    if (!w->in_flight) return GWAOI_ESTATE;
-    if (int rw = finish_out(w)) return poison(w, rw);
-    const uint64_t regrows = w->dbg.event_regrows;
-    bool committed = false;
-    const int rc = end_begin(w, &committed);
-    if (!committed) return rc;
+// Queues the copy of the committed flush's events to h_events on the copy-out stream (directed
+// events, or one per mirrored pair); gwaoi_events_host / gwaoi_pairs_host wait for it.
+// regrows: the regrow count before the flush ended (a re-run of its pair passes ends later than
+// its done event).
+int copy_out(gwaoi_world *w, bool pairs, uint64_t regrows) {
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
     FlushSet &S = w->fs[w->last_set];
     w->out_pairs = pairs;
-    if (tot) {  // queued as in gwaoi_tick_end_begin; waited for by gwaoi_events_host / _pairs_host
+    w->out_n_enter = w->last_n_enter;
+    w->out_n_leave = w->last_n_leave;
+    if (tot) {
+        // ordered after the flush's last kernel (its event's release makes the writes visible to the
+        // copy engine); after a re-run of its pair passes, after the wait that followed the re-run
         HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
         if (pairs) {
-            gw::launch_pairs_out(S.events, tot / 2, w->h_events, w->out_st);
+            gw::launch_pairs_out(S.events, tot / 2, w->d_h_events, w->out_st);
             HIP_TRY(hipGetLastError());
         } else {
             HIP_TRY(hipMemcpyAsync(w->h_events, S.events, 2 * tot * sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -2458,73 +2435,21 @@ int end_begin_async(gwaoi_world *w, bool pairs, uint64_t *n_enter, uint64_t *n_l
         HIP_TRY(hipEventRecord(w->out_ev, w->out_st));
         w->out_pending = true;
     }
-    if (n_enter) *n_enter = w->last_n_enter;
-    if (n_leave) *n_leave = w->last_n_leave;
-    return rc;
-}
-}  // namespace
-
-int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
-    return end_begin_async(w, false, n_enter, n_leave);
-    });
-}
-
-int gwaoi_tick_end_begin_pairs_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
-    return gw::api_guard([&]() -> int {
-    if (!w) return GWAOI_EINVAL;
-    return end_begin_async(w, true, n_enter, n_leave);
-    });
-}
-
-int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out) {
-    return gw::api_guard([&]() -> int {
-    if (!w || !out) return GWAOI_EINVAL;
-    out->n_enter = out->n_leave = 0;
-    out->enter = out->leave = nullptr;
-    GW_LIVE(w);
-    if (w->out_pairs) return GWAOI_ESTATE;  // the last copy-out holds pairs: gwaoi_pairs_host
-    if (int rw = finish_out(w)) return poison(w, rw);
-    out->n_enter = w->last_n_enter;
-    out->n_leave = w->last_n_leave;
-    out->enter = w->h_events;
-    out->leave = w->h_events ? w->h_events + 2 * w->last_n_enter : nullptr;
     return GWAOI_OK;
-    });
 }
 
-int gwaoi_pairs_host(gwaoi_world *w, gwaoi_events *out) {
-    return gw::api_guard([&]() -> int {
-    if (!w || !out) return GWAOI_EINVAL;
-    out->n_enter = out->n_leave = 0;
-    out->enter = out->leave = nullptr;
-    GW_LIVE(w);
-    if (!w->out_pairs) return GWAOI_ESTATE;
-    if (int rw = finish_out(w)) return poison(w, rw);
-    out->n_enter = w->last_n_enter / 2;
-    out->n_leave = w->last_n_leave / 2;
-    out->enter = w->h_events;
-    out->leave = w->h_events ? w->h_events + w->last_n_enter : nullptr;
-    return GWAOI_OK;
-    });
-}
-
-int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
-    return gw::api_guard([&]() -> int {
-    if (!w || !out) return GWAOI_EINVAL;
-    out->n_enter = out->n_leave = 0;
-    out->enter = out->leave = nullptr;
-    GW_LIVE(w);
-    if (!w->in_flight) return GWAOI_ESTATE;
-    bool committed;
-    int rc = tick_finish(w, &committed);
-    if (!committed) return rc;
+// The flush's end with its events copied to host memory on its own stream, no next flush
+// (gwaoi_tick, gwaoi_tick_finish(GWAOI_END_HOST)): the copy is the D2H stage of the stage timing.
+int end_host(gwaoi_world *w, bool *committed) {
+    int rc = tick_finish(w, committed);
+    if (!*committed) return rc;
     // committed: deliver the events whatever the status (InterestedIn/By must follow the frame)
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
-    int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1));
-    if (rc2) return poison(w, rc2);  // the committed events cannot reach the caller
+    if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1)))
+        return poison(w, rc2);  // the committed events cannot reach the caller
     w->out_pairs = false;
+    w->out_n_enter = w->last_n_enter;
+    w->out_n_leave = w->last_n_leave;
     FlushSet &S = w->fs[w->last_set];
     stage_begin(w, S, ST_D2H);
     if (tot) {
@@ -2541,13 +2466,79 @@ int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out) {
         (void)hipStreamSynchronize(w->stream);
         stage_collect(w, S);
     }
-    out->n_enter = w->last_n_enter;
-    out->n_leave = w->last_n_leave;
-    out->enter = w->h_events;
-    out->leave = w->h_events + 2 * w->last_n_enter;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gwaoi_tick_finish(gwaoi_world *w, uint32_t mode, uint64_t *n_enter, uint64_t *n_leave) {
+    return gw::api_guard([&]() -> int {
+    if (!w) return GWAOI_EINVAL;
+    if (n_enter) *n_enter = 0;
+    if (n_leave) *n_leave = 0;
+    if (mode & ~(GWAOI_END_NEXT | GWAOI_END_HOST | GWAOI_END_PAIRS)) return GWAOI_EINVAL;
+    GW_LIVE(w);
+    if (!w->in_flight) return GWAOI_ESTATE;
+    const bool next = (mode & GWAOI_END_NEXT) != 0, pairs = (mode & GWAOI_END_PAIRS) != 0;
+    const bool host = pairs || (mode & GWAOI_END_HOST) != 0;
+    if (host) {
+        // the host copy is being replaced: until this flush's copy is queued it holds nothing
+        if (int rw = finish_out(w)) return poison(w, rw);
+        w->out_n_enter = w->out_n_leave = 0;
+        w->out_pairs = pairs;
+    }
+    bool committed = false;
+    int rc;
+    if (host && !next && !pairs) {
+        rc = end_host(w, &committed);
+    } else {
+        const uint64_t regrows = w->dbg.event_regrows;
+        rc = next ? end_begin(w, &committed) : tick_finish(w, &committed);
+        if (committed && host)
+            if (int rc2 = copy_out(w, pairs, regrows)) return rc2;
+    }
+    if (committed) {
+        if (n_enter) *n_enter = w->last_n_enter;
+        if (n_leave) *n_leave = w->last_n_leave;
+    }
     return rc;
     });
 }
+
+int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out) return GWAOI_EINVAL;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    GW_LIVE(w);
+    if (w->out_pairs) return GWAOI_ESTATE;  // the last copy-out holds pairs: gwaoi_pairs_host
+    if (int rw = finish_out(w)) return poison(w, rw);
+    out->n_enter = w->out_n_enter;
+    out->n_leave = w->out_n_leave;
+    out->enter = w->h_events;
+    out->leave = w->h_events ? w->h_events + 2 * w->out_n_enter : nullptr;
+    return GWAOI_OK;
+    });
+}
+
+int gwaoi_pairs_host(gwaoi_world *w, gwaoi_events *out) {
+    return gw::api_guard([&]() -> int {
+    if (!w || !out) return GWAOI_EINVAL;
+    out->n_enter = out->n_leave = 0;
+    out->enter = out->leave = nullptr;
+    GW_LIVE(w);
+    if (!w->out_pairs) return GWAOI_ESTATE;
+    if (int rw = finish_out(w)) return poison(w, rw);
+    out->n_enter = w->out_n_enter / 2;
+    out->n_leave = w->out_n_leave / 2;
+    out->enter = w->h_events;
+    out->leave = w->h_events ? w->h_events + w->out_n_enter : nullptr;
+    return GWAOI_OK;
+    });
+}
+
 
 int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
     const int sp = w ? gw::api_guard([&]() -> int {
@@ -2564,7 +2555,7 @@ int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave) {
         if (n_leave) *n_leave = 0;
         return rc;
     }
-    return gwaoi_tick_end_device(w, n_enter, n_leave);
+    return gwaoi_tick_finish(w, 0u, n_enter, n_leave);
 }
 
 int gwaoi_events_device(gwaoi_world *w, const uint32_t **d_enter, const uint32_t **d_leave) {
@@ -2588,6 +2579,8 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
         const uint64_t tot = w->last_n_enter + w->last_n_leave;
         if (int rc2 = ensure_host_events(w, std::max<uint64_t>(tot, 1))) return poison(w, rc2);
         w->out_pairs = false;
+        w->out_n_enter = w->last_n_enter;
+        w->out_n_leave = w->last_n_leave;
         if (tot) {
             HIP_TRY(hipMemcpyAsync(w->h_events, w->fs[w->last_set].events, 2 * tot * sizeof(uint32_t),
                                    hipMemcpyDeviceToHost, w->stream));
@@ -2601,7 +2594,17 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out) {
     });
     if (sp <= 0) return sp;  // committed sparse flush, or an error
     if (int rc = gwaoi_tick_begin(w)) return rc;
-    return gwaoi_tick_end(w, out);
+    return gw::api_guard([&]() -> int {
+        bool committed = false;
+        const int rc = end_host(w, &committed);
+        if (committed) {
+            out->n_enter = w->out_n_enter;
+            out->n_leave = w->out_n_leave;
+            out->enter = w->h_events;
+            out->leave = w->h_events + 2 * w->out_n_enter;
+        }
+        return rc;
+    });
 }
 
 namespace {

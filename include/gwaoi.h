@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GWAOI_ABI_VERSION 3
+#define GWAOI_ABI_VERSION 4  /* 4: the six flush-ending calls folded into gwaoi_tick_finish */
 
 typedef struct gwaoi_world gwaoi_world;
 
@@ -111,7 +111,7 @@ typedef struct {
     uint64_t combined_queue_drains; /* combined-pass survivor queues drained in the middle of a sweep         */
     uint64_t special_global;        /* special-pass lanes whose events spilled past their LDS slots          */
     uint64_t event_regrows;         /* flushes that grew the device event buffer and re-ran the pair passes  */
-    uint64_t speculative_launches;  /* flushes gwaoi_tick_end_begin_device queued before the commit of the  */
+    uint64_t speculative_launches;  /* flushes GWAOI_END_NEXT queued before the commit of the       */
                                     /* one in flight                                                         */
     uint64_t cell_size_switches;    /* flushes that rebuilt every grid with another automatic cell size      */
     uint32_t cells_per_dist;        /* cells per AOI distance of the grids in use (2 or 3 when automatic)    */
@@ -120,6 +120,7 @@ typedef struct {
     uint64_t sparse_flushes;        /* flushes of a few Moved calls done on the frame in place (gwaoi_tick*) */
     uint64_t sparse_declined;       /* sparse flushes that fell back to the full one (long shifts, capacity)  */
     uint64_t premarked_runs;        /* flushes whose first batch's claims were stored beside the flush before */
+    uint64_t sparse_unfused;        /* sparse flushes that ran the kernel sequence (an op outgrew its row)    */
 } gwaoi_debug;
 
 typedef struct {
@@ -205,54 +206,57 @@ int gwaoi_tick(gwaoi_world *w, gwaoi_events *out);
 /* Run the tick; events stay in device memory (see gwaoi_events_device). */
 int gwaoi_tick_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
 
-/* Asynchronous flush: gwaoi_tick == gwaoi_tick_begin + gwaoi_tick_end.
+/* Asynchronous flush: gwaoi_tick == gwaoi_tick_begin + gwaoi_tick_finish(GWAOI_END_HOST).
  * _begin closes the op queue, queues the whole pipeline on the GPU and returns
- * at once.  Until _end, the AOIManager calls (enter / leave / moved and their
+ * at once.  Until _finish, the AOIManager calls (enter / leave / moved and their
  * batch forms, except explicit-seq device batches) stay available: they are
  * validated and numbered at the call -- a gwaoi_moved_batch is also staged
  * and sent to the GPU on a copy stream, overlapping the flush -- and queued
- * for the NEXT flush when _end commits this one.  Everything else
+ * for the NEXT flush when _finish commits this one.  Everything else
  * (neighbours, snapshot/restore, the sync layer, another _begin) returns
- * GWAOI_ESTATE while a flush is in flight.  _end waits, commits and returns
- * the events as gwaoi_tick / gwaoi_tick_device do. */
+ * GWAOI_ESTATE while a flush is in flight. */
 int gwaoi_tick_begin(gwaoi_world *w);
-int gwaoi_tick_end(gwaoi_world *w, gwaoi_events *out);
-int gwaoi_tick_end_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
-/* The steady game loop's flush: _end_device of the flush in flight, then
- * _begin of the next one with the calls queued meanwhile -- one call per tick,
- * the next flush in flight on return.  When those calls are device Moved
- * batches only (gwaoi_moved_batch_device: implicit seqs, no Enter / Leave /
- * space change, no host op) and the flush in flight has no explicit-seq batch,
- * the next flush is queued on the GPU BEFORE this one's summary is waited for,
- * so the GPU runs the two back to back (its frame, S', candidates and events
- * live in a second buffer set; an event-buffer overflow of the first is still
- * re-run exactly).  Otherwise the next flush starts after the commit.  Returns
- * the finished flush's status and counts; its events stay readable through
- * gwaoi_events_device until the next commit.  The next flush is in flight on
- * return whenever the finished one committed. */
-int gwaoi_tick_end_begin_device(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
-/* The same with the finished flush's events copied to host memory (as
- * gwaoi_tick_end; valid until the next call that returns events).  The copy
- * runs on its own stream, beside the next flush. */
-int gwaoi_tick_end_begin(gwaoi_world *w, gwaoi_events *out);
-/* The same without waiting for the copy: the finished flush's events are on
- * their way to host memory when this returns (counts in *n_enter / *n_leave),
- * and gwaoi_events_host waits for them.  The caller queues the next tick's
- * batch (e.g. gwaoi_moved_batch_pinned) in between, so that batch's H2D copy
- * and this D2H copy run at the same time.  Any later call that returns events
- * or starts another copy-out waits for this one first. */
-int gwaoi_tick_end_begin_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
-/* The events of the last gwaoi_tick_end_begin_async, in host memory (waits
- * for their copy); valid until the next call that returns events. */
+
+/* gwaoi_tick_finish: wait for the flush in flight, commit it, and return its
+ * status and counts (directed events; zero unless it committed).  `mode` is an
+ * OR of:
+ *   GWAOI_END_NEXT   begin the next flush with the calls queued meanwhile (the
+ *                    steady game loop: one call per tick, the next flush in
+ *                    flight on return whenever this one committed).  When those
+ *                    calls are device Moved batches only (implicit seqs, no
+ *                    Enter / Leave / space change, no host op) and the flush in
+ *                    flight has no explicit-seq batch, the next flush is queued
+ *                    on the GPU BEFORE this one's summary is waited for, so the
+ *                    GPU runs the two back to back (a second buffer set; an
+ *                    event-buffer overflow of the first is still re-run
+ *                    exactly).
+ *   GWAOI_END_HOST   copy the events to host memory: gwaoi_events_host returns
+ *                    them (with GWAOI_END_NEXT the copy runs beside the next
+ *                    flush and gwaoi_events_host waits for it, so a caller can
+ *                    queue the next tick's batch -- e.g. gwaoi_moved_batch_pinned
+ *                    -- while the copy runs).
+ *   GWAOI_END_PAIRS  as GWAOI_END_HOST with half the bytes: the flush reports
+ *                    every relation change as the mirrored pair (a,b),(b,a), and
+ *                    only (a,b) is copied.  gwaoi_pairs_host returns them:
+ *                    n_enter / n_leave pairs, each entry (a,b) standing for the
+ *                    events (a,b) and (b,a) -- OnEnterAOI / OnLeaveAOI on both
+ *                    entities.  (The counts returned here are directed events.)
+ * Events stay in device memory in every mode (gwaoi_events_device).
+ *
+ * Buffer lifetime, the one rule for every flush-ending call: events in device
+ * memory (gwaoi_events_device, gwaoi_events_csr_device) are valid until the
+ * next commit; events in host memory (gwaoi_tick's *out, gwaoi_events_host,
+ * gwaoi_pairs_host, gwaoi_events_csr) until the next call that copies events to
+ * host memory (gwaoi_tick, or gwaoi_tick_finish with GWAOI_END_HOST /
+ * GWAOI_END_PAIRS).  gwaoi_events_host / gwaoi_pairs_host always describe the
+ * last host copy, whatever committed since; after a GWAOI_END_PAIRS copy
+ * gwaoi_events_host (and gwaoi_pairs_host after any other) returns
+ * GWAOI_ESTATE. */
+#define GWAOI_END_NEXT 1u
+#define GWAOI_END_HOST 2u
+#define GWAOI_END_PAIRS 4u
+int gwaoi_tick_finish(gwaoi_world *w, uint32_t mode, uint64_t *n_enter, uint64_t *n_leave);
 int gwaoi_events_host(gwaoi_world *w, gwaoi_events *out);
-/* gwaoi_tick_end_begin_async copying half the bytes: the flush reports every
- * relation change as the mirrored pair (a,b),(b,a), and only (a,b) crosses
- * PCIe.  gwaoi_pairs_host returns them: n_enter / n_leave pairs, each entry
- * (a,b) standing for the two events (a,b) and (b,a) -- OnEnterAOI / OnLeaveAOI
- * on both entities.  (The counts of _pairs_async are directed events, as
- * elsewhere.)  gwaoi_events_host after a _pairs_async (and gwaoi_pairs_host
- * after anything else) returns GWAOI_ESTATE. */
-int gwaoi_tick_end_begin_pairs_async(gwaoi_world *w, uint64_t *n_enter, uint64_t *n_leave);
 int gwaoi_pairs_host(gwaoi_world *w, gwaoi_events *out);
 
 /* ---- zero-copy host move batches ---------------------------------------------

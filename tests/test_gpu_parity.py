@@ -1091,7 +1091,7 @@ def _device_events(w, ne, nl):
 @pytest.mark.parametrize("event_capacity,repeats,ready", [(0, False, False), (3000, False, False), (0, True, False),
                                                           (0, True, True), (3000, False, True)])
 def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats, ready):
-    """gwaoi_tick_end_begin_device: the next flush queued before the commit of the one in
+    """gwaoi_tick_finish(NEXT): the next flush queued before the commit of the one in
     flight (device Moved batches only) gives every flush the events of the serial path -- also when the
     flush in flight overflows its event buffer and is re-run after its successor
     (event_capacity=3000), when a batch moves slots more than once (repeats: the last
@@ -1346,8 +1346,8 @@ def test_device_enter_of_live_slot_poisons_gpu():
 
 def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
     """gwaoi_moved_batch_stage / _commit (moves written straight into pinned staging, checked
-    on the device) == gwaoi_moved_batch, serial and pipelined with gwaoi_tick_end_begin (the
-    event copy beside the next flush) and with gwaoi_tick_end_begin_async + gwaoi_events_host;
+    on the device) == gwaoi_moved_batch, serial and pipelined with gwaoi_tick_finish(NEXT|HOST) (the
+    event copy beside the next flush) and with gwaoi_tick_finish(NEXT|HOST) + gwaoi_events_host;
     a partial commit, a batch after an Enter in the same flush (host-checked, space column),
     and a dead slot dropped and reported by the flush."""
     wl = make_workload("cfg3", n=40000)
@@ -1431,7 +1431,7 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             np.testing.assert_array_equal(pair_keys(ea), pair_keys(eb), err_msg=f"pipelined tick {t}")
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"pipelined tick {t}")
         assert A.debug_counters()["speculative_launches"] >= 3
-        # pipelined with the copy-out left running (gwaoi_tick_end_begin_async): batch t+1 queued from
+        # pipelined with the copy-out left running (gwaoi_tick_finish(NEXT|HOST)): batch t+1 queued from
         # the caller's pinned buffer, tick t-1's events taken (gwaoi_events_host), then t finished
         host = [wl.tick(9 + t) for t in range(5)]
         ptrs, got = [], []
@@ -1461,7 +1461,7 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             np.testing.assert_array_equal(pair_keys(got[t][1]), pair_keys(lb), err_msg=f"async tick {t}")
         for p in ptrs:
             A.free_pinned_batch(p)
-        # the same with one event per mirrored pair copied out (gwaoi_tick_end_begin_pairs_async):
+        # the same with one event per mirrored pair copied out (gwaoi_tick_finish(NEXT|PAIRS)):
         # the pairs and their mirrors are the directed events
         host = [wl.tick(14 + t) for t in range(4)]
         ptrs, got = [], []
@@ -1489,6 +1489,16 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"pairs tick {t}")
         for p in ptrs:
             A.free_pinned_batch(p)
+        # a commit without a copy-out (gwaoi_tick_device) leaves the host copy and its counts
+        # alone: gwaoi_events_host still describes the buffer it points at
+        prev = A.events_host()
+        A.moved_batch(*wl.tick(20))
+        ne, nl = A.tick_device()
+        again = A.events_host()
+        assert (len(again[0]), len(again[1])) == (len(prev[0]), len(prev[1]))
+        assert (ne, nl) != (len(prev[0]), len(prev[1]))
+        np.testing.assert_array_equal(again[0], prev[0])
+        np.testing.assert_array_equal(again[1], prev[1])
         # a move of a slot that is not live: dropped on the device, reported by the flush
         A.leave(5)
         A.tick()
@@ -1501,14 +1511,21 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
         np.testing.assert_array_equal(A.snapshot()["x"][A.snapshot()["slot"] == 6], [np.float32(2.0)])
 
 
-@pytest.mark.parametrize("cfg,n,seed", [("cfg3", 30000, 5), ("cfg2", 20000, 9)])
-def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, cfg, n, seed):
+@pytest.mark.parametrize("cfg,n,seed,mode", [("cfg3", 30000, 5, "fused"), ("cfg2", 20000, 9, "fused"),
+                                             ("cfg3", 30000, 6, "scr2"), ("cfg2", 20000, 10, "sequence")])
+def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, monkeypatch, cfg, n, seed, mode):
     """The sparse flush (a few Moved calls: events against the frame in place, the frame patched
     in place, a cell changer shifted into its new cell) gives exactly the events of the full
     flush and of the sequential oracle, flush after flush; the full flushes in between start
     from the patched frame.  Batches of 1-300 moves: host calls (< 64) and staged host batches
     (64..256), repeated slots, steps across cells and rows, and teleports far enough that the
-    shifts are declined (the full flush runs instead)."""
+    shifts are declined (the full flush runs instead).  mode: the one-launch form (fused), the
+    same with two-event scratch rows so that busy ops fall back to the kernel sequence (scr2),
+    and the kernel sequence alone (GWAOI_SPARSE_FUSED=0)."""
+    if mode == "scr2":
+        monkeypatch.setenv("GWAOI_SPARSE_SCR", "2")
+    if mode == "sequence":
+        monkeypatch.setenv("GWAOI_SPARSE_FUSED", "0")
     wl = make_workload(cfg, n=n, seed=seed)
     slots, x0, z0, _ = wl.initial()
     m = oracle_mod.XZList(wl.D, n)
@@ -1557,4 +1574,5 @@ def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, cfg, n, se
                     np.testing.assert_array_equal(A.neighbors(i), m.neighbors(i).astype(np.uint32))
         d = A.debug_counters()
         assert d["sparse_flushes"] >= 20, d
+        assert (d["sparse_unfused"] > 0) == (mode == "scr2"), d
         assert B.debug_counters()["sparse_flushes"] == 0

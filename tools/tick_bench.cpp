@@ -11,7 +11,7 @@
 // Three measurements, one JSON line:
 //   serial     gwaoi_moved_batch_pinned + gwaoi_tick per tick (latency p50 / p99)
 //   pipelined  gwaoi_tick_begin(t); gwaoi_moved_batch_pinned(t+1) while the GPU runs;
-//              gwaoi_tick_end(t)  (period = host replay overlapped with the flush)
+//              gwaoi_tick_finish(t)  (period = host replay overlapped with the flush)
 //   replay     the tick's events into the sets: the event pairs on one thread;
 //              the per-entity rows of gwaoi_events_csr on one and on T threads
 //              (each thread owns the sets of a slot range; persistent pool)
@@ -299,7 +299,7 @@ int main(int argc, char **argv) {
     }
     // ---- pipelined leg: while the GPU runs the flush of tick t, the host stages the batch of
     // t+1 and replays the callbacks of t-1 on T threads (the events of t-1 stay in the pinned
-    // buffer until gwaoi_tick_end(t) replaces them)
+    // buffer until gwaoi_tick_finish(t) replaces them)
     std::vector<double> p_lat, t_repT, p_host;
     auto replay_T = [&]() {  // the rows of the last gwaoi_events_csr, T pool threads over slot ranges
         const double r0 = now();
@@ -319,7 +319,7 @@ int main(int argc, char **argv) {
         if (have_prev) replay_T();  // tick t-1's callbacks, overlapping the flush of t
         p_host.push_back(now() - h0);
         uint64_t ne_, nl_;
-        check(gwaoi_tick_end_device(w, &ne_, &nl_), "tick_end", w);
+        check(gwaoi_tick_finish(w, 0u, &ne_, &nl_), "tick_end", w);
         check(gwaoi_events_csr(w, &coff, &citems, &cn), "events_csr", w);
         p_lat.push_back(now() - t_issue);  // from this tick's batch call to its rows in host memory
         have_prev = true;
