@@ -1017,22 +1017,36 @@ def cfg5_job(args, ws, rank, local):
         cmd.append("--no-cpu-baseline")
     t0 = time.perf_counter()
     err_path = out + ".err"
-    with open(err_path, "w") as err_fh:
+    err_text = ""
+    with open(err_path, "w") as err_fh, open(err_path) as tail_fh:
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=err_fh)
-        try:
-            rc = p.wait(timeout=args.cfg5_timeout)
-        except subprocess.TimeoutExpired:
-            p.kill()
-            p.wait()
-            rc = "timeout"
+        rc = None
+        beat = t0
+        while rc is None:  # the child's stderr passed on as it comes (its phase lines show a slow run live)
+            try:
+                rc = p.wait(timeout=2.0)
+            except subprocess.TimeoutExpired:
+                now = time.perf_counter()
+                if now - t0 > args.cfg5_timeout:
+                    p.kill()
+                    p.wait()
+                    rc = "timeout"
+                elif now - beat >= 60.0:
+                    beat = now
+                    print(f"[cfg5 job, rank {rank}] child running for {now - t0:.0f} s", file=sys.stderr, flush=True)
+            new = tail_fh.read()
+            if new:
+                err_text += new
+                sys.stderr.write(new)
+                sys.stderr.flush()
+        new = tail_fh.read()
+        err_text += new
+        sys.stderr.write(new)
     wall = round(time.perf_counter() - t0, 1)
-    try:  # the child's stderr, passed on, and its phase lines (where a slow or killed run spent its time)
-        with open(err_path) as fh:
-            err_text = fh.read()
+    try:
         os.unlink(err_path)
     except OSError:
-        err_text = ""
-    sys.stderr.write(err_text)
+        pass
     phase_lines = [ln for ln in err_text.splitlines() if ln.startswith("[cfg5 rank")]
     if rank != 0:
         return None
@@ -1292,7 +1306,8 @@ def main():
 
     timed_stages = w.stage_times() if not args.no_timing else {}
     info = w.info()
-    spec_launches = w.debug_counters()["speculative_launches"]
+    dbg_all = w.debug_counters()
+    spec_launches = dbg_all["speculative_launches"]
     # ---- per-stage breakdown: separate ticks, every stage bracketed by HIP events
     stages = {}
     if bd:
@@ -1390,6 +1405,9 @@ def main():
                           f"({spec_launches} of {args.steps} timed flushes)" if spec else
                           "overlap: batch t+1 registered while flush t runs" if overlap else "serial"),
             "roofline": roofline,
+            "debug_counters": {k: int(dbg_all[k]) for k in ("flushes", "combined_replays", "combined_queue_drains",
+                                                             "special_global", "event_regrows", "speculative_launches")
+                               if k in dbg_all},
             "host_to_host_tick": ({k: host_io[k] for k in ("value", "unit", "ms_per_step", "p50_tick_ms", "p99_tick_ms")}
                                   | {"serial_p50_tick_ms": host_io["serial"]["p50_tick_ms"],
                                      "serial_p99_tick_ms": host_io["serial"]["p99_tick_ms"],
