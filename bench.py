@@ -868,10 +868,12 @@ def run_strips(args, ws, rank, local, dist):
     cpu_here = rank == 0 and ws == 1 and not args.no_cpu_baseline
     x0h = wl.x.cpu().numpy() if cpu_here else None
     z0h = wl.z.cpu().numpy() if cpu_here else None
-    init_ops = wl.initial_ops(edges_t, rank)
-    ops = [wl.tick_ops(edges_t, rank) for _ in range(ticks)]
+    torch.cuda.synchronize()
+    ph.mark("positions")  # (the process's first GPU work: its HIP context)
+    allops = wl.strip_ops(edges_t, rank, ticks)  # one host sync
+    init_ops, ops = allops[0], allops[1:]
     ops0h = ops[0].cpu().numpy() if cpu_here else None
-    del wl
+    del wl, allops
     torch.cuda.synchronize()
     ph.mark("inputs")
     sh = StripShard(n, float(D_CFG5), edges, rank, device=local, cells_per_dist=args.cells_per_dist)

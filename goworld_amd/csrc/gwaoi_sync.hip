@@ -699,163 +699,6 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
     }
 }
 
-// k_fan_write with its stores taken off the loading waves (GWAOI_FW_SPLIT=1, A/B): 2 * ST threads,
-// waves 0..3 find and gather the records exactly as k_fan_write does and stage each group of 64 in
-// an LDS ring; wave w + 4 stores wave w's groups.  A wave's loads wait, in issue order, behind its
-// own earlier stores (one vmcnt counter for both on gfx950); here the loading waves issue no
-// stores and the storing waves never wait on a load.
-#ifndef GWAOI_FW_SPLIT
-#define GWAOI_FW_SPLIT 0
-#endif
-constexpr int FWS_NS = 2;  // ring slots per loader/storer pair
-
-__global__ __launch_bounds__(2 * ST) void k_fan_write_split(FanArgs A) {
-    extern __shared__ uint32_t lds[];  // bin[G + 1] | gbase[G] | seg[G]
-    __shared__ uint32_t s_pre[ST], s_sb[ST], s_gate[ST];
-    __shared__ uint4 s_cli[ST];
-    __shared__ uint4 ring[ST / 64][FWS_NS][3 * 64];
-    __shared__ uint32_t rpos[ST / 64][FWS_NS][64];
-    __shared__ uint32_t rfull[ST / 64][FWS_NS];  // records staged in the slot (0: free)
-    __shared__ uint32_t s_ws[2 * ST / 64];
-    __shared__ uint32_t s_R;
-    uint32_t *bin = lds, *gbase = lds + A.G + 1, *seg = gbase + A.G;
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
-    const uint32_t ne = A.F.n + A.n_left;
-    const uint32_t ln = s_lane(), wv = threadIdx.x / 64;
-    const bool loader = threadIdx.x < ST;
-    const uint32_t w = wv & (ST / 64 - 1);  // the pair
-    for (uint32_t q = threadIdx.x; q <= A.G; q += blockDim.x) bin[q] = 0u;
-    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) gbase[q] = A.blk_cnt[(size_t)q * A.nb + blk];
-    if (threadIdx.x < (ST / 64) * FWS_NS) (&rfull[0][0])[threadIdx.x] = 0u;
-    __syncthreads();
-    const uint32_t i = blk * ST + threadIdx.x;
-    const uint32_t g = loader && i < ne ? A.rg[i] : NO_GATE;
-    const uint32_t key = g == NO_GATE ? A.G : g;
-    const uint32_t r0 = loader ? atomicAdd(&bin[key], 1u) : 0u;
-    __syncthreads();
-    lds_excl_scan(bin, A.G + 1, s_ws);
-    if (loader) {
-        const uint32_t p = bin[key] + r0;
-        const uint32_t c = g != NO_GATE ? A.fcnt[i] : 0u;
-        s_pre[p] = c;
-        s_sb[p] = c ? A.fsb[i] : 0u;
-        s_gate[p] = key;
-        if (c) s_cli[p] = A.cid[A.rslot[i]];
-    }
-    __syncthreads();
-    uint32_t x = 0;  // inclusive prefix of the records per receiver (ST entries, waves 0..3)
-    if (loader) {
-        x = s_pre[threadIdx.x];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if ((int)ln >= o) x += y;
-        }
-        if (ln == 63) s_ws[wv] = x;
-    }
-    __syncthreads();
-    if (loader) {
-        uint32_t pre = 0;
-        for (uint32_t q = 0; q < wv; ++q) pre += s_ws[q];
-        s_pre[threadIdx.x] = pre + x;
-        if (threadIdx.x == ST - 1) s_R = pre + x;
-    }
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) seg[q] = bin[q] ? s_pre[bin[q] - 1] : 0u;
-    __syncthreads();
-    const uint32_t R = s_R;
-    const uint32_t per = (R + ST - 1u) / ST * 64u;  // ST / 64 chunks, as k_fan_write
-    const uint32_t c0 = min(R, w * per), c1 = min(R, c0 + per);
-    if (!loader) {  // ---- the storing wave of pair w
-        uint32_t k = 0;
-        for (uint32_t rk = c0; rk < c1; rk += 64, ++k) {
-            const uint32_t sl = k % FWS_NS;
-            uint32_t nrec;
-            while ((nrec = __hip_atomic_load(&rfull[w][sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u)
-                __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            uint4 v[3];
-            uint32_t o[3];
-#pragma unroll
-            for (uint32_t j = 0; j < 3; ++j) {
-                const uint32_t e = ln + 64u * j, rr = e / 3u;
-                v[j] = ring[w][sl][e];
-                o[j] = rr < nrec ? 3u * rpos[w][sl][rr] + (e - 3u * rr) : 0xFFFFFFFFu;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the slot's reads are done
-            if (ln == 0) __hip_atomic_store(&rfull[w][sl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-            for (uint32_t j = 0; j < 3; ++j)
-                if (o[j] != 0xFFFFFFFFu) st_stream(A.out + (size_t)o[j], v[j]);
-        }
-        return;
-    }
-    // ---- the loading wave of pair w (k_fan_write's loop, its emit into the ring)
-    const uint4 *srec = A.srec;
-    auto place = [&](uint32_t r, uint32_t q, uint32_t &sidx, uint32_t &pos) {
-        const uint32_t gq = s_gate[q];
-        sidx = s_sb[q] + r - (q ? s_pre[q - 1] : 0u);
-        pos = gbase[gq] + (r - seg[gq]);
-    };
-    auto search = [&](uint32_t r) {
-        uint32_t lo = 0, hi = ST - 1;
-        while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (s_pre[m] > r) hi = m;
-            else lo = m + 1;
-        }
-        return lo;
-    };
-    uint32_t kslot = 0;
-    auto emit = [&](uint32_t nrec, bool ok, uint32_t q, uint32_t pos, const uint4 &id, const uint4 &pv) {
-        const uint32_t sl = kslot % FWS_NS;
-        while (__hip_atomic_load(&rfull[w][sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u)
-            __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (ok) {
-            rpos[w][sl][ln] = pos;
-            ring[w][sl][3 * ln] = s_cli[q];
-            ring[w][sl][3 * ln + 1] = id;
-            ring[w][sl][3 * ln + 2] = pv;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (ln == 0) __hip_atomic_store(&rfull[w][sl], nrec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        ++kslot;
-    };
-    uint32_t qc = c0 + ln < c1 ? search(c0 + ln) : 0u;
-    for (uint32_t rw = c0; rw < c1; rw += FW_G * 64) {
-        uint32_t q[FW_G], pos[FW_G], h[FW_G];
-        bool ok[FW_G];
-#pragma unroll
-        for (int k = 0; k < FW_G; ++k) {
-            const uint32_t r = rw + (uint32_t)k * 64u + ln;
-            ok[k] = r < c1;
-            uint32_t sidx = 0;
-            q[k] = pos[k] = 0;
-            if (ok[k]) {
-                while (s_pre[qc] <= r) ++qc;
-                q[k] = qc;
-                place(r, qc, sidx, pos[k]);
-            }
-            h[k] = ok[k] ? A.scr[sidx] : 0u;
-        }
-        uint4 id[FW_G], pv[FW_G];
-#pragma unroll
-        for (int k = 0; k < FW_G; ++k) {
-            id[k] = pv[k] = make_uint4(0, 0, 0, 0);
-            if (ok[k]) {
-                id[k] = srec[2 * (size_t)h[k]];
-                pv[k] = srec[2 * (size_t)h[k] + 1];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < FW_G; ++k) {
-            const uint32_t rk = rw + (uint32_t)k * 64u;
-            if (rk < c1) emit(min(64u, c1 - rk), ok[k], q[k], pos[k], id[k], pv[k]);
-        }
-    }
-}
-
 // -------------------------------------------------------------- route ------
 struct RouteArgs {
     const uint32_t *ev;  // (a,b) pairs: [enters | leaves]
@@ -1417,10 +1260,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     }
     if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;
     A.out = S->out;
-    if (total) {
-        if (GWAOI_FW_SPLIT) k_fan_write_split<<<nb, 2 * ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
-        else k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
-    }
+    if (total) k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
     SY_TRY(hipGetLastError());
     S->h_off.assign(S->h_off_raw.begin(), S->h_off_raw.end());
     if (to_host) {

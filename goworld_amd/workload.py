@@ -224,32 +224,38 @@ class DeviceUniformWorkload:
     def owner(self, x, edges_t):
         return self.torch.bucketize(x, edges_t, right=True)
 
-    def initial_ops(self, edges_t, rank: int):
-        """Enter ops (kind 1) of the entities whose start position is in strip `rank`; seq = 1 + slot."""
+    def strip_ops(self, edges_t, rank: int, ticks: int):
+        """[Enter ops of the entities whose start position is in strip `rank` (kind 1, seq = 1 +
+        slot)] + [Moved ops of each of `ticks` ticks for the entities the strip owns before it
+        (kind 0)], advancing the world; int32 (m, 6) halo records, slots ascending.  One host
+        sync for all of them (the owned counts): several ranks sharing one GPU (the gloo
+        rehearsal) time-slice the device, and a sync per tick cost seconds each there."""
         torch = self.torch
+        pend = []
         own = self.owner(self.x, edges_t) == rank
-        slots = torch.nonzero(own).flatten()
-        seq = 1 + slots.to(torch.int64)
+        pend.append(self._owned_first(own, self.x, self.z, 1, 1 + torch.arange(self.n, device=self.dev)))
         self.next_seq = max(self.next_seq, self.n + 1)
-        return self._records(slots, self.x[slots], self.z[slots], 1, seq)
+        for _ in range(ticks):
+            g = torch.Generator(device=self.dev)
+            g.manual_seed((self.seed * 1000003 + self.t) & 0x7FFFFFFFFFFFFFFF)
+            sx = (2 * torch.rand(self.n, generator=g, device=self.dev, dtype=torch.float64) - 1).to(torch.float32)
+            sz = (2 * torch.rand(self.n, generator=g, device=self.dev, dtype=torch.float64) - 1).to(torch.float32)
+            order = torch.randperm(self.n, generator=g, device=self.dev)
+            pos = torch.empty_like(order)
+            pos[order] = torch.arange(self.n, device=self.dev)
+            own = self.owner(self.x, edges_t) == rank
+            nx = self.x + sx
+            nz = self.z + sz
+            pend.append(self._owned_first(own, nx, nz, 0, self.next_seq + pos))
+            self.x, self.z = nx, nz
+            self.next_seq += self.n
+            self.t += 1
+        counts = torch.stack([c for _, c in pend]).cpu().tolist()  # the one host sync
+        return [r[:c].clone() for (r, _), c in zip(pend, counts)]
 
-    def tick_ops(self, edges_t, rank: int):
-        """Moved ops of tick t for the entities strip `rank` owns before it; advances the world."""
+    def _owned_first(self, own, x, z, kind, seq):
+        """Records of every entity, the owned ones first in slot order (a stable sort of the
+        ownership flag), and the owned count on the device."""
         torch = self.torch
-        g = torch.Generator(device=self.dev)
-        g.manual_seed((self.seed * 1000003 + self.t) & 0x7FFFFFFFFFFFFFFF)
-        sx = (2 * torch.rand(self.n, generator=g, device=self.dev, dtype=torch.float64) - 1).to(torch.float32)
-        sz = (2 * torch.rand(self.n, generator=g, device=self.dev, dtype=torch.float64) - 1).to(torch.float32)
-        order = torch.randperm(self.n, generator=g, device=self.dev)
-        pos = torch.empty_like(order)
-        pos[order] = torch.arange(self.n, device=self.dev)
-        own = self.owner(self.x, edges_t) == rank
-        nx = self.x + sx
-        nz = self.z + sz
-        slots = torch.nonzero(own).flatten()
-        seq = self.next_seq + pos[slots]
-        rec = self._records(slots, nx[slots], nz[slots], 0, seq)
-        self.x, self.z = nx, nz
-        self.next_seq += self.n
-        self.t += 1
-        return rec
+        idx = torch.argsort((~own).to(torch.uint8), stable=True)
+        return self._records(idx, x[idx], z[idx], kind, seq[idx]), own.sum()

@@ -159,3 +159,40 @@ def test_count_row_round_trip():
         assert (got[2] is None) == (want[2] is None)
         if want[2] is not None:
             assert np.array_equal(got[2], want[2])
+
+
+def test_device_workload_strip_ops_one_sync():
+    """DeviceUniformWorkload.strip_ops (one host sync for every tick's ops, the owned records
+    first by a stable sort) gives exactly the records of the per-tick selection by nonzero it
+    replaced, on the CPU device: Enter ops of the starting strip, then each tick's Moved ops of
+    the entities the strip owns before the tick, slots ascending, seqs in global call order."""
+    import torch
+    from goworld_amd.strips import even_edges
+    from goworld_amd.workload import DeviceUniformWorkload
+    n, ticks, ws = 5000, 3, 3
+    for rank in range(ws):
+        wl = DeviceUniformWorkload(n, 77, "cpu")
+        edges_t = torch.from_numpy(even_edges(ws, -wl.L / 2, wl.L / 2))
+        got = wl.strip_ops(edges_t, rank, ticks)
+        ref = DeviceUniformWorkload(n, 77, "cpu")
+        own = ref.owner(ref.x, edges_t) == rank
+        slots = torch.nonzero(own).flatten()
+        want = [ref._records(slots, ref.x[slots], ref.z[slots], 1, 1 + slots.to(torch.int64))]
+        seq_next = n + 1
+        for t in range(ticks):
+            g = torch.Generator(device="cpu")
+            g.manual_seed((77 * 1000003 + t) & 0x7FFFFFFFFFFFFFFF)
+            sx = (2 * torch.rand(n, generator=g, dtype=torch.float64) - 1).to(torch.float32)
+            sz = (2 * torch.rand(n, generator=g, dtype=torch.float64) - 1).to(torch.float32)
+            order = torch.randperm(n, generator=g)
+            pos = torch.empty_like(order)
+            pos[order] = torch.arange(n)
+            own = ref.owner(ref.x, edges_t) == rank
+            nx, nz = ref.x + sx, ref.z + sz
+            slots = torch.nonzero(own).flatten()
+            want.append(ref._records(slots, nx[slots], nz[slots], 0, seq_next + pos[slots]))
+            ref.x, ref.z = nx, nz
+            seq_next += n
+        assert len(got) == len(want) == ticks + 1
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
