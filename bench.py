@@ -837,30 +837,16 @@ class PhaseClock:
         return dict(self.phases, total=round(time.perf_counter() - self.t0, 3))
 
 
-def run_strips(args, ws, rank, local, dist):
-    """Config 5: one 2^24-entity space cut into one x-strip per rank; every
-    tick routes the owned moves, exchanges halo records over RCCL (counts,
-    with the ENTER / LEAVE statistics, all-gathered on the host over gloo;
-    records point to point to the neighbour strips in one RCCL send/recv
-    group) and queues each strip's tick on the GPU (the strip records become
-    device Leave / Enter / Moved batches of its world, which flushes; the
-    filter keeps the strip's events).  The next tick's route waits once for
-    its counts and completes the previous tick with that same wait
-    (goworld_amd/strips.py).  Inputs are generated on the GPU before timing
-    (DeviceUniformWorkload); value = all N moves per tick / max time."""
+def strip_inputs(args, ws, rank, local):
+    """Config 5's inputs for this rank's strip, generated on the GPU (DeviceUniformWorkload) before
+    the process group exists: in a gloo job, GPU work after init_process_group ran ~500x slower
+    on the one-GPU rehearsal box.  Returns the inputs and their phase times."""
     import torch
-    from goworld_amd.shard import reduce_over_ranks
-    from goworld_amd.strips import StripShard, even_edges, exchange, exchange_local, local_slice, setup_count_group
+    from goworld_amd.strips import even_edges
     from goworld_amd.workload import DeviceUniformWorkload
-
     dev = torch.device(f"cuda:{local}")
-    ph = PhaseClock(f"cfg5 rank {rank}", args.phases_t0, args.phases_pre)  # wall time per phase (JSON + stderr)
-    if dist is not None:
-        setup_count_group(dist)  # collective over every rank: the host count all-gather's gloo group
-        dist.barrier()  # RCCL's communicator exists before the first batched send/recv
-        ph.mark("count_group_and_barrier")
+    t0 = time.perf_counter()
     n = args.n or (1 << 24)
-    t_setup = time.perf_counter()
     wl = DeviceUniformWorkload(n, 0x5EED0005, dev)
     edges = even_edges(ws, -wl.L / 2, wl.L / 2)
     edges_t = torch.from_numpy(edges).to(dev)
@@ -869,13 +855,42 @@ def run_strips(args, ws, rank, local, dist):
     x0h = wl.x.cpu().numpy() if cpu_here else None
     z0h = wl.z.cpu().numpy() if cpu_here else None
     torch.cuda.synchronize()
-    ph.mark("positions")  # (the process's first GPU work: its HIP context)
+    t1 = time.perf_counter()
     allops = wl.strip_ops(edges_t, rank, ticks)  # one host sync
     init_ops, ops = allops[0], allops[1:]
     ops0h = ops[0].cpu().numpy() if cpu_here else None
     del wl, allops
     torch.cuda.synchronize()
-    ph.mark("inputs")
+    t2 = time.perf_counter()
+    return {"n": n, "edges": edges, "ticks": ticks, "cpu_here": cpu_here, "x0h": x0h, "z0h": z0h,
+            "init_ops": init_ops, "ops": ops, "ops0h": ops0h,
+            "phases": {"positions": round(t1 - t0, 3), "inputs": round(t2 - t1, 3)}}
+
+
+def run_strips(args, ws, rank, local, dist, inp):
+    """Config 5: one 2^24-entity space cut into one x-strip per rank; every
+    tick routes the owned moves, exchanges halo records (the count rows
+    all-gathered on the device, RCCL; records point to point to the neighbour
+    strips in one RCCL send/recv group) and queues each strip's tick on the
+    GPU (the strip records become device Leave / Enter / Moved batches of its
+    world, which flushes; the filter keeps the strip's events).  The next
+    tick's route waits once for its counts and completes the previous tick
+    with that same wait (goworld_amd/strips.py).  Inputs (``strip_inputs``)
+    were generated on the GPU before the process group; value = all N moves
+    per tick / max time."""
+    import torch
+    from goworld_amd.shard import reduce_over_ranks
+    from goworld_amd.strips import StripShard, exchange, exchange_local, local_slice, setup_count_group
+
+    dev = torch.device(f"cuda:{local}")
+    ph = PhaseClock(f"cfg5 rank {rank}", args.phases_t0, args.phases_pre)  # wall time per phase (JSON + stderr)
+    if dist is not None:
+        setup_count_group(dist)  # collective over every rank: the host count all-gather's gloo group
+        dist.barrier()  # RCCL's communicator exists before the first batched send/recv
+        ph.mark("count_group_and_barrier")
+    n, edges, ticks, cpu_here = inp["n"], inp["edges"], inp["ticks"], inp["cpu_here"]
+    x0h, z0h, init_ops, ops, ops0h = inp["x0h"], inp["z0h"], inp["init_ops"], inp["ops"], inp["ops0h"]
+    t_setup = time.perf_counter() - sum(inp["phases"].values())
     sh = StripShard(n, float(D_CFG5), edges, rank, device=local, cells_per_dist=args.cells_per_dist)
     ph.mark("strip_world_create")
     via_cpu = args.dist_backend == "gloo"
@@ -1148,6 +1163,7 @@ def main():
     dist = None
     args.phases_t0 = T_START
     args.phases_pre = {}
+    strip_inp = None
     if ws > 1:
         import torch
         import torch.distributed as dist
@@ -1159,16 +1175,25 @@ def main():
         if args.dist_backend == "gloo":  # rehearsal: several ranks may share a GPU
             local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
+        t_in = time.perf_counter()
+        if args.workload == "cfg5":  # the inputs before the process group (strip_inputs)
+            strip_inp = strip_inputs(args, ws, rank, local)
         t_pg = time.perf_counter()
         dist.init_process_group(args.dist_backend)
-        args.phases_pre = {"start_to_process_group": round(t_pg - T_START, 3),
-                           "init_process_group": round(time.perf_counter() - t_pg, 3)}
+        args.phases_pre = {"start_to_inputs": round(t_in - T_START, 3)}
+        if strip_inp is not None:
+            args.phases_pre.update(strip_inp["phases"])
+        args.phases_pre["init_process_group"] = round(time.perf_counter() - t_pg, 3)
         if args.workload == "cfg5":
             print(f"[cfg5 rank {rank}] {args.phases_pre}", file=sys.stderr, flush=True)
     device = local
     red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{device}"
     if args.workload == "cfg5":
-        run_strips(args, ws, rank, local, dist)
+        if strip_inp is None:
+            t_in = time.perf_counter()
+            strip_inp = strip_inputs(args, ws, rank, local)
+            args.phases_pre = {"start_to_inputs": round(t_in - T_START, 3)} | strip_inp["phases"]
+        run_strips(args, ws, rank, local, dist, strip_inp)
         if dist is not None:
             dist.destroy_process_group()
         return

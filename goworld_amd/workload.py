@@ -26,6 +26,9 @@ world bounds (Space.GetSpaceRange is unused, engine/entity/Space.go:52-54).
 from __future__ import annotations
 
 import math
+import os
+import sys
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -231,6 +234,8 @@ class DeviceUniformWorkload:
         sync for all of them (the owned counts): several ranks sharing one GPU (the gloo
         rehearsal) time-slice the device, and a sync per tick cost seconds each there."""
         torch = self.torch
+        trace = os.environ.get("GWAOI_INPUT_TRACE") == "1"  # per-tick wall times to stderr (diagnostics)
+        t0 = time.perf_counter()
         pend = []
         own = self.owner(self.x, edges_t) == rank
         pend.append(self._owned_first(own, self.x, self.z, 1, 1 + torch.arange(self.n, device=self.dev)))
@@ -250,6 +255,10 @@ class DeviceUniformWorkload:
             self.x, self.z = nx, nz
             self.next_seq += self.n
             self.t += 1
+            if trace:
+                torch.cuda.synchronize(self.dev) if self.dev.type == "cuda" else None
+                print(f"[strip_ops rank {rank}] tick {self.t} at {time.perf_counter() - t0:.2f} s", file=sys.stderr,
+                      flush=True)
         counts = torch.stack([c for _, c in pend]).cpu().tolist()  # the one host sync
         return [r[:c].clone() for (r, _), c in zip(pend, counts)]
 
