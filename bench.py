@@ -837,33 +837,48 @@ class PhaseClock:
         return dict(self.phases, total=round(time.perf_counter() - self.t0, 3))
 
 
-def strip_inputs(args, ws, rank, local):
-    """Config 5's inputs for this rank's strip, generated on the GPU (DeviceUniformWorkload) before
-    the process group exists: in a gloo job, GPU work after init_process_group ran ~500x slower
-    on the one-GPU rehearsal box.  Returns the inputs and their phase times."""
+def strip_inputs(args, ws, rank, local, on_host: bool = False):
+    """Config 5's inputs for this rank's strip, generated before the process group exists:
+    on the GPU (DeviceUniformWorkload), or, when several ranks share one GPU (on_host: the gloo
+    rehearsal), on the host (HostUniformWorkload) and sent in one copy -- there, torch's
+    generation kernels from several processes at once stalled the shared GPU for 40-90 s per
+    tick.  Returns the inputs and their phase times."""
     import torch
     from goworld_amd.strips import even_edges
-    from goworld_amd.workload import DeviceUniformWorkload
+    from goworld_amd.workload import DeviceUniformWorkload, HostUniformWorkload
     dev = torch.device(f"cuda:{local}")
     t0 = time.perf_counter()
     n = args.n or (1 << 24)
-    wl = DeviceUniformWorkload(n, 0x5EED0005, dev)
-    edges = even_edges(ws, -wl.L / 2, wl.L / 2)
-    edges_t = torch.from_numpy(edges).to(dev)
     ticks = args.warmup + args.steps
     cpu_here = rank == 0 and ws == 1 and not args.no_cpu_baseline
-    x0h = wl.x.cpu().numpy() if cpu_here else None
-    z0h = wl.z.cpu().numpy() if cpu_here else None
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    allops = wl.strip_ops(edges_t, rank, ticks)  # one host sync
+    if on_host:
+        wl = HostUniformWorkload(n, 0x5EED0005)
+        edges = even_edges(ws, -wl.L / 2, wl.L / 2)
+        x0h, z0h = (wl.x.copy(), wl.z.copy()) if cpu_here else (None, None)
+        t1 = time.perf_counter()
+        parts = wl.strip_ops(edges, rank, ticks)
+        rows = np.cumsum([0] + [p.shape[0] for p in parts])
+        allh = torch.from_numpy(np.concatenate(parts))
+        ops0h = parts[1] if cpu_here else None
+        alld = allh.to(dev)  # one allocation, one copy
+        allops = [alld[int(rows[q]):int(rows[q + 1])] for q in range(len(parts))]
+        del parts, allh
+    else:
+        wl = DeviceUniformWorkload(n, 0x5EED0005, dev)
+        edges = even_edges(ws, -wl.L / 2, wl.L / 2)
+        edges_t = torch.from_numpy(edges).to(dev)
+        x0h = wl.x.cpu().numpy() if cpu_here else None
+        z0h = wl.z.cpu().numpy() if cpu_here else None
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        allops = wl.strip_ops(edges_t, rank, ticks)  # one host sync
+        ops0h = allops[1].cpu().numpy() if cpu_here else None
     init_ops, ops = allops[0], allops[1:]
-    ops0h = ops[0].cpu().numpy() if cpu_here else None
     del wl, allops
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     return {"n": n, "edges": edges, "ticks": ticks, "cpu_here": cpu_here, "x0h": x0h, "z0h": z0h,
-            "init_ops": init_ops, "ops": ops, "ops0h": ops0h,
+            "init_ops": init_ops, "ops": ops, "ops0h": ops0h, "generated_on": "host" if on_host else "gpu",
             "phases": {"positions": round(t1 - t0, 3), "inputs": round(t2 - t1, 3)}}
 
 
@@ -995,6 +1010,7 @@ def run_strips(args, ws, rank, local, dist, inp):
             "host_waits_per_tick": waits_all / ws / max(args.steps, 1),
             "strip_world_entities_sum": live_all, "setup_s": round(setup_s, 2), "phases_s": ph.record(),
             "strip_counts": args.strip_counts if dist is not None else "local",
+            "inputs_generated_on": inp["generated_on"],
             "rank0_phase_ms_per_tick": {"route_and_previous_tick_wait": round(phases[0] / args.steps * 1e3, 4),
                                         "exchange": round(phases[1] / args.steps * 1e3, 4),
                                         "tick_queue": round(phases[2] / args.steps * 1e3, 4)},
@@ -1177,7 +1193,7 @@ def main():
         torch.cuda.set_device(local)
         t_in = time.perf_counter()
         if args.workload == "cfg5":  # the inputs before the process group (strip_inputs)
-            strip_inp = strip_inputs(args, ws, rank, local)
+            strip_inp = strip_inputs(args, ws, rank, local, on_host=ws > torch.cuda.device_count())
         t_pg = time.perf_counter()
         dist.init_process_group(args.dist_backend)
         args.phases_pre = {"start_to_inputs": round(t_in - T_START, 3)}

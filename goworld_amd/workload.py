@@ -268,3 +268,57 @@ class DeviceUniformWorkload:
         torch = self.torch
         idx = torch.argsort((~own).to(torch.uint8), stable=True)
         return self._records(idx, x[idx], z[idx], kind, seq[idx]), own.sum()
+
+
+class HostUniformWorkload:
+    """Config 5 as DeviceUniformWorkload lays it out, generated on the host with numpy (bench
+    only): the same shape (N uniform in [-L/2, L/2)^2, U(-1,1) steps per axis in float32, a
+    random global call order per tick), another random stream.  For ranks that share one GPU
+    (the gloo rehearsal): torch's generation kernels from several processes at once stalled the
+    shared GPU for tens of seconds per tick there, and these records reach the GPU in one copy."""
+
+    def __init__(self, n: int, seed: int):
+        self.n = n
+        self.L = math.sqrt(n * 1250.0)
+        self.D = D_DEFAULT
+        self.seed = seed
+        rng = np.random.default_rng(seed)
+        self.x = (rng.random(n) * self.L - self.L / 2).astype(np.float32)
+        self.z = (rng.random(n) * self.L - self.L / 2).astype(np.float32)
+        self.t = 0
+
+    @staticmethod
+    def _records(slots, x, z, kind, seq):
+        r = np.empty((slots.size, 6), np.int32)
+        r[:, 0] = slots.astype(np.int32)
+        r[:, 1] = x.view(np.int32)
+        r[:, 2] = z.view(np.int32)
+        r[:, 3] = kind
+        r[:, 4] = (seq & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+        r[:, 5] = (seq >> 32).astype(np.int32)
+        return r
+
+    def strip_ops(self, edges: np.ndarray, rank: int, ticks: int):
+        """The records of DeviceUniformWorkload.strip_ops (Enter ops of the starting strip, then each
+        tick's Moved ops of the entities the strip owns before it), as numpy arrays."""
+        e = np.asarray(edges, np.float32)
+        own = np.searchsorted(e, self.x, side="right") == rank  # torch.bucketize(..., right=True)
+        slots = np.nonzero(own)[0]
+        out = [self._records(slots, self.x[slots], self.z[slots], 1, 1 + slots.astype(np.int64))]
+        next_seq = self.n + 1
+        for _ in range(ticks):
+            rng = np.random.default_rng((self.seed * 1000003 + self.t) & 0x7FFFFFFFFFFFFFFF)
+            sx = (2 * rng.random(self.n) - 1).astype(np.float32)
+            sz = (2 * rng.random(self.n) - 1).astype(np.float32)
+            order = rng.permutation(self.n)
+            pos = np.empty(self.n, np.int64)
+            pos[order] = np.arange(self.n)
+            own = np.searchsorted(e, self.x, side="right") == rank
+            nx = self.x + sx
+            nz = self.z + sz
+            slots = np.nonzero(own)[0]
+            out.append(self._records(slots, nx[slots], nz[slots], 0, next_seq + pos[slots]))
+            self.x, self.z = nx, nz
+            next_seq += self.n
+            self.t += 1
+        return out

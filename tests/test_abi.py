@@ -45,6 +45,11 @@ def test_pure_host_entry_points(lib):
     # null-argument handling never touches the device
     assert lib.gwaoi_world_create(None, None) == -1
     assert lib.gwaoi_tick(None, None) == -1
+    # the flush end (one entry point, mode bits) and its host readers validate the handle first
+    assert lib.gwaoi_tick_finish(None, 0, None, None) == -1
+    assert lib.gwaoi_tick_finish(None, 7, None, None) == -1
+    assert lib.gwaoi_events_host(None, None) == -1
+    assert lib.gwaoi_pairs_host(None, None) == -1
     assert lib.gwaoi_world_destroy(None) == -1
     # entity-sync entry points validate before any device work
     assert lib.gwaoi_entity_bind(None, 0, None) == -1

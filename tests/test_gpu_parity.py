@@ -1576,3 +1576,85 @@ def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, monkeypatc
         assert d["sparse_flushes"] >= 20, d
         assert (d["sparse_unfused"] > 0) == (mode == "scr2"), d
         assert B.debug_counters()["sparse_flushes"] == 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_sparse_flushes_multi_space_gpu(monkeypatch, fused):
+    """Sparse flushes in a world of several spaces whose coordinates overlap (each space its own
+    grid, space-major cells): a mover's partners come from its own space only, and the frame
+    patch (shifts into a new cell) keeps every space's cell ranges exact.  Each flush equals the
+    full-flush world's; the spaces' sizes differ (one nearly empty), and some moves cross many
+    cells."""
+    if not fused:
+        monkeypatch.setenv("GWAOI_SPARSE_FUSED", "0")
+    rng = np.random.default_rng(31)
+    sizes = [4000, 2500, 7, 1500]
+    n = sum(sizes)
+    with World(n + 16, max_spaces=8) as A, World(n + 16, max_spaces=8, sparse=False) as B:
+        spaces = [(A.space_create(D), B.space_create(D)) for _ in sizes]
+        lo = 0
+        x = np.empty(n, np.float32)
+        z = np.empty(n, np.float32)
+        for (sa, sb), k in zip(spaces, sizes):
+            sl = np.arange(lo, lo + k, dtype=np.uint32)
+            x[lo:lo + k] = rng.uniform(-800, 800, k).astype(np.float32)
+            z[lo:lo + k] = rng.uniform(-800, 800, k).astype(np.float32)
+            A.enter_batch(sa, sl, x[lo:lo + k], z[lo:lo + k])
+            B.enter_batch(sb, sl, x[lo:lo + k], z[lo:lo + k])
+            lo += k
+        A.tick()
+        B.tick()
+        for it in range(30):
+            k = int(rng.choice([1, 3, 20, 70, 200]))
+            sl = rng.choice(n, k, replace=True).astype(np.uint32)
+            step = np.where(rng.random(k) < 0.8, rng.uniform(-2, 2, k), rng.uniform(-150, 150, k)).astype(np.float32)
+            nx = (x[sl] + step).astype(np.float32)
+            nz = (z[sl] + rng.uniform(-2, 2, k).astype(np.float32)).astype(np.float32)
+            A.moved_batch(sl, nx, nz)
+            B.moved_batch(sl, nx, nz)
+            for s_, x_, z_ in zip(sl.tolist(), nx.tolist(), nz.tolist()):
+                x[s_], z[s_] = x_, z_
+            ea, la = (pair_keys(e) for e in A.tick())
+            eb, lb = (pair_keys(e) for e in B.tick())
+            np.testing.assert_array_equal(ea, eb, err_msg=f"flush {it} ({k} moves): enters")
+            np.testing.assert_array_equal(la, lb, err_msg=f"flush {it} ({k} moves): leaves")
+            if it % 10 == 9:
+                for i in rng.choice(n, 20, replace=False).tolist():
+                    np.testing.assert_array_equal(A.neighbors(i), B.neighbors(i))
+        assert A.debug_counters()["sparse_flushes"] >= 20
+
+
+def test_tick_finish_modes_and_states_gpu():
+    """gwaoi_tick_finish: unknown mode bits -> GWAOI_EINVAL and nothing happens; no flush in
+    flight -> GWAOI_ESTATE; GWAOI_END_HOST / GWAOI_END_PAIRS copies are what events_host /
+    pairs_host return (pairs_host after a directed copy and events_host after a pairs copy
+    -> GWAOI_ESTATE); mode 0 leaves the last host copy and its counts as they were."""
+    from goworld_amd._lib import GWAOI_END_HOST, GWAOI_END_NEXT, GWAOI_END_PAIRS
+    with World(64) as w:
+        s = w.space_create(D)
+        for i in range(10):
+            w.enter(s, i, float(i), 0.0)
+        with pytest.raises(GwaoiError) as ei:
+            w.finish(0)
+        assert ei.value.code == -3  # nothing in flight
+        w.tick_begin()
+        with pytest.raises(GwaoiError) as ei:
+            w.finish(8)
+        assert ei.value.code == -1  # unknown bit: the flush stays in flight
+        ne, nl = w.finish(GWAOI_END_HOST)
+        assert (ne, nl) == (90, 0)
+        ent, lev = w.events_host()
+        assert len(ent) == 90 and len(lev) == 0
+        with pytest.raises(GwaoiError):
+            w.pairs_host()
+        w.moved(0, 500.0, 0.0)  # 0 leaves 9 neighbours: 18 directed leaves
+        w.tick_begin()
+        ne, nl = w.finish(GWAOI_END_NEXT | GWAOI_END_PAIRS)
+        assert (ne, nl) == (0, 18)
+        pe, pl = w.pairs_host()
+        assert len(pe) == 0 and len(pl) == 9
+        with pytest.raises(GwaoiError):
+            w.events_host()
+        w.finish(0)  # the (empty) next flush; the pairs copy stays what pairs_host returns
+        pe2, pl2 = w.pairs_host()
+        np.testing.assert_array_equal(pl2, pl)

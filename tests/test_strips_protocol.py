@@ -196,3 +196,35 @@ def test_device_workload_strip_ops_one_sync():
         assert len(got) == len(want) == ticks + 1
         for a, b in zip(got, want):
             assert torch.equal(a, b)
+
+
+def test_host_workload_strip_ops_partition():
+    """HostUniformWorkload.strip_ops (the gloo rehearsal's host-generated config-5 inputs): over
+    all ranks, every tick's records cover each entity exactly once, owned by the strip its
+    position lay in before the tick, with the tick's seqs a permutation of one block of n (the
+    global call order); the first batch is the Enter of every entity (seq 1 + slot)."""
+    from goworld_amd.strips import even_edges
+    from goworld_amd.workload import HostUniformWorkload
+    n, ticks, ws = 3000, 3, 4
+    per_rank = []
+    for rank in range(ws):
+        wl = HostUniformWorkload(n, 99)
+        per_rank.append(wl.strip_ops(even_edges(ws, -wl.L / 2, wl.L / 2), rank, ticks))
+    ref = HostUniformWorkload(n, 99)
+    edges = even_edges(ws, -ref.L / 2, ref.L / 2).astype(np.float32)
+    for t in range(ticks + 1):
+        recs = np.concatenate([per_rank[r][t] for r in range(ws)])
+        assert np.array_equal(np.sort(recs[:, 0]), np.arange(n))
+        seq = recs[:, 4].view(np.uint32).astype(np.int64) | (recs[:, 5].astype(np.int64) << 32)
+        if t == 0:
+            assert (recs[:, 3] == 1).all() and np.array_equal(np.sort(seq), 1 + np.arange(n))
+        else:
+            assert (recs[:, 3] == 0).all()
+            assert np.array_equal(np.sort(seq), n + 1 + (t - 1) * n + np.arange(n))
+        if t:  # ownership by the position before the tick (the previous batch's x)
+            own_x = np.concatenate([per_rank[r][t - 1] for r in range(ws)])
+            xs = np.empty(n, np.float32)
+            xs[own_x[:, 0]] = own_x[:, 1].view(np.float32)
+            for r in range(ws):
+                sl = per_rank[r][t][:, 0]
+                assert (np.searchsorted(edges, xs[sl], side="right") == r).all()
