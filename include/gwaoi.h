@@ -81,7 +81,9 @@ typedef struct {
 #define GWAOI_F_NO_SPARSE 2u /* never take the sparse flush (every flush rebuilds the frame; A/B, tests) */
 /* Device Moved batches (gwaoi_moved_batch_device) are complete in memory when passed, not
  * produced on another stream behind gwaoi_stream_after: a batch queued while a flush is in
- * flight then has its last-op claims stored beside that flush, off the next flush's path. */
+ * flight then has its last-op claims stored beside that flush, off the next flush's path.
+ * Measured slower at 1M entities (the claims kernel slows the flush it runs beside more than it
+ * saves the next one: DESIGN.md §3 step 1); for hosts whose GPU idles between flushes. */
 #define GWAOI_F_BATCH_READY 4u
 
 typedef struct {

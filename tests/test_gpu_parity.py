@@ -189,6 +189,50 @@ def test_boundary_stream_gpu(oracle_mod, seed, flush_every):
     run_stream_vs_oracle(oracle_mod, ops, 64, flush_every)
 
 
+@pytest.mark.parametrize("seed", [15, 16])
+def test_boundary_stream_1m_background_gpu(oracle_mod, seed):
+    """The flush_every=1 boundary stream inside a 1M-entity world: the stream's 64 entities move
+    on each other's window edges (+- a few ulps) near the origin, flushed after every op -- a
+    Moved flush is a sparse flush of one call against the 1M-entry frame, an Enter / Leave flush
+    a full one -- while 2^20 background entities of the same space sit far to the side (same
+    grid rows, so a stream entity that changes row shifts background entries of the frame).  No
+    background entity is ever within reach, so the events and relations are exactly the
+    sequential oracle's over the stream alone."""
+    rng = np.random.default_rng(seed)
+    n_s, n_bg = 64, 1 << 20
+    ops = boundary_ops(rng, n_s, 700)
+    orc = oracle_mod.SpacesOracle({0: D}, n_s)
+    L = float(np.sqrt(n_bg * 1250.0))
+    bx = rng.uniform(100000.0, 100000.0 + L, n_bg).astype(np.float32)
+    bz = rng.uniform(-L / 2, L / 2, n_bg).astype(np.float32)
+    with World(n_s + n_bg) as w:
+        s = w.space_create(D)
+        w.enter_batch(s, np.arange(n_s, n_s + n_bg, dtype=np.uint32), bx, bz)
+        w.tick_device()  # the background's own relation (not part of the comparison)
+        sparse0 = w.debug_counters()["sparse_flushes"]
+        for k, op in enumerate(ops):
+            if op[0] == 1:
+                _, i, x, z, _sp = op
+                w.enter(s, i, x, z)
+                orc.enter(0, i, x, z)
+            elif op[0] == 0:
+                _, i, x, z = op[:4]
+                w.moved(i, x, z)
+                orc.moved(i, x, z)
+            else:
+                w.leave(op[1])
+                orc.leave(op[1])
+            ge, gl = flush(w)
+            oe, ol = oracle_mod.net_events(*orc.take_events(with_space=True))
+            np.testing.assert_array_equal(ge, oe, err_msg=f"op {k}: enters")
+            np.testing.assert_array_equal(gl, ol, err_msg=f"op {k}: leaves")
+            if k % 100 == 99:
+                for i in range(0, n_s, 4):
+                    if i in orc.local:
+                        np.testing.assert_array_equal(w.neighbors(i), orc.neighbors(i).astype(np.uint32))
+        assert w.debug_counters()["sparse_flushes"] - sparse0 > 200
+
+
 def test_boundary_stream_multispace_gpu(oracle_mod):
     rng = np.random.default_rng(21)
     ops = boundary_ops(rng, 96, 1500, span=800.0, spaces=(0, 1, 2))
