@@ -2428,6 +2428,9 @@ static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 #ifndef GWAOI_ORDER_BANDS
 #define GWAOI_ORDER_BANDS 1
 #endif
+#ifndef GWAOI_ORDER_STABLE
+#define GWAOI_ORDER_STABLE 0  // A/B: the counting sort keeps the frame order inside a class
+#endif
 constexpr int TO_NB = 64;
 constexpr int TO_BANDS = GWAOI_ORDER_BANDS;
 static_assert(TO_NB * TO_BANDS <= 256, "one histogram bin per thread");
@@ -2452,7 +2455,24 @@ __device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t lo,
     __syncthreads();
     hist[threadIdx.x] = ex;
     __syncthreads();
+#if GWAOI_ORDER_STABLE
+    // stable: tiles of one class keep their frame order (neighbours in flight together share rows)
+    __shared__ uint16_t s_cls[256];
+    for (uint32_t c0 = lo; c0 < hi; c0 += 256) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t k = i < hi ? cls(i) : 0xFFFFu;
+        s_cls[threadIdx.x] = (uint16_t)k;
+        __syncthreads();
+        uint32_t rank = 0;
+        for (uint32_t q = 0; q < threadIdx.x; ++q) rank += s_cls[q] == k;
+        if (i < hi) dst[lo + hist[k] + rank] = i;
+        __syncthreads();
+        if (i < hi) atomicAdd(&hist[k], 1u);
+        __syncthreads();
+    }
+#else
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) dst[lo + atomicAdd(&hist[cls(i)], 1u)] = i;
+#endif
 }
 
 
