@@ -2386,13 +2386,14 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
 #define GWAOI_TILE_TIME 1
 #endif
     if (tile_work && tid == 0) {
+        uint32_t wk = CT;
+        for (int q = 0; q < CW; ++q) wk += L.wwork[q];
 #if GWAOI_TILE_TIME
         tile_work[t] = max(1u, (uint32_t)min(wall_clock64() - t_start, 0xFFFFFFFFull));
 #else
-        uint32_t wk = CT;
-        for (int q = 0; q < CW; ++q) wk += L.wwork[q];
         tile_work[t] = wk;
 #endif
+        tile_work[n_tiles + t] = wk;  // its candidates: how uneven a range's work is (order_range)
     }
 #ifdef GWAOI_EXP_BLOCKTIME  // diagnostics build only: per-block start/end (wall clock) and hardware ids
     if (tid == 0 && t < BT_MAX) {
@@ -2428,25 +2429,63 @@ static_assert(FT <= WAVE, "one wave scans a finish block's tile totals");
 #ifndef GWAOI_ORDER_BANDS
 #define GWAOI_ORDER_BANDS 1
 #endif
-#ifndef GWAOI_ORDER_STABLE
-#define GWAOI_ORDER_STABLE 0  // A/B: the counting sort keeps the frame order inside a class
+#ifndef GWAOI_ORDER_SKEW
+#define GWAOI_ORDER_SKEW 4  // even ranges (top percentile within this many work classes of the median) keep frame order; 0: off
+#endif
+#ifndef GWAOI_ORDER_TOP
+#define GWAOI_ORDER_TOP 2  // ... the percentile, from the heaviest
 #endif
 constexpr int TO_NB = 64;
 constexpr int TO_BANDS = GWAOI_ORDER_BANDS;
 static_assert(TO_NB * TO_BANDS <= 256, "one histogram bin per thread");
 
 // Counting sort of range [lo, hi) of tiles by (band, descending work class) into tile_order[1 + ...].
-__device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t lo, uint32_t hi, uint32_t *tile_order) {
+// tile_work: [measured time of each of the nb tiles | their candidate counts].
+__device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t lo, uint32_t hi,
+                            uint32_t *tile_order) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t ws[256 / WAVE];
     const uint32_t len = hi - lo;
     uint32_t *dst = tile_order + 1;
+    // descending: 0 = heaviest; 8 classes per factor 2 from 2^(off/8): the measured times (100 MHz
+    // ticks: 30 us = 3000) from 2^5, the candidate counts (256 entities x ~27 = 7000) from 2^8
+    auto wcls = [](uint32_t v, int off) {
+        const int c = (int)(8.0f * __log2f((float)v + 1.0f)) - off;
+        return (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
+    };
+#if GWAOI_ORDER_SKEW
+    // An even range -- its heaviest GWAOI_ORDER_TOP percent of tiles within GWAOI_ORDER_SKEW
+    // classes of its median by candidate count (deterministic, unlike the measured time) -- runs in
+    // frame order: reordering only scatters the tiles in flight (their candidate rows no longer
+    // shared in L2), and nothing in it makes a tail.  Uniform worlds (config 5) take this; crowd
+    // hotspots (config 3, tiles 14x apart) are ordered heaviest first.
+    {
+        __shared__ uint32_t s_top, s_p50;
+        hist[threadIdx.x] = 0;
+        if (threadIdx.x == 0) s_top = s_p50 = 0;
+        __syncthreads();
+        for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[wcls(tile_work[nb + i], 64)], 1u);
+        __syncthreads();
+        uint32_t total;
+        const uint32_t ex = block_excl_scan<256>(hist[threadIdx.x], ws, total);
+        const uint32_t incl = ex + hist[threadIdx.x];
+        if (hist[threadIdx.x]) {
+            if (ex * 100 <= len * GWAOI_ORDER_TOP && incl * 100 > len * GWAOI_ORDER_TOP) s_top = threadIdx.x;
+            if (ex * 2 <= len && incl * 2 > len) s_p50 = threadIdx.x;
+        }
+        __syncthreads();
+        if (TO_BANDS == 1 && s_p50 - s_top <= (uint32_t)GWAOI_ORDER_SKEW) {
+            for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) dst[i] = i;
+            return;
+        }
+        __syncthreads();
+    }
+#endif
     hist[threadIdx.x] = 0;
     __syncthreads();
     auto cls = [&](uint32_t i) {  // band-major, then descending work: bin 0 = heaviest of band 0
-        const int c = (int)(8.0f * __log2f((float)tile_work[i] + 1.0f)) - 40;
         const uint32_t band = (uint32_t)(((unsigned long long)(i - lo) * TO_BANDS) / max(len, 1u));
-        return band * TO_NB + (uint32_t)(TO_NB - 1 - min(max(c, 0), TO_NB - 1));
+        return band * TO_NB + wcls(tile_work[i], 40);
     };
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(i)], 1u);
     __syncthreads();
@@ -2455,24 +2494,7 @@ __device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t lo,
     __syncthreads();
     hist[threadIdx.x] = ex;
     __syncthreads();
-#if GWAOI_ORDER_STABLE
-    // stable: tiles of one class keep their frame order (neighbours in flight together share rows)
-    __shared__ uint16_t s_cls[256];
-    for (uint32_t c0 = lo; c0 < hi; c0 += 256) {
-        const uint32_t i = c0 + threadIdx.x;
-        const uint32_t k = i < hi ? cls(i) : 0xFFFFu;
-        s_cls[threadIdx.x] = (uint16_t)k;
-        __syncthreads();
-        uint32_t rank = 0;
-        for (uint32_t q = 0; q < threadIdx.x; ++q) rank += s_cls[q] == k;
-        if (i < hi) dst[lo + hist[k] + rank] = i;
-        __syncthreads();
-        if (i < hi) atomicAdd(&hist[k], 1u);
-        __syncthreads();
-    }
-#else
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) dst[lo + atomicAdd(&hist[cls(i)], 1u)] = i;
-#endif
 }
 
 
@@ -2527,7 +2549,7 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
         }
     }
     __syncthreads();
-    order_range(tile_work, s_cut[x], s_cut[x + 1], tile_order);
+    order_range(tile_work, nb, s_cut[x], s_cut[x + 1], tile_order);
     if (x == 0 && tid <= N_XCD) tile_order[order_meta(nb) + tid] = s_cut[tid];
     if (x == 0 && tid == 0) tile_order[0] = nb;
 }

@@ -221,7 +221,7 @@ struct gwaoi_world {
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
     uint32_t *coll = nullptr;  // slots moved twice in one flush (single-pass apply)
     uint32_t *special = nullptr;  // per previous-frame tile: keygen saw a special entity (the special pass's skip list)
-    uint32_t *tile_work = nullptr;   // per combined tile: its measured time this flush (k_combined)
+    uint32_t *tile_work = nullptr;   // per combined tile: its measured time, then its candidates (k_combined)
     uint32_t *tile_order = nullptr;  // the next flush's combined tile order, heaviest first (k_tile_order)
     uint32_t *ework = nullptr;       // per frame entry: candidates its lane swept (the next flush's deal to waves)
     bool tile_order_on = true;       // GWAOI_TILE_ORDER=0: tiles in xcd_block order
@@ -1608,7 +1608,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
-        (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, N / gw::COMBINED_TILE + 2)) ||
+        (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, 2 * (N / gw::COMBINED_TILE + 2))) ||
         (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 16)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
