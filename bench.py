@@ -1148,6 +1148,9 @@ def main():
     ap.add_argument("--batch-ready", action="store_true",
                     help="A/B: the next batch's claims stored beside the flush in flight (GWAOI_F_BATCH_READY), "
                          "not by the next flush's prologue; slower at config 3 (DESIGN.md sec. 3 step 1)")
+    ap.add_argument("--claims", action="store_true",
+                    help="A/B: apply the moves through the last-op claims + repeated-slot fixup instead of "
+                         "GWAOI_F_UNIQUE_MOVES (the workload's batches name every entity once per tick)")
     ap.add_argument("--small-flush-reps", type=int, default=20,
                     help="cfg3: timed flushes per size of the small-flush leg (1/64/4096/65536 moves; 0 = off)")
     ap.add_argument("--strip-counts", default="device", choices=["device", "host"],
@@ -1255,9 +1258,11 @@ def main():
     del batches
     torch.cuda.synchronize()
 
-    # the move batches are in HBM before the timed region: complete when passed (GWAOI_F_BATCH_READY)
+    # the move batches are in HBM before the timed region: complete when passed (GWAOI_F_BATCH_READY);
+    # each names every moving entity once (a permutation per tick): GWAOI_F_UNIQUE_MOVES, checked on the
+    # device by every flush (a repeated slot would fail the tick)
     w = World(n, max_spaces=wl.n_spaces, device=device, cells_per_dist=args.cells_per_dist,
-              batch_ready=args.batch_ready)
+              batch_ready=args.batch_ready, unique_moves=not args.claims)
     spaces = [w.space_create(wl.D) for _ in range(wl.n_spaces)]
     wl0 = wl_factory()  # initial positions (wl has advanced through the batches)
     slots, x0, z0, sp = wl0.initial()
@@ -1437,7 +1442,10 @@ def main():
                        "parallelism": (f"spaces sharded over {ws} ranks, contiguous blocks balanced by entity count"
                                        if args.workload == "cfg4" else
                                        f"one independent space per rank x{ws}") + " (no data-path collective)",
-                       "total_cells": info["total_cells"]},
+                       "total_cells": info["total_cells"],
+                       "move_apply": ("claims (last-op claims + repeated-slot fixup)" if args.claims else
+                                      "GWAOI_F_UNIQUE_MOVES (each batch names every entity once; checked on the "
+                                      "device every flush)")},
             "events_per_s": events_all / elapsed_max,
             "p50_tick_ms": float(np.percentile(lat_ms, 50)),
             "p99_tick_ms": float(np.percentile(lat_ms, 99)),
@@ -1449,7 +1457,8 @@ def main():
                           "overlap: batch t+1 registered while flush t runs" if overlap else "serial"),
             "roofline": roofline,
             "debug_counters": {k: int(dbg_all[k]) for k in ("flushes", "combined_replays", "combined_queue_drains",
-                                                             "special_global", "event_regrows", "speculative_launches")
+                                                             "special_global", "event_regrows", "speculative_launches",
+                                                             "unique_flushes")
                                if k in dbg_all},
             "host_to_host_tick": ({k: host_io[k] for k in ("value", "unit", "ms_per_step", "p50_tick_ms", "p99_tick_ms")}
                                   | {"serial_p50_tick_ms": host_io["serial"]["p50_tick_ms"],

@@ -21,6 +21,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "gwaoi.h")
 GWAOI_F_TIMING = 1
 GWAOI_F_NO_SPARSE = 2  # never the sparse flush (include/gwaoi.h)
 GWAOI_F_BATCH_READY = 4  # device batches complete when passed: claims stored beside the flush before
+GWAOI_F_UNIQUE_MOVES = 8  # a flush's Moved batches never repeat a slot: no last-op claims (checked on device)
 
 STATUS = {
     0: "GWAOI_OK", -1: "GWAOI_EINVAL", -2: "GWAOI_EBADSLOT", -3: "GWAOI_ESTATE", -4: "GWAOI_ENOMEM",
@@ -112,7 +113,8 @@ class Debug(C.Structure):
                 ("special_global", C.c_uint64), ("event_regrows", C.c_uint64), ("speculative_launches", C.c_uint64),
                 ("cell_size_switches", C.c_uint64), ("cells_per_dist", C.c_uint32), ("pad", C.c_uint32),
                 ("incremental_sorts", C.c_uint64), ("sparse_flushes", C.c_uint64), ("sparse_declined", C.c_uint64),
-                ("premarked_runs", C.c_uint64), ("sparse_unfused", C.c_uint64)]
+                ("premarked_runs", C.c_uint64), ("sparse_unfused", C.c_uint64),
+                ("unique_flushes", C.c_uint64)]
 
 
 class StageTime(C.Structure):
@@ -250,10 +252,10 @@ class World:
 
     def __init__(self, max_slots: int, max_spaces: int = 1, device: int = -1, timing: bool = False,
                  event_capacity: int = 0, cells_per_dist: float = 0.0, sparse: bool = True,
-                 batch_ready: bool = False):
+                 batch_ready: bool = False, unique_moves: bool = False):
         self._L = load()
         flags = ((GWAOI_F_TIMING if timing else 0) | (0 if sparse else GWAOI_F_NO_SPARSE) |
-                 (GWAOI_F_BATCH_READY if batch_ready else 0))
+                 (GWAOI_F_BATCH_READY if batch_ready else 0) | (GWAOI_F_UNIQUE_MOVES if unique_moves else 0))
         cfg = Config(max_slots, max_spaces, device, flags, event_capacity, cells_per_dist)
         h = C.c_void_p()
         self._check(self._L.gwaoi_world_create(C.byref(cfg), C.byref(h)), world=False)

@@ -38,6 +38,7 @@ constexpr uint32_t ERR_BAD_SLOT = 4u;
 constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreement (bug guard)
 constexpr uint32_t ERR_SEQ = 16u;            // explicit device seq below the flush's floor
 constexpr uint32_t ERR_ENTER_LIVE = 32u;     // device Enter of a slot live when the flush began
+constexpr uint32_t ERR_DUP_SLOT = 64u;       // GWAOI_F_UNIQUE_MOVES flush whose moves named a slot twice
 
 constexpr uint32_t TILE_A = 256;  // entities per pair-pass tile (= threads per workgroup)
 
@@ -91,13 +92,13 @@ struct FrameView {
 // Per-tick scalars written by device kernels.
 struct TickScalars {
     uint32_t err;
-    uint32_t pad;
+    uint32_t ndrop;              // unique-moves flush: ops that wrote nothing (placeholders, dropped ops)
     unsigned long long counter;  // directed event pairs reserved by the pair passes
     float d_rel;                 // largest displacement / D of "near" entities
     float bmax;                  // largest |x|,|z| of live entities (new positions)
     unsigned long long seq_max;  // largest explicit seq of the device batches (0 = none)
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
-    uint32_t pad2;
+    uint32_t n_unique;           // unique-moves flush: its ops (keygen's written entries + ndrop must match; 0 = no check)
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
     uint32_t pad3[18];
     // One 128-B line per XCD shard q (zeroed by the prologue): [q][2..3] = the u64 length of
@@ -186,6 +187,9 @@ struct MoveRuns {
 // holds an older seq than seq_floor, so k_keygen takes the previous frame's
 // record for it and writes it back).  n_marked: runs whose claims are stored
 // already (by the prologue: run 0; by launch_moves_mark: every run).
+// unique (GWAOI_F_UNIQUE_MOVES): no run repeats a slot, so no claims are stored or compared and
+// no fixup runs; keygen counts the entries the ops wrote and the scan's fold block checks the
+// count against TickScalars::n_unique (ERR_DUP_SLOT).
 // The re-apply of the slots moved more than once (k_moves_fixup's arguments).
 struct FixupArgs {
     MoveRuns RS;
@@ -200,7 +204,7 @@ struct FixupArgs {
 };
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st);
+                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, hipStream_t st);
 // The same flush through slot buckets (gwaoi_kernels.hip k_mv_*), for worlds whose
 // SlotInfo outgrows the MALL (max_slots > MV_MIN_SLOTS; moves_buckets(max_slots) <=
 // MV_NB_MAX).  hist: moves_hist_elems(n ops, max_slots) uint32; scan_tmp:
@@ -214,14 +218,15 @@ void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *inf
                            uint32_t *scan_tmp, void *binned, hipStream_t st);
 // Zero the per-tick counters and two ranges; bbox entries get the fold
 // identity; S' <- the previous frame's first n_copy entries; and (mark != nullptr)
-// the claims of a moves-only flush's first run.
+// the claims of a moves-only flush's first run.  n_unique: TickScalars::n_unique (0 = no check).
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
                      uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
                      SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
-                     hipStream_t st);
+                     uint32_t n_unique, hipStream_t st);
 
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
-// partials in blk, 2 * cdiv(n, 256) floats).  cnt64 != nullptr (grid
+// partials in blk, 2 * cdiv(n, 256) floats, then cdiv(n, 256) u32 counts of the
+// entries this flush's ops wrote).  cnt64 != nullptr (grid
 // unchanged): also per-cell entity counts (low word) and arrival counts
 // (high word; arrival = cell differs from p_key[i], or i >= n_prev).
 // S' entries i < n_prev whose seq is below seq_base (not written by this flush's

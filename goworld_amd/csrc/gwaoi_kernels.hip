@@ -49,7 +49,7 @@ inline uint32_t cdiv(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t *z1, uint32_t n1, int4 *bbox,
                            uint32_t n_spaces, uint32_t n_copy, const Rec16 *__restrict__ p_rec,
                            const SlotSp *__restrict__ p_ss, Rec16 *s_rec, SlotSp *s_ss, MoveRun mark,
-                           uint32_t max_slots, SlotInfo *info, uint32_t tick) {
+                           uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_unique) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < mark.n) {
         const uint32_t s = mark.ds[i];
@@ -66,6 +66,8 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->bmax = 0.0f;
         sc->seq_max = 0;
         sc->ncoll = 0;
+        sc->ndrop = 0;
+        sc->n_unique = n_unique;
         for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
     if (i < n0) z0[i] = 0;
@@ -245,7 +247,10 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint
 #ifndef GWAOI_APPLY_PER
 #define GWAOI_APPLY_PER 4  // moves per thread of the single-pass apply (all SlotInfo lines in flight at once)
 #endif
-template <int PER>
+// UNIQUE (GWAOI_F_UNIQUE_MOVES): no op shares its slot with another op of the flush, so every op
+// applies without a claim; the ops that write nothing are counted (sc->ndrop, one atomic per wave)
+// for keygen's written-entry check.
+template <int PER, bool UNIQUE>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
                                                        SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
@@ -262,13 +267,26 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
     for (int u = 0; u < PER; ++u)  // every SlotInfo line in flight at once
         si[u] = o[u].slot < max_slots ? slot_info(info, o[u].slot) : make_uint4(0, 0, 0, 0);
     unsigned long long smax = 0;
+    uint32_t drop = 0;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t i = i0 + (uint32_t)u * 256u;
         const uint32_t s = o[u].slot;
-        if (i >= R.n || s == SLOT_NONE) continue;
+        if (i >= R.n) continue;
+        if (s == SLOT_NONE) {
+            ++drop;
+            continue;
+        }
         if (s >= max_slots) {
             atomicOr(&sc->err, ERR_BAD_SLOT);
+            ++drop;
+            continue;
+        }
+        if (UNIQUE) {
+            const unsigned long long q =
+                op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false);
+            if (!q) ++drop;
+            smax = q > smax ? q : smax;
             continue;
         }
         const unsigned long long mine = ((unsigned long long)tick << 32) | (R.j0 + i);
@@ -281,6 +299,10 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
             atomicMax(&info[s].lastop, mine);
             coll[atomicAdd(&sc->ncoll, 1u)] = s;
         }
+    }
+    if (UNIQUE) {
+        for (int q = 32; q > 0; q >>= 1) drop += __shfl_xor(drop, q, WAVE);
+        if (lane() == 0 && drop) atomicAdd(&sc->ndrop, drop);
     }
     if (R.dseq) {
         for (int q = 32; q > 0; q >>= 1) {
@@ -371,10 +393,12 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     float dr = 0.0f, bm = 0.0f;
     uint32_t key = sentinel;
     bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
+    bool written = false;
     if (i < n) {
         const uint32_t s = ld_ss(s_ss, i).sp;
         if (s != SP_DEAD) {
             Rec16 r = ld_rec(s_rec, i);
+            written = r.s >= seq_base;
             const bool same = i < n_prev && ld_ss(p_ss, i).sp == s;
             if (same || (i < n_prev && r.s < seq_base)) {
                 const Rec16 p = ld_rec(p_rec, i);
@@ -422,7 +446,10 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     // an entity that is not near (left, changed space, jumped)?  k_pairs<1> skips the tiles without
     const bool sp_any = __syncthreads_or(i < n_prev && !near);
     if (special && threadIdx.x == 0 && blockIdx.x * 256u < n_prev) special[blockIdx.x] = sp_any ? 1u : 0u;
+    // the entries this flush's ops wrote (GWAOI_F_UNIQUE_MOVES: one per op that applied)
+    const uint32_t nw = (uint32_t)__syncthreads_count(written);
     if (threadIdx.x == 0) {
+        reinterpret_cast<uint32_t *>(blk)[2 * gridDim.x + blockIdx.x] = nw;
         float a = s_m[0][0], b = s_m[1][0];
         for (int q = 1; q < 256 / WAVE; ++q) {
             a = fmaxf(a, s_m[0][q]);
@@ -430,6 +457,27 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         }
         blk[2 * blockIdx.x] = a;
         blk[2 * blockIdx.x + 1] = b;
+    }
+}
+
+// GWAOI_F_UNIQUE_MOVES: the entries the ops wrote (keygen's per-block counts after the 2 nb
+// partials) plus the ops that wrote nothing must be the flush's ops; fewer means two ops shared a
+// slot, and which one's position the frame holds is then not defined (ERR_DUP_SLOT).  T threads.
+template <int T>
+__device__ __forceinline__ void unique_check(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
+    __shared__ uint32_t s_c[T / WAVE];
+    const uint32_t want = sc->n_unique;  // block-uniform
+    if (!want) return;
+    const uint32_t *cnt = reinterpret_cast<const uint32_t *>(blk) + 2 * nb;
+    uint32_t c = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += T) c += cnt[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane() == 0) s_c[threadIdx.x / WAVE] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < T / WAVE; ++q) c += s_c[q];
+        if (c + sc->ndrop != want) atomicOr(&sc->err, ERR_DUP_SLOT);
     }
 }
 
@@ -464,6 +512,7 @@ __device__ __forceinline__ void keygen_fold(const float *__restrict__ blk, uint3
 __global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict__ blk, uint32_t nb,
                                                         TickScalars *sc) {
     keygen_fold(blk, nb, sc);
+    unique_check<1024>(blk, nb, sc);
 }
 
 // ----------------------------------------------------------------- scan ------
@@ -998,6 +1047,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     const uint32_t b = blockIdx.x;
     if (b == nb) {
         keygen_fold256(blk, nbk, sc);
+        unique_check<SC_T>(blk, nbk, sc);
         return;
     }
     __shared__ unsigned long long tile[S64_TILE + S64_TILE / 16];
@@ -2851,12 +2901,12 @@ void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_to
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
                      uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
                      SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
-                     hipStream_t st) {
+                     uint32_t n_unique, hipStream_t st) {
     MoveRun mk{};
     if (mark) mk = *mark;
     const size_t m = std::max<size_t>({n0, n1, (size_t)n_spaces, (size_t)n_copy, (size_t)mk.n, (size_t)EV_SHARDS * 32});
     k_prologue<<<cdiv(m, 256), 256, 0, st>>>(sc, z0, (uint32_t)n0, z1, (uint32_t)n1, bbox, n_spaces, n_copy, p_rec,
-                                             p_ss, s_rec, s_ss, mk, max_slots, info, tick_id);
+                                             p_ss, s_rec, s_ss, mk, max_slots, info, tick_id, n_unique);
 }
 
 void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
@@ -2875,12 +2925,19 @@ void launch_moves_mark(const MoveRun &R, uint32_t max_slots, SlotInfo *info, uin
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, hipStream_t st) {
+                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, hipStream_t st) {
+    if (unique) {  // no claims, no fixup
+        for (uint32_t q = 0; q < RS.count; ++q)
+            if (RS.r[q].n)
+                k_moves_apply_n<GWAOI_APPLY_PER, true><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+                    RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
+        return;
+    }
     for (uint32_t q = n_marked; q < RS.count; ++q)  // every run's claims before any apply
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
-            k_moves_apply_n<GWAOI_APPLY_PER><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+            k_moves_apply_n<GWAOI_APPLY_PER, false><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
     {
         FixupArgs F;

@@ -315,6 +315,8 @@ struct gwaoi_world {
     // GWAOI_F_BATCH_READY: the first device Moved batch queued while a flush is in flight gets its
     // claims on mark_st once that flush's apply is done (apply_ev), beside the rest of the flush
     bool batch_ready = false;
+    // GWAOI_F_UNIQUE_MOVES: the Moved batches of one flush never repeat a slot (no claims, no fixup)
+    bool unique_moves = false;
     hipStream_t mark_st = nullptr;
     hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
     bool apply_ev_valid = false;
@@ -950,25 +952,32 @@ int tick_launch(gwaoi_world *w) {
     // counters, tile totals, bbox fold identity; S' <- the previous frame unless virtual; the
     // first Moved run's claims
     const bool bucketed = moves_only && w->mv_binned;
-    const gw::MoveRun *mark = moves_only && !bucketed ? &RS.r[0] : nullptr;
+    // GWAOI_F_UNIQUE_MOVES: plain device Moved batches (implicit seqs, the slot's own space) are
+    // applied without last-op claims; keygen's written-entry count checks the promise
+    bool uniq = w->unique_moves && moves_only && virt && !bucketed;
+    for (const Run &r : w->runs)
+        if (uniq && (!r.device || r.kind != RUN_MOVE || r.dseq || r.dsp)) uniq = false;
+    const gw::MoveRun *mark = moves_only && !bucketed && !uniq ? &RS.r[0] : nullptr;
     // the first run's claims stored already, beside the previous flush (GWAOI_F_BATCH_READY)
-    if (mark && w->premark.on && w->premark.tick == tick_id && w->premark.ds == RS.r[0].ds &&
+    if (moves_only && !bucketed && w->premark.on && w->premark.tick == tick_id && w->premark.ds == RS.r[0].ds &&
         w->premark.n == RS.r[0].n) {
         HIP_TRY(hipStreamWaitEvent(st, w->mark_ev, 0));
+        if (mark) w->dbg.premarked_runs++;
         mark = nullptr;
-        w->dbg.premarked_runs++;
     }
+    if (uniq) w->dbg.unique_flushes++;
+    const uint32_t n_unique = uniq ? (uint32_t)n_ops : 0u;
     w->premark.on = false;
     const uint32_t n_copy = virt ? 0u : n_prev;
     if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
                             gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
                             gw::tile_total_elems(entries), dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
-                            w->max_slots, w->sinfo, tick_id, st);
+                            w->max_slots, w->sinfo, tick_id, n_unique, st);
     else
         gw::launch_prologue(S.sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, gw::tile_total_elems(entries), dev_bbox(S),
                             w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark, w->max_slots, w->sinfo,
-                            tick_id, st);
+                            tick_id, n_unique, st);
 
     // ---- apply queued ops onto S'
     stage_begin(w, S, ST_APPLY);
@@ -990,7 +999,7 @@ int tick_launch(gwaoi_world *w) {
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
     } else if (moves_only) {  // one pass + fixup of repeated slots (run 0's claims: prologue or premark)
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
-                         P.rec, n_prev, S.sc, w->coll, 1u, st);
+                         P.rec, n_prev, S.sc, w->coll, 1u, uniq, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -1276,6 +1285,11 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
                             : "live-count mismatch between host and device (a device Enter/Leave batch broke its "
                               "rules, or an internal error)";
         return poison(w, GWAOI_EDEVICE);
+    }
+    if (r.err & gw::ERR_DUP_SLOT) {
+        w->last_error = "GWAOI_F_UNIQUE_MOVES: a slot was moved twice in one flush (its position is one of its "
+                        "moves, not necessarily the last)";
+        return GWAOI_ESTATE;
     }
     if (r.err & gw::ERR_NONFINITE) {
         w->last_error = "device batch held a non-finite coordinate (move dropped)";
@@ -1572,6 +1586,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->batch_ready = (cfg->flags & GWAOI_F_BATCH_READY) != 0;
     if (const char *e = std::getenv("GWAOI_BATCH_READY")) w->batch_ready = w->batch_ready && e[0] != '0';  // A/B
     if (const char *e = std::getenv("GWAOI_PREMARK_LATE")) w->premark_late = e[0] == '1';
+    w->unique_moves = (cfg->flags & GWAOI_F_UNIQUE_MOVES) != 0;
+    if (const char *e = std::getenv("GWAOI_UNIQUE_MOVES")) w->unique_moves = w->unique_moves && e[0] != '0';  // A/B
     if (w->batch_ready && (hipStreamCreateWithFlags(&w->mark_st, hipStreamNonBlocking) != hipSuccess ||
                            hipEventCreateWithFlags(&w->apply_ev, hipEventDisableTiming) != hipSuccess ||
                            hipEventCreateWithFlags(&w->mark_ev, hipEventDisableTiming) != hipSuccess))
@@ -1607,7 +1623,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if ((rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
         (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
-        (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 2 * (N / 256 + 2))) ||
+        (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 3 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, 2 * (N / gw::COMBINED_TILE + 2))) ||
         (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 16)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))

@@ -85,6 +85,15 @@ typedef struct {
  * Measured slower at 1M entities (the claims kernel slows the flush it runs beside more than it
  * saves the next one: DESIGN.md §3 step 1); for hosts whose GPU idles between flushes. */
 #define GWAOI_F_BATCH_READY 4u
+/* The Moved batches of one flush never name a slot twice (a per-tick position array with one
+ * entry per moving entity).  A flush of plain device Moved batches (gwaoi_moved_batch_device,
+ * or gwaoi_moved_batch's staged batches) then applies every move without the last-op claims
+ * and the repeated-slot fixup.  The promise is checked on the device: keygen counts the frame
+ * entries the moves wrote, and a flush with fewer than its moves commits, with the repeated
+ * slot at the position of one of its moves (not necessarily the last), and returns
+ * GWAOI_ESTATE.  Batches with explicit seqs, decoded sync batches and mixed queues keep the
+ * claims.  Measured at 1M entities: DESIGN.md §3 step 2. */
+#define GWAOI_F_UNIQUE_MOVES 8u
 
 typedef struct {
     uint64_t n_enter;      /* directed enter events; replay pair (a,b) as a.OnEnterAOI(b) */
@@ -123,6 +132,7 @@ typedef struct {
     uint64_t sparse_declined;       /* sparse flushes that fell back to the full one (long shifts, capacity)  */
     uint64_t premarked_runs;        /* flushes whose first batch's claims were stored beside the flush before */
     uint64_t sparse_unfused;        /* sparse flushes that ran the kernel sequence (an op outgrew its row)    */
+    uint64_t unique_flushes;        /* flushes applied without last-op claims (GWAOI_F_UNIQUE_MOVES)          */
 } gwaoi_debug;
 
 typedef struct {
