@@ -460,59 +460,50 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     }
 }
 
-// GWAOI_F_UNIQUE_MOVES: the entries the ops wrote (keygen's per-block counts after the 2 nb
-// partials) plus the ops that wrote nothing must be the flush's ops; fewer means two ops shared a
-// slot, and which one's position the frame holds is then not defined (ERR_DUP_SLOT).  T threads.
+// Fold keygen's per-block partials (T threads, one pass): d_rel / bmax into sc, and under
+// GWAOI_F_UNIQUE_MOVES the written-entry counts (after the 2 nb float partials): those plus the ops
+// that wrote nothing must be the flush's ops; fewer means two ops shared a slot, and which one's
+// position the frame holds is then not defined (ERR_DUP_SLOT).
 template <int T>
-__device__ __forceinline__ void unique_check(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
+__device__ __forceinline__ void keygen_fold_t(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
+    __shared__ float s_m[2][T / WAVE];
     __shared__ uint32_t s_c[T / WAVE];
-    const uint32_t want = sc->n_unique;  // block-uniform
-    if (!want) return;
     const uint32_t *cnt = reinterpret_cast<const uint32_t *>(blk) + 2 * nb;
-    uint32_t c = 0;
-    for (uint32_t i = threadIdx.x; i < nb; i += T) c += cnt[i];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if (lane() == 0) s_c[threadIdx.x / WAVE] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int q = 1; q < T / WAVE; ++q) c += s_c[q];
-        if (c + sc->ndrop != want) atomicOr(&sc->err, ERR_DUP_SLOT);
-    }
-}
-
-// Fold keygen's per-block partials into sc->d_rel / sc->bmax (1024 threads).
-__device__ __forceinline__ void keygen_fold(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
-    __shared__ float s_m[2][1024 / WAVE];
     float a = 0.0f, b = 0.0f;
-    for (uint32_t i = threadIdx.x; i < nb; i += 1024) {
+    uint32_t c = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += T) {
         a = fmaxf(a, blk[2 * i]);
         b = fmaxf(b, blk[2 * i + 1]);
+        c += cnt[i];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         a = fmaxf(a, __shfl_xor(a, o));
         b = fmaxf(b, __shfl_xor(b, o));
+        c += __shfl_xor(c, o);
     }
     if (lane() == 0) {
         s_m[0][threadIdx.x / WAVE] = a;
         s_m[1][threadIdx.x / WAVE] = b;
+        s_c[threadIdx.x / WAVE] = c;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int q = 1; q < 1024 / WAVE; ++q) {
+        for (int q = 1; q < T / WAVE; ++q) {
             a = fmaxf(a, s_m[0][q]);
             b = fmaxf(b, s_m[1][q]);
+            c += s_c[q];
         }
         sc->d_rel = a;
         sc->bmax = b;
+        const uint32_t want = sc->n_unique;
+        if (want && c + sc->ndrop != want) atomicOr(&sc->err, ERR_DUP_SLOT);
     }
 }
 
 __global__ __launch_bounds__(1024) void k_keygen_reduce(const float *__restrict__ blk, uint32_t nb,
                                                         TickScalars *sc) {
-    keygen_fold(blk, nb, sc);
-    unique_check<1024>(blk, nb, sc);
+    keygen_fold_t<1024>(blk, nb, sc);
 }
 
 // ----------------------------------------------------------------- scan ------
@@ -983,33 +974,10 @@ __device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long lo
 __device__ __forceinline__ uint32_t p64(uint32_t i) { return i + (i >> 4); }
 
 // Exclusive scan of the packed (lo = arrivals, hi = departures) cell counts, one
-// tile per block, the tile offsets from k_scan64_agg's totals.  The extra block nb
+// tile per block, the tile offsets from k_scan64_agg's totals.  Block 0 (the tiles are blocks 1..nb)
 // folds keygen's d_rel / bmax partials.
 __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
-    __shared__ float s_m[2][SC_T / WAVE];
-    float a = 0.0f, b = 0.0f;
-    for (uint32_t i = threadIdx.x; i < nb; i += SC_T) {
-        a = fmaxf(a, blk[2 * i]);
-        b = fmaxf(b, blk[2 * i + 1]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        a = fmaxf(a, __shfl_xor(a, o));
-        b = fmaxf(b, __shfl_xor(b, o));
-    }
-    if (lane() == 0) {
-        s_m[0][threadIdx.x / WAVE] = a;
-        s_m[1][threadIdx.x / WAVE] = b;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int q = 1; q < SC_T / WAVE; ++q) {
-            a = fmaxf(a, s_m[0][q]);
-            b = fmaxf(b, s_m[1][q]);
-        }
-        sc->d_rel = a;
-        sc->bmax = b;
-    }
+    keygen_fold_t<SC_T>(blk, nb, sc);
 }
 
 // The counts are not cleared here: k_arrive zeroes the two cells of every entity that changed
@@ -1044,12 +1012,11 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
                                                     const uint32_t *__restrict__ p_cs, uint32_t *shift,
                                                     uint32_t *list, unsigned long long *tcnt) {
-    const uint32_t b = blockIdx.x;
-    if (b == nb) {
+    if (blockIdx.x == 0) {  // first, so that its serial loop overlaps the tiles
         keygen_fold256(blk, nbk, sc);
-        unique_check<SC_T>(blk, nbk, sc);
         return;
     }
+    const uint32_t b = blockIdx.x - 1;
     __shared__ unsigned long long tile[S64_TILE + S64_TILE / 16];
     __shared__ unsigned long long ws[SC_T / WAVE];
     const size_t base = (size_t)b * S64_TILE;
