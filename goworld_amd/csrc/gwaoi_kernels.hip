@@ -2580,12 +2580,15 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
                                                 uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
                                                 uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt) {
-    const uint32_t b = blockIdx.x, R = gridDim.x - 1 - (tile_order ? N_XCD : 0u);
-    if (b > R) {
-        tile_order_block(b - R - 1, tile_work, n_tiles, tile_order);
+    // blocks [0, nx): the next flush's tile order; block nx: the summary; then R copy blocks.  The
+    // two serial kinds go first so that they overlap the copies instead of trailing them.
+    const uint32_t nx = tile_order ? N_XCD : 0u, R = gridDim.x - 1 - nx;
+    if (blockIdx.x < nx) {
+        tile_order_block(blockIdx.x, tile_work, n_tiles, tile_order);
         return;
     }
-    if (b == R) {  // scalars + bbox fold (level 2 of the per-space bounding box)
+    const uint32_t b = blockIdx.x - nx - 1;
+    if (blockIdx.x == nx) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         if (threadIdx.x == 0) {
             res->err = sc->err;
             // the scratch extent the pair passes needed (each stream's last chunk), against the capacity
