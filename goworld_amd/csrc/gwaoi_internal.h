@@ -100,7 +100,8 @@ struct TickScalars {
     uint32_t ncoll;              // slots moved more than once in this flush (k_moves_apply_n)
     uint32_t n_unique;           // unique-moves flush: its ops (keygen's written entries + ndrop must match; 0 = no check)
     uint32_t dbg[4];             // path counters of this flush (DBG_*), copied to TickOut
-    uint32_t pad3[18];
+    uint32_t err_apply;          // unique-moves apply's ERR_* bits (folded into err by the keygen fold, which resets it)
+    uint32_t pad3[17];
     // One 128-B line per XCD shard q (zeroed by the prologue): [q][2..3] = the u64 length of
     // event stream q (the pair passes' event allocator: ev_phys).  Sharded because one device-scope atomic word saturates
     // at ~88 returning atomics per us (MI355X_MICROARCH.md, dequeue).
@@ -231,10 +232,23 @@ void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, siz
 // (high word; arrival = cell differs from p_key[i], or i >= n_prev).
 // S' entries i < n_prev whose seq is below seq_base (not written by this flush's
 // ops) take the previous frame's record, written back into s_rec (see launch_moves).
+// The prologue's per-flush zeroing, done by keygen instead when a unique-moves flush skips the
+// prologue (its apply writes only sc->err_apply / sc->ndrop, which the keygen fold reads and
+// resets, so they are zero when any flush begins): sc's counters, z1[0, n1), the bbox fold
+// identity of n_spaces spaces, and sc->n_unique = n_unique.  sc == nullptr: nothing (the prologue ran).
+struct TickZero {
+    TickScalars *sc;
+    uint32_t *z1;
+    uint32_t n1;
+    int4 *bbox;
+    uint32_t n_spaces;
+    uint32_t n_unique;
+};
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st);
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const TickZero &tz,
+                   hipStream_t st);
 // special (optional, cdiv(n_prev, TILE_A) words): keygen marks the previous-frame tiles that hold an
 // entity the special pass must look at; launch_pairs skips the others.
 // The stable sort of S' by key when the grid is the previous frame's: the

@@ -67,6 +67,7 @@ __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t 
         sc->seq_max = 0;
         sc->ncoll = 0;
         sc->ndrop = 0;
+        sc->err_apply = 0;
         sc->n_unique = n_unique;
         for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
     }
@@ -157,19 +158,19 @@ __device__ __forceinline__ uint4 slot_info(const SlotInfo *info, uint32_t s) {
 __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32_t j, const uint4 &si,
                                                            SlotInfo *info, uint32_t tick, uint32_t n_total,
                                                            unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss,
-                                                           TickScalars *sc, bool check_claim) {
+                                                           TickScalars *sc, bool check_claim, uint32_t *errw) {
     const uint32_t s = o.slot;
     if (check_claim && (((unsigned long long)si.y << 32) | si.x) != (((unsigned long long)tick << 32) | j)) return 0;
     const uint32_t idx = si.z, cur_sp = si.w;
     if (idx >= n_total) {
-        atomicOr(&sc->err, ERR_MOVE_DEAD);
+        atomicOr(errw, ERR_MOVE_DEAD);
         return 0;
     }
     uint32_t sp = o.sp;
     Rec16 r;
     r.s = o.seq;
     if (r.s < seq_floor) {  // explicit seq older than an earlier flush: the closed form would be wrong
-        atomicOr(&sc->err, ERR_SEQ);
+        atomicOr(errw, ERR_SEQ);
         return 0;
     }
     if (sp == SP_DEAD) {  // Leave: the slot drops out of the next frame
@@ -183,20 +184,20 @@ __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32
     if (keep) {  // device-side Moved
         sp = cur_sp;
         if (sp == SP_DEAD) {
-            atomicOr(&sc->err, ERR_MOVE_DEAD);
+            atomicOr(errw, ERR_MOVE_DEAD);
             return 0;
         }
     }
     r.x = o.x;
     r.z = o.z;
     if (!isfinite(r.x) || !isfinite(r.z)) {
-        atomicOr(&sc->err, ERR_NONFINITE);
+        atomicOr(errw, ERR_NONFINITE);
         return 0;
     }
     st_rec(s_rec, idx, r);
     if (!keep && sp != cur_sp) {
         if (s_ss) st_ss(s_ss, idx, s, sp);
-        else atomicOr(&sc->err, ERR_COUNT_MISMATCH);  // moves-only flush (S' spaces = previous frame): bug guard
+        else atomicOr(errw, ERR_COUNT_MISMATCH);  // moves-only flush (S' spaces = previous frame): bug guard
     }
     return r.s;
 }
@@ -218,7 +219,7 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
         o.seq = seqs ? seqs[i] : seq0 + i;
         if (o.slot < max_slots)
             smax = op_apply_one(o, j0 + i, slot_info(info, o.slot), info, tick, n_total, seq_floor, s_rec, s_ss, sc,
-                                true);
+                                true, &sc->err);
     }
     if (track_max) {  // one atomic per wave, not per op
         for (int o = 32; o > 0; o >>= 1) {
@@ -268,6 +269,7 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
         si[u] = o[u].slot < max_slots ? slot_info(info, o[u].slot) : make_uint4(0, 0, 0, 0);
     unsigned long long smax = 0;
     uint32_t drop = 0;
+    uint32_t *errw = UNIQUE ? &sc->err_apply : &sc->err;  // unique: sc->err is zeroed by keygen, after this
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t i = i0 + (uint32_t)u * 256u;
@@ -278,13 +280,13 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
             continue;
         }
         if (s >= max_slots) {
-            atomicOr(&sc->err, ERR_BAD_SLOT);
+            atomicOr(errw, ERR_BAD_SLOT);
             ++drop;
             continue;
         }
         if (UNIQUE) {
             const unsigned long long q =
-                op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false);
+                op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false, errw);
             if (!q) ++drop;
             smax = q > smax ? q : smax;
             continue;
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
         const unsigned long long seen = ((unsigned long long)si[u].y << 32) | si[u].x;
         if (seen == mine) {
             const unsigned long long q =
-                op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false);
+                op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false, errw);
             smax = q > smax ? q : smax;
         } else {
             atomicMax(&info[s].lastop, mine);
@@ -328,7 +330,7 @@ __device__ __forceinline__ void moves_fixup(const FixupArgs &F, uint32_t t0, uin
         // start from the previous state so that a dropped (invalid) winner leaves it unchanged
         if (si.z < F.n_prev) st_rec(F.s_rec, si.z, ld_rec(F.p_rec, si.z));
         const OpIn o = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, j - R.j0);
-        op_apply_one(o, j, si, F.info, F.tick, F.n_total, F.seq_floor, F.s_rec, F.s_ss, F.sc, true);
+        op_apply_one(o, j, si, F.info, F.tick, F.n_total, F.seq_floor, F.s_rec, F.s_ss, F.sc, true, &F.sc->err);
     }
 }
 
@@ -387,9 +389,28 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
-                                                unsigned long long seq_base, uint32_t *special) {
+                                                unsigned long long seq_base, uint32_t *special, TickZero tz) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tz.sc) {  // the prologue's zeroing (a unique-moves flush without one; see TickZero)
+        const uint32_t m = max(max(tz.n1, tz.n_spaces), EV_SHARDS * 32u), stride = gridDim.x * blockDim.x;
+        for (uint32_t j = i; j < m; j += stride) {
+            if (j < tz.n1) tz.z1[j] = 0;
+            if (j < tz.n_spaces) tz.bbox[j] = make_int4(INT_MAX, INT_MAX, INT_MIN, INT_MIN);
+            if (j < EV_SHARDS * 32) (&tz.sc->shard[0][0])[j] = 0;
+        }
+        if (i == 0) {
+            TickScalars *sc = tz.sc;
+            sc->err = 0;
+            sc->counter = 0;
+            sc->d_rel = 0.0f;
+            sc->bmax = 0.0f;
+            sc->seq_max = 0;
+            sc->ncoll = 0;
+            sc->n_unique = tz.n_unique;
+            for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
+        }
+    }
     float dr = 0.0f, bm = 0.0f;
     uint32_t key = sentinel;
     bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
@@ -496,8 +517,12 @@ __device__ __forceinline__ void keygen_fold_t(const float *__restrict__ blk, uin
         }
         sc->d_rel = a;
         sc->bmax = b;
-        const uint32_t want = sc->n_unique;
-        if (want && c + sc->ndrop != want) atomicOr(&sc->err, ERR_DUP_SLOT);
+        const uint32_t want = sc->n_unique, ea = sc->err_apply, nd = sc->ndrop;
+        uint32_t e = ea;
+        if (want && c + nd != want) e |= ERR_DUP_SLOT;
+        if (e) atomicOr(&sc->err, e);
+        if (ea) sc->err_apply = 0;  // zero again for the next flush of this set (one without a prologue)
+        if (nd) sc->ndrop = 0;
     }
 }
 
@@ -758,7 +783,7 @@ __global__ __launch_bounds__(MV_T) void k_mv_apply(MoveRuns RS, const uint32_t *
         o.sp = R.dsp ? R.dsp[k] : R.sp_def;
         o.seq = R.dseq ? R.dseq[k] : R.seq0 + k;
         const unsigned long long q =
-            op_apply_one(o, m.j, slot_info(info, m.slot), info, 0u, n_total, seq_floor, s_rec, s_ss, sc, false);
+            op_apply_one(o, m.j, slot_info(info, m.slot), info, 0u, n_total, seq_floor, s_rec, s_ss, sc, false, &sc->err);
         smax = q > smax ? q : smax;
     }
     if (track_max) {  // one atomic per wave
@@ -2978,15 +3003,16 @@ void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, con
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
-                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, hipStream_t st) {
-    if (!n_total) return;  // the prologue left d_rel = bmax = 0
+                   unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const TickZero &tz,
+                   hipStream_t st) {
+    if (!n_total) return;  // the prologue left d_rel = bmax = 0 (a flush without one has moves: n_total > 0)
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64, seq_base, special);  // folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base, special, tz);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr, seq_base, special);
+                                            n_prev, blk, nullptr, nullptr, seq_base, special, tz);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }

@@ -317,6 +317,7 @@ struct gwaoi_world {
     bool batch_ready = false;
     // GWAOI_F_UNIQUE_MOVES: the Moved batches of one flush never repeat a slot (no claims, no fixup)
     bool unique_moves = false;
+    bool skip_prologue = true;  // ... and on the previous grid without the prologue launch (GWAOI_SKIP_PROLOGUE=0: A/B)
     hipStream_t mark_st = nullptr;
     hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
     bool apply_ev_valid = false;
@@ -969,7 +970,17 @@ int tick_launch(gwaoi_world *w) {
     const uint32_t n_unique = uniq ? (uint32_t)n_ops : 0u;
     w->premark.on = false;
     const uint32_t n_copy = virt ? 0u : n_prev;
-    if (incr)
+    // a unique-moves flush on the previous grid has no prologue: its apply writes only
+    // sc->err_apply / ndrop (zero whenever a flush begins) and keygen does the zeroing (TickZero)
+    gw::TickZero tz{};
+    if (uniq && incr && w->skip_prologue) {
+        tz.sc = S.sc;
+        tz.z1 = w->tile_total;
+        tz.n1 = (uint32_t)gw::tile_total_elems(entries);
+        tz.bbox = dev_bbox(S);
+        tz.n_spaces = w->n_space_ids;
+        tz.n_unique = n_unique;
+    } else if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
                             gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
                             gw::tile_total_elems(entries), dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
@@ -1051,7 +1062,7 @@ int tick_launch(gwaoi_world *w) {
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
     gw::launch_keygen(S.srec, s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, st);
+                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, tz, st);
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;
@@ -1588,6 +1599,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (const char *e = std::getenv("GWAOI_PREMARK_LATE")) w->premark_late = e[0] == '1';
     w->unique_moves = (cfg->flags & GWAOI_F_UNIQUE_MOVES) != 0;
     if (const char *e = std::getenv("GWAOI_UNIQUE_MOVES")) w->unique_moves = w->unique_moves && e[0] != '0';  // A/B
+    if (const char *e = std::getenv("GWAOI_SKIP_PROLOGUE")) w->skip_prologue = e[0] != '0';  // A/B
     if (w->batch_ready && (hipStreamCreateWithFlags(&w->mark_st, hipStreamNonBlocking) != hipSuccess ||
                            hipEventCreateWithFlags(&w->apply_ev, hipEventDisableTiming) != hipSuccess ||
                            hipEventCreateWithFlags(&w->mark_ev, hipEventDisableTiming) != hipSuccess))
@@ -1608,6 +1620,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
             return fail(rc);
         // S' records seq 0 (virtual S': never "written")
         if (hipMemset(S.srec, 0, N * sizeof(gw::Rec16)) != hipSuccess) return fail(GWAOI_EDEVICE);
+        // err_apply / ndrop are zero whenever a flush begins (a flush without a prologue relies on it)
+        if (hipMemset(S.sc, 0, sizeof(gw::TickScalars)) != hipSuccess) return fail(GWAOI_EDEVICE);
         // k_finish writes the summary here while the host polls done_ev: coherent (uncached, system
         // scope) memory, so that the writes are visible once the event is seen whatever the runtime's
         // default coherence of pinned allocations

@@ -95,26 +95,43 @@ def test_unique_moves_match_claims_and_oracle_gpu(spec):
 def test_unique_moves_repeated_slot_is_reported_gpu():
     """A flagged world given a batch that moves one slot twice: the flush commits, returns
     GWAOI_ESTATE (ERR_DUP_SLOT, found by keygen's written-entry count), and the slot holds one of
-    its two positions.  The next unique tick brings the world back in step with a claims world."""
+    its two positions.  A later batch that moves a slot that is not live: GWAOI_ESTATE (move
+    dropped, no DUP: the dropped op is counted).  The flushes after each error report nothing
+    (the apply's error word and drop count are reset for the next flush without a prologue), and a
+    unique tick that moves every entity brings the world back in step with a claims world.  Three
+    clean ticks first, so that the bad batches meet the steady flush (previous grid, no prologue)."""
     torch = pytest.importorskip("torch")
-    n = 5000
+    n, warm = 5000, 3
     wa = make_workload("cfg2", n=n)
     slots, x0, z0, _ = wa.initial()
-    sl0, nx0, nz0 = wa.tick(0)
+    clean = [wa.tick(t) for t in range(warm)]
+    sl0, nx0, nz0 = wa.tick(warm)
     # one slot moved twice: an extra move appended after its regular one
     v = int(sl0[17])
     sl = np.concatenate([sl0, [v]]).astype(np.uint32)
-    nx = np.concatenate([nx0, [np.float32(x0[v] + 3.0)]]).astype(np.float32)
-    nz = np.concatenate([nz0, [np.float32(z0[v] - 2.0)]]).astype(np.float32)
-    sl1, nx1, nz1 = wa.tick(1)
-    d0 = [torch.from_numpy(a).to("cuda:0") for a in (sl.astype(np.int32), nx, nz)]
-    d1 = [torch.from_numpy(a).to("cuda:0") for a in (sl1.astype(np.int32), nx1, nz1)]
+    nx = np.concatenate([nx0, [np.float32(nx0[17] + 3.0)]]).astype(np.float32)
+    nz = np.concatenate([nz0, [np.float32(nz0[17] - 2.0)]]).astype(np.float32)
+    after = [wa.tick(warm + 1 + t) for t in range(3)]
+    # a batch naming slot n (never entered) besides the regular moves
+    sl2, nx2, nz2 = after[1]
+    bad = (np.concatenate([sl2, [n]]).astype(np.uint32), np.concatenate([nx2, [np.float32(1.0)]]),
+           np.concatenate([nz2, [np.float32(2.0)]]))
+
+    def dev(b):
+        return [torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0") for a in (b[0].astype(np.int32), b[1], b[2])]
+
+    d_clean = [dev(b) for b in clean]
+    d0 = dev((sl, nx, nz))
+    d_after = [dev(after[0]), dev(bad), dev(after[2])]
     torch.cuda.synchronize()
     with World(n + 1, unique_moves=True) as A, World(n + 1) as B:
         for w in (A, B):
             s = w.space_create(wa.D)
             w.enter_batch(s, slots, x0, z0)
             w.tick()
+            for b, h in zip(d_clean, clean):
+                w.moved_batch_device(*(t.data_ptr() for t in b), h[0].size)
+                w.tick_device()
         A.moved_batch_device(*(b.data_ptr() for b in d0), sl.size)
         with pytest.raises(GwaoiError) as ei:
             A.tick_device()
@@ -129,10 +146,19 @@ def test_unique_moves_repeated_slot_is_reported_gpu():
         assert (float(xa[v][0]), float(xa[v][1])) in cand
         others = np.arange(n) != v
         np.testing.assert_array_equal(xa[others], xb[others])
-        # a unique tick that moves every entity: both worlds hold the same state again
+        # a clean unique tick (no stale error), then the dead-slot batch, then a clean one
         for w in (A, B):
-            w.moved_batch_device(*(b.data_ptr() for b in d1), sl1.size)
+            w.moved_batch_device(*(b.data_ptr() for b in d_after[0]), after[0][0].size)
+            w.tick_device()
+        for w in (A, B):
+            w.moved_batch_device(*(b.data_ptr() for b in d_after[1]), bad[0].size)
+            with pytest.raises(GwaoiError) as ei:
+                w.tick_device()
+            assert ei.value.code == ESTATE and "not live" in str(ei.value), str(ei.value)
+        for w in (A, B):
+            w.moved_batch_device(*(b.data_ptr() for b in d_after[2]), after[2][0].size)
             w.tick_device()
         np.testing.assert_array_equal(_positions(A, n), _positions(B, n))
         for i in range(0, n, 97):
             np.testing.assert_array_equal(np.sort(A.neighbors(i)), np.sort(B.neighbors(i)))
+        assert A.debug_counters()["unique_flushes"] == warm + 4

@@ -2,7 +2,8 @@
 """Median per-kernel duration over the steady cfg3 ticks of a rocprofv3 kernel trace.
 
     python tools/tick_kernels.py run_kernel_trace.csv [label]
-A tick starts at k_prologue; the first 3 ticks and the stage-timed tail are skipped.
+A tick starts at k_prologue, or at the apply when no prologue precedes it (a unique-moves flush
+on the previous grid); the first 3 ticks and the stage-timed tail are skipped.
 """
 import csv
 import re
@@ -17,12 +18,13 @@ def short(n):
 
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-    ticks, cur = [], None
+    ticks, cur, prev = [], None, None
     for r in rows:
         k = short(r["Kernel_Name"])
-        if k == "k_prologue":
+        if k == "k_prologue" or (k.startswith("k_moves_apply_n") and prev != "k_prologue"):
             cur = []
             ticks.append(cur)
+        prev = k
         if cur is not None:
             cur.append((k, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     steady = ticks[3:-12] if len(ticks) > 16 else ticks[1:]
