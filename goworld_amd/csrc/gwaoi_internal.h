@@ -260,11 +260,27 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 size_t incr_sort_tmp_elems(size_t cells);
 // true: the sort leaves cnt64 zero for the next flush (zeroed once when allocated)
 bool scan_rezeroes_counts();
+// The special pass (launch_pairs' arguments), run inside the incremental sort's arrival launch
+// (k_arrive_special) when sp != nullptr; n_tiles = the previous frame's tiles.
+struct SpecialJob {
+    FrameView F;
+    const Rec16 *O_rec;
+    const SlotSp *O_ss;
+    unsigned long long seq_base;
+    TickScalars *sc;
+    uint2 *tmp;
+    uint64_t cap;
+    uint32_t *tile_total;
+    unsigned long long *tile_base;
+    uint32_t tile_off, leave_off;
+    const uint32_t *special;
+    uint32_t n_tiles;
+};
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, hipStream_t st);
+                      TickScalars *sc, const SpecialJob *sp, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {

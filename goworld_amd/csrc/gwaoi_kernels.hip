@@ -1112,11 +1112,10 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
 // zeroes the counts of both its cells (k_scan64 has read them).  A stayer
 // of an unchanged cell (no arrival, no departure) keeps its rank in the run,
 // so its frame position is its S' index plus the cell's shift.
-__global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
+__device__ __forceinline__ void arrive_one(const uint32_t i, const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
                          const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
                          unsigned long long *cnt64, const uint32_t *__restrict__ shift, uint32_t *perm,
                          uint32_t *skeys) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t key = keys[i];
     const uint32_t old = i < n_prev ? p_key[i] : sentinel;
@@ -1133,6 +1132,13 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
     if (key == sentinel) return;
     cnt64[key] = 0ull;
     arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
+}
+
+__global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
+                         const uint32_t *__restrict__ p_key, uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
+                         unsigned long long *cnt64, const uint32_t *__restrict__ shift, uint32_t *perm,
+                         uint32_t *skeys) {
+    arrive_one(blockIdx.x * blockDim.x + threadIdx.x, keys, n, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64, shift, perm, skeys);
 }
 
 // One lane per changed cell c (k_scan64 lists them per scan tile; k_arrive placed the
@@ -1483,12 +1489,11 @@ __device__ void enum_global(const FrameView &F, const Rec16 *O_rec, const SlotSp
 }
 
 template <int MODE>
-__global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restrict__ O_rec,
-                                              const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
-                                              TickScalars *scw, uint2 *tmp, uint64_t cap,
-                                              uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
-                                              uint32_t leave_off, uint32_t *dbg, const uint32_t *__restrict__ special) {
-    if (MODE == 1 && special && !special[blockIdx.x]) return;  // keygen saw no special entity in this tile
+__device__ __forceinline__ void pairs_tile(const uint32_t t, FrameView F, const Rec16 *__restrict__ O_rec,
+                           const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
+                           TickScalars *scw, uint2 *tmp, uint64_t cap,
+                           uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
+                           uint32_t leave_off, uint32_t *dbg) {
     __shared__ uint4 s_now[PCAP];
     __shared__ uint4 s_oth[PCAP];
     __shared__ uint32_t s_slot[PCAP];
@@ -1501,7 +1506,7 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
 
     __shared__ uint32_t s_spr[2];  // smallest / largest space among the active lanes
     __shared__ uint32_t s_nglob;   // lanes taking the global write path (DBG_SPECIAL_GLOBAL)
-    const uint32_t t = blockIdx.x;  // entries [t*PT, t*PT + PT) of the frame
+    // tile t: entries [t*PT, t*PT + PT) of the frame
     const uint32_t tid = threadIdx.x;
     PairCtx A;
     A.seq_base = seq_base;
@@ -1690,6 +1695,37 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
     }
     __syncthreads();
     if (tid == 0 && s_nglob) atomicAdd(dbg + DBG_SPECIAL_GLOBAL, s_nglob);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restrict__ O_rec,
+                                              const SlotSp *__restrict__ O_ss, unsigned long long seq_base, const TickScalars *__restrict__ sc,
+                                              TickScalars *scw, uint2 *tmp, uint64_t cap,
+                                              uint32_t *tile_total, unsigned long long *tile_base, uint32_t tile_off,
+                                              uint32_t leave_off, uint32_t *dbg, const uint32_t *__restrict__ special) {
+    if (MODE == 1 && special && !special[blockIdx.x]) return;  // keygen saw no special entity in this tile
+    pairs_tile<MODE>(blockIdx.x, F, O_rec, O_ss, seq_base, sc, scw, tmp, cap, tile_total, tile_base, tile_off,
+                     leave_off, dbg);
+}
+
+// k_arrive with the special pass in front (the steady incremental flush): workgroup t < n_tiles is
+// the special pass's tile t (it leaves at once unless keygen flagged the tile), the rest run k_arrive.  The special pass needs only keygen and its fold (k_scan64), so it
+// rides on this launch instead of one of its own: a launch costs ~4.5 us on this chip however
+// little it does, and a steady config-3 flush flags no tile.  Same tiles, same events, same
+// per-tile totals as k_pairs<1>; an overflow re-run still launches k_pairs<1>.
+__global__ __launch_bounds__(PT) void k_arrive_special(SpecialJob J, const uint32_t *__restrict__ keys, uint32_t n,
+                                                       uint32_t n_prev, const uint32_t *__restrict__ p_key,
+                                                       uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
+                                                       unsigned long long *cnt64, const uint32_t *__restrict__ shift,
+                                                       uint32_t *perm, uint32_t *skeys) {
+    if (blockIdx.x >= J.n_tiles) {
+        arrive_one((blockIdx.x - J.n_tiles) * PT + threadIdx.x, keys, n, n_prev, p_key, sentinel, arr_pos, arr_idx,
+                   cnt64, shift, perm, skeys);
+        return;
+    }
+    if (!J.special[blockIdx.x]) return;  // keygen saw no special entity in this tile
+    pairs_tile<1>(blockIdx.x, J.F, J.O_rec, J.O_ss, J.seq_base, J.sc, J.sc, J.tmp, J.cap, J.tile_total, J.tile_base,
+                  J.tile_off, J.leave_off, J.sc->dbg);
 }
 
 // ------------------------------------------------------- combined pass ------
@@ -3026,7 +3062,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, hipStream_t st) {
+                      TickScalars *sc, const SpecialJob *sp, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
     uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 3 (total_cells + 1) words
@@ -3035,9 +3071,14 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
     k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
     k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
                                       cdiv(n_total, 256), sc, p_cell_start, shift, list, tcnt);
-    if (n_total)
+    if (sp && sp->n_tiles) {
+        const SpecialJob &J = *sp;
+        k_arrive_special<<<J.n_tiles + cdiv(n_total, PT), PT, 0, st>>>(J, keys, n_total, n_prev, p_key, sentinel, arr_pos,
+                                                                 arr_idx, cnt64, shift, perm, skeys);
+    } else if (n_total) {
         k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
                                                      shift, perm, skeys);
+    }
     k_cell_merge<<<nb, 256, 0, st>>>(
         p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_total, sentinel, perm, skeys, list, tcnt);
 }

@@ -317,7 +317,8 @@ struct gwaoi_world {
     bool batch_ready = false;
     // GWAOI_F_UNIQUE_MOVES: the Moved batches of one flush never repeat a slot (no claims, no fixup)
     bool unique_moves = false;
-    bool skip_prologue = true;  // ... and on the previous grid without the prologue launch (GWAOI_SKIP_PROLOGUE=0: A/B)
+    bool skip_prologue = true;
+    bool special_fused = true;  // the special pass inside k_arrive_special (GWAOI_SPECIAL_FUSED=0: A/B)  // ... and on the previous grid without the prologue launch (GWAOI_SKIP_PROLOGUE=0: A/B)
     hipStream_t mark_st = nullptr;
     hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
     bool apply_ev_valid = false;
@@ -815,7 +816,7 @@ uint32_t *last_events(gwaoi_world *w) { return w->fs[w->last_set].events; }
 // work) for the flush after it, so a re-run neither reads nor writes them, and keygen's special-tile
 // flags may be the successor's too, so every tile is visited.
 uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
-                            const gw::SlotSp *s_ss_view, bool rerun = false) {
+                            const gw::SlotSp *s_ss_view, bool rerun = false, bool special_done = false) {
     hipStream_t st = w->stream;
     const uint32_t TBn = gw::combined_tiles(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
@@ -828,7 +829,7 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
     const bool order = w->tile_order_on && !rerun;
     // The special pass needs nothing of the combined pass: it runs beside it on a side stream (in
     // the combined pass's tail, whose CUs empty as its last tiles drain), unless it is timed.
-    const bool side = w->special_side && !(w->timing_mask >> ST_SPECIAL & 1u);
+    const bool side = w->special_side && !(w->timing_mask >> ST_SPECIAL & 1u) && !special_done;
     if (side) {
         HIP_TRY(hipEventRecord(w->side_fork, st));
         HIP_TRY(hipStreamWaitEvent(w->side_st, w->side_fork, 0));
@@ -842,7 +843,7 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
     if (side) {
         HIP_TRY(hipStreamWaitEvent(st, w->side_join, 0));
-    } else {
+    } else if (!special_done) {  // (special_done: it ran in the sort's arrival launch)
         stage_begin(w, S, ST_SPECIAL);
         gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn,
                          half, rerun ? nullptr : w->special, st);
@@ -1066,11 +1067,32 @@ int tick_launch(gwaoi_world *w) {
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;
+    // the special pass rides on the sort's arrival launch (k_arrive_special) unless it is timed or
+    // runs on the side stream (A/Bs); launch_pair_passes then skips its own launch
+    const bool sp_fused = incr && w->special_fused && !w->special_side && !(w->timing_mask >> ST_SPECIAL & 1u) &&
+                          n_prev > 0;
+    gw::SpecialJob spj{};
+    if (sp_fused) {
+        const uint32_t TBn = gw::combined_tiles(n_new), TBp = gw::combined_blocks(n_prev);
+        spj.F = view_of(P);
+        spj.O_rec = S.srec;
+        spj.O_ss = s_ss_view;
+        spj.seq_base = seq_base;
+        spj.sc = S.sc;
+        spj.tmp = reinterpret_cast<uint2 *>(w->events_tmp);
+        spj.cap = std::min(S.ev_cap, w->evtmp_cap);
+        spj.tile_total = w->tile_total;
+        spj.tile_base = w->tile_base;
+        spj.tile_off = TBn;
+        spj.leave_off = TBn + TBp;
+        spj.special = w->special;
+        spj.n_tiles = TBp;
+    }
     if (incr) {
         w->dbg.incremental_sorts++;
         gw::incremental_sort(w->keys[0], n_total, n_prev, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             Fn.key, w->blk, S.sc, st);  // the sorted keys ARE the frame's
+                             Fn.key, w->blk, S.sc, sp_fused ? &spj : nullptr, st);  // the sorted keys ARE the frame's
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -1108,7 +1130,7 @@ int tick_launch(gwaoi_world *w) {
         w->apply_ev_valid = true;
     }
     // ---- pair passes: combined over the new grid, special entities over the previous one
-    const uint64_t ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view);
+    const uint64_t ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view, false, sp_fused);
 
     // from here on the device has rewritten SlotInfo for the new frame: any failure before the
     // commit below leaves the world inconsistent (poisoned)
@@ -1600,6 +1622,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->unique_moves = (cfg->flags & GWAOI_F_UNIQUE_MOVES) != 0;
     if (const char *e = std::getenv("GWAOI_UNIQUE_MOVES")) w->unique_moves = w->unique_moves && e[0] != '0';  // A/B
     if (const char *e = std::getenv("GWAOI_SKIP_PROLOGUE")) w->skip_prologue = e[0] != '0';  // A/B
+    if (const char *e = std::getenv("GWAOI_SPECIAL_FUSED")) w->special_fused = e[0] != '0';  // A/B
     if (w->batch_ready && (hipStreamCreateWithFlags(&w->mark_st, hipStreamNonBlocking) != hipSuccess ||
                            hipEventCreateWithFlags(&w->apply_ev, hipEventDisableTiming) != hipSuccess ||
                            hipEventCreateWithFlags(&w->mark_ev, hipEventDisableTiming) != hipSuccess))
