@@ -415,15 +415,24 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     uint32_t key = sentinel;
     bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
     bool written = false;
+    uint32_t old = sentinel;  // the previous frame's key (INCR)
     if (i < n) {
+        // every operand of the entry in one round trip (none depends on another): the S' record and
+        // space, the previous frame's record, space and key (round 4 loaded them in three steps)
+        const bool inp = i < n_prev;
         const uint32_t s = ld_ss(s_ss, i).sp;
+        Rec16 r = ld_rec(s_rec, i);
+        const uint32_t ps = inp ? ld_ss(p_ss, i).sp : SP_DEAD;
+        Rec16 p;
+        p.x = p.z = 0.0f;
+        p.s = 0;
+        if (inp) p = ld_rec(p_rec, i);
+        if (INCR && inp) old = p_key[i];
         if (s != SP_DEAD) {
-            Rec16 r = ld_rec(s_rec, i);
             written = r.s >= seq_base;
-            const bool same = i < n_prev && ld_ss(p_ss, i).sp == s;
-            if (same || (i < n_prev && r.s < seq_base)) {
-                const Rec16 p = ld_rec(p_rec, i);
-                if (r.s < seq_base && i < n_prev) {  // not written by this flush's ops: the previous state
+            const bool same = inp && ps == s;
+            if (same || (inp && r.s < seq_base)) {
+                if (r.s < seq_base && inp) {  // not written by this flush's ops: the previous state
                     if (r.x != p.x || r.z != p.z || r.s != p.s) st_rec(s_rec, i, p);  // (virtual S': no prologue copy)
                     r = p;
                 }
@@ -447,7 +456,6 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         // departure from the old one (high word); a cell's stayers are its previous count minus
         // its departures, which k_scan64 takes from the previous cell_start
         if (i < n) {
-            const uint32_t old = i < n_prev ? p_key[i] : sentinel;
             if (key != old) {
                 if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
                 if (old != sentinel) atomicAdd(&cnt64[old], 1ull << 32);
@@ -1354,8 +1362,16 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
         cand[k] = make_uint4(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u);
         return;
     }
+    // S' and previous-frame operands of entry i in one round trip (the previous record is loaded
+    // before its space is compared, not after)
     const SlotSp ss = ld_ss(s_ss, i);
     const Rec16 now = ld_rec(s_rec, i);
+    const bool inp = i < n_prev;
+    const uint32_t psp = inp ? ld_ss(p_ss, i).sp : SP_DEAD;
+    Rec16 pr;
+    pr.x = pr.z = 0.0f;
+    pr.s = 0;
+    if (inp) pr = ld_rec(p_rec, i);
     st_rec(f_rec, k, now);
     reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(ss.slot, ss.sp);
     reinterpret_cast<uint2 *>(info + ss.slot)[1] = make_uint2(k, ss.sp);
@@ -1363,7 +1379,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     Rec16 o;
     o.x = o.z = qnan();
     o.s = 0;
-    if (i < n_prev && ld_ss(p_ss, i).sp == ss.sp) o = ld_rec(p_rec, i);
+    if (inp && psp == ss.sp) o = pr;
     st_rec(o_rec, k, o);
     const float thr = FAR_FRAC * grid[ss.sp].D;
     const uint4 c = cand_of(now, o, thr);
