@@ -1054,10 +1054,16 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     __shared__ unsigned long long ws[SC_T / WAVE];
     const size_t base = (size_t)b * S64_TILE;
     const uint32_t tid = threadIdx.x;
+    // every global operand first, in one round trip: the tile's counts, the previous starts of its
+    // cells (for the final write) and this thread's share of the earlier tiles' totals
+    unsigned long long pre = 0;
+    for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
+    uint32_t pcs[S64_I];
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {
         const uint32_t j = (uint32_t)q * SC_T + tid;
         tile[p64(j)] = base + j < n ? in[base + j] : 0ull;
+        pcs[q] = base + j < n ? p_cs[base + j] : 0u;
     }
     __syncthreads();
     unsigned long long v[S64_I];
@@ -1084,8 +1090,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     // the tile's offset: the sum of the earlier tiles' totals (k_scan64_agg), no look-back chain:
     // a chain serialises ~500 tiles at ~20 ns a hop, the block-wide sum of <= 1k words does not
     __shared__ unsigned long long s_pre[SC_T / WAVE];
-    unsigned long long pre = 0;
-    for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
     if (lane() == 0) s_pre[tid / WAVE] = pre;
@@ -1108,7 +1112,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
             // e = (departures before c) << 32 | (arrivals before c): cell c starts at its previous
             // start plus the arrivals minus the departures of the cells before it
             const uint32_t arr = (uint32_t)e & ~SHIFT_CHANGED, d = arr - (uint32_t)(e >> 32);
-            lo[base + j] = p_cs[base + j] + d;
+            lo[base + j] = pcs[q] + d;
             hi[base + j] = arr;
             shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
         }
