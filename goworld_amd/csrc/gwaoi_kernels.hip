@@ -1162,10 +1162,12 @@ __device__ __forceinline__ void cell_merge_one(uint32_t c, const uint32_t *__res
                                                const uint32_t *__restrict__ cell_start,
                                                const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                                                uint32_t *arr_idx, uint32_t sentinel, uint32_t *perm, uint32_t *skeys) {
+    // the cell's six bounds in one round trip
     uint32_t o = cell_start[c];
     const uint32_t oe = cell_start[c + 1];
-    if (o == oe) return;
     const uint32_t ab = c ? arr_pos[c - 1] : 0u, ae = arr_pos[c];
+    const uint32_t ps = p_cell_start[c], pe = p_cell_start[c + 1];
+    if (o == oe) return;
     for (uint32_t k = ab + 1; k < ae; ++k) {  // insertion sort of the arrivals
         const uint32_t v = arr_idx[k];
         uint32_t j = k;
@@ -1178,7 +1180,6 @@ __device__ __forceinline__ void cell_merge_one(uint32_t c, const uint32_t *__res
     // An arrival is new to c, so its S' index lies outside c's previous run [ps, pe) (which
     // holds exactly the entries whose previous key is c): the cell's order is the arrivals
     // below ps, the stayers in run order, then the arrivals past pe -- no merge.
-    const uint32_t ps = p_cell_start[c], pe = p_cell_start[c + 1];
     uint32_t a = ab;
     for (; a < ae; ++a) {
         const uint32_t v = arr_idx[a];
@@ -2726,23 +2727,27 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     const uint32_t e0 = b * FT;
     __shared__ uint32_t s_agg;
     uint32_t cnt = 0, incl = 0;
+    unsigned long long src = 0;  // the tile's stream position, loaded with its total (one round trip)
+    // the offset: the totals of the groups before e0's, then its group's entries before e0 (their
+    // loads issued before wave 0's own scan)
+    __shared__ uint32_t s_pw[256 / WAVE];
+    uint32_t gsum = 0;
+    {
+        const uint32_t *grp = tile_total + n_entries + 1, g = e0 / FG;
+        for (uint32_t q = threadIdx.x; q < g; q += blockDim.x) gsum += grp[q];
+        for (uint32_t e = g * FG + threadIdx.x; e < e0; e += blockDim.x) gsum += tile_total[e];
+    }
     if (threadIdx.x < WAVE) {
         const uint32_t l = lane(), e = e0 + l;
-        cnt = l < (uint32_t)FT && e < n_entries ? tile_total[e] : 0u;
+        const bool own = l < (uint32_t)FT && e < n_entries;
+        cnt = own ? tile_total[e] : 0u;
+        src = own ? tile_base[e] : 0ull;
         incl = wave_incl_scan(cnt);
         const uint32_t agg = __shfl(incl, WAVE - 1);
         if (l == 0) s_agg = agg;
     }
-    // the offset: the totals of the groups before e0's, then its group's entries before e0
-    __shared__ uint32_t s_pw[256 / WAVE];
-    {
-        const uint32_t *grp = tile_total + n_entries + 1, g = e0 / FG;
-        uint32_t p = 0;
-        for (uint32_t q = threadIdx.x; q < g; q += blockDim.x) p += grp[q];
-        for (uint32_t e = g * FG + threadIdx.x; e < e0; e += blockDim.x) p += tile_total[e];
-        p = wave_sum_u32(p);
-        if (lane() == 0) s_pw[threadIdx.x / WAVE] = p;
-    }
+    gsum = wave_sum_u32(gsum);
+    if (lane() == 0) s_pw[threadIdx.x / WAVE] = gsum;
     __syncthreads();
     uint32_t excl = 0;
     for (uint32_t q = 0; q < blockDim.x / WAVE; ++q) excl += s_pw[q];
@@ -2752,7 +2757,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         const uint32_t off = excl + incl - cnt;
         if (l < (uint32_t)FT) {
             s_off[l] = off;
-            s_src[l] = e < n_entries ? tile_base[e] : 0ull;
+            s_src[l] = src;
             if (e == n_enter_entries) {
                 res->n_enter = off;
                 if (dcnt) dcnt[0] = off;  // device copy of the counts (events read on the device before the host)
