@@ -145,9 +145,7 @@ struct TickOut {
     uint32_t pad;
     unsigned long long total64;
     unsigned long long seq_max;
-    // the flush's completion signal when its done event was deferred: the tick id, written by the
-    // next flush's first kernel (it starts once this flush's last kernel has ended)
-    unsigned long long done_tick;
+    unsigned long long pad2;
     uint32_t dbg[4];  // TickScalars::dbg
     // followed by int4 bbox[n_spaces] (ordered-int min x, min z, max x, max z)
 };
@@ -205,12 +203,9 @@ struct FixupArgs {
     TickScalars *sc;
     const uint32_t *coll;
 };
-// sig != nullptr (unique only): the first workgroup stores sigv there first (the previous flush's
-// completion signal, TickOut::done_tick in mapped host memory).
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, unsigned long long *sig,
-                  unsigned long long sigv, hipStream_t st);
+                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, hipStream_t st);
 // The same flush through slot buckets (gwaoi_kernels.hip k_mv_*), for worlds whose
 // SlotInfo outgrows the MALL (max_slots > MV_MIN_SLOTS; moves_buckets(max_slots) <=
 // MV_NB_MAX).  hist: moves_hist_elems(n ops, max_slots) uint32; scan_tmp:
@@ -248,7 +243,6 @@ struct TickZero {
     int4 *bbox;
     uint32_t n_spaces;
     uint32_t n_unique;
-    uint32_t *probe;  // probe (GWAOI_PROBE_HOSTWRITE=1): the last block stores 4 B to mapped host memory
 };
 void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const SpaceGrid *grid,
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,

@@ -254,11 +254,7 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint
 template <int PER, bool UNIQUE>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
-                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll,
-                                                       unsigned long long *sig, unsigned long long sigv) {
-    // the previous flush has ended (this launch started after its last kernel): tell the host
-    if (sig && blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(sig, sigv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                                       SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
     const uint32_t i0 = blockIdx.x * (256u * PER) + threadIdx.x;
     OpIn o[PER];
     uint4 si[PER];
@@ -396,8 +392,6 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 unsigned long long seq_base, uint32_t *special, TickZero tz) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tz.probe && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-        __hip_atomic_store(tz.probe, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tz.sc) {  // the prologue's zeroing (a unique-moves flush without one; see TickZero)
         const uint32_t m = max(max(tz.n1, tz.n_spaces), EV_SHARDS * 32u), stride = gridDim.x * blockDim.x;
         for (uint32_t j = i; j < m; j += stride) {
@@ -2987,15 +2981,12 @@ void launch_moves_mark(const MoveRun &R, uint32_t max_slots, SlotInfo *info, uin
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
-                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, unsigned long long *sig,
-                  unsigned long long sigv, hipStream_t st) {
+                  TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, hipStream_t st) {
     if (unique) {  // no claims, no fixup
         for (uint32_t q = 0; q < RS.count; ++q)
-            if (RS.r[q].n) {
+            if (RS.r[q].n)
                 k_moves_apply_n<GWAOI_APPLY_PER, true><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
-                    RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll, sig, sigv);
-                sig = nullptr;
-            }
+                    RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
         return;
     }
     for (uint32_t q = n_marked; q < RS.count; ++q)  // every run's claims before any apply
@@ -3003,7 +2994,7 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32
     for (uint32_t q = 0; q < RS.count; ++q)
         if (RS.r[q].n)
             k_moves_apply_n<GWAOI_APPLY_PER, false><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
-                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll, nullptr, 0ull);
+                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
     {
         FixupArgs F;
         F.RS = RS;

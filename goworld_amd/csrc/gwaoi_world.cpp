@@ -15,7 +15,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <condition_variable>
 #include <functional>
@@ -182,7 +181,6 @@ struct FlushSet {
     char *h_out = nullptr;       // pinned: the flush summary (TickOut + bbox)
     char *d_hout = nullptr;      // h_out as the device sees it: k_finish writes the summary there
     hipEvent_t done_ev = nullptr;  // recorded after the flush's last kernel
-    bool ev_valid = false;         // done_ev marks this set's last flush (not deferred, or recorded late)
     hipEvent_t ev[ST_N][2] = {};   // stage timing
     bool ev_used[ST_N] = {};
 };
@@ -320,10 +318,7 @@ struct gwaoi_world {
     // GWAOI_F_UNIQUE_MOVES: the Moved batches of one flush never repeat a slot (no claims, no fixup)
     bool unique_moves = false;
     bool skip_prologue = true;
-    bool special_fused = true;
-    int extra_markers = 0;
-    bool probe_hostwrite = false;
-    hipEvent_t probe_ev = nullptr;  // the special pass inside k_arrive_special (GWAOI_SPECIAL_FUSED=0: A/B)  // ... and on the previous grid without the prologue launch (GWAOI_SKIP_PROLOGUE=0: A/B)
+    bool special_fused = true;  // the special pass inside k_arrive_special (GWAOI_SPECIAL_FUSED=0: A/B)  // ... and on the previous grid without the prologue launch (GWAOI_SKIP_PROLOGUE=0: A/B)
     hipStream_t mark_st = nullptr;
     hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
     bool apply_ev_valid = false;
@@ -368,18 +363,8 @@ struct gwaoi_world {
         int p_idx, n_idx;   // previous / new frame
         const gw::SlotSp *s_ss_view;  // its S' spaces: the set's sss, or the previous frame's (virtual S')
         uint64_t cap;       // event capacity its pair passes were launched with (writes clipped to it)
-        bool ev_deferred = false;  // no done event after it: the next flush's first kernel signals its end
         std::vector<uint8_t> touched_alive;  // liveness of touched[i] when the queue was closed
     } fl;
-    // Deferred done events (GWAOI_DEFER_DONE=0: A/B).  A marker packet between two flushes costs
-    // ~4.4 us of GPU idle per tick on this chip (profiles/r05_probe_markers.txt), so a speculative
-    // device-mode launch of a unique-moves flush records none; the flush launched after it stores
-    // its tick id into its TickOut::done_tick from its first kernel, and the host polls that.
-    bool defer_done = true;
-    bool spec_ctx = false;                // tick_launch called by a speculative device-mode end_begin
-    unsigned long long *sig_ptr = nullptr;  // ... with the flight before it deferred: where to signal
-    uint32_t sig_tick = 0;
-    bool sig_given = false;               // the launch passed the signal to its apply (for sig_tick)
 
     std::vector<Deferred> deferred;
     std::vector<DeferredBox> deferred_boxes;
@@ -996,7 +981,6 @@ int tick_launch(gwaoi_world *w) {
         tz.bbox = dev_bbox(S);
         tz.n_spaces = w->n_space_ids;
         tz.n_unique = n_unique;
-        if (w->probe_hostwrite) tz.probe = reinterpret_cast<uint32_t *>(S.d_hout) + 3;  // TickOut::pad
     } else if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
                             gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
@@ -1026,10 +1010,8 @@ int tick_launch(gwaoi_world *w) {
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
     } else if (moves_only) {  // one pass + fixup of repeated slots (run 0's claims: prologue or premark)
-        unsigned long long *sig = uniq ? w->sig_ptr : nullptr;
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
-                         P.rec, n_prev, S.sc, w->coll, 1u, uniq, sig, w->sig_tick, st);
-        if (sig) w->sig_given = true;
+                         P.rec, n_prev, S.sc, w->coll, 1u, uniq, st);
     } else if (n_ops) {
         // host runs -> device op buffers; device runs are read in place
         size_t hat = 0;
@@ -1157,17 +1139,10 @@ int tick_launch(gwaoi_world *w) {
         return poison(w, GWAOI_EDEVICE);
     }
     // (k_finish writes the summary straight into pinned host memory: no copy)
-    // a steady speculative device-mode flush bets that the next one signals its end (finish_flight
-    // records the event late when that does not happen)
-    const bool defer = w->defer_done && w->spec_ctx && uniq && !w->blocking_sync;
-    if (!defer && hipEventRecord(S.done_ev, st) != hipSuccess) {
+    if (hipEventRecord(S.done_ev, st) != hipSuccess) {
         w->last_error = "flush done event failed";
         return poison(w, GWAOI_EDEVICE);
     }
-    S.ev_valid = !defer;
-    // probe (GWAOI_EXTRA_MARKERS=k): k more event records after the flush, to price a marker packet
-    // between two flushes in the kernel trace's tick gap
-    for (int q = 0; q < w->extra_markers; ++q) (void)hipEventRecord(w->probe_ev, st);
     // the queue is closed: what the commit needs of it
     w->in_flight = true;
     w->fl.tick_id = tick_id;
@@ -1180,7 +1155,6 @@ int tick_launch(gwaoi_world *w) {
     w->fl.n_idx = n_idx;
     w->fl.s_ss_view = s_ss_view;
     w->fl.cap = ev_cap;
-    w->fl.ev_deferred = defer;
     w->launch_set ^= 1;
     w->fl.touched_alive.resize(w->touched.size());
     for (size_t i = 0; i < w->touched.size(); ++i) w->fl.touched_alive[i] = w->alive[w->touched[i]];
@@ -1199,30 +1173,6 @@ int wait_done(gwaoi_world *w, hipEvent_t ev) {
     hipError_t e;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
     HIP_TRY(e);
-    return GWAOI_OK;
-}
-
-// Wait for a deferred flush's end signal (TickOut::done_tick == tick, stored by the next flush's
-// first kernel).  The stream is queried now and then, so that a device fault or a signal that can
-// no longer come (the stream drained without it) ends the wait with an error instead of a hang.
-int wait_signal(gwaoi_world *w, FlushSet &S, uint32_t tick) {
-    volatile unsigned long long *p = &reinterpret_cast<gw::TickOut *>(S.h_out)->done_tick;
-    for (uint32_t spin = 1;; ++spin) {
-        if (*p == tick) break;
-        if (!(spin & 1023u)) {
-            const hipError_t e = hipStreamQuery(w->stream);
-            if (e != hipErrorNotReady && e != hipSuccess) {
-                w->last_error = std::string("stream: ") + hipGetErrorString(e);
-                return GWAOI_EDEVICE;
-            }
-            if (e == hipSuccess && *p != tick) {
-                w->last_error = "flush end signal missing";
-                return GWAOI_EDEVICE;
-            }
-        }
-        __builtin_ia32_pause();
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
     return GWAOI_OK;
 }
 
@@ -1272,16 +1222,7 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
     FlushSet &S = w->fs[f.set];
     DevFrame &P = w->fr[f.p_idx];
     DevFrame &Fn = w->fr[f.n_idx];
-    int wr;
-    if (!f.ev_deferred) {
-        wr = wait_done(w, S.done_ev);
-    } else if (w->sig_given && w->sig_tick == f.tick_id) {
-        wr = wait_signal(w, S, f.tick_id);  // S.ev_valid stays false: copy_out records its own event
-    } else {  // no flush after it signals: the event goes on the stream now (after whatever followed it)
-        wr = hipEventRecord(S.done_ev, st) == hipSuccess ? wait_done(w, S.done_ev) : GWAOI_EDEVICE;
-        S.ev_valid = wr == GWAOI_OK;
-    }
-    if (wr != GWAOI_OK) {
+    if (wait_done(w, S.done_ev) != GWAOI_OK) {
         w->last_error = "flush did not complete: " + w->last_error;
         if (w->fault_stage)
             w->last_error += std::string(" (first failed stage wait: ") + (w->fault_before ? "before " : "after ") +
@@ -1465,7 +1406,6 @@ int sparse_try(gwaoi_world *w) {
             w->last_error = "sparse flush launch failed";
             return poison(w, GWAOI_EDEVICE);  // the frame may be half patched
         }
-        S.ev_valid = true;
         if (wait_done(w, S.done_ev) != GWAOI_OK) {
             w->last_error = "sparse flush did not complete: " + w->last_error;
             return poison(w, GWAOI_EDEVICE);
@@ -1606,7 +1546,6 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->out_ev) (void)hipEventDestroy(w->out_ev);
     if (w->out_st) (void)hipStreamDestroy(w->out_st);
     if (w->done_ev) (void)hipEventDestroy(w->done_ev);
-    if (w->probe_ev) (void)hipEventDestroy(w->probe_ev);
     if (w->order_ev) (void)hipEventDestroy(w->order_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
@@ -1684,13 +1623,6 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (const char *e = std::getenv("GWAOI_UNIQUE_MOVES")) w->unique_moves = w->unique_moves && e[0] != '0';  // A/B
     if (const char *e = std::getenv("GWAOI_SKIP_PROLOGUE")) w->skip_prologue = e[0] != '0';  // A/B
     if (const char *e = std::getenv("GWAOI_SPECIAL_FUSED")) w->special_fused = e[0] != '0';  // A/B
-    if (const char *e = std::getenv("GWAOI_DEFER_DONE")) w->defer_done = e[0] != '0';  // A/B
-    if (const char *e = std::getenv("GWAOI_PROBE_HOSTWRITE")) w->probe_hostwrite = e[0] == '1';  // probe
-    if (const char *e = std::getenv("GWAOI_EXTRA_MARKERS")) {  // probe
-        w->extra_markers = std::atoi(e);
-        if (w->extra_markers > 0 && hipEventCreateWithFlags(&w->probe_ev, hipEventDisableTiming) != hipSuccess)
-            return fail(GWAOI_EDEVICE);
-    }
     if (w->batch_ready && (hipStreamCreateWithFlags(&w->mark_st, hipStreamNonBlocking) != hipSuccess ||
                            hipEventCreateWithFlags(&w->apply_ev, hipEventDisableTiming) != hipSuccess ||
                            hipEventCreateWithFlags(&w->mark_ev, hipEventDisableTiming) != hipSuccess))
@@ -1720,7 +1652,6 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
             hipHostGetDevicePointer((void **)&S.d_hout, S.h_out, 0) != hipSuccess)
             return fail(GWAOI_ENOMEM);
         std::memset(S.h_out, 0, out_bytes);
-        reinterpret_cast<gw::TickOut *>(S.h_out)->done_tick = ~0ull;  // no tick id
         for (int st = 0; st < ST_N; ++st)
             for (int q = 0; q < 2; ++q)
                 if (hipEventCreate(&S.ev[st][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
@@ -2513,7 +2444,7 @@ namespace {
 
 // gwaoi_tick_finish(GWAOI_END_NEXT): finish the flush in flight, begin the next one (speculatively,
 // before the finished one's summary is read, when the queue allows it).
-int end_begin(gwaoi_world *w, bool *committed_out, bool device_mode) {
+int end_begin(gwaoi_world *w, bool *committed_out) {
     bool committed = false;
     int rc, lrc = GWAOI_OK;
     if (speculative_ok(w)) {
@@ -2521,13 +2452,7 @@ int end_begin(gwaoi_world *w, bool *committed_out, bool device_mode) {
         // no idle gap on the GPU between the two
         const Flight f = w->fl;
         commit_host(w, nullptr);
-        w->spec_ctx = device_mode;  // (host copies keep their done events: copy_out waits on them)
-        w->sig_ptr = f.ev_deferred ? &reinterpret_cast<gw::TickOut *>(w->fs[f.set].d_hout)->done_tick : nullptr;
-        w->sig_tick = f.tick_id;
-        w->sig_given = false;
         lrc = tick_launch(w);
-        w->spec_ctx = false;
-        w->sig_ptr = nullptr;
         if (lrc == GWAOI_OK) w->dbg.speculative_launches++;
         rc = finish_flight(w, f, true, &committed);
     } else {
@@ -2552,11 +2477,6 @@ int copy_out(gwaoi_world *w, bool pairs, uint64_t regrows) {
     if (tot) {
         // ordered after the flush's last kernel (its event's release makes the writes visible to the
         // copy engine); after a re-run of its pair passes, after the wait that followed the re-run
-        if (w->dbg.event_regrows == regrows && !S.ev_valid) {
-            // its end was signalled, not marked: an event now (after whatever the stream holds since)
-            HIP_TRY(hipEventRecord(S.done_ev, w->stream));
-            S.ev_valid = true;
-        }
         HIP_TRY(hipStreamWaitEvent(w->out_st, w->dbg.event_regrows != regrows ? w->done_ev : S.done_ev, 0));
         if (pairs) {
             gw::launch_pairs_out(S.events, tot / 2, w->d_h_events, w->out_st);
@@ -2628,7 +2548,7 @@ int gwaoi_tick_finish(gwaoi_world *w, uint32_t mode, uint64_t *n_enter, uint64_t
         rc = end_host(w, &committed);
     } else {
         const uint64_t regrows = w->dbg.event_regrows;
-        rc = next ? end_begin(w, &committed, !host) : tick_finish(w, &committed);
+        rc = next ? end_begin(w, &committed) : tick_finish(w, &committed);
         if (committed && host)
             if (int rc2 = copy_out(w, pairs, regrows)) return rc2;
     }
