@@ -1729,8 +1729,9 @@ __global__ __launch_bounds__(PT) void k_pairs(FrameView F, const Rec16 *__restri
                      leave_off, dbg);
 }
 
-// k_arrive with the special pass in front (the steady incremental flush): workgroup t < n_tiles is
-// the special pass's tile t (it leaves at once unless keygen flagged the tile), the rest run k_arrive.  The special pass needs only keygen and its fold (k_scan64), so it
+// k_arrive with the special pass behind it (the steady incremental flush): the first cdiv(n, PT)
+// workgroups run k_arrive, workgroup na + t is the special pass's tile t (it leaves at once unless
+// keygen flagged the tile).  The special pass needs only keygen and its fold (k_scan64), so it
 // rides on this launch instead of one of its own: a launch costs ~4.5 us on this chip however
 // little it does, and a steady config-3 flush flags no tile.  Same tiles, same events, same
 // per-tile totals as k_pairs<1>; an overflow re-run still launches k_pairs<1>.
@@ -1739,13 +1740,15 @@ __global__ __launch_bounds__(PT) void k_arrive_special(SpecialJob J, const uint3
                                                        uint32_t sentinel, uint32_t *arr_pos, uint32_t *arr_idx,
                                                        unsigned long long *cnt64, const uint32_t *__restrict__ shift,
                                                        uint32_t *perm, uint32_t *skeys) {
-    if (blockIdx.x >= J.n_tiles) {
-        arrive_one((blockIdx.x - J.n_tiles) * PT + threadIdx.x, keys, n, n_prev, p_key, sentinel, arr_pos, arr_idx,
-                   cnt64, shift, perm, skeys);
+    const uint32_t na = (n + PT - 1) / PT;  // the arrival workgroups first, the special pass's after them
+    if (blockIdx.x < na) {
+        arrive_one(blockIdx.x * PT + threadIdx.x, keys, n, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64, shift,
+                   perm, skeys);
         return;
     }
-    if (!J.special[blockIdx.x]) return;  // keygen saw no special entity in this tile
-    pairs_tile<1>(blockIdx.x, J.F, J.O_rec, J.O_ss, J.seq_base, J.sc, J.sc, J.tmp, J.cap, J.tile_total, J.tile_base,
+    const uint32_t t = blockIdx.x - na;
+    if (!J.special[t]) return;  // keygen saw no special entity in this tile
+    pairs_tile<1>(t, J.F, J.O_rec, J.O_ss, J.seq_base, J.sc, J.sc, J.tmp, J.cap, J.tile_total, J.tile_base,
                   J.tile_off, J.leave_off, J.sc->dbg);
 }
 
