@@ -3069,7 +3069,11 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
                    unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const TickZero &tz,
                    hipStream_t st) {
-    if (!n_total) return;  // the prologue left d_rel = bmax = 0 (a flush without one has moves: n_total > 0)
+    if (!n_total) {  // no entry: only the fold (d_rel = bmax = 0; a unique-moves apply's dropped ops and
+                     // errors reach sc->err, and its error word and drop count are reset for the next flush)
+        k_keygen_reduce<<<1, 1024, 0, st>>>(blk, 0u, sc);
+        return;
+    }
     const uint32_t nb = cdiv(n_total, 256);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,

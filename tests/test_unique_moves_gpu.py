@@ -162,3 +162,34 @@ def test_unique_moves_repeated_slot_is_reported_gpu():
         for i in range(0, n, 97):
             np.testing.assert_array_equal(np.sort(A.neighbors(i)), np.sort(B.neighbors(i)))
         assert A.debug_counters()["unique_flushes"] == warm + 4
+
+
+def test_unique_moves_on_an_empty_world_report_and_do_not_leak_gpu():
+    """Moves of slots that are not live, on a flagged world with no entity yet: the flush has no
+    entry (keygen does not run, only its fold), yet it must report the dropped moves
+    (GWAOI_ESTATE), and the apply's error word and drop count must not leak into the next flushes."""
+    torch = pytest.importorskip("torch")
+    n = 3000
+    wa = make_workload("cfg2", n=n)
+    slots, x0, z0, _ = wa.initial()
+    sl, nx, nz = wa.tick(0)
+    d0 = [torch.from_numpy(a).to("cuda:0") for a in (sl.astype(np.int32), nx, nz)]
+    ticks = [wa.tick(1 + t) for t in range(3)]
+    dt = [[torch.from_numpy(a).to("cuda:0") for a in (b[0].astype(np.int32), b[1], b[2])] for b in ticks]
+    torch.cuda.synchronize()
+    with World(n, unique_moves=True) as A, World(n) as B:
+        s = A.space_create(wa.D)
+        A.moved_batch_device(*(b.data_ptr() for b in d0), sl.size)
+        with pytest.raises(GwaoiError) as ei:
+            A.tick_device()
+        assert ei.value.code == ESTATE and "not live" in str(ei.value), str(ei.value)
+        sb = B.space_create(wa.D)
+        for w, sp in ((A, s), (B, sb)):
+            w.enter_batch(sp, slots, x0, z0)
+            w.tick()
+            for b, h in zip(dt, ticks):  # clean unique ticks: no error may surface
+                w.moved_batch_device(*(t.data_ptr() for t in b), h[0].size)
+                w.tick_device()
+        np.testing.assert_array_equal(_positions(A, n), _positions(B, n))
+        for i in range(0, n, 101):
+            np.testing.assert_array_equal(np.sort(A.neighbors(i)), np.sort(B.neighbors(i)))
