@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the GWAOI_EXTRA_MARKERS probe hook was removed after this run: profiles/r05_probe_markers.txt)
 # Probe: the price of a marker packet between two flushes (GWAOI_EXTRA_MARKERS=0/2/4 more event
 # records after each flush's done event), from the kernel trace's gap between ticks
 set -o pipefail

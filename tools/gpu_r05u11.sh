@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the GWAOI_DEFER_DONE deferral was removed after this run: profiles/r05_ab_defer_done.txt)
 # Deferred done events (the next flush signals a flush's end): the whole GPU suite, the cfg3 bench
 # with GWAOI_DEFER_DONE=1 (default) / 0 interleaved twice, a kernel trace
 set -o pipefail

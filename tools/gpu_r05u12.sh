@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the GWAOI_PROBE_HOSTWRITE hook was removed after this run: profiles/r05_probe_hostwrite.txt)
 # Probe: does a kernel that stores to mapped host memory end late?  keygen's last block stores 4 B
 # there (GWAOI_PROBE_HOSTWRITE=1) or not; kernel-trace gaps after keygen and between ticks
 set -o pipefail
