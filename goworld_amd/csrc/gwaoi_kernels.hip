@@ -382,6 +382,13 @@ constexpr int S64_TILE = SC_T * S64_I;
 // differs from their previous-frame cell, or new in the frame (high word).
 // S' is the previous frame (sorted by the same keys) plus appended entries,
 // so equal keys come in runs and one atomic per run and wave suffices.
+#ifndef GWAOI_KG_PER
+#define GWAOI_KG_PER 2  // S' entries per keygen thread (their operands in flight together)
+#endif
+constexpr int KG_PER = GWAOI_KG_PER;
+static_assert(KG_PER == 1 || KG_PER == 2, "the written-entry count below takes one or two entries per thread");
+constexpr uint32_t keygen_blocks(uint32_t n) { return (n + 256u * KG_PER - 1) / (256u * KG_PER); }
+
 template <bool INCR>
 __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__restrict__ s_ss,
                                                 uint32_t n, const SpaceGrid *__restrict__ grid, uint32_t sentinel,
@@ -391,15 +398,15 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
                                                 unsigned long long seq_base, uint32_t *special, TickZero tz) {
     __shared__ float s_m[2][256 / WAVE];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
     if (tz.sc) {  // the prologue's zeroing (a unique-moves flush without one; see TickZero)
         const uint32_t m = max(max(tz.n1, tz.n_spaces), EV_SHARDS * 32u), stride = gridDim.x * blockDim.x;
-        for (uint32_t j = i; j < m; j += stride) {
+        for (uint32_t j = gt; j < m; j += stride) {
             if (j < tz.n1) tz.z1[j] = 0;
             if (j < tz.n_spaces) tz.bbox[j] = make_int4(INT_MAX, INT_MAX, INT_MIN, INT_MIN);
             if (j < EV_SHARDS * 32) (&tz.sc->shard[0][0])[j] = 0;
         }
-        if (i == 0) {
+        if (gt == 0) {
             TickScalars *sc = tz.sc;
             sc->err = 0;
             sc->counter = 0;
@@ -411,55 +418,65 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
             for (int q = 0; q < (int)DBG_N; ++q) sc->dbg[q] = 0;
         }
     }
+    // KG_PER entries per thread, 256 apart: entry i_u = base + 256 u is of the special pass's tile
+    // KG_PER b + u.  Every operand of every entry first, in one round trip (none depends on
+    // another): the S' record and space, the previous frame's record, space and key.
+    const uint32_t base = blockIdx.x * (256u * KG_PER) + threadIdx.x;
+    uint32_t s[KG_PER], ps[KG_PER], old[KG_PER];
+    Rec16 r[KG_PER], p[KG_PER];
+#pragma unroll
+    for (int u = 0; u < KG_PER; ++u) {
+        const uint32_t i = base + 256u * (uint32_t)u;
+        const bool in = i < n, inp = i < n_prev;
+        s[u] = in ? ld_ss(s_ss, i).sp : SP_DEAD;
+        r[u].x = r[u].z = 0.0f;
+        r[u].s = 0;
+        if (in) r[u] = ld_rec(s_rec, i);
+        ps[u] = inp ? ld_ss(p_ss, i).sp : SP_DEAD;
+        p[u].x = p[u].z = 0.0f;
+        p[u].s = 0;
+        if (inp) p[u] = ld_rec(p_rec, i);
+        old[u] = INCR && inp ? p_key[i] : sentinel;
+    }
     float dr = 0.0f, bm = 0.0f;
-    uint32_t key = sentinel;
-    bool near = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
-    bool written = false;
-    uint32_t old = sentinel;  // the previous frame's key (INCR)
-    if (i < n) {
-        // every operand of the entry in one round trip (none depends on another): the S' record and
-        // space, the previous frame's record, space and key (round 4 loaded them in three steps)
+    bool near[KG_PER];
+    uint32_t nwr = 0;  // entries this flush's ops wrote (GWAOI_F_UNIQUE_MOVES: one per op that applied)
+#pragma unroll
+    for (int u = 0; u < KG_PER; ++u) {
+        const uint32_t i = base + 256u * (uint32_t)u;
         const bool inp = i < n_prev;
-        const uint32_t s = ld_ss(s_ss, i).sp;
-        Rec16 r = ld_rec(s_rec, i);
-        const uint32_t ps = inp ? ld_ss(p_ss, i).sp : SP_DEAD;
-        Rec16 p;
-        p.x = p.z = 0.0f;
-        p.s = 0;
-        if (inp) p = ld_rec(p_rec, i);
-        if (INCR && inp) old = p_key[i];
-        if (s != SP_DEAD) {
-            written = r.s >= seq_base;
-            const bool same = inp && ps == s;
-            if (same || (inp && r.s < seq_base)) {
-                if (r.s < seq_base && inp) {  // not written by this flush's ops: the previous state
-                    if (r.x != p.x || r.z != p.z || r.s != p.s) st_rec(s_rec, i, p);  // (virtual S': no prologue copy)
-                    r = p;
+        near[u] = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
+        if (i >= n) continue;
+        uint32_t key = sentinel;
+        Rec16 rr = r[u];
+        if (s[u] != SP_DEAD) {
+            nwr += rr.s >= seq_base ? 1u : 0u;
+            const bool same = inp && ps[u] == s[u];
+            if (same || (inp && rr.s < seq_base)) {
+                if (rr.s < seq_base && inp) {  // not written by this flush's ops: the previous state
+                    if (rr.x != p[u].x || rr.z != p[u].z || rr.s != p[u].s) st_rec(s_rec, i, p[u]);  // (virtual S')
+                    rr = p[u];
                 }
-                const float D = p_grid[s].D;
-                if (same && is_near(r.x, r.z, p.x, p.z, FAR_FRAC * D)) {
-                    dr = fmaxf(fabsf(r.x - p.x), fabsf(r.z - p.z)) / D;
-                    near = true;
+                const float D = p_grid[s[u]].D;
+                if (same && is_near(rr.x, rr.z, p[u].x, p[u].z, FAR_FRAC * D)) {
+                    dr = fmaxf(dr, fmaxf(fabsf(rr.x - p[u].x), fabsf(rr.z - p[u].z)) / D);
+                    near[u] = true;
                 }
             }
-            const SpaceGrid g = grid[s];
-            const int cx = cell_of(r.x, g.ox, g.inv, g.gx);
-            const int cz = cell_of(r.z, g.oz, g.inv, g.gz);
+            const SpaceGrid g = grid[s[u]];
+            const int cx = cell_of(rr.x, g.ox, g.inv, g.gx);
+            const int cz = cell_of(rr.z, g.oz, g.inv, g.gz);
             key = g.base + (uint32_t)cz * g.gx + (uint32_t)cx;
-            bm = fmaxf(fabsf(r.x), fabsf(r.z));
+            bm = fmaxf(bm, fmaxf(fabsf(rr.x), fabsf(rr.z)));
         }
         keys[i] = key;
         if (!INCR) vals[i] = i;
-    }
-    if (INCR) {
-        // only the entities that changed cell count: an arrival in the new cell (low word), a
+        // INCR: only the entities that changed cell count: an arrival in the new cell (low word), a
         // departure from the old one (high word); a cell's stayers are its previous count minus
         // its departures, which k_scan64 takes from the previous cell_start
-        if (i < n) {
-            if (key != old) {
-                if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
-                if (old != sentinel) atomicAdd(&cnt64[old], 1ull << 32);
-            }
+        if (INCR && key != old[u]) {
+            if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
+            if (old[u] != sentinel) atomicAdd(&cnt64[old[u]], 1ull << 32);
         }
     }
 #pragma unroll
@@ -471,12 +488,15 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         s_m[0][threadIdx.x / WAVE] = dr;
         s_m[1][threadIdx.x / WAVE] = bm;
     }
-    // the special pass's tile of this block (previous-frame entries [256 b, 256 b + 256)): does it hold
-    // an entity that is not near (left, changed space, jumped)?  k_pairs<1> skips the tiles without
-    const bool sp_any = __syncthreads_or(i < n_prev && !near);
-    if (special && threadIdx.x == 0 && blockIdx.x * 256u < n_prev) special[blockIdx.x] = sp_any ? 1u : 0u;
-    // the entries this flush's ops wrote (GWAOI_F_UNIQUE_MOVES: one per op that applied)
-    const uint32_t nw = (uint32_t)__syncthreads_count(written);
+    // the special pass's tiles of this block (previous-frame entries [256 t, 256 t + 256)): does one
+    // hold an entity that is not near (left, changed space, jumped)?  k_pairs<1> skips the tiles without
+#pragma unroll
+    for (int u = 0; u < KG_PER; ++u) {
+        const uint32_t t = blockIdx.x * (uint32_t)KG_PER + (uint32_t)u;
+        const bool sp_any = __syncthreads_or(base + 256u * (uint32_t)u < n_prev && !near[u]);
+        if (special && threadIdx.x == 0 && t * 256u < n_prev) special[t] = sp_any ? 1u : 0u;
+    }
+    const uint32_t nw = (uint32_t)__syncthreads_count(nwr >= 1) + (KG_PER > 1 ? (uint32_t)__syncthreads_count(nwr >= 2) : 0u);
     if (threadIdx.x == 0) {
         reinterpret_cast<uint32_t *>(blk)[2 * gridDim.x + blockIdx.x] = nw;
         float a = s_m[0][0], b = s_m[1][0];
@@ -3074,7 +3094,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, 0u, sc);
         return;
     }
-    const uint32_t nb = cdiv(n_total, 256);
+    const uint32_t nb = keygen_blocks(n_total);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
                                            n_prev, blk, p_key, cnt64, seq_base, special, tz);  // folded by incremental_sort
@@ -3102,7 +3122,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
     unsigned long long *tcnt = tmp + nb;
     k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
     k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
-                                      cdiv(n_total, 256), sc, p_cell_start, shift, list, tcnt);
+                                      keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt);
     if (sp && sp->n_tiles) {
         const SpecialJob &J = *sp;
         k_arrive_special<<<J.n_tiles + cdiv(n_total, PT), PT, 0, st>>>(J, keys, n_total, n_prev, p_key, sentinel, arr_pos,
