@@ -601,6 +601,8 @@ def line_summary(out: dict) -> dict:
     cfg5 = out.get("cfg5_strips") or {}
     return {
         "ms_per_step": g(out, "ms_per_step"), "p99_tick_ms": g(out, "p99_tick_ms"),
+        "claims_ms_per_step": g(out, "claims_tick", "ms_per_step"), "claims_p99_ms": g(out, "claims_tick", "p99_tick_ms"),
+        "claims_counts_equal": g(out, "claims_tick", "counts_equal_headline"),
         "combined_ms": g(out, "roofline", "avg_launch_ms"), "roofline_frac": g(out, "roofline", "frac"),
         "host_to_host_tick_ms": g(out, "host_to_host_tick", "ms_per_step"),
         "host_to_host_p50_ms": g(out, "host_to_host_tick", "p50_tick_ms"),
@@ -616,6 +618,60 @@ def line_summary(out: dict) -> dict:
         "cpu_port_moves_per_s": g(out, "cpu_baseline", "value"),
         "cpu_grid_ms_per_tick": g(out, "cpu_baseline", "cpu_grid", "ms_per_tick"),
     }
+
+
+def claims_leg(args, n, n_spaces, D, initial, device, row_ptrs, moves_per_tick, t0: int, t1: int, ref_counts):
+    """The headline's ticks through the general AOIManager contract: a world WITHOUT
+    GWAOI_F_UNIQUE_MOVES, so every flush stores the last-op claims and runs the repeated-slot fixup
+    that go-aoi's Moved semantics need when a batch may name an entity twice (the gate appends every
+    client sync record without deduplication, /root/reference/components/gate/GateService.go:398-405,
+    and the game applies each in order, components/game/GameService.go:396-403).  Same initial state,
+    same device batches, same speculative loop as the timed region: ticks t0 .. t1-1 after ticks
+    0 .. t0-1 untimed.  Every tick's (enters, leaves) must equal the headline world's."""
+    from goworld_amd import World
+    slots, x0, z0, sp = initial
+    w = World(n, max_spaces=n_spaces, device=device, cells_per_dist=args.cells_per_dist, unique_moves=False)
+    try:
+        spaces = [w.space_create(D) for _ in range(n_spaces)]
+        for s in range(n_spaces):
+            sel = np.nonzero(sp == s)[0] if n_spaces > 1 else slice(None)
+            w.enter_batch(spaces[s], slots[sel], x0[sel], z0[sel])
+        w.tick_device()
+        counts = {}
+        for t in range(t0):
+            ps, px, pz = row_ptrs[t]
+            w.moved_batch_device(ps, px, pz, moves_per_tick[t])
+            counts[t] = w.tick_device()
+        w.sync()
+        lat = []
+        a0 = time.perf_counter()
+        ps, px, pz = row_ptrs[t0]
+        w.moved_batch_device(ps, px, pz, moves_per_tick[t0])
+        w.tick_begin()
+        for t in range(t0, t1):
+            a = time.perf_counter()
+            if t + 1 < t1:
+                ps, px, pz = row_ptrs[t + 1]
+                w.moved_batch_device(ps, px, pz, moves_per_tick[t + 1])
+                counts[t] = w.tick_end_begin_device()
+            else:
+                counts[t] = w.tick_end_device()
+            lat.append(time.perf_counter() - a)
+        w.sync()
+        elapsed = time.perf_counter() - a0
+        dbg = w.debug_counters()
+    finally:
+        w.close()
+    k = t1 - t0
+    lat_ms = np.array(lat) * 1e3
+    bad = [t for t in ref_counts if counts.get(t) != ref_counts[t]]
+    moves = sum(moves_per_tick[t0:t1])
+    return {"value": moves / elapsed, "unit": "entity-moves/s", "steps": k, "ms_per_step": elapsed / k * 1e3,
+            "p50_tick_ms": float(np.percentile(lat_ms, 50)), "p99_tick_ms": float(np.percentile(lat_ms, 99)),
+            "unique_flushes": int(dbg["unique_flushes"]), "speculative_launches": int(dbg["speculative_launches"]),
+            "counts_equal_headline": not bad, "ticks_compared": len(ref_counts), "mismatched_ticks": bad[:8],
+            "note": "general contract (last-op claims + repeated-slot fixup: a batch may repeat an entity, the "
+                    "last call wins); the headline's batches, initial state and speculative loop"}
 
 
 def small_flush_leg(w, last, reps: int, sizes=(1, 64, 4096, 65536)):
@@ -1145,12 +1201,12 @@ def main():
     ap.add_argument("--wire-records", type=int, default=1_000_000, help="32-B client records per wire regroup call")
     ap.add_argument("--wire-out-records", type=int, default=4_000_000,
                     help="48-B game records per gate_to_clients call (one gate's share of a cfg3 collect)")
-    ap.add_argument("--batch-ready", action="store_true",
-                    help="A/B: the next batch's claims stored beside the flush in flight (GWAOI_F_BATCH_READY), "
-                         "not by the next flush's prologue; slower at config 3 (DESIGN.md sec. 3 step 1)")
     ap.add_argument("--claims", action="store_true",
                     help="A/B: apply the moves through the last-op claims + repeated-slot fixup instead of "
                          "GWAOI_F_UNIQUE_MOVES (the workload's batches name every entity once per tick)")
+    ap.add_argument("--claims-steps", type=int, default=20,
+                    help="cfg3 at N=1: timed ticks of the claims sub-record (the general-contract flush: a batch "
+                         "may repeat an entity; 0 = off)")
     ap.add_argument("--small-flush-reps", type=int, default=20,
                     help="cfg3: timed flushes per size of the small-flush leg (1/64/4096/65536 moves; 0 = off)")
     ap.add_argument("--strip-counts", default="device", choices=["device", "host"],
@@ -1258,14 +1314,15 @@ def main():
     del batches
     torch.cuda.synchronize()
 
-    # the move batches are in HBM before the timed region: complete when passed (GWAOI_F_BATCH_READY);
-    # each names every moving entity once (a permutation per tick): GWAOI_F_UNIQUE_MOVES, checked on the
-    # device by every flush (a repeated slot would fail the tick)
+    # the move batches are in HBM before the timed region; each names every moving entity once (a
+    # permutation per tick): GWAOI_F_UNIQUE_MOVES, checked on the device by every flush (a repeated slot
+    # would fail the tick).  The claims sub-record times the general contract beside it.
     w = World(n, max_spaces=wl.n_spaces, device=device, cells_per_dist=args.cells_per_dist,
-              batch_ready=args.batch_ready, unique_moves=not args.claims)
+              unique_moves=not args.claims)
     spaces = [w.space_create(wl.D) for _ in range(wl.n_spaces)]
     wl0 = wl_factory()  # initial positions (wl has advanced through the batches)
-    slots, x0, z0, sp = wl0.initial()
+    initial = wl0.initial()
+    slots, x0, z0, sp = initial
     del wl0
     for s in range(wl.n_spaces):
         sel = np.nonzero(sp == s)[0] if wl.n_spaces > 1 else slice(None)
@@ -1277,10 +1334,13 @@ def main():
     # per call, during which the GPU would sit idle between ticks)
     row_ptrs = [(d_slots[t].data_ptr(), d_x[t].data_ptr(), d_z[t].data_ptr()) for t in range(ticks)]
 
+    tick_counts = {}  # (enters, leaves) per tick: the claims sub-record must match them
+
     def step(t):
         ps, px, pz = row_ptrs[t]
         w.moved_batch_device(ps, px, pz, moves_per_tick[t])
-        return w.tick_device()
+        tick_counts[t] = w.tick_device()
+        return tick_counts[t]
 
     # warmup; its last ticks time every stage to find the dominant one
     dom = "combined"
@@ -1344,6 +1404,7 @@ def main():
             timing_for(t)
             ne, nl = step(t)
         lat.append(time.perf_counter() - a)
+        tick_counts[t] = (ne, nl)
         events += ne + nl
         moves += moves_per_tick[t]
     w.sync()
@@ -1367,6 +1428,15 @@ def main():
         stages = w.stage_times()
         w.set_stage_timing([])
 
+    claims = None
+    if args.claims_steps > 0 and ws == 1 and args.workload == "cfg3" and not args.claims:
+        c1 = min(timed_end, args.warmup + args.claims_steps)
+        try:
+            claims = claims_leg(args, n, wl.n_spaces, wl.D, initial, device, row_ptrs, moves_per_tick, args.warmup,
+                                c1, {t: tick_counts[t] for t in range(c1) if t in tick_counts})
+        except Exception as e:  # a side leg must not take the headline down with it
+            claims = {"error": repr(e)}
+    del initial
     small = None
     if args.small_flush_reps > 0 and ws == 1 and args.workload == "cfg3":
         small = small_flush_leg(w, last_batch, args.small_flush_reps)
@@ -1469,6 +1539,7 @@ def main():
                                              "one event per mirrored pair; serial and directed_events_out: every "
                                              "directed event); details in pcie_inclusive"} if host_io else None),
             "pcie_inclusive": host_io,
+            "claims_tick": claims,
             "small_flush": small,
             "sync_leg": sync,
             "wire_leg": wire,

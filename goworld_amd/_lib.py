@@ -20,8 +20,16 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "gwaoi.h")
 
 GWAOI_F_TIMING = 1
 GWAOI_F_NO_SPARSE = 2  # never the sparse flush (include/gwaoi.h)
-GWAOI_F_BATCH_READY = 4  # device batches complete when passed: claims stored beside the flush before
+GWAOI_F_BATCH_READY = 4  # accepted and ignored since ABI 5
 GWAOI_F_UNIQUE_MOVES = 8  # a flush's Moved batches never repeat a slot: no last-op claims (checked on device)
+# test and diagnostics flags (include/gwaoi.h): a slower or failing path, to compare with the default one
+GWAOI_F_TEST_FORCE_RADIX = 0x100
+GWAOI_F_TEST_FORCE_COPY = 0x200
+GWAOI_F_TEST_BUCKETED = 0x400
+GWAOI_F_TEST_REGROW_FAIL = 0x800
+GWAOI_F_TEST_SPARSE_SEQUENCE = 0x1000
+GWAOI_F_TEST_SPARSE_SCR2 = 0x2000
+GWAOI_F_TEST_CHECK_STAGES = 0x4000
 
 STATUS = {
     0: "GWAOI_OK", -1: "GWAOI_EINVAL", -2: "GWAOI_EBADSLOT", -3: "GWAOI_ESTATE", -4: "GWAOI_ENOMEM",
@@ -252,10 +260,11 @@ class World:
 
     def __init__(self, max_slots: int, max_spaces: int = 1, device: int = -1, timing: bool = False,
                  event_capacity: int = 0, cells_per_dist: float = 0.0, sparse: bool = True,
-                 batch_ready: bool = False, unique_moves: bool = False):
+                 unique_moves: bool = False, test_flags: int = 0):
+        """test_flags: an OR of GWAOI_F_TEST_* (tests comparing a slower path with the default one)."""
         self._L = load()
         flags = ((GWAOI_F_TIMING if timing else 0) | (0 if sparse else GWAOI_F_NO_SPARSE) |
-                 (GWAOI_F_BATCH_READY if batch_ready else 0) | (GWAOI_F_UNIQUE_MOVES if unique_moves else 0))
+                 (GWAOI_F_UNIQUE_MOVES if unique_moves else 0) | int(test_flags))
         cfg = Config(max_slots, max_spaces, device, flags, event_capacity, cells_per_dist)
         h = C.c_void_p()
         self._check(self._L.gwaoi_world_create(C.byref(cfg), C.byref(h)), world=False)

@@ -145,7 +145,7 @@ struct TickOut {
     uint32_t pad;
     unsigned long long total64;
     unsigned long long seq_max;
-    unsigned long long pad2;
+    unsigned long long ext64;  // the scratch extent the pair passes reached (their 8 event streams interleaved)
     uint32_t dbg[4];  // TickScalars::dbg
     // followed by int4 bbox[n_spaces] (ordered-int min x, min z, max x, max z)
 };
@@ -187,7 +187,7 @@ struct MoveRuns {
 // the spaces are the previous frame's, and an entry of S' not written by an op
 // holds an older seq than seq_floor, so k_keygen takes the previous frame's
 // record for it and writes it back).  n_marked: runs whose claims are stored
-// already (by the prologue: run 0; by launch_moves_mark: every run).
+// already (by the prologue: run 0).
 // unique (GWAOI_F_UNIQUE_MOVES): no run repeats a slot, so no claims are stored or compared and
 // no fixup runs; keygen counts the entries the ops wrote and the scan's fold block checks the
 // count against TickScalars::n_unique (ERR_DUP_SLOT).
@@ -342,8 +342,8 @@ size_t tile_total_elems(size_t n_entries);
 void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream_t st);
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, const uint32_t *tmp_pairs,
-                   uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
+                   uint32_t *out_pairs, uint64_t cap_tmp, uint64_t cap_out, const TickScalars *sc, TickOut *out,
+                   uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
                    uint32_t *dcount, hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
@@ -357,9 +357,6 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st);
 void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_total, uint32_t n_rows, uint32_t *cnt,
                        uint32_t *off, uint32_t *scan_tmp, uint32_t *items, uint32_t *scratch, uint32_t *long_rows,
                        hipStream_t st);
-
-// The claims (tick << 32 | j0 + i) of one Moved run (k_moves_mark), on any stream.
-void launch_moves_mark(const MoveRun &R, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st);
 
 // Sparse flush of k host Moved calls on a frame in place (gwaoi_sparse.hip): claims must be stored
 // first (launch_ops_claim, this tick).  cnt: sparse_cnt_elems(k) words.  The flush's summary goes to

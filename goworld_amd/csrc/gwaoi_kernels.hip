@@ -2680,8 +2680,8 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
 __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ tile_total,
                                                 const unsigned long long *__restrict__ tile_base, uint32_t n_entries,
                                                 uint32_t n_enter_entries,
-                                                const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap,
-                                                const TickScalars *__restrict__ sc, TickOut *res,
+                                                const uint2 *__restrict__ tmp, uint2 *out, uint64_t cap_tmp,
+                                                uint64_t cap_out, const TickScalars *__restrict__ sc, TickOut *res,
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
                                                 uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
                                                 uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt) {
@@ -2696,13 +2696,16 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     if (blockIdx.x == nx) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         if (threadIdx.x == 0) {
             res->err = sc->err;
-            // the scratch extent the pair passes needed (each stream's last chunk), against the capacity
-            unsigned long long ext = 0;
+            // the events (the streams' lengths) and the scratch extent the pair passes needed (each
+            // stream's last chunk): against the set's and the scratch's capacity
+            unsigned long long ext = 0, tot = 0;
             for (uint32_t q = 0; q < EV_SHARDS; ++q) {
                 const unsigned long long len = *reinterpret_cast<const unsigned long long *>(&sc->shard[q][2]);
                 if (len) ext = max(ext, ev_phys(ev_enc(q, len - 1)) + 1);
+                tot += len;
             }
-            res->total64 = ext;
+            res->total64 = tot;
+            res->ext64 = ext;
             res->seq_max = sc->seq_max;
             for (int q = 0; q < (int)DBG_N; ++q) res->dbg[q] = sc->dbg[q];
             if (n_entries == 0) {
@@ -2808,13 +2811,13 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
             if (p < o1) {
                 while (s_off[t + 1] <= p) ++t;  // last tile t with s_off[t] <= p (s_off[FT] = o1 > p)
                 const unsigned long long src = ev_phys(s_src[t] + (p - s_off[t]));
-                if (src < cap) v[u] = tmp[src];
+                if (src < cap_tmp) v[u] = tmp[src];
             }
         }
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const uint32_t p = p0 + (uint32_t)u * blockDim.x;
-            if (p < o1 && p < cap) out[p] = v[u];
+            if (p < o1 && p < cap_out) out[p] = v[u];
         }
     }
 }
@@ -2996,10 +2999,6 @@ void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t ba
                           SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st) {
     if (!n_app) return;
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
-}
-
-void launch_moves_mark(const MoveRun &R, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, hipStream_t st) {
-    if (R.n) k_moves_mark<<<cdiv(R.n, 256), 256, 0, st>>>(R, max_slots, info, tick_id);
 }
 
 void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
@@ -3241,7 +3240,8 @@ size_t tile_total_elems(size_t n_entries) { return n_entries + 1 + cdiv(n_entrie
 
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, const uint32_t *tmp_pairs,
-                   uint32_t *out_pairs, uint64_t cap, const TickScalars *sc, TickOut *out, uint32_t n_new, int4 *bbox,
+                   uint32_t *out_pairs, uint64_t cap_tmp, uint64_t cap_out, const TickScalars *sc, TickOut *out,
+                   uint32_t n_new, int4 *bbox,
                    uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
                    uint32_t *dcount, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
@@ -3249,7 +3249,8 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
     if (!n_new) tile_order = nullptr;
     k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
         tile_total, tile_base, n_entries, n_enter_entries, reinterpret_cast<const uint2 *>(tmp_pairs),
-        reinterpret_cast<uint2 *>(out_pairs), cap, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem), np, bbox,
+        reinterpret_cast<uint2 *>(out_pairs), cap_tmp, cap_out, sc, out, reinterpret_cast<const BBoxPart *>(parts_mem),
+        np, bbox,
         n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount);
 }
 

@@ -164,6 +164,12 @@ struct DeferredBox {  // Enter/Moved positions of a deferred staged batch, per s
     float x0, z0, x1, z1;
 };
 
+// Event capacities of one launch of the pair passes: the shared scratch (in pairs of the streams'
+// interleaved extent) and the flush set's buffer (in events).
+struct EvCaps {
+    uint64_t tmp, out;
+};
+
 // The buffers one flush writes that the flush after it must leave alone while the
 // first may still be re-run (event buffer regrow) or read by the caller: two
 // sets, alternated per launch, so that flush t+1 can be launched before flush
@@ -224,20 +230,17 @@ struct gwaoi_world {
     uint32_t *tile_work = nullptr;   // per combined tile: its measured time, then its candidates (k_combined)
     uint32_t *tile_order = nullptr;  // the next flush's combined tile order, heaviest first (k_tile_order)
     uint32_t *ework = nullptr;       // per frame entry: candidates its lane swept (the next flush's deal to waves)
-    bool tile_order_on = true;       // GWAOI_TILE_ORDER=0: tiles in xcd_block order
     uint32_t *mv_hist = nullptr;  // bucketed apply: the bucket-major histogram, scanned (gw::launch_moves_bucketed)
     uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
     bool moves_bucketed = false;   // the bucketed apply (max_slots > MV_MIN_SLOTS; GWAOI_MOVES_BUCKETED forces it)
     size_t cnt64_cap = 0;
-    bool force_radix = false;  // GWAOI_FORCE_RADIX=1: always the full radix sort (A/B check)
-    bool force_copy = false;   // GWAOI_FORCE_COPY=1: S' always copied by the prologue (A/B check of virtual S')
-    bool inject_regrow_fail = false;  // GWAOI_INJECT_REGROW_FAIL=1 (tests): the event regrow fails
-    // End-of-flush wait: poll an event (default) or block in hipStreamSynchronize
-    // (GWAOI_BLOCKING_SYNC=1, A/B check).
-    hipEvent_t done_ev = nullptr;  // wait_stream's marker
+    // test and diagnostics flags (GWAOI_F_TEST_*, include/gwaoi.h)
+    bool force_radix = false;  // always the full radix sort (checks the incremental sort against it)
+    bool force_copy = false;   // S' always copied by the prologue (checks virtual S' against it)
+    bool inject_regrow_fail = false;  // the event regrow fails (the poison path)
+    hipEvent_t done_ev = nullptr;  // wait_stream's marker (polled)
     hipEvent_t order_ev = nullptr;  // gwaoi_stream_after / _before
-    bool blocking_sync = false;
-    bool check_stages = false;   // GWAOI_CHECK_STAGES=1: wait after every flush stage (fault diagnosis)
+    bool check_stages = false;   // wait after every flush stage (fault diagnosis)
     const char *fault_stage = nullptr;  // stage at the first failed wait
     bool fault_before = false;          // ... the wait before it (else after it)
     uint32_t *new_slots_d = nullptr;
@@ -292,11 +295,10 @@ struct gwaoi_world {
     // (sp_ops_layout: pinned -> device in one copy); off with GWAOI_F_NO_SPARSE
     uint32_t *sp_cnt = nullptr;
     uint8_t *h_sp_ops = nullptr, *d_sp_ops = nullptr;
-    // the fused form (one launch; GWAOI_SPARSE_FUSED=0: the kernel sequence): per-op scratch rows of
-    // sp_scr_cap events per kind (GWAOI_SPARSE_SCR, tests), and its arrival counter
+    // the fused form (one launch; GWAOI_F_TEST_SPARSE_SEQUENCE: the kernel sequence): per-op scratch
+    // rows of sp_scr_cap events per kind (GWAOI_F_TEST_SPARSE_SCR2: 2), and its arrival counter
     uint32_t *sp_scr = nullptr, *sp_done = nullptr;
     uint32_t sp_scr_cap = 512;
-    size_t stage_min = 64;  // host move batches of this many moves or more are staged (GWAOI_STAGE_MIN: A/B)
     bool sparse_fused = true;
     bool sparse_on = true;
     // zero-copy batch (gwaoi_moved_batch_stage / _commit): the caller fills [slots | x | z | space]
@@ -312,33 +314,13 @@ struct gwaoi_world {
     // gwaoi_tick_finish without a host mode, changes last_n_* but not the host copy)
     uint64_t out_n_enter = 0, out_n_leave = 0;
     uint32_t *d_h_events = nullptr;  // h_events as the device sees it (k_pairs_out writes through it)
-    // GWAOI_F_BATCH_READY: the first device Moved batch queued while a flush is in flight gets its
-    // claims on mark_st once that flush's apply is done (apply_ev), beside the rest of the flush
-    bool batch_ready = false;
     // GWAOI_F_UNIQUE_MOVES: the Moved batches of one flush never repeat a slot (no claims, no fixup)
     bool unique_moves = false;
-    bool skip_prologue = true;
-    bool special_fused = true;  // the special pass inside k_arrive_special (GWAOI_SPECIAL_FUSED=0: A/B)  // ... and on the previous grid without the prologue launch (GWAOI_SKIP_PROLOGUE=0: A/B)
-    hipStream_t mark_st = nullptr;
-    hipEvent_t apply_ev = nullptr, mark_ev = nullptr;
-    bool apply_ev_valid = false;
-    bool premark_late = false;  // the claims beside the pair passes rather than after the apply
-    // the special pass beside the combined pass on a side stream (GWAOI_SPECIAL_SIDE=1, A/B):
-    // measured slower at config 3 (0.2375 against 0.2202 ms per tick, profiles/r05_ab_side_premark.txt)
-    bool special_side = false;
-    hipStream_t side_st = nullptr;
-    hipEvent_t side_fork = nullptr, side_join = nullptr;
-    struct {
-        bool on;
-        uint32_t tick;
-        const uint32_t *ds;
-        size_t n;
-    } premark{};
     hipStream_t copy_st = nullptr;  // staging H2D copies
     hipEvent_t copy_ev = nullptr;   // recorded after the last staging copy
     bool copy_pending = false;      // the flush must wait for copy_ev
     StagePool pool;
-    unsigned stage_threads = 8;  // host threads validating + staging one big batch (GWAOI_STAGE_THREADS)
+    unsigned stage_threads = 8;  // host threads validating + staging one big batch
     std::vector<uint32_t> new_slots;
     std::vector<uint32_t> touched;  // slots whose liveness changed since the last flush
     // seq_next: the seq the next implicit call gets (advanced at queue time);
@@ -362,7 +344,7 @@ struct gwaoi_world {
         int set;            // FlushSet it writes
         int p_idx, n_idx;   // previous / new frame
         const gw::SlotSp *s_ss_view;  // its S' spaces: the set's sss, or the previous frame's (virtual S')
-        uint64_t cap;       // event capacity its pair passes were launched with (writes clipped to it)
+        EvCaps cap;         // event capacities its pair passes were launched with (writes clipped to them)
         std::vector<uint8_t> touched_alive;  // liveness of touched[i] when the queue was closed
     } fl;
 
@@ -457,7 +439,7 @@ void stage_collect(gwaoi_world *w, FlushSet &S) {
 // where the blocking wait of hipStreamSynchronize adds tens of microseconds of
 // wake-up latency to every tick.
 int wait_stream(gwaoi_world *w) {
-    if (w->blocking_sync || !w->done_ev) {
+    if (!w->done_ev) {
         HIP_TRY(hipStreamSynchronize(w->stream));
         return GWAOI_OK;
     }
@@ -479,12 +461,14 @@ int ensure_scan_tmp(gwaoi_world *w, size_t n) {
     return GWAOI_OK;
 }
 
-// Room for `pairs` directed events in set S's event buffer and in the shared scratch.  Grows only
-// S's buffer: the other set may hold the events of a committed flush the caller has not read yet.
-// exact: grow to `pairs` and no more (matching the twin set's capacity: with slack, the two sets
-// would outgrow each other on every flush).
-int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs, bool exact = false) {
-    if (pairs <= S.ev_cap && pairs <= w->evtmp_cap) return GWAOI_OK;
+// Room for `pairs` directed events in set S's event buffer and for a scratch extent of `extent`
+// pairs in the shared scratch (the pair passes' eight event streams interleave there, so their
+// extent may exceed the event count).  Grows only S's buffer: the other set may hold the events of
+// a committed flush the caller has not read yet.  exact: grow S's buffer to `pairs` and no more
+// (matching the twin set's capacity: with slack, the two sets would outgrow each other on every
+// flush).
+int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs, uint64_t extent, bool exact = false) {
+    if (pairs <= S.ev_cap && extent <= w->evtmp_cap) return GWAOI_OK;
     HIP_TRY(hipStreamSynchronize(w->stream));
     int rc;
     if (pairs > S.ev_cap) {
@@ -494,8 +478,8 @@ int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs, bool exact = fals
         if ((rc = dalloc(w, &S.events, 2 * cap))) return rc;
         S.ev_cap = cap;
     }
-    if (pairs > w->evtmp_cap) {
-        const uint64_t cap = std::max<uint64_t>(pairs + pairs / 4, w->evtmp_cap * 2);
+    if (extent > w->evtmp_cap) {
+        const uint64_t cap = std::max<uint64_t>(extent + extent / 4, w->evtmp_cap * 2);
         dfree(w->events_tmp);
         w->evtmp_cap = 0;
         if ((rc = dalloc(w, &w->events_tmp, 2 * cap))) return rc;
@@ -809,41 +793,32 @@ uint32_t *last_events(gwaoi_world *w) { return w->fs[w->last_set].events; }
 // new-frame blocks | previous-frame blocks] then [leave totals: same order];
 // their exclusive scan is the final layout [enters | leaves] in block order.
 
-// Returns the event capacity the passes were given (what the flush's finish must compare the total
-// against: the set's buffer or the shared scratch may grow later, by another flush's regrow).
+// Returns the event capacities the passes were given (what the flush's finish must compare the
+// count and the scratch extent against: the set's buffer or the shared scratch may grow later, by
+// another flush's regrow).
 // rerun: the flush's pair passes again after an event-buffer overflow.  By then a speculatively
 // launched successor may have rebuilt the shared scheduling buffers (tile order, tile work, per-entry
 // work) for the flush after it, so a re-run neither reads nor writes them, and keygen's special-tile
 // flags may be the successor's too, so every tile is visited.
-uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
+EvCaps launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P, uint64_t seq_base,
                             const gw::SlotSp *s_ss_view, bool rerun = false, bool special_done = false) {
     hipStream_t st = w->stream;
     const uint32_t TBn = gw::combined_tiles(Fn.n), TBp = gw::combined_blocks(P.n);
     const uint32_t half = TBn + TBp, entries = 2 * half;
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
-    // the pair passes may emit min(set capacity, scratch capacity) pairs; more is an overflow (re-run)
-    const uint64_t cap = std::min(S.ev_cap, w->evtmp_cap);
+    // the pair passes write their streams into the scratch (capacity evtmp_cap), and k_finish copies
+    // them into the set's buffer (ev_cap); a larger extent or count is an overflow (re-run)
+    const EvCaps caps{w->evtmp_cap, S.ev_cap};
+    const uint64_t cap = caps.tmp;
     // timed with the launch's own start/end events (no marker packets)
     const bool tc = w->timing_mask >> ST_COMBINED & 1u;
     if (tc) S.ev_used[ST_COMBINED] = true;
-    const bool order = w->tile_order_on && !rerun;
-    // The special pass needs nothing of the combined pass: it runs beside it on a side stream (in
-    // the combined pass's tail, whose CUs empty as its last tiles drain), unless it is timed.
-    const bool side = w->special_side && !(w->timing_mask >> ST_SPECIAL & 1u) && !special_done;
-    if (side) {
-        HIP_TRY(hipEventRecord(w->side_fork, st));
-        HIP_TRY(hipStreamWaitEvent(w->side_st, w->side_fork, 0));
-        gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn,
-                         half, rerun ? nullptr : w->special, w->side_st);
-        HIP_TRY(hipEventRecord(w->side_join, w->side_st));
-    }
+    const bool order = !rerun;
     gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, half,
                         order ? w->tile_order : nullptr, order ? w->tile_work : nullptr, rerun ? nullptr : w->ework,
                         st,
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
-    if (side) {
-        HIP_TRY(hipStreamWaitEvent(st, w->side_join, 0));
-    } else if (!special_done) {  // (special_done: it ran in the sort's arrival launch)
+    if (!special_done) {  // (special_done: it ran in the sort's arrival launch)
         stage_begin(w, S, ST_SPECIAL);
         gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn,
                          half, rerun ? nullptr : w->special, st);
@@ -852,13 +827,13 @@ uint64_t launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame 
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
     stage_begin(w, S, ST_FINISH);
     gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->events_tmp, S.events,
-                      cap, S.sc, reinterpret_cast<gw::TickOut *>(S.d_hout), Fn.n,
+                      caps.tmp, caps.out, S.sc, reinterpret_cast<gw::TickOut *>(S.d_hout), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts,
                       reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
                       order ? w->tile_work : nullptr, order ? w->tile_order : nullptr,
                       reinterpret_cast<uint32_t *>(S.dev_out), st);
     stage_end(w, S, ST_FINISH);
-    return cap;
+    return caps;
 }
 
 int poison(gwaoi_world *w, int rc) {
@@ -906,7 +881,7 @@ int tick_launch(gwaoi_world *w) {
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
     if ((rc = ensure_tile_entries(w, entries))) return rc;
     // a set whose twin grew on an overflow grows alike before its next flush (one re-run, not two)
-    if (S.ev_cap < w->fs[set ^ 1].ev_cap && (rc = ensure_events(w, S, w->fs[set ^ 1].ev_cap, true))) return rc;
+    if (S.ev_cap < w->fs[set ^ 1].ev_cap && (rc = ensure_events(w, S, w->fs[set ^ 1].ev_cap, 0, true))) return rc;
     size_t host_ops = 0;
     for (const Run &r : w->runs)
         if (!r.device) host_ops += r.hend - r.hbegin;
@@ -960,21 +935,13 @@ int tick_launch(gwaoi_world *w) {
     for (const Run &r : w->runs)
         if (uniq && (!r.device || r.kind != RUN_MOVE || r.dseq || r.dsp)) uniq = false;
     const gw::MoveRun *mark = moves_only && !bucketed && !uniq ? &RS.r[0] : nullptr;
-    // the first run's claims stored already, beside the previous flush (GWAOI_F_BATCH_READY)
-    if (moves_only && !bucketed && w->premark.on && w->premark.tick == tick_id && w->premark.ds == RS.r[0].ds &&
-        w->premark.n == RS.r[0].n) {
-        HIP_TRY(hipStreamWaitEvent(st, w->mark_ev, 0));
-        if (mark) w->dbg.premarked_runs++;
-        mark = nullptr;
-    }
     if (uniq) w->dbg.unique_flushes++;
     const uint32_t n_unique = uniq ? (uint32_t)n_ops : 0u;
-    w->premark.on = false;
     const uint32_t n_copy = virt ? 0u : n_prev;
     // a unique-moves flush on the previous grid has no prologue: its apply writes only
     // sc->err_apply / ndrop (zero whenever a flush begins) and keygen does the zeroing (TickZero)
     gw::TickZero tz{};
-    if (uniq && incr && w->skip_prologue) {
+    if (uniq && incr) {
         tz.sc = S.sc;
         tz.z1 = w->tile_total;
         tz.n1 = (uint32_t)gw::tile_total_elems(entries);
@@ -1009,7 +976,7 @@ int tick_launch(gwaoi_world *w) {
     if (bucketed) {  // the per-tick position sync: ops regrouped by slot bucket, last op per slot in LDS
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
-    } else if (moves_only) {  // one pass + fixup of repeated slots (run 0's claims: prologue or premark)
+    } else if (moves_only) {  // one pass + fixup of repeated slots (run 0's claims: the prologue)
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                          P.rec, n_prev, S.sc, w->coll, 1u, uniq, st);
     } else if (n_ops) {
@@ -1055,10 +1022,6 @@ int tick_launch(gwaoi_world *w) {
         }
     }
     stage_end(w, S, ST_APPLY);
-    if (w->batch_ready && !w->premark_late) {  // from here on this flush no longer reads the claims
-        HIP_TRY(hipEventRecord(w->apply_ev, st));
-        w->apply_ev_valid = true;
-    }
 
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
@@ -1067,10 +1030,9 @@ int tick_launch(gwaoi_world *w) {
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;
-    // the special pass rides on the sort's arrival launch (k_arrive_special) unless it is timed or
-    // runs on the side stream (A/Bs); launch_pair_passes then skips its own launch
-    const bool sp_fused = incr && w->special_fused && !w->special_side && !(w->timing_mask >> ST_SPECIAL & 1u) &&
-                          n_prev > 0;
+    // the special pass rides on the sort's arrival launch (k_arrive_special) unless it is timed;
+    // launch_pair_passes then skips its own launch
+    const bool sp_fused = incr && !(w->timing_mask >> ST_SPECIAL & 1u) && n_prev > 0;
     gw::SpecialJob spj{};
     if (sp_fused) {
         const uint32_t TBn = gw::combined_tiles(n_new), TBp = gw::combined_blocks(n_prev);
@@ -1080,7 +1042,7 @@ int tick_launch(gwaoi_world *w) {
         spj.seq_base = seq_base;
         spj.sc = S.sc;
         spj.tmp = reinterpret_cast<uint2 *>(w->events_tmp);
-        spj.cap = std::min(S.ev_cap, w->evtmp_cap);
+        spj.cap = w->evtmp_cap;
         spj.tile_total = w->tile_total;
         spj.tile_base = w->tile_base;
         spj.tile_off = TBn;
@@ -1124,13 +1086,8 @@ int tick_launch(gwaoi_world *w) {
         stage_end(w, S, ST_CELLS);
     }
 
-    // the next batch's claims beside the pair passes instead (GWAOI_PREMARK_LATE=1: A/B)
-    if (w->batch_ready && w->premark_late) {
-        HIP_TRY(hipEventRecord(w->apply_ev, st));
-        w->apply_ev_valid = true;
-    }
     // ---- pair passes: combined over the new grid, special entities over the previous one
-    const uint64_t ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view, false, sp_fused);
+    const EvCaps ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view, false, sp_fused);
 
     // from here on the device has rewritten SlotInfo for the new frame: any failure before the
     // commit below leaves the world inconsistent (poisoned)
@@ -1164,12 +1121,8 @@ int tick_launch(gwaoi_world *w) {
     return GWAOI_OK;
 }
 
-// Wait for a flush's summary: blocks on its event (GWAOI_BLOCKING_SYNC=1) or polls it.
+// Wait for a flush's summary: polls its event (a blocking wait adds tens of microseconds of wake-up).
 int wait_done(gwaoi_world *w, hipEvent_t ev) {
-    if (w->blocking_sync) {
-        HIP_TRY(hipEventSynchronize(ev));
-        return GWAOI_OK;
-    }
     hipError_t e;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
     HIP_TRY(e);
@@ -1235,14 +1188,14 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
         w->last_error = "more than 2^32-1 events in one flush";
         return poison(w, GWAOI_ECAPACITY);
     }
-    // compared with the capacity the passes had at launch: a regrow by another flush since then
-    // (shared scratch, or the twin set's catch-up) does not make the clipped events complete
+    // compared with the capacities the passes had at launch: a regrow by another flush since then
+    // (shared scratch, or the twin set's catch-up) does not make the clipped events complete.
     // The scratch extent is not the event count: the pair passes deal their pairs to the event
     // streams by the XCD each block lands on, so a re-run's extent may differ from the overflowed
     // run's.  The first re-run is sized for the extent seen; a second one for the worst case (every
-    // pair in one stream), which cannot overflow.
-    uint64_t cap_used = f.cap;
-    for (int attempt = 0; r.total64 > cap_used; ++attempt) {  // grow and re-run the pair passes
+    // pair in one stream), which cannot overflow.  The set's buffer is sized by the count.
+    EvCaps cap_used = f.cap;
+    for (int attempt = 0; r.total64 > cap_used.out || r.ext64 > cap_used.tmp; ++attempt) {  // grow, re-run
         stage_collect(w, S);
         if (w->inject_regrow_fail) {
             w->last_error = "event buffer regrow failed (injected)";
@@ -1252,13 +1205,14 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
             w->last_error = "pair passes re-run: the event extent exceeds its worst-case bound";
             return poison(w, GWAOI_EDEVICE);
         }
-        const uint64_t need = attempt == 0 ? r.total64 : std::max<uint64_t>(r.total64, gw::ev_worst_extent(r.n_total));
-        if ((rc = ensure_events(w, S, need))) return poison(w, rc);
+        const uint64_t need = attempt == 0 ? r.ext64 : std::max<uint64_t>(r.ext64, gw::ev_worst_extent(r.total64));
+        if ((rc = ensure_events(w, S, r.total64, need))) return poison(w, rc);
         (void)hipGetLastError();  // a failure of an unrelated earlier call is not this re-run's
         gw::launch_zero(w->tile_total, gw::tile_total_elems(f.entries), st);
         gw::launch_zero(&S.sc->shard[0][0], gw::EV_SHARDS * 32, st);  // event streams
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
-        if ((cap_used = launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true)) < need) {
+        cap_used = launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true);
+        if (cap_used.tmp < need || cap_used.out < r.total64) {
             w->last_error = "pair passes re-run: event buffers did not grow";
             return poison(w, GWAOI_EDEVICE);
         }
@@ -1319,24 +1273,22 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
                               "rules, or an internal error)";
         return poison(w, GWAOI_EDEVICE);
     }
-    if (r.err & gw::ERR_DUP_SLOT) {
-        w->last_error = "GWAOI_F_UNIQUE_MOVES: a slot was moved twice in one flush (its position is one of its "
-                        "moves, not necessarily the last)";
-        return GWAOI_ESTATE;
-    }
-    if (r.err & gw::ERR_NONFINITE) {
-        w->last_error = "device batch held a non-finite coordinate (move dropped)";
-        return GWAOI_ENONFINITE;
-    }
-    if (r.err & gw::ERR_SEQ) {
-        w->last_error = "device batch held an explicit seq below the flush's floor (op dropped)";
-        return GWAOI_EINVAL;
-    }
-    if (r.err & (gw::ERR_MOVE_DEAD | gw::ERR_BAD_SLOT)) {
-        w->last_error = "device batch moved a slot that is not live (move dropped)";
-        return GWAOI_ESTATE;
-    }
-    return GWAOI_OK;
+    // every problem of the flush goes into last_error; the status is the first one's
+    int st_err = GWAOI_OK;
+    std::string msg;
+    auto note = [&](uint32_t bits, int code, const char *text) {
+        if (!(r.err & bits)) return;
+        if (st_err == GWAOI_OK) st_err = code;
+        msg += msg.empty() ? text : std::string("; ") + text;
+    };
+    note(gw::ERR_DUP_SLOT, GWAOI_ESTATE,
+         "GWAOI_F_UNIQUE_MOVES: a slot was moved twice in one flush (its position is unspecified: in practice one "
+         "of its moves, not necessarily the last)");
+    note(gw::ERR_NONFINITE, GWAOI_ENONFINITE, "device batch held a non-finite coordinate (move dropped)");
+    note(gw::ERR_SEQ, GWAOI_EINVAL, "device batch held an explicit seq below the flush's floor (op dropped)");
+    note(gw::ERR_MOVE_DEAD | gw::ERR_BAD_SLOT, GWAOI_ESTATE, "device batch moved a slot that is not live (move dropped)");
+    if (st_err != GWAOI_OK) w->last_error = msg;
+    return st_err;
 }
 
 int tick_finish(gwaoi_world *w, bool *committed) { return finish_flight(w, w->fl, false, committed); }
@@ -1367,16 +1319,36 @@ int sparse_try(gwaoi_world *w) {
     const int set = w->launch_set;
     FlushSet &S = w->fs[set];
     int rc;
-    if (!w->sp_cnt && (rc = dalloc(w, &w->sp_cnt, gw::sparse_cnt_elems((uint32_t)kSparseMaxOps)))) return rc;
+    // the sparse flush is optional: a failed allocation of its buffers turns it off, and the full
+    // flush runs over the same queue (nothing was launched yet)
+    auto give_up = [&]() {
+        w->sparse_on = false;
+        w->dbg.sparse_declined++;
+        return 1;
+    };
+    if (!w->sp_cnt && dalloc(w, &w->sp_cnt, gw::sparse_cnt_elems((uint32_t)kSparseMaxOps)) != GWAOI_OK) return give_up();
+    if (!run.device && !w->h_sp_ops) {  // the host ops' one pinned upload buffer
+        if (hipHostMalloc((void **)&w->h_sp_ops, kSpOpsBytes, hipHostMallocDefault) != hipSuccess) {
+            w->h_sp_ops = nullptr;
+            return give_up();
+        }
+        if (dalloc(w, &w->d_sp_ops, kSpOpsBytes) != GWAOI_OK) return give_up();
+    }
+    const bool fused = w->sparse_fused && k <= gw::sparse_fused_max();
+    if (fused && !w->sp_scr) {
+        if (dalloc(w, &w->sp_scr, (size_t)gw::sparse_fused_max() * 2 * w->sp_scr_cap) != GWAOI_OK ||
+            dalloc(w, &w->sp_done, 1) != GWAOI_OK) {
+            dfree(w->sp_scr);
+            w->sparse_fused = false;  // the kernel sequence needs neither
+        } else {
+            HIP_TRY(hipMemsetAsync(w->sp_done, 0, sizeof(uint32_t), st));
+        }
+    }
     if (w->out_pending) HIP_TRY(hipStreamWaitEvent(st, w->out_ev, 0));  // a copy-out still reads S's events
     const uint32_t *d_slot = run.ds;
     const float *d_x = run.dx, *d_z = run.dz;
     const unsigned long long *d_seq = nullptr;
     if (!run.device) {  // one pinned upload (four pageable copies cost ~8 us each)
-        if (!w->h_sp_ops) {
-            HIP_TRY(hipHostMalloc((void **)&w->h_sp_ops, kSpOpsBytes, hipHostMallocDefault));
-            if ((rc = dalloc(w, &w->d_sp_ops, kSpOpsBytes))) return rc;
-        }
         std::memcpy(w->h_sp_ops + kSpSeq, w->h_op_seq.data(), k * 8);
         std::memcpy(w->h_sp_ops + kSpSlot, w->h_op_slot.data(), k * 4);
         std::memcpy(w->h_sp_ops + kSpX, w->h_op_x.data(), k * 4);
@@ -1412,15 +1384,9 @@ int sparse_try(gwaoi_world *w) {
         }
         return GWAOI_OK;
     };
-    const bool fused = w->sparse_fused && k <= gw::sparse_fused_max();
-    if (fused && !w->sp_scr) {
-        if ((rc = dalloc(w, &w->sp_scr, (size_t)gw::sparse_fused_max() * 2 * w->sp_scr_cap)) ||
-            (rc = dalloc(w, &w->sp_done, 1)))
-            return rc;
-        HIP_TRY(hipMemsetAsync(w->sp_done, 0, sizeof(uint32_t), st));
-    }
-    if ((rc = run_sparse(fused))) return rc;
-    if (fused && tick_out(S)->pad == 3u) {  // an op outgrew its scratch row: the kernel sequence
+    const bool use_fused = fused && w->sparse_fused;
+    if ((rc = run_sparse(use_fused))) return rc;
+    if (use_fused && tick_out(S)->pad == 3u) {  // an op outgrew its scratch row: the kernel sequence
         w->dbg.sparse_unfused++;
         if ((rc = run_sparse(false))) return rc;
     }
@@ -1532,14 +1498,6 @@ int gwaoi_world_destroy(gwaoi_world *w) {
         if (w->h_stage[h]) (void)hipHostFree(w->h_stage[h]);
         dfree(w->d_stage[h]);
     }
-    if (w->side_st) (void)hipStreamSynchronize(w->side_st);
-    if (w->side_fork) (void)hipEventDestroy(w->side_fork);
-    if (w->side_join) (void)hipEventDestroy(w->side_join);
-    if (w->side_st) (void)hipStreamDestroy(w->side_st);
-    if (w->mark_st) (void)hipStreamSynchronize(w->mark_st);
-    if (w->apply_ev) (void)hipEventDestroy(w->apply_ev);
-    if (w->mark_ev) (void)hipEventDestroy(w->mark_ev);
-    if (w->mark_st) (void)hipStreamDestroy(w->mark_st);
     if (w->copy_ev) (void)hipEventDestroy(w->copy_ev);
     if (w->copy_st) (void)hipStreamDestroy(w->copy_st);
     if (w->out_st) (void)hipStreamSynchronize(w->out_st);
@@ -1567,14 +1525,14 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     w->cells_auto = !(cfg->cells_per_dist > 0.f);
     w->timing_mask = (cfg->flags & GWAOI_F_TIMING) ? (1u << ST_N) - 1u : 0u;
     w->sparse_on = !(cfg->flags & GWAOI_F_NO_SPARSE);
-    if (const char *e = std::getenv("GWAOI_SPARSE")) w->sparse_on = w->sparse_on && e[0] != '0';
-    if (const char *e = std::getenv("GWAOI_SPARSE_FUSED")) w->sparse_fused = e[0] != '0';
-    if (const char *e = std::getenv("GWAOI_STAGE_MIN")) w->stage_min = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
-    if (const char *e = std::getenv("GWAOI_SPARSE_SCR")) w->sp_scr_cap = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
-    if (const char *e = std::getenv("GWAOI_FORCE_RADIX")) w->force_radix = e[0] == '1';
-    if (const char *e = std::getenv("GWAOI_FORCE_COPY")) w->force_copy = e[0] == '1';
-    if (const char *e = std::getenv("GWAOI_INJECT_REGROW_FAIL")) w->inject_regrow_fail = e[0] == '1';
-    if (const char *e = std::getenv("GWAOI_STAGE_THREADS")) w->stage_threads = (unsigned)std::max(1, std::atoi(e));
+    // GWAOI_F_BATCH_READY is accepted and has no effect (include/gwaoi.h)
+    w->unique_moves = (cfg->flags & GWAOI_F_UNIQUE_MOVES) != 0;
+    w->sparse_fused = !(cfg->flags & GWAOI_F_TEST_SPARSE_SEQUENCE);
+    if (cfg->flags & GWAOI_F_TEST_SPARSE_SCR2) w->sp_scr_cap = 2;
+    w->force_radix = (cfg->flags & GWAOI_F_TEST_FORCE_RADIX) != 0;
+    w->force_copy = (cfg->flags & GWAOI_F_TEST_FORCE_COPY) != 0;
+    w->inject_regrow_fail = (cfg->flags & GWAOI_F_TEST_REGROW_FAIL) != 0;
+    w->check_stages = (cfg->flags & GWAOI_F_TEST_CHECK_STAGES) != 0;
     int rc = GWAOI_OK;
     auto fail = [&](int code) {
         gwaoi_world_destroy(w);
@@ -1611,22 +1569,6 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         w->out_ev = nullptr;
         return fail(GWAOI_EDEVICE);
     }
-    if (hipStreamCreateWithFlags(&w->side_st, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&w->side_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&w->side_join, hipEventDisableTiming) != hipSuccess)
-        return fail(GWAOI_EDEVICE);
-    if (const char *e = std::getenv("GWAOI_SPECIAL_SIDE")) w->special_side = e[0] == '1';
-    w->batch_ready = (cfg->flags & GWAOI_F_BATCH_READY) != 0;
-    if (const char *e = std::getenv("GWAOI_BATCH_READY")) w->batch_ready = w->batch_ready && e[0] != '0';  // A/B
-    if (const char *e = std::getenv("GWAOI_PREMARK_LATE")) w->premark_late = e[0] == '1';
-    w->unique_moves = (cfg->flags & GWAOI_F_UNIQUE_MOVES) != 0;
-    if (const char *e = std::getenv("GWAOI_UNIQUE_MOVES")) w->unique_moves = w->unique_moves && e[0] != '0';  // A/B
-    if (const char *e = std::getenv("GWAOI_SKIP_PROLOGUE")) w->skip_prologue = e[0] != '0';  // A/B
-    if (const char *e = std::getenv("GWAOI_SPECIAL_FUSED")) w->special_fused = e[0] != '0';  // A/B
-    if (w->batch_ready && (hipStreamCreateWithFlags(&w->mark_st, hipStreamNonBlocking) != hipSuccess ||
-                           hipEventCreateWithFlags(&w->apply_ev, hipEventDisableTiming) != hipSuccess ||
-                           hipEventCreateWithFlags(&w->mark_ev, hipEventDisableTiming) != hipSuccess))
-        return fail(GWAOI_EDEVICE);
     const size_t N = w->max_slots;
     for (DevFrame &f : w->fr) {
         if ((rc = dalloc(w, &f.rec, N)) || (rc = dalloc(w, &f.ss, N)) || (rc = dalloc(w, &f.key, N)) ||
@@ -1668,14 +1610,12 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess ||  // no order yet
         hipMemset(w->ework, 0, N * sizeof(uint32_t)) != hipSuccess)
         return fail(GWAOI_EDEVICE);
-    if (const char *e = std::getenv("GWAOI_TILE_ORDER")) w->tile_order_on = e[0] != '0';
     // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
     if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
         hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
         return fail(GWAOI_EDEVICE);
-    // the bucketed apply for worlds whose SlotInfo outgrows the MALL (GWAOI_MOVES_BUCKETED=0/1 forces it)
-    w->moves_bucketed = N > gw::MV_MIN_SLOTS;
-    if (const char *e = std::getenv("GWAOI_MOVES_BUCKETED")) w->moves_bucketed = e[0] == '1';
+    // the bucketed apply for worlds whose SlotInfo outgrows the MALL (GWAOI_F_TEST_BUCKETED forces it)
+    w->moves_bucketed = N > gw::MV_MIN_SLOTS || (cfg->flags & GWAOI_F_TEST_BUCKETED);
     size_t mv_hist_n = 0;
     if (w->moves_bucketed && gw::moves_buckets((uint32_t)N) <= gw::MV_NB_MAX) {
         mv_hist_n = std::max(gw::moves_hist_elems((uint32_t)N, (uint32_t)N),
@@ -1687,15 +1627,14 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     for (FlushSet &S : w->fs)
-        if ((rc = ensure_events(w, S, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
+        if ((rc = ensure_events(w, S, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16),
+                                cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16))))
             return fail(rc);
     if (hipHostMalloc((void **)&w->h_grid, sizeof(SpaceGrid) * w->max_spaces, hipHostMallocDefault) != hipSuccess)
         return fail(GWAOI_ENOMEM);
     if (hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&w->order_ev, hipEventDisableTiming) != hipSuccess)
         return fail(GWAOI_EDEVICE);
-    if (const char *e = std::getenv("GWAOI_BLOCKING_SYNC")) w->blocking_sync = e[0] == '1';
-    if (const char *e = std::getenv("GWAOI_CHECK_STAGES")) w->check_stages = e[0] == '1';
     w->alive.assign(N, 0);
     w->in_frame.assign(N, 0);
     w->appended.assign(N, 0);
@@ -1922,6 +1861,7 @@ size_t stage_chunk(const gwaoi_world *w, const uint32_t *slots, const float *x, 
 // seq_next.. and the slot's space at call time (explicit, so a slot that entered earlier in this
 // flush moves exactly as a host op would).  Nothing is queued if any move is rejected.
 constexpr size_t kStageThreadMin = 1 << 16;  // moves per extra thread
+constexpr size_t kStageMin = 64;             // host move batches of this many moves or more are staged
 
 int stage_moves(gwaoi_world *w, const uint32_t *slots, const float *x, const float *z, size_t n) {
     const int half = w->stage_cur;
@@ -2075,9 +2015,9 @@ int gwaoi_moved_batch(gwaoi_world *w, const uint32_t *slots, const float *x, con
     GW_LIVE(w);
     if (w->dev_seq_pending) return GWAOI_ESTATE;
     if (int rc = host_slots(w)) return rc;
-    // Batches of stage_min+ moves go through pinned staging as one device batch (single-pass
+    // Batches of kStageMin+ moves go through pinned staging as one device batch (single-pass
     // move apply); without room (or if the staging allocation failed) they queue as host ops.
-    if (n >= w->stage_min && n <= 0xFFFFFFFFull - w->n_ops && ensure_stage(w, 4 * n) == GWAOI_OK)
+    if (n >= kStageMin && n <= 0xFFFFFFFFull - w->n_ops && ensure_stage(w, 4 * n) == GWAOI_OK)
         return stage_moves(w, slots, x, z, n);
     for (size_t i = 0; i < n; ++i) {
         if (slots[i] >= w->max_slots) return GWAOI_EBADSLOT;
@@ -2107,21 +2047,6 @@ int gwaoi_moved_batch_device(gwaoi_world *w, const uint32_t *d_slots, const floa
     r.dn = n;
     w->seq_next += n;
     if (w->in_flight) {
-        // the next flush's first run (nothing else deferred yet): its claims beside the flush in
-        // flight, once that flush's apply is done (the batch is complete: GWAOI_F_BATCH_READY)
-        if (w->batch_ready && w->deferred.empty() && w->apply_ev_valid && !w->mv_binned &&
-            w->fl.tick_id == w->tick_id) {
-            gw::MoveRun m{};
-            m.ds = d_slots; m.dx = d_x; m.dz = d_z; m.seq0 = r.seq0; m.sp_def = gw::SP_KEEP;
-            m.j0 = 0; m.n = (uint32_t)n;
-            HIP_TRY(hipStreamWaitEvent(w->mark_st, w->apply_ev, 0));
-            gw::launch_moves_mark(m, w->max_slots, w->sinfo, w->tick_id + 1, w->mark_st);
-            HIP_TRY(hipEventRecord(w->mark_ev, w->mark_st));
-            w->premark.on = true;
-            w->premark.tick = w->tick_id + 1;
-            w->premark.ds = d_slots;
-            w->premark.n = n;
-        }
         Deferred q{};
         q.kind = Deferred::RUN;
         q.run = r;
@@ -2396,7 +2321,7 @@ void world_flush_events(gwaoi_world *w, const uint32_t **events, const uint32_t 
     FlushSet &S = w->fs[w->in_flight ? w->fl.set : w->last_set];
     *events = S.events;
     *dcount = reinterpret_cast<const uint32_t *>(S.dev_out);
-    *cap = w->in_flight ? w->fl.cap : std::min(S.ev_cap, w->evtmp_cap);
+    *cap = w->in_flight ? w->fl.cap.out : S.ev_cap;  // events the set's buffer holds (clipped to it)
 }
 
 uint32_t world_slot_space(gwaoi_world *w, uint32_t slot) {

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GWAOI_ABI_VERSION 4  /* 4: the six flush-ending calls folded into gwaoi_tick_finish */
+#define GWAOI_ABI_VERSION 5  /* 5: GWAOI_F_TEST_* flags replace environment switches; GWAOI_F_BATCH_READY ignored */
 
 typedef struct gwaoi_world gwaoi_world;
 
@@ -79,21 +79,29 @@ typedef struct {
 
 #define GWAOI_F_TIMING 1u /* time every pipeline stage with HIP events (gwaoi_stage_times) */
 #define GWAOI_F_NO_SPARSE 2u /* never take the sparse flush (every flush rebuilds the frame; A/B, tests) */
-/* Device Moved batches (gwaoi_moved_batch_device) are complete in memory when passed, not
- * produced on another stream behind gwaoi_stream_after: a batch queued while a flush is in
- * flight then has its last-op claims stored beside that flush, off the next flush's path.
- * Measured slower at 1M entities (the claims kernel slows the flush it runs beside more than it
- * saves the next one: DESIGN.md §3 step 1); for hosts whose GPU idles between flushes. */
+/* Accepted for compatibility and ignored since ABI 5.  (Until then: the next flush's last-op
+ * claims stored beside the flush in flight.  Measured slower at 1M entities, DESIGN.md §3 step 1,
+ * and removed with the side stream it needed.) */
 #define GWAOI_F_BATCH_READY 4u
 /* The Moved batches of one flush never name a slot twice (a per-tick position array with one
  * entry per moving entity).  A flush of plain device Moved batches (gwaoi_moved_batch_device,
  * or gwaoi_moved_batch's staged batches) then applies every move without the last-op claims
  * and the repeated-slot fixup.  The promise is checked on the device: keygen counts the frame
  * entries the moves wrote, and a flush with fewer than its moves commits, with the repeated
- * slot at the position of one of its moves (not necessarily the last), and returns
- * GWAOI_ESTATE.  Batches with explicit seqs, decoded sync batches and mixed queues keep the
+ * slot's position unspecified (each move writes its 16-B record with one store, so in practice
+ * one of its moves, not necessarily the last), and returns GWAOI_ESTATE (gwaoi_last_error also
+ * names any other problem the device found in that flush).  Batches with explicit seqs, decoded sync batches and mixed queues keep the
  * claims.  Measured at 1M entities: DESIGN.md §3 step 2. */
 #define GWAOI_F_UNIQUE_MOVES 8u
+/* Test and diagnostics flags: they select a slower or failing path so that tests can compare
+ * it with the default one.  Not for production worlds. */
+#define GWAOI_F_TEST_FORCE_RADIX 0x100u      /* every flush sorts the frame with the full radix sort  */
+#define GWAOI_F_TEST_FORCE_COPY 0x200u       /* S' is always copied from the previous frame            */
+#define GWAOI_F_TEST_BUCKETED 0x400u         /* Moved batches take the bucketed apply at any size       */
+#define GWAOI_F_TEST_REGROW_FAIL 0x800u      /* an event-buffer regrow fails (the poison path)          */
+#define GWAOI_F_TEST_SPARSE_SEQUENCE 0x1000u /* the sparse flush runs its kernel sequence, not one launch */
+#define GWAOI_F_TEST_SPARSE_SCR2 0x2000u     /* sparse one-launch scratch rows of 2 events per kind     */
+#define GWAOI_F_TEST_CHECK_STAGES 0x4000u    /* wait after every flush stage (names a faulting stage)   */
 
 typedef struct {
     uint64_t n_enter;      /* directed enter events; replay pair (a,b) as a.OnEnterAOI(b) */
@@ -130,7 +138,7 @@ typedef struct {
     uint64_t incremental_sorts;     /* flush launches whose frame sort was the per-cell merge (grid unchanged) */
     uint64_t sparse_flushes;        /* flushes of a few Moved calls done on the frame in place (gwaoi_tick*) */
     uint64_t sparse_declined;       /* sparse flushes that fell back to the full one (long shifts, capacity)  */
-    uint64_t premarked_runs;        /* flushes whose first batch's claims were stored beside the flush before */
+    uint64_t premarked_runs;        /* always 0 since ABI 5 (GWAOI_F_BATCH_READY is ignored)                 */
     uint64_t sparse_unfused;        /* sparse flushes that ran the kernel sequence (an op outgrew its row)    */
     uint64_t unique_flushes;        /* flushes applied without last-op claims (GWAOI_F_UNIQUE_MOVES)          */
 } gwaoi_debug;

@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 
 from goworld_amd import World, GwaoiError, pair_keys
+from goworld_amd._lib import (GWAOI_F_TEST_BUCKETED, GWAOI_F_TEST_FORCE_COPY, GWAOI_F_TEST_FORCE_RADIX,
+                              GWAOI_F_TEST_REGROW_FAIL, GWAOI_F_TEST_SPARSE_SCR2, GWAOI_F_TEST_SPARSE_SEQUENCE)
 from goworld_amd.workload import make_workload
 
 pytestmark = pytest.mark.gpu
@@ -489,16 +491,15 @@ def test_device_batch_repeated_slots_gpu():
             np.testing.assert_array_equal(wa.neighbors(i), wb.neighbors(i))
 
 
-@pytest.mark.parametrize("bucketed", ["0", "1"])
-def test_device_batches_many_buckets_vs_closed_form_gpu(oracle_mod, monkeypatch, bucketed):
-    """Moves-only flushes through the global-claim apply and (GWAOI_MOVES_BUCKETED=1)
+@pytest.mark.parametrize("bucketed", [False, True])
+def test_device_batches_many_buckets_vs_closed_form_gpu(oracle_mod, bucketed):
+    """Moves-only flushes through the global-claim apply and (GWAOI_F_TEST_BUCKETED)
     the bucketed one (slots regrouped by 4096-slot bucket, last op per slot by LDS
     claim): live slots scattered over 14 buckets, three device batches per flush
     with slots repeated inside a batch and across batches, one batch with
     explicit seqs.  Last call wins (Space.go:259 in call order); events vs the
     closed form."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("GWAOI_MOVES_BUCKETED", bucketed)
     O = oracle_mod
     rng = np.random.default_rng(77)
     N = 57000
@@ -510,7 +511,7 @@ def test_device_batches_many_buckets_vs_closed_form_gpu(oracle_mod, monkeypatch,
     sp = np.full(N, O.DEAD, np.uint32)
     x[live] = rng.uniform(-L / 2, L / 2, live.size).astype(np.float32)
     z[live] = rng.uniform(-L / 2, L / 2, live.size).astype(np.float32)
-    with World(N) as w:
+    with World(N, test_flags=GWAOI_F_TEST_BUCKETED if bucketed else 0) as w:
         s = w.space_create(D)
         w.enter_batch(s, live, x[live], z[live])
         seq[live] = 1 + np.arange(live.size, dtype=np.uint64)
@@ -645,16 +646,14 @@ def test_mixed_churn_vs_closed_form_gpu(oracle_mod, seed, spaces):
 
 
 @pytest.mark.parametrize("cfg,n", [("cfg3", 60000), ("cfg2", 30000)])
-def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
+def test_incremental_sort_equals_radix_gpu(cfg, n):
     """The incremental frame sort (grid unchanged) is the stable sort by cell
     key: the flush's event arrays -- order included -- equal those of the
     full radix-sort path (GWAOI_FORCE_RADIX=1), with churn in every flush."""
     rng = np.random.default_rng(9)
     wl = make_workload(cfg, n=n)
     slots, x0, z0, _ = wl.initial()
-    monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
-    wr = World(n + 500)
-    monkeypatch.delenv("GWAOI_FORCE_RADIX")
+    wr = World(n + 500, test_flags=GWAOI_F_TEST_FORCE_RADIX)
     wi = World(n + 500)
     try:
         for w in (wr, wi):
@@ -693,16 +692,15 @@ def test_incremental_sort_equals_radix_gpu(monkeypatch, cfg, n):
 
 
 @pytest.mark.parametrize("n", [255, 257, 4095, 4097, 16383, 16385, 32769])
-def test_chain_free_offsets_at_tile_boundaries_gpu(monkeypatch, oracle_mod, n):
+def test_chain_free_offsets_at_tile_boundaries_gpu(oracle_mod, n):
     """Frame sizes either side of the block boundaries of the chain-free offsets (the cell scan's
     tiles, k_finish's groups of 256 tile entries, the combined pass's tiles): three churned
     flushes, incremental and radix paths equal (order included) and equal to the oracle."""
     rng = np.random.default_rng(n)
     wl = make_workload("cfg2", n=n)
     slots, x0, z0, _ = wl.initial()
-    monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
-    wr = World(n, cells_per_dist=3.0, sparse=False)  # full flushes only: the sort paths are the subject
-    monkeypatch.delenv("GWAOI_FORCE_RADIX")
+    wr = World(n, cells_per_dist=3.0, sparse=False,  # full flushes only: the sort paths are the subject
+               test_flags=GWAOI_F_TEST_FORCE_RADIX)
     wi = World(n, cells_per_dist=3.0, sparse=False)
     ref = oracle_mod.SpacesOracle({0: wl.D}, n)
     try:
@@ -735,7 +733,7 @@ def test_chain_free_offsets_at_tile_boundaries_gpu(monkeypatch, oracle_mod, n):
         wi.close()
 
 
-def test_incremental_sort_pileup_gpu(monkeypatch, oracle_mod):
+def test_incremental_sort_pileup_gpu(oracle_mod):
     """Crowds piling into and draining out of a few cells, grid unchanged: hot cells
     get hundreds of arrivals a flush -- from below and above their previous run in S'
     order, and appended entries -- while others lose most of their run.  k_cell_merge's
@@ -747,9 +745,8 @@ def test_incremental_sort_pileup_gpu(monkeypatch, oracle_mod):
     z = rng.uniform(-L / 2, L / 2, n).astype(np.float32)
     x[:4], z[:4] = [-L / 2, L / 2, -L / 2, L / 2], [-L / 2, -L / 2, L / 2, L / 2]  # fixed corners: same grid
     hot = np.array([[-700.0, 300.0], [0.0, 0.0], [650.0, -420.0]], np.float32)
-    monkeypatch.setenv("GWAOI_FORCE_RADIX", "1")
-    wr = World(n + 400, cells_per_dist=3.0)  # a fixed cell size: the grid stays the same all along
-    monkeypatch.delenv("GWAOI_FORCE_RADIX")
+    wr = World(n + 400, cells_per_dist=3.0,  # a fixed cell size: the grid stays the same all along
+               test_flags=GWAOI_F_TEST_FORCE_RADIX)
     wi = World(n + 400, cells_per_dist=3.0)
     ref = oracle_mod.SpacesOracle({0: D}, n + 400)
     try:
@@ -799,7 +796,7 @@ def test_incremental_sort_pileup_gpu(monkeypatch, oracle_mod):
         wi.close()
 
 
-def test_virtual_sprime_equals_copied_sprime_gpu(monkeypatch):
+def test_virtual_sprime_equals_copied_sprime_gpu():
     """A flush of Moved batches only skips the prologue's copy of the previous
     frame (k_keygen takes the records no op wrote from the previous frame, by
     their seq).  Its event arrays -- order included -- and neighbour rows equal
@@ -812,9 +809,7 @@ def test_virtual_sprime_equals_copied_sprime_gpu(monkeypatch):
     wl = make_workload("cfg3", n=30000)
     slots, x0, z0, _ = wl.initial()
     n = wl.n
-    monkeypatch.setenv("GWAOI_FORCE_COPY", "1")
-    wc = World(n + 200)
-    monkeypatch.delenv("GWAOI_FORCE_COPY")
+    wc = World(n + 200, test_flags=GWAOI_F_TEST_FORCE_COPY)
     wv = World(n + 200)
 
     def both(fn):
@@ -939,13 +934,11 @@ def test_committed_events_delivered_on_device_error_gpu():
         assert ent.size == 2 and lev.size == 16
 
 
-def test_failed_event_regrow_poisons_world_gpu(monkeypatch):
+def test_failed_event_regrow_poisons_world_gpu():
     """A failure after the flush's kernels rewrote the per-slot records but
     before the commit (here an injected failure of the event-buffer regrow)
     leaves host and device apart: the world refuses every later call."""
-    monkeypatch.setenv("GWAOI_INJECT_REGROW_FAIL", "1")
-    w = World(64, event_capacity=16)
-    monkeypatch.delenv("GWAOI_INJECT_REGROW_FAIL")
+    w = World(64, event_capacity=16, test_flags=GWAOI_F_TEST_REGROW_FAIL)
     try:
         s = w.space_create(D)
         for i in range(20):
@@ -1132,15 +1125,13 @@ def _device_events(w, ne, nl):
     return out
 
 
-@pytest.mark.parametrize("event_capacity,repeats,ready", [(0, False, False), (3000, False, False), (0, True, False),
-                                                          (0, True, True), (3000, False, True)])
-def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats, ready):
+@pytest.mark.parametrize("event_capacity,repeats", [(0, False), (3000, False), (0, True)])
+def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats):
     """gwaoi_tick_finish(NEXT): the next flush queued before the commit of the one in
     flight (device Moved batches only) gives every flush the events of the serial path -- also when the
     flush in flight overflows its event buffer and is re-run after its successor
     (event_capacity=3000), when a batch moves slots more than once (repeats: the last
-    call wins), and when a host call in flight forces the fallback.  ready
-    (GWAOI_F_BATCH_READY): the next batch's claims are stored beside the flush in flight."""
+    call wins), and when a host call in flight forces the fallback."""
     torch = pytest.importorskip("torch")
     n = 20000
     wa, wb = make_workload("cfg2", n=n), make_workload("cfg2", n=n)
@@ -1162,7 +1153,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats, read
         batches.append([torch.from_numpy(a).to("cuda:0") for a in (sl.astype(np.int32), nx, nz)])
     torch.cuda.synchronize()
     cap = 2 * n if repeats else n  # a speculative launch takes at most max_slots ops
-    with World(cap, event_capacity=event_capacity, batch_ready=ready) as A, World(cap) as B:
+    with World(cap, event_capacity=event_capacity) as A, World(cap) as B:
         for w in (A, B):
             s = w.space_create(wa.D)
             w.enter_batch(s, slots, x0, z0)
@@ -1189,7 +1180,7 @@ def test_speculative_next_flush_matches_serial_gpu(event_capacity, repeats, read
             np.testing.assert_array_equal(pair_keys(la), pair_keys(lb), err_msg=f"tick {t}: leaves")
         d = A.debug_counters()
         assert d["speculative_launches"] >= ticks - 3
-        assert (d["premarked_runs"] >= ticks - 3) if ready else d["premarked_runs"] == 0
+        assert d["premarked_runs"] == 0  # GWAOI_F_BATCH_READY is gone (ABI 5)
         # the two event sets match each other's capacity without outgrowing it (was: x1.25 per flush)
         assert caps[-1] == caps[ticks // 2], caps
         if event_capacity:
@@ -1557,7 +1548,7 @@ def test_zero_copy_batches_match_host_batches_gpu(oracle_mod):
 
 @pytest.mark.parametrize("cfg,n,seed,mode", [("cfg3", 30000, 5, "fused"), ("cfg2", 20000, 9, "fused"),
                                              ("cfg3", 30000, 6, "scr2"), ("cfg2", 20000, 10, "sequence")])
-def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, monkeypatch, cfg, n, seed, mode):
+def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, cfg, n, seed, mode):
     """The sparse flush (a few Moved calls: events against the frame in place, the frame patched
     in place, a cell changer shifted into its new cell) gives exactly the events of the full
     flush and of the sequential oracle, flush after flush; the full flushes in between start
@@ -1566,17 +1557,14 @@ def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, monkeypatc
     shifts are declined (the full flush runs instead).  mode: the one-launch form (fused), the
     same with two-event scratch rows so that busy ops fall back to the kernel sequence (scr2),
     and the kernel sequence alone (GWAOI_SPARSE_FUSED=0)."""
-    if mode == "scr2":
-        monkeypatch.setenv("GWAOI_SPARSE_SCR", "2")
-    if mode == "sequence":
-        monkeypatch.setenv("GWAOI_SPARSE_FUSED", "0")
+    tf = {"scr2": GWAOI_F_TEST_SPARSE_SCR2, "sequence": GWAOI_F_TEST_SPARSE_SEQUENCE}.get(mode, 0)
     wl = make_workload(cfg, n=n, seed=seed)
     slots, x0, z0, _ = wl.initial()
     m = oracle_mod.XZList(wl.D, n)
     rng = np.random.default_rng(seed)
     px, pz = x0.astype(np.float32).copy(), z0.astype(np.float32).copy()
     lo, hi = float(min(px.min(), pz.min())), float(max(px.max(), pz.max()))
-    with World(n) as A, World(n, sparse=False) as B:
+    with World(n, test_flags=tf) as A, World(n, sparse=False) as B:
         for w in (A, B):
             s = w.space_create(wl.D)
             w.enter_batch(s, slots, x0, z0)
@@ -1623,18 +1611,16 @@ def test_sparse_flushes_match_full_flushes_and_oracle_gpu(oracle_mod, monkeypatc
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_sparse_flushes_multi_space_gpu(monkeypatch, fused):
+def test_sparse_flushes_multi_space_gpu(fused):
     """Sparse flushes in a world of several spaces whose coordinates overlap (each space its own
     grid, space-major cells): a mover's partners come from its own space only, and the frame
     patch (shifts into a new cell) keeps every space's cell ranges exact.  Each flush equals the
     full-flush world's; the spaces' sizes differ (one nearly empty), and some moves cross many
     cells."""
-    if not fused:
-        monkeypatch.setenv("GWAOI_SPARSE_FUSED", "0")
     rng = np.random.default_rng(31)
     sizes = [4000, 2500, 7, 1500]
     n = sum(sizes)
-    with World(n + 16, max_spaces=8) as A, World(n + 16, max_spaces=8, sparse=False) as B:
+    with World(n + 16, max_spaces=8, test_flags=0 if fused else GWAOI_F_TEST_SPARSE_SEQUENCE) as A, World(n + 16, max_spaces=8, sparse=False) as B:
         spaces = [(A.space_create(D), B.space_create(D)) for _ in sizes]
         lo = 0
         x = np.empty(n, np.float32)
