@@ -981,7 +981,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 // block's offset from totals written by an earlier launch -- per scan tile (k_scan64_agg)
 // or per group of FG tile entries (the pair passes' atomics) -- summed by the whole block,
 // with no chain between blocks.  Rounds 2-4 used a decoupled look-back instead: its chain
-// cost 10 us in the cell scan and 3.5 us in k_finish per cfg3 tick (profiles/r04_variants_scan.log).
+// cost 10 us in the cell scan and 3.5 us in k_finish per cfg3 tick (profiles/archive/r04_variants_scan.log).
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
@@ -2233,11 +2233,14 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
     }
 }
 
+// The wave's index in its block as a scalar (an SGPR: the per-wave LDS bases then cost no VGPR).
+__device__ __forceinline__ int wave_id() { return (int)__builtin_amdgcn_readfirstlane(threadIdx.x / WAVE); }
+
 __device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
                                const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
                                uint32_t &lw, uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
                                bool replay) {
-    const int w = threadIdx.x / WAVE;
+    const int w = wave_id();
     const SpaceGrid &g = C.g;
     WaveQueue Q{0u, ne, nl, lw};
     const float lo = C.lo, hi = C.hi, M = C.M;
@@ -2334,7 +2337,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     const unsigned long long bt0 = t_start;
 #endif
     const uint32_t tid = threadIdx.x, ln = lane();
-    const int w = tid / WAVE;
+    const int w = wave_id();
     const uint32_t e0 = t * CT;
     if (tid < CW) L.wwork[tid] = L.ndrain[tid] = 0;
     if (tid == 0) L.overflow = 0;
@@ -2343,11 +2346,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
     // A block holds its LDS until its slowest wave ends, so the waves get equal
     // work: the block's entries are ranked by the candidates their lanes swept
     // last flush (stable, by ballots over log2 classes) and dealt round-robin,
-    // rank r to wave r mod 4; lane tid takes entry e0 + perm[tid] (1).
-    // Lock-step sweeps (1=0) run a wave as long as its busiest lane
-    // instead, so there the class is the shape of the entity's strips: whether
-    // the Z strip spans two grid rows and whether the X' strip spans two cells
-    // per row (either happens to ~1 entity in 6), or a whole-window sweep.
+    // rank r to wave r mod 4; lane tid takes entry e0 + perm[tid].
     uint32_t off = tid;
     {
         const uint32_t a = e0 + tid;
@@ -2357,20 +2356,6 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         if (a < F.n) {
             const uint32_t wk = ework ? ework[a] : 0u;
             cls = (uint32_t)(NCLS - 2) - min((uint32_t)(NCLS - 2), (uint32_t)(31 - __clz((int)(wk | 1u))));
-        }
-        if (false) {
-            const uint4 c0 = cand[a];
-            const Rec16 r0 = ld_rec(F.rec, a);
-            const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
-            const float M = (sc->bmax + 3.0f * g.D) * 0x1p-20f, BW = 2.0f * sc->d_rel * g.D + M;
-            const float lo = g.D - BW, hi = g.D + BW;
-            if (__uint_as_float(c0.x) != __uint_as_float(c0.x) || !(lo > 0.f)) {
-                cls = 4;
-            } else {
-                const int zr = cell_of(r0.z + hi + M, g.oz, g.inv, g.gz) - cell_of(r0.z + lo - M, g.oz, g.inv, g.gz);
-                const int xs = cell_of(r0.x + hi + M, g.ox, g.inv, g.gx) - cell_of(r0.x + lo - M, g.ox, g.inv, g.gx);
-                cls = (zr > 0 ? 1u : 0u) | (xs > 0 ? 2u : 0u);
-            }
         }
         unsigned long long mine = 0;
 #pragma unroll

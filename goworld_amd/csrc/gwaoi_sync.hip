@@ -223,7 +223,7 @@ __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, con
 // (Space.go:253-257) and only yaw changes.  Both raise sifSyncNeighborClients.
 // PER records per thread, strided by the block: every slot record is loaded before any is used.
 #ifndef GWAOI_DEC_PER
-#define GWAOI_DEC_PER 2  // records per k_decode thread (2: 102 vs 113 us at 1M records, profiles/r04_variants_sync.log)
+#define GWAOI_DEC_PER 2  // records per k_decode thread (2: 102 vs 113 us at 1M records, profiles/archive/r04_variants_sync.log)
 #endif
 template <int PER>
 __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {

@@ -30,9 +30,9 @@
 
 using gw::SpaceGrid;
 
-// 1: k_finish writes the flush summary (TickOut + per-space boxes) straight into
-// pinned host memory; 0: it writes device memory and a copy follows (a blit
-// kernel of ~4 us per flush at config 3, profiles/r03_trace_base.txt)
+// k_finish writes the flush summary (TickOut + per-space boxes) straight into
+// pinned host memory: a copy after it would be a blit kernel of ~4 us per flush
+// at config 3 (profiles/archive/r03_trace_base.txt)
 
 namespace {
 

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 cd /tmp
-ARGS="--steps 6 --warmup 1 --no-cpu-baseline --host-io-steps 0 --sync-steps 0 --cfg4-steps 0 --cfg5-steps 0 --small-flush-reps 0 --wire-steps 0 --host-tick-steps 0"
+ARGS="--steps 6 --warmup 1 --no-cpu-baseline --host-io-steps 0 --sync-steps 0 --cfg4-steps 0 --cfg5-steps 0 --small-flush-reps 0 --wire-steps 0 --host-tick-steps 0 --claims-steps 0"
 i=0
 for C in "$@"; do
   i=$((i+1))
