@@ -687,7 +687,7 @@ def small_flush_leg(w, last, reps: int, sizes=(1, 64, 4096, 65536)):
     for k in sizes:
         res = {}
         for mode in ("device", "host"):
-            ts, evs, sparse0 = [], [], w.debug_counters().get("sparse_flushes", 0)
+            ts, tq, evs, sparse0 = [], [], [], w.debug_counters().get("sparse_flushes", 0)
             for r in range(reps + 3):
                 idx = rng.choice(sl.size, k, replace=False)
                 x[idx] += rng.uniform(-1.0, 1.0, k).astype(np.float32)
@@ -695,6 +695,7 @@ def small_flush_leg(w, last, reps: int, sizes=(1, 64, 4096, 65536)):
                 bs, bx, bz = sl[idx], x[idx], z[idx]
                 a = time.perf_counter()
                 w.moved_batch(bs, bx, bz)
+                b = time.perf_counter()
                 if mode == "device":
                     ne, nl = w.tick_device()
                 else:
@@ -702,14 +703,18 @@ def small_flush_leg(w, last, reps: int, sizes=(1, 64, 4096, 65536)):
                     ne, nl = len(e), len(l)
                 if r >= 3:
                     ts.append(time.perf_counter() - a)
+                    tq.append(b - a)
                     evs.append(ne + nl)
             t = np.array(ts) * 1e3
+            q = np.array(tq) * 1e3
             res[mode] = {"p50_ms": round(float(np.percentile(t, 50)), 4), "p99_ms": round(float(np.percentile(t, 99)), 4),
                          "mean_ms": round(float(t.mean()), 4), "events_mean": float(np.mean(evs)),
+                         "queue_p50_ms": round(float(np.percentile(q, 50)), 4),
                          "sparse_flushes": w.debug_counters().get("sparse_flushes", 0) - sparse0}
         out[str(k)] = res
     out["note"] = ("one flush of k Moved calls on the 1M-entity config-3 world, wall clock from the host batch call "
-                   "to the events (device: in HBM; host: in host memory); reps per size after 3 untimed")
+                   "to the events (device: in HBM; host: in host memory); reps per size after 3 untimed; "
+                   "queue_p50_ms: the gwaoi_moved_batch call alone (host validation + staging + H2D issue)")
     return out
 
 
