@@ -53,15 +53,16 @@ struct alignas(8) SlotSp {  // caller slot handle + space id (SP_DEAD = not live
     uint32_t slot, sp;
 };
 
-// Per-slot record, indexed by the caller's slot: everything the op kernels
-// look up for a slot in one 16 B line.  lastop = (tick << 32 | op index) of
-// the slot's last op this flush; rank = its index in S' (previous frame
-// order, or appended); sp = its space in S' before this flush's ops
-// (SP_DEAD if not live).
-struct alignas(16) SlotInfo {
-    unsigned long long lastop;
-    uint32_t rank;
-    uint32_t sp;
+// Per-slot table, indexed by the caller's slot, as two arrays: lastop[s] = (tick << 32 | op
+// index) of the slot's last op this flush (the claims path only); rs[s] = {rank, sp}: its index
+// in S' (previous frame order, or appended) and its space in S' before this flush's ops (SP_DEAD
+// if not live).  Two arrays, not one 16-B record, because the hot passes touch one of them per
+// random slot: the unique-moves apply reads rs and the gather writes rs, so their random lines
+// come from an 8 B-per-slot array (half the lines of the record; at 1M slots 8 MB, against
+// 4 MB of L2 per XCD), and only the claims path also touches lastop.
+struct SlotTab {
+    unsigned long long *lastop;
+    uint2 *rs;
 };
 
 // Uniform grid of one space for one flush.  Cell (cx,cz) of space s has the
@@ -154,17 +155,17 @@ struct TickOut {
 // S' entries base .. base+n_app-1 for the entering slots new_slots[] (host-checked, or a device
 // Enter batch: slots out of range or live when the flush began are flagged and left dead).
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t base, Rec16 *s_rec, SlotSp *s_ss,
-                          SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st);
+                          SlotTab info, uint32_t max_slots, TickScalars *sc, hipStream_t st);
 // One run of the op queue: ops j0 .. j0+n-1 of this flush.  sp == nullptr
 // means a device-resident Moved batch (keep the space).  Op i gets seq
 // seqs[i] when seqs is given (explicit: checked >= seq_floor, the largest
 // folded into sc->seq_max when track_max), else seq0 + i.
 void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots,
-                      SlotInfo *info, uint32_t tick_id, TickScalars *sc, hipStream_t st);
+                      SlotTab info, uint32_t tick_id, TickScalars *sc, hipStream_t st);
 // sp == nullptr: every op has space sp_def (SP_KEEP: Moved; a space: Enter; SP_DEAD: Leave, whose
 // x / z may be nullptr).
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t sp_def,
-                      uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+                      uint32_t n, uint32_t j0, uint32_t max_slots, SlotTab info, uint32_t tick_id,
                       uint32_t n_total, const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor,
                       bool track_max, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st);
 // A flush whose queue is only device Moved batches (<= MAX_MOVE_RUNS of them):
@@ -196,14 +197,14 @@ struct FixupArgs {
     MoveRuns RS;
     uint32_t max_slots, tick, n_total, n_prev;
     unsigned long long seq_floor;
-    SlotInfo *info;
+    SlotTab info;
     Rec16 *s_rec;
     SlotSp *s_ss;
     const Rec16 *p_rec;
     TickScalars *sc;
     const uint32_t *coll;
 };
-void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotTab info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, hipStream_t st);
 // The same flush through slot buckets (gwaoi_kernels.hip k_mv_*), for worlds whose
@@ -214,7 +215,7 @@ constexpr uint32_t MV_NB_MAX = 8192;
 constexpr uint32_t MV_MIN_SLOTS = 1u << 22;
 uint32_t moves_buckets(uint32_t max_slots);
 size_t moves_hist_elems(uint32_t n, uint32_t max_slots);
-void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t n_total,
+void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotTab info, uint32_t n_total,
                            uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *hist,
                            uint32_t *scan_tmp, void *binned, hipStream_t st);
 // Zero the per-tick counters and two ranges; bbox entries get the fold
@@ -222,7 +223,7 @@ void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *inf
 // the claims of a moves-only flush's first run.  n_unique: TickScalars::n_unique (0 = no check).
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
                      uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
-                     SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+                     SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotTab info, uint32_t tick_id,
                      uint32_t n_unique, hipStream_t st);
 
 // Cell keys of S' and the per-tick scalars d_rel / bmax (via per-block
@@ -299,7 +300,7 @@ size_t scan_tmp_elems(size_t n);
 // combined pass's candidate records cand = {x, z, old x, old z} (x, z NaN for a jumper).
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
-                   const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
+                   const SpaceGrid *grid, uint64_t seq_base, SlotTab info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                    uint32_t n_spaces, void *bbox_parts, hipStream_t st);
 void launch_cell_count(const uint32_t *sorted_keys, uint32_t n, uint32_t *cnt, hipStream_t st);
@@ -347,7 +348,7 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
                    uint32_t *dcount, hipStream_t st);
 // Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
 size_t bbox_part_bytes(uint32_t n);
-void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
+void launch_neighbors(FrameView F, SlotTab info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);
 // Zero `n` uint32 (rare re-run path).
 void launch_zero(uint32_t *p, size_t n, hipStream_t st);
@@ -364,7 +365,7 @@ void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_to
 size_t sparse_cnt_elems(uint32_t k);
 // op_seq == nullptr: op j's seq is seq0 + j.
 void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
-                   SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                   SlotTab info, const uint32_t *op_slot, const float *op_x, const float *op_z,
                    const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t tick, uint32_t *cnt,
                    uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st);
 // The same flush in one launch for k <= sparse_fused_max() ops (no claims stored): scr holds
@@ -372,7 +373,7 @@ void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, 
 // outgrew its scratch row (nothing written; run launch_sparse instead).
 uint32_t sparse_fused_max();
 void launch_sparse_fused(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
-                         SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                         SlotTab info, const uint32_t *op_slot, const float *op_x, const float *op_z,
                          const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t *cnt, uint32_t *scr,
                          uint32_t scr_cap, uint32_t *done, uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st);
 
@@ -380,7 +381,7 @@ void launch_sparse_fused(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_s
 struct SyncState;
 struct WorldView {
     FrameView F;           // frame of the last flush
-    const SlotInfo *info;  // per slot: .rank = index in F for slots in F
+    SlotTab info;  // per slot: .rank = index in F for slots in F
     hipStream_t st;
     uint32_t max_slots;
     size_t pending_ops;     // calls queued since the last flush (or a flush in flight)

@@ -49,11 +49,11 @@ inline uint32_t cdiv(size_t a, size_t b) { return (uint32_t)((a + b - 1) / b); }
 __global__ void k_prologue(TickScalars *sc, uint32_t *z0, uint32_t n0, uint32_t *z1, uint32_t n1, int4 *bbox,
                            uint32_t n_spaces, uint32_t n_copy, const Rec16 *__restrict__ p_rec,
                            const SlotSp *__restrict__ p_ss, Rec16 *s_rec, SlotSp *s_ss, MoveRun mark,
-                           uint32_t max_slots, SlotInfo *info, uint32_t tick, uint32_t n_unique) {
+                           uint32_t max_slots, SlotTab info, uint32_t tick, uint32_t n_unique) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < mark.n) {
         const uint32_t s = mark.ds[i];
-        if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (mark.j0 + i);
+        if (s < max_slots) info.lastop[s] = ((unsigned long long)tick << 32) | (mark.j0 + i);
     }
     if (i < n_copy) {
         reinterpret_cast<uint4 *>(s_rec)[i] = reinterpret_cast<const uint4 *>(p_rec)[i];
@@ -85,7 +85,7 @@ __global__ void k_zero(uint32_t *p, size_t n) {
 // ------------------------------------------------------------ op apply ------
 
 __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t n_app, uint32_t base,
-                                Rec16 *s_rec, SlotSp *s_ss, SlotInfo *info, uint32_t max_slots, TickScalars *sc) {
+                                Rec16 *s_rec, SlotSp *s_ss, SlotTab info, uint32_t max_slots, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_app) return;
     const uint32_t s = new_slots[i];
@@ -100,15 +100,15 @@ __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t
         return;
     }
     // a slot live when the flush began keeps its entry (a device Enter batch breaking the rules)
-    if (reinterpret_cast<const uint2 *>(info + s)[1].y != SP_DEAD) {
+    if (info.rs[s].y != SP_DEAD) {
         atomicOr(&sc->err, ERR_ENTER_LIVE);
         return;
     }
-    reinterpret_cast<uint2 *>(info + s)[1] = make_uint2(idx, SP_DEAD);
+    info.rs[s] = make_uint2(idx, SP_DEAD);
 }
 
 __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint32_t j0, uint32_t max_slots,
-                            SlotInfo *info, uint32_t tick, TickScalars *sc) {
+                            SlotTab info, uint32_t tick, TickScalars *sc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slots[i];
@@ -117,7 +117,7 @@ __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint
         atomicOr(&sc->err, ERR_BAD_SLOT);
         return;
     }
-    atomicMax(&info[s].lastop, ((unsigned long long)tick << 32) | (j0 + i));
+    atomicMax(&info.lastop[s], ((unsigned long long)tick << 32) | (j0 + i));
 }
 
 // The last op of a slot in this flush determines its state (closed form:
@@ -143,20 +143,27 @@ __device__ __forceinline__ OpIn op_in(const uint32_t *__restrict__ slots, const 
     return o;
 }
 
-// The slot's SlotInfo line (lastop, rank, sp) in one 16-B load; the empty asm
-// keeps the compiler from splitting it into a claim load and a later
-// dependent rank load.
-__device__ __forceinline__ uint4 slot_info(const SlotInfo *info, uint32_t s) {
-    uint4 si = reinterpret_cast<const uint4 *>(info)[s];
+// The slot's table entry as (lastop lo, lastop hi, rank, sp): both loads issued together (the
+// empty asm keeps the compiler from making the rank load wait for the claim compare).
+__device__ __forceinline__ uint4 slot_info(SlotTab info, uint32_t s) {
+    const unsigned long long lo = info.lastop[s];
+    const uint2 rs = info.rs[s];
+    uint4 si = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), rs.x, rs.y);
     asm volatile("" : "+v"(si.x), "+v"(si.y), "+v"(si.z), "+v"(si.w));
     return si;
 }
+// Only {rank, sp} (the unique-moves apply compares no claim): one random line per op, from the
+// 8 B-per-slot array.
+__device__ __forceinline__ uint4 slot_rs(SlotTab info, uint32_t s) {
+    const uint2 rs = info.rs[s];
+    return make_uint4(0u, 0u, rs.x, rs.y);
+}
 
 // Apply op o (index j in the flush) if it is its slot's last op of this flush
-// (check_claim; si = the slot's SlotInfo line); returns its seq (0 if not
+// (check_claim; si = the slot's table entry, slot_info); returns its seq (0 if not
 // applied) for the seq_max fold.
 __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32_t j, const uint4 &si,
-                                                           SlotInfo *info, uint32_t tick, uint32_t n_total,
+                                                           SlotTab info, uint32_t tick, uint32_t n_total,
                                                            unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss,
                                                            TickScalars *sc, bool check_claim, uint32_t *errw) {
     const uint32_t s = o.slot;
@@ -177,7 +184,7 @@ __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32
         r.x = r.z = 0.0f;
         st_rec(s_rec, idx, r);
         st_ss(s_ss, idx, s, SP_DEAD);
-        reinterpret_cast<uint2 *>(info + s)[1] = make_uint2(0xFFFFFFFFu, SP_DEAD);
+        info.rs[s] = make_uint2(0xFFFFFFFFu, SP_DEAD);
         return r.s;
     }
     const bool keep = sp == SP_KEEP;
@@ -204,7 +211,7 @@ __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32
 
 __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__restrict__ xs,
                             const float *__restrict__ zs, const uint32_t *__restrict__ sps, uint32_t sp_def,
-                            uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick,
+                            uint32_t n, uint32_t j0, uint32_t max_slots, SlotTab info, uint32_t tick,
                             uint32_t n_total, const unsigned long long *__restrict__ seqs, unsigned long long seq0,
                             unsigned long long seq_floor, int track_max, Rec16 *s_rec, SlotSp *s_ss,
                             TickScalars *sc) {
@@ -238,21 +245,21 @@ __global__ void k_ops_apply(const uint32_t *__restrict__ slots, const float *__r
 // op that finds another op's claim folds its own in with atomicMax
 // (repeated slots only, rare) and lists the slot, so that k_moves_fixup
 // re-applies the true last op once this kernel has drained.
-__global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick) {
+__global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotTab info, uint32_t tick) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R.n) return;
     const uint32_t s = R.ds[i];
-    if (s < max_slots) info[s].lastop = ((unsigned long long)tick << 32) | (R.j0 + i);
+    if (s < max_slots) info.lastop[s] = ((unsigned long long)tick << 32) | (R.j0 + i);
 }
 
 #ifndef GWAOI_APPLY_PER
-#define GWAOI_APPLY_PER 4  // moves per thread of the single-pass apply (all SlotInfo lines in flight at once)
+#define GWAOI_APPLY_PER 4  // moves per thread of the single-pass apply (all slot-table lines in flight at once)
 #endif
 // UNIQUE (GWAOI_F_UNIQUE_MOVES): no op shares its slot with another op of the flush, so every op
 // applies without a claim; the ops that write nothing are counted (sc->ndrop, one atomic per wave)
 // for keygen's written-entry check.
 template <int PER, bool UNIQUE>
-__global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotInfo *info, uint32_t tick,
+__global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotTab info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
                                                        SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
     const uint32_t i0 = blockIdx.x * (256u * PER) + threadIdx.x;
@@ -265,8 +272,9 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
         if (i < R.n) o[u] = op_in(R.ds, R.dx, R.dz, R.dsp, R.sp_def, R.dseq, R.seq0, i);
     }
 #pragma unroll
-    for (int u = 0; u < PER; ++u)  // every SlotInfo line in flight at once
-        si[u] = o[u].slot < max_slots ? slot_info(info, o[u].slot) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < PER; ++u)  // every slot-table line in flight at once
+        si[u] = o[u].slot >= max_slots ? make_uint4(0, 0, 0, 0)
+                : UNIQUE ? slot_rs(info, o[u].slot) : slot_info(info, o[u].slot);
     unsigned long long smax = 0;
     uint32_t drop = 0;
     uint32_t *errw = UNIQUE ? &sc->err_apply : &sc->err;  // unique: sc->err is zeroed by keygen, after this
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
                 op_apply_one(o[u], R.j0 + i, si[u], info, tick, n_total, seq_floor, s_rec, s_ss, sc, false, errw);
             smax = q > smax ? q : smax;
         } else {
-            atomicMax(&info[s].lastop, mine);
+            atomicMax(&info.lastop[s], mine);
             coll[atomicAdd(&sc->ncoll, 1u)] = s;
         }
     }
@@ -322,7 +330,7 @@ __device__ __forceinline__ void moves_fixup(const FixupArgs &F, uint32_t t0, uin
     const uint32_t nc = F.sc->ncoll;
     for (uint32_t k = t0; k < nc; k += stride) {
         const uint32_t s = F.coll[k];
-        const uint4 si = reinterpret_cast<const uint4 *>(F.info)[s];
+        const uint4 si = slot_info(F.info, s);
         const uint32_t j = si.x;  // the winner (lastop low word; high word == tick)
         uint32_t q = 0;
         while (q + 1 < F.RS.count && j >= F.RS.r[q + 1].j0) ++q;
@@ -787,7 +795,7 @@ __global__ __launch_bounds__(MV_T) void k_mv_scatter(MoveRuns RS, uint32_t n, ui
 __global__ __launch_bounds__(MV_T) void k_mv_apply(MoveRuns RS, const uint32_t *__restrict__ hist, uint32_t G,
                                                   const MvOp *__restrict__ binned, uint32_t n_total,
                                                   unsigned long long seq_floor, Rec16 *s_rec, SlotSp *s_ss,
-                                                  SlotInfo *info, TickScalars *sc, int track_max) {
+                                                  SlotTab info, TickScalars *sc, int track_max) {
     __shared__ uint32_t claim[MV_R];
     const uint32_t b = blockIdx.x;
     for (uint32_t i = threadIdx.x; i < MV_R; i += MV_T) claim[i] = 0;
@@ -1334,7 +1342,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
                                            Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                                            const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
-                                           SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
+                                           SlotTab info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
                                            int (&bv)[4]);
 
@@ -1349,7 +1357,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
                          const Rec16 *__restrict__ s_rec, const SlotSp *__restrict__ s_ss,
                          const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss, Rec16 *f_rec,
                          SlotSp *f_ss, Rec16 *o_rec, uint4 *cand, const SpaceGrid *__restrict__ grid,
-                         unsigned long long seq_base, SlotInfo *info, const uint32_t *__restrict__ sorted_keys,
+                         unsigned long long seq_base, SlotTab info, const uint32_t *__restrict__ sorted_keys,
                          uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                          uint32_t n_spaces, BBoxPart *parts) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1366,7 +1374,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            const Rec16 *__restrict__ p_rec, const SlotSp *__restrict__ p_ss,
                                            Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
                                            const SpaceGrid *__restrict__ grid, unsigned long long seq_base,
-                                           SlotInfo *info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
+                                           SlotTab info, const uint32_t *__restrict__ sorted_keys, uint32_t sentinel,
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
                                            int (&bv)[4]) {
     const uint32_t key = sorted_keys[k];
@@ -1399,7 +1407,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     if (inp) pr = ld_rec(p_rec, i);
     st_rec(f_rec, k, now);
     reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(ss.slot, ss.sp);
-    reinterpret_cast<uint2 *>(info + ss.slot)[1] = make_uint2(k, ss.sp);
+    info.rs[ss.slot] = make_uint2(k, ss.sp);
     // previous state of the same entity, NaN position unless live in the same space then
     Rec16 o;
     o.x = o.z = qnan();
@@ -2809,9 +2817,9 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
 
 // ------------------------------------------------------------ neighbors ------
 
-__global__ __launch_bounds__(256) void k_neighbors(FrameView F, const SlotInfo *__restrict__ info, uint32_t slot,
+__global__ __launch_bounds__(256) void k_neighbors(FrameView F, SlotTab info, uint32_t slot,
                                                    uint32_t *out, uint32_t cap, uint32_t *count) {
-    const uint32_t a = info[slot].rank;
+    const uint32_t a = info.rs[slot].x;
     if (a >= F.n || ld_ss(F.ss, a).slot != slot) return;
     const Rec16 A = ld_rec(F.rec, a);
     const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
@@ -2967,7 +2975,7 @@ void launch_events_csr(const uint32_t *ev_pairs, uint64_t n_enter, uint64_t n_to
 
 void launch_prologue(TickScalars *sc, uint32_t *z0, size_t n0, uint32_t *z1, size_t n1, int4 *bbox,
                      uint32_t n_spaces, uint32_t n_copy, const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *s_rec,
-                     SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotInfo *info, uint32_t tick_id,
+                     SlotSp *s_ss, const MoveRun *mark, uint32_t max_slots, SlotTab info, uint32_t tick_id,
                      uint32_t n_unique, hipStream_t st) {
     MoveRun mk{};
     if (mark) mk = *mark;
@@ -2981,12 +2989,12 @@ void launch_zero(uint32_t *p, size_t n, hipStream_t st) {
 }
 
 void launch_init_appended(const uint32_t *new_slots, uint32_t n_app, uint32_t base, Rec16 *s_rec, SlotSp *s_ss,
-                          SlotInfo *info, uint32_t max_slots, TickScalars *sc, hipStream_t st) {
+                          SlotTab info, uint32_t max_slots, TickScalars *sc, hipStream_t st) {
     if (!n_app) return;
     k_init_appended<<<cdiv(n_app, 256), 256, 0, st>>>(new_slots, n_app, base, s_rec, s_ss, info, max_slots, sc);
 }
 
-void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotTab info, uint32_t tick_id, uint32_t n_total,
                   uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, const Rec16 *p_rec, uint32_t n_prev,
                   TickScalars *sc, uint32_t *coll, uint32_t n_marked, bool unique, hipStream_t st) {
     if (unique) {  // no claims, no fixup
@@ -3033,7 +3041,7 @@ size_t moves_hist_elems(uint32_t n, uint32_t max_slots) {
     return (size_t)nb * cdiv(std::max(n, 1u), (size_t)MV_T * mv_per(n, nb)) + 1;
 }
 
-void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *info, uint32_t n_total,
+void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotTab info, uint32_t n_total,
                            uint64_t seq_floor, Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, uint32_t *hist,
                            uint32_t *scan_tmp, void *binned, hipStream_t st) {
     const uint32_t n = RS.count ? RS.r[RS.count - 1].j0 + RS.r[RS.count - 1].n : 0u;
@@ -3053,14 +3061,14 @@ void launch_moves_bucketed(const MoveRuns &RS, uint32_t max_slots, SlotInfo *inf
     k_mv_apply<<<nb, MV_T, 0, st>>>(RS, hist, G, bo, n_total, seq_floor, s_rec, s_ss, info, sc, track ? 1 : 0);
 }
 
-void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info,
+void launch_ops_claim(const uint32_t *slots, uint32_t n, uint32_t j0, uint32_t max_slots, SlotTab info,
                       uint32_t tick_id, TickScalars *sc, hipStream_t st) {
     if (!n) return;
     k_ops_claim<<<cdiv(n, 256), 256, 0, st>>>(slots, n, j0, max_slots, info, tick_id, sc);
 }
 
 void launch_ops_apply(const uint32_t *slots, const float *x, const float *z, const uint32_t *sp, uint32_t sp_def,
-                      uint32_t n, uint32_t j0, uint32_t max_slots, SlotInfo *info, uint32_t tick_id, uint32_t n_total,
+                      uint32_t n, uint32_t j0, uint32_t max_slots, SlotTab info, uint32_t tick_id, uint32_t n_total,
                       const unsigned long long *seqs, uint64_t seq0, uint64_t seq_floor, bool track_max,
                       Rec16 *s_rec, SlotSp *s_ss, TickScalars *sc, hipStream_t st) {
     if (!n) return;
@@ -3163,7 +3171,7 @@ int radix_sort(SortBuffers &b, uint32_t n, int bits, hipStream_t st) {
 
 void launch_gather(const uint32_t *perm, uint32_t n_new, uint32_t n_prev, const Rec16 *s_rec, const SlotSp *s_ss,
                    const Rec16 *p_rec, const SlotSp *p_ss, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
-                   const SpaceGrid *grid, uint64_t seq_base, SlotInfo *info, const uint32_t *sorted_keys,
+                   const SpaceGrid *grid, uint64_t seq_base, SlotTab info, const uint32_t *sorted_keys,
                    uint32_t sentinel, uint32_t n_total, TickScalars *sc, uint32_t *f_key, int4 *bbox,
                    uint32_t n_spaces, void *bbox_parts, hipStream_t st) {
     const uint32_t nt = std::max<uint32_t>(n_new, 1u);
@@ -3241,7 +3249,7 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
 
 size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }
 
-void launch_neighbors(FrameView F, const SlotInfo *info, uint32_t slot, uint32_t *out, uint32_t cap,
+void launch_neighbors(FrameView F, SlotTab info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st) {
     k_neighbors<<<1, 256, 0, st>>>(F, info, slot, out, cap, count);
 }

@@ -37,7 +37,7 @@ struct SparseArgs {
     uint32_t *key;
     uint32_t *cell_start;
     const SpaceGrid *grid;
-    SlotInfo *info;
+    SlotTab info;
     const uint32_t *op_slot;
     const float *op_x, *op_z;
     const unsigned long long *op_seq;  // nullptr: op j's seq is seq0 + j
@@ -55,7 +55,7 @@ __device__ __forceinline__ unsigned long long op_seq(const SparseArgs &A, uint32
 }
 
 __device__ __forceinline__ bool winner(const SparseArgs &A, uint32_t j, uint32_t slot) {
-    return A.info[slot].lastop == (((unsigned long long)A.tick << 32) | j);
+    return A.info.lastop[slot] == (((unsigned long long)A.tick << 32) | j);
 }
 
 // Block-wide exclusive scan of two flags, in thread order, and their block totals.
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(SP_T) void k_sp_events(SparseArgs A) {
         if (PHASE == 0 && tid == 0) A.cnt[j] = A.cnt[A.k + j] = 0;
         return;
     }
-    const uint32_t ra = A.info[slot].rank;
+    const uint32_t ra = A.info.rs[slot].x;
     const Rec16 ao = ld_rec(A.rec, ra);
     const uint32_t sp = ld_ss(A.ss, ra).sp;
     const SpaceGrid g = A.grid[sp];
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(SP_T) void k_sp_events(SparseArgs A) {
             uint32_t b_slot = 0;
             if (b < je && b != ra) {
                 b_slot = ld_ss(A.ss, b).slot;
-                if ((uint32_t)(A.info[b_slot].lastop >> 32) != A.tick) {
+                if ((uint32_t)(A.info.lastop[b_slot] >> 32) != A.tick) {
                     const Rec16 br = ld_rec(A.rec, b);
                     const bool was = rel(ao.x, ao.z, ao.s, br.x, br.z, br.s, D);
                     const bool is = rel(nx, nz, ns, br.x, br.z, br.s, D);
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(SP_T) void k_sp_events(SparseArgs A) {
         if (q < A.k) {
             b_slot = A.op_slot[q];
             if (b_slot > slot && winner(A, q, b_slot)) {
-                const uint32_t rb = A.info[b_slot].rank;
+                const uint32_t rb = A.info.rs[b_slot].x;
                 if (ld_ss(A.ss, rb).sp == sp) {
                     const Rec16 bo = ld_rec(A.rec, rb);
                     const bool was = rel(ao.x, ao.z, ao.s, bo.x, bo.z, bo.s, D);
@@ -266,7 +266,7 @@ __device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t 
                 reinterpret_cast<uint4 *>(A.rec)[i - 1] = s_rec[tid];
                 reinterpret_cast<uint2 *>(A.ss)[i - 1] = s_ss[tid];
                 A.key[i - 1] = s_key[tid];
-                A.info[s_ss[tid].x].rank = i - 1;
+                A.info.rs[s_ss[tid].x].x = i - 1;
             }
             __syncthreads();
         }
@@ -289,7 +289,7 @@ __device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t 
                 reinterpret_cast<uint4 *>(A.rec)[i + 1] = s_rec[tid];
                 reinterpret_cast<uint2 *>(A.ss)[i + 1] = s_ss[tid];
                 A.key[i + 1] = s_key[tid];
-                A.info[s_ss[tid].x].rank = i + 1;
+                A.info.rs[s_ss[tid].x].x = i + 1;
             }
             __syncthreads();
             hi = lo;
@@ -302,7 +302,7 @@ __device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t 
         reinterpret_cast<uint4 *>(A.rec)[dst] = m_rec;
         reinterpret_cast<uint2 *>(A.ss)[dst] = m_ss;
         A.key[dst] = k2;
-        A.info[m_ss.x].rank = dst;
+        A.info.rs[m_ss.x].x = dst;
     }
     __syncthreads();
 }
@@ -324,7 +324,7 @@ __device__ void sp_apply_body(const SparseArgs &A, Win win) {
     for (uint32_t j = tid; j < A.k; j += SA_T) {
         const uint32_t slot = A.op_slot[j];
         if (!win(j, slot)) continue;
-        const uint32_t r = A.info[slot].rank;
+        const uint32_t r = A.info.rs[slot].x;
         const uint32_t k1 = A.key[r], k2 = key_of(A.grid[ld_ss(A.ss, r).sp], A.op_x[j], A.op_z[j]);
         if (k1 == k2) continue;
         const uint32_t c = atomicAdd(&n_chg, 1u);
@@ -346,7 +346,7 @@ __device__ void sp_apply_body(const SparseArgs &A, Win win) {
         r.x = A.op_x[j];
         r.z = A.op_z[j];
         r.s = op_seq(A, j);
-        st_rec(A.rec, A.info[slot].rank, r);
+        st_rec(A.rec, A.info.rs[slot].x, r);
     }
     // changers in op order (deterministic frame): rank-sort the short list
     __shared__ uint32_t ord[SP_MAX_CHANGERS];
@@ -359,7 +359,7 @@ __device__ void sp_apply_body(const SparseArgs &A, Win win) {
     __syncthreads();
     for (uint32_t c = 0; c < nc; ++c) {
         const uint32_t j = ord[c], slot = A.op_slot[j];
-        const uint32_t p = A.info[slot].rank;
+        const uint32_t p = A.info.rs[slot].x;
         const uint32_t k1 = A.key[p], k2 = key_of(A.grid[ld_ss(A.ss, p).sp], A.op_x[j], A.op_z[j]);
         sp_shift(A, p, k1, k2);
     }
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(SA_T) void k_sp_fused(SparseArgs A, uint32_t *scr, 
     uint32_t ne = 0, nl = 0;
     bool ovf = false;
     if (win(j)) {
-        const uint32_t ra = A.info[slot].rank;
+        const uint32_t ra = A.info.rs[slot].x;
         const Rec16 ao = ld_rec(A.rec, ra);
         const uint32_t sp = ld_ss(A.ss, ra).sp;
         const SpaceGrid g = A.grid[sp];
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(SA_T) void k_sp_fused(SparseArgs A, uint32_t *scr, 
                 if (q < k) {
                     b_slot = s_slot[q];
                     if (b_slot > slot && win(q)) {
-                        const uint32_t rb = A.info[b_slot].rank;
+                        const uint32_t rb = A.info.rs[b_slot].x;
                         if (ld_ss(A.ss, rb).sp == sp) {
                             const Rec16 bo = ld_rec(A.rec, rb);
                             const bool was = rel(ao.x, ao.z, ao.s, bo.x, bo.z, bo.s, D);
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(SA_T) void k_sp_fused(SparseArgs A, uint32_t *scr, 
 size_t sparse_cnt_elems(uint32_t k) { return 4 * (size_t)k + 3; }
 
 void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
-                   SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                   SlotTab info, const uint32_t *op_slot, const float *op_x, const float *op_z,
                    const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t tick, uint32_t *cnt,
                    uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st) {
     SparseArgs A{rec, ss, key, cell_start, grid, info, op_slot, op_x, op_z, op_seq, seq0, k, tick, cnt,
@@ -634,7 +634,7 @@ void launch_sparse(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, 
 uint32_t sparse_fused_max() { return SP_FUSED_MAX; }
 
 void launch_sparse_fused(Rec16 *rec, SlotSp *ss, uint32_t *key, uint32_t *cell_start, const SpaceGrid *grid,
-                         SlotInfo *info, const uint32_t *op_slot, const float *op_x, const float *op_z,
+                         SlotTab info, const uint32_t *op_slot, const float *op_x, const float *op_z,
                          const unsigned long long *op_seq, uint64_t seq0, uint32_t k, uint32_t *cnt, uint32_t *scr,
                          uint32_t scr_cap, uint32_t *done, uint32_t *out, uint64_t cap, TickOut *res, hipStream_t st) {
     SparseArgs A{rec, ss, key, cell_start, grid, info, op_slot, op_x, op_z, op_seq, seq0, k, 0u, cnt,

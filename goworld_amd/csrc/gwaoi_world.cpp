@@ -221,7 +221,7 @@ struct gwaoi_world {
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;
     size_t scan_tmp_cap = 0;
-    gw::SlotInfo *sinfo = nullptr;  // per slot: last op claim, S' index, space
+    gw::SlotTab sinfo{};  // per slot: last op claim; S' index and space (two arrays)
     // incremental frame sort (grid unchanged): per-cell counts, arrival lists
     unsigned long long *cnt64 = nullptr, *scan64_tmp = nullptr;
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
@@ -1480,7 +1480,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
         if (S.done_ev) (void)hipEventDestroy(S.done_ev);
     }
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
-    dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo); dfree(w->new_slots_d);
+    dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo.lastop); dfree(w->sinfo.rs); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll); dfree(w->special);
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
@@ -1601,7 +1601,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     }
     if ((rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
-        (rc = dalloc(w, &w->sinfo, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
+        (rc = dalloc(w, &w->sinfo.lastop, N)) || (rc = dalloc(w, &w->sinfo.rs, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 3 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, 2 * (N / gw::COMBINED_TILE + 2))) ||
         (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 16)) || (rc = dalloc(w, &w->ework, N)) ||
@@ -1611,8 +1611,8 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         hipMemset(w->ework, 0, N * sizeof(uint32_t)) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
-    if (hipMemset(w->sinfo, 0xFF, N * sizeof(gw::SlotInfo)) != hipSuccess ||
-        hipMemset2D(w->sinfo, sizeof(gw::SlotInfo), 0, sizeof(unsigned long long), N) != hipSuccess)
+    if (hipMemset(w->sinfo.rs, 0xFF, N * sizeof(uint2)) != hipSuccess ||
+        hipMemset(w->sinfo.lastop, 0, N * sizeof(unsigned long long)) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     // the bucketed apply for worlds whose SlotInfo outgrows the MALL (GWAOI_F_TEST_BUCKETED forces it)
     w->moves_bucketed = N > gw::MV_MIN_SLOTS || (cfg->flags & GWAOI_F_TEST_BUCKETED);
