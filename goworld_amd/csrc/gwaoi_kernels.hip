@@ -1068,11 +1068,40 @@ __global__ __launch_bounds__(SC_T) void k_scan64_agg(const unsigned long long *_
     }
 }
 
+// FUSED (one launch, no k_scan64_agg): each tile publishes its total as two 8-B granules
+// {epoch, value} with write-through (sc1) stores the moment it has summed its tile, and sums the
+// earlier tiles' granules polled with sc1 loads (MI355X: the XCDs' L2s are not coherent; an sc1
+// access goes past them, so no fence is needed: cdna_hip_programming.md §6 Guideline 16, R2).
+// The earlier tiles are dispatched first and never wait for a later one, and the host launches
+// this form only when the whole grid fits on the chip at once (scan64_resident_blocks), so every
+// wait ends; a wait that still runs past its bound sets ERR_SCAN_STALL (the flush fails).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+__device__ __forceinline__ void granule_put(unsigned long long *g, uint32_t epoch, uint32_t v) {
+    __hip_atomic_store((gu64_t *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The value of granule g once its tag is `epoch`; false when the bounded wait ran out.
+__device__ __forceinline__ bool granule_get(unsigned long long *g, uint32_t epoch, uint32_t &v) {
+    for (uint32_t spin = 0; spin < (1u << 20); ++spin) {
+        const unsigned long long x =
+            __hip_atomic_load((gu64_t *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == epoch) {
+            v = (uint32_t)x;
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+template <bool FUSED>
 __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
-                                                    const unsigned long long *__restrict__ agg, uint32_t *lo, uint32_t *hi,
+                                                    unsigned long long *agg, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
                                                     const uint32_t *__restrict__ p_cs, uint32_t *shift,
-                                                    uint32_t *list, unsigned long long *tcnt) {
+                                                    uint32_t *list, unsigned long long *tcnt, uint32_t epoch) {
     if (blockIdx.x == 0) {  // first, so that its serial loop overlaps the tiles
         keygen_fold256(blk, nbk, sc);
         return;
@@ -1085,7 +1114,8 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     // every global operand first, in one round trip: the tile's counts, the previous starts of its
     // cells (for the final write) and this thread's share of the earlier tiles' totals
     unsigned long long pre = 0;
-    for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
+    if (!FUSED)
+        for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
     uint32_t pcs[S64_I];
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {
@@ -1103,6 +1133,20 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     }
     unsigned long long tot;
     unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot);
+    if (FUSED) {  // publish this tile's total, then sum the earlier tiles' (agg = the granules)
+        if (tid == 0) {
+            granule_put(agg + 2 * b, epoch, (uint32_t)tot);
+            granule_put(agg + 2 * b + 1, epoch, (uint32_t)(tot >> 32));
+        }
+        bool ok = true;
+        for (uint32_t q = tid; q < b; q += SC_T) {
+            uint32_t a = 0, d = 0;
+            ok &= granule_get(agg + 2 * q, epoch, a);
+            ok &= granule_get(agg + 2 * q + 1, epoch, d);
+            pre += ((unsigned long long)d << 32) | a;
+        }
+        if (!ok) atomicOr(&sc->err, ERR_SCAN_STALL);
+    }
     {  // the tile's changed cells (not the dead-entry cell n - 1), in cell order, for k_cell_merge
         __shared__ uint32_t ws32[SC_T / WAVE];
         uint32_t nch = 0, t32;
@@ -1816,6 +1860,7 @@ constexpr int CW = CT / WAVE;  // waves per k_combined workgroup
 #ifndef GWAOI_FLAT_U
 #define GWAOI_FLAT_U 2  // flat sweep: 64-candidate chunks per iteration
 #endif
+
 constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= one sweep iteration + a drain batch)
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
 static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
@@ -2145,6 +2190,8 @@ __device__ __forceinline__ void sweep_flat(CombinedLds &L, int w, WaveQueue &Q, 
             const uint32_t idx = (kk >= s.z ? s.y : s.x) + kk;
             ao[u] = s.w >> 24;
             bi[u] = p < T ? idx : 0u;
+            // (from an LDS table: the owner's registers by ds_bpermute, 4 per position, cost 81.7
+            // against 78.0 us at config 3, and 87.0 with the freed LDS spent on an 8th wave per SIMD)
             const float4 ap = L.atab[w][o];
             ax[u] = ap.x;
             az[u] = ap.y;
@@ -2244,11 +2291,10 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
 // The wave's index in its block as a scalar (an SGPR: the per-wave LDS bases then cost no VGPR).
 __device__ __forceinline__ int wave_id() { return (int)__builtin_amdgcn_readfirstlane(threadIdx.x / WAVE); }
 
-__device__ void combined_sweep(CombinedLds &L, const LaneA &A, const uint4 *__restrict__ cand, const FrameView &F,
-                               const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne, uint32_t &nl,
-                               uint32_t &lw, uint2 *out, uint64_t cap, unsigned long long pe, unsigned long long pl,
-                               bool replay) {
-    const int w = wave_id();
+__device__ void combined_sweep(CombinedLds &L, const int w, const LaneA &A, const uint4 *__restrict__ cand,
+                               const FrameView &F, const Rec16 *__restrict__ O_rec, const CombinedCtx &C, uint32_t &ne,
+                               uint32_t &nl, uint32_t &lw, uint2 *out, uint64_t cap, unsigned long long pe,
+                               unsigned long long pl, bool replay) {
     const SpaceGrid &g = C.g;
     WaveQueue Q{0u, ne, nl, lw};
     const float lo = C.lo, hi = C.hi, M = C.M;
@@ -2433,7 +2479,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
             C.proto.chg = false;
             LaneA B = A;
             B.valid = mine;
-            combined_sweep(L, B, cand, F, O_rec, C, e, l, lw, o, cap, pe, pl, replay);
+            combined_sweep(L, w, B, cand, F, O_rec, C, e, l, lw, o, cap, pe, pl, replay);
         }
     };
     run(false, nullptr, 0ull, 0ull, ne, nl);
@@ -3100,21 +3146,36 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // k_arrive re-zeroes the counted cells (no clearing pass over cnt64)
 bool scan_rezeroes_counts() { return true; }
 
-size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }  // tile totals, counts
+// tile totals, changed-cell counts, and the one-launch scan's granules (two per tile)
+size_t incr_sort_tmp_elems(size_t cells) { return 4 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
+
+uint32_t scan64_resident_blocks(int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_scan64<true>, SC_T, 0) != hipSuccess)
+        return 0;
+    // one block per CU of margin (the occupancy query can be one block high: MI355X_MICROARCH.md)
+    return per > 1 ? (uint32_t)(cus * (per - 1)) : 0u;
+}
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, const SpecialJob *sp, hipStream_t st) {
+                      TickScalars *sc, const SpecialJob *sp, uint32_t resident, uint32_t epoch, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
     uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 3 (total_cells + 1) words
     uint32_t *list = shift + m;  // the changed cells, per scan tile
     unsigned long long *tcnt = tmp + nb;
-    k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
-    k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
-                                      keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt);
+    if (nb + 1 <= resident) {  // one launch: the tile totals handed over inside it
+        k_scan64<true><<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp + 2 * ((size_t)nb + 1), cell_start, arr_pos, blk,
+                                                keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt, epoch);
+    } else {
+        k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
+        k_scan64<false><<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
+                                                 keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt, 0u);
+    }
     if (sp && sp->n_tiles) {
         const SpecialJob &J = *sp;
         k_arrive_special<<<J.n_tiles + cdiv(n_total, PT), PT, 0, st>>>(J, keys, n_total, n_prev, p_key, sentinel, arr_pos,

@@ -5,7 +5,7 @@ set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
-ARGS="--steps 20 --warmup 3 --no-cpu-baseline --host-io-steps 0 --sync-steps 0 --cfg4-steps 0 --cfg5-steps 0 --small-flush-reps 0 --host-tick-steps 0 --wire-steps 0"
+ARGS="--steps 20 --warmup 3 --no-cpu-baseline --host-io-steps 0 --sync-steps 0 --cfg4-steps 0 --cfg5-steps 0 --small-flush-reps 0 --host-tick-steps 0 --wire-steps 0 --claims-steps 0"
 for v in "$@"; do
   OUT=$R/gpurun_out/tv_${TAG}_$v
   mkdir -p $OUT

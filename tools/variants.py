@@ -30,7 +30,8 @@ def main():
                 env["GWAOI_LIB"] = os.path.join(VDIR, name + ".so")
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline",
                                 "--host-io-steps", "0", "--sync-steps", "0", "--cfg4-steps", "0",
-                                "--host-tick-steps", "0", "--wire-steps", "0", "--cfg5-steps", "0", "--small-flush-reps", "0", *bargs],
+                                "--host-tick-steps", "0", "--wire-steps", "0", "--cfg5-steps", "0", "--small-flush-reps", "0",
+                                "--claims-steps", "0", *bargs],
                                env=env, capture_output=True, text=True, timeout=400)
             try:
                 b = json.loads(r.stdout.strip().splitlines()[-1])
