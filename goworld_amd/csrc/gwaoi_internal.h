@@ -39,7 +39,6 @@ constexpr uint32_t ERR_COUNT_MISMATCH = 8u;  // host/device live-count disagreem
 constexpr uint32_t ERR_SEQ = 16u;            // explicit device seq below the flush's floor
 constexpr uint32_t ERR_ENTER_LIVE = 32u;     // device Enter of a slot live when the flush began
 constexpr uint32_t ERR_DUP_SLOT = 64u;       // GWAOI_F_UNIQUE_MOVES flush whose moves named a slot twice
-constexpr uint32_t ERR_SCAN_STALL = 128u;    // the one-launch cell scan waited too long for a tile total (bug guard)
 
 constexpr uint32_t TILE_A = 256;  // entities per pair-pass tile (= threads per workgroup)
 
@@ -282,11 +281,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, const SpecialJob *sp, uint32_t resident, uint32_t epoch, hipStream_t st);
-// Blocks of the one-launch cell scan that fit on the device at once (with a block per CU of
-// margin); incremental_sort takes that form only when its grid is no larger (resident), with
-// epoch = a value never used by an earlier flush of the world (the tick id).
-uint32_t scan64_resident_blocks(int device);
+                      TickScalars *sc, const SpecialJob *sp, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {

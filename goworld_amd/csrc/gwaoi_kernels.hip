@@ -1068,40 +1068,11 @@ __global__ __launch_bounds__(SC_T) void k_scan64_agg(const unsigned long long *_
     }
 }
 
-// FUSED (one launch, no k_scan64_agg): each tile publishes its total as two 8-B granules
-// {epoch, value} with write-through (sc1) stores the moment it has summed its tile, and sums the
-// earlier tiles' granules polled with sc1 loads (MI355X: the XCDs' L2s are not coherent; an sc1
-// access goes past them, so no fence is needed: cdna_hip_programming.md §6 Guideline 16, R2).
-// The earlier tiles are dispatched first and never wait for a later one, and the host launches
-// this form only when the whole grid fits on the chip at once (scan64_resident_blocks), so every
-// wait ends; a wait that still runs past its bound sets ERR_SCAN_STALL (the flush fails).
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-
-__device__ __forceinline__ void granule_put(unsigned long long *g, uint32_t epoch, uint32_t v) {
-    __hip_atomic_store((gu64_t *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The value of granule g once its tag is `epoch`; false when the bounded wait ran out.
-__device__ __forceinline__ bool granule_get(unsigned long long *g, uint32_t epoch, uint32_t &v) {
-    for (uint32_t spin = 0; spin < (1u << 20); ++spin) {
-        const unsigned long long x =
-            __hip_atomic_load((gu64_t *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(x >> 32) == epoch) {
-            v = (uint32_t)x;
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-template <bool FUSED>
 __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
-                                                    unsigned long long *agg, uint32_t *lo, uint32_t *hi,
+                                                    const unsigned long long *__restrict__ agg, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
                                                     const uint32_t *__restrict__ p_cs, uint32_t *shift,
-                                                    uint32_t *list, unsigned long long *tcnt, uint32_t epoch) {
+                                                    uint32_t *list, unsigned long long *tcnt) {
     if (blockIdx.x == 0) {  // first, so that its serial loop overlaps the tiles
         keygen_fold256(blk, nbk, sc);
         return;
@@ -1114,8 +1085,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     // every global operand first, in one round trip: the tile's counts, the previous starts of its
     // cells (for the final write) and this thread's share of the earlier tiles' totals
     unsigned long long pre = 0;
-    if (!FUSED)
-        for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
+    for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
     uint32_t pcs[S64_I];
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {
@@ -1133,20 +1103,6 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     }
     unsigned long long tot;
     unsigned long long run = block_excl_scan64<SC_T>(s, ws, tot);
-    if (FUSED) {  // publish this tile's total, then sum the earlier tiles' (agg = the granules)
-        if (tid == 0) {
-            granule_put(agg + 2 * b, epoch, (uint32_t)tot);
-            granule_put(agg + 2 * b + 1, epoch, (uint32_t)(tot >> 32));
-        }
-        bool ok = true;
-        for (uint32_t q = tid; q < b; q += SC_T) {
-            uint32_t a = 0, d = 0;
-            ok &= granule_get(agg + 2 * q, epoch, a);
-            ok &= granule_get(agg + 2 * q + 1, epoch, d);
-            pre += ((unsigned long long)d << 32) | a;
-        }
-        if (!ok) atomicOr(&sc->err, ERR_SCAN_STALL);
-    }
     {  // the tile's changed cells (not the dead-entry cell n - 1), in cell order, for k_cell_merge
         __shared__ uint32_t ws32[SC_T / WAVE];
         uint32_t nch = 0, t32;
@@ -1860,7 +1816,6 @@ constexpr int CW = CT / WAVE;  // waves per k_combined workgroup
 #ifndef GWAOI_FLAT_U
 #define GWAOI_FLAT_U 2  // flat sweep: 64-candidate chunks per iteration
 #endif
-
 constexpr int QCAP = GWAOI_QCAP;  // per-wave queue of filter survivors (>= one sweep iteration + a drain batch)
 constexpr int EVW = GWAOI_EVW;    // events buffered per wave
 static_assert(QCAP >= GWAOI_SW_U * WAVE, "queue must hold one sweep iteration");
@@ -3146,36 +3101,21 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
 // k_arrive re-zeroes the counted cells (no clearing pass over cnt64)
 bool scan_rezeroes_counts() { return true; }
 
-// tile totals, changed-cell counts, and the one-launch scan's granules (two per tile)
-size_t incr_sort_tmp_elems(size_t cells) { return 4 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }
-
-uint32_t scan64_resident_blocks(int device) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_scan64<true>, SC_T, 0) != hipSuccess)
-        return 0;
-    // one block per CU of margin (the occupancy query can be one block high: MI355X_MICROARCH.md)
-    return per > 1 ? (uint32_t)(cus * (per - 1)) : 0u;
-}
+size_t incr_sort_tmp_elems(size_t cells) { return 2 * ((size_t)cdiv(cells + 1, S64_TILE) + 1); }  // tile totals, counts
 
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, const SpecialJob *sp, uint32_t resident, uint32_t epoch, hipStream_t st) {
+                      TickScalars *sc, const SpecialJob *sp, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
     uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 3 (total_cells + 1) words
     uint32_t *list = shift + m;  // the changed cells, per scan tile
     unsigned long long *tcnt = tmp + nb;
-    if (nb + 1 <= resident) {  // one launch: the tile totals handed over inside it
-        k_scan64<true><<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp + 2 * ((size_t)nb + 1), cell_start, arr_pos, blk,
-                                                keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt, epoch);
-    } else {
-        k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
-        k_scan64<false><<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
-                                                 keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt, 0u);
-    }
+    k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
+    k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
+                                      keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt);
     if (sp && sp->n_tiles) {
         const SpecialJob &J = *sp;
         k_arrive_special<<<J.n_tiles + cdiv(n_total, PT), PT, 0, st>>>(J, keys, n_total, n_prev, p_key, sentinel, arr_pos,

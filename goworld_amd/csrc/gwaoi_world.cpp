@@ -234,7 +234,6 @@ struct gwaoi_world {
     uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
     bool moves_bucketed = false;   // the bucketed apply (max_slots > MV_MIN_SLOTS; GWAOI_MOVES_BUCKETED forces it)
     size_t cnt64_cap = 0;
-    uint32_t scan_resident = 0;  // blocks of the one-launch cell scan the device holds at once (0: two launches)
     // test and diagnostics flags (GWAOI_F_TEST_*, include/gwaoi.h)
     bool force_radix = false;  // always the full radix sort (checks the incremental sort against it)
     bool force_copy = false;   // S' always copied by the prologue (checks virtual S' against it)
@@ -1055,8 +1054,7 @@ int tick_launch(gwaoi_world *w) {
         w->dbg.incremental_sorts++;
         gw::incremental_sort(w->keys[0], n_total, n_prev, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             Fn.key, w->blk, S.sc, sp_fused ? &spj : nullptr, w->scan_resident, tick_id,
-                             st);  // the sorted keys ARE the frame's
+                             Fn.key, w->blk, S.sc, sp_fused ? &spj : nullptr, st);  // the sorted keys ARE the frame's
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -1268,11 +1266,9 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
     *committed = true;
     // problems the device found in the queued ops: the frame is committed (the offending ops were
     // dropped), so the flush's events are valid and the caller still receives them
-    if (r.err & (gw::ERR_COUNT_MISMATCH | gw::ERR_ENTER_LIVE | gw::ERR_SCAN_STALL)) {
+    if (r.err & (gw::ERR_COUNT_MISMATCH | gw::ERR_ENTER_LIVE)) {
         w->last_error = (r.err & gw::ERR_ENTER_LIVE)
                             ? "device Enter batch of a slot live when the flush began (frame count broken)"
-                        : (r.err & gw::ERR_SCAN_STALL)
-                            ? "the one-launch cell scan waited past its bound for a tile total (internal error)"
                             : "live-count mismatch between host and device (a device Enter/Leave batch broke its "
                               "rules, or an internal error)";
         return poison(w, GWAOI_EDEVICE);
@@ -1553,7 +1549,6 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         delete w;
         return GWAOI_EDEVICE;
     }
-    w->scan_resident = gw::scan64_resident_blocks(w->device);
     if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
         w->stream = nullptr;
         return fail(GWAOI_EDEVICE);
