@@ -608,7 +608,8 @@ def line_summary(out: dict) -> dict:
         "host_to_host_p50_ms": g(out, "host_to_host_tick", "p50_tick_ms"),
         "host_to_host_p99_ms": g(out, "host_to_host_tick", "p99_tick_ms"),
         "host_to_host_serial_p99_ms": g(out, "host_to_host_tick", "serial_p99_tick_ms"),
-        "host_tick_with_replay_ms": g(out, "host_tick", "ms_per_tick"),
+        "host_tick_with_replay_ms": g(out, "host_tick", "pipelined", "ms_per_tick"),
+        "host_tick_with_replay_p99_ms": g(out, "host_tick", "pipelined", "latency_ms_p99"),
         "small_flush_p50_ms": {k: g(v, "device", "p50_ms") for k, v in (out.get("small_flush") or {}).items()
                                if isinstance(v, dict)},
         "sync_decode_flush_ms": g(out, "sync_leg", "decode_flush_ms"), "sync_collect_ms": g(out, "sync_leg", "collect_ms"),
