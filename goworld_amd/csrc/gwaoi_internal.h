@@ -53,16 +53,17 @@ struct alignas(8) SlotSp {  // caller slot handle + space id (SP_DEAD = not live
     uint32_t slot, sp;
 };
 
-// Per-slot table, indexed by the caller's slot, as two arrays: lastop[s] = (tick << 32 | op
-// index) of the slot's last op this flush (the claims path only); rs[s] = {rank, sp}: its index
-// in S' (previous frame order, or appended) and its space in S' before this flush's ops (SP_DEAD
-// if not live).  Two arrays, not one 16-B record, because the hot passes touch one of them per
-// random slot: the unique-moves apply reads rs and the gather writes rs, so their random lines
-// come from an 8 B-per-slot array (half the lines of the record; at 1M slots 8 MB, against
-// 4 MB of L2 per XCD), and only the claims path also touches lastop.
+// Per-slot table, indexed by the caller's slot, as three arrays: lastop[s] = (tick << 32 | op
+// index) of the slot's last op this flush (the claims path only); rank[s] = its index in S'
+// (previous frame order, or appended; 0xFFFFFFFF if not live); sp[s] = its space in S' before
+// this flush's ops (SP_DEAD if not live).  Arrays, not one 16-B record, because the hot passes
+// touch few of them per random slot: the unique-moves apply reads only rank, so its one random
+// line per move comes from a 4 B-per-slot array (at 1M slots 4 MB, an XCD's L2; the record was
+// 16 MB); the gather writes rank and sp; only the claims path reads all three.
 struct SlotTab {
     unsigned long long *lastop;
-    uint2 *rs;
+    uint32_t *rank;
+    uint32_t *sp;
 };
 
 // Uniform grid of one space for one flush.  Cell (cx,cz) of space s has the
@@ -318,7 +319,7 @@ constexpr uint32_t COMBINED_TILE = GWAOI_CT;
 __host__ __device__ inline uint32_t combined_tiles(uint32_t n) { return (n + COMBINED_TILE - 1) / COMBINED_TILE; }
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,
+                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint8_t *ework,
                      hipStream_t st,
                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // The schedule: tile_order[1 + i] = the i-th tile of the XCD ranges laid end to end, heaviest first

@@ -100,11 +100,12 @@ __global__ void k_init_appended(const uint32_t *__restrict__ new_slots, uint32_t
         return;
     }
     // a slot live when the flush began keeps its entry (a device Enter batch breaking the rules)
-    if (info.rs[s].y != SP_DEAD) {
+    if (info.sp[s] != SP_DEAD) {
         atomicOr(&sc->err, ERR_ENTER_LIVE);
         return;
     }
-    info.rs[s] = make_uint2(idx, SP_DEAD);
+    info.rank[s] = idx;
+    info.sp[s] = SP_DEAD;
 }
 
 __global__ void k_ops_claim(const uint32_t *__restrict__ slots, uint32_t n, uint32_t j0, uint32_t max_slots,
@@ -147,16 +148,16 @@ __device__ __forceinline__ OpIn op_in(const uint32_t *__restrict__ slots, const 
 // empty asm keeps the compiler from making the rank load wait for the claim compare).
 __device__ __forceinline__ uint4 slot_info(SlotTab info, uint32_t s) {
     const unsigned long long lo = info.lastop[s];
-    const uint2 rs = info.rs[s];
-    uint4 si = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), rs.x, rs.y);
+    uint4 si = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), info.rank[s], info.sp[s]);
     asm volatile("" : "+v"(si.x), "+v"(si.y), "+v"(si.z), "+v"(si.w));
     return si;
 }
-// Only {rank, sp} (the unique-moves apply compares no claim): one random line per op, from the
-// 8 B-per-slot array.
-__device__ __forceinline__ uint4 slot_rs(SlotTab info, uint32_t s) {
-    const uint2 rs = info.rs[s];
-    return make_uint4(0u, 0u, rs.x, rs.y);
+// Only the rank (the unique-moves apply compares no claim, and its flush appends no entry, so a
+// slot is live exactly when its rank is not 0xFFFFFFFF): one random line per op, from the 4 B-per-
+// slot array.  The space word returned is any live space (0) for a live slot, SP_DEAD otherwise.
+__device__ __forceinline__ uint4 slot_rank(SlotTab info, uint32_t s) {
+    const uint32_t r = info.rank[s];
+    return make_uint4(0u, 0u, r, r == 0xFFFFFFFFu ? SP_DEAD : 0u);
 }
 
 // Apply op o (index j in the flush) if it is its slot's last op of this flush
@@ -184,7 +185,8 @@ __device__ __forceinline__ unsigned long long op_apply_one(const OpIn &o, uint32
         r.x = r.z = 0.0f;
         st_rec(s_rec, idx, r);
         st_ss(s_ss, idx, s, SP_DEAD);
-        info.rs[s] = make_uint2(0xFFFFFFFFu, SP_DEAD);
+        info.rank[s] = 0xFFFFFFFFu;
+        info.sp[s] = SP_DEAD;
         return r.s;
     }
     const bool keep = sp == SP_KEEP;
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
 #pragma unroll
     for (int u = 0; u < PER; ++u)  // every slot-table line in flight at once
         si[u] = o[u].slot >= max_slots ? make_uint4(0, 0, 0, 0)
-                : UNIQUE ? slot_rs(info, o[u].slot) : slot_info(info, o[u].slot);
+                : UNIQUE ? slot_rank(info, o[u].slot) : slot_info(info, o[u].slot);
     unsigned long long smax = 0;
     uint32_t drop = 0;
     uint32_t *errw = UNIQUE ? &sc->err_apply : &sc->err;  // unique: sc->err is zeroed by keygen, after this
@@ -1407,7 +1409,8 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     if (inp) pr = ld_rec(p_rec, i);
     st_rec(f_rec, k, now);
     reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(ss.slot, ss.sp);
-    info.rs[ss.slot] = make_uint2(k, ss.sp);
+    info.rank[ss.slot] = k;
+    info.sp[ss.slot] = ss.sp;
     // previous state of the same entity, NaN position unless live in the same space then
     Rec16 o;
     o.x = o.z = qnan();
@@ -2323,7 +2326,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
                                                  uint2 *out, uint64_t cap, uint32_t *tile_total,
                                                  unsigned long long *tile_base, uint32_t leave_off, uint32_t *dbg,
                                                  const uint32_t *__restrict__ tile_order, uint32_t *tile_work,
-                                                 uint32_t *ework, uint32_t n_tiles) {
+                                                 uint8_t *ework, uint32_t n_tiles) {
     __shared__ CombinedLds L;
     uint32_t t;
     {
@@ -2363,8 +2366,8 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         // by the work this entry's lane had last flush (the frame index then held about the same
         // entity), heaviest first, dealt round-robin to the waves below
         if (a < F.n) {
-            const uint32_t wk = ework ? ework[a] : 0u;
-            cls = (uint32_t)(NCLS - 2) - min((uint32_t)(NCLS - 2), (uint32_t)(31 - __clz((int)(wk | 1u))));
+            const uint32_t lg = ework ? ework[a] : 0u;  // log2 of the candidates, one byte per entry
+            cls = (uint32_t)(NCLS - 2) - min((uint32_t)(NCLS - 2), lg);
         }
         unsigned long long mine = 0;
 #pragma unroll
@@ -2438,7 +2441,7 @@ __global__ __launch_bounds__(CT) COMBINED_ATTR void k_combined(FrameView F, cons
         }
     };
     run(false, nullptr, 0ull, 0ull, ne, nl);
-    if (ework && A.valid) ework[A.a] = lw;
+    if (ework && A.valid) ework[A.a] = (uint8_t)(31 - __clz((int)(lw | 1u)));
     if (ln == 0) {
         L.wcnt[w][0] = ne;
         L.wcnt[w][1] = nl;
@@ -2820,7 +2823,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
 
 __global__ __launch_bounds__(256) void k_neighbors(FrameView F, SlotTab info, uint32_t slot,
                                                    uint32_t *out, uint32_t cap, uint32_t *count) {
-    const uint32_t a = info.rs[slot].x;
+    const uint32_t a = info.rank[slot];
     if (a >= F.n || ld_ss(F.ss, a).slot != slot) return;
     const Rec16 A = ld_rec(F.rec, a);
     const SpaceGrid g = F.grid[ld_ss(F.ss, a).sp];
@@ -3197,7 +3200,7 @@ void launch_pairs(FrameView F, const Rec16 *O_rec, const SlotSp *O_ss, uint64_t 
 
 void launch_combined(FrameView F, const uint4 *cand, const Rec16 *O_rec, uint64_t seq_base, TickScalars *sc,
                      uint32_t *tmp_pairs, uint64_t cap, uint32_t *tile_total, unsigned long long *tile_base,
-                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint32_t *ework,
+                     uint32_t leave_off, const uint32_t *tile_order, uint32_t *tile_work, uint8_t *ework,
                      hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (!F.n) return;
     // hipExtLaunchKernelGGL records the events at the kernel's own start and

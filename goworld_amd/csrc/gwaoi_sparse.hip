@@ -93,7 +93,7 @@ __global__ __launch_bounds__(SP_T) void k_sp_events(SparseArgs A) {
         if (PHASE == 0 && tid == 0) A.cnt[j] = A.cnt[A.k + j] = 0;
         return;
     }
-    const uint32_t ra = A.info.rs[slot].x;
+    const uint32_t ra = A.info.rank[slot];
     const Rec16 ao = ld_rec(A.rec, ra);
     const uint32_t sp = ld_ss(A.ss, ra).sp;
     const SpaceGrid g = A.grid[sp];
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(SP_T) void k_sp_events(SparseArgs A) {
         if (q < A.k) {
             b_slot = A.op_slot[q];
             if (b_slot > slot && winner(A, q, b_slot)) {
-                const uint32_t rb = A.info.rs[b_slot].x;
+                const uint32_t rb = A.info.rank[b_slot];
                 if (ld_ss(A.ss, rb).sp == sp) {
                     const Rec16 bo = ld_rec(A.rec, rb);
                     const bool was = rel(ao.x, ao.z, ao.s, bo.x, bo.z, bo.s, D);
@@ -266,7 +266,7 @@ __device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t 
                 reinterpret_cast<uint4 *>(A.rec)[i - 1] = s_rec[tid];
                 reinterpret_cast<uint2 *>(A.ss)[i - 1] = s_ss[tid];
                 A.key[i - 1] = s_key[tid];
-                A.info.rs[s_ss[tid].x].x = i - 1;
+                A.info.rank[s_ss[tid].x] = i - 1;
             }
             __syncthreads();
         }
@@ -289,7 +289,7 @@ __device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t 
                 reinterpret_cast<uint4 *>(A.rec)[i + 1] = s_rec[tid];
                 reinterpret_cast<uint2 *>(A.ss)[i + 1] = s_ss[tid];
                 A.key[i + 1] = s_key[tid];
-                A.info.rs[s_ss[tid].x].x = i + 1;
+                A.info.rank[s_ss[tid].x] = i + 1;
             }
             __syncthreads();
             hi = lo;
@@ -302,7 +302,7 @@ __device__ void sp_shift(const SparseArgs &A, uint32_t p, uint32_t k1, uint32_t 
         reinterpret_cast<uint4 *>(A.rec)[dst] = m_rec;
         reinterpret_cast<uint2 *>(A.ss)[dst] = m_ss;
         A.key[dst] = k2;
-        A.info.rs[m_ss.x].x = dst;
+        A.info.rank[m_ss.x] = dst;
     }
     __syncthreads();
 }
@@ -324,7 +324,7 @@ __device__ void sp_apply_body(const SparseArgs &A, Win win) {
     for (uint32_t j = tid; j < A.k; j += SA_T) {
         const uint32_t slot = A.op_slot[j];
         if (!win(j, slot)) continue;
-        const uint32_t r = A.info.rs[slot].x;
+        const uint32_t r = A.info.rank[slot];
         const uint32_t k1 = A.key[r], k2 = key_of(A.grid[ld_ss(A.ss, r).sp], A.op_x[j], A.op_z[j]);
         if (k1 == k2) continue;
         const uint32_t c = atomicAdd(&n_chg, 1u);
@@ -346,7 +346,7 @@ __device__ void sp_apply_body(const SparseArgs &A, Win win) {
         r.x = A.op_x[j];
         r.z = A.op_z[j];
         r.s = op_seq(A, j);
-        st_rec(A.rec, A.info.rs[slot].x, r);
+        st_rec(A.rec, A.info.rank[slot], r);
     }
     // changers in op order (deterministic frame): rank-sort the short list
     __shared__ uint32_t ord[SP_MAX_CHANGERS];
@@ -359,7 +359,7 @@ __device__ void sp_apply_body(const SparseArgs &A, Win win) {
     __syncthreads();
     for (uint32_t c = 0; c < nc; ++c) {
         const uint32_t j = ord[c], slot = A.op_slot[j];
-        const uint32_t p = A.info.rs[slot].x;
+        const uint32_t p = A.info.rank[slot];
         const uint32_t k1 = A.key[p], k2 = key_of(A.grid[ld_ss(A.ss, p).sp], A.op_x[j], A.op_z[j]);
         sp_shift(A, p, k1, k2);
     }
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(SA_T) void k_sp_fused(SparseArgs A, uint32_t *scr, 
     uint32_t ne = 0, nl = 0;
     bool ovf = false;
     if (win(j)) {
-        const uint32_t ra = A.info.rs[slot].x;
+        const uint32_t ra = A.info.rank[slot];
         const Rec16 ao = ld_rec(A.rec, ra);
         const uint32_t sp = ld_ss(A.ss, ra).sp;
         const SpaceGrid g = A.grid[sp];
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(SA_T) void k_sp_fused(SparseArgs A, uint32_t *scr, 
                 if (q < k) {
                     b_slot = s_slot[q];
                     if (b_slot > slot && win(q)) {
-                        const uint32_t rb = A.info.rs[b_slot].x;
+                        const uint32_t rb = A.info.rank[b_slot];
                         if (ld_ss(A.ss, rb).sp == sp) {
                             const Rec16 bo = ld_rec(A.rec, rb);
                             const bool was = rel(ao.x, ao.z, ao.s, bo.x, bo.z, bo.s, D);

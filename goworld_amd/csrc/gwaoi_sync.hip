@@ -364,7 +364,7 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
         if (fl) A.sst[4 * (size_t)s + SST_FLAGS] = 0u;
     } else {
         // a listed slot back in the frame is its frame entry's; a slot listed twice is sent once
-        const uint32_t r = A.info.rs[s].x;
+        const uint32_t r = A.info.rank[s];
         fl = (r < nf && ld_ss(A.F.ss, r).slot == s) ? 0u : atomicExch(&A.sst[4 * (size_t)s + SST_FLAGS], 0u);
     }
     A.snd[i] = fl;
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(ST) void k_route(RouteArgs A) {
             const uint32_t p = atomicAdd(&lds[(create ? 0u : A.G) + g], 1u);
             if (PASS == 1) {
                 if (create) {
-                    const uint32_t r = A.info.rs[ab.y].x;  // b is live after the flush
+                    const uint32_t r = A.info.rank[ab.y];  // b is live after the flush
                     const Rec16 B = ld_rec(A.F.rec, r);
                     const float4 P = A.pos[ab.y];
                     uint4 *o = A.out_c + 3 * (size_t)p;

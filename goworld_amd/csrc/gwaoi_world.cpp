@@ -221,7 +221,7 @@ struct gwaoi_world {
     uint32_t *hist = nullptr;
     uint32_t *scan_tmp = nullptr;
     size_t scan_tmp_cap = 0;
-    gw::SlotTab sinfo{};  // per slot: last op claim; S' index and space (two arrays)
+    gw::SlotTab sinfo{};  // per slot: last op claim, S' index, space (three arrays)
     // incremental frame sort (grid unchanged): per-cell counts, arrival lists
     unsigned long long *cnt64 = nullptr, *scan64_tmp = nullptr;
     uint32_t *arr_pos = nullptr, *arr_idx = nullptr;
@@ -229,7 +229,7 @@ struct gwaoi_world {
     uint32_t *special = nullptr;  // per previous-frame tile: keygen saw a special entity (the special pass's skip list)
     uint32_t *tile_work = nullptr;   // per combined tile: its measured time, then its candidates (k_combined)
     uint32_t *tile_order = nullptr;  // the next flush's combined tile order, heaviest first (k_tile_order)
-    uint32_t *ework = nullptr;       // per frame entry: candidates its lane swept (the next flush's deal to waves)
+    uint8_t *ework = nullptr;        // per frame entry: log2 of the candidates its lane swept (the next flush's deal)
     uint32_t *mv_hist = nullptr;  // bucketed apply: the bucket-major histogram, scanned (gw::launch_moves_bucketed)
     uint4 *mv_binned = nullptr;  // bucketed apply: the ops regrouped by slot bucket (16 B each)
     bool moves_bucketed = false;   // the bucketed apply (max_slots > MV_MIN_SLOTS; GWAOI_MOVES_BUCKETED forces it)
@@ -1480,7 +1480,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
         if (S.done_ev) (void)hipEventDestroy(S.done_ev);
     }
     for (int i = 0; i < 2; ++i) { dfree(w->keys[i]); dfree(w->vals[i]); }
-    dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo.lastop); dfree(w->sinfo.rs); dfree(w->new_slots_d);
+    dfree(w->hist); dfree(w->scan_tmp); dfree(w->sinfo.lastop); dfree(w->sinfo.rank); dfree(w->sinfo.sp); dfree(w->new_slots_d);
     dfree(w->cnt64); dfree(w->scan64_tmp); dfree(w->arr_pos); dfree(w->arr_idx); dfree(w->coll); dfree(w->special);
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
@@ -1601,17 +1601,19 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     }
     if ((rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
-        (rc = dalloc(w, &w->sinfo.lastop, N)) || (rc = dalloc(w, &w->sinfo.rs, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
+        (rc = dalloc(w, &w->sinfo.lastop, N)) || (rc = dalloc(w, &w->sinfo.rank, N)) ||
+        (rc = dalloc(w, &w->sinfo.sp, N)) || (rc = dalloc(w, &w->new_slots_d, N)) || (rc = dalloc(w, &w->arr_idx, N)) ||
         (rc = dalloc(w, &w->coll, N)) || (rc = dalloc(w, &w->blk, 3 * (N / 256 + 2))) ||
         (rc = dalloc(w, &w->special, N / 256 + 2)) || (rc = dalloc(w, &w->tile_work, 2 * (N / gw::COMBINED_TILE + 2))) ||
         (rc = dalloc(w, &w->tile_order, 1 + (size_t)gw::combined_tiles((uint32_t)N) + 16)) || (rc = dalloc(w, &w->ework, N)) ||
         (rc = dalloc(w, &w->nb_count, 1)))
         return fail(rc);
     if (hipMemset(w->tile_order, 0, sizeof(uint32_t)) != hipSuccess ||  // no order yet
-        hipMemset(w->ework, 0, N * sizeof(uint32_t)) != hipSuccess)
+        hipMemset(w->ework, 0, N * sizeof(uint8_t)) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     // lastop = 0, rank = sp = 0xFFFFFFFF (not live)
-    if (hipMemset(w->sinfo.rs, 0xFF, N * sizeof(uint2)) != hipSuccess ||
+    if (hipMemset(w->sinfo.rank, 0xFF, N * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(w->sinfo.sp, 0xFF, N * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(w->sinfo.lastop, 0, N * sizeof(unsigned long long)) != hipSuccess)
         return fail(GWAOI_EDEVICE);
     // the bucketed apply for worlds whose SlotInfo outgrows the MALL (GWAOI_F_TEST_BUCKETED forces it)
