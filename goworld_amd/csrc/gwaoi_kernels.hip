@@ -160,6 +160,18 @@ __device__ __forceinline__ uint4 slot_rank(SlotTab info, uint32_t s) {
     return make_uint4(0u, 0u, r, r == 0xFFFFFFFFu ? SP_DEAD : 0u);
 }
 
+// The claim and the rank (a claims-path flush that appends no entry and changes no space, i.e.
+// virtual S': a slot is live exactly when its rank is not 0xFFFFFFFF, and an op with an explicit
+// space moves the slot within it): two random lines per op, not three.
+__device__ __forceinline__ uint4 slot_claim_rank(SlotTab info, uint32_t s, uint32_t op_sp) {
+    const unsigned long long lo = info.lastop[s];
+    const uint32_t r = info.rank[s];
+    uint4 si = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), r,
+                          r == 0xFFFFFFFFu ? SP_DEAD : op_sp == SP_KEEP ? 0u : op_sp);
+    asm volatile("" : "+v"(si.x), "+v"(si.y), "+v"(si.z));
+    return si;
+}
+
 // Apply op o (index j in the flush) if it is its slot's last op of this flush
 // (check_claim; si = the slot's table entry, slot_info); returns its seq (0 if not
 // applied) for the seq_max fold.
@@ -260,7 +272,8 @@ __global__ void k_moves_mark(MoveRun R, uint32_t max_slots, SlotTab info, uint32
 // UNIQUE (GWAOI_F_UNIQUE_MOVES): no op shares its slot with another op of the flush, so every op
 // applies without a claim; the ops that write nothing are counted (sc->ndrop, one atomic per wave)
 // for keygen's written-entry check.
-template <int PER, bool UNIQUE>
+// VIRT (a flush with virtual S', no Enter/Leave): the claims path loads the claim and the rank only.
+template <int PER, bool UNIQUE, bool VIRT>
 __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_slots, SlotTab info, uint32_t tick,
                                                        uint32_t n_total, unsigned long long seq_floor, Rec16 *s_rec,
                                                        SlotSp *s_ss, TickScalars *sc, uint32_t *coll) {
@@ -276,7 +289,9 @@ __global__ __launch_bounds__(256) void k_moves_apply_n(MoveRun R, uint32_t max_s
 #pragma unroll
     for (int u = 0; u < PER; ++u)  // every slot-table line in flight at once
         si[u] = o[u].slot >= max_slots ? make_uint4(0, 0, 0, 0)
-                : UNIQUE ? slot_rank(info, o[u].slot) : slot_info(info, o[u].slot);
+                : UNIQUE ? slot_rank(info, o[u].slot)
+                : VIRT   ? slot_claim_rank(info, o[u].slot, o[u].sp)
+                         : slot_info(info, o[u].slot);
     unsigned long long smax = 0;
     uint32_t drop = 0;
     uint32_t *errw = UNIQUE ? &sc->err_apply : &sc->err;  // unique: sc->err is zeroed by keygen, after this
@@ -3007,16 +3022,21 @@ void launch_moves(const MoveRuns &RS, uint32_t max_slots, SlotTab info, uint32_t
     if (unique) {  // no claims, no fixup
         for (uint32_t q = 0; q < RS.count; ++q)
             if (RS.r[q].n)
-                k_moves_apply_n<GWAOI_APPLY_PER, true><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+                k_moves_apply_n<GWAOI_APPLY_PER, true, true><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
                     RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
         return;
     }
     for (uint32_t q = n_marked; q < RS.count; ++q)  // every run's claims before any apply
         if (RS.r[q].n) k_moves_mark<<<cdiv(RS.r[q].n, 256), 256, 0, st>>>(RS.r[q], max_slots, info, tick_id);
-    for (uint32_t q = 0; q < RS.count; ++q)
-        if (RS.r[q].n)
-            k_moves_apply_n<GWAOI_APPLY_PER, false><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+    for (uint32_t q = 0; q < RS.count; ++q) {
+        if (!RS.r[q].n) continue;
+        if (!s_ss)  // virtual S'
+            k_moves_apply_n<GWAOI_APPLY_PER, false, true><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
                 RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
+        else
+            k_moves_apply_n<GWAOI_APPLY_PER, false, false><<<cdiv(RS.r[q].n, 256 * GWAOI_APPLY_PER), 256, 0, st>>>(
+                RS.r[q], max_slots, info, tick_id, n_total, seq_floor, s_rec, s_ss, sc, coll);
+    }
     {
         FixupArgs F;
         F.RS = RS;
