@@ -250,7 +250,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
                    unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const TickZero &tz,
-                   hipStream_t st);
+                   unsigned long long *tent, hipStream_t st);
 // special (optional, cdiv(n_prev, TILE_A) words): keygen marks the previous-frame tiles that hold an
 // entity the special pass must look at; launch_pairs skips the others.
 // The stable sort of S' by key when the grid is the previous frame's: the

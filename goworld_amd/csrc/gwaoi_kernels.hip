@@ -421,7 +421,8 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
                                                 const SlotSp *__restrict__ p_ss,
                                                 const SpaceGrid *__restrict__ p_grid, uint32_t n_prev, float *blk,
                                                 const uint32_t *__restrict__ p_key, unsigned long long *cnt64,
-                                                unsigned long long seq_base, uint32_t *special, TickZero tz) {
+                                                unsigned long long seq_base, uint32_t *special, TickZero tz,
+                                                unsigned long long *tent) {
     __shared__ float s_m[2][256 / WAVE];
     const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
     if (tz.sc) {  // the prologue's zeroing (a unique-moves flush without one; see TickZero)
@@ -465,12 +466,14 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     }
     float dr = 0.0f, bm = 0.0f;
     bool near[KG_PER];
+    uint32_t kt[KG_PER];  // INCR: the scan tile of each entry's new key (0xFFFFFFFF: no entry)
     uint32_t nwr = 0;  // entries this flush's ops wrote (GWAOI_F_UNIQUE_MOVES: one per op that applied)
 #pragma unroll
     for (int u = 0; u < KG_PER; ++u) {
         const uint32_t i = base + 256u * (uint32_t)u;
         const bool inp = i < n_prev;
         near[u] = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
+        kt[u] = 0xFFFFFFFFu;
         if (i >= n) continue;
         uint32_t key = sentinel;
         Rec16 rr = r[u];
@@ -495,6 +498,7 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
             bm = fmaxf(bm, fmaxf(fabsf(rr.x), fabsf(rr.z)));
         }
         keys[i] = key;
+        kt[u] = key / (uint32_t)S64_TILE;
         if (!INCR) vals[i] = i;
         // INCR: only the entities that changed cell count: an arrival in the new cell (low word), a
         // departure from the old one (high word); a cell's stayers are its previous count minus
@@ -502,6 +506,23 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         if (INCR && key != old[u]) {
             if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
             if (old[u] != sentinel) atomicAdd(&cnt64[old[u]], 1ull << 32);
+        }
+    }
+    // INCR: entries per scan tile of the new keys (dead entries in the sentinel cell's tile), one
+    // atomic per distinct tile per wave: S' is in the previous frame's order, so a wave's entries
+    // almost always share one tile.  k_scan64 takes a tile's start in the new frame from these
+    // (no pass over the cell counts before it); k_cell_merge zeroes them again.
+    if (INCR) {
+#pragma unroll
+        for (int u = 0; u < KG_PER; ++u) {
+            unsigned long long act = __ballot(kt[u] != 0xFFFFFFFFu);
+            while (act) {
+                const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1u;
+                const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)kt[u], (int)lead);
+                const unsigned long long m = __ballot(kt[u] == t);
+                if (lane() == lead) atomicAdd(&tent[t], (unsigned long long)__popcll(m));
+                act &= ~m;
+            }
         }
     }
 #pragma unroll
@@ -1003,8 +1024,8 @@ __global__ __launch_bounds__(RS_T) void k_rs_downsweep(const uint32_t *__restric
 
 // ------------------------------------------------------ block offsets ------
 // The two scans across blocks (the sort's cell counts, k_finish's tile totals) take a
-// block's offset from totals written by an earlier launch -- per scan tile (k_scan64_agg)
-// or per group of FG tile entries (the pair passes' atomics) -- summed by the whole block,
+// block's offset from totals written by an earlier launch -- per scan tile (keygen's entries
+// per tile) or per group of FG tile entries (the pair passes' atomics) -- summed by the whole block,
 // with no chain between blocks.  Rounds 2-4 used a decoupled look-back instead: its chain
 // cost 10 us in the cell scan and 3.5 us in k_finish per cfg3 tick (profiles/archive/r04_variants_scan.log).
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -1052,7 +1073,7 @@ __device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long lo
 __device__ __forceinline__ uint32_t p64(uint32_t i) { return i + (i >> 4); }
 
 // Exclusive scan of the packed (lo = arrivals, hi = departures) cell counts, one
-// tile per block, the tile offsets from k_scan64_agg's totals.  Block 0 (the tiles are blocks 1..nb)
+// tile per block, the tile offsets from keygen's entries per tile.  Block 0 (the tiles are blocks 1..nb)
 // folds keygen's d_rel / bmax partials.
 __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, uint32_t nb, TickScalars *sc) {
     keygen_fold_t<SC_T>(blk, nb, sc);
@@ -1063,28 +1084,6 @@ __device__ __forceinline__ void keygen_fold256(const float *__restrict__ blk, ui
 // without a store per cell.  shift[c]: SHIFT_CHANGED for a cell with arrivals or departures, else
 // how far its run moved (new start - previous start): k_arrive places such a cell's stayers itself.
 constexpr uint32_t SHIFT_CHANGED = 0x80000000u;
-// The packed counts' total per scan tile (one block per tile).
-__global__ __launch_bounds__(SC_T) void k_scan64_agg(const unsigned long long *__restrict__ in, size_t n,
-                                                     unsigned long long *agg) {
-    __shared__ unsigned long long s_w[SC_T / WAVE];
-    const size_t base = (size_t)blockIdx.x * S64_TILE;
-    unsigned long long v = 0;
-#pragma unroll
-    for (int q = 0; q < S64_I; ++q) {
-        const size_t j = base + (uint32_t)q * SC_T + threadIdx.x;
-        v += j < n ? in[j] : 0ull;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane() == 0) s_w[threadIdx.x / WAVE] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int q = 0; q < SC_T / WAVE; ++q) t += s_w[q];
-        agg[blockIdx.x] = t;
-    }
-}
-
 __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__restrict__ in, size_t n, uint32_t nb,
                                                     const unsigned long long *__restrict__ agg, uint32_t *lo, uint32_t *hi,
                                                     const float *__restrict__ blk, uint32_t nbk, TickScalars *sc,
@@ -1100,9 +1099,11 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     const size_t base = (size_t)b * S64_TILE;
     const uint32_t tid = threadIdx.x;
     // every global operand first, in one round trip: the tile's counts, the previous starts of its
-    // cells (for the final write) and this thread's share of the earlier tiles' totals
+    // cells (for the final write) and this thread's share of the earlier tiles' entries (keygen's
+    // per-tile counts of the new keys: their sum is where this tile starts in the new frame)
     unsigned long long pre = 0;
     for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
+    const uint32_t p_cs0 = p_cs[base];  // where this tile started in the previous frame
     uint32_t pcs[S64_I];
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {
@@ -1132,8 +1133,10 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
             if (v[q] && c0 + q + 1 < n) list[base + off++] = (uint32_t)(c0 + q);
         if (tid == 0) tcnt[b] = t32;
     }
-    // the tile's offset: the sum of the earlier tiles' totals (k_scan64_agg), no look-back chain:
-    // a chain serialises ~500 tiles at ~20 ns a hop, the block-wide sum of <= 1k words does not
+    // the tile's offset: the sum of the earlier tiles' entries, no look-back chain: a chain
+    // serialises ~500 tiles at ~20 ns a hop, the block-wide sum of <= 1k words does not.  Its
+    // first cell moves by dt = (new start) - (previous start) = the arrivals minus the departures
+    // of every cell before the tile.
     __shared__ unsigned long long s_pre[SC_T / WAVE];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
@@ -1142,7 +1145,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     unsigned long long e = 0;
 #pragma unroll
     for (int q = 0; q < SC_T / WAVE; ++q) e += s_pre[q];
-    run += e;
+    const uint32_t dt = (uint32_t)e - p_cs0;
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read; bit 31: c changed
         tile[p64(tid * S64_I + (uint32_t)q)] = run | (v[q] ? (unsigned long long)SHIFT_CHANGED : 0ull);
@@ -1154,11 +1157,13 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
         const uint32_t j = (uint32_t)q * SC_T + tid;
         if (base + j < n) {
             const unsigned long long e = tile[p64(j)];
-            // e = (departures before c) << 32 | (arrivals before c): cell c starts at its previous
-            // start plus the arrivals minus the departures of the cells before it
-            const uint32_t arr = (uint32_t)e & ~SHIFT_CHANGED, d = arr - (uint32_t)(e >> 32);
+            // e = (departures before c in the tile) << 32 | (arrivals before c in the tile): cell c
+            // starts at its previous start plus the arrivals minus the departures of the cells
+            // before it.  Its arrivals are listed from its new start on (k_arrive): a cell has at
+            // least as many new entries as arrivals, so the lists of two cells never overlap.
+            const uint32_t arr = (uint32_t)e & ~SHIFT_CHANGED, d = dt + arr - (uint32_t)(e >> 32);
             lo[base + j] = pcs[q] + d;
-            hi[base + j] = arr;
+            hi[base + j] = pcs[q] + d;
             shift[base + j] = ((uint32_t)e & SHIFT_CHANGED) ? SHIFT_CHANGED : d;
         }
     }
@@ -1207,10 +1212,10 @@ __device__ __forceinline__ void cell_merge_one(uint32_t c, const uint32_t *__res
                                                const uint32_t *__restrict__ cell_start,
                                                const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                                                uint32_t *arr_idx, uint32_t sentinel, uint32_t *perm, uint32_t *skeys) {
-    // the cell's six bounds in one round trip
+    // the cell's five bounds in one round trip; its arrivals are listed from its new start on
     uint32_t o = cell_start[c];
     const uint32_t oe = cell_start[c + 1];
-    const uint32_t ab = c ? arr_pos[c - 1] : 0u, ae = arr_pos[c];
+    const uint32_t ab = o, ae = arr_pos[c];
     const uint32_t ps = p_cell_start[c], pe = p_cell_start[c + 1];
     if (o == oe) return;
     for (uint32_t k = ab + 1; k < ae; ++k) {  // insertion sort of the arrivals
@@ -1257,8 +1262,9 @@ __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const ui
                              const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
                              uint32_t *arr_idx, uint32_t total_cells, uint32_t n_total, uint32_t sentinel,
                              uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ list,
-                             const unsigned long long *__restrict__ tcnt) {
+                             const unsigned long long *__restrict__ tcnt, unsigned long long *tent) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (threadIdx.x == 0) tent[blockIdx.x] = 0ull;  // keygen's per-tile entries, read by k_scan64: zero for the next flush
     // entries past the live count are dead: sentinel keys, no source (so a host count that
     // disagrees with the device's -- a device batch breaking its rules -- finds sentinels, not
     // a previous flush's values, at [n_new, n_total))
@@ -3107,7 +3113,7 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
                    uint32_t sentinel, uint32_t *keys, uint32_t *vals, const Rec16 *p_rec, const SlotSp *p_ss,
                    const SpaceGrid *p_grid, uint32_t n_prev, float *blk, TickScalars *sc, const uint32_t *p_key,
                    unsigned long long *cnt64, uint64_t seq_base, uint32_t *special, const TickZero &tz,
-                   hipStream_t st) {
+                   unsigned long long *tent, hipStream_t st) {
     if (!n_total) {  // no entry: only the fold (d_rel = bmax = 0; a unique-moves apply's dropped ops and
                      // errors reach sc->err, and its error word and drop count are reset for the next flush)
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, 0u, sc);
@@ -3116,10 +3122,10 @@ void launch_keygen(Rec16 *s_rec, const SlotSp *s_ss, uint32_t n_total, const Spa
     const uint32_t nb = keygen_blocks(n_total);
     if (cnt64)
         k_keygen<true><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                           n_prev, blk, p_key, cnt64, seq_base, special, tz);  // folded by incremental_sort
+                                           n_prev, blk, p_key, cnt64, seq_base, special, tz, tent);  // folded by incremental_sort
     else {
         k_keygen<false><<<nb, 256, 0, st>>>(s_rec, s_ss, n_total, grid, sentinel, keys, vals, p_rec, p_ss, p_grid,
-                                            n_prev, blk, nullptr, nullptr, seq_base, special, tz);
+                                            n_prev, blk, nullptr, nullptr, seq_base, special, tz, nullptr);
         k_keygen_reduce<<<1, 1024, 0, st>>>(blk, nb, sc);
     }
 }
@@ -3139,8 +3145,8 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
     uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 3 (total_cells + 1) words
     uint32_t *list = shift + m;  // the changed cells, per scan tile
     unsigned long long *tcnt = tmp + nb;
-    k_scan64_agg<<<nb, SC_T, 0, st>>>(cnt64, m, tmp);
-    k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tmp, cell_start, arr_pos, blk,
+    unsigned long long *tent = tmp;  // keygen's entries per tile (incr_keygen_tiles)
+    k_scan64<<<nb + 1, SC_T, 0, st>>>(cnt64, m, nb, tent, cell_start, arr_pos, blk,
                                       keygen_blocks(n_total), sc, p_cell_start, shift, list, tcnt);
     if (sp && sp->n_tiles) {
         const SpecialJob &J = *sp;
@@ -3151,7 +3157,8 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
                                                      shift, perm, skeys);
     }
     k_cell_merge<<<nb, 256, 0, st>>>(
-        p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_total, sentinel, perm, skeys, list, tcnt);
+        p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_total, sentinel, perm, skeys, list, tcnt,
+        tent);
 }
 
 size_t scan_tmp_elems(size_t n) {

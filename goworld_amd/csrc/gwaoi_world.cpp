@@ -1026,7 +1026,8 @@ int tick_launch(gwaoi_world *w) {
     // ---- keys (+ d_rel, bmax) and stable sort
     stage_begin(w, S, ST_KEYGEN);
     gw::launch_keygen(S.srec, s_ss_view, n_total, Fn.grid, total_cells, w->keys[0], w->vals[0], P.rec, P.ss, P.grid,
-                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, tz, st);
+                      n_prev, w->blk, S.sc, P.key, incr ? w->cnt64 : nullptr, seq_base, w->special, tz,
+                      incr ? w->scan64_tmp : nullptr, st);
     stage_end(w, S, ST_KEYGEN);
     stage_begin(w, S, ST_SORT);
     int which = 1;
