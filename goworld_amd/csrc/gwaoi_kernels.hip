@@ -1184,7 +1184,7 @@ __device__ __forceinline__ void arrive_one(const uint32_t i, const uint32_t *__r
     if (key == old) {
         if (key == sentinel) return;
         const uint32_t d = shift[key];
-        if (d != SHIFT_CHANGED) {
+        if (d != SHIFT_CHANGED && i + d < n) {  // (the bound only guards against a broken scan)
             perm[i + d] = i;
             skeys[i + d] = key;
         }
@@ -1193,7 +1193,8 @@ __device__ __forceinline__ void arrive_one(const uint32_t i, const uint32_t *__r
     if (old != sentinel) cnt64[old] = 0ull;
     if (key == sentinel) return;
     cnt64[key] = 0ull;
-    arr_idx[atomicAdd(&arr_pos[key], 1u)] = i;
+    const uint32_t pos = atomicAdd(&arr_pos[key], 1u);
+    if (pos < n) arr_idx[pos] = i;
 }
 
 __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t n_prev,
@@ -1211,11 +1212,13 @@ __global__ void k_arrive(const uint32_t *__restrict__ keys, uint32_t n, uint32_t
 __device__ __forceinline__ void cell_merge_one(uint32_t c, const uint32_t *__restrict__ p_cell_start,
                                                const uint32_t *__restrict__ cell_start,
                                                const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
-                                               uint32_t *arr_idx, uint32_t sentinel, uint32_t *perm, uint32_t *skeys) {
+                                               uint32_t *arr_idx, uint32_t sentinel, uint32_t *perm, uint32_t *skeys,
+                                               uint32_t n_total) {
     // the cell's five bounds in one round trip; its arrivals are listed from its new start on
-    uint32_t o = cell_start[c];
-    const uint32_t oe = cell_start[c + 1];
-    const uint32_t ab = o, ae = arr_pos[c];
+    // (the clamps to n_total only guard the buffers against a broken scan)
+    uint32_t o = min(cell_start[c], n_total);
+    const uint32_t oe = min(cell_start[c + 1], n_total);
+    const uint32_t ab = o, ae = min(arr_pos[c], n_total);
     const uint32_t ps = p_cell_start[c], pe = p_cell_start[c + 1];
     if (o == oe) return;
     for (uint32_t k = ab + 1; k < ae; ++k) {  // insertion sort of the arrivals
@@ -1277,7 +1280,7 @@ __global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const ui
     const uint32_t nc = (uint32_t)tcnt[blockIdx.x];
     const uint32_t *L = list + (size_t)blockIdx.x * S64_TILE;
     for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
-        cell_merge_one(L[k], p_cell_start, cell_start, keys, arr_pos, arr_idx, sentinel, perm, skeys);
+        cell_merge_one(L[k], p_cell_start, cell_start, keys, arr_pos, arr_idx, sentinel, perm, skeys, n_total);
 }
 // ----------------------------------------------------------------- bbox ------
 
