@@ -508,20 +508,36 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
             if (old[u] != sentinel) atomicAdd(&cnt64[old[u]], 1ull << 32);
         }
     }
-    // INCR: entries per scan tile of the new keys (dead entries in the sentinel cell's tile), one
-    // atomic per distinct tile per wave: S' is in the previous frame's order, so a wave's entries
-    // almost always share one tile.  k_scan64 takes a tile's start in the new frame from these
-    // (no pass over the cell counts before it); k_cell_merge zeroes them again.
+    // INCR: entries per scan tile of the new keys (dead entries in the sentinel cell's tile).  S'
+    // is in the previous frame's order, so a wave's entries almost always share one tile: each
+    // wave notes (tile, count) in LDS and thread 0 adds the block's few distinct tiles after the
+    // barrier below (an atomic wave-instruction costs ~50 ns of its CU's atomic path whatever its
+    // lanes: one per wave made keygen 13 -> 22 us); a wave that spans tiles adds its own.
+    // k_scan64 takes a tile's start in the new frame from these counts (no pass over the cell
+    // counts before it); k_cell_merge zeroes them again.
+    __shared__ uint32_t s_tt[256 / WAVE][KG_PER], s_tc[256 / WAVE][KG_PER];
     if (INCR) {
 #pragma unroll
         for (int u = 0; u < KG_PER; ++u) {
             unsigned long long act = __ballot(kt[u] != 0xFFFFFFFFu);
-            while (act) {
+            uint32_t t0 = 0xFFFFFFFFu, c0 = 0u;
+            if (act) {
+                const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1u;
+                t0 = (uint32_t)__builtin_amdgcn_readlane((int)kt[u], (int)lead);
+                const unsigned long long m = __ballot(kt[u] == t0);
+                c0 = (uint32_t)__popcll(m);
+                act &= ~m;
+            }
+            while (act) {  // rare: the wave's entries span tiles
                 const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1u;
                 const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)kt[u], (int)lead);
                 const unsigned long long m = __ballot(kt[u] == t);
                 if (lane() == lead) atomicAdd(&tent[t], (unsigned long long)__popcll(m));
                 act &= ~m;
+            }
+            if (lane() == 0) {
+                s_tt[threadIdx.x / WAVE][u] = t0;
+                s_tc[threadIdx.x / WAVE][u] = c0;
             }
         }
     }
@@ -543,6 +559,21 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         if (special && threadIdx.x == 0 && t * 256u < n_prev) special[t] = sp_any ? 1u : 0u;
     }
     const uint32_t nw = (uint32_t)__syncthreads_count(nwr >= 1) + (KG_PER > 1 ? (uint32_t)__syncthreads_count(nwr >= 2) : 0u);
+    if (INCR && threadIdx.x == 0) {  // the block's (tile, count) notes, one add per distinct tile
+        uint32_t t = 0xFFFFFFFFu, c = 0u;
+        for (int u = 0; u < KG_PER; ++u)  // (entry order: the notes of one tile come together)
+            for (int q = 0; q < 256 / WAVE; ++q) {
+                const uint32_t tq = s_tt[q][u], cq = s_tc[q][u];
+                if (!cq) continue;
+                if (tq != t) {
+                    if (c) atomicAdd(&tent[t], (unsigned long long)c);
+                    t = tq;
+                    c = 0u;
+                }
+                c += cq;
+            }
+        if (c) atomicAdd(&tent[t], (unsigned long long)c);
+    }
     if (threadIdx.x == 0) {
         reinterpret_cast<uint32_t *>(blk)[2 * gridDim.x + blockIdx.x] = nw;
         float a = s_m[0][0], b = s_m[1][0];
