@@ -466,12 +466,14 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
     }
     float dr = 0.0f, bm = 0.0f;
     bool near[KG_PER];
+    uint32_t kt[KG_PER];  // INCR: the scan tile of each entry's new key (0xFFFFFFFF: no entry)
     uint32_t nwr = 0;  // entries this flush's ops wrote (GWAOI_F_UNIQUE_MOVES: one per op that applied)
 #pragma unroll
     for (int u = 0; u < KG_PER; ++u) {
         const uint32_t i = base + 256u * (uint32_t)u;
         const bool inp = i < n_prev;
         near[u] = false;  // live at t-1 and t in the same space, moved <= FAR_FRAC * D per axis
+        kt[u] = 0xFFFFFFFFu;
         if (i >= n) continue;
         uint32_t key = sentinel;
         Rec16 rr = r[u];
@@ -496,6 +498,7 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
             bm = fmaxf(bm, fmaxf(fabsf(rr.x), fabsf(rr.z)));
         }
         keys[i] = key;
+        kt[u] = key / (uint32_t)S64_TILE;
         if (!INCR) vals[i] = i;
         // INCR: only the entities that changed cell count: an arrival in the new cell (low word), a
         // departure from the old one (high word); a cell's stayers are its previous count minus
@@ -503,15 +506,38 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         if (INCR && key != old[u]) {
             if (key != sentinel) atomicAdd(&cnt64[key], 1ull);
             if (old[u] != sentinel) atomicAdd(&cnt64[old[u]], 1ull << 32);
-            // ... and, when it changes scan tile (a few hundred entities per tick at config 3),
-            // the net flow of entries into each tile (two's complement): k_scan64 moves a tile's
-            // first cell by the flow into the tiles before it, with no pass over their cells.
-            // (Entries entering or leaving the frame flow from / to the sentinel cell's tile,
-            // the last one, whose own flow no tile start includes.)
-            const uint32_t tn = key / (uint32_t)S64_TILE, to = old[u] / (uint32_t)S64_TILE;
-            if (tn != to) {
-                atomicAdd(&tent[tn], 1ull);
-                atomicAdd(&tent[to], ~0ull);
+        }
+    }
+    // INCR: entries per scan tile of the new keys (dead entries in the sentinel cell's tile).  S'
+    // is in the previous frame's order, so a wave's entries almost always share one tile: each
+    // wave notes (tile, count) in LDS and thread 0 adds the block's few distinct tiles after the
+    // barrier below (an atomic wave-instruction costs ~50 ns of its CU's atomic path whatever its
+    // lanes: one per wave made keygen 13 -> 22 us); a wave that spans tiles adds its own.
+    // k_scan64 takes a tile's start in the new frame from these counts (no pass over the cell
+    // counts before it); k_cell_merge zeroes them again.
+    __shared__ uint32_t s_tt[256 / WAVE][KG_PER], s_tc[256 / WAVE][KG_PER];
+    if (INCR) {
+#pragma unroll
+        for (int u = 0; u < KG_PER; ++u) {
+            unsigned long long act = __ballot(kt[u] != 0xFFFFFFFFu);
+            uint32_t t0 = 0xFFFFFFFFu, c0 = 0u;
+            if (act) {
+                const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1u;
+                t0 = (uint32_t)__builtin_amdgcn_readlane((int)kt[u], (int)lead);
+                const unsigned long long m = __ballot(kt[u] == t0);
+                c0 = (uint32_t)__popcll(m);
+                act &= ~m;
+            }
+            while (act) {  // rare: the wave's entries span tiles
+                const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1u;
+                const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)kt[u], (int)lead);
+                const unsigned long long m = __ballot(kt[u] == t);
+                if (lane() == lead) atomicAdd(&tent[t], (unsigned long long)__popcll(m));
+                act &= ~m;
+            }
+            if (lane() == 0) {
+                s_tt[threadIdx.x / WAVE][u] = t0;
+                s_tc[threadIdx.x / WAVE][u] = c0;
             }
         }
     }
@@ -533,6 +559,21 @@ __global__ __launch_bounds__(256) void k_keygen(Rec16 *s_rec, const SlotSp *__re
         if (special && threadIdx.x == 0 && t * 256u < n_prev) special[t] = sp_any ? 1u : 0u;
     }
     const uint32_t nw = (uint32_t)__syncthreads_count(nwr >= 1) + (KG_PER > 1 ? (uint32_t)__syncthreads_count(nwr >= 2) : 0u);
+    if (INCR && threadIdx.x == 0) {  // the block's (tile, count) notes, one add per distinct tile
+        uint32_t t = 0xFFFFFFFFu, c = 0u;
+        for (int u = 0; u < KG_PER; ++u)  // (entry order: the notes of one tile come together)
+            for (int q = 0; q < 256 / WAVE; ++q) {
+                const uint32_t tq = s_tt[q][u], cq = s_tc[q][u];
+                if (!cq) continue;
+                if (tq != t) {
+                    if (c) atomicAdd(&tent[t], (unsigned long long)c);
+                    t = tq;
+                    c = 0u;
+                }
+                c += cq;
+            }
+        if (c) atomicAdd(&tent[t], (unsigned long long)c);
+    }
     if (threadIdx.x == 0) {
         reinterpret_cast<uint32_t *>(blk)[2 * gridDim.x + blockIdx.x] = nw;
         float a = s_m[0][0], b = s_m[1][0];
@@ -1089,10 +1130,11 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     const size_t base = (size_t)b * S64_TILE;
     const uint32_t tid = threadIdx.x;
     // every global operand first, in one round trip: the tile's counts, the previous starts of its
-    // cells (for the final write) and this thread's share of the earlier tiles' net flows
-    // (keygen's, two's complement: their sum is how far this tile's first cell moves)
+    // cells (for the final write) and this thread's share of the earlier tiles' entries (keygen's
+    // per-tile counts of the new keys: their sum is where this tile starts in the new frame)
     unsigned long long pre = 0;
     for (uint32_t q = tid; q < b; q += SC_T) pre += agg[q];
+    const uint32_t p_cs0 = p_cs[base];  // where this tile started in the previous frame
     uint32_t pcs[S64_I];
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {
@@ -1122,10 +1164,10 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
             if (v[q] && c0 + q + 1 < n) list[base + off++] = (uint32_t)(c0 + q);
         if (tid == 0) tcnt[b] = t32;
     }
-    // the tile's offset: the sum of the earlier tiles' flows, no look-back chain: a chain
+    // the tile's offset: the sum of the earlier tiles' entries, no look-back chain: a chain
     // serialises ~500 tiles at ~20 ns a hop, the block-wide sum of <= 1k words does not.  Its
     // first cell moves by dt = (new start) - (previous start) = the arrivals minus the departures
-    // of every cell before the tile = the net flow into the tiles before it.
+    // of every cell before the tile.
     __shared__ unsigned long long s_pre[SC_T / WAVE];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
@@ -1134,7 +1176,7 @@ __global__ __launch_bounds__(SC_T) void k_scan64(const unsigned long long *__res
     unsigned long long e = 0;
 #pragma unroll
     for (int q = 0; q < SC_T / WAVE; ++q) e += s_pre[q];
-    const uint32_t dt = (uint32_t)e;
+    const uint32_t dt = (uint32_t)e - p_cs0;
 #pragma unroll
     for (int q = 0; q < S64_I; ++q) {  // a thread rewrites only the words it read; bit 31: c changed
         tile[p64(tid * S64_I + (uint32_t)q)] = run | (v[q] ? (unsigned long long)SHIFT_CHANGED : 0ull);
