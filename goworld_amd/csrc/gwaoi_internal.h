@@ -278,11 +278,34 @@ struct SpecialJob {
     const uint32_t *special;
     uint32_t n_tiles;
 };
+// The gather (launch_gather's arguments), run inside the incremental sort's merge launch
+// (k_merge_gather) when gj != nullptr: block b gathers scan tile b's range of the new frame once it
+// has merged the tile's changed cells, and writes bbox part b (incr_sort_tiles parts, which
+// launch_finish folds).  The sort's perm / skeys are the gather's.
+struct GatherJob {
+    uint32_t n_new, n_prev;
+    const Rec16 *s_rec;
+    const SlotSp *s_ss;
+    const Rec16 *p_rec;
+    const SlotSp *p_ss;
+    Rec16 *f_rec;
+    SlotSp *f_ss;
+    Rec16 *o_rec;
+    uint4 *cand;
+    const SpaceGrid *grid;
+    SlotTab info;
+    TickScalars *sc;
+    int4 *bbox;
+    uint32_t n_spaces;
+    void *parts;
+};
+// scan tiles of a grid of total_cells cells (the fused gather's bbox parts)
+uint32_t incr_sort_tiles(uint32_t total_cells);
 void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, const uint32_t *p_key,
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, const SpecialJob *sp, hipStream_t st);
+                      TickScalars *sc, const SpecialJob *sp, const GatherJob *gj, hipStream_t st);
 // LSD radix sort of (key,val) pairs on `bits` low key bits.  Returns which
 // buffer (0 or 1) holds the result.
 struct SortBuffers {
@@ -345,10 +368,12 @@ void launch_pairs_out(const void *events, uint64_t n_pairs, void *dst, hipStream
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap_tmp, uint64_t cap_out, const TickScalars *sc, TickOut *out,
-                   uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   uint32_t *dcount, hipStream_t st);
-// Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish.
+                   uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, uint32_t n_parts, int4 *hbbox,
+                   const uint32_t *tile_work, uint32_t *tile_order, uint32_t *dcount, hipStream_t st);
+// Size of k_gather's level-1 bbox parts (+ the fold's scratch part), folded by launch_finish;
+// gather_parts: how many k_gather writes for n entries.
 size_t bbox_part_bytes(uint32_t n);
+uint32_t gather_parts(uint32_t n);
 void launch_neighbors(FrameView F, SlotTab info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st);
 // Zero `n` uint32 (rare re-run path).

@@ -1292,27 +1292,38 @@ __device__ __forceinline__ void cell_merge_one(uint32_t c, const uint32_t *__res
     }
 }
 
-__global__ void k_cell_merge(const uint32_t *__restrict__ p_cell_start, const uint32_t *__restrict__ cell_start,
-                             const uint32_t *__restrict__ keys, const uint32_t *__restrict__ arr_pos,
-                             uint32_t *arr_idx, uint32_t total_cells, uint32_t n_total, uint32_t sentinel,
-                             uint32_t *perm, uint32_t *skeys, const uint32_t *__restrict__ list,
-                             const unsigned long long *__restrict__ tcnt, unsigned long long *tent) {
+struct MergeArgs {
+    const uint32_t *p_cell_start, *cell_start, *keys, *arr_pos;
+    uint32_t *arr_idx;
+    uint32_t total_cells, n_total, sentinel;
+    uint32_t *perm, *skeys;
+    const uint32_t *list;
+    const unsigned long long *tcnt;
+    unsigned long long *tent;
+};
+
+// Block b of the merge: scan tile b's changed cells (k_scan64's list), every lane busy (one lane per
+// cell of the whole grid, most of them idle: 10.2 against 7.6 us at cfg3).  Dead tail: the entries
+// past the device's live count get sentinel keys and no source (so a host count that disagrees
+// with the device's -- a device batch breaking its rules -- finds sentinels, not a previous
+// flush's values, at [n_new, n_total)); returns that count.
+__device__ __forceinline__ uint32_t merge_tile(const MergeArgs &M) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (threadIdx.x == 0) tent[blockIdx.x] = 0ull;  // keygen's per-tile entries, read by k_scan64: zero for the next flush
-    // entries past the live count are dead: sentinel keys, no source (so a host count that
-    // disagrees with the device's -- a device batch breaking its rules -- finds sentinels, not
-    // a previous flush's values, at [n_new, n_total))
-    for (uint32_t k = cell_start[total_cells] + c; k < n_total; k += gridDim.x * blockDim.x) {
-        skeys[k] = sentinel;
-        perm[k] = 0xFFFFFFFFu;
+    if (threadIdx.x == 0) M.tent[blockIdx.x] = 0ull;  // keygen's per-tile entries, read by k_scan64: zero for the next flush
+    const uint32_t n_live = M.cell_start[M.total_cells];
+    for (uint32_t k = n_live + c; k < M.n_total; k += gridDim.x * blockDim.x) {
+        M.skeys[k] = M.sentinel;
+        M.perm[k] = 0xFFFFFFFFu;
     }
-    // block b: scan tile b's changed cells (k_scan64's list), every lane busy (one lane per
-    // cell of the whole grid, most of them idle: 10.2 against 7.6 us at cfg3)
-    const uint32_t nc = (uint32_t)tcnt[blockIdx.x];
-    const uint32_t *L = list + (size_t)blockIdx.x * S64_TILE;
+    const uint32_t nc = (uint32_t)M.tcnt[blockIdx.x];
+    const uint32_t *L = M.list + (size_t)blockIdx.x * S64_TILE;
     for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
-        cell_merge_one(L[k], p_cell_start, cell_start, keys, arr_pos, arr_idx, sentinel, perm, skeys, n_total);
+        cell_merge_one(L[k], M.p_cell_start, M.cell_start, M.keys, M.arr_pos, M.arr_idx, M.sentinel, M.perm, M.skeys,
+                       M.n_total);
+    return n_live;
 }
+
+__global__ void k_cell_merge(MergeArgs M) { (void)merge_tile(M); }
 // ----------------------------------------------------------------- bbox ------
 
 __device__ __forceinline__ int f2o(float f) {
@@ -1403,6 +1414,22 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
                                            uint32_t n_total, TickScalars *sc, uint32_t *f_key, uint32_t &cur,
                                            int (&bv)[4]);
 
+// Fewer live entries than the host counted (a device Enter / Leave batch broke its rules, or a
+// broken permutation): the flush fails and poisons the world, but it must not fault first.  The
+// entry becomes an inert placeholder: slot 0 of space 0 at NaN (no relation, no slot-indexed
+// write, no bbox).
+__device__ __forceinline__ void gather_placeholder(uint32_t k, Rec16 *f_rec, SlotSp *f_ss, Rec16 *o_rec, uint4 *cand,
+                                                   TickScalars *sc) {
+    atomicOr(&sc->err, ERR_COUNT_MISMATCH);
+    Rec16 z;
+    z.x = z.z = qnan();
+    z.s = 0;
+    st_rec(f_rec, k, z);
+    st_rec(o_rec, k, z);
+    reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(0u, 0u);
+    cand[k] = make_uint4(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u);
+}
+
 // Per-cell x bounds of the new frame (k_combined trims the X' rows' end cells by them).  The
 // frame is sorted by cell, so a cell's entries are one run: a segmented fold inside the wave,
 // then the run's first lane writes.  A run that crosses a wave boundary gets (-inf, +inf) from the
@@ -1438,18 +1465,7 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     if (f_key) f_key[k] = key;  // (nullptr: the sort wrote the frame's keys in place)
     const uint32_t i = perm[k];
     if (key >= sentinel || i >= n_total) {
-        // Fewer live entries than the host counted (a device Enter / Leave batch broke its rules, or a
-        // broken permutation): the flush fails and poisons the world, but it must not fault first.  The
-        // entry becomes an inert placeholder: slot 0 of space 0 at NaN (no relation, no slot-indexed
-        // write, no bbox).
-        atomicOr(&sc->err, ERR_COUNT_MISMATCH);
-        Rec16 z;
-        z.x = z.z = qnan();
-        z.s = 0;
-        st_rec(f_rec, k, z);
-        st_rec(o_rec, k, z);
-        reinterpret_cast<uint2 *>(f_ss)[k] = make_uint2(0u, 0u);
-        cand[k] = make_uint4(0x7FC00000u, 0x7FC00000u, 0x7FC00000u, 0x7FC00000u);
+        gather_placeholder(k, f_rec, f_ss, o_rec, cand, sc);
         return;
     }
     // S' and previous-frame operands of entry i in one round trip (the previous record is loaded
@@ -1482,6 +1498,91 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
     cur = ss.sp;
     bv[0] = bv[2] = f2o(now.x);
     bv[1] = bv[3] = f2o(now.z);
+}
+
+// The incremental sort's merge and the gather in one launch (GatherJob): block b merges scan tile
+// b's changed cells, then gathers the tile's range of the new frame, [cell_start[b S64_TILE],
+// cell_start[(b + 1) S64_TILE]): k_arrive placed the stayers of its unchanged cells and the block
+// itself its changed cells, so the permutation it reads is complete with no grid-wide barrier
+// (and the launch boundary between the two passes, with the tail of each, is gone).  GU entries
+// per thread in flight (every load of the group before its stores); the block folds its entries'
+// bbox into part b (a thread's entries are in key order, so its runs of one space are too).
+constexpr int GU = 4;
+__global__ __launch_bounds__(256) void k_merge_gather(MergeArgs M, GatherJob G) {
+    const uint32_t n_live = merge_tile(M);
+    __syncthreads();  // the block's merged cells before their gather
+    const uint32_t b = blockIdx.x, tc = M.total_cells, n_new = G.n_new, sentinel = M.sentinel;
+    if (b == 0 && threadIdx.x == 0 && n_live != n_new) atomicOr(&G.sc->err, ERR_COUNT_MISMATCH);
+    // entries the host counted but the device did not (placed in no tile's range): placeholders
+    for (uint32_t k = n_live + b * blockDim.x + threadIdx.x; k < n_new; k += gridDim.x * blockDim.x)
+        gather_placeholder(k, G.f_rec, G.f_ss, G.o_rec, G.cand, G.sc);
+    const uint32_t lo = min(M.cell_start[min(b * S64_TILE, tc)], n_new);
+    const uint32_t hi = min(M.cell_start[min((b + 1) * S64_TILE, tc)], n_new);
+    uint32_t cur = SP_DEAD;
+    int bv[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+    for (uint32_t k0 = lo + threadIdx.x; k0 < hi; k0 += GU * 256) {
+        uint32_t key[GU], idx[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const uint32_t k = k0 + u * 256;
+            key[u] = k < hi ? M.skeys[k] : sentinel;
+            idx[u] = k < hi ? M.perm[k] : 0xFFFFFFFFu;
+        }
+        SlotSp ss[GU];
+        Rec16 now[GU], pr[GU];
+        uint32_t psp[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const uint32_t i = idx[u];
+            const bool ok = key[u] < sentinel && i < M.n_total, inp = ok && i < G.n_prev;
+            ss[u].slot = 0;
+            ss[u].sp = SP_DEAD;
+            now[u].x = now[u].z = 0.0f;
+            now[u].s = 0;
+            pr[u] = now[u];
+            psp[u] = SP_DEAD;
+            if (ok) {
+                ss[u] = ld_ss(G.s_ss, i);
+                now[u] = ld_rec(G.s_rec, i);
+            }
+            if (inp) {
+                psp[u] = ld_ss(G.p_ss, i).sp;
+                pr[u] = ld_rec(G.p_rec, i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const uint32_t k = k0 + u * 256, i = idx[u];
+            if (k >= hi) continue;
+            if (key[u] >= sentinel || i >= M.n_total) {
+                gather_placeholder(k, G.f_rec, G.f_ss, G.o_rec, G.cand, G.sc);
+                continue;
+            }
+            const bool inp = i < G.n_prev;
+            st_rec(G.f_rec, k, now[u]);
+            reinterpret_cast<uint2 *>(G.f_ss)[k] = make_uint2(ss[u].slot, ss[u].sp);
+            G.info.rank[ss[u].slot] = k;
+            if (!inp || psp[u] != ss[u].sp) G.info.sp[ss[u].slot] = ss[u].sp;  // (as gather_one)
+            Rec16 o;
+            o.x = o.z = qnan();
+            o.s = 0;
+            if (inp && psp[u] == ss[u].sp) o = pr[u];
+            st_rec(G.o_rec, k, o);
+            G.cand[k] = cand_of(now[u], o, FAR_FRAC * G.grid[ss[u].sp].D);
+            if (ss[u].sp != cur) {
+                if (cur != SP_DEAD) bbox_flush(G.bbox, G.n_spaces, cur, bv);
+                cur = ss[u].sp;
+                bv[0] = bv[1] = INT_MAX;
+                bv[2] = bv[3] = INT_MIN;
+            }
+            const int fx = f2o(now[u].x), fz = f2o(now[u].z);
+            bv[0] = min(bv[0], fx);
+            bv[1] = min(bv[1], fz);
+            bv[2] = max(bv[2], fx);
+            bv[3] = max(bv[3], fz);
+        }
+    }
+    bbox_block(cur, bv, G.bbox, G.n_spaces, reinterpret_cast<BBoxPart *>(G.parts) + b);
 }
 
 // Entities per cell from the sorted keys: one atomic per run of equal keys
@@ -3173,7 +3274,7 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
                       const uint32_t *p_cell_start, unsigned long long *cnt64, uint32_t total_cells,
                       uint32_t sentinel, uint32_t *cell_start, uint32_t *arr_pos, uint32_t *arr_idx,
                       unsigned long long *tmp, uint32_t *perm, uint32_t *skeys, const float *blk,
-                      TickScalars *sc, const SpecialJob *sp, hipStream_t st) {
+                      TickScalars *sc, const SpecialJob *sp, const GatherJob *gj, hipStream_t st) {
     const size_t m = (size_t)total_cells + 1;
     const uint32_t nb = cdiv(m, S64_TILE);
     uint32_t *shift = arr_pos + m;  // the caller allocates arr_pos with 3 (total_cells + 1) words
@@ -3190,10 +3291,13 @@ void incremental_sort(const uint32_t *keys, uint32_t n_total, uint32_t n_prev, c
         k_arrive<<<cdiv(n_total, 256), 256, 0, st>>>(keys, n_total, n_prev, p_key, sentinel, arr_pos, arr_idx, cnt64,
                                                      shift, perm, skeys);
     }
-    k_cell_merge<<<nb, 256, 0, st>>>(
-        p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_total, sentinel, perm, skeys, list, tcnt,
-        tent);
+    const MergeArgs M{p_cell_start, cell_start, keys, arr_pos, arr_idx, total_cells, n_total, sentinel,
+                      perm, skeys, list, tcnt, tent};
+    if (gj) k_merge_gather<<<nb, 256, 0, st>>>(M, *gj);
+    else k_cell_merge<<<nb, 256, 0, st>>>(M);
 }
+
+uint32_t incr_sort_tiles(uint32_t total_cells) { return cdiv((size_t)total_cells + 1, S64_TILE); }
 
 size_t scan_tmp_elems(size_t n) {
     if (n <= SC1_MAX) return 0;
@@ -3302,11 +3406,9 @@ size_t tile_total_elems(size_t n_entries) { return n_entries + 1 + cdiv(n_entrie
 void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_base, uint32_t n_entries,
                    uint32_t n_enter_entries, const uint32_t *tmp_pairs,
                    uint32_t *out_pairs, uint64_t cap_tmp, uint64_t cap_out, const TickScalars *sc, TickOut *out,
-                   uint32_t n_new, int4 *bbox,
-                   uint32_t n_spaces, void *parts_mem, int4 *hbbox, const uint32_t *tile_work, uint32_t *tile_order,
-                   uint32_t *dcount, hipStream_t st) {
+                   uint32_t n_new, int4 *bbox, uint32_t n_spaces, void *parts_mem, uint32_t np, int4 *hbbox,
+                   const uint32_t *tile_work, uint32_t *tile_order, uint32_t *dcount, hipStream_t st) {
     const uint32_t R = cdiv(n_entries, FT);
-    const uint32_t np = cdiv(std::max(n_new, 1u), 256);  // k_gather's blocks
     if (!n_new) tile_order = nullptr;
     k_finish<<<R + 1 + (tile_order ? N_XCD : 0u), 256, 0, st>>>(
         tile_total, tile_base, n_entries, n_enter_entries, reinterpret_cast<const uint2 *>(tmp_pairs),
@@ -3315,7 +3417,8 @@ void launch_finish(const uint32_t *tile_total, const unsigned long long *tile_ba
         n_spaces, hbbox, tile_work, combined_tiles(n_new), tile_order, dcount);
 }
 
-size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)cdiv(std::max(n, 1u), 256) + 2); }
+size_t bbox_part_bytes(uint32_t n) { return sizeof(BBoxPart) * ((size_t)gather_parts(n) + 2); }
+uint32_t gather_parts(uint32_t n) { return cdiv(std::max(n, 1u), 256); }  // k_gather's blocks
 
 void launch_neighbors(FrameView F, SlotTab info, uint32_t slot, uint32_t *out, uint32_t cap,
                       uint32_t *count, hipStream_t st) {

@@ -183,6 +183,7 @@ struct FlushSet {
     uint32_t *events = nullptr;  // ev_cap (a,b) pairs: [enters | leaves] in tile order
     uint64_t ev_cap = 0;         // capacity in directed pairs
     void *bbox_parts = nullptr;  // bbox level-1 partials
+    uint32_t n_parts = 0;        // ... written by the flush (k_gather's blocks or k_merge_gather's tiles)
     char *dev_out = nullptr;     // TickOut + int4 bbox[max_spaces] (device: the bbox fold)
     char *h_out = nullptr;       // pinned: the flush summary (TickOut + bbox)
     char *d_hout = nullptr;      // h_out as the device sees it: k_finish writes the summary there
@@ -828,7 +829,7 @@ EvCaps launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P
     stage_begin(w, S, ST_FINISH);
     gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->events_tmp, S.events,
                       caps.tmp, caps.out, S.sc, reinterpret_cast<gw::TickOut *>(S.d_hout), Fn.n,
-                      dev_bbox(S), w->n_space_ids, S.bbox_parts,
+                      dev_bbox(S), w->n_space_ids, S.bbox_parts, S.n_parts,
                       reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
                       order ? w->tile_work : nullptr, order ? w->tile_order : nullptr,
                       reinterpret_cast<uint32_t *>(S.dev_out), st);
@@ -1051,11 +1052,36 @@ int tick_launch(gwaoi_world *w) {
         spj.special = w->special;
         spj.n_tiles = TBp;
     }
+    // the gather rides on the incremental sort's merge launch (k_merge_gather, one bbox part per
+    // scan tile) unless it is timed or the grid has more scan tiles than the set has parts
+    const bool ga_fused = incr && !(w->timing_mask >> ST_GATHER & 1u) &&
+                          gw::incr_sort_tiles(total_cells) <= gw::gather_parts(w->max_slots);
+    S.n_parts = ga_fused ? gw::incr_sort_tiles(total_cells) : gw::gather_parts(n_new);
+    gw::GatherJob gj{};
+    if (ga_fused) {
+        gj.n_new = n_new;
+        gj.n_prev = n_prev;
+        gj.s_rec = S.srec;
+        gj.s_ss = s_ss_view;
+        gj.p_rec = P.rec;
+        gj.p_ss = P.ss;
+        gj.f_rec = Fn.rec;
+        gj.f_ss = Fn.ss;
+        gj.o_rec = S.orec;
+        gj.cand = S.cand;
+        gj.grid = Fn.grid;
+        gj.info = w->sinfo;
+        gj.sc = S.sc;
+        gj.bbox = dev_bbox(S);
+        gj.n_spaces = w->n_space_ids;
+        gj.parts = S.bbox_parts;
+    }
     if (incr) {
         w->dbg.incremental_sorts++;
         gw::incremental_sort(w->keys[0], n_total, n_prev, P.key, P.cell_start, w->cnt64, total_cells,
                              total_cells, Fn.cell_start, w->arr_pos, w->arr_idx, w->scan64_tmp, w->vals[1],
-                             Fn.key, w->blk, S.sc, sp_fused ? &spj : nullptr, st);  // the sorted keys ARE the frame's
+                             Fn.key, w->blk, S.sc, sp_fused ? &spj : nullptr, ga_fused ? &gj : nullptr,
+                             st);  // the sorted keys ARE the frame's
     } else {
         gw::SortBuffers sb;
         sb.keys[0] = w->keys[0];
@@ -1071,12 +1097,13 @@ int tick_launch(gwaoi_world *w) {
     const uint32_t *perm = w->vals[which];
 
     // ---- new frame + previous state in the new order
-    stage_begin(w, S, ST_GATHER);
-    gw::launch_gather(perm, n_new, n_prev, S.srec, s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, S.orec, S.cand, Fn.grid,
-                      seq_base, w->sinfo, skeys,
-                      total_cells, n_total, S.sc, incr ? nullptr : Fn.key, dev_bbox(S), w->n_space_ids,
-                      S.bbox_parts, st);
-    stage_end(w, S, ST_GATHER);
+    if (!ga_fused) {
+        stage_begin(w, S, ST_GATHER);
+        gw::launch_gather(perm, n_new, n_prev, S.srec, s_ss_view, P.rec, P.ss, Fn.rec, Fn.ss, S.orec, S.cand,
+                          Fn.grid, seq_base, w->sinfo, skeys, total_cells, n_total, S.sc, incr ? nullptr : Fn.key,
+                          dev_bbox(S), w->n_space_ids, S.bbox_parts, st);
+        stage_end(w, S, ST_GATHER);
+    }
 
     // ---- cell_start = exclusive scan of entities per cell (zeroed by the prologue;
     // the incremental sort has written it already)
