@@ -1522,11 +1522,13 @@ __global__ __launch_bounds__(256) void k_merge_gather(MergeArgs M, GatherJob G) 
     int bv[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
     for (uint32_t k0 = lo + threadIdx.x; k0 < hi; k0 += GU * 256) {
         uint32_t key[GU], idx[GU];
+        // every load of the group in flight: indices clamped to a valid entry, not branched on (a
+        // load under a branch is waited for before the next); the values of the clamped ones unused
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
-            const uint32_t k = k0 + u * 256;
-            key[u] = k < hi ? M.skeys[k] : sentinel;
-            idx[u] = k < hi ? M.perm[k] : 0xFFFFFFFFu;
+            const uint32_t k = min(k0 + u * 256, hi - 1);
+            key[u] = M.skeys[k];
+            idx[u] = M.perm[k];
         }
         SlotSp ss[GU];
         Rec16 now[GU], pr[GU];
@@ -1535,20 +1537,11 @@ __global__ __launch_bounds__(256) void k_merge_gather(MergeArgs M, GatherJob G) 
         for (int u = 0; u < GU; ++u) {
             const uint32_t i = idx[u];
             const bool ok = key[u] < sentinel && i < M.n_total, inp = ok && i < G.n_prev;
-            ss[u].slot = 0;
-            ss[u].sp = SP_DEAD;
-            now[u].x = now[u].z = 0.0f;
-            now[u].s = 0;
-            pr[u] = now[u];
-            psp[u] = SP_DEAD;
-            if (ok) {
-                ss[u] = ld_ss(G.s_ss, i);
-                now[u] = ld_rec(G.s_rec, i);
-            }
-            if (inp) {
-                psp[u] = ld_ss(G.p_ss, i).sp;
-                pr[u] = ld_rec(G.p_rec, i);
-            }
+            const uint32_t ic = ok ? i : 0u, ip = inp ? i : 0u;  // (S' and the previous frame hold >= 1 entry)
+            ss[u] = ld_ss(G.s_ss, ic);
+            now[u] = ld_rec(G.s_rec, ic);
+            psp[u] = ld_ss(G.p_ss, ip).sp;
+            pr[u] = ld_rec(G.p_rec, ip);  // (psp / pr are read only for an entry in the previous frame)
         }
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
@@ -2466,6 +2459,22 @@ __device__ void combined_sweep(CombinedLds &L, const int w, const LaneA &A, cons
 #ifdef GWAOI_EXP_BLOCKTIME
 constexpr uint32_t BT_MAX = 65536;
 __device__ unsigned long long gw_blocktime[3 * BT_MAX];
+constexpr uint32_t BT_FIN = 40000;  // k_finish's blocks (k_combined's units stay below it at config 3)
+#define BT_STAMP(slot) \
+    do { \
+        if (threadIdx.x == 0) gw_blocktime[3 * (BT_FIN + 2000) + (slot)] = wall_clock64(); \
+    } while (0)
+#define BT_OSTAMP(slot) \
+    do { \
+        if (threadIdx.x == 0 && blockIdx.x == 0) gw_blocktime[3 * (BT_FIN + 2004) + (slot)] = wall_clock64(); \
+    } while (0)
+#else
+#define BT_STAMP(slot) \
+    do { \
+    } while (0)
+#define BT_OSTAMP(slot) \
+    do { \
+    } while (0)
 #endif
 // The schedule (tile_order, built by k_finish for the next flush from this flush's measured time
 // per tile; any schedule gives the same events): each XCD x gets a contiguous range of tiles, cut
@@ -2718,9 +2727,9 @@ constexpr int TO_BANDS = GWAOI_ORDER_BANDS;
 static_assert(TO_NB * TO_BANDS <= 256, "one histogram bin per thread");
 
 // Counting sort of range [lo, hi) of tiles by (band, descending work class) into tile_order[1 + ...].
-// tile_work: [measured time of each of the nb tiles | their candidate counts].
-__device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t lo, uint32_t hi,
-                            uint32_t *tile_order) {
+// wt(i), wc(i): tile i's measured time and candidate count (tile_work's two halves, 16-bit).
+template <class WT, class WC>
+__device__ void order_range(WT wt, WC wc, uint32_t lo, uint32_t hi, uint32_t *tile_order) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t ws[256 / WAVE];
     const uint32_t len = hi - lo;
@@ -2742,7 +2751,7 @@ __device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t nb,
         hist[threadIdx.x] = 0;
         if (threadIdx.x == 0) s_top = s_p50 = 0;
         __syncthreads();
-        for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[wcls(tile_work[nb + i], 64)], 1u);
+        for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[wcls(wc(i), 64)], 1u);
         __syncthreads();
         uint32_t total;
         const uint32_t ex = block_excl_scan<256>(hist[threadIdx.x], ws, total);
@@ -2763,7 +2772,7 @@ __device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t nb,
     __syncthreads();
     auto cls = [&](uint32_t i) {  // band-major, then descending work: bin 0 = heaviest of band 0
         const uint32_t band = (uint32_t)(((unsigned long long)(i - lo) * TO_BANDS) / max(len, 1u));
-        return band * TO_NB + wcls(tile_work[i], 40);
+        return band * TO_NB + wcls(wt(i), 40);
     };
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(i)], 1u);
     __syncthreads();
@@ -2780,15 +2789,50 @@ __device__ void order_range(const uint32_t *__restrict__ tile_work, uint32_t nb,
 // the eight ranges cut at the eighths of the cumulative measured time (every block computes the
 // same cuts; each thread sums a contiguous segment, so one scan finds them), at most range_max
 // long; range x heaviest first; the cuts at tile_order[order_meta .. order_meta + 8].
+// Tiles whose times and counts the block stages in LDS (2 x 16 KB), as 16-bit values: 655 us of
+// measured time or 65535 candidates saturate, above every work class's top (and no tile of a launch
+// takes that long), so the schedule is the same from either copy.
+constexpr uint32_t TO_LDS = 8192;
 __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
     __shared__ uint32_t s_cut[N_XCD + 1];
     __shared__ unsigned long long s_sum[256];
+    __shared__ uint16_t s_t[TO_LDS], s_c[TO_LDS];
     const uint32_t tid = threadIdx.x;
+    // both halves into LDS with coalesced loads (TO_U of each in flight per thread), then every pass
+    // reads LDS: a thread's contiguous segment read from global memory touched a line per lane per
+    // load, and the range's counts were a round trip of their own (12 us at config 3)
+    const bool lds = nb <= TO_LDS;
+    if (lds) {
+        constexpr uint32_t TO_U = 8;
+        for (uint32_t i0 = tid; i0 < nb; i0 += TO_U * 256) {
+            uint32_t t[TO_U], c[TO_U];
+#pragma unroll
+            for (uint32_t u = 0; u < TO_U; ++u) {  // (clamped, not branched: a load under a branch
+                const uint32_t i = min(i0 + u * 256, nb - 1);  // waits for itself before the next)
+                t[u] = tile_work[i];
+                c[u] = tile_work[nb + i];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < TO_U; ++u) {
+                const uint32_t i = i0 + u * 256;
+                if (i < nb) {
+                    s_t[i] = (uint16_t)min(t[u], 65535u);
+                    s_c[i] = (uint16_t)min(c[u], 65535u);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    auto wt = [&](uint32_t i) -> uint32_t { return lds ? (uint32_t)s_t[i] : min(tile_work[i], 65535u); };
+    auto wc = [&](uint32_t i) -> uint32_t { return lds ? (uint32_t)s_c[i] : min(tile_work[nb + i], 65535u); };
+    BT_OSTAMP(0);
     const uint32_t seg = (nb + 255) / 256, s0 = min(nb, tid * seg), s1 = min(nb, s0 + seg);
     unsigned long long my = 0;
-    for (uint32_t i = s0; i < s1; ++i) my += tile_work[i];
+    for (uint32_t i = s0; i < s1; ++i) my += wt(i);
     s_sum[tid] = my;
     if (tid <= N_XCD) s_cut[tid] = tid == N_XCD ? nb : 0u;
+    __shared__ uint32_t s_own[N_XCD];
+    if (tid < N_XCD) s_own[tid] = 0xFFFFFFFFu;
     __syncthreads();
     if (tid < WAVE) {  // inclusive scan of the 256 segment sums by one wave (4 per lane)
         unsigned long long v[4], tt = 0;
@@ -2805,17 +2849,46 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
         for (int q = 0; q < 4; ++q) s_sum[4 * tid + q] = ex + v[q];
     }
     __syncthreads();
+    BT_OSTAMP(1);
+    // cut q: the first tile whose exclusive prefix reaches q W / 8.  The one segment whose prefixes
+    // cross q W / 8 holds it; then one wave scans that segment's tiles, a lane each (a serial walk
+    // or every thread testing every cut on every tile of its segment cost 4 us of VALU at config 3)
     const unsigned long long W = s_sum[255];
-    unsigned long long e = tid ? s_sum[tid - 1] : 0ull;  // work before this segment
-    for (uint32_t i = s0; i < s1; ++i) {  // cut q: the first tile whose exclusive prefix reaches q W / 8
-        const unsigned long long in = e + tile_work[i];
+    {
+        const unsigned long long e0 = tid ? s_sum[tid - 1] : 0ull, e1 = s_sum[tid];
         for (uint32_t q = 1; q < N_XCD; ++q) {
             const unsigned long long T = (W * q) / N_XCD;
-            if (e < T && in >= T) s_cut[q] = i + 1;
+            if (e0 < T && e1 >= T) s_own[q] = tid;
         }
-        e = in;
     }
     __syncthreads();
+    if (seg <= WAVE) {
+        for (uint32_t q = tid / WAVE + 1; q < N_XCD; q += 256 / WAVE) {
+            const uint32_t sg = s_own[q];
+            if (sg == 0xFFFFFFFFu) continue;
+            const uint32_t a0 = min(nb, sg * seg), a1 = min(nb, a0 + seg), i = a0 + lane();
+            const uint32_t val = i < a1 ? wt(min(i, nb - 1)) : 0u;
+            const uint32_t inc = wave_incl_scan(val);  // (a segment's sum fits: <= 64 x 65535)
+            const unsigned long long base = sg ? s_sum[sg - 1] : 0ull, T = (W * q) / N_XCD;
+            const unsigned long long hits = __ballot(i < a1 && base + (inc - val) < T && base + inc >= T);
+            if (hits && lane() == 0) s_cut[q] = a0 + (uint32_t)__ffsll((long long)hits);
+        }
+    } else {  // (segments wider than a wave: their owners walk them)
+        unsigned long long e = tid ? s_sum[tid - 1] : 0ull;
+        for (uint32_t i = s0; i < s1; ++i) {
+            const unsigned long long in = e + wt(i);
+            for (uint32_t q = 1; q < N_XCD; ++q) {
+                const unsigned long long T = (W * q) / N_XCD;
+                if (e < T && in >= T) s_cut[q] = i + 1;
+            }
+            e = in;
+        }
+    }
+#ifdef GWAOI_EXP_BLOCKTIME
+    if (blockIdx.x == 0 && lane() == 0) gw_blocktime[3 * (BT_FIN + 2006) + tid / WAVE] = wall_clock64();
+#endif
+    __syncthreads();
+    BT_OSTAMP(4);
     if (tid == 0) {  // at most range_max per range (the launch grid's bound), in order
         const uint32_t Lmax = range_max(nb);
         for (uint32_t q = 1; q < N_XCD; ++q) {
@@ -2827,7 +2900,9 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
         }
     }
     __syncthreads();
-    order_range(tile_work, nb, s_cut[x], s_cut[x + 1], tile_order);
+    BT_OSTAMP(2);
+    order_range(wt, wc, s_cut[x], s_cut[x + 1], tile_order);
+    BT_OSTAMP(3);
     if (x == 0 && tid <= N_XCD) tile_order[order_meta(nb) + tid] = s_cut[tid];
     if (x == 0 && tid == 0) tile_order[0] = nb;
 }
@@ -2841,6 +2916,20 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                                                 const BBoxPart *__restrict__ parts, uint32_t np, int4 *bbox,
                                                 uint32_t ns, int4 *hbbox, const uint32_t *__restrict__ tile_work,
                                                 uint32_t n_tiles, uint32_t *tile_order, uint32_t *dcnt) {
+#ifdef GWAOI_EXP_BLOCKTIME  // diagnostics build only: thread 0's start / return per block, from BT_FIN on
+    struct BtFin {
+        unsigned long long t0 = wall_clock64();
+        __device__ ~BtFin() {
+            const uint32_t t = BT_FIN + blockIdx.x;
+            if (threadIdx.x == 0 && t < BT_MAX) {
+                gw_blocktime[3 * t] = t0;
+                gw_blocktime[3 * t + 1] = wall_clock64();
+                gw_blocktime[3 * t + 2] = (unsigned long long)__smid() |
+                                          ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32);
+            }
+        }
+    } bt_fin;
+#endif
     // blocks [0, nx): the next flush's tile order; block nx: the summary; then R copy blocks.  The
     // two serial kinds go first so that they overlap the copies instead of trailing them.
     const uint32_t nx = tile_order ? N_XCD : 0u, R = gridDim.x - 1 - nx;
@@ -2848,8 +2937,70 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         tile_order_block(blockIdx.x, tile_work, n_tiles, tile_order);
         return;
     }
-    const uint32_t b = blockIdx.x - nx - 1;
-    if (blockIdx.x == nx) {  // scalars + bbox fold (level 2 of the per-space bounding box)
+    const uint32_t b = blockIdx.x - nx;
+    if (blockIdx.x == gridDim.x - 1) {  // scalars + bbox fold (level 2 of the per-space bounding box)
+        BT_STAMP(0);
+        // thread t folds parts t, t + 256, ... (coalesced; the parts are in space order, so a
+        // thread's spaces only move forward and it flushes a run when its space changes)
+        uint32_t cur = SP_DEAD;
+        int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+        constexpr uint32_t PF = 8;  // parts in flight per thread (the loads of a group before its fold)
+        for (uint32_t pb = threadIdx.x; pb < np; pb += PF * BB_T) {
+            BBoxPart q[PF];
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {  // (clamped, not branched: every load in flight)
+                q[u] = parts[min(pb + u * BB_T, np - 1)];
+                if (pb + u * BB_T >= np) q[u].sp = SP_DEAD;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+                if (q[u].sp == SP_DEAD) continue;
+                if (q[u].sp != cur) {
+                    if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
+                    cur = q[u].sp;
+                    v[0] = v[1] = INT_MAX;
+                    v[2] = v[3] = INT_MIN;
+                }
+                v[0] = min(v[0], q[u].v[0]);
+                v[1] = min(v[1], q[u].v[1]);
+                v[2] = max(v[2], q[u].v[2]);
+                v[3] = max(v[3], q[u].v[3]);
+            }
+        }
+        BT_STAMP(1);
+#ifdef GWAOI_EXP_BLOCKTIME
+        if (lane() == 0) gw_blocktime[3 * (BT_FIN + 2002) + threadIdx.x / WAVE] = wall_clock64() + (uint32_t)(v[0] == 12345);
+#endif
+        __shared__ BBoxPart s_fold;
+        bbox_block(cur, v, bbox, ns, &s_fold);
+        // The boxes: what the runs of mixed spaces flushed into bbox (the pair passes' and this
+        // block's atomics, complete before the barrier) plus the fold, straight into the host's
+        // summary -- the fold is not added to bbox with atomics first: this block's atomics issued
+        // while the copy blocks stream held it 9-12 us at config 3 (bbox only accumulates a flush)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        BT_STAMP(2);
+        const BBoxPart F = s_fold;
+        if (hbbox) {
+            for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
+                const int *q = reinterpret_cast<const int *>(bbox + i);
+                int4 r = make_int4(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (F.sp == i) {
+                    r.x = min(r.x, F.v[0]);
+                    r.y = min(r.y, F.v[1]);
+                    r.z = max(r.z, F.v[2]);
+                    r.w = max(r.w, F.v[3]);
+                }
+                hbbox[i] = r;
+            }
+        } else if (threadIdx.x == 0 && F.sp != SP_DEAD) {
+            bbox_flush(bbox, ns, F.sp, F.v);
+        }
+        // the scalars last: host writes (uncached, over PCIe) queued ahead of the fold's memory
+        // operations held them (the fold ended 13 us into the launch at config 3)
         if (threadIdx.x == 0) {
             res->err = sc->err;
             // the events (the streams' lengths) and the scratch extent the pair passes needed (each
@@ -2869,39 +3020,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
                 if (dcnt) dcnt[0] = dcnt[1] = 0;
             }
         }
-        const uint32_t per = (np + BB_T - 1) / BB_T;
-        const uint32_t p0 = threadIdx.x * per, p1 = min(p0 + per, np);
-        uint32_t cur = SP_DEAD;
-        int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
-        for (uint32_t p = p0; p < p1; ++p) {
-            const BBoxPart q = parts[p];
-            if (q.sp == SP_DEAD) continue;
-            if (q.sp != cur) {
-                if (cur != SP_DEAD) bbox_flush(bbox, ns, cur, v);
-                cur = q.sp;
-                v[0] = v[1] = INT_MAX;
-                v[2] = v[3] = INT_MIN;
-            }
-            v[0] = min(v[0], q.v[0]);
-            v[1] = min(v[1], q.v[1]);
-            v[2] = max(v[2], q.v[2]);
-            v[3] = max(v[3], q.v[3]);
-        }
-        BBoxPart *fold = const_cast<BBoxPart *>(parts) + np;
-        bbox_block(cur, v, bbox, ns, fold);
-        __syncthreads();
-        if (threadIdx.x == 0 && fold->sp != SP_DEAD) bbox_flush(bbox, ns, fold->sp, fold->v);
-        if (hbbox) {  // the folded boxes straight into the host's summary (read past L1: atomics land in L2)
-            __threadfence();
-            __syncthreads();
-            for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
-                const int *q = reinterpret_cast<const int *>(bbox + i);
-                hbbox[i] = make_int4(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                     __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                     __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                     __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            }
-        }
+        BT_STAMP(4);
         return;
     }
     __shared__ uint32_t s_off[FT + 1];
@@ -2958,24 +3077,30 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     constexpr int FU = 8;
     const uint32_t o0 = s_off[0], o1 = s_off[FT];
     uint32_t t = 0;
-    for (uint32_t p0 = o0 + threadIdx.x; p0 < o1; p0 += FU * blockDim.x) {
-        uint2 v[FU];
+    // (the loads take clamped positions instead of a branch each: a load under a branch is waited
+    // for before the next one issues)
+    for (uint32_t p0 = o0 + threadIdx.x; p0 < o1 && cap_tmp; p0 += FU * blockDim.x) {
+        unsigned long long src[FU];
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const uint32_t p = p0 + (uint32_t)u * blockDim.x;
-            v[u] = make_uint2(0u, 0u);
+            src[u] = cap_tmp;
             if (p < o1) {
                 while (s_off[t + 1] <= p) ++t;  // last tile t with s_off[t] <= p (s_off[FT] = o1 > p)
-                const unsigned long long src = ev_phys(s_src[t] + (p - s_off[t]));
-                if (src < cap_tmp) v[u] = tmp[src];
+                src[u] = ev_phys(s_src[t] + (p - s_off[t]));
             }
         }
+        uint2 v[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) v[u] = tmp[src[u] < cap_tmp ? src[u] : 0ull];
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const uint32_t p = p0 + (uint32_t)u * blockDim.x;
-            if (p < o1 && p < cap_out) out[p] = v[u];
+            if (p < o1 && p < cap_out) out[p] = src[u] < cap_tmp ? v[u] : make_uint2(0u, 0u);
         }
     }
+    for (uint32_t p = o0 + threadIdx.x; p < o1 && !cap_tmp; p += blockDim.x)  // (no scratch: zeros, as ever)
+        if (p < cap_out) out[p] = make_uint2(0u, 0u);
 }
 
 // ------------------------------------------------------------ neighbors ------

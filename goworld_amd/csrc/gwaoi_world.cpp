@@ -184,7 +184,7 @@ struct FlushSet {
     uint64_t ev_cap = 0;         // capacity in directed pairs
     void *bbox_parts = nullptr;  // bbox level-1 partials
     uint32_t n_parts = 0;        // ... written by the flush (k_gather's blocks or k_merge_gather's tiles)
-    char *dev_out = nullptr;     // TickOut + int4 bbox[max_spaces] (device: the bbox fold)
+    char *dev_out = nullptr;     // device counts (2 words) | int4 bbox[max_spaces] from kDevBBox on (the bbox fold)
     char *h_out = nullptr;       // pinned: the flush summary (TickOut + bbox)
     char *d_hout = nullptr;      // h_out as the device sees it: k_finish writes the summary there
     hipEvent_t done_ev = nullptr;  // recorded after the flush's last kernel
@@ -786,7 +786,10 @@ int bitlen(uint32_t v) {
 
 gw::TickOut *tick_out(FlushSet &S) { return reinterpret_cast<gw::TickOut *>(S.h_out); }
 const int4 *tick_bbox(FlushSet &S) { return reinterpret_cast<const int4 *>(S.h_out + sizeof(gw::TickOut)); }
-int4 *dev_bbox(FlushSet &S) { return reinterpret_cast<int4 *>(S.dev_out + sizeof(gw::TickOut)); }
+// The device boxes a line apart from the device counts: k_finish's copy block storing a count while
+// its fold block's atomics land on the boxes shared one line and stalled both (6 us at config 3).
+constexpr size_t kDevBBox = 256;
+int4 *dev_bbox(FlushSet &S) { return reinterpret_cast<int4 *>(S.dev_out + kDevBBox); }
 // the events of the last committed flush
 uint32_t *last_events(gwaoi_world *w) { return w->fs[w->last_set].events; }
 
@@ -1054,8 +1057,12 @@ int tick_launch(gwaoi_world *w) {
     }
     // the gather rides on the incremental sort's merge launch (k_merge_gather, one bbox part per
     // scan tile) unless it is timed or the grid has more scan tiles than the set has parts
+#ifdef GWAOI_EXP_UNFUSED_GATHER  // diagnostics build only: the two launches
+    const bool ga_fused = false;
+#else
     const bool ga_fused = incr && !(w->timing_mask >> ST_GATHER & 1u) &&
                           gw::incr_sort_tiles(total_cells) <= gw::gather_parts(w->max_slots);
+#endif
     S.n_parts = ga_fused ? gw::incr_sort_tiles(total_cells) : gw::gather_parts(n_new);
     gw::GatherJob gj{};
     if (ga_fused) {
@@ -1609,7 +1616,7 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         if ((rc = dalloc(w, &S.srec, N)) || (rc = dalloc(w, &S.sss, N)) || (rc = dalloc(w, &S.orec, N)) ||
             (rc = dalloc(w, &S.cand, N)) || (rc = dalloc(w, &S.sc, 1)) ||
             (rc = dalloc(w, (char **)&S.bbox_parts, gw::bbox_part_bytes((uint32_t)N))) ||
-            (rc = dalloc(w, &S.dev_out, out_bytes)))
+            (rc = dalloc(w, &S.dev_out, kDevBBox + sizeof(int4) * (size_t)w->max_spaces)))
             return fail(rc);
         // S' records seq 0 (virtual S': never "written")
         if (hipMemset(S.srec, 0, N * sizeof(gw::Rec16)) != hipSuccess) return fail(GWAOI_EDEVICE);
