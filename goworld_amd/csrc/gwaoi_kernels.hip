@@ -2771,7 +2771,9 @@ __device__ void order_range(WT wt, WC wc, uint32_t lo, uint32_t hi, uint32_t *ti
     hist[threadIdx.x] = 0;
     __syncthreads();
     auto cls = [&](uint32_t i) {  // band-major, then descending work: bin 0 = heaviest of band 0
-        const uint32_t band = (uint32_t)(((unsigned long long)(i - lo) * TO_BANDS) / max(len, 1u));
+        // (one band: no 64-bit division per tile)
+        const uint32_t band =
+            TO_BANDS == 1 ? 0u : (uint32_t)(((unsigned long long)(i - lo) * TO_BANDS) / max(len, 1u));
         return band * TO_NB + wcls(wt(i), 40);
     };
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&hist[cls(i)], 1u);
@@ -2796,13 +2798,18 @@ constexpr uint32_t TO_LDS = 8192;
 __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_work, uint32_t nb, uint32_t *tile_order) {
     __shared__ uint32_t s_cut[N_XCD + 1];
     __shared__ unsigned long long s_sum[256];
-    __shared__ uint16_t s_t[TO_LDS], s_c[TO_LDS];
+    __shared__ __attribute__((aligned(16))) uint16_t s_t[TO_LDS];
+    __shared__ uint16_t s_c[TO_LDS];
     const uint32_t tid = threadIdx.x;
     // both halves into LDS with coalesced loads (TO_U of each in flight per thread), then every pass
     // reads LDS: a thread's contiguous segment read from global memory touched a line per lane per
     // load, and the range's counts were a round trip of their own (12 us at config 3)
     const bool lds = nb <= TO_LDS;
+    // segments of seg contiguous tiles per thread; in LDS a multiple of 8 (16-B reads), the tail
+    // past nb zero
+    const uint32_t seg = lds ? ((nb + 255) / 256 + 7) & ~7u : (nb + 255) / 256;
     if (lds) {
+        for (uint32_t i = nb + tid; i < 256 * seg; i += 256) s_t[i] = 0;
         constexpr uint32_t TO_U = 8;
         for (uint32_t i0 = tid; i0 < nb; i0 += TO_U * 256) {
             uint32_t t[TO_U], c[TO_U];
@@ -2826,9 +2833,18 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
     auto wt = [&](uint32_t i) -> uint32_t { return lds ? (uint32_t)s_t[i] : min(tile_work[i], 65535u); };
     auto wc = [&](uint32_t i) -> uint32_t { return lds ? (uint32_t)s_c[i] : min(tile_work[nb + i], 65535u); };
     BT_OSTAMP(0);
-    const uint32_t seg = (nb + 255) / 256, s0 = min(nb, tid * seg), s1 = min(nb, s0 + seg);
+    const uint32_t s0 = min(nb, tid * seg), s1 = min(nb, s0 + seg);
     unsigned long long my = 0;
-    for (uint32_t i = s0; i < s1; ++i) my += wt(i);
+    if (lds) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(s_t + tid * seg);
+        for (uint32_t r = 0; r < seg / 8; ++r) {
+            const uint4 q = p[r];
+            my += (q.x & 0xFFFFu) + (q.x >> 16) + (q.y & 0xFFFFu) + (q.y >> 16) + (q.z & 0xFFFFu) + (q.z >> 16) +
+                  (q.w & 0xFFFFu) + (q.w >> 16);
+        }
+    } else {
+        for (uint32_t i = s0; i < s1; ++i) my += wt(i);
+    }
     s_sum[tid] = my;
     if (tid <= N_XCD) s_cut[tid] = tid == N_XCD ? nb : 0u;
     __shared__ uint32_t s_own[N_XCD];
