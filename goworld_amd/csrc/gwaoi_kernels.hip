@@ -2900,11 +2900,7 @@ __device__ void tile_order_block(uint32_t x, const uint32_t *__restrict__ tile_w
             e = in;
         }
     }
-#ifdef GWAOI_EXP_BLOCKTIME
-    if (blockIdx.x == 0 && lane() == 0) gw_blocktime[3 * (BT_FIN + 2006) + tid / WAVE] = wall_clock64();
-#endif
     __syncthreads();
-    BT_OSTAMP(4);
     if (tid == 0) {  // at most range_max per range (the launch grid's bound), in order
         const uint32_t Lmax = range_max(nb);
         for (uint32_t q = 1; q < N_XCD; ++q) {
@@ -2957,7 +2953,9 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
     if (blockIdx.x == gridDim.x - 1) {  // scalars + bbox fold (level 2 of the per-space bounding box)
         BT_STAMP(0);
         // thread t folds parts t, t + 256, ... (coalesced; the parts are in space order, so a
-        // thread's spaces only move forward and it flushes a run when its space changes)
+        // thread's spaces only move forward and it flushes a run when its space changes).  Read
+        // thread-contiguous (t: parts 5t .. 5t + 4), each 20-B load instruction touched 64 lines
+        // and held every block on this block's CU for up to 13 us at config 3.
         uint32_t cur = SP_DEAD;
         int v[4] = {INT_MAX, INT_MAX, INT_MIN, INT_MIN};
         constexpr uint32_t PF = 8;  // parts in flight per thread (the loads of a group before its fold)
@@ -2984,15 +2982,12 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
             }
         }
         BT_STAMP(1);
-#ifdef GWAOI_EXP_BLOCKTIME
-        if (lane() == 0) gw_blocktime[3 * (BT_FIN + 2002) + threadIdx.x / WAVE] = wall_clock64() + (uint32_t)(v[0] == 12345);
-#endif
         __shared__ BBoxPart s_fold;
         bbox_block(cur, v, bbox, ns, &s_fold);
-        // The boxes: what the runs of mixed spaces flushed into bbox (the pair passes' and this
-        // block's atomics, complete before the barrier) plus the fold, straight into the host's
-        // summary -- the fold is not added to bbox with atomics first: this block's atomics issued
-        // while the copy blocks stream held it 9-12 us at config 3 (bbox only accumulates a flush)
+        // The boxes: what the runs of mixed spaces flushed into bbox (the gather's atomics, and this
+        // block's, complete before the barrier: each wave waits for its own) plus the fold, straight
+        // into the host's summary.  bbox only accumulates one flush, so the fold need not be added
+        // to it first (four atomics and a fence less on the launch's serial path).
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         BT_STAMP(2);
@@ -3015,8 +3010,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t *__restrict__ til
         } else if (threadIdx.x == 0 && F.sp != SP_DEAD) {
             bbox_flush(bbox, ns, F.sp, F.v);
         }
-        // the scalars last: host writes (uncached, over PCIe) queued ahead of the fold's memory
-        // operations held them (the fold ended 13 us into the launch at config 3)
+        // the scalars
         if (threadIdx.x == 0) {
             res->err = sc->err;
             // the events (the streams' lengths) and the scratch extent the pair passes needed (each

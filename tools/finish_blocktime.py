@@ -50,13 +50,9 @@ def main():
     st = [int(r[BT_FIN + 2000][0]), int(r[BT_FIN + 2000][1]), int(r[BT_FIN + 2000][2]), int(r[BT_FIN + 2001][1])]
     print("  fold block stamps (us from its start): summary %.1f, fold loop %.1f, bbox_block + barrier %.1f, end %.1f" %
           tuple((x - int(t0[nb - 1])) * 0.01 for x in st))
-    print("  fold loop done per wave (us from its start):", [round((int(x) - int(t0[nb - 1])) * 0.01, 1)
-                                                          for x in r[BT_FIN + 2002:BT_FIN + 2004].reshape(-1)[:4]])
     o = [int(x) for x in r[BT_FIN + 2004:BT_FIN + 2006].reshape(-1)[:4]]
     print("  tile order block 0 stamps (us from its start): LDS staged %.1f, segment scan %.1f, cuts %.1f, order_range %.1f"
           % tuple((x - int(t0[0])) * 0.01 for x in o))
-    print("  tile order block 0: cut loop done per wave", [round((int(x) - int(t0[0])) * 0.01, 1) for x in r[BT_FIN + 2006:BT_FIN + 2008].reshape(-1)[:4]],
-          "after its barrier %.1f" % ((int(r[BT_FIN + 2005][1]) - int(t0[0])) * 0.01))
     order = np.argsort(e)[-5:]
     print("  last 5 to end (block, start, end):", [(int(i), round(float(s[i]), 1), round(float(e[i]), 1)) for i in order])
 
