@@ -586,7 +586,7 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
 // order is Go map order, EntityManager.go's entity loop: the order of
 // records inside a gate is not part of the contract.)
 #ifndef GWAOI_FW_G
-#define GWAOI_FW_G 4
+#define GWAOI_FW_G 12  // A/B (profiles/r06_ab_fan_write.txt): collect 1.355 (4), 1.285 (6), 1.242 (8), 1.203 (12), 1.210 (16) ms once the hit loads stopped serialising
 #endif
 constexpr int FW_G = GWAOI_FW_G;  // record groups of 64 per wave with their loads in flight together
 
@@ -680,8 +680,8 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
                 q[k] = qc;
                 place(r, qc, sidx, pos[k]);
             }
-            h[k] = ok[k] ? A.scr[sidx] : 0u;
-        }
+            h[k] = A.scr[sidx];  // (sidx 0 when !ok: a load under a per-lane branch is waited for
+        }                        // before the next one issues, which serialised the groups)
         uint4 id[FW_G], pv[FW_G];
 #pragma unroll
         for (int k = 0; k < FW_G; ++k) {
