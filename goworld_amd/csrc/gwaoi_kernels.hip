@@ -2374,13 +2374,16 @@ __device__ __forceinline__ void sweep_rows_merged(CombinedLds &L, int w, WaveQue
     const uint32_t gx = C.g.gx;
     const uint32_t xb = C.g.base + (uint32_t)xr0 * gx + (uint32_t)xc0, xs = (uint32_t)(xc1 - xc0) + 1u;
     const uint32_t zb = C.g.base + (uint32_t)zr0 * gx + (uint32_t)zc0, zs = (uint32_t)(zc1 - zc0) + 1u;
+    // (both bounds loaded whatever q, cell 0 past the lane's rows: under a per-lane branch each
+    // load was waited for on its own, and the next group's ranges were not in flight during the
+    // current group's sweep)
     auto range = [&](uint32_t q, uint32_t &b, uint32_t &l) {
-        b = l = 0;
-        if (q < nr) {
-            const uint32_t rb = q < nx ? xb + q * gx : zb + (q - nx) * gx;
-            b = cs[rb];
-            l = cs[rb + (q < nx ? xs : zs)] - b;
-        }
+        const bool v = q < nr;
+        const uint32_t rb = !v ? 0u : q < nx ? xb + q * gx : zb + (q - nx) * gx;
+        const uint32_t re = !v ? 0u : rb + (q < nx ? xs : zs);
+        const uint32_t b0 = cs[rb], e0 = cs[re];
+        b = v ? b0 : 0u;
+        l = v ? e0 - b0 : 0u;
     };
     uint32_t jb[P], ln[P];
 #pragma unroll
