@@ -122,7 +122,7 @@ class Debug(C.Structure):
                 ("cell_size_switches", C.c_uint64), ("cells_per_dist", C.c_uint32), ("pad", C.c_uint32),
                 ("incremental_sorts", C.c_uint64), ("sparse_flushes", C.c_uint64), ("sparse_declined", C.c_uint64),
                 ("premarked_runs", C.c_uint64), ("sparse_unfused", C.c_uint64),
-                ("unique_flushes", C.c_uint64)]
+                ("unique_flushes", C.c_uint64), ("overlapped_flushes", C.c_uint64)]
 
 
 class StageTime(C.Structure):

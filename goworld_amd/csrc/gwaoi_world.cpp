@@ -182,6 +182,16 @@ struct FlushSet {
     gw::TickScalars *sc = nullptr;
     uint32_t *events = nullptr;  // ev_cap (a,b) pairs: [enters | leaves] in tile order
     uint64_t ev_cap = 0;         // capacity in directed pairs
+    // the pair passes' scratch (evtmp_cap pairs: per-tile chunks of the eight event streams) and the
+    // per-tile event totals / stream positions: per set, so that a flush's pair passes and finish
+    // can run while the next flush's first kernels (which zero the totals and write the special
+    // pass's events) already run on the early stream
+    uint32_t *evtmp = nullptr;
+    uint64_t evtmp_cap = 0;
+    uint32_t *tile_total = nullptr;
+    unsigned long long *tile_base = nullptr;
+    size_t tile_entries_cap = 0;
+    hipEvent_t mid_ev = nullptr;  // recorded after the flush's early kernels (the next flush's early stream waits)
     void *bbox_parts = nullptr;  // bbox level-1 partials
     uint32_t n_parts = 0;        // ... written by the flush (k_gather's blocks or k_merge_gather's tiles)
     char *dev_out = nullptr;     // device counts (2 words) | int4 bbox[max_spaces] from kDevBBox on (the bbox fold)
@@ -241,6 +251,14 @@ struct gwaoi_world {
     bool inject_regrow_fail = false;  // the event regrow fails (the poison path)
     hipEvent_t done_ev = nullptr;  // wait_stream's marker (polled)
     hipEvent_t order_ev = nullptr;  // gwaoi_stream_after / _before
+    // Overlapped flushes (speculative launches only): flush t+1's early kernels (apply .. gather)
+    // run on early_st while flush t's pair passes and finish still run on the stream.  gen counts
+    // the enqueues on the stream from anything but a flush; an early stream may skip only work
+    // the previous flush queued (gen unchanged since its launch: gen_launch).
+    hipStream_t early_st = nullptr;
+    uint64_t gen = 0, gen_launch = ~0ull;
+    bool ovl_ok = false;   // set around a speculative launch (end_begin)
+    bool mid_last = false;  // the last flush recorded its set's mid_ev
     bool check_stages = false;   // wait after every flush stage (fault diagnosis)
     const char *fault_stage = nullptr;  // stage at the first failed wait
     bool fault_before = false;          // ... the wait before it (else after it)
@@ -249,11 +267,6 @@ struct gwaoi_world {
     float *op_x = nullptr, *op_z = nullptr;
     unsigned long long *op_seq = nullptr;
     size_t op_cap = 0;
-    uint32_t *events_tmp = nullptr;  // evtmp_cap pairs: per-tile chunks at reserved offsets (shared by the sets)
-    uint64_t evtmp_cap = 0;
-    uint32_t *tile_total = nullptr;
-    unsigned long long *tile_base = nullptr;
-    size_t tile_entries_cap = 0;
     float *blk = nullptr;        // keygen per-block partials
     uint32_t *nb_out = nullptr, *nb_count = nullptr;
     size_t nb_cap = 0;
@@ -454,6 +467,7 @@ int wait_stream(gwaoi_world *w) {
 int ensure_scan_tmp(gwaoi_world *w, size_t n) {
     size_t need = gw::scan_tmp_elems(n) + 16;
     if (need <= w->scan_tmp_cap) return GWAOI_OK;
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->scan_tmp);
     int rc = dalloc(w, &w->scan_tmp, need);
@@ -469,7 +483,8 @@ int ensure_scan_tmp(gwaoi_world *w, size_t n) {
 // (matching the twin set's capacity: with slack, the two sets would outgrow each other on every
 // flush).
 int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs, uint64_t extent, bool exact = false) {
-    if (pairs <= S.ev_cap && extent <= w->evtmp_cap) return GWAOI_OK;
+    if (pairs <= S.ev_cap && extent <= S.evtmp_cap) return GWAOI_OK;
+    w->gen++;
     HIP_TRY(hipStreamSynchronize(w->stream));
     int rc;
     if (pairs > S.ev_cap) {
@@ -479,30 +494,31 @@ int ensure_events(gwaoi_world *w, FlushSet &S, uint64_t pairs, uint64_t extent, 
         if ((rc = dalloc(w, &S.events, 2 * cap))) return rc;
         S.ev_cap = cap;
     }
-    if (extent > w->evtmp_cap) {
-        const uint64_t cap = std::max<uint64_t>(extent + extent / 4, w->evtmp_cap * 2);
-        dfree(w->events_tmp);
-        w->evtmp_cap = 0;
-        if ((rc = dalloc(w, &w->events_tmp, 2 * cap))) return rc;
-        w->evtmp_cap = cap;
+    if (extent > S.evtmp_cap) {
+        const uint64_t cap = std::max<uint64_t>(extent + extent / 4, S.evtmp_cap * 2);
+        dfree(S.evtmp);
+        S.evtmp_cap = 0;
+        if ((rc = dalloc(w, &S.evtmp, 2 * cap))) return rc;
+        S.evtmp_cap = cap;
     }
     return GWAOI_OK;
 }
 
 
-int ensure_tile_entries(gwaoi_world *w, size_t entries) {
-    if (entries + 1 <= w->tile_entries_cap) return GWAOI_OK;
+int ensure_tile_entries(gwaoi_world *w, FlushSet &S, size_t entries) {
+    if (entries + 1 <= S.tile_entries_cap) return GWAOI_OK;
+    w->gen++;
     size_t cap = std::max<size_t>(entries + 1 + entries / 4, 1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
-    dfree(w->tile_total);
-    dfree(w->tile_base);
+    dfree(S.tile_total);
+    dfree(S.tile_base);
     int rc;
-    if ((rc = dalloc(w, &w->tile_total, gw::tile_total_elems(cap))) ||
-        (rc = dalloc(w, &w->tile_base, cap))) {
-        w->tile_entries_cap = 0;
+    if ((rc = dalloc(w, &S.tile_total, gw::tile_total_elems(cap))) ||
+        (rc = dalloc(w, &S.tile_base, cap))) {
+        S.tile_entries_cap = 0;
         return rc;
     }
-    w->tile_entries_cap = cap;
+    S.tile_entries_cap = cap;
     return GWAOI_OK;
 }
 
@@ -530,6 +546,7 @@ int ensure_host_events(gwaoi_world *w, uint64_t pairs) {
 
 int ensure_ops(gwaoi_world *w, size_t n) {
     if (n <= w->op_cap) return GWAOI_OK;
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     size_t cap = std::max<size_t>(n, w->op_cap * 2);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->op_slot);
@@ -550,6 +567,7 @@ int ensure_ops(gwaoi_world *w, size_t n) {
 int ensure_incr(gwaoi_world *w, size_t cells) {
     const size_t need = cells + 1;
     if (need <= w->cnt64_cap) return GWAOI_OK;
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     const size_t cap = std::max(need + need / 4, (size_t)1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(w->cnt64);
@@ -570,6 +588,7 @@ int ensure_incr(gwaoi_world *w, size_t cells) {
 int ensure_cells(gwaoi_world *w, DevFrame &f, size_t cells) {
     size_t need = cells + 1;
     if (need <= f.cell_cap) return GWAOI_OK;
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     size_t cap = std::max(need + need / 4, (size_t)1024);
     HIP_TRY(hipStreamSynchronize(w->stream));
     dfree(f.cell_start);
@@ -812,25 +831,25 @@ EvCaps launch_pair_passes(gwaoi_world *w, FlushSet &S, DevFrame &Fn, DevFrame &P
     gw::FrameView Vn = view_of(Fn), Vp = view_of(P);
     // the pair passes write their streams into the scratch (capacity evtmp_cap), and k_finish copies
     // them into the set's buffer (ev_cap); a larger extent or count is an overflow (re-run)
-    const EvCaps caps{w->evtmp_cap, S.ev_cap};
+    const EvCaps caps{S.evtmp_cap, S.ev_cap};
     const uint64_t cap = caps.tmp;
     // timed with the launch's own start/end events (no marker packets)
     const bool tc = w->timing_mask >> ST_COMBINED & 1u;
     if (tc) S.ev_used[ST_COMBINED] = true;
     const bool order = !rerun;
-    gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, half,
+    gw::launch_combined(Vn, S.cand, S.orec, seq_base, S.sc, S.evtmp, cap, S.tile_total, S.tile_base, half,
                         order ? w->tile_order : nullptr, order ? w->tile_work : nullptr, rerun ? nullptr : w->ework,
                         st,
                         tc ? S.ev[ST_COMBINED][0] : nullptr, tc ? S.ev[ST_COMBINED][1] : nullptr);
     if (!special_done) {  // (special_done: it ran in the sort's arrival launch)
         stage_begin(w, S, ST_SPECIAL);
-        gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, w->events_tmp, cap, w->tile_total, w->tile_base, TBn,
+        gw::launch_pairs(Vp, S.srec, s_ss_view, seq_base, S.sc, S.evtmp, cap, S.tile_total, S.tile_base, TBn,
                          half, rerun ? nullptr : w->special, st);
         stage_end(w, S, ST_SPECIAL);
     }
     // tile order + TickOut + the per-space bboxes for the next flush's grid (one launch)
     stage_begin(w, S, ST_FINISH);
-    gw::launch_finish(w->tile_total, w->tile_base, entries, half, w->events_tmp, S.events,
+    gw::launch_finish(S.tile_total, S.tile_base, entries, half, S.evtmp, S.events,
                       caps.tmp, caps.out, S.sc, reinterpret_cast<gw::TickOut *>(S.d_hout), Fn.n,
                       dev_bbox(S), w->n_space_ids, S.bbox_parts, S.n_parts,
                       reinterpret_cast<int4 *>(S.d_hout + sizeof(gw::TickOut)),
@@ -883,7 +902,7 @@ int tick_launch(gwaoi_world *w) {
     for (uint32_t s = 0; s < w->n_space_ids; ++s) w->spaces[s].pend = false;  // consumed by this grid
     const size_t entries = 2 * ((size_t)gw::combined_tiles(n_new) + gw::combined_blocks(n_prev));
     if ((rc = ensure_cells(w, Fn, total_cells))) return rc;
-    if ((rc = ensure_tile_entries(w, entries))) return rc;
+    if ((rc = ensure_tile_entries(w, S, entries))) return rc;
     // a set whose twin grew on an overflow grows alike before its next flush (one re-run, not two)
     if (S.ev_cap < w->fs[set ^ 1].ev_cap && (rc = ensure_events(w, S, w->fs[set ^ 1].ev_cap, 0, true))) return rc;
     size_t host_ops = 0;
@@ -902,6 +921,21 @@ int tick_launch(gwaoi_world *w) {
     const bool incr = !w->force_radix && n_prev > 0 && P.total_cells == total_cells && P.hgrid.size() == ns &&
                       !std::memcmp(P.hgrid.data(), w->h_grid, ns * sizeof(SpaceGrid));
     if (incr && (rc = ensure_incr(w, total_cells))) return rc;
+    // Overlap (speculative launches): this flush's early kernels (apply .. gather) go on the early
+    // stream behind the previous flush's early kernels (its set's mid_ev), while that flush's pair
+    // passes and finish still run on the stream; this flush's pair passes wait for its own early
+    // kernels.  Nothing the early kernels touch is read or written by the previous flush's pair
+    // passes or finish: the scratch, tile totals and boxes are per set, the frames rotate over three,
+    // and the special pass rides on the arrival launch (it reads the previous frame early).  Only when
+    // nothing else was queued on the stream since the previous flush's launch (gen), and with no
+    // stage timing but the combined pass's.
+    const bool ovl = w->ovl_ok && w->mid_last && w->gen == w->gen_launch && incr && n_prev > 0 &&
+                     (w->timing_mask & ~(1u << ST_COMBINED)) == 0 && !w->check_stages;
+    if (ovl) {
+        st = w->early_st;
+        HIP_TRY(hipStreamWaitEvent(st, w->fs[set ^ 1].mid_ev, 0));
+        w->dbg.overlapped_flushes++;
+    }
     if (!grid_same) {
         HIP_TRY(hipMemcpyAsync(Fn.grid, w->h_grid, sizeof(SpaceGrid) * ns, hipMemcpyHostToDevice, st));
         Fn.hgrid.assign(w->h_grid, w->h_grid + ns);
@@ -947,18 +981,18 @@ int tick_launch(gwaoi_world *w) {
     gw::TickZero tz{};
     if (uniq && incr) {
         tz.sc = S.sc;
-        tz.z1 = w->tile_total;
+        tz.z1 = S.tile_total;
         tz.n1 = (uint32_t)gw::tile_total_elems(entries);
         tz.bbox = dev_bbox(S);
         tz.n_spaces = w->n_space_ids;
         tz.n_unique = n_unique;
     } else if (incr)
         gw::launch_prologue(S.sc, reinterpret_cast<uint32_t *>(w->cnt64),
-                            gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), w->tile_total,
+                            gw::scan_rezeroes_counts() ? 0 : 2 * ((size_t)total_cells + 1), S.tile_total,
                             gw::tile_total_elems(entries), dev_bbox(S), w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark,
                             w->max_slots, w->sinfo, tick_id, n_unique, st);
     else
-        gw::launch_prologue(S.sc, Fn.cell_start, (size_t)total_cells + 1, w->tile_total, gw::tile_total_elems(entries), dev_bbox(S),
+        gw::launch_prologue(S.sc, Fn.cell_start, (size_t)total_cells + 1, S.tile_total, gw::tile_total_elems(entries), dev_bbox(S),
                             w->n_space_ids, n_copy, P.rec, P.ss, S.srec, S.sss, mark, w->max_slots, w->sinfo,
                             tick_id, n_unique, st);
 
@@ -1046,10 +1080,10 @@ int tick_launch(gwaoi_world *w) {
         spj.O_ss = s_ss_view;
         spj.seq_base = seq_base;
         spj.sc = S.sc;
-        spj.tmp = reinterpret_cast<uint2 *>(w->events_tmp);
-        spj.cap = w->evtmp_cap;
-        spj.tile_total = w->tile_total;
-        spj.tile_base = w->tile_base;
+        spj.tmp = reinterpret_cast<uint2 *>(S.evtmp);
+        spj.cap = S.evtmp_cap;
+        spj.tile_total = S.tile_total;
+        spj.tile_base = S.tile_base;
         spj.tile_off = TBn;
         spj.leave_off = TBn + TBp;
         spj.special = w->special;
@@ -1121,6 +1155,19 @@ int tick_launch(gwaoi_world *w) {
         stage_end(w, S, ST_CELLS);
     }
 
+    // the early kernels' end: the next (speculative) flush's early stream starts behind it, and an
+    // overlapped flush's pair passes wait for it on the stream
+    w->mid_last = false;
+    if (w->ovl_ok || ovl) {
+        if (hipEventRecord(S.mid_ev, st) != hipSuccess ||
+            (ovl && hipStreamWaitEvent(w->stream, S.mid_ev, 0) != hipSuccess)) {
+            w->last_error = "flush mid event failed";
+            return poison(w, GWAOI_EDEVICE);
+        }
+        w->mid_last = true;
+    }
+    st = w->stream;
+
     // ---- pair passes: combined over the new grid, special entities over the previous one
     const EvCaps ev_cap = launch_pair_passes(w, S, Fn, P, seq_base, s_ss_view, false, sp_fused);
 
@@ -1153,6 +1200,7 @@ int tick_launch(gwaoi_world *w) {
     w->stage_cur ^= 1;  // calls made in flight stage into the other half (free: its flush has ended)
     w->stage_used[w->stage_cur] = 0;
     w->space_ops_queued = false;
+    w->gen_launch = w->gen;
     return GWAOI_OK;
 }
 
@@ -1243,7 +1291,8 @@ int finish_flight(gwaoi_world *w, const Flight &f, bool host_done, bool *committ
         const uint64_t need = attempt == 0 ? r.ext64 : std::max<uint64_t>(r.ext64, gw::ev_worst_extent(r.total64));
         if ((rc = ensure_events(w, S, r.total64, need))) return poison(w, rc);
         (void)hipGetLastError();  // a failure of an unrelated earlier call is not this re-run's
-        gw::launch_zero(w->tile_total, gw::tile_total_elems(f.entries), st);
+        w->gen++;
+        gw::launch_zero(S.tile_total, gw::tile_total_elems(f.entries), st);
         gw::launch_zero(&S.sc->shard[0][0], gw::EV_SHARDS * 32, st);  // event streams
         gw::launch_zero(S.sc->dbg, gw::DBG_N, st);
         cap_used = launch_pair_passes(w, S, Fn, P, f.seq_base, f.s_ss_view, true);
@@ -1351,6 +1400,7 @@ int sparse_try(gwaoi_world *w) {
         if (sp == gw::SP_DEAD) return 1;
     const uint32_t k = (uint32_t)w->n_ops;
     hipStream_t st = w->stream;
+    w->gen++;  // (the sparse flush's kernels: the next flush's early kernels wait for them)
     const int set = w->launch_set;
     FlushSet &S = w->fs[set];
     int rc;
@@ -1497,6 +1547,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     if (w->stream) (void)hipStreamSynchronize(w->stream);
+    if (w->early_st) (void)hipStreamSynchronize(w->early_st);
     if (w->copy_st) (void)hipStreamSynchronize(w->copy_st);
     if (w->out_st) (void)hipStreamSynchronize(w->out_st);
     if (w->sync) gw::sync_destroy(w->sync);
@@ -1506,7 +1557,8 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     }
     for (FlushSet &S : w->fs) {
         dfree(S.srec); dfree(S.sss); dfree(S.orec); dfree(S.cand); dfree(S.sc); dfree(S.events);
-        dfree(S.bbox_parts); dfree(S.dev_out);
+        dfree(S.bbox_parts); dfree(S.dev_out); dfree(S.evtmp); dfree(S.tile_total); dfree(S.tile_base);
+        if (S.mid_ev) (void)hipEventDestroy(S.mid_ev);
         if (S.h_out) (void)hipHostFree(S.h_out);
         S.h_out = nullptr;
         for (int st = 0; st < ST_N; ++st)
@@ -1520,7 +1572,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     dfree(w->tile_work); dfree(w->tile_order); dfree(w->ework);
     dfree(w->mv_hist); dfree(w->mv_binned);
     dfree(w->op_slot); dfree(w->op_sp); dfree(w->op_x); dfree(w->op_z); dfree(w->op_seq);
-    dfree(w->events_tmp); dfree(w->tile_total); dfree(w->tile_base); dfree(w->sp_cnt); dfree(w->d_sp_ops); dfree(w->sp_scr); dfree(w->sp_done);
+    dfree(w->sp_cnt); dfree(w->d_sp_ops); dfree(w->sp_scr); dfree(w->sp_done);
     if (w->h_sp_ops) (void)hipHostFree(w->h_sp_ops);
     dfree(w->blk);
     dfree(w->nb_out); dfree(w->nb_count);
@@ -1541,6 +1593,7 @@ int gwaoi_world_destroy(gwaoi_world *w) {
     if (w->done_ev) (void)hipEventDestroy(w->done_ev);
     if (w->order_ev) (void)hipEventDestroy(w->order_ev);
     if (w->stream) (void)hipStreamDestroy(w->stream);
+    if (w->early_st) (void)hipStreamDestroy(w->early_st);
     delete w;
     return GWAOI_OK;
     });
@@ -1583,6 +1636,10 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
     if (hipGetDevice(&w->device) != hipSuccess) {
         delete w;
         return GWAOI_EDEVICE;
+    }
+    if (hipStreamCreateWithFlags(&w->early_st, hipStreamNonBlocking) != hipSuccess) {
+        w->early_st = nullptr;
+        return fail(GWAOI_EDEVICE);
     }
     if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
         w->stream = nullptr;
@@ -1632,7 +1689,9 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         for (int st = 0; st < ST_N; ++st)
             for (int q = 0; q < 2; ++q)
                 if (hipEventCreate(&S.ev[st][q]) != hipSuccess) return fail(GWAOI_EDEVICE);
-        if (hipEventCreateWithFlags(&S.done_ev, hipEventDisableTiming) != hipSuccess) return fail(GWAOI_EDEVICE);
+        if (hipEventCreateWithFlags(&S.done_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&S.mid_ev, hipEventDisableTiming) != hipSuccess)
+            return fail(GWAOI_EDEVICE);
     }
     if ((rc = dalloc(w, &w->keys[0], N)) || (rc = dalloc(w, &w->keys[1], N)) || (rc = dalloc(w, &w->vals[0], N)) ||
         (rc = dalloc(w, &w->vals[1], N)) || (rc = dalloc(w, &w->hist, gw::radix_hist_elems((uint32_t)N))) ||
@@ -1660,8 +1719,9 @@ int gwaoi_world_create(const gwaoi_config *cfg, gwaoi_world **out) {
         if ((rc = dalloc(w, &w->mv_hist, mv_hist_n)) || (rc = dalloc(w, &w->mv_binned, N))) return fail(rc);
     }
     if ((rc = ensure_scan_tmp(w, std::max(gw::radix_hist_elems((uint32_t)N), mv_hist_n)))) return fail(rc);
-    if ((rc = ensure_tile_entries(w, 2 * ((size_t)gw::combined_tiles((uint32_t)N) + gw::combined_blocks((uint32_t)N)))))
-        return fail(rc);
+    for (FlushSet &S : w->fs)
+        if ((rc = ensure_tile_entries(w, S, 2 * ((size_t)gw::combined_tiles((uint32_t)N) + gw::combined_blocks((uint32_t)N)))))
+            return fail(rc);
     if ((rc = ensure_ops(w, 1024))) return fail(rc);
     for (FlushSet &S : w->fs)
         if ((rc = ensure_events(w, S, cfg->event_capacity ? cfg->event_capacity : std::max<uint64_t>(4 * N, 1 << 16),
@@ -1720,6 +1780,7 @@ namespace {
 // after device Enter/Leave batches (the frame holds exactly the live slots); GWAOI_ESTATE while
 // such a batch is queued or in flight (its slots are not known on the host yet).
 int host_slots(gwaoi_world *w) {
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     if (w->dev_struct || (w->in_flight && w->slots_stale)) {
         w->last_error = "a device Enter/Leave batch is queued or in flight: flush before host per-slot calls";
         return GWAOI_ESTATE;
@@ -2337,6 +2398,7 @@ int gwaoi_pinned_free(gwaoi_world *w, void *p) {
 namespace gw {
 
 WorldView world_view(gwaoi_world *w) {
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     WorldView v{};
     v.F = view_of(w->fr[w->cur]);
     v.info = w->sinfo;
@@ -2414,7 +2476,9 @@ int end_begin(gwaoi_world *w, bool *committed_out) {
         // no idle gap on the GPU between the two
         const Flight f = w->fl;
         commit_host(w, nullptr);
+        w->ovl_ok = true;
         lrc = tick_launch(w);
+        w->ovl_ok = false;
         if (lrc == GWAOI_OK) w->dbg.speculative_launches++;
         rc = finish_flight(w, f, true, &committed);
     } else {
@@ -2456,6 +2520,7 @@ int copy_out(gwaoi_world *w, bool pairs, uint64_t regrows) {
 // The flush's end with its events copied to host memory on its own stream, no next flush
 // (gwaoi_tick, gwaoi_tick_finish(GWAOI_END_HOST)): the copy is the D2H stage of the stage timing.
 int end_host(gwaoi_world *w, bool *committed) {
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     int rc = tick_finish(w, committed);
     if (!*committed) return rc;
     // committed: deliver the events whatever the status (InterestedIn/By must follow the frame)
@@ -2626,6 +2691,7 @@ namespace {
 
 // Build the last flush's event rows on the device (once per flush).
 int build_csr(gwaoi_world *w) {
+    w->gen++;  // (an enqueue on the stream that no flush made: the next flush's early kernels wait for it)
     const uint64_t tot = w->last_n_enter + w->last_n_leave;
     if (w->csr_tick == w->ticks) return GWAOI_OK;
     const size_t rows = w->max_slots;
@@ -2682,6 +2748,7 @@ int gwaoi_events_csr(gwaoi_world *w, const uint32_t **offsets, const uint32_t **
         HIP_TRY(hipHostMalloc((void **)&w->h_csr_items, cap * 4, hipHostMallocDefault));
         w->h_csr_items_cap = cap;
     }
+    w->gen++;
     HIP_TRY(hipMemcpyAsync(w->h_csr_off, w->csr_off, ((size_t)w->max_slots + 1) * 4, hipMemcpyDeviceToHost, w->stream));
     if (tot) HIP_TRY(hipMemcpyAsync(w->h_csr_items, w->csr_items, tot * 4, hipMemcpyDeviceToHost, w->stream));
     if (int rc = wait_stream(w)) return rc;
@@ -2709,6 +2776,7 @@ int gwaoi_neighbors(gwaoi_world *w, uint32_t slot, uint32_t *out, size_t cap, si
         w->nb_cap = need;
     }
     const DevFrame &F = w->fr[w->cur];
+    w->gen++;
     HIP_TRY(hipMemsetAsync(w->nb_count, 0, sizeof(uint32_t), w->stream));
     gw::launch_neighbors(view_of(F), w->sinfo, slot, w->nb_out, (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFu),
                          w->nb_count, w->stream);
@@ -2738,6 +2806,7 @@ int gwaoi_snapshot(gwaoi_world *w, uint32_t *slots, uint32_t *spaces, float *x, 
     if (!slots || !spaces || !x || !z || !seq) return GWAOI_EINVAL;
     std::vector<gw::Rec16> rec(F.n);
     std::vector<gw::SlotSp> ss(F.n);
+    w->gen++;
     HIP_TRY(hipMemcpyAsync(rec.data(), F.rec, F.n * sizeof(gw::Rec16), hipMemcpyDeviceToHost, w->stream));
     HIP_TRY(hipMemcpyAsync(ss.data(), F.ss, F.n * sizeof(gw::SlotSp), hipMemcpyDeviceToHost, w->stream));
     HIP_TRY(hipStreamSynchronize(w->stream));
@@ -2797,7 +2866,7 @@ int gwaoi_world_info(gwaoi_world *w, gwaoi_info *info) {
     info->spaces = w->n_spaces_live;
     info->total_cells = w->fr[w->cur].total_cells;
     info->pending_ops = (uint32_t)w->n_ops;
-    info->event_capacity = std::min(w->fs[w->launch_set].ev_cap, w->evtmp_cap);
+    info->event_capacity = std::min(w->fs[w->launch_set].ev_cap, w->fs[w->launch_set].evtmp_cap);
     info->max_slots = w->max_slots;
     info->max_spaces = w->max_spaces;
     return GWAOI_OK;
@@ -2854,13 +2923,18 @@ int gwaoi_sync(gwaoi_world *w) {
     });
 }
 
-void *gwaoi_stream(gwaoi_world *w) { return w ? (void *)w->stream : nullptr; }
+void *gwaoi_stream(gwaoi_world *w) {
+    if (!w) return nullptr;
+    w->gen++;  // the caller may queue work the next flush depends on
+    return (void *)w->stream;
+}
 
 int gwaoi_stream_after(gwaoi_world *w, void *other) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
     HIP_TRY(hipEventRecord(w->order_ev, (hipStream_t)other));
     HIP_TRY(hipStreamWaitEvent(w->stream, w->order_ev, 0));
+    w->gen++;  // the next flush's early kernels wait for the other stream too
     return GWAOI_OK;
     });
 }

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GWAOI_ABI_VERSION 5  /* 5: GWAOI_F_TEST_* flags replace environment switches; GWAOI_F_BATCH_READY ignored */
+#define GWAOI_ABI_VERSION 6  /* 6: gwaoi_debug.overlapped_flushes; 5: GWAOI_F_TEST_* flags replace environment switches, GWAOI_F_BATCH_READY ignored */
 
 typedef struct gwaoi_world gwaoi_world;
 
@@ -141,6 +141,8 @@ typedef struct {
     uint64_t premarked_runs;        /* always 0 since ABI 5 (GWAOI_F_BATCH_READY is ignored)                 */
     uint64_t sparse_unfused;        /* sparse flushes that ran the kernel sequence (an op outgrew its row)    */
     uint64_t unique_flushes;        /* flushes applied without last-op claims (GWAOI_F_UNIQUE_MOVES)          */
+    uint64_t overlapped_flushes;    /* speculative flushes whose first kernels ran beside the pair passes and */
+                                    /* finish of the flush before them (two streams)                        */
 } gwaoi_debug;
 
 typedef struct {

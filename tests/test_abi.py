@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_pure_host_entry_points(lib):
-    assert lib.gwaoi_abi_version() == 5
+    assert lib.gwaoi_abi_version() == 6
     assert lib.gwaoi_strerror(0) == b"ok"
     assert b"state" in lib.gwaoi_strerror(-3)
     # null-argument handling never touches the device

@@ -69,6 +69,10 @@ def test_cfg3_unique_moves_chained_ticks_vs_closed_form_gpu(oracle_mod):
         d1 = w.debug_counters()
         assert d1["unique_flushes"] - d0["unique_flushes"] == ticks, (d0, d1)
         assert d1["speculative_launches"] - d0["speculative_launches"] == ticks - 1, (d0, d1)
+        # the speculative launches after the first ran their first kernels on the early stream, beside the
+        # pair passes and finish of the flush before it (the first has no predecessor's mid event; a
+        # flush on a new grid has no incremental sort and runs alone)
+        assert d1["overlapped_flushes"] - d0["overlapped_flushes"] >= ticks - 3, (d0, d1)
         assert d1["incremental_sorts"] - d0["incremental_sorts"] >= ticks - 1, (d0, d1)
         rng = np.random.default_rng(0xC3C3)
         q = rng.choice(n, 500, replace=False)
