@@ -929,8 +929,12 @@ int tick_launch(gwaoi_world *w) {
     // and the special pass rides on the arrival launch (it reads the previous frame early).  Only when
     // nothing else was queued on the stream since the previous flush's launch (gen), and with no
     // stage timing but the combined pass's.
+#ifdef GWAOI_EXP_NO_OVERLAP  // diagnostics build only: one flush at a time (the A/B of the overlap)
+    const bool ovl = false;
+#else
     const bool ovl = w->ovl_ok && w->mid_last && w->gen == w->gen_launch && incr && n_prev > 0 &&
                      (w->timing_mask & ~(1u << ST_COMBINED)) == 0 && !w->check_stages;
+#endif
     if (ovl) {
         st = w->early_st;
         HIP_TRY(hipStreamWaitEvent(st, w->fs[set ^ 1].mid_ev, 0));
