@@ -20,6 +20,9 @@
 #include <functional>
 #include <mutex>
 #include <cstdio>
+#ifdef GWAOI_EXP_HOSTTIME
+#include <chrono>
+#endif
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -258,6 +261,10 @@ struct gwaoi_world {
     hipStream_t early_st = nullptr;
     uint64_t gen = 0, gen_launch = ~0ull;
     bool ovl_ok = false;   // set around a speculative launch (end_begin)
+#ifdef GWAOI_EXP_HOSTTIME  // diagnostics build only: host time per phase of gwaoi_tick_finish(NEXT), printed at destroy
+    double ht[6] = {};     // entry -> first kernel queued, launch total, wait for the summary, commit, call total, calls
+    std::chrono::steady_clock::time_point ht_entry;
+#endif
     bool mid_last = false;  // the last flush recorded its set's mid_ev
     bool check_stages = false;   // wait after every flush stage (fault diagnosis)
     const char *fault_stage = nullptr;  // stage at the first failed wait
@@ -1019,6 +1026,10 @@ int tick_launch(gwaoi_world *w) {
         gw::launch_moves_bucketed(RS, w->max_slots, w->sinfo, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                                   S.sc, w->mv_hist, w->scan_tmp, w->mv_binned, st);
     } else if (moves_only) {  // one pass + fixup of repeated slots (run 0's claims: the prologue)
+#ifdef GWAOI_EXP_HOSTTIME
+        if (w->ovl_ok)  // (speculative launches only: ht_entry is their gwaoi_tick_finish call's)
+            w->ht[0] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w->ht_entry).count();
+#endif
         gw::launch_moves(RS, w->max_slots, w->sinfo, tick_id, n_total, seq_base, S.srec, virt ? nullptr : S.sss,
                          P.rec, n_prev, S.sc, w->coll, 1u, uniq, st);
     } else if (n_ops) {
@@ -1550,6 +1561,14 @@ const char *gwaoi_last_error(gwaoi_world *w) { return w ? w->last_error.c_str() 
 int gwaoi_world_destroy(gwaoi_world *w) {
     return gw::api_guard([&]() -> int {
     if (!w) return GWAOI_EINVAL;
+#ifdef GWAOI_EXP_HOSTTIME
+    if (w->ht[5] > 0)
+        fprintf(stderr, "hosttime per gwaoi_tick_finish (%.0f calls, %llu speculative): entry->first kernel %.1f us, launch %.1f, "
+                "summary wait %.1f, commit %.1f (speculative calls); call %.1f (all)\n", w->ht[5],
+                (unsigned long long)w->dbg.speculative_launches, w->ht[0] / std::max<double>(1, w->dbg.speculative_launches),
+                w->ht[1] / std::max<double>(1, w->dbg.speculative_launches), w->ht[2] / std::max<double>(1, w->dbg.speculative_launches),
+                w->ht[3] / std::max<double>(1, w->dbg.speculative_launches), w->ht[4] / w->ht[5]);
+#endif
     if (w->stream) (void)hipStreamSynchronize(w->stream);
     if (w->early_st) (void)hipStreamSynchronize(w->early_st);
     if (w->copy_st) (void)hipStreamSynchronize(w->copy_st);
@@ -2481,10 +2500,24 @@ int end_begin(gwaoi_world *w, bool *committed_out) {
         const Flight f = w->fl;
         commit_host(w, nullptr);
         w->ovl_ok = true;
+#ifdef GWAOI_EXP_HOSTTIME
+        const auto h0 = std::chrono::steady_clock::now();
+#endif
         lrc = tick_launch(w);
         w->ovl_ok = false;
         if (lrc == GWAOI_OK) w->dbg.speculative_launches++;
+#ifdef GWAOI_EXP_HOSTTIME
+        const auto h1 = std::chrono::steady_clock::now();
+        (void)wait_done(w, w->fs[f.set].done_ev);
+        const auto h2 = std::chrono::steady_clock::now();
+#endif
         rc = finish_flight(w, f, true, &committed);
+#ifdef GWAOI_EXP_HOSTTIME
+        const auto h3 = std::chrono::steady_clock::now();
+        w->ht[1] += std::chrono::duration<double, std::micro>(h1 - h0).count();
+        w->ht[2] += std::chrono::duration<double, std::micro>(h2 - h1).count();
+        w->ht[3] += std::chrono::duration<double, std::micro>(h3 - h2).count();
+#endif
     } else {
         rc = tick_finish(w, &committed);
         if (committed && !w->poisoned) lrc = tick_launch(w);
@@ -2575,6 +2608,16 @@ int gwaoi_tick_finish(gwaoi_world *w, uint32_t mode, uint64_t *n_enter, uint64_t
     }
     bool committed = false;
     int rc;
+#ifdef GWAOI_EXP_HOSTTIME
+    w->ht_entry = std::chrono::steady_clock::now();
+    struct HtCall {
+        gwaoi_world *w;
+        ~HtCall() {
+            w->ht[4] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w->ht_entry).count();
+            w->ht[5] += 1.0;
+        }
+    } ht_call{w};
+#endif
     if (host && !next && !pairs) {
         rc = end_host(w, &committed);
     } else {
