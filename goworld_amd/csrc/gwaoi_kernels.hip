@@ -1507,7 +1507,10 @@ __device__ __forceinline__ void gather_one(uint32_t k, const uint32_t *__restric
 // (and the launch boundary between the two passes, with the tail of each, is gone).  GU entries
 // per thread in flight (every load of the group before its stores); the block folds its entries'
 // bbox into part b (a thread's entries are in key order, so its runs of one space are too).
-constexpr int GU = 4;
+#ifndef GWAOI_MG_GU
+#define GWAOI_MG_GU 4
+#endif
+constexpr int GU = GWAOI_MG_GU;  // entries per thread in flight (k_merge_gather)
 __global__ __launch_bounds__(256) void k_merge_gather(MergeArgs M, GatherJob G) {
     const uint32_t n_live = merge_tile(M);
     __syncthreads();  // the block's merged cells before their gather
