@@ -345,6 +345,7 @@ struct FanArgs {
     uint32_t G, nb;
     uint32_t *blk_cnt;  // [G][nb] (pass 1 writes, the scan turns it into bases)
     uint4 *out;         // 3 uint4 per record (pass 2)
+    unsigned long long out_recs;  // records out holds (pass 2 writes nothing past a larger total)
 };
 
 __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
@@ -597,6 +598,10 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
     __shared__ uint4 s_rec[ST / 64][3 * 64];  // a wave's 64 records, staged for contiguous stores
     __shared__ uint32_t s_pos[ST / 64][64];
     __shared__ uint32_t s_ws[ST / 64];
+    // launched behind the hits pass without a host round trip: nothing to do when the hits
+    // overflowed the scratch or the total (the scan's last entry) outgrew the output; the host
+    // sees both after its one sync and reruns
+    if (*A.scr_cursor > A.scr_cap || A.blk_cnt[(size_t)A.G * A.nb] > A.out_recs) return;
     uint32_t *bin = lds, *gbase = lds + A.G + 1, *seg = gbase + A.G;
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t ne = A.F.n + A.n_left;
@@ -1248,6 +1253,17 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             if (int rc = part_bases(S, G, nb, false)) return rc;
             unsigned long long used = 0;
             SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
+            // the write pass follows on the device with the output as it is (the last collect's
+            // size); it writes nothing when either capacity fell short, which the host sees below
+            A.out = S->out;
+            A.out_recs = S->out_cap / 3;
+#ifdef GWAOI_EXP_FW_ROUNDTRIP  // A/B: the write pass launched after the host's sync (before round 6)
+            A.out_recs = 0;
+#endif
+            if (A.out_recs) {
+                k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
+                SY_TRY(hipGetLastError());
+            }
             SY_TRY(hipStreamSynchronize(S->st));
             if (used <= A.scr_cap) break;
             if (attempt || used >= SCR_FULL) {
@@ -1258,10 +1274,14 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
         }
         total = S->h_off_raw[G];
     }
-    if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * std::max<uint64_t>(total, 1))) return rc;
-    A.out = S->out;
-    if (total) k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
-    SY_TRY(hipGetLastError());
+    if (total > A.out_recs) {  // (first collect, or more records than the output holds)
+        if (int rc = ensure_out(S, &S->out, &S->out_cap, 3 * total)) return rc;
+        A.out = S->out;
+        A.out_recs = S->out_cap / 3;
+        k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
+        SY_TRY(hipGetLastError());
+    }
+    if (int rc = ensure_out(S, &S->out, &S->out_cap, 3)) return rc;  // (an empty collect's pointer)
     S->h_off.assign(S->h_off_raw.begin(), S->h_off_raw.end());
     if (to_host) {
         if (int rc = ensure_host(S, &S->h_rec, &S->h_rec_cap, std::max<uint64_t>(total, 1) * 48)) return rc;

@@ -216,6 +216,20 @@ def test_sync_dense_crowd_regrows_fanout_scratch():
 
 
 @pytest.mark.gpu
+def test_sync_output_regrows_between_collects():
+    """A small collect (10 entities in the spaces), then a dense one (the other
+    entities enter a 60 x 60 square): the write pass, launched behind the hits
+    pass without a host round trip, finds the previous collect's output too
+    small and writes nothing; the host regrows the output and relaunches it."""
+    sc = SS.make(seed=14, n=800, n_outside=20, flushes=2, L=60.0)
+    enters = [op for op in sc["setup"] if op[0] == "enter"]
+    keep = {op[1] for op in enters[:10]}
+    sc["setup"] = [op for op in sc["setup"] if op[0] != "enter" or op[1] in keep]
+    sc["flushes"].insert(0, [op for op in enters if op[1] not in keep])
+    check_run(sc)
+
+
+@pytest.mark.gpu
 def test_sync_errors():
     from goworld_amd import GwaoiError, World
     with World(16, device=0) as w:
