@@ -1138,7 +1138,9 @@ int ensure_host(SyncState *S, uint8_t **p, size_t *cap, size_t bytes) {
 
 // Multisplit bases: blk_cnt [parts][nb] -> exclusive scan (parts*nb + 1
 // entries, the last is the total) -> h_off_raw[0..parts].
-int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true) {
+int fetch_bases(SyncState *S, uint32_t parts, bool sync);
+
+int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true, bool copy = true) {
     const size_t n = (size_t)parts * nb + 1;
     if (int rc = ensure_u32(S, &S->scan_tmp, &S->scan_cap, scan_tmp_elems(n) + 4)) return rc;
     if (parts + 1 > S->off_cap) {
@@ -1149,6 +1151,11 @@ int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true) {
     scan_exclusive(S->blk_cnt, S->blk_cnt, n, S->scan_tmp, S->st);
     k_part_offsets<<<cdivu(parts + 1, ST), ST, 0, S->st>>>(S->blk_cnt, parts, nb, S->d_off);
     SY_TRY(hipGetLastError());
+    return copy ? fetch_bases(S, parts, sync) : GWAOI_OK;
+}
+
+// the bases part_bases left in d_off, to the host (a pageable copy: the host waits for it)
+int fetch_bases(SyncState *S, uint32_t parts, bool sync) {
     S->h_off_raw.resize(parts + 1);
     SY_TRY(hipMemcpyAsync(S->h_off_raw.data(), S->d_off, (parts + 1) * 8, hipMemcpyDeviceToHost, S->st));
     if (sync) SY_TRY(hipStreamSynchronize(S->st));
@@ -1249,12 +1256,11 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             k_fan_hits<<<nb, ST, (size_t)G * 4, S->st>>>(A);
             SY_TRY(hipGetLastError());
             // the per-gate bases are scanned before the capacity check: one host round trip
-            // for both (a rerun rewrites every count the scan read)
-            if (int rc = part_bases(S, G, nb, false)) return rc;
-            unsigned long long used = 0;
-            SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
-            // the write pass follows on the device with the output as it is (the last collect's
-            // size); it writes nothing when either capacity fell short, which the host sees below
+            // for both (a rerun rewrites every count the scan read).  The write pass follows on
+            // the device with the output as it is (the last collect's size), queued before the
+            // (pageable, host-blocking) copies of the bases and the cursor; it writes nothing
+            // when either capacity fell short, which the host sees below
+            if (int rc = part_bases(S, G, nb, false, false)) return rc;
             A.out = S->out;
             A.out_recs = S->out_cap / 3;
 #ifdef GWAOI_EXP_FW_ROUNDTRIP  // A/B: the write pass launched after the host's sync (before round 6)
@@ -1264,6 +1270,9 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
                 k_fan_write<<<nb, ST, (3 * (size_t)G + 1) * 4, S->st>>>(A);
                 SY_TRY(hipGetLastError());
             }
+            if (int rc = fetch_bases(S, G, false)) return rc;
+            unsigned long long used = 0;
+            SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
             SY_TRY(hipStreamSynchronize(S->st));
             if (used <= A.scr_cap) break;
             if (attempt || used >= SCR_FULL) {
