@@ -577,6 +577,141 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
     for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) A.blk_cnt[(size_t)q * A.nb + blk] = gcnt[q];
 }
 
+// Fan-out pass 1, a wave per receiver (the default): the run sizing and placement
+// are k_fan_hits' (one lane per entry, cell_start loads only), then each wave
+// takes its walking receivers one at a time.  The receiver's window rows are
+// laid end to end (lane j loads row j's bounds; a wave scan gives each row's
+// first position) and the wave deals out 64 consecutive positions per step: a
+// lane's candidate is found from the rows starting in the step (an LDS mark per
+// position, a ballot) and the row's offset (LDS), so one load instruction reads
+// 64 consecutive candidates instead of one candidate from each of 64 windows,
+// and the hits are compacted by a ballot into consecutive 4-B stores.  The hits
+// and their order (rows in order, frame order inside a row) are k_fan_hits'.
+#ifndef GWAOI_FAN_WU
+#define GWAOI_FAN_WU 2  // steps of 64 positions with their loads in flight together
+#endif
+constexpr int FAN_WU = GWAOI_FAN_WU;
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t k) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k);
+}
+
+__global__ __launch_bounds__(ST) void k_fan_hits_wave(FanArgs A) {
+    extern __shared__ uint32_t gcnt[];  // [G] records per gate of the block
+    __shared__ uint32_t s_ws[ST / 64];
+    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_adj[ST / 64][64];            // candidate index - position, per non-empty row
+    __shared__ uint32_t s_mark[ST / 64][FAN_WU * 64];  // a non-empty row starts at this position
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t nf = A.F.n, ne = nf + A.n_left;
+    const uint32_t w = threadIdx.x / 64, ln = s_lane();
+    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) gcnt[q] = 0u;
+    const uint32_t i = blk * ST + threadIdx.x;
+    const uint32_t g = i < ne ? A.rg[i] : NO_GATE;
+    const bool on = g != NO_GATE;
+    const bool own = on && (A.snd[i] & GWAOI_SIF_OWN_CLIENT);
+    const bool walk = on && i < nf;
+    const uint32_t *cs = A.F.cell_start;
+    FanWin W{};
+    uint32_t ub = own ? 1u : 0u;
+    if (walk) {
+        W = fan_window(A.F, i);
+        const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
+        for (int cz = W.cz0; cz <= W.cz1; ++cz) {
+            const uint32_t rb = W.row0 + (uint32_t)(cz - W.cz0) * W.gx;
+            ub += cs[rb + span] - cs[rb];
+        }
+    }
+    ub = (ub + 3u) & ~3u;  // (k_fan_hits' run sizes, so the two passes place runs alike)
+    uint32_t tot;
+    const uint32_t off = block_excl(ub, s_ws, tot);
+    if (threadIdx.x == 0) {
+        const unsigned long long b = tot ? atomicAdd(A.scr_cursor, (unsigned long long)tot) : 0ull;
+        s_base = b + tot <= A.scr_cap ? (uint32_t)b : SCR_FULL;
+    }
+    __syncthreads();
+    const bool fits = s_base != SCR_FULL;
+    const uint32_t sb = s_base + off;
+    if (own && fits) A.scr[sb] = i;
+    uint32_t c = own ? 1u : 0u;
+    const unsigned long long lt = (1ull << ln) - 1ull;
+    const unsigned long long le = ln == 63 ? ~0ull : (2ull << ln) - 1ull;
+    unsigned long long todo = __ballot(walk);
+    while (todo) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(todo);
+        todo &= todo - 1ull;
+        const uint32_t ri = blk * ST + w * 64u + k;
+        const float rx = __uint_as_float(rdl(__float_as_uint(W.R.x), k));
+        const float rz = __uint_as_float(rdl(__float_as_uint(W.R.z), k));
+        const float D = __uint_as_float(rdl(__float_as_uint(W.D), k));
+        const unsigned long long rs = ((unsigned long long)rdl((uint32_t)(W.R.s >> 32), k) << 32) |
+                                      rdl((uint32_t)W.R.s, k);
+        const uint32_t row0 = rdl(W.row0, k), gx = rdl(W.gx, k);
+        const uint32_t span = rdl((uint32_t)(W.cx1 - W.cx0), k) + 1u;
+        const uint32_t nrows = rdl((uint32_t)(W.cz1 - W.cz0), k) + 1u;
+        const uint32_t rsb = rdl(sb, k);
+        uint32_t rc = rdl(c, k);
+        for (uint32_t j0 = 0; j0 < nrows; j0 += 64u) {
+            // lane t: row j0 + t of the window, its candidates [jb, jb + len)
+            const uint32_t t = j0 + ln;
+            const uint32_t rb = row0 + min(t, nrows - 1u) * gx;
+            const uint32_t jb = cs[rb], je = cs[rb + span];
+            const uint32_t len = t < nrows ? je - jb : 0u;
+            uint32_t incl = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if ((int)ln >= o) incl += y;
+            }
+            const uint32_t ex = incl - len, T = rdl(incl, 63);
+            const unsigned long long nem = __ballot(len != 0u);
+            if (len) s_adj[w][__popcll(nem & lt)] = jb - ex;
+            for (uint32_t p0 = 0; p0 < T; p0 += FAN_WU * 64u) {
+#pragma unroll
+                for (int u = 0; u < FAN_WU; ++u) s_mark[w][u * 64 + ln] = 0u;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                if (len && ex >= p0 && ex - p0 < FAN_WU * 64u) s_mark[w][ex - p0] = 1u;
+                const uint32_t before = (uint32_t)__popcll(__ballot(len != 0u && ex < p0));
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                uint32_t b[FAN_WU];
+                uint4 q[FAN_WU];
+                uint32_t nr = before;  // non-empty rows started before this step of 64
+#pragma unroll
+                for (int u = 0; u < FAN_WU; ++u) {
+                    const unsigned long long m = __ballot(s_mark[w][u * 64 + ln] != 0u);
+                    const uint32_t p = p0 + (uint32_t)u * 64u + ln;
+                    const uint32_t row = nr + (uint32_t)__popcll(m & le);  // rows started at or before p
+                    nr += (uint32_t)__popcll(m);
+                    b[u] = p < T ? p + s_adj[w][row - 1u] : ri;  // (row >= 1 whenever p < T)
+                    q[u] = A.frec[b[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < FAN_WU; ++u) {
+                    const uint32_t p = p0 + (uint32_t)u * 64u + ln;
+                    const unsigned long long bs = ((unsigned long long)(q[u].w & 0x7FFFFFFFu) << 32) | q[u].z;
+                    const bool hit = p < T && b[u] != ri && (q[u].w >> 31) &&
+                                     rel(rx, rz, rs, __uint_as_float(q[u].x), __uint_as_float(q[u].y), bs, D);
+                    const unsigned long long hm = __ballot(hit);
+                    if (hit && fits) A.scr[rsb + rc + (uint32_t)__popcll(hm & lt)] = b[u];
+                    rc += (uint32_t)__popcll(hm);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // s_adj is rewritten by the next row group
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+        if (ln == k) c = rc;
+    }
+    if (i < ne) {
+        A.fcnt[i] = c;
+        A.fsb[i] = sb;
+    }
+    if (c) atomicAdd(&gcnt[g], c);
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) A.blk_cnt[(size_t)q * A.nb + blk] = gcnt[q];
+}
+
 // Fan-out pass 2 (write): block blk expands the hits of its receivers into
 // 48-B records (receiver's ClientID, sender's EntityID, x, y, z, yaw).  The
 // receivers are regrouped by gate (stable), so the block's records of gate g
@@ -1253,7 +1388,11 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
                 SY_TRY(hipMemsetAsync(S->scr_cursor, 0, 8, S->st));
                 SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
             }
+#ifdef GWAOI_EXP_FAN_LANE  // A/B: one lane per receiver walking its own window
             k_fan_hits<<<nb, ST, (size_t)G * 4, S->st>>>(A);
+#else
+            k_fan_hits_wave<<<nb, ST, (size_t)G * 4, S->st>>>(A);
+#endif
             SY_TRY(hipGetLastError());
             // the per-gate bases are scanned before the capacity check: one host round trip
             // for both (a rerun rewrites every count the scan read).  The write pass follows on
