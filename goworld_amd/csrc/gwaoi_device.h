@@ -84,4 +84,32 @@ __device__ __forceinline__ void ev_put2(uint2 *out, uint64_t cap, unsigned long 
     }
 }
 
+// Inclusive wave-wide scans by DPP (rows of 16 lanes, then the row broadcasts).
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t v, int n) {
+    switch (n) {
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    case 4: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    }
+}
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += dpp_shr(v, 1);
+    v += dpp_shr(v, 2);
+    v += dpp_shr(v, 4);
+    v += dpp_shr(v, 8);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, dpp_shr(v, 1));
+    v = max(v, dpp_shr(v, 2));
+    v = max(v, dpp_shr(v, 4));
+    v = max(v, dpp_shr(v, 8));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
 }  // namespace gw

@@ -588,9 +588,14 @@ __global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
 // and the hits are compacted by a ballot into consecutive 4-B stores.  The hits
 // and their order (rows in order, frame order inside a row) are k_fan_hits'.
 #ifndef GWAOI_FAN_WU
-#define GWAOI_FAN_WU 2  // steps of 64 positions with their loads in flight together
+#define GWAOI_FAN_WU 2  // steps of 64 positions per receiver with their loads in flight together
 #endif
 constexpr int FAN_WU = GWAOI_FAN_WU;
+#ifndef GWAOI_FAN_NR
+#define GWAOI_FAN_NR 2  // receivers of a wave dealt together (A/B, profiles/r06_ab_fan_hits.txt: k_fan_hits
+                        // 252 us at NR 2 / WU 2, 259 at 3 / 2, 279 at 4 / 2, 283 at 2 / 4, 267 at 1 / 4)
+#endif
+constexpr int FAN_NR = GWAOI_FAN_NR;
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t k) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k);
@@ -600,8 +605,8 @@ __global__ __launch_bounds__(ST) void k_fan_hits_wave(FanArgs A) {
     extern __shared__ uint32_t gcnt[];  // [G] records per gate of the block
     __shared__ uint32_t s_ws[ST / 64];
     __shared__ uint32_t s_base;
-    __shared__ uint32_t s_adj[ST / 64][64];            // candidate index - position, per non-empty row
-    __shared__ uint32_t s_mark[ST / 64][FAN_WU * 64];  // a non-empty row starts at this position
+    __shared__ uint32_t s_adj[ST / 64][FAN_NR][64];            // candidate index - position, per non-empty row
+    __shared__ uint32_t s_mark[ST / 64][FAN_NR][FAN_WU * 64];  // a non-empty row starts at this position
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t nf = A.F.n, ne = nf + A.n_left;
     const uint32_t w = threadIdx.x / 64, ln = s_lane();
@@ -637,71 +642,104 @@ __global__ __launch_bounds__(ST) void k_fan_hits_wave(FanArgs A) {
     const unsigned long long lt = (1ull << ln) - 1ull;
     const unsigned long long le = ln == 63 ? ~0ull : (2ull << ln) - 1ull;
     unsigned long long todo = __ballot(walk);
+#ifdef GWAOI_EXP_FAN_NOWALK  // timing only: the run sizing and placement without the walks (no neighbour records)
+    todo = 0;
+#endif
     while (todo) {
-        const uint32_t k = (uint32_t)__builtin_ctzll(todo);
-        todo &= todo - 1ull;
-        const uint32_t ri = blk * ST + w * 64u + k;
-        const float rx = __uint_as_float(rdl(__float_as_uint(W.R.x), k));
-        const float rz = __uint_as_float(rdl(__float_as_uint(W.R.z), k));
-        const float D = __uint_as_float(rdl(__float_as_uint(W.D), k));
-        const unsigned long long rs = ((unsigned long long)rdl((uint32_t)(W.R.s >> 32), k) << 32) |
-                                      rdl((uint32_t)W.R.s, k);
-        const uint32_t row0 = rdl(W.row0, k), gx = rdl(W.gx, k);
-        const uint32_t span = rdl((uint32_t)(W.cx1 - W.cx0), k) + 1u;
-        const uint32_t nrows = rdl((uint32_t)(W.cz1 - W.cz0), k) + 1u;
-        const uint32_t rsb = rdl(sb, k);
-        uint32_t rc = rdl(c, k);
-        for (uint32_t j0 = 0; j0 < nrows; j0 += 64u) {
-            // lane t: row j0 + t of the window, its candidates [jb, jb + len)
+        // FAN_NR receivers at a time, their steps interleaved (a receiver's chain of row-bound
+        // loads, then candidate loads, is latency-bound alone); a missing one has no rows
+        uint32_t k[FAN_NR], ri[FAN_NR], row0[FAN_NR], gx[FAN_NR], span[FAN_NR], nrows[FAN_NR], rsb[FAN_NR],
+            rc[FAN_NR];
+        float rx[FAN_NR], rz[FAN_NR], D[FAN_NR];
+        unsigned long long rs[FAN_NR];
+        uint32_t maxrows = 0;
+#pragma unroll
+        for (int r = 0; r < FAN_NR; ++r) {
+            k[r] = todo ? (uint32_t)__builtin_ctzll(todo) : 64u;
+            todo &= todo - 1ull;
+            const uint32_t kk = min(k[r], 63u);
+            ri[r] = blk * ST + w * 64u + kk;
+            rx[r] = __uint_as_float(rdl(__float_as_uint(W.R.x), kk));
+            rz[r] = __uint_as_float(rdl(__float_as_uint(W.R.z), kk));
+            D[r] = __uint_as_float(rdl(__float_as_uint(W.D), kk));
+            rs[r] = ((unsigned long long)rdl((uint32_t)(W.R.s >> 32), kk) << 32) | rdl((uint32_t)W.R.s, kk);
+            row0[r] = rdl(W.row0, kk);
+            gx[r] = rdl(W.gx, kk);
+            span[r] = rdl((uint32_t)(W.cx1 - W.cx0), kk) + 1u;
+            nrows[r] = k[r] < 64u ? rdl((uint32_t)(W.cz1 - W.cz0), kk) + 1u : 0u;
+            rsb[r] = rdl(sb, kk);
+            rc[r] = rdl(c, kk);
+            maxrows = max(maxrows, nrows[r]);
+        }
+        for (uint32_t j0 = 0; j0 < maxrows; j0 += 64u) {
+            // lane t: row j0 + t of each window, its candidates [jb, jb + len)
             const uint32_t t = j0 + ln;
-            const uint32_t rb = row0 + min(t, nrows - 1u) * gx;
-            const uint32_t jb = cs[rb], je = cs[rb + span];
-            const uint32_t len = t < nrows ? je - jb : 0u;
-            uint32_t incl = len;
+            uint32_t jb[FAN_NR], je[FAN_NR], len[FAN_NR], ex[FAN_NR], T[FAN_NR];
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if ((int)ln >= o) incl += y;
+            for (int r = 0; r < FAN_NR; ++r) {
+                const uint32_t rb = row0[r] + min(t, max(nrows[r], 1u) - 1u) * gx[r];
+                jb[r] = cs[rb];
+                je[r] = cs[rb + span[r]];
             }
-            const uint32_t ex = incl - len, T = rdl(incl, 63);
-            const unsigned long long nem = __ballot(len != 0u);
-            if (len) s_adj[w][__popcll(nem & lt)] = jb - ex;
-            for (uint32_t p0 = 0; p0 < T; p0 += FAN_WU * 64u) {
+            uint32_t Tm = 0;
 #pragma unroll
-                for (int u = 0; u < FAN_WU; ++u) s_mark[w][u * 64 + ln] = 0u;
+            for (int r = 0; r < FAN_NR; ++r) {
+                len[r] = t < nrows[r] ? je[r] - jb[r] : 0u;
+                const uint32_t incl = wave_scan_add(len[r]);
+                ex[r] = incl - len[r];
+                T[r] = rdl(incl, 63);
+                Tm = max(Tm, T[r]);
+                const unsigned long long nem = __ballot(len[r] != 0u);
+                if (len[r]) s_adj[w][r][__popcll(nem & lt)] = jb[r] - ex[r];
+            }
+            for (uint32_t p0 = 0; p0 < Tm; p0 += FAN_WU * 64u) {
+#pragma unroll
+                for (int r = 0; r < FAN_NR; ++r)
+#pragma unroll
+                    for (int u = 0; u < FAN_WU; ++u) s_mark[w][r][u * 64 + ln] = 0u;
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                if (len && ex >= p0 && ex - p0 < FAN_WU * 64u) s_mark[w][ex - p0] = 1u;
-                const uint32_t before = (uint32_t)__popcll(__ballot(len != 0u && ex < p0));
+                uint32_t nr[FAN_NR];  // non-empty rows started before this step
+#pragma unroll
+                for (int r = 0; r < FAN_NR; ++r) {
+                    if (len[r] && ex[r] >= p0 && ex[r] - p0 < FAN_WU * 64u) s_mark[w][r][ex[r] - p0] = 1u;
+                    nr[r] = (uint32_t)__popcll(__ballot(len[r] != 0u && ex[r] < p0));
+                }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                uint32_t b[FAN_WU];
-                uint4 q[FAN_WU];
-                uint32_t nr = before;  // non-empty rows started before this step of 64
+                uint32_t b[FAN_NR][FAN_WU];
+                uint4 q[FAN_NR][FAN_WU];
 #pragma unroll
-                for (int u = 0; u < FAN_WU; ++u) {
-                    const unsigned long long m = __ballot(s_mark[w][u * 64 + ln] != 0u);
-                    const uint32_t p = p0 + (uint32_t)u * 64u + ln;
-                    const uint32_t row = nr + (uint32_t)__popcll(m & le);  // rows started at or before p
-                    nr += (uint32_t)__popcll(m);
-                    b[u] = p < T ? p + s_adj[w][row - 1u] : ri;  // (row >= 1 whenever p < T)
-                    q[u] = A.frec[b[u]];
-                }
+                for (int r = 0; r < FAN_NR; ++r)
 #pragma unroll
-                for (int u = 0; u < FAN_WU; ++u) {
-                    const uint32_t p = p0 + (uint32_t)u * 64u + ln;
-                    const unsigned long long bs = ((unsigned long long)(q[u].w & 0x7FFFFFFFu) << 32) | q[u].z;
-                    const bool hit = p < T && b[u] != ri && (q[u].w >> 31) &&
-                                     rel(rx, rz, rs, __uint_as_float(q[u].x), __uint_as_float(q[u].y), bs, D);
-                    const unsigned long long hm = __ballot(hit);
-                    if (hit && fits) A.scr[rsb + rc + (uint32_t)__popcll(hm & lt)] = b[u];
-                    rc += (uint32_t)__popcll(hm);
-                }
+                    for (int u = 0; u < FAN_WU; ++u) {
+                        const unsigned long long m = __ballot(s_mark[w][r][u * 64 + ln] != 0u);
+                        const uint32_t p = p0 + (uint32_t)u * 64u + ln;
+                        const uint32_t row = nr[r] + (uint32_t)__popcll(m & le);  // rows started at or before p
+                        nr[r] += (uint32_t)__popcll(m);
+                        b[r][u] = p < T[r] ? p + s_adj[w][r][row - 1u] : ri[r];  // (row >= 1 whenever p < T)
+                        q[r][u] = A.frec[b[r][u]];
+                    }
+#pragma unroll
+                for (int r = 0; r < FAN_NR; ++r)
+#pragma unroll
+                    for (int u = 0; u < FAN_WU; ++u) {
+                        const uint32_t p = p0 + (uint32_t)u * 64u + ln;
+                        const uint4 &Q = q[r][u];
+                        const unsigned long long bs = ((unsigned long long)(Q.w & 0x7FFFFFFFu) << 32) | Q.z;
+                        const bool hit = p < T[r] && b[r][u] != ri[r] && (Q.w >> 31) &&
+                                         rel(rx[r], rz[r], rs[r], __uint_as_float(Q.x), __uint_as_float(Q.y), bs, D[r]);
+                        const unsigned long long hm = __ballot(hit);
+                        if (hit && fits) A.scr[rsb[r] + rc[r] + (uint32_t)__popcll(hm & lt)] = b[r][u];
+                        rc[r] += (uint32_t)__popcll(hm);
+                    }
             }
             __builtin_amdgcn_wave_barrier();  // s_adj is rewritten by the next row group
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }
-        if (ln == k) c = rc;
+#pragma unroll
+        for (int r = 0; r < FAN_NR; ++r)
+            if (ln == k[r]) c = rc[r];
     }
     if (i < ne) {
         A.fcnt[i] = c;
