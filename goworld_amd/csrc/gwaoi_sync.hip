@@ -147,6 +147,7 @@ struct DecodeArgs {
     unsigned long long *cl;
     float4 *pos;
     uint32_t *oflag, *oflag_n;  // slots flagged outside every AOI space (own-client records)
+    uint32_t *h_ndec;           // pinned host word: *oflag_n once the batch is decoded
     uint32_t oflag_cap;         // entries oflag holds (max_slots: one per slot, see k_decode)
     uint32_t *dups, *ndup;      // slots with a record whose claim store did not survive (1)
 };
@@ -299,6 +300,7 @@ __global__ __launch_bounds__(ST) void k_decode_apply(DecodeArgs A) {
 // Listed slots (rare; may repeat): apply the records holding the final claims.
 __global__ __launch_bounds__(ST) void k_decode_dups(DecodeArgs A) {
     const uint32_t nd = *A.ndup;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *A.h_ndec = *A.oflag_n;  // (for the collect, no copy)
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
         const uint32_t s = A.dups[k];
         const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
@@ -932,9 +934,10 @@ __global__ __launch_bounds__(ST) void k_route(RouteArgs A) {
 
 // offsets[k] = scanned[k * nb] for k in [0, parts]; scanned has parts*nb + 1 entries
 __global__ void k_part_offsets(const uint32_t *__restrict__ scanned, uint32_t parts, uint32_t nb,
-                               unsigned long long *off) {
+                               unsigned long long *off, const unsigned long long *extra) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k <= parts) off[k] = scanned[(size_t)k * nb];
+    if (k == parts) off[parts + 1] = extra ? *extra : 0ull;  // (one copy brings both to the host)
 }
 
 }  // namespace
@@ -953,6 +956,8 @@ struct SyncState {
     uint32_t *oflag = nullptr, *oflag_n = nullptr;  // decode: slots flagged outside every AOI space
     uint32_t oflag_cap = 0;                           // entries of oflag (max_slots)
     bool decoded = false;                           // a decode ran since the last collect
+    uint32_t *h_ndec = nullptr;                     // pinned: oflag_n after the last decode
+    hipEvent_t ndec_ev = nullptr;                   // that copy
     // id -> slot hash table (device, host mirror)
     uint4 *htab = nullptr;  // 4 per bucket: 3 keys, (slot, slot, slot, -)
     uint32_t hcap = 0, hused = 0;  // entries (3 per 64-B bucket), live + tombstones
@@ -990,6 +995,8 @@ struct SyncState {
     size_t blk_cap = 0, scan_cap = 0;
     unsigned long long *d_off = nullptr;
     size_t off_cap = 0;
+    uint8_t *h_offp = nullptr;  // pinned: d_off (and the extra word) on the host
+    size_t h_offp_cap = 0;
     uint32_t *d_left = nullptr;
     size_t left_cap = 0;
     // fan-out scratch, frame order (fan_cap entries each)
@@ -1159,7 +1166,9 @@ int create(gwaoi_world *w, SyncState **out) {
               hipMemsetAsync(S->eid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->cid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->htab, 0xFF, (size_t)nbk * 64, S->st) == hipSuccess &&  // every entry H_EMPTY
-              hipEventCreateWithFlags(&S->stage_ev, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&S->stage_ev, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&S->ndec_ev, hipEventDisableTiming) == hipSuccess &&
+              hipHostMalloc((void **)&S->h_ndec, 4, hipHostMallocDefault) == hipSuccess;
     if (!ok) {
         sync_destroy(S);
         return GWAOI_EDEVICE;
@@ -1313,25 +1322,38 @@ int ensure_host(SyncState *S, uint8_t **p, size_t *cap, size_t bytes) {
 // entries, the last is the total) -> h_off_raw[0..parts].
 int fetch_bases(SyncState *S, uint32_t parts, bool sync);
 
-int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true, bool copy = true) {
+unsigned long long unpack_bases(SyncState *S, uint32_t parts) {  // -> the extra word
+    const unsigned long long *h = reinterpret_cast<const unsigned long long *>(S->h_offp);
+    S->h_off_raw.assign(h, h + parts + 1);
+    return h[parts + 1];
+}
+
+// per-part bases of the [parts][nb] counts in blk_cnt (scanned in place) into d_off[0, parts],
+// with *extra (a device word, e.g. a cursor) in d_off[parts + 1]
+int part_bases(SyncState *S, uint32_t parts, uint32_t nb, bool sync = true, bool copy = true,
+               const unsigned long long *extra = nullptr) {
     const size_t n = (size_t)parts * nb + 1;
     if (int rc = ensure_u32(S, &S->scan_tmp, &S->scan_cap, scan_tmp_elems(n) + 4)) return rc;
-    if (parts + 1 > S->off_cap) {
+    if (parts + 2 > S->off_cap) {
         sfree(S->d_off);
-        if (int rc = salloc(S, &S->d_off, parts + 1)) return rc;
-        S->off_cap = parts + 1;
+        if (int rc = salloc(S, &S->d_off, parts + 2)) return rc;
+        S->off_cap = parts + 2;
     }
     scan_exclusive(S->blk_cnt, S->blk_cnt, n, S->scan_tmp, S->st);
-    k_part_offsets<<<cdivu(parts + 1, ST), ST, 0, S->st>>>(S->blk_cnt, parts, nb, S->d_off);
+    k_part_offsets<<<cdivu(parts + 1, ST), ST, 0, S->st>>>(S->blk_cnt, parts, nb, S->d_off, extra);
     SY_TRY(hipGetLastError());
     return copy ? fetch_bases(S, parts, sync) : GWAOI_OK;
 }
 
-// the bases part_bases left in d_off, to the host (a pageable copy: the host waits for it)
+// the bases part_bases left in d_off (and the extra word), to pinned host memory; unpack_bases
+// turns them into h_off_raw once the stream has reached the copy
 int fetch_bases(SyncState *S, uint32_t parts, bool sync) {
-    S->h_off_raw.resize(parts + 1);
-    SY_TRY(hipMemcpyAsync(S->h_off_raw.data(), S->d_off, (parts + 1) * 8, hipMemcpyDeviceToHost, S->st));
-    if (sync) SY_TRY(hipStreamSynchronize(S->st));
+    if (int rc = ensure_host(S, &S->h_offp, &S->h_offp_cap, (parts + 2) * 8)) return rc;
+    SY_TRY(hipMemcpyAsync(S->h_offp, S->d_off, (parts + 2) * 8, hipMemcpyDeviceToHost, S->st));
+    if (sync) {
+        SY_TRY(hipStreamSynchronize(S->st));
+        unpack_bases(S, parts);
+    }
     return GWAOI_OK;
 }
 
@@ -1358,9 +1380,9 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
         if (world_slot_space(w, s) == SP_DEAD) left.push_back(s);
     S->left.clear();
     uint32_t n_dec = 0;
-    if (S->decoded) {
-        SY_TRY(hipMemcpyAsync(&n_dec, S->oflag_n, 4, hipMemcpyDeviceToHost, S->st));
-        SY_TRY(hipStreamSynchronize(S->st));
+    if (S->decoded) {  // copied behind the last decode: done by now unless that flush is still running
+        SY_TRY(hipEventSynchronize(S->ndec_ev));
+        n_dec = *S->h_ndec;
         S->decoded = false;
         n_dec = std::min(n_dec, S->oflag_cap);  // k_decode lists a slot at most once (atomicOr claim)
     }
@@ -1437,7 +1459,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
             // the device with the output as it is (the last collect's size), queued before the
             // (pageable, host-blocking) copies of the bases and the cursor; it writes nothing
             // when either capacity fell short, which the host sees below
-            if (int rc = part_bases(S, G, nb, false, false)) return rc;
+            if (int rc = part_bases(S, G, nb, false, false, S->scr_cursor)) return rc;
             A.out = S->out;
             A.out_recs = S->out_cap / 3;
 #ifdef GWAOI_EXP_FW_ROUNDTRIP  // A/B: the write pass launched after the host's sync (before round 6)
@@ -1448,9 +1470,8 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
                 SY_TRY(hipGetLastError());
             }
             if (int rc = fetch_bases(S, G, false)) return rc;
-            unsigned long long used = 0;
-            SY_TRY(hipMemcpyAsync(&used, S->scr_cursor, 8, hipMemcpyDeviceToHost, S->st));
             SY_TRY(hipStreamSynchronize(S->st));
+            const unsigned long long used = unpack_bases(S, G);
             if (used <= A.scr_cap) break;
             if (attempt || used >= SCR_FULL) {
                 world_set_error(w, "sync: fan-out scratch exceeds 2^32 entries");
@@ -1552,6 +1573,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     A.pos = S->pos;
     A.oflag = S->oflag;
     A.oflag_n = S->oflag_n;
+    A.h_ndec = S->h_ndec;
     A.oflag_cap = S->oflag_cap;
     A.dups = reinterpret_cast<uint32_t *>(base + 5 * al(n * 4));
     A.ndup = reinterpret_cast<uint32_t *>(base + 6 * al(n * 4));
@@ -1561,6 +1583,7 @@ int decode(gwaoi_world *w, const uint8_t *payload, size_t n, bool on_device) {
     k_decode_apply<<<cdivu(n, ST), ST, 0, S->st>>>(A);
     k_decode_dups<<<std::min<uint32_t>(cdivu(n, ST), 64u), ST, 0, S->st>>>(A);
     SY_TRY(hipGetLastError());
+    SY_TRY(hipEventRecord(S->ndec_ev, S->st));
     return world_queue_decoded(w, o_slot, o_x, o_z, o_sp, n);
 }
 
@@ -1590,6 +1613,9 @@ void sync_destroy(SyncState *S) {
     if (S->h_rec) (void)hipHostFree(S->h_rec);
     if (S->h_rec_d) (void)hipHostFree(S->h_rec_d);
     if (S->stage_ev) (void)hipEventDestroy(S->stage_ev);
+    if (S->ndec_ev) (void)hipEventDestroy(S->ndec_ev);
+    if (S->h_ndec) (void)hipHostFree(S->h_ndec);
+    if (S->h_offp) (void)hipHostFree(S->h_offp);
     delete S;
 }
 
