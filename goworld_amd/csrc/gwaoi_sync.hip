@@ -91,11 +91,16 @@ __global__ void k_scatter128(const W128 *__restrict__ w, uint32_t n, ArrTable T)
 }
 
 // Per-slot sync state is packed so that one pass touches one line per slot:
-//   sst[s]  uint4 {gate index, space in call order, syncing, sync flags}
+//   one 64-B record per slot (SLOT_U4 uint4): sst {gate index, space in call
+//           order, syncing, sync flags}, pos {x, y, z, yaw}, eid, cid -- the
+//           fan-out's sender pass reads the first three from one line, the
+//           decode writes pos and the flags into it
 //   cl[s]   ulonglong2 {Position claim, yaw claim}
 //   htab    64-B buckets {3 entity ids; their 3 slots}: a probe reads keys and
 //           values from one line (see lookup).
 enum SstField { SST_GATE = 0, SST_SPACE = 1, SST_SYNCING = 2, SST_FLAGS = 3 };
+constexpr uint32_t SLOT_U4 = 4;             // uint4 per slot record: sst, pos, eid, cid
+constexpr uint32_t SLOT_W = 4 * SLOT_U4;    // its 32-bit words
 
 // Host position/yaw writes (set_position_yaw, entity_set_position_yaw,
 // entity_enter_plain) and flag-only ops (Space.enter): claim, then the winner
@@ -117,14 +122,14 @@ __global__ void k_side_claim(const SideOp *__restrict__ ops, uint32_t n, unsigne
     const SideOp o = ops[i];
     if (o.bits & SIDE_POS) atomicMax(&cl[2 * (size_t)o.slot], o.claim);
     if (o.bits & SIDE_YAW) atomicMax(&cl[2 * (size_t)o.slot + 1], o.claim);
-    if (o.bits & SIDE_SIF) atomicOr(&sst[4 * (size_t)o.slot + SST_FLAGS], o.bits & SIDE_SIF);
+    if (o.bits & SIDE_SIF) atomicOr(&sst[SLOT_W * (size_t)o.slot + SST_FLAGS], o.bits & SIDE_SIF);
 }
 
 __global__ void k_side_write(const SideOp *__restrict__ ops, uint32_t n, const unsigned long long *cl, float4 *pos) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const SideOp o = ops[i];
-    float *p = reinterpret_cast<float *>(pos + o.slot);
+    float *p = reinterpret_cast<float *>(pos + SLOT_U4 * (size_t)o.slot);
     if ((o.bits & SIDE_POS) && cl[2 * (size_t)o.slot] == o.claim) {
         p[0] = o.pos.x;
         p[1] = o.pos.y;
@@ -199,7 +204,7 @@ __device__ __forceinline__ void decode_rest(const DecodeArgs &A, uint32_t i, con
         if (move) reinterpret_cast<ulonglong2 *>(A.cl)[s] = make_ulonglong2(c, c);
         else A.cl[2 * (size_t)s + 1] = c;
         // (the flags word came with the slot's record; records of one slot all set the same bit)
-        uint32_t *fl = A.sst + 4 * (size_t)s + SST_FLAGS;
+        uint32_t *fl = A.sst + SLOT_W * (size_t)s + SST_FLAGS;
         if (!move && old == 0u) {
             // first flag of a slot outside the frame since the last collect: the flag is
             // claimed atomically, so a slot with several records in the batch is listed
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
     uint4 st[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u)  // every slot record in flight together
-        st[u] = s[u] != SLOT_NONE ? reinterpret_cast<const uint4 *>(A.sst)[s[u]] : make_uint4(0, 0, 0, 0);
+        st[u] = s[u] != SLOT_NONE ? reinterpret_cast<const uint4 *>(A.sst)[SLOT_U4 * (size_t)s[u]] : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t i = i0 + (uint32_t)u * ST;
@@ -269,11 +274,11 @@ __global__ __launch_bounds__(ST) void k_decode_apply(DecodeArgs A) {
     if (s == SLOT_NONE) return;
     const unsigned long long c = A.claim0 + i;
     const uint4 pv = A.pay[2 * (size_t)i + 1];
-    float *p = reinterpret_cast<float *>(A.pos + s);
+    float *p = reinterpret_cast<float *>(A.pos + SLOT_U4 * (size_t)s);
     const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
     const bool moves = A.o_sp[i] != SP_DEAD;
     if (moves && cs.x == c && cs.y == c) {  // the common case: one 16-B store of position and yaw
-        A.pos[s] = make_float4(__uint_as_float(pv.x), __uint_as_float(pv.y), __uint_as_float(pv.z),
+        A.pos[SLOT_U4 * (size_t)s] = make_float4(__uint_as_float(pv.x), __uint_as_float(pv.y), __uint_as_float(pv.z),
                                __uint_as_float(pv.w));
         return;
     }
@@ -304,7 +309,7 @@ __global__ __launch_bounds__(ST) void k_decode_dups(DecodeArgs A) {
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
         const uint32_t s = A.dups[k];
         const ulonglong2 cs = reinterpret_cast<const ulonglong2 *>(A.cl)[s];
-        float *p = reinterpret_cast<float *>(A.pos + s);
+        float *p = reinterpret_cast<float *>(A.pos + SLOT_U4 * (size_t)s);
         const unsigned long long ix = cs.x - A.claim0, iy = cs.y - A.claim0;  // claims of older batches wrap
         if (ix < A.n && A.o_ys[ix] == s && A.o_sp[ix] != SP_DEAD) {
             const uint4 pv = A.pay[2 * (size_t)ix + 1];
@@ -360,15 +365,15 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     if (i >= nf + A.n_left) return;
     const bool in_frame = i < nf;
     const uint32_t s = in_frame ? ld_ss(A.F.ss, i).slot : A.left[i - nf];
-    const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[s];  // gate, space, syncing, flags
+    const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[SLOT_U4 * (size_t)s];  // gate, space, syncing, flags
     uint32_t fl;
     if (in_frame) {
         fl = st.w;
-        if (fl) A.sst[4 * (size_t)s + SST_FLAGS] = 0u;
+        if (fl) A.sst[SLOT_W * (size_t)s + SST_FLAGS] = 0u;
     } else {
         // a listed slot back in the frame is its frame entry's; a slot listed twice is sent once
         const uint32_t r = A.info.rank[s];
-        fl = (r < nf && ld_ss(A.F.ss, r).slot == s) ? 0u : atomicExch(&A.sst[4 * (size_t)s + SST_FLAGS], 0u);
+        fl = (r < nf && ld_ss(A.F.ss, r).slot == s) ? 0u : atomicExch(&A.sst[SLOT_W * (size_t)s + SST_FLAGS], 0u);
     }
     A.snd[i] = fl;
     A.rg[i] = st.x;
@@ -382,13 +387,13 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     }
     if (fl) {
         // the frame holds the AOI position; outside the frame, the last Position written
-        const float4 P = A.pos[s];
+        const float4 P = A.pos[SLOT_U4 * (size_t)s];
         float x = P.x, z = P.z;
         if (in_frame) {
             x = __uint_as_float(q.x);
             z = __uint_as_float(q.y);
         }
-        A.srec[2 * (size_t)i] = A.eid[s];
+        A.srec[2 * (size_t)i] = A.eid[SLOT_U4 * (size_t)s];
         A.srec[2 * (size_t)i + 1] = make_uint4(__float_as_uint(x), __float_as_uint(P.y), __float_as_uint(z), __float_as_uint(P.w));
     }
 }
@@ -795,7 +800,7 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
     s_pre[p] = c;
     s_sb[p] = c ? A.fsb[i] : 0u;
     s_gate[p] = key;
-    if (c) s_cli[p] = A.cid[A.rslot[i]];
+    if (c) s_cli[p] = A.cid[SLOT_U4 * (size_t)A.rslot[i]];
     __syncthreads();
     uint32_t R;
     const uint32_t mine = s_pre[threadIdx.x];
@@ -905,7 +910,7 @@ __global__ __launch_bounds__(ST) void k_route(RouteArgs A) {
     const uint32_t e = blk * ST + threadIdx.x;
     if (e < A.n_total) {
         const uint2 ab = reinterpret_cast<const uint2 *>(A.ev)[e];
-        const uint32_t g = A.sst[4 * (size_t)ab.x + SST_GATE];
+        const uint32_t g = A.sst[SLOT_W * (size_t)ab.x + SST_GATE];
         if (g != NO_GATE) {
             const bool create = e < A.n_enter;
             const uint32_t p = atomicAdd(&lds[(create ? 0u : A.G) + g], 1u);
@@ -913,16 +918,16 @@ __global__ __launch_bounds__(ST) void k_route(RouteArgs A) {
                 if (create) {
                     const uint32_t r = A.info.rank[ab.y];  // b is live after the flush
                     const Rec16 B = ld_rec(A.F.rec, r);
-                    const float4 P = A.pos[ab.y];
+                    const float4 P = A.pos[SLOT_U4 * (size_t)ab.y];
                     uint4 *o = A.out_c + 3 * (size_t)p;
-                    o[0] = A.cid[ab.x];
-                    o[1] = A.eid[ab.y];
+                    o[0] = A.cid[SLOT_U4 * (size_t)ab.x];
+                    o[1] = A.eid[SLOT_U4 * (size_t)ab.y];
                     o[2] = make_uint4(__float_as_uint(B.x), __float_as_uint(P.y), __float_as_uint(B.z),
                                       __float_as_uint(P.w));
                 } else {
                     uint4 *o = A.out_d + 2 * (size_t)(p - A.split);
-                    o[0] = A.cid[ab.x];
-                    o[1] = A.eid[ab.y];
+                    o[0] = A.cid[SLOT_U4 * (size_t)ab.x];
+                    o[1] = A.eid[SLOT_U4 * (size_t)ab.y];
                 }
             }
         }
@@ -949,8 +954,9 @@ struct SyncState {
     hipStream_t st = nullptr;
     uint32_t max_slots = 0;
     // device, per slot
+    uint4 *slots = nullptr;   // SLOT_U4 per slot (the allocation); the fields below point into it
     uint4 *eid = nullptr, *cid = nullptr;
-    uint32_t *sst = nullptr;  // 4 per slot: gate, space, syncing, flags
+    uint32_t *sst = nullptr;  // gate, space, syncing, flags
     float4 *pos = nullptr;
     unsigned long long *cl = nullptr;  // 2 per slot: Position / yaw last-writer claims
     uint32_t *oflag = nullptr, *oflag_n = nullptr;  // decode: slots flagged outside every AOI space
@@ -1051,7 +1057,7 @@ ArrTable table32(SyncState *S) {
     T.p[A_QSPACE] = S->sst + SST_SPACE;
     T.p[A_SYNCING] = S->sst + SST_SYNCING;
     T.p[A_SFLAGS] = S->sst + SST_FLAGS;
-    for (int a = A_CGATE; a <= A_SFLAGS; ++a) T.stride[a] = 4;
+    for (int a = A_CGATE; a <= A_SFLAGS; ++a) T.stride[a] = SLOT_W;
     T.p[A_HVAL] = reinterpret_cast<uint32_t *>(S->htab);  // index: the slot word of an entry (hval_word)
     T.stride[A_HVAL] = 1;
     return T;
@@ -1059,9 +1065,9 @@ ArrTable table32(SyncState *S) {
 ArrTable table128(SyncState *S) {
     ArrTable T{};
     T.p[B_EID] = S->eid;
-    T.stride[B_EID] = 1;
+    T.stride[B_EID] = SLOT_U4;
     T.p[B_CID] = S->cid;
-    T.stride[B_CID] = 1;
+    T.stride[B_CID] = SLOT_U4;
     T.p[B_HKEY] = S->htab;  // index: the key of an entry (hkey_vec)
     T.stride[B_HKEY] = 1;
     return T;
@@ -1154,17 +1160,18 @@ int create(gwaoi_world *w, SyncState **out) {
     const size_t N = v.max_slots;
     S->oflag_cap = (uint32_t)N;
     int rc;
-    if ((rc = salloc(S, &S->eid, N)) || (rc = salloc(S, &S->cid, N)) || (rc = salloc(S, &S->sst, 4 * N)) ||
-        (rc = salloc(S, &S->pos, N)) || (rc = salloc(S, &S->cl, 2 * N)) || (rc = salloc(S, &S->oflag, N)) ||
+    if ((rc = salloc(S, &S->slots, SLOT_U4 * N)) || (rc = salloc(S, &S->cl, 2 * N)) || (rc = salloc(S, &S->oflag, N)) ||
         (rc = salloc(S, &S->oflag_n, 1)) || (rc = salloc(S, &S->htab, 4 * (size_t)nbk))) {
         sync_destroy(S);
         return rc;
     }
-    bool ok = hipMemsetAsync(S->pos, 0, N * 16, S->st) == hipSuccess &&
+    S->sst = reinterpret_cast<uint32_t *>(S->slots);
+    S->pos = reinterpret_cast<float4 *>(S->slots + 1);
+    S->eid = S->slots + 2;
+    S->cid = S->slots + 3;
+    bool ok = hipMemsetAsync(S->slots, 0, N * 16 * SLOT_U4, S->st) == hipSuccess &&
               hipMemsetAsync(S->cl, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->oflag_n, 0, 4, S->st) == hipSuccess &&
-              hipMemsetAsync(S->eid, 0, N * 16, S->st) == hipSuccess &&
-              hipMemsetAsync(S->cid, 0, N * 16, S->st) == hipSuccess &&
               hipMemsetAsync(S->htab, 0xFF, (size_t)nbk * 64, S->st) == hipSuccess &&  // every entry H_EMPTY
               hipEventCreateWithFlags(&S->stage_ev, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&S->ndec_ev, hipEventDisableTiming) == hipSuccess &&
@@ -1176,7 +1183,7 @@ int create(gwaoi_world *w, SyncState **out) {
     // space of every slot in call order (the world may hold entities already)
     std::vector<uint4> qs(N);
     for (uint32_t s = 0; s < N; ++s) qs[s] = make_uint4(NO_GATE, world_slot_space(w, s), 0u, 0u);
-    if (hipMemcpyAsync(S->sst, qs.data(), N * 16, hipMemcpyHostToDevice, S->st) != hipSuccess ||
+    if (hipMemcpy2DAsync(S->sst, 16 * SLOT_U4, qs.data(), 16, 16, N, hipMemcpyHostToDevice, S->st) != hipSuccess ||
         hipStreamSynchronize(S->st) != hipSuccess) {
         sync_destroy(S);
         return GWAOI_EDEVICE;
@@ -1602,8 +1609,8 @@ bool sync_slot_plain(const SyncState *S, uint32_t slot) { return slot < S->max_s
 void sync_destroy(SyncState *S) {
     if (!S) return;
     if (S->st) (void)hipStreamSynchronize(S->st);
-    sfree(S->eid); sfree(S->cid); sfree(S->sst);
-    sfree(S->pos); sfree(S->cl); sfree(S->oflag); sfree(S->oflag_n);
+    sfree(S->slots);
+    sfree(S->cl); sfree(S->oflag); sfree(S->oflag_n);
     sfree(S->htab);
     sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec); sfree(S->f_frec);
     sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->scr); sfree(S->scr_cursor); sfree(S->f_cnt); sfree(S->f_sb); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
