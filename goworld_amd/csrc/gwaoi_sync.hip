@@ -603,6 +603,10 @@ constexpr int FAN_WU = GWAOI_FAN_WU;
                         // 252 us at NR 2 / WU 2, 259 at 3 / 2, 279 at 4 / 2, 283 at 2 / 4, 267 at 1 / 4)
 #endif
 constexpr int FAN_NR = GWAOI_FAN_NR;
+#ifndef GWAOI_FAN_UBU
+#define GWAOI_FAN_UBU 4  // window rows whose bounds the run sizing loads together
+#endif
+constexpr int FAN_UBU = GWAOI_FAN_UBU;
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t k) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k);
@@ -629,9 +633,17 @@ __global__ __launch_bounds__(ST) void k_fan_hits_wave(FanArgs A) {
     if (walk) {
         W = fan_window(A.F, i);
         const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
-        for (int cz = W.cz0; cz <= W.cz1; ++cz) {
-            const uint32_t rb = W.row0 + (uint32_t)(cz - W.cz0) * W.gx;
-            ub += cs[rb + span] - cs[rb];
+        for (int cz = W.cz0; cz <= W.cz1; cz += FAN_UBU) {  // FAN_UBU rows' bounds in flight together
+            uint32_t lo[FAN_UBU], hi[FAN_UBU];
+#pragma unroll
+            for (int u = 0; u < FAN_UBU; ++u) {
+                const uint32_t rb = W.row0 + (uint32_t)(min(cz + u, W.cz1) - W.cz0) * W.gx;
+                lo[u] = cs[rb];
+                hi[u] = cs[rb + span];
+            }
+#pragma unroll
+            for (int u = 0; u < FAN_UBU; ++u)
+                if (cz + u <= W.cz1) ub += hi[u] - lo[u];
         }
     }
     ub = (ub + 3u) & ~3u;  // (k_fan_hits' run sizes, so the two passes place runs alike)
