@@ -53,8 +53,16 @@ __host__ __device__ inline uint32_t id_hash(uint32_t a, uint32_t b, uint32_t c, 
 
 // The fan-out's 16-B output and scratch stores.  Plain stores: the non-temporal form was
 // slower.
+// 16-B record stores that nothing in the kernel reads back: nontemporal (A/B,
+// profiles/r06_ab_fan_write.txt: k_fan_write 661 -> 630 us against plain stores)
 __device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
+#ifdef GWAOI_EXP_FW_PLAIN
     *p = v;
+#else
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(p));
+#endif
 }
 
 __device__ __forceinline__ bool eq4(uint4 a, uint4 b) {
@@ -468,132 +476,23 @@ __device__ __forceinline__ FanWin fan_window(const FrameView &F, uint32_t i) {
     return W;
 }
 
-// Fan-out pass 1 (hits): one lane per entry i (frame order, then the listed
-// slots outside the frame).  A receiver (an entry with a client) lists the
-// senders of its records in the scratch: itself first if sifSyncOwnClient,
-// then every A in its go-aoi window with sifSyncNeighborClients and rel(A,B).
-// Its scratch run is sized by the window's candidate count (cell_start
-// loads only) and placed by one atomic per block, so the window is walked
-// once.  A block past the scratch capacity writes no hits (the host regrows
-// the scratch and reruns this pass; it has no other side effect).
-#ifndef GWAOI_FAN_U
-#define GWAOI_FAN_U 6  // A/B: 6 -0.03 ms collect vs 4; 8 and 2 no better (profiles/r02_variants_fan_hits.log)
-#endif
-constexpr int FAN_U = GWAOI_FAN_U;  // window candidates loaded together per lane
-__device__ __forceinline__ void st_hits(uint4 *p, const uint4 &v) {
-    st_stream(p, v);
-}
-
-__global__ __launch_bounds__(ST) void k_fan_hits(FanArgs A) {
-    extern __shared__ uint32_t gcnt[];  // [G] records per gate of the block
-    __shared__ uint32_t s_ws[ST / 64];
-    __shared__ uint32_t s_base;
-    __shared__ uint16_t s_n[2][ST / 64];
-    __shared__ uint8_t s_perm[ST];
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
-    const uint32_t nf = A.F.n, ne = nf + A.n_left;
-    const uint32_t w = threadIdx.x / 64, ln = s_lane();
-    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) gcnt[q] = 0u;
-    // receivers that walk a window first (stable), so that whole waves idle instead of half lanes
-    {
-        const uint32_t i0 = blk * ST + threadIdx.x;
-        const bool wk = i0 < nf && A.rg[i0] != NO_GATE;
-        const unsigned long long m = __ballot(wk);
-        if (ln == 0) {
-            s_n[0][w] = (uint16_t)__popcll(m);
-            s_n[1][w] = (uint16_t)(64 - __popcll(m));
-        }
-        __syncthreads();
-        const unsigned long long lt = (1ull << ln) - 1ull;
-        uint32_t pos = wk ? (uint32_t)__popcll(m & lt) : (uint32_t)__popcll(~m & lt);
-        for (uint32_t q = 0; q < ST / 64; ++q) {
-            if (!wk) pos += s_n[0][q];
-            if (q < w) pos += s_n[wk ? 0 : 1][q];
-        }
-        s_perm[pos] = (uint8_t)threadIdx.x;
-        __syncthreads();
-    }
-    const uint32_t i = blk * ST + s_perm[threadIdx.x];
-    const uint32_t g = i < ne ? A.rg[i] : NO_GATE;
-    const bool on = g != NO_GATE;
-    const bool own = on && (A.snd[i] & GWAOI_SIF_OWN_CLIENT);
-    const bool walk = on && i < nf;
-    const uint32_t *cs = A.F.cell_start;
-    FanWin W{};
-    uint32_t ub = own ? 1u : 0u;
-    if (walk) {
-        W = fan_window(A.F, i);
-        const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
-        for (int cz = W.cz0; cz <= W.cz1; ++cz) {
-            const uint32_t rb = W.row0 + (uint32_t)(cz - W.cz0) * W.gx;
-            ub += cs[rb + span] - cs[rb];
-        }
-    }
-    ub = (ub + 3u) & ~3u;  // runs start 16-B aligned: hits are stored four at a time
-    uint32_t tot;
-    const uint32_t off = block_excl(ub, s_ws, tot);
-    if (threadIdx.x == 0) {
-        const unsigned long long b = tot ? atomicAdd(A.scr_cursor, (unsigned long long)tot) : 0ull;
-        s_base = b + tot <= A.scr_cap ? (uint32_t)b : SCR_FULL;
-    }
-    __syncthreads();
-    const uint32_t base = s_base;
-    const bool fits = base != SCR_FULL;
-    const uint32_t sb = base + off;
-    uint4 *run = reinterpret_cast<uint4 *>(A.scr + sb);
-    uint32_t c = 0;
-    uint4 buf = make_uint4(i, 0u, 0u, 0u);
-    if (own) c = 1;
-    if (walk) {
-        const uint32_t span = (uint32_t)(W.cx1 - W.cx0) + 1u;
-        const unsigned long long rs = W.R.s;
-        for (int cz = W.cz0; cz <= W.cz1; ++cz) {
-            const uint32_t rb = W.row0 + (uint32_t)(cz - W.cz0) * W.gx;
-            const uint32_t jb = cs[rb], je = cs[rb + span];
-            for (uint32_t b0 = jb; b0 < je; b0 += FAN_U) {
-                uint4 q[FAN_U];
-#pragma unroll
-                for (int u = 0; u < FAN_U; ++u) q[u] = A.frec[b0 + u < je ? b0 + u : b0];
-#pragma unroll
-                for (int u = 0; u < FAN_U; ++u) {
-                    const uint32_t b = b0 + (uint32_t)u;
-                    const unsigned long long bs = ((unsigned long long)(q[u].w & 0x7FFFFFFFu) << 32) | q[u].z;
-                    const bool hit = b < je && b != i && (q[u].w >> 31) &&
-                                     rel(W.R.x, W.R.z, rs, __uint_as_float(q[u].x), __uint_as_float(q[u].y), bs, W.D);
-                    if (hit) {
-                        switch (c & 3u) {
-                            case 0: buf.x = b; break;
-                            case 1: buf.y = b; break;
-                            case 2: buf.z = b; break;
-                            default: buf.w = b; break;
-                        }
-                        ++c;
-                        if (!(c & 3u) && fits) st_hits(run + (c >> 2) - 1u, buf);
-                    }
-                }
-            }
-        }
-    }
-    if ((c & 3u) && fits) st_hits(run + (c >> 2), buf);
-    if (i < ne) {
-        A.fcnt[i] = c;
-        A.fsb[i] = sb;
-    }
-    if (c) atomicAdd(&gcnt[g], c);
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) A.blk_cnt[(size_t)q * A.nb + blk] = gcnt[q];
-}
-
-// Fan-out pass 1, a wave per receiver (the default): the run sizing and placement
-// are k_fan_hits' (one lane per entry, cell_start loads only), then each wave
-// takes its walking receivers one at a time.  The receiver's window rows are
-// laid end to end (lane j loads row j's bounds; a wave scan gives each row's
-// first position) and the wave deals out 64 consecutive positions per step: a
-// lane's candidate is found from the rows starting in the step (an LDS mark per
-// position, a ballot) and the row's offset (LDS), so one load instruction reads
-// 64 consecutive candidates instead of one candidate from each of 64 windows,
-// and the hits are compacted by a ballot into consecutive 4-B stores.  The hits
-// and their order (rows in order, frame order inside a row) are k_fan_hits'.
+// Fan-out pass 1 (hits).  Entry i (frame order, then the listed slots outside
+// the frame) with a client is a receiver: it lists the senders of its records
+// in the scratch, itself first if sifSyncOwnClient, then every A in its go-aoi
+// window with sifSyncNeighborClients and rel(A,B), rows in order and frame
+// order inside a row.  Its scratch run is sized by the window's candidate
+// count (one lane per entry, cell_start loads only) and placed by one atomic
+// per block, so the window is walked once; a block past the scratch capacity
+// writes no hits (the host regrows the scratch and reruns this pass; it has no
+// other side effect).  The walk takes a wave per receiver (FAN_NR of a wave's
+// receivers at a time): the window rows are laid end to end (lane j loads row
+// j's bounds; a DPP scan gives each row's first position) and the wave deals
+// out 64 consecutive positions per step.  A lane's candidate is found from the
+// rows starting in the step (an LDS mark per position, a ballot) and the row's
+// offset (LDS), so one load instruction reads 64 consecutive candidates instead
+// of one candidate from each of 64 windows (the round-5 lane-per-receiver walk:
+// 353 against 249 us, profiles/r06_ab_fan_hits.txt), and the hits are
+// compacted by a ballot into consecutive 4-B stores.
 #ifndef GWAOI_FAN_WU
 #define GWAOI_FAN_WU 2  // steps of 64 positions per receiver with their loads in flight together
 #endif
@@ -646,7 +545,7 @@ __global__ __launch_bounds__(ST) void k_fan_hits_wave(FanArgs A) {
                 if (cz + u <= W.cz1) ub += hi[u] - lo[u];
         }
     }
-    ub = (ub + 3u) & ~3u;  // (k_fan_hits' run sizes, so the two passes place runs alike)
+    ub = (ub + 3u) & ~3u;  // (runs start 16-B aligned)
     uint32_t tot;
     const uint32_t off = block_excl(ub, s_ws, tot);
     if (threadIdx.x == 0) {
@@ -1467,11 +1366,7 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
                 SY_TRY(hipMemsetAsync(S->scr_cursor, 0, 8, S->st));
                 SY_TRY(hipMemsetAsync(S->blk_cnt + (size_t)G * nb, 0, 4, S->st));
             }
-#ifdef GWAOI_EXP_FAN_LANE  // A/B: one lane per receiver walking its own window
-            k_fan_hits<<<nb, ST, (size_t)G * 4, S->st>>>(A);
-#else
             k_fan_hits_wave<<<nb, ST, (size_t)G * 4, S->st>>>(A);
-#endif
             SY_TRY(hipGetLastError());
             // the per-gate bases are scanned before the capacity check: one host round trip
             // for both (a rerun rewrites every count the scan read).  The write pass follows on
