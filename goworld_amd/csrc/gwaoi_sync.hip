@@ -350,9 +350,9 @@ struct FanArgs {
     // frame-ordered (n + n_left entries), written by k_fan_prep
     uint32_t *snd;    // sender flags
     uint32_t *rg;     // receiver gate (NO_GATE: no client)
-    uint32_t *rslot;  // slot
     uint4 *srec;      // 2 per entry: sender id, then x, y, z, yaw (one 32-B load per record)
     uint4 *frec;      // frame records (x, z, seq) with sifSyncNeighborClients in bit 63
+    uint4 *fcid;      // receiver's ClientID (entries with a client; from the slot record's line)
     uint32_t *fcnt, *fsb;  // records of each entry, its run in the scratch
     uint32_t *scr;         // hits: sender entry of each record, receiver-contiguous runs
     unsigned long long *scr_cursor;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     }
     A.snd[i] = fl;
     A.rg[i] = st.x;
-    A.rslot[i] = s;
+    A.fcid[i] = A.cid[SLOT_U4 * (size_t)s];  // (the line st came from; loaded with it, no branch)
     uint4 q = make_uint4(0, 0, 0, 0);
     if (in_frame) {  // the walk's candidate record: x, z, seq with the sender flag in bit 63
         q = reinterpret_cast<const uint4 *>(A.F.rec)[i];
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
     s_pre[p] = c;
     s_sb[p] = c ? A.fsb[i] : 0u;
     s_gate[p] = key;
-    if (c) s_cli[p] = A.cid[SLOT_U4 * (size_t)A.rslot[i]];
+    if (c) s_cli[p] = A.fcid[i];
     __syncthreads();
     uint32_t R;
     const uint32_t mine = s_pre[threadIdx.x];
@@ -917,12 +917,12 @@ struct SyncState {
     uint32_t *d_left = nullptr;
     size_t left_cap = 0;
     // fan-out scratch, frame order (fan_cap entries each)
-    uint32_t *f_snd = nullptr, *f_rg = nullptr, *f_slot = nullptr, *f_cnt = nullptr, *f_sb = nullptr;
+    uint32_t *f_snd = nullptr, *f_rg = nullptr, *f_cnt = nullptr, *f_sb = nullptr;
     uint32_t *scr = nullptr;  // fan-out hits (sender entries), receiver runs
     size_t scr_cap = 0;
     unsigned long long *scr_cursor = nullptr;
     uint4 *f_rec = nullptr;  // 2 per entry
-    uint4 *f_frec = nullptr;
+    uint4 *f_frec = nullptr, *f_cid = nullptr;
     size_t fan_cap = 0;
     uint4 *out = nullptr, *out_d = nullptr;
     size_t out_cap = 0, outd_cap = 0;  // in uint4
@@ -1332,13 +1332,13 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     if (int rc = ensure_u32(S, &S->blk_cnt, &S->blk_cap, (size_t)G * nb + 1)) return rc;
     A.blk_cnt = S->blk_cnt;
     if (n_ent > S->fan_cap) {
-        sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec); sfree(S->f_frec);
+        sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_rec); sfree(S->f_frec); sfree(S->f_cid);
         sfree(S->f_cnt); sfree(S->f_sb);
         S->fan_cap = 0;
         const size_t c = std::max<size_t>(n_ent + n_ent / 8, 1024);
         int rc;
-        if ((rc = salloc(S, &S->f_snd, c)) || (rc = salloc(S, &S->f_rg, c)) || (rc = salloc(S, &S->f_slot, c)) ||
-            (rc = salloc(S, &S->f_rec, 2 * c)) || (rc = salloc(S, &S->f_frec, c)) || (rc = salloc(S, &S->f_cnt, c)) ||
+        if ((rc = salloc(S, &S->f_snd, c)) || (rc = salloc(S, &S->f_rg, c)) ||
+            (rc = salloc(S, &S->f_rec, 2 * c)) || (rc = salloc(S, &S->f_frec, c)) || (rc = salloc(S, &S->f_cid, c)) || (rc = salloc(S, &S->f_cnt, c)) ||
             (rc = salloc(S, &S->f_sb, c)))
             return rc;
         S->fan_cap = c;
@@ -1349,9 +1349,9 @@ int collect_sync(gwaoi_world *w, gwaoi_gate_records *out, bool to_host) {
     A.fsb = S->f_sb;
     A.snd = S->f_snd;
     A.rg = S->f_rg;
-    A.rslot = S->f_slot;
     A.srec = S->f_rec;
     A.frec = S->f_frec;
+    A.fcid = S->f_cid;
     A.scr_cursor = S->scr_cursor;
     if (n_ent) k_fan_prep<<<cdivu(n_ent, ST), ST, 0, S->st>>>(A);  // also clears the flags
     uint64_t total = 0;
@@ -1519,7 +1519,7 @@ void sync_destroy(SyncState *S) {
     sfree(S->slots);
     sfree(S->cl); sfree(S->oflag); sfree(S->oflag_n);
     sfree(S->htab);
-    sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_slot); sfree(S->f_rec); sfree(S->f_frec);
+    sfree(S->f_snd); sfree(S->f_rg); sfree(S->f_rec); sfree(S->f_frec); sfree(S->f_cid);
     sfree(S->blk_cnt); sfree(S->scan_tmp); sfree(S->scr); sfree(S->scr_cursor); sfree(S->f_cnt); sfree(S->f_sb); sfree(S->d_off); sfree(S->d_left); sfree(S->out); sfree(S->out_d);
     sfree(S->d_stage);
     for (auto &c : S->arena) (void)hipFree(c.p);
