@@ -373,7 +373,14 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     if (i >= nf + A.n_left) return;
     const bool in_frame = i < nf;
     const uint32_t s = in_frame ? ld_ss(A.F.ss, i).slot : A.left[i - nf];
-    const uint4 st = reinterpret_cast<const uint4 *>(A.sst)[SLOT_U4 * (size_t)s];  // gate, space, syncing, flags
+    // the slot's whole 64-B record and the frame record, all loaded before any is used (a load
+    // under a per-lane branch is waited for before the next one issues)
+    const uint4 *rec = reinterpret_cast<const uint4 *>(A.sst) + SLOT_U4 * (size_t)s;
+    const uint4 st = rec[0];  // gate, space, syncing, flags
+    const uint4 pw = rec[1];  // Position, yaw
+    const uint4 id = rec[2];  // EntityID
+    const uint4 ci = rec[3];  // ClientID
+    const uint4 q = reinterpret_cast<const uint4 *>(A.F.rec)[in_frame ? i : 0u];
     uint32_t fl;
     if (in_frame) {
         fl = st.w;
@@ -385,24 +392,17 @@ __global__ __launch_bounds__(ST) void k_fan_prep(FanArgs A) {
     }
     A.snd[i] = fl;
     A.rg[i] = st.x;
-    A.fcid[i] = A.cid[SLOT_U4 * (size_t)s];  // (the line st came from; loaded with it, no branch)
-    uint4 q = make_uint4(0, 0, 0, 0);
+    A.fcid[i] = ci;  // (the receiver's, read in frame order by the write pass)
     if (in_frame) {  // the walk's candidate record: x, z, seq with the sender flag in bit 63
-        q = reinterpret_cast<const uint4 *>(A.F.rec)[i];
         uint4 f = q;
         if (fl & GWAOI_SIF_NEIGHBOR_CLIENTS) f.w |= 0x80000000u;
         A.frec[i] = f;
     }
     if (fl) {
         // the frame holds the AOI position; outside the frame, the last Position written
-        const float4 P = A.pos[SLOT_U4 * (size_t)s];
-        float x = P.x, z = P.z;
-        if (in_frame) {
-            x = __uint_as_float(q.x);
-            z = __uint_as_float(q.y);
-        }
-        A.srec[2 * (size_t)i] = A.eid[SLOT_U4 * (size_t)s];
-        A.srec[2 * (size_t)i + 1] = make_uint4(__float_as_uint(x), __float_as_uint(P.y), __float_as_uint(z), __float_as_uint(P.w));
+        const uint32_t x = in_frame ? q.x : pw.x, z = in_frame ? q.y : pw.z;
+        A.srec[2 * (size_t)i] = id;
+        A.srec[2 * (size_t)i + 1] = make_uint4(x, pw.y, z, pw.w);
     }
 }
 
