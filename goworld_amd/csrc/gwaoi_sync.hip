@@ -169,9 +169,28 @@ struct DecodeArgs {
 // the three slots in words 12..14 (H_EMPTY never used, H_TOMB freed).  Linear
 // probing over entries e = 3 b + way, so a probe reads one line per step and
 // almost always stops in the first (half the bytes of the 32-B bucket layout).
-__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t bmask, uint4 id) {
-    uint32_t b = id_hash(id.x, id.y, id.z, id.w) & bmask;
-    for (uint32_t probe = 0; probe <= bmask; ++probe, b = (b + 1) & bmask) {
+// One bucket's three entries against id: true when the probe ends here (found, or an
+// empty entry: not in the table), with the slot (or SLOT_NONE) in *out.
+__device__ __forceinline__ bool probe_bucket(const uint4 (&k)[3], const uint4 &m, const uint4 &id, uint32_t *out) {
+    const uint32_t v[3] = {m.x, m.y, m.z};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (v[q] == H_EMPTY) {
+            *out = SLOT_NONE;
+            return true;
+        }
+        if (v[q] != H_TOMB && eq4(k[q], id)) {
+            *out = v[q];
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ uint32_t lookup(const uint4 *__restrict__ htab, uint32_t bmask, uint4 id,
+                                           uint32_t probe0 = 0) {
+    uint32_t b = (id_hash(id.x, id.y, id.z, id.w) + probe0) & bmask;
+    for (uint32_t probe = probe0; probe <= bmask; ++probe, b = (b + 1) & bmask) {
         uint4 k[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) k[q] = htab[4 * (size_t)b + (uint32_t)q];
@@ -248,18 +267,32 @@ __global__ __launch_bounds__(ST) void k_decode(DecodeArgs A) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t i = i0 + (uint32_t)u * ST;
-        id[u] = pv[u] = make_uint4(0, 0, 0, 0);
-        if (i < A.n) {
-            id[u] = A.pay[2 * (size_t)i];
-            pv[u] = A.pay[2 * (size_t)i + 1];
-        }
+        const size_t ic = i < A.n ? i : 0u;  // (clamped: the loads issue together)
+        id[u] = A.pay[2 * ic];
+        pv[u] = A.pay[2 * ic + 1];
+    }
+    // the first bucket of every record's probe in flight together (a probe almost always ends
+    // there); the rare longer probe continues from the next bucket
+    uint4 hk[PER][3], hm[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const size_t b = id_hash(id[u].x, id[u].y, id[u].z, id[u].w) & A.hmask;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) hk[u][q] = A.htab[4 * b + (uint32_t)q];
+        hm[u] = A.htab[4 * b + 3];
     }
 #pragma unroll
-    for (int u = 0; u < PER; ++u) s[u] = i0 + (uint32_t)u * ST < A.n ? lookup(A.htab, A.hmask, id[u]) : SLOT_NONE;
+    for (int u = 0; u < PER; ++u) {
+        s[u] = SLOT_NONE;
+        if (i0 + (uint32_t)u * ST < A.n && !probe_bucket(hk[u], hm[u], id[u], &s[u]))
+            s[u] = lookup(A.htab, A.hmask, id[u], 1u);
+    }
     uint4 st[PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u)  // every slot record in flight together
-        st[u] = s[u] != SLOT_NONE ? reinterpret_cast<const uint4 *>(A.sst)[SLOT_U4 * (size_t)s[u]] : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < PER; ++u) {  // every slot record in flight together (clamped slot: no branch)
+        st[u] = reinterpret_cast<const uint4 *>(A.sst)[SLOT_U4 * (size_t)(s[u] != SLOT_NONE ? s[u] : 0u)];
+        if (s[u] == SLOT_NONE) st[u] = make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const uint32_t i = i0 + (uint32_t)u * ST;

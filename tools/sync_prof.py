@@ -5,7 +5,7 @@ import os
 import sqlite3
 import sys
 
-KERNELS = ("k_fan_prep", "k_fan_hits", "k_fan_write")
+KERNELS = ("k_decode<", "k_decode_apply", "k_fan_prep", "k_fan_hits", "k_fan_write")
 
 for d in sys.argv[1:]:
     for db in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
