@@ -734,17 +734,22 @@ __global__ __launch_bounds__(ST) void k_fan_write(FanArgs A) {
     for (uint32_t q = threadIdx.x; q < A.G; q += blockDim.x) gbase[q] = A.blk_cnt[(size_t)q * A.nb + blk];
     __syncthreads();
     const uint32_t i = blk * ST + threadIdx.x;
-    const uint32_t g = i < ne ? A.rg[i] : NO_GATE;
+    // the receiver's gate, record count, run and ClientID in one round trip (clamped index, no
+    // load under a branch)
+    const uint32_t ic = i < ne ? i : 0u;
+    const uint32_t g0 = A.rg[ic], cnt0 = A.fcnt[ic], sb0 = A.fsb[ic];
+    const uint4 cli = A.fcid[ic];
+    const uint32_t g = i < ne ? g0 : NO_GATE;
     const uint32_t key = g == NO_GATE ? A.G : g;
     const uint32_t r0 = atomicAdd(&bin[key], 1u);
     __syncthreads();
     lds_excl_scan(bin, A.G + 1, s_ws);
     const uint32_t p = bin[key] + r0;  // (the order inside a gate's run is not part of the contract)
-    const uint32_t c = g != NO_GATE ? A.fcnt[i] : 0u;
+    const uint32_t c = g != NO_GATE ? cnt0 : 0u;
     s_pre[p] = c;
-    s_sb[p] = c ? A.fsb[i] : 0u;
+    s_sb[p] = c ? sb0 : 0u;
     s_gate[p] = key;
-    if (c) s_cli[p] = A.fcid[i];
+    if (c) s_cli[p] = cli;
     __syncthreads();
     uint32_t R;
     const uint32_t mine = s_pre[threadIdx.x];
